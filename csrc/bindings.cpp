@@ -1,0 +1,132 @@
+// pybind11 bindings for the sparkmi HIP kernel library (sparkmi._C).
+// Every launcher takes raw device pointers (uintptr_t, from torch's tensor.data_ptr()) and the
+// HIP stream handle (torch.cuda.current_stream().cuda_stream), so launches land on torch's
+// stream and are captured by torch.cuda.graph().  Non-zero return codes raise RuntimeError.
+#include <pybind11/pybind11.h>
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+namespace py = pybind11;
+using u = uintptr_t;
+#define P(x) reinterpret_cast<void*>(x)
+#define PF(x) reinterpret_cast<float*>(x)
+#define S(x) reinterpret_cast<hipStream_t>(x)
+
+#include "smi_attention.h"
+
+extern "C" {
+int smi_ln_fwd(const void*, const void*, const float*, const float*, void*, void*, float*, float*, int, int, float,
+               const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
+int smi_ln_bwd(const void*, const void*, const float*, const float*, const float*, void*, void*, const void*, float*,
+               float*, int, float*, float*, int, int, int, const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
+int smi_attn_fwd(const AttnFwdArgs*, hipStream_t);
+int smi_attn_bwd(const AttnBwdArgs*, const void*, float*, hipStream_t);
+int smi_ce_fwd(const void*, int, const long long*, int, int, long long, float*, float*, float*, float*, hipStream_t);
+int smi_ce_bwd(const void*, int, const long long*, int, int, long long, const float*, const float*, const float*, void*,
+               hipStream_t);
+int smi_emb_fwd(const long long*, const void*, const float*, void*, long, int, int, const uint32_t*, uint32_t, uint32_t, float,
+                hipStream_t);
+int smi_emb_bwd(const long long*, const void*, float*, long, int, long long, const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
+int smi_bias_act_drop_fwd(const void*, const float*, void*, long, int, int, const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
+int smi_act_drop_bwd(const void*, const void*, void*, long, int, const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
+int smi_colsum_bf16(const void*, long, int, float*, int, float*, int, hipStream_t);
+int smi_cast_f32_bf16(const float*, void*, long, hipStream_t);
+int smi_add_bf16(const void*, const void*, void*, long, hipStream_t);
+int smi_step_inc(float*, hipStream_t);
+int smi_adam(float*, float*, float*, float*, void*, long, const float*, const float*, float, float, float, float, float,
+             int, int, hipStream_t);
+int smi_sgd(float*, float*, float*, void*, long, const float*, const float*, float, float, float, int, float, int,
+            hipStream_t);
+}
+
+static void chk(int rc, const char* what) {
+  if (rc != 0) throw std::runtime_error(std::string("sparkmi._C.") + what + " failed: " +
+                                        (rc > 0 ? hipGetErrorString((hipError_t)rc) : "unsupported shape"));
+}
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "sparkmi HIP/CDNA4 kernels for MI355X (gfx950)";
+  m.attr("ARCH") = "gfx950";
+
+  m.def("ln_fwd", [](u h, u r, u gamma, u beta, u y, u xsave, u mean, u rstd, int M, int D, float eps, u seedp, uint32_t salt,
+                     uint32_t thresh, float dscale, u st) {
+    chk(smi_ln_fwd(P(h), P(r), PF(gamma), PF(beta), P(y), P(xsave), PF(mean), PF(rstd), M, D, eps, (const uint32_t*)seedp, salt, thresh, dscale,
+                   S(st)), "ln_fwd");
+  });
+  m.def("ln_bwd", [](u dy, u xs, u mean, u rstd, u gamma, u dres, u dh, u dres_add, u pg, u pb, int nblocks, u dgamma,
+                     u dbeta, int accumulate, int M, int D, u seedp, uint32_t salt, uint32_t thresh, float dscale, u st) {
+    chk(smi_ln_bwd(P(dy), P(xs), PF(mean), PF(rstd), PF(gamma), P(dres), P(dh), P(dres_add), PF(pg), PF(pb), nblocks,
+                   PF(dgamma), PF(dbeta), accumulate, M, D, (const uint32_t*)seedp, salt, thresh, dscale, S(st)), "ln_bwd");
+  });
+  m.def("attn_fwd", [](u q, u k, u v, py::tuple qs, py::tuple ks, py::tuple vs, u o, py::tuple os, u lse, u kpad, int B,
+                       int H, int Sq, int Sk, int mode, float scale_log2, u st) {
+    AttnFwdArgs a{};
+    a.q = (const unsigned short*)q; a.k = (const unsigned short*)k; a.v = (const unsigned short*)v;
+    a.q_sb = qs[0].cast<long>(); a.q_ss = qs[1].cast<long>(); a.q_sh = qs[2].cast<long>();
+    a.k_sb = ks[0].cast<long>(); a.k_ss = ks[1].cast<long>(); a.k_sh = ks[2].cast<long>();
+    a.v_sb = vs[0].cast<long>(); a.v_ss = vs[1].cast<long>(); a.v_sh = vs[2].cast<long>();
+    a.o = (unsigned short*)o; a.o_sb = os[0].cast<long>(); a.o_ss = os[1].cast<long>(); a.o_sh = os[2].cast<long>();
+    a.lse = (float*)lse; a.kpad = (const unsigned char*)kpad;
+    a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk; a.mode = mode; a.scale_log2 = scale_log2;
+    chk(smi_attn_fwd(&a, S(st)), "attn_fwd");
+  });
+  m.def("attn_bwd", [](u q, u k, u v, py::tuple qs, py::tuple ks, py::tuple vs, u o, u dout, py::tuple os, u lse,
+                       u delta, u dq, u dk, u dv, u kpad, int B, int H, int Sq, int Sk, int mode, float scale_log2,
+                       float scale, u st) {
+    AttnBwdArgs a{};
+    a.q = (const unsigned short*)q; a.k = (const unsigned short*)k; a.v = (const unsigned short*)v;
+    a.q_sb = qs[0].cast<long>(); a.q_ss = qs[1].cast<long>(); a.q_sh = qs[2].cast<long>();
+    a.k_sb = ks[0].cast<long>(); a.k_ss = ks[1].cast<long>(); a.k_sh = ks[2].cast<long>();
+    a.v_sb = vs[0].cast<long>(); a.v_ss = vs[1].cast<long>(); a.v_sh = vs[2].cast<long>();
+    a.dout = (const unsigned short*)dout;
+    a.o_sb = os[0].cast<long>(); a.o_ss = os[1].cast<long>(); a.o_sh = os[2].cast<long>();
+    a.lse = (const float*)lse; a.delta = (const float*)delta;
+    a.dq = (unsigned short*)dq; a.dk = (unsigned short*)dk; a.dv = (unsigned short*)dv;
+    a.kpad = (const unsigned char*)kpad;
+    a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk; a.mode = mode; a.scale_log2 = scale_log2; a.scale = scale;
+    chk(smi_attn_bwd(&a, P(o), PF(delta), S(st)), "attn_bwd");
+  });
+  m.def("ce_fwd", [](u logits, int is_bf16, u labels, int M, int V, long long ignore, u lse, u count, u loss,
+                     u row_loss, u st) {
+    chk(smi_ce_fwd(P(logits), is_bf16, (const long long*)labels, M, V, ignore, PF(lse), PF(count), PF(loss),
+                   PF(row_loss), S(st)), "ce_fwd");
+  });
+  m.def("ce_bwd", [](u logits, int is_bf16, u labels, int M, int V, long long ignore, u lse, u count, u dloss, u grad,
+                     u st) {
+    chk(smi_ce_bwd(P(logits), is_bf16, (const long long*)labels, M, V, ignore, PF(lse), PF(count), PF(dloss), P(grad),
+                   S(st)), "ce_bwd");
+  });
+  m.def("emb_fwd", [](u ids, u table, u pe, u out, long T, int D, int Sp, u seedp, uint32_t salt, uint32_t thresh, float dscale,
+                      u st) {
+    chk(smi_emb_fwd((const long long*)ids, P(table), PF(pe), P(out), T, D, Sp, (const uint32_t*)seedp, salt, thresh, dscale, S(st)), "emb_fwd");
+  });
+  m.def("emb_bwd", [](u ids, u dout, u dtable, long T, int D, long long pad, u seedp, uint32_t salt, uint32_t thresh,
+                      float dscale, u st) {
+    chk(smi_emb_bwd((const long long*)ids, P(dout), PF(dtable), T, D, pad, (const uint32_t*)seedp, salt, thresh, dscale, S(st)), "emb_bwd");
+  });
+  m.def("bias_act_drop_fwd", [](u x, u bias, u y, long total, int N, int act, u seedp, uint32_t salt, uint32_t thresh,
+                                float dscale, u st) {
+    chk(smi_bias_act_drop_fwd(P(x), PF(bias), P(y), total, N, act, (const uint32_t*)seedp, salt, thresh, dscale, S(st)), "bias_act_drop_fwd");
+  });
+  m.def("act_drop_bwd", [](u dy, u y, u dx, long total, int act, u seedp, uint32_t salt, uint32_t thresh, float dscale, u st) {
+    chk(smi_act_drop_bwd(P(dy), P(y), P(dx), total, act, (const uint32_t*)seedp, salt, thresh, dscale, S(st)), "act_drop_bwd");
+  });
+  m.def("colsum_bf16", [](u x, long M, int N, u part, int rpb, u out, int acc, u st) {
+    chk(smi_colsum_bf16(P(x), M, N, PF(part), rpb, PF(out), acc, S(st)), "colsum_bf16");
+  });
+  m.def("cast_f32_bf16", [](u x, u y, long n, u st) { chk(smi_cast_f32_bf16(PF(x), P(y), n, S(st)), "cast_f32_bf16"); });
+  m.def("add_bf16", [](u a, u b, u y, long n, u st) { chk(smi_add_bf16(P(a), P(b), P(y), n, S(st)), "add_bf16"); });
+  m.def("step_inc", [](u step, u st) { chk(smi_step_inc(PF(step), S(st)), "step_inc"); });
+  m.def("adam", [](u p, u g, u mm, u v, u pbf, long n, u lr, u step, float b1, float b2, float eps, float wd,
+                   float gscale, int adamw, int zero_grad, u st) {
+    chk(smi_adam(PF(p), PF(g), PF(mm), PF(v), P(pbf), n, PF(lr), PF(step), b1, b2, eps, wd, gscale, adamw, zero_grad,
+                 S(st)), "adam");
+  });
+  m.def("sgd", [](u p, u g, u buf, u pbf, long n, u lr, u step, float mom, float damp, float wd, int nesterov,
+                  float gscale, int zero_grad, u st) {
+    chk(smi_sgd(PF(p), PF(g), PF(buf), P(pbf), n, PF(lr), PF(step), mom, damp, wd, nesterov, gscale, zero_grad, S(st)),
+        "sgd");
+  });
+}

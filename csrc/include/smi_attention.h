@@ -1,0 +1,21 @@
+// Argument blocks shared by csrc/kernels/attention.hip and csrc/bindings.cpp.
+#pragma once
+struct AttnFwdArgs {
+  const unsigned short* q; const unsigned short* k; const unsigned short* v;
+  long q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh;
+  unsigned short* o; long o_sb, o_ss, o_sh;
+  float* lse;                 // [B,H,Sq], log2 units of the scaled+biased scores
+  const unsigned char* kpad;  // [B,Sk] or null
+  int B, H, Sq, Sk, mode;
+  float scale_log2;           // log2(e)/sqrt(head_dim)
+};
+struct AttnBwdArgs {
+  const unsigned short* q; const unsigned short* k; const unsigned short* v;
+  long q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh;
+  const unsigned short* dout; long o_sb, o_ss, o_sh;   // dO shares O's layout
+  const float* lse; const float* delta;                // [B,H,Sq]
+  unsigned short* dq; unsigned short* dk; unsigned short* dv;  // same layouts as q / k / v
+  const unsigned char* kpad;
+  int B, H, Sq, Sk, mode;
+  float scale_log2, scale;    // scale = 1/sqrt(head_dim)
+};

@@ -1,0 +1,72 @@
+// sparkmi common device helpers for gfx950 (CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SMI_WAVE 64
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8_t;   // MFMA A/B operand (16x16x32 / 32x32x16)
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;    // 16x16 accumulator
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;  // 32x32 accumulator
+typedef __attribute__((ext_vector_type(4))) unsigned short u16x4_t;
+typedef __attribute__((ext_vector_type(8))) unsigned short u16x8_t;
+
+// ---- bf16 <-> f32 (bit-level, round-to-nearest-even; NaN-preserving via quiet bit) ----
+__device__ __forceinline__ float bf2f(unsigned short h) {
+  return __uint_as_float(((unsigned int)h) << 16);
+}
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  unsigned int u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (unsigned short)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+__device__ __forceinline__ unsigned int pack2bf(float a, float b) {
+  return (unsigned int)f2bf(a) | ((unsigned int)f2bf(b) << 16);
+}
+
+// ---- wave64 reductions ----
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// sum over groups of `width` consecutive lanes (width power of two <= 64)
+template <int W>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <int W>
+__device__ __forceinline__ float group_max(float v) {
+#pragma unroll
+  for (int o = W / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---- counter-based dropout RNG ----
+// keep(i) = hash(seed, i) >= p * 2^32. The same hash is implemented in
+// sparkmi/ops/dropout.py (torch int64 arithmetic) so CPU and GPU masks are bit-identical.
+__device__ __forceinline__ uint32_t smi_hash(uint32_t seed, uint32_t idx) {
+  uint32_t h = idx * 0x9E3779B1u ^ (seed * 0x85EBCA77u + 0x165667B1u);
+  h ^= h >> 16; h *= 0x7FEB352Du;
+  h ^= h >> 15; h *= 0x846CA68Bu;
+  h ^= h >> 16;
+  return h;
+}
+// Per-call seed = device step seed (bumped by a captured kernel every step, so HIP-graph replays
+// draw fresh masks) mixed with a static per-call-site salt.
+__device__ __forceinline__ uint32_t smi_seed(const uint32_t* seedp, uint32_t salt) {
+  return (seedp ? seedp[0] : 0u) * 0x9E3779B9u + salt;
+}
+__device__ __forceinline__ bool smi_keep(uint32_t seed, uint32_t idx, uint32_t thresh) {
+  return smi_hash(seed, idx) >= thresh;
+}
+
+#define SMI_CHECK_LAUNCH() return (int)hipGetLastError()

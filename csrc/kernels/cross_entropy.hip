@@ -1,0 +1,160 @@
+// Softmax cross-entropy with ignore_index and mean over non-ignored rows, bf16/fp32 logits.
+//
+// Reference: nn.CrossEntropyLoss(ignore_index=0, reduction='none') followed by a manual masked
+// mean over non-pad targets (pytorch_machine_translator.py:125-126,182-188); with ignore=-100
+// and all rows valid it is the plain mean CE of the MLP/CNN/LSTM scripts
+// (distributed_cnn.py:141, distributed_lstm.py:142,189).
+// Forward: one 256-thread block per row, single online (max, sum) pass over V with 16-B
+// loads; stores the row logsumexp and atomically adds loss/count into a device scalar.
+// Backward: grad = (softmax - onehot) * dloss / count, written in place or out of place.
+// The valid-row count lives on the device, so the whole loss is graph-capturable.
+#include "smi_common.h"
+
+__global__ void ce_count_kernel(const long long* __restrict__ labels, int M, long long ignore, float* __restrict__ count,
+                                float* __restrict__ loss) {
+  __shared__ float part[4];
+  float c = 0.f;
+  for (int i = threadIdx.x; i < M; i += blockDim.x) c += (labels[i] != ignore) ? 1.f : 0.f;
+  c = wave_sum(c);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += part[w];
+    count[0] = t;
+    loss[0] = 0.f;
+  }
+}
+
+template <bool BF16>
+__device__ __forceinline__ void load8f(const void* p, long idx, float (&x)[8]) {
+  if (BF16) {
+    u16x8_t v = *(const u16x8_t*)((const unsigned short*)p + idx);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = bf2f(v[j]);
+  } else {
+    float4 a = *(const float4*)((const float*)p + idx);
+    float4 b = *(const float4*)((const float*)p + idx + 4);
+    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+  }
+}
+template <bool BF16>
+__device__ __forceinline__ float load1f(const void* p, long idx) {
+  return BF16 ? bf2f(((const unsigned short*)p)[idx]) : ((const float*)p)[idx];
+}
+
+template <bool BF16>
+__global__ __launch_bounds__(256) void ce_fwd_kernel(const void* __restrict__ logits, const long long* __restrict__ labels,
+                                                     int V, long long ignore, float* __restrict__ lse_out,
+                                                     const float* __restrict__ count, float* __restrict__ loss,
+                                                     float* __restrict__ row_loss) {
+  const int row = blockIdx.x;
+  const long base = (long)row * V;
+  float m = -INFINITY, s = 0.f;
+  const int nvec = (V % 8 == 0) ? V / 8 : 0;
+  for (int i = threadIdx.x; i < nvec; i += 256) {
+    float x[8];
+    load8f<BF16>(logits, base + (long)i * 8, x);
+    float lm = x[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) lm = fmaxf(lm, x[j]);
+    const float nm = fmaxf(m, lm);
+    float acc = s * __expf(m - nm);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += __expf(x[j] - nm);
+    s = acc; m = nm;
+  }
+  for (int i = nvec * 8 + threadIdx.x; i < V; i += 256) {
+    const float x = load1f<BF16>(logits, base + i);
+    const float nm = fmaxf(m, x);
+    s = s * __expf(m - nm) + __expf(x - nm);
+    m = nm;
+  }
+  // block-wide (max, sum) merge
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+    const float nm = fmaxf(m, om);
+    s = (nm == -INFINITY) ? 0.f : s * __expf(m - nm) + os * __expf(om - nm);
+    m = nm;
+  }
+  __shared__ float sm[4], ss[4];
+  if ((threadIdx.x & 63) == 0) { sm[threadIdx.x >> 6] = m; ss[threadIdx.x >> 6] = s; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M0 = sm[0], S0 = ss[0];
+    for (int w = 1; w < 4; ++w) {
+      const float nm = fmaxf(M0, sm[w]);
+      S0 = S0 * __expf(M0 - nm) + ss[w] * __expf(sm[w] - nm);
+      M0 = nm;
+    }
+    const float lse = M0 + __logf(S0);
+    lse_out[row] = lse;
+    const long long lab = labels[row];
+    float rl = 0.f;
+    if (lab != ignore) {
+      rl = lse - load1f<BF16>(logits, base + lab);
+      const float c = count[0];
+      atomicAdd(loss, c > 0.f ? rl / c : 0.f);
+    }
+    if (row_loss) row_loss[row] = rl;
+  }
+}
+
+template <bool BF16>
+__global__ __launch_bounds__(256) void ce_bwd_kernel(const void* __restrict__ logits, const long long* __restrict__ labels,
+                                                     int V, long long ignore, const float* __restrict__ lse_in,
+                                                     const float* __restrict__ count, const float* __restrict__ dloss,
+                                                     void* __restrict__ grad) {
+  const int row = blockIdx.x;
+  const long base = (long)row * V;
+  const long long lab = labels[row];
+  const float c = count[0];
+  const float scale = (lab == ignore || c <= 0.f) ? 0.f : dloss[0] / c;
+  const float lse = lse_in[row];
+  const int nvec = (V % 8 == 0) ? V / 8 : 0;
+  for (int i = threadIdx.x; i < nvec; i += 256) {
+    float x[8];
+    load8f<BF16>(logits, base + (long)i * 8, x);
+    float gq[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = i * 8 + j;
+      gq[j] = (__expf(x[j] - lse) - (col == lab ? 1.f : 0.f)) * scale;
+    }
+    if (BF16) {
+      u16x8_t o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(gq[j]);
+      *(u16x8_t*)((unsigned short*)grad + base + (long)i * 8) = o;
+    } else {
+      *(float4*)((float*)grad + base + (long)i * 8) = make_float4(gq[0], gq[1], gq[2], gq[3]);
+      *(float4*)((float*)grad + base + (long)i * 8 + 4) = make_float4(gq[4], gq[5], gq[6], gq[7]);
+    }
+  }
+  for (int i = nvec * 8 + threadIdx.x; i < V; i += 256) {
+    const float x = load1f<BF16>(logits, base + i);
+    const float gq = (__expf(x - lse) - (i == lab ? 1.f : 0.f)) * scale;
+    if (BF16) ((unsigned short*)grad)[base + i] = f2bf(gq);
+    else ((float*)grad)[base + i] = gq;
+  }
+}
+
+extern "C" int smi_ce_fwd(const void* logits, int is_bf16, const long long* labels, int M, int V, long long ignore,
+                          float* lse, float* count, float* loss, float* row_loss, hipStream_t st) {
+  hipLaunchKernelGGL(ce_count_kernel, dim3(1), dim3(256), 0, st, labels, M, ignore, count, loss);
+  if (is_bf16)
+    hipLaunchKernelGGL(ce_fwd_kernel<true>, dim3(M), dim3(256), 0, st, logits, labels, V, ignore, lse, count, loss, row_loss);
+  else
+    hipLaunchKernelGGL(ce_fwd_kernel<false>, dim3(M), dim3(256), 0, st, logits, labels, V, ignore, lse, count, loss, row_loss);
+  SMI_CHECK_LAUNCH();
+}
+
+extern "C" int smi_ce_bwd(const void* logits, int is_bf16, const long long* labels, int M, int V, long long ignore,
+                          const float* lse, const float* count, const float* dloss, void* grad, hipStream_t st) {
+  if (is_bf16)
+    hipLaunchKernelGGL(ce_bwd_kernel<true>, dim3(M), dim3(256), 0, st, logits, labels, V, ignore, lse, count, dloss, grad);
+  else
+    hipLaunchKernelGGL(ce_bwd_kernel<false>, dim3(M), dim3(256), 0, st, logits, labels, V, ignore, lse, count, dloss, grad);
+  SMI_CHECK_LAUNCH();
+}

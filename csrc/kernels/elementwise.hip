@@ -1,0 +1,156 @@
+// Memory-bound elementwise kernels: bias + activation + dropout epilogues (fwd/bwd), bf16
+// column sums (bias gradients), fp32 <-> bf16 casts.  All 16-B vectorized (8 bf16 / lane).
+//
+// Reference: PositionwiseFeedForward Linear -> ReLU -> Dropout (transformer.py:107-117),
+// the MLP/CNN ReLU/Sigmoid activations (distributed_multilayer_perceptron.py:47-53,
+// distributed_cnn.py:57-71) and every nn.Dropout(p) of transformer.py.
+#include "smi_common.h"
+
+// act: 0 identity, 1 relu, 2 sigmoid
+__device__ __forceinline__ float act_f(float x, int act) {
+  if (act == 1) return fmaxf(x, 0.f);
+  if (act == 2) return 1.f / (1.f + __expf(-x));
+  return x;
+}
+
+// y = dropout(act(x + bias[col])) ; x,y bf16 [M,N] (may alias)
+__global__ void bias_act_drop_fwd_kernel(const unsigned short* __restrict__ x, const float* __restrict__ bias,
+                                         unsigned short* __restrict__ y, long total, int N, int act,
+                                         const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale) {
+  const uint32_t seed = smi_seed(seedp, salt);
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i >= total) return;
+  u16x8_t v = *(const u16x8_t*)(x + i);
+  const int col = (int)(i % N);
+  u16x8_t o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float a = bf2f(v[j]) + (bias ? bias[col + j] : 0.f);
+    a = act_f(a, act);
+    if (thresh) a = smi_keep(seed, (uint32_t)(i + j), thresh) ? a * dscale : 0.f;
+    o[j] = f2bf(a);
+  }
+  *(u16x8_t*)(y + i) = o;
+}
+
+// dx = dy * dact(y) * dropmask*scale.  For relu the saved output y decides (y > 0 implies kept
+// and positive); for sigmoid y must be the pre-dropout activation (dropout unsupported there);
+// for identity the mask is recomputed from the seed.
+__global__ void act_drop_bwd_kernel(const unsigned short* __restrict__ dy, const unsigned short* __restrict__ y,
+                                    unsigned short* __restrict__ dx, long total, int act,
+                                    const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale) {
+  const uint32_t seed = smi_seed(seedp, salt);
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i >= total) return;
+  u16x8_t d = *(const u16x8_t*)(dy + i);
+  u16x8_t yy;
+  if (act) yy = *(const u16x8_t*)(y + i);
+  u16x8_t o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float g = bf2f(d[j]);
+    if (act == 1) g = bf2f(yy[j]) > 0.f ? g * (thresh ? dscale : 1.f) : 0.f;
+    else {
+      if (act == 2) { const float s = bf2f(yy[j]); g *= s * (1.f - s); }
+      if (thresh) g = smi_keep(seed, (uint32_t)(i + j), thresh) ? g * dscale : 0.f;
+    }
+    o[j] = f2bf(g);
+  }
+  *(u16x8_t*)(dx + i) = o;
+}
+
+// out[c] (+)= sum_r x[r][c]   (bf16 input [M,N], fp32 out).  Block = 256 threads covering
+// 64 columns x 4 row-phases... each thread sums 8 consecutive columns over a strided row set.
+__global__ void colsum_bf16_kernel(const unsigned short* __restrict__ x, long M, int N, float* __restrict__ part,
+                                   int rows_per_block) {
+  const int cv = blockIdx.x * 32 + (threadIdx.x & 31);  // column-vector index (8 cols each)
+  const int rphase = threadIdx.x >> 5;                  // 0..7
+  const long r0 = (long)blockIdx.y * rows_per_block;
+  const long r1 = min(M, r0 + rows_per_block);
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  if (cv * 8 < N) {
+    for (long r = r0 + rphase; r < r1; r += 8) {
+      u16x8_t v = *(const u16x8_t*)(x + r * N + cv * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[j]);
+    }
+  }
+  __shared__ float red[8][32 * 8 + 1];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rphase][(threadIdx.x & 31) * 8 + j] = acc[j];
+  __syncthreads();
+  for (int c = threadIdx.x; c < 256; c += 256) {
+    float s = 0.f;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) s += red[p][c];
+    const int col = blockIdx.x * 256 + c;
+    if (col < N) part[(long)blockIdx.y * N + col] = s;
+  }
+}
+
+__global__ void colsum_final_kernel(const float* __restrict__ part, int nparts, int N, float* __restrict__ out,
+                                    int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= N) return;
+  float s = 0.f;
+  for (int p = 0; p < nparts; ++p) s += part[(long)p * N + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x, unsigned short* __restrict__ y, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = f2bf(x[i]);
+}
+
+__global__ void add_bf16_kernel(const unsigned short* __restrict__ a, const unsigned short* __restrict__ b,
+                                unsigned short* __restrict__ y, long total) {
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i >= total) return;
+  u16x8_t va = *(const u16x8_t*)(a + i), vb = *(const u16x8_t*)(b + i), o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(va[j]) + bf2f(vb[j]));
+  *(u16x8_t*)(y + i) = o;
+}
+
+static inline unsigned nblk8(long total) { return (unsigned)((total / 8 + 255) / 256); }
+
+extern "C" int smi_bias_act_drop_fwd(const void* x, const float* bias, void* y, long total, int N, int act,
+                                     const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, hipStream_t st) {
+  if (total % 8 || N % 8) return -1;
+  hipLaunchKernelGGL(bias_act_drop_fwd_kernel, dim3(nblk8(total)), dim3(256), 0, st, (const unsigned short*)x, bias,
+                     (unsigned short*)y, total, N, act, seedp, salt, thresh, dscale);
+  SMI_CHECK_LAUNCH();
+}
+
+extern "C" int smi_act_drop_bwd(const void* dy, const void* y, void* dx, long total, int act, const uint32_t* seedp, uint32_t salt,
+                                uint32_t thresh, float dscale, hipStream_t st) {
+  if (total % 8) return -1;
+  hipLaunchKernelGGL(act_drop_bwd_kernel, dim3(nblk8(total)), dim3(256), 0, st, (const unsigned short*)dy,
+                     (const unsigned short*)y, (unsigned short*)dx, total, act, seedp, salt, thresh, dscale);
+  SMI_CHECK_LAUNCH();
+}
+
+// part must hold nparts*N floats, nparts = ceil(M / rows_per_block)
+extern "C" int smi_colsum_bf16(const void* x, long M, int N, float* part, int rows_per_block, float* out,
+                               int accumulate, hipStream_t st) {
+  if (N % 8) return -1;
+  const int nparts = (int)((M + rows_per_block - 1) / rows_per_block);
+  hipLaunchKernelGGL(colsum_bf16_kernel, dim3((N + 255) / 256, nparts), dim3(256), 0, st, (const unsigned short*)x, M,
+                     N, part, rows_per_block);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, st, part, nparts, N, out, accumulate);
+  SMI_CHECK_LAUNCH();
+}
+
+extern "C" int smi_cast_f32_bf16(const float* x, void* y, long n, hipStream_t st) {
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, (unsigned short*)y, n);
+  SMI_CHECK_LAUNCH();
+}
+
+extern "C" int smi_add_bf16(const void* a, const void* b, void* y, long total, hipStream_t st) {
+  if (total % 8) return -1;
+  hipLaunchKernelGGL(add_bf16_kernel, dim3(nblk8(total)), dim3(256), 0, st, (const unsigned short*)a,
+                     (const unsigned short*)b, (unsigned short*)y, total);
+  SMI_CHECK_LAUNCH();
+}

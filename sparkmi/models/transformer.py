@@ -1,0 +1,297 @@
+"""Encoder-decoder Transformer translator (the reference's transformer.py), MI355X-native.
+
+Module tree, attribute and parameter names match the reference exactly
+(transformer.py:44-284), so a reference ``state_dict`` loads unchanged
+(e.g. ``encoder.layers.0.attention.qkv_layer.weight``, ``decoder.layers.0.layer_norm1.gamma``,
+``linear.weight``).  The per-head interleaved qkv / kv weight layouts (transformer.py:76-79,
+:183-187) are kept, and the attention kernel reads them in place.
+
+Each sublayer is one chain of fused ops (sparkmi.ops):
+  linear(qkv) -> attention core -> linear(out) -> dropout+residual+LayerNorm
+  linear1+ReLU+dropout -> linear2 -> dropout+residual+LayerNorm
+bf16 activations on GPU (fp32 master weights in the model's flat buffer), fp32 on CPU.
+
+Mask semantics:
+  mask_mode="reference" reproduces the reference numerically: the encoder padding mask is a
+  no-op, the decoder self- and cross-attention "look-ahead" masks become a +1.0 bias on
+  strictly-past keys.  mask_mode="causal" is the corrected semantics: key-padding masking in
+  the encoder and cross attention, true causal masking in decoder self-attention.
+"""
+from dataclasses import dataclass
+
+import torch
+from torch import nn
+
+from ..ops import (DropoutRNG, add_dropout_layernorm, cross_attention, embedding, linear, self_attention,
+                   sinusoid_table)
+from ..ops.loss import cross_entropy
+from ..ops.rng import new_salt
+
+
+def get_device():
+    """transformer.py:8-9."""
+    return torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+
+
+@dataclass
+class TransformerConfig:
+    d_model: int = 512
+    ffn_hidden: int = 1024
+    num_heads: int = 8
+    drop_prob: float = 0.1
+    num_layers: int = 1
+    max_sequence_length: int = 200
+    src_vocab_size: int = 10000
+    tgt_vocab_size: int = 10000
+    emb_dropout: float = 0.1          # SentenceEmbedding hard-codes p=0.1 (transformer.py:53)
+    mask_mode: str = "reference"      # or "causal"
+    pad_id: int = 0
+
+
+def _share(obj, name, value):
+    object.__setattr__(obj, name, value)
+
+
+class PositionalEncoding(nn.Module):
+    """transformer.py:27-42; computed once and cached instead of on every forward (Q8)."""
+
+    def __init__(self, d_model, max_sequence_length):
+        super().__init__()
+        self.max_sequence_length = max_sequence_length
+        self.d_model = d_model
+        self.register_buffer("table", sinusoid_table(max_sequence_length, d_model), persistent=False)
+
+    def forward(self):
+        return self.table
+
+
+class SentenceEmbedding(nn.Module):
+    def __init__(self, max_sequence_length, d_model, vocab_size, rng, p=0.1):
+        super().__init__()
+        self.vocab_size = vocab_size
+        self.max_sequence_length = max_sequence_length
+        self.embedding = nn.Embedding(vocab_size, d_model)
+        self.position_encoder = PositionalEncoding(d_model, max_sequence_length)
+        self.dropout = nn.Dropout(p=p)
+        _share(self, "_rng", rng)
+        self.salt = new_salt()
+
+    def forward(self, x):
+        p = self.dropout.p if self.training else 0.0
+        dtype = torch.bfloat16 if x.is_cuda else torch.float32
+        return embedding(x, self.embedding.weight, self.position_encoder.table, p, self._rng, self.salt,
+                         out_dtype=dtype)
+
+
+class MultiHeadAttention(nn.Module):
+    def __init__(self, d_model, num_heads):
+        super().__init__()
+        self.d_model = d_model
+        self.num_heads = num_heads
+        self.head_dim = d_model // num_heads
+        self.qkv_layer = nn.Linear(d_model, 3 * d_model)
+        self.linear_layer = nn.Linear(d_model, d_model)
+
+    def forward(self, x, mode="none", key_padding=None):
+        qkv = linear(x, self.qkv_layer.weight, self.qkv_layer.bias)
+        values = self_attention(qkv, self.num_heads, mode, key_padding)
+        return linear(values, self.linear_layer.weight, self.linear_layer.bias)
+
+
+class MultiHeadCrossAttention(nn.Module):
+    def __init__(self, d_model, num_heads):
+        super().__init__()
+        self.d_model = d_model
+        self.num_heads = num_heads
+        self.head_dim = d_model // num_heads
+        self.kv_layer = nn.Linear(d_model, 2 * d_model)
+        self.q_layer = nn.Linear(d_model, d_model)
+        self.linear_layer = nn.Linear(d_model, d_model)
+
+    def forward(self, x, y, mode="none", key_padding=None):
+        kv = linear(x, self.kv_layer.weight, self.kv_layer.bias)
+        q = linear(y, self.q_layer.weight, self.q_layer.bias)
+        values = cross_attention(q, kv, self.num_heads, mode, key_padding)
+        return linear(values, self.linear_layer.weight, self.linear_layer.bias)
+
+
+class LayerNormalization(nn.Module):
+    """transformer.py:86-101 (parameter names gamma/beta kept)."""
+
+    def __init__(self, parameters_shape, eps=1e-5):
+        super().__init__()
+        self.parameters_shape = list(parameters_shape)
+        self.eps = eps
+        self.gamma = nn.Parameter(torch.ones(parameters_shape))
+        self.beta = nn.Parameter(torch.zeros(parameters_shape))
+
+    def forward(self, inputs, residual=None, p=0.0, rng=None, salt=0):
+        return add_dropout_layernorm(inputs, residual, self.gamma, self.beta, p, rng, salt, self.eps)
+
+
+class PositionwiseFeedForward(nn.Module):
+    def __init__(self, d_model, hidden, drop_prob=0.1, rng=None):
+        super().__init__()
+        self.linear1 = nn.Linear(d_model, hidden)
+        self.linear2 = nn.Linear(hidden, d_model)
+        self.relu = nn.ReLU()
+        self.dropout = nn.Dropout(p=drop_prob)
+        _share(self, "_rng", rng)
+        self.salt = new_salt()
+
+    def forward(self, x):
+        p = self.dropout.p if self.training else 0.0
+        h = linear(x, self.linear1.weight, self.linear1.bias, act="relu", p=p, rng=self._rng, salt=self.salt)
+        return linear(h, self.linear2.weight, self.linear2.bias)
+
+
+class EncoderLayer(nn.Module):
+    def __init__(self, d_model, ffn_hidden, num_heads, drop_prob, rng):
+        super().__init__()
+        self.attention = MultiHeadAttention(d_model=d_model, num_heads=num_heads)
+        self.norm1 = LayerNormalization(parameters_shape=[d_model])
+        self.dropout1 = nn.Dropout(p=drop_prob)
+        self.ffn = PositionwiseFeedForward(d_model=d_model, hidden=ffn_hidden, drop_prob=drop_prob, rng=rng)
+        self.norm2 = LayerNormalization(parameters_shape=[d_model])
+        self.dropout2 = nn.Dropout(p=drop_prob)
+        _share(self, "_rng", rng)
+        self.salts = (new_salt(), new_salt())
+
+    def forward(self, x, mode="none", key_padding=None):
+        p1 = self.dropout1.p if self.training else 0.0
+        p2 = self.dropout2.p if self.training else 0.0
+        a = self.attention(x, mode, key_padding)
+        x = self.norm1(a, x, p1, self._rng, self.salts[0])
+        f = self.ffn(x)
+        return self.norm2(f, x, p2, self._rng, self.salts[1])
+
+
+class SequentialEncoder(nn.Sequential):
+    def forward(self, *inputs):
+        x, mode, key_padding = inputs
+        for module in self._modules.values():
+            x = module(x, mode, key_padding)
+        return x
+
+
+class Encoder(nn.Module):
+    def __init__(self, d_model, ffn_hidden, num_heads, drop_prob, num_layers, max_sequence_length, vocab_size, rng,
+                 emb_dropout=0.1):
+        super().__init__()
+        self.sentence_embedding = SentenceEmbedding(max_sequence_length, d_model, vocab_size, rng, emb_dropout)
+        self.layers = SequentialEncoder(*[EncoderLayer(d_model, ffn_hidden, num_heads, drop_prob, rng)
+                                          for _ in range(num_layers)])
+
+    def forward(self, x, mode="none", key_padding=None):
+        x = self.sentence_embedding(x)
+        return self.layers(x, mode, key_padding)
+
+
+class DecoderLayer(nn.Module):
+    def __init__(self, d_model, ffn_hidden, num_heads, drop_prob, rng):
+        super().__init__()
+        self.self_attention = MultiHeadAttention(d_model=d_model, num_heads=num_heads)
+        self.layer_norm1 = LayerNormalization(parameters_shape=[d_model])
+        self.dropout1 = nn.Dropout(p=drop_prob)
+        self.encoder_decoder_attention = MultiHeadCrossAttention(d_model=d_model, num_heads=num_heads)
+        self.layer_norm2 = LayerNormalization(parameters_shape=[d_model])
+        self.dropout2 = nn.Dropout(p=drop_prob)
+        self.ffn = PositionwiseFeedForward(d_model=d_model, hidden=ffn_hidden, drop_prob=drop_prob, rng=rng)
+        self.layer_norm3 = LayerNormalization(parameters_shape=[d_model])
+        self.dropout3 = nn.Dropout(p=drop_prob)
+        _share(self, "_rng", rng)
+        self.salts = (new_salt(), new_salt(), new_salt())
+
+    def forward(self, x, y, self_mode="none", cross_mode="none", key_padding=None):
+        ps = [d.p if self.training else 0.0 for d in (self.dropout1, self.dropout2, self.dropout3)]
+        a = self.self_attention(y, self_mode)
+        y = self.layer_norm1(a, y, ps[0], self._rng, self.salts[0])
+        c = self.encoder_decoder_attention(x, y, cross_mode, key_padding)
+        y = self.layer_norm2(c, y, ps[1], self._rng, self.salts[1])
+        f = self.ffn(y)
+        return self.layer_norm3(f, y, ps[2], self._rng, self.salts[2])
+
+
+class SequentialDecoder(nn.Sequential):
+    def forward(self, *inputs):
+        x, y, self_mode, cross_mode, key_padding = inputs
+        for module in self._modules.values():
+            y = module(x, y, self_mode, cross_mode, key_padding)
+        return y
+
+
+class Decoder(nn.Module):
+    def __init__(self, d_model, ffn_hidden, num_heads, drop_prob, num_layers, max_sequence_length, vocab_size, rng,
+                 emb_dropout=0.1):
+        super().__init__()
+        self.sentence_embedding = SentenceEmbedding(max_sequence_length, d_model, vocab_size, rng, emb_dropout)
+        self.layers = SequentialDecoder(*[DecoderLayer(d_model, ffn_hidden, num_heads, drop_prob, rng)
+                                          for _ in range(num_layers)])
+
+    def forward(self, x, y, self_mode="none", cross_mode="none", key_padding=None):
+        y = self.sentence_embedding(y)
+        return self.layers(x, y, self_mode, cross_mode, key_padding)
+
+
+class Transformer(nn.Module):
+    """transformer.py:255-284.  ``forward(x, y, ...)`` returns logits [B, S, tgt_vocab]."""
+
+    def __init__(self, d_model=512, ffn_hidden=1024, num_heads=8, drop_prob=0.1, num_layers=1,
+                 max_sequence_length=200, de_vocab_size=10000, src_vocab_size=None, tgt_vocab_size=None,
+                 mask_mode="reference", emb_dropout=0.1, pad_id=0, seed=0):
+        super().__init__()
+        src_vocab_size = src_vocab_size or de_vocab_size
+        tgt_vocab_size = tgt_vocab_size or de_vocab_size
+        self.config = TransformerConfig(d_model, ffn_hidden, num_heads, drop_prob, num_layers, max_sequence_length,
+                                        src_vocab_size, tgt_vocab_size, emb_dropout, mask_mode, pad_id)
+        self.rng = DropoutRNG(seed)
+        self.encoder = Encoder(d_model, ffn_hidden, num_heads, drop_prob, num_layers, max_sequence_length,
+                               src_vocab_size, self.rng, emb_dropout)
+        self.decoder = Decoder(d_model, ffn_hidden, num_heads, drop_prob, num_layers, max_sequence_length,
+                               tgt_vocab_size, self.rng, emb_dropout)
+        self.linear = nn.Linear(d_model, tgt_vocab_size)
+
+    @classmethod
+    def from_config(cls, cfg: TransformerConfig, seed=0):
+        return cls(cfg.d_model, cfg.ffn_hidden, cfg.num_heads, cfg.drop_prob, cfg.num_layers,
+                   cfg.max_sequence_length, cfg.tgt_vocab_size, cfg.src_vocab_size, cfg.tgt_vocab_size,
+                   cfg.mask_mode, cfg.emb_dropout, cfg.pad_id, seed)
+
+    def _modes(self, x, encoder_self_attention_mask, decoder_self_attention_mask, decoder_cross_attention_mask):
+        if self.config.mask_mode == "reference":
+            # Q6: padding mask -> no-op; any look-ahead mask -> +1.0 on strictly-past keys
+            self_mode = "reference" if decoder_self_attention_mask is not None else "none"
+            cross_mode = "reference" if decoder_cross_attention_mask is not None else "none"
+            return "none", self_mode, cross_mode, None
+        key_padding = (x == self.config.pad_id)
+        return "none", "causal", "none", key_padding
+
+    def forward(self, x, y, encoder_self_attention_mask=None, decoder_self_attention_mask=None,
+                decoder_cross_attention_mask=None, enc_key_padding=None):
+        enc_mode, self_mode, cross_mode, kp = self._modes(x, encoder_self_attention_mask,
+                                                          decoder_self_attention_mask, decoder_cross_attention_mask)
+        if enc_key_padding is not None:
+            kp = enc_key_padding
+        x = self.encoder(x, enc_mode, kp)
+        out = self.decoder(x, y, self_mode, cross_mode, kp)
+        return linear(out, self.linear.weight, self.linear.bias)
+
+    def loss(self, logits, target):
+        """Token CE ignoring pad, mean over non-pad targets (pytorch_machine_translator.py:182-188)."""
+        return cross_entropy(logits, target, ignore_index=self.config.pad_id)
+
+    def training_step_loss(self, src, tgt, shift_targets=False):
+        """Reference recipe (Q7: decoder input == target, no shift) or shifted teacher forcing."""
+        if shift_targets:
+            dec_in, target = tgt[:, :-1], tgt[:, 1:]
+        else:
+            dec_in, target = tgt, tgt
+        la = torch.ones(1, dtype=torch.bool)  # marker: look-ahead mask present
+        logits = self(src, dec_in, None, la, la)
+        return self.loss(logits, target)
+
+
+def create_look_ahead_mask(size):
+    """pytorch_machine_translator.py:102-104."""
+    mask = torch.tril(torch.ones(size, size)) == 0
+    return mask.unsqueeze(0).unsqueeze(0)

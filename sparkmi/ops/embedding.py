@@ -1,0 +1,86 @@
+"""Embedding gather (+ optional positional-encoding add + dropout) and its scatter-add backward.
+
+Reference: SentenceEmbedding (transformer.py:44-62: dropout_{0.1}(Embedding(x) + PE)) and the
+LSTM's nn.Embedding(V, 32, padding_idx) (distributed_lstm.py:115).  GPU:
+csrc/kernels/embedding.hip; the weight gradient is accumulated in fp32 straight into the
+(flat) gradient buffer, rows equal to padding_idx receive no gradient.
+"""
+import math
+
+import torch
+
+from .. import _native
+from . import rng as _rng
+from ._grad import bf16_weight, grad_buf, grad_ready
+
+
+def sinusoid_table(max_len: int, d_model: int) -> torch.Tensor:
+    """Positional-encoding table identical to transformer.py:33-42 (interleaved sin/cos, fp32)."""
+    even_i = torch.arange(0, d_model, 2).float()
+    denominator = torch.pow(10000, even_i / d_model)
+    position = torch.arange(max_len).reshape(max_len, 1)
+    even_pe = torch.sin(position / denominator)
+    odd_pe = torch.cos(position / denominator)
+    return torch.stack([even_pe, odd_pe], dim=2).flatten(start_dim=1, end_dim=2)
+
+
+class EmbeddingFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, weight, pe, p, rng, salt, padding_idx, out_dtype):
+        B = ids.shape
+        D = weight.shape[1]
+        T = ids.numel()
+        S = ids.shape[-1]
+        ctx.p, ctx.rng, ctx.salt, ctx.pad = p, rng, salt, -1 if padding_idx is None else padding_idx
+        ctx.native = _native.use_native(ids)
+        ids_c = ids.contiguous().to(torch.int64)
+        if ctx.native:
+            C = _native.C()
+            out = torch.empty(*B, D, device=ids.device, dtype=torch.bfloat16)
+            if pe is not None and pe.shape[0] < S:
+                raise ValueError(f"sequence length {S} exceeds positional table {pe.shape[0]}")
+            C.emb_fwd(ids_c.data_ptr(), bf16_weight(weight).data_ptr(), _native.ptr(pe), out.data_ptr(), T, D,
+                      S if pe is not None else 1, rng.ptr(), salt, _rng.threshold(p), _rng.scale(p),
+                      _native.stream())
+            ctx.seed = 0
+        else:
+            x = weight.float()[ids_c]
+            if pe is not None:
+                x = x + pe[:S].float()
+            ctx.seed = rng.current() if p > 0 else 0
+            if p > 0:
+                x = x * _rng.keep_mask(x.shape, p, ctx.seed, salt, x.device).to(x.dtype) * _rng.scale(p)
+            out = x.to(out_dtype)
+        ctx.save_for_backward(ids_c, weight)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        ids, weight = ctx.saved_tensors
+        D = weight.shape[1]
+        T = ids.numel()
+        gw = grad_buf(weight)
+        if ctx.native:
+            C = _native.C()
+            dout = dout.contiguous()
+            C.emb_bwd(ids.data_ptr(), dout.data_ptr(), gw.data_ptr(), T, D, ctx.pad, ctx.rng.ptr(), ctx.salt,
+                      _rng.threshold(ctx.p), _rng.scale(ctx.p), _native.stream())
+        else:
+            g = dout.float()
+            if ctx.p > 0:
+                g = g * _rng.keep_mask(g.shape, ctx.p, ctx.seed, ctx.salt, g.device).to(g.dtype) * _rng.scale(ctx.p)
+            g = g.reshape(T, D)
+            idf = ids.reshape(T)
+            if ctx.pad >= 0:
+                keep = idf != ctx.pad
+                g, idf = g[keep], idf[keep]
+            gw.index_add_(0, idf, g)
+        grad_ready(weight)
+        return None, None, None, None, None, None, None, None
+
+
+def embedding(ids, weight, pe=None, p=0.0, rng=None, salt=0, padding_idx=None, out_dtype=torch.float32):
+    if rng is None:
+        from .layernorm import _NULL_RNG
+        rng, p = _NULL_RNG, 0.0
+    return EmbeddingFn.apply(ids, weight, pe, float(p), rng, int(salt), padding_idx, out_dtype)

@@ -1,0 +1,64 @@
+"""Softmax cross-entropy with ignore_index, mean over non-ignored targets.
+
+Reference: CrossEntropyLoss(ignore_index=0, reduction='none') + masked mean
+(pytorch_machine_translator.py:125-126,182-188) and plain mean CE
+(distributed_cnn.py:141, distributed_lstm.py:142).  GPU: csrc/kernels/cross_entropy.hip —
+online logsumexp forward (loss accumulated on the device, valid-row count on the device),
+recompute-softmax backward writing the logit gradient in one pass.
+"""
+import torch
+
+from .. import _native
+
+
+class CrossEntropyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index):
+        V = logits.shape[-1]
+        x2 = logits.reshape(-1, V)
+        lab = labels.reshape(-1).to(torch.int64).contiguous()
+        M = x2.shape[0]
+        ctx.ignore = ignore_index
+        ctx.native = _native.use_native(logits) and logits.dtype in (torch.bfloat16, torch.float32)
+        if ctx.native:
+            C = _native.C()
+            x2 = x2.contiguous()
+            lse = torch.empty(M, device=x2.device, dtype=torch.float32)
+            stats = torch.empty(2, device=x2.device, dtype=torch.float32)  # [count, loss]
+            C.ce_fwd(x2.data_ptr(), int(x2.dtype == torch.bfloat16), lab.data_ptr(), M, V, ignore_index,
+                     lse.data_ptr(), stats[0:1].data_ptr(), stats[1:2].data_ptr(), 0, _native.stream())
+            ctx.save_for_backward(x2, lab, lse, stats)
+            ctx.shape = logits.shape
+            return stats[1].clone()
+        xf = x2.float()
+        lse = torch.logsumexp(xf, dim=-1)
+        valid = lab != ignore_index
+        safe = torch.where(valid, lab, torch.zeros_like(lab))
+        rl = (lse - xf.gather(1, safe[:, None]).squeeze(1)) * valid.float()
+        count = valid.float().sum()
+        ctx.save_for_backward(x2, lab, lse, count.reshape(1))
+        ctx.shape = logits.shape
+        return (rl.sum() / count.clamp_min(1.0)).to(torch.float32)
+
+    @staticmethod
+    def backward(ctx, dloss):
+        x2, lab, lse, stats = ctx.saved_tensors
+        M, V = x2.shape
+        if ctx.native:
+            C = _native.C()
+            grad = torch.empty_like(x2)
+            dl = dloss.reshape(1).to(torch.float32).contiguous()
+            C.ce_bwd(x2.data_ptr(), int(x2.dtype == torch.bfloat16), lab.data_ptr(), M, V, ctx.ignore, lse.data_ptr(),
+                     stats[0:1].data_ptr(), dl.data_ptr(), grad.data_ptr(), _native.stream())
+            return grad.reshape(ctx.shape), None, None
+        count = stats[0].clamp_min(1.0)
+        p = torch.exp(x2.float() - lse[:, None])
+        valid = lab != ctx.ignore
+        safe = torch.where(valid, lab, torch.zeros_like(lab))
+        p[torch.arange(M), safe] -= 1.0
+        p = p * (valid.float() * dloss / count)[:, None]
+        return p.to(x2.dtype).reshape(ctx.shape), None, None
+
+
+def cross_entropy(logits, labels, ignore_index=-100):
+    return CrossEntropyFn.apply(logits, labels, int(ignore_index))

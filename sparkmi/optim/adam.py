@@ -1,0 +1,95 @@
+"""Adam / AdamW over a :class:`FlatParams` buffer.
+
+torch.optim.Adam semantics (pytorch_machine_translator.py:129, distributed_lstm.py:141):
+m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2; p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps).
+``grad_scale`` multiplies the gradient first (1/world for data-parallel averaging folded in).
+lr and the step counter are device tensors, so the update is HIP-graph capturable.
+"""
+import torch
+
+from .. import _native
+
+
+class _FlatOptimizer:
+    def __init__(self, flat, lr):
+        self.flat = flat
+        dev = flat.device
+        self.lr_t = torch.tensor([float(lr)], dtype=torch.float32, device=dev)
+        self.step_t = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.grad_scale = 1.0
+        self.zero_grad_after_step = True
+
+    @property
+    def lr(self):
+        return float(self.lr_t.item())
+
+    def set_lr(self, lr):
+        self.lr_t.fill_(float(lr))
+
+    def zero_grad(self, set_to_none=False):
+        self.flat.zero_grad()
+
+    def state_dict(self):
+        return {"lr": self.lr_t.clone(), "step": self.step_t.clone()}
+
+    def load_state_dict(self, sd):
+        self.lr_t.copy_(sd["lr"])
+        self.step_t.copy_(sd["step"])
+
+
+class Adam(_FlatOptimizer):
+    adamw = False
+
+    def __init__(self, flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        super().__init__(flat, lr)
+        self.b1, self.b2 = betas
+        self.eps = eps
+        self.weight_decay = weight_decay
+        self.m = torch.zeros_like(flat.master)
+        self.v = torch.zeros_like(flat.master)
+
+    def step(self):
+        f = self.flat
+        if _native.use_native(f.master):
+            C = _native.C()
+            st = _native.stream()
+            C.step_inc(self.step_t.data_ptr(), st)
+            C.adam(f.master.data_ptr(), f.grad.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), _native.ptr(f.shadow),
+                   f.numel, self.lr_t.data_ptr(), self.step_t.data_ptr(), self.b1, self.b2, self.eps,
+                   self.weight_decay, self.grad_scale, int(self.adamw), int(self.zero_grad_after_step), st)
+            return
+        with torch.no_grad():
+            self.step_t.add_(1)
+            t = float(self.step_t.item())
+            lr = float(self.lr_t.item())
+            g = f.grad * self.grad_scale
+            p = f.master
+            if self.weight_decay:
+                if self.adamw:
+                    p.mul_(1 - lr * self.weight_decay)
+                else:
+                    g = g + self.weight_decay * p
+            self.m.mul_(self.b1).add_(g, alpha=1 - self.b1)
+            self.v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+            bc1 = 1 - self.b1 ** t
+            bc2 = 1 - self.b2 ** t
+            denom = self.v.sqrt() / (bc2 ** 0.5) + self.eps
+            p.addcdiv_(self.m, denom, value=-lr / bc1)
+            if self.zero_grad_after_step:
+                f.grad.zero_()
+            if f.shadow is not None:
+                f.shadow.copy_(p.to(torch.bfloat16))
+
+    def state_dict(self):
+        sd = super().state_dict()
+        sd.update(m=self.m.clone(), v=self.v.clone())
+        return sd
+
+    def load_state_dict(self, sd):
+        super().load_state_dict(sd)
+        self.m.copy_(sd["m"])
+        self.v.copy_(sd["v"])
+
+
+class AdamW(Adam):
+    adamw = True

@@ -1,0 +1,102 @@
+"""Synchronous data parallelism with bucketed, backward-overlapped gradient all-reduce.
+
+This is what the reference *intended* with DDP but never executed (the raw
+module was called, so gradients were never synchronised).  Design for MI355X + RCCL/xGMI:
+
+* gradients already live in ONE flat fp32 buffer (sparkmi.utils.flat.FlatParams), laid out in
+  reverse layer order, so buckets are plain contiguous slices — no pack/unpack kernels;
+* a bucket's all-reduce is issued the moment its last parameter's backward kernel has been
+  enqueued (ops call ``grad_ready``), on RCCL's stream, so communication of late layers runs
+  under the backward of early layers;
+* buckets are large (default 64 MiB): an 8-GPU ring over xGMI is per-link bandwidth bound, and
+  fewer, larger collectives amortise the per-call latency;
+* averaging is folded into the optimizer (``grad_scale = 1/world``) instead of a division
+  pass over the buffer.
+The CPU/gloo path runs the identical logic (multi-process CPU tests).
+"""
+import torch
+import torch.distributed as dist
+
+from ..ops import _grad
+
+
+def broadcast_flat(flat, src=0, group=None):
+    """Rank-0 parameter broadcast (the DDP-constructor sync of distributed.py:862-867)."""
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.broadcast(flat.master, src=src, group=group)
+        flat.refresh_shadow()
+
+
+class DataParallel:
+    def __init__(self, flat, group=None, bucket_mb=64.0, overlap=True, broadcast=True):
+        self.flat = flat
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.overlap = overlap
+        self.buckets = []  # (start, end, param indices)
+        limit = int(bucket_mb * (1 << 20) / 4)
+        cur, start = [], 0
+        for i, p in enumerate(flat.params):
+            s = flat.offsets[i]
+            e = flat.offsets[i + 1] if i + 1 < len(flat.params) else flat.numel
+            if cur and (e - start) > limit:
+                self.buckets.append((start, s, cur))
+                cur, start = [], s
+            cur.append(i)
+        if cur:
+            self.buckets.append((start, flat.numel, cur))
+        self.bucket_of = {}
+        for b, (_, _, idx) in enumerate(self.buckets):
+            for i in idx:
+                self.bucket_of[i] = b
+        self._pending = None
+        self._works = []
+        self._listener = None
+        if self.world > 1:
+            if broadcast:
+                broadcast_flat(flat, 0, group)
+            if overlap:
+                self._listener = _grad.add_listener(self._on_ready)
+        self.reset()
+
+    def reset(self):
+        self._pending = [len(idx) for (_, _, idx) in self.buckets]
+        self._launched = [False] * len(self.buckets)
+        self._works = []
+
+    def _launch(self, b):
+        if self._launched[b]:
+            return
+        s, e, _ = self.buckets[b]
+        self._launched[b] = True
+        w = dist.all_reduce(self.flat.grad[s:e], group=self.group, async_op=True)
+        self._works.append(w)
+
+    def _on_ready(self, p):
+        i = self.flat.index.get(id(p))
+        if i is None or self._pending is None:
+            return
+        b = self.bucket_of[i]
+        self._pending[b] -= 1
+        if self._pending[b] == 0:
+            self._launch(b)
+
+    def finish(self):
+        """Complete every bucket's all-reduce (launching any not yet issued) before the optimizer."""
+        if self.world <= 1:
+            self.reset()
+            return
+        for b in range(len(self.buckets)):
+            self._launch(b)
+        for w in self._works:
+            w.wait()
+        self.reset()
+
+    @property
+    def grad_scale(self):
+        return 1.0 / self.world
+
+    def close(self):
+        if self._listener is not None:
+            _grad.remove_listener(self._listener)
+            self._listener = None

@@ -1,0 +1,62 @@
+"""Training-step executor: eager or HIP-graph-captured, optionally data-parallel.
+
+A "step" = dropout-seed bump -> forward -> loss -> backward (gradients land in the flat fp32
+buffer, bucketed all-reduce overlapped when data-parallel) -> fused optimizer launch.
+With ``graph=True`` (single process) the whole step is captured once into a hipGraph after
+a few eager warm-up steps and then replayed: one host launch per step instead of hundreds,
+which matters at the reference's small per-GPU batches.  Inputs are
+copied into static device buffers before each replay.
+"""
+import torch
+
+
+class StepRunner:
+    def __init__(self, model, loss_fn, optimizer, ddp=None, graph=False, warmup_eager=3):
+        self.model = model
+        self.loss_fn = loss_fn          # loss_fn(model, *batch) -> scalar loss tensor
+        self.opt = optimizer
+        self.ddp = ddp
+        self.graph_requested = graph
+        self.warmup_eager = warmup_eager
+        self.graph = None
+        self.static_in = None
+        self.static_loss = None
+        self.steps = 0
+        if ddp is not None:
+            optimizer.grad_scale = ddp.grad_scale
+
+    def _eager(self, *batch):
+        rng = getattr(self.model, "rng", None)
+        if rng is not None:
+            rng.advance()
+        loss = self.loss_fn(self.model, *batch)
+        loss.backward()
+        if self.ddp is not None:
+            self.ddp.finish()
+        self.opt.step()
+        return loss.detach()
+
+    def _capture(self, batch):
+        self.static_in = [b.clone() for b in batch]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._eager(*self.static_in)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.static_loss = self._eager(*self.static_in)
+        self.graph = g
+
+    def step(self, *batch):
+        self.steps += 1
+        use_graph = self.graph_requested and batch[0].is_cuda and (self.ddp is None or self.ddp.world == 1)
+        if not use_graph or self.steps <= self.warmup_eager:
+            return self._eager(*batch)
+        if self.graph is None:
+            self._capture(batch)
+        for dst, src in zip(self.static_in, batch):
+            dst.copy_(src, non_blocking=True)
+        self.graph.replay()
+        return self.static_loss

@@ -1,0 +1,79 @@
+"""Flat parameter / gradient / bf16-shadow storage for a model.
+
+All trainable parameters of a module are re-pointed into ONE contiguous fp32 master buffer
+(``p.data`` becomes a view), their ``.grad`` into ONE fp32 gradient buffer, and (on GPU) a bf16
+compute shadow is kept in a third buffer (``p._smi_bf16``).  Consequences on MI355X:
+  * the optimizer is a single fused HIP launch over the whole model (csrc/kernels/optim.hip),
+    which also refreshes the bf16 shadow — no multi-tensor-apply bookkeeping;
+  * data-parallel gradient sync works on large contiguous buckets of the gradient buffer
+    (few, big RCCL all-reduces — what xGMI rings want);
+  * parameters are laid out in REVERSE registration order, so the backward pass finishes the
+    front of the buffer first and bucket 0 can be all-reduced while backward continues.
+Each parameter starts on a 64-element boundary (256-B aligned fp32, 128-B aligned bf16).
+"""
+import torch
+
+from .. import _native
+
+ALIGN = 64
+
+
+def _round(n, a=ALIGN):
+    return (n + a - 1) // a * a
+
+
+class FlatParams:
+    def __init__(self, module: torch.nn.Module, device=None, reverse=True, shadow=None):
+        params = []
+        seen = set()
+        for name, p in module.named_parameters():
+            if p.requires_grad and id(p) not in seen:
+                seen.add(id(p))
+                params.append((name, p))
+        if reverse:
+            params = params[::-1]
+        device = torch.device(device) if device is not None else (params[0][1].device if params else torch.device("cpu"))
+        self.device = device
+        self.names = [n for n, _ in params]
+        self.params = [p for _, p in params]
+        self.offsets = []
+        off = 0
+        for p in self.params:
+            self.offsets.append(off)
+            off += _round(p.numel())
+        self.numel = off
+        self.master = torch.zeros(off, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(off, dtype=torch.float32, device=device)
+        use_shadow = device.type == "cuda" if shadow is None else shadow
+        self.shadow = torch.zeros(off, dtype=torch.bfloat16, device=device) if use_shadow else None
+        with torch.no_grad():
+            for p, o in zip(self.params, self.offsets):
+                n = p.numel()
+                self.master[o:o + n].copy_(p.data.reshape(-1).to(device=device, dtype=torch.float32))
+                p.data = self.master[o:o + n].view(p.shape)
+                p.grad = self.grad[o:o + n].view(p.shape)
+                if self.shadow is not None:
+                    p._smi_bf16 = self.shadow[o:o + n].view(p.shape)
+        self.index = {id(p): i for i, p in enumerate(self.params)}
+        self.refresh_shadow()
+
+    def refresh_shadow(self):
+        if self.shadow is None:
+            return
+        if _native.use_native(self.master):
+            _native.C().cast_f32_bf16(self.master.data_ptr(), self.shadow.data_ptr(), self.numel, _native.stream())
+        else:
+            self.shadow.copy_(self.master.to(torch.bfloat16))
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def param_range(self, p):
+        i = self.index[id(p)]
+        return self.offsets[i], self.offsets[i] + p.numel()
+
+    def nbytes(self):
+        return self.master.numel() * 4
+
+    def state_dict_view(self):
+        return {n: p for n, p in zip(self.names, self.params)}

@@ -1,0 +1,209 @@
+"""T4: every HIP kernel against the fp32 torch reference path of the same op (same dropout
+mask via the shared counter-based hash).  Runs on an MI355X only."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from sparkmi import _native  # noqa: E402
+from sparkmi.ops import rng as R  # noqa: E402
+from sparkmi.ops.attention import cross_attention, self_attention  # noqa: E402
+from sparkmi.ops.embedding import embedding, sinusoid_table  # noqa: E402
+from sparkmi.ops.layernorm import add_dropout_layernorm  # noqa: E402
+from sparkmi.ops.linear import linear  # noqa: E402
+from sparkmi.ops.loss import cross_entropy  # noqa: E402
+
+dev = "cuda"
+
+
+def _close(a, b, atol, rtol, msg=""):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol)
+    assert not bad.any(), f"{msg}: {bad.sum().item()} / {bad.numel()} mismatches, max err {err.max().item():.4g}"
+
+
+def test_native_loaded():
+    C = _native.C()
+    assert C.ARCH == "gfx950"
+    assert "_C" in C.__file__
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_layernorm(p):
+    torch.manual_seed(0)
+    M, D = 1000, 512
+    rng_g, rng_c = R.DropoutRNG(7).to(dev), R.DropoutRNG(7)
+    h = torch.randn(M, D)
+    r = torch.randn(M, D)
+    gamma = torch.nn.Parameter(torch.randn(D) * 0.5 + 1)
+    beta = torch.nn.Parameter(torch.randn(D) * 0.1)
+    gamma_g = torch.nn.Parameter(gamma.detach().to(dev))
+    beta_g = torch.nn.Parameter(beta.detach().to(dev))
+    hb, rb = h.bfloat16(), r.bfloat16()
+    hg = hb.to(dev).requires_grad_()
+    rg = rb.to(dev).requires_grad_()
+    hc = hb.float().requires_grad_()
+    rc = rb.float().requires_grad_()
+    yg = add_dropout_layernorm(hg, rg, gamma_g, beta_g, p, rng_g, 1234)
+    yc = add_dropout_layernorm(hc, rc, gamma, beta, p, rng_c, 1234)
+    _close(yg, yc, 3e-2, 2e-2, "ln fwd")
+    dy = torch.randn(M, D).bfloat16()
+    yg.backward(dy.to(dev))
+    yc.backward(dy.float())
+    _close(hg.grad, hc.grad, 3e-2, 3e-2, "dh")
+    _close(rg.grad, rc.grad, 3e-2, 3e-2, "dres")
+    _close(gamma_g.grad, gamma.grad, 0.5, 2e-2, "dgamma")
+    _close(beta_g.grad, beta.grad, 0.5, 2e-2, "dbeta")
+
+
+def _attn_case(B, H, Sq, Sk, mode, cross, kp):
+    torch.manual_seed(1)
+    hd = 64
+    if cross:
+        q = torch.randn(B, Sq, H * hd).bfloat16()
+        kv = torch.randn(B, Sk, 2 * H * hd).bfloat16()
+        kpad = None
+        if kp:
+            kpad = torch.zeros(B, Sk, dtype=torch.bool)
+            kpad[0, Sk // 2:] = True
+        qg, kvg = q.to(dev).requires_grad_(), kv.to(dev).requires_grad_()
+        qc, kvc = q.float().requires_grad_(), kv.float().requires_grad_()
+        og = cross_attention(qg, kvg, H, mode, kpad.to(dev) if kpad is not None else None)
+        oc = cross_attention(qc, kvc, H, mode, kpad)
+        do = torch.randn_like(oc).bfloat16()
+        og.backward(do.to(dev))
+        oc.backward(do.float())
+        _close(og, oc, 2e-2, 2e-2, f"attn fwd {mode}")
+        _close(qg.grad, qc.grad, 3e-2, 3e-2, "dq")
+        _close(kvg.grad, kvc.grad, 3e-2, 3e-2, "dkv")
+    else:
+        qkv = torch.randn(B, Sq, 3 * H * hd).bfloat16()
+        qg = qkv.to(dev).requires_grad_()
+        qc = qkv.float().requires_grad_()
+        og = self_attention(qg, H, mode)
+        oc = self_attention(qc, H, mode)
+        do = torch.randn_like(oc).bfloat16()
+        og.backward(do.to(dev))
+        oc.backward(do.float())
+        _close(og, oc, 2e-2, 2e-2, f"attn fwd {mode}")
+        _close(qg.grad, qc.grad, 3e-2, 3e-2, f"dqkv {mode}")
+
+
+@pytest.mark.parametrize("mode", ["none", "reference", "causal"])
+@pytest.mark.parametrize("S", [256, 200, 37])
+def test_self_attention(mode, S):
+    _attn_case(2, 4, S, S, mode, False, False)
+
+
+@pytest.mark.parametrize("mode", ["none", "reference"])
+@pytest.mark.parametrize("kp", [False, True])
+def test_cross_attention(mode, kp):
+    _attn_case(2, 3, 130, 130 if mode == "reference" else 77, mode, True, kp)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_cross_entropy(dtype):
+    torch.manual_seed(2)
+    M, V = 777, 10000
+    x = torch.randn(M, V).to(dtype)
+    lab = torch.randint(0, V, (M,))
+    lab[:50] = 0
+    xg = x.to(dev).requires_grad_()
+    xc = x.float().requires_grad_()
+    lg = cross_entropy(xg, lab.to(dev), ignore_index=0)
+    lc = cross_entropy(xc, lab, ignore_index=0)
+    ref = torch.nn.functional.cross_entropy(x.float(), lab, ignore_index=0)
+    _close(lg, ref, 1e-3, 1e-3, "ce loss")
+    _close(lc, ref, 1e-5, 1e-5, "ce loss ref")
+    lg.backward()
+    lc.backward()
+    _close(xg.grad, xc.grad, 1e-5, 2e-2, "ce grad")
+
+
+def test_embedding():
+    torch.manual_seed(3)
+    V, D, B, S = 1000, 512, 4, 64
+    w = torch.nn.Parameter(torch.randn(V, D))
+    wg = torch.nn.Parameter(w.detach().to(dev))
+    ids = torch.randint(0, V, (B, S))
+    ids[0, :5] = 7
+    pe = sinusoid_table(S, D)
+    rg, rc = R.DropoutRNG(3).to(dev), R.DropoutRNG(3)
+    og = embedding(ids.to(dev), wg, pe.to(dev), 0.1, rg, 99, padding_idx=7)
+    oc = embedding(ids, w, pe, 0.1, rc, 99, padding_idx=7)
+    _close(og, oc, 2e-2, 1e-2, "emb fwd")
+    do = torch.randn(B, S, D).bfloat16()
+    og.backward(do.to(dev))
+    oc.backward(do.float())
+    _close(wg.grad, w.grad, 2e-2, 2e-2, "emb grad")
+    assert float(wg.grad[7].abs().sum()) == 0.0
+
+
+@pytest.mark.parametrize("act,p", [(None, 0.0), ("relu", 0.1), ("relu", 0.0)])
+def test_linear(act, p):
+    torch.manual_seed(4)
+    M, K, N = 512, 256, 384
+    lin = torch.nn.Linear(K, N)
+    wg = torch.nn.Parameter(lin.weight.detach().to(dev))
+    bg = torch.nn.Parameter(lin.bias.detach().to(dev))
+    x = torch.randn(M, K).bfloat16()
+    xg = x.to(dev).requires_grad_()
+    xc = x.float().requires_grad_()
+    rg, rc = R.DropoutRNG(5).to(dev), R.DropoutRNG(5)
+    yg = linear(xg, wg, bg, act, p, rg, 11)
+    yc = linear(xc, lin.weight, lin.bias, act, p, rc, 11)
+    _close(yg, yc, 5e-2, 2e-2, "linear fwd")
+    dy = torch.randn(M, N).bfloat16()
+    yg.backward(dy.to(dev))
+    yc.backward(dy.float())
+    _close(xg.grad, xc.grad, 5e-2, 3e-2, "dx")
+    _close(wg.grad, lin.weight.grad, 0.5, 3e-2, "dw")
+    _close(bg.grad, lin.bias.grad, 0.5, 3e-2, "db")
+
+
+def test_adam_sgd_flat():
+    from sparkmi.optim import SGD, Adam
+    from sparkmi.utils.flat import FlatParams
+    torch.manual_seed(5)
+    for Opt, kw in ((Adam, dict(lr=1e-2, weight_decay=0.01)), (SGD, dict(lr=0.1, momentum=0.9))):
+        mc = torch.nn.Sequential(torch.nn.Linear(33, 17), torch.nn.Linear(17, 5))
+        mg = torch.nn.Sequential(torch.nn.Linear(33, 17), torch.nn.Linear(17, 5)).to(dev)
+        mg.load_state_dict(mc.state_dict())
+        fc, fg = FlatParams(mc), FlatParams(mg)
+        oc, og = Opt(fc, **kw), Opt(fg, **kw)
+        for _ in range(3):
+            g = torch.randn(fc.numel)
+            fc.grad.copy_(g)
+            fg.grad.copy_(g.to(dev))
+            oc.step()
+            og.step()
+        _close(fg.master, fc.master, 1e-5, 1e-5, Opt.__name__)
+        _close(fg.shadow, fg.master, 1e-2, 1e-2, "shadow")
+
+
+def test_transformer_gpu_vs_cpu():
+    import os
+    from safetensors.torch import load_file
+    from sparkmi.models.transformer import Transformer
+    from sparkmi.utils.flat import FlatParams
+    gold = load_file(os.path.join(os.path.dirname(__file__), "fixtures", "transformer_ref.safetensors"))
+    sd = {k[len("param."):]: v for k, v in gold.items() if k.startswith("param.")}
+    m = Transformer(d_model=128, ffn_hidden=256, num_heads=2, num_layers=2, max_sequence_length=16,
+                    src_vocab_size=50, tgt_vocab_size=60)
+    m.load_state_dict(sd)
+    m = m.to(dev).eval()
+    FlatParams(m)
+    la = torch.ones(1, dtype=torch.bool)
+    logits = m(gold["src"].to(dev), gold["tgt"].to(dev), None, la, la)
+    _close(logits, gold["logits"], 0.15, 0.05, "logits")
+    loss = m.loss(logits, gold["tgt"].to(dev))
+    _close(loss.reshape(1), gold["loss"], 2e-2, 2e-2, "loss")
+    loss.backward()
+    for name, p in m.named_parameters():
+        g = gold["grad." + name]
+        rel = (p.grad.cpu() - g).norm() / (g.norm() + 1e-6)
+        assert rel < 0.1, (name, float(rel))
