@@ -15,6 +15,10 @@ using u = uintptr_t;
 #define S(x) reinterpret_cast<hipStream_t>(x)
 
 #include "smi_attention.h"
+#include "smi_mlp.h"
+#include "smi_gemm.h"
+#include <pybind11/stl.h>
+#include <vector>
 
 extern "C" {
 int smi_ln_fwd(const void*, const void*, const float*, const float*, void*, void*, float*, float*, int, int, float,
@@ -35,6 +39,11 @@ int smi_colsum_bf16(const void*, long, int, float*, int, float*, int, hipStream_
 int smi_cast_f32_bf16(const float*, void*, long, hipStream_t);
 int smi_add_bf16(const void*, const void*, void*, long, hipStream_t);
 int smi_step_inc(float*, hipStream_t);
+int smi_mlp_fwd(const MLPArgs*, hipStream_t);
+int smi_gemm(const GemmArgs*, hipStream_t);
+int smi_gather_rows(const void*, const long long*, void*, long, long, hipStream_t);
+int smi_gather_u8_scale(const void*, const long long*, void*, long, long, float, int, hipStream_t);
+int smi_mlp_bwd(const MLPArgs*, hipStream_t);
 int smi_adam(float*, float*, float*, float*, void*, long, const float*, const float*, float, float, float, float, float,
              int, int, hipStream_t);
 int smi_sgd(float*, float*, float*, void*, long, const float*, const float*, float, float, float, int, float, int,
@@ -128,5 +137,40 @@ PYBIND11_MODULE(_C, m) {
                   float gscale, int zero_grad, u st) {
     chk(smi_sgd(PF(p), PF(g), PF(buf), P(pbf), n, PF(lr), PF(step), mom, damp, wd, nesterov, gscale, zero_grad, S(st)),
         "sgd");
+  });
+
+  // MLP: dims list, per-layer pointer lists (weights torch [out,in] layout, fp32)
+  m.def("mlp", [](int backward, u x, u y, u row_w, int n, std::vector<int> dims, std::vector<u> W, std::vector<u> b,
+                  std::vector<u> gW, std::vector<u> gb, u logits, u loss, u dloss, int act, u st) {
+    MLPArgs a{};
+    const int L = (int)dims.size() - 1;
+    if (L < 1 || L > MLP_MAXL || (int)W.size() != L || (int)b.size() != L) throw std::runtime_error("mlp: bad layer lists");
+    a.x = (const float*)x; a.y = (const long long*)y; a.row_w = (const float*)row_w; a.n = n; a.nlayers = L;
+    for (int i = 0; i <= L; ++i) a.dims[i] = dims[i];
+    for (int l = 0; l < L; ++l) {
+      a.W[l] = (const float*)W[l]; a.b[l] = (const float*)b[l];
+      a.gW[l] = backward ? (float*)gW.at(l) : nullptr; a.gb[l] = backward ? (float*)gb.at(l) : nullptr;
+    }
+    a.logits = (float*)logits; a.loss = (float*)loss; a.dloss = (const float*)dloss; a.act = act;
+    chk(backward ? smi_mlp_bwd(&a, S(st)) : smi_mlp_fwd(&a, S(st)), "mlp");
+  });
+
+  m.def("gemm", [](int mode, u A, long lda, u B, long ldb, int M, int N, int K, u C, long ldc, int out_f32, int atomic,
+                   int beta_acc, float alpha, u bias, u resid, long ldr, int act, u dact_y, long ldy, u seedp,
+                   uint32_t salt, uint32_t thresh, float dscale, int splits, u st) {
+    GemmArgs g{};
+    g.mode = mode; g.A = (const unsigned short*)A; g.lda = lda; g.B = (const unsigned short*)B; g.ldb = ldb;
+    g.M = M; g.N = N; g.K = K; g.C = (void*)C; g.ldc = ldc; g.out_f32 = out_f32; g.atomic = atomic;
+    g.beta_acc = beta_acc; g.alpha = alpha; g.bias = (const float*)bias; g.resid = (const unsigned short*)resid;
+    g.ldr = ldr; g.act = act; g.dact_y = (const unsigned short*)dact_y; g.ldy = ldy;
+    g.seedp = (const uint32_t*)seedp; g.salt = salt; g.thresh = thresh; g.dscale = dscale; g.splits = splits;
+    chk(smi_gemm(&g, S(st)), "gemm");
+  });
+
+  m.def("gather_rows", [](u src, u idx, u out, long n, long row_bytes, u st) {
+    chk(smi_gather_rows(P(src), (const long long*)idx, P(out), n, row_bytes, S(st)), "gather_rows");
+  });
+  m.def("gather_u8_scale", [](u src, u idx, u out, long n, long row, float scale, int bf16, u st) {
+    chk(smi_gather_u8_scale(P(src), (const long long*)idx, P(out), n, row, scale, bf16, S(st)), "gather_u8_scale");
   });
 }

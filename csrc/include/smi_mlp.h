@@ -1,0 +1,23 @@
+// Argument block shared by csrc/kernels/mlp.hip and csrc/bindings.cpp.
+#pragma once
+#define MLP_MAXL 6
+#define MLP_MAXW 32
+#define MLP_ACT_STRIDE (MLP_MAXW * (MLP_MAXL + 1))
+
+struct MLPArgs {
+  const float* x;            // [n, dims[0]] row-major
+  const long long* y;        // [n] class index
+  const float* row_w;        // [n] per-row loss weight or null (-> 1/n)
+  int n;
+  int nlayers;
+  int dims[MLP_MAXL + 1];
+  const float* W[MLP_MAXL];  // torch layout [out, in]
+  const float* b[MLP_MAXL];
+  float* gW[MLP_MAXL];
+  float* gb[MLP_MAXL];
+  float* logits;             // optional [n, C]
+  float* loss;               // scalar, accumulated
+  const float* dloss;        // scalar upstream gradient (bwd)
+  int act;                   // 1 relu, 2 sigmoid
+};
+

@@ -59,9 +59,10 @@ __global__ void act_drop_bwd_kernel(const unsigned short* __restrict__ dy, const
   *(u16x8_t*)(dx + i) = o;
 }
 
-// out[c] (+)= sum_r x[r][c]   (bf16 input [M,N], fp32 out).  Block = 256 threads covering
-// 64 columns x 4 row-phases... each thread sums 8 consecutive columns over a strided row set.
-__global__ void colsum_bf16_kernel(const unsigned short* __restrict__ x, long M, int N, float* __restrict__ part,
+// out[c] += sum_r x[r][c]  (bf16 [M,N] -> fp32 [N], accumulated into a gradient buffer).
+// Block = 32 column-vectors (8 columns each, 16-B loads) x 8 row phases over a 256-row chunk;
+// LDS reduce over the phases, then one fp32 atomic per column per block.  Single launch.
+__global__ void colsum_bf16_kernel(const unsigned short* __restrict__ x, long M, int N, float* __restrict__ out,
                                    int rows_per_block) {
   const int cv = blockIdx.x * 32 + (threadIdx.x & 31);  // column-vector index (8 cols each)
   const int rphase = threadIdx.x >> 5;                  // 0..7
@@ -70,33 +71,30 @@ __global__ void colsum_bf16_kernel(const unsigned short* __restrict__ x, long M,
   float acc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-  if (cv * 8 < N) {
+  if (cv * 8 + 8 <= N && (N % 8) == 0) {
     for (long r = r0 + rphase; r < r1; r += 8) {
       u16x8_t v = *(const u16x8_t*)(x + r * N + cv * 8);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[j]);
     }
+  } else if (cv * 8 < N) {  // ragged / unaligned rows: scalar loads
+    for (long r = r0 + rphase; r < r1; r += 8)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (cv * 8 + j < N) acc[j] += bf2f(x[r * N + cv * 8 + j]);
   }
   __shared__ float red[8][32 * 8 + 1];
 #pragma unroll
   for (int j = 0; j < 8; ++j) red[rphase][(threadIdx.x & 31) * 8 + j] = acc[j];
   __syncthreads();
-  for (int c = threadIdx.x; c < 256; c += 256) {
+  {
+    const int c = threadIdx.x;  // 256 columns per block
     float s = 0.f;
 #pragma unroll
     for (int p = 0; p < 8; ++p) s += red[p][c];
     const int col = blockIdx.x * 256 + c;
-    if (col < N) part[(long)blockIdx.y * N + col] = s;
+    if (col < N) atomicAdd(out + col, s);
   }
-}
-
-__global__ void colsum_final_kernel(const float* __restrict__ part, int nparts, int N, float* __restrict__ out,
-                                    int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= N) return;
-  float s = 0.f;
-  for (int p = 0; p < nparts; ++p) s += part[(long)p * N + c];
-  out[c] = accumulate ? out[c] + s : s;
 }
 
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ x, unsigned short* __restrict__ y, long n) {
@@ -132,14 +130,14 @@ extern "C" int smi_act_drop_bwd(const void* dy, const void* y, void* dx, long to
   SMI_CHECK_LAUNCH();
 }
 
-// part must hold nparts*N floats, nparts = ceil(M / rows_per_block)
+// out (fp32 [N]) += column sums of x (bf16 [M,N]); `part`/`accumulate` kept for ABI stability
 extern "C" int smi_colsum_bf16(const void* x, long M, int N, float* part, int rows_per_block, float* out,
                                int accumulate, hipStream_t st) {
-  if (N % 8) return -1;
+  (void)part;
+  if (!accumulate) hipMemsetAsync(out, 0, sizeof(float) * N, st);
   const int nparts = (int)((M + rows_per_block - 1) / rows_per_block);
   hipLaunchKernelGGL(colsum_bf16_kernel, dim3((N + 255) / 256, nparts), dim3(256), 0, st, (const unsigned short*)x, M,
-                     N, part, rows_per_block);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, st, part, nparts, N, out, accumulate);
+                     N, out, rows_per_block);
   SMI_CHECK_LAUNCH();
 }
 

@@ -32,24 +32,22 @@ __global__ void emb_fwd_kernel(const long long* __restrict__ ids, const unsigned
   *(u16x8_t*)(out + t * D + c) = o;
 }
 
+// one wave per token, lane = column (64 consecutive floats per atomic wave-instruction: the
+// 256-B contiguous shape the memory-side float atomics run at full rate)
 __global__ void emb_bwd_kernel(const long long* __restrict__ ids, const unsigned short* __restrict__ dout,
                                float* __restrict__ dtable, long T, int D, long long padding_idx,
                                const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale) {
   const uint32_t seed = smi_seed(seedp, salt);
-  const int vpr = D / 8;
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= T * vpr) return;
-  const long t = i / vpr;
-  const int c = (int)(i % vpr) * 8;
-  const long long id = ids[t];
-  if (id == padding_idx) return;
-  u16x8_t d = *(const u16x8_t*)(dout + t * D + c);
-  float* dst = dtable + id * D + c;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float g = bf2f(d[j]);
-    if (thresh) g = smi_keep(seed, (uint32_t)(t * D + c + j), thresh) ? g * dscale : 0.f;
-    atomicAdd(dst + j, g);
+  const int lane = threadIdx.x & 63;
+  for (long t = (long)blockIdx.x * 4 + (threadIdx.x >> 6); t < T; t += (long)gridDim.x * 4) {
+    const long long id = ids[t];
+    if (id == padding_idx) continue;
+    float* dst = dtable + id * D;
+    for (int c = lane; c < D; c += 64) {
+      float g = bf2f(dout[t * D + c]);
+      if (thresh) g = smi_keep(seed, (uint32_t)(t * D + c), thresh) ? g * dscale : 0.f;
+      atomicAdd(dst + c, g);
+    }
   }
 }
 
@@ -64,9 +62,9 @@ extern "C" int smi_emb_fwd(const long long* ids, const void* table, const float*
 
 extern "C" int smi_emb_bwd(const long long* ids, const void* dout, float* dtable, long T, int D, long long padding_idx,
                            const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, hipStream_t st) {
-  if (D % 8) return -1;
-  const long n = T * (D / 8);
-  hipLaunchKernelGGL(emb_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ids,
+  long nb = (T + 3) / 4;
+  if (nb > 4096) nb = 4096;
+  hipLaunchKernelGGL(emb_bwd_kernel, dim3((unsigned)nb), dim3(256), 0, st, ids,
                      (const unsigned short*)dout, dtable, T, D, padding_idx, seedp, salt, thresh, dscale);
   SMI_CHECK_LAUNCH();
 }

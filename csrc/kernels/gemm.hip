@@ -1,0 +1,372 @@
+// bf16 GEMM on MFMA (v_mfma_f32_16x16x32_bf16) with fused epilogues, for the three GEMMs of
+// every linear layer of the reference models (transformer.py Linear layers, MLP/CNN heads):
+//
+//   FWD   C[M,N]  = X[M,K] . W[N,K]^T  (+bias, ReLU, dropout)        A k-contig, B k-contig
+//   DGRAD dX[M,K] = dY[M,N] . W[N,K]   (+residual, x relu'/dropout)  A k-contig, B k-major
+//   WGRAD dW[N,K] += dY[M,N]^T . X[M,K]  (fp32, split-K atomics)     A k-major,  B k-major
+//
+// CDNA4 structure: PERSISTENT workgroups (one per CU: 256 threads = 4 waves 2x2, 128x128
+// output tile, BK = 64, three LDS stages = 96 KiB) walk a flattened stream of (tile, k-step)
+// work items, so the DMA pipeline never drains between tiles: the next tile's first k-steps are
+// in flight while the current tile's epilogue stores.  Tiles are staged by
+// buffer_load_dwordx4 ... lds (LDS-DMA, no VGPR round trip; per-lane offsets computed once per
+// tile, the k advance is a scalar soffset, out-of-range rows read as 0 through the descriptor's
+// bounds) in the operand's NATURAL global layout —
+// no transpose kernels: k-contiguous tiles are read with ds_read_b128 through an XOR chunk
+// swizzle (c ^ (row&7): conflict-free for the 16x16x32 operand groups), k-major tiles with the
+// gfx950 transposing read ds_read_b64_tr_b16 through a pair swizzle (conflict-free per 32-lane
+// half).  Swizzles are applied to the per-lane SOURCE address of the DMA (LDS image stays
+// lane-linear; cdna_hip_programming.md rule 21).  Two k-steps stay in flight across raw
+// s_barriers with counted `s_waitcnt vmcnt(N)` waits (never 0 inside the loop).
+// Tile order is XCD-aware (bijective remap: tiles sharing an A row-panel run on one XCD's L2).
+// bf16/plain-fp32 epilogues use the operand-swapped MFMA so each lane owns 4 consecutive output
+// columns (8-/16-byte stores); the split-K fp32 atomic epilogue keeps lanes along columns
+// (64-byte row segments per atomic wave-instruction).  A ragged K (multiple of 8) is handled by
+// zeroing the out-of-range A columns of the last k-tile in LDS.
+#include "smi_common.h"
+#include "smi_gemm.h"
+
+#define BM 128
+#define BN 128
+#define BKK 64
+#define NSTAGE 3
+#define TILE_ELEMS (BM * BKK)  // 8192 bf16 = 16 KiB per operand per stage
+#define NUM_CU 256
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((ext_vector_type(4))) short s16x4_t;
+
+// LDS-DMA through a buffer descriptor: 32-bit per-lane voffset (fixed per tile), scalar soffset
+// (the k advance), out-of-range records read as 0 — no per-step address VALU, no clamping.
+__device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t rsrc, unsigned short* lds_base, uint32_t voff,
+                                       uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds_base, 16, voff, soff, 0, 0);
+}
+
+// pair swizzle for k-major tiles (128 cols = 16 chunks of 8 bf16 per k-row)
+__device__ __forceinline__ int kmaj_s(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+
+// Per-lane byte offsets (relative to the operand base, k0 = 0) of the 4 DMA pieces this wave
+// issues for one 128 x 64 (k-contig: [128 rows][64 k]) or 64 x 128 (k-major: [64 k][128 cols])
+// bf16 tile.  The XOR swizzle lives in these SOURCE offsets; the LDS image is lane-linear.
+template <bool KMAJ>
+__device__ __forceinline__ void tile_voffsets(long ld, int r0, int w, int lane, uint32_t (&vo)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ins = w * 4 + i;
+    if (!KMAJ) {
+      const int row = ins * 8 + (lane >> 3);
+      const int lc = (lane & 7) ^ (row & 7);
+      vo[i] = (uint32_t)(((long)(r0 + row) * ld + lc * 8) * 2);
+    } else {
+      const int row = ins * 4 + (lane >> 4);  // k row 0..63
+      const int lc = (lane & 15) ^ (kmaj_s(row) << 1);
+      vo[i] = (uint32_t)(((long)row * ld + r0 + lc * 8) * 2);
+    }
+  }
+}
+
+// Issue the 4 DMA pieces of one tile at k0 (soffset = k0 * k-stride bytes).
+template <bool KMAJ>
+__device__ __forceinline__ void stage_tile(__amdgpu_buffer_rsrc_t rsrc, long ld, int k0, const uint32_t (&vo)[4],
+                                           unsigned short* tile, int w) {
+  const uint32_t soff = KMAJ ? (uint32_t)((long)k0 * ld * 2) : (uint32_t)(k0 * 2);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bdma16(rsrc, tile + (w * 4 + i) * 512, vo[i], soff);
+}
+
+// zero logical k-columns >= kvalid of a staged tile (ragged-K tail)
+template <bool KMAJ>
+__device__ __forceinline__ void zero_ktail(unsigned short* tile, int kvalid, int tid) {
+  if (!KMAJ) {
+    for (int e = tid; e < 128 * 8; e += 256) {
+      const int row = e >> 3, c = e & 7;
+      if (c * 8 >= kvalid) *(uint4*)(tile + row * 64 + ((c ^ (row & 7)) << 3)) = make_uint4(0, 0, 0, 0);
+      else if (c * 8 + 8 > kvalid) {
+        unsigned short* p = tile + row * 64 + ((c ^ (row & 7)) << 3);
+        for (int j = kvalid - c * 8; j < 8; ++j) p[j] = 0;
+      }
+    }
+  } else {
+    for (int e = tid; e < 64 * 16; e += 256) {
+      const int kr = e >> 4;
+      if (kr >= kvalid) *(uint4*)(tile + kr * 128 + (e & 15) * 8) = make_uint4(0, 0, 0, 0);
+    }
+  }
+}
+
+// A/B fragment (8 bf16) for the 16-row sub-tile starting at tile-row/col `r0`, k-step ks (0/1)
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8_t read_frag(const unsigned short* tile, int r0, int ks, int lane) {
+  if (!KMAJ) {
+    const int row = r0 + (lane & 15);
+    const int c = ks * 4 + (lane >> 4);
+    return *(const bf16x8_t*)(tile + row * 64 + ((c ^ (row & 7)) << 3));
+  } else {
+    const int q = (lane & 15) >> 2, p = lane & 3, g = lane >> 4;
+    const int col = r0 + 4 * p;
+    bf16x8_t out;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int kr = ks * 32 + 8 * g + 4 * h + q;
+      const int c = col >> 3;
+      const int pc = c ^ (kmaj_s(kr) << 1);
+      const unsigned short* addr = tile + kr * 128 + pc * 8 + (col & 7);
+      s16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)addr);
+      out[4 * h + 0] = v[0]; out[4 * h + 1] = v[1]; out[4 * h + 2] = v[2]; out[4 * h + 3] = v[3];
+    }
+    return out;
+  }
+}
+
+// epilogue value transform for bf16 outputs
+__device__ __forceinline__ float epi_val(const GemmArgs& g, float v, float bia, int row, int col, long cidx,
+                                         uint32_t seed) {
+  v = v * g.alpha + bia;
+  if (g.resid) v += bf2f(g.resid[(long)row * g.ldr + col]);
+  if (g.act == 1) v = fmaxf(v, 0.f);
+  if (g.dact_y) {  // backward of relu+dropout: y > 0 <=> kept and positive
+    v = bf2f(g.dact_y[(long)row * g.ldy + col]) > 0.f ? v * g.dscale : 0.f;
+  } else if (g.thresh) {
+    v = smi_keep(seed, (uint32_t)cidx, g.thresh) ? v * g.dscale : 0.f;
+  }
+  return v;
+}
+
+struct TileInfo {
+  int m0, n0, kbeg, nk;
+};
+
+__device__ __forceinline__ TileInfo tile_of(const GemmArgs& g, int t, int ntn, int nwg) {
+  // t enumerates (split, tile); XCD-aware bijective remap inside one split's tile set
+  const int split = t / nwg;
+  const int orig = t - split * nwg;
+  int wgid = orig;
+  if (nwg >= 16) {
+    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  }
+  TileInfo ti;
+  ti.m0 = (wgid / ntn) * BM;
+  ti.n0 = (wgid % ntn) * BN;
+  ti.kbeg = split * g.k_per_split;
+  const int kend = min(g.K, ti.kbeg + g.k_per_split);
+  ti.nk = (kend - ti.kbeg + BKK - 1) / BKK;
+  return ti;
+}
+
+// SWAP: accumulate C^T tiles (lane owns 4 consecutive output columns of one row).
+template <bool AK, bool BKM, bool SWAP>
+__global__ __launch_bounds__(256, 1) void gemm_bf16_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) unsigned short smem[NSTAGE * 2 * TILE_ELEMS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int ntn = (g.N + BN - 1) / BN;
+  const int ntm = (g.M + BM - 1) / BM;
+  const int nwg = ntm * ntn;
+  const int total_tiles = nwg * g.splits;
+  const int ragged = (g.K % BKK) != 0 || (g.K % g.k_per_split) != 0;
+  const uint32_t seed = smi_seed(g.seedp, g.salt);
+
+  // my tiles: blockIdx.x, +gridDim.x, ...
+  const int my_ntiles = (total_tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  if (my_ntiles <= 0) return;
+
+  // work-item stream: (tile index i in my list, k-step kt)
+  int st_i = 0, st_kt = 0;  // next item to STAGE
+  TileInfo st_tile = tile_of(g, blockIdx.x, ntn, nwg);
+  int cu_i = 0, cu_kt = 0;  // item being COMPUTED
+  TileInfo cu_tile = st_tile;
+
+  // buffer descriptors over the whole operands (wave-uniform by construction)
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, 0, (int)g.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, 0, (int)g.b_bytes, 0x00020000);
+  uint32_t voA[4], voB[4];
+  tile_voffsets<AK>(g.lda, st_tile.m0, w, lane, voA);
+  tile_voffsets<BKM>(g.ldb, st_tile.n0, w, lane, voB);
+  auto stage_next = [&](int slot) {
+    unsigned short* st = smem + slot * 2 * TILE_ELEMS;
+    const int k0 = st_tile.kbeg + st_kt * BKK;
+    stage_tile<AK>(rA, g.lda, k0, voA, st, w);
+    stage_tile<BKM>(rB, g.ldb, k0, voB, st + TILE_ELEMS, w);
+    if (++st_kt == st_tile.nk) {
+      st_kt = 0;
+      if (++st_i < my_ntiles) {
+        st_tile = tile_of(g, blockIdx.x + st_i * gridDim.x, ntn, nwg);
+        tile_voffsets<AK>(g.lda, st_tile.m0, w, lane, voA);
+        tile_voffsets<BKM>(g.ldb, st_tile.n0, w, lane, voB);
+      }
+    }
+  };
+  auto have_stage = [&]() { return st_i < my_ntiles; };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  int n_in_flight = 0;  // staged-but-not-consumed items beyond the current one
+  if (have_stage()) { stage_next(0); }
+  if (have_stage()) { stage_next(1); n_in_flight = 1; }
+  int rd = 0;
+  int extra_vm = 0;  // vector-memory ops issued after the youngest DMA (epilogue stores)
+  while (true) {
+    // wait for the item in stage `rd`
+    if (n_in_flight >= 1) {
+      if (extra_vm >= 16) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    extra_vm = 0;
+    __builtin_amdgcn_s_barrier();
+    if (ragged) {
+      const int k0 = cu_tile.kbeg + cu_kt * BKK;
+      const int kv = min(g.K, cu_tile.kbeg + g.k_per_split) - k0;
+      if (kv < BKK) {
+        zero_ktail<AK>(smem + rd * 2 * TILE_ELEMS, kv, tid);
+        __syncthreads();
+      }
+    }
+    const bool more = have_stage();
+    if (more) {
+      int ws = rd + 2;
+      if (ws >= NSTAGE) ws -= NSTAGE;
+      stage_next(ws);
+    }
+    const unsigned short* ta = smem + rd * 2 * TILE_ELEMS;
+    const unsigned short* tb = ta + TILE_ELEMS;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8_t af[4], bf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = read_frag<AK>(ta, wm * 64 + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = read_frag<BKM>(tb, wn * 64 + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (SWAP) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+          else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    rd = (rd + 1 == NSTAGE) ? 0 : rd + 1;
+    if (!more) n_in_flight--;
+
+    if (++cu_kt == cu_tile.nk) {
+      // ---------------- epilogue of tile cu_tile ----------------
+      const int m0 = cu_tile.m0, n0 = cu_tile.n0;
+      if (SWAP) {
+        // acc[i][j][r] = C[m0 + wm*64 + i*16 + (lane&15)][n0 + wn*64 + j*16 + 4*(lane>>4) + r]
+        const int cl = 4 * (lane >> 4);
+        const bool interior = (m0 + BM <= g.M) && (n0 + BN <= g.N);
+        // 16 stores per lane issued after the youngest DMA (interior, store-only epilogue): the next
+        // wait may leave them in flight.  Any count <= the true number of younger ops is safe.
+        const bool plain = interior && !g.resid && !g.dact_y && !(g.out_f32 && g.beta_acc);
+        if (plain) extra_vm = 16;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = n0 + wn * 64 + j * 16 + cl;
+          float4 bia = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (g.bias && (interior || col + 3 < g.N)) bia = *(const float4*)(g.bias + col);
+          else if (g.bias) {
+            if (col < g.N) bia.x = g.bias[col];
+            if (col + 1 < g.N) bia.y = g.bias[col + 1];
+            if (col + 2 < g.N) bia.z = g.bias[col + 2];
+          }
+          const float bb[4] = {bia.x, bia.y, bia.z, bia.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = m0 + wm * 64 + i * 16 + (lane & 15);
+            const long cidx = (long)row * g.ldc + col;
+            if (g.out_f32) {
+              float* C = (float*)g.C + cidx;
+              float4 v = make_float4(acc[i][j][0] * g.alpha, acc[i][j][1] * g.alpha, acc[i][j][2] * g.alpha,
+                                     acc[i][j][3] * g.alpha);
+              if (interior || (row < g.M && col + 3 < g.N)) {
+                if (g.beta_acc) { float4 o = *(float4*)C; v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w; }
+                *(float4*)C = v;
+              } else if (row < g.M) {
+                float vv[4] = {v.x, v.y, v.z, v.w};
+                for (int r = 0; r < 4; ++r)
+                  if (col + r < g.N) C[r] = g.beta_acc ? C[r] + vv[r] : vv[r];
+              }
+            } else if (interior || (row < g.M && col + 3 < g.N)) {
+              float o[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o[r] = epi_val(g, acc[i][j][r], bb[r], row, col + r, cidx + r, seed);
+              uint2 pk;
+              pk.x = pack2bf(o[0], o[1]);
+              pk.y = pack2bf(o[2], o[3]);
+              *(uint2*)((unsigned short*)g.C + cidx) = pk;
+            } else if (row < g.M) {
+              for (int r = 0; r < 4; ++r)
+                if (col + r < g.N)
+                  ((unsigned short*)g.C)[cidx + r] = f2bf(epi_val(g, acc[i][j][r], bb[r], row, col + r, cidx + r, seed));
+            }
+            acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+          }
+        }
+      } else {
+        // acc[i][j][r] = C[m0 + wm*64 + i*16 + 4*(lane>>4) + r][n0 + wn*64 + j*16 + (lane&15)]
+        const int cl = lane & 15, rg = (lane >> 4) * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = n0 + wn * 64 + j * 16 + cl;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = m0 + wm * 64 + i * 16 + rg + r;
+              if (row < g.M && col < g.N) {
+                const long cidx = (long)row * g.ldc + col;
+                float* C = (float*)g.C;
+                const float v = acc[i][j][r] * g.alpha;
+                if (g.atomic) atomicAdd(C + cidx, v);
+                else C[cidx] = g.beta_acc ? C[cidx] + v : v;
+              }
+            }
+            acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+          }
+        }
+        extra_vm = 0;
+      }
+      cu_kt = 0;
+      if (++cu_i >= my_ntiles) break;
+      cu_tile = tile_of(g, blockIdx.x + cu_i * gridDim.x, ntn, nwg);
+    }
+    if (n_in_flight < 0) break;  // defensive: never spin past the stream
+  }
+}
+
+extern "C" int smi_gemm(const GemmArgs* args, hipStream_t st) {
+  GemmArgs g = *args;
+  if (g.K % 8 != 0 || g.K < 8 || g.M < 8 || g.N < 8 || (g.mode != 0 && (g.M % 8 || g.N % 8))) return -1;
+  if (g.splits < 1) g.splits = 1;
+  int kps = (g.K / g.splits + BKK - 1) / BKK * BKK;
+  if (kps < BKK) kps = BKK;
+  g.k_per_split = kps;
+  g.splits = (g.K + kps - 1) / kps;
+  if (g.splits > 1 && !(g.out_f32 && g.atomic)) return -1;
+  // operand extents (elements -> bytes) for the DMA buffer descriptors
+  const bool ak = g.mode == 2, bk = g.mode != 0;
+  g.a_bytes = 2 * (ak ? (long)(g.K - 1) * g.lda + g.M : (long)(g.M - 1) * g.lda + g.K);
+  g.b_bytes = 2 * (bk ? (long)(g.K - 1) * g.ldb + g.N : (long)(g.N - 1) * g.ldb + g.K);
+  if (g.a_bytes >= (1L << 31) || g.b_bytes >= (1L << 31)) return -1;
+  const int ntiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN) * g.splits;
+  const int grid = ntiles < NUM_CU ? ntiles : NUM_CU;
+  const bool atomic = g.out_f32 && g.atomic;
+  switch (g.mode) {
+    case 0: hipLaunchKernelGGL((gemm_bf16_kernel<false, false, true>), dim3(grid), dim3(256), 0, st, g); break;
+    case 1: hipLaunchKernelGGL((gemm_bf16_kernel<false, true, true>), dim3(grid), dim3(256), 0, st, g); break;
+    case 2:
+      if (atomic) hipLaunchKernelGGL((gemm_bf16_kernel<true, true, false>), dim3(grid), dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((gemm_bf16_kernel<true, true, true>), dim3(grid), dim3(256), 0, st, g);
+      break;
+    default: return -1;
+  }
+  SMI_CHECK_LAUNCH();
+}

@@ -8,15 +8,14 @@
 // by a second kernel that accumulates into the caller's (flat) fp32 gradient buffer.
 #include "smi_common.h"
 
-template <int VPL>  // 8-element vectors per lane: D = VPL * 512
+template <int VPL>  // 8-element vectors per lane: D <= VPL * 512, D % 8 == 0
 __global__ __launch_bounds__(256) void ln_fwd_kernel(
     const unsigned short* __restrict__ h, const unsigned short* __restrict__ r,
     const float* __restrict__ gamma, const float* __restrict__ beta,
     unsigned short* __restrict__ y, unsigned short* __restrict__ xsave,
     float* __restrict__ mean_out, float* __restrict__ rstd_out,
-    int M, float eps, const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale) {
+    int M, int D, float eps, const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale) {
   const uint32_t seed = smi_seed(seedp, salt);
-  constexpr int D = VPL * 512;
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int row = blockIdx.x * 4 + wid;
@@ -26,6 +25,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
 #pragma unroll
   for (int v = 0; v < VPL; ++v) {
     const int col = v * 512 + lane * 8;
+    if (col >= D) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[v][j] = 0.f;
+      continue;
+    }
     u16x8_t hv = *(const u16x8_t*)(h + base + col);
     u16x8_t rv;
     if (r) rv = *(const u16x8_t*)(r + base + col);
@@ -41,17 +45,19 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
   for (int v = 0; v < VPL; ++v)
 #pragma unroll
     for (int j = 0; j < 8; ++j) s += x[v][j];
-  const float mean = wave_sum(s) * (1.0f / D);
+  const float invD = 1.0f / (float)D;
+  const float mean = wave_sum(s) * invD;
   float q = 0.f;
 #pragma unroll
   for (int v = 0; v < VPL; ++v)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { float d = x[v][j] - mean; q += d * d; }
-  const float var = wave_sum(q) * (1.0f / D);
+    for (int j = 0; j < 8; ++j) { float d = (v * 512 + lane * 8 < D) ? x[v][j] - mean : 0.f; q += d * d; }
+  const float var = wave_sum(q) * invD;
   const float rstd = 1.0f / sqrtf(var + eps);
 #pragma unroll
   for (int v = 0; v < VPL; ++v) {
     const int col = v * 512 + lane * 8;
+    if (col >= D) continue;
     u16x8_t out, xs;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -74,9 +80,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     unsigned short* __restrict__ dres, unsigned short* __restrict__ dh,
     const unsigned short* __restrict__ dres_add,
     float* __restrict__ part_g, float* __restrict__ part_b,
-    int M, const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale) {
+    int M, int D, const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale) {
   const uint32_t seed = smi_seed(seedp, salt);
-  constexpr int D = VPL * 512;
+  const float invD = 1.0f / (float)D;
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   float pg[VPL][8], pb[VPL][8];
@@ -88,7 +94,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 #pragma unroll
   for (int v = 0; v < VPL; ++v)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) gam[v][j] = gamma[v * 512 + lane * 8 + j];
+    for (int j = 0; j < 8; ++j) gam[v][j] = (v * 512 + lane * 8 < D) ? gamma[v * 512 + lane * 8 + j] : 0.f;
 
   for (int row = blockIdx.x * 4 + wid; row < M; row += gridDim.x * 4) {
     const size_t base = (size_t)row * D;
@@ -98,6 +104,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 #pragma unroll
     for (int v = 0; v < VPL; ++v) {
       const int col = v * 512 + lane * 8;
+      if (col >= D) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { xh[v][j] = 0.f; g[v][j] = 0.f; }
+        continue;
+      }
       u16x8_t dv = *(const u16x8_t*)(dy + base + col);
       u16x8_t xv = *(const u16x8_t*)(xs + base + col);
 #pragma unroll
@@ -111,11 +122,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
         pb[v][j] += d;
       }
     }
-    s1 = wave_sum(s1) * (1.0f / D);
-    s2 = wave_sum(s2) * (1.0f / D);
+    s1 = wave_sum(s1) * invD;
+    s2 = wave_sum(s2) * invD;
 #pragma unroll
     for (int v = 0; v < VPL; ++v) {
       const int col = v * 512 + lane * 8;
+      if (col >= D) continue;
       u16x8_t o1, o2, ad;
       if (dres_add) ad = *(const u16x8_t*)(dres_add + base + col);
 #pragma unroll
@@ -131,7 +143,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       if (dh) *(u16x8_t*)(dh + base + col) = o2;
     }
   }
-  __shared__ float red[2][4][D];
+  __shared__ float red[2][4][VPL * 512];
 #pragma unroll
   for (int v = 0; v < VPL; ++v)
 #pragma unroll
@@ -146,14 +158,23 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
 }
 
-// out[c] (+)= sum_b part[b][c]; two outputs (gamma, beta)
+// out[c] (+)= sum_b part[b][c]; two outputs (gamma, beta).  Block: 32 columns x 8 partial-row
+// phases, so the nb-long sums run 8-wide in parallel and finish through LDS.
 __global__ void colsum2_kernel(const float* __restrict__ pg, const float* __restrict__ pb, int nb, int D,
                                float* __restrict__ og, float* __restrict__ ob, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= D) return;
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const int ph = threadIdx.x >> 5;
   float sg = 0.f, sb = 0.f;
-  for (int b = 0; b < nb; ++b) { sg += pg[(size_t)b * D + c]; sb += pb[(size_t)b * D + c]; }
-  if (accumulate) { og[c] += sg; ob[c] += sb; } else { og[c] = sg; ob[c] = sb; }
+  if (c < D)
+    for (int b = ph; b < nb; b += 8) { sg += pg[(size_t)b * D + c]; sb += pb[(size_t)b * D + c]; }
+  __shared__ float rg[8][33], rb[8][33];
+  rg[ph][threadIdx.x & 31] = sg;
+  rb[ph][threadIdx.x & 31] = sb;
+  __syncthreads();
+  if (ph == 0 && c < D) {
+    for (int p = 1; p < 8; ++p) { sg += rg[p][threadIdx.x]; sb += rb[p][threadIdx.x]; }
+    if (accumulate) { og[c] += sg; ob[c] += sb; } else { og[c] = sg; ob[c] = sb; }
+  }
 }
 
 extern "C" int smi_ln_fwd(const void* h, const void* r, const float* gamma, const float* beta, void* y,
@@ -162,12 +183,12 @@ extern "C" int smi_ln_fwd(const void* h, const void* r, const float* gamma, cons
   dim3 grid((M + 3) / 4), block(256);
   const auto* hh = (const unsigned short*)h; const auto* rr = (const unsigned short*)r;
   auto* yy = (unsigned short*)y; auto* xx = (unsigned short*)xsave;
-  switch (D) {
-    case 512: hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, eps, seedp, salt, thresh, dscale); break;
-    case 1024: hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, eps, seedp, salt, thresh, dscale); break;
-    case 2048: hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, eps, seedp, salt, thresh, dscale); break;
-    default: return -1;
-  }
+  if (D % 8 || D > 4096) return -1;
+  const int vpl = (D + 511) / 512;
+  if (vpl == 1) hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale);
+  else if (vpl == 2) hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale);
+  else if (vpl <= 4) hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale);
+  else hipLaunchKernelGGL(ln_fwd_kernel<8>, grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale);
   SMI_CHECK_LAUNCH();
 }
 
@@ -180,11 +201,11 @@ extern "C" int smi_ln_bwd(const void* dy, const void* xs, const float* mean, con
   const auto* a = (const unsigned short*)dy; const auto* b = (const unsigned short*)xs;
   auto* o1 = (unsigned short*)dres; auto* o2 = (unsigned short*)dh;
   const auto* ad = (const unsigned short*)dres_add;
-  switch (D) {
-    case 512: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, seedp, salt, thresh, dscale); break;
-    case 1024: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, seedp, salt, thresh, dscale); break;
-    default: return -1;
-  }
-  hipLaunchKernelGGL(colsum2_kernel, dim3((D + 255) / 256), dim3(256), 0, st, part_g, part_b, nblocks, D, dgamma, dbeta, accumulate);
+  if (D % 8 || D > 2048) return -1;
+  const int vpl = (D + 511) / 512;
+  if (vpl == 1) hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, D, seedp, salt, thresh, dscale);
+  else if (vpl == 2) hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, D, seedp, salt, thresh, dscale);
+  else hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, D, seedp, salt, thresh, dscale);
+  hipLaunchKernelGGL(colsum2_kernel, dim3((D + 31) / 32), dim3(256), 0, st, part_g, part_b, nblocks, D, dgamma, dbeta, accumulate);
   SMI_CHECK_LAUNCH();
 }

@@ -1,0 +1,151 @@
+// Fused small-MLP forward/backward: affine -> sigmoid|relu hidden layers -> affine logits ->
+// softmax cross-entropy, for the reference's 4-5-4-3 sigmoid MLP (distributed_multilayer_
+// perceptron.py:44-53, pytorch_multilayer_perceptron.py:33-42) and Spark MLlib's
+// MultilayerPerceptronClassifier topology (AffineLayer + Sigmoid, SoftmaxLayerWithCrossEntropy;
+// SURVEY App. A.1), which is the same model.
+//
+// The whole network is a few dozen parameters, so the GPU cost is launch latency, not FLOPs:
+// one kernel does the full-batch (or minibatch) forward + loss, one does forward-recompute +
+// backward + gradient accumulation; each wave64 handles 64 rows (one row per lane), per-lane
+// activations live in LDS, weight gradients are summed per block with LDS atomics and flushed
+// with one global atomic per parameter per block.  Row weights implement MLlib's per-block
+// loss averaging (or 1/n for the torch-style mean).
+#include "smi_common.h"
+
+#include "smi_mlp.h"
+
+__device__ __forceinline__ float mlp_act(float v, int act) {
+  return act == 1 ? fmaxf(v, 0.f) : 1.f / (1.f + __expf(-v));
+}
+
+// forward one row; activations of every layer stored in a (lane-private) LDS slab
+__device__ float mlp_forward_row(const MLPArgs& a, int row, float* act_s) {
+  int off = 0;
+  const int d0 = a.dims[0];
+  for (int i = 0; i < d0; ++i) act_s[i] = a.x[(long)row * d0 + i];
+  for (int l = 0; l < a.nlayers; ++l) {
+    const int din = a.dims[l], dout = a.dims[l + 1];
+    const float* in = act_s + off;
+    float* out = act_s + off + din;
+    const bool last = l == a.nlayers - 1;
+    for (int o = 0; o < dout; ++o) {
+      float s = a.b[l][o];
+      const float* w = a.W[l] + o * din;
+      for (int i = 0; i < din; ++i) s += w[i] * in[i];
+      out[o] = last ? s : mlp_act(s, a.act);
+    }
+    off += din;
+  }
+  // softmax CE on the last layer (offset `off`)
+  const int C = a.dims[a.nlayers];
+  const float* z = act_s + off;
+  float m = z[0];
+  for (int c = 1; c < C; ++c) m = fmaxf(m, z[c]);
+  float se = 0.f;
+  for (int c = 0; c < C; ++c) se += __expf(z[c] - m);
+  const float lse = m + __logf(se);
+  const long long lab = a.y ? a.y[row] : 0;
+  return lse - z[lab];
+}
+
+__global__ __launch_bounds__(64) void mlp_fwd_kernel(MLPArgs a) {
+  __shared__ float acts[64 * MLP_ACT_STRIDE];
+  float* act_s = acts + threadIdx.x * MLP_ACT_STRIDE;
+  float lsum = 0.f;
+  for (int row = blockIdx.x * 64 + threadIdx.x; row < a.n; row += gridDim.x * 64) {
+    const float l = mlp_forward_row(a, row, act_s);
+    const float w = a.row_w ? a.row_w[row] : 1.f / (float)a.n;
+    lsum += w * l;
+    if (a.logits) {
+      int off = 0;
+      for (int k = 0; k < a.nlayers; ++k) off += a.dims[k];
+      const int C = a.dims[a.nlayers];
+      for (int c = 0; c < C; ++c) a.logits[(long)row * C + c] = act_s[off + c];
+    }
+  }
+  lsum = wave_sum(lsum);
+  if (threadIdx.x == 0 && a.loss) atomicAdd(a.loss, lsum);
+}
+
+__global__ __launch_bounds__(64) void mlp_bwd_kernel(MLPArgs a) {
+  __shared__ float acts[64 * MLP_ACT_STRIDE];
+  __shared__ float delta[64 * 2 * MLP_MAXW];
+  __shared__ float gacc[8192];
+  int total = 0;
+  int goff[MLP_MAXL];
+  for (int l = 0; l < a.nlayers; ++l) { goff[l] = total; total += a.dims[l + 1] * (a.dims[l] + 1); }
+  for (int i = threadIdx.x; i < total; i += 64) gacc[i] = 0.f;
+  __syncthreads();
+  float* act_s = acts + threadIdx.x * MLP_ACT_STRIDE;
+  const float dl = a.dloss ? a.dloss[0] : 1.f;
+  for (int row = blockIdx.x * 64 + threadIdx.x; row < a.n; row += gridDim.x * 64) {
+    mlp_forward_row(a, row, act_s);
+    float* dcur = delta + threadIdx.x * 2 * MLP_MAXW;
+    float* dnext = dcur + MLP_MAXW;
+    const float w = (a.row_w ? a.row_w[row] : 1.f / (float)a.n) * dl;
+    int offs[MLP_MAXL + 1];
+    offs[0] = 0;
+    for (int l = 0; l < a.nlayers; ++l) offs[l + 1] = offs[l] + a.dims[l];
+    const int L = a.nlayers;
+    const int C = a.dims[L];
+    const float* z = act_s + offs[L];
+    float m = z[0];
+    for (int c = 1; c < C; ++c) m = fmaxf(m, z[c]);
+    float se = 0.f;
+    for (int c = 0; c < C; ++c) se += __expf(z[c] - m);
+    const long long lab = a.y[row];
+    for (int c = 0; c < C; ++c) dcur[c] = (__expf(z[c] - m) / se - (c == lab ? 1.f : 0.f)) * w;
+    for (int l = L - 1; l >= 0; --l) {
+      const int din = a.dims[l], dout = a.dims[l + 1];
+      const float* in = act_s + offs[l];
+      float* g = gacc + goff[l];
+      for (int o = 0; o < dout; ++o) {
+        const float d = dcur[o];
+        for (int i = 0; i < din; ++i) atomicAdd(&g[o * din + i], d * in[i]);
+        atomicAdd(&g[dout * din + o], d);
+      }
+      if (l > 0) {
+        for (int i = 0; i < din; ++i) {
+          float s = 0.f;
+          for (int o = 0; o < dout; ++o) s += a.W[l][o * din + i] * dcur[o];
+          const float h = in[i];
+          dnext[i] = a.act == 1 ? (h > 0.f ? s : 0.f) : s * h * (1.f - h);
+        }
+        float* t = dcur; dcur = dnext; dnext = t;
+      }
+    }
+  }
+  __syncthreads();
+  for (int l = 0; l < a.nlayers; ++l) {
+    const int din = a.dims[l], dout = a.dims[l + 1];
+    const float* g = gacc + goff[l];
+    for (int i = threadIdx.x; i < dout * din; i += 64) atomicAdd(&a.gW[l][i], g[i]);
+    for (int i = threadIdx.x; i < dout; i += 64) atomicAdd(&a.gb[l][i], g[dout * din + i]);
+  }
+}
+
+static int mlp_check(const MLPArgs& a) {
+  if (a.nlayers < 1 || a.nlayers > MLP_MAXL) return -1;
+  int total = 0;
+  for (int l = 0; l <= a.nlayers; ++l) if (a.dims[l] < 1 || a.dims[l] > MLP_MAXW) return -1;
+  for (int l = 0; l < a.nlayers; ++l) total += a.dims[l + 1] * (a.dims[l] + 1);
+  if (total > 8192) return -1;
+  return 0;
+}
+
+static unsigned mlp_grid(int n) {
+  int b = (n + 63) / 64;
+  return (unsigned)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
+}
+
+extern "C" int smi_mlp_fwd(const MLPArgs* args, hipStream_t st) {
+  if (mlp_check(*args)) return -1;
+  hipLaunchKernelGGL(mlp_fwd_kernel, dim3(mlp_grid(args->n)), dim3(64), 0, st, *args);
+  SMI_CHECK_LAUNCH();
+}
+
+extern "C" int smi_mlp_bwd(const MLPArgs* args, hipStream_t st) {
+  if (mlp_check(*args)) return -1;
+  hipLaunchKernelGGL(mlp_bwd_kernel, dim3(mlp_grid(args->n)), dim3(64), 0, st, *args);
+  SMI_CHECK_LAUNCH();
+}

@@ -1,0 +1,217 @@
+"""Executor-side data path: partitioning, samplers and HBM-resident / streamed loaders.
+
+Replaces the reference's DataLoader + DistributedSampler + random_split stack
+(distributed_multilayer_perceptron.py:82-94, distributed_cnn.py:109-124,
+distributed_lstm.py:147-153) and fixes its sharding bugs: every executor gets
+a disjoint shard chosen by its real rank.
+
+MI355X design: each executor's whole partition is uploaded ONCE into HBM
+(288 GB holds every reference dataset many times over); per epoch a device-side permutation is
+drawn and each minibatch is a gather from HBM (HIP gather kernel, fused with uint8 -> float
+``ToTensor`` scaling for images).  For data larger than HBM, :class:`PinnedStreamLoader`
+double-buffers pinned host batches onto the device on a side HIP stream.
+"""
+import math
+
+import numpy as np
+import torch
+
+from .. import _native
+
+
+class ArrayDataset:
+    """TensorDataset equivalent (indexable tuple of equally long tensors/arrays)."""
+
+    def __init__(self, *arrays):
+        n = len(arrays[0])
+        assert all(len(a) == n for a in arrays), "all arrays must have the same length"
+        self.arrays = [a if isinstance(a, torch.Tensor) else torch.as_tensor(np.asarray(a)) for a in arrays]
+
+    def __len__(self):
+        return len(self.arrays[0])
+
+    def __getitem__(self, i):
+        return tuple(a[i] for a in self.arrays)
+
+    def subset(self, idx):
+        idx = torch.as_tensor(idx, dtype=torch.long)
+        return ArrayDataset(*[a[idx] for a in self.arrays])
+
+
+def random_split(dataset, lengths, seed=None):
+    """torch.utils.data.random_split semantics (fractions or absolute lengths), seeded (Q19)."""
+    n = len(dataset)
+    if all(isinstance(x, float) for x in lengths) and abs(sum(lengths) - 1.0) < 1e-6:
+        sizes = [int(math.floor(n * f)) for f in lengths]
+        for i in range(n - sum(sizes)):
+            sizes[i % len(sizes)] += 1
+    else:
+        sizes = list(lengths)
+    if sum(sizes) != n:
+        raise ValueError("sum of lengths must equal dataset length")
+    g = torch.Generator()
+    g.manual_seed(0 if seed is None else int(seed))
+    perm = torch.randperm(n, generator=g)
+    out, off = [], 0
+    for s in sizes:
+        out.append(dataset.subset(perm[off:off + s]))
+        off += s
+    return out
+
+
+class DistributedSampler:
+    """Correct rank partitioning (fixes Q2's hard-coded num_replicas=2, rank=0): indices of
+    rank r are perm[r::world] of a (seed+epoch)-shuffled, padded-to-divisible index list —
+    torch.utils.data.DistributedSampler semantics (torch/utils/data/distributed.py:134)."""
+
+    def __init__(self, n, num_replicas=None, rank=None, shuffle=True, seed=0, drop_last=False):
+        from ..parallel import rank as _rank, world_size as _ws
+        self.n = n if isinstance(n, int) else len(n)
+        self.num_replicas = num_replicas if num_replicas is not None else _ws()
+        self.rank = rank if rank is not None else _rank()
+        if not 0 <= self.rank < self.num_replicas:
+            raise ValueError(f"rank {self.rank} out of range for {self.num_replicas} replicas")
+        self.shuffle, self.seed, self.drop_last = shuffle, seed, drop_last
+        self.epoch = 0
+        if drop_last and self.n % self.num_replicas:
+            self.num_samples = self.n // self.num_replicas
+        else:
+            self.num_samples = math.ceil(self.n / self.num_replicas)
+        self.total_size = self.num_samples * self.num_replicas
+
+    def set_epoch(self, epoch):
+        self.epoch = epoch
+
+    def indices(self):
+        if self.shuffle:
+            g = torch.Generator()
+            g.manual_seed(self.seed + self.epoch)
+            idx = torch.randperm(self.n, generator=g).tolist()
+        else:
+            idx = list(range(self.n))
+        if not self.drop_last:
+            pad = self.total_size - len(idx)
+            if pad > 0:
+                idx += (idx * math.ceil(pad / max(1, len(idx))))[:pad]
+        else:
+            idx = idx[:self.total_size]
+        return idx[self.rank:self.total_size:self.num_replicas]
+
+    def __iter__(self):
+        return iter(self.indices())
+
+    def __len__(self):
+        return self.num_samples
+
+
+def gather_rows(src: torch.Tensor, idx: torch.Tensor, out=None, scale=None, out_dtype=None):
+    """out[i] = src[idx[i]] (rows of any width); on GPU a HIP gather kernel with 16-B
+    vectorised row copies, optionally fused with uint8 -> float scaling (ToTensor's /255)."""
+    if src.is_cuda and _native.use_native(src):
+        idx = idx.to(device=src.device, dtype=torch.int64).contiguous()
+        src = src.contiguous()
+        shape = (idx.shape[0],) + tuple(src.shape[1:])
+        row = int(np.prod(src.shape[1:])) if src.dim() > 1 else 1
+        C = _native.C()
+        if scale is not None and src.dtype == torch.uint8:
+            dt = out_dtype or torch.float32
+            out = out if out is not None else torch.empty(shape, device=src.device, dtype=dt)
+            C.gather_u8_scale(src.data_ptr(), idx.data_ptr(), out.data_ptr(), idx.shape[0], row, float(scale),
+                              int(dt == torch.bfloat16), _native.stream())
+            return out
+        out = out if out is not None else torch.empty(shape, device=src.device, dtype=src.dtype)
+        C.gather_rows(src.data_ptr(), idx.data_ptr(), out.data_ptr(), idx.shape[0], row * src.element_size(),
+                      _native.stream())
+        return out
+    res = src[idx.to(src.device)]
+    if scale is not None:
+        res = res.to(out_dtype or torch.float32) * scale
+    return res
+
+
+class DeviceLoader:
+    """HBM-resident minibatch loader for one executor's shard.
+
+    ``arrays`` are uploaded once to ``device``; each epoch draws a device-side permutation
+    (seeded by seed+epoch: reproducible, identical on every run) and yields gathered batches.
+    ``image_scale`` applies the uint8 -> float ``/255`` of torchvision's ToTensor inside the
+    gather (first tensor only)."""
+
+    def __init__(self, arrays, batch_size, device, shuffle=True, drop_last=False, seed=0, image_scale=None,
+                 image_dtype=torch.float32):
+        self.device = torch.device(device)
+        self.arrays = [torch.as_tensor(a).to(self.device) for a in arrays]
+        self.n = len(self.arrays[0])
+        self.batch_size, self.shuffle, self.drop_last, self.seed = batch_size, shuffle, drop_last, seed
+        self.image_scale, self.image_dtype = image_scale, image_dtype
+        self.epoch = 0
+
+    def set_epoch(self, e):
+        self.epoch = e
+
+    def __len__(self):
+        return self.n // self.batch_size if self.drop_last else math.ceil(self.n / self.batch_size)
+
+    def _perm(self):
+        if not self.shuffle:
+            return torch.arange(self.n, device=self.device)
+        g = torch.Generator(device=self.device)
+        g.manual_seed(self.seed + self.epoch)
+        return torch.randperm(self.n, generator=g, device=self.device)
+
+    def __iter__(self):
+        perm = self._perm()
+        for b in range(len(self)):
+            idx = perm[b * self.batch_size:(b + 1) * self.batch_size]
+            out = []
+            for i, a in enumerate(self.arrays):
+                if i == 0 and self.image_scale is not None:
+                    out.append(gather_rows(a, idx, scale=self.image_scale, out_dtype=self.image_dtype))
+                else:
+                    out.append(gather_rows(a, idx))
+            yield tuple(out)
+        self.epoch += 1
+
+
+class PinnedStreamLoader:
+    """Streams host minibatches to the GPU through pinned staging buffers on a side stream,
+    double-buffered so the H2D copy of batch i+1 overlaps compute on batch i (for datasets that
+    do not fit in HBM)."""
+
+    def __init__(self, arrays, batch_size, device, shuffle=False, drop_last=True, seed=0):
+        self.arrays = [torch.as_tensor(np.asarray(a)) for a in arrays]
+        self.n = len(self.arrays[0])
+        self.batch_size, self.shuffle, self.drop_last, self.seed = batch_size, shuffle, drop_last, seed
+        self.device = torch.device(device)
+        self.stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        self.epoch = 0
+
+    def __len__(self):
+        return self.n // self.batch_size if self.drop_last else math.ceil(self.n / self.batch_size)
+
+    def _host_batches(self):
+        order = np.random.default_rng(self.seed + self.epoch).permutation(self.n) if self.shuffle else np.arange(self.n)
+        for b in range(len(self)):
+            idx = torch.as_tensor(order[b * self.batch_size:(b + 1) * self.batch_size])
+            yield [a[idx].pin_memory() if self.stream is not None else a[idx] for a in self.arrays]
+
+    def __iter__(self):
+        if self.stream is None:
+            for hb in self._host_batches():
+                yield tuple(hb)
+            self.epoch += 1
+            return
+        pending = None
+        for hb in self._host_batches():
+            with torch.cuda.stream(self.stream):
+                db = [t.to(self.device, non_blocking=True) for t in hb]
+                ev = torch.cuda.Event()
+                ev.record(self.stream)
+            if pending is not None:
+                torch.cuda.current_stream().wait_event(pending[1])
+                yield tuple(pending[0])
+            pending = (db, ev)
+        if pending is not None:
+            torch.cuda.current_stream().wait_event(pending[1])
+            yield tuple(pending[0])
+        self.epoch += 1

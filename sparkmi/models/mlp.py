@@ -1,0 +1,40 @@
+"""Multilayer perceptron classifier (the reference's ``Multilayer_perceptor``:
+distributed_multilayer_perceptron.py:44-53 — Linear(4,5) -> Sigmoid -> Linear(5,4) -> Sigmoid
+-> Linear(4,3), logits out).  Same attribute names (layer_1.., sigmoid) so reference
+state_dicts load.  ``forward`` returns logits; ``loss`` runs the fused HIP MLP+CE kernels.
+"""
+import torch
+from torch import nn
+
+from ..ops.mlp import mlp_logits, mlp_loss
+
+
+class MultilayerPerceptron(nn.Module):
+    def __init__(self, layers=(4, 5, 4, 3), activation="sigmoid"):
+        super().__init__()
+        self.layer_sizes = list(layers)
+        self.activation = activation
+        for i in range(len(layers) - 1):
+            setattr(self, f"layer_{i + 1}", nn.Linear(layers[i], layers[i + 1]))
+        self.sigmoid = nn.Sigmoid()
+
+    def linears(self):
+        return [getattr(self, f"layer_{i + 1}") for i in range(len(self.layer_sizes) - 1)]
+
+    def forward(self, x):
+        lins = self.linears()
+        if x.is_cuda:
+            return mlp_logits(x, [l.weight for l in lins], [l.bias for l in lins], self.activation)
+        h = x
+        for i, l in enumerate(lins):
+            h = l(h)
+            if i < len(lins) - 1:
+                h = torch.sigmoid(h) if self.activation == "sigmoid" else torch.relu(h)
+        return h
+
+    def loss(self, x, y, row_weight=None):
+        lins = self.linears()
+        return mlp_loss(x, y, [l.weight for l in lins], [l.bias for l in lins], self.activation, row_weight)
+
+
+Multilayer_perceptor = MultilayerPerceptron  # reference class name

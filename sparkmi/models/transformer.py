@@ -24,6 +24,7 @@ from torch import nn
 
 from ..ops import (DropoutRNG, add_dropout_layernorm, cross_attention, embedding, linear, self_attention,
                    sinusoid_table)
+from ..ops.linear import ffn
 from ..ops.loss import cross_entropy
 from ..ops.rng import new_salt
 
@@ -141,8 +142,7 @@ class PositionwiseFeedForward(nn.Module):
 
     def forward(self, x):
         p = self.dropout.p if self.training else 0.0
-        h = linear(x, self.linear1.weight, self.linear1.bias, act="relu", p=p, rng=self._rng, salt=self.salt)
-        return linear(h, self.linear2.weight, self.linear2.bias)
+        return ffn(x, self.linear1, self.linear2, p, self._rng, self.salt)
 
 
 class EncoderLayer(nn.Module):

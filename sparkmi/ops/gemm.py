@@ -1,0 +1,73 @@
+"""Python front-end of the MFMA GEMM (csrc/kernels/gemm.hip).
+
+Three entry points, one per GEMM of a linear layer, each with its fused epilogue:
+  fwd(x, w)        -> y = dropout(act(x @ w^T + bias))               bf16 out
+  dgrad(dy, w)     -> dx = (dy @ w) [+ resid] [* relu'/dropout mask]  bf16 out
+  wgrad(dy, x, gw) -> gw += dy^T @ x                                  fp32 accumulate (split-K)
+``supported(...)`` says whether a shape can run on the kernel (K multiple of 64, dims multiple
+of 8, 16-B aligned rows); callers fall back to hipBLASLt otherwise.
+"""
+import os
+
+import torch
+
+from .. import _native
+
+_DISABLE = os.environ.get("SPARKMI_GEMM", "1") == "0"
+NUM_CU = 256
+
+
+def _aligned(*ts):
+    return all(t is None or (t.data_ptr() % 16 == 0) for t in ts)
+
+
+def supported(M, N, K, *tensors, mode=0):
+    if _DISABLE:
+        return False
+    if K % 8 or K < 64 or M < 8 or N < 8:
+        return False
+    if mode != 0 and (M % 8 or N % 8):
+        return False
+    for t in tensors:
+        if t is not None and (t.stride(-1) != 1 or (t.dim() > 1 and t.stride(-2) % 8)):
+            return False
+    return _aligned(*tensors)
+
+
+def fwd(x, w, bias=None, act=0, rng=None, salt=0, thresh=0, dscale=1.0, out=None):
+    M, K = x.shape
+    N = w.shape[0]
+    y = out if out is not None else torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
+    _native.C().gemm(0, x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), M, N, K, y.data_ptr(), y.stride(0), 0, 0,
+                     0, 1.0, _native.ptr(bias), 0, 0, act, 0, 0, rng.ptr() if rng is not None else 0, salt, thresh,
+                     dscale, 1, _native.stream())
+    return y
+
+
+def dgrad(dy, w, resid=None, dact_y=None, dscale=1.0, out=None):
+    M, N = dy.shape
+    K = w.shape[1]
+    dx = out if out is not None else torch.empty(M, K, device=dy.device, dtype=torch.bfloat16)
+    _native.C().gemm(1, dy.data_ptr(), dy.stride(0), w.data_ptr(), w.stride(0), M, K, N, dx.data_ptr(), dx.stride(0),
+                     0, 0, 0, 1.0, 0, _native.ptr(resid), resid.stride(0) if resid is not None else 0, 0,
+                     _native.ptr(dact_y), dact_y.stride(0) if dact_y is not None else 0, 0, 0, 0, dscale, 1,
+                     _native.stream())
+    return dx
+
+
+def wgrad_splits(N, K, M):
+    tiles = ((N + 127) // 128) * ((K + 127) // 128)
+    s = 1
+    while tiles * s < NUM_CU and (M // (s * 2)) >= 256:
+        s *= 2
+    return s
+
+
+def wgrad(dy, x, gw, splits=None):
+    """gw [N,K] fp32 += dy[M,N]^T @ x[M,K]."""
+    M, N = dy.shape
+    K = x.shape[1]
+    s = splits or wgrad_splits(N, K, M)
+    _native.C().gemm(2, dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), N, K, M, gw.data_ptr(), gw.stride(0),
+                     1, 1, 1, 1.0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1.0, s, _native.stream())
+    return gw

@@ -1,4 +1,4 @@
-"""Linear layer with fused bias / activation / dropout epilogue and direct fp32 weight-grad
+"""Linear layer and fused FFN with MFMA GEMMs, fused epilogues and direct fp32 weight-grad
 accumulation.
 
 y = dropout_p(act(x @ W^T + b)).  Reference call sites: every nn.Linear of transformer.py
@@ -6,27 +6,34 @@ y = dropout_p(act(x @ W^T + b)).  Reference call sites: every nn.Linear of trans
 :271), the MLP (distributed_multilayer_perceptron.py:47-53) and the CNN classifier
 (distributed_cnn.py:74-78).
 
-GPU path (bf16 activations, bf16 weight shadow, fp32 master/grad):
-  * forward GEMM on MFMA: sparkmi's own HIP GEMM (csrc/kernels/gemm.hip) when the shape is
-    supported, hipBLASLt (through torch.addmm) otherwise; the act+dropout epilogue is a HIP
-    kernel (csrc/kernels/elementwise.hip) keyed by a counter-based mask (no mask tensor saved).
-  * backward: dgrad GEMM, wgrad GEMM accumulated in fp32 into the flat gradient buffer
-    (addmm with out_dtype=fp32, beta=1), bias grad by a HIP column-sum kernel.
+GPU path (bf16 activations, bf16 weight shadow, fp32 master/grad) — sparkmi's own MFMA GEMM
+(csrc/kernels/gemm.hip, sparkmi/ops/gemm.py) whenever the shape fits (K % 64 == 0, rows 16-B
+aligned), hipBLASLt through torch otherwise:
+  * forward: ONE kernel = GEMM + bias + ReLU + dropout epilogue (counter-based mask, nothing
+    saved but the output);
+  * backward: dgrad GEMM (bf16 out), wgrad GEMM accumulating fp32 straight into the flat
+    gradient buffer (split-K atomics), bias grad by a HIP column-sum kernel.
+``ffn()`` fuses PositionwiseFeedForward (Linear -> ReLU -> Dropout -> Linear): its backward
+applies the ReLU/dropout mask inside linear2's dgrad epilogue (no elementwise pass).
 CPU path: fp32 torch math with the identical dropout mask.
 """
 import torch
 
 from .. import _native
+from . import gemm as G
 from . import rng as _rng
 from ._grad import bf16_weight, grad_buf, grad_ready
 
 ACTS = {None: 0, "none": 0, "relu": 1, "sigmoid": 2}
 
-_colsum_part = {}
-
 
 def _wgrad_accumulate(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor):
     """gw (fp32 [N,K]) += dy2^T @ x2 with fp32 accumulation on the GPU."""
+    N, K = gw.shape
+    M = dy2.shape[0]
+    if G.supported(N, K, M, dy2, x2, mode=2) and gw.is_contiguous():
+        G.wgrad(dy2, x2, gw)
+        return
     try:
         torch.addmm(gw, dy2.t(), x2, out_dtype=torch.float32, out=gw)
         return
@@ -35,18 +42,60 @@ def _wgrad_accumulate(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor):
     gw.add_(torch.mm(dy2.t(), x2).float())
 
 
+def _dgrad(g2, w_bf, resid=None, dact_y=None, dscale=1.0):
+    M, N = g2.shape
+    K = w_bf.shape[1]
+    if G.supported(M, K, N, g2, w_bf, resid, dact_y, mode=1):
+        return G.dgrad(g2, w_bf, resid=resid, dact_y=dact_y, dscale=dscale)
+    dx = torch.mm(g2, w_bf)
+    if resid is not None:
+        dx = dx + resid
+    if dact_y is not None:
+        dx = dx * (dact_y > 0).to(dx.dtype) * dscale
+    return dx
+
+
 def _colsum(dy2: torch.Tensor, out: torch.Tensor):
+    """out (fp32 [N]) += column sums of dy2 (bf16 [M,N]); one HIP launch, fp32 atomics per block."""
     M, N = dy2.shape
+    _native.C().colsum_bf16(dy2.data_ptr(), M, N, 0, 256, out.data_ptr(), 1, _native.stream())
+
+
+def _fwd_native(x2, weight, bias, act, p, rng, salt):
+    N, K = weight.shape
+    w = bf16_weight(weight)
+    if G.supported(x2.shape[0], N, K, x2, w, mode=0) and act in (0, 1):
+        return G.fwd(x2, w, bias, act, rng, salt, _rng.threshold(p), _rng.scale(p))
     C = _native.C()
-    rpb = 256
-    nparts = (M + rpb - 1) // rpb
-    key = (dy2.device, nparts * N)
-    part = _colsum_part.get(key)
-    if part is None or torch.cuda.is_current_stream_capturing():
-        part = torch.empty(nparts * N, device=dy2.device, dtype=torch.float32)
-        if not torch.cuda.is_current_stream_capturing():
-            _colsum_part[key] = part
-    C.colsum_bf16(dy2.data_ptr(), M, N, part.data_ptr(), rpb, out.data_ptr(), 1, _native.stream())
+    y2 = torch.addmm(bf16_weight(bias), x2, w.t()) if bias is not None else torch.mm(x2, w.t())
+    if act or p > 0:
+        C.bias_act_drop_fwd(y2.data_ptr(), 0, y2.data_ptr(), y2.numel(), N, act, rng.ptr(), salt,
+                            _rng.threshold(p), _rng.scale(p), _native.stream())
+    return y2
+
+
+def _ref_fwd(x2, weight, bias, act, p, seed, salt):
+    y2 = x2.float() @ weight.float().t()
+    if bias is not None:
+        y2 = y2 + bias.float()
+    if act == 1:
+        y2 = torch.relu(y2)
+    elif act == 2:
+        y2 = torch.sigmoid(y2)
+    if p > 0:
+        y2 = y2 * _rng.keep_mask(y2.shape, p, seed, salt, y2.device).to(y2.dtype) * _rng.scale(p)
+    return y2
+
+
+def _ref_act_bwd(g2, y2, act, p, seed, salt):
+    if act == 1:
+        return g2 * (y2.float() > 0).to(g2.dtype) * (_rng.scale(p) if p > 0 else 1.0)
+    if act == 2:
+        s = y2.float()
+        g2 = g2 * s * (1 - s)
+    if p > 0:
+        g2 = g2 * _rng.keep_mask(g2.shape, p, seed, salt, g2.device).to(g2.dtype) * _rng.scale(p)
+    return g2
 
 
 class LinearFn(torch.autograd.Function):
@@ -57,34 +106,14 @@ class LinearFn(torch.autograd.Function):
         N = weight.shape[0]
         x2 = x.reshape(-1, K)
         ctx.act, ctx.p, ctx.rng, ctx.salt = act, p, rng, salt
-        ctx.has_bias = bias is not None
         ctx.native = _native.use_native(x)
         if ctx.native:
-            C = _native.C()
             x2 = x2.contiguous()
-            w = bf16_weight(weight)
-            if bias is not None:
-                y2 = torch.addmm(bf16_weight(bias), x2, w.t())
-            else:
-                y2 = torch.mm(x2, w.t())
-            if act or p > 0:
-                C.bias_act_drop_fwd(y2.data_ptr(), 0, y2.data_ptr(), y2.numel(), N, act, rng.ptr(), salt,
-                                    _rng.threshold(p), _rng.scale(p), _native.stream())
+            y2 = _fwd_native(x2, weight, bias, act, p, rng, salt)
             ctx.seed = 0
         else:
-            w = weight
-            y2 = x2.float() @ w.float().t()
-            if bias is not None:
-                y2 = y2 + bias.float()
-            if act == 1:
-                y2 = torch.relu(y2)
-            elif act == 2:
-                y2 = torch.sigmoid(y2)
             ctx.seed = rng.current() if p > 0 else 0
-            if p > 0:
-                y2 = y2 * _rng.keep_mask(y2.shape, p, ctx.seed, salt, y2.device).to(y2.dtype) * _rng.scale(p)
-            y2 = y2.to(x.dtype)
-        # relu/sigmoid backward needs the output; identity+dropout recomputes the mask
+            y2 = _ref_fwd(x2, weight, bias, act, p, ctx.seed, salt).to(x.dtype)
         ctx.save_for_backward(x2, weight, bias, y2 if act else None)
         return y2.reshape(*shp[:-1], N)
 
@@ -104,20 +133,12 @@ class LinearFn(torch.autograd.Function):
                                ctx.salt, _rng.threshold(p), _rng.scale(p), _native.stream())
             else:
                 g2 = dy2
-            dx = torch.mm(g2, bf16_weight(weight)) if ctx.needs_input_grad[0] else None
+            dx = _dgrad(g2, bf16_weight(weight)) if ctx.needs_input_grad[0] else None
             _wgrad_accumulate(gw, g2, x2)
             if bias is not None:
                 _colsum(g2, grad_buf(bias))
         else:
-            g2 = dy2.float()
-            if act == 1:
-                g2 = g2 * (y2.float() > 0).to(g2.dtype) * (_rng.scale(p) if p > 0 else 1.0)
-            else:
-                if act == 2:
-                    s = y2.float()
-                    g2 = g2 * s * (1 - s)
-                if p > 0:
-                    g2 = g2 * _rng.keep_mask(g2.shape, p, ctx.seed, ctx.salt, g2.device).to(g2.dtype) * _rng.scale(p)
+            g2 = _ref_act_bwd(dy2.float(), y2, act, p, ctx.seed, ctx.salt)
             dx = (g2 @ weight.float()).to(dy.dtype) if ctx.needs_input_grad[0] else None
             gw.add_(g2.t() @ x2.float())
             if bias is not None:
@@ -137,3 +158,64 @@ def linear(x, weight, bias=None, act=None, p=0.0, rng=None, salt=0):
         from .layernorm import _NULL_RNG
         rng, p = _NULL_RNG, 0.0
     return LinearFn.apply(x, weight, bias, a, float(p), rng, int(salt))
+
+
+class FFNFn(torch.autograd.Function):
+    """y = linear2(dropout(relu(linear1(x)))) with a single saved hidden activation."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, p, rng, salt):
+        shp = x.shape
+        D = shp[-1]
+        x2 = x.reshape(-1, D)
+        ctx.p, ctx.rng, ctx.salt = p, rng, salt
+        ctx.native = _native.use_native(x)
+        if ctx.native:
+            x2 = x2.contiguous()
+            h = _fwd_native(x2, w1, b1, 1, p, rng, salt)
+            y = _fwd_native(h, w2, b2, 0, 0.0, rng, 0)
+            ctx.seed = 0
+        else:
+            ctx.seed = rng.current() if p > 0 else 0
+            h = _ref_fwd(x2, w1, b1, 1, p, ctx.seed, salt).to(x.dtype)
+            y = _ref_fwd(h, w2, b2, 0, 0.0, 0, 0).to(x.dtype)
+        ctx.save_for_backward(x2, h, w1, b1, w2, b2)
+        return y.reshape(shp)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, h, w1, b1, w2, b2 = ctx.saved_tensors
+        D = w2.shape[0]
+        dy2 = dy.reshape(-1, D)
+        p = ctx.p
+        if ctx.native:
+            dy2 = dy2.contiguous()
+            # dh_pre = (dy @ W2) * relu'/dropout mask (from the saved output h), fused epilogue
+            dh = _dgrad(dy2, bf16_weight(w2), dact_y=h, dscale=_rng.scale(p))
+            _wgrad_accumulate(grad_buf(w2), dy2, h)
+            _colsum(dy2, grad_buf(b2))
+            grad_ready(w2, b2)
+            dx = _dgrad(dh, bf16_weight(w1)) if ctx.needs_input_grad[0] else None
+            _wgrad_accumulate(grad_buf(w1), dh, x2)
+            _colsum(dh, grad_buf(b1))
+            grad_ready(w1, b1)
+        else:
+            g = dy2.float()
+            grad_buf(w2).add_(g.t() @ h.float())
+            grad_buf(b2).add_(g.sum(0))
+            grad_ready(w2, b2)
+            dh = _ref_act_bwd(g @ w2.float(), h, 1, p, ctx.seed, ctx.salt)
+            dx = (dh @ w1.float()).to(dy.dtype) if ctx.needs_input_grad[0] else None
+            grad_buf(w1).add_(dh.t() @ x2.float())
+            grad_buf(b1).add_(dh.sum(0))
+            grad_ready(w1, b1)
+        if dx is not None:
+            dx = dx.reshape(dy.shape)
+        return dx, None, None, None, None, None, None, None
+
+
+def ffn(x, linear1, linear2, p=0.0, rng=None, salt=0):
+    if rng is None:
+        from .layernorm import _NULL_RNG
+        rng, p = _NULL_RNG, 0.0
+    return FFNFn.apply(x, linear1.weight, linear1.bias, linear2.weight, linear2.bias, float(p), rng, int(salt))

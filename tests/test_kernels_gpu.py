@@ -148,6 +148,9 @@ def test_linear(act, p):
     torch.manual_seed(4)
     M, K, N = 512, 256, 384
     lin = torch.nn.Linear(K, N)
+    with torch.no_grad():  # the GPU computes with the bf16 weight shadow: give the reference the same weights
+        lin.weight.copy_(lin.weight.bfloat16().float())
+        lin.bias.copy_(lin.bias.bfloat16().float())
     wg = torch.nn.Parameter(lin.weight.detach().to(dev))
     bg = torch.nn.Parameter(lin.bias.detach().to(dev))
     x = torch.randn(M, K).bfloat16()
@@ -207,3 +210,31 @@ def test_transformer_gpu_vs_cpu():
         g = gold["grad." + name]
         rel = (p.grad.cpu() - g).norm() / (g.norm() + 1e-6)
         assert rel < 0.1, (name, float(rel))
+
+
+def test_ffn_fused():
+    from sparkmi.ops.linear import ffn
+    torch.manual_seed(6)
+    M, D, H = 1024, 512, 1024
+    l1, l2 = torch.nn.Linear(D, H), torch.nn.Linear(H, D)
+    with torch.no_grad():
+        for l in (l1, l2):
+            l.weight.copy_(l.weight.bfloat16().float())
+    g1, g2 = torch.nn.Linear(D, H).to(dev), torch.nn.Linear(H, D).to(dev)
+    g1.load_state_dict(l1.state_dict())
+    g2.load_state_dict(l2.state_dict())
+    x = torch.randn(M, D).bfloat16()
+    xg = x.to(dev).requires_grad_()
+    xc = x.float().requires_grad_()
+    rg, rc = R.DropoutRNG(8).to(dev), R.DropoutRNG(8)
+    yg = ffn(xg, g1, g2, 0.1, rg, 77)
+    yc = ffn(xc, l1, l2, 0.1, rc, 77)
+    _close(yg, yc, 6e-2, 3e-2, "ffn fwd")
+    dy = torch.randn(M, D).bfloat16()
+    yg.backward(dy.to(dev))
+    yc.backward(dy.float())
+    _close(xg.grad, xc.grad, 6e-2, 3e-2, "ffn dx")
+    for a, b, n in ((g1.weight, l1.weight, "w1"), (g2.weight, l2.weight, "w2"), (g1.bias, l1.bias, "b1"),
+                    (g2.bias, l2.bias, "b2")):
+        rel = (a.grad.cpu() - b.grad).norm() / b.grad.norm()
+        assert rel < 2e-2, (n, float(rel))
