@@ -33,7 +33,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--model", default="transformer", choices=["transformer"])
+    ap.add_argument("--model", default="all", choices=["all", "transformer", "cnn"])
+    ap.add_argument("--cnn-batch", type=int, default=32)
+    ap.add_argument("--cnn-steps", type=int, default=200)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--seq", type=int, default=256)
     ap.add_argument("--layers", type=int, default=6)
@@ -43,11 +45,73 @@ def parse():
     return ap.parse_args()
 
 
+def time_steps(runner, batches, steps, warmup, device, world):
+    from sparkmi.parallel import barrier
+    sync = (lambda: torch.cuda.synchronize()) if device.type == "cuda" else (lambda: None)
+    n = len(batches)
+    loss = None
+    for i in range(warmup):
+        loss = runner.step(*batches[i % n])
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        loss = runner.step(*batches[i % n])
+    sync()
+    barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, loss
+
+
+def bench_cnn(args, rank, world, device):
+    """distributed_cnn.py workload: FashionMNISTModel, batch 32/GPU, SGD lr 0.01, mean CE."""
+    from sparkmi.data.synthetic import fashion_mnist_like
+    from sparkmi.models.cnn import FashionMNISTModel
+    from sparkmi.optim import SGD
+    from sparkmi.parallel.ddp import DataParallel
+    from sparkmi.train.runner import StepRunner
+    from sparkmi.utils.flat import FlatParams
+    torch.manual_seed(4321)
+    model = FashionMNISTModel(1, 10, 10).to(device).train()
+    flat = FlatParams(model)
+    opt = SGD(flat, lr=0.01)
+    ddp = DataParallel(flat) if world > 1 else None
+    use_graph = device.type == "cuda" and (world == 1 or args.graph == "on")
+    runner = StepRunner(model, lambda m, x, y: m.loss(x, y), opt, ddp, graph=use_graph)
+    imgs, labels = fashion_mnist_like(16 * args.cnn_batch, seed=7 + rank, device=device)
+    batches = [(imgs[i * args.cnn_batch:(i + 1) * args.cnn_batch], labels[i * args.cnn_batch:(i + 1) * args.cnn_batch])
+               for i in range(16)]
+    elapsed, loss = time_steps(runner, batches, args.cnn_steps, max(args.warmup, 5), device, world)
+    if ddp is not None:
+        ddp.close()
+    return world * args.cnn_batch * args.cnn_steps / elapsed, elapsed / args.cnn_steps * 1000, float(loss)
+
+
 def main():
     args = parse()
     from sparkmi.parallel import barrier, init_distributed
     from sparkmi.parallel.ddp import DataParallel
     rank, world, device = init_distributed()
+    cnn = None
+    if args.model in ("all", "cnn"):
+        cnn = bench_cnn(args, rank, world, device)
+    if args.model == "cnn":
+        if rank == 0:
+            v, ms, l = cnn
+            print(json.dumps({"metric": "samples/sec (whole node) distributed_cnn at 1/2/4/8 MI355X", "value": round(v, 1),
+                              "unit": "samples/s", "n_gpus": world, "steps": args.cnn_steps, "warmup": args.warmup,
+                              "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+                              "vs_baseline": round(v / BASELINE_CNN, 2), "dtype": "fp32", "data": "synthetic",
+                              "config": {"model": "FashionMNISTModel", "global_batch": world * args.cnn_batch,
+                                         "seq_len": None, "parallelism": f"dp{world}", "final_loss": round(l, 4)}}))
+        return
     torch.manual_seed(1234)
     from sparkmi.models.transformer import Transformer
     from sparkmi.optim import Adam
@@ -69,28 +133,8 @@ def main():
     src = src.view(pool, args.batch, args.seq)
     tgt = tgt.view(pool, args.batch, args.seq)
 
-    def sync():
-        if device.type == "cuda":
-            torch.cuda.synchronize()
-
-    loss = None
-    for i in range(args.warmup):
-        loss = runner.step(src[i % pool], tgt[i % pool])
-    sync()
-    barrier()
-    sync()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss = runner.step(src[i % pool], tgt[i % pool])
-    sync()
-    barrier()
-    sync()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    batches = [(src[i], tgt[i]) for i in range(pool)]
+    elapsed, loss = time_steps(runner, batches, args.steps, args.warmup, device, world)
     final_loss = float(loss.float().item()) if loss is not None else float("nan")
     value = world * args.batch * args.steps / elapsed
     if rank == 0:
@@ -119,6 +163,12 @@ def main():
                 "final_loss": round(final_loss, 4),
             },
         }
+        if cnn is not None:
+            out["extra"] = {"cnn_samples_per_s": round(cnn[0], 1), "cnn_ms_per_step": round(cnn[1], 4),
+                            "cnn_vs_baseline": round(cnn[0] / BASELINE_CNN, 2),
+                            "cnn_config": f"FashionMNISTModel fp32 fused HIP kernel, batch {args.cnn_batch}/GPU, "
+                                          f"SGD lr0.01, dp{world}, {args.cnn_steps} steps",
+                            "cnn_baseline_ref": "BASELINE.md §2 CNN CPU proxy 5,655 samples/s (1 proc x 8 threads)"}
         print(json.dumps(out), flush=True)
     from sparkmi.parallel import destroy
     destroy()

@@ -17,6 +17,7 @@ using u = uintptr_t;
 #include "smi_attention.h"
 #include "smi_mlp.h"
 #include "smi_gemm.h"
+#include "smi_cnn.h"
 #include <pybind11/stl.h>
 #include <vector>
 
@@ -41,6 +42,8 @@ int smi_add_bf16(const void*, const void*, void*, long, hipStream_t);
 int smi_step_inc(float*, hipStream_t);
 int smi_mlp_fwd(const MLPArgs*, hipStream_t);
 int smi_gemm(const GemmArgs*, hipStream_t);
+int smi_cnn(const CNNArgs*, hipStream_t);
+int smi_cnn_reduce(const CNNArgs*, hipStream_t);
 int smi_gather_rows(const void*, const long long*, void*, long, long, hipStream_t);
 int smi_gather_u8_scale(const void*, const long long*, void*, long, long, float, int, hipStream_t);
 int smi_mlp_bwd(const MLPArgs*, hipStream_t);
@@ -172,5 +175,25 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("gather_u8_scale", [](u src, u idx, u out, long n, long row, float scale, int bf16, u st) {
     chk(smi_gather_u8_scale(P(src), (const long long*)idx, P(out), n, row, scale, bf16, S(st)), "gather_u8_scale");
+  });
+
+  // fused CNN: phase 0 = fwd(+bwd if train), 1 = gradient reduce
+  m.def("cnn", [](int phase, u x, int x_u8, float x_scale, u y, int B, int cin, int C, int classes, std::vector<u> w,
+                  std::vector<u> b, std::vector<u> gw, std::vector<u> gb, u slab, u row_loss, u pred, u logits,
+                  u loss, float loss_scale, u dloss, int train, u st) {
+    CNNArgs a{};
+    if (w.size() != 5 || b.size() != 5) throw std::runtime_error("cnn: need 5 weight and 5 bias pointers");
+    a.x = (const void*)x; a.x_u8 = x_u8; a.x_scale = x_scale; a.y = (const long long*)y;
+    a.B = B; a.cin = cin; a.C = C; a.classes = classes;
+    for (int i = 0; i < 5; ++i) {
+      a.w[i] = (const float*)w[i]; a.b[i] = (const float*)b[i];
+      a.gw[i] = gw.size() == 5 ? (float*)gw[i] : nullptr; a.gb[i] = gb.size() == 5 ? (float*)gb[i] : nullptr;
+    }
+    const int sz[10] = {C * cin * 9, C, C * C * 9, C, C * C * 9, C, C * C * 9, C, classes * C * 49, classes};
+    int o = 0;
+    for (int i = 0; i < 10; ++i) { a.off[i] = o; o += sz[i]; }
+    a.P = o; a.slab = (float*)slab; a.row_loss = (float*)row_loss; a.pred = (int*)pred; a.logits = (float*)logits;
+    a.loss = (float*)loss; a.loss_scale = loss_scale; a.dloss = (const float*)dloss; a.train = train;
+    chk(phase == 0 ? smi_cnn(&a, S(st)) : smi_cnn_reduce(&a, S(st)), "cnn");
   });
 }

@@ -1,0 +1,315 @@
+// Fused FashionMNIST CNN training kernel: one workgroup = one image, the WHOLE forward
+// (conv3x3+ReLU x2, maxpool, conv3x3+ReLU x2, maxpool, flatten, linear, softmax-CE) AND backward
+// (CE grad, linear, unpool, ReLU', transposed convs, weight/bias gradients) in one launch,
+// every activation resident in LDS (zero-halo padded planes, no bounds checks in the conv
+// loops), weights read through the scalar cache (wave-uniform indices).
+//
+// Reference model: FashionMNISTModel (distributed_cnn.py:47-86 / pytorch_cnn.py:12-49):
+// block_1 = Conv(Cin->C,3,p1) ReLU Conv(C->C,3,p1) ReLU MaxPool(2); block_2 = same at 14x14;
+// classifier = Flatten (NCHW order) + Linear(C*7*7 -> classes); trained with CrossEntropyLoss
+// (mean) + SGD (distributed_cnn.py:138-141).  At the reference batch (32 images/GPU) the step is
+// latency-bound (6.7 MFLOP/image), so whole-step fusion beats per-layer GEMMs: one launch per
+// step for fwd+bwd, one for the cross-image gradient reduction (+dloss scale), one for SGD.
+// ToTensor()'s uint8 -> [0,1] scaling is fused into the image load.
+//
+// Per-image gradients go to a slab [B][P] (P = all parameters, packed in the order
+// w1 b1 w2 b2 w3 b3 w4 b4 wfc bfc); cnn_grad_reduce sums the slab over images (fixed order:
+// bit-reproducible) and accumulates into the model's gradient buffers.
+#include "smi_common.h"
+#include "smi_cnn.h"
+
+#define P28 30   // 28x28 plane with 1-pixel zero halo
+#define P14 16   // 14x14 plane with 1-pixel zero halo
+#define PL28 (P28 * P28)
+#define PL14 (P14 * P14)
+
+__device__ __forceinline__ int i28(int c, int y, int x) { return c * PL28 + (y + 1) * P28 + (x + 1); }
+__device__ __forceinline__ int i14(int c, int y, int x) { return c * PL14 + (y + 1) * P14 + (x + 1); }
+
+// forward 3x3 conv + bias + relu over an HxH plane set; in/out padded with pitch PP
+template <int H, int PP>
+__device__ void conv_fwd(const float* __restrict__ in, int cin, float* __restrict__ out, int cout,
+                         const float* __restrict__ w, const float* __restrict__ b) {
+  for (int pos = threadIdx.x; pos < H * H; pos += blockDim.x) {
+    const int y = pos / H, x = pos % H;
+    float acc[CNN_MAXC];
+#pragma unroll
+    for (int co = 0; co < CNN_MAXC; ++co) acc[co] = co < cout ? b[co] : 0.f;
+    for (int ci = 0; ci < cin; ++ci) {
+      const float* ip = in + ci * PP * PP + y * PP + x;  // top-left of the 3x3 window (halo coords)
+      float v[9];
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) v[ky * 3 + kx] = ip[ky * PP + kx];
+#pragma unroll
+      for (int co = 0; co < CNN_MAXC; ++co) {
+        if (co < cout) {
+          const float* wp = w + (co * cin + ci) * 9;
+          float s = acc[co];
+#pragma unroll
+          for (int k = 0; k < 9; ++k) s += wp[k] * v[k];
+          acc[co] = s;
+        }
+      }
+    }
+#pragma unroll
+    for (int co = 0; co < CNN_MAXC; ++co)
+      if (co < cout) out[co * PP * PP + (y + 1) * PP + (x + 1)] = fmaxf(acc[co], 0.f);
+  }
+}
+
+// 2x2/2 max pool of H x H (pitch PPI) into H/2 planes (pitch PPO, halo offset HO)
+template <int H, int PPI, int PPO, int HO>
+__device__ void pool_fwd(const float* __restrict__ in, float* __restrict__ out, int c) {
+  constexpr int Ho = H / 2;
+  for (int e = threadIdx.x; e < c * Ho * Ho; e += blockDim.x) {
+    const int ch = e / (Ho * Ho), r = e % (Ho * Ho), py = r / Ho, px = r % Ho;
+    const float* p = in + ch * PPI * PPI + (2 * py + 1) * PPI + (2 * px + 1);
+    const float m = fmaxf(fmaxf(p[0], p[1]), fmaxf(p[PPI], p[PPI + 1]));
+    out[HO ? (ch * PPO * PPO + (py + 1) * PPO + (px + 1)) : (ch * Ho * Ho + py * Ho + px)] = m;
+  }
+}
+
+// unpool the gradient g (per pooled element) into the pre-pool activation buffer a IN PLACE:
+// a <- (pos == first argmax of its window && a > 0) ? g : 0   (torch max_pool2d + relu backward)
+template <int H, int PPI>
+__device__ void unpool_relu_inplace(float* __restrict__ a, const float* __restrict__ g, int gpitch, int ghalo,
+                                    int c) {
+  constexpr int Ho = H / 2;
+  for (int e = threadIdx.x; e < c * Ho * Ho; e += blockDim.x) {
+    const int ch = e / (Ho * Ho), r = e % (Ho * Ho), py = r / Ho, px = r % Ho;
+    float* p = a + ch * PPI * PPI + (2 * py + 1) * PPI + (2 * px + 1);
+    const float gv = ghalo ? g[ch * gpitch * gpitch + (py + 1) * gpitch + (px + 1)] : g[ch * Ho * Ho + py * Ho + px];
+    const float v0 = p[0], v1 = p[1], v2 = p[PPI], v3 = p[PPI + 1];
+    int am = 0;
+    float m = v0;
+    if (v1 > m) { m = v1; am = 1; }
+    if (v2 > m) { m = v2; am = 2; }
+    if (v3 > m) { m = v3; am = 3; }
+    const float gg = m > 0.f ? gv : 0.f;
+    p[0] = am == 0 ? gg : 0.f;
+    p[1] = am == 1 ? gg : 0.f;
+    p[PPI] = am == 2 ? gg : 0.f;
+    p[PPI + 1] = am == 3 ? gg : 0.f;
+  }
+}
+
+// dW[co][ci][k] = sum_pos dz[co][pos] * in[ci][pos+k-1]; db[co] = sum_pos dz[co][pos]
+// tasks = (co, ci, row-chunk); partials accumulated with LDS atomics into acc (cout*cin*9 + cout)
+template <int H, int PP, int CHUNKS>
+__device__ void conv_wgrad(const float* __restrict__ dz, const float* __restrict__ in, int cin, int cout,
+                           float* __restrict__ acc) {
+  const int ntask = cout * cin * CHUNKS;
+  constexpr int RPC = (H + CHUNKS - 1) / CHUNKS;
+  for (int t = threadIdx.x; t < ntask; t += blockDim.x) {
+    const int chunk = t % CHUNKS;
+    const int pair = t / CHUNKS;
+    const int co = pair / cin, ci = pair % cin;
+    float s[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) s[k] = 0.f;
+    float sb = 0.f;
+    const int y0 = chunk * RPC, y1 = min(H, y0 + RPC);
+    for (int y = y0; y < y1; ++y) {
+      const float* dzr = dz + co * PP * PP + (y + 1) * PP + 1;
+      const float* inr = in + ci * PP * PP + y * PP;  // row y-1 (halo coords), col x-1
+      for (int x = 0; x < H; ++x) {
+        const float d = dzr[x];
+        sb += d;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) s[ky * 3 + kx] += d * inr[ky * PP + x + kx];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) atomicAdd(&acc[(co * cin + ci) * 9 + k], s[k]);
+    if (ci == 0) atomicAdd(&acc[cout * cin * 9 + co], sb);
+  }
+}
+
+// in-place transposed conv + relu': a[ci][pos] <- (a[ci][pos] > 0) ? sum_co sum_k w[co][ci][k] dz[co][pos-k+1] : 0
+// (relu=false: plain write into out)
+template <int H, int PP>
+__device__ void conv_dgrad(const float* __restrict__ dz, int cout, const float* __restrict__ w, int cin,
+                           float* __restrict__ a, bool relu) {
+  for (int e = threadIdx.x; e < cin * H * H; e += blockDim.x) {
+    const int ci = e / (H * H), r = e % (H * H), y = r / H, x = r % H;
+    float s = 0.f;
+    for (int co = 0; co < cout; ++co) {
+      const float* wp = w + (co * cin + ci) * 9;
+      const float* dp = dz + co * PP * PP + (y + 2) * PP + (x + 2);  // dz at (y+1, x+1) in halo coords, minus k
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) s += wp[ky * 3 + kx] * dp[-ky * PP - kx];
+    }
+    float* ap = a + ci * PP * PP + (y + 1) * PP + (x + 1);
+    *ap = relu ? (*ap > 0.f ? s : 0.f) : s;
+  }
+}
+
+__global__ __launch_bounds__(256) void cnn_kernel(CNNArgs g) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int C = g.C, CI = g.cin, NC = g.classes;
+  const int img = blockIdx.x;
+  float* xin = sm;                       // CI x 30x30
+  float* a1 = xin + CI * PL28;           // C x 30x30
+  float* a2 = a1 + C * PL28;             // C x 30x30
+  float* p1 = a2 + C * PL28;             // C x 16x16
+  float* a3 = p1 + C * PL14;             // C x 16x16
+  float* a4 = a3 + C * PL14;             // C x 16x16
+  float* p2 = a4 + C * PL14;             // C*49 (flat, NCHW)
+  float* lg = p2 + C * 49;               // logits / dlogits [16]
+  float* wacc = lg + 16;                 // C*C*9 + C wgrad accumulators
+  const int total = CI * PL28 + 2 * C * PL28 + 3 * C * PL14 + C * 49 + 16 + C * C * 9 + C;
+  for (int i = threadIdx.x; i < total; i += blockDim.x) sm[i] = 0.f;
+  __syncthreads();
+  // image load (+ ToTensor scaling)
+  for (int e = threadIdx.x; e < CI * 784; e += blockDim.x) {
+    const int c = e / 784, r = e % 784;
+    const long gi = (long)img * CI * 784 + e;
+    const float v = g.x_u8 ? (float)((const unsigned char*)g.x)[gi] * g.x_scale : ((const float*)g.x)[gi];
+    xin[i28(c, r / 28, r % 28)] = v;
+  }
+  __syncthreads();
+  conv_fwd<28, P28>(xin, CI, a1, C, g.w[0], g.b[0]);
+  __syncthreads();
+  conv_fwd<28, P28>(a1, C, a2, C, g.w[1], g.b[1]);
+  __syncthreads();
+  pool_fwd<28, P28, P14, 1>(a2, p1, C);
+  __syncthreads();
+  conv_fwd<14, P14>(p1, C, a3, C, g.w[2], g.b[2]);
+  __syncthreads();
+  conv_fwd<14, P14>(a3, C, a4, C, g.w[3], g.b[3]);
+  __syncthreads();
+  pool_fwd<14, P14, 7, 0>(a4, p2, C);
+  __syncthreads();
+  // classifier: wave w computes logits o = w, w+4, ...
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int F = C * 49;
+  for (int o = wv; o < NC; o += 4) {
+    float s = 0.f;
+    for (int i = lane; i < F; i += 64) s += g.w[4][o * F + i] * p2[i];
+    s = wave_sum(s);
+    if (lane == 0) lg[o] = s + g.b[4][o];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = lg[0];
+    int am = 0;
+    for (int o = 1; o < NC; ++o) if (lg[o] > m) { m = lg[o]; am = o; }
+    float se = 0.f;
+    for (int o = 0; o < NC; ++o) se += __expf(lg[o] - m);
+    const float lse = m + __logf(se);
+    const long long lab = g.y ? g.y[img] : 0;
+    if (g.row_loss) g.row_loss[img] = lse - lg[lab];
+    if (g.pred) g.pred[img] = am;
+    if (g.logits)
+      for (int o = 0; o < NC; ++o) g.logits[(long)img * NC + o] = lg[o];
+    if (g.train) {
+      // dlogits = (softmax - onehot) * loss_scale   (loss_scale = 1/B for a mean loss)
+      for (int o = 0; o < NC; ++o) lg[o] = (__expf(lg[o] - lse) - (o == lab ? 1.f : 0.f)) * g.loss_scale;
+    }
+  }
+  if (!g.train) return;
+  __syncthreads();
+  float* gs = g.slab + (long)img * g.P;  // this image's gradient slab
+  // fc grads: gW[o][i] = dl[o] * p2[i]; gb[o] = dl[o]; dp2[i] = sum_o W[o][i] dl[o] (into p2 buffer after)
+  for (int e = threadIdx.x; e < NC * F; e += blockDim.x) gs[g.off[8] + e] = lg[e / F] * p2[e % F];
+  for (int o = threadIdx.x; o < NC; o += blockDim.x) gs[g.off[9] + o] = lg[o];
+  __syncthreads();
+  for (int i = threadIdx.x; i < F; i += blockDim.x) {
+    float s = 0.f;
+    for (int o = 0; o < NC; ++o) s += g.w[4][o * F + i] * lg[o];
+    p2[i] = s;  // dp2 (flat NCHW)
+  }
+  __syncthreads();
+  // pool2 backward + relu'(a4): dz4 in a4
+  unpool_relu_inplace<14, P14>(a4, p2, 7, 0, C);
+  __syncthreads();
+  // conv4: dW4, db4 (from dz4, a3); then dz3 = convT(dz4) * relu'(a3) in a3
+  conv_wgrad<14, P14, 2>(a4, a3, C, C, wacc);
+  __syncthreads();
+  for (int e = threadIdx.x; e < C * C * 9 + C; e += blockDim.x) {
+    gs[(e < C * C * 9 ? g.off[6] + e : g.off[7] + e - C * C * 9)] = wacc[e];
+    wacc[e] = 0.f;
+  }
+  conv_dgrad<14, P14>(a4, C, g.w[3], C, a3, true);
+  __syncthreads();
+  // conv3: dW3 (dz3, p1); dp1 = convT(dz3) into p1 (no relu: p1 is a pool output)
+  conv_wgrad<14, P14, 2>(a3, p1, C, C, wacc);
+  __syncthreads();
+  for (int e = threadIdx.x; e < C * C * 9 + C; e += blockDim.x) {
+    gs[(e < C * C * 9 ? g.off[4] + e : g.off[5] + e - C * C * 9)] = wacc[e];
+    wacc[e] = 0.f;
+  }
+  conv_dgrad<14, P14>(a3, C, g.w[2], C, p1, false);
+  __syncthreads();
+  // pool1 backward + relu'(a2): dz2 in a2
+  unpool_relu_inplace<28, P28>(a2, p1, P14, 1, C);
+  __syncthreads();
+  // conv2: dW2 (dz2, a1); dz1 = convT(dz2) * relu'(a1) in a1
+  conv_wgrad<28, P28, 2>(a2, a1, C, C, wacc);
+  __syncthreads();
+  for (int e = threadIdx.x; e < C * C * 9 + C; e += blockDim.x) {
+    gs[(e < C * C * 9 ? g.off[2] + e : g.off[3] + e - C * C * 9)] = wacc[e];
+    wacc[e] = 0.f;
+  }
+  conv_dgrad<28, P28>(a2, C, g.w[1], C, a1, true);
+  __syncthreads();
+  // conv1: dW1 (dz1, x)
+  conv_wgrad<28, P28, 8>(a1, xin, CI, C, wacc);
+  __syncthreads();
+  for (int e = threadIdx.x; e < C * CI * 9 + C; e += blockDim.x)
+    gs[(e < C * CI * 9 ? g.off[0] + e : g.off[1] + e - C * CI * 9)] = wacc[e];
+}
+
+// grad[p] (+)= dloss * sum_img slab[img][p], scattered to the 10 parameter tensors; also the mean
+// loss / correct-count reductions (thread 0 of block 0)
+__global__ void cnn_reduce_kernel(CNNArgs g) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const float dl = g.dloss ? g.dloss[0] : 1.f;
+  if (p < g.P) {
+    float s = 0.f;
+    for (int i = 0; i < g.B; ++i) s += g.slab[(long)i * g.P + p];
+    int seg = 0;
+    while (seg < 9 && p >= g.off[seg + 1]) ++seg;
+    float* dst = seg % 2 == 0 ? g.gw[seg / 2] : g.gb[seg / 2];
+    dst[p - g.off[seg]] += s * dl;
+  }
+}
+
+__global__ void cnn_loss_kernel(const float* __restrict__ row_loss, int B, float scale, float* __restrict__ loss) {
+  float s = 0.f;
+  for (int i = threadIdx.x; i < B; i += blockDim.x) s += row_loss[i];
+  s = wave_sum(s);
+  __shared__ float part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) loss[0] = (part[0] + part[1] + part[2] + part[3]) * scale;
+}
+
+static size_t cnn_lds_bytes(const CNNArgs& g) {
+  const int C = g.C, CI = g.cin;
+  return sizeof(float) * (size_t)(CI * PL28 + 2 * C * PL28 + 3 * C * PL14 + C * 49 + 16 + C * C * 9 + C + 4);
+}
+
+extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
+  CNNArgs g = *args;
+  if (g.C < 1 || g.C > CNN_MAXC || g.cin < 1 || g.cin > 4 || g.classes < 1 || g.classes > 16) return -1;
+  const size_t lds = cnn_lds_bytes(g);
+  if (lds > 160 * 1024) return -1;
+  hipFuncSetAttribute((const void*)cnn_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(cnn_kernel, dim3(g.B), dim3(256), lds, st, g);
+  if (g.loss && g.row_loss)
+    hipLaunchKernelGGL(cnn_loss_kernel, dim3(1), dim3(256), 0, st, g.row_loss, g.B, g.loss_scale, g.loss);
+  SMI_CHECK_LAUNCH();
+}
+
+extern "C" int smi_cnn_reduce(const CNNArgs* args, hipStream_t st) {
+  const CNNArgs& g = *args;
+  hipLaunchKernelGGL(cnn_reduce_kernel, dim3((g.P + 255) / 256), dim3(256), 0, st, g);
+  SMI_CHECK_LAUNCH();
+}

@@ -6,7 +6,7 @@
 //   WGRAD dW[N,K] += dY[M,N]^T . X[M,K]  (fp32, split-K atomics)     A k-major,  B k-major
 //
 // CDNA4 structure: PERSISTENT workgroups (one per CU: 256 threads = 4 waves 2x2, 128x128
-// output tile, BK = 64, three LDS stages = 96 KiB) walk a flattened stream of (tile, k-step)
+// output tile, BK = 64, four LDS stages = 128 KiB) walk a flattened stream of (tile, k-step)
 // work items, so the DMA pipeline never drains between tiles: the next tile's first k-steps are
 // in flight while the current tile's epilogue stores.  Tiles are staged by
 // buffer_load_dwordx4 ... lds (LDS-DMA, no VGPR round trip; per-lane offsets computed once per
@@ -16,7 +16,7 @@
 // swizzle (c ^ (row&7): conflict-free for the 16x16x32 operand groups), k-major tiles with the
 // gfx950 transposing read ds_read_b64_tr_b16 through a pair swizzle (conflict-free per 32-lane
 // half).  Swizzles are applied to the per-lane SOURCE address of the DMA (LDS image stays
-// lane-linear; cdna_hip_programming.md rule 21).  Two k-steps stay in flight across raw
+// lane-linear; cdna_hip_programming.md rule 21).  Up to three k-steps stay in flight across raw
 // s_barriers with counted `s_waitcnt vmcnt(N)` waits (never 0 inside the loop).
 // Tile order is XCD-aware (bijective remap: tiles sharing an A row-panel run on one XCD's L2).
 // bf16/plain-fp32 epilogues use the operand-swapped MFMA so each lane owns 4 consecutive output
@@ -29,7 +29,9 @@
 #define BM 128
 #define BN 128
 #define BKK 64
-#define NSTAGE 3
+#ifndef GEMM_NS
+#define GEMM_NS 2
+#endif
 #define TILE_ELEMS (BM * BKK)  // 8192 bf16 = 16 KiB per operand per stage
 #define NUM_CU 256
 
@@ -156,9 +158,12 @@ __device__ __forceinline__ TileInfo tile_of(const GemmArgs& g, int t, int ntn, i
 }
 
 // SWAP: accumulate C^T tiles (lane owns 4 consecutive output columns of one row).
-template <bool AK, bool BKM, bool SWAP>
-__global__ __launch_bounds__(256, 1) void gemm_bf16_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) unsigned short smem[NSTAGE * 2 * TILE_ELEMS];
+// Persistent over tiles (grid = min(tiles, WG_PER_CU * 256)); per tile: NS-deep DMA prologue,
+// k-loop with counted waits, drain, epilogue.  With NS = 2 (64 KiB LDS) two workgroups share a
+// CU, so one's prologue/epilogue overlaps the other's MFMA loop.
+template <bool AK, bool BKM, bool SWAP, int NS>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) unsigned short smem[NS * 2 * TILE_ELEMS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
@@ -166,179 +171,140 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_kernel(GemmArgs g) {
   const int ntm = (g.M + BM - 1) / BM;
   const int nwg = ntm * ntn;
   const int total_tiles = nwg * g.splits;
-  const int ragged = (g.K % BKK) != 0 || (g.K % g.k_per_split) != 0;
+  const bool ragged = (g.K % BKK) != 0 || (g.K % g.k_per_split) != 0;
   const uint32_t seed = smi_seed(g.seedp, g.salt);
-
-  // my tiles: blockIdx.x, +gridDim.x, ...
-  const int my_ntiles = (total_tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-  if (my_ntiles <= 0) return;
-
-  // work-item stream: (tile index i in my list, k-step kt)
-  int st_i = 0, st_kt = 0;  // next item to STAGE
-  TileInfo st_tile = tile_of(g, blockIdx.x, ntn, nwg);
-  int cu_i = 0, cu_kt = 0;  // item being COMPUTED
-  TileInfo cu_tile = st_tile;
-
-  // buffer descriptors over the whole operands (wave-uniform by construction)
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, 0, (int)g.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, 0, (int)g.b_bytes, 0x00020000);
-  uint32_t voA[4], voB[4];
-  tile_voffsets<AK>(g.lda, st_tile.m0, w, lane, voA);
-  tile_voffsets<BKM>(g.ldb, st_tile.n0, w, lane, voB);
-  auto stage_next = [&](int slot) {
-    unsigned short* st = smem + slot * 2 * TILE_ELEMS;
-    const int k0 = st_tile.kbeg + st_kt * BKK;
-    stage_tile<AK>(rA, g.lda, k0, voA, st, w);
-    stage_tile<BKM>(rB, g.ldb, k0, voB, st + TILE_ELEMS, w);
-    if (++st_kt == st_tile.nk) {
-      st_kt = 0;
-      if (++st_i < my_ntiles) {
-        st_tile = tile_of(g, blockIdx.x + st_i * gridDim.x, ntn, nwg);
-        tile_voffsets<AK>(g.lda, st_tile.m0, w, lane, voA);
-        tile_voffsets<BKM>(g.ldb, st_tile.n0, w, lane, voB);
+
+  for (int t = blockIdx.x; t < total_tiles; t += gridDim.x) {
+    const TileInfo ti = tile_of(g, t, ntn, nwg);
+    const int m0 = ti.m0, n0 = ti.n0, nk = ti.nk;
+    uint32_t voA[4], voB[4];
+    tile_voffsets<AK>(g.lda, m0, w, lane, voA);
+    tile_voffsets<BKM>(g.ldb, n0, w, lane, voB);
+    f32x4_t acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s0 = 0; s0 < NS - 1; ++s0) {
+      if (s0 < nk) {
+        unsigned short* st = smem + s0 * 2 * TILE_ELEMS;
+        stage_tile<AK>(rA, g.lda, ti.kbeg + s0 * BKK, voA, st, w);
+        stage_tile<BKM>(rB, g.ldb, ti.kbeg + s0 * BKK, voB, st + TILE_ELEMS, w);
       }
     }
-  };
-  auto have_stage = [&]() { return st_i < my_ntiles; };
-
-  f32x4_t acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-
-  int n_in_flight = 0;  // staged-but-not-consumed items beyond the current one
-  if (have_stage()) { stage_next(0); }
-  if (have_stage()) { stage_next(1); n_in_flight = 1; }
-  int rd = 0;
-  int extra_vm = 0;  // vector-memory ops issued after the youngest DMA (epilogue stores)
-  while (true) {
-    // wait for the item in stage `rd`
-    if (n_in_flight >= 1) {
-      if (extra_vm >= 16) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    extra_vm = 0;
-    __builtin_amdgcn_s_barrier();
-    if (ragged) {
-      const int k0 = cu_tile.kbeg + cu_kt * BKK;
-      const int kv = min(g.K, cu_tile.kbeg + g.k_per_split) - k0;
-      if (kv < BKK) {
-        zero_ktail<AK>(smem + rd * 2 * TILE_ELEMS, kv, tid);
-        __syncthreads();
-      }
-    }
-    const bool more = have_stage();
-    if (more) {
-      int ws = rd + 2;
-      if (ws >= NSTAGE) ws -= NSTAGE;
-      stage_next(ws);
-    }
-    const unsigned short* ta = smem + rd * 2 * TILE_ELEMS;
-    const unsigned short* tb = ta + TILE_ELEMS;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8_t af[4], bf[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = read_frag<AK>(ta, wm * 64 + i * 16, ks, lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bf[j] = read_frag<BKM>(tb, wn * 64 + j * 16, ks, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (SWAP) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
-          else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    int rd = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      const int ahead = min(NS - 2, nk - 1 - kt);  // items staged beyond kt
+      if (NS >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else if (NS >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (ragged) {
+        const int kv = min(g.K, ti.kbeg + g.k_per_split) - (ti.kbeg + kt * BKK);
+        if (kv < BKK) {
+          zero_ktail<AK>(smem + rd * 2 * TILE_ELEMS, kv, tid);
+          __syncthreads();
         }
-    }
-    rd = (rd + 1 == NSTAGE) ? 0 : rd + 1;
-    if (!more) n_in_flight--;
-
-    if (++cu_kt == cu_tile.nk) {
-      // ---------------- epilogue of tile cu_tile ----------------
-      const int m0 = cu_tile.m0, n0 = cu_tile.n0;
-      if (SWAP) {
-        // acc[i][j][r] = C[m0 + wm*64 + i*16 + (lane&15)][n0 + wn*64 + j*16 + 4*(lane>>4) + r]
-        const int cl = 4 * (lane >> 4);
-        const bool interior = (m0 + BM <= g.M) && (n0 + BN <= g.N);
-        // 16 stores per lane issued after the youngest DMA (interior, store-only epilogue): the next
-        // wait may leave them in flight.  Any count <= the true number of younger ops is safe.
-        const bool plain = interior && !g.resid && !g.dact_y && !(g.out_f32 && g.beta_acc);
-        if (plain) extra_vm = 16;
+      }
+      if (kt + NS - 1 < nk) {
+        int ws = rd + NS - 1;
+        if (ws >= NS) ws -= NS;
+        unsigned short* st = smem + ws * 2 * TILE_ELEMS;
+        stage_tile<AK>(rA, g.lda, ti.kbeg + (kt + NS - 1) * BKK, voA, st, w);
+        stage_tile<BKM>(rB, g.ldb, ti.kbeg + (kt + NS - 1) * BKK, voB, st + TILE_ELEMS, w);
+      }
+      const unsigned short* ta = smem + rd * 2 * TILE_ELEMS;
+      const unsigned short* tb = ta + TILE_ELEMS;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int col = n0 + wn * 64 + j * 16 + cl;
-          float4 bia = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (g.bias && (interior || col + 3 < g.N)) bia = *(const float4*)(g.bias + col);
-          else if (g.bias) {
-            if (col < g.N) bia.x = g.bias[col];
-            if (col + 1 < g.N) bia.y = g.bias[col + 1];
-            if (col + 2 < g.N) bia.z = g.bias[col + 2];
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t af[4], bf[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = read_frag<AK>(ta, wm * 64 + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf[j] = read_frag<BKM>(tb, wn * 64 + j * 16, ks, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (SWAP) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+            else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
           }
-          const float bb[4] = {bia.x, bia.y, bia.z, bia.w};
+      }
+      rd = (rd + 1 == NS) ? 0 : rd + 1;
+    }
+    // ---------------- epilogue (no DMA in flight) ----------------
+    if (SWAP) {
+      // acc[i][j][r] = C[m0 + wm*64 + i*16 + (lane&15)][n0 + wn*64 + j*16 + 4*(lane>>4) + r]
+      const int cl = 4 * (lane >> 4);
+      const bool interior = (m0 + BM <= g.M) && (n0 + BN <= g.N);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int row = m0 + wm * 64 + i * 16 + (lane & 15);
-            const long cidx = (long)row * g.ldc + col;
-            if (g.out_f32) {
-              float* C = (float*)g.C + cidx;
-              float4 v = make_float4(acc[i][j][0] * g.alpha, acc[i][j][1] * g.alpha, acc[i][j][2] * g.alpha,
-                                     acc[i][j][3] * g.alpha);
-              if (interior || (row < g.M && col + 3 < g.N)) {
-                if (g.beta_acc) { float4 o = *(float4*)C; v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w; }
-                *(float4*)C = v;
-              } else if (row < g.M) {
-                float vv[4] = {v.x, v.y, v.z, v.w};
-                for (int r = 0; r < 4; ++r)
-                  if (col + r < g.N) C[r] = g.beta_acc ? C[r] + vv[r] : vv[r];
-              }
-            } else if (interior || (row < g.M && col + 3 < g.N)) {
-              float o[4];
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wn * 64 + j * 16 + cl;
+        float4 bia = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (g.bias && (interior || col + 3 < g.N)) bia = *(const float4*)(g.bias + col);
+        else if (g.bias) {
+          if (col < g.N) bia.x = g.bias[col];
+          if (col + 1 < g.N) bia.y = g.bias[col + 1];
+          if (col + 2 < g.N) bia.z = g.bias[col + 2];
+        }
+        const float bb[4] = {bia.x, bia.y, bia.z, bia.w};
 #pragma unroll
-              for (int r = 0; r < 4; ++r) o[r] = epi_val(g, acc[i][j][r], bb[r], row, col + r, cidx + r, seed);
-              uint2 pk;
-              pk.x = pack2bf(o[0], o[1]);
-              pk.y = pack2bf(o[2], o[3]);
-              *(uint2*)((unsigned short*)g.C + cidx) = pk;
+        for (int i = 0; i < 4; ++i) {
+          const int row = m0 + wm * 64 + i * 16 + (lane & 15);
+          const long cidx = (long)row * g.ldc + col;
+          if (g.out_f32) {
+            float* C = (float*)g.C + cidx;
+            float4 v = make_float4(acc[i][j][0] * g.alpha, acc[i][j][1] * g.alpha, acc[i][j][2] * g.alpha,
+                                   acc[i][j][3] * g.alpha);
+            if (interior || (row < g.M && col + 3 < g.N)) {
+              if (g.beta_acc) { float4 o = *(float4*)C; v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w; }
+              *(float4*)C = v;
             } else if (row < g.M) {
+              float vv[4] = {v.x, v.y, v.z, v.w};
               for (int r = 0; r < 4; ++r)
-                if (col + r < g.N)
-                  ((unsigned short*)g.C)[cidx + r] = f2bf(epi_val(g, acc[i][j][r], bb[r], row, col + r, cidx + r, seed));
+                if (col + r < g.N) C[r] = g.beta_acc ? C[r] + vv[r] : vv[r];
             }
-            acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+          } else if (interior || (row < g.M && col + 3 < g.N)) {
+            float o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = epi_val(g, acc[i][j][r], bb[r], row, col + r, cidx + r, seed);
+            uint2 pk;
+            pk.x = pack2bf(o[0], o[1]);
+            pk.y = pack2bf(o[2], o[3]);
+            *(uint2*)((unsigned short*)g.C + cidx) = pk;
+          } else if (row < g.M) {
+            for (int r = 0; r < 4; ++r)
+              if (col + r < g.N)
+                ((unsigned short*)g.C)[cidx + r] = f2bf(epi_val(g, acc[i][j][r], bb[r], row, col + r, cidx + r, seed));
           }
         }
-      } else {
-        // acc[i][j][r] = C[m0 + wm*64 + i*16 + 4*(lane>>4) + r][n0 + wn*64 + j*16 + (lane&15)]
-        const int cl = lane & 15, rg = (lane >> 4) * 4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int col = n0 + wn * 64 + j * 16 + cl;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int row = m0 + wm * 64 + i * 16 + rg + r;
-              if (row < g.M && col < g.N) {
-                const long cidx = (long)row * g.ldc + col;
-                float* C = (float*)g.C;
-                const float v = acc[i][j][r] * g.alpha;
-                if (g.atomic) atomicAdd(C + cidx, v);
-                else C[cidx] = g.beta_acc ? C[cidx] + v : v;
-              }
-            }
-            acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-          }
-        }
-        extra_vm = 0;
       }
-      cu_kt = 0;
-      if (++cu_i >= my_ntiles) break;
-      cu_tile = tile_of(g, blockIdx.x + cu_i * gridDim.x, ntn, nwg);
+    } else {
+      // acc[i][j][r] = C[m0 + wm*64 + i*16 + 4*(lane>>4) + r][n0 + wn*64 + j*16 + (lane&15)]
+      const int cl = lane & 15, rg = (lane >> 4) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wn * 64 + j * 16 + cl;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = m0 + wm * 64 + i * 16 + rg + r;
+            if (row < g.M && col < g.N) {
+              const long cidx = (long)row * g.ldc + col;
+              float* C = (float*)g.C;
+              const float v = acc[i][j][r] * g.alpha;
+              if (g.atomic) atomicAdd(C + cidx, v);
+              else C[cidx] = g.beta_acc ? C[cidx] + v : v;
+            }
+          }
+        }
+      }
     }
-    if (n_in_flight < 0) break;  // defensive: never spin past the stream
+    __syncthreads();  // every wave is done with the LDS stages before the next tile's prologue
   }
 }
 
@@ -357,14 +323,15 @@ extern "C" int smi_gemm(const GemmArgs* args, hipStream_t st) {
   g.b_bytes = 2 * (bk ? (long)(g.K - 1) * g.ldb + g.N : (long)(g.N - 1) * g.ldb + g.K);
   if (g.a_bytes >= (1L << 31) || g.b_bytes >= (1L << 31)) return -1;
   const int ntiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN) * g.splits;
-  const int grid = ntiles < NUM_CU ? ntiles : NUM_CU;
+  const int maxg = NUM_CU * (GEMM_NS == 2 ? 2 : 1);
+  const int grid = ntiles < maxg ? ntiles : maxg;
   const bool atomic = g.out_f32 && g.atomic;
   switch (g.mode) {
-    case 0: hipLaunchKernelGGL((gemm_bf16_kernel<false, false, true>), dim3(grid), dim3(256), 0, st, g); break;
-    case 1: hipLaunchKernelGGL((gemm_bf16_kernel<false, true, true>), dim3(grid), dim3(256), 0, st, g); break;
+    case 0: hipLaunchKernelGGL((gemm_bf16_kernel<false, false, true, GEMM_NS>), dim3(grid), dim3(256), 0, st, g); break;
+    case 1: hipLaunchKernelGGL((gemm_bf16_kernel<false, true, true, GEMM_NS>), dim3(grid), dim3(256), 0, st, g); break;
     case 2:
-      if (atomic) hipLaunchKernelGGL((gemm_bf16_kernel<true, true, false>), dim3(grid), dim3(256), 0, st, g);
-      else hipLaunchKernelGGL((gemm_bf16_kernel<true, true, true>), dim3(grid), dim3(256), 0, st, g);
+      if (atomic) hipLaunchKernelGGL((gemm_bf16_kernel<true, true, false, GEMM_NS>), dim3(grid), dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((gemm_bf16_kernel<true, true, true, GEMM_NS>), dim3(grid), dim3(256), 0, st, g);
       break;
     default: return -1;
   }

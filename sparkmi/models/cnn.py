@@ -1,0 +1,40 @@
+"""FashionMNISTModel — the reference CNN (distributed_cnn.py:47-86, pytorch_cnn.py:12-49) with the
+same module names (block_1 / block_2 / classifier, nn.Sequential indices) so reference
+state_dicts load.  ``loss(x, y)`` runs the fused whole-network HIP kernel (sparkmi/ops/cnn.py);
+``forward(x)`` returns logits (fused inference kernel on GPU, torch ops on CPU).
+"""
+import torch
+from torch import nn
+
+from ..ops.cnn import cnn_logits, cnn_loss
+
+
+class FashionMNISTModel(nn.Module):
+    def __init__(self, input_shape: int = 1, hidden_units: int = 10, output_shape: int = 10):
+        super().__init__()
+        self.block_1 = nn.Sequential(
+            nn.Conv2d(input_shape, hidden_units, kernel_size=3, stride=1, padding=1), nn.ReLU(),
+            nn.Conv2d(hidden_units, hidden_units, kernel_size=3, stride=1, padding=1), nn.ReLU(),
+            nn.MaxPool2d(kernel_size=2, stride=2))
+        self.block_2 = nn.Sequential(
+            nn.Conv2d(hidden_units, hidden_units, 3, padding=1), nn.ReLU(),
+            nn.Conv2d(hidden_units, hidden_units, 3, padding=1), nn.ReLU(),
+            nn.MaxPool2d(2))
+        self.classifier = nn.Sequential(nn.Flatten(), nn.Linear(hidden_units * 7 * 7, output_shape))
+
+    def param_list(self):
+        c = [self.block_1[0], self.block_1[2], self.block_2[0], self.block_2[2], self.classifier[1]]
+        out = []
+        for m in c:
+            out += [m.weight, m.bias]
+        return out
+
+    def forward(self, x):
+        return cnn_logits(x, self.param_list())
+
+    def loss(self, x, y):
+        """Mean CE over the batch (distributed_cnn.py:141,177)."""
+        return cnn_loss(x, y, self.param_list())
+
+
+CNN = FashionMNISTModel
