@@ -18,6 +18,7 @@ using u = uintptr_t;
 #include "smi_mlp.h"
 #include "smi_gemm.h"
 #include "smi_cnn.h"
+#include "smi_lstm.h"
 #include <pybind11/stl.h>
 #include <vector>
 
@@ -47,6 +48,8 @@ int smi_cnn_reduce(const CNNArgs*, hipStream_t);
 int smi_gather_rows(const void*, const long long*, void*, long, long, hipStream_t);
 int smi_gather_u8_scale(const void*, const long long*, void*, long, long, float, int, hipStream_t);
 int smi_mlp_bwd(const MLPArgs*, hipStream_t);
+int smi_lstm(const LSTMArgs*, int, hipStream_t);
+int smi_lstm_supported(int, int, int, int);
 int smi_adam(float*, float*, float*, float*, void*, long, const float*, const float*, float, float, float, float, float,
              int, int, hipStream_t);
 int smi_sgd(float*, float*, float*, void*, long, const float*, const float*, float, float, float, int, float, int,
@@ -195,5 +198,38 @@ PYBIND11_MODULE(_C, m) {
     a.P = o; a.slab = (float*)slab; a.row_loss = (float*)row_loss; a.pred = (int*)pred; a.logits = (float*)logits;
     a.loss = (float*)loss; a.loss_scale = loss_scale; a.dloss = (const float*)dloss; a.train = train;
     chk(phase == 0 ? smi_cnn(&a, S(st)) : smi_cnn_reduce(&a, S(st)), "cnn");
+  });
+
+  m.def("lstm_supported", [](int E, int H, int L, int C) { return smi_lstm_supported(E, H, L, C) != 0; });
+  // LSTM: pointer lists per layer; dict-free flat signature (forward fills pred/hn/cn/ws,
+  // backward reads ws + dpred/dhn/dcn and accumulates into the g_* buffers).
+  m.def("lstm", [](int backward, u ids, int B, int T, int E, int H, int L, int C, long long pad_idx, u emb,
+                   std::vector<u> w_ih, std::vector<u> w_hh, std::vector<u> b_ih, std::vector<u> b_hh, u w_fc, u b_fc,
+                   u h0, u c0, u pred, u hn, u cn, u ws, u ws_da, u seedp, uint32_t salt, uint32_t thresh, float dscale,
+                   u dpred, u dhn, u dcn, u g_emb, std::vector<u> g_w_ih, std::vector<u> g_w_hh, std::vector<u> g_b_ih,
+                   std::vector<u> g_b_hh, u g_w_fc, u g_b_fc, u dh0, u dc0, u st) {
+    if (L < 1 || L > LSTM_MAXL || (int)w_ih.size() != L || (int)w_hh.size() != L || (int)b_ih.size() != L ||
+        (int)b_hh.size() != L)
+      throw std::runtime_error("lstm: need L pointers per weight list");
+    if (backward && ((int)g_w_ih.size() != L || (int)g_w_hh.size() != L || (int)g_b_ih.size() != L ||
+                     (int)g_b_hh.size() != L))
+      throw std::runtime_error("lstm: need L gradient pointers per list");
+    LSTMArgs a{};
+    a.ids = (const long long*)ids; a.B = B; a.T = T; a.E = E; a.H = H; a.L = L; a.C = C; a.pad_idx = pad_idx;
+    a.emb = (const float*)emb;
+    for (int i = 0; i < L; ++i) {
+      a.w_ih[i] = (const float*)w_ih[i]; a.w_hh[i] = (const float*)w_hh[i];
+      a.b_ih[i] = (const float*)b_ih[i]; a.b_hh[i] = (const float*)b_hh[i];
+      if (backward) {
+        a.g_w_ih[i] = (float*)g_w_ih[i]; a.g_w_hh[i] = (float*)g_w_hh[i];
+        a.g_b_ih[i] = (float*)g_b_ih[i]; a.g_b_hh[i] = (float*)g_b_hh[i];
+      }
+    }
+    a.w_fc = (const float*)w_fc; a.b_fc = (const float*)b_fc; a.h0 = (const float*)h0; a.c0 = (const float*)c0;
+    a.pred = (float*)pred; a.hn = (float*)hn; a.cn = (float*)cn; a.ws = (float*)ws; a.ws_da = (float*)ws_da;
+    a.seedp = (const uint32_t*)seedp; a.salt = salt; a.thresh = thresh; a.dscale = dscale;
+    a.dpred = (const float*)dpred; a.dhn = (const float*)dhn; a.dcn = (const float*)dcn;
+    a.g_emb = (float*)g_emb; a.g_w_fc = (float*)g_w_fc; a.g_b_fc = (float*)g_b_fc; a.dh0 = (float*)dh0; a.dc0 = (float*)dc0;
+    chk(smi_lstm(&a, backward, S(st)), "lstm");
   });
 }

@@ -1,0 +1,28 @@
+// Argument block shared by csrc/kernels/lstm.hip and csrc/bindings.cpp.
+#pragma once
+#include <stdint.h>
+#define LSTM_MAXL 4
+#define LSTM_MAXC 16
+struct LSTMArgs {
+  const long long* ids;                    // token ids [B][T]
+  int B, T, E, H, L, C;                    // batch, steps, embed dim, hidden, layers, fc outputs
+  long long pad_idx;                       // embedding row that receives no gradient (-1: none)
+  const float* emb;                        // [V][E]
+  const float* w_ih[LSTM_MAXL];            // [4H][E | H], gate order i,f,g,o (torch nn.LSTM)
+  const float* w_hh[LSTM_MAXL];            // [4H][H]
+  const float* b_ih[LSTM_MAXL];
+  const float* b_hh[LSTM_MAXL];
+  const float* w_fc; const float* b_fc;    // [C][H], [C]
+  const float* h0; const float* c0;        // [L][B][H] (null: zeros)
+  float* pred;                             // [B][T][C]
+  float* hn; float* cn;                    // [L][B][H]
+  float* ws;                               // saved activations [B][L][T][6H] (i,f,g,o,c,h)
+  float* ws_da;                            // layer-0 gate grads [B][T][4H] (backward scratch)
+  const uint32_t* seedp; uint32_t salt; uint32_t thresh; float dscale;  // inter-layer dropout
+  // backward
+  const float* dpred; const float* dhn; const float* dcn;
+  float* g_emb; float* g_w_ih[LSTM_MAXL]; float* g_w_hh[LSTM_MAXL];
+  float* g_b_ih[LSTM_MAXL]; float* g_b_hh[LSTM_MAXL];
+  float* g_w_fc; float* g_b_fc;
+  float* dh0; float* dc0;
+};

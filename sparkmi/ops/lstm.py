@@ -1,0 +1,131 @@
+"""Fused embedding -> stacked LSTM -> per-step linear head (csrc/kernels/lstm.hip).
+
+``lstm_classifier(ids, h0, c0, params, ...)`` returns ``(pred [B,T,C], h_n [L,B,H], c_n)`` —
+exactly ``fc_out(lstm(embedding(ids), (h0, c0))[0])`` of the reference model
+(distributed_lstm.py:110-135), including nn.LSTM's inter-layer dropout.  GPU: one persistent
+workgroup per sequence for the forward, one for BPTT; weight gradients are accumulated in fp32
+straight into ``param.grad`` (flat buffers), the embedding rows equal to ``padding_idx`` get no
+gradient.  CPU: the identical math written with torch ops (same counter-hash dropout masks),
+which is what the GPU kernel is tested against.
+"""
+import torch
+
+from .. import _native
+from . import rng as _rng
+from ._grad import grad_buf, grad_ready
+
+
+def unpack(params, L):
+    emb = params[0]
+    layers = [params[1 + 4 * i:5 + 4 * i] for i in range(L)]
+    w_fc, b_fc = params[1 + 4 * L], params[2 + 4 * L]
+    return emb, layers, w_fc, b_fc
+
+
+def reference_forward(ids, h0, c0, params, L, p=0.0, step_seed=0, salt=0, padding_idx=None):
+    """Torch reference (autograd-capable): embedding, L LSTM layers (gate order i,f,g,o), dropout
+    between layers with the kernel's counter-hash mask, linear head at every step."""
+    emb, layers, w_fc, b_fc = unpack(params, L)
+    B, T = ids.shape
+    H = layers[0][1].shape[1]
+    x = torch.nn.functional.embedding(ids, emb, padding_idx=padding_idx)
+    mask = None
+    if p > 0:
+        mask = _rng.keep_mask((B, T, L, H), p, step_seed, salt, ids.device)
+    hs, cs = [], []
+    for li, (w_ih, w_hh, b_ih, b_hh) in enumerate(layers):
+        h = h0[li] if h0 is not None else x.new_zeros(B, H)
+        c = c0[li] if c0 is not None else x.new_zeros(B, H)
+        outs = []
+        for t in range(T):
+            z = x[:, t] @ w_ih.t() + b_ih + h @ w_hh.t() + b_hh
+            i, f, g, o = z.chunk(4, dim=1)
+            i, f, g, o = torch.sigmoid(i), torch.sigmoid(f), torch.tanh(g), torch.sigmoid(o)
+            c = f * c + i * g
+            h = o * torch.tanh(c)
+            outs.append(h)
+        hs.append(h)
+        cs.append(c)
+        x = torch.stack(outs, 1)
+        if mask is not None and li + 1 < L:
+            x = x * mask[:, :, li, :].to(x.dtype) * _rng.scale(p)
+    pred = x @ w_fc.t() + b_fc
+    return pred, torch.stack(hs), torch.stack(cs)
+
+
+def supported(E, H, L, C):
+    return _native.has_native() and bool(_native.C().lstm_supported(E, H, L, C))
+
+
+class LSTMFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, h0, c0, meta, *params):
+        L, p, rng, salt, pad_idx = meta
+        emb, layers, w_fc, b_fc = unpack(params, L)
+        B, T = ids.shape
+        E, H, C = emb.shape[1], layers[0][1].shape[1], w_fc.shape[0]
+        dev = ids.device
+        ids = ids.to(torch.int64).contiguous()
+        if not all(t.is_contiguous() and t.dtype == torch.float32 for t in params):
+            raise ValueError("LSTM parameters must be contiguous fp32")
+        pred = torch.empty(B, T, C, device=dev, dtype=torch.float32)
+        hn = torch.empty(L, B, H, device=dev, dtype=torch.float32)
+        cn = torch.empty_like(hn)
+        ws = torch.empty(B, L, T, 6 * H, device=dev, dtype=torch.float32)
+        h0c = h0.float().contiguous() if h0 is not None else None
+        c0c = c0.float().contiguous() if c0 is not None else None
+        thresh = _rng.threshold(p)
+        _native.C().lstm(0, ids.data_ptr(), B, T, E, H, L, C, pad_idx, emb.data_ptr(),
+                         [lw[0].data_ptr() for lw in layers], [lw[1].data_ptr() for lw in layers],
+                         [lw[2].data_ptr() for lw in layers], [lw[3].data_ptr() for lw in layers],
+                         w_fc.data_ptr(), b_fc.data_ptr(), _native.ptr(h0c), _native.ptr(c0c), pred.data_ptr(),
+                         hn.data_ptr(), cn.data_ptr(), ws.data_ptr(), 0, rng.ptr() if rng is not None else 0, salt,
+                         thresh, _rng.scale(p), 0, 0, 0, 0, [], [], [], [], 0, 0, 0, 0, _native.stream())
+        ctx.meta = (L, p, rng, salt, pad_idx, B, T, E, H, C)
+        ctx.has_h0, ctx.has_c0 = h0 is not None, c0 is not None
+        ctx.save_for_backward(ids, ws, h0c, c0c, *params)
+        return pred, hn, cn
+
+    @staticmethod
+    def backward(ctx, dpred, dhn, dcn):
+        L, p, rng, salt, pad_idx, B, T, E, H, C = ctx.meta
+        ids, ws, h0c, c0c, *params = ctx.saved_tensors
+        emb, layers, w_fc, b_fc = unpack(params, L)
+        dev = ids.device
+        dpred = dpred.float().contiguous() if dpred is not None else torch.zeros(B, T, C, device=dev)
+        dhn = dhn.float().contiguous() if dhn is not None else None
+        dcn = dcn.float().contiguous() if dcn is not None else None
+        ws_da = torch.empty(B, T, 4 * H, device=dev, dtype=torch.float32)
+        dh0 = torch.empty(L, B, H, device=dev) if ctx.needs_input_grad[1] else None
+        dc0 = torch.empty(L, B, H, device=dev) if ctx.needs_input_grad[2] else None
+        orig = params
+        g = [grad_buf(t) for t in orig]
+        g_emb, g_layers, g_fc, g_bfc = unpack(g, L)
+        _native.C().lstm(1, ids.data_ptr(), B, T, E, H, L, C, pad_idx, emb.data_ptr(),
+                         [lw[0].data_ptr() for lw in layers], [lw[1].data_ptr() for lw in layers],
+                         [lw[2].data_ptr() for lw in layers], [lw[3].data_ptr() for lw in layers],
+                         w_fc.data_ptr(), b_fc.data_ptr(), _native.ptr(h0c), _native.ptr(c0c), 0, 0, 0,
+                         ws.data_ptr(), ws_da.data_ptr(), rng.ptr() if rng is not None else 0, salt,
+                         _rng.threshold(p), _rng.scale(p), dpred.data_ptr(), _native.ptr(dhn), _native.ptr(dcn),
+                         g_emb.data_ptr() if orig[0].requires_grad else 0,
+                         [lw[0].data_ptr() for lw in g_layers], [lw[1].data_ptr() for lw in g_layers],
+                         [lw[2].data_ptr() for lw in g_layers], [lw[3].data_ptr() for lw in g_layers],
+                         g_fc.data_ptr(), g_bfc.data_ptr(), _native.ptr(dh0), _native.ptr(dc0), _native.stream())
+        grad_ready(*orig)
+        return (None, dh0 if ctx.has_h0 else None, dc0 if ctx.has_c0 else None, None) + (None,) * len(params)
+
+
+def lstm_classifier(ids, h0, c0, params, num_layers, dropout=0.0, training=True, rng=None, salt=0,
+                    padding_idx=None):
+    """pred, h_n, c_n of embedding -> LSTM(num_layers, dropout) -> linear head (every step)."""
+    p = dropout if training else 0.0
+    emb, layers, w_fc, _ = unpack(params, num_layers)
+    E, H, C = emb.shape[1], layers[0][1].shape[1], w_fc.shape[0]
+    if ids.is_cuda and _native.use_native(ids):
+        if not supported(E, H, num_layers, C):
+            raise NotImplementedError(f"sparkmi LSTM kernel: unsupported shape E={E} H={H} L={num_layers} C={C} "
+                                      "(H in {16,32,64}, 4*H*L <= 512, E <= 2H and <= 64, C <= 16)")
+        pad = -1 if padding_idx is None else int(padding_idx)
+        return LSTMFn.apply(ids, h0, c0, (num_layers, p, rng, salt, pad), *params)
+    seed = rng.current() if (rng is not None and p > 0) else 0
+    return reference_forward(ids, h0, c0, params, num_layers, p, seed, salt, padding_idx)
