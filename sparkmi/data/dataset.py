@@ -145,6 +145,7 @@ class DeviceLoader:
         self.batch_size, self.shuffle, self.drop_last, self.seed = batch_size, shuffle, drop_last, seed
         self.image_scale, self.image_dtype = image_scale, image_dtype
         self.epoch = 0
+        self.skip = 0  # batches of the current epoch already consumed (exact resume)
 
     def set_epoch(self, e):
         self.epoch = e
@@ -161,7 +162,8 @@ class DeviceLoader:
 
     def __iter__(self):
         perm = self._perm()
-        for b in range(len(self)):
+        start, self.skip = self.skip, 0
+        for b in range(start, len(self)):
             idx = perm[b * self.batch_size:(b + 1) * self.batch_size]
             out = []
             for i, a in enumerate(self.arrays):

@@ -108,3 +108,52 @@ def sentences(n, min_words=4, max_words=14, seed=0):
             s += ","
         out.append(s + rng.choice([".", "!", "?"]))
     return out
+
+
+_TOPICS = {
+    1: "world government minister election president war peace talks country leaders capital".split(),
+    2: "sports game team season coach player win championship league score match".split(),
+    3: "business market stocks company profit shares oil prices economy deal bank".split(),
+    4: "technology software internet computer space research science phone web data".split(),
+}
+
+
+def ag_news_text(n, seed=0, min_words=8, max_words=60):
+    """AG_NEWS-like (label, text) pairs with labels 1..4 (torchtext AG_NEWS yields 1-based labels,
+    distributed_lstm.py:180 subtracts 1).  Each text mixes topic words with filler words and
+    numbers, so basic_english tokenisation, vocab building and the <sos>/<eos>/truncate/pad
+    transforms are exercised on realistic strings."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        lab = int(rng.integers(1, 5))
+        k = int(rng.integers(min_words, max_words + 1))
+        topic = _TOPICS[lab]
+        words = []
+        for _ in range(k):
+            r = rng.random()
+            if r < 0.35:
+                words.append(topic[int(rng.integers(0, len(topic)))])
+            elif r < 0.45:
+                words.append(str(int(rng.integers(0, 100))))
+            else:
+                words.append(_WORDS[int(rng.integers(0, len(_WORDS)))])
+        text = " ".join(words).capitalize() + rng.choice([".", "!", "?", " (AP)"])
+        out.append((lab, text))
+    return out
+
+
+def _pseudo_de(word):
+    return (word[::-1] + "en") if word.isalpha() else word
+
+
+def translation_text(n, seed=0, min_words=4, max_words=14):
+    """Multi30k-like parallel corpus of (english, pseudo-german) sentence pairs; the German side
+    is a deterministic word-level mapping of the English side, so a translator can learn it
+    (pytorch_machine_translator.py:14-16 reads Multi30k, unavailable offline)."""
+    out = []
+    for s in sentences(n, min_words, max_words, seed):
+        words = s.split(" ")
+        de = " ".join(_pseudo_de(w.lower().strip(".,!?")) for w in words) + s[-1]
+        out.append((s, de.capitalize()))
+    return out

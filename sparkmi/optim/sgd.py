@@ -39,3 +39,14 @@ class SGD(_FlatOptimizer):
                 f.grad.zero_()
             if f.shadow is not None:
                 f.shadow.copy_(f.master.to(torch.bfloat16))
+
+    def state_dict(self):
+        sd = super().state_dict()
+        if self.buf is not None:
+            sd["momentum_buffer"] = self.buf.clone()
+        return sd
+
+    def load_state_dict(self, sd):
+        super().load_state_dict(sd)
+        if self.buf is not None and "momentum_buffer" in sd:
+            self.buf.copy_(sd["momentum_buffer"])

@@ -1,0 +1,119 @@
+"""Epoch/step training loop shared by every recipe.
+
+One executor (= one MI355X, one process) runs ``Trainer.fit``: per step the StepRunner does
+seed bump -> fused forward/loss -> fused backward (grads into the flat fp32 buffer; with
+data parallelism bucketed RCCL all-reduces overlap the backward) -> fused optimizer, captured
+in a HIP graph when running on a single executor.  Around it: ROCTx ranges, device-side
+metrics accumulation (one host sync per ``log_every`` steps), fault-injection points,
+periodic atomic checkpoints, and exact resume (model + optimizer + dropout seeds + RNG + epoch
++ batch cursor; the per-epoch shuffles are seeded by seed+epoch so the resumed order matches).
+
+Reference loops this replaces: distributed_multilayer_perceptron.py:97-145,
+distributed_cnn.py:149-193, distributed_lstm.py:156-205, pytorch_machine_translator.py:140-209.
+"""
+import time
+
+import torch
+
+from ..parallel import DataParallel, init_distributed
+from ..runtime.fault import fault_point
+from ..utils import trace
+from ..utils.checkpoint import CheckpointManager
+from ..utils.flat import FlatParams
+from ..utils.metrics import MetricsLogger
+from .runner import StepRunner
+
+
+def setup_executor(cfg):
+    """Process-group + device for this executor (RCCL on GPU executors, gloo on CPU)."""
+    import os
+    if cfg.device == "cpu":
+        os.environ["SPARKMI_FORCE_CPU"] = "1"
+    rank, world, device = init_distributed()
+    torch.manual_seed(cfg.seed)
+    return rank, world, device
+
+
+class Trainer:
+    def __init__(self, model, loss_fn, make_optimizer, cfg, device, rank=0, world=1, name="run", shadow=None):
+        self.model = model.to(device)
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.rank, self.world = rank, world
+        self.flat = FlatParams(self.model, device=self.device, shadow=shadow)
+        self.opt = make_optimizer(self.flat)
+        self.ddp = DataParallel(self.flat, bucket_mb=cfg.bucket_mb) if world > 1 else None
+        use_graph = bool(cfg.graph) and self.device.type == "cuda" and world == 1
+        self.runner = StepRunner(self.model, loss_fn, self.opt, ddp=self.ddp, graph=use_graph)
+        path = f"{cfg.metrics}.rank{rank}.jsonl" if cfg.metrics else None
+        self.metrics = MetricsLogger(path, rank=rank, every=cfg.log_every, echo=cfg.verbose and rank == 0,
+                                     extra={"run": name, "world": world})
+        self.ckpt = CheckpointManager(cfg.ckpt_dir, rank=rank) if cfg.ckpt_dir else None
+        self.step = 0
+        self.epoch = 0
+        self.cursor = 0
+        self.resumed_from = None
+
+    def maybe_resume(self):
+        if self.ckpt is None or not self.cfg.resume:
+            return None
+        meta = self.ckpt.restore(self.model, self.opt)
+        if meta is None:
+            return None
+        self.step, self.epoch, self.cursor = meta["step"], meta["epoch"], meta["cursor"]
+        self.resumed_from = self.ckpt.latest()
+        return meta
+
+    def _save(self, cursor):
+        if self.ckpt is not None:
+            with trace.range("checkpoint"):
+                self.ckpt.save(self.step, self.model, self.opt, self.epoch, cursor)
+            if self.world > 1:
+                from ..parallel import barrier
+                barrier()
+
+    def fit(self, loader, epochs, samples_per_batch=None):
+        """Train over ``loader`` (an epoch-seeded DeviceLoader-like iterable) for ``epochs``."""
+        cfg = self.cfg
+        self.maybe_resume()
+        t0 = time.perf_counter()
+        steps_run, last = 0, None
+        done = False
+        while self.epoch < epochs and not done:
+            if hasattr(loader, "set_epoch"):
+                loader.set_epoch(self.epoch)
+            if hasattr(loader, "skip"):
+                loader.skip = self.cursor
+            i = self.cursor
+            for batch in loader:
+                n = samples_per_batch or int(batch[0].shape[0])
+                with trace.range("step"):
+                    last = self.runner.step(*batch)
+                self.step += 1
+                steps_run += 1
+                i += 1
+                self.metrics.step(last, n * self.world)
+                fault_point(self.step)
+                if self.ckpt is not None and cfg.ckpt_every and self.step % cfg.ckpt_every == 0:
+                    self.cursor = i
+                    self._save(i)
+                if cfg.max_steps and self.step >= cfg.max_steps:
+                    done = True
+                    break
+            if not done:
+                self.epoch += 1
+                self.cursor = 0
+                if self.ckpt is not None and not cfg.ckpt_every:
+                    self._save(0)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        dt = time.perf_counter() - t0
+        self.metrics.flush()
+        return {"steps": steps_run, "global_step": self.step, "time_s": dt,
+                "final_loss": float(last.item()) if last is not None else None,
+                "resumed_from": self.resumed_from}
+
+    def close(self):
+        self.metrics.close()
+        if self.ddp is not None:
+            self.ddp.close()

@@ -55,6 +55,7 @@ class FlatParams:
                 if self.shadow is not None:
                     p._smi_bf16 = self.shadow[o:o + n].view(p.shape)
         self.index = {id(p): i for i, p in enumerate(self.params)}
+        object.__setattr__(module, "_smi_flat", self)  # checkpoint loads refresh the bf16 shadow
         self.refresh_shadow()
 
     def refresh_shadow(self):
