@@ -46,12 +46,13 @@ def iris_libsvm_text(n=150, num_features=4, num_classes=3, seed=1234, sparsify=T
     return "\n".join(lines) + "\n"
 
 
-def fashion_mnist_like(n=60000, seed=0, device="cpu"):
+def fashion_mnist_like(n=60000, seed=0, device="cpu", proto_seed=0):
     """uint8 images [n,1,28,28] and int64 labels [n] with class-dependent structure (10 classes),
-    the shape of torchvision FashionMNIST (distributed_cnn.py:90-106)."""
+    the shape of torchvision FashionMNIST (distributed_cnn.py:90-106).  The class prototypes come
+    from ``proto_seed`` (shared by train and test splits), the samples from ``seed``."""
+    proto = torch.rand(10, 1, 28, 28, generator=_gen(proto_seed + 7919, "cpu")).to(device)
     g = _gen(seed, device)
     labels = torch.randint(0, 10, (n,), generator=g, device=device)
-    proto = torch.rand(10, 1, 28, 28, generator=g, device=device)
     noise = torch.rand(n, 1, 28, 28, generator=g, device=device)
     img = (0.6 * proto[labels] + 0.4 * noise) * 255.0
     return img.to(torch.uint8), labels
