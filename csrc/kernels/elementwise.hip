@@ -72,6 +72,7 @@ __global__ void colsum_bf16_kernel(const unsigned short* __restrict__ x, long M,
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
   if (cv * 8 + 8 <= N && (N % 8) == 0) {
+#pragma unroll 8  // independent loads in flight (a rolled loop is one memory latency per row)
     for (long r = r0 + rphase; r < r1; r += 8) {
       u16x8_t v = *(const u16x8_t*)(x + r * N + cv * 8);
 #pragma unroll

@@ -25,6 +25,7 @@
 // zeroing the out-of-range A columns of the last k-tile in LDS.
 #include "smi_common.h"
 #include "smi_gemm.h"
+#include <stdlib.h>
 
 #define BM 128
 #define BN 128
@@ -162,7 +163,7 @@ __device__ __forceinline__ TileInfo tile_of(const GemmArgs& g, int t, int ntn, i
 // k-loop with counted waits, drain, epilogue.  With NS = 2 (64 KiB LDS) two workgroups share a
 // CU, so one's prologue/epilogue overlaps the other's MFMA loop.
 template <bool AK, bool BKM, bool SWAP, int NS>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
+__global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void gemm_bf16_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) unsigned short smem[NS * 2 * TILE_ELEMS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -323,17 +324,28 @@ extern "C" int smi_gemm(const GemmArgs* args, hipStream_t st) {
   g.b_bytes = 2 * (bk ? (long)(g.K - 1) * g.ldb + g.N : (long)(g.N - 1) * g.ldb + g.K);
   if (g.a_bytes >= (1L << 31) || g.b_bytes >= (1L << 31)) return -1;
   const int ntiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN) * g.splits;
-  const int maxg = NUM_CU * (GEMM_NS == 2 ? 2 : 1);
+  // pipeline depth: NS=2 (64 KiB LDS, two workgroups per CU) or NS=4 (128 KiB, one per CU,
+  // three k-steps in flight).  SMI_GEMM_NS overrides the default.
+  static int ns_env = -1;
+  if (ns_env < 0) {
+    const char* e = getenv("SMI_GEMM_NS");
+    ns_env = e ? atoi(e) : 0;
+  }
+  const int ns = ns_env == 2 || ns_env == 4 ? ns_env : GEMM_NS;
+  const int maxg = NUM_CU * (ns == 2 ? 2 : 1);
   const int grid = ntiles < maxg ? ntiles : maxg;
   const bool atomic = g.out_f32 && g.atomic;
-  switch (g.mode) {
-    case 0: hipLaunchKernelGGL((gemm_bf16_kernel<false, false, true, GEMM_NS>), dim3(grid), dim3(256), 0, st, g); break;
-    case 1: hipLaunchKernelGGL((gemm_bf16_kernel<false, true, true, GEMM_NS>), dim3(grid), dim3(256), 0, st, g); break;
-    case 2:
-      if (atomic) hipLaunchKernelGGL((gemm_bf16_kernel<true, true, false, GEMM_NS>), dim3(grid), dim3(256), 0, st, g);
-      else hipLaunchKernelGGL((gemm_bf16_kernel<true, true, true, GEMM_NS>), dim3(grid), dim3(256), 0, st, g);
-      break;
-    default: return -1;
+#define SMI_GEMM_LAUNCH(NSV)                                                                                         \
+  switch (g.mode) {                                                                                                  \
+    case 0: hipLaunchKernelGGL((gemm_bf16_kernel<false, false, true, NSV>), dim3(grid), dim3(256), 0, st, g); break; \
+    case 1: hipLaunchKernelGGL((gemm_bf16_kernel<false, true, true, NSV>), dim3(grid), dim3(256), 0, st, g); break;  \
+    case 2:                                                                                                          \
+      if (atomic) hipLaunchKernelGGL((gemm_bf16_kernel<true, true, false, NSV>), dim3(grid), dim3(256), 0, st, g);   \
+      else hipLaunchKernelGGL((gemm_bf16_kernel<true, true, true, NSV>), dim3(grid), dim3(256), 0, st, g);           \
+      break;                                                                                                         \
+    default: return -1;                                                                                              \
   }
+  if (ns == 4) { SMI_GEMM_LAUNCH(4) } else { SMI_GEMM_LAUNCH(2) }
+#undef SMI_GEMM_LAUNCH
   SMI_CHECK_LAUNCH();
 }

@@ -12,7 +12,6 @@ from .. import _native
 from . import rng as _rng
 from ._grad import grad_buf, grad_ready
 
-_LN_BWD_BLOCKS = 256
 
 
 def _ref_forward(h, r, gamma, beta, p, seed, salt, eps):
@@ -66,7 +65,9 @@ class AddDropoutLayerNorm(torch.autograd.Function):
             dy = dy.contiguous()
             dres = torch.empty_like(dy) if ctx.has_r else None
             dh = torch.empty_like(dy)
-            nb = min(_LN_BWD_BLOCKS, (M + 3) // 4)
+            vpl = (D + 511) // 512
+            rows_per_block = 4 * (4 if vpl == 1 else (2 if vpl == 2 else 1))  # ln_bwd_kernel<VPL, RPW>
+            nb = (M + rows_per_block - 1) // rows_per_block
             part = torch.empty(2, nb, D, device=dy.device, dtype=torch.float32)
             C.ln_bwd(dy.data_ptr(), xs.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(),
                      _native.ptr(dres), dh.data_ptr(), 0, part[0].data_ptr(), part[1].data_ptr(), nb,

@@ -76,7 +76,7 @@ def _colsum(dy2: torch.Tensor, out: torch.Tensor):
     """out (fp32 [N]) += column sums of dy2 (bf16 [M,N]); one HIP launch, fp32 atomics per block."""
     M, N = dy2.shape
     col_blocks = (N + 255) // 256
-    rpb = max(32, min(1024, ((M * col_blocks) // 512 + 7) // 8 * 8))  # ~512 blocks
+    rpb = max(64, min(1024, (M // 32 + 7) // 8 * 8))  # <= 32 adders per column (atomic contention)
     _native.C().colsum_bf16(dy2.data_ptr(), M, N, 0, rpb, out.data_ptr(), 1, _native.stream())
 
 

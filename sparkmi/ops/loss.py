@@ -25,8 +25,10 @@ class CrossEntropyFn(torch.autograd.Function):
             x2 = x2.contiguous()
             lse = torch.empty(M, device=x2.device, dtype=torch.float32)
             stats = torch.empty(2, device=x2.device, dtype=torch.float32)  # [count, loss]
+            row_loss = torch.empty(M, device=x2.device, dtype=torch.float32)
             C.ce_fwd(x2.data_ptr(), int(x2.dtype == torch.bfloat16), lab.data_ptr(), M, V, ignore_index,
-                     lse.data_ptr(), stats[0:1].data_ptr(), stats[1:2].data_ptr(), 0, _native.stream())
+                     lse.data_ptr(), stats[0:1].data_ptr(), stats[1:2].data_ptr(), row_loss.data_ptr(),
+                     _native.stream())
             ctx.save_for_backward(x2, lab, lse, stats)
             ctx.shape = logits.shape
             return stats[1].clone()

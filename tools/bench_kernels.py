@@ -10,16 +10,28 @@ from sparkmi import _native  # noqa: E402
 from sparkmi.ops import rng as R  # noqa: E402
 
 
-def timeit(fn, it=20):
-    for _ in range(3):
+def timeit(fn, reps=20, it=5):
+    """Replay a HIP graph of `reps` back-to-back launches: device time per launch, no host overhead."""
+    fn()
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
         fn()
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(it):
-        fn()
+        g.replay()
     e.record()
     e.synchronize()
-    return s.elapsed_time(e) / it * 1000  # us
+    return s.elapsed_time(e) / (reps * it) * 1000  # us
 
 
 def main():
@@ -38,10 +50,10 @@ def main():
     t = timeit(lambda: C.ln_fwd(h.data_ptr(), r.data_ptr(), g.data_ptr(), b.data_ptr(), y.data_ptr(), xs.data_ptr(),
                                 mean.data_ptr(), rstd.data_ptr(), M, D, 1e-5, seed.data_ptr(), 7, thr, 1.1, st()))
     print(f"ln_fwd      {t:8.1f} us  {4 * M * D * 2 / t / 1e3:7.0f} GB/s")
-    part = torch.empty(2, 256, D, device=dev)
+    part = torch.empty(2, 2048, D, device=dev)
     dres, dh = torch.empty_like(h), torch.empty_like(h)
     t = timeit(lambda: C.ln_bwd(h.data_ptr(), xs.data_ptr(), mean.data_ptr(), rstd.data_ptr(), g.data_ptr(),
-                                dres.data_ptr(), dh.data_ptr(), 0, part[0].data_ptr(), part[1].data_ptr(), 256,
+                                dres.data_ptr(), dh.data_ptr(), 0, part[0].data_ptr(), part[1].data_ptr(), 2048,
                                 g.data_ptr(), b.data_ptr(), 1, M, D, seed.data_ptr(), 7, thr, 1.1, st()))
     print(f"ln_bwd      {t:8.1f} us  {4 * M * D * 2 / t / 1e3:7.0f} GB/s")
     out = torch.zeros(D, device=dev)
@@ -75,8 +87,9 @@ def main():
     lab = torch.randint(0, V, (M,), device=dev)
     lse2 = torch.empty(M, device=dev)
     stats = torch.empty(2, device=dev)
+    rl = torch.empty(M, device=dev)
     t = timeit(lambda: C.ce_fwd(logits.data_ptr(), 1, lab.data_ptr(), M, V, 0, lse2.data_ptr(), stats.data_ptr(),
-                                stats.data_ptr() + 4, 0, st()))
+                                stats.data_ptr() + 4, rl.data_ptr(), st()))
     print(f"ce_fwd      {t:8.1f} us  {M * V * 2 / t / 1e3:7.0f} GB/s")
     grad = torch.empty_like(logits)
     dl = torch.ones(1, device=dev)
