@@ -12,60 +12,78 @@
 // kernels read q/k/v straight out of the fused qkv / kv projection outputs (per-head
 // interleaved [q_h|k_h|v_h] layout of transformer.py:76-79) and write O already head-merged.
 //
-// Structure (MI355X): one workgroup = 4 waves = 64 rows of the "owned" axis, 16 per wave.
-// The streamed operand (64-row chunks) is staged in LDS: a row-major image with the 16-B
-// chunk XOR swizzle (c ^ (row & 7)) for the ds_read_b128 A-operand reads, and a transposed
-// image with a 144-B row pitch (conflict-free ds_read_b64) for the B operand of the second
-// product.  S is computed transposed (K·Qᵀ) so each lane owns one query column and the
-// 16x16 accumulators of two adjacent key tiles form the bf16 A operand of P·V directly
-// (k order permuted identically on both operands; cdna_hip_programming.md §3).
+// Structure (MI355X): one workgroup = 4 waves = 128 rows of the "owned" axis (queries for the
+// forward and dQ, keys for dK/dV), 32 per wave as two 16-row MFMA sub-tiles that share every
+// LDS fragment.  The streamed operand goes through double-buffered 64-row LDS chunks (below).
+// Scores are computed with the owned axis on the lane (S^T = K Q^T in the forward), so the
+// online-softmax statistics and the output rescale are lane-local, and the 16x16 accumulators
+// of two adjacent 16-row tiles form the bf16 operand of the second product directly (k order
+// permuted identically on both operands; cdna_hip_programming.md §3).  Outputs are produced
+// transposed (O^T = V^T P^T etc.), so each lane stores 4 consecutive head-dim values.
 #include "smi_common.h"
 
 #define LOG2E_F 1.4426950408889634f
 
 #include "smi_attention.h"
 
-#define VT_PITCH 72  // transposed image row pitch in bf16 elements (144 B)
+// ---------------------------------------------------------------------------------------------
+// LDS images: 64 rows x 64 bf16 (128-B rows), 16-B chunk c of row r stored at chunk c ^ (r & 7).
+// The same image serves both operand reads conflict-free:
+//  * row fragments (ds_read_b128: 8 consecutive d of one row) — A operand with k = d;
+//  * transposed fragments (ds_read_b64_tr_b16: one d column of 4+4 rows) — A/B operand with
+//    k = row, in the permuted key order of two adjacent 16-row accumulator tiles, so a P / dS
+//    tile packed straight from the accumulators multiplies it without any register shuffle.
+// Chunks are double-buffered: the global loads of chunk c+1 are issued (16 B per lane, into
+// registers) before chunk c's MFMAs and stored to the other buffer after them.
+#define IMG_ELEMS (64 * 64)
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 64 + ((chunk ^ (row & 7)) << 3); }
 
-// Stage 64 rows x 64 d of X (row-major, swizzled) and optionally its transpose into LDS.
-__device__ __forceinline__ void stage_rows(const unsigned short* __restrict__ base, long ss, int r0, int rmax,
-                                           unsigned short* rowimg, unsigned short* trimg) {
-  for (int i = threadIdx.x; i < 512; i += 256) {
+struct Piece2 { u16x8_t v[2]; };
+
+__device__ __forceinline__ void load_chunk(const unsigned short* __restrict__ base, long ss, int r0, int rmax, Piece2& p) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = threadIdx.x + 256 * u;
     const int row = i >> 3, c = i & 7, r = r0 + row;
-    u16x8_t val;
-    if (r < rmax) val = *(const u16x8_t*)(base + (long)r * ss + c * 8);
+    if (r < rmax) p.v[u] = *(const u16x8_t*)(base + (long)r * ss + c * 8);
     else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) val[j] = 0;
-    }
-    if (rowimg) *(u16x8_t*)(rowimg + swz(row, c)) = val;
-    if (trimg) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) trimg[(c * 8 + j) * VT_PITCH + row] = val[j];
+      for (int j = 0; j < 8; ++j) p.v[u][j] = 0;
     }
   }
 }
+__device__ __forceinline__ void store_chunk(unsigned short* img, const Piece2& p) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = threadIdx.x + 256 * u;
+    *(u16x8_t*)(img + swz(i >> 3, i & 7)) = p.v[u];
+  }
+}
 
-__device__ __forceinline__ bf16x8_t lds_a(const unsigned short* img, int row, int chunk) {
+// row fragment: 8 bf16 of row `row`, 16-B chunk `chunk`
+__device__ __forceinline__ bf16x8_t frag_row(const unsigned short* img, int row, int chunk) {
   return *(const bf16x8_t*)(img + swz(row, chunk));
 }
-// B operand of the second product: 8 values of transposed row `drow` at keys
-// {32s+4g .. +3} and {32s+16+4g .. +3} (the permuted k order).
-__device__ __forceinline__ bf16x8_t lds_bt(const unsigned short* tr, int drow, int s, int g) {
-  const uint2 lo = *(const uint2*)(tr + drow * VT_PITCH + 32 * s + 4 * g);
-  const uint2 hi = *(const uint2*)(tr + drow * VT_PITCH + 32 * s + 16 + 4 * g);
-  bf16x8_t r;
-  r[0] = (short)(lo.x & 0xffff); r[1] = (short)(lo.x >> 16); r[2] = (short)(lo.y & 0xffff); r[3] = (short)(lo.y >> 16);
-  r[4] = (short)(hi.x & 0xffff); r[5] = (short)(hi.x >> 16); r[6] = (short)(hi.y & 0xffff); r[7] = (short)(hi.y >> 16);
-  return r;
-}
-__device__ __forceinline__ bf16x8_t pack_acc(const f32x4_t& a, const f32x4_t& b) {
-  bf16x8_t r;
+// transposed fragment: element jj = img[krow0 + (jj < 4 ? 4g + jj : 16 + 4g + jj - 4)][col0 + (lane & 15)]
+typedef __attribute__((ext_vector_type(4))) short s16x4_t;
+__device__ __forceinline__ bf16x8_t frag_tr(const unsigned short* img, int krow0, int col0, int lane) {
+  const int q = (lane & 15) >> 2, p = lane & 3, g = lane >> 4;
+  const int col = col0 + 4 * p;
+  bf16x8_t out;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) { r[j] = (short)f2bf(a[j]); r[4 + j] = (short)f2bf(b[j]); }
-  return r;
+  for (int h = 0; h < 2; ++h) {
+    const int row = krow0 + 16 * h + 4 * g + q;
+    const unsigned short* addr = img + row * 64 + (((col >> 3) ^ (row & 7)) << 3) + (col & 7);
+    const s16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)addr);
+    out[4 * h + 0] = v[0]; out[4 * h + 1] = v[1]; out[4 * h + 2] = v[2]; out[4 * h + 3] = v[3];
+  }
+  return out;
+}
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+__device__ __forceinline__ bf16x8_t pack_acc(const f32x4_t& a, const f32x4_t& b) {
+  const u32x4_t w = {pack2bf(a[0], a[1]), pack2bf(a[2], a[3]), pack2bf(b[0], b[1]), pack2bf(b[2], b[3])};
+  return __builtin_bit_cast(bf16x8_t, w);
 }
 __device__ __forceinline__ bf16x8_t load8(const unsigned short* p, bool ok) {
   bf16x8_t r;
@@ -76,103 +94,146 @@ __device__ __forceinline__ bf16x8_t load8(const unsigned short* p, bool ok) {
   }
   return r;
 }
+__device__ __forceinline__ void store4(unsigned short* p, const f32x4_t& v, float sc) {
+  uint2 pk;
+  pk.x = pack2bf(v[0] * sc, v[1] * sc);
+  pk.y = pack2bf(v[2] * sc, v[3] * sc);
+  *(uint2*)p = pk;
+}
 
 #define MFMA16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 
-// masked, biased, log2-scaled score; returns -inf for masked-out entries
-__device__ __forceinline__ float score_adj(float s, int qi, int kj, int Sk, int mode, const unsigned char* kp,
+// Masked, biased, log2-scaled score for key kj / query qi; -inf where masked.  Specialised on
+// the mask mode at compile time (the generic form was ~4x the VALU work of the softmax itself):
+// `full` (uniform) = the whole 64-key chunk is inside Sk; `kmask` = the chunk's padded keys.
+template <int MODE, bool KPAD>
+__device__ __forceinline__ float score_adj(float s, int qi, int kj, int kl, bool full, int Sk, unsigned long long kmask,
                                            float scale_log2) {
-  if (kj >= Sk) return -INFINITY;
-  if (mode == 2 && kj > qi) return -INFINITY;
-  if (kp && kp[kj]) return -INFINITY;
   float x = s * scale_log2;
-  if (mode == 1 && kj < qi) x += LOG2E_F;
+  if (MODE == 1) x += (kj < qi) ? LOG2E_F : 0.f;
+  if (MODE == 2) x = (kj > qi) ? -INFINITY : x;
+  if (KPAD) x = ((kmask >> kl) & 1ull) ? -INFINITY : x;
+  if (!full) x = (kj >= Sk) ? -INFINITY : x;
   return x;
 }
 
+__device__ __forceinline__ unsigned long long chunk_pad_mask(const unsigned char* kp, int k0, int Sk) {
+  const int k = k0 + (threadIdx.x & 63);
+  return __ballot(k < Sk && kp[k] != 0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Forward: workgroup = 4 waves x 32 queries (two 16-query sub-tiles per wave); K/V streamed in
+// 64-key chunks.  S^T = K Q^T (lane owns one query column), online softmax in registers,
+// O^T += V^T P^T (so O's rescale by the running max is lane-local too).
+template <int MODE, bool KPAD>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnFwdArgs a) {
-  __shared__ __attribute__((aligned(16))) unsigned short Ks[64 * 64];
-  __shared__ __attribute__((aligned(16))) unsigned short Vt[64 * VT_PITCH];
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  __shared__ __attribute__((aligned(16))) unsigned short Ks[2][IMG_ELEMS];
+  __shared__ __attribute__((aligned(16))) unsigned short Vs[2][IMG_ELEMS];
+  const int h = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int n = lane & 15, g = lane >> 4;
-  const int q0 = qb * 64 + w * 16;
-  const int qi = q0 + n;
+  const int qwave = blockIdx.x * 128 + w * 32;
   const unsigned short* Q = a.q + b * a.q_sb + h * a.q_sh;
   const unsigned short* K = a.k + b * a.k_sb + h * a.k_sh;
   const unsigned short* V = a.v + b * a.v_sb + h * a.v_sh;
   const unsigned char* kp = a.kpad ? a.kpad + (long)b * a.Sk : nullptr;
-  bf16x8_t qf[2];
-  qf[0] = load8(Q + (long)qi * a.q_ss + 8 * g, qi < a.Sq);
-  qf[1] = load8(Q + (long)qi * a.q_ss + 32 + 8 * g, qi < a.Sq);
-  float m = -INFINITY, l = 0.f;
-  f32x4_t o[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
   int kend = a.Sk;
-  if (a.mode == 2) kend = min(a.Sk, qb * 64 + 64);
-  for (int k0 = 0; k0 < kend; k0 += 64) {
-    __syncthreads();
-    stage_rows(K, a.k_ss, k0, a.Sk, Ks, nullptr);
-    stage_rows(V, a.v_ss, k0, a.Sk, nullptr, Vt);
-    __syncthreads();
-    f32x4_t s[4];
+  if (MODE == 2) kend = min(a.Sk, blockIdx.x * 128 + 128);
+  const int nchunks = (kend + 63) / 64;
+  Piece2 pk, pv;
+  load_chunk(K, a.k_ss, 0, a.Sk, pk);
+  load_chunk(V, a.v_ss, 0, a.Sk, pv);
+  bf16x8_t qf[2][2];
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    const int qi = qwave + qs * 16 + n;
+    qf[qs][0] = load8(Q + (long)qi * a.q_ss + 8 * g, qi < a.Sq);
+    qf[qs][1] = load8(Q + (long)qi * a.q_ss + 32 + 8 * g, qi < a.Sq);
+  }
+  store_chunk(Ks[0], pk);
+  store_chunk(Vs[0], pv);
+  __syncthreads();
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  f32x4_t o[2][4];
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[qs][dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1, k0 = c * 64;
+    const bool more = c + 1 < nchunks;
+    if (more) { load_chunk(K, a.k_ss, k0 + 64, a.Sk, pk); load_chunk(V, a.v_ss, k0 + 64, a.Sk, pv); }
+    const unsigned short* ks_ = Ks[buf];
+    const unsigned short* vs_ = Vs[buf];
+    const bool full = k0 + 64 <= a.Sk;
+    const unsigned long long kmask = KPAD ? chunk_pad_mask(kp, k0, a.Sk) : 0ull;
+    f32x4_t s[2][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      s[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      const bf16x8_t k0f = frag_row(ks_, t * 16 + n, g), k1f = frag_row(ks_, t * 16 + n, 4 + g);
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) s[t] = MFMA16(lds_a(Ks, t * 16 + n, 4 * ks + g), qf[ks], s[t]);
-    }
-    float cmax = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int kj = k0 + t * 16 + 4 * g + j;
-        s[t][j] = score_adj(s[t][j], qi, kj, a.Sk, a.mode, kp, a.scale_log2);
-        cmax = fmaxf(cmax, s[t][j]);
+      for (int qs = 0; qs < 2; ++qs) {
+        s[qs][t] = MFMA16(k0f, qf[qs][0], ((f32x4_t){0.f, 0.f, 0.f, 0.f}));
+        s[qs][t] = MFMA16(k1f, qf[qs][1], s[qs][t]);
       }
-    cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
-    cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
-    const float mnew = fmaxf(m, cmax);
-    const float mref = (mnew == -INFINITY) ? 0.f : mnew;
-    const float alpha = exp2f(m - mref);
-    float psum = 0.f;
+    }
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int qs = 0; qs < 2; ++qs) {
+      const int qi = qwave + qs * 16 + n;
+      float cmax = -INFINITY;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { s[t][j] = exp2f(s[t][j] - mref); psum += s[t][j]; }
-    psum += __shfl_xor(psum, 16, 64);
-    psum += __shfl_xor(psum, 32, 64);
-    l = l * alpha + psum;
-    m = mnew;
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float aj = __shfl(alpha, 4 * g + j, 64);
+        for (int j = 0; j < 4; ++j) {
+          const int kl = t * 16 + 4 * g + j;
+          s[qs][t][j] = score_adj<MODE, KPAD>(s[qs][t][j], qi, k0 + kl, kl, full, a.Sk, kmask, a.scale_log2);
+          cmax = fmaxf(cmax, s[qs][t][j]);
+        }
+      cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+      cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+      const float mnew = fmaxf(m[qs], cmax);
+      const float mref = (mnew == -INFINITY) ? 0.f : mnew;
+      const float alpha = exp2f(m[qs] - mref);
+      float psum = 0.f;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[dt][j] *= aj;
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { s[qs][t][j] = exp2f(s[qs][t][j] - mref); psum += s[qs][t][j]; }
+      psum += __shfl_xor(psum, 16, 64);
+      psum += __shfl_xor(psum, 32, 64);
+      l[qs] = l[qs] * alpha + psum;
+      m[qs] = mnew;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[qs][dt] *= alpha;
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8_t pa = pack_acc(s[2 * s2], s[2 * s2 + 1]);
+      const bf16x8_t pa0 = pack_acc(s[0][2 * s2], s[0][2 * s2 + 1]);
+      const bf16x8_t pa1 = pack_acc(s[1][2 * s2], s[1][2 * s2 + 1]);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[dt] = MFMA16(pa, lds_bt(Vt, dt * 16 + n, s2, g), o[dt]);
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8_t vf = frag_tr(vs_, 32 * s2, dt * 16, lane);
+        o[0][dt] = MFMA16(vf, pa0, o[0][dt]);
+        o[1][dt] = MFMA16(vf, pa1, o[1][dt]);
+      }
     }
+    if (more) { store_chunk(Ks[buf ^ 1], pk); store_chunk(Vs[buf ^ 1], pv); }
+    __syncthreads();
   }
   unsigned short* O = a.o + b * a.o_sb + h * a.o_sh;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float lj = __shfl(l, 4 * g + j, 64);
-    const float inv = lj > 0.f ? 1.0f / lj : 0.f;
-    const int qq = q0 + 4 * g + j;
-    if (qq < a.Sq) {
+  for (int qs = 0; qs < 2; ++qs) {
+    const int qi = qwave + qs * 16 + n;
+    if (qi < a.Sq) {
+      const float inv = l[qs] > 0.f ? 1.0f / l[qs] : 0.f;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) O[(long)qq * a.o_ss + dt * 16 + n] = f2bf(o[dt][j] * inv);
+      for (int dt = 0; dt < 4; ++dt) store4(O + (long)qi * a.o_ss + dt * 16 + 4 * g, o[qs][dt], inv);
+      if (g == 0) {
+        const float mref = (m[qs] == -INFINITY) ? 0.f : m[qs];
+        a.lse[((long)b * a.H + h) * a.Sq + qi] = l[qs] > 0.f ? mref + log2f(l[qs]) : INFINITY;
+      }
     }
-  }
-  if (g == 0 && qi < a.Sq) {
-    const float mref = (m == -INFINITY) ? 0.f : m;
-    a.lse[((long)b * a.H + h) * a.Sq + qi] = l > 0.f ? mref + log2f(l) : INFINITY;
   }
 }
 
@@ -199,173 +260,263 @@ __global__ void attn_delta_kernel(const unsigned short* __restrict__ o, const un
   if (h < H && (lane & 7) == 0) delta[((long)b * H + h) * Sq + q] = s;
 }
 
-// dQ: one workgroup per (q-block of 64, h, b); queries on lanes, keys streamed.
+// dQ: workgroup = 4 waves x 32 queries; K/V streamed.  S^T = K Q^T, dP^T = V dO^T,
+// dS^T = P^T o (dP^T - delta), dQ^T += K^T dS^T.
+template <int MODE, bool KPAD>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) unsigned short Ks[64 * 64];
-  __shared__ __attribute__((aligned(16))) unsigned short Vs[64 * 64];
-  __shared__ __attribute__((aligned(16))) unsigned short Kt[64 * VT_PITCH];
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  __shared__ __attribute__((aligned(16))) unsigned short Ks[2][IMG_ELEMS];
+  __shared__ __attribute__((aligned(16))) unsigned short Vs[2][IMG_ELEMS];
+  const int h = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int n = lane & 15, g = lane >> 4;
-  const int q0 = qb * 64 + w * 16;
-  const int qi = q0 + n;
+  const int qwave = blockIdx.x * 128 + w * 32;
   const unsigned short* Q = a.q + b * a.q_sb + h * a.q_sh;
   const unsigned short* K = a.k + b * a.k_sb + h * a.k_sh;
   const unsigned short* V = a.v + b * a.v_sb + h * a.v_sh;
   const unsigned short* dO = a.dout + b * a.o_sb + h * a.o_sh;
   const unsigned char* kp = a.kpad ? a.kpad + (long)b * a.Sk : nullptr;
-  const bool qok = qi < a.Sq;
-  bf16x8_t qf[2], df[2];
-  qf[0] = load8(Q + (long)qi * a.q_ss + 8 * g, qok);
-  qf[1] = load8(Q + (long)qi * a.q_ss + 32 + 8 * g, qok);
-  df[0] = load8(dO + (long)qi * a.o_ss + 8 * g, qok);
-  df[1] = load8(dO + (long)qi * a.o_ss + 32 + 8 * g, qok);
-  const long rowidx = ((long)b * a.H + h) * a.Sq + qi;
-  const float lse = qok ? a.lse[rowidx] : INFINITY;
-  const float dl = qok ? a.delta[rowidx] : 0.f;
-  f32x4_t acc[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) acc[dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
   int kend = a.Sk;
-  if (a.mode == 2) kend = min(a.Sk, qb * 64 + 64);
-  for (int k0 = 0; k0 < kend; k0 += 64) {
-    __syncthreads();
-    stage_rows(K, a.k_ss, k0, a.Sk, Ks, Kt);
-    stage_rows(V, a.v_ss, k0, a.Sk, Vs, nullptr);
-    __syncthreads();
-    f32x4_t s[4], dp[4];
+  if (MODE == 2) kend = min(a.Sk, blockIdx.x * 128 + 128);
+  const int nchunks = (kend + 63) / 64;
+  Piece2 pk, pv;
+  load_chunk(K, a.k_ss, 0, a.Sk, pk);
+  load_chunk(V, a.v_ss, 0, a.Sk, pv);
+  bf16x8_t qf[2][2], df[2][2];
+  float lse[2], dl[2];
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    const int qi = qwave + qs * 16 + n;
+    const bool ok = qi < a.Sq;
+    qf[qs][0] = load8(Q + (long)qi * a.q_ss + 8 * g, ok);
+    qf[qs][1] = load8(Q + (long)qi * a.q_ss + 32 + 8 * g, ok);
+    df[qs][0] = load8(dO + (long)qi * a.o_ss + 8 * g, ok);
+    df[qs][1] = load8(dO + (long)qi * a.o_ss + 32 + 8 * g, ok);
+    const long ri = ((long)b * a.H + h) * a.Sq + qi;
+    lse[qs] = ok ? a.lse[ri] : INFINITY;
+    dl[qs] = ok ? a.delta[ri] : 0.f;
+  }
+  store_chunk(Ks[0], pk);
+  store_chunk(Vs[0], pv);
+  __syncthreads();
+  f32x4_t acc[2][4];
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) acc[qs][dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1, k0 = c * 64;
+    const bool more = c + 1 < nchunks;
+    if (more) { load_chunk(K, a.k_ss, k0 + 64, a.Sk, pk); load_chunk(V, a.v_ss, k0 + 64, a.Sk, pv); }
+    const unsigned short* ks_ = Ks[buf];
+    const unsigned short* vs_ = Vs[buf];
+    const bool full = k0 + 64 <= a.Sk;
+    const unsigned long long kmask = KPAD ? chunk_pad_mask(kp, k0, a.Sk) : 0ull;
+    f32x4_t s[2][4], dp[2][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      s[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-      dp[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      const bf16x8_t k0f = frag_row(ks_, t * 16 + n, g), k1f = frag_row(ks_, t * 16 + n, 4 + g);
+      const bf16x8_t v0f = frag_row(vs_, t * 16 + n, g), v1f = frag_row(vs_, t * 16 + n, 4 + g);
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        s[t] = MFMA16(lds_a(Ks, t * 16 + n, 4 * ks + g), qf[ks], s[t]);
-        dp[t] = MFMA16(lds_a(Vs, t * 16 + n, 4 * ks + g), df[ks], dp[t]);
+      for (int qs = 0; qs < 2; ++qs) {
+        s[qs][t] = MFMA16(k0f, qf[qs][0], ((f32x4_t){0.f, 0.f, 0.f, 0.f}));
+        s[qs][t] = MFMA16(k1f, qf[qs][1], s[qs][t]);
+        dp[qs][t] = MFMA16(v0f, df[qs][0], ((f32x4_t){0.f, 0.f, 0.f, 0.f}));
+        dp[qs][t] = MFMA16(v1f, df[qs][1], dp[qs][t]);
       }
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int qs = 0; qs < 2; ++qs) {
+      const int qi = qwave + qs * 16 + n;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int kj = k0 + t * 16 + 4 * g + j;
-        const float x = score_adj(s[t][j], qi, kj, a.Sk, a.mode, kp, a.scale_log2);
-        const float p = (x == -INFINITY) ? 0.f : exp2f(x - lse);
-        s[t][j] = p * (dp[t][j] - dl);  // dS (w.r.t. the scaled score)
-      }
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int kl = t * 16 + 4 * g + j;
+          const float x = score_adj<MODE, KPAD>(s[qs][t][j], qi, k0 + kl, kl, full, a.Sk, kmask, a.scale_log2);
+          const float p = exp2f(x - lse[qs]);  // exp2(-inf) = 0 for masked entries
+          s[qs][t][j] = p * (dp[qs][t][j] - dl[qs]);
+        }
+    }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8_t pa = pack_acc(s[2 * s2], s[2 * s2 + 1]);
+      const bf16x8_t d0 = pack_acc(s[0][2 * s2], s[0][2 * s2 + 1]);
+      const bf16x8_t d1 = pack_acc(s[1][2 * s2], s[1][2 * s2 + 1]);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) acc[dt] = MFMA16(pa, lds_bt(Kt, dt * 16 + n, s2, g), acc[dt]);
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8_t kt = frag_tr(ks_, 32 * s2, dt * 16, lane);
+        acc[0][dt] = MFMA16(kt, d0, acc[0][dt]);
+        acc[1][dt] = MFMA16(kt, d1, acc[1][dt]);
+      }
     }
+    if (more) { store_chunk(Ks[buf ^ 1], pk); store_chunk(Vs[buf ^ 1], pv); }
+    __syncthreads();
   }
   unsigned short* dQ = a.dq + b * a.q_sb + h * a.q_sh;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int qq = q0 + 4 * g + j;
-    if (qq < a.Sq) {
+  for (int qs = 0; qs < 2; ++qs) {
+    const int qi = qwave + qs * 16 + n;
+    if (qi < a.Sq) {
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) dQ[(long)qq * a.q_ss + dt * 16 + n] = f2bf(acc[dt][j] * a.scale);
+      for (int dt = 0; dt < 4; ++dt) store4(dQ + (long)qi * a.q_ss + dt * 16 + 4 * g, acc[qs][dt], a.scale);
     }
   }
 }
 
-// dK, dV: one workgroup per (k-block of 64, h, b); keys on lanes, queries streamed.
+// dK, dV: workgroup = 4 waves x 32 keys; Q / dO streamed.  S = Q K^T and dP = dO V^T with the
+// key on the lane, P = exp2(S' - lse), dS = P o (dP - delta), dV^T += dO^T P, dK^T += Q^T dS.
+template <int MODE, bool KPAD>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) unsigned short Qs[64 * 64];
-  __shared__ __attribute__((aligned(16))) unsigned short Ds[64 * 64];
-  __shared__ __attribute__((aligned(16))) unsigned short Qt[64 * VT_PITCH];
-  __shared__ __attribute__((aligned(16))) unsigned short Dt[64 * VT_PITCH];
-  __shared__ float lse_s[64], dl_s[64];
-  const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  __shared__ __attribute__((aligned(16))) unsigned short Qs[2][IMG_ELEMS];
+  __shared__ __attribute__((aligned(16))) unsigned short Ds[2][IMG_ELEMS];
+  __shared__ float lse_s[2][64], dl_s[2][64];
+  const int h = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int n = lane & 15, g = lane >> 4;
-  const int kw0 = kb * 64 + w * 16;
-  const int kj = kw0 + n;
+  const int kwave = blockIdx.x * 128 + w * 32;
   const unsigned short* Q = a.q + b * a.q_sb + h * a.q_sh;
   const unsigned short* K = a.k + b * a.k_sb + h * a.k_sh;
   const unsigned short* V = a.v + b * a.v_sb + h * a.v_sh;
   const unsigned short* dO = a.dout + b * a.o_sb + h * a.o_sh;
-  const bool kok = kj < a.Sk && !(a.kpad && a.kpad[(long)b * a.Sk + kj]);
-  bf16x8_t kf[2], vf[2];
-  kf[0] = load8(K + (long)kj * a.k_ss + 8 * g, kj < a.Sk);
-  kf[1] = load8(K + (long)kj * a.k_ss + 32 + 8 * g, kj < a.Sk);
-  vf[0] = load8(V + (long)kj * a.v_ss + 8 * g, kj < a.Sk);
-  vf[1] = load8(V + (long)kj * a.v_ss + 32 + 8 * g, kj < a.Sk);
-  f32x4_t dk[4], dv[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) { dk[dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f}; dv[dt] = dk[dt]; }
   const long rowbase = ((long)b * a.H + h) * a.Sq;
   int qstart = 0;
-  if (a.mode == 2) qstart = (kb * 64) & ~63;
-  for (int q0 = qstart; q0 < a.Sq; q0 += 64) {
-    __syncthreads();
-    stage_rows(Q, a.q_ss, q0, a.Sq, Qs, Qt);
-    stage_rows(dO, a.o_ss, q0, a.Sq, Ds, Dt);
-    if (threadIdx.x < 64) {
-      const int qq = q0 + threadIdx.x;
-      lse_s[threadIdx.x] = qq < a.Sq ? a.lse[rowbase + qq] : INFINITY;
-      dl_s[threadIdx.x] = qq < a.Sq ? a.delta[rowbase + qq] : 0.f;
+  if (MODE == 2) qstart = (blockIdx.x * 128) & ~63;
+  const int nchunks = qstart < a.Sq ? (a.Sq - qstart + 63) / 64 : 0;
+  Piece2 pq, pd;
+  float lse_r = INFINITY, dl_r = 0.f;
+  if (nchunks) {
+    load_chunk(Q, a.q_ss, qstart, a.Sq, pq);
+    load_chunk(dO, a.o_ss, qstart, a.Sq, pd);
+    if (threadIdx.x < 64 && qstart + (int)threadIdx.x < a.Sq) {
+      lse_r = a.lse[rowbase + qstart + threadIdx.x];
+      dl_r = a.delta[rowbase + qstart + threadIdx.x];
     }
-    __syncthreads();
-    f32x4_t s[4], dp[4];
+  }
+  bf16x8_t kf[2][2], vf[2][2];
+  bool kok[2];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int kj = kwave + kt * 16 + n;
+    const bool ok = kj < a.Sk;
+    kok[kt] = ok && !(KPAD && a.kpad[(long)b * a.Sk + kj]);
+    kf[kt][0] = load8(K + (long)kj * a.k_ss + 8 * g, ok);
+    kf[kt][1] = load8(K + (long)kj * a.k_ss + 32 + 8 * g, ok);
+    vf[kt][0] = load8(V + (long)kj * a.v_ss + 8 * g, ok);
+    vf[kt][1] = load8(V + (long)kj * a.v_ss + 32 + 8 * g, ok);
+  }
+  f32x4_t dk[2][4], dv[2][4];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) { dk[kt][dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f}; dv[kt][dt] = dk[kt][dt]; }
+  if (nchunks) {
+    store_chunk(Qs[0], pq);
+    store_chunk(Ds[0], pd);
+    if (threadIdx.x < 64) { lse_s[0][threadIdx.x] = lse_r; dl_s[0][threadIdx.x] = dl_r; }
+  }
+  __syncthreads();
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1, q0 = qstart + c * 64;
+    const bool more = c + 1 < nchunks;
+    if (more) {
+      load_chunk(Q, a.q_ss, q0 + 64, a.Sq, pq);
+      load_chunk(dO, a.o_ss, q0 + 64, a.Sq, pd);
+      lse_r = INFINITY; dl_r = 0.f;
+      if (threadIdx.x < 64 && q0 + 64 + (int)threadIdx.x < a.Sq) {
+        lse_r = a.lse[rowbase + q0 + 64 + threadIdx.x];
+        dl_r = a.delta[rowbase + q0 + 64 + threadIdx.x];
+      }
+    }
+    const unsigned short* qs_ = Qs[buf];
+    const unsigned short* ds_ = Ds[buf];
+    f32x4_t s[2][4], dp[2][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      s[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-      dp[t] = s[t];
+      const bf16x8_t q0f = frag_row(qs_, t * 16 + n, g), q1f = frag_row(qs_, t * 16 + n, 4 + g);
+      const bf16x8_t d0f = frag_row(ds_, t * 16 + n, g), d1f = frag_row(ds_, t * 16 + n, 4 + g);
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        s[t] = MFMA16(lds_a(Qs, t * 16 + n, 4 * ks + g), kf[ks], s[t]);
-        dp[t] = MFMA16(lds_a(Ds, t * 16 + n, 4 * ks + g), vf[ks], dp[t]);
+      for (int kt = 0; kt < 2; ++kt) {
+        s[kt][t] = MFMA16(q0f, kf[kt][0], ((f32x4_t){0.f, 0.f, 0.f, 0.f}));
+        s[kt][t] = MFMA16(q1f, kf[kt][1], s[kt][t]);
+        dp[kt][t] = MFMA16(d0f, vf[kt][0], ((f32x4_t){0.f, 0.f, 0.f, 0.f}));
+        dp[kt][t] = MFMA16(d1f, vf[kt][1], dp[kt][t]);
       }
     }
-    // s[t][j] : query q0 + t*16 + 4g + j, key kj
+    // s[kt][t][j]: query q0 + t*16 + 4g + j, key kwave + kt*16 + n.  Rows past Sq carry
+    // lse = +inf (p = 0); a masked key lane has kok = false.
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int kt = 0; kt < 2; ++kt) {
+      const int kj = kwave + kt * 16 + n;
+      const float kbias = kok[kt] ? 0.f : -INFINITY;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int ql = t * 16 + 4 * g + j;
-        const int qq = q0 + ql;
-        float p = 0.f;
-        if (kok && qq < a.Sq && !(a.mode == 2 && kj > qq)) {
-          float x = s[t][j] * a.scale_log2;
-          if (a.mode == 1 && kj < qq) x += LOG2E_F;
-          p = exp2f(x - lse_s[ql]);
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int ql = t * 16 + 4 * g + j;
+          const int qq = q0 + ql;
+          float x = s[kt][t][j] * a.scale_log2 + kbias;
+          if (MODE == 1) x += (kj < qq) ? LOG2E_F : 0.f;
+          if (MODE == 2) x = (kj > qq) ? -INFINITY : x;
+          const float p = exp2f(x - lse_s[buf][ql]);
+          s[kt][t][j] = p;
+          dp[kt][t][j] = p * (dp[kt][t][j] - dl_s[buf][ql]);
         }
-        s[t][j] = p;
-        dp[t][j] = p * (dp[t][j] - dl_s[ql]);
-      }
+    }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8_t pa = pack_acc(s[2 * s2], s[2 * s2 + 1]);
-      const bf16x8_t da = pack_acc(dp[2 * s2], dp[2 * s2 + 1]);
+      const bf16x8_t p0 = pack_acc(s[0][2 * s2], s[0][2 * s2 + 1]);
+      const bf16x8_t p1 = pack_acc(s[1][2 * s2], s[1][2 * s2 + 1]);
+      const bf16x8_t e0 = pack_acc(dp[0][2 * s2], dp[0][2 * s2 + 1]);
+      const bf16x8_t e1 = pack_acc(dp[1][2 * s2], dp[1][2 * s2 + 1]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        dv[dt] = MFMA16(pa, lds_bt(Dt, dt * 16 + n, s2, g), dv[dt]);
-        dk[dt] = MFMA16(da, lds_bt(Qt, dt * 16 + n, s2, g), dk[dt]);
+        const bf16x8_t dot = frag_tr(ds_, 32 * s2, dt * 16, lane);
+        const bf16x8_t qt = frag_tr(qs_, 32 * s2, dt * 16, lane);
+        dv[0][dt] = MFMA16(dot, p0, dv[0][dt]);
+        dv[1][dt] = MFMA16(dot, p1, dv[1][dt]);
+        dk[0][dt] = MFMA16(qt, e0, dk[0][dt]);
+        dk[1][dt] = MFMA16(qt, e1, dk[1][dt]);
       }
     }
+    if (more) {
+      store_chunk(Qs[buf ^ 1], pq);
+      store_chunk(Ds[buf ^ 1], pd);
+      if (threadIdx.x < 64) { lse_s[buf ^ 1][threadIdx.x] = lse_r; dl_s[buf ^ 1][threadIdx.x] = dl_r; }
+    }
+    __syncthreads();
   }
   unsigned short* dK = a.dk + b * a.k_sb + h * a.k_sh;
   unsigned short* dV = a.dv + b * a.v_sb + h * a.v_sh;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int kk = kw0 + 4 * g + j;
-    if (kk < a.Sk) {
+  for (int kt = 0; kt < 2; ++kt) {
+    const int kj = kwave + kt * 16 + n;
+    if (kj < a.Sk) {
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        dK[(long)kk * a.k_ss + dt * 16 + n] = f2bf(dk[dt][j] * a.scale);
-        dV[(long)kk * a.v_ss + dt * 16 + n] = f2bf(dv[dt][j]);
+        store4(dK + (long)kj * a.k_ss + dt * 16 + 4 * g, dk[kt][dt], a.scale);
+        store4(dV + (long)kj * a.v_ss + dt * 16 + 4 * g, dv[kt][dt], 1.0f);
       }
     }
   }
 }
 
+#define SMI_ATTN_DISPATCH(KERNEL, GRID, ARGS)                                                               \
+  do {                                                                                                     \
+    const bool kp_ = (ARGS).kpad != nullptr;                                                               \
+    switch ((ARGS).mode) {                                                                                 \
+      case 0: if (kp_) hipLaunchKernelGGL((KERNEL<0, true>), GRID, dim3(256), 0, st, ARGS);                \
+              else hipLaunchKernelGGL((KERNEL<0, false>), GRID, dim3(256), 0, st, ARGS); break;            \
+      case 1: if (kp_) hipLaunchKernelGGL((KERNEL<1, true>), GRID, dim3(256), 0, st, ARGS);                \
+              else hipLaunchKernelGGL((KERNEL<1, false>), GRID, dim3(256), 0, st, ARGS); break;            \
+      case 2: if (kp_) hipLaunchKernelGGL((KERNEL<2, true>), GRID, dim3(256), 0, st, ARGS);                \
+              else hipLaunchKernelGGL((KERNEL<2, false>), GRID, dim3(256), 0, st, ARGS); break;            \
+      default: return -1;                                                                                  \
+    }                                                                                                      \
+  } while (0)
+
 extern "C" int smi_attn_fwd(const AttnFwdArgs* args, hipStream_t st) {
   const AttnFwdArgs& a = *args;
-  dim3 grid((a.Sq + 63) / 64, a.H, a.B);
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, st, a);
+  dim3 grid((a.Sq + 127) / 128, a.H, a.B);
+  SMI_ATTN_DISPATCH(attn_fwd_kernel, grid, a);
   SMI_CHECK_LAUNCH();
 }
 
@@ -376,7 +527,7 @@ extern "C" int smi_attn_bwd(const AttnBwdArgs* args, const void* o, float* delta
                      (const unsigned short*)o, a.dout, a.o_sb, a.o_ss, a.o_sh, delta, a.B, a.H, a.Sq);
   AttnBwdArgs b2 = a;
   b2.delta = delta;
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((a.Sq + 63) / 64, a.H, a.B), dim3(256), 0, st, b2);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((a.Sk + 63) / 64, a.H, a.B), dim3(256), 0, st, b2);
+  SMI_ATTN_DISPATCH(attn_bwd_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), b2);
+  SMI_ATTN_DISPATCH(attn_bwd_dkdv_kernel, dim3((a.Sk + 127) / 128, a.H, a.B), b2);
   SMI_CHECK_LAUNCH();
 }

@@ -17,13 +17,16 @@ def test_cnn_recipe_gpu_resume_exact(tmp_path):
     from sparkmi.recipes import cnn
     base = GPU + ["--n-train", "640", "--n-test", "64", "--epochs", "2"]
     full = cnn.main(base + ["--ckpt-dir", str(tmp_path / "a"), "--no-resume"])
+    full2 = cnn.main(base + ["--ckpt-dir", str(tmp_path / "a2"), "--no-resume"])
     cnn.main(base + ["--ckpt-dir", str(tmp_path / "b"), "--max-steps", "25", "--ckpt-every", "25"])
     rest = cnn.main(base + ["--ckpt-dir", str(tmp_path / "b")])
     assert rest["steps"] == 40 - 25
-    # the fused CNN kernel's weight-gradient reduction uses LDS float atomics (order is not
-    # deterministic), so a resumed run matches to float rounding, not bit-for-bit as on CPU
+    # the fused CNN kernel's weight-gradient reduction uses LDS float atomics (summation order is
+    # not deterministic), so even two uninterrupted runs differ in the last bits and the
+    # difference grows over training; a resumed run must be as close as that run-to-run noise
     for k, v in full["state_dict"].items():
-        torch.testing.assert_close(rest["state_dict"][k], v, rtol=1e-3, atol=5e-4)
+        noise = (full2["state_dict"][k] - v).abs().max().item()
+        torch.testing.assert_close(rest["state_dict"][k], v, rtol=0, atol=max(5e-4, 4 * noise))
 
 
 @pytest.mark.gpu
