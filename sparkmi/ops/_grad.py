@@ -6,9 +6,64 @@ flat gradient buffer when the model was flattened by :class:`sparkmi.utils.flat.
 then call :func:`grad_ready` so the data-parallel engine can launch the all-reduce of a
 gradient bucket as soon as its last parameter is final (overlap with the rest of backward).
 """
+import contextlib
+import os
+
 import torch
 
 _listeners = []
+
+# ---- weight-gradient side stream ---------------------------------------------------------
+# A linear layer's weight gradient (dW = dY^T X, plus the bias column sum) is off the critical
+# path of backward: only dX feeds the next op.  The fused ops enqueue those GEMMs on a second
+# HIP stream so they run concurrently with the dgrad / attention / norm kernels of the layers
+# below (each of those GEMMs alone leaves most of the chip waiting on memory at these sizes).
+# Inside a HIP-graph capture the fork/join becomes parallel graph branches.  The main stream
+# joins the side stream before anything reads the gradients: at the end of every backward pass
+# (autograd final callback), before a data-parallel bucket all-reduce, and before the optimizer.
+_SIDE_ENABLED = os.environ.get("SPARKMI_WGRAD_STREAM", "1") != "0"
+_side_streams = {}
+_pending = set()
+
+
+def _side_stream(device):
+    s = _side_streams.get(device)
+    if s is None:
+        s = torch.cuda.Stream(device=device)
+        _side_streams[device] = s
+    return s
+
+
+def join(device=None):
+    """Make the current stream of ``device`` (all devices if None) wait for the side stream."""
+    devs = list(_pending) if device is None else [device]
+    for d in devs:
+        if d in _pending:
+            torch.cuda.current_stream(d).wait_stream(_side_streams[d])
+            _pending.discard(d)
+
+
+@contextlib.contextmanager
+def side(device, *tensors):
+    """Run the enclosed launches on the weight-gradient side stream of ``device``."""
+    if not _SIDE_ENABLED or device.type != "cuda":
+        yield
+        return
+    dev = device.index if device.index is not None else torch.cuda.current_device()
+    main = torch.cuda.current_stream(dev)
+    s = _side_stream(dev)
+    s.wait_stream(main)
+    for t in tensors:
+        if t is not None:
+            t.record_stream(s)
+    if dev not in _pending:
+        _pending.add(dev)
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(lambda: join(dev))
+        except RuntimeError:
+            pass  # not inside a backward pass: callers join explicitly
+    with torch.cuda.stream(s):
+        yield
 
 
 def add_listener(fn):

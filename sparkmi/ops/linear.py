@@ -22,6 +22,7 @@ import torch
 from .. import _native
 from . import gemm as G
 from . import rng as _rng
+from . import _grad
 from ._grad import bf16_weight, grad_buf, grad_ready
 
 ACTS = {None: 0, "none": 0, "relu": 1, "sigmoid": 2}
@@ -162,9 +163,11 @@ class LinearFn(torch.autograd.Function):
             else:
                 g2 = dy2
             dx = _dgrad(g2, bf16_weight(weight)) if ctx.needs_input_grad[0] else None
-            _wgrad_accumulate(gw, g2, x2)
-            if bias is not None:
-                _colsum(g2, grad_buf(bias))
+            bgrad = grad_buf(bias) if bias is not None else None
+            with _grad.side(g2.device, g2, x2):
+                _wgrad_accumulate(gw, g2, x2)
+                if bias is not None:
+                    _colsum(g2, bgrad)
         else:
             g2 = _ref_act_bwd(dy2.float(), y2, act, p, ctx.seed, ctx.salt)
             dx = (g2 @ weight.float()).to(dy.dtype) if ctx.needs_input_grad[0] else None
@@ -220,12 +223,15 @@ class FFNFn(torch.autograd.Function):
             dy2 = dy2.contiguous()
             # dh_pre = (dy @ W2) * relu'/dropout mask (from the saved output h), fused epilogue
             dh = _dgrad(dy2, bf16_weight(w2), dact_y=h, dscale=_rng.scale(p))
-            _wgrad_accumulate(grad_buf(w2), dy2, h)
-            _colsum(dy2, grad_buf(b2))
+            gw2, gb2, gw1, gb1 = grad_buf(w2), grad_buf(b2), grad_buf(w1), grad_buf(b1)
+            with _grad.side(dy2.device, dy2, h):
+                _wgrad_accumulate(gw2, dy2, h)
+                _colsum(dy2, gb2)
             grad_ready(w2, b2)
             dx = _dgrad(dh, bf16_weight(w1)) if ctx.needs_input_grad[0] else None
-            _wgrad_accumulate(grad_buf(w1), dh, x2)
-            _colsum(dh, grad_buf(b1))
+            with _grad.side(dh.device, dh, x2):
+                _wgrad_accumulate(gw1, dh, x2)
+                _colsum(dh, gb1)
             grad_ready(w1, b1)
         else:
             g = dy2.float()

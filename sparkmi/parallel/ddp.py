@@ -69,6 +69,8 @@ class DataParallel:
             return
         s, e, _ = self.buckets[b]
         self._launched[b] = True
+        if self.flat.grad.is_cuda:
+            _grad.join(self.flat.grad.device.index)  # weight grads may still be in flight on the side stream
         w = dist.all_reduce(self.flat.grad[s:e], group=self.group, async_op=True)
         self._works.append(w)
 

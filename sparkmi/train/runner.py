@@ -9,6 +9,8 @@ copied into static device buffers before each replay.
 """
 import torch
 
+from ..ops import _grad
+
 
 class StepRunner:
     def __init__(self, model, loss_fn, optimizer, ddp=None, graph=False, warmup_eager=3):
@@ -31,19 +33,19 @@ class StepRunner:
             rng.advance()
         loss = self.loss_fn(self.model, *batch)
         loss.backward()
+        _grad.join()
         if self.ddp is not None:
             self.ddp.finish()
         self.opt.step()
         return loss.detach()
 
     def _capture(self, batch):
+        """Record one step into a HIP graph.  Capture only records (nothing executes), so no
+        extra optimizer updates happen here: the ``warmup_eager`` eager steps before it already
+        did every lazy initialisation (allocator pools, GEMM autotuning, library handles), and
+        the caller replays the graph for the current step right after."""
         self.static_in = [b.clone() for b in batch]
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(2):
-                self._eager(*self.static_in)
-        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self.static_loss = self._eager(*self.static_in)
@@ -55,7 +57,7 @@ class StepRunner:
         if not use_graph or self.steps <= self.warmup_eager:
             return self._eager(*batch)
         if self.graph is None:
-            self._capture(batch)
+            self._capture(batch)  # then replayed below for this step
         for dst, src in zip(self.static_in, batch):
             dst.copy_(src, non_blocking=True)
         self.graph.replay()
