@@ -5,7 +5,8 @@
 // PE table transformer.py:33-42, precomputed once here instead of per forward) and
 // the LSTM's plain nn.Embedding with padding_idx (distributed_lstm.py:115,128).
 // Forward: one thread per 8 contiguous features (16-B loads of the bf16 table copy), bf16 out.
-// Backward: fp32 atomic adds into the dense fp32 gradient table, rows == padding_idx skipped
+// Backward: fp32 atomic adds (runs of equal ids merged first) into the dense fp32 gradient
+// table, rows == padding_idx skipped
 // (that row's gradient stays zero like torch's padding_idx).  Dense semantics are kept on
 // purpose: the reference's Adam decays every row.
 #include "smi_common.h"
@@ -32,21 +33,59 @@ __global__ void emb_fwd_kernel(const long long* __restrict__ ids, const unsigned
   *(u16x8_t*)(out + t * D + c) = o;
 }
 
-// one wave per token, lane = column (64 consecutive floats per atomic wave-instruction: the
-// 256-B contiguous shape the memory-side float atomics run at full rate)
-__global__ void emb_bwd_kernel(const long long* __restrict__ ids, const unsigned short* __restrict__ dout,
-                               float* __restrict__ dtable, long T, int D, long long padding_idx,
-                               const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale) {
-  const uint32_t seed = smi_seed(seedp, salt);
+// One wave per run of EMB_RUN consecutive tokens, lane = column (a wave-instruction covers 64
+// consecutive columns: 128-B coalesced loads, and 256-B contiguous float atomics — the shape the
+// memory-side atomics run at full rate).  The wave loads all its rows first, then walks them in
+// order and merges consecutive tokens with the same id in registers, so a run of equal ids (the
+// padding tail of every sequence: ~25 % of the reference's tokens share one id) costs one atomic
+// row per wave instead of one per token (same-address float atomics serialise at the L2).
+#define EMB_RUN 8
+__global__ __launch_bounds__(256) void emb_bwd_kernel(const long long* __restrict__ ids,
+                                                      const unsigned short* __restrict__ dout,
+                                                      float* __restrict__ dtable, long T, int D, long long padding_idx,
+                                                      const uint32_t* seedp, uint32_t salt, uint32_t thresh,
+                                                      float dscale) {
+  const uint32_t seed = thresh ? smi_seed(seedp, salt) : 0u;
   const int lane = threadIdx.x & 63;
-  for (long t = (long)blockIdx.x * 4 + (threadIdx.x >> 6); t < T; t += (long)gridDim.x * 4) {
-    const long long id = ids[t];
-    if (id == padding_idx) continue;
-    float* dst = dtable + id * D;
-    for (int c = lane; c < D; c += 64) {
-      float g = bf2f(dout[t * D + c]);
-      if (thresh) g = smi_keep(seed, (uint32_t)(t * D + c), thresh) ? g * dscale : 0.f;
-      atomicAdd(dst + c, g);
+  const long t0 = ((long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * EMB_RUN;
+  if (t0 >= T) return;
+  const int nt = (int)min((long)EMB_RUN, T - t0);
+  long long id[EMB_RUN];
+#pragma unroll
+  for (int i = 0; i < EMB_RUN; ++i) id[i] = i < nt ? ids[t0 + i] : padding_idx;
+  for (int c0 = 0; c0 < D; c0 += 512) {
+    unsigned short v[EMB_RUN][8];
+#pragma unroll
+    for (int i = 0; i < EMB_RUN; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j * 64 + lane;
+        v[i][j] = (i < nt && c < D) ? dout[(t0 + i) * D + c] : (unsigned short)0;
+      }
+    float acc[8];
+    long long cur = -1;
+#pragma unroll
+    for (int i = 0; i <= EMB_RUN; ++i) {
+      const long long nid = (i < nt) ? id[i] : -2;
+      if (nid != cur) {
+        if (cur >= 0 && cur != padding_idx) {
+          float* dst = dtable + cur * D + c0 + lane;
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (c0 + j * 64 + lane < D) atomicAdd(dst + j * 64, acc[j]);
+        }
+        cur = nid;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+      }
+      if (i < nt) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float g = bf2f(v[i][j]);
+          if (thresh) g = smi_keep(seed, (uint32_t)((t0 + i) * D + c0 + j * 64 + lane), thresh) ? g * dscale : 0.f;
+          acc[j] += g;
+        }
+      }
     }
   }
 }
@@ -62,9 +101,8 @@ extern "C" int smi_emb_fwd(const long long* ids, const void* table, const float*
 
 extern "C" int smi_emb_bwd(const long long* ids, const void* dout, float* dtable, long T, int D, long long padding_idx,
                            const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, hipStream_t st) {
-  long nb = (T + 3) / 4;
-  if (nb > 4096) nb = 4096;
-  hipLaunchKernelGGL(emb_bwd_kernel, dim3((unsigned)nb), dim3(256), 0, st, ids,
+  const long waves = (T + EMB_RUN - 1) / EMB_RUN;
+  hipLaunchKernelGGL(emb_bwd_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, ids,
                      (const unsigned short*)dout, dtable, T, D, padding_idx, seedp, salt, thresh, dscale);
   SMI_CHECK_LAUNCH();
 }

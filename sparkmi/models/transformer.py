@@ -24,6 +24,7 @@ from torch import nn
 
 from ..ops import (DropoutRNG, add_dropout_layernorm, cross_attention, embedding, linear, self_attention,
                    sinusoid_table)
+from ..ops._grad import ResidualGrad
 from ..ops.linear import ffn
 from ..ops.loss import cross_entropy
 from ..ops.rng import new_salt
@@ -93,8 +94,8 @@ class MultiHeadAttention(nn.Module):
         self.qkv_layer = nn.Linear(d_model, 3 * d_model)
         self.linear_layer = nn.Linear(d_model, d_model)
 
-    def forward(self, x, mode="none", key_padding=None):
-        qkv = linear(x, self.qkv_layer.weight, self.qkv_layer.bias)
+    def forward(self, x, mode="none", key_padding=None, x_slot=None):
+        qkv = linear(x, self.qkv_layer.weight, self.qkv_layer.bias, x_slot=x_slot)
         values = self_attention(qkv, self.num_heads, mode, key_padding)
         return linear(values, self.linear_layer.weight, self.linear_layer.bias)
 
@@ -109,9 +110,9 @@ class MultiHeadCrossAttention(nn.Module):
         self.q_layer = nn.Linear(d_model, d_model)
         self.linear_layer = nn.Linear(d_model, d_model)
 
-    def forward(self, x, y, mode="none", key_padding=None):
+    def forward(self, x, y, mode="none", key_padding=None, y_slot=None):
         kv = linear(x, self.kv_layer.weight, self.kv_layer.bias)
-        q = linear(y, self.q_layer.weight, self.q_layer.bias)
+        q = linear(y, self.q_layer.weight, self.q_layer.bias, x_slot=y_slot)
         values = cross_attention(q, kv, self.num_heads, mode, key_padding)
         return linear(values, self.linear_layer.weight, self.linear_layer.bias)
 
@@ -126,8 +127,8 @@ class LayerNormalization(nn.Module):
         self.gamma = nn.Parameter(torch.ones(parameters_shape))
         self.beta = nn.Parameter(torch.zeros(parameters_shape))
 
-    def forward(self, inputs, residual=None, p=0.0, rng=None, salt=0):
-        return add_dropout_layernorm(inputs, residual, self.gamma, self.beta, p, rng, salt, self.eps)
+    def forward(self, inputs, residual=None, p=0.0, rng=None, salt=0, r_slot=None):
+        return add_dropout_layernorm(inputs, residual, self.gamma, self.beta, p, rng, salt, self.eps, r_slot)
 
 
 class PositionwiseFeedForward(nn.Module):
@@ -140,9 +141,9 @@ class PositionwiseFeedForward(nn.Module):
         _share(self, "_rng", rng)
         self.salt = new_salt()
 
-    def forward(self, x):
+    def forward(self, x, x_slot=None):
         p = self.dropout.p if self.training else 0.0
-        return ffn(x, self.linear1, self.linear2, p, self._rng, self.salt)
+        return ffn(x, self.linear1, self.linear2, p, self._rng, self.salt, x_slot)
 
 
 class EncoderLayer(nn.Module):
@@ -160,10 +161,12 @@ class EncoderLayer(nn.Module):
     def forward(self, x, mode="none", key_padding=None):
         p1 = self.dropout1.p if self.training else 0.0
         p2 = self.dropout2.p if self.training else 0.0
-        a = self.attention(x, mode, key_padding)
-        x = self.norm1(a, x, p1, self._rng, self.salts[0])
-        f = self.ffn(x)
-        return self.norm2(f, x, p2, self._rng, self.salts[1])
+        # residual gradients ride the dgrad epilogue of the block's first linear (ResidualGrad)
+        s1, s2 = ResidualGrad(), ResidualGrad()
+        a = self.attention(x, mode, key_padding, x_slot=s1)
+        x = self.norm1(a, x, p1, self._rng, self.salts[0], r_slot=s1)
+        f = self.ffn(x, x_slot=s2)
+        return self.norm2(f, x, p2, self._rng, self.salts[1], r_slot=s2)
 
 
 class SequentialEncoder(nn.Sequential):
@@ -204,12 +207,13 @@ class DecoderLayer(nn.Module):
 
     def forward(self, x, y, self_mode="none", cross_mode="none", key_padding=None):
         ps = [d.p if self.training else 0.0 for d in (self.dropout1, self.dropout2, self.dropout3)]
-        a = self.self_attention(y, self_mode)
-        y = self.layer_norm1(a, y, ps[0], self._rng, self.salts[0])
-        c = self.encoder_decoder_attention(x, y, cross_mode, key_padding)
-        y = self.layer_norm2(c, y, ps[1], self._rng, self.salts[1])
-        f = self.ffn(y)
-        return self.layer_norm3(f, y, ps[2], self._rng, self.salts[2])
+        s1, s2, s3 = ResidualGrad(), ResidualGrad(), ResidualGrad()
+        a = self.self_attention(y, self_mode, x_slot=s1)
+        y = self.layer_norm1(a, y, ps[0], self._rng, self.salts[0], r_slot=s1)
+        c = self.encoder_decoder_attention(x, y, cross_mode, key_padding, y_slot=s2)
+        y = self.layer_norm2(c, y, ps[1], self._rng, self.salts[1], r_slot=s2)
+        f = self.ffn(y, x_slot=s3)
+        return self.layer_norm3(f, y, ps[2], self._rng, self.salts[2], r_slot=s3)
 
 
 class SequentialDecoder(nn.Sequential):

@@ -106,3 +106,23 @@ def bf16_weight(p: torch.Tensor) -> torch.Tensor:
 
 def needs_input_grad(ctx, i):
     return ctx.needs_input_grad[i]
+
+
+class ResidualGrad:
+    """Routes a residual branch's gradient into the dgrad GEMM of the sibling consumer.
+
+    In a post-LN block ``y = LN(dropout(F(x)) + x)`` the block input ``x`` feeds both the first
+    linear of F and the residual.  Autograd would add the two gradients with a separate
+    elementwise pass; instead the LayerNorm backward (which always runs first) parks the
+    residual gradient here and the linear's backward adds it in its dgrad epilogue (the
+    ``resid`` term of the GEMM), so dX leaves the GEMM complete.
+    """
+
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
+
+    def take(self):
+        g, self.grad = self.grad, None
+        return g

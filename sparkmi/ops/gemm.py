@@ -89,10 +89,16 @@ def dgrad(dy, w, resid=None, dact_y=None, dscale=1.0, out=None):
     return dx
 
 
+# split-K target (workgroups) for the weight-gradient GEMM: it runs on the side stream next to
+# the backward's critical path, so it need not fill the chip alone; fewer splits = fewer fp32
+# atomic partial sums (each split adds one full N x K slab).
+_WGRAD_TARGET = int(os.environ.get("SPARKMI_WGRAD_TARGET", "128"))
+
+
 def wgrad_splits(N, K, M):
     tiles = ((N + 127) // 128) * ((K + 127) // 128)
     s = 1
-    while tiles * s < NUM_CU and (M // (s * 2)) >= 256:
+    while tiles * s < _WGRAD_TARGET and (M // (s * 2)) >= 256:
         s *= 2
     return s
 

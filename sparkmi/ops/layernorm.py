@@ -29,11 +29,12 @@ def _ref_forward(h, r, gamma, beta, p, seed, salt, eps):
 
 class AddDropoutLayerNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, r, gamma, beta, p, rng, salt, eps):
+    def forward(ctx, h, r, gamma, beta, p, rng, salt, eps, r_slot=None):
         D = h.shape[-1]
         M = h.numel() // D
         ctx.p, ctx.rng, ctx.salt, ctx.D, ctx.M = p, rng, salt, D, M
         ctx.has_r = r is not None
+        ctx.r_slot = r_slot
         if _native.use_native(h):
             C = _native.C()
             h = h.contiguous()
@@ -87,14 +88,19 @@ class AddDropoutLayerNorm(torch.autograd.Function):
                 dhh = dhh * _rng.keep_mask((M, D), p, ctx.seed, ctx.salt, dx.device).to(dx.dtype) * _rng.scale(p)
             dh = dhh.reshape(dy.shape).to(dy.dtype)
         grad_ready(gamma, beta)
-        return dh, dres, None, None, None, None, None, None
+        if ctx.r_slot is not None and dres is not None:
+            ctx.r_slot.grad = dres  # added by the sibling linear's dgrad epilogue instead
+            dres = None
+        return dh, dres, None, None, None, None, None, None, None
 
 
-def add_dropout_layernorm(h, residual, gamma, beta, p=0.0, rng=None, salt=0, eps=1e-5):
+def add_dropout_layernorm(h, residual, gamma, beta, p=0.0, rng=None, salt=0, eps=1e-5, r_slot=None):
+    """LayerNorm(dropout_p(h) + residual); with ``r_slot`` the residual's gradient is handed to
+    the linear that consumes the same tensor (see ResidualGrad) instead of returned."""
     if rng is None:
         p = 0.0
         rng = _NULL_RNG
-    return AddDropoutLayerNorm.apply(h, residual, gamma, beta, float(p), rng, int(salt), float(eps))
+    return AddDropoutLayerNorm.apply(h, residual, gamma, beta, float(p), rng, int(salt), float(eps), r_slot)
 
 
 class _NullRNG:

@@ -129,7 +129,7 @@ def _ref_act_bwd(g2, y2, act, p, seed, salt):
 
 class LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, act, p, rng, salt):
+    def forward(ctx, x, weight, bias, act, p, rng, salt, x_slot=None):
         shp = x.shape
         K = shp[-1]
         N = weight.shape[0]
@@ -143,6 +143,7 @@ class LinearFn(torch.autograd.Function):
         else:
             ctx.seed = rng.current() if p > 0 else 0
             y2 = _ref_fwd(x2, weight, bias, act, p, ctx.seed, salt).to(x.dtype)
+        ctx.x_slot = x_slot
         ctx.save_for_backward(x2, weight, bias, y2 if act else None)
         return y2.reshape(*shp[:-1], N)
 
@@ -162,7 +163,8 @@ class LinearFn(torch.autograd.Function):
                                ctx.salt, _rng.threshold(p), _rng.scale(p), _native.stream())
             else:
                 g2 = dy2
-            dx = _dgrad(g2, bf16_weight(weight)) if ctx.needs_input_grad[0] else None
+            resid = _slot_grad(ctx.x_slot, g2.shape[0])
+            dx = _dgrad(g2, bf16_weight(weight), resid=resid) if ctx.needs_input_grad[0] else None
             bgrad = grad_buf(bias) if bias is not None else None
             with _grad.side(g2.device, g2, x2):
                 _wgrad_accumulate(gw, g2, x2)
@@ -170,32 +172,47 @@ class LinearFn(torch.autograd.Function):
                     _colsum(g2, bgrad)
         else:
             g2 = _ref_act_bwd(dy2.float(), y2, act, p, ctx.seed, ctx.salt)
-            dx = (g2 @ weight.float()).to(dy.dtype) if ctx.needs_input_grad[0] else None
+            resid = _slot_grad(ctx.x_slot, g2.shape[0])
+            dx = None
+            if ctx.needs_input_grad[0]:
+                dx = g2 @ weight.float()
+                if resid is not None:
+                    dx = dx + resid.float()
+                dx = dx.to(dy.dtype)
             gw.add_(g2.t() @ x2.float())
             if bias is not None:
                 grad_buf(bias).add_(g2.sum(0))
         grad_ready(weight, bias)
         if dx is not None:
             dx = dx.reshape(*dy.shape[:-1], K)
-        return dx, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None
 
 
-def linear(x, weight, bias=None, act=None, p=0.0, rng=None, salt=0):
-    """y = dropout_p(act(x @ weight^T + bias)); act in {None, 'relu', 'sigmoid'}."""
+def _slot_grad(slot, rows):
+    """The residual gradient parked for this op's input (see _grad.ResidualGrad), 2-D, or None."""
+    if slot is None:
+        return None
+    g = slot.take()
+    return g.reshape(rows, -1).contiguous() if g is not None else None
+
+
+def linear(x, weight, bias=None, act=None, p=0.0, rng=None, salt=0, x_slot=None):
+    """y = dropout_p(act(x @ weight^T + bias)); act in {None, 'relu', 'sigmoid'}.  ``x_slot``:
+    a ResidualGrad whose parked gradient is added to dX in the dgrad epilogue."""
     a = ACTS[act] if not isinstance(act, int) else act
     if a == 2 and p > 0:
         raise ValueError("sigmoid + dropout epilogue is not supported")
     if rng is None:
         from .layernorm import _NULL_RNG
         rng, p = _NULL_RNG, 0.0
-    return LinearFn.apply(x, weight, bias, a, float(p), rng, int(salt))
+    return LinearFn.apply(x, weight, bias, a, float(p), rng, int(salt), x_slot)
 
 
 class FFNFn(torch.autograd.Function):
     """y = linear2(dropout(relu(linear1(x)))) with a single saved hidden activation."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, p, rng, salt):
+    def forward(ctx, x, w1, b1, w2, b2, p, rng, salt, x_slot=None):
         shp = x.shape
         D = shp[-1]
         x2 = x.reshape(-1, D)
@@ -210,6 +227,7 @@ class FFNFn(torch.autograd.Function):
             ctx.seed = rng.current() if p > 0 else 0
             h = _ref_fwd(x2, w1, b1, 1, p, ctx.seed, salt).to(x.dtype)
             y = _ref_fwd(h, w2, b2, 0, 0.0, 0, 0).to(x.dtype)
+        ctx.x_slot = x_slot
         ctx.save_for_backward(x2, h, w1, b1, w2, b2)
         return y.reshape(shp)
 
@@ -228,7 +246,8 @@ class FFNFn(torch.autograd.Function):
                 _wgrad_accumulate(gw2, dy2, h)
                 _colsum(dy2, gb2)
             grad_ready(w2, b2)
-            dx = _dgrad(dh, bf16_weight(w1)) if ctx.needs_input_grad[0] else None
+            resid = _slot_grad(ctx.x_slot, dh.shape[0])
+            dx = _dgrad(dh, bf16_weight(w1), resid=resid) if ctx.needs_input_grad[0] else None
             with _grad.side(dh.device, dh, x2):
                 _wgrad_accumulate(gw1, dh, x2)
                 _colsum(dh, gb1)
@@ -239,17 +258,24 @@ class FFNFn(torch.autograd.Function):
             grad_buf(b2).add_(g.sum(0))
             grad_ready(w2, b2)
             dh = _ref_act_bwd(g @ w2.float(), h, 1, p, ctx.seed, ctx.salt)
-            dx = (dh @ w1.float()).to(dy.dtype) if ctx.needs_input_grad[0] else None
+            resid = _slot_grad(ctx.x_slot, dh.shape[0])
+            dx = None
+            if ctx.needs_input_grad[0]:
+                dx = dh @ w1.float()
+                if resid is not None:
+                    dx = dx + resid.float()
+                dx = dx.to(dy.dtype)
             grad_buf(w1).add_(dh.t() @ x2.float())
             grad_buf(b1).add_(dh.sum(0))
             grad_ready(w1, b1)
         if dx is not None:
             dx = dx.reshape(dy.shape)
-        return dx, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None
 
 
-def ffn(x, linear1, linear2, p=0.0, rng=None, salt=0):
+def ffn(x, linear1, linear2, p=0.0, rng=None, salt=0, x_slot=None):
     if rng is None:
         from .layernorm import _NULL_RNG
         rng, p = _NULL_RNG, 0.0
-    return FFNFn.apply(x, linear1.weight, linear1.bias, linear2.weight, linear2.bias, float(p), rng, int(salt))
+    return FFNFn.apply(x, linear1.weight, linear1.bias, linear2.weight, linear2.bias, float(p), rng, int(salt),
+                       x_slot)
