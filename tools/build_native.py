@@ -7,7 +7,7 @@
                               vocab encoder, batch padding, shuffling (csrc/runtime/*.cpp), g++.
 
 Incremental: an object is rebuilt when its source or any header under csrc/include changes.
-Usage: python tools/build_native.py [--force] [--jobs N] [--debug-asan]
+Usage: python tools/build_native.py [--force] [--jobs N] [--asan-runtime]
 """
 import argparse
 import os
@@ -106,12 +106,36 @@ def build(force=False, jobs=8, verbose=True):
     return c_so, rt_so
 
 
+SAN_FLAGS = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined", "-g",
+             "-O1"]
+
+
+def build_runtime_sanitized(out_dir=None, verbose=True):
+    """Host-runtime extension built with AddressSanitizer + UBSan into
+    build/asan/_runtime<suffix>; load it in a process started with libasan preloaded
+    (tools/sanitize_runtime.py does both)."""
+    out_dir = out_dir or os.path.join(ROOT, "build", "asan")
+    os.makedirs(out_dir, exist_ok=True)
+    inc = ["-I" + os.path.join(CSRC, "include")] + ["-I" + p for p in _pybind_includes()]
+    rt_dir = os.path.join(CSRC, "runtime")
+    srcs = sorted(os.path.join(rt_dir, f) for f in os.listdir(rt_dir) if f.endswith(".cpp"))
+    so = os.path.join(out_dir, "_runtime" + _ext_suffix())
+    _run(["g++", "-std=c++17", "-fPIC", "-shared", "-pthread", "-fvisibility=hidden", "-o", so] + SAN_FLAGS + inc +
+         srcs)
+    if verbose:
+        print("[asan]", os.path.relpath(so, ROOT), flush=True)
+    return so
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("--asan-runtime", action="store_true", help="also build the sanitizer runtime extension")
     args = ap.parse_args()
     build(force=args.force, jobs=args.jobs)
+    if args.asan_runtime:
+        build_runtime_sanitized()
 
 
 if __name__ == "__main__":
