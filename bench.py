@@ -83,7 +83,7 @@ def bench_cnn(args, rank, world, device):
     flat = FlatParams(model)
     opt = SGD(flat, lr=0.01)
     ddp = DataParallel(flat) if world > 1 else None
-    use_graph = device.type == "cuda" and (world == 1 or args.graph == "on")
+    use_graph = device.type == "cuda" and args.graph != "off"
     runner = StepRunner(model, lambda m, x, y: m.loss(x, y), opt, ddp, graph=use_graph)
     imgs, labels = fashion_mnist_like(16 * args.cnn_batch, seed=7 + rank, device=device)
     batches = [(imgs[i * args.cnn_batch:(i + 1) * args.cnn_batch], labels[i * args.cnn_batch:(i + 1) * args.cnn_batch])
@@ -126,7 +126,7 @@ def main():
     flat = FlatParams(model)
     opt = Adam(flat, lr=1e-3)
     ddp = DataParallel(flat, bucket_mb=args.bucket_mb) if world > 1 else None
-    use_graph = {"on": True, "off": False, "auto": world == 1}[args.graph] and device.type == "cuda"
+    use_graph = args.graph != "off" and device.type == "cuda"
     runner = StepRunner(model, lambda m, s, t: m.training_step_loss(s, t), opt, ddp, graph=use_graph)
     pool = 8
     src, tgt = translation_pairs(pool * args.batch, args.seq, args.vocab, args.vocab, seed=100 + rank, device=device)

@@ -59,6 +59,15 @@ class DataParallel:
                 self._listener = _grad.add_listener(self._on_ready)
         self.reset()
 
+    def set_overlap(self, on):
+        """Enable / disable launching bucket all-reduces from inside backward (grad_ready)."""
+        if on and self._listener is None and self.world > 1:
+            self._listener = _grad.add_listener(self._on_ready)
+        elif not on and self._listener is not None:
+            _grad.remove_listener(self._listener)
+            self._listener = None
+        self.overlap = bool(on)
+
     def reset(self):
         self._pending = [len(idx) for (_, _, idx) in self.buckets]
         self._launched = [False] * len(self.buckets)

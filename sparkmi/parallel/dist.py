@@ -41,7 +41,7 @@ def init_distributed(backend=None, timeout_s=600):
     if ws > 1 and not is_dist():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
-        backend = backend or ("nccl" if use_gpu else "gloo")
+        backend = backend or os.environ.get("SPARKMI_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         kw = {}
         if backend == "nccl":
             kw["device_id"] = device

@@ -1,11 +1,16 @@
 """Training-step executor: eager or HIP-graph-captured, optionally data-parallel.
 
 A "step" = dropout-seed bump -> forward -> loss -> backward (gradients land in the flat fp32
-buffer, bucketed all-reduce overlapped when data-parallel) -> fused optimizer launch.
-With ``graph=True`` (single process) the whole step is captured once into a hipGraph after
-a few eager warm-up steps and then replayed: one host launch per step instead of hundreds,
-which matters at the reference's small per-GPU batches.  Inputs are
-copied into static device buffers before each replay.
+buffer) -> gradient all-reduce (data-parallel) -> fused optimizer launch.
+With ``graph=True`` the step's kernels are captured once into a hipGraph after a few eager
+warm-up steps and then replayed: one host launch per step instead of hundreds, which matters
+at the reference's small per-GPU batches.  Inputs are copied into static
+device buffers before each replay.
+  * one executor: the whole step (optimizer included) is one graph;
+  * data-parallel: the graph holds forward + backward; the gradient buckets are then
+    all-reduced by RCCL (a few large collectives over the flat buffer) and the optimizer runs
+    as one launch.  Collectives stay outside the graph, so no RCCL-in-capture dependency;
+    eager data-parallel steps instead overlap the bucket all-reduces with backward.
 """
 import torch
 
@@ -27,17 +32,25 @@ class StepRunner:
         if ddp is not None:
             optimizer.grad_scale = ddp.grad_scale
 
-    def _eager(self, *batch):
+    @property
+    def _dp(self):
+        return self.ddp is not None and self.ddp.world > 1
+
+    def _fwd_bwd(self, *batch):
         rng = getattr(self.model, "rng", None)
         if rng is not None:
             rng.advance()
         loss = self.loss_fn(self.model, *batch)
         loss.backward()
         _grad.join()
+        return loss.detach()
+
+    def _eager(self, *batch):
+        loss = self._fwd_bwd(*batch)
         if self.ddp is not None:
             self.ddp.finish()
         self.opt.step()
-        return loss.detach()
+        return loss
 
     def _capture(self, batch):
         """Record one step into a HIP graph.  Capture only records (nothing executes), so no
@@ -47,13 +60,18 @@ class StepRunner:
         self.static_in = [b.clone() for b in batch]
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self.static_loss = self._eager(*self.static_in)
+        if self._dp:
+            self.ddp.set_overlap(False)  # no collective may be enqueued during capture
+            with torch.cuda.graph(g):
+                self.static_loss = self._fwd_bwd(*self.static_in)
+        else:
+            with torch.cuda.graph(g):
+                self.static_loss = self._eager(*self.static_in)
         self.graph = g
 
     def step(self, *batch):
         self.steps += 1
-        use_graph = self.graph_requested and batch[0].is_cuda and (self.ddp is None or self.ddp.world == 1)
+        use_graph = self.graph_requested and batch[0].is_cuda
         if not use_graph or self.steps <= self.warmup_eager:
             return self._eager(*batch)
         if self.graph is None:
@@ -61,4 +79,7 @@ class StepRunner:
         for dst, src in zip(self.static_in, batch):
             dst.copy_(src, non_blocking=True)
         self.graph.replay()
+        if self._dp:
+            self.ddp.finish()   # bucketed RCCL all-reduce of the flat gradient buffer
+            self.opt.step()
         return self.static_loss
