@@ -33,6 +33,11 @@
 #ifndef GEMM_NS
 #define GEMM_NS 2
 #endif
+#ifdef GEMM_PROBE_NOEPI
+static constexpr bool kProbeNoEpi = true;
+#else
+static constexpr bool kProbeNoEpi = false;
+#endif
 #define TILE_ELEMS (BM * BKK)  // 8192 bf16 = 16 KiB per operand per stage
 #define NUM_CU 256
 
@@ -49,14 +54,15 @@ __device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t rsrc, unsigned sho
 // pair swizzle for k-major tiles (128 cols = 16 chunks of 8 bf16 per k-row)
 __device__ __forceinline__ int kmaj_s(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
 
-// Per-lane byte offsets (relative to the operand base, k0 = 0) of the 4 DMA pieces this wave
-// issues for one 128 x 64 (k-contig: [128 rows][64 k]) or 64 x 128 (k-major: [64 k][128 cols])
-// bf16 tile.  The XOR swizzle lives in these SOURCE offsets; the LDS image is lane-linear.
-template <bool KMAJ>
-__device__ __forceinline__ void tile_voffsets(long ld, int r0, int w, int lane, uint32_t (&vo)[4]) {
+// Per-lane byte offsets (relative to the operand base, k0 = 0) of the NP DMA pieces this wave
+// issues for one (32*NP) x 64 k-contig tile ([rows][64 k]) or a 64 x 128 k-major tile
+// ([64 k][128 cols], NP = 4).  The XOR swizzle lives in these SOURCE offsets; the LDS image is
+// lane-linear (each piece = one wave-instruction = 1 KiB).
+template <bool KMAJ, int NP>
+__device__ __forceinline__ void tile_voffsets(long ld, int r0, int w, int lane, uint32_t (&vo)[NP]) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int ins = w * 4 + i;
+  for (int i = 0; i < NP; ++i) {
+    const int ins = w * NP + i;
     if (!KMAJ) {
       const int row = ins * 8 + (lane >> 3);
       const int lc = (lane & 7) ^ (row & 7);
@@ -69,20 +75,23 @@ __device__ __forceinline__ void tile_voffsets(long ld, int r0, int w, int lane, 
   }
 }
 
-// Issue the 4 DMA pieces of one tile at k0 (soffset = k0 * k-stride bytes).
-template <bool KMAJ>
-__device__ __forceinline__ void stage_tile(__amdgpu_buffer_rsrc_t rsrc, long ld, int k0, const uint32_t (&vo)[4],
+// Issue the NP DMA pieces of one tile at k0 (soffset = k0 * k-stride bytes).
+template <bool KMAJ, int NP>
+__device__ __forceinline__ void stage_tile(__amdgpu_buffer_rsrc_t rsrc, long ld, int k0, const uint32_t (&vo)[NP],
                                            unsigned short* tile, int w) {
+#ifdef GEMM_PROBE_NODMA
+  return;
+#endif
   const uint32_t soff = KMAJ ? (uint32_t)((long)k0 * ld * 2) : (uint32_t)(k0 * 2);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) bdma16(rsrc, tile + (w * 4 + i) * 512, vo[i], soff);
+  for (int i = 0; i < NP; ++i) bdma16(rsrc, tile + (w * NP + i) * 512, vo[i], soff);
 }
 
-// zero logical k-columns >= kvalid of a staged tile (ragged-K tail)
+// zero logical k-columns >= kvalid of a staged tile (ragged-K tail); `rows` rows for k-contig
 template <bool KMAJ>
-__device__ __forceinline__ void zero_ktail(unsigned short* tile, int kvalid, int tid) {
+__device__ __forceinline__ void zero_ktail(unsigned short* tile, int kvalid, int tid, int rows) {
   if (!KMAJ) {
-    for (int e = tid; e < 128 * 8; e += 256) {
+    for (int e = tid; e < rows * 8; e += 256) {
       const int row = e >> 3, c = e & 7;
       if (c * 8 >= kvalid) *(uint4*)(tile + row * 64 + ((c ^ (row & 7)) << 3)) = make_uint4(0, 0, 0, 0);
       else if (c * 8 + 8 > kvalid) {
@@ -140,7 +149,7 @@ struct TileInfo {
   int m0, n0, kbeg, nk;
 };
 
-__device__ __forceinline__ TileInfo tile_of(const GemmArgs& g, int t, int ntn, int nwg) {
+__device__ __forceinline__ TileInfo tile_of(const GemmArgs& g, int t, int ntn, int nwg, int bm) {
   // t enumerates (split, tile); XCD-aware bijective remap inside one split's tile set
   const int split = t / nwg;
   const int orig = t - split * nwg;
@@ -150,7 +159,7 @@ __device__ __forceinline__ TileInfo tile_of(const GemmArgs& g, int t, int ntn, i
     wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
   }
   TileInfo ti;
-  ti.m0 = (wgid / ntn) * BM;
+  ti.m0 = (wgid / ntn) * bm;
   ti.n0 = (wgid % ntn) * BN;
   ti.kbeg = split * g.k_per_split;
   const int kend = min(g.K, ti.kbeg + g.k_per_split);
@@ -162,14 +171,23 @@ __device__ __forceinline__ TileInfo tile_of(const GemmArgs& g, int t, int ntn, i
 // Persistent over tiles (grid = min(tiles, WG_PER_CU * 256)); per tile: NS-deep DMA prologue,
 // k-loop with counted waits, drain, epilogue.  With NS = 2 (64 KiB LDS) two workgroups share a
 // CU, so one's prologue/epilogue overlaps the other's MFMA loop.
-template <bool AK, bool BKM, bool SWAP, int NS>
-__global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void gemm_bf16_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) unsigned short smem[NS * 2 * TILE_ELEMS];
+// FM = 16-row A fragments per wave: 4 -> 128 x 128 tiles, 2 -> 64 x 128 tiles (twice the
+// workgroups for the transformer's N = 512 GEMMs, so two tiles share a CU and one's load /
+// store phases overlap the other's MFMAs).  A k-major A operand (wgrad) always uses FM = 4.
+template <bool AK, bool BKM, bool SWAP, int NS, int FM>
+__global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_bf16_kernel(GemmArgs g) {
+  constexpr int BMT = 32 * FM;                 // tile rows (M)
+  constexpr int NPA = AK ? 4 : FM;             // DMA pieces per wave per stage, A operand
+  constexpr int A_ELEMS = BMT * BKK;
+  constexpr int STAGE = A_ELEMS + TILE_ELEMS;  // A then B (128 rows) per stage
+  constexpr int VM1 = NPA + 4;                 // vector-memory ops per wave per stage
+  static_assert(!AK || FM == 4, "k-major A needs 128-wide tiles");
+  __shared__ __attribute__((aligned(16))) unsigned short smem[NS * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
   const int ntn = (g.N + BN - 1) / BN;
-  const int ntm = (g.M + BM - 1) / BM;
+  const int ntm = (g.M + BMT - 1) / BMT;
   const int nwg = ntm * ntn;
   const int total_tiles = nwg * g.splits;
   const bool ragged = (g.K % BKK) != 0 || (g.K % g.k_per_split) != 0;
@@ -178,69 +196,142 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void gemm_bf16_kernel(GemmA
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, 0, (int)g.b_bytes, 0x00020000);
 
   for (int t = blockIdx.x; t < total_tiles; t += gridDim.x) {
-    const TileInfo ti = tile_of(g, t, ntn, nwg);
+    const TileInfo ti = tile_of(g, t, ntn, nwg, BMT);
     const int m0 = ti.m0, n0 = ti.n0, nk = ti.nk;
-    uint32_t voA[4], voB[4];
-    tile_voffsets<AK>(g.lda, m0, w, lane, voA);
-    tile_voffsets<BKM>(g.ldb, n0, w, lane, voB);
-    f32x4_t acc[4][4];
+    uint32_t voA[NPA], voB[4];
+    tile_voffsets<AK, NPA>(g.lda, m0, w, lane, voA);
+    tile_voffsets<BKM, 4>(g.ldb, n0, w, lane, voB);
+    f32x4_t acc[FM][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s0 = 0; s0 < NS - 1; ++s0) {
       if (s0 < nk) {
-        unsigned short* st = smem + s0 * 2 * TILE_ELEMS;
-        stage_tile<AK>(rA, g.lda, ti.kbeg + s0 * BKK, voA, st, w);
-        stage_tile<BKM>(rB, g.ldb, ti.kbeg + s0 * BKK, voB, st + TILE_ELEMS, w);
+        unsigned short* st = smem + s0 * STAGE;
+        stage_tile<AK, NPA>(rA, g.lda, ti.kbeg + s0 * BKK, voA, st, w);
+        stage_tile<BKM, 4>(rB, g.ldb, ti.kbeg + s0 * BKK, voB, st + A_ELEMS, w);
       }
     }
     int rd = 0;
     for (int kt = 0; kt < nk; ++kt) {
       const int ahead = min(NS - 2, nk - 1 - kt);  // items staged beyond kt
-      if (NS >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else if (NS >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (NS >= 4 && ahead >= 2) {
+        if (VM1 == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      } else if (NS >= 3 && ahead >= 1) {
+        if (VM1 == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       __builtin_amdgcn_s_barrier();
       if (ragged) {
         const int kv = min(g.K, ti.kbeg + g.k_per_split) - (ti.kbeg + kt * BKK);
         if (kv < BKK) {
-          zero_ktail<AK>(smem + rd * 2 * TILE_ELEMS, kv, tid);
+          zero_ktail<AK>(smem + rd * STAGE, kv, tid, BMT);
           __syncthreads();
         }
       }
       if (kt + NS - 1 < nk) {
         int ws = rd + NS - 1;
         if (ws >= NS) ws -= NS;
-        unsigned short* st = smem + ws * 2 * TILE_ELEMS;
-        stage_tile<AK>(rA, g.lda, ti.kbeg + (kt + NS - 1) * BKK, voA, st, w);
-        stage_tile<BKM>(rB, g.ldb, ti.kbeg + (kt + NS - 1) * BKK, voB, st + TILE_ELEMS, w);
+        unsigned short* st = smem + ws * STAGE;
+        stage_tile<AK, NPA>(rA, g.lda, ti.kbeg + (kt + NS - 1) * BKK, voA, st, w);
+        stage_tile<BKM, 4>(rB, g.ldb, ti.kbeg + (kt + NS - 1) * BKK, voB, st + A_ELEMS, w);
       }
-      const unsigned short* ta = smem + rd * 2 * TILE_ELEMS;
-      const unsigned short* tb = ta + TILE_ELEMS;
+      const unsigned short* ta = smem + rd * STAGE;
+      const unsigned short* tb = ta + A_ELEMS;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        bf16x8_t af[4], bf[4];
+        bf16x8_t af[FM], bf[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = read_frag<AK>(ta, wm * 64 + i * 16, ks, lane);
+        for (int i = 0; i < FM; ++i) af[i] = read_frag<AK>(ta, wm * 16 * FM + i * 16, ks, lane);
 #pragma unroll
         for (int j = 0; j < 4; ++j) bf[j] = read_frag<BKM>(tb, wn * 64 + j * 16, ks, lane);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
+#ifdef GEMM_PROBE_NOMFMA
+            acc[i][j][0] += (float)af[i][0] + (float)bf[j][0];
+#else
             if (SWAP) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
             else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+#endif
           }
       }
       rd = (rd + 1 == NS) ? 0 : rd + 1;
     }
     // ---------------- epilogue (no DMA in flight) ----------------
-    if (SWAP) {
+#ifdef GEMM_PROBE_NOEPI
+    {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+      if (t == 1234.5f) ((float*)g.C)[tid] = t;
+    }
+    if (false) {
+#else
+    const bool vec8 = (g.N % 8 == 0) && (g.ldc % 8 == 0) && (!g.resid || g.ldr % 8 == 0) && (!g.dact_y || g.ldy % 8 == 0);
+    if (SWAP && !g.out_f32 && vec8) {
+      // LDS-staged bf16 epilogue.  Each wave parks its 64x64 fp32 sub-tile in its own 16 KiB of the
+      // (now idle) staging LDS — 16-B chunk c of row r at c ^ (r & 15), conflict-free for both
+      // passes — then re-reads it row-wise so every lane owns 8 consecutive columns: residual /
+      // mask operands are 16-B loads and each store instruction writes 8 full 128-B row segments
+      // (the direct form wrote 32-B pieces of 16 rows).
+      __syncthreads();  // every wave is done reading the k-loop's staging buffers
+      float* ep = (float*)smem + w * (FM * 16 * 64);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = i * 16 + (lane & 15), c = j * 4 + (lane >> 4);
+          *(f32x4_t*)(ep + r * 64 + ((c ^ (r & 15)) << 2)) = acc[i][j];
+        }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are done
+      const int q = lane & 7;               // 8-column group of this lane
+      const int col = n0 + wn * 64 + q * 8;
+      float bb[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bb[e] = 0.f;
+      if (g.bias && col < g.N) {
+        const float4 b0 = *(const float4*)(g.bias + col), b1 = *(const float4*)(g.bias + col + 4);
+        bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w; bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+      }
+#pragma unroll 2
+      for (int it = 0; it < 2 * FM; ++it) {
+        const int r = it * 8 + (lane >> 3);
+        const int row = m0 + wm * 16 * FM + r;
+        const f32x4_t lo = *(const f32x4_t*)(ep + r * 64 + (((2 * q) ^ (r & 15)) << 2));
+        const f32x4_t hi = *(const f32x4_t*)(ep + r * 64 + (((2 * q + 1) ^ (r & 15)) << 2));
+        if (row >= g.M || col >= g.N) continue;
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const long cidx = (long)row * g.ldc + col;
+        u16x8_t rs, dy;
+        if (g.resid) rs = *(const u16x8_t*)(g.resid + (long)row * g.ldr + col);
+        if (g.dact_y) dy = *(const u16x8_t*)(g.dact_y + (long)row * g.ldy + col);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float x = v[e] * g.alpha + bb[e];
+          if (g.resid) x += bf2f(rs[e]);
+          if (g.act == 1) x = fmaxf(x, 0.f);
+          if (g.dact_y) x = bf2f(dy[e]) > 0.f ? x * g.dscale : 0.f;
+          else if (g.thresh) x = smi_keep(seed, (uint32_t)(cidx + e), g.thresh) ? x * g.dscale : 0.f;
+          v[e] = x;
+        }
+        uint4 pk;
+        pk.x = pack2bf(v[0], v[1]); pk.y = pack2bf(v[2], v[3]); pk.z = pack2bf(v[4], v[5]); pk.w = pack2bf(v[6], v[7]);
+        *(uint4*)((unsigned short*)g.C + cidx) = pk;
+      }
+    } else if (SWAP) {
+#endif
       // acc[i][j][r] = C[m0 + wm*64 + i*16 + (lane&15)][n0 + wn*64 + j*16 + 4*(lane>>4) + r]
       const int cl = 4 * (lane >> 4);
-      const bool interior = (m0 + BM <= g.M) && (n0 + BN <= g.N);
+      const bool interior = (m0 + BMT <= g.M) && (n0 + BN <= g.N);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int col = n0 + wn * 64 + j * 16 + cl;
@@ -253,8 +344,8 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void gemm_bf16_kernel(GemmA
         }
         const float bb[4] = {bia.x, bia.y, bia.z, bia.w};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = m0 + wm * 64 + i * 16 + (lane & 15);
+        for (int i = 0; i < FM; ++i) {
+          const int row = m0 + wm * 16 * FM + i * 16 + (lane & 15);
           const long cidx = (long)row * g.ldc + col;
           if (g.out_f32) {
             float* C = (float*)g.C + cidx;
@@ -283,17 +374,17 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void gemm_bf16_kernel(GemmA
           }
         }
       }
-    } else {
+    } else if (!kProbeNoEpi) {
       // acc[i][j][r] = C[m0 + wm*64 + i*16 + 4*(lane>>4) + r][n0 + wn*64 + j*16 + (lane&15)]
       const int cl = lane & 15, rg = (lane >> 4) * 4;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int col = n0 + wn * 64 + j * 16 + cl;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < FM; ++i) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int row = m0 + wm * 64 + i * 16 + rg + r;
+            const int row = m0 + wm * 16 * FM + i * 16 + rg + r;
             if (row < g.M && col < g.N) {
               const long cidx = (long)row * g.ldc + col;
               float* C = (float*)g.C;
@@ -323,29 +414,44 @@ extern "C" int smi_gemm(const GemmArgs* args, hipStream_t st) {
   g.a_bytes = 2 * (ak ? (long)(g.K - 1) * g.lda + g.M : (long)(g.M - 1) * g.lda + g.K);
   g.b_bytes = 2 * (bk ? (long)(g.K - 1) * g.ldb + g.N : (long)(g.N - 1) * g.ldb + g.K);
   if (g.a_bytes >= (1L << 31) || g.b_bytes >= (1L << 31)) return -1;
-  const int ntiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN) * g.splits;
-  // pipeline depth: NS=2 (64 KiB LDS, two workgroups per CU) or NS=4 (128 KiB, one per CU,
-  // three k-steps in flight).  SMI_GEMM_NS overrides the default.
-  static int ns_env = -1;
-  if (ns_env < 0) {
-    const char* e = getenv("SMI_GEMM_NS");
-    ns_env = e ? atoi(e) : 0;
+  // tile height: 64 rows (up to 3 workgroups per CU whose load / MFMA / store phases overlap)
+  // unless there are > 4 128-row tiles per CU anyway (the vocab projection); measured on the
+  // transformer shapes (tools/probes/run_gemm_probe3.sh).  SMI_GEMM_BM overrides (64 / 128).
+  static int bm_env = -1, ns_env = -1;
+  if (bm_env < 0) {
+    const char* e = getenv("SMI_GEMM_BM");
+    bm_env = e ? atoi(e) : 0;
+    const char* e2 = getenv("SMI_GEMM_NS");
+    ns_env = e2 ? atoi(e2) : 0;
   }
+  const int tiles128 = ((g.M + 127) / 128) * ((g.N + BN - 1) / BN) * g.splits;
+  int bm = (ak || tiles128 > 1024) ? 128 : 64;
+  if (!ak && (bm_env == 64 || bm_env == 128)) bm = bm_env;
+  const int ntiles = ((g.M + bm - 1) / bm) * ((g.N + BN - 1) / BN) * g.splits;
+  // pipeline depth: NS=2 (two workgroups per CU) or NS=4 (one per CU, three k-steps in flight)
   const int ns = ns_env == 2 || ns_env == 4 ? ns_env : GEMM_NS;
-  const int maxg = NUM_CU * (ns == 2 ? 2 : 1);
+  const int maxg = NUM_CU * (ns == 2 ? (bm == 64 ? 3 : 2) : 1);
   const int grid = ntiles < maxg ? ntiles : maxg;
   const bool atomic = g.out_f32 && g.atomic;
-#define SMI_GEMM_LAUNCH(NSV)                                                                                         \
-  switch (g.mode) {                                                                                                  \
-    case 0: hipLaunchKernelGGL((gemm_bf16_kernel<false, false, true, NSV>), dim3(grid), dim3(256), 0, st, g); break; \
-    case 1: hipLaunchKernelGGL((gemm_bf16_kernel<false, true, true, NSV>), dim3(grid), dim3(256), 0, st, g); break;  \
-    case 2:                                                                                                          \
-      if (atomic) hipLaunchKernelGGL((gemm_bf16_kernel<true, true, false, NSV>), dim3(grid), dim3(256), 0, st, g);   \
-      else hipLaunchKernelGGL((gemm_bf16_kernel<true, true, true, NSV>), dim3(grid), dim3(256), 0, st, g);           \
-      break;                                                                                                         \
-    default: return -1;                                                                                              \
+#define SMI_GEMM_LAUNCH(NSV, FMV)                                                                                         \
+  switch (g.mode) {                                                                                                       \
+    case 0: hipLaunchKernelGGL((gemm_bf16_kernel<false, false, true, NSV, FMV>), dim3(grid), dim3(256), 0, st, g); break; \
+    case 1: hipLaunchKernelGGL((gemm_bf16_kernel<false, true, true, NSV, FMV>), dim3(grid), dim3(256), 0, st, g); break;  \
+    default: return -1;                                                                                                   \
   }
-  if (ns == 4) { SMI_GEMM_LAUNCH(4) } else { SMI_GEMM_LAUNCH(2) }
+  if (g.mode == 2) {
+    if (ns == 4) {
+      if (atomic) hipLaunchKernelGGL((gemm_bf16_kernel<true, true, false, 4, 4>), dim3(grid), dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((gemm_bf16_kernel<true, true, true, 4, 4>), dim3(grid), dim3(256), 0, st, g);
+    } else {
+      if (atomic) hipLaunchKernelGGL((gemm_bf16_kernel<true, true, false, 2, 4>), dim3(grid), dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((gemm_bf16_kernel<true, true, true, 2, 4>), dim3(grid), dim3(256), 0, st, g);
+    }
+  } else if (ns == 4) {
+    if (bm == 64) { SMI_GEMM_LAUNCH(4, 2) } else { SMI_GEMM_LAUNCH(4, 4) }
+  } else {
+    if (bm == 64) { SMI_GEMM_LAUNCH(2, 2) } else { SMI_GEMM_LAUNCH(2, 4) }
+  }
 #undef SMI_GEMM_LAUNCH
   SMI_CHECK_LAUNCH();
 }
