@@ -117,6 +117,20 @@ __device__ __forceinline__ float score_adj(float s, int qi, int kj, int kl, bool
   return x;
 }
 
+// Chunk-vs-rows classification (wave-uniform): with keys [k0, k0+64) and query rows
+// [qlo, qhi], is the mask/bias the same for every pair?  Returns true and the common log2-domain
+// bias (0, LOG2E, or -inf = all masked) when it is, so the per-element path only runs on the
+// diagonal chunk and on ragged / padded chunks.
+template <int MODE, bool KPAD>
+__device__ __forceinline__ bool uniform_bias(int k0, int qlo, int qhi, bool full, float& bias) {
+  if (KPAD || !full) return false;
+  if (MODE == 0) { bias = 0.f; return true; }
+  if (k0 + 63 < qlo) { bias = (MODE == 1) ? LOG2E_F : 0.f; return true; }  // every key before every query
+  if (MODE == 1 && k0 >= qhi) { bias = 0.f; return true; }                   // no key strictly before
+  if (MODE == 2 && k0 > qhi) { bias = -INFINITY; return true; }              // every key after every query
+  return false;
+}
+
 __device__ __forceinline__ unsigned long long chunk_pad_mask(const unsigned char* kp, int k0, int Sk) {
   const int k = k0 + (threadIdx.x & 63);
   return __ballot(k < Sk && kp[k] != 0);
@@ -127,7 +141,7 @@ __device__ __forceinline__ unsigned long long chunk_pad_mask(const unsigned char
 // 64-key chunks.  S^T = K Q^T (lane owns one query column), online softmax in registers,
 // O^T += V^T P^T (so O's rescale by the running max is lane-local too).
 template <int MODE, bool KPAD>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnFwdArgs a) {
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned short Ks[2][IMG_ELEMS];
   __shared__ __attribute__((aligned(16))) unsigned short Vs[2][IMG_ELEMS];
   const int h = blockIdx.y, b = blockIdx.z;
@@ -181,25 +195,46 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnFwdArgs a) {
 #pragma unroll
     for (int qs = 0; qs < 2; ++qs) {
       const int qi = qwave + qs * 16 + n;
+      const int qlo = qwave + qs * 16;
+      float ub;
+      const bool uni = uniform_bias<MODE, KPAD>(k0, qlo, qlo + 15, full, ub);
       float cmax = -INFINITY;
+      if (uni) {  // x = s*scale + ub for every entry: max on the raw scores, one FMA per exp below
+        float r = -INFINITY;
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < 4; ++t) r = fmaxf(r, fmaxf(fmaxf(s[qs][t][0], s[qs][t][1]), fmaxf(s[qs][t][2], s[qs][t][3])));
+        cmax = r * a.scale_log2 + ub;
+      } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int kl = t * 16 + 4 * g + j;
-          s[qs][t][j] = score_adj<MODE, KPAD>(s[qs][t][j], qi, k0 + kl, kl, full, a.Sk, kmask, a.scale_log2);
-          cmax = fmaxf(cmax, s[qs][t][j]);
-        }
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int kl = t * 16 + 4 * g + j;
+            s[qs][t][j] = score_adj<MODE, KPAD>(s[qs][t][j], qi, k0 + kl, kl, full, a.Sk, kmask, a.scale_log2);
+            cmax = fmaxf(cmax, s[qs][t][j]);
+          }
+      }
       cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
       cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
       const float mnew = fmaxf(m[qs], cmax);
       const float mref = (mnew == -INFINITY) ? 0.f : mnew;
-      const float alpha = exp2f(m[qs] - mref);
+      const float alpha = __builtin_amdgcn_exp2f(m[qs] - mref);
       float psum = 0.f;
+      if (uni) {
+        const float off = ub - mref;
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { s[qs][t][j] = exp2f(s[qs][t][j] - mref); psum += s[qs][t][j]; }
+          for (int j = 0; j < 4; ++j) {
+            s[qs][t][j] = __builtin_amdgcn_exp2f(fmaf(s[qs][t][j], a.scale_log2, off));
+            psum += s[qs][t][j];
+          }
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { s[qs][t][j] = __builtin_amdgcn_exp2f(s[qs][t][j] - mref); psum += s[qs][t][j]; }
+      }
       psum += __shfl_xor(psum, 16, 64);
       psum += __shfl_xor(psum, 32, 64);
       l[qs] = l[qs] * alpha + psum;
@@ -263,7 +298,7 @@ __global__ void attn_delta_kernel(const unsigned short* __restrict__ o, const un
 // dQ: workgroup = 4 waves x 32 queries; K/V streamed.  S^T = K Q^T, dP^T = V dO^T,
 // dS^T = P^T o (dP^T - delta), dQ^T += K^T dS^T.
 template <int MODE, bool KPAD>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned short Ks[2][IMG_ELEMS];
   __shared__ __attribute__((aligned(16))) unsigned short Vs[2][IMG_ELEMS];
   const int h = blockIdx.y, b = blockIdx.z;
@@ -327,15 +362,28 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
 #pragma unroll
     for (int qs = 0; qs < 2; ++qs) {
       const int qi = qwave + qs * 16 + n;
+      const int qlo = qwave + qs * 16;
+      float ub;
+      if (uniform_bias<MODE, KPAD>(k0, qlo, qlo + 15, full, ub)) {
+        const float off = ub - lse[qs];
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int kl = t * 16 + 4 * g + j;
-          const float x = score_adj<MODE, KPAD>(s[qs][t][j], qi, k0 + kl, kl, full, a.Sk, kmask, a.scale_log2);
-          const float p = exp2f(x - lse[qs]);  // exp2(-inf) = 0 for masked entries
-          s[qs][t][j] = p * (dp[qs][t][j] - dl[qs]);
-        }
+          for (int j = 0; j < 4; ++j) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(s[qs][t][j], a.scale_log2, off));
+            s[qs][t][j] = p * (dp[qs][t][j] - dl[qs]);
+          }
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int kl = t * 16 + 4 * g + j;
+            const float x = score_adj<MODE, KPAD>(s[qs][t][j], qi, k0 + kl, kl, full, a.Sk, kmask, a.scale_log2);
+            const float p = __builtin_amdgcn_exp2f(x - lse[qs]);  // exp2(-inf) = 0 for masked entries
+            s[qs][t][j] = p * (dp[qs][t][j] - dl[qs]);
+          }
+      }
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -365,7 +413,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
 // dK, dV: workgroup = 4 waves x 32 keys; Q / dO streamed.  S = Q K^T and dP = dO V^T with the
 // key on the lane, P = exp2(S' - lse), dS = P o (dP - delta), dV^T += dO^T P, dK^T += Q^T dS.
 template <int MODE, bool KPAD>
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned short Qs[2][IMG_ELEMS];
   __shared__ __attribute__((aligned(16))) unsigned short Ds[2][IMG_ELEMS];
   __shared__ float lse_s[2][64], dl_s[2][64];
@@ -453,10 +501,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
         for (int j = 0; j < 4; ++j) {
           const int ql = t * 16 + 4 * g + j;
           const int qq = q0 + ql;
-          float x = s[kt][t][j] * a.scale_log2 + kbias;
+          float x = fmaf(s[kt][t][j], a.scale_log2, kbias);
           if (MODE == 1) x += (kj < qq) ? LOG2E_F : 0.f;
           if (MODE == 2) x = (kj > qq) ? -INFINITY : x;
-          const float p = exp2f(x - lse_s[buf][ql]);
+          const float p = __builtin_amdgcn_exp2f(x - lse_s[buf][ql]);
           s[kt][t][j] = p;
           dp[kt][t][j] = p * (dp[kt][t][j] - dl_s[buf][ql]);
         }

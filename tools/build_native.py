@@ -24,6 +24,11 @@ ARCH = os.environ.get("SPARKMI_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
+# per-kernel compiler flags: attention keeps its MFMA accumulators in VGPRs (the softmax works on
+# them every chunk; the default AGPR form cost two accvgpr moves per element per chunk)
+KERNEL_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def _ext_suffix():
     return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 
@@ -69,8 +74,9 @@ def build(force=False, jobs=8, verbose=True):
         o = os.path.join(OBJ, os.path.basename(s) + ".o")
         objs.append(o)
         if _needs(s, o, hdr_t, force):
+            extra = KERNEL_FLAGS.get(os.path.basename(s), [])
             jobs_list.append([HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-c", s, "-o", o,
-                              "-munsafe-fp-atomics"] + inc)
+                              "-munsafe-fp-atomics"] + extra + inc)
     bind_src = os.path.join(CSRC, "bindings.cpp")
     bind_obj = os.path.join(OBJ, "bindings.o")
     objs.append(bind_obj)
