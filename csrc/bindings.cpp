@@ -27,6 +27,7 @@ int smi_ln_fwd(const void*, const void*, const float*, const float*, void*, void
                const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
 int smi_ln_bwd(const void*, const void*, const float*, const float*, const float*, void*, void*, const void*, float*,
                float*, int, float*, float*, int, int, int, const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
+int smi_ln_bwd_reduce(const float*, const float*, int, int, float*, float*, int, hipStream_t);
 int smi_attn_fwd(const AttnFwdArgs*, hipStream_t);
 int smi_attn_bwd(const AttnBwdArgs*, const void*, float*, hipStream_t);
 int smi_ce_fwd(const void*, int, const long long*, int, int, long long, float*, float*, float*, float*, hipStream_t);
@@ -74,6 +75,9 @@ PYBIND11_MODULE(_C, m) {
                      u dbeta, int accumulate, int M, int D, u seedp, uint32_t salt, uint32_t thresh, float dscale, u st) {
     chk(smi_ln_bwd(P(dy), P(xs), PF(mean), PF(rstd), PF(gamma), P(dres), P(dh), P(dres_add), PF(pg), PF(pb), nblocks,
                    PF(dgamma), PF(dbeta), accumulate, M, D, (const uint32_t*)seedp, salt, thresh, dscale, S(st)), "ln_bwd");
+  });
+  m.def("ln_bwd_reduce", [](u pg, u pb, int nb, int D, u dgamma, u dbeta, int accumulate, u st) {
+    chk(smi_ln_bwd_reduce(PF(pg), PF(pb), nb, D, PF(dgamma), PF(dbeta), accumulate, S(st)), "ln_bwd_reduce");
   });
   m.def("attn_fwd", [](u q, u k, u v, py::tuple qs, py::tuple ks, py::tuple vs, u o, py::tuple os, u lse, u kpad, int B,
                        int H, int Sq, int Sk, int mode, float scale_log2, u st) {

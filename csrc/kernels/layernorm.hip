@@ -240,14 +240,26 @@ extern "C" int smi_ln_bwd(const void* dy, const void* xs, const float* mean, con
   const auto* ad = (const unsigned short*)dres_add;
   if (D % 8 || D > 2048) return -1;
   const int vpl = (D + 511) / 512;
-  const int rpw = vpl == 1 ? 4 : (vpl == 2 ? 2 : 1);
+  const int rpw = vpl <= 2 ? 2 : 1;
   const int nb = (M + 4 * rpw - 1) / (4 * rpw);
   if (nb > nblocks) return -1;
   dim3 grid(nb), block(256);
-  if (vpl == 1) hipLaunchKernelGGL((ln_bwd_kernel<1, 4>), grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, D, seedp, salt, thresh, dscale);
+  if (vpl == 1) hipLaunchKernelGGL((ln_bwd_kernel<1, 2>), grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, D, seedp, salt, thresh, dscale);
   else if (vpl == 2) hipLaunchKernelGGL((ln_bwd_kernel<2, 2>), grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, D, seedp, salt, thresh, dscale);
   else hipLaunchKernelGGL((ln_bwd_kernel<4, 1>), grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, D, seedp, salt, thresh, dscale);
-  const int groups = accumulate ? (nb >= 256 ? 8 : (nb >= 64 ? 4 : 1)) : 1;
-  hipLaunchKernelGGL(colsum2_kernel, dim3((D + 63) / 64, groups), dim3(256), 0, st, part_g, part_b, nb, D, dgamma, dbeta, accumulate);
+  if (dgamma) {  // else the caller reduces the partials itself (smi_ln_bwd_reduce, e.g. on a side stream)
+    const int groups = accumulate ? (nb >= 1024 ? 16 : (nb >= 256 ? 8 : (nb >= 64 ? 4 : 1))) : 1;
+    hipLaunchKernelGGL(colsum2_kernel, dim3((D + 63) / 64, groups), dim3(256), 0, st, part_g, part_b, nb, D, dgamma, dbeta,
+                       accumulate);
+  }
+  SMI_CHECK_LAUNCH();
+}
+
+// dgamma/dbeta (+)= column sums of the nb partial rows written by smi_ln_bwd
+extern "C" int smi_ln_bwd_reduce(const float* part_g, const float* part_b, int nb, int D, float* dgamma, float* dbeta,
+                                 int accumulate, hipStream_t st) {
+  const int groups = accumulate ? (nb >= 1024 ? 16 : (nb >= 256 ? 8 : (nb >= 64 ? 4 : 1))) : 1;
+  hipLaunchKernelGGL(colsum2_kernel, dim3((D + 63) / 64, groups), dim3(256), 0, st, part_g, part_b, nb, D, dgamma, dbeta,
+                     accumulate);
   SMI_CHECK_LAUNCH();
 }

@@ -23,7 +23,7 @@ _listeners = []
 # (autograd final callback), before a data-parallel bucket all-reduce, and before the optimizer.
 _SIDE_ENABLED = os.environ.get("SPARKMI_WGRAD_STREAM", "1") != "0"
 _side_streams = {}
-_pending = set()
+_pending = {}  # device -> the stream the side work was forked from (and must be joined back into)
 
 
 def _side_stream(device):
@@ -35,12 +35,16 @@ def _side_stream(device):
 
 
 def join(device=None):
-    """Make the current stream of ``device`` (all devices if None) wait for the side stream."""
+    """Make the stream the side work was forked from wait for the side stream (all devices if None).
+
+    The join target is the RECORDED fork stream, not the caller's current stream: the autograd
+    final callback may run on an engine thread whose current stream is not the backward's (during
+    a graph capture that would leave the side branch unjoined)."""
     devs = list(_pending) if device is None else [device]
     for d in devs:
-        if d in _pending:
-            torch.cuda.current_stream(d).wait_stream(_side_streams[d])
-            _pending.discard(d)
+        main = _pending.pop(d, None)
+        if main is not None:
+            main.wait_stream(_side_streams[d])
 
 
 @contextlib.contextmanager
@@ -57,7 +61,7 @@ def side(device, *tensors):
         if t is not None:
             t.record_stream(s)
     if dev not in _pending:
-        _pending.add(dev)
+        _pending[dev] = main
         try:
             torch.autograd.Variable._execution_engine.queue_callback(lambda: join(dev))
         except RuntimeError:
@@ -106,6 +110,7 @@ def bf16_weight(p: torch.Tensor) -> torch.Tensor:
 
 def needs_input_grad(ctx, i):
     return ctx.needs_input_grad[i]
+
 
 
 class ResidualGrad:

@@ -10,6 +10,7 @@ import torch
 
 from .. import _native
 from . import rng as _rng
+from . import _grad
 from ._grad import grad_buf, grad_ready
 
 
@@ -67,13 +68,16 @@ class AddDropoutLayerNorm(torch.autograd.Function):
             dres = torch.empty_like(dy) if ctx.has_r else None
             dh = torch.empty_like(dy)
             vpl = (D + 511) // 512
-            rows_per_block = 4 * (4 if vpl == 1 else (2 if vpl == 2 else 1))  # ln_bwd_kernel<VPL, RPW>
+            rows_per_block = 4 * (2 if vpl <= 2 else 1)  # ln_bwd_kernel<VPL, RPW>
             nb = (M + rows_per_block - 1) // rows_per_block
             part = torch.empty(2, nb, D, device=dy.device, dtype=torch.float32)
             C.ln_bwd(dy.data_ptr(), xs.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(),
                      _native.ptr(dres), dh.data_ptr(), 0, part[0].data_ptr(), part[1].data_ptr(), nb,
-                     gg.data_ptr(), gb.data_ptr(), 1, M, D, ctx.rng.ptr(), ctx.salt, _rng.threshold(p),
-                     _rng.scale(p), _native.stream())
+                     0, 0, 1, M, D, ctx.rng.ptr(), ctx.salt, _rng.threshold(p), _rng.scale(p), _native.stream())
+            # dgamma / dbeta are off the critical path: reduce the partial rows on the side stream
+            with _grad.side(dy.device, part):
+                C.ln_bwd_reduce(part[0].data_ptr(), part[1].data_ptr(), nb, D, gg.data_ptr(), gb.data_ptr(), 1,
+                                _native.stream())
         else:
             x = xs.reshape(M, D).float()
             g = dy.reshape(M, D).float()

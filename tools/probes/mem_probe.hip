@@ -67,7 +67,7 @@ int main() {
   unsigned int* seed;
   CK(hipMalloc(&a, n * 2)); CK(hipMalloc(&b, n * 2)); CK(hipMalloc(&c, n * 2)); CK(hipMalloc(&d, n * 2));
   CK(hipMalloc(&g, D * 4)); CK(hipMalloc(&be, D * 4)); CK(hipMalloc(&mean, M * 4)); CK(hipMalloc(&rstd, M * 4));
-  CK(hipMalloc(&pg, 1024 * D * 4)); CK(hipMalloc(&pb, 1024 * D * 4)); CK(hipMalloc(&seed, 4));
+  CK(hipMalloc(&pg, 2048 * D * 4)); CK(hipMalloc(&pb, 2048 * D * 4)); CK(hipMalloc(&seed, 4));
   CK(hipMemset(a, 0, n * 2)); CK(hipMemset(b, 0, n * 2)); CK(hipMemset(g, 0, D * 4)); CK(hipMemset(be, 0, D * 4));
   CK(hipMemset(seed, 0, 4));
   const double bytes = 4.0 * n * 2;
@@ -82,18 +82,17 @@ int main() {
   }
   rep("ln_fwd (drop+resid)", timeit([&] { smi_ln_fwd(a, b, g, be, c, d, mean, rstd, M, D, 1e-5f, seed, 7, 429496730u, 1.1f, 0); }));
   rep("ln_fwd (no drop)", timeit([&] { smi_ln_fwd(a, b, g, be, c, d, mean, rstd, M, D, 1e-5f, seed, 7, 0u, 1.f, 0); }));
-  rep("ln_bwd (drop)", timeit([&] { smi_ln_bwd(a, b, mean, rstd, g, c, d, nullptr, pg, pb, 1024, g, be, 1, M, D, seed, 7, 429496730u, 1.1f, 0); }));
-  rep("ln_bwd (no drop)", timeit([&] { smi_ln_bwd(a, b, mean, rstd, g, c, d, nullptr, pg, pb, 1024, g, be, 1, M, D, seed, 7, 0u, 1.f, 0); }));
-  for (int rpw : {1, 2, 4}) {
-    const int nb = M / (4 * rpw);
-    char nm[64]; snprintf(nm, 64, "ln_bwd_kernel<1,%d> only", rpw);
-    auto k = rpw == 1 ? ln_bwd_kernel<1, 1> : (rpw == 2 ? ln_bwd_kernel<1, 2> : ln_bwd_kernel<1, 4>);
-    rep(nm, timeit([&] { hipLaunchKernelGGL(k, dim3(nb), dim3(256), 0, 0, a, b, mean, rstd, g, c, d, nullptr, pg, pb, M, D, seed, 7, 429496730u, 1.1f); }));
-    snprintf(nm, 64, "colsum2 nb=%d", nb);
-    for (int gy : {1, 4, 8, 16}) {
-      char nm2[80]; snprintf(nm2, 80, "%s groups %d", nm, gy);
-      rep(nm2, timeit([&] { hipLaunchKernelGGL(colsum2_kernel, dim3(D / 64, gy), dim3(256), 0, 0, pg, pb, nb, D, g, be, 1); }));
-    }
+  rep("ln_bwd (drop)", timeit([&] { smi_ln_bwd(a, b, mean, rstd, g, c, d, nullptr, pg, pb, 2048, g, be, 1, M, D, seed, 7, 429496730u, 1.1f, 0); }));
+  rep("ln_bwd (no drop)", timeit([&] { smi_ln_bwd(a, b, mean, rstd, g, c, d, nullptr, pg, pb, 2048, g, be, 1, M, D, seed, 7, 0u, 1.f, 0); }));
+  {
+    rep("ln_bwd_kernel<1,1> only", timeit([&] { hipLaunchKernelGGL((ln_bwd_kernel<1, 1>), dim3(M / 4), dim3(256), 0, 0, a, b, mean, rstd, g, c, d, nullptr, pg, pb, M, D, seed, 7, 429496730u, 1.1f); }));
+    rep("ln_bwd_kernel<1,2> only", timeit([&] { hipLaunchKernelGGL((ln_bwd_kernel<1, 2>), dim3(M / 8), dim3(256), 0, 0, a, b, mean, rstd, g, c, d, nullptr, pg, pb, M, D, seed, 7, 429496730u, 1.1f); }));
+    rep("ln_bwd_kernel<1,4> only", timeit([&] { hipLaunchKernelGGL((ln_bwd_kernel<1, 4>), dim3(M / 16), dim3(256), 0, 0, a, b, mean, rstd, g, c, d, nullptr, pg, pb, M, D, seed, 7, 429496730u, 1.1f); }));
+    for (int nb : {512, 1024, 2048})
+      for (int gy : {1, 4, 8, 16}) {
+        char nm2[80]; snprintf(nm2, 80, "colsum2 nb=%d groups %d", nb, gy);
+        rep(nm2, timeit([&] { hipLaunchKernelGGL(colsum2_kernel, dim3(D / 64, gy), dim3(256), 0, 0, pg, pb, nb, D, g, be, 1); }));
+      }
   }
   CK(hipDeviceSynchronize());
   return 0;
