@@ -44,6 +44,7 @@ int smi_add_bf16(const void*, const void*, void*, long, hipStream_t);
 int smi_step_inc(float*, hipStream_t);
 int smi_mlp_fwd(const MLPArgs*, hipStream_t);
 int smi_gemm(const GemmArgs*, hipStream_t);
+int smi_splitk_reduce(const float*, int, long, float*, int, hipStream_t);
 int smi_cnn(const CNNArgs*, hipStream_t);
 int smi_cnn_reduce(const CNNArgs*, hipStream_t);
 int smi_gather_rows(const void*, const long long*, void*, long, long, hipStream_t);
@@ -177,6 +178,18 @@ PYBIND11_MODULE(_C, m) {
     chk(smi_gemm(&g, S(st)), "gemm");
   });
 
+  // weight-gradient GEMM in slab mode: split s of dW[N,K] = dY^T X (M split into `splits`) is
+  // written (fp32, no atomics) to slab + s*N*K; splitk_reduce then folds the slabs into the grad
+  m.def("gemm_wgrad_slab", [](u A, long lda, u B, long ldb, int N, int K, int M, u slab, int splits, u st) {
+    GemmArgs g{};
+    g.mode = 2; g.A = (const unsigned short*)A; g.lda = lda; g.B = (const unsigned short*)B; g.ldb = ldb;
+    g.M = N; g.N = K; g.K = M; g.C = (void*)slab; g.ldc = K; g.out_f32 = 1; g.atomic = 0; g.beta_acc = 0;
+    g.alpha = 1.f; g.dscale = 1.f; g.splits = splits; g.c_split_stride = (long)N * K;
+    chk(smi_gemm(&g, S(st)), "gemm_wgrad_slab");
+  });
+  m.def("splitk_reduce", [](u slab, int splits, long n, u out, int accumulate, u st) {
+    chk(smi_splitk_reduce((const float*)slab, splits, n, (float*)out, accumulate, S(st)), "splitk_reduce");
+  });
   m.def("gather_rows", [](u src, u idx, u out, long n, long row_bytes, u st) {
     chk(smi_gather_rows(P(src), (const long long*)idx, P(out), n, row_bytes, S(st)), "gather_rows");
   });

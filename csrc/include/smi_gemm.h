@@ -17,4 +17,5 @@ struct GemmArgs {
   int splits;
   int k_per_split;          // filled by the launcher
   long a_bytes, b_bytes;    // operand extents for the buffer descriptors (filled by the launcher)
+  long c_split_stride;      // split-K into slabs: split s writes C + s * c_split_stride (no atomics)
 };

@@ -146,7 +146,7 @@ __device__ __forceinline__ float epi_val(const GemmArgs& g, float v, float bia, 
 }
 
 struct TileInfo {
-  int m0, n0, kbeg, nk;
+  int m0, n0, kbeg, nk, split;
 };
 
 __device__ __forceinline__ TileInfo tile_of(const GemmArgs& g, int t, int ntn, int nwg, int bm) {
@@ -161,6 +161,7 @@ __device__ __forceinline__ TileInfo tile_of(const GemmArgs& g, int t, int ntn, i
   TileInfo ti;
   ti.m0 = (wgid / ntn) * bm;
   ti.n0 = (wgid % ntn) * BN;
+  ti.split = split;
   ti.kbeg = split * g.k_per_split;
   const int kend = min(g.K, ti.kbeg + g.k_per_split);
   ti.nk = (kend - ti.kbeg + BKK - 1) / BKK;
@@ -348,7 +349,7 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
           const int row = m0 + wm * 16 * FM + i * 16 + (lane & 15);
           const long cidx = (long)row * g.ldc + col;
           if (g.out_f32) {
-            float* C = (float*)g.C + cidx;
+            float* C = (float*)g.C + cidx + (long)ti.split * g.c_split_stride;
             float4 v = make_float4(acc[i][j][0] * g.alpha, acc[i][j][1] * g.alpha, acc[i][j][2] * g.alpha,
                                    acc[i][j][3] * g.alpha);
             if (interior || (row < g.M && col + 3 < g.N)) {
@@ -408,7 +409,7 @@ extern "C" int smi_gemm(const GemmArgs* args, hipStream_t st) {
   if (kps < BKK) kps = BKK;
   g.k_per_split = kps;
   g.splits = (g.K + kps - 1) / kps;
-  if (g.splits > 1 && !(g.out_f32 && g.atomic)) return -1;
+  if (g.splits > 1 && !(g.out_f32 && (g.atomic || g.c_split_stride >= (long)g.M * g.ldc))) return -1;
   // operand extents (elements -> bytes) for the DMA buffer descriptors
   const bool ak = g.mode == 2, bk = g.mode != 0;
   g.a_bytes = 2 * (ak ? (long)(g.K - 1) * g.lda + g.M : (long)(g.M - 1) * g.lda + g.K);
@@ -453,5 +454,33 @@ extern "C" int smi_gemm(const GemmArgs* args, hipStream_t st) {
     if (bm == 64) { SMI_GEMM_LAUNCH(2, 2) } else { SMI_GEMM_LAUNCH(2, 4) }
   }
 #undef SMI_GEMM_LAUNCH
+  SMI_CHECK_LAUNCH();
+}
+
+// out[i] (+)= sum_s slab[s][i]: the split-K combine of a slab-mode GEMM (deterministic, no atomics)
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, int splits, long n,
+                                                           float* __restrict__ out, int accumulate) {
+  const long n4 = n / 4;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float4 acc = accumulate ? ((const float4*)out)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+    for (int s = 0; s < splits; ++s) {
+      const float4 v = ((const float4*)(slab + (long)s * n))[i];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    ((float4*)out)[i] = acc;
+  }
+  for (long i = n4 * 4 + (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    float acc = accumulate ? out[i] : 0.f;
+    for (int s = 0; s < splits; ++s) acc += slab[(long)s * n + i];
+    out[i] = acc;
+  }
+}
+
+extern "C" int smi_splitk_reduce(const float* slab, int splits, long n, float* out, int accumulate, hipStream_t st) {
+  long blocks = (n / 4 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, slab, splits, n, out, accumulate);
   SMI_CHECK_LAUNCH();
 }

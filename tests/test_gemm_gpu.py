@@ -79,3 +79,21 @@ def test_epilogues():
     dh = G.dgrad(dy, w2, resid=resid, dact_y=y, dscale=R.scale(p))
     ref = (dy.float() @ w2.float() + resid.float()) * (y.float() > 0) * R.scale(p)
     assert _rel(dh, ref) < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["slab", "atomic"])
+@pytest.mark.parametrize("N,K,M,splits", [(512, 512, 8192, 16), (1536, 512, 2048, 3), (200, 72, 4104, 5)])
+def test_wgrad_split_modes(mode, N, K, M, splits):
+    torch.manual_seed(3)
+    dy = torch.randn(M, N, device="cuda").bfloat16()
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    gw = torch.randn(N, K, device="cuda")
+    ref = gw + dy.float().t() @ x.float()
+    old = G._WGRAD_MODE
+    G._WGRAD_MODE = mode
+    try:
+        G.wgrad(dy, x, gw, splits=splits)
+    finally:
+        G._WGRAD_MODE = old
+    torch.testing.assert_close(gw, ref, rtol=2e-3, atol=2e-2)
