@@ -180,12 +180,23 @@ PYBIND11_MODULE(_C, m) {
 
   // weight-gradient GEMM in slab mode: split s of dW[N,K] = dY^T X (M split into `splits`) is
   // written (fp32, no atomics) to slab + s*N*K; splitk_reduce then folds the slabs into the grad
-  m.def("gemm_wgrad_slab", [](u A, long lda, u B, long ldb, int N, int K, int M, u slab, int splits, u st) {
+  // bias_slab (optional, [splits][N]) receives the per-split column sums of dY (the bias gradient)
+  m.def("gemm_wgrad_slab", [](u A, long lda, u B, long ldb, int N, int K, int M, u slab, int splits, u bias_slab, u st) {
     GemmArgs g{};
     g.mode = 2; g.A = (const unsigned short*)A; g.lda = lda; g.B = (const unsigned short*)B; g.ldb = ldb;
     g.M = N; g.N = K; g.K = M; g.C = (void*)slab; g.ldc = K; g.out_f32 = 1; g.atomic = 0; g.beta_acc = 0;
     g.alpha = 1.f; g.dscale = 1.f; g.splits = splits; g.c_split_stride = (long)N * K;
+    g.bias_grad = (float*)bias_slab; g.bias_split_stride = N;
     chk(smi_gemm(&g, S(st)), "gemm_wgrad_slab");
+  });
+  // atomic-accumulate form: gw[N,K] += dY^T X (split-K fp32 atomics), gb[N] += dY^T 1 when given
+  m.def("gemm_wgrad_atomic", [](u A, long lda, u B, long ldb, int N, int K, int M, u gw, long ldgw, int splits, u gb,
+                                u st) {
+    GemmArgs g{};
+    g.mode = 2; g.A = (const unsigned short*)A; g.lda = lda; g.B = (const unsigned short*)B; g.ldb = ldb;
+    g.M = N; g.N = K; g.K = M; g.C = (void*)gw; g.ldc = ldgw; g.out_f32 = 1; g.atomic = 1; g.beta_acc = 1;
+    g.alpha = 1.f; g.dscale = 1.f; g.splits = splits; g.bias_grad = (float*)gb;
+    chk(smi_gemm(&g, S(st)), "gemm_wgrad_atomic");
   });
   m.def("splitk_reduce", [](u slab, int splits, long n, u out, int accumulate, u st) {
     chk(smi_splitk_reduce((const float*)slab, splits, n, (float*)out, accumulate, S(st)), "splitk_reduce");

@@ -18,4 +18,6 @@ struct GemmArgs {
   int k_per_split;          // filled by the launcher
   long a_bytes, b_bytes;    // operand extents for the buffer descriptors (filled by the launcher)
   long c_split_stride;      // split-K into slabs: split s writes C + s * c_split_stride (no atomics)
+  float* bias_grad;         // WGRAD only: column sums of A (= dY^T 1, the bias gradient) computed by an
+  long bias_split_stride;   // extra MFMA per fragment; slab mode writes + s*stride, atomic mode adds
 };

@@ -207,6 +207,12 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    // fused bias gradient (WGRAD): the workgroups of the first output-column block multiply
+    // their A fragments by a ones fragment — one extra MFMA per A fragment, no extra loads
+    const bool do_bias = AK && g.bias_grad && n0 == 0 && wn == 0;
+    f32x4_t accb[FM];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) accb[i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s0 = 0; s0 < NS - 1; ++s0) {
       if (s0 < nk) {
@@ -262,6 +268,16 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
             else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
 #endif
           }
+        if (AK && do_bias) {
+          bf16x8_t ones;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ones[e] = (short)0x3F80;  // bf16 1.0
+#pragma unroll
+          for (int i = 0; i < FM; ++i) {
+            if (SWAP) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[i], accb[i], 0, 0, 0);
+            else accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, accb[i], 0, 0, 0);
+          }
+        }
       }
       rd = (rd + 1 == NS) ? 0 : rd + 1;
     }
@@ -392,6 +408,30 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
               const float v = acc[i][j][r] * g.alpha;
               if (g.atomic) atomicAdd(C + cidx, v);
               else C[cidx] = g.beta_acc ? C[cidx] + v : v;
+            }
+          }
+        }
+      }
+    }
+    if (AK && do_bias) {
+      // SWAP: lane holds sum_k A[k][c] for c = i*16 + (lane & 15) in all four registers;
+      // non-SWAP: lane holds rows 4*(lane>>4) + r of fragment i in register r
+      float* bdst = g.bias_grad + (g.atomic ? 0 : (long)ti.split * g.bias_split_stride);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        if (SWAP) {
+          const int row = m0 + wm * 16 * FM + i * 16 + (lane & 15);
+          if ((lane >> 4) == 0 && row < g.M) {
+            if (g.atomic) atomicAdd(bdst + row, accb[i][0]);
+            else bdst[row] = accb[i][0];
+          }
+        } else if ((lane & 15) == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = m0 + wm * 16 * FM + i * 16 + 4 * (lane >> 4) + r;
+            if (row < g.M) {
+              if (g.atomic) atomicAdd(bdst + row, accb[i][r]);
+              else bdst[row] = accb[i][r];
             }
           }
         }

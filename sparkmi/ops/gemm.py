@@ -112,8 +112,9 @@ def _actual_splits(M, s):
     return (M + kps - 1) // kps
 
 
-def wgrad(dy, x, gw, splits=None):
-    """gw [N,K] fp32 += dy[M,N]^T @ x[M,K].
+def wgrad(dy, x, gw, splits=None, gb=None):
+    """gw [N,K] fp32 += dy[M,N]^T @ x[M,K]; with ``gb`` also gb[N] += column sums of dy (the bias
+    gradient, computed inside the same kernel by an extra MFMA per dy fragment).
 
     Split-K over M.  Slab mode (default): every split writes its partial tile to an fp32 slab
     with plain stores and one vectorised pass folds the slabs into ``gw`` — deterministic, and
@@ -125,11 +126,14 @@ def wgrad(dy, x, gw, splits=None):
     C = _native.C()
     if _WGRAD_MODE == "slab" and s > 1:
         s = _actual_splits(M, s)
-        slab = torch.empty(s, N, K, device=gw.device, dtype=torch.float32)
+        slab = torch.empty(s * N * K + (s * N if gb is not None else 0), device=gw.device, dtype=torch.float32)
+        bslab = slab[s * N * K:] if gb is not None else None
         C.gemm_wgrad_slab(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), N, K, M, slab.data_ptr(), s,
-                          _native.stream())
+                          _native.ptr(bslab), _native.stream())
         C.splitk_reduce(slab.data_ptr(), s, N * K, gw.data_ptr(), 1, _native.stream())
+        if gb is not None:
+            C.splitk_reduce(bslab.data_ptr(), s, N, gb.data_ptr(), 1, _native.stream())
         return gw
-    C.gemm(2, dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), N, K, M, gw.data_ptr(), gw.stride(0),
-                     1, 1, 1, 1.0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1.0, s, _native.stream())
+    C.gemm_wgrad_atomic(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), N, K, M, gw.data_ptr(),
+                        gw.stride(0), s, _native.ptr(gb), _native.stream())
     return gw

@@ -35,19 +35,28 @@ def _blaslt_wgrad(gw, dy2, x2):
         gw.add_(torch.mm(dy2.t(), x2).float())
 
 
-def _wgrad_accumulate(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor):
-    """gw (fp32 [N,K]) += dy2^T @ x2 with fp32 accumulation on the GPU."""
+def _wgrad_accumulate(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, gb=None):
+    """gw (fp32 [N,K]) += dy2^T @ x2 with fp32 accumulation on the GPU; gb (fp32 [N], optional)
+    += column sums of dy2 — fused into sparkmi's wgrad kernel, a column-sum kernel otherwise."""
     N, K = gw.shape
     M = dy2.shape[0]
     if G.supported(N, K, M, dy2, x2, mode=2) and gw.is_contiguous():
-        key = ("wgrad", N, K, M)
+        key = ("wgrad", N, K, M, gb is not None)
         if key not in G._choices and not torch.cuda.is_current_stream_capturing():
-            scratch = torch.zeros_like(gw)  # the timing runs must not touch the real gradient
-            G.choose(key, lambda: G.wgrad(dy2, x2, scratch), lambda: _blaslt_wgrad(scratch, dy2, x2))
+            scratch = torch.zeros_like(gw)  # the timing runs must not touch the real gradients
+            bscr = torch.zeros_like(gb) if gb is not None else None
+
+            def run_blaslt():
+                _blaslt_wgrad(scratch, dy2, x2)
+                if bscr is not None:
+                    _colsum(dy2, bscr)
+            G.choose(key, lambda: G.wgrad(dy2, x2, scratch, gb=bscr), run_blaslt)
         if G.choose(key, None, None) == "smi":
-            G.wgrad(dy2, x2, gw)
+            G.wgrad(dy2, x2, gw, gb=gb)
             return
     _blaslt_wgrad(gw, dy2, x2)
+    if gb is not None:
+        _colsum(dy2, gb)
 
 
 def _blaslt_dgrad(g2, w_bf, resid, dact_y, dscale):
@@ -167,9 +176,7 @@ class LinearFn(torch.autograd.Function):
             dx = _dgrad(g2, bf16_weight(weight), resid=resid) if ctx.needs_input_grad[0] else None
             bgrad = grad_buf(bias) if bias is not None else None
             with _grad.side(g2.device, g2, x2):
-                _wgrad_accumulate(gw, g2, x2)
-                if bias is not None:
-                    _colsum(g2, bgrad)
+                _wgrad_accumulate(gw, g2, x2, bgrad)
         else:
             g2 = _ref_act_bwd(dy2.float(), y2, act, p, ctx.seed, ctx.salt)
             resid = _slot_grad(ctx.x_slot, g2.shape[0])
@@ -243,14 +250,12 @@ class FFNFn(torch.autograd.Function):
             dh = _dgrad(dy2, bf16_weight(w2), dact_y=h, dscale=_rng.scale(p))
             gw2, gb2, gw1, gb1 = grad_buf(w2), grad_buf(b2), grad_buf(w1), grad_buf(b1)
             with _grad.side(dy2.device, dy2, h):
-                _wgrad_accumulate(gw2, dy2, h)
-                _colsum(dy2, gb2)
+                _wgrad_accumulate(gw2, dy2, h, gb2)
             grad_ready(w2, b2)
             resid = _slot_grad(ctx.x_slot, dh.shape[0])
             dx = _dgrad(dh, bf16_weight(w1), resid=resid) if ctx.needs_input_grad[0] else None
             with _grad.side(dh.device, dh, x2):
-                _wgrad_accumulate(gw1, dh, x2)
-                _colsum(dh, gb1)
+                _wgrad_accumulate(gw1, dh, x2, gb1)
             grad_ready(w1, b1)
         else:
             g = dy2.float()

@@ -97,3 +97,23 @@ def test_wgrad_split_modes(mode, N, K, M, splits):
     finally:
         G._WGRAD_MODE = old
     torch.testing.assert_close(gw, ref, rtol=2e-3, atol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["slab", "atomic"])
+@pytest.mark.parametrize("N,K,M,splits", [(512, 512, 8192, 16), (1536, 512, 2048, 1), (200, 72, 4104, 5)])
+def test_wgrad_fused_bias_grad(mode, N, K, M, splits):
+    torch.manual_seed(4)
+    dy = torch.randn(M, N, device="cuda").bfloat16()
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    gw = torch.zeros(N, K, device="cuda")
+    gb = torch.randn(N, device="cuda")
+    ref_b = gb + dy.float().sum(0)
+    old = G._WGRAD_MODE
+    G._WGRAD_MODE = mode
+    try:
+        G.wgrad(dy, x, gw, splits=splits, gb=gb)
+    finally:
+        G._WGRAD_MODE = old
+    torch.testing.assert_close(gw, dy.float().t() @ x.float(), rtol=2e-3, atol=2e-2)
+    torch.testing.assert_close(gb, ref_b, rtol=1e-3, atol=2e-2)
