@@ -18,6 +18,22 @@
 #include "smi_common.h"
 #include "smi_cnn.h"
 
+// One workgroup per image; 1024 threads (16 waves) so every phase of the per-image pipeline has
+// enough independent work items (the batch of 32 images occupies only 32 CUs)
+#define CNN_THREADS 1024
+#ifdef CNN_STAMPS  // diagnostic build only (tools/probes/cnn_probe.hip): per-phase s_memtime
+__device__ unsigned long long cnn_stamps[64 * 32];
+#define STAMP(i)                                                                            \
+  do {                                                                                      \
+    if (threadIdx.x == 0) {                                                                 \
+      unsigned long long t_;                                                                \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");           \
+      cnn_stamps[blockIdx.x * 32 + (i)] = t_;                                               \
+    }                                                                                       \
+  } while (0)
+#else
+#define STAMP(i) do {} while (0)
+#endif
 #define P28 30   // 28x28 plane with 1-pixel zero halo
 #define P14 16   // 14x14 plane with 1-pixel zero halo
 #define PL28 (P28 * P28)
@@ -26,12 +42,23 @@
 __device__ __forceinline__ int i28(int c, int y, int x) { return c * PL28 + (y + 1) * P28 + (x + 1); }
 __device__ __forceinline__ int i14(int c, int y, int x) { return c * PL14 + (y + 1) * P14 + (x + 1); }
 
+// Weights and biases are read through the constant address space: every lane reads the same
+// element, so these become s_load (scalar cache) operands of the FMAs instead of per-lane vector
+// loads (global_load) or LDS reads — the vector form made the conv loops load-bound (~14x off).
+typedef const __attribute__((address_space(4))) float* cfp;
+
 // forward 3x3 conv + bias + relu over an HxH plane set; in/out padded with pitch PP
 template <int H, int PP>
-__device__ void conv_fwd(const float* __restrict__ in, int cin, float* __restrict__ out, int cout,
-                         const float* __restrict__ w, const float* __restrict__ b) {
-  for (int pos = threadIdx.x; pos < H * H; pos += blockDim.x) {
-    const int y = pos / H, x = pos % H;
+__device__ __forceinline__ void conv_fwd(const float* __restrict__ in, int cin, float* __restrict__ out, int cout,
+                         const float* __restrict__ wg, const float* __restrict__ bg) {
+  const cfp w = (cfp)wg;
+  const cfp b = (cfp)bg;
+  // uniform trip count (masked tail) so the weight indices stay wave-uniform -> scalar loads
+  for (int base = 0; base < H * H; base += blockDim.x) {
+    const int pos = base + threadIdx.x;
+    const bool ok = pos < H * H;
+    const int pp = ok ? pos : 0;
+    const int y = pp / H, x = pp % H;
     float acc[CNN_MAXC];
 #pragma unroll
     for (int co = 0; co < CNN_MAXC; ++co) acc[co] = co < cout ? b[co] : 0.f;
@@ -45,7 +72,7 @@ __device__ void conv_fwd(const float* __restrict__ in, int cin, float* __restric
 #pragma unroll
       for (int co = 0; co < CNN_MAXC; ++co) {
         if (co < cout) {
-          const float* wp = w + (co * cin + ci) * 9;
+          const cfp wp = w + (co * cin + ci) * 9;
           float s = acc[co];
 #pragma unroll
           for (int k = 0; k < 9; ++k) s += wp[k] * v[k];
@@ -53,15 +80,17 @@ __device__ void conv_fwd(const float* __restrict__ in, int cin, float* __restric
         }
       }
     }
+    if (ok) {
 #pragma unroll
-    for (int co = 0; co < CNN_MAXC; ++co)
-      if (co < cout) out[co * PP * PP + (y + 1) * PP + (x + 1)] = fmaxf(acc[co], 0.f);
+      for (int co = 0; co < CNN_MAXC; ++co)
+        if (co < cout) out[co * PP * PP + (y + 1) * PP + (x + 1)] = fmaxf(acc[co], 0.f);
+    }
   }
 }
 
 // 2x2/2 max pool of H x H (pitch PPI) into H/2 planes (pitch PPO, halo offset HO)
 template <int H, int PPI, int PPO, int HO>
-__device__ void pool_fwd(const float* __restrict__ in, float* __restrict__ out, int c) {
+__device__ __forceinline__ void pool_fwd(const float* __restrict__ in, float* __restrict__ out, int c) {
   constexpr int Ho = H / 2;
   for (int e = threadIdx.x; e < c * Ho * Ho; e += blockDim.x) {
     const int ch = e / (Ho * Ho), r = e % (Ho * Ho), py = r / Ho, px = r % Ho;
@@ -74,7 +103,7 @@ __device__ void pool_fwd(const float* __restrict__ in, float* __restrict__ out, 
 // unpool the gradient g (per pooled element) into the pre-pool activation buffer a IN PLACE:
 // a <- (pos == first argmax of its window && a > 0) ? g : 0   (torch max_pool2d + relu backward)
 template <int H, int PPI>
-__device__ void unpool_relu_inplace(float* __restrict__ a, const float* __restrict__ g, int gpitch, int ghalo,
+__device__ __forceinline__ void unpool_relu_inplace(float* __restrict__ a, const float* __restrict__ g, int gpitch, int ghalo,
                                     int c) {
   constexpr int Ho = H / 2;
   for (int e = threadIdx.x; e < c * Ho * Ho; e += blockDim.x) {
@@ -96,61 +125,77 @@ __device__ void unpool_relu_inplace(float* __restrict__ a, const float* __restri
 }
 
 // dW[co][ci][k] = sum_pos dz[co][pos] * in[ci][pos+k-1]; db[co] = sum_pos dz[co][pos]
-// tasks = (co, ci, row-chunk); partials accumulated with LDS atomics into acc (cout*cin*9 + cout)
-template <int H, int PP, int CHUNKS>
-__device__ void conv_wgrad(const float* __restrict__ dz, const float* __restrict__ in, int cin, int cout,
+// One wave per (co, ci) pair, lanes over pixels (consecutive x -> conflict-free LDS reads; the
+// former lane-per-(co,ci,rows) mapping put every channel plane on the same banks), per-lane
+// partial sums reduced across the wave once per pair; each pair has one owner, so plain stores.
+template <int H, int PP>
+__device__ __forceinline__ void conv_wgrad(const float* __restrict__ dz, const float* __restrict__ in, int cin, int cout,
                            float* __restrict__ acc) {
-  const int ntask = cout * cin * CHUNKS;
-  constexpr int RPC = (H + CHUNKS - 1) / CHUNKS;
-  for (int t = threadIdx.x; t < ntask; t += blockDim.x) {
-    const int chunk = t % CHUNKS;
-    const int pair = t / CHUNKS;
-    const int co = pair / cin, ci = pair % cin;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int pair = wv; pair < cout * cin; pair += nw) {
+    const int co = pair / cin, ci = pair - co * cin;
     float s[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) s[k] = 0.f;
     float sb = 0.f;
-    const int y0 = chunk * RPC, y1 = min(H, y0 + RPC);
-    for (int y = y0; y < y1; ++y) {
-      const float* dzr = dz + co * PP * PP + (y + 1) * PP + 1;
-      const float* inr = in + ci * PP * PP + y * PP;  // row y-1 (halo coords), col x-1
-      for (int x = 0; x < H; ++x) {
-        const float d = dzr[x];
-        sb += d;
+    for (int p = lane; p < H * H; p += 64) {
+      const int y = p / H, x = p - y * H;
+      const float d = dz[co * PP * PP + (y + 1) * PP + x + 1];
+      const float* ir = in + ci * PP * PP + y * PP + x;  // row y-1, col x-1 in halo coords
+      sb += d;
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
+      for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-          for (int kx = 0; kx < 3; ++kx) s[ky * 3 + kx] += d * inr[ky * PP + x + kx];
-      }
+        for (int kx = 0; kx < 3; ++kx) s[ky * 3 + kx] += d * ir[ky * PP + kx];
     }
 #pragma unroll
-    for (int k = 0; k < 9; ++k) atomicAdd(&acc[(co * cin + ci) * 9 + k], s[k]);
-    if (ci == 0) atomicAdd(&acc[cout * cin * 9 + co], sb);
+    for (int k = 0; k < 9; ++k) s[k] = wave_sum(s[k]);
+    if (ci == 0) sb = wave_sum(sb);
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) acc[(co * cin + ci) * 9 + k] = s[k];
+      if (ci == 0) acc[cout * cin * 9 + co] = sb;
+    }
   }
 }
 
 // in-place transposed conv + relu': a[ci][pos] <- (a[ci][pos] > 0) ? sum_co sum_k w[co][ci][k] dz[co][pos-k+1] : 0
 // (relu=false: plain write into out)
 template <int H, int PP>
-__device__ void conv_dgrad(const float* __restrict__ dz, int cout, const float* __restrict__ w, int cin,
+__device__ __forceinline__ void conv_dgrad(const float* __restrict__ dz, int cout, const float* __restrict__ wg, int cin,
                            float* __restrict__ a, bool relu) {
-  for (int e = threadIdx.x; e < cin * H * H; e += blockDim.x) {
-    const int ci = e / (H * H), r = e % (H * H), y = r / H, x = r % H;
+  const cfp w = (cfp)wg;
+  for (int base = 0; base < cin * H * H; base += blockDim.x) {  // uniform trip count (see conv_fwd)
+    const int e = base + threadIdx.x;
+    const bool ok = e < cin * H * H;
+    const int ee = ok ? e : 0;
+    const int ci = ee / (H * H), r = ee % (H * H), y = r / H, x = r % H;
     float s = 0.f;
     for (int co = 0; co < cout; ++co) {
-      const float* wp = w + (co * cin + ci) * 9;
+      const int ciu = __builtin_amdgcn_readfirstlane(ci);
       const float* dp = dz + co * PP * PP + (y + 2) * PP + (x + 2);  // dz at (y+1, x+1) in halo coords, minus k
+      if (ciu == ci) {  // the whole wave shares one input channel: uniform weights
+        const cfp wp = w + (co * cin + ciu) * 9;
 #pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
+        for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx) s += wp[ky * 3 + kx] * dp[-ky * PP - kx];
+          for (int kx = 0; kx < 3; ++kx) s += wp[ky * 3 + kx] * dp[-ky * PP - kx];
+      } else {
+        const float* wp = wg + (co * cin + ci) * 9;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) s += wp[ky * 3 + kx] * dp[-ky * PP - kx];
+      }
     }
-    float* ap = a + ci * PP * PP + (y + 1) * PP + (x + 1);
-    *ap = relu ? (*ap > 0.f ? s : 0.f) : s;
+    if (ok) {
+      float* ap = a + ci * PP * PP + (y + 1) * PP + (x + 1);
+      *ap = relu ? (*ap > 0.f ? s : 0.f) : s;
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void cnn_kernel(CNNArgs g) {
+__global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int C = g.C, CI = g.cin, NC = g.classes;
   const int img = blockIdx.x;
@@ -166,6 +211,7 @@ __global__ __launch_bounds__(256) void cnn_kernel(CNNArgs g) {
   const int total = CI * PL28 + 2 * C * PL28 + 3 * C * PL14 + C * 49 + 16 + C * C * 9 + C;
   for (int i = threadIdx.x; i < total; i += blockDim.x) sm[i] = 0.f;
   __syncthreads();
+  STAMP(0);
   // image load (+ ToTensor scaling)
   for (int e = threadIdx.x; e < CI * 784; e += blockDim.x) {
     const int c = e / 784, r = e % 784;
@@ -174,28 +220,36 @@ __global__ __launch_bounds__(256) void cnn_kernel(CNNArgs g) {
     xin[i28(c, r / 28, r % 28)] = v;
   }
   __syncthreads();
+  STAMP(1);
   conv_fwd<28, P28>(xin, CI, a1, C, g.w[0], g.b[0]);
   __syncthreads();
+  STAMP(2);
   conv_fwd<28, P28>(a1, C, a2, C, g.w[1], g.b[1]);
   __syncthreads();
+  STAMP(3);
   pool_fwd<28, P28, P14, 1>(a2, p1, C);
   __syncthreads();
+  STAMP(4);
   conv_fwd<14, P14>(p1, C, a3, C, g.w[2], g.b[2]);
   __syncthreads();
+  STAMP(5);
   conv_fwd<14, P14>(a3, C, a4, C, g.w[3], g.b[3]);
   __syncthreads();
+  STAMP(6);
   pool_fwd<14, P14, 7, 0>(a4, p2, C);
   __syncthreads();
+  STAMP(7);
   // classifier: wave w computes logits o = w, w+4, ...
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int F = C * 49;
-  for (int o = wv; o < NC; o += 4) {
+  for (int o = wv; o < NC; o += CNN_THREADS / 64) {
     float s = 0.f;
     for (int i = lane; i < F; i += 64) s += g.w[4][o * F + i] * p2[i];
     s = wave_sum(s);
     if (lane == 0) lg[o] = s + g.b[4][o];
   }
   __syncthreads();
+  STAMP(8);
   if (threadIdx.x == 0) {
     float m = lg[0];
     int am = 0;
@@ -215,53 +269,65 @@ __global__ __launch_bounds__(256) void cnn_kernel(CNNArgs g) {
   }
   if (!g.train) return;
   __syncthreads();
+  STAMP(9);
   float* gs = g.slab + (long)img * g.P;  // this image's gradient slab
   // fc grads: gW[o][i] = dl[o] * p2[i]; gb[o] = dl[o]; dp2[i] = sum_o W[o][i] dl[o] (into p2 buffer after)
   for (int e = threadIdx.x; e < NC * F; e += blockDim.x) gs[g.off[8] + e] = lg[e / F] * p2[e % F];
   for (int o = threadIdx.x; o < NC; o += blockDim.x) gs[g.off[9] + o] = lg[o];
   __syncthreads();
+  STAMP(10);
   for (int i = threadIdx.x; i < F; i += blockDim.x) {
     float s = 0.f;
     for (int o = 0; o < NC; ++o) s += g.w[4][o * F + i] * lg[o];
     p2[i] = s;  // dp2 (flat NCHW)
   }
   __syncthreads();
+  STAMP(11);
   // pool2 backward + relu'(a4): dz4 in a4
   unpool_relu_inplace<14, P14>(a4, p2, 7, 0, C);
   __syncthreads();
+  STAMP(12);
   // conv4: dW4, db4 (from dz4, a3); then dz3 = convT(dz4) * relu'(a3) in a3
-  conv_wgrad<14, P14, 2>(a4, a3, C, C, wacc);
+  conv_wgrad<14, P14>(a4, a3, C, C, wacc);
   __syncthreads();
+  STAMP(13);
   for (int e = threadIdx.x; e < C * C * 9 + C; e += blockDim.x) {
     gs[(e < C * C * 9 ? g.off[6] + e : g.off[7] + e - C * C * 9)] = wacc[e];
     wacc[e] = 0.f;
   }
   conv_dgrad<14, P14>(a4, C, g.w[3], C, a3, true);
   __syncthreads();
+  STAMP(14);
   // conv3: dW3 (dz3, p1); dp1 = convT(dz3) into p1 (no relu: p1 is a pool output)
-  conv_wgrad<14, P14, 2>(a3, p1, C, C, wacc);
+  conv_wgrad<14, P14>(a3, p1, C, C, wacc);
   __syncthreads();
+  STAMP(15);
   for (int e = threadIdx.x; e < C * C * 9 + C; e += blockDim.x) {
     gs[(e < C * C * 9 ? g.off[4] + e : g.off[5] + e - C * C * 9)] = wacc[e];
     wacc[e] = 0.f;
   }
   conv_dgrad<14, P14>(a3, C, g.w[2], C, p1, false);
   __syncthreads();
+  STAMP(16);
   // pool1 backward + relu'(a2): dz2 in a2
   unpool_relu_inplace<28, P28>(a2, p1, P14, 1, C);
   __syncthreads();
+  STAMP(17);
   // conv2: dW2 (dz2, a1); dz1 = convT(dz2) * relu'(a1) in a1
-  conv_wgrad<28, P28, 2>(a2, a1, C, C, wacc);
+  conv_wgrad<28, P28>(a2, a1, C, C, wacc);
   __syncthreads();
+  STAMP(18);
   for (int e = threadIdx.x; e < C * C * 9 + C; e += blockDim.x) {
     gs[(e < C * C * 9 ? g.off[2] + e : g.off[3] + e - C * C * 9)] = wacc[e];
     wacc[e] = 0.f;
   }
   conv_dgrad<28, P28>(a2, C, g.w[1], C, a1, true);
   __syncthreads();
+  STAMP(19);
   // conv1: dW1 (dz1, x)
-  conv_wgrad<28, P28, 8>(a1, xin, CI, C, wacc);
+  conv_wgrad<28, P28>(a1, xin, CI, C, wacc);
   __syncthreads();
+  STAMP(20);
   for (int e = threadIdx.x; e < C * CI * 9 + C; e += blockDim.x)
     gs[(e < C * CI * 9 ? g.off[0] + e : g.off[1] + e - C * CI * 9)] = wacc[e];
 }
@@ -302,7 +368,7 @@ extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
   const size_t lds = cnn_lds_bytes(g);
   if (lds > 160 * 1024) return -1;
   hipFuncSetAttribute((const void*)cnn_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(cnn_kernel, dim3(g.B), dim3(256), lds, st, g);
+  hipLaunchKernelGGL(cnn_kernel, dim3(g.B), dim3(CNN_THREADS), lds, st, g);
   if (g.loss && g.row_loss)
     hipLaunchKernelGGL(cnn_loss_kernel, dim3(1), dim3(256), 0, st, g.row_loss, g.B, g.loss_scale, g.loss);
   SMI_CHECK_LAUNCH();

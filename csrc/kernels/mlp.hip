@@ -19,7 +19,7 @@ __device__ __forceinline__ float mlp_act(float v, int act) {
 }
 
 // forward one row; activations of every layer stored in a (lane-private) LDS slab
-__device__ float mlp_forward_row(const MLPArgs& a, int row, float* act_s) {
+__device__ __forceinline__ float mlp_forward_row(const MLPArgs& a, int row, float* act_s) {
   int off = 0;
   const int d0 = a.dims[0];
   for (int i = 0; i < d0; ++i) act_s[i] = a.x[(long)row * d0 + i];

@@ -1,0 +1,49 @@
+// Per-phase timing of the fused CNN kernel (one workgroup per image): s_memtime after every
+// barrier (-DCNN_STAMPS diagnostic build), averaged over images.
+#define CNN_STAMPS
+#include "../../csrc/kernels/cnn.hip"
+#include <cstdio>
+#include <vector>
+
+int main() {
+  const int B = 32, C = 10, CI = 1, NC = 10;
+  CNNArgs g{};
+  g.B = B; g.cin = CI; g.C = C; g.classes = NC; g.x_u8 = 1; g.x_scale = 1.f / 255.f; g.train = 1; g.loss_scale = 1.f / B;
+  unsigned char* x; long long* y; float *w[5], *b[5], *slab, *rl, *loss; int* pred;
+  (void)hipMalloc(&x, B * 784); (void)hipMemset(x, 7, B * 784);
+  (void)hipMalloc(&y, B * 8); (void)hipMemset(y, 0, B * 8);
+  const int sz[5] = {C * CI * 9, C * C * 9, C * C * 9, C * C * 9, NC * C * 49};
+  int off = 0;
+  const int bs[10] = {C * CI * 9, C, C * C * 9, C, C * C * 9, C, C * C * 9, C, NC * C * 49, NC};
+  for (int i = 0; i < 10; ++i) { g.off[i] = off; off += bs[i]; }
+  g.P = off;
+  for (int i = 0; i < 5; ++i) {
+    (void)hipMalloc(&w[i], sz[i] * 4); (void)hipMemset(w[i], 0, sz[i] * 4);
+    (void)hipMalloc(&b[i], 64); (void)hipMemset(b[i], 0, 64);
+    g.w[i] = w[i]; g.b[i] = b[i];
+  }
+  (void)hipMalloc(&slab, (size_t)B * g.P * 4); (void)hipMalloc(&rl, B * 4); (void)hipMalloc(&loss, 4); (void)hipMalloc(&pred, B * 4);
+  g.x = x; g.y = y; g.slab = slab; g.row_loss = rl; g.loss = loss; g.pred = pred;
+  for (int it = 0; it < 20; ++it) smi_cnn(&g, 0);
+  (void)hipDeviceSynchronize();
+  std::vector<unsigned long long> st(64 * 32);
+  (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(cnn_stamps), st.size() * 8);
+  int nph = 0;
+  for (int i = 0; i < 32; ++i) if (st[i]) nph = i + 1;
+  printf("phases %d\n", nph);
+  for (int p = 1; p < nph; ++p) {
+    double d = 0;
+    for (int im = 0; im < B; ++im) d += (double)(st[im * 32 + p] - st[im * 32 + p - 1]);
+    printf("phase %2d -> %2d: %8.0f ticks\n", p - 1, p, d / B);
+  }
+  double tot = 0;
+  for (int im = 0; im < B; ++im) tot += (double)(st[im * 32 + nph - 1] - st[im * 32]);
+  printf("total %8.0f ticks\n", tot / B);
+  hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0);
+  for (int it = 0; it < 50; ++it) smi_cnn(&g, 0);
+  (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+  float ms; (void)hipEventElapsedTime(&ms, e0, e1);
+  printf("kernel+loss: %.1f us per call\n", ms * 1000 / 50);
+  return 0;
+}
