@@ -44,7 +44,8 @@ int smi_add_bf16(const void*, const void*, void*, long, hipStream_t);
 int smi_step_inc(float*, hipStream_t);
 int smi_mlp_fwd(const MLPArgs*, hipStream_t);
 int smi_gemm(const GemmArgs*, hipStream_t);
-int smi_splitk_reduce(const float*, int, long, float*, int, hipStream_t);
+int smi_splitk_reduce(const float*, int, long, float*, long, float*, int, hipStream_t);
+void smi_gemm_set_pipe(int, int, int);
 int smi_cnn(const CNNArgs*, hipStream_t);
 int smi_cnn_reduce(const CNNArgs*, hipStream_t);
 int smi_gather_rows(const void*, const long long*, void*, long, long, hipStream_t);
@@ -198,9 +199,13 @@ PYBIND11_MODULE(_C, m) {
     g.alpha = 1.f; g.dscale = 1.f; g.splits = splits; g.bias_grad = (float*)gb;
     chk(smi_gemm(&g, S(st)), "gemm_wgrad_atomic");
   });
-  m.def("splitk_reduce", [](u slab, int splits, long n, u out, int accumulate, u st) {
-    chk(smi_splitk_reduce((const float*)slab, splits, n, (float*)out, accumulate, S(st)), "splitk_reduce");
+  // out[n] (+)= sum_s slab[s][:n]; with bout, also bout[nb] (+)= sum_s bias_slab[s][:nb] where the
+  // bias slabs follow the weight slabs (slab + splits * n) — one launch for both
+  m.def("splitk_reduce", [](u slab, int splits, long n, u out, long nb, u bout, int accumulate, u st) {
+    chk(smi_splitk_reduce((const float*)slab, splits, n, (float*)out, nb, (float*)bout, accumulate, S(st)),
+        "splitk_reduce");
   });
+  m.def("gemm_set_pipe", [](int tpw, int ns, int bm) { smi_gemm_set_pipe(tpw, ns, bm); });
   m.def("gather_rows", [](u src, u idx, u out, long n, long row_bytes, u st) {
     chk(smi_gather_rows(P(src), (const long long*)idx, P(out), n, row_bytes, S(st)), "gather_rows");
   });

@@ -38,6 +38,18 @@ static constexpr bool kProbeNoEpi = true;
 #else
 static constexpr bool kProbeNoEpi = false;
 #endif
+#ifdef GEMM_STAMPS
+// diagnostic build only (tools/probes/gemm_stamp_probe.hip): s_memrealtime (100 MHz) stamps of
+// each workgroup's phases, written by lane 0 of wave 0 to a buffer no output depends on
+__device__ unsigned long long* g_gemm_stamps;
+#define GSTAMP(slot)                                                                       \
+  do {                                                                                     \
+    if (threadIdx.x == 0 && t == (int)blockIdx.x)                                          \
+      g_gemm_stamps[(long)blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime();      \
+  } while (0)
+#else
+#define GSTAMP(slot) do {} while (0)
+#endif
 #define TILE_ELEMS (BM * BKK)  // 8192 bf16 = 16 KiB per operand per stage
 #define NUM_CU 256
 
@@ -197,6 +209,7 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, 0, (int)g.b_bytes, 0x00020000);
 
   for (int t = blockIdx.x; t < total_tiles; t += gridDim.x) {
+    GSTAMP(0);
     const TileInfo ti = tile_of(g, t, ntn, nwg, BMT);
     const int m0 = ti.m0, n0 = ti.n0, nk = ti.nk;
     uint32_t voA[NPA], voB[4];
@@ -234,6 +247,8 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __builtin_amdgcn_s_barrier();
+      if (kt == 0) GSTAMP(1);
+      if (kt == 1) GSTAMP(2);
       if (ragged) {
         const int kv = min(g.K, ti.kbeg + g.k_per_split) - (ti.kbeg + kt * BKK);
         if (kv < BKK) {
@@ -281,6 +296,7 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
       }
       rd = (rd + 1 == NS) ? 0 : rd + 1;
     }
+    GSTAMP(3);
     // ---------------- epilogue (no DMA in flight) ----------------
 #ifdef GEMM_PROBE_NOEPI
     {
@@ -319,18 +335,24 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
         const float4 b0 = *(const float4*)(g.bias + col), b1 = *(const float4*)(g.bias + col + 4);
         bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w; bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
       }
-#pragma unroll 2
+      // two passes: every load (LDS image, residual, mask source) and all the epilogue math
+      // first, then all the stores — a load issued after a store would make the wave wait for
+      // that store's completion (vmcnt counts both in issue order), serialising the tile's stores
+      uint4 pk[2 * FM];
+      bool ok[2 * FM];
+#pragma unroll
       for (int it = 0; it < 2 * FM; ++it) {
         const int r = it * 8 + (lane >> 3);
         const int row = m0 + wm * 16 * FM + r;
         const f32x4_t lo = *(const f32x4_t*)(ep + r * 64 + (((2 * q) ^ (r & 15)) << 2));
         const f32x4_t hi = *(const f32x4_t*)(ep + r * 64 + (((2 * q + 1) ^ (r & 15)) << 2));
-        if (row >= g.M || col >= g.N) continue;
+        ok[it] = row < g.M && col < g.N;
+        const int rowc = ok[it] ? row : 0, colc = ok[it] ? col : 0;
         float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        const long cidx = (long)row * g.ldc + col;
+        const long cidx = (long)rowc * g.ldc + colc;
         u16x8_t rs, dy;
-        if (g.resid) rs = *(const u16x8_t*)(g.resid + (long)row * g.ldr + col);
-        if (g.dact_y) dy = *(const u16x8_t*)(g.dact_y + (long)row * g.ldy + col);
+        if (g.resid) rs = *(const u16x8_t*)(g.resid + (long)rowc * g.ldr + colc);
+        if (g.dact_y) dy = *(const u16x8_t*)(g.dact_y + (long)rowc * g.ldy + colc);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           float x = v[e] * g.alpha + bb[e];
@@ -340,9 +362,13 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
           else if (g.thresh) x = smi_keep(seed, (uint32_t)(cidx + e), g.thresh) ? x * g.dscale : 0.f;
           v[e] = x;
         }
-        uint4 pk;
-        pk.x = pack2bf(v[0], v[1]); pk.y = pack2bf(v[2], v[3]); pk.z = pack2bf(v[4], v[5]); pk.w = pack2bf(v[6], v[7]);
-        *(uint4*)((unsigned short*)g.C + cidx) = pk;
+        pk[it].x = pack2bf(v[0], v[1]); pk[it].y = pack2bf(v[2], v[3]);
+        pk[it].z = pack2bf(v[4], v[5]); pk[it].w = pack2bf(v[6], v[7]);
+      }
+#pragma unroll
+      for (int it = 0; it < 2 * FM; ++it) {
+        const int row = m0 + wm * 16 * FM + it * 8 + (lane >> 3);
+        if (ok[it]) *(uint4*)((unsigned short*)g.C + (long)row * g.ldc + col) = pk[it];
       }
     } else if (SWAP) {
 #endif
@@ -437,8 +463,207 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
         }
       }
     }
+    GSTAMP(4);
     __syncthreads();  // every wave is done with the LDS stages before the next tile's prologue
   }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Cross-tile pipelined variant (FWD / DGRAD, bf16 output, no split-K, K % 64 == 0).
+// A workgroup owns tiles t = blockIdx.x + j * gridDim.x and walks ONE flattened stream of
+// (tile, k-step) items through an NS-deep LDS ring: the first k-steps of tile j+1 are issued
+// before tile j's epilogue, and the epilogue stores straight from the accumulators (no LDS, no
+// barrier), so the stores and the epilogue VALU run while the next tile's DMA is in flight.
+// Stores are widened to 16 B per lane: v_permlane16_swap pairs the 4-column groups of
+// neighbouring 16-column blocks (lanes of 16-lane rows g / g+1), so each lane writes 8
+// consecutive bf16 and each row gets 64 contiguous bytes per store instruction.
+// The counted waits include the epilogue's stores (vmcnt counts loads, stores and LDS-DMA in
+// issue order): S = 2 * FM dwordx4 stores per lane for an interior tile, vmcnt(0) after an
+// edge tile (its scalar tail stores are not counted).
+__device__ __forceinline__ void vm_wait_n(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+template <bool BKM, int NS, int FM>
+__global__ __launch_bounds__(256, 2) void gemm_pipe_kernel(GemmArgs g) {
+  constexpr int BMT = 32 * FM;
+  constexpr int NPA = FM;
+  constexpr int A_ELEMS = BMT * BKK;
+  constexpr int STAGE = A_ELEMS + TILE_ELEMS;
+  constexpr int VM1 = NPA + 4;       // DMA instructions per wave per item
+  constexpr int S_EPI = 2 * FM;      // dwordx4 stores per lane, interior tile
+  __shared__ __attribute__((aligned(16))) unsigned short smem[NS * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int ntn = (g.N + BN - 1) / BN;
+  const int ntm = (g.M + BMT - 1) / BMT;
+  const int nwg = ntm * ntn;
+  const int nk = g.K / BKK;
+  const int G = gridDim.x;
+  const int my_tiles = (nwg - (int)blockIdx.x + G - 1) / G;
+  const int total = my_tiles * nk;
+  const uint32_t seed = smi_seed(g.seedp, g.salt);
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, 0, (int)g.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, 0, (int)g.b_bytes, 0x00020000);
+  if (my_tiles <= 0) return;
+
+  // issue side: tile being staged and its per-lane DMA offsets
+  int iss_j = 0, iss_kt = 0;
+  uint32_t voA[NPA], voB[4];
+  {
+    const TileInfo t0 = tile_of(g, blockIdx.x, ntn, nwg, BMT);
+    tile_voffsets<false, NPA>(g.lda, t0.m0, w, lane, voA);
+    tile_voffsets<BKM, 4>(g.ldb, t0.n0, w, lane, voB);
+  }
+  int issued = 0;
+  auto issue_next = [&]() {
+    if (issued >= total) return;
+    if (iss_kt == nk) {  // next tile: recompute the DMA offsets
+      iss_kt = 0;
+      ++iss_j;
+      const TileInfo tn = tile_of(g, blockIdx.x + iss_j * G, ntn, nwg, BMT);
+      tile_voffsets<false, NPA>(g.lda, tn.m0, w, lane, voA);
+      tile_voffsets<BKM, 4>(g.ldb, tn.n0, w, lane, voB);
+    }
+    unsigned short* st = smem + (issued % NS) * STAGE;
+    stage_tile<false, NPA>(rA, g.lda, iss_kt * BKK, voA, st, w);
+    stage_tile<BKM, 4>(rB, g.ldb, iss_kt * BKK, voB, st + A_ELEMS, w);
+    ++iss_kt;
+    ++issued;
+  };
+#pragma unroll
+  for (int s0 = 0; s0 < NS - 1; ++s0) issue_next();
+
+  int last_epi = -1000;      // item index of the most recent epilogue
+  bool last_epi_counted = true;
+  int q = 0;
+  for (int j = 0; j < my_tiles; ++j) {
+    const int t = blockIdx.x + j * G;
+    (void)t;
+    if (j == 0) GSTAMP(0);
+    const TileInfo ti = tile_of(g, blockIdx.x + j * G, ntn, nwg, BMT);
+    const int m0 = ti.m0, n0 = ti.n0;
+    f32x4_t acc[FM][4];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) acc[i][jj] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt, ++q) {
+      // VMEM ops younger than item q's DMA: later items already issued + epilogue stores
+      const int later = issued - q - 1;
+      const bool epi_after = last_epi >= q - (NS - 1) && last_epi <= q - 1;
+      if (epi_after && !last_epi_counted) vm_wait_n(0);
+      else vm_wait_n(later * VM1 + (epi_after ? S_EPI : 0));
+      __builtin_amdgcn_s_barrier();
+      if (q == 0) GSTAMP(1);
+      if (q == 1) GSTAMP(2);
+      issue_next();
+      const unsigned short* ta = smem + (q % NS) * STAGE;
+      const unsigned short* tb = ta + A_ELEMS;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t af[FM], bf[4];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = read_frag<false>(ta, wm * 16 * FM + i * 16, ks, lane);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) bf[jj] = read_frag<BKM>(tb, wn * 64 + jj * 16, ks, lane);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj)
+            acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[jj], af[i], acc[i][jj], 0, 0, 0);
+      }
+    }
+    GSTAMP(3);
+    // ---- epilogue straight from registers; the next tile's first items are in flight ----
+    // acc[i][jj][r] = C[m0 + wm*16*FM + i*16 + (lane&15)][n0 + wn*64 + jj*16 + 4*(lane>>4) + r]
+    const int gq = lane >> 4;
+    const bool interior = (m0 + BMT <= g.M) && (n0 + BN <= g.N) && (g.ldc % 8 == 0);
+    last_epi = q - 1;
+    last_epi_counted = interior;
+    if (interior) {
+      uint2 pk[FM][4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int col = n0 + wn * 64 + jj * 16 + 4 * gq;
+        float4 bia = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (g.bias) bia = *(const float4*)(g.bias + col);
+        const float bb[4] = {bia.x, bia.y, bia.z, bia.w};
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int row = m0 + wm * 16 * FM + i * 16 + (lane & 15);
+          const long cidx = (long)row * g.ldc + col;
+          u16x4_t rs, dy;
+          if (g.resid) rs = *(const u16x4_t*)(g.resid + (long)row * g.ldr + col);
+          if (g.dact_y) dy = *(const u16x4_t*)(g.dact_y + (long)row * g.ldy + col);
+          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float x = acc[i][jj][r] * g.alpha + bb[r];
+            if (g.resid) x += bf2f(rs[r]);
+            if (g.act == 1) x = fmaxf(x, 0.f);
+            if (g.dact_y) x = bf2f(dy[r]) > 0.f ? x * g.dscale : 0.f;
+            else if (g.thresh) x = smi_keep(seed, (uint32_t)(cidx + r), g.thresh) ? x * g.dscale : 0.f;
+            o[r] = x;
+          }
+          pk[i][jj].x = pack2bf(o[0], o[1]);
+          pk[i][jj].y = pack2bf(o[2], o[3]);
+        }
+      }
+      // widen: rows g / g+1 of blocks (jj, jj+1) -> each lane 8 consecutive columns
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int jp = 0; jp < 4; jp += 2) {
+          auto sx = __builtin_amdgcn_permlane16_swap(pk[i][jp].x, pk[i][jp + 1].x, false, false);
+          auto sy = __builtin_amdgcn_permlane16_swap(pk[i][jp].y, pk[i][jp + 1].y, false, false);
+          const uint4 v = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+          const int row = m0 + wm * 16 * FM + i * 16 + (lane & 15);
+          const int col = n0 + wn * 64 + ((gq & 1) ? (jp + 1) * 16 + 4 * (gq - 1) : jp * 16 + 4 * gq);
+          *(uint4*)((unsigned short*)g.C + (long)row * g.ldc + col) = v;
+        }
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int col = n0 + wn * 64 + jj * 16 + 4 * gq;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int row = m0 + wm * 16 * FM + i * 16 + (lane & 15);
+          if (row >= g.M) continue;
+          const long cidx = (long)row * g.ldc + col;
+          for (int r = 0; r < 4; ++r) {
+            if (col + r >= g.N) break;
+            const float bia = g.bias ? g.bias[col + r] : 0.f;
+            ((unsigned short*)g.C)[cidx + r] = f2bf(epi_val(g, acc[i][jj][r], bia, row, col + r, cidx + r, seed));
+          }
+        }
+      }
+    }
+    GSTAMP(4);
+  }
+}
+
+static int g_pipe_tpw = -1, g_pipe_ns = 3, g_bm_force = 0;
+// runtime override of the pipelined-kernel policy (tiles per workgroup, ring depth; tpw 0 = off)
+// and of the tile height (bm 64 / 128; 0 = automatic)
+extern "C" void smi_gemm_set_pipe(int tpw, int ns, int bm) {
+  g_pipe_tpw = tpw;
+  g_pipe_ns = ns;
+  g_bm_force = bm;
 }
 
 extern "C" int smi_gemm(const GemmArgs* args, hipStream_t st) {
@@ -468,12 +693,36 @@ extern "C" int smi_gemm(const GemmArgs* args, hipStream_t st) {
   const int tiles128 = ((g.M + 127) / 128) * ((g.N + BN - 1) / BN) * g.splits;
   int bm = (ak || tiles128 > 1024) ? 128 : 64;
   if (!ak && (bm_env == 64 || bm_env == 128)) bm = bm_env;
+  if (!ak && (g_bm_force == 64 || g_bm_force == 128)) bm = g_bm_force;
   const int ntiles = ((g.M + bm - 1) / bm) * ((g.N + BN - 1) / BN) * g.splits;
   // pipeline depth: NS=2 (two workgroups per CU) or NS=4 (one per CU, three k-steps in flight)
   const int ns = ns_env == 2 || ns_env == 4 ? ns_env : GEMM_NS;
   const int maxg = NUM_CU * (ns == 2 ? (bm == 64 ? 3 : 2) : 1);
   const int grid = ntiles < maxg ? ntiles : maxg;
   const bool atomic = g.out_f32 && g.atomic;
+  // cross-tile pipelined kernel (SMI_GEMM_PIPE=<tiles per workgroup>, 0 = off)
+  if (g_pipe_tpw < 0) {
+    const char* e = getenv("SMI_GEMM_PIPE");
+    g_pipe_tpw = e ? atoi(e) : 0;
+    const char* e2 = getenv("SMI_GEMM_PIPE_NS");
+    g_pipe_ns = e2 ? atoi(e2) : 3;
+  }
+  const int pipe_env = g_pipe_tpw, pipe_ns = g_pipe_ns;
+  if (pipe_env > 0 && g.mode != 2 && !g.out_f32 && g.splits == 1 && g.K % BKK == 0 && g.K / BKK >= 4) {
+    const int nt = ((g.M + bm - 1) / bm) * ((g.N + BN - 1) / BN);
+    int pg = (nt + pipe_env - 1) / pipe_env;
+    if (pg > 2 * NUM_CU) pg = 2 * NUM_CU;
+#define SMI_PIPE_LAUNCH(BKMV, NSV)                                                                              \
+  if (bm == 64) hipLaunchKernelGGL((gemm_pipe_kernel<BKMV, NSV, 2>), dim3(pg), dim3(256), 0, st, g);            \
+  else hipLaunchKernelGGL((gemm_pipe_kernel<BKMV, NSV, 4>), dim3(pg), dim3(256), 0, st, g);
+    if (g.mode == 0) {
+      if (pipe_ns == 2) { SMI_PIPE_LAUNCH(false, 2) } else if (pipe_ns == 4) { SMI_PIPE_LAUNCH(false, 4) } else { SMI_PIPE_LAUNCH(false, 3) }
+    } else {
+      if (pipe_ns == 2) { SMI_PIPE_LAUNCH(true, 2) } else if (pipe_ns == 4) { SMI_PIPE_LAUNCH(true, 4) } else { SMI_PIPE_LAUNCH(true, 3) }
+    }
+#undef SMI_PIPE_LAUNCH
+    SMI_CHECK_LAUNCH();
+  }
 #define SMI_GEMM_LAUNCH(NSV, FMV)                                                                                         \
   switch (g.mode) {                                                                                                       \
     case 0: hipLaunchKernelGGL((gemm_bf16_kernel<false, false, true, NSV, FMV>), dim3(grid), dim3(256), 0, st, g); break; \
@@ -497,30 +746,74 @@ extern "C" int smi_gemm(const GemmArgs* args, hipStream_t st) {
   SMI_CHECK_LAUNCH();
 }
 
-// out[i] (+)= sum_s slab[s][i]: the split-K combine of a slab-mode GEMM (deterministic, no atomics)
+// out[i] (+)= sum_s slab[s][i]: the split-K combine of a slab-mode GEMM (deterministic, no atomics).
+// One launch folds BOTH the weight slabs (n elements per split) and the optional bias slabs (nb
+// per split, stored after the weight slabs): the bias range is handled by the grid's tail blocks.
+// Each thread owns one float4 and issues the loads of all its splits before adding (SPLITS is a
+// compile-time constant, so all S loads are in flight at once — the fold is HBM/MALL-bound, not
+// latency-bound); the running sum is added in split order, so the result is deterministic.
+template <int SPLITS>
+__device__ __forceinline__ void fold4(const float* __restrict__ slab, long stride4, long i, float4* __restrict__ out,
+                                      int accumulate) {
+  float4 v[SPLITS];
+#pragma unroll
+  for (int s = 0; s < SPLITS; ++s) v[s] = ((const float4*)slab)[(long)s * stride4 + i];
+  float4 acc = accumulate ? out[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int s = 0; s < SPLITS; ++s) { acc.x += v[s].x; acc.y += v[s].y; acc.z += v[s].z; acc.w += v[s].w; }
+  out[i] = acc;
+}
+
+template <int SPLITS>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, int splits, long n,
-                                                           float* __restrict__ out, int accumulate) {
-  const long n4 = n / 4;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-    float4 acc = accumulate ? ((const float4*)out)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll 4
-    for (int s = 0; s < splits; ++s) {
-      const float4 v = ((const float4*)(slab + (long)s * n))[i];
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+                                                           float* __restrict__ out, long nb, float* __restrict__ bout,
+                                                           int accumulate, int wblocks) {
+  if ((int)blockIdx.x < wblocks) {
+    const long n4 = n / 4;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)wblocks * 256) {
+      if constexpr (SPLITS > 0) fold4<SPLITS>(slab, n4, i, (float4*)out, accumulate);
+      else {
+        float4 acc = accumulate ? ((const float4*)out)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int s = 0; s < splits; ++s) {
+          const float4 v = ((const float4*)(slab + (long)s * n))[i];
+          acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
+        ((float4*)out)[i] = acc;
+      }
     }
-    ((float4*)out)[i] = acc;
-  }
-  for (long i = n4 * 4 + (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    float acc = accumulate ? out[i] : 0.f;
-    for (int s = 0; s < splits; ++s) acc += slab[(long)s * n + i];
-    out[i] = acc;
+    for (long i = n4 * 4 + (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)wblocks * 256) {
+      float acc = accumulate ? out[i] : 0.f;
+      for (int s = 0; s < splits; ++s) acc += slab[(long)s * n + i];
+      out[i] = acc;
+    }
+  } else {
+    const float* bslab = slab + (long)splits * n;
+    for (long i = (long)(blockIdx.x - wblocks) * 256 + threadIdx.x; i < nb; i += (long)(gridDim.x - wblocks) * 256) {
+      float acc = accumulate ? bout[i] : 0.f;
+      for (int s = 0; s < splits; ++s) acc += bslab[(long)s * nb + i];
+      bout[i] = acc;
+    }
   }
 }
 
-extern "C" int smi_splitk_reduce(const float* slab, int splits, long n, float* out, int accumulate, hipStream_t st) {
+extern "C" int smi_splitk_reduce(const float* slab, int splits, long n, float* out, long nb, float* bout,
+                                 int accumulate, hipStream_t st) {
   long blocks = (n / 4 + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
+  if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, slab, splits, n, out, accumulate);
+  const int bblocks = (nb > 0 && bout) ? (int)((nb + 255) / 256 < 8 ? (nb + 255) / 256 : 8) : 0;
+  if (!bout) nb = 0;
+  const dim3 grid((unsigned)(blocks + bblocks));
+  const int wb = (int)blocks;
+#define SMI_RED(S) hipLaunchKernelGGL(splitk_reduce_kernel<S>, grid, dim3(256), 0, st, slab, splits, n, out, nb, bout, accumulate, wb)
+  if (n % 4 != 0) { SMI_RED(0); }
+  else switch (splits) {
+    case 2: SMI_RED(2); break;
+    case 4: SMI_RED(4); break;
+    case 8: SMI_RED(8); break;
+    case 16: SMI_RED(16); break;
+    default: SMI_RED(0); break;
+  }
+#undef SMI_RED
   SMI_CHECK_LAUNCH();
 }

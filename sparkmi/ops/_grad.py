@@ -21,7 +21,11 @@ _listeners = []
 # Inside a HIP-graph capture the fork/join becomes parallel graph branches.  The main stream
 # joins the side stream before anything reads the gradients: at the end of every backward pass
 # (autograd final callback), before a data-parallel bucket all-reduce, and before the optimizer.
-_SIDE_ENABLED = os.environ.get("SPARKMI_WGRAD_STREAM", "1") != "0"
+# OFF by default (SPARKMI_WGRAD_STREAM=1 enables it): measured on MI355X, a replayed graph with
+# the fork/join branches leaves the GPU idle 15-20 us at each cross-queue dependency (1.06 ms of
+# idle per transformer step in 108 such gaps) — more than the overlap wins; the single-stream
+# step has no idle gaps at all (profiles/timeline_*).
+_SIDE_ENABLED = os.environ.get("SPARKMI_WGRAD_STREAM", "0") != "0"
 _side_streams = {}
 _pending = {}  # device -> the stream the side work was forked from (and must be joined back into)
 

@@ -130,9 +130,8 @@ def wgrad(dy, x, gw, splits=None, gb=None):
         bslab = slab[s * N * K:] if gb is not None else None
         C.gemm_wgrad_slab(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), N, K, M, slab.data_ptr(), s,
                           _native.ptr(bslab), _native.stream())
-        C.splitk_reduce(slab.data_ptr(), s, N * K, gw.data_ptr(), 1, _native.stream())
-        if gb is not None:
-            C.splitk_reduce(bslab.data_ptr(), s, N, gb.data_ptr(), 1, _native.stream())
+        C.splitk_reduce(slab.data_ptr(), s, N * K, gw.data_ptr(), N if gb is not None else 0, _native.ptr(gb), 1,
+                        _native.stream())
         return gw
     C.gemm_wgrad_atomic(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), N, K, M, gw.data_ptr(),
                         gw.stride(0), s, _native.ptr(gb), _native.stream())
