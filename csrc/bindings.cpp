@@ -45,7 +45,7 @@ int smi_step_inc(float*, hipStream_t);
 int smi_mlp_fwd(const MLPArgs*, hipStream_t);
 int smi_gemm(const GemmArgs*, hipStream_t);
 int smi_splitk_reduce(const float*, int, long, float*, long, float*, int, hipStream_t);
-void smi_gemm_set_pipe(int, int, int);
+void smi_gemm_set_bm(int);
 int smi_cnn(const CNNArgs*, hipStream_t);
 int smi_cnn_reduce(const CNNArgs*, hipStream_t);
 int smi_gather_rows(const void*, const long long*, void*, long, long, hipStream_t);
@@ -205,7 +205,7 @@ PYBIND11_MODULE(_C, m) {
     chk(smi_splitk_reduce((const float*)slab, splits, n, (float*)out, nb, (float*)bout, accumulate, S(st)),
         "splitk_reduce");
   });
-  m.def("gemm_set_pipe", [](int tpw, int ns, int bm) { smi_gemm_set_pipe(tpw, ns, bm); });
+  m.def("gemm_set_bm", [](int bm) { smi_gemm_set_bm(bm); });
   m.def("gather_rows", [](u src, u idx, u out, long n, long row_bytes, u st) {
     chk(smi_gather_rows(P(src), (const long long*)idx, P(out), n, row_bytes, S(st)), "gather_rows");
   });

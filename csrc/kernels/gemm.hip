@@ -469,202 +469,9 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
 }
 
 
-// ---------------------------------------------------------------------------------------------
-// Cross-tile pipelined variant (FWD / DGRAD, bf16 output, no split-K, K % 64 == 0).
-// A workgroup owns tiles t = blockIdx.x + j * gridDim.x and walks ONE flattened stream of
-// (tile, k-step) items through an NS-deep LDS ring: the first k-steps of tile j+1 are issued
-// before tile j's epilogue, and the epilogue stores straight from the accumulators (no LDS, no
-// barrier), so the stores and the epilogue VALU run while the next tile's DMA is in flight.
-// Stores are widened to 16 B per lane: v_permlane16_swap pairs the 4-column groups of
-// neighbouring 16-column blocks (lanes of 16-lane rows g / g+1), so each lane writes 8
-// consecutive bf16 and each row gets 64 contiguous bytes per store instruction.
-// The counted waits include the epilogue's stores (vmcnt counts loads, stores and LDS-DMA in
-// issue order): S = 2 * FM dwordx4 stores per lane for an interior tile, vmcnt(0) after an
-// edge tile (its scalar tail stores are not counted).
-__device__ __forceinline__ void vm_wait_n(int n) {
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-    case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-
-template <bool BKM, int NS, int FM>
-__global__ __launch_bounds__(256, 2) void gemm_pipe_kernel(GemmArgs g) {
-  constexpr int BMT = 32 * FM;
-  constexpr int NPA = FM;
-  constexpr int A_ELEMS = BMT * BKK;
-  constexpr int STAGE = A_ELEMS + TILE_ELEMS;
-  constexpr int VM1 = NPA + 4;       // DMA instructions per wave per item
-  constexpr int S_EPI = 2 * FM;      // dwordx4 stores per lane, interior tile
-  __shared__ __attribute__((aligned(16))) unsigned short smem[NS * STAGE];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 1, wn = w & 1;
-  const int ntn = (g.N + BN - 1) / BN;
-  const int ntm = (g.M + BMT - 1) / BMT;
-  const int nwg = ntm * ntn;
-  const int nk = g.K / BKK;
-  const int G = gridDim.x;
-  const int my_tiles = (nwg - (int)blockIdx.x + G - 1) / G;
-  const int total = my_tiles * nk;
-  const uint32_t seed = smi_seed(g.seedp, g.salt);
-  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, 0, (int)g.a_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, 0, (int)g.b_bytes, 0x00020000);
-  if (my_tiles <= 0) return;
-
-  // issue side: tile being staged and its per-lane DMA offsets
-  int iss_j = 0, iss_kt = 0;
-  uint32_t voA[NPA], voB[4];
-  {
-    const TileInfo t0 = tile_of(g, blockIdx.x, ntn, nwg, BMT);
-    tile_voffsets<false, NPA>(g.lda, t0.m0, w, lane, voA);
-    tile_voffsets<BKM, 4>(g.ldb, t0.n0, w, lane, voB);
-  }
-  int issued = 0;
-  auto issue_next = [&]() {
-    if (issued >= total) return;
-    if (iss_kt == nk) {  // next tile: recompute the DMA offsets
-      iss_kt = 0;
-      ++iss_j;
-      const TileInfo tn = tile_of(g, blockIdx.x + iss_j * G, ntn, nwg, BMT);
-      tile_voffsets<false, NPA>(g.lda, tn.m0, w, lane, voA);
-      tile_voffsets<BKM, 4>(g.ldb, tn.n0, w, lane, voB);
-    }
-    unsigned short* st = smem + (issued % NS) * STAGE;
-    stage_tile<false, NPA>(rA, g.lda, iss_kt * BKK, voA, st, w);
-    stage_tile<BKM, 4>(rB, g.ldb, iss_kt * BKK, voB, st + A_ELEMS, w);
-    ++iss_kt;
-    ++issued;
-  };
-#pragma unroll
-  for (int s0 = 0; s0 < NS - 1; ++s0) issue_next();
-
-  int last_epi = -1000;      // item index of the most recent epilogue
-  bool last_epi_counted = true;
-  int q = 0;
-  for (int j = 0; j < my_tiles; ++j) {
-    const int t = blockIdx.x + j * G;
-    (void)t;
-    if (j == 0) GSTAMP(0);
-    const TileInfo ti = tile_of(g, blockIdx.x + j * G, ntn, nwg, BMT);
-    const int m0 = ti.m0, n0 = ti.n0;
-    f32x4_t acc[FM][4];
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) acc[i][jj] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < nk; ++kt, ++q) {
-      // VMEM ops younger than item q's DMA: later items already issued + epilogue stores
-      const int later = issued - q - 1;
-      const bool epi_after = last_epi >= q - (NS - 1) && last_epi <= q - 1;
-      if (epi_after && !last_epi_counted) vm_wait_n(0);
-      else vm_wait_n(later * VM1 + (epi_after ? S_EPI : 0));
-      __builtin_amdgcn_s_barrier();
-      if (q == 0) GSTAMP(1);
-      if (q == 1) GSTAMP(2);
-      issue_next();
-      const unsigned short* ta = smem + (q % NS) * STAGE;
-      const unsigned short* tb = ta + A_ELEMS;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8_t af[FM], bf[4];
-#pragma unroll
-        for (int i = 0; i < FM; ++i) af[i] = read_frag<false>(ta, wm * 16 * FM + i * 16, ks, lane);
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) bf[jj] = read_frag<BKM>(tb, wn * 64 + jj * 16, ks, lane);
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj)
-            acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[jj], af[i], acc[i][jj], 0, 0, 0);
-      }
-    }
-    GSTAMP(3);
-    // ---- epilogue straight from registers; the next tile's first items are in flight ----
-    // acc[i][jj][r] = C[m0 + wm*16*FM + i*16 + (lane&15)][n0 + wn*64 + jj*16 + 4*(lane>>4) + r]
-    const int gq = lane >> 4;
-    const bool interior = (m0 + BMT <= g.M) && (n0 + BN <= g.N) && (g.ldc % 8 == 0);
-    last_epi = q - 1;
-    last_epi_counted = interior;
-    if (interior) {
-      uint2 pk[FM][4];
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int col = n0 + wn * 64 + jj * 16 + 4 * gq;
-        float4 bia = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (g.bias) bia = *(const float4*)(g.bias + col);
-        const float bb[4] = {bia.x, bia.y, bia.z, bia.w};
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          const int row = m0 + wm * 16 * FM + i * 16 + (lane & 15);
-          const long cidx = (long)row * g.ldc + col;
-          u16x4_t rs, dy;
-          if (g.resid) rs = *(const u16x4_t*)(g.resid + (long)row * g.ldr + col);
-          if (g.dact_y) dy = *(const u16x4_t*)(g.dact_y + (long)row * g.ldy + col);
-          float o[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float x = acc[i][jj][r] * g.alpha + bb[r];
-            if (g.resid) x += bf2f(rs[r]);
-            if (g.act == 1) x = fmaxf(x, 0.f);
-            if (g.dact_y) x = bf2f(dy[r]) > 0.f ? x * g.dscale : 0.f;
-            else if (g.thresh) x = smi_keep(seed, (uint32_t)(cidx + r), g.thresh) ? x * g.dscale : 0.f;
-            o[r] = x;
-          }
-          pk[i][jj].x = pack2bf(o[0], o[1]);
-          pk[i][jj].y = pack2bf(o[2], o[3]);
-        }
-      }
-      // widen: rows g / g+1 of blocks (jj, jj+1) -> each lane 8 consecutive columns
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int jp = 0; jp < 4; jp += 2) {
-          auto sx = __builtin_amdgcn_permlane16_swap(pk[i][jp].x, pk[i][jp + 1].x, false, false);
-          auto sy = __builtin_amdgcn_permlane16_swap(pk[i][jp].y, pk[i][jp + 1].y, false, false);
-          const uint4 v = make_uint4(sx[0], sy[0], sx[1], sy[1]);
-          const int row = m0 + wm * 16 * FM + i * 16 + (lane & 15);
-          const int col = n0 + wn * 64 + ((gq & 1) ? (jp + 1) * 16 + 4 * (gq - 1) : jp * 16 + 4 * gq);
-          *(uint4*)((unsigned short*)g.C + (long)row * g.ldc + col) = v;
-        }
-    } else {
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int col = n0 + wn * 64 + jj * 16 + 4 * gq;
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          const int row = m0 + wm * 16 * FM + i * 16 + (lane & 15);
-          if (row >= g.M) continue;
-          const long cidx = (long)row * g.ldc + col;
-          for (int r = 0; r < 4; ++r) {
-            if (col + r >= g.N) break;
-            const float bia = g.bias ? g.bias[col + r] : 0.f;
-            ((unsigned short*)g.C)[cidx + r] = f2bf(epi_val(g, acc[i][jj][r], bia, row, col + r, cidx + r, seed));
-          }
-        }
-      }
-    }
-    GSTAMP(4);
-  }
-}
-
-static int g_pipe_tpw = -1, g_pipe_ns = 3, g_bm_force = 0;
-// runtime override of the pipelined-kernel policy (tiles per workgroup, ring depth; tpw 0 = off)
-// and of the tile height (bm 64 / 128; 0 = automatic)
-extern "C" void smi_gemm_set_pipe(int tpw, int ns, int bm) {
-  g_pipe_tpw = tpw;
-  g_pipe_ns = ns;
-  g_bm_force = bm;
-}
+static int g_bm_force = 0;
+// runtime override of the tile height (64 / 128; 0 = automatic) — A/B probes in one process
+extern "C" void smi_gemm_set_bm(int bm) { g_bm_force = bm; }
 
 extern "C" int smi_gemm(const GemmArgs* args, hipStream_t st) {
   GemmArgs g = *args;
@@ -700,29 +507,8 @@ extern "C" int smi_gemm(const GemmArgs* args, hipStream_t st) {
   const int maxg = NUM_CU * (ns == 2 ? (bm == 64 ? 3 : 2) : 1);
   const int grid = ntiles < maxg ? ntiles : maxg;
   const bool atomic = g.out_f32 && g.atomic;
-  // cross-tile pipelined kernel (SMI_GEMM_PIPE=<tiles per workgroup>, 0 = off)
-  if (g_pipe_tpw < 0) {
-    const char* e = getenv("SMI_GEMM_PIPE");
-    g_pipe_tpw = e ? atoi(e) : 0;
-    const char* e2 = getenv("SMI_GEMM_PIPE_NS");
-    g_pipe_ns = e2 ? atoi(e2) : 3;
-  }
-  const int pipe_env = g_pipe_tpw, pipe_ns = g_pipe_ns;
-  if (pipe_env > 0 && g.mode != 2 && !g.out_f32 && g.splits == 1 && g.K % BKK == 0 && g.K / BKK >= 4) {
-    const int nt = ((g.M + bm - 1) / bm) * ((g.N + BN - 1) / BN);
-    int pg = (nt + pipe_env - 1) / pipe_env;
-    if (pg > 2 * NUM_CU) pg = 2 * NUM_CU;
-#define SMI_PIPE_LAUNCH(BKMV, NSV)                                                                              \
-  if (bm == 64) hipLaunchKernelGGL((gemm_pipe_kernel<BKMV, NSV, 2>), dim3(pg), dim3(256), 0, st, g);            \
-  else hipLaunchKernelGGL((gemm_pipe_kernel<BKMV, NSV, 4>), dim3(pg), dim3(256), 0, st, g);
-    if (g.mode == 0) {
-      if (pipe_ns == 2) { SMI_PIPE_LAUNCH(false, 2) } else if (pipe_ns == 4) { SMI_PIPE_LAUNCH(false, 4) } else { SMI_PIPE_LAUNCH(false, 3) }
-    } else {
-      if (pipe_ns == 2) { SMI_PIPE_LAUNCH(true, 2) } else if (pipe_ns == 4) { SMI_PIPE_LAUNCH(true, 4) } else { SMI_PIPE_LAUNCH(true, 3) }
-    }
-#undef SMI_PIPE_LAUNCH
-    SMI_CHECK_LAUNCH();
-  }
+
+
 #define SMI_GEMM_LAUNCH(NSV, FMV)                                                                                         \
   switch (g.mode) {                                                                                                       \
     case 0: hipLaunchKernelGGL((gemm_bf16_kernel<false, false, true, NSV, FMV>), dim3(grid), dim3(256), 0, st, g); break; \

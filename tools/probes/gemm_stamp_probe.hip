@@ -17,12 +17,10 @@ static unsigned short rbf(unsigned& st) {
 }
 
 int main() {
-  struct Sh { int M, N, K, mode, bm, tpw, ns; };
-  std::vector<Sh> shapes = {{8192, 512, 512, 0, 64, 0, 3},  {8192, 512, 512, 0, 64, 1, 3},  {8192, 512, 512, 0, 128, 0, 3},
-                            {8192, 512, 512, 0, 128, 1, 3}, {8192, 512, 512, 0, 128, 1, 4}, {8192, 1536, 512, 0, 64, 0, 3},
-                            {8192, 1536, 512, 0, 64, 1, 3}, {8192, 1536, 512, 0, 128, 1, 4}, {8192, 512, 1024, 0, 64, 0, 3},
-                            {8192, 512, 512, 1, 64, 0, 3}};
-  const size_t maxe = (size_t)8192 * 2048;
+  struct Sh { int M, N, K, mode, bm; };
+  std::vector<Sh> shapes = {{8192, 512, 512, 0, 64},  {8192, 512, 512, 0, 128}, {8192, 1536, 512, 0, 64},
+                            {8192, 1536, 512, 0, 128}, {8192, 512, 1024, 0, 64}, {8192, 512, 512, 1, 64}};
+  const size_t maxe = (size_t)8192 * 10240;
   unsigned short *A, *B, *C;
   (void)hipMalloc(&A, maxe * 2); (void)hipMalloc(&B, maxe * 2); (void)hipMalloc(&C, maxe * 2);
   std::vector<unsigned short> h(maxe);
@@ -40,7 +38,7 @@ int main() {
     g.mode = sh.mode; g.alpha = 1.f; g.dscale = 1.f; g.splits = 1;
     g.A = A; g.lda = sh.K; g.B = B; g.ldb = sh.mode == 0 ? sh.K : sh.N; g.M = sh.M; g.N = sh.N; g.K = sh.K;
     g.C = C; g.ldc = sh.N;
-    smi_gemm_set_pipe(sh.tpw, sh.ns, sh.bm);
+    smi_gemm_set_bm(sh.bm);
     for (int i = 0; i < 30; ++i) smi_gemm(&g, 0);  // warm, clocks up
     (void)hipMemset(stamps, 0, maxwg * 64);
     (void)hipDeviceSynchronize();
@@ -52,7 +50,7 @@ int main() {
     unsigned long long t0 = ~0ull, tend = 0;
     for (int b = 0; b < maxwg; ++b)
       if (hs[b * 8]) { ++nwg; t0 = std::min(t0, hs[b * 8]); tend = std::max(tend, hs[b * 8 + 4]); }
-    printf("M%d N%d K%d mode%d bm%d pipe%d ns%d: %d WGs, first-tile span %.2f us\n", sh.M, sh.N, sh.K, sh.mode, sh.bm, sh.tpw, sh.ns, nwg,
+    printf("M%d N%d K%d mode%d bm%d: %d WGs, first-tile span %.2f us\n", sh.M, sh.N, sh.K, sh.mode, sh.bm, nwg,
            (tend - t0) / 100.0);
     const char* names[5] = {"start", "kt0 landed", "kt1 landed", "kloop end", "epi end"};
     for (int p = 0; p < 5; ++p) {
