@@ -294,6 +294,26 @@ class Transformer(nn.Module):
         logits = self(src, dec_in, None, la, la)
         return self.loss(logits, target)
 
+    def training_step_split(self, src, tgt, shift_targets=False):
+        """The same loss with the autograd graph cut at the encoder output, for a backward in two
+        segments (``StepRunner(split_fn=...)``): returns ``(loss, enc_leaf, enc)`` where the
+        decoder consumed ``enc_leaf`` (a detached leaf of ``enc``).  ``loss.backward()`` then
+        finishes every decoder / vocab-projection gradient and leaves d(enc) in
+        ``enc_leaf.grad``; ``enc.backward(enc_leaf.grad)`` runs the encoder's backward.  A
+        data-parallel step all-reduces the decoder's gradient buckets while the encoder
+        backward runs."""
+        if shift_targets:
+            dec_in, target = tgt[:, :-1], tgt[:, 1:]
+        else:
+            dec_in, target = tgt, tgt
+        la = torch.ones(1, dtype=torch.bool)
+        enc_mode, self_mode, cross_mode, kp = self._modes(src, None, la, la)
+        enc = self.encoder(src, enc_mode, kp)
+        enc_leaf = enc.detach().requires_grad_()
+        out = self.decoder(enc_leaf, dec_in, self_mode, cross_mode, kp)
+        logits = linear(out, self.linear.weight, self.linear.bias)
+        return self.loss(logits, target), enc_leaf, enc
+
 
 def create_look_ahead_mask(size):
     """pytorch_machine_translator.py:102-104."""

@@ -33,13 +33,29 @@ class DataParallel:
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.overlap = overlap
+        self._limit = int(bucket_mb * (1 << 20) / 4)
+        self._build_buckets()
+        self._pending = None
+        self._works = []
+        self._listener = None
+        if self.world > 1:
+            if broadcast:
+                broadcast_flat(flat, 0, group)
+            if overlap:
+                self._listener = _grad.add_listener(self._on_ready)
+        self.reset()
+
+    def _build_buckets(self, cuts=()):
+        """Contiguous buckets of <= bucket_mb over the flat gradient buffer; a bucket never spans
+        one of the parameter indices in ``cuts`` (a new bucket starts there)."""
+        flat = self.flat
         self.buckets = []  # (start, end, param indices)
-        limit = int(bucket_mb * (1 << 20) / 4)
+        cut_set = set(cuts)
         cur, start = [], 0
         for i, p in enumerate(flat.params):
             s = flat.offsets[i]
             e = flat.offsets[i + 1] if i + 1 < len(flat.params) else flat.numel
-            if cur and (e - start) > limit:
+            if cur and ((e - start) > self._limit or i in cut_set):
                 self.buckets.append((start, s, cur))
                 cur, start = [], s
             cur.append(i)
@@ -49,14 +65,13 @@ class DataParallel:
         for b, (_, _, idx) in enumerate(self.buckets):
             for i in idx:
                 self.bucket_of[i] = b
-        self._pending = None
-        self._works = []
-        self._listener = None
-        if self.world > 1:
-            if broadcast:
-                broadcast_flat(flat, 0, group)
-            if overlap:
-                self._listener = _grad.add_listener(self._on_ready)
+
+    def align_buckets(self, ready_ids):
+        """Re-cut the buckets so none mixes parameters in ``ready_ids`` (a set of id(param): the
+        gradients final after the first backward segment) with the others."""
+        inside = [id(p) in ready_ids for p in self.flat.params]
+        cuts = [i for i in range(1, len(inside)) if inside[i] != inside[i - 1]]
+        self._build_buckets(cuts)
         self.reset()
 
     def set_overlap(self, on):
@@ -82,6 +97,15 @@ class DataParallel:
             _grad.join(self.flat.grad.device.index)  # weight grads may still be in flight on the side stream
         w = dist.all_reduce(self.flat.grad[s:e], group=self.group, async_op=True)
         self._works.append(w)
+
+    def launch(self, b):
+        """Start bucket ``b``'s all-reduce now (idempotent within a step)."""
+        self._launch(b)
+
+    def complete_buckets(self, ready_ids):
+        """Indices of the buckets whose parameters are all in ``ready_ids`` (a set of id(param))."""
+        return [b for b, (_, _, idx) in enumerate(self.buckets)
+                if all(id(self.flat.params[i]) in ready_ids for i in idx)]
 
     def _on_ready(self, p):
         i = self.flat.index.get(id(p))

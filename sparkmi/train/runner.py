@@ -11,6 +11,12 @@ device buffers before each replay.
     all-reduced by RCCL (a few large collectives over the flat buffer) and the optimizer runs
     as one launch.  Collectives stay outside the graph, so no RCCL-in-capture dependency;
     eager data-parallel steps instead overlap the bucket all-reduces with backward.
+  * data-parallel with ``split_fn`` (a loss whose autograd graph is cut in two, e.g.
+    Transformer.training_step_split at the encoder output): the step is TWO graphs — G1 =
+    forward + backward of the upper segment (decoder + vocab projection), G2 = backward of the
+    lower segment (encoder).  Buckets whose parameters all became final inside G1 are
+    all-reduced on RCCL's stream while G2 replays, so most of the gradient traffic hides under
+    the encoder backward; the rest is reduced after G2.  Still no collective inside a graph.
 """
 import torch
 
@@ -18,9 +24,13 @@ from ..ops import _grad
 
 
 class StepRunner:
-    def __init__(self, model, loss_fn, optimizer, ddp=None, graph=False, warmup_eager=3):
+    def __init__(self, model, loss_fn, optimizer, ddp=None, graph=False, warmup_eager=3, split_fn=None):
         self.model = model
         self.loss_fn = loss_fn          # loss_fn(model, *batch) -> scalar loss tensor
+        self.split_fn = split_fn        # split_fn(model, *batch) -> (loss, leaf, root), see module doc
+        self.graph2 = None
+        self.early_buckets = []
+        self._split_keep = None
         self.opt = optimizer
         self.ddp = ddp
         self.graph_requested = graph
@@ -52,6 +62,40 @@ class StepRunner:
         self.opt.step()
         return loss
 
+    def _fwd_bwd_split(self, *batch):
+        rng = getattr(self.model, "rng", None)
+        if rng is not None:
+            rng.advance()
+        loss, leaf, root = self.split_fn(self.model, *batch)
+        loss.backward()
+        _grad.join()
+        return loss.detach(), leaf, root
+
+    def _capture_split(self):
+        """G1 = forward + upper backward, G2 = lower backward (shares G1's memory pool); records
+        which gradient buckets are final after G1."""
+        ready = set()
+        listener = _grad.add_listener(lambda p: ready.add(id(p)))
+        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(g1):
+                self.static_loss, leaf, root = self._fwd_bwd_split(*self.static_in)
+        finally:
+            _grad.remove_listener(listener)
+        late = set()
+        listener = _grad.add_listener(lambda p: late.add(id(p)))
+        try:
+            with torch.cuda.graph(g2, pool=g1.pool()):
+                root.backward(leaf.grad)
+                _grad.join()
+        finally:
+            _grad.remove_listener(listener)
+        ready -= late  # a gradient also accumulated in the lower segment is not final after G1
+        self._split_keep = (leaf, root)  # G2 reads leaf.grad / root's saved tensors at fixed addresses
+        self.graph, self.graph2 = g1, g2
+        self.ddp.align_buckets(ready)
+        self.early_buckets = self.ddp.complete_buckets(ready)
+
     def _capture(self, batch):
         """Record one step into a HIP graph.  Capture only records (nothing executes), so no
         extra optimizer updates happen here: the ``warmup_eager`` eager steps before it already
@@ -60,6 +104,10 @@ class StepRunner:
         self.static_in = [b.clone() for b in batch]
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
+        if self._dp and self.split_fn is not None:
+            self.ddp.set_overlap(False)
+            self._capture_split()
+            return
         if self._dp:
             self.ddp.set_overlap(False)  # no collective may be enqueued during capture
             with torch.cuda.graph(g):
@@ -79,6 +127,10 @@ class StepRunner:
         for dst, src in zip(self.static_in, batch):
             dst.copy_(src, non_blocking=True)
         self.graph.replay()
+        if self.graph2 is not None:
+            for b in self.early_buckets:   # decoder buckets: RCCL runs under the encoder backward
+                self.ddp.launch(b)
+            self.graph2.replay()
         if self._dp:
             self.ddp.finish()   # bucketed RCCL all-reduce of the flat gradient buffer
             self.opt.step()

@@ -14,7 +14,7 @@ from sparkmi.runtime.launcher import launch
 cloudpickle.register_pickle_by_value(sys.modules[__name__])
 
 
-def _train(graph, steps):
+def _train(graph, steps, split=False):
     import torch
     import torch.distributed as dist
     from sparkmi.models.transformer import Transformer
@@ -29,7 +29,9 @@ def _train(graph, steps):
     flat = FlatParams(m)
     opt = SGD(flat, lr=0.05)  # linear in the gradients: no amplification of last-bit noise
     ddp = DataParallel(flat, bucket_mb=0.5)
-    runner = StepRunner(m, lambda mm, s, t: mm.training_step_loss(s, t), opt, ddp, graph=graph, warmup_eager=2)
+    split_fn = (lambda mm, s, t: mm.training_step_split(s, t)) if split else None
+    runner = StepRunner(m, lambda mm, s, t: mm.training_step_loss(s, t), opt, ddp, graph=graph, warmup_eager=2,
+                        split_fn=split_fn)
     g = torch.Generator().manual_seed(1)
     data = torch.randint(4, 300, (steps, 2, 8, 64), generator=g).to(device)
     for i in range(steps):
@@ -39,13 +41,28 @@ def _train(graph, steps):
     ref = p.clone()
     dist.broadcast(ref, 0)
     synced = bool(torch.equal(ref, p))
-    return p.cpu(), synced
+    info = (len(runner.early_buckets), len(ddp.buckets)) if split else None
+    return p.cpu(), synced, info
 
 
 @pytest.mark.gpu
 def test_graph_dp_matches_eager_dp():
     env = {"SPARKMI_DIST_BACKEND": "gloo", "SPARKMI_GEMM_POLICY": "smi"}  # same kernels in both runs
-    pg, sg = launch(_train, (True, 6), {}, num_processes=2, use_gpu=True, env=env, log_sink=None, timeout=300)
-    pe, se = launch(_train, (False, 6), {}, num_processes=2, use_gpu=True, env=env, log_sink=None, timeout=300)
+    pg, sg, _ = launch(_train, (True, 6), {}, num_processes=2, use_gpu=True, env=env, log_sink=None, timeout=300)
+    pe, se, _ = launch(_train, (False, 6), {}, num_processes=2, use_gpu=True, env=env, log_sink=None, timeout=300)
     assert sg and se
     torch.testing.assert_close(pg, pe, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_split_graph_dp_matches_eager_dp():
+    """Two-graph step (decoder backward, then encoder backward with the decoder's buckets
+    all-reduced in between) == eager DP."""
+    env = {"SPARKMI_DIST_BACKEND": "gloo", "SPARKMI_GEMM_POLICY": "smi"}
+    ps, ss, info = launch(_train, (True, 6, True), {}, num_processes=2, use_gpu=True, env=env, log_sink=None,
+                          timeout=300)
+    pe, se, _ = launch(_train, (False, 6), {}, num_processes=2, use_gpu=True, env=env, log_sink=None, timeout=300)
+    assert ss and se
+    early, total = info
+    assert 0 < early < total, info
+    torch.testing.assert_close(ps, pe, rtol=1e-4, atol=1e-5)
