@@ -143,15 +143,31 @@ __device__ __forceinline__ bf16x8_t read_frag(const unsigned short* tile, int r0
   }
 }
 
+// Epilogue feature set.  EPI >= 0: a compile-time bitmask (the kernel is specialised: no
+// runtime tests, no speculatively computed dropout hash per element); EPI < 0: generic (runtime
+// tests on the argument block).  Measured: the generic epilogue of a 64 x 128 tile issued ~1200
+// instructions per wave (if-converted dropout hash and per-element flag selects) = 2-4 us per
+// tile, a third of a K = 512 GEMM (tools/probes/gemm_stamp_probe.hip).
+enum : int { EPI_BIAS = 1, EPI_RESID = 2, EPI_RELU = 4, EPI_DACT = 8, EPI_DROP = 16 };
+struct EpiFlags {
+  bool bias, resid, relu, dact, drop;
+};
+template <int EPI>
+__device__ __forceinline__ EpiFlags epi_flags(const GemmArgs& g) {
+  if constexpr (EPI < 0) return EpiFlags{g.bias != nullptr, g.resid != nullptr, g.act == 1, g.dact_y != nullptr, g.thresh != 0};
+  else return EpiFlags{(EPI & EPI_BIAS) != 0, (EPI & EPI_RESID) != 0, (EPI & EPI_RELU) != 0, (EPI & EPI_DACT) != 0,
+                       (EPI & EPI_DROP) != 0};
+}
+
 // epilogue value transform for bf16 outputs
-__device__ __forceinline__ float epi_val(const GemmArgs& g, float v, float bia, int row, int col, long cidx,
-                                         uint32_t seed) {
+__device__ __forceinline__ float epi_val(const GemmArgs& g, const EpiFlags& f, float v, float bia, int row, int col,
+                                         long cidx, uint32_t seed) {
   v = v * g.alpha + bia;
-  if (g.resid) v += bf2f(g.resid[(long)row * g.ldr + col]);
-  if (g.act == 1) v = fmaxf(v, 0.f);
-  if (g.dact_y) {  // backward of relu+dropout: y > 0 <=> kept and positive
+  if (f.resid) v += bf2f(g.resid[(long)row * g.ldr + col]);
+  if (f.relu) v = fmaxf(v, 0.f);
+  if (f.dact) {  // backward of relu+dropout: y > 0 <=> kept and positive
     v = bf2f(g.dact_y[(long)row * g.ldy + col]) > 0.f ? v * g.dscale : 0.f;
-  } else if (g.thresh) {
+  } else if (f.drop) {
     v = smi_keep(seed, (uint32_t)cidx, g.thresh) ? v * g.dscale : 0.f;
   }
   return v;
@@ -187,7 +203,7 @@ __device__ __forceinline__ TileInfo tile_of(const GemmArgs& g, int t, int ntn, i
 // FM = 16-row A fragments per wave: 4 -> 128 x 128 tiles, 2 -> 64 x 128 tiles (twice the
 // workgroups for the transformer's N = 512 GEMMs, so two tiles share a CU and one's load /
 // store phases overlap the other's MFMAs).  A k-major A operand (wgrad) always uses FM = 4.
-template <bool AK, bool BKM, bool SWAP, int NS, int FM>
+template <bool AK, bool BKM, bool SWAP, int NS, int FM, int EPI>
 __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_bf16_kernel(GemmArgs g) {
   constexpr int BMT = 32 * FM;                 // tile rows (M)
   constexpr int NPA = AK ? 4 : FM;             // DMA pieces per wave per stage, A operand
@@ -205,6 +221,7 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
   const int total_tiles = nwg * g.splits;
   const bool ragged = (g.K % BKK) != 0 || (g.K % g.k_per_split) != 0;
   const uint32_t seed = smi_seed(g.seedp, g.salt);
+  const EpiFlags ef = epi_flags<EPI>(g);
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, 0, (int)g.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, 0, (int)g.b_bytes, 0x00020000);
 
@@ -309,7 +326,7 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
     }
     if (false) {
 #else
-    const bool vec8 = (g.N % 8 == 0) && (g.ldc % 8 == 0) && (!g.resid || g.ldr % 8 == 0) && (!g.dact_y || g.ldy % 8 == 0);
+    const bool vec8 = (g.N % 8 == 0) && (g.ldc % 8 == 0) && (!ef.resid || g.ldr % 8 == 0) && (!ef.dact || g.ldy % 8 == 0);
     if (SWAP && !g.out_f32 && vec8) {
       // LDS-staged bf16 epilogue.  Each wave parks its 64x64 fp32 sub-tile in its own 16 KiB of the
       // (now idle) staging LDS — 16-B chunk c of row r at c ^ (r & 15), conflict-free for both
@@ -317,6 +334,7 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
       // mask operands are 16-B loads and each store instruction writes 8 full 128-B row segments
       // (the direct form wrote 32-B pieces of 16 rows).
       __syncthreads();  // every wave is done reading the k-loop's staging buffers
+      GSTAMP(5);
       float* ep = (float*)smem + w * (FM * 16 * 64);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -326,12 +344,13 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
           *(f32x4_t*)(ep + r * 64 + ((c ^ (r & 15)) << 2)) = acc[i][j];
         }
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are done
+      GSTAMP(6);
       const int q = lane & 7;               // 8-column group of this lane
       const int col = n0 + wn * 64 + q * 8;
       float bb[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) bb[e] = 0.f;
-      if (g.bias && col < g.N) {
+      if (ef.bias && col < g.N) {
         const float4 b0 = *(const float4*)(g.bias + col), b1 = *(const float4*)(g.bias + col + 4);
         bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w; bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
       }
@@ -351,24 +370,29 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
         float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         const long cidx = (long)rowc * g.ldc + colc;
         u16x8_t rs, dy;
-        if (g.resid) rs = *(const u16x8_t*)(g.resid + (long)rowc * g.ldr + colc);
-        if (g.dact_y) dy = *(const u16x8_t*)(g.dact_y + (long)rowc * g.ldy + colc);
+        if (ef.resid) rs = *(const u16x8_t*)(g.resid + (long)rowc * g.ldr + colc);
+        if (ef.dact) dy = *(const u16x8_t*)(g.dact_y + (long)rowc * g.ldy + colc);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           float x = v[e] * g.alpha + bb[e];
-          if (g.resid) x += bf2f(rs[e]);
-          if (g.act == 1) x = fmaxf(x, 0.f);
-          if (g.dact_y) x = bf2f(dy[e]) > 0.f ? x * g.dscale : 0.f;
-          else if (g.thresh) x = smi_keep(seed, (uint32_t)(cidx + e), g.thresh) ? x * g.dscale : 0.f;
+          if (ef.resid) x += bf2f(rs[e]);
+          if (ef.relu) x = fmaxf(x, 0.f);
+          if (ef.dact) x = bf2f(dy[e]) > 0.f ? x * g.dscale : 0.f;
+          else if (ef.drop) x = smi_keep(seed, (uint32_t)(cidx + e), g.thresh) ? x * g.dscale : 0.f;
           v[e] = x;
         }
         pk[it].x = pack2bf(v[0], v[1]); pk[it].y = pack2bf(v[2], v[3]);
         pk[it].z = pack2bf(v[4], v[5]); pk[it].w = pack2bf(v[6], v[7]);
       }
+      GSTAMP(7);
 #pragma unroll
       for (int it = 0; it < 2 * FM; ++it) {
         const int row = m0 + wm * 16 * FM + it * 8 + (lane >> 3);
+#if defined(GEMM_PROBE_NOSTORE)
+        if (ok[it] && pk[it].x == 0x12345678u) *(uint4*)((unsigned short*)g.C + (long)row * g.ldc + col) = pk[it];
+#else
         if (ok[it]) *(uint4*)((unsigned short*)g.C + (long)row * g.ldc + col) = pk[it];
+#endif
       }
     } else if (SWAP) {
 #endif
@@ -379,8 +403,8 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
       for (int j = 0; j < 4; ++j) {
         const int col = n0 + wn * 64 + j * 16 + cl;
         float4 bia = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (g.bias && (interior || col + 3 < g.N)) bia = *(const float4*)(g.bias + col);
-        else if (g.bias) {
+        if (ef.bias && (interior || col + 3 < g.N)) bia = *(const float4*)(g.bias + col);
+        else if (ef.bias) {
           if (col < g.N) bia.x = g.bias[col];
           if (col + 1 < g.N) bia.y = g.bias[col + 1];
           if (col + 2 < g.N) bia.z = g.bias[col + 2];
@@ -405,7 +429,7 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
           } else if (interior || (row < g.M && col + 3 < g.N)) {
             float o[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = epi_val(g, acc[i][j][r], bb[r], row, col + r, cidx + r, seed);
+            for (int r = 0; r < 4; ++r) o[r] = epi_val(g, ef, acc[i][j][r], bb[r], row, col + r, cidx + r, seed);
             uint2 pk;
             pk.x = pack2bf(o[0], o[1]);
             pk.y = pack2bf(o[2], o[3]);
@@ -413,7 +437,7 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
           } else if (row < g.M) {
             for (int r = 0; r < 4; ++r)
               if (col + r < g.N)
-                ((unsigned short*)g.C)[cidx + r] = f2bf(epi_val(g, acc[i][j][r], bb[r], row, col + r, cidx + r, seed));
+                ((unsigned short*)g.C)[cidx + r] = f2bf(epi_val(g, ef, acc[i][j][r], bb[r], row, col + r, cidx + r, seed));
           }
         }
       }
@@ -509,19 +533,36 @@ extern "C" int smi_gemm(const GemmArgs* args, hipStream_t st) {
   const bool atomic = g.out_f32 && g.atomic;
 
 
-#define SMI_GEMM_LAUNCH(NSV, FMV)                                                                                         \
-  switch (g.mode) {                                                                                                       \
-    case 0: hipLaunchKernelGGL((gemm_bf16_kernel<false, false, true, NSV, FMV>), dim3(grid), dim3(256), 0, st, g); break; \
-    case 1: hipLaunchKernelGGL((gemm_bf16_kernel<false, true, true, NSV, FMV>), dim3(grid), dim3(256), 0, st, g); break;  \
-    default: return -1;                                                                                                   \
+  const int epi = (g.bias ? EPI_BIAS : 0) | (g.resid ? EPI_RESID : 0) | (g.act == 1 ? EPI_RELU : 0) |
+                  (g.dact_y ? EPI_DACT : 0) | (!g.dact_y && g.thresh ? EPI_DROP : 0);
+#define SMI_K(MODEB, NSV, FMV, E) hipLaunchKernelGGL((gemm_bf16_kernel<false, MODEB, true, NSV, FMV, E>), dim3(grid), dim3(256), 0, st, g)
+  // specialised epilogues for the feature sets the models use; anything else -> generic (-1)
+#define SMI_GEMM_LAUNCH(NSV, FMV)                                                            \
+  if (g.mode == 0) {                                                                         \
+    switch (epi) {                                                                           \
+      case 0: SMI_K(false, NSV, FMV, 0); break;                                              \
+      case EPI_BIAS: SMI_K(false, NSV, FMV, EPI_BIAS); break;                                \
+      case EPI_BIAS | EPI_RELU: SMI_K(false, NSV, FMV, EPI_BIAS | EPI_RELU); break;          \
+      case EPI_BIAS | EPI_RELU | EPI_DROP: SMI_K(false, NSV, FMV, EPI_BIAS | EPI_RELU | EPI_DROP); break; \
+      default: SMI_K(false, NSV, FMV, -1); break;                                            \
+    }                                                                                        \
+  } else if (g.mode == 1) {                                                                  \
+    switch (epi) {                                                                           \
+      case 0: SMI_K(true, NSV, FMV, 0); break;                                               \
+      case EPI_RESID: SMI_K(true, NSV, FMV, EPI_RESID); break;                               \
+      case EPI_DACT: SMI_K(true, NSV, FMV, EPI_DACT); break;                                 \
+      default: SMI_K(true, NSV, FMV, -1); break;                                             \
+    }                                                                                        \
+  } else {                                                                                   \
+    return -1;                                                                               \
   }
   if (g.mode == 2) {
     if (ns == 4) {
-      if (atomic) hipLaunchKernelGGL((gemm_bf16_kernel<true, true, false, 4, 4>), dim3(grid), dim3(256), 0, st, g);
-      else hipLaunchKernelGGL((gemm_bf16_kernel<true, true, true, 4, 4>), dim3(grid), dim3(256), 0, st, g);
+      if (atomic) hipLaunchKernelGGL((gemm_bf16_kernel<true, true, false, 4, 4, 0>), dim3(grid), dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((gemm_bf16_kernel<true, true, true, 4, 4, 0>), dim3(grid), dim3(256), 0, st, g);
     } else {
-      if (atomic) hipLaunchKernelGGL((gemm_bf16_kernel<true, true, false, 2, 4>), dim3(grid), dim3(256), 0, st, g);
-      else hipLaunchKernelGGL((gemm_bf16_kernel<true, true, true, 2, 4>), dim3(grid), dim3(256), 0, st, g);
+      if (atomic) hipLaunchKernelGGL((gemm_bf16_kernel<true, true, false, 2, 4, 0>), dim3(grid), dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((gemm_bf16_kernel<true, true, true, 2, 4, 0>), dim3(grid), dim3(256), 0, st, g);
     }
   } else if (ns == 4) {
     if (bm == 64) { SMI_GEMM_LAUNCH(4, 2) } else { SMI_GEMM_LAUNCH(4, 4) }
@@ -529,6 +570,7 @@ extern "C" int smi_gemm(const GemmArgs* args, hipStream_t st) {
     if (bm == 64) { SMI_GEMM_LAUNCH(2, 2) } else { SMI_GEMM_LAUNCH(2, 4) }
   }
 #undef SMI_GEMM_LAUNCH
+#undef SMI_K
   SMI_CHECK_LAUNCH();
 }
 
