@@ -129,17 +129,18 @@ __device__ __forceinline__ bf16x8_t read_frag(const unsigned short* tile, int r0
   } else {
     const int q = (lane & 15) >> 2, p = lane & 3, g = lane >> 4;
     const int col = r0 + 4 * p;
-    bf16x8_t out;
+    s16x4_t v[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int kr = ks * 32 + 8 * g + 4 * h + q;
       const int c = col >> 3;
       const int pc = c ^ (kmaj_s(kr) << 1);
       const unsigned short* addr = tile + kr * 128 + pc * 8 + (col & 7);
-      s16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)addr);
-      out[4 * h + 0] = v[0]; out[4 * h + 1] = v[1]; out[4 * h + 2] = v[2]; out[4 * h + 3] = v[3];
+      v[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)addr);
     }
-    return out;
+    // concatenate as one vector op so the two 64-bit reads can land in adjacent registers
+    // (element-wise assembly left ~60 v_mov per k-step in the weight-gradient loop)
+    return __builtin_shufflevector(v[0], v[1], 0, 1, 2, 3, 4, 5, 6, 7);
   }
 }
 
@@ -204,7 +205,7 @@ __device__ __forceinline__ TileInfo tile_of(const GemmArgs& g, int t, int ntn, i
 // workgroups for the transformer's N = 512 GEMMs, so two tiles share a CU and one's load /
 // store phases overlap the other's MFMAs).  A k-major A operand (wgrad) always uses FM = 4.
 template <bool AK, bool BKM, bool SWAP, int NS, int FM, int EPI>
-__global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_bf16_kernel(GemmArgs g) {
+__global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : (NS == 3 && FM == 2 ? 2 : 1))) void gemm_bf16_kernel(GemmArgs g) {
   constexpr int BMT = 32 * FM;                 // tile rows (M)
   constexpr int NPA = AK ? 4 : FM;             // DMA pieces per wave per stage, A operand
   constexpr int A_ELEMS = BMT * BKK;
@@ -273,6 +274,21 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
           __syncthreads();
         }
       }
+      // Read BOTH k-substeps' fragments of this stage before issuing the next stage's DMA:
+      // hipcc orders an LDS-DMA before any later ds_read_b64_tr_b16 builtin with vmcnt(0) (it
+      // cannot prove they touch different stages), which made every DGRAD / WGRAD k-step wait
+      // for the DMA it had just issued.  Reads first, DMA second, MFMAs last keeps the DMA of
+      // step kt+NS-1 in flight under this step's MFMAs.
+      const unsigned short* ta = smem + rd * STAGE;
+      const unsigned short* tb = ta + A_ELEMS;
+      bf16x8_t af[2][FM], bf[2][4];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[ks][i] = read_frag<AK>(ta, wm * 16 * FM + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf[ks][j] = read_frag<BKM>(tb, wn * 64 + j * 16, ks, lane);
+      }
       if (kt + NS - 1 < nk) {
         int ws = rd + NS - 1;
         if (ws >= NS) ws -= NS;
@@ -280,24 +296,17 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
         stage_tile<AK, NPA>(rA, g.lda, ti.kbeg + (kt + NS - 1) * BKK, voA, st, w);
         stage_tile<BKM, 4>(rB, g.ldb, ti.kbeg + (kt + NS - 1) * BKK, voB, st + A_ELEMS, w);
       }
-      const unsigned short* ta = smem + rd * STAGE;
-      const unsigned short* tb = ta + A_ELEMS;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        bf16x8_t af[FM], bf[4];
-#pragma unroll
-        for (int i = 0; i < FM; ++i) af[i] = read_frag<AK>(ta, wm * 16 * FM + i * 16, ks, lane);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bf[j] = read_frag<BKM>(tb, wn * 64 + j * 16, ks, lane);
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
 #ifdef GEMM_PROBE_NOMFMA
-            acc[i][j][0] += (float)af[i][0] + (float)bf[j][0];
+            acc[i][j][0] += (float)af[ks][i][0] + (float)bf[ks][j][0];
 #else
-            if (SWAP) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
-            else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+            if (SWAP) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
+            else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bf[ks][j], acc[i][j], 0, 0, 0);
 #endif
           }
         if (AK && do_bias) {
@@ -306,8 +315,8 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : 1)) void gemm_b
           for (int e = 0; e < 8; ++e) ones[e] = (short)0x3F80;  // bf16 1.0
 #pragma unroll
           for (int i = 0; i < FM; ++i) {
-            if (SWAP) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[i], accb[i], 0, 0, 0);
-            else accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, accb[i], 0, 0, 0);
+            if (SWAP) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[ks][i], accb[i], 0, 0, 0);
+            else accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], ones, accb[i], 0, 0, 0);
           }
         }
       }
@@ -527,8 +536,15 @@ extern "C" int smi_gemm(const GemmArgs* args, hipStream_t st) {
   if (!ak && (g_bm_force == 64 || g_bm_force == 128)) bm = g_bm_force;
   const int ntiles = ((g.M + bm - 1) / bm) * ((g.N + BN - 1) / BN) * g.splits;
   // pipeline depth: NS=2 (two workgroups per CU) or NS=4 (one per CU, three k-steps in flight)
-  const int ns = ns_env == 2 || ns_env == 4 ? ns_env : GEMM_NS;
-  const int maxg = NUM_CU * (ns == 2 ? (bm == 64 ? 3 : 2) : 1);
+  // ring depth: 2 stages (2-3 WGs per CU) everywhere by default — measured: 3 or 4 stages
+  // (fewer WGs per CU) were 3-5 % slower per step, for WGRAD too (SMI_GEMM_WGRAD_NS=4 / SMI_GEMM_NS).
+  static int wns_env = -1;
+  if (wns_env < 0) {
+    const char* e = getenv("SMI_GEMM_WGRAD_NS");
+    wns_env = e ? atoi(e) : 2;
+  }
+  const int ns = ak ? (wns_env == 4 ? 4 : 2) : (ns_env >= 2 && ns_env <= 4 ? ns_env : GEMM_NS);
+  const int maxg = NUM_CU * (ns == 2 ? (bm == 64 ? 3 : 2) : (ns == 3 && bm == 64 ? 2 : 1));
   const int grid = ntiles < maxg ? ntiles : maxg;
   const bool atomic = g.out_f32 && g.atomic;
 
@@ -566,6 +582,8 @@ extern "C" int smi_gemm(const GemmArgs* args, hipStream_t st) {
     }
   } else if (ns == 4) {
     if (bm == 64) { SMI_GEMM_LAUNCH(4, 2) } else { SMI_GEMM_LAUNCH(4, 4) }
+  } else if (ns == 3) {
+    if (bm == 64) { SMI_GEMM_LAUNCH(3, 2) } else { SMI_GEMM_LAUNCH(3, 4) }
   } else {
     if (bm == 64) { SMI_GEMM_LAUNCH(2, 2) } else { SMI_GEMM_LAUNCH(2, 4) }
   }
