@@ -70,15 +70,16 @@ typedef __attribute__((ext_vector_type(4))) short s16x4_t;
 __device__ __forceinline__ bf16x8_t frag_tr(const unsigned short* img, int krow0, int col0, int lane) {
   const int q = (lane & 15) >> 2, p = lane & 3, g = lane >> 4;
   const int col = col0 + 4 * p;
-  bf16x8_t out;
+  s16x4_t v[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int row = krow0 + 16 * h + 4 * g + q;
     const unsigned short* addr = img + row * 64 + (((col >> 3) ^ (row & 7)) << 3) + (col & 7);
-    const s16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)addr);
-    out[4 * h + 0] = v[0]; out[4 * h + 1] = v[1]; out[4 * h + 2] = v[2]; out[4 * h + 3] = v[3];
+    v[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)addr);
   }
-  return out;
+  // one vector concatenation: the two 64-bit reads can land in adjacent registers (element-wise
+  // assembly costs v_mov per element, as measured in the GEMM k-loop)
+  return __builtin_shufflevector(v[0], v[1], 0, 1, 2, 3, 4, 5, 6, 7);
 }
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 __device__ __forceinline__ bf16x8_t pack_acc(const f32x4_t& a, const f32x4_t& b) {
