@@ -18,4 +18,6 @@ struct AttnBwdArgs {
   const unsigned char* kpad;
   int B, H, Sq, Sk, mode;
   float scale_log2, scale;    // scale = 1/sqrt(head_dim)
+  const unsigned short* o;    // forward output (O's layout): the dQ kernel computes delta = rowsum(dO*O)
+  float* delta_out;           // ... and writes it here for the dK/dV kernel
 };

@@ -273,29 +273,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
   }
 }
 
-// delta[b,h,q] = sum_d dO * O
-__global__ void attn_delta_kernel(const unsigned short* __restrict__ o, const unsigned short* __restrict__ dout,
-                                  long o_sb, long o_ss, long o_sh, float* __restrict__ delta, int B, int H, int Sq) {
-  const int lane = threadIdx.x & 63;
-  const long wg = (long)blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per (b, q, head-group of 8)
-  const int hg_n = (H + 7) / 8;
-  if (wg >= (long)B * Sq * hg_n) return;
-  const int hg = wg % hg_n;
-  const int q = (wg / hg_n) % Sq;
-  const int b = wg / ((long)hg_n * Sq);
-  const int h = hg * 8 + (lane >> 3);
-  float s = 0.f;
-  if (h < H) {
-    const long off = b * o_sb + (long)q * o_ss + h * o_sh + (lane & 7) * 8;
-    u16x8_t x = *(const u16x8_t*)(o + off);
-    u16x8_t y = *(const u16x8_t*)(dout + off);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s += bf2f(x[j]) * bf2f(y[j]);
-  }
-  s = group_sum<8>(s);
-  if (h < H && (lane & 7) == 0) delta[((long)b * H + h) * Sq + q] = s;
-}
-
 // dQ: workgroup = 4 waves x 32 queries; K/V streamed.  S^T = K Q^T, dP^T = V dO^T,
 // dS^T = P^T o (dP^T - delta), dQ^T += K^T dS^T.
 template <int MODE, bool KPAD>
@@ -317,8 +294,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   Piece2 pk, pv;
   load_chunk(K, a.k_ss, 0, a.Sk, pk);
   load_chunk(V, a.v_ss, 0, a.Sk, pv);
-  bf16x8_t qf[2][2], df[2][2];
+  bf16x8_t qf[2][2], df[2][2], of[2][2];
   float lse[2], dl[2];
+  const unsigned short* Og = a.o + b * a.o_sb + h * a.o_sh;
 #pragma unroll
   for (int qs = 0; qs < 2; ++qs) {
     const int qi = qwave + qs * 16 + n;
@@ -327,9 +305,25 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnBwdArgs a) {
     qf[qs][1] = load8(Q + (long)qi * a.q_ss + 32 + 8 * g, ok);
     df[qs][0] = load8(dO + (long)qi * a.o_ss + 8 * g, ok);
     df[qs][1] = load8(dO + (long)qi * a.o_ss + 32 + 8 * g, ok);
-    const long ri = ((long)b * a.H + h) * a.Sq + qi;
-    lse[qs] = ok ? a.lse[ri] : INFINITY;
-    dl[qs] = ok ? a.delta[ri] : 0.f;
+    of[qs][0] = load8(Og + (long)qi * a.o_ss + 8 * g, ok);
+    of[qs][1] = load8(Og + (long)qi * a.o_ss + 32 + 8 * g, ok);
+    lse[qs] = ok ? a.lse[((long)b * a.H + h) * a.Sq + qi] : INFINITY;
+  }
+  // delta = rowsum(dO * O) for this wave's queries (the four lanes n, n+16, n+32, n+48 hold a
+  // row's 64 values between them); written once for the dK/dV kernel, which runs next
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    float sacc = 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        sacc += bf2f((unsigned short)df[qs][u][j]) * bf2f((unsigned short)of[qs][u][j]);
+    sacc += __shfl_xor(sacc, 16, 64);
+    sacc += __shfl_xor(sacc, 32, 64);
+    dl[qs] = sacc;
+    const int qi = qwave + qs * 16 + n;
+    if (g == 0 && qi < a.Sq) a.delta_out[((long)b * a.H + h) * a.Sq + qi] = sacc;
   }
   store_chunk(Ks[0], pk);
   store_chunk(Vs[0], pv);
@@ -571,10 +565,11 @@ extern "C" int smi_attn_fwd(const AttnFwdArgs* args, hipStream_t st) {
 
 extern "C" int smi_attn_bwd(const AttnBwdArgs* args, const void* o, float* delta, hipStream_t st) {
   const AttnBwdArgs& a = *args;
-  const long waves = (long)a.B * a.Sq * ((a.H + 7) / 8);
-  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st,
-                     (const unsigned short*)o, a.dout, a.o_sb, a.o_ss, a.o_sh, delta, a.B, a.H, a.Sq);
+  // delta = rowsum(dO * O) is computed inside the dQ kernel (it already holds dO's rows) and
+  // handed to the dK/dV kernel through `delta` — no separate launch
   AttnBwdArgs b2 = a;
+  b2.o = (const unsigned short*)o;
+  b2.delta_out = delta;
   b2.delta = delta;
   SMI_ATTN_DISPATCH(attn_bwd_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), b2);
   SMI_ATTN_DISPATCH(attn_bwd_dkdv_kernel, dim3((a.Sk + 127) / 128, a.H, a.B), b2);
