@@ -294,25 +294,35 @@ class Transformer(nn.Module):
         logits = self(src, dec_in, None, la, la)
         return self.loss(logits, target)
 
-    def training_step_split(self, src, tgt, shift_targets=False):
-        """The same loss with the autograd graph cut at the encoder output, for a backward in two
-        segments (``StepRunner(split_fn=...)``): returns ``(loss, enc_leaf, enc)`` where the
-        decoder consumed ``enc_leaf`` (a detached leaf of ``enc``).  ``loss.backward()`` then
-        finishes every decoder / vocab-projection gradient and leaves d(enc) in
-        ``enc_leaf.grad``; ``enc.backward(enc_leaf.grad)`` runs the encoder's backward.  A
-        data-parallel step all-reduces the decoder's gradient buckets while the encoder
-        backward runs."""
+    def training_step_split(self, src, tgt, shift_targets=False, enc_cuts=None):
+        """The same loss with the autograd graph cut into segments, for a backward in several
+        pieces (``StepRunner(split_fn=...)``): the encoder output and the encoder layer outputs
+        listed in ``enc_cuts`` (default: the middle layer) become detached leaves.  Returns
+        ``(loss, segments)`` with ``segments = [(leaf, root), ...]`` in BACKWARD order:
+        ``loss.backward()`` finishes every decoder / vocab-projection gradient and leaves the
+        top leaf's gradient; then, for each segment, ``root.backward(leaf.grad)`` runs the next
+        slice of the encoder backward.  A data-parallel step all-reduces the gradient buckets
+        that are final after each piece while the next piece runs."""
         if shift_targets:
             dec_in, target = tgt[:, :-1], tgt[:, 1:]
         else:
             dec_in, target = tgt, tgt
         la = torch.ones(1, dtype=torch.bool)
         enc_mode, self_mode, cross_mode, kp = self._modes(src, None, la, la)
-        enc = self.encoder(src, enc_mode, kp)
-        enc_leaf = enc.detach().requires_grad_()
-        out = self.decoder(enc_leaf, dec_in, self_mode, cross_mode, kp)
+        layers = list(self.encoder.layers)
+        n = len(layers)
+        cuts = sorted({c for c in (enc_cuts if enc_cuts is not None else [n // 2]) if 0 < c < n})
+        x = self.encoder.sentence_embedding(src)
+        segments, start = [], 0
+        for c in cuts + [n]:
+            for layer in layers[start:c]:
+                x = layer(x, enc_mode, kp)
+            leaf = x.detach().requires_grad_()
+            segments.append((leaf, x))
+            x, start = leaf, c
+        out = self.decoder(x, dec_in, self_mode, cross_mode, kp)
         logits = linear(out, self.linear.weight, self.linear.bias)
-        return self.loss(logits, target), enc_leaf, enc
+        return self.loss(logits, target), segments[::-1]
 
 
 def create_look_ahead_mask(size):

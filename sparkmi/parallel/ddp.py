@@ -66,11 +66,15 @@ class DataParallel:
             for i in idx:
                 self.bucket_of[i] = b
 
-    def align_buckets(self, ready_ids):
-        """Re-cut the buckets so none mixes parameters in ``ready_ids`` (a set of id(param): the
-        gradients final after the first backward segment) with the others."""
-        inside = [id(p) in ready_ids for p in self.flat.params]
-        cuts = [i for i in range(1, len(inside)) if inside[i] != inside[i - 1]]
+    def align_buckets(self, groups):
+        """Re-cut the buckets so none mixes parameters of different ``groups`` (a list of sets of
+        id(param): the gradients final after each backward piece; parameters in no group form
+        the last segment)."""
+        seg = []
+        for p in self.flat.params:
+            k = next((i for i, gset in enumerate(groups) if id(p) in gset), len(groups))
+            seg.append(k)
+        cuts = [i for i in range(1, len(seg)) if seg[i] != seg[i - 1]]
         self._build_buckets(cuts)
         self.reset()
 

@@ -11,12 +11,13 @@ device buffers before each replay.
     all-reduced by RCCL (a few large collectives over the flat buffer) and the optimizer runs
     as one launch.  Collectives stay outside the graph, so no RCCL-in-capture dependency;
     eager data-parallel steps instead overlap the bucket all-reduces with backward.
-  * data-parallel with ``split_fn`` (a loss whose autograd graph is cut in two, e.g.
-    Transformer.training_step_split at the encoder output): the step is TWO graphs — G1 =
-    forward + backward of the upper segment (decoder + vocab projection), G2 = backward of the
-    lower segment (encoder).  Buckets whose parameters all became final inside G1 are
-    all-reduced on RCCL's stream while G2 replays, so most of the gradient traffic hides under
-    the encoder backward; the rest is reduced after G2.  Still no collective inside a graph.
+  * data-parallel with ``split_fn`` (a loss whose autograd graph is cut into segments, e.g.
+    Transformer.training_step_split at the encoder output and mid-encoder): the step is
+    several graphs — G1 = forward + backward of the top segment (decoder + vocab projection),
+    then one graph per lower segment's backward.  After each graph replays, the gradient
+    buckets whose parameters all became final in it are all-reduced on RCCL's stream while the
+    next graph replays; only the last segment's buckets are reduced after the backward.  Still
+    no collective inside a graph.
 """
 import torch
 
@@ -28,8 +29,8 @@ class StepRunner:
         self.model = model
         self.loss_fn = loss_fn          # loss_fn(model, *batch) -> scalar loss tensor
         self.split_fn = split_fn        # split_fn(model, *batch) -> (loss, leaf, root), see module doc
-        self.graph2 = None
-        self.early_buckets = []
+        self.graph2 = None              # split mode: the lower segments' backward graphs
+        self.bucket_waves = []          # split mode: buckets to launch after each graph
         self._split_keep = None
         self.opt = optimizer
         self.ddp = ddp
@@ -66,35 +67,49 @@ class StepRunner:
         rng = getattr(self.model, "rng", None)
         if rng is not None:
             rng.advance()
-        loss, leaf, root = self.split_fn(self.model, *batch)
+        loss, segments = self.split_fn(self.model, *batch)
         loss.backward()
         _grad.join()
-        return loss.detach(), leaf, root
+        return loss.detach(), segments
 
     def _capture_split(self):
-        """G1 = forward + upper backward, G2 = lower backward (shares G1's memory pool); records
-        which gradient buckets are final after G1."""
-        ready = set()
-        listener = _grad.add_listener(lambda p: ready.add(id(p)))
-        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        """G1 = forward + top-segment backward, then one graph per lower segment (all sharing
+        G1's memory pool); records which gradient buckets are final after each graph."""
+        ready = []
+
+        def record(into):
+            return _grad.add_listener(lambda p: into.add(id(p)))
+
+        first = set()
+        listener = record(first)
+        g1 = torch.cuda.CUDAGraph()
         try:
             with torch.cuda.graph(g1):
-                self.static_loss, leaf, root = self._fwd_bwd_split(*self.static_in)
+                self.static_loss, segments = self._fwd_bwd_split(*self.static_in)
         finally:
             _grad.remove_listener(listener)
-        late = set()
-        listener = _grad.add_listener(lambda p: late.add(id(p)))
-        try:
-            with torch.cuda.graph(g2, pool=g1.pool()):
-                root.backward(leaf.grad)
-                _grad.join()
-        finally:
-            _grad.remove_listener(listener)
-        ready -= late  # a gradient also accumulated in the lower segment is not final after G1
-        self._split_keep = (leaf, root)  # G2 reads leaf.grad / root's saved tensors at fixed addresses
-        self.graph, self.graph2 = g1, g2
+        ready.append(first)
+        graphs = [g1]
+        for leaf, root in segments:
+            seen = set()
+            listener = record(seen)
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g, pool=g1.pool()):
+                    root.backward(leaf.grad)
+                    _grad.join()
+            finally:
+                _grad.remove_listener(listener)
+            ready.append(seen)
+            graphs.append(g)
+        # a gradient also accumulated by a later graph is not final after an earlier one
+        for i in range(len(ready)):
+            for later in ready[i + 1:]:
+                ready[i] -= later
+        self._split_keep = segments  # later graphs read leaf.grad / roots' saved tensors at fixed addresses
+        self.graph, self.graph2 = graphs[0], graphs[1:]
         self.ddp.align_buckets(ready)
-        self.early_buckets = self.ddp.complete_buckets(ready)
+        self.bucket_waves = [self.ddp.complete_buckets(r) for r in ready]
 
     def _capture(self, batch):
         """Record one step into a HIP graph.  Capture only records (nothing executes), so no
@@ -128,9 +143,11 @@ class StepRunner:
             dst.copy_(src, non_blocking=True)
         self.graph.replay()
         if self.graph2 is not None:
-            for b in self.early_buckets:   # decoder buckets: RCCL runs under the encoder backward
-                self.ddp.launch(b)
-            self.graph2.replay()
+            # after each backward piece, its final buckets go to RCCL while the next piece runs
+            for g, wave in zip(self.graph2, self.bucket_waves):
+                for b in wave:
+                    self.ddp.launch(b)
+                g.replay()
         if self._dp:
             self.ddp.finish()   # bucketed RCCL all-reduce of the flat gradient buffer
             self.opt.step()

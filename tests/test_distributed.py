@@ -138,3 +138,29 @@ def test_bucketing_covers_flat_buffer():
     assert spans[0][0] == 0 and spans[-1][1] == flat.numel
     assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
     assert sorted(i for _, _, idx in ddp.buckets for i in idx) == list(range(len(flat.params)))
+
+
+def test_align_buckets_to_backward_segments():
+    """Buckets re-cut at the split-backward segment boundaries: no bucket mixes parameters of
+    two segments, the buckets still tile the flat buffer, and complete_buckets() returns exactly
+    the buckets of one segment (the StepRunner split path launches those between graphs)."""
+    from sparkmi.models.transformer import Transformer
+    from sparkmi.parallel import DataParallel
+    from sparkmi.utils.flat import FlatParams
+    m = Transformer(d_model=64, ffn_hidden=128, num_heads=4, num_layers=2, max_sequence_length=16,
+                    src_vocab_size=50, tgt_vocab_size=60)
+    flat = FlatParams(m)
+    ddp = DataParallel(flat, bucket_mb=0.05)
+    top = {id(p) for n, p in m.named_parameters() if n.startswith(("decoder.", "linear."))}
+    mid = {id(p) for n, p in m.named_parameters() if n.startswith("encoder.layers.1.")}
+    ddp.align_buckets([top, mid])
+    seg = lambda p: 0 if id(p) in top else (1 if id(p) in mid else 2)  # noqa: E731
+    pos = 0
+    for s, e, idx in ddp.buckets:
+        assert s == pos and e > s
+        pos = e
+        assert len({seg(flat.params[i]) for i in idx}) == 1
+    assert pos == flat.numel
+    w0, w1 = ddp.complete_buckets(top), ddp.complete_buckets(mid)
+    assert w0 and w1 and not set(w0) & set(w1)
+    assert {i for b in w0 for i in ddp.buckets[b][2]} == {i for i, p in enumerate(flat.params) if id(p) in top}

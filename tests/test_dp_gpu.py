@@ -41,7 +41,7 @@ def _train(graph, steps, split=False):
     ref = p.clone()
     dist.broadcast(ref, 0)
     synced = bool(torch.equal(ref, p))
-    info = (len(runner.early_buckets), len(ddp.buckets)) if split else None
+    info = ([len(w) for w in runner.bucket_waves], len(ddp.buckets)) if split else None
     return p.cpu(), synced, info
 
 
@@ -56,13 +56,13 @@ def test_graph_dp_matches_eager_dp():
 
 @pytest.mark.gpu
 def test_split_graph_dp_matches_eager_dp():
-    """Two-graph step (decoder backward, then encoder backward with the decoder's buckets
-    all-reduced in between) == eager DP."""
+    """Three-graph step (decoder backward, upper-encoder backward, lower-encoder backward, with
+    each piece's final buckets all-reduced while the next runs) == eager DP."""
     env = {"SPARKMI_DIST_BACKEND": "gloo", "SPARKMI_GEMM_POLICY": "smi"}
     ps, ss, info = launch(_train, (True, 6, True), {}, num_processes=2, use_gpu=True, env=env, log_sink=None,
                           timeout=300)
     pe, se, _ = launch(_train, (False, 6), {}, num_processes=2, use_gpu=True, env=env, log_sink=None, timeout=300)
     assert ss and se
-    early, total = info
-    assert 0 < early < total, info
+    waves, total = info
+    assert len(waves) == 3 and all(w > 0 for w in waves[:2]) and sum(waves) <= total, info
     torch.testing.assert_close(ps, pe, rtol=1e-4, atol=1e-5)
