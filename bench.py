@@ -46,6 +46,18 @@ def parse():
     return ap.parse_args()
 
 
+def transformer_flops_per_sample(layers, seq, vocab, d=512, ffn=1024):
+    """Matmul FLOPs of one training sample (forward + backward = 3x forward): per token, each
+    encoder layer's QKV / out-projection / FFN GEMMs, each decoder layer's self QKV / out,
+    cross Q / KV / out and FFN GEMMs, the vocab projection, plus QK^T and PV of the 3 attention
+    sites per layer pair (63.4 GFLOP at L6 S256 V10k)."""
+    enc = 2 * d * (3 * d + d + 2 * ffn)
+    dec = 2 * d * (3 * d + d + d + 2 * d + d + 2 * ffn)
+    attn = 3 * 4 * seq * d
+    per_token = layers * (enc + dec + attn) + 2 * d * vocab
+    return 3 * per_token * seq
+
+
 def time_steps(runner, batches, steps, warmup, device, world):
     from sparkmi.parallel import barrier
     sync = (lambda: torch.cuda.synchronize()) if device.type == "cuda" else (lambda: None)
@@ -142,6 +154,7 @@ def main():
     elapsed, loss = time_steps(runner, batches, args.steps, args.warmup, device, world)
     final_loss = float(loss.float().item()) if loss is not None else float("nan")
     value = world * args.batch * args.steps / elapsed
+    tflops = transformer_flops_per_sample(args.layers, args.seq, args.vocab) * value / world / 1e12
     if rank == 0:
         out = {
             "metric": "samples/sec (whole node) distributed_cnn + transformer at 1/2/4/8 MI355X",
@@ -167,6 +180,8 @@ def main():
                 "overlap": "decoder buckets all-reduced under the encoder backward" if split_fn else None,
                 "baseline_ref": "BASELINE.md §2 transformer L6/S256 CPU proxy 4.79 samples/s",
                 "final_loss": round(final_loss, 4),
+                "model_tflops_per_gpu": round(tflops, 1),
+                "mfu_vs_2.5pf_dense_bf16": round(tflops / 2500.0, 3),
             },
         }
         if cnn is not None:
