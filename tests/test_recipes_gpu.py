@@ -32,8 +32,11 @@ def test_cnn_recipe_gpu_resume_exact(tmp_path):
 @pytest.mark.gpu
 def test_lstm_recipe_gpu_learns():
     from sparkmi.recipes import lstm
-    r = lstm.main(GPU + ["--n-train", "8000", "--n-test", "800", "--epochs", "2", "--lr", "0.01"])
-    assert r["test_acc"] > 40.0
+    # 2 epochs sit on the loss plateau of this small LSTM (runs ranged 23-74 % test accuracy,
+    # fp32-atomic gradient order differs run to run); 4 epochs clear it in every run measured
+    # (99.6-99.7 %, tools/lstm_check.py)
+    r = lstm.main(GPU + ["--n-train", "8000", "--n-test", "800", "--epochs", "4", "--lr", "0.01"])
+    assert r["test_acc"] > 80.0
 
 
 @pytest.mark.gpu
