@@ -26,6 +26,8 @@ sys.path.insert(0, ROOT)
 # transformer L6/S256/B32 CPU proxy, best whole-node figure (1 proc x 8 threads)
 BASELINE_TRANSFORMER = 4.79
 BASELINE_CNN = 5655.0
+BASELINE_LSTM = 1365.0    # 1 proc x 8 threads
+BASELINE_MLP = 130476.0   # world 1, 1 thread
 
 
 def parse():
@@ -34,6 +36,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="all", choices=["all", "transformer", "cnn"])
+    ap.add_argument("--aux-steps", type=int, default=100, help="timed steps of the LSTM / MLP extras")
     ap.add_argument("--cnn-batch", type=int, default=32)
     ap.add_argument("--cnn-steps", type=int, default=200)
     ap.add_argument("--batch", type=int, default=32)
@@ -107,14 +110,65 @@ def bench_cnn(args, rank, world, device):
     return world * args.cnn_batch * args.cnn_steps / elapsed, elapsed / args.cnn_steps * 1000, float(loss)
 
 
+def bench_lstm(args, rank, world, device):
+    """distributed_lstm.py workload: Embedding(V~95.8k, 32) -> LSTM(32, 32, 2 layers, dropout 0.5)
+    -> fc(4) at every step, CE on the last step; batch 32/GPU, T = 129, Adam lr 1e-3."""
+    from sparkmi.models.lstm import LSTM
+    from sparkmi.optim import Adam
+    from sparkmi.parallel.ddp import DataParallel
+    from sparkmi.train.runner import StepRunner
+    from sparkmi.utils.flat import FlatParams
+    V, B, T = 95812, 32, 129
+    torch.manual_seed(11)
+    model = LSTM(V, 32, 32, 4, num_layers=2, padding_idx=7).to(device).train()
+    flat = FlatParams(model, shadow=False)
+    opt = Adam(flat, lr=1e-3)
+    ddp = DataParallel(flat) if world > 1 else None
+    runner = StepRunner(model, lambda m, x, y: m.loss(x, y)[0], opt, ddp, graph=device.type == "cuda" and args.graph != "off")
+    g = torch.Generator().manual_seed(21 + rank)
+    batches = [(torch.randint(0, V, (B, T), generator=g).to(device), torch.randint(0, 4, (B,), generator=g).to(device))
+               for _ in range(8)]
+    steps = args.aux_steps
+    elapsed, _ = time_steps(runner, batches, steps, max(args.warmup, 5), device, world)
+    if ddp is not None:
+        ddp.close()
+    return world * B * steps / elapsed, elapsed / steps * 1000
+
+
+def bench_mlp(args, rank, world, device):
+    """distributed_multilayer_perceptron.py workload: 4-5-4-3 sigmoid MLP, batch 30/GPU, SGD."""
+    from sparkmi.models.mlp import MultilayerPerceptron
+    from sparkmi.optim import SGD
+    from sparkmi.parallel.ddp import DataParallel
+    from sparkmi.train.runner import StepRunner
+    from sparkmi.utils.flat import FlatParams
+    torch.manual_seed(5)
+    model = MultilayerPerceptron((4, 5, 4, 3)).to(device).train()
+    flat = FlatParams(model, shadow=False)
+    opt = SGD(flat, lr=0.01)
+    ddp = DataParallel(flat) if world > 1 else None
+    runner = StepRunner(model, lambda m, x, y: m.loss(x, y), opt, ddp, graph=device.type == "cuda" and args.graph != "off")
+    g = torch.Generator().manual_seed(31 + rank)
+    batches = [(torch.rand(30, 4, generator=g).to(device) * 2 - 1, torch.randint(0, 3, (30,), generator=g).to(device))
+               for _ in range(8)]
+    steps = args.aux_steps
+    elapsed, _ = time_steps(runner, batches, steps, max(args.warmup, 5), device, world)
+    if ddp is not None:
+        ddp.close()
+    return world * 30 * steps / elapsed, elapsed / steps * 1000
+
+
 def main():
     args = parse()
     from sparkmi.parallel import barrier, init_distributed
     from sparkmi.parallel.ddp import DataParallel
     rank, world, device = init_distributed()
-    cnn = None
+    cnn = lstm = mlp = None
     if args.model in ("all", "cnn"):
         cnn = bench_cnn(args, rank, world, device)
+    if args.model == "all":
+        lstm = bench_lstm(args, rank, world, device)
+        mlp = bench_mlp(args, rank, world, device)
     if args.model == "cnn":
         if rank == 0:
             v, ms, l = cnn
@@ -190,6 +244,15 @@ def main():
                             "cnn_config": f"FashionMNISTModel fp32 fused HIP kernel, batch {args.cnn_batch}/GPU, "
                                           f"SGD lr0.01, dp{world}, {args.cnn_steps} steps",
                             "cnn_baseline_ref": "BASELINE.md §2 CNN CPU proxy 5,655 samples/s (1 proc x 8 threads)"}
+            if lstm is not None:
+                out["extra"].update({
+                    "lstm_samples_per_s": round(lstm[0], 1), "lstm_ms_per_step": round(lstm[1], 4),
+                    "lstm_vs_baseline": round(lstm[0] / BASELINE_LSTM, 2),
+                    "lstm_config": f"Embedding(95812,32)+LSTM(32,32,L2)+fc4, T129, batch 32/GPU, Adam, fp32, dp{world}",
+                    "mlp_samples_per_s": round(mlp[0], 1), "mlp_ms_per_step": round(mlp[1], 4),
+                    "mlp_vs_baseline": round(mlp[0] / BASELINE_MLP, 2),
+                    "mlp_config": f"MLP 4-5-4-3 sigmoid, batch 30/GPU, SGD, fp32, dp{world}",
+                    "aux_baseline_ref": "BASELINE.md §2 best CPU proxy: LSTM 1,365, MLP 130,476 samples/s"})
         print(json.dumps(out), flush=True)
     from sparkmi.parallel import destroy
     destroy()
