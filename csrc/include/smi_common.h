@@ -27,15 +27,51 @@ __device__ __forceinline__ unsigned int pack2bf(float a, float b) {
 }
 
 // ---- wave64 reductions ----
+// All-lane butterfly on VALU cross-lane ops: DPP quad_perm [1,0,3,2] / [2,3,0,1] and the
+// row_half_mirror / row_mirror patterns inside each 16-lane row, then the gfx950 row swaps
+// v_permlane16_swap / v_permlane32_swap across rows.  (__shfl_xor lowers to ds_bpermute /
+// ds_swizzle, an LDS-crossbar round trip per step: six dependent ~100-cycle steps per reduction.)
+// Mirror patterns pair every lane with one from the other half of its group, so after the
+// quad steps each step sums (or maxes) two disjoint, already-reduced halves.
+#define SMI_DPP_QP1032 0xB1   // quad_perm [1,0,3,2]
+#define SMI_DPP_QP2301 0x4E   // quad_perm [2,3,0,1]
+#define SMI_DPP_HMIRROR 0x141 // row_half_mirror
+#define SMI_DPP_MIRROR 0x140  // row_mirror
+template <int CTRL>
+__device__ __forceinline__ float smi_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float smi_row16_swap_sum(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(a[0]) + __uint_as_float(a[1]);
+}
+__device__ __forceinline__ float smi_row32_swap_sum(float v) {
+  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(a[0]) + __uint_as_float(a[1]);
+}
+__device__ __forceinline__ float smi_row16_swap_max(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+}
+__device__ __forceinline__ float smi_row32_swap_max(float v) {
+  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += smi_dpp<SMI_DPP_QP1032>(v);
+  v += smi_dpp<SMI_DPP_QP2301>(v);
+  v += smi_dpp<SMI_DPP_HMIRROR>(v);
+  v += smi_dpp<SMI_DPP_MIRROR>(v);
+  v = smi_row16_swap_sum(v);
+  return smi_row32_swap_sum(v);
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmaxf(v, smi_dpp<SMI_DPP_QP1032>(v));
+  v = fmaxf(v, smi_dpp<SMI_DPP_QP2301>(v));
+  v = fmaxf(v, smi_dpp<SMI_DPP_HMIRROR>(v));
+  v = fmaxf(v, smi_dpp<SMI_DPP_MIRROR>(v));
+  v = smi_row16_swap_max(v);
+  return smi_row32_swap_max(v);
 }
 // sum over groups of `width` consecutive lanes (width power of two <= 64)
 template <int W>

@@ -102,6 +102,25 @@ __device__ __forceinline__ void store4(unsigned short* p, const f32x4_t& v, floa
   *(uint2*)p = pk;
 }
 
+
+// Reductions across the four 16-lane rows of a wave (lanes n, n+16, n+32, n+48) with the gfx950
+// row-swap instructions (VALU, a few cycles) instead of __shfl_xor (ds_bpermute through the LDS
+// crossbar, ~100+ cycles of latency on the softmax's critical path).  permlane16_swap(v, v)
+// returns rows (R0,R0,R2,R2) and (R1,R1,R3,R3): their combination is the xor-16 reduction in
+// every lane; permlane32_swap(v, v) likewise gives halves (lo,lo) and (hi,hi) for xor-32.
+__device__ __forceinline__ float rows4_max(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float rows4_sum(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 #define MFMA16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 
 // Masked, biased, log2-scaled score for key kj / query qi; -inf where masked.  Specialised on
@@ -215,8 +234,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
             cmax = fmaxf(cmax, s[qs][t][j]);
           }
       }
-      cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
-      cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+      cmax = rows4_max(cmax);
       const float mnew = fmaxf(m[qs], cmax);
       const float mref = (mnew == -INFINITY) ? 0.f : mnew;
       const float alpha = __builtin_amdgcn_exp2f(m[qs] - mref);
@@ -236,8 +254,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) { s[qs][t][j] = __builtin_amdgcn_exp2f(s[qs][t][j] - mref); psum += s[qs][t][j]; }
       }
-      psum += __shfl_xor(psum, 16, 64);
-      psum += __shfl_xor(psum, 32, 64);
+      psum = rows4_sum(psum);
       l[qs] = l[qs] * alpha + psum;
       m[qs] = mnew;
 #pragma unroll
@@ -319,8 +336,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnBwdArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         sacc += bf2f((unsigned short)df[qs][u][j]) * bf2f((unsigned short)of[qs][u][j]);
-    sacc += __shfl_xor(sacc, 16, 64);
-    sacc += __shfl_xor(sacc, 32, 64);
+    sacc = rows4_sum(sacc);
     dl[qs] = sacc;
     const int qi = qwave + qs * 16 + n;
     if (g == 0 && qi < a.Sq) a.delta_out[((long)b * a.H + h) * a.Sq + qi] = sacc;
