@@ -25,8 +25,11 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
 # per-kernel compiler flags: attention keeps its MFMA accumulators in VGPRs (the softmax works on
-# them every chunk; the default AGPR form cost two accvgpr moves per element per chunk)
-KERNEL_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+# them every chunk; the default AGPR form cost two accvgpr moves per element per chunk).
+# -fno-honor-nans on the softmax kernels: fmaxf otherwise canonicalises both operands
+# (v_max_f32 v, v, v) before every max of the online softmax; infinities keep their meaning.
+KERNEL_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-honor-nans"],
+                "cross_entropy.hip": ["-fno-honor-nans"]}
 
 
 def _ext_suffix():
