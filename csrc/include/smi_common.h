@@ -73,6 +73,39 @@ __device__ __forceinline__ float wave_max(float v) {
   v = smi_row16_swap_max(v);
   return smi_row32_swap_max(v);
 }
+// Transposing reduction of 64 per-lane values: lane L returns the wave-wide sum of t[L].
+// Each exchange step halves the live values (a lane keeps the half selected by one bit of its
+// lane id and receives the partner's copy of it), so 64 sums cost 63 exchanges + adds instead
+// of 64 x 6 for independent wave_sum calls.  Partner sets: lane ^ 32, ^ 16 (permlane swaps),
+// ^ 15 (row mirror), ^ 7 (half mirror), ^ 2, ^ 1 (quad perms) — independent over GF(2), so
+// every lane's result covers all 64 lanes exactly once.  t is clobbered.
+template <int W, int CTRL, int BIT>
+__device__ __forceinline__ void smi_tsum_dpp_step(float (&t)[64], int lane) {
+  const bool hi = (lane >> BIT) & 1;
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    const float keep = hi ? t[j + W] : t[j], send = hi ? t[j] : t[j + W];
+    t[j] = keep + smi_dpp<CTRL>(send);
+  }
+}
+__device__ __forceinline__ float wave_transpose_sum64(float (&t)[64]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {  // lanes < 32 keep t[j], lanes >= 32 keep t[j + 32]
+    auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(t[j]), __float_as_uint(t[j + 32]), false, false);
+    t[j] = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {  // even rows keep t[j], odd rows t[j + 16]
+    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(t[j]), __float_as_uint(t[j + 16]), false, false);
+    t[j] = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  }
+  smi_tsum_dpp_step<8, SMI_DPP_MIRROR, 3>(t, lane);
+  smi_tsum_dpp_step<4, SMI_DPP_HMIRROR, 2>(t, lane);
+  smi_tsum_dpp_step<2, SMI_DPP_QP2301, 1>(t, lane);
+  smi_tsum_dpp_step<1, SMI_DPP_QP1032, 0>(t, lane);
+  return t[0];
+}
 // sum over groups of `width` consecutive lanes (width power of two <= 64)
 template <int W>
 __device__ __forceinline__ float group_sum(float v) {
