@@ -35,7 +35,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--model", default="all", choices=["all", "transformer", "cnn"])
+    ap.add_argument("--model", default="all", choices=["all", "transformer", "cnn", "aux"])
     ap.add_argument("--aux-steps", type=int, default=100, help="timed steps of the LSTM / MLP extras")
     ap.add_argument("--cnn-batch", type=int, default=32)
     ap.add_argument("--cnn-steps", type=int, default=200)
@@ -166,9 +166,15 @@ def main():
     cnn = lstm = mlp = None
     if args.model in ("all", "cnn"):
         cnn = bench_cnn(args, rank, world, device)
-    if args.model == "all":
+    if args.model in ("all", "aux"):
         lstm = bench_lstm(args, rank, world, device)
         mlp = bench_mlp(args, rank, world, device)
+    if args.model == "aux":  # LSTM + MLP extras only (profiling)
+        if rank == 0:
+            print(json.dumps({"lstm_samples_per_s": round(lstm[0], 1), "lstm_ms_per_step": round(lstm[1], 4),
+                              "mlp_samples_per_s": round(mlp[0], 1), "mlp_ms_per_step": round(mlp[1], 4),
+                              "n_gpus": world}))
+        return
     if args.model == "cnn":
         if rank == 0:
             v, ms, l = cnn

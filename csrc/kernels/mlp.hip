@@ -7,8 +7,10 @@
 // The whole network is a few dozen parameters, so the GPU cost is launch latency, not FLOPs:
 // one kernel does the full-batch (or minibatch) forward + loss, one does forward-recompute +
 // backward + gradient accumulation; each wave64 handles 64 rows (one row per lane), per-lane
-// activations live in LDS, weight gradients are summed per block with LDS atomics and flushed
-// with one global atomic per parameter per block.  Row weights implement MLlib's per-block
+// activations and pre-activation gradients live in LDS rows with an odd pitch (an even
+// multiple-of-32 pitch put all 64 lanes on one bank: 74 us per backward at batch 30), and each
+// weight-gradient entry is summed over the 64 rows by one lane (no LDS atomics, fixed order),
+// then flushed with one global atomic per parameter per block.  Row weights implement MLlib's per-block
 // loss averaging (or 1/n for the torch-style mean).
 #include "smi_common.h"
 
@@ -48,9 +50,12 @@ __device__ __forceinline__ float mlp_forward_row(const MLPArgs& a, int row, floa
   return lse - z[lab];
 }
 
+#define MLP_ACT_LD (MLP_ACT_STRIDE + 1)        // odd LDS pitch: lane-private rows on distinct banks
+#define MLP_DEL_LD (MLP_MAXW * MLP_MAXL + 1)
+
 __global__ __launch_bounds__(64) void mlp_fwd_kernel(MLPArgs a) {
-  __shared__ float acts[64 * MLP_ACT_STRIDE];
-  float* act_s = acts + threadIdx.x * MLP_ACT_STRIDE;
+  __shared__ float acts[64 * MLP_ACT_LD];
+  float* act_s = acts + threadIdx.x * MLP_ACT_LD;
   float lsum = 0.f;
   for (int row = blockIdx.x * 64 + threadIdx.x; row < a.n; row += gridDim.x * 64) {
     const float l = mlp_forward_row(a, row, act_s);
@@ -68,59 +73,71 @@ __global__ __launch_bounds__(64) void mlp_fwd_kernel(MLPArgs a) {
 }
 
 __global__ __launch_bounds__(64) void mlp_bwd_kernel(MLPArgs a) {
-  __shared__ float acts[64 * MLP_ACT_STRIDE];
-  __shared__ float delta[64 * 2 * MLP_MAXW];
+  __shared__ float acts[64 * MLP_ACT_LD];  // per row: layer inputs (dims[0..L-1]) + logits
+  __shared__ float dls[64 * MLP_DEL_LD];   // per row: grad wrt each layer's pre-activation output
   __shared__ float gacc[8192];
+  const int L = a.nlayers, lane = threadIdx.x;
+  int offs[MLP_MAXL + 1];  // activation offsets (offs[l] = input of layer l)
+  offs[0] = 0;
+  for (int l = 0; l < L; ++l) offs[l + 1] = offs[l] + a.dims[l];
   int total = 0;
-  int goff[MLP_MAXL];
-  for (int l = 0; l < a.nlayers; ++l) { goff[l] = total; total += a.dims[l + 1] * (a.dims[l] + 1); }
-  for (int i = threadIdx.x; i < total; i += 64) gacc[i] = 0.f;
-  __syncthreads();
-  float* act_s = acts + threadIdx.x * MLP_ACT_STRIDE;
+  for (int l = 0; l < L; ++l) total += a.dims[l + 1] * (a.dims[l] + 1);
+  for (int i = lane; i < total; i += 64) gacc[i] = 0.f;
+  float* act_s = acts + lane * MLP_ACT_LD;
+  float* del_s = dls + lane * MLP_DEL_LD;
   const float dl = a.dloss ? a.dloss[0] : 1.f;
-  for (int row = blockIdx.x * 64 + threadIdx.x; row < a.n; row += gridDim.x * 64) {
-    mlp_forward_row(a, row, act_s);
-    float* dcur = delta + threadIdx.x * 2 * MLP_MAXW;
-    float* dnext = dcur + MLP_MAXW;
-    const float w = (a.row_w ? a.row_w[row] : 1.f / (float)a.n) * dl;
-    int offs[MLP_MAXL + 1];
-    offs[0] = 0;
-    for (int l = 0; l < a.nlayers; ++l) offs[l + 1] = offs[l] + a.dims[l];
-    const int L = a.nlayers;
-    const int C = a.dims[L];
-    const float* z = act_s + offs[L];
-    float m = z[0];
-    for (int c = 1; c < C; ++c) m = fmaxf(m, z[c]);
-    float se = 0.f;
-    for (int c = 0; c < C; ++c) se += __expf(z[c] - m);
-    const long long lab = a.y[row];
-    for (int c = 0; c < C; ++c) dcur[c] = (__expf(z[c] - m) / se - (c == lab ? 1.f : 0.f)) * w;
-    for (int l = L - 1; l >= 0; --l) {
-      const int din = a.dims[l], dout = a.dims[l + 1];
-      const float* in = act_s + offs[l];
-      float* g = gacc + goff[l];
-      for (int o = 0; o < dout; ++o) {
-        const float d = dcur[o];
-        for (int i = 0; i < din; ++i) atomicAdd(&g[o * din + i], d * in[i]);
-        atomicAdd(&g[dout * din + o], d);
-      }
-      if (l > 0) {
+  const int d0 = a.dims[0];
+  for (int chunk = blockIdx.x * 64; chunk < a.n; chunk += gridDim.x * 64) {
+    const int row = chunk + lane;
+    if (row < a.n) {
+      mlp_forward_row(a, row, act_s);
+      const float w = (a.row_w ? a.row_w[row] : 1.f / (float)a.n) * dl;
+      const int C = a.dims[L];
+      const float* z = act_s + offs[L];
+      float* dz = del_s + offs[L] - d0;
+      float m = z[0];
+      for (int c = 1; c < C; ++c) m = fmaxf(m, z[c]);
+      float se = 0.f;
+      for (int c = 0; c < C; ++c) se += __expf(z[c] - m);
+      const long long lab = a.y[row];
+      for (int c = 0; c < C; ++c) dz[c] = (__expf(z[c] - m) / se - (c == lab ? 1.f : 0.f)) * w;
+      for (int l = L - 1; l > 0; --l) {  // grad wrt layer l-1's pre-activation output
+        const int din = a.dims[l], dout = a.dims[l + 1];
+        const float* dcur = del_s + offs[l + 1] - d0;
+        float* dprev = del_s + offs[l] - d0;
+        const float* h = act_s + offs[l];
         for (int i = 0; i < din; ++i) {
           float s = 0.f;
           for (int o = 0; o < dout; ++o) s += a.W[l][o * din + i] * dcur[o];
-          const float h = in[i];
-          dnext[i] = a.act == 1 ? (h > 0.f ? s : 0.f) : s * h * (1.f - h);
+          dprev[i] = a.act == 1 ? (h[i] > 0.f ? s : 0.f) : s * h[i] * (1.f - h[i]);
         }
-        float* t = dcur; dcur = dnext; dnext = t;
       }
+    } else {  // rows past n contribute nothing
+      for (int j = 0; j < offs[L] + a.dims[L] - d0; ++j) del_s[j] = 0.f;
+      for (int j = 0; j < offs[L]; ++j) act_s[j] = 0.f;
     }
+    __syncthreads();
+    // gradient entry e (layer-major: W[o][i] then b[o]) summed over the chunk's 64 rows, in row order
+    for (int e = lane; e < total; e += 64) {
+      int l = 0, base = 0;
+      while (e >= base + a.dims[l + 1] * (a.dims[l] + 1)) { base += a.dims[l + 1] * (a.dims[l] + 1); ++l; }
+      const int din = a.dims[l], dout = a.dims[l + 1], r = e - base;
+      const bool bias = r >= dout * din;
+      const int o = bias ? r - dout * din : r / din, i = bias ? 0 : r - (r / din) * din;
+      const float* dp = dls + offs[l + 1] - d0 + o;
+      const float* ap = acts + offs[l] + i;
+      float s = 0.f;
+      for (int k = 0; k < 64; ++k) s += dp[k * MLP_DEL_LD] * (bias ? 1.f : ap[k * MLP_ACT_LD]);
+      gacc[e] += s;
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  for (int l = 0; l < a.nlayers; ++l) {
+  for (int l = 0, base = 0; l < L; ++l) {
     const int din = a.dims[l], dout = a.dims[l + 1];
-    const float* g = gacc + goff[l];
-    for (int i = threadIdx.x; i < dout * din; i += 64) atomicAdd(&a.gW[l][i], g[i]);
-    for (int i = threadIdx.x; i < dout; i += 64) atomicAdd(&a.gb[l][i], g[dout * din + i]);
+    const float* g = gacc + base;
+    for (int i = lane; i < dout * din; i += 64) atomicAdd(&a.gW[l][i], g[i]);
+    for (int i = lane; i < dout; i += 64) atomicAdd(&a.gb[l][i], g[dout * din + i]);
+    base += dout * (din + 1);
   }
 }
 
