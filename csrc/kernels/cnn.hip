@@ -57,19 +57,40 @@ typedef const __attribute__((address_space(4))) float* cfp;
 // that runs past cout computes on clamped weights and skips the store — runtime per-channel
 // guards compiled into one scalar branch + s_waitcnt lgkmcnt(0) per channel (conv2 forward
 // 41k -> 19k cycles; docs/PERF_NOTES.md CNN section).
+//
+// Each lane computes a horizontal PAIR of output positions with packed fp32 FMAs
+// (v_pk_fma_f32, scalar weight broadcast to both halves): one 3x4 window (3 aligned 8-B LDS
+// reads x 2) serves both outputs, and every weight s_load and FMA issue covers two outputs.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pkfma(float w, f2 v, f2 acc) { return __builtin_elementwise_fma((f2)(w), v, acc); }
+
 template <int H, int CC>
 struct ConvGroups {
-  static constexpr int NCH = (H * H + 63) / 64;          // 64-position chunks
+  static constexpr int NPAIR = H * H / 2;                // H even: pairs (y, 2i), (y, 2i+1)
+  static constexpr int NCH = (NPAIR + 63) / 64;          // 64-pair chunks
   static constexpr int NW = CNN_THREADS / 64;
   static constexpr int NG0 = NW / NCH > 0 ? NW / NCH : 1;
   static constexpr int NGRP = NG0 < CC ? NG0 : CC;       // channel groups
   static constexpr int CG = (CC + NGRP - 1) / NGRP;      // channels per group
 };
 
+// 3 x 4 window at row pointer r (8-B aligned, pitch PP): per row, pairs (c0,c1), (c1,c2), (c2,c3)
+template <int PP>
+__device__ __forceinline__ void load_win(const float* r, f2 (&A)[3], f2 (&M)[3], f2 (&B)[3], int rstep) {
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+    const f2* q = (const f2*)(r + ky * rstep);
+    A[ky] = q[0];
+    B[ky] = q[1];
+    M[ky] = f2{A[ky].y, B[ky].x};
+  }
+}
+
 template <int H, int PP, int CC, bool EX>
 __device__ __forceinline__ void conv_fwd(const float* __restrict__ in, int cin, float* __restrict__ out, int cout,
                          const float* __restrict__ wg, const float* __restrict__ bg) {
   using G = ConvGroups<H, CC>;
+  constexpr int HP = H / 2;
   const cfp w = (cfp)wg;
   const cfp b = (cfp)bg;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -83,32 +104,36 @@ __device__ __forceinline__ void conv_fwd(const float* __restrict__ in, int cin, 
     int wrow[G::CG];
 #pragma unroll
     for (int c = 0; c < G::CG; ++c) wrow[c] = EX ? base + c : min(base + c, cout - 1);
-    const int pos = chunk * 64 + lane;
-    const bool ok = pos < H * H;
-    const int pp = ok ? pos : 0;
-    const int y = pp / H, x = pp % H;
-    float acc[G::CG];
+    const int q = chunk * 64 + lane;
+    const bool ok = q < G::NPAIR;
+    const int qq = ok ? q : 0;
+    const int y = qq / HP, x0 = (qq - y * HP) * 2;
+    f2 acc[G::CG];
 #pragma unroll
-    for (int c = 0; c < G::CG; ++c) acc[c] = b[wrow[c]];
+    for (int c = 0; c < G::CG; ++c) acc[c] = (f2)(b[wrow[c]]);
 #pragma unroll 1  // a full unroll (cin is compile-time with EX) hoists every weight into SGPRs and spills
     for (int ci = 0; ci < cin; ++ci) {
-      const float* ip = in + ci * PP * PP + y * PP + x;  // top-left of the 3x3 window (halo coords)
-      float v[9];
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) v[ky * 3 + kx] = ip[ky * PP + kx];
+      f2 A[3], M[3], B[3];  // output x0 uses cols x0..x0+2, x0+1 uses x0+1..x0+3 (halo coords)
+      load_win<PP>(in + ci * PP * PP + y * PP + x0, A, M, B, PP);
 #pragma unroll
       for (int c = 0; c < G::CG; ++c) {
         const cfp wp = w + (wrow[c] * cin + ci) * 9;
 #pragma unroll
-        for (int k = 0; k < 9; ++k) acc[c] = __builtin_fmaf(wp[k], v[k], acc[c]);
+        for (int ky = 0; ky < 3; ++ky) {
+          acc[c] = pkfma(wp[ky * 3 + 0], A[ky], acc[c]);
+          acc[c] = pkfma(wp[ky * 3 + 1], M[ky], acc[c]);
+          acc[c] = pkfma(wp[ky * 3 + 2], B[ky], acc[c]);
+        }
       }
     }
     if (ok) {
 #pragma unroll
       for (int c = 0; c < G::CG; ++c)
-        if (base + c >= co0 && base + c < cout) out[(base + c) * PP * PP + (y + 1) * PP + (x + 1)] = fmaxf(acc[c], 0.f);
+        if (base + c >= co0 && base + c < cout) {
+          float* op = out + (base + c) * PP * PP + (y + 1) * PP + (x0 + 1);
+          op[0] = fmaxf(acc[c].x, 0.f);
+          op[1] = fmaxf(acc[c].y, 0.f);
+        }
     }
   }
 }
@@ -233,6 +258,7 @@ template <int H, int PP, int CC, bool EX>
 __device__ __forceinline__ void conv_dgrad(const float* __restrict__ dz, int cout, const float* __restrict__ wg, int cin,
                            float* __restrict__ a, bool relu) {
   using G = ConvGroups<H, CC>;
+  constexpr int HP = H / 2;
   const cfp w = (cfp)wg;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   for (int u = wv; u < G::NGRP * G::NCH; u += G::NW) {
@@ -243,34 +269,36 @@ __device__ __forceinline__ void conv_dgrad(const float* __restrict__ dz, int cou
     int wcol[G::CG];
 #pragma unroll
     for (int c = 0; c < G::CG; ++c) wcol[c] = EX ? base + c : min(base + c, cin - 1);
-    const int pos = chunk * 64 + lane;
-    const bool ok = pos < H * H;
-    const int pp = ok ? pos : 0;
-    const int y = pp / H, x = pp % H;
-    float acc[G::CG];
+    const int q = chunk * 64 + lane;
+    const bool ok = q < G::NPAIR;
+    const int qq = ok ? q : 0;
+    const int y = qq / HP, x0 = (qq - y * HP) * 2;
+    f2 acc[G::CG];
 #pragma unroll
-    for (int c = 0; c < G::CG; ++c) acc[c] = 0.f;
+    for (int c = 0; c < G::CG; ++c) acc[c] = f2{0.f, 0.f};
 #pragma unroll 1
     for (int co = 0; co < cout; ++co) {
-      const float* dp = dz + co * PP * PP + (y + 2) * PP + (x + 2);  // dz at (y+1, x+1) in halo coords, minus k
-      float v[9];
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) v[ky * 3 + kx] = dp[-ky * PP - kx];
+      // rows y+2-ky (ky = 0..2) of dz, cols x0..x0+3: output x0 takes col x0+2-kx, x0+1 takes x0+3-kx
+      f2 A[3], M[3], B[3];
+      load_win<PP>(dz + co * PP * PP + (y + 2) * PP + x0, A, M, B, -PP);
 #pragma unroll
       for (int c = 0; c < G::CG; ++c) {
         const cfp wp = w + (co * cin + wcol[c]) * 9;
 #pragma unroll
-        for (int k = 0; k < 9; ++k) acc[c] = __builtin_fmaf(wp[k], v[k], acc[c]);
+        for (int ky = 0; ky < 3; ++ky) {
+          acc[c] = pkfma(wp[ky * 3 + 0], B[ky], acc[c]);
+          acc[c] = pkfma(wp[ky * 3 + 1], M[ky], acc[c]);
+          acc[c] = pkfma(wp[ky * 3 + 2], A[ky], acc[c]);
+        }
       }
     }
     if (ok) {
 #pragma unroll
       for (int c = 0; c < G::CG; ++c) {
         if (base + c >= ci0 && base + c < cin) {
-          float* ap = a + (base + c) * PP * PP + (y + 1) * PP + (x + 1);
-          *ap = relu ? (*ap > 0.f ? acc[c] : 0.f) : acc[c];
+          float* ap = a + (base + c) * PP * PP + (y + 1) * PP + (x0 + 1);
+          ap[0] = relu ? (ap[0] > 0.f ? acc[c].x : 0.f) : acc[c].x;
+          ap[1] = relu ? (ap[1] > 0.f ? acc[c].y : 0.f) : acc[c].y;
         }
       }
     }
