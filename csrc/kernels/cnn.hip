@@ -175,76 +175,94 @@ __device__ __forceinline__ void unpool_relu_inplace(float* __restrict__ a, const
 }
 
 // dW[co][ci][k] = sum_pos dz[co][pos] * in[ci][pos+k-1]; db[co] = sum_pos dz[co][pos]
-// Work unit = (input channel ci, group of WG_CG output channels, position chunk), one per wave:
-// lanes walk the positions, each lane loads its 3x3 input window ONCE and reuses it for all
-// WG_CG output channels (45 FMAs per 14 LDS loads; the former wave-per-(co,ci) mapping re-read
-// the window per output channel: 10 FMAs per 10 loads, 60k cycles for conv2).  Per-wave sums
-// are reduced across lanes by one transposing reduction (wave_transpose_sum64: 63 exchanges for
-// all 50 sums; 50 separate wave_sum calls cost more than the accumulation) into an LDS scratch row per unit; a final pass adds
-// the chunks of each (co, ci) in fixed order, so the result is deterministic.
-#define WG_CG 5
+// as a GEMM on the fp32 matrix cores: D[co][n] = sum_p dz[co][p] * X[p][n] with n = ci*9 + k
+// (im2col gathered straight from the LDS planes) and one extra all-ones column n = cin*9 for
+// the bias.  v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulation): A[i][k] = dz of
+// output channel i (lane & 15) at position 4s + (lane >> 4), B[k][j] = im2col element of column
+// j (lane & 15) at the same position; co is padded to 16, n to whole 16-column tiles.  Work
+// unit = (n tile, chunk of k-steps); per-unit 16x16 tiles go to LDS scratch and a final pass
+// sums the chunks of each entry in chunk order (deterministic).  The VALU version (window
+// reuse across 5 output channels + a 64-value transposing wave reduction) spent 4 cycles of
+// SIMD issue per FMA-equivalent and was 45 % of the fused step.
+typedef float f4 __attribute__((ext_vector_type(4)));
+#define WG_SCRATCH (12 * 256)  // floats: up to 12 units of one 16x16 tile
+
 template <int H, int PP>
 __device__ __forceinline__ void conv_wgrad(const float* __restrict__ dz, const float* __restrict__ in, int cin, int cout,
-                           float* __restrict__ acc, float* __restrict__ scratch) {
+                           float* __restrict__ acc, float* __restrict__ scratch, int sb = -1) {
+  // k-steps come in groups of 7 = 28 positions (one row at H = 28, two at H = 14), so a lane's
+  // 7 gather offsets inside a group are fixed: per group, 14 LDS reads at precomputed addresses,
+  // 14 address increments and 7 MFMAs — no per-step index math (per-step y/x updates and
+  // mode selects made the VALU, not the matrix core, the bottleneck: ~240 cycles per k-step).
+  constexpr int GS = 7, NG = H * H / 28, GROWS = 28 / H;
+  static_assert(H * H % 28 == 0, "position groups");
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
-  const int ngrp = (cout + WG_CG - 1) / WG_CG;
-  const int nch = max(1, nw / (cin * ngrp));  // position chunks per (ci, group)
-  const int units = cin * ngrp * nch;
-  constexpr int ROW = WG_CG * 9 + WG_CG;      // scratch row: weights then biases
+  const int ncol = cin * 9 + 1;            // im2col columns + bias column
+  const int nt = (ncol + 15) >> 4;         // 16-column tiles
+  const int nch = max(1, min(min(nw, WG_SCRATCH / 256) / nt, NG));  // group chunks per tile
+  const int units = nt * nch;
+  const int i = lane & 15, kq = lane >> 4;
+  const float* zero_cell = scratch + WG_SCRATCH;      // 0.f (A padding rows, B padding columns)
+  const float* one_cell = scratch + WG_SCRATCH + 1;   // 1.f (bias column)
+  int off[GS];
+#pragma unroll
+  for (int q = 0; q < GS; ++q) {
+    const int pp = 4 * q + kq;
+    off[q] = (pp / H) * PP + pp % H;
+  }
+  const bool aok = i < cout;
+  const int astr = aok ? GROWS * PP : 0;
   for (int u = wv; u < units; u += nw) {
-    const int ch = u % nch, rest = u / nch, grp = rest % ngrp, ci = rest / ngrp;
-    const int co0 = grp * WG_CG;
-    float s[WG_CG][9], sb[WG_CG];
-#pragma unroll
-    for (int c = 0; c < WG_CG; ++c) {
-      sb[c] = 0.f;
-#pragma unroll
-      for (int k = 0; k < 9; ++k) s[c][k] = 0.f;
+    const int t = u % nt, ch = u / nt;
+    const int n = t * 16 + i;              // this lane's B column (j = lane & 15)
+    const float* bbase;
+    int bstr = 0;
+    const bool bg = n < cin * 9;
+    if (bg) {
+      const int ci = n / 9, k = n - ci * 9;
+      bbase = in + ci * PP * PP + (k / 3) * PP + (k % 3);
+      bstr = GROWS * PP;
+    } else {
+      bbase = n == cin * 9 ? one_cell : zero_cell;
     }
-    for (int p = ch * 64 + lane; p < H * H; p += nch * 64) {
-      const int y = p / H, x = p - y * H;
-      const float* ir = in + ci * PP * PP + y * PP + x;  // row y-1, col x-1 in halo coords
-      float v[9];
+    const int g0 = ch * NG / nch, g1 = (ch + 1) * NG / nch;
+    const float* pa[GS];
+    const float* pb[GS];
 #pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
+    for (int q = 0; q < GS; ++q) {
+      pa[q] = aok ? dz + i * PP * PP + PP + 1 + off[q] + g0 * astr : zero_cell;  // dz at (y+1, x+1)
+      pb[q] = bbase + (bg ? off[q] : 0) + g0 * bstr;
+    }
+    f4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};  // MFMA dependent latency 40 > issue 32
+    for (int g = g0; g < g1; ++g) {
+      float av[GS], bv[GS];
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx) v[ky * 3 + kx] = ir[ky * PP + kx];
+      for (int q = 0; q < GS; ++q) { av[q] = *pa[q]; bv[q] = *pb[q]; }
 #pragma unroll
-      for (int c = 0; c < WG_CG; ++c) {
-        const int co = co0 + c;
-        const float d = co < cout ? dz[co * PP * PP + (y + 1) * PP + x + 1] : 0.f;
-        sb[c] += d;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) s[c][k] += d * v[k];
+      for (int q = 0; q < GS; ++q) {
+        if (q & 1) d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bv[q], d1, 0, 0, 0);
+        else d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bv[q], d0, 0, 0, 0);
+        pa[q] += astr;
+        pb[q] += bstr;
       }
     }
-    float t[64];
+    const f4 d = d0 + d1;
+    float* row = scratch + u * 256;        // [co 16][col 16]: lane holds rows 4*(lane>>4)+r, col lane&15
 #pragma unroll
-    for (int c = 0; c < WG_CG; ++c) {
-#pragma unroll
-      for (int k = 0; k < 9; ++k) t[c * 9 + k] = s[c][k];
-      t[WG_CG * 9 + c] = sb[c];
-    }
-#pragma unroll
-    for (int j = ROW; j < 64; ++j) t[j] = 0.f;
-    const float r = wave_transpose_sum64(t);  // lane j holds scratch-row entry j
-    if (lane < ROW) scratch[u * ROW + lane] = r;
+    for (int r = 0; r < 4; ++r) row[(kq * 4 + r) * 16 + i] = d[r];
   }
+  if (sb >= 0) STAMP(sb);      // probe build: wave 0's units done
   __syncthreads();
-  // combine the chunks of every (co, ci) pair in chunk order; biases from the ci == 0 units
-  const int nw_ = cout * cin * 9;
-  for (int e = threadIdx.x; e < nw_ + cout; e += blockDim.x) {
-    float t = 0.f;
-    if (e < nw_) {
-      const int co = e / (cin * 9), r = e - co * cin * 9, ci = r / 9, k = r - ci * 9;
-      const int grp = co / WG_CG, c = co - grp * WG_CG;
-      for (int ch = 0; ch < nch; ++ch) t += scratch[((ci * ngrp + grp) * nch + ch) * ROW + c * 9 + k];
-      acc[(co * cin + ci) * 9 + k] = t;
-    } else {
-      const int co = e - nw_, grp = co / WG_CG, c = co - grp * WG_CG;
-      for (int ch = 0; ch < nch; ++ch) t += scratch[((0 * ngrp + grp) * nch + ch) * ROW + WG_CG * 9 + c];
-      acc[nw_ + co] = t;
-    }
+  if (sb >= 0) STAMP(sb + 1);  // all units done
+  // combine the chunks of every entry in chunk order; weights [co][ci*9+k], then biases
+  const int nwt = cout * cin * 9;
+  for (int e = threadIdx.x; e < nwt + cout; e += blockDim.x) {
+    const int co = e < nwt ? e / (cin * 9) : e - nwt;
+    const int col = e < nwt ? e - co * cin * 9 : cin * 9;
+    const int tt = col >> 4, j = col & 15;
+    float v = 0.f;
+    for (int c = 0; c < nch; ++c) v += scratch[(c * nt + tt) * 256 + co * 16 + j];
+    acc[e] = v;
   }
 }
 
@@ -319,10 +337,12 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   float* a4 = a3 + C * PL14;             // C x 16x16
   float* p2 = a4 + C * PL14;             // C*49 (flat, NCHW)
   float* lg = p2 + C * 49;               // logits / dlogits [16]
-  float* wacc = lg + 16;                 // C*C*9 + C wgrad accumulators
-  float* wscr = wacc + C * C * 9 + C;    // conv_wgrad per-unit partial sums (16 waves x row)
-  const int total = CI * PL28 + 2 * C * PL28 + 3 * C * PL14 + C * 49 + 16 + C * C * 9 + C;
+  float* wacc = lg + 16;                 // max(C, CI)*C*9 + C wgrad accumulators
+  const int WC = C > CI ? C : CI;
+  float* wscr = wacc + WC * C * 9 + C;   // conv_wgrad per-unit 16x16 partial tiles (WG_SCRATCH floats)
+  const int total = CI * PL28 + 2 * C * PL28 + 3 * C * PL14 + C * 49 + 16 + WC * C * 9 + C;
   for (int i = threadIdx.x; i < total; i += blockDim.x) sm[i] = 0.f;
+  if (threadIdx.x == 0) { wscr[WG_SCRATCH] = 0.f; wscr[WG_SCRATCH + 1] = 1.f; }  // conv_wgrad pad cells
   __syncthreads();
   STAMP(0);
   // image load (+ ToTensor scaling)
@@ -401,7 +421,7 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   __syncthreads();
   STAMP(12);
   // conv4: dW4, db4 (from dz4, a3); then dz3 = convT(dz4) * relu'(a3) in a3
-  conv_wgrad<14, P14>(a4, a3, C, C, wacc, wscr);
+  conv_wgrad<14, P14>(a4, a3, C, C, wacc, wscr, 25);
   __syncthreads();
   STAMP(13);
   for (int e = threadIdx.x; e < C * C * 9 + C; e += blockDim.x) {
@@ -427,7 +447,7 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   __syncthreads();
   STAMP(17);
   // conv2: dW2 (dz2, a1); dz1 = convT(dz2) * relu'(a1) in a1
-  conv_wgrad<28, P28>(a2, a1, C, C, wacc, wscr);
+  conv_wgrad<28, P28>(a2, a1, C, C, wacc, wscr, 21);
   __syncthreads();
   STAMP(18);
   for (int e = threadIdx.x; e < C * C * 9 + C; e += blockDim.x) {
@@ -438,7 +458,7 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   __syncthreads();
   STAMP(19);
   // conv1: dW1 (dz1, x)
-  conv_wgrad<28, P28>(a1, xin, CI, C, wacc, wscr);
+  conv_wgrad<28, P28>(a1, xin, CI, C, wacc, wscr, 23);
   __syncthreads();
   STAMP(20);
   for (int e = threadIdx.x; e < C * CI * 9 + C; e += blockDim.x)
@@ -472,11 +492,10 @@ __global__ void cnn_loss_kernel(const float* __restrict__ row_loss, int B, float
 
 static size_t cnn_lds_bytes(const CNNArgs& g) {
   const int C = g.C, CI = g.cin;
-  // + conv_wgrad scratch: one row of WG_CG*10 floats per work unit
-  const int ngrp = (C + WG_CG - 1) / WG_CG;
-  const int rows = (C * ngrp > 2 * (CNN_THREADS / 64)) ? C * ngrp : 2 * (CNN_THREADS / 64);
-  return sizeof(float) * (size_t)(CI * PL28 + 2 * C * PL28 + 3 * C * PL14 + C * 49 + 16 + C * C * 9 + C + 4 +
-                                  rows * WG_CG * 10);
+  // + conv_wgrad scratch (WG_SCRATCH floats)
+  const int WC = C > CI ? C : CI;  // wgrad accumulators hold [C][max(C, CI)*9] + C
+  return sizeof(float) * (size_t)(CI * PL28 + 2 * C * PL28 + 3 * C * PL14 + C * 49 + 16 + WC * C * 9 + C + 4 +
+                                  WG_SCRATCH + 2);
 }
 
 extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {

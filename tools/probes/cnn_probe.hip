@@ -29,12 +29,26 @@ int main() {
   std::vector<unsigned long long> st(64 * 32);
   (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(cnn_stamps), st.size() * 8);
   int nph = 0;
-  for (int i = 0; i < 32; ++i) if (st[i]) nph = i + 1;
+  for (int i = 0; i < 21; ++i) if (st[i]) nph = i + 1;
   printf("phases %d\n", nph);
   for (int p = 1; p < nph; ++p) {
     double d = 0;
     for (int im = 0; im < B; ++im) d += (double)(st[im * 32 + p] - st[im * 32 + p - 1]);
     printf("phase %2d -> %2d: %8.0f ticks\n", p - 1, p, d / B);
+  }
+  // conv_wgrad sub-stamps (slot sb: wave 0's units done, sb+1: all units done; phase end = combine done)
+  const int sub[3][3] = {{21, 17, 18}, {23, 19, 20}, {25, 12, 13}};
+  const char* nm[3] = {"conv2 wgrad", "conv1 wgrad", "conv4 wgrad"};
+  for (int k = 0; k < 3; ++k) {
+    const int sb = sub[k][0], p0 = sub[k][1], p1 = sub[k][2];
+    if (!st[sb]) continue;
+    double u0 = 0, ua = 0, cb = 0;
+    for (int im = 0; im < B; ++im) {
+      u0 += (double)(st[im * 32 + sb] - st[im * 32 + p0]);
+      ua += (double)(st[im * 32 + sb + 1] - st[im * 32 + p0]);
+      cb += (double)(st[im * 32 + p1] - st[im * 32 + sb + 1]);
+    }
+    printf("%s: wave0 units %8.0f, all units %8.0f, combine+write %8.0f ticks\n", nm[k], u0 / B, ua / B, cb / B);
   }
   double tot = 0;
   for (int im = 0; im < B; ++im) tot += (double)(st[im * 32 + nph - 1] - st[im * 32]);
