@@ -53,10 +53,11 @@ int smi_gather_u8_scale(const void*, const long long*, void*, long, long, float,
 int smi_mlp_bwd(const MLPArgs*, hipStream_t);
 int smi_lstm(const LSTMArgs*, int, hipStream_t);
 int smi_lstm_supported(int, int, int, int);
-int smi_adam(float*, float*, float*, float*, void*, long, const float*, const float*, float, float, float, float, float,
+int smi_adam(float*, float*, float*, float*, void*, long, const float*, float*, unsigned*, float, float, float, float, float,
              int, int, hipStream_t);
-int smi_sgd(float*, float*, float*, void*, long, const float*, const float*, float, float, float, int, float, int,
+int smi_sgd(float*, float*, float*, void*, long, const float*, float*, unsigned*, float, float, float, int, float, int,
             hipStream_t);
+int smi_multi_copy(void* const*, const void* const*, const long*, int, hipStream_t);
 }
 
 static void chk(int rc, const char* what) {
@@ -140,15 +141,23 @@ PYBIND11_MODULE(_C, m) {
   m.def("cast_f32_bf16", [](u x, u y, long n, u st) { chk(smi_cast_f32_bf16(PF(x), P(y), n, S(st)), "cast_f32_bf16"); });
   m.def("add_bf16", [](u a, u b, u y, long n, u st) { chk(smi_add_bf16(P(a), P(b), P(y), n, S(st)), "add_bf16"); });
   m.def("step_inc", [](u step, u st) { chk(smi_step_inc(PF(step), S(st)), "step_inc"); });
-  m.def("adam", [](u p, u g, u mm, u v, u pbf, long n, u lr, u step, float b1, float b2, float eps, float wd,
+  // step: device step counter (advanced by the kernel); done: zeroed uint32 ticket word
+  m.def("adam", [](u p, u g, u mm, u v, u pbf, long n, u lr, u step, u done, float b1, float b2, float eps, float wd,
                    float gscale, int adamw, int zero_grad, u st) {
-    chk(smi_adam(PF(p), PF(g), PF(mm), PF(v), P(pbf), n, PF(lr), PF(step), b1, b2, eps, wd, gscale, adamw, zero_grad,
-                 S(st)), "adam");
+    chk(smi_adam(PF(p), PF(g), PF(mm), PF(v), P(pbf), n, PF(lr), PF(step), reinterpret_cast<unsigned*>(done), b1, b2,
+                 eps, wd, gscale, adamw, zero_grad, S(st)), "adam");
   });
-  m.def("sgd", [](u p, u g, u buf, u pbf, long n, u lr, u step, float mom, float damp, float wd, int nesterov,
+  m.def("sgd", [](u p, u g, u buf, u pbf, long n, u lr, u step, u done, float mom, float damp, float wd, int nesterov,
                   float gscale, int zero_grad, u st) {
-    chk(smi_sgd(PF(p), PF(g), PF(buf), P(pbf), n, PF(lr), PF(step), mom, damp, wd, nesterov, gscale, zero_grad, S(st)),
-        "sgd");
+    chk(smi_sgd(PF(p), PF(g), PF(buf), P(pbf), n, PF(lr), PF(step), reinterpret_cast<unsigned*>(done), mom, damp, wd,
+                nesterov, gscale, zero_grad, S(st)), "sgd");
+  });
+  m.def("multi_copy", [](std::vector<u> dst, std::vector<u> src, std::vector<long> bytes, u st) {
+    if (dst.size() != src.size() || dst.size() != bytes.size()) throw std::runtime_error("multi_copy: list sizes differ");
+    std::vector<void*> d(dst.size());
+    std::vector<const void*> s(src.size());
+    for (size_t i = 0; i < dst.size(); ++i) { d[i] = P(dst[i]); s[i] = reinterpret_cast<const void*>(src[i]); }
+    chk(smi_multi_copy(d.data(), s.data(), bytes.data(), (int)dst.size(), S(st)), "multi_copy");
   });
 
   // MLP: dims list, per-layer pointer lists (weights torch [out,in] layout, fp32)

@@ -47,6 +47,9 @@ __device__ __forceinline__ int i14(int c, int y, int x) { return c * PL14 + (y +
 // loads (global_load) or LDS reads — the vector form made the conv loops load-bound (~14x off).
 typedef const __attribute__((address_space(4))) float* cfp;
 
+// ticket of the in-kernel mean-loss reduction (one training step in flight per device)
+__device__ unsigned cnn_loss_ticket = 0u;
+
 // forward 3x3 conv + bias + relu over an HxH plane set; in/out padded with pitch PP.
 // Work unit = (output-channel group, 64-position chunk), one per wave: at 14 x 14 (196
 // positions = 4 chunks) the 16 waves split the output channels 4 ways, so every wave works
@@ -400,6 +403,28 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
       for (int o = 0; o < NC; ++o) lg[o] = (__expf(lg[o] - lse) - (o == lab ? 1.f : 0.f)) * g.loss_scale;
     }
   }
+  // mean loss without a second launch: the last workgroup to get here (atomic ticket) sums
+  // row_loss in image order with wave 0 and re-arms the ticket
+  if (g.loss && g.row_loss) {
+    __shared__ int cnn_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence();
+      cnn_last = atomicAdd(&cnn_loss_ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (cnn_last && threadIdx.x < 64) {
+      __threadfence();
+      float s = 0.f;
+      for (int i = threadIdx.x; i < g.B; i += 64)
+        s += __hip_atomic_load(g.row_loss + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s = wave_sum(s);
+      if (threadIdx.x == 0) {
+        g.loss[0] = s * g.loss_scale;
+        cnn_loss_ticket = 0u;
+      }
+    }
+  }
   if (!g.train) return;
   __syncthreads();
   STAMP(9);
@@ -480,16 +505,6 @@ __global__ void cnn_reduce_kernel(CNNArgs g) {
   }
 }
 
-__global__ void cnn_loss_kernel(const float* __restrict__ row_loss, int B, float scale, float* __restrict__ loss) {
-  float s = 0.f;
-  for (int i = threadIdx.x; i < B; i += blockDim.x) s += row_loss[i];
-  s = wave_sum(s);
-  __shared__ float part[4];
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) loss[0] = (part[0] + part[1] + part[2] + part[3]) * scale;
-}
-
 static size_t cnn_lds_bytes(const CNNArgs& g) {
   const int C = g.C, CI = g.cin;
   // + conv_wgrad scratch (WG_SCRATCH floats)
@@ -508,8 +523,6 @@ extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
   auto kern = g.C == 10 ? cnn_kernel<10, true> : cnn_kernel<CNN_MAXC, false>;
   hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(g.B), dim3(CNN_THREADS), lds, st, g);
-  if (g.loss && g.row_loss)
-    hipLaunchKernelGGL(cnn_loss_kernel, dim3(1), dim3(256), 0, st, g.row_loss, g.B, g.loss_scale, g.loss);
   SMI_CHECK_LAUNCH();
 }
 

@@ -16,6 +16,8 @@ class _FlatOptimizer:
         dev = flat.device
         self.lr_t = torch.tensor([float(lr)], dtype=torch.float32, device=dev)
         self.step_t = torch.zeros(1, dtype=torch.float32, device=dev)
+        # ticket word of the update kernel's in-kernel step advance (csrc/kernels/optim.hip)
+        self.done_t = torch.zeros(1, dtype=torch.int32, device=dev)
         self.grad_scale = 1.0
         self.zero_grad_after_step = True
 
@@ -53,9 +55,8 @@ class Adam(_FlatOptimizer):
         if _native.use_native(f.master):
             C = _native.C()
             st = _native.stream()
-            C.step_inc(self.step_t.data_ptr(), st)
             C.adam(f.master.data_ptr(), f.grad.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), _native.ptr(f.shadow),
-                   f.numel, self.lr_t.data_ptr(), self.step_t.data_ptr(), self.b1, self.b2, self.eps,
+                   f.numel, self.lr_t.data_ptr(), self.step_t.data_ptr(), self.done_t.data_ptr(), self.b1, self.b2, self.eps,
                    self.weight_decay, self.grad_scale, int(self.adamw), int(self.zero_grad_after_step), st)
             return
         with torch.no_grad():

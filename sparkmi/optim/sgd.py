@@ -17,9 +17,8 @@ class SGD(_FlatOptimizer):
         if _native.use_native(f.master):
             C = _native.C()
             st = _native.stream()
-            C.step_inc(self.step_t.data_ptr(), st)
             C.sgd(f.master.data_ptr(), f.grad.data_ptr(), _native.ptr(self.buf), _native.ptr(f.shadow), f.numel,
-                  self.lr_t.data_ptr(), self.step_t.data_ptr(), self.momentum, self.dampening, self.weight_decay,
+                  self.lr_t.data_ptr(), self.step_t.data_ptr(), self.done_t.data_ptr(), self.momentum, self.dampening, self.weight_decay,
                   int(self.nesterov), self.grad_scale, int(self.zero_grad_after_step), st)
             return
         with torch.no_grad():

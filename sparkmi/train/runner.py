@@ -52,9 +52,30 @@ class StepRunner:
         if rng is not None:
             rng.advance()
         loss = self.loss_fn(self.model, *batch)
-        loss.backward()
+        loss.backward(self._seed(loss))
         _grad.join()
         return loss.detach()
+
+    def _seed(self, loss):
+        """Persistent d(loss)/d(loss) = 1 (``backward()`` without it materialises ones_like
+        every step: one fill launch inside every replayed graph)."""
+        s = getattr(self, "_seed_t", None)
+        if s is None or s.shape != loss.shape or s.dtype != loss.dtype or s.device != loss.device:
+            s = self._seed_t = torch.ones_like(loss)
+        return s
+
+    def _refresh_inputs(self, batch):
+        """Copy the step's inputs into the graph's static buffers: one multi-buffer copy launch
+        on the GPU (one blit launch per input otherwise)."""
+        from .. import _native
+        st = self.static_in
+        if (len(batch) <= 8 and all(b.is_cuda and b.is_contiguous() and b.shape == d.shape and b.dtype == d.dtype
+                                    for b, d in zip(batch, st)) and _native.use_native(st[0])):
+            _native.C().multi_copy([d.data_ptr() for d in st], [b.data_ptr() for b in batch],
+                                   [b.numel() * b.element_size() for b in batch], _native.stream())
+            return
+        for dst, src in zip(st, batch):
+            dst.copy_(src, non_blocking=True)
 
     def _eager(self, *batch):
         loss = self._fwd_bwd(*batch)
@@ -68,7 +89,7 @@ class StepRunner:
         if rng is not None:
             rng.advance()
         loss, segments = self.split_fn(self.model, *batch)
-        loss.backward()
+        loss.backward(self._seed(loss))
         _grad.join()
         return loss.detach(), segments
 
@@ -139,8 +160,7 @@ class StepRunner:
             return self._eager(*batch)
         if self.graph is None:
             self._capture(batch)  # then replayed below for this step
-        for dst, src in zip(self.static_in, batch):
-            dst.copy_(src, non_blocking=True)
+        self._refresh_inputs(batch)
         self.graph.replay()
         if self.graph2 is not None:
             # after each backward piece, its final buckets go to RCCL while the next piece runs

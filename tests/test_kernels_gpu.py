@@ -186,6 +186,51 @@ def test_adam_sgd_flat():
             og.step()
         _close(fg.master, fc.master, 1e-5, 1e-5, Opt.__name__)
         _close(fg.shadow, fg.master, 1e-2, 1e-2, "shadow")
+        assert float(og.step_t.item()) == 3.0
+
+
+def test_optimizer_step_counter_many_blocks_graph():
+    """The update kernels advance the device step counter themselves (last block's ticket):
+    check it with a multi-thousand-block grid, eagerly and inside a replayed HIP graph, against
+    torch.optim.Adam (bias corrections depend on the count)."""
+    from sparkmi.optim import Adam
+    from sparkmi.utils.flat import FlatParams
+    torch.manual_seed(6)
+    mc = torch.nn.Linear(2048, 1024)
+    mg = torch.nn.Linear(2048, 1024).to(dev)
+    mg.load_state_dict(mc.state_dict())
+    fg = FlatParams(mg)
+    og = Adam(fg, lr=1e-3)
+    ref = torch.optim.Adam(mc.parameters(), lr=1e-3)
+    grads = [torch.randn(fg.numel) for _ in range(6)]
+
+    pairs = list(zip(mc.parameters(), mg.parameters()))
+
+    def ref_step(g):  # the flat layout is padded and in reverse order: map through param_range
+        for pc, pg in pairs:
+            a, b = fg.param_range(pg)
+            pc.grad = g[a:b].view_as(pc).clone()
+        ref.step()
+
+    for g in grads[:2]:
+        fg.grad.copy_(g.to(dev))
+        og.step()
+        ref_step(g)
+    static_g = torch.empty(fg.numel, device=dev)
+    graph = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(graph):
+        fg.grad.copy_(static_g)
+        og.step()
+    for g in grads[2:]:
+        static_g.copy_(g.to(dev))
+        graph.replay()
+        ref_step(g)
+    torch.cuda.synchronize()
+    assert float(og.step_t.item()) == 6.0
+    for pc, pg in pairs:
+        a, b = fg.param_range(pg)
+        _close(fg.master[a:b].cpu(), pc.detach().reshape(-1), 1e-5, 1e-5, "adam graph")
 
 
 def test_transformer_gpu_vs_cpu():
