@@ -9,6 +9,10 @@ not the reference script); it exists only to put sparkmi's number next to what s
 does on the same MI355X.  Prints one JSON line.
 
     python tools/bench_torch_baseline.py [--steps 20 --warmup 5 --batch 32 --seq 256 --layers 6]
+    python tools/bench_torch_baseline.py --model cnn|lstm|mlp [--steps 200]
+
+``--model cnn|lstm|mlp``: the other three reference workloads in stock torch.nn (MIOpen convs,
+cuDNN-style fused nn.LSTM, nn.Linear MLP), same shapes/optimizers as bench.py's extras, eager.
 """
 import argparse
 import json
@@ -84,8 +88,74 @@ class Seq2Seq(nn.Module):
         return self.head(y)
 
 
+def _time(step, warmup, steps):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0, loss
+
+
+def small_model(a):
+    """distributed_cnn.py / distributed_lstm.py / distributed_multilayer_perceptron.py shapes."""
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    if a.model == "cnn":
+        B = 32
+        m = nn.Sequential(nn.Conv2d(1, 10, 3, padding=1), nn.ReLU(), nn.Conv2d(10, 10, 3, padding=1), nn.ReLU(),
+                          nn.MaxPool2d(2), nn.Conv2d(10, 10, 3, padding=1), nn.ReLU(), nn.Conv2d(10, 10, 3, padding=1),
+                          nn.ReLU(), nn.MaxPool2d(2), nn.Flatten(), nn.Linear(490, 10)).to(dev)
+        opt = torch.optim.SGD(m.parameters(), lr=0.01)
+        x = torch.rand(B, 1, 28, 28, device=dev)
+        y = torch.randint(0, 10, (B,), device=dev)
+        fwd = lambda: F.cross_entropy(m(x), y)  # noqa: E731
+    elif a.model == "lstm":
+        B, T, V = 32, 129, 95812
+
+        class L(nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.emb = nn.Embedding(V, 32, padding_idx=7)
+                self.lstm = nn.LSTM(32, 32, num_layers=2, batch_first=True, dropout=0.5)
+                self.fc = nn.Linear(32, 4)
+
+            def forward(self, t):
+                h, _ = self.lstm(self.emb(t))
+                return self.fc(h)
+
+        m = L().to(dev)
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+        x = torch.randint(0, V, (B, T), device=dev)
+        y = torch.randint(0, 4, (B,), device=dev)
+        fwd = lambda: F.cross_entropy(m(x)[:, -1, :], y)  # noqa: E731
+    else:
+        B = 30
+        m = nn.Sequential(nn.Linear(4, 5), nn.Sigmoid(), nn.Linear(5, 4), nn.Sigmoid(), nn.Linear(4, 3)).to(dev)
+        opt = torch.optim.SGD(m.parameters(), lr=0.01)
+        x = torch.rand(B, 4, device=dev) * 2 - 1
+        y = torch.randint(0, 3, (B,), device=dev)
+        fwd = lambda: F.cross_entropy(m(x), y)  # noqa: E731
+    m.train()
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss = fwd()
+        loss.backward()
+        opt.step()
+        return loss
+
+    dt, loss = _time(step, a.warmup, a.steps)
+    print(json.dumps({"metric": f"stock PyTorch eager {a.model} samples/s (1 GPU)", "value": round(B * a.steps / dt, 1),
+                      "ms_per_step": round(dt / a.steps * 1000, 4), "batch": B, "dtype": "fp32",
+                      "final_loss": round(float(loss), 4), "torch": torch.__version__}))
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="transformer", choices=["transformer", "cnn", "lstm", "mlp"])
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32)
@@ -93,6 +163,8 @@ def main():
     ap.add_argument("--layers", type=int, default=6)
     ap.add_argument("--vocab", type=int, default=10000)
     a = ap.parse_args()
+    if a.model != "transformer":
+        return small_model(a)
     dev = torch.device("cuda")
     torch.manual_seed(0)
     m = Seq2Seq(a.layers, 512, 8, 1024, a.vocab, a.vocab, a.seq).to(dev).train()
