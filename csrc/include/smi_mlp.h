@@ -16,7 +16,7 @@ struct MLPArgs {
   float* gW[MLP_MAXL];
   float* gb[MLP_MAXL];
   float* logits;             // optional [n, C]
-  float* loss;               // scalar, accumulated
+  float* loss;               // scalar, written (mean loss of the whole batch)
   const float* dloss;        // scalar upstream gradient (bwd)
   int act;                   // 1 relu, 2 sigmoid
 };

@@ -496,8 +496,16 @@ __global__ void cnn_reduce_kernel(CNNArgs g) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   const float dl = g.dloss ? g.dloss[0] : 1.f;
   if (p < g.P) {
-    float s = 0.f;
-    for (int i = 0; i < g.B; ++i) s += g.slab[(long)i * g.P + p];
+    // 8 independent partial sums: all 8 loads of a round are in flight together (a plain
+    // serial loop waited one memory round trip per image: 10 us for 32 images), fixed order
+    float q[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int i = 0;
+    for (; i + 8 <= g.B; i += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q[j] += g.slab[(long)(i + j) * g.P + p];
+    }
+    for (int j = 0; i < g.B; ++i, ++j) q[j] += g.slab[(long)i * g.P + p];
+    const float s = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
     int seg = 0;
     while (seg < 9 && p >= g.off[seg + 1]) ++seg;
     float* dst = seg % 2 == 0 ? g.gw[seg / 2] : g.gb[seg / 2];

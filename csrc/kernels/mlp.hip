@@ -50,6 +50,9 @@ __device__ __forceinline__ float mlp_forward_row(const MLPArgs& a, int row, floa
   return lse - z[lab];
 }
 
+__device__ unsigned mlp_loss_ticket = 0u;
+__device__ float mlp_loss_part[1024];  // per-block partial losses (grid <= 1024, mlp_grid)
+
 #define MLP_ACT_LD (MLP_ACT_STRIDE + 1)        // odd LDS pitch: lane-private rows on distinct banks
 #define MLP_DEL_LD (MLP_MAXW * MLP_MAXL + 1)
 
@@ -69,7 +72,27 @@ __global__ __launch_bounds__(64) void mlp_fwd_kernel(MLPArgs a) {
     }
   }
   lsum = wave_sum(lsum);
-  if (threadIdx.x == 0 && a.loss) atomicAdd(a.loss, lsum);
+  if (!a.loss) return;
+  // mean loss without a zeroed accumulator (one fill launch per step): per-block partials, the
+  // last block (atomic ticket) adds them in block order and re-arms the ticket
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    mlp_loss_part[blockIdx.x] = lsum;
+    __threadfence();
+    last = atomicAdd(&mlp_loss_ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (last) {
+    __threadfence();
+    float s = 0.f;
+    for (int i = threadIdx.x; i < (int)gridDim.x; i += 64)
+      s += __hip_atomic_load(mlp_loss_part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s = wave_sum(s);
+    if (threadIdx.x == 0) {
+      a.loss[0] = s;
+      mlp_loss_ticket = 0u;
+    }
+  }
 }
 
 __global__ __launch_bounds__(64) void mlp_bwd_kernel(MLPArgs a) {

@@ -33,7 +33,7 @@ class MLPLossFn(torch.autograd.Function):
         y = y.to(torch.int64).contiguous()
         ctx.save_for_backward(x, y, row_weight, *params)
         if ctx.native:
-            loss = torch.zeros(1, device=x.device, dtype=torch.float32)
+            loss = torch.empty(1, device=x.device, dtype=torch.float32)  # written by the kernel
             dims = [Ws[0].shape[1]] + [W.shape[0] for W in Ws]
             _native.C().mlp(0, x.data_ptr(), y.data_ptr(), _native.ptr(row_weight), x.shape[0], dims,
                             [W.data_ptr() for W in Ws], [b.data_ptr() for b in bs], [], [], 0, loss.data_ptr(), 0,
