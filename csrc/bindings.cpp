@@ -28,6 +28,8 @@ int smi_ln_fwd(const void*, const void*, const float*, const float*, void*, void
 int smi_ln_bwd(const void*, const void*, const float*, const float*, const float*, void*, void*, const void*, float*,
                float*, int, float*, float*, int, int, int, const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
 int smi_ln_bwd_reduce(const float*, const float*, int, int, float*, float*, int, hipStream_t);
+int smi_ln_bwd_reduce_multi(const float* const*, const float* const*, float* const*, float* const*, const int*, const int*,
+                            int, int, hipStream_t);
 int smi_attn_fwd(const AttnFwdArgs*, hipStream_t);
 int smi_attn_bwd(const AttnBwdArgs*, const void*, float*, hipStream_t);
 int smi_ce_fwd(const void*, int, const long long*, int, int, long long, float*, float*, float*, float*, hipStream_t);
@@ -78,6 +80,17 @@ PYBIND11_MODULE(_C, m) {
                      u dbeta, int accumulate, int M, int D, u seedp, uint32_t salt, uint32_t thresh, float dscale, u st) {
     chk(smi_ln_bwd(P(dy), P(xs), PF(mean), PF(rstd), PF(gamma), P(dres), P(dh), P(dres_add), PF(pg), PF(pb), nblocks,
                    PF(dgamma), PF(dbeta), accumulate, M, D, (const uint32_t*)seedp, salt, thresh, dscale, S(st)), "ln_bwd");
+  });
+  m.def("ln_bwd_reduce_multi", [](std::vector<u> pg, std::vector<u> pb, std::vector<u> og, std::vector<u> ob,
+                                  std::vector<int> nb, std::vector<int> D, int accumulate, u st) {
+    const size_t n = pg.size();
+    if (pb.size() != n || og.size() != n || ob.size() != n || nb.size() != n || D.size() != n)
+      throw std::runtime_error("ln_bwd_reduce_multi: list sizes differ");
+    std::vector<const float*> a(n), b(n);
+    std::vector<float*> c(n), d(n);
+    for (size_t i = 0; i < n; ++i) { a[i] = PF(pg[i]); b[i] = PF(pb[i]); c[i] = PF(og[i]); d[i] = PF(ob[i]); }
+    chk(smi_ln_bwd_reduce_multi(a.data(), b.data(), c.data(), d.data(), nb.data(), D.data(), (int)n, accumulate, S(st)),
+        "ln_bwd_reduce_multi");
   });
   m.def("ln_bwd_reduce", [](u pg, u pb, int nb, int D, u dgamma, u dbeta, int accumulate, u st) {
     chk(smi_ln_bwd_reduce(PF(pg), PF(pb), nb, D, PF(dgamma), PF(dbeta), accumulate, S(st)), "ln_bwd_reduce");

@@ -135,3 +135,40 @@ class ResidualGrad:
     def take(self):
         g, self.grad = self.grad, None
         return g
+
+
+# ---- deferred LayerNorm dgamma/dbeta folds ----
+# Each LayerNorm backward leaves per-block partial rows; instead of one small fold launch per
+# LayerNorm (30 per transformer step, ~5 us each), the folds are queued and run as ONE batched
+# launch at the end of the backward (autograd final callback), after which the parameters are
+# reported ready (DDP bucket hooks / split-graph ready sets see them at the end of their
+# backward piece).  SPARKMI_LN_DEFER=0 restores the per-LayerNorm fold.
+LN_DEFER = os.environ.get("SPARKMI_LN_DEFER", "1") != "0"
+_ln_queue = []
+_ln_cb = [False]
+
+
+def defer_ln_fold(part_g, part_b, nb, D, gg, gb, params, stream):
+    _ln_queue.append((part_g, part_b, nb, D, gg, gb, params, stream))
+    if not _ln_cb[0]:
+        _ln_cb[0] = True
+        torch.autograd.Variable._execution_engine.queue_callback(flush_ln_folds)
+
+
+def flush_ln_folds():
+    from .. import _native
+    _ln_cb[0] = False
+    q = list(_ln_queue)
+    _ln_queue.clear()
+    by_stream = {}
+    for e in q:
+        by_stream.setdefault(e[7], []).append(e)
+    C = _native.C()
+    for st, es in by_stream.items():
+        for i in range(0, len(es), 32):
+            ch = es[i:i + 32]
+            C.ln_bwd_reduce_multi([e[0].data_ptr() for e in ch], [e[1].data_ptr() for e in ch],
+                                  [e[4].data_ptr() for e in ch], [e[5].data_ptr() for e in ch],
+                                  [e[2] for e in ch], [e[3] for e in ch], 1, st)
+    for e in q:
+        grad_ready(*e[6])

@@ -74,10 +74,13 @@ class AddDropoutLayerNorm(torch.autograd.Function):
             C.ln_bwd(dy.data_ptr(), xs.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(),
                      _native.ptr(dres), dh.data_ptr(), 0, part[0].data_ptr(), part[1].data_ptr(), nb,
                      0, 0, 1, M, D, ctx.rng.ptr(), ctx.salt, _rng.threshold(p), _rng.scale(p), _native.stream())
-            # dgamma / dbeta are off the critical path: reduce the partial rows on the side stream
-            with _grad.side(dy.device, part):
-                C.ln_bwd_reduce(part[0].data_ptr(), part[1].data_ptr(), nb, D, gg.data_ptr(), gb.data_ptr(), 1,
-                                _native.stream())
+            if _grad.LN_DEFER:  # folded with every other LayerNorm's at the end of the backward
+                _grad.defer_ln_fold(part[0], part[1], nb, D, gg, gb, (gamma, beta), _native.stream())
+            else:
+                # dgamma / dbeta are off the critical path: reduce the partial rows on the side stream
+                with _grad.side(dy.device, part):
+                    C.ln_bwd_reduce(part[0].data_ptr(), part[1].data_ptr(), nb, D, gg.data_ptr(), gb.data_ptr(), 1,
+                                    _native.stream())
         else:
             x = xs.reshape(M, D).float()
             g = dy.reshape(M, D).float()
@@ -91,7 +94,8 @@ class AddDropoutLayerNorm(torch.autograd.Function):
             if p > 0:
                 dhh = dhh * _rng.keep_mask((M, D), p, ctx.seed, ctx.salt, dx.device).to(dx.dtype) * _rng.scale(p)
             dh = dhh.reshape(dy.shape).to(dy.dtype)
-        grad_ready(gamma, beta)
+        if not (ctx.native and _grad.LN_DEFER):
+            grad_ready(gamma, beta)
         if ctx.r_slot is not None and dres is not None:
             ctx.r_slot.grad = dres  # added by the sibling linear's dgrad epilogue instead
             dres = None
