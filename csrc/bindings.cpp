@@ -47,6 +47,8 @@ int smi_step_inc(float*, hipStream_t);
 int smi_mlp_fwd(const MLPArgs*, hipStream_t);
 int smi_gemm(const GemmArgs*, hipStream_t);
 int smi_splitk_reduce(const float*, int, long, float*, long, float*, int, hipStream_t);
+int smi_splitk_fold_multi(const float* const*, float* const*, float* const*, const long*, const int*, const int*, int,
+                          hipStream_t);
 void smi_gemm_set_bm(int);
 int smi_cnn(const CNNArgs*, hipStream_t);
 int smi_cnn_reduce(const CNNArgs*, hipStream_t);
@@ -223,6 +225,17 @@ PYBIND11_MODULE(_C, m) {
   });
   // out[n] (+)= sum_s slab[s][:n]; with bout, also bout[nb] (+)= sum_s bias_slab[s][:nb] where the
   // bias slabs follow the weight slabs (slab + splits * n) — one launch for both
+  m.def("splitk_fold_multi", [](std::vector<u> slab, std::vector<u> out, std::vector<u> bout, std::vector<long> n,
+                                std::vector<int> nb, std::vector<int> splits, u st) {
+    const size_t c = slab.size();
+    if (out.size() != c || bout.size() != c || n.size() != c || nb.size() != c || splits.size() != c)
+      throw std::runtime_error("splitk_fold_multi: list sizes differ");
+    std::vector<const float*> a(c);
+    std::vector<float*> o(c), bo(c);
+    for (size_t i = 0; i < c; ++i) { a[i] = PF(slab[i]); o[i] = PF(out[i]); bo[i] = PF(bout[i]); }
+    chk(smi_splitk_fold_multi(a.data(), o.data(), bo.data(), n.data(), nb.data(), splits.data(), (int)c, S(st)),
+        "splitk_fold_multi");
+  });
   m.def("splitk_reduce", [](u slab, int splits, long n, u out, long nb, u bout, int accumulate, u st) {
     chk(smi_splitk_reduce((const float*)slab, splits, n, (float*)out, nb, (float*)bout, accumulate, S(st)),
         "splitk_reduce");

@@ -663,3 +663,78 @@ extern "C" int smi_splitk_reduce(const float* slab, int splits, long n, float* o
 #undef SMI_RED
   SMI_CHECK_LAUNCH();
 }
+
+// Deferred split-K folds of many weight-gradient GEMMs in ONE launch (sparkmi/ops/_grad.py:
+// queued during the backward, flushed by the autograd final callback).  Entry e owns blocks
+// [blk0[e], blk0[e+1]): its weight float4s first (one per thread), then its bias elements.
+// Outputs of one batch are distinct (the host splits batches on a repeated output).
+#define FOLD_MAX 64
+struct FoldBatch {
+  const float* slab[FOLD_MAX]; float* out[FOLD_MAX]; float* bout[FOLD_MAX];
+  long n[FOLD_MAX]; int nb[FOLD_MAX]; int splits[FOLD_MAX]; int wblk[FOLD_MAX];
+  int blk0[FOLD_MAX + 1]; int count;
+};
+__global__ __launch_bounds__(256) void splitk_fold_multi_kernel(FoldBatch a) {
+  const int b = blockIdx.x;
+  int e = 0;
+  while (e + 1 < a.count && b >= a.blk0[e + 1]) ++e;  // wave-uniform scan over <= 64 entries
+  const int lb = b - a.blk0[e];
+  const float* slab = a.slab[e];
+  const long n = a.n[e];
+  const int S = a.splits[e];
+  if (lb < a.wblk[e]) {
+    const long n4 = n / 4;
+    const long i = (long)lb * 256 + threadIdx.x;
+    if (i < n4) {
+      float4 acc = ((const float4*)a.out[e])[i];
+      if (S <= 16) {  // all split loads in flight, then summed in split order
+        float4 p[16];
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2)
+          if (s2 < S) p[s2] = ((const float4*)(slab + (long)s2 * n))[i];
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2)
+          if (s2 < S) { acc.x += p[s2].x; acc.y += p[s2].y; acc.z += p[s2].z; acc.w += p[s2].w; }
+      } else {
+        for (int s2 = 0; s2 < S; ++s2) {
+          const float4 v = ((const float4*)(slab + (long)s2 * n))[i];
+          acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
+      }
+      ((float4*)a.out[e])[i] = acc;
+    }
+    if (lb == 0)  // n % 4 tail
+      for (long t = n4 * 4 + threadIdx.x; t < n; t += 256) {
+        float acc = a.out[e][t];
+        for (int s2 = 0; s2 < S; ++s2) acc += slab[(long)s2 * n + t];
+        a.out[e][t] = acc;
+      }
+  } else {
+    const long i = (long)(lb - a.wblk[e]) * 256 + threadIdx.x;
+    if (i < a.nb[e]) {
+      const float* bslab = slab + (long)S * n;
+      float acc = a.bout[e][i];
+      for (int s2 = 0; s2 < S; ++s2) acc += bslab[(long)s2 * a.nb[e] + i];
+      a.bout[e][i] = acc;
+    }
+  }
+}
+
+extern "C" int smi_splitk_fold_multi(const float* const* slab, float* const* out, float* const* bout, const long* n,
+                                     const int* nb, const int* splits, int count, hipStream_t st) {
+  if (count < 1 || count > FOLD_MAX) return -1;
+  FoldBatch a{};
+  int tot = 0;
+  for (int i = 0; i < count; ++i) {
+    a.slab[i] = slab[i]; a.out[i] = out[i]; a.bout[i] = bout[i]; a.n[i] = n[i];
+    a.nb[i] = bout[i] ? nb[i] : 0; a.splits[i] = splits[i];
+    a.wblk[i] = (int)((n[i] / 4 + 255) / 256);
+    if (a.wblk[i] < 1) a.wblk[i] = 1;
+    a.blk0[i] = tot;
+    tot += a.wblk[i] + (a.nb[i] + 255) / 256;
+  }
+  a.blk0[count] = tot;
+  a.count = count;
+  hipLaunchKernelGGL(splitk_fold_multi_kernel, dim3((unsigned)tot), dim3(256), 0, st, a);
+  SMI_CHECK_LAUNCH();
+}

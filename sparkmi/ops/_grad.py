@@ -143,32 +143,69 @@ class ResidualGrad:
 # launch at the end of the backward (autograd final callback), after which the parameters are
 # reported ready (DDP bucket hooks / split-graph ready sets see them at the end of their
 # backward piece).  SPARKMI_LN_DEFER=0 restores the per-LayerNorm fold.
-LN_DEFER = os.environ.get("SPARKMI_LN_DEFER", "1") != "0"
+LN_DEFER = os.environ.get("SPARKMI_LN_DEFER", "1") != "0" and not _SIDE_ENABLED
 _ln_queue = []
-_ln_cb = [False]
+_cb = [False]
+
+
+def _queue_flush():
+    if not _cb[0]:
+        _cb[0] = True
+        torch.autograd.Variable._execution_engine.queue_callback(flush_deferred)
 
 
 def defer_ln_fold(part_g, part_b, nb, D, gg, gb, params, stream):
     _ln_queue.append((part_g, part_b, nb, D, gg, gb, params, stream))
-    if not _ln_cb[0]:
-        _ln_cb[0] = True
-        torch.autograd.Variable._execution_engine.queue_callback(flush_ln_folds)
+    _queue_flush()
 
 
-def flush_ln_folds():
+# ---- deferred split-K weight-gradient folds ----
+# Same idea for the split-K slabs of the weight-gradient GEMMs (sparkmi/ops/gemm.py:wgrad):
+# one fold launch per Linear (66 per transformer step) becomes one batched launch per backward
+# piece; the slabs stay alive until then.  SPARKMI_FOLD_DEFER=0 folds each GEMM immediately.
+FOLD_DEFER = os.environ.get("SPARKMI_FOLD_DEFER", "1") != "0" and not _SIDE_ENABLED
+_fold_queue = []
+
+
+def defer_wgrad_fold(slab, splits, n, gw, nb, gb, params, stream):
+    _fold_queue.append((slab, splits, n, gw, nb, gb, params, stream))
+    _queue_flush()
+
+
+def flush_deferred():
     from .. import _native
-    _ln_cb[0] = False
-    q = list(_ln_queue)
+    _cb[0] = False
+    C = _native.C()
+    lq = list(_ln_queue)
     _ln_queue.clear()
     by_stream = {}
-    for e in q:
+    for e in lq:
         by_stream.setdefault(e[7], []).append(e)
-    C = _native.C()
     for st, es in by_stream.items():
         for i in range(0, len(es), 32):
             ch = es[i:i + 32]
             C.ln_bwd_reduce_multi([e[0].data_ptr() for e in ch], [e[1].data_ptr() for e in ch],
                                   [e[4].data_ptr() for e in ch], [e[5].data_ptr() for e in ch],
                                   [e[2] for e in ch], [e[3] for e in ch], 1, st)
-    for e in q:
+    fq = list(_fold_queue)
+    _fold_queue.clear()
+    by_stream = {}
+    for e in fq:
+        by_stream.setdefault(e[7], []).append(e)
+    for st, es in by_stream.items():
+        batch, outs = [], set()
+        for e in es + [None]:
+            # a batch's outputs must be distinct (its blocks run concurrently)
+            if e is None or len(batch) == 64 or e[3].data_ptr() in outs:
+                if batch:
+                    C.splitk_fold_multi([b[0].data_ptr() for b in batch], [b[3].data_ptr() for b in batch],
+                                        [b[5].data_ptr() if b[5] is not None else 0 for b in batch],
+                                        [b[2] for b in batch], [b[4] for b in batch], [b[1] for b in batch], st)
+                batch, outs = [], set()
+            if e is not None:
+                batch.append(e)
+                outs.add(e[3].data_ptr())
+    for e in lq:
+        grad_ready(*e[6])
+    for e in fq:
         grad_ready(*e[6])

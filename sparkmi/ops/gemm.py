@@ -12,6 +12,7 @@ import os
 import torch
 
 from .. import _native
+from . import _grad
 
 # Per-shape implementation choice between sparkmi's MFMA kernel (with its fused epilogue) and
 # hipBLASLt (+ a separate HIP epilogue kernel), measured once per (op, shape, epilogue) on the
@@ -112,14 +113,18 @@ def _actual_splits(M, s):
     return (M + kps - 1) // kps
 
 
-def wgrad(dy, x, gw, splits=None, gb=None):
+def wgrad(dy, x, gw, splits=None, gb=None, ready=None):
     """gw [N,K] fp32 += dy[M,N]^T @ x[M,K]; with ``gb`` also gb[N] += column sums of dy (the bias
     gradient, computed inside the same kernel by an extra MFMA per dy fragment).
 
     Split-K over M.  Slab mode (default): every split writes its partial tile to an fp32 slab
     with plain stores and one vectorised pass folds the slabs into ``gw`` — deterministic, and
     cheaper than fp32 atomics (which serialise at ~1.3 TB/s chip-wide: 16 splits of a 512x512
-    gradient = 16 MB of atomic traffic).  Atomic mode accumulates straight into ``gw``."""
+    gradient = 16 MB of atomic traffic).  Atomic mode accumulates straight into ``gw``.
+
+    ``ready`` (the parameters whose gradients this completes): when given, the slab fold is
+    queued (sparkmi/ops/_grad.py: one batched fold launch at the end of the backward, which then
+    reports ``ready`` final) and True is returned; the caller must not report them itself."""
     M, N = dy.shape
     K = x.shape[1]
     s = splits or wgrad_splits(N, K, M)
@@ -130,6 +135,9 @@ def wgrad(dy, x, gw, splits=None, gb=None):
         bslab = slab[s * N * K:] if gb is not None else None
         C.gemm_wgrad_slab(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), N, K, M, slab.data_ptr(), s,
                           _native.ptr(bslab), _native.stream())
+        if ready is not None and _grad.FOLD_DEFER:
+            _grad.defer_wgrad_fold(slab, s, N * K, gw, N if gb is not None else 0, gb, ready, _native.stream())
+            return True
         C.splitk_reduce(slab.data_ptr(), s, N * K, gw.data_ptr(), N if gb is not None else 0, _native.ptr(gb), 1,
                         _native.stream())
         return gw

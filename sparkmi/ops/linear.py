@@ -35,9 +35,11 @@ def _blaslt_wgrad(gw, dy2, x2):
         gw.add_(torch.mm(dy2.t(), x2).float())
 
 
-def _wgrad_accumulate(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, gb=None):
+def _wgrad_accumulate(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, gb=None, ready=None):
     """gw (fp32 [N,K]) += dy2^T @ x2 with fp32 accumulation on the GPU; gb (fp32 [N], optional)
-    += column sums of dy2 — fused into sparkmi's wgrad kernel, a column-sum kernel otherwise."""
+    += column sums of dy2 — fused into sparkmi's wgrad kernel, a column-sum kernel otherwise.
+    Returns True when the split-K fold was deferred (then ``ready`` is reported final by the
+    end-of-backward flush, sparkmi/ops/_grad.py); otherwise the caller reports it."""
     N, K = gw.shape
     M = dy2.shape[0]
     if G.supported(N, K, M, dy2, x2, mode=2) and gw.is_contiguous():
@@ -52,11 +54,11 @@ def _wgrad_accumulate(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, gb=
                     _colsum(dy2, bscr)
             G.choose(key, lambda: G.wgrad(dy2, x2, scratch, gb=bscr), run_blaslt)
         if G.choose(key, None, None) == "smi":
-            G.wgrad(dy2, x2, gw, gb=gb)
-            return
+            return G.wgrad(dy2, x2, gw, gb=gb, ready=ready) is True
     _blaslt_wgrad(gw, dy2, x2)
     if gb is not None:
         _colsum(dy2, gb)
+    return False
 
 
 def _blaslt_dgrad(g2, w_bf, resid, dact_y, dscale):
@@ -176,7 +178,7 @@ class LinearFn(torch.autograd.Function):
             dx = _dgrad(g2, bf16_weight(weight), resid=resid) if ctx.needs_input_grad[0] else None
             bgrad = grad_buf(bias) if bias is not None else None
             with _grad.side(g2.device, g2, x2):
-                _wgrad_accumulate(gw, g2, x2, bgrad)
+                deferred = _wgrad_accumulate(gw, g2, x2, bgrad, ready=(weight, bias))
         else:
             g2 = _ref_act_bwd(dy2.float(), y2, act, p, ctx.seed, ctx.salt)
             resid = _slot_grad(ctx.x_slot, g2.shape[0])
@@ -189,7 +191,9 @@ class LinearFn(torch.autograd.Function):
             gw.add_(g2.t() @ x2.float())
             if bias is not None:
                 grad_buf(bias).add_(g2.sum(0))
-        grad_ready(weight, bias)
+            deferred = False
+        if not deferred:
+            grad_ready(weight, bias)
         if dx is not None:
             dx = dx.reshape(*dy.shape[:-1], K)
         return dx, None, None, None, None, None, None, None
@@ -250,13 +254,13 @@ class FFNFn(torch.autograd.Function):
             dh = _dgrad(dy2, bf16_weight(w2), dact_y=h, dscale=_rng.scale(p))
             gw2, gb2, gw1, gb1 = grad_buf(w2), grad_buf(b2), grad_buf(w1), grad_buf(b1)
             with _grad.side(dy2.device, dy2, h):
-                _wgrad_accumulate(gw2, dy2, h, gb2)
-            grad_ready(w2, b2)
+                if not _wgrad_accumulate(gw2, dy2, h, gb2, ready=(w2, b2)):
+                    grad_ready(w2, b2)
             resid = _slot_grad(ctx.x_slot, dh.shape[0])
             dx = _dgrad(dh, bf16_weight(w1), resid=resid) if ctx.needs_input_grad[0] else None
             with _grad.side(dh.device, dh, x2):
-                _wgrad_accumulate(gw1, dh, x2, gb1)
-            grad_ready(w1, b1)
+                if not _wgrad_accumulate(gw1, dh, x2, gb1, ready=(w1, b1)):
+                    grad_ready(w1, b1)
         else:
             g = dy2.float()
             grad_buf(w2).add_(g.t() @ h.float())
