@@ -50,6 +50,8 @@ int smi_splitk_reduce(const float*, int, long, float*, long, float*, int, hipStr
 int smi_splitk_fold_multi(const float* const*, float* const*, float* const*, const long*, const int*, const int*, int,
                           hipStream_t);
 void smi_gemm_set_bm(int);
+int smi_gemm_wgrad_group(const void* const*, const long*, const void* const*, const long*, void* const*, void* const*,
+                         const int*, const int*, const int*, int, hipStream_t);
 int smi_cnn(const CNNArgs*, hipStream_t);
 int smi_cnn_reduce(const CNNArgs*, hipStream_t);
 int smi_gather_rows(const void*, const long long*, void*, long, long, hipStream_t);
@@ -235,6 +237,21 @@ PYBIND11_MODULE(_C, m) {
     for (size_t i = 0; i < c; ++i) { a[i] = PF(slab[i]); o[i] = PF(out[i]); bo[i] = PF(bout[i]); }
     chk(smi_splitk_fold_multi(a.data(), o.data(), bo.data(), n.data(), nb.data(), splits.data(), (int)c, S(st)),
         "splitk_fold_multi");
+  });
+  // grouped no-split wgrad: gw_e[n,k] += A_e[T,n]^T B_e[T,k] (+ gb_e[n] += A_e^T 1) for every entry, one launch
+  m.def("gemm_wgrad_group", [](std::vector<u> A, std::vector<long> lda, std::vector<u> B, std::vector<long> ldb,
+                               std::vector<u> C, std::vector<u> bias, std::vector<int> n, std::vector<int> k,
+                               std::vector<int> T, u st) {
+    const size_t c = A.size();
+    if (lda.size() != c || B.size() != c || ldb.size() != c || C.size() != c || bias.size() != c || n.size() != c ||
+        k.size() != c || T.size() != c)
+      throw std::runtime_error("gemm_wgrad_group: list sizes differ");
+    std::vector<const void*> a(c), b(c);
+    std::vector<void*> o(c), bo(c);
+    for (size_t i = 0; i < c; ++i) { a[i] = (const void*)A[i]; b[i] = (const void*)B[i]; o[i] = (void*)C[i]; bo[i] = (void*)bias[i]; }
+    chk(smi_gemm_wgrad_group(a.data(), lda.data(), b.data(), ldb.data(), o.data(), bo.data(), n.data(), k.data(),
+                             T.data(), (int)c, S(st)),
+        "gemm_wgrad_group");
   });
   m.def("splitk_reduce", [](u slab, int splits, long n, u out, long nb, u bout, int accumulate, u st) {
     chk(smi_splitk_reduce((const float*)slab, splits, n, (float*)out, nb, (float*)bout, accumulate, S(st)),

@@ -196,37 +196,28 @@ __device__ __forceinline__ TileInfo tile_of(const GemmArgs& g, int t, int ntn, i
   ti.nk = (kend - ti.kbeg + BKK - 1) / BKK;
   return ti;
 }
-
-// SWAP: accumulate C^T tiles (lane owns 4 consecutive output columns of one row).
-// Persistent over tiles (grid = min(tiles, WG_PER_CU * 256)); per tile: NS-deep DMA prologue,
-// k-loop with counted waits, drain, epilogue.  With NS = 2 (64 KiB LDS) two workgroups share a
-// CU, so one's prologue/epilogue overlaps the other's MFMA loop.
-// FM = 16-row A fragments per wave: 4 -> 128 x 128 tiles, 2 -> 64 x 128 tiles (twice the
-// workgroups for the transformer's N = 512 GEMMs, so two tiles share a CU and one's load /
-// store phases overlap the other's MFMAs).  A k-major A operand (wgrad) always uses FM = 4.
+// One output tile (all its k-steps and the epilogue) of the problem in `g`; t = the tile
+// index within that problem's (split, tile) enumeration.  `smem` = the NS-stage LDS ring.
 template <bool AK, bool BKM, bool SWAP, int NS, int FM, int EPI>
-__global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : (NS == 3 && FM == 2 ? 2 : 1))) void gemm_bf16_kernel(GemmArgs g) {
+__device__ __forceinline__ void gemm_tile(const GemmArgs& g, const int t, unsigned short* smem) {
   constexpr int BMT = 32 * FM;                 // tile rows (M)
   constexpr int NPA = AK ? 4 : FM;             // DMA pieces per wave per stage, A operand
   constexpr int A_ELEMS = BMT * BKK;
   constexpr int STAGE = A_ELEMS + TILE_ELEMS;  // A then B (128 rows) per stage
   constexpr int VM1 = NPA + 4;                 // vector-memory ops per wave per stage
   static_assert(!AK || FM == 4, "k-major A needs 128-wide tiles");
-  __shared__ __attribute__((aligned(16))) unsigned short smem[NS * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
   const int ntn = (g.N + BN - 1) / BN;
   const int ntm = (g.M + BMT - 1) / BMT;
   const int nwg = ntm * ntn;
-  const int total_tiles = nwg * g.splits;
   const bool ragged = (g.K % BKK) != 0 || (g.K % g.k_per_split) != 0;
   const uint32_t seed = smi_seed(g.seedp, g.salt);
   const EpiFlags ef = epi_flags<EPI>(g);
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, 0, (int)g.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, 0, (int)g.b_bytes, 0x00020000);
 
-  for (int t = blockIdx.x; t < total_tiles; t += gridDim.x) {
     GSTAMP(0);
     const TileInfo ti = tile_of(g, t, ntn, nwg, BMT);
     const int m0 = ti.m0, n0 = ti.n0, nk = ti.nk;
@@ -482,7 +473,7 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : (NS == 3 && FM 
           const int row = m0 + wm * 16 * FM + i * 16 + (lane & 15);
           if ((lane >> 4) == 0 && row < g.M) {
             if (g.atomic) atomicAdd(bdst + row, accb[i][0]);
-            else bdst[row] = accb[i][0];
+            else bdst[row] = g.beta_acc ? bdst[row] + accb[i][0] : accb[i][0];
           }
         } else if ((lane & 15) == 0) {
 #pragma unroll
@@ -490,7 +481,7 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : (NS == 3 && FM 
             const int row = m0 + wm * 16 * FM + i * 16 + 4 * (lane >> 4) + r;
             if (row < g.M) {
               if (g.atomic) atomicAdd(bdst + row, accb[i][r]);
-              else bdst[row] = accb[i][r];
+              else bdst[row] = g.beta_acc ? bdst[row] + accb[i][r] : accb[i][r];
             }
           }
         }
@@ -498,7 +489,26 @@ __global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : (NS == 3 && FM 
     }
     GSTAMP(4);
     __syncthreads();  // every wave is done with the LDS stages before the next tile's prologue
-  }
+}
+
+
+// SWAP: accumulate C^T tiles (lane owns 4 consecutive output columns of one row).
+// Persistent over tiles (grid = min(tiles, WG_PER_CU * 256)); per tile: NS-deep DMA prologue,
+// k-loop with counted waits, drain, epilogue.  With NS = 2 (64 KiB LDS) two workgroups share a
+// CU, so one's prologue/epilogue overlaps the other's MFMA loop.
+// FM = 16-row A fragments per wave: 4 -> 128 x 128 tiles, 2 -> 64 x 128 tiles (twice the
+// workgroups for the transformer's N = 512 GEMMs, so two tiles share a CU and one's load /
+// store phases overlap the other's MFMAs).  A k-major A operand (wgrad) always uses FM = 4.
+template <bool AK, bool BKM, bool SWAP, int NS, int FM, int EPI>
+__global__ __launch_bounds__(256, (NS <= 2 ? (FM == 2 ? 3 : 2) : (NS == 3 && FM == 2 ? 2 : 1))) void gemm_bf16_kernel(GemmArgs g) {
+  constexpr int BMT = 32 * FM;                 // tile rows (M)
+  constexpr int NPA = AK ? 4 : FM;             // DMA pieces per wave per stage, A operand
+  constexpr int A_ELEMS = BMT * BKK;
+  constexpr int STAGE = A_ELEMS + TILE_ELEMS;  // A then B (128 rows) per stage
+  __shared__ __attribute__((aligned(16))) unsigned short smem[NS * STAGE];
+  const int nwg = ((g.M + BMT - 1) / BMT) * ((g.N + BN - 1) / BN);
+  const int total_tiles = nwg * g.splits;
+  for (int t = blockIdx.x; t < total_tiles; t += gridDim.x) gemm_tile<AK, BKM, SWAP, NS, FM, EPI>(g, t, smem);
 }
 
 
@@ -736,5 +746,67 @@ extern "C" int smi_splitk_fold_multi(const float* const* slab, float* const* out
   a.blk0[count] = tot;
   a.count = count;
   hipLaunchKernelGGL(splitk_fold_multi_kernel, dim3((unsigned)tot), dim3(256), 0, st, a);
+  SMI_CHECK_LAUNCH();
+}
+
+// Grouped weight-gradient GEMMs: gw_e[N,K] += dY_e[T,N]^T X_e[T,K] (and gb_e[N] += dY_e^T 1)
+// for up to WG_MAX problems in ONE persistent launch, with no split-K (sparkmi/ops/_grad.py:
+// every Linear's wgrad is queued during the backward — it is off the critical path — and the
+// queue is flushed by the autograd final callback).  One launch covers ~2,000 128 x 128 output
+// tiles of the whole backward, each with its FULL token reduction (T / 64 k-steps), so the
+// per-tile prologue / epilogue is amortised over ~128 k-steps instead of 8-16 split-K steps, and
+// the fp32 slabs (~1.4 GB written + read per transformer step) disappear: each tile owns its
+// output and adds straight into gw.  Problem e's tiles start at t0[e], a multiple of 8, so the
+// XCD-aware remap inside tile_of sees the same XCD pattern as a standalone launch.
+#define WG_MAX 40
+struct WgradGroup {
+  const unsigned short* A[WG_MAX]; const unsigned short* B[WG_MAX];
+  float* C[WG_MAX]; float* bias[WG_MAX];
+  int lda[WG_MAX], ldb[WG_MAX], n[WG_MAX], k[WG_MAX], T[WG_MAX];
+  int t0[WG_MAX + 1]; int count;
+};
+__global__ __launch_bounds__(256, 2) void gemm_wgrad_group_kernel(WgradGroup gr) {
+  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * (2 * TILE_ELEMS)];
+  const int total = gr.t0[gr.count];
+  for (int t = blockIdx.x; t < total; t += gridDim.x) {
+    int e = 0;
+    while (e + 1 < gr.count && t >= gr.t0[e + 1]) ++e;  // uniform scan over <= WG_MAX entries
+    GemmArgs g{};
+    g.mode = 2; g.A = gr.A[e]; g.lda = gr.lda[e]; g.B = gr.B[e]; g.ldb = gr.ldb[e];
+    g.M = gr.n[e]; g.N = gr.k[e]; g.K = gr.T[e]; g.C = gr.C[e]; g.ldc = gr.k[e];
+    g.out_f32 = 1; g.atomic = 0; g.beta_acc = 1; g.alpha = 1.f; g.dscale = 1.f;
+    g.splits = 1; g.k_per_split = g.K;
+    g.a_bytes = 2 * ((long)(g.K - 1) * g.lda + g.M);
+    g.b_bytes = 2 * ((long)(g.K - 1) * g.ldb + g.N);
+    g.bias_grad = gr.bias[e];
+    const int lt = t - gr.t0[e];
+    const int nwg = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+    if (lt < nwg) gemm_tile<true, true, true, 2, 4, 0>(g, lt, smem);  // lt >= nwg: alignment padding
+  }
+}
+
+extern "C" int smi_gemm_wgrad_group(const void* const* A, const long* lda, const void* const* B, const long* ldb,
+                                    void* const* C, void* const* bias, const int* n, const int* k, const int* T,
+                                    int count, hipStream_t st) {
+  if (count < 1 || count > WG_MAX) return -1;
+  WgradGroup gr{};
+  int tot = 0;
+  for (int i = 0; i < count; ++i) {
+    // same preconditions as smi_gemm's WGRAD path (multiples of 8, descriptor-addressable operands)
+    if (T[i] < 8 || n[i] < 8 || k[i] < 8 || T[i] % 8 || n[i] % 8 || k[i] % 8) return -1;
+    if (lda[i] < n[i] || ldb[i] < k[i] || lda[i] > (1L << 30) || ldb[i] > (1L << 30)) return -1;
+    if (2 * ((long)(T[i] - 1) * lda[i] + n[i]) >= (1L << 31) || 2 * ((long)(T[i] - 1) * ldb[i] + k[i]) >= (1L << 31))
+      return -1;
+    gr.A[i] = (const unsigned short*)A[i]; gr.B[i] = (const unsigned short*)B[i];
+    gr.C[i] = (float*)C[i]; gr.bias[i] = (float*)bias[i];
+    gr.lda[i] = (int)lda[i]; gr.ldb[i] = (int)ldb[i]; gr.n[i] = n[i]; gr.k[i] = k[i]; gr.T[i] = T[i];
+    gr.t0[i] = tot;
+    const int nwg = ((n[i] + BM - 1) / BM) * ((k[i] + BN - 1) / BN);
+    tot += (nwg + 7) / 8 * 8;
+  }
+  gr.t0[count] = tot;
+  gr.count = count;
+  const int grid = tot < 2 * NUM_CU ? tot : 2 * NUM_CU;
+  hipLaunchKernelGGL(gemm_wgrad_group_kernel, dim3(grid), dim3(256), 0, st, gr);
   SMI_CHECK_LAUNCH();
 }

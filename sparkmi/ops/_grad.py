@@ -172,10 +172,56 @@ def defer_wgrad_fold(slab, splits, n, gw, nb, gb, params, stream):
     _queue_flush()
 
 
+# ---- grouped weight-gradient GEMMs ----
+# A Linear's weight gradient is off the critical path of the backward (only dX feeds the next
+# op), so instead of one split-K GEMM per Linear (8-16 k-steps per tile, fp32 slabs, a fold)
+# every wgrad is queued here and the whole backward's wgrads run as ONE grouped launch at its
+# end (csrc/kernels/gemm.hip:gemm_wgrad_group_kernel: no split-K, each tile reduces all tokens
+# and adds into the fp32 gradient).  The queued dY / X stay referenced until then (autograd
+# then never accumulates into them in place).  SPARKMI_WGRAD_GROUP=0 restores per-Linear GEMMs.
+WGRAD_GROUP = os.environ.get("SPARKMI_WGRAD_GROUP", "1") != "0" and not _SIDE_ENABLED
+_group_queue = []
+GROUP_MAX = 40  # csrc/kernels/gemm.hip WG_MAX
+
+
+def defer_wgrad_group(dy, x, gw, gb, params, stream):
+    _group_queue.append((dy, x, gw, gb, params, stream))
+    _queue_flush()
+
+
+def _flush_groups(C):
+    gq = list(_group_queue)
+    _group_queue.clear()
+    by_stream = {}
+    for e in gq:
+        by_stream.setdefault(e[5], []).append(e)
+    for st, es in by_stream.items():
+        batch, outs = [], set()
+        for e in es + [None]:
+            # one batch's tiles run concurrently and add without atomics: outputs must be distinct
+            if e is None or len(batch) == GROUP_MAX or e[2].data_ptr() in outs or (
+                    e[3] is not None and e[3].data_ptr() in outs):
+                if batch:
+                    C.gemm_wgrad_group([b[0].data_ptr() for b in batch], [b[0].stride(0) for b in batch],
+                                       [b[1].data_ptr() for b in batch], [b[1].stride(0) for b in batch],
+                                       [b[2].data_ptr() for b in batch],
+                                       [b[3].data_ptr() if b[3] is not None else 0 for b in batch],
+                                       [b[2].shape[0] for b in batch], [b[2].shape[1] for b in batch],
+                                       [b[0].shape[0] for b in batch], st)
+                batch, outs = [], set()
+            if e is not None:
+                batch.append(e)
+                outs.add(e[2].data_ptr())
+                if e[3] is not None:
+                    outs.add(e[3].data_ptr())
+    return gq
+
+
 def flush_deferred():
     from .. import _native
     _cb[0] = False
     C = _native.C()
+    gq = _flush_groups(C)
     lq = list(_ln_queue)
     _ln_queue.clear()
     by_stream = {}
@@ -209,3 +255,5 @@ def flush_deferred():
         grad_ready(*e[6])
     for e in fq:
         grad_ready(*e[6])
+    for e in gq:
+        grad_ready(*e[4])

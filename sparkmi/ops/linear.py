@@ -42,6 +42,10 @@ def _wgrad_accumulate(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, gb=
     end-of-backward flush, sparkmi/ops/_grad.py); otherwise the caller reports it."""
     N, K = gw.shape
     M = dy2.shape[0]
+    if (ready is not None and _grad.WGRAD_GROUP and G.supported(N, K, M, dy2, x2, mode=2) and gw.is_contiguous()
+            and (gb is None or gb.is_contiguous()) and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16):
+        _grad.defer_wgrad_group(dy2, x2, gw, gb, ready, _native.stream())
+        return True
     if G.supported(N, K, M, dy2, x2, mode=2) and gw.is_contiguous():
         key = ("wgrad", N, K, M, gb is not None)
         if key not in G._choices and not torch.cuda.is_current_stream_capturing():
