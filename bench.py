@@ -3,22 +3,28 @@
 
 Flagship = the BASELINE.json transformer config: encoder-decoder Transformer (transformer.py),
 6 layers, d_model 512, 8 heads, ffn 1024, seq 256, vocab 10k/10k, batch 32 per GPU, Adam
-lr 1e-3, dropout 0.1, reference mask semantics, bf16 compute / fp32 master weights — a full
-training step (forward, masked token CE, backward, gradient all-reduce, optimizer) per
-iteration, synthetic Multi30k-shaped data resident in HBM, random-init weights.
+lr 1e-3, dropout 0.1, reference mask semantics — a full training step (forward, masked token
+CE, backward, gradient all-reduce, optimizer) per iteration, synthetic Multi30k-shaped data
+resident in HBM, random-init weights.  ``value`` is measured at the REFERENCE precision: fp32
+activations, fp32 weights, fp32 MFMA (v_mfma_f32_32x32x2_f32) GEMMs and attention, exactly as
+the reference trains (pytorch_machine_translator.py:120-137, default fp32 modules).  The bf16
+(fp32-master) variant of the same step and the distributed_cnn workload (the other half of the
+BASELINE metric) are reported beside it for the same N, plus the LSTM / MLP workloads.
 
-Contract: ``python bench.py --gpus N --steps K --warmup W``; multi-GPU runs are launched by
-torch.distributed.run (one rank per GPU, RCCL).  W untimed warm-up steps, then K steps timed
-between barrier+synchronize on both sides; the MAX elapsed over ranks is used; rank 0 prints
-one JSON line.  ``value`` = whole-job samples/s = N * batch * K / max_elapsed (weak scaling).
+Contract: ``python bench.py --gpus N --steps K --warmup W``.  Multi-GPU runs are launched by
+torch.distributed.run (one rank per GPU, RCCL); when ``--gpus N > 1`` is given WITHOUT a
+launcher (no WORLD_SIZE in the environment) this script spawns the N ranks itself before any
+GPU call (reference launch: distributed_cnn.py:227-231, TorchDistributor(num_processes=N)).
+W untimed warm-up steps, then K steps timed between barrier+synchronize on both sides; the MAX
+elapsed over ranks is used; rank 0 prints one JSON line.  ``value`` = whole-job samples/s =
+N * batch * K / max_elapsed (weak scaling).
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
-
-import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -28,14 +34,18 @@ BASELINE_TRANSFORMER = 4.79
 BASELINE_CNN = 5655.0
 BASELINE_LSTM = 1365.0    # 1 proc x 8 threads
 BASELINE_MLP = 130476.0   # world 1, 1 thread
+METRIC = "samples/sec (whole node) distributed_cnn + transformer at 1/2/4/8 MI355X"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="all", choices=["all", "transformer", "cnn", "aux"])
+    ap.add_argument("--dtype", default="auto", choices=["auto", "fp32", "bf16", "both"],
+                    help="transformer compute dtype; auto = fp32 headline + bf16 beside it on GPU, fp32 on CPU")
+    ap.add_argument("--device", default="auto", choices=["auto", "cpu", "cuda"])
     ap.add_argument("--aux-steps", type=int, default=100, help="timed steps of the LSTM / MLP extras")
     ap.add_argument("--cnn-batch", type=int, default=32)
     ap.add_argument("--cnn-steps", type=int, default=200)
@@ -45,8 +55,46 @@ def parse():
     ap.add_argument("--vocab", type=int, default=10000)
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--bucket-mb", type=float, default=64.0)
-    ap.add_argument("--split", type=int, default=1, help="two-graph backward with overlapped all-reduce (DP)")
-    return ap.parse_args()
+    ap.add_argument("--split", type=int, default=1, help="multi-graph backward with overlapped all-reduce (DP)")
+    ap.add_argument("--no-aux", action="store_true", help="skip the LSTM / MLP extras")
+    return ap.parse_args(argv)
+
+
+def spawn_ranks(n, argv):
+    """Launch ``n`` ranks of this script (torchrun env contract, 127.0.0.1 rendezvous) and
+    relay rank 0's stdout.  Runs in a process that has not touched the GPU, and never execs."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                    "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                    "PYTHONUNBUFFERED": "1"})
+        env.setdefault("OMP_NUM_THREADS", "1")
+        out = None if r == 0 else subprocess.DEVNULL
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env, stdout=out))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                c = p.poll()
+                if c is None:
+                    continue
+                procs.remove(p)
+                if c != 0:
+                    rc = c
+                    for q in procs:  # one rank failed: the group cannot finish its collectives
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait()
+    return rc
 
 
 def transformer_flops_per_sample(layers, seq, vocab, d=512, ffn=1024):
@@ -61,22 +109,28 @@ def transformer_flops_per_sample(layers, seq, vocab, d=512, ffn=1024):
     return 3 * per_token * seq
 
 
+def _sync(device):
+    import torch
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+
+
 def time_steps(runner, batches, steps, warmup, device, world):
+    import torch
     from sparkmi.parallel import barrier
-    sync = (lambda: torch.cuda.synchronize()) if device.type == "cuda" else (lambda: None)
     n = len(batches)
     loss = None
     for i in range(warmup):
         loss = runner.step(*batches[i % n])
-    sync()
+    _sync(device)
     barrier()
-    sync()
+    _sync(device)
     t0 = time.perf_counter()
     for i in range(steps):
         loss = runner.step(*batches[i % n])
-    sync()
+    _sync(device)
     barrier()
-    sync()
+    _sync(device)
     elapsed = time.perf_counter() - t0
     if world > 1:
         import torch.distributed as dist
@@ -86,8 +140,32 @@ def time_steps(runner, batches, steps, warmup, device, world):
     return elapsed, loss
 
 
+def time_allreduce(flat, device, world, iters=10):
+    """Isolated cost of the step's gradient all-reduce (the whole flat fp32 gradient buffer,
+    same buckets and backend as the step): the communication phase, in ms, max over ranks."""
+    if world <= 1:
+        return None
+    import torch
+    import torch.distributed as dist
+    g = flat.grad
+    for _ in range(2):
+        dist.all_reduce(g)
+    _sync(device)
+    from sparkmi.parallel import barrier
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        dist.all_reduce(g)
+    _sync(device)
+    el = (time.perf_counter() - t0) / iters
+    t = torch.tensor([el], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return round(float(t.item()) * 1000, 3)
+
+
 def bench_cnn(args, rank, world, device):
     """distributed_cnn.py workload: FashionMNISTModel, batch 32/GPU, SGD lr 0.01, mean CE."""
+    import torch
     from sparkmi.data.synthetic import fashion_mnist_like
     from sparkmi.models.cnn import FashionMNISTModel
     from sparkmi.optim import SGD
@@ -105,14 +183,22 @@ def bench_cnn(args, rank, world, device):
     batches = [(imgs[i * args.cnn_batch:(i + 1) * args.cnn_batch], labels[i * args.cnn_batch:(i + 1) * args.cnn_batch])
                for i in range(16)]
     elapsed, loss = time_steps(runner, batches, args.cnn_steps, max(args.warmup, 5), device, world)
+    ar = time_allreduce(flat, device, world)
     if ddp is not None:
         ddp.close()
-    return world * args.cnn_batch * args.cnn_steps / elapsed, elapsed / args.cnn_steps * 1000, float(loss)
+    v = world * args.cnn_batch * args.cnn_steps / elapsed
+    return {"samples_per_s": round(v, 1), "ms_per_step": round(elapsed / args.cnn_steps * 1000, 4),
+            "vs_baseline": round(v / BASELINE_CNN, 2), "final_loss": round(float(loss), 4),
+            "dtype": "fp32", "global_batch": world * args.cnn_batch, "steps": args.cnn_steps,
+            "allreduce_ms": ar, "grad_bytes": flat.numel * 4,
+            "config": f"FashionMNISTModel fused HIP kernel, batch {args.cnn_batch}/GPU, SGD lr0.01, dp{world}",
+            "baseline_ref": "BASELINE.md §2 CNN CPU proxy 5,655 samples/s (1 proc x 8 threads)"}
 
 
 def bench_lstm(args, rank, world, device):
     """distributed_lstm.py workload: Embedding(V~95.8k, 32) -> LSTM(32, 32, 2 layers, dropout 0.5)
     -> fc(4) at every step, CE on the last step; batch 32/GPU, T = 129, Adam lr 1e-3."""
+    import torch
     from sparkmi.models.lstm import LSTM
     from sparkmi.optim import Adam
     from sparkmi.parallel.ddp import DataParallel
@@ -132,11 +218,15 @@ def bench_lstm(args, rank, world, device):
     elapsed, _ = time_steps(runner, batches, steps, max(args.warmup, 5), device, world)
     if ddp is not None:
         ddp.close()
-    return world * B * steps / elapsed, elapsed / steps * 1000
+    v = world * B * steps / elapsed
+    return {"samples_per_s": round(v, 1), "ms_per_step": round(elapsed / steps * 1000, 4),
+            "vs_baseline": round(v / BASELINE_LSTM, 2),
+            "config": f"Embedding(95812,32)+LSTM(32,32,L2)+fc4, T129, batch 32/GPU, Adam, fp32, dp{world}"}
 
 
 def bench_mlp(args, rank, world, device):
     """distributed_multilayer_perceptron.py workload: 4-5-4-3 sigmoid MLP, batch 30/GPU, SGD."""
+    import torch
     from sparkmi.models.mlp import MultilayerPerceptron
     from sparkmi.optim import SGD
     from sparkmi.parallel.ddp import DataParallel
@@ -155,112 +245,135 @@ def bench_mlp(args, rank, world, device):
     elapsed, _ = time_steps(runner, batches, steps, max(args.warmup, 5), device, world)
     if ddp is not None:
         ddp.close()
-    return world * 30 * steps / elapsed, elapsed / steps * 1000
+    v = world * 30 * steps / elapsed
+    return {"samples_per_s": round(v, 1), "ms_per_step": round(elapsed / steps * 1000, 4),
+            "vs_baseline": round(v / BASELINE_MLP, 2), "config": f"MLP 4-5-4-3 sigmoid, batch 30/GPU, SGD, fp32, dp{world}"}
 
 
-def main():
-    args = parse()
-    from sparkmi.parallel import barrier, init_distributed
-    from sparkmi.parallel.ddp import DataParallel
-    rank, world, device = init_distributed()
-    cnn = lstm = mlp = None
-    if args.model in ("all", "cnn"):
-        cnn = bench_cnn(args, rank, world, device)
-    if args.model in ("all", "aux"):
-        lstm = bench_lstm(args, rank, world, device)
-        mlp = bench_mlp(args, rank, world, device)
-    if args.model == "aux":  # LSTM + MLP extras only (profiling)
-        if rank == 0:
-            print(json.dumps({"lstm_samples_per_s": round(lstm[0], 1), "lstm_ms_per_step": round(lstm[1], 4),
-                              "mlp_samples_per_s": round(mlp[0], 1), "mlp_ms_per_step": round(mlp[1], 4),
-                              "n_gpus": world}))
-        return
-    if args.model == "cnn":
-        if rank == 0:
-            v, ms, l = cnn
-            print(json.dumps({"metric": "samples/sec (whole node) distributed_cnn at 1/2/4/8 MI355X", "value": round(v, 1),
-                              "unit": "samples/s", "n_gpus": world, "steps": args.cnn_steps, "warmup": args.warmup,
-                              "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
-                              "vs_baseline": round(v / BASELINE_CNN, 2), "dtype": "fp32", "data": "synthetic",
-                              "config": {"model": "FashionMNISTModel", "global_batch": world * args.cnn_batch,
-                                         "seq_len": None, "parallelism": f"dp{world}", "final_loss": round(l, 4)}}))
-        return
-    torch.manual_seed(1234)
+def bench_transformer(args, rank, world, device, dtype):
+    """One full training step of the BASELINE transformer at ``dtype`` ('fp32' = reference
+    precision, or 'bf16' = bf16 activations/weights with fp32 master weights and fp32 accumulate)."""
+    import torch
+    from sparkmi.data.synthetic import translation_pairs
     from sparkmi.models.transformer import Transformer
     from sparkmi.optim import Adam
+    from sparkmi.parallel.ddp import DataParallel
     from sparkmi.train.runner import StepRunner
     from sparkmi.utils.flat import FlatParams
-    from sparkmi.data.synthetic import translation_pairs
-
+    torch.manual_seed(1234)
     model = Transformer(d_model=512, ffn_hidden=1024, num_heads=8, drop_prob=0.1, num_layers=args.layers,
                         max_sequence_length=args.seq, src_vocab_size=args.vocab, tgt_vocab_size=args.vocab,
-                        mask_mode="reference", seed=1234 + rank).to(device)
+                        mask_mode="reference", seed=1234 + rank, dtype=dtype).to(device)
     model.train()
-    flat = FlatParams(model)
+    flat = FlatParams(model, shadow=(dtype == "bf16" and device.type == "cuda"))
     opt = Adam(flat, lr=1e-3)
     ddp = DataParallel(flat, bucket_mb=args.bucket_mb) if world > 1 else None
     use_graph = args.graph != "off" and device.type == "cuda"
-    # data-parallel: backward in two graphs (decoder, then encoder) so the decoder's gradient
-    # buckets are all-reduced while the encoder backward runs (sparkmi/train/runner.py)
-    split_fn = (lambda m, s, t: m.training_step_split(s, t)) if (world > 1 and args.split) else None
+    # data-parallel: backward in several graphs (decoder, then encoder halves) so the finished
+    # gradient buckets are all-reduced while the rest of the backward runs (sparkmi/train/runner.py)
+    split_fn = (lambda m, s, t: m.training_step_split(s, t)) if (world > 1 and args.split and use_graph) else None
     runner = StepRunner(model, lambda m, s, t: m.training_step_loss(s, t), opt, ddp, graph=use_graph,
                         split_fn=split_fn)
     pool = 8
     src, tgt = translation_pairs(pool * args.batch, args.seq, args.vocab, args.vocab, seed=100 + rank, device=device)
     src = src.view(pool, args.batch, args.seq)
     tgt = tgt.view(pool, args.batch, args.seq)
-
     batches = [(src[i], tgt[i]) for i in range(pool)]
     elapsed, loss = time_steps(runner, batches, args.steps, args.warmup, device, world)
     final_loss = float(loss.float().item()) if loss is not None else float("nan")
+    ar = time_allreduce(flat, device, world)
+    if ddp is not None:
+        ddp.close()
     value = world * args.batch * args.steps / elapsed
     tflops = transformer_flops_per_sample(args.layers, args.seq, args.vocab) * value / world / 1e12
+    peak = 157.3 if dtype == "fp32" else 2500.0
+    res = {"samples_per_s": round(value, 2), "ms_per_step": round(elapsed / args.steps * 1000, 3),
+           "final_loss": round(final_loss, 4), "model_tflops_per_gpu": round(tflops, 1),
+           f"mfu_vs_{'157tf_fp32' if dtype == 'fp32' else '2.5pf_bf16'}_dense": round(tflops / peak, 3),
+           "allreduce_ms": ar, "grad_bytes": flat.numel * 4, "dtype": dtype,
+           "overlap": "finished buckets all-reduced under the rest of the backward" if split_fn else None,
+           "hip_graph": use_graph}
+    del runner, opt, flat, model, ddp, batches, src, tgt
+    if device.type == "cuda":
+        torch.cuda.empty_cache()
+    return res
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: become the launcher (before importing anything that touches the GPU)
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    if args.device == "cpu":
+        os.environ["SPARKMI_FORCE_CPU"] = "1"
+    import torch
+    from sparkmi.parallel import destroy, init_distributed
+    rank, world, device = init_distributed()
+    if args.dtype == "auto":
+        dtypes = ["fp32", "bf16"] if device.type == "cuda" else ["fp32"]
+    elif args.dtype == "both":
+        dtypes = ["fp32", "bf16"]
+    else:
+        dtypes = [args.dtype]
+    cnn = lstm = mlp = None
+    if args.model in ("all", "cnn"):
+        cnn = bench_cnn(args, rank, world, device)
+    if args.model in ("all", "aux") and not args.no_aux:
+        lstm = bench_lstm(args, rank, world, device)
+        mlp = bench_mlp(args, rank, world, device)
+    if args.model == "aux":  # LSTM + MLP extras only (profiling)
+        if rank == 0:
+            print(json.dumps({"lstm": lstm, "mlp": mlp, "n_gpus": world}))
+        destroy()
+        return
+    if args.model == "cnn":
+        if rank == 0:
+            print(json.dumps({"metric": "samples/sec (whole node) distributed_cnn at 1/2/4/8 MI355X",
+                              "value": cnn["samples_per_s"], "unit": "samples/s", "n_gpus": world,
+                              "steps": args.cnn_steps, "warmup": args.warmup, "ms_per_step": cnn["ms_per_step"],
+                              "higher_is_better": True, "scaling": "weak", "vs_baseline": cnn["vs_baseline"],
+                              "dtype": cnn["dtype"], "data": "synthetic",
+                              "config": {"model": "FashionMNISTModel", "global_batch": cnn["global_batch"],
+                                         "seq_len": None, "parallelism": f"dp{world}"}, "cnn": cnn}))
+        destroy()
+        return
+    tr = {dt: bench_transformer(args, rank, world, device, dt) for dt in dtypes}
+    head = tr[dtypes[0]]
     if rank == 0:
         out = {
-            "metric": "samples/sec (whole node) distributed_cnn + transformer at 1/2/4/8 MI355X",
-            "value": round(value, 2),
+            "metric": METRIC,
+            "value": head["samples_per_s"],
             "unit": "samples/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1000, 3),
+            "ms_per_step": head["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / BASELINE_TRANSFORMER, 2),
-            "dtype": "bf16",
+            "vs_baseline": round(head["samples_per_s"] / BASELINE_TRANSFORMER, 2),
+            "dtype": dtypes[0],
             "data": "synthetic (Multi30k-shaped token ids, HBM-resident); random-init weights",
             "config": {
                 "model": f"transformer.py enc-dec L{args.layers} d512 h8 ffn1024 V{args.vocab}/{args.vocab}",
                 "global_batch": world * args.batch,
                 "seq_len": args.seq,
                 "parallelism": f"dp{world}",
-                "optimizer": "Adam lr1e-3 (fp32 master, fused HIP)",
+                "optimizer": "Adam lr1e-3 (fp32, fused HIP)",
                 "mask_mode": "reference",
-                "hip_graph": use_graph,
-                "overlap": "decoder buckets all-reduced under the encoder backward" if split_fn else None,
+                "precision": ("fp32 activations/weights, fp32 MFMA GEMMs + attention (reference precision)"
+                              if dtypes[0] == "fp32" else "bf16 activations, fp32 master weights + accumulate"),
                 "baseline_ref": "BASELINE.md §2 transformer L6/S256 CPU proxy 4.79 samples/s",
-                "final_loss": round(final_loss, 4),
-                "model_tflops_per_gpu": round(tflops, 1),
-                "mfu_vs_2.5pf_dense_bf16": round(tflops / 2500.0, 3),
             },
+            "allreduce_ms": head["allreduce_ms"],
         }
+        for dt in dtypes:
+            out[f"transformer_{dt}"] = tr[dt]
         if cnn is not None:
-            out["extra"] = {"cnn_samples_per_s": round(cnn[0], 1), "cnn_ms_per_step": round(cnn[1], 4),
-                            "cnn_vs_baseline": round(cnn[0] / BASELINE_CNN, 2),
-                            "cnn_config": f"FashionMNISTModel fp32 fused HIP kernel, batch {args.cnn_batch}/GPU, "
-                                          f"SGD lr0.01, dp{world}, {args.cnn_steps} steps",
-                            "cnn_baseline_ref": "BASELINE.md §2 CNN CPU proxy 5,655 samples/s (1 proc x 8 threads)"}
-            if lstm is not None:
-                out["extra"].update({
-                    "lstm_samples_per_s": round(lstm[0], 1), "lstm_ms_per_step": round(lstm[1], 4),
-                    "lstm_vs_baseline": round(lstm[0] / BASELINE_LSTM, 2),
-                    "lstm_config": f"Embedding(95812,32)+LSTM(32,32,L2)+fc4, T129, batch 32/GPU, Adam, fp32, dp{world}",
-                    "mlp_samples_per_s": round(mlp[0], 1), "mlp_ms_per_step": round(mlp[1], 4),
-                    "mlp_vs_baseline": round(mlp[0] / BASELINE_MLP, 2),
-                    "mlp_config": f"MLP 4-5-4-3 sigmoid, batch 30/GPU, SGD, fp32, dp{world}",
-                    "aux_baseline_ref": "BASELINE.md §2 best CPU proxy: LSTM 1,365, MLP 130,476 samples/s"})
+            out["cnn"] = cnn
+        if lstm is not None:
+            out["extra"] = {"lstm": lstm, "mlp": mlp,
+                            "aux_baseline_ref": "BASELINE.md §2 best CPU proxy: LSTM 1,365, MLP 130,476 samples/s"}
         print(json.dumps(out), flush=True)
-    from sparkmi.parallel import destroy
     destroy()
 
 

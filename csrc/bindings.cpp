@@ -17,6 +17,7 @@ using u = uintptr_t;
 #include "smi_attention.h"
 #include "smi_mlp.h"
 #include "smi_gemm.h"
+#include "smi_gemm_f32.h"
 #include "smi_cnn.h"
 #include "smi_lstm.h"
 #include <pybind11/stl.h>
@@ -30,7 +31,17 @@ int smi_ln_bwd(const void*, const void*, const float*, const float*, const float
 int smi_ln_bwd_reduce(const float*, const float*, int, int, float*, float*, int, hipStream_t);
 int smi_ln_bwd_reduce_multi(const float* const*, const float* const*, float* const*, float* const*, const int*, const int*,
                             int, int, hipStream_t);
+int smi_ln_fwd_f32(const void*, const void*, const float*, const float*, void*, void*, float*, float*, int, int, float,
+                   const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
+int smi_ln_bwd_f32(const void*, const void*, const float*, const float*, const float*, void*, void*, const void*, float*,
+                   float*, int, float*, float*, int, int, int, const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
+int smi_emb_fwd_f32(const long long*, const void*, const float*, void*, long, int, int, const uint32_t*, uint32_t, uint32_t,
+                    float, hipStream_t);
+int smi_emb_bwd_f32(const long long*, const void*, float*, long, int, long long, const uint32_t*, uint32_t, uint32_t, float,
+                    hipStream_t);
 int smi_attn_fwd(const AttnFwdArgs*, hipStream_t);
+int smi_attn_f32_fwd(const AttnF32Args*, hipStream_t);
+int smi_attn_f32_bwd(const AttnF32Args*, hipStream_t);
 int smi_attn_bwd(const AttnBwdArgs*, const void*, float*, hipStream_t);
 int smi_ce_fwd(const void*, int, const long long*, int, int, long long, float*, float*, float*, float*, hipStream_t);
 int smi_ce_bwd(const void*, int, const long long*, int, int, long long, const float*, const float*, const float*, void*,
@@ -40,12 +51,17 @@ int smi_emb_fwd(const long long*, const void*, const float*, void*, long, int, i
 int smi_emb_bwd(const long long*, const void*, float*, long, int, long long, const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
 int smi_bias_act_drop_fwd(const void*, const float*, void*, long, int, int, const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
 int smi_act_drop_bwd(const void*, const void*, void*, long, int, const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
+int smi_act_drop_bwd_f32(const float*, const float*, float*, long, int, const uint32_t*, uint32_t, uint32_t, float,
+                         hipStream_t);
 int smi_colsum_bf16(const void*, long, int, float*, int, float*, int, hipStream_t);
 int smi_cast_f32_bf16(const float*, void*, long, hipStream_t);
 int smi_add_bf16(const void*, const void*, void*, long, hipStream_t);
 int smi_step_inc(float*, hipStream_t);
 int smi_mlp_fwd(const MLPArgs*, hipStream_t);
 int smi_gemm(const GemmArgs*, hipStream_t);
+int smi_gemm_f32(const GemmF32Args*, hipStream_t);
+int smi_gemm_f32_wgrad_group(const void* const*, const long*, const void* const*, const long*, void* const*, void* const*,
+                             const int*, const int*, const int*, int, hipStream_t);
 int smi_splitk_reduce(const float*, int, long, float*, long, float*, int, hipStream_t);
 int smi_splitk_fold_multi(const float* const*, float* const*, float* const*, const long*, const int*, const int*, int,
                           hipStream_t);
@@ -84,6 +100,27 @@ PYBIND11_MODULE(_C, m) {
                      u dbeta, int accumulate, int M, int D, u seedp, uint32_t salt, uint32_t thresh, float dscale, u st) {
     chk(smi_ln_bwd(P(dy), P(xs), PF(mean), PF(rstd), PF(gamma), P(dres), P(dh), P(dres_add), PF(pg), PF(pb), nblocks,
                    PF(dgamma), PF(dbeta), accumulate, M, D, (const uint32_t*)seedp, salt, thresh, dscale, S(st)), "ln_bwd");
+  });
+  m.def("ln_fwd_f32", [](u h, u r, u gamma, u beta, u y, u xsave, u mean, u rstd, int M, int D, float eps, u seedp,
+                         uint32_t salt, uint32_t thresh, float dscale, u st) {
+    chk(smi_ln_fwd_f32(P(h), P(r), PF(gamma), PF(beta), P(y), P(xsave), PF(mean), PF(rstd), M, D, eps,
+                       (const uint32_t*)seedp, salt, thresh, dscale, S(st)), "ln_fwd_f32");
+  });
+  m.def("ln_bwd_f32", [](u dy, u xs, u mean, u rstd, u gamma, u dres, u dh, u dres_add, u pg, u pb, int nblocks, u dgamma,
+                         u dbeta, int accumulate, int M, int D, u seedp, uint32_t salt, uint32_t thresh, float dscale, u st) {
+    chk(smi_ln_bwd_f32(P(dy), P(xs), PF(mean), PF(rstd), PF(gamma), P(dres), P(dh), P(dres_add), PF(pg), PF(pb), nblocks,
+                       PF(dgamma), PF(dbeta), accumulate, M, D, (const uint32_t*)seedp, salt, thresh, dscale, S(st)),
+        "ln_bwd_f32");
+  });
+  m.def("emb_fwd_f32", [](u ids, u table, u pe, u out, long T, int D, int Sp, u seedp, uint32_t salt, uint32_t thresh,
+                          float dscale, u st) {
+    chk(smi_emb_fwd_f32((const long long*)ids, P(table), PF(pe), P(out), T, D, Sp, (const uint32_t*)seedp, salt, thresh,
+                        dscale, S(st)), "emb_fwd_f32");
+  });
+  m.def("emb_bwd_f32", [](u ids, u dout, u dtable, long T, int D, long long pad, u seedp, uint32_t salt, uint32_t thresh,
+                          float dscale, u st) {
+    chk(smi_emb_bwd_f32((const long long*)ids, P(dout), PF(dtable), T, D, pad, (const uint32_t*)seedp, salt, thresh,
+                        dscale, S(st)), "emb_bwd_f32");
   });
   m.def("ln_bwd_reduce_multi", [](std::vector<u> pg, std::vector<u> pb, std::vector<u> og, std::vector<u> ob,
                                   std::vector<int> nb, std::vector<int> D, int accumulate, u st) {
@@ -127,6 +164,34 @@ PYBIND11_MODULE(_C, m) {
     a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk; a.mode = mode; a.scale_log2 = scale_log2; a.scale = scale;
     chk(smi_attn_bwd(&a, P(o), PF(delta), S(st)), "attn_bwd");
   });
+  // fp32 attention: (q, k, v) pointers + (batch, seq, head) strides; o/lse written by the forward
+  m.def("attn_f32_fwd", [](u q, u k, u v, py::tuple qs, py::tuple ks, py::tuple vs, u o, py::tuple os, u lse, u kpad,
+                           int B, int H, int Sq, int Sk, int mode, float scale_log2, u st) {
+    AttnF32Args a{};
+    a.q = (const float*)q; a.k = (const float*)k; a.v = (const float*)v;
+    a.q_sb = qs[0].cast<long>(); a.q_ss = qs[1].cast<long>(); a.q_sh = qs[2].cast<long>();
+    a.k_sb = ks[0].cast<long>(); a.k_ss = ks[1].cast<long>(); a.k_sh = ks[2].cast<long>();
+    a.v_sb = vs[0].cast<long>(); a.v_ss = vs[1].cast<long>(); a.v_sh = vs[2].cast<long>();
+    a.o = (float*)o; a.o_sb = os[0].cast<long>(); a.o_ss = os[1].cast<long>(); a.o_sh = os[2].cast<long>();
+    a.lse = (float*)lse; a.kpad = (const unsigned char*)kpad;
+    a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk; a.mode = mode; a.scale_log2 = scale_log2;
+    chk(smi_attn_f32_fwd(&a, S(st)), "attn_f32_fwd");
+  });
+  m.def("attn_f32_bwd", [](u q, u k, u v, py::tuple qs, py::tuple ks, py::tuple vs, u o, u dout, py::tuple os, u lse,
+                           u delta, u dq, u dk, u dv, u kpad, int B, int H, int Sq, int Sk, int mode, float scale_log2,
+                           float scale, u st) {
+    AttnF32Args a{};
+    a.q = (const float*)q; a.k = (const float*)k; a.v = (const float*)v;
+    a.q_sb = qs[0].cast<long>(); a.q_ss = qs[1].cast<long>(); a.q_sh = qs[2].cast<long>();
+    a.k_sb = ks[0].cast<long>(); a.k_ss = ks[1].cast<long>(); a.k_sh = ks[2].cast<long>();
+    a.v_sb = vs[0].cast<long>(); a.v_ss = vs[1].cast<long>(); a.v_sh = vs[2].cast<long>();
+    a.o = (float*)o; a.dout = (const float*)dout;
+    a.o_sb = os[0].cast<long>(); a.o_ss = os[1].cast<long>(); a.o_sh = os[2].cast<long>();
+    a.lse = (float*)lse; a.delta = (float*)delta;
+    a.dq = (float*)dq; a.dk = (float*)dk; a.dv = (float*)dv; a.kpad = (const unsigned char*)kpad;
+    a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk; a.mode = mode; a.scale_log2 = scale_log2; a.scale = scale;
+    chk(smi_attn_f32_bwd(&a, S(st)), "attn_f32_bwd");
+  });
   m.def("ce_fwd", [](u logits, int is_bf16, u labels, int M, int V, long long ignore, u lse, u count, u loss,
                      u row_loss, u st) {
     chk(smi_ce_fwd(P(logits), is_bf16, (const long long*)labels, M, V, ignore, PF(lse), PF(count), PF(loss),
@@ -151,6 +216,11 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("act_drop_bwd", [](u dy, u y, u dx, long total, int act, u seedp, uint32_t salt, uint32_t thresh, float dscale, u st) {
     chk(smi_act_drop_bwd(P(dy), P(y), P(dx), total, act, (const uint32_t*)seedp, salt, thresh, dscale, S(st)), "act_drop_bwd");
+  });
+  m.def("act_drop_bwd_f32", [](u dy, u y, u dx, long total, int act, u seedp, uint32_t salt, uint32_t thresh, float dscale,
+                               u st) {
+    chk(smi_act_drop_bwd_f32(PF(dy), PF(y), PF(dx), total, act, (const uint32_t*)seedp, salt, thresh, dscale, S(st)),
+        "act_drop_bwd_f32");
   });
   m.def("colsum_bf16", [](u x, long M, int N, u part, int rpb, u out, int acc, u st) {
     chk(smi_colsum_bf16(P(x), M, N, PF(part), rpb, PF(out), acc, S(st)), "colsum_bf16");
@@ -258,6 +328,32 @@ PYBIND11_MODULE(_C, m) {
         "splitk_reduce");
   });
   m.def("gemm_set_bm", [](int bm) { smi_gemm_set_bm(bm); });
+  // fp32 (reference-precision) GEMM on v_mfma_f32_32x32x2_f32: mode 0 FWD, 1 DGRAD, 2 WGRAD
+  m.def("gemm_f32", [](int mode, u A, long lda, u B, long ldb, int M, int N, int K, u C, long ldc, int beta_acc,
+                       int atomic, u bias, int relu, u resid, long ldr, u dact_y, long ldy, u seedp, uint32_t salt,
+                       uint32_t thresh, float dscale, int splits, u bias_grad, u st) {
+    GemmF32Args g{};
+    g.mode = mode; g.A = (const float*)A; g.lda = lda; g.B = (const float*)B; g.ldb = ldb;
+    g.M = M; g.N = N; g.K = K; g.C = (float*)C; g.ldc = ldc; g.beta_acc = beta_acc; g.atomic = atomic;
+    g.bias = (const float*)bias; g.relu = relu; g.resid = (const float*)resid; g.ldr = ldr;
+    g.dact_y = (const float*)dact_y; g.ldy = ldy; g.seedp = (const uint32_t*)seedp; g.salt = salt;
+    g.thresh = thresh; g.dscale = dscale; g.splits = splits; g.bias_grad = (float*)bias_grad;
+    chk(smi_gemm_f32(&g, S(st)), "gemm_f32");
+  });
+  m.def("gemm_f32_wgrad_group", [](std::vector<u> A, std::vector<long> lda, std::vector<u> B, std::vector<long> ldb,
+                                   std::vector<u> C, std::vector<u> bias, std::vector<int> n, std::vector<int> k,
+                                   std::vector<int> T, u st) {
+    const size_t c = A.size();
+    if (lda.size() != c || B.size() != c || ldb.size() != c || C.size() != c || bias.size() != c || n.size() != c ||
+        k.size() != c || T.size() != c)
+      throw std::runtime_error("gemm_f32_wgrad_group: list sizes differ");
+    std::vector<const void*> a(c), b(c);
+    std::vector<void*> o(c), bo(c);
+    for (size_t i = 0; i < c; ++i) { a[i] = (const void*)A[i]; b[i] = (const void*)B[i]; o[i] = (void*)C[i]; bo[i] = (void*)bias[i]; }
+    chk(smi_gemm_f32_wgrad_group(a.data(), lda.data(), b.data(), ldb.data(), o.data(), bo.data(), n.data(), k.data(),
+                                 T.data(), (int)c, S(st)),
+        "gemm_f32_wgrad_group");
+  });
   m.def("gather_rows", [](u src, u idx, u out, long n, long row_bytes, u st) {
     chk(smi_gather_rows(P(src), (const long long*)idx, P(out), n, row_bytes, S(st)), "gather_rows");
   });

@@ -21,3 +21,17 @@ struct AttnBwdArgs {
   const unsigned short* o;    // forward output (O's layout): the dQ kernel computes delta = rowsum(dO*O)
   float* delta_out;           // ... and writes it here for the dK/dV kernel
 };
+// fp32 (reference-precision) attention, csrc/kernels/attention_f32.hip: same layouts as above
+// with fp32 elements; one block serves the forward and both backward kernels.
+struct AttnF32Args {
+  const float* q; const float* k; const float* v;
+  long q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh;
+  float* o; long o_sb, o_ss, o_sh;   // forward output / backward: the saved output (O's layout)
+  const float* dout;                 // backward: dO (O's layout)
+  float* lse;                        // [B,H,Sq] log2 units: written by the forward, read by the backward
+  float* delta;                      // [B,H,Sq] rowsum(dO * O): written by the dQ kernel, read by dK/dV
+  float* dq; float* dk; float* dv;   // same layouts as q / k / v
+  const unsigned char* kpad;         // [B,Sk] or null
+  int B, H, Sq, Sk, mode;
+  float scale_log2, scale;           // log2(e)/sqrt(hd), 1/sqrt(hd)
+};

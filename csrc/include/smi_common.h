@@ -26,6 +26,32 @@ __device__ __forceinline__ unsigned int pack2bf(float a, float b) {
   return __builtin_bit_cast(unsigned int, __builtin_convertvector(((smi_f32x2_t){a, b}), smi_bf16x2_t));
 }
 
+// ---- 8-element activation vectors, bf16 (16 B) or fp32 (32 B) storage, fp32 math ----
+// Kernels that serve both the bf16 path and the fp32 reference-precision path are templated on
+// the storage type T and load / store through V8<T>.
+template <typename T> struct V8;
+template <> struct V8<unsigned short> {
+  u16x8_t v;
+  __device__ __forceinline__ void load(const unsigned short* p) { v = *(const u16x8_t*)p; }
+  __device__ __forceinline__ float operator[](int j) const { return bf2f(v[j]); }
+  __device__ __forceinline__ static void store(unsigned short* p, const float (&x)[8]) {
+    uint4 o;
+    o.x = pack2bf(x[0], x[1]); o.y = pack2bf(x[2], x[3]); o.z = pack2bf(x[4], x[5]); o.w = pack2bf(x[6], x[7]);
+    *(uint4*)p = o;
+  }
+};
+template <> struct V8<float> {
+  float4 a, b;
+  __device__ __forceinline__ void load(const float* p) { a = *(const float4*)p; b = *(const float4*)(p + 4); }
+  __device__ __forceinline__ float operator[](int j) const {
+    return j < 4 ? (j == 0 ? a.x : j == 1 ? a.y : j == 2 ? a.z : a.w) : (j == 4 ? b.x : j == 5 ? b.y : j == 6 ? b.z : b.w);
+  }
+  __device__ __forceinline__ static void store(float* p, const float (&x)[8]) {
+    *(float4*)p = make_float4(x[0], x[1], x[2], x[3]);
+    *(float4*)(p + 4) = make_float4(x[4], x[5], x[6], x[7]);
+  }
+};
+
 // ---- wave64 reductions ----
 // All-lane butterfly on VALU cross-lane ops: DPP quad_perm [1,0,3,2] / [2,3,0,1] and the
 // row_half_mirror / row_mirror patterns inside each 16-lane row, then the gfx950 row swaps

@@ -22,9 +22,9 @@
 // transposed (O^T = V^T P^T etc.), so each lane stores 4 consecutive head-dim values.
 #include "smi_common.h"
 
-#define LOG2E_F 1.4426950408889634f
 
 #include "smi_attention.h"
+#include "smi_attn_mask.h"
 
 // ---------------------------------------------------------------------------------------------
 // LDS images: 64 rows x 64 bf16 (128-B rows), 16-B chunk c of row r stored at chunk c ^ (r & 7).
@@ -122,39 +122,6 @@ __device__ __forceinline__ float rows4_sum(float v) {
 }
 
 #define MFMA16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
-
-// Masked, biased, log2-scaled score for key kj / query qi; -inf where masked.  Specialised on
-// the mask mode at compile time (the generic form was ~4x the VALU work of the softmax itself):
-// `full` (uniform) = the whole 64-key chunk is inside Sk; `kmask` = the chunk's padded keys.
-template <int MODE, bool KPAD>
-__device__ __forceinline__ float score_adj(float s, int qi, int kj, int kl, bool full, int Sk, unsigned long long kmask,
-                                           float scale_log2) {
-  float x = s * scale_log2;
-  if (MODE == 1) x += (kj < qi) ? LOG2E_F : 0.f;
-  if (MODE == 2) x = (kj > qi) ? -INFINITY : x;
-  if (KPAD) x = ((kmask >> kl) & 1ull) ? -INFINITY : x;
-  if (!full) x = (kj >= Sk) ? -INFINITY : x;
-  return x;
-}
-
-// Chunk-vs-rows classification (wave-uniform): with keys [k0, k0+64) and query rows
-// [qlo, qhi], is the mask/bias the same for every pair?  Returns true and the common log2-domain
-// bias (0, LOG2E, or -inf = all masked) when it is, so the per-element path only runs on the
-// diagonal chunk and on ragged / padded chunks.
-template <int MODE, bool KPAD>
-__device__ __forceinline__ bool uniform_bias(int k0, int qlo, int qhi, bool full, float& bias) {
-  if (KPAD || !full) return false;
-  if (MODE == 0) { bias = 0.f; return true; }
-  if (k0 + 63 < qlo) { bias = (MODE == 1) ? LOG2E_F : 0.f; return true; }  // every key before every query
-  if (MODE == 1 && k0 >= qhi) { bias = 0.f; return true; }                   // no key strictly before
-  if (MODE == 2 && k0 > qhi) { bias = -INFINITY; return true; }              // every key after every query
-  return false;
-}
-
-__device__ __forceinline__ unsigned long long chunk_pad_mask(const unsigned char* kp, int k0, int Sk) {
-  const int k = k0 + (threadIdx.x & 63);
-  return __ballot(k < Sk && kp[k] != 0);
-}
 
 // ---------------------------------------------------------------------------------------------
 // Forward: workgroup = 4 waves x 32 queries (two 16-query sub-tiles per wave); K/V streamed in

@@ -1,0 +1,449 @@
+// Fused scaled-dot-product attention at the REFERENCE precision: fp32 Q/K/V/O, fp32 scores,
+// softmax and accumulation, on the fp32-input matrix cores (v_mfma_f32_32x32x2_f32, exact f32
+// products).  head_dim = 64.  Forward + dQ + dK/dV, no S x S tensor in HBM.
+//
+// Reference semantics: transformer.py:12-25 (scaled_dot_product) as called by MultiHeadAttention
+// (:74-83) and MultiHeadCrossAttention (:177-191), run in fp32 by pytorch_machine_translator.py
+// (model built at :120 and trained at :129-196 with default fp32 modules).  Mask modes as in
+// csrc/include/smi_attn_mask.h (Q6: "reference" = +1.0 on strictly-past keys).
+//
+// CDNA4 structure.  A 32x32x2 f32 MFMA takes 64 cycles, so the work per 32-key x 32-query block
+// (64 MFMAs forward, 96 for dQ, 128 for dK/dV) dwarfs its softmax VALU (16 scores per lane) —
+// the kernels are matrix-core bound and built so the MFMA stream has no bubbles:
+//  * workgroup = 4 waves x 32 rows of the OWNED axis (queries: forward, dQ; keys: dK/dV); the
+//    owned rows' Q (or K, V) stay in registers, lane l / l+32 hold the two 32-wide halves of row
+//    l & 31 of the head dimension (k = 32h + s for step s);
+//  * the STREAMED operand goes through double-buffered 32-row LDS chunks (register-staged float4
+//    loads of chunk c+1 in flight under chunk c's MFMAs);
+//  * scores are produced with the owned row on the lane (S^T = K Q^T in the forward), so the
+//    online-softmax statistics are lane-local up to one permlane32 swap, and the accumulator of
+//    the first product IS the B operand of the second: register s of the 32x32 accumulator holds
+//    key (s&3) + 8(s>>2) + 4h, which is exactly the k the 32x32x2 MFMA takes from lane half h at
+//    step s when the other operand is read in that key order (ds_read_b32 rows of the LDS image).
+//  * outputs come out transposed (O^T = V^T P^T ...): each lane owns one row and stores 4
+//    consecutive head-dim values per register group (16-B stores).
+// LDS images: [32 rows][68 floats] for row-fragment (ds_read_b128, conflict-free at pitch 68)
+// operands, [32][64] for column-only operands (ds_read_b32 rows, conflict-free at any pitch).
+// 32-row chunks keep the staging registers at 16 per thread (64-row chunks spilled dK/dV).
+#include "smi_common.h"
+#include "smi_attention.h"
+#include "smi_attn_mask.h"
+
+#define FCH 32    // rows per streamed chunk (= one 32-row MFMA block)
+#define FPR 68    // padded pitch (floats) of row-fragment images
+#define MF32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x2f32((a), (b), (c), 0, 0, 0)
+
+struct FStage { float4 v[2]; };  // one 32 x 64 fp32 chunk = 2 float4 per thread
+
+__device__ __forceinline__ void fa_load_chunk(const float* __restrict__ base, long ss, int r0, int rmax, FStage& p) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = threadIdx.x + 256 * u;
+    const int row = i >> 4, c = i & 15, r = r0 + row;
+    p.v[u] = r < rmax ? *(const float4*)(base + (long)r * ss + c * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+template <int PITCH>
+__device__ __forceinline__ void fa_store_chunk(float* img, const FStage& p) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = threadIdx.x + 256 * u;
+    *(float4*)(img + (i >> 4) * PITCH + (i & 15) * 4) = p.v[u];
+  }
+}
+// row fragment: f[s] = img[row0 + (lane & 31)][32h + s], s = 0..31 (eight ds_read_b128)
+__device__ __forceinline__ void fa_rowfrag(const float* img, int row0, int lane, float (&f)[32]) {
+  const float* p = img + (row0 + (lane & 31)) * FPR + 32 * (lane >> 5);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float4 t = *(const float4*)(p + 4 * q);
+    f[4 * q] = t.x; f[4 * q + 1] = t.y; f[4 * q + 2] = t.z; f[4 * q + 3] = t.w;
+  }
+}
+// column fragment in accumulator row order: f[s] = img[row0 + (s&3) + 8(s>>2) + 4h][col0 + (lane & 31)]
+template <int PITCH>
+__device__ __forceinline__ void fa_colfrag(const float* img, int row0, int col0, int lane, float (&f)[16]) {
+  const float* p = img + (row0 + 4 * (lane >> 5)) * PITCH + col0 + (lane & 31);
+#pragma unroll
+  for (int s = 0; s < 16; ++s) f[s] = p[((s & 3) + 8 * (s >> 2)) * PITCH];
+}
+// own row of a global [rows][64] operand: f[s] = base[row][32h + s] (zero past rmax)
+__device__ __forceinline__ void fa_ownrow(const float* __restrict__ base, long ss, int row, int rmax, int lane, float (&f)[32]) {
+  const bool ok = row < rmax;
+  const float* p = base + (long)row * ss + 32 * (lane >> 5);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float4 t = ok ? *(const float4*)(p + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+    f[4 * q] = t.x; f[4 * q + 1] = t.y; f[4 * q + 2] = t.z; f[4 * q + 3] = t.w;
+  }
+}
+// store a transposed 32x32 accumulator tile: lane's row gets d = col0 + (r&3) + 8(r>>2) + 4h
+__device__ __forceinline__ void fa_store_rowT(float* __restrict__ dst, const f32x16_t& a, int lane, float sc) {
+  const int h = lane >> 5;
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+    *(float4*)(dst + 8 * g + 4 * h) = make_float4(a[4 * g] * sc, a[4 * g + 1] * sc, a[4 * g + 2] * sc, a[4 * g + 3] * sc);
+}
+__device__ __forceinline__ int fa_kl(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// ---------------------------------------------------------------------------------------------
+// Forward: S^T = K Q^T (query on the lane), online softmax, O^T += V^T P^T.
+template <int MODE, bool KPAD>
+__global__ __launch_bounds__(256, 2) void attn_f32_fwd_kernel(AttnF32Args a) {
+  __shared__ __attribute__((aligned(16))) float Ks[2][FCH * FPR];
+  __shared__ __attribute__((aligned(16))) float Vs[2][FCH * 64];
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int qwave = blockIdx.x * 128 + w * 32;
+  const int qi = qwave + (lane & 31);
+  const float* Q = a.q + b * a.q_sb + hh * a.q_sh;
+  const float* K = a.k + b * a.k_sb + hh * a.k_sh;
+  const float* V = a.v + b * a.v_sb + hh * a.v_sh;
+  const unsigned char* kp = a.kpad ? a.kpad + (long)b * a.Sk : nullptr;
+  int kend = a.Sk;
+  if (MODE == 2) kend = min(a.Sk, blockIdx.x * 128 + 128);
+  const int nchunks = (kend + FCH - 1) / FCH;
+  FStage pk, pv;
+  fa_load_chunk(K, a.k_ss, 0, a.Sk, pk);
+  fa_load_chunk(V, a.v_ss, 0, a.Sk, pv);
+  float qf[32];
+  fa_ownrow(Q, a.q_ss, qi, a.Sq, lane, qf);
+  fa_store_chunk<FPR>(Ks[0], pk);
+  fa_store_chunk<64>(Vs[0], pv);
+  __syncthreads();
+  float m = -INFINITY, l = 0.f;
+  f32x16_t o[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1;
+    const bool more = c + 1 < nchunks;
+    if (more) { fa_load_chunk(K, a.k_ss, (c + 1) * FCH, a.Sk, pk); fa_load_chunk(V, a.v_ss, (c + 1) * FCH, a.Sk, pv); }
+    const unsigned long long kmask = KPAD ? chunk_pad_mask(kp, c * FCH, a.Sk) : 0ull;
+    do {
+      const int kb = 0, k0 = c * FCH;
+      float ub;
+      const bool full = k0 + 32 <= a.Sk;
+      const bool uni = uniform_bias<MODE, KPAD, 32>(k0, qwave, qwave + 31, full, ub);
+      if (uni && ub == -INFINITY) break;  // every key of this block after every query (causal)
+      f32x16_t s;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[r] = 0.f;
+      {
+        float kf[32];
+        fa_rowfrag(Ks[buf], kb, lane, kf);
+#pragma unroll
+        for (int t = 0; t < 32; ++t) s = MF32(kf[t], qf[t], s);
+      }
+      float cmax = -INFINITY;
+      if (uni) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cmax = fmaxf(cmax, s[r]);
+        cmax = cmax * a.scale_log2 + ub;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kl = kb + fa_kl(r, h);
+          s[r] = score_adj<MODE, KPAD>(s[r], qi, c * FCH + kl, kl, full, a.Sk, kmask, a.scale_log2);
+          cmax = fmaxf(cmax, s[r]);
+        }
+      }
+      cmax = smi_row32_swap_max(cmax);
+      const float mnew = fmaxf(m, cmax);
+      const float mref = (mnew == -INFINITY) ? 0.f : mnew;
+      const float alpha = __builtin_amdgcn_exp2f(m - mref);
+      float psum = 0.f;
+      if (uni) {
+        const float off = ub - mref;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { s[r] = __builtin_amdgcn_exp2f(fmaf(s[r], a.scale_log2, off)); psum += s[r]; }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { s[r] = __builtin_amdgcn_exp2f(s[r] - mref); psum += s[r]; }
+      }
+      psum = smi_row32_swap_sum(psum);
+      l = l * alpha + psum;
+      m = mnew;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        o[dt] *= alpha;
+        float vf[16];
+        fa_colfrag<64>(Vs[buf], kb, dt * 32, lane, vf);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) o[dt] = MF32(vf[t], s[t], o[dt]);
+      }
+    } while (0);
+    if (more) { fa_store_chunk<FPR>(Ks[buf ^ 1], pk); fa_store_chunk<64>(Vs[buf ^ 1], pv); }
+    __syncthreads();
+  }
+  if (qi < a.Sq) {
+    float* O = a.o + b * a.o_sb + hh * a.o_sh + (long)qi * a.o_ss;
+    const float inv = l > 0.f ? 1.0f / l : 0.f;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) fa_store_rowT(O + dt * 32, o[dt], lane, inv);
+    if (h == 0) {
+      const float mref = (m == -INFINITY) ? 0.f : m;
+      a.lse[((long)b * a.H + hh) * a.Sq + qi] = l > 0.f ? mref + log2f(l) : INFINITY;
+    }
+  }
+}
+
+// dQ: S^T = K Q^T, dP^T = V dO^T, dS^T = P^T o (dP^T - delta), dQ^T += K^T dS^T; also writes
+// delta = rowsum(dO * O) for the dK/dV kernel.
+template <int MODE, bool KPAD>
+__global__ __launch_bounds__(256, 2) void attn_f32_dq_kernel(AttnF32Args a) {
+  __shared__ __attribute__((aligned(16))) float Ks[2][FCH * FPR];
+  __shared__ __attribute__((aligned(16))) float Vs[2][FCH * FPR];
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int qwave = blockIdx.x * 128 + w * 32;
+  const int qi = qwave + (lane & 31);
+  const float* Q = a.q + b * a.q_sb + hh * a.q_sh;
+  const float* K = a.k + b * a.k_sb + hh * a.k_sh;
+  const float* V = a.v + b * a.v_sb + hh * a.v_sh;
+  const float* dO = a.dout + b * a.o_sb + hh * a.o_sh;
+  const float* Og = a.o + b * a.o_sb + hh * a.o_sh;
+  const unsigned char* kp = a.kpad ? a.kpad + (long)b * a.Sk : nullptr;
+  int kend = a.Sk;
+  if (MODE == 2) kend = min(a.Sk, blockIdx.x * 128 + 128);
+  const int nchunks = (kend + FCH - 1) / FCH;
+  FStage pk, pv;
+  fa_load_chunk(K, a.k_ss, 0, a.Sk, pk);
+  fa_load_chunk(V, a.v_ss, 0, a.Sk, pv);
+  float qf[32], df[32];
+  fa_ownrow(Q, a.q_ss, qi, a.Sq, lane, qf);
+  fa_ownrow(dO, a.o_ss, qi, a.Sq, lane, df);
+  float dl;
+  {
+    float of[32];
+    fa_ownrow(Og, a.o_ss, qi, a.Sq, lane, of);
+    float sacc = 0.f;
+#pragma unroll
+    for (int t = 0; t < 32; ++t) sacc = fmaf(df[t], of[t], sacc);
+    dl = smi_row32_swap_sum(sacc);
+  }
+  const long rbase = ((long)b * a.H + hh) * a.Sq;
+  if (h == 0 && qi < a.Sq) a.delta[rbase + qi] = dl;
+  const float lse = qi < a.Sq ? a.lse[rbase + qi] : INFINITY;
+  fa_store_chunk<FPR>(Ks[0], pk);
+  fa_store_chunk<FPR>(Vs[0], pv);
+  __syncthreads();
+  f32x16_t acc[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[dt][r] = 0.f;
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1;
+    const bool more = c + 1 < nchunks;
+    if (more) { fa_load_chunk(K, a.k_ss, (c + 1) * FCH, a.Sk, pk); fa_load_chunk(V, a.v_ss, (c + 1) * FCH, a.Sk, pv); }
+    const unsigned long long kmask = KPAD ? chunk_pad_mask(kp, c * FCH, a.Sk) : 0ull;
+    do {
+      const int kb = 0, k0 = c * FCH;
+      float ub;
+      const bool full = k0 + 32 <= a.Sk;
+      const bool uni = uniform_bias<MODE, KPAD, 32>(k0, qwave, qwave + 31, full, ub);
+      if (uni && ub == -INFINITY) break;
+      f32x16_t s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+      {
+        float kf[32];
+        fa_rowfrag(Ks[buf], kb, lane, kf);
+#pragma unroll
+        for (int t = 0; t < 32; ++t) s = MF32(kf[t], qf[t], s);
+      }
+      {
+        float vf[32];
+        fa_rowfrag(Vs[buf], kb, lane, vf);
+#pragma unroll
+        for (int t = 0; t < 32; ++t) dp = MF32(vf[t], df[t], dp);
+      }
+      if (uni) {
+        const float off = ub - lse;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = __builtin_amdgcn_exp2f(fmaf(s[r], a.scale_log2, off)) * (dp[r] - dl);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kl = kb + fa_kl(r, h);
+          const float x = score_adj<MODE, KPAD>(s[r], qi, c * FCH + kl, kl, full, a.Sk, kmask, a.scale_log2);
+          s[r] = __builtin_amdgcn_exp2f(x - lse) * (dp[r] - dl);  // exp2(-inf) = 0 for masked entries
+        }
+      }
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        float kc[16];
+        fa_colfrag<FPR>(Ks[buf], kb, dt * 32, lane, kc);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) acc[dt] = MF32(kc[t], s[t], acc[dt]);
+      }
+    } while (0);
+    if (more) { fa_store_chunk<FPR>(Ks[buf ^ 1], pk); fa_store_chunk<FPR>(Vs[buf ^ 1], pv); }
+    __syncthreads();
+  }
+  if (qi < a.Sq) {
+    float* dQ = a.dq + b * a.q_sb + hh * a.q_sh + (long)qi * a.q_ss;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) fa_store_rowT(dQ + dt * 32, acc[dt], lane, a.scale);
+  }
+}
+
+// dK, dV: key on the lane.  S = Q K^T, dP = dO V^T, P = exp2(S' - lse), dS = P o (dP - delta),
+// dV^T += dO^T P, dK^T += Q^T dS.
+template <int MODE, bool KPAD>
+__global__ __launch_bounds__(256, 2) void attn_f32_dkdv_kernel(AttnF32Args a) {
+  __shared__ __attribute__((aligned(16))) float Qs[2][FCH * FPR];
+  __shared__ __attribute__((aligned(16))) float Ds[2][FCH * FPR];
+  __shared__ float lse_s[2][FCH], dl_s[2][FCH];
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int kwave = blockIdx.x * 128 + w * 32;
+  const int kj = kwave + (lane & 31);
+  const float* Q = a.q + b * a.q_sb + hh * a.q_sh;
+  const float* K = a.k + b * a.k_sb + hh * a.k_sh;
+  const float* V = a.v + b * a.v_sb + hh * a.v_sh;
+  const float* dO = a.dout + b * a.o_sb + hh * a.o_sh;
+  const long rbase = ((long)b * a.H + hh) * a.Sq;
+  int qstart = 0;
+  if (MODE == 2) qstart = (blockIdx.x * 128) & ~(FCH - 1);
+  const int nchunks = qstart < a.Sq ? (a.Sq - qstart + FCH - 1) / FCH : 0;
+  FStage pq, pd;
+  float lse_r = INFINITY, dl_r = 0.f;
+  if (nchunks) {
+    fa_load_chunk(Q, a.q_ss, qstart, a.Sq, pq);
+    fa_load_chunk(dO, a.o_ss, qstart, a.Sq, pd);
+    if (threadIdx.x < FCH && qstart + (int)threadIdx.x < a.Sq) {
+      lse_r = a.lse[rbase + qstart + threadIdx.x];
+      dl_r = a.delta[rbase + qstart + threadIdx.x];
+    }
+  }
+  float kf[32], vf[32];
+  fa_ownrow(K, a.k_ss, kj, a.Sk, lane, kf);
+  fa_ownrow(V, a.v_ss, kj, a.Sk, lane, vf);
+  const bool kok = kj < a.Sk && !(KPAD && a.kpad[(long)b * a.Sk + kj]);
+  const float kbias = kok ? 0.f : -INFINITY;
+  f32x16_t dk[2], dv[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
+  if (nchunks) {
+    fa_store_chunk<FPR>(Qs[0], pq);
+    fa_store_chunk<FPR>(Ds[0], pd);
+    if (threadIdx.x < FCH) { lse_s[0][threadIdx.x] = lse_r; dl_s[0][threadIdx.x] = dl_r; }
+  }
+  __syncthreads();
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1, q0 = qstart + c * FCH;
+    const bool more = c + 1 < nchunks;
+    if (more) {
+      fa_load_chunk(Q, a.q_ss, q0 + FCH, a.Sq, pq);
+      fa_load_chunk(dO, a.o_ss, q0 + FCH, a.Sq, pd);
+      lse_r = INFINITY; dl_r = 0.f;
+      if (threadIdx.x < FCH && q0 + FCH + (int)threadIdx.x < a.Sq) {
+        lse_r = a.lse[rbase + q0 + FCH + threadIdx.x];
+        dl_r = a.delta[rbase + q0 + FCH + threadIdx.x];
+      }
+    }
+    do {
+      const int qb = 0;
+      if (MODE == 2 && q0 + 31 < kwave) break;  // every query of the block before every key
+      f32x16_t s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+      {
+        float qr[32];
+        fa_rowfrag(Qs[buf], qb, lane, qr);
+#pragma unroll
+        for (int t = 0; t < 32; ++t) s = MF32(qr[t], kf[t], s);
+      }
+      {
+        float dr[32];
+        fa_rowfrag(Ds[buf], qb, lane, dr);
+#pragma unroll
+        for (int t = 0; t < 32; ++t) dp = MF32(dr[t], vf[t], dp);
+      }
+      // s[r]: query q0 + qb + fa_kl(r, h), key kj.  Rows past Sq carry lse = +inf (p = 0).
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ql = qb + fa_kl(r, h);
+        const int qq = q0 + ql;
+        float x = fmaf(s[r], a.scale_log2, kbias);
+        if (MODE == 1) x += (kj < qq) ? LOG2E_F : 0.f;
+        if (MODE == 2) x = (kj > qq) ? -INFINITY : x;
+        const float p = __builtin_amdgcn_exp2f(x - lse_s[buf][ql]);
+        s[r] = p;
+        dp[r] = p * (dp[r] - dl_s[buf][ql]);
+      }
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        float dc[16];
+        fa_colfrag<FPR>(Ds[buf], qb, dt * 32, lane, dc);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) dv[dt] = MF32(dc[t], s[t], dv[dt]);
+        float qc[16];
+        fa_colfrag<FPR>(Qs[buf], qb, dt * 32, lane, qc);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) dk[dt] = MF32(qc[t], dp[t], dk[dt]);
+      }
+    } while (0);
+    if (more) {
+      fa_store_chunk<FPR>(Qs[buf ^ 1], pq);
+      fa_store_chunk<FPR>(Ds[buf ^ 1], pd);
+      if (threadIdx.x < FCH) { lse_s[buf ^ 1][threadIdx.x] = lse_r; dl_s[buf ^ 1][threadIdx.x] = dl_r; }
+    }
+    __syncthreads();
+  }
+  if (kj < a.Sk) {
+    float* dK = a.dk + b * a.k_sb + hh * a.k_sh + (long)kj * a.k_ss;
+    float* dV = a.dv + b * a.v_sb + hh * a.v_sh + (long)kj * a.v_ss;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      fa_store_rowT(dK + dt * 32, dk[dt], lane, a.scale);
+      fa_store_rowT(dV + dt * 32, dv[dt], lane, 1.0f);
+    }
+  }
+}
+
+#define SMI_ATTN_F32_DISPATCH(KERNEL, GRID, ARGS)                                                           \
+  do {                                                                                                     \
+    const bool kp_ = (ARGS).kpad != nullptr;                                                               \
+    switch ((ARGS).mode) {                                                                                 \
+      case 0: if (kp_) hipLaunchKernelGGL((KERNEL<0, true>), GRID, dim3(256), 0, st, ARGS);                \
+              else hipLaunchKernelGGL((KERNEL<0, false>), GRID, dim3(256), 0, st, ARGS); break;            \
+      case 1: if (kp_) hipLaunchKernelGGL((KERNEL<1, true>), GRID, dim3(256), 0, st, ARGS);                \
+              else hipLaunchKernelGGL((KERNEL<1, false>), GRID, dim3(256), 0, st, ARGS); break;            \
+      case 2: if (kp_) hipLaunchKernelGGL((KERNEL<2, true>), GRID, dim3(256), 0, st, ARGS);                \
+              else hipLaunchKernelGGL((KERNEL<2, false>), GRID, dim3(256), 0, st, ARGS); break;            \
+      default: return -1;                                                                                  \
+    }                                                                                                      \
+  } while (0)
+
+static int fa_ok(const AttnF32Args& a) {
+  // float4 access to every row: 16-B aligned bases and strides that are multiples of 4 floats
+  const long st[] = {a.q_ss, a.k_ss, a.v_ss, a.o_ss, a.q_sh, a.k_sh, a.v_sh, a.o_sh, a.q_sb, a.k_sb, a.v_sb, a.o_sb};
+  for (long s : st)
+    if (s % 4) return 0;
+  if ((((uintptr_t)a.q) | ((uintptr_t)a.k) | ((uintptr_t)a.v) | ((uintptr_t)a.o)) & 15) return 0;
+  return a.B > 0 && a.H > 0 && a.Sq > 0 && a.Sk > 0;
+}
+
+extern "C" int smi_attn_f32_fwd(const AttnF32Args* args, hipStream_t st) {
+  const AttnF32Args& a = *args;
+  if (!fa_ok(a)) return -1;
+  dim3 grid((a.Sq + 127) / 128, a.H, a.B);
+  SMI_ATTN_F32_DISPATCH(attn_f32_fwd_kernel, grid, a);
+  SMI_CHECK_LAUNCH();
+}
+
+extern "C" int smi_attn_f32_bwd(const AttnF32Args* args, hipStream_t st) {
+  const AttnF32Args& a = *args;
+  if (!fa_ok(a) || !a.dout || !a.delta || (((uintptr_t)a.dout | (uintptr_t)a.dq | (uintptr_t)a.dk | (uintptr_t)a.dv) & 15))
+    return -1;
+  SMI_ATTN_F32_DISPATCH(attn_f32_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), a);
+  SMI_ATTN_F32_DISPATCH(attn_f32_dkdv_kernel, dim3((a.Sk + 127) / 128, a.H, a.B), a);
+  SMI_CHECK_LAUNCH();
+}

@@ -59,6 +59,31 @@ __global__ void act_drop_bwd_kernel(const unsigned short* __restrict__ dy, const
   *(u16x8_t*)(dx + i) = o;
 }
 
+// fp32 form of act_drop_bwd (reference-precision path): 4 floats per lane, 16-B accesses.
+__global__ void act_drop_bwd_f32_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                        float* __restrict__ dx, long total, int act,
+                                        const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale) {
+  const uint32_t seed = smi_seed(seedp, salt);
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= total) return;
+  const float4 d = *(const float4*)(dy + i);
+  float4 yy = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (act) yy = *(const float4*)(y + i);
+  const float dv[4] = {d.x, d.y, d.z, d.w}, yv[4] = {yy.x, yy.y, yy.z, yy.w};
+  float o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float g = dv[j];
+    if (act == 1) g = yv[j] > 0.f ? g * (thresh ? dscale : 1.f) : 0.f;
+    else {
+      if (act == 2) g *= yv[j] * (1.f - yv[j]);
+      if (thresh) g = smi_keep(seed, (uint32_t)(i + j), thresh) ? g * dscale : 0.f;
+    }
+    o[j] = g;
+  }
+  *(float4*)(dx + i) = make_float4(o[0], o[1], o[2], o[3]);
+}
+
 // out[c] += sum_r x[r][c]  (bf16 [M,N] -> fp32 [N], accumulated into a gradient buffer).
 // Block = 32 column-vectors (8 columns each, 16-B loads) x 8 row phases over a 256-row chunk;
 // LDS reduce over the phases, then one fp32 atomic per column per block.  Single launch.
@@ -128,6 +153,14 @@ extern "C" int smi_act_drop_bwd(const void* dy, const void* y, void* dx, long to
   if (total % 8) return -1;
   hipLaunchKernelGGL(act_drop_bwd_kernel, dim3(nblk8(total)), dim3(256), 0, st, (const unsigned short*)dy,
                      (const unsigned short*)y, (unsigned short*)dx, total, act, seedp, salt, thresh, dscale);
+  SMI_CHECK_LAUNCH();
+}
+
+extern "C" int smi_act_drop_bwd_f32(const float* dy, const float* y, float* dx, long total, int act, const uint32_t* seedp,
+                                    uint32_t salt, uint32_t thresh, float dscale, hipStream_t st) {
+  if (total % 4) return -1;
+  hipLaunchKernelGGL(act_drop_bwd_f32_kernel, dim3((unsigned)((total / 4 + 255) / 256)), dim3(256), 0, st, dy, y, dx, total,
+                     act, seedp, salt, thresh, dscale);
   SMI_CHECK_LAUNCH();
 }
 

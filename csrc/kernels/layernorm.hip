@@ -2,34 +2,35 @@
 //
 // Reference semantics: transformer.py:86-101 (LayerNormalization: biased variance, eps inside
 // sqrt, gamma*y+beta) applied as norm(dropout(sublayer(x)) + x) at transformer.py:131-138 and
-// :209-223. One wave64 owns one row; each lane holds 8 contiguous bf16 (16-B loads), so D=512
-// is one 1-KiB wave-instruction per tensor. Statistics are fp32; the pre-norm sum is saved in
-// bf16 for the backward. dgamma/dbeta are reduced per block into fp32 partial slabs and summed
+// :209-223. One wave64 owns one row; each lane holds 8 contiguous elements (bf16: one 16-B load,
+// fp32 reference-precision path: two), so D=512 is one 1-KiB (2-KiB) wave-instruction per tensor.
+// Statistics are fp32; the pre-norm sum is saved in the activation dtype for the backward. dgamma/dbeta are reduced per block into fp32 partial slabs and summed
 // by a second kernel that accumulates into the caller's (flat) fp32 gradient buffer.
 #include "smi_common.h"
 
 // Every global load a row needs (h, r, gamma, beta; the dropout seed) is issued before the
 // first reduction: a load that depends on a reduction result serialises two memory latencies
 // per wave (measured: 20 us -> 8.6 us at 8192 x 512 for hoisting gamma/beta alone).
-template <int VPL>  // 8-element vectors per lane: D <= VPL * 512, D % 8 == 0
+// T = activation storage: unsigned short (bf16 path) or float (fp32 reference-precision path).
+template <int VPL, typename T>  // 8-element vectors per lane: D <= VPL * 512, D % 8 == 0
 __global__ __launch_bounds__(256) void ln_fwd_kernel(
-    const unsigned short* __restrict__ h, const unsigned short* __restrict__ r,
+    const T* __restrict__ h, const T* __restrict__ r,
     const float* __restrict__ gamma, const float* __restrict__ beta,
-    unsigned short* __restrict__ y, unsigned short* __restrict__ xsave,
+    T* __restrict__ y, T* __restrict__ xsave,
     float* __restrict__ mean_out, float* __restrict__ rstd_out,
     int M, int D, float eps, const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (row >= M) return;
   const size_t base = (size_t)row * D;
-  u16x8_t hv[VPL], rv[VPL];
+  V8<T> hv[VPL], rv[VPL];
   float4 g0[VPL], g1[VPL], b0[VPL], b1[VPL];
 #pragma unroll
   for (int v = 0; v < VPL; ++v) {
     const int col = v * 512 + lane * 8;
     if (col < D) {
-      hv[v] = *(const u16x8_t*)(h + base + col);
-      if (r) rv[v] = *(const u16x8_t*)(r + base + col);
+      hv[v].load(h + base + col);
+      if (r) rv[v].load(r + base + col);
       g0[v] = *(const float4*)(gamma + col); g1[v] = *(const float4*)(gamma + col + 4);
       b0[v] = *(const float4*)(beta + col); b1[v] = *(const float4*)(beta + col + 4);
     }
@@ -44,9 +45,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
     for (int j = 0; j < 8; ++j) {
       float a = 0.f;
       if (col < D) {
-        a = bf2f(hv[v][j]);
+        a = hv[v][j];
         if (thresh) a = smi_keep(seed, (uint32_t)(base + col + j), thresh) ? a * dscale : 0.f;
-        if (r) a += bf2f(rv[v][j]);
+        if (r) a += rv[v][j];
       }
       x[v][j] = a;
       s += a;
@@ -66,14 +67,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
     if (col >= D) continue;
     const float gg[8] = {g0[v].x, g0[v].y, g0[v].z, g0[v].w, g1[v].x, g1[v].y, g1[v].z, g1[v].w};
     const float bb[8] = {b0[v].x, b0[v].y, b0[v].z, b0[v].w, b1[v].x, b1[v].y, b1[v].z, b1[v].w};
-    u16x8_t out, xs;
+    float out[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      out[j] = f2bf((x[v][j] - mean) * rstd * gg[j] + bb[j]);
-      xs[j] = f2bf(x[v][j]);
-    }
-    *(u16x8_t*)(y + base + col) = out;
-    if (xsave) *(u16x8_t*)(xsave + base + col) = xs;
+    for (int j = 0; j < 8; ++j) out[j] = (x[v][j] - mean) * rstd * gg[j] + bb[j];
+    V8<T>::store(y + base + col, out);
+    if (xsave) V8<T>::store(xsave + base + col, x[v]);
   }
   if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
 }
@@ -81,20 +79,20 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
 // Backward: each wave owns RPW consecutive rows and issues ALL their loads (dy, xs, dres_add,
 // mean, rstd) up front, then runs the per-row math; dgamma/dbeta partials of the block's
 // 4*RPW rows are reduced across waves through LDS into one [D] slab row per block.
-template <int VPL, int RPW>
+template <int VPL, int RPW, typename T>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(
-    const unsigned short* __restrict__ dy, const unsigned short* __restrict__ xs,
+    const T* __restrict__ dy, const T* __restrict__ xs,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const float* __restrict__ gamma,
-    unsigned short* __restrict__ dres, unsigned short* __restrict__ dh,
-    const unsigned short* __restrict__ dres_add,
+    T* __restrict__ dres, T* __restrict__ dh,
+    const T* __restrict__ dres_add,
     float* __restrict__ part_g, float* __restrict__ part_b,
     int M, int D, const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale) {
   const float invD = 1.0f / (float)D;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int row0 = (blockIdx.x * 4 + wid) * RPW;
-  u16x8_t dv[RPW][VPL], xv[RPW][VPL], av[RPW][VPL];
+  V8<T> dv[RPW][VPL], xv[RPW][VPL], av[RPW][VPL];
   float mean[RPW], rstd[RPW];
   float4 ga[VPL], gb[VPL];
 #pragma unroll
@@ -113,9 +111,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     for (int v = 0; v < VPL; ++v) {
       const int col = v * 512 + lane * 8;
       if (col < D) {
-        dv[rr][v] = *(const u16x8_t*)(dy + base + col);
-        xv[rr][v] = *(const u16x8_t*)(xs + base + col);
-        if (dres_add) av[rr][v] = *(const u16x8_t*)(dres_add + base + col);
+        dv[rr][v].load(dy + base + col);
+        xv[rr][v].load(xs + base + col);
+        if (dres_add) av[rr][v].load(dres_add + base + col);
       }
     }
   }
@@ -139,8 +137,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         if (col < D) {
-          const float d = bf2f(dv[rr][v][j]);
-          xh[v][j] = (bf2f(xv[rr][v][j]) - mean[rr]) * rstd[rr];
+          const float d = dv[rr][v][j];
+          xh[v][j] = (xv[rr][v][j] - mean[rr]) * rstd[rr];
           g[v][j] = d * gam[j];
           pg[v][j] += d * xh[v][j];
           pb[v][j] += d;
@@ -157,17 +155,17 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     for (int v = 0; v < VPL; ++v) {
       const int col = v * 512 + lane * 8;
       if (col >= D) continue;
-      u16x8_t o1, o2;
+      float o1[8], o2[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float dx = rstd[rr] * (g[v][j] - s1 - xh[v][j] * s2);
-        o1[j] = f2bf(dx + (dres_add ? bf2f(av[rr][v][j]) : 0.f));
+        o1[j] = dx + (dres_add ? av[rr][v][j] : 0.f);
         float dd = dx;
         if (thresh) dd = smi_keep(seed, (uint32_t)(base + col + j), thresh) ? dx * dscale : 0.f;
-        o2[j] = f2bf(dd);
+        o2[j] = dd;
       }
-      if (dres) *(u16x8_t*)(dres + base + col) = o1;
-      if (dh) *(u16x8_t*)(dh + base + col) = o2;
+      if (dres) V8<T>::store(dres + base + col, o1);
+      if (dh) V8<T>::store(dh + base + col, o2);
     }
   }
   __shared__ float red[2][4][VPL * 512];
@@ -214,18 +212,57 @@ __global__ __launch_bounds__(256) void colsum2_kernel(const float* __restrict__ 
   }
 }
 
+template <typename T>
+static int ln_fwd_launch(const void* h, const void* r, const float* gamma, const float* beta, void* y, void* xsave,
+                         float* mean, float* rstd, int M, int D, float eps, const uint32_t* seedp, uint32_t salt,
+                         uint32_t thresh, float dscale, hipStream_t st) {
+  dim3 grid((M + 3) / 4), block(256);
+  const T* hh = (const T*)h; const T* rr = (const T*)r;
+  T* yy = (T*)y; T* xx = (T*)xsave;
+  if (D % 8 || D > 4096) return -1;
+  const int vpl = (D + 511) / 512;
+  if (vpl == 1) hipLaunchKernelGGL((ln_fwd_kernel<1, T>), grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale);
+  else if (vpl == 2) hipLaunchKernelGGL((ln_fwd_kernel<2, T>), grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale);
+  else if (vpl <= 4) hipLaunchKernelGGL((ln_fwd_kernel<4, T>), grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale);
+  else hipLaunchKernelGGL((ln_fwd_kernel<8, T>), grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale);
+  SMI_CHECK_LAUNCH();
+}
+
 extern "C" int smi_ln_fwd(const void* h, const void* r, const float* gamma, const float* beta, void* y,
                           void* xsave, float* mean, float* rstd, int M, int D, float eps,
                           const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, hipStream_t st) {
-  dim3 grid((M + 3) / 4), block(256);
-  const auto* hh = (const unsigned short*)h; const auto* rr = (const unsigned short*)r;
-  auto* yy = (unsigned short*)y; auto* xx = (unsigned short*)xsave;
-  if (D % 8 || D > 4096) return -1;
+  return ln_fwd_launch<unsigned short>(h, r, gamma, beta, y, xsave, mean, rstd, M, D, eps, seedp, salt, thresh, dscale, st);
+}
+extern "C" int smi_ln_fwd_f32(const void* h, const void* r, const float* gamma, const float* beta, void* y,
+                              void* xsave, float* mean, float* rstd, int M, int D, float eps,
+                              const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, hipStream_t st) {
+  return ln_fwd_launch<float>(h, r, gamma, beta, y, xsave, mean, rstd, M, D, eps, seedp, salt, thresh, dscale, st);
+}
+
+template <typename T>
+static int ln_bwd_launch(const void* dy, const void* xs, const float* mean, const float* rstd,
+                         const float* gamma, void* dres, void* dh, const void* dres_add,
+                         float* part_g, float* part_b, int nblocks, float* dgamma, float* dbeta,
+                         int accumulate, int M, int D, const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale,
+                         hipStream_t st) {
+  // nblocks = capacity (rows) of the partial slabs; the kernel needs ceil(M / (4 * RPW)) of them
+  const T* a = (const T*)dy; const T* b = (const T*)xs;
+  T* o1 = (T*)dres; T* o2 = (T*)dh;
+  const T* ad = (const T*)dres_add;
+  if (D % 8 || D > 2048) return -1;
   const int vpl = (D + 511) / 512;
-  if (vpl == 1) hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale);
-  else if (vpl == 2) hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale);
-  else if (vpl <= 4) hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale);
-  else hipLaunchKernelGGL(ln_fwd_kernel<8>, grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale);
+  const int rpw = vpl <= 2 ? 2 : 1;
+  const int nb = (M + 4 * rpw - 1) / (4 * rpw);
+  if (nb > nblocks) return -1;
+  dim3 grid(nb), block(256);
+  if (vpl == 1) hipLaunchKernelGGL((ln_bwd_kernel<1, 2, T>), grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, D, seedp, salt, thresh, dscale);
+  else if (vpl == 2) hipLaunchKernelGGL((ln_bwd_kernel<2, 2, T>), grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, D, seedp, salt, thresh, dscale);
+  else hipLaunchKernelGGL((ln_bwd_kernel<4, 1, T>), grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, D, seedp, salt, thresh, dscale);
+  if (dgamma) {  // else the caller reduces the partials itself (smi_ln_bwd_reduce, e.g. on a side stream)
+    const int groups = accumulate ? (nb >= 1024 ? 16 : (nb >= 256 ? 8 : (nb >= 64 ? 4 : 1))) : 1;
+    hipLaunchKernelGGL(colsum2_kernel, dim3((D + 63) / 64, groups), dim3(256), 0, st, part_g, part_b, nb, D, dgamma, dbeta,
+                       accumulate);
+  }
   SMI_CHECK_LAUNCH();
 }
 
@@ -234,25 +271,16 @@ extern "C" int smi_ln_bwd(const void* dy, const void* xs, const float* mean, con
                           float* part_g, float* part_b, int nblocks, float* dgamma, float* dbeta,
                           int accumulate, int M, int D, const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale,
                           hipStream_t st) {
-  // nblocks = capacity (rows) of the partial slabs; the kernel needs ceil(M / (4 * RPW)) of them
-  const auto* a = (const unsigned short*)dy; const auto* b = (const unsigned short*)xs;
-  auto* o1 = (unsigned short*)dres; auto* o2 = (unsigned short*)dh;
-  const auto* ad = (const unsigned short*)dres_add;
-  if (D % 8 || D > 2048) return -1;
-  const int vpl = (D + 511) / 512;
-  const int rpw = vpl <= 2 ? 2 : 1;
-  const int nb = (M + 4 * rpw - 1) / (4 * rpw);
-  if (nb > nblocks) return -1;
-  dim3 grid(nb), block(256);
-  if (vpl == 1) hipLaunchKernelGGL((ln_bwd_kernel<1, 2>), grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, D, seedp, salt, thresh, dscale);
-  else if (vpl == 2) hipLaunchKernelGGL((ln_bwd_kernel<2, 2>), grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, D, seedp, salt, thresh, dscale);
-  else hipLaunchKernelGGL((ln_bwd_kernel<4, 1>), grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, D, seedp, salt, thresh, dscale);
-  if (dgamma) {  // else the caller reduces the partials itself (smi_ln_bwd_reduce, e.g. on a side stream)
-    const int groups = accumulate ? (nb >= 1024 ? 16 : (nb >= 256 ? 8 : (nb >= 64 ? 4 : 1))) : 1;
-    hipLaunchKernelGGL(colsum2_kernel, dim3((D + 63) / 64, groups), dim3(256), 0, st, part_g, part_b, nb, D, dgamma, dbeta,
-                       accumulate);
-  }
-  SMI_CHECK_LAUNCH();
+  return ln_bwd_launch<unsigned short>(dy, xs, mean, rstd, gamma, dres, dh, dres_add, part_g, part_b, nblocks, dgamma,
+                                       dbeta, accumulate, M, D, seedp, salt, thresh, dscale, st);
+}
+extern "C" int smi_ln_bwd_f32(const void* dy, const void* xs, const float* mean, const float* rstd,
+                              const float* gamma, void* dres, void* dh, const void* dres_add,
+                              float* part_g, float* part_b, int nblocks, float* dgamma, float* dbeta,
+                              int accumulate, int M, int D, const uint32_t* seedp, uint32_t salt, uint32_t thresh,
+                              float dscale, hipStream_t st) {
+  return ln_bwd_launch<float>(dy, xs, mean, rstd, gamma, dres, dh, dres_add, part_g, part_b, nblocks, dgamma, dbeta,
+                              accumulate, M, D, seedp, salt, thresh, dscale, st);
 }
 
 // dgamma/dbeta (+)= column sums of the nb partial rows written by smi_ln_bwd

@@ -9,7 +9,9 @@ Module tree, attribute and parameter names match the reference exactly
 Each sublayer is one chain of fused ops (sparkmi.ops):
   linear(qkv) -> attention core -> linear(out) -> dropout+residual+LayerNorm
   linear1+ReLU+dropout -> linear2 -> dropout+residual+LayerNorm
-bf16 activations on GPU (fp32 master weights in the model's flat buffer), fp32 on CPU.
+GPU activation dtype per model: ``dtype="fp32"`` is the reference precision (fp32 activations and
+weights, fp32-input MFMA GEMMs and attention); ``dtype="bf16"`` runs bf16 activations / bf16
+weight shadow with fp32 master weights and fp32 accumulation.  CPU: fp32 torch math.
 
 Mask semantics:
   mask_mode="reference" reproduces the reference numerically: the encoder padding mask is a
@@ -48,6 +50,7 @@ class TransformerConfig:
     emb_dropout: float = 0.1          # SentenceEmbedding hard-codes p=0.1 (transformer.py:53)
     mask_mode: str = "reference"      # or "causal"
     pad_id: int = 0
+    dtype: str = "bf16"               # GPU activation dtype: "bf16" (fp32 master) or "fp32" (reference precision)
 
 
 def _share(obj, name, value):
@@ -68,8 +71,9 @@ class PositionalEncoding(nn.Module):
 
 
 class SentenceEmbedding(nn.Module):
-    def __init__(self, max_sequence_length, d_model, vocab_size, rng, p=0.1):
+    def __init__(self, max_sequence_length, d_model, vocab_size, rng, p=0.1, dtype="bf16"):
         super().__init__()
+        self.act_dtype = dtype
         self.vocab_size = vocab_size
         self.max_sequence_length = max_sequence_length
         self.embedding = nn.Embedding(vocab_size, d_model)
@@ -80,7 +84,8 @@ class SentenceEmbedding(nn.Module):
 
     def forward(self, x):
         p = self.dropout.p if self.training else 0.0
-        dtype = torch.bfloat16 if x.is_cuda else torch.float32
+        # the embedding's output dtype sets the dtype of every downstream fused op
+        dtype = torch.bfloat16 if (x.is_cuda and self.act_dtype == "bf16") else torch.float32
         return embedding(x, self.embedding.weight, self.position_encoder.table, p, self._rng, self.salt,
                          out_dtype=dtype)
 
@@ -179,9 +184,9 @@ class SequentialEncoder(nn.Sequential):
 
 class Encoder(nn.Module):
     def __init__(self, d_model, ffn_hidden, num_heads, drop_prob, num_layers, max_sequence_length, vocab_size, rng,
-                 emb_dropout=0.1):
+                 emb_dropout=0.1, dtype="bf16"):
         super().__init__()
-        self.sentence_embedding = SentenceEmbedding(max_sequence_length, d_model, vocab_size, rng, emb_dropout)
+        self.sentence_embedding = SentenceEmbedding(max_sequence_length, d_model, vocab_size, rng, emb_dropout, dtype)
         self.layers = SequentialEncoder(*[EncoderLayer(d_model, ffn_hidden, num_heads, drop_prob, rng)
                                           for _ in range(num_layers)])
 
@@ -226,9 +231,9 @@ class SequentialDecoder(nn.Sequential):
 
 class Decoder(nn.Module):
     def __init__(self, d_model, ffn_hidden, num_heads, drop_prob, num_layers, max_sequence_length, vocab_size, rng,
-                 emb_dropout=0.1):
+                 emb_dropout=0.1, dtype="bf16"):
         super().__init__()
-        self.sentence_embedding = SentenceEmbedding(max_sequence_length, d_model, vocab_size, rng, emb_dropout)
+        self.sentence_embedding = SentenceEmbedding(max_sequence_length, d_model, vocab_size, rng, emb_dropout, dtype)
         self.layers = SequentialDecoder(*[DecoderLayer(d_model, ffn_hidden, num_heads, drop_prob, rng)
                                           for _ in range(num_layers)])
 
@@ -242,24 +247,26 @@ class Transformer(nn.Module):
 
     def __init__(self, d_model=512, ffn_hidden=1024, num_heads=8, drop_prob=0.1, num_layers=1,
                  max_sequence_length=200, de_vocab_size=10000, src_vocab_size=None, tgt_vocab_size=None,
-                 mask_mode="reference", emb_dropout=0.1, pad_id=0, seed=0):
+                 mask_mode="reference", emb_dropout=0.1, pad_id=0, seed=0, dtype="bf16"):
         super().__init__()
+        if dtype not in ("bf16", "fp32"):
+            raise ValueError(f"dtype must be 'bf16' or 'fp32', got {dtype!r}")
         src_vocab_size = src_vocab_size or de_vocab_size
         tgt_vocab_size = tgt_vocab_size or de_vocab_size
         self.config = TransformerConfig(d_model, ffn_hidden, num_heads, drop_prob, num_layers, max_sequence_length,
-                                        src_vocab_size, tgt_vocab_size, emb_dropout, mask_mode, pad_id)
+                                        src_vocab_size, tgt_vocab_size, emb_dropout, mask_mode, pad_id, dtype)
         self.rng = DropoutRNG(seed)
         self.encoder = Encoder(d_model, ffn_hidden, num_heads, drop_prob, num_layers, max_sequence_length,
-                               src_vocab_size, self.rng, emb_dropout)
+                               src_vocab_size, self.rng, emb_dropout, dtype)
         self.decoder = Decoder(d_model, ffn_hidden, num_heads, drop_prob, num_layers, max_sequence_length,
-                               tgt_vocab_size, self.rng, emb_dropout)
+                               tgt_vocab_size, self.rng, emb_dropout, dtype)
         self.linear = nn.Linear(d_model, tgt_vocab_size)
 
     @classmethod
     def from_config(cls, cfg: TransformerConfig, seed=0):
         return cls(cfg.d_model, cfg.ffn_hidden, cfg.num_heads, cfg.drop_prob, cfg.num_layers,
                    cfg.max_sequence_length, cfg.tgt_vocab_size, cfg.src_vocab_size, cfg.tgt_vocab_size,
-                   cfg.mask_mode, cfg.emb_dropout, cfg.pad_id, seed)
+                   cfg.mask_mode, cfg.emb_dropout, cfg.pad_id, seed, cfg.dtype)
 
     def _modes(self, x, encoder_self_attention_mask, decoder_self_attention_mask, decoder_cross_attention_mask):
         if self.config.mask_mode == "reference":

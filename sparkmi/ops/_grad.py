@@ -149,14 +149,61 @@ _cb = [False]
 
 
 def _queue_flush():
+    """Schedule the end-of-backward flush once per backward.  The flag is set only after the
+    callback is registered; outside a backward pass (no engine to call back) flush now."""
     if not _cb[0]:
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(flush_deferred)
+        except RuntimeError:
+            flush_deferred()
+            return
         _cb[0] = True
-        torch.autograd.Variable._execution_engine.queue_callback(flush_deferred)
+
+
+# Listeners told when a parameter's gradient is QUEUED (not yet final): the data-parallel engine
+# flushes the queues early once every parameter of a gradient bucket is queued or final, so that
+# bucket's all-reduce starts during the backward instead of after it (sparkmi/parallel/ddp.py).
+_defer_listeners = []
+
+
+def add_defer_listener(fn):
+    _defer_listeners.append(fn)
+    return fn
+
+
+def remove_defer_listener(fn):
+    if fn in _defer_listeners:
+        _defer_listeners.remove(fn)
+
+
+def _queued(params):
+    for fn in list(_defer_listeners):
+        for p in params:
+            if p is not None:
+                fn(p)
+
+
+def pending():
+    """True when deferred work is queued or a flush is scheduled."""
+    return bool(_cb[0] or _ln_queue or _fold_queue or _group_queue)
+
+
+def reset_deferred():
+    """Drop stale deferred state before a new backward.  A backward that raised after queueing
+    work leaves the queues filled and the flush flag set (autograd discards its final callbacks);
+    without this reset every later backward would queue work that is never flushed."""
+    stale = pending()
+    _ln_queue.clear()
+    _fold_queue.clear()
+    _group_queue.clear()
+    _cb[0] = False
+    return stale
 
 
 def defer_ln_fold(part_g, part_b, nb, D, gg, gb, params, stream):
     _ln_queue.append((part_g, part_b, nb, D, gg, gb, params, stream))
     _queue_flush()
+    _queued(params)
 
 
 # ---- deferred split-K weight-gradient folds ----
@@ -170,6 +217,7 @@ _fold_queue = []
 def defer_wgrad_fold(slab, splits, n, gw, nb, gb, params, stream):
     _fold_queue.append((slab, splits, n, gw, nb, gb, params, stream))
     _queue_flush()
+    _queued(params)
 
 
 # ---- grouped weight-gradient GEMMs ----
@@ -187,11 +235,10 @@ GROUP_MAX = 40  # csrc/kernels/gemm.hip WG_MAX
 def defer_wgrad_group(dy, x, gw, gb, params, stream):
     _group_queue.append((dy, x, gw, gb, params, stream))
     _queue_flush()
+    _queued(params)
 
 
-def _flush_groups(C):
-    gq = list(_group_queue)
-    _group_queue.clear()
+def _flush_groups(C, gq):
     by_stream = {}
     for e in gq:
         by_stream.setdefault(e[5], []).append(e)
@@ -202,39 +249,43 @@ def _flush_groups(C):
             if e is None or len(batch) == GROUP_MAX or e[2].data_ptr() in outs or (
                     e[3] is not None and e[3].data_ptr() in outs):
                 if batch:
-                    C.gemm_wgrad_group([b[0].data_ptr() for b in batch], [b[0].stride(0) for b in batch],
-                                       [b[1].data_ptr() for b in batch], [b[1].stride(0) for b in batch],
-                                       [b[2].data_ptr() for b in batch],
-                                       [b[3].data_ptr() if b[3] is not None else 0 for b in batch],
-                                       [b[2].shape[0] for b in batch], [b[2].shape[1] for b in batch],
-                                       [b[0].shape[0] for b in batch], st)
+                    fn = C.gemm_wgrad_group if batch[0][0].dtype == torch.bfloat16 else C.gemm_f32_wgrad_group
+                    fn([b[0].data_ptr() for b in batch], [b[0].stride(0) for b in batch],
+                       [b[1].data_ptr() for b in batch], [b[1].stride(0) for b in batch],
+                       [b[2].data_ptr() for b in batch],
+                       [b[3].data_ptr() if b[3] is not None else 0 for b in batch],
+                       [b[2].shape[0] for b in batch], [b[2].shape[1] for b in batch],
+                       [b[0].shape[0] for b in batch], st)
                 batch, outs = [], set()
             if e is not None:
                 batch.append(e)
                 outs.add(e[2].data_ptr())
                 if e[3] is not None:
                     outs.add(e[3].data_ptr())
-    return gq
 
 
-def flush_deferred():
-    from .. import _native
-    _cb[0] = False
-    C = _native.C()
-    gq = _flush_groups(C)
-    lq = list(_ln_queue)
-    _ln_queue.clear()
+def _flush_ln(C, lq):
     by_stream = {}
     for e in lq:
         by_stream.setdefault(e[7], []).append(e)
     for st, es in by_stream.items():
-        for i in range(0, len(es), 32):
-            ch = es[i:i + 32]
-            C.ln_bwd_reduce_multi([e[0].data_ptr() for e in ch], [e[1].data_ptr() for e in ch],
-                                  [e[4].data_ptr() for e in ch], [e[5].data_ptr() for e in ch],
-                                  [e[2] for e in ch], [e[3] for e in ch], 1, st)
-    fq = list(_fold_queue)
-    _fold_queue.clear()
+        batch, outs = [], set()
+        for e in es + [None]:
+            # a batch's blocks add into their outputs without atomics: a LayerNorm used twice in
+            # one backward (same gamma/beta) must land in different launches
+            if e is None or len(batch) == 32 or e[4].data_ptr() in outs or e[5].data_ptr() in outs:
+                if batch:
+                    C.ln_bwd_reduce_multi([b[0].data_ptr() for b in batch], [b[1].data_ptr() for b in batch],
+                                          [b[4].data_ptr() for b in batch], [b[5].data_ptr() for b in batch],
+                                          [b[2] for b in batch], [b[3] for b in batch], 1, st)
+                batch, outs = [], set()
+            if e is not None:
+                batch.append(e)
+                outs.add(e[4].data_ptr())
+                outs.add(e[5].data_ptr())
+
+
+def _flush_folds(C, fq):
     by_stream = {}
     for e in fq:
         by_stream.setdefault(e[7], []).append(e)
@@ -242,7 +293,8 @@ def flush_deferred():
         batch, outs = [], set()
         for e in es + [None]:
             # a batch's outputs must be distinct (its blocks run concurrently)
-            if e is None or len(batch) == 64 or e[3].data_ptr() in outs:
+            if e is None or len(batch) == 64 or e[3].data_ptr() in outs or (
+                    e[5] is not None and e[5].data_ptr() in outs):
                 if batch:
                     C.splitk_fold_multi([b[0].data_ptr() for b in batch], [b[3].data_ptr() for b in batch],
                                         [b[5].data_ptr() if b[5] is not None else 0 for b in batch],
@@ -251,6 +303,25 @@ def flush_deferred():
             if e is not None:
                 batch.append(e)
                 outs.add(e[3].data_ptr())
+                if e[5] is not None:
+                    outs.add(e[5].data_ptr())
+
+
+def flush_deferred():
+    """Launch every queued weight-gradient GEMM / fold, then report the parameters final.
+    The queues are emptied first (try/finally): a launch that raises leaves no stale entries."""
+    from .. import _native
+    gq, lq, fq = list(_group_queue), list(_ln_queue), list(_fold_queue)
+    _group_queue.clear()
+    _ln_queue.clear()
+    _fold_queue.clear()
+    _cb[0] = False
+    if not (gq or lq or fq):
+        return
+    C = _native.C()
+    _flush_groups(C, gq)
+    _flush_ln(C, lq)
+    _flush_folds(C, fq)
     for e in lq:
         grad_ready(*e[6])
     for e in fq:

@@ -12,8 +12,10 @@ Mask modes (SURVEY.md Q6 — the reference's boolean-mask addition semantics):
                   "look-ahead" mask after its permute; used for decoder self and cross attn);
   * "causal"    — true causal masking (-inf on future keys; upper tiles skipped);
   * key_padding — optional bool [B,Sk], -inf on padded keys (true padding masking).
-GPU: csrc/kernels/attention.hip (flash-style fwd; dQ and dK/dV backward kernels, no S x S
-tensor in HBM).  CPU: torch reference math in fp32.
+GPU: csrc/kernels/attention.hip (bf16 activations, 16x16x32 bf16 MFMA) or
+csrc/kernels/attention_f32.hip (fp32 activations = reference precision, 32x32x2 f32 MFMA); both
+flash-style forward + dQ and dK/dV backward kernels, no S x S tensor in HBM.  CPU: torch
+reference math in fp32.
 """
 import math
 
@@ -92,28 +94,33 @@ class _AttnCore(torch.autograd.Function):
             return _merge(o.detach()).to(qsrc.dtype)
         C = _native.C()
         qsrc = qsrc.contiguous()
+        f32 = qsrc.dtype == torch.float32
+        es = qsrc.element_size()  # pointer offsets below are in bytes
         B, Sq = qsrc.shape[0], qsrc.shape[1]
         if cross:
             kvsrc = kvsrc.contiguous()
+            if kvsrc.dtype != qsrc.dtype:
+                raise TypeError(f"cross attention: q dtype {qsrc.dtype} != kv dtype {kvsrc.dtype}")
             hd = qsrc.shape[2] // H
             Sk = kvsrc.shape[1]
             qp, qs = qsrc.data_ptr(), (Sq * H * hd, H * hd, hd)
             kp, ks = kvsrc.data_ptr(), (Sk * 2 * H * hd, 2 * H * hd, 2 * hd)
-            vp, vs = kp + hd * 2, ks
+            vp, vs = kp + hd * es, ks
         else:
             hd = qsrc.shape[2] // (3 * H)
             Sk = Sq
             qp, qs = qsrc.data_ptr(), (Sq * 3 * H * hd, 3 * H * hd, 3 * hd)
-            kp, ks = qp + hd * 2, qs
-            vp, vs = qp + 2 * hd * 2, qs
+            kp, ks = qp + hd * es, qs
+            vp, vs = qp + 2 * hd * es, qs
         if hd != 64:
             raise NotImplementedError("sparkmi attention kernel supports head_dim 64")
-        o = torch.empty(B, Sq, H * hd, device=qsrc.device, dtype=torch.bfloat16)
+        o = torch.empty(B, Sq, H * hd, device=qsrc.device, dtype=qsrc.dtype if f32 else torch.bfloat16)
         lse = torch.empty(B, H, Sq, device=qsrc.device, dtype=torch.float32)
         os_ = (Sq * H * hd, H * hd, hd)
         kpad = key_padding.to(torch.uint8).contiguous() if key_padding is not None else None
-        C.attn_fwd(qp, kp, vp, qs, ks, vs, o.data_ptr(), os_, lse.data_ptr(), _native.ptr(kpad), B, H, Sq, Sk, mode,
-                   _LOG2E / math.sqrt(hd), _native.stream())
+        fwd = C.attn_f32_fwd if f32 else C.attn_fwd
+        fwd(qp, kp, vp, qs, ks, vs, o.data_ptr(), os_, lse.data_ptr(), _native.ptr(kpad), B, H, Sq, Sk, mode,
+            _LOG2E / math.sqrt(hd), _native.stream())
         ctx.geom = (B, Sq, Sk, hd, qs, ks, vs, os_)
         ctx.kpad = kpad
         ctx.save_for_backward(qsrc, kvsrc if cross else None, o, lse)
@@ -137,23 +144,27 @@ class _AttnCore(torch.autograd.Function):
         B, Sq, Sk, hd, qs, ks, vs, os_ = ctx.geom
         H = ctx.H
         do = do.contiguous()
+        if do.dtype != o.dtype:
+            do = do.to(o.dtype)
+        es = qsrc.element_size()
         delta = torch.empty(B, H, Sq, device=do.device, dtype=torch.float32)
         if ctx.cross:
             dq = torch.empty_like(qsrc)
             dkv = torch.empty_like(kvsrc)
             qp, kp = qsrc.data_ptr(), kvsrc.data_ptr()
-            vp = kp + hd * 2
+            vp = kp + hd * es
             dqp, dkp = dq.data_ptr(), dkv.data_ptr()
-            dvp = dkp + hd * 2
+            dvp = dkp + hd * es
         else:
             dqkv = torch.empty_like(qsrc)
             qp = qsrc.data_ptr()
-            kp, vp = qp + hd * 2, qp + 4 * hd
+            kp, vp = qp + hd * es, qp + 2 * hd * es
             dqp = dqkv.data_ptr()
-            dkp, dvp = dqp + hd * 2, dqp + 4 * hd
-        C.attn_bwd(qp, kp, vp, qs, ks, vs, o.data_ptr(), do.data_ptr(), os_, lse.data_ptr(), delta.data_ptr(), dqp,
-                   dkp, dvp, _native.ptr(ctx.kpad), B, H, Sq, Sk, ctx.mode, _LOG2E / math.sqrt(hd),
-                   1.0 / math.sqrt(hd), _native.stream())
+            dkp, dvp = dqp + hd * es, dqp + 2 * hd * es
+        bwd = C.attn_f32_bwd if qsrc.dtype == torch.float32 else C.attn_bwd
+        bwd(qp, kp, vp, qs, ks, vs, o.data_ptr(), do.data_ptr(), os_, lse.data_ptr(), delta.data_ptr(), dqp,
+            dkp, dvp, _native.ptr(ctx.kpad), B, H, Sq, Sk, ctx.mode, _LOG2E / math.sqrt(hd),
+            1.0 / math.sqrt(hd), _native.stream())
         if ctx.cross:
             return dq, dkv, None, None, None, None
         return dqkv, None, None, None, None, None

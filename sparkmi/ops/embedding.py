@@ -36,12 +36,14 @@ class EmbeddingFn(torch.autograd.Function):
         ids_c = ids.contiguous().to(torch.int64)
         if ctx.native:
             C = _native.C()
-            out = torch.empty(*B, D, device=ids.device, dtype=torch.bfloat16)
+            f32 = out_dtype == torch.float32
+            out = torch.empty(*B, D, device=ids.device, dtype=torch.float32 if f32 else torch.bfloat16)
             if pe is not None and pe.shape[0] < S:
                 raise ValueError(f"sequence length {S} exceeds positional table {pe.shape[0]}")
-            C.emb_fwd(ids_c.data_ptr(), bf16_weight(weight).data_ptr(), _native.ptr(pe), out.data_ptr(), T, D,
-                      S if pe is not None else 1, rng.ptr(), salt, _rng.threshold(p), _rng.scale(p),
-                      _native.stream())
+            table = weight.detach() if f32 else bf16_weight(weight)
+            (C.emb_fwd_f32 if f32 else C.emb_fwd)(ids_c.data_ptr(), table.data_ptr(), _native.ptr(pe), out.data_ptr(),
+                                                  T, D, S if pe is not None else 1, rng.ptr(), salt,
+                                                  _rng.threshold(p), _rng.scale(p), _native.stream())
             ctx.seed = 0
         else:
             x = weight.float()[ids_c]
@@ -63,8 +65,9 @@ class EmbeddingFn(torch.autograd.Function):
         if ctx.native:
             C = _native.C()
             dout = dout.contiguous()
-            C.emb_bwd(ids.data_ptr(), dout.data_ptr(), gw.data_ptr(), T, D, ctx.pad, ctx.rng.ptr(), ctx.salt,
-                      _rng.threshold(ctx.p), _rng.scale(ctx.p), _native.stream())
+            bwd = C.emb_bwd_f32 if dout.dtype == torch.float32 else C.emb_bwd
+            bwd(ids.data_ptr(), dout.data_ptr(), gw.data_ptr(), T, D, ctx.pad, ctx.rng.ptr(), ctx.salt,
+                _rng.threshold(ctx.p), _rng.scale(ctx.p), _native.stream())
         else:
             g = dout.float()
             if ctx.p > 0:

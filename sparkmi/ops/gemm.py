@@ -144,3 +144,57 @@ def wgrad(dy, x, gw, splits=None, gb=None, ready=None):
     C.gemm_wgrad_atomic(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), N, K, M, gw.data_ptr(),
                         gw.stride(0), s, _native.ptr(gb), _native.stream())
     return gw
+
+# ---- fp32 (reference-precision) GEMM: csrc/kernels/gemm_f32.hip on v_mfma_f32_32x32x2_f32 ----
+def supported32(M, N, K, *tensors, mode=0):
+    """fp32 GEMM preconditions: float4 granularity along each operand's contiguous dimension
+    (mode 0/1: K % 4; mode 1: N % 4; mode 2: the two output dims % 4), 16-B aligned rows."""
+    if _DISABLE or M < 1 or N < 1 or K < 1:
+        return False
+    if mode in (0, 1) and K % 4:
+        return False
+    if mode in (1, 2) and N % 4:
+        return False
+    if mode == 2 and M % 4:
+        return False
+    for t in tensors:
+        if t is not None and (t.dtype != torch.float32 or t.stride(-1) != 1 or (t.dim() > 1 and t.stride(-2) % 4)):
+            return False
+    return _aligned(*tensors)
+
+
+def fwd32(x, w, bias=None, act=0, rng=None, salt=0, thresh=0, dscale=1.0, out=None):
+    """y[M,N] = dropout(act(x[M,K] @ w[N,K]^T + bias)), fp32 in / out; act 0 none, 1 relu, 2 sigmoid."""
+    M, K = x.shape
+    N = w.shape[0]
+    y = out if out is not None else torch.empty(M, N, device=x.device, dtype=torch.float32)
+    _native.C().gemm_f32(0, x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), M, N, K, y.data_ptr(), y.stride(0),
+                         0, 0, _native.ptr(bias), int(act), 0, 0, 0, 0,
+                         rng.ptr() if rng is not None else 0, salt, thresh, dscale, 1, 0, _native.stream())
+    return y
+
+
+def dgrad32(dy, w, resid=None, dact_y=None, dscale=1.0, out=None):
+    """dx[M,K] = (dy[M,N] @ w[N,K]) (+ resid) (* [dact_y > 0] * dscale), fp32."""
+    M, N = dy.shape
+    K = w.shape[1]
+    dx = out if out is not None else torch.empty(M, K, device=dy.device, dtype=torch.float32)
+    _native.C().gemm_f32(1, dy.data_ptr(), dy.stride(0), w.data_ptr(), w.stride(0), M, K, N, dx.data_ptr(),
+                         dx.stride(0), 0, 0, 0, 0, _native.ptr(resid), resid.stride(0) if resid is not None else 0,
+                         _native.ptr(dact_y), dact_y.stride(0) if dact_y is not None else 0, 0, 0, 0, dscale, 1, 0,
+                         _native.stream())
+    return dx
+
+
+def wgrad32(dy, x, gw, gb=None, splits=None):
+    """gw[N,K] += dy[M,N]^T @ x[M,K] (and gb[N] += column sums of dy), fp32.  Standalone form:
+    split-K over the M tokens with fp32 atomics so a few output tiles still fill the chip (the
+    training path queues wgrads into one grouped launch instead, sparkmi/ops/_grad.py)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    tiles = ((N + 127) // 128) * ((K + 127) // 128)
+    s = splits or max(1, min(M // 256, (2 * NUM_CU + tiles - 1) // tiles))
+    _native.C().gemm_f32(2, dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), N, K, M, gw.data_ptr(),
+                         gw.stride(0), 1, int(s > 1), 0, 0, 0, 0, 0, 0, 0, 0, 0, 1.0, s, _native.ptr(gb),
+                         _native.stream())
+    return gw

@@ -44,7 +44,10 @@ class AddDropoutLayerNorm(torch.autograd.Function):
             xs = torch.empty_like(h)
             mean = torch.empty(M, device=h.device, dtype=torch.float32)
             rstd = torch.empty(M, device=h.device, dtype=torch.float32)
-            C.ln_fwd(h.data_ptr(), _native.ptr(r), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(), xs.data_ptr(),
+            if r is not None and r.dtype != h.dtype:
+                raise TypeError(f"layernorm: residual dtype {r.dtype} != input dtype {h.dtype}")
+            fwd = C.ln_fwd_f32 if h.dtype == torch.float32 else C.ln_fwd
+            fwd(h.data_ptr(), _native.ptr(r), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(), xs.data_ptr(),
                      mean.data_ptr(), rstd.data_ptr(), M, D, eps, rng.ptr(), salt, _rng.threshold(p), _rng.scale(p),
                      _native.stream())
             ctx.native = True
@@ -71,7 +74,8 @@ class AddDropoutLayerNorm(torch.autograd.Function):
             rows_per_block = 4 * (2 if vpl <= 2 else 1)  # ln_bwd_kernel<VPL, RPW>
             nb = (M + rows_per_block - 1) // rows_per_block
             part = torch.empty(2, nb, D, device=dy.device, dtype=torch.float32)
-            C.ln_bwd(dy.data_ptr(), xs.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(),
+            bwd = C.ln_bwd_f32 if dy.dtype == torch.float32 else C.ln_bwd
+            bwd(dy.data_ptr(), xs.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(),
                      _native.ptr(dres), dh.data_ptr(), 0, part[0].data_ptr(), part[1].data_ptr(), nb,
                      0, 0, 1, M, D, ctx.rng.ptr(), ctx.salt, _rng.threshold(p), _rng.scale(p), _native.stream())
             if _grad.LN_DEFER:  # folded with every other LayerNorm's at the end of the backward

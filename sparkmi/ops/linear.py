@@ -6,9 +6,11 @@ y = dropout_p(act(x @ W^T + b)).  Reference call sites: every nn.Linear of trans
 :271), the MLP (distributed_multilayer_perceptron.py:47-53) and the CNN classifier
 (distributed_cnn.py:74-78).
 
-GPU path (bf16 activations, bf16 weight shadow, fp32 master/grad) — sparkmi's own MFMA GEMM
-(csrc/kernels/gemm.hip, sparkmi/ops/gemm.py) whenever the shape fits (K % 64 == 0, rows 16-B
-aligned), hipBLASLt through torch otherwise:
+GPU paths, chosen by the activation dtype:
+  * fp32 (reference precision): csrc/kernels/gemm_f32.hip on the fp32-input matrix cores
+    (v_mfma_f32_32x32x2_f32), fp32 master weights used directly, the same fused epilogues;
+  * bf16 (bf16 weight shadow, fp32 master/grad): csrc/kernels/gemm.hip (16x16x32 bf16 MFMA)
+    whenever the shape fits (K % 64 == 0, rows 16-B aligned), hipBLASLt through torch otherwise.
   * forward: ONE kernel = GEMM + bias + ReLU + dropout epilogue (counter-based mask, nothing
     saved but the output);
   * backward: dgrad GEMM (bf16 out), wgrad GEMM accumulating fp32 straight into the flat
@@ -35,6 +37,13 @@ def _blaslt_wgrad(gw, dy2, x2):
         gw.add_(torch.mm(dy2.t(), x2).float())
 
 
+_GROUP_LIMIT = 1 << 31  # descriptor / 32-bit offset range of the grouped wgrad launches
+
+
+def _groupable(*ts):
+    return all(t.numel() * t.element_size() < _GROUP_LIMIT for t in ts)
+
+
 def _wgrad_accumulate(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, gb=None, ready=None):
     """gw (fp32 [N,K]) += dy2^T @ x2 with fp32 accumulation on the GPU; gb (fp32 [N], optional)
     += column sums of dy2 — fused into sparkmi's wgrad kernel, a column-sum kernel otherwise.
@@ -42,8 +51,17 @@ def _wgrad_accumulate(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, gb=
     end-of-backward flush, sparkmi/ops/_grad.py); otherwise the caller reports it."""
     N, K = gw.shape
     M = dy2.shape[0]
+    if dy2.dtype == torch.float32:
+        if not G.supported32(N, K, M, dy2, x2, mode=2) or not gw.is_contiguous():
+            raise RuntimeError(f"fp32 wgrad: unsupported shape/layout N={N} K={K} M={M}")
+        if ready is not None and _grad.WGRAD_GROUP and _groupable(dy2, x2) and (gb is None or gb.is_contiguous()):
+            _grad.defer_wgrad_group(dy2, x2, gw, gb, ready, _native.stream())
+            return True
+        G.wgrad32(dy2, x2, gw, gb=gb)
+        return False
     if (ready is not None and _grad.WGRAD_GROUP and G.supported(N, K, M, dy2, x2, mode=2) and gw.is_contiguous()
-            and (gb is None or gb.is_contiguous()) and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16):
+            and (gb is None or gb.is_contiguous()) and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
+            and _groupable(dy2, x2)):
         _grad.defer_wgrad_group(dy2, x2, gw, gb, ready, _native.stream())
         return True
     if G.supported(N, K, M, dy2, x2, mode=2) and gw.is_contiguous():
@@ -79,6 +97,10 @@ def _blaslt_dgrad(g2, w_bf, resid, dact_y, dscale):
 def _dgrad(g2, w_bf, resid=None, dact_y=None, dscale=1.0):
     M, N = g2.shape
     K = w_bf.shape[1]
+    if g2.dtype == torch.float32:
+        if not G.supported32(M, K, N, g2, w_bf, resid, dact_y, mode=1):
+            raise RuntimeError(f"fp32 dgrad: unsupported shape/layout M={M} K={K} N={N}")
+        return G.dgrad32(g2, w_bf, resid=resid, dact_y=dact_y, dscale=dscale)
     if G.supported(M, K, N, g2, w_bf, resid, dact_y, mode=1):
         key = ("dgrad", M, K, N, resid is not None, dact_y is not None)
         c = G.choose(key, lambda: G.dgrad(g2, w_bf, resid=resid, dact_y=dact_y, dscale=dscale),
@@ -105,10 +127,20 @@ def _blaslt_fwd(x2, weight, w, bias, act, p, rng, salt):
     return y2
 
 
+def compute_weight(p: torch.Tensor, dtype) -> torch.Tensor:
+    """The weight operand for activations of ``dtype``: the fp32 master itself, or its bf16 shadow."""
+    return p.detach() if dtype == torch.float32 else bf16_weight(p)
+
+
 def _fwd_native(x2, weight, bias, act, p, rng, salt):
     N, K = weight.shape
-    w = bf16_weight(weight)
     M = x2.shape[0]
+    if x2.dtype == torch.float32:
+        w = weight.detach()
+        if not G.supported32(M, N, K, x2, w, mode=0):
+            raise RuntimeError(f"fp32 linear: unsupported shape/layout M={M} N={N} K={K}")
+        return G.fwd32(x2, w, bias, act, rng, salt, _rng.threshold(p), _rng.scale(p))
+    w = bf16_weight(weight)
     if G.supported(M, N, K, x2, w, mode=0) and act in (0, 1):
         key = ("fwd", M, N, K, bias is not None, act, p > 0)
         c = G.choose(key, lambda: G.fwd(x2, w, bias, act, rng, salt, _rng.threshold(p), _rng.scale(p)),
@@ -174,12 +206,13 @@ class LinearFn(torch.autograd.Function):
             dy2 = dy2.contiguous()
             if act or p > 0:
                 g2 = torch.empty_like(dy2)
-                C.act_drop_bwd(dy2.data_ptr(), _native.ptr(y2), g2.data_ptr(), dy2.numel(), act, ctx.rng.ptr(),
-                               ctx.salt, _rng.threshold(p), _rng.scale(p), _native.stream())
+                fn = C.act_drop_bwd_f32 if dy2.dtype == torch.float32 else C.act_drop_bwd
+                fn(dy2.data_ptr(), _native.ptr(y2), g2.data_ptr(), dy2.numel(), act, ctx.rng.ptr(),
+                   ctx.salt, _rng.threshold(p), _rng.scale(p), _native.stream())
             else:
                 g2 = dy2
             resid = _slot_grad(ctx.x_slot, g2.shape[0])
-            dx = _dgrad(g2, bf16_weight(weight), resid=resid) if ctx.needs_input_grad[0] else None
+            dx = _dgrad(g2, compute_weight(weight, g2.dtype), resid=resid) if ctx.needs_input_grad[0] else None
             bgrad = grad_buf(bias) if bias is not None else None
             with _grad.side(g2.device, g2, x2):
                 deferred = _wgrad_accumulate(gw, g2, x2, bgrad, ready=(weight, bias))
@@ -255,13 +288,13 @@ class FFNFn(torch.autograd.Function):
         if ctx.native:
             dy2 = dy2.contiguous()
             # dh_pre = (dy @ W2) * relu'/dropout mask (from the saved output h), fused epilogue
-            dh = _dgrad(dy2, bf16_weight(w2), dact_y=h, dscale=_rng.scale(p))
+            dh = _dgrad(dy2, compute_weight(w2, dy2.dtype), dact_y=h, dscale=_rng.scale(p))
             gw2, gb2, gw1, gb1 = grad_buf(w2), grad_buf(b2), grad_buf(w1), grad_buf(b1)
             with _grad.side(dy2.device, dy2, h):
                 if not _wgrad_accumulate(gw2, dy2, h, gb2, ready=(w2, b2)):
                     grad_ready(w2, b2)
             resid = _slot_grad(ctx.x_slot, dh.shape[0])
-            dx = _dgrad(dh, bf16_weight(w1), resid=resid) if ctx.needs_input_grad[0] else None
+            dx = _dgrad(dh, compute_weight(w1, dh.dtype), resid=resid) if ctx.needs_input_grad[0] else None
             with _grad.side(dh.device, dh, x2):
                 if not _wgrad_accumulate(gw1, dh, x2, gb1, ready=(w1, b1)):
                     grad_ready(w1, b1)

@@ -7,7 +7,10 @@ module was called, so gradients were never synchronised).  Design for MI355X + R
   reverse layer order, so buckets are plain contiguous slices — no pack/unpack kernels;
 * a bucket's all-reduce is issued the moment its last parameter's backward kernel has been
   enqueued (ops call ``grad_ready``), on RCCL's stream, so communication of late layers runs
-  under the backward of early layers;
+  under the backward of early layers.  Weight gradients that the fused ops DEFER (grouped
+  weight-gradient GEMMs, LayerNorm / split-K folds, sparkmi/ops/_grad.py) are flushed early,
+  per bucket: once every parameter of a bucket is queued or final, the queues are launched, the
+  parameters become final and the bucket goes to RCCL — in reverse layer order, during backward;
 * buckets are large (default 64 MiB): an 8-GPU ring over xGMI is per-link bandwidth bound, and
   fewer, larger collectives amortise the per-call latency;
 * averaging is folded into the optimizer (``grad_scale = 1/world``) instead of a division
@@ -38,11 +41,13 @@ class DataParallel:
         self._pending = None
         self._works = []
         self._listener = None
+        self._dlistener = None
         if self.world > 1:
             if broadcast:
                 broadcast_flat(flat, 0, group)
             if overlap:
                 self._listener = _grad.add_listener(self._on_ready)
+                self._dlistener = _grad.add_defer_listener(self._on_queued)
         self.reset()
 
     def _build_buckets(self, cuts=()):
@@ -82,15 +87,20 @@ class DataParallel:
         """Enable / disable launching bucket all-reduces from inside backward (grad_ready)."""
         if on and self._listener is None and self.world > 1:
             self._listener = _grad.add_listener(self._on_ready)
+            self._dlistener = _grad.add_defer_listener(self._on_queued)
         elif not on and self._listener is not None:
             _grad.remove_listener(self._listener)
-            self._listener = None
+            _grad.remove_defer_listener(self._dlistener)
+            self._listener = self._dlistener = None
         self.overlap = bool(on)
 
     def reset(self):
         self._pending = [len(idx) for (_, _, idx) in self.buckets]
+        self._unsettled = [len(idx) for (_, _, idx) in self.buckets]
+        self._settled = set()
         self._launched = [False] * len(self.buckets)
         self._works = []
+        self.early_flushes = 0
 
     def _launch(self, b):
         if self._launched[b]:
@@ -111,10 +121,31 @@ class DataParallel:
         return [b for b, (_, _, idx) in enumerate(self.buckets)
                 if all(id(self.flat.params[i]) in ready_ids for i in idx)]
 
+    def _settle(self, i):
+        """Count parameter ``i`` as queued-or-final; returns its bucket if that completed it."""
+        if i in self._settled:
+            return None
+        self._settled.add(i)
+        b = self.bucket_of[i]
+        self._unsettled[b] -= 1
+        return b if self._unsettled[b] == 0 else None
+
+    def _on_queued(self, p):
+        i = self.flat.index.get(id(p))
+        if i is None or self._pending is None:
+            return
+        b = self._settle(i)
+        if b is not None and self._pending[b] > 0:
+            # every parameter of bucket b is queued or final: launch the queued weight-gradient
+            # work now (its completion reports the parameters ready -> _on_ready launches b)
+            self.early_flushes += 1
+            _grad.flush_deferred()
+
     def _on_ready(self, p):
         i = self.flat.index.get(id(p))
         if i is None or self._pending is None:
             return
+        self._settle(i)
         b = self.bucket_of[i]
         self._pending[b] -= 1
         if self._pending[b] == 0:
@@ -139,3 +170,6 @@ class DataParallel:
         if self._listener is not None:
             _grad.remove_listener(self._listener)
             self._listener = None
+        if self._dlistener is not None:
+            _grad.remove_defer_listener(self._dlistener)
+            self._dlistener = None

@@ -48,6 +48,7 @@ class StepRunner:
         return self.ddp is not None and self.ddp.world > 1
 
     def _fwd_bwd(self, *batch):
+        _grad.reset_deferred()  # a previous backward that raised must not leave queued work behind
         rng = getattr(self.model, "rng", None)
         if rng is not None:
             rng.advance()
@@ -85,6 +86,7 @@ class StepRunner:
         return loss
 
     def _fwd_bwd_split(self, *batch):
+        _grad.reset_deferred()
         rng = getattr(self.model, "rng", None)
         if rng is not None:
             rng.advance()

@@ -43,7 +43,7 @@ class Trainer:
         self.flat = FlatParams(self.model, device=self.device, shadow=shadow)
         self.opt = make_optimizer(self.flat)
         self.ddp = DataParallel(self.flat, bucket_mb=cfg.bucket_mb) if world > 1 else None
-        use_graph = bool(cfg.graph) and self.device.type == "cuda" and world == 1
+        use_graph = bool(cfg.graph) and self.device.type == "cuda"
         self.runner = StepRunner(self.model, loss_fn, self.opt, ddp=self.ddp, graph=use_graph)
         path = f"{cfg.metrics}.rank{rank}.jsonl" if cfg.metrics else None
         self.metrics = MetricsLogger(path, rank=rank, every=cfg.log_every, echo=cfg.verbose and rank == 0,

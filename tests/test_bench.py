@@ -1,0 +1,56 @@
+"""bench.py contract on CPU (gloo): ``--gpus N`` runs N ranks (self-spawned, or under
+torch.distributed.run), reports ``n_gpus = N`` and ``global_batch = N x batch`` (weak scaling),
+and rank 0 prints exactly one JSON line with the driver's keys."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TINY = ["--device", "cpu", "--model", "transformer", "--layers", "1", "--seq", "16", "--vocab", "64", "--batch", "2",
+        "--steps", "2", "--warmup", "1"]
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _run(cmd, env=None):
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    e.pop("RANK", None)
+    e.update(env or {})
+    r = subprocess.run(cmd, cwd=ROOT, env=e, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def _check(out, n):
+    assert KEYS <= set(out)
+    assert out["n_gpus"] == n
+    assert out["config"]["global_batch"] == 2 * n
+    assert out["config"]["parallelism"] == f"dp{n}"
+    assert out["steps"] == 2 and out["warmup"] == 1
+    assert out["dtype"] == "fp32" and out["value"] > 0
+    assert out["scaling"] == "weak" and out["higher_is_better"] is True
+
+
+def test_bench_single_rank():
+    out = _run([sys.executable, "bench.py", "--gpus", "1"] + TINY)
+    _check(out, 1)
+    assert out["allreduce_ms"] is None
+
+
+def test_bench_spawns_ranks():
+    out = _run([sys.executable, "bench.py", "--gpus", "2"] + TINY)
+    _check(out, 2)
+    assert out["allreduce_ms"] is not None and out["transformer_fp32"]["grad_bytes"] > 0
+
+
+@pytest.mark.slow
+def test_bench_under_torchrun():
+    out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", "29631", "bench.py", "--gpus", "2"] + TINY)
+    _check(out, 2)

@@ -1,0 +1,302 @@
+"""T4/T5 for the REFERENCE-PRECISION (fp32) GPU path: every fp32 HIP kernel (gemm_f32.hip,
+attention_f32.hip, fp32 LayerNorm / embedding / act-backward instances) against a float64 torch
+reference of the same op at fp32 tolerances, and the fp32 transformer against the CPU fp32
+reference modules — one step (logits + every gradient) and a multi-step Adam loss curve."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from sparkmi import _native  # noqa: E402
+from sparkmi.ops import gemm as G  # noqa: E402
+from sparkmi.ops import rng as R  # noqa: E402
+from sparkmi.ops.attention import attention_reference, cross_attention, self_attention  # noqa: E402
+
+dev = "cuda"
+
+
+def _close(a, b, atol, rtol, msg=""):
+    a, b = a.double().cpu(), b.double().cpu()
+    err = (a - b).abs()
+    bad = err > atol + rtol * b.abs()
+    assert not bad.any(), f"{msg}: {bad.sum().item()} / {bad.numel()} mismatches, max err {err.max().item():.4g}"
+
+
+def _gemm_tol(a, b):
+    """fp32 fma-chain error bound scale: sum_k |a||b| (float64)."""
+    return a.double().abs() @ b.double().abs()
+
+
+def test_f32_kernels_loaded():
+    C = _native.C()
+    for n in ("gemm_f32", "gemm_f32_wgrad_group", "attn_f32_fwd", "attn_f32_bwd", "ln_fwd_f32", "ln_bwd_f32",
+              "emb_fwd_f32", "emb_bwd_f32", "act_drop_bwd_f32"):
+        assert hasattr(C, n), n
+
+
+def test_gemm_f32_layout_exact():
+    """Small integers: every product and sum is exact in fp32, so any fragment / k-permutation /
+    store-layout slip shows as an exact mismatch (asymmetric operands: row/col swaps visible)."""
+    g = torch.Generator().manual_seed(0)
+    M, N, K = 200, 136, 96
+    a = torch.randint(-3, 4, (M, K), generator=g).float()
+    w = torch.randint(-3, 4, (N, K), generator=g).float()
+    a[0, :] = torch.arange(K) % 5
+    y = G.fwd32(a.to(dev), w.to(dev))
+    assert torch.equal(y.cpu(), a @ w.t())
+    dy = torch.randint(-3, 4, (M, N), generator=g).float()
+    dx = G.dgrad32(dy.to(dev), w.to(dev))
+    assert torch.equal(dx.cpu(), dy @ w)
+    gw = torch.zeros(N, K, device=dev)
+    gb = torch.zeros(N, device=dev)
+    G.wgrad32(dy.to(dev), a.to(dev), gw, gb=gb, splits=1)
+    assert torch.equal(gw.cpu(), dy.t() @ a)
+    assert torch.equal(gb.cpu(), dy.sum(0))
+
+
+@pytest.mark.parametrize("M,N,K", [(8192, 512, 512), (1000, 1536, 512), (1024, 10000, 512), (333, 1024, 1024),
+                                   (64, 12, 20)])
+def test_gemm_f32_shapes(M, N, K):
+    torch.manual_seed(1)
+    a, w = torch.randn(M, K), torch.randn(N, K)
+    y = G.fwd32(a.to(dev), w.to(dev))
+    err = (y.cpu().double() - a.double() @ w.double().t()).abs()
+    assert (err <= 2e-6 * _gemm_tol(a, w.t()) + 1e-6).all(), float(err.max())
+    dy = torch.randn(M, N)
+    dx = G.dgrad32(dy.to(dev), w.to(dev))
+    err = (dx.cpu().double() - dy.double() @ w.double()).abs()
+    assert (err <= 2e-6 * _gemm_tol(dy, w) + 1e-6).all(), float(err.max())
+
+
+@pytest.mark.parametrize("N,K,M,splits", [(512, 512, 8192, 1), (1536, 512, 4096, 4), (10000, 512, 2048, 2),
+                                          (24, 40, 300, 1)])
+def test_gemm_f32_wgrad(N, K, M, splits):
+    torch.manual_seed(2)
+    dy, x = torch.randn(M, N), torch.randn(M, K)
+    gw0, gb0 = torch.randn(N, K), torch.randn(N)
+    gw, gb = gw0.to(dev), gb0.to(dev)
+    G.wgrad32(dy.to(dev), x.to(dev), gw, gb=gb, splits=splits)
+    ref = gw0.double() + dy.double().t() @ x.double()
+    err = (gw.cpu().double() - ref).abs()
+    assert (err <= 2e-6 * (_gemm_tol(dy.t(), x) + gw0.double().abs()) + 1e-6).all(), float(err.max())
+    _close(gb, gb0.double() + dy.double().sum(0), 1e-3, 1e-5, "bias grad")
+
+
+def test_gemm_f32_wgrad_group():
+    """The grouped no-split launch (several problems, one launch) == per-problem float64."""
+    torch.manual_seed(3)
+    C = _native.C()
+    probs = [(512, 512, 2048), (1536, 512, 2048), (1000, 512, 2048), (64, 128, 300)]
+    dys, xs, gws, gbs, refs, brefs = [], [], [], [], [], []
+    for (n, k, T) in probs:
+        dy, x = torch.randn(T, n), torch.randn(T, k)
+        gw, gb = torch.randn(n, k), torch.randn(n)
+        refs.append(gw.double() + dy.double().t() @ x.double())
+        brefs.append(gb.double() + dy.double().sum(0))
+        dys.append(dy.to(dev)); xs.append(x.to(dev)); gws.append(gw.to(dev)); gbs.append(gb.to(dev))
+    C.gemm_f32_wgrad_group([d.data_ptr() for d in dys], [d.stride(0) for d in dys], [x.data_ptr() for x in xs],
+                           [x.stride(0) for x in xs], [g.data_ptr() for g in gws], [b.data_ptr() for b in gbs],
+                           [p[0] for p in probs], [p[1] for p in probs], [p[2] for p in probs],
+                           _native.stream())
+    for i in range(len(probs)):
+        _close(gws[i], refs[i], 1e-3, 1e-5, f"group wgrad {i}")
+        _close(gbs[i], brefs[i], 1e-3, 1e-5, f"group bias {i}")
+
+
+@pytest.mark.parametrize("act,p", [(0, 0.0), (1, 0.0), (1, 0.1), (2, 0.0)])
+def test_linear_f32_epilogues(act, p):
+    from sparkmi.ops.linear import linear
+    torch.manual_seed(4)
+    M, N, K = 1000, 1024, 512
+    lin = torch.nn.Linear(K, N)
+    ling = torch.nn.Linear(K, N).to(dev)
+    ling.load_state_dict(lin.state_dict())
+    x = torch.randn(M, K)
+    xg, xc = x.to(dev).requires_grad_(), x.clone().requires_grad_()
+    rg, rc = R.DropoutRNG(5).to(dev), R.DropoutRNG(5)
+    yg = linear(xg, ling.weight, ling.bias, act, p, rg, 99)
+    yc = linear(xc, lin.weight, lin.bias, act, p, rc, 99)
+    assert yg.dtype == torch.float32
+    _close(yg, yc, 1e-4, 1e-5, "fwd")
+    dy = torch.randn(M, N)
+    yg.backward(dy.to(dev))
+    yc.backward(dy)
+    _close(xg.grad, xc.grad, 1e-4, 1e-5, "dx")
+    _close(ling.weight.grad, lin.weight.grad, 2e-3, 1e-5, "dw")
+    _close(ling.bias.grad, lin.bias.grad, 2e-3, 1e-5, "db")
+
+
+def test_ffn_f32():
+    from sparkmi.ops.linear import ffn
+    torch.manual_seed(6)
+    M, D, H = 1024, 512, 1024
+    l1, l2 = torch.nn.Linear(D, H), torch.nn.Linear(H, D)
+    g1, g2 = torch.nn.Linear(D, H).to(dev), torch.nn.Linear(H, D).to(dev)
+    g1.load_state_dict(l1.state_dict())
+    g2.load_state_dict(l2.state_dict())
+    x = torch.randn(M, D)
+    xg, xc = x.to(dev).requires_grad_(), x.clone().requires_grad_()
+    rg, rc = R.DropoutRNG(8).to(dev), R.DropoutRNG(8)
+    yg = ffn(xg, g1, g2, 0.1, rg, 77)
+    yc = ffn(xc, l1, l2, 0.1, rc, 77)
+    _close(yg, yc, 1e-4, 1e-5, "ffn fwd")
+    dy = torch.randn(M, D)
+    yg.backward(dy.to(dev))
+    yc.backward(dy)
+    _close(xg.grad, xc.grad, 1e-4, 1e-5, "ffn dx")
+    for a, b, n in ((g1.weight, l1.weight, "w1"), (g2.weight, l2.weight, "w2"), (g1.bias, l1.bias, "b1"),
+                    (g2.bias, l2.bias, "b2")):
+        _close(a.grad, b.grad, 2e-3, 1e-5, n)
+
+
+def _attn_f32(B, H, Sq, Sk, mode, cross, kp):
+    torch.manual_seed(7)
+    hd = 64
+    kpad = None
+    if cross:
+        q, kv = torch.randn(B, Sq, H * hd), torch.randn(B, Sk, 2 * H * hd)
+        if kp:
+            kpad = torch.zeros(B, Sk, dtype=torch.bool)
+            kpad[0, Sk // 2:] = True
+        qg, kvg = q.to(dev).requires_grad_(), kv.to(dev).requires_grad_()
+        og = cross_attention(qg, kvg, H, mode, kpad.to(dev) if kpad is not None else None)
+        qh = q.double().reshape(B, Sq, H, hd).permute(0, 2, 1, 3).requires_grad_()
+        t = kv.double().reshape(B, Sk, H, 2 * hd).permute(0, 2, 1, 3)
+        kh, vh = t[..., :hd].detach().requires_grad_(), t[..., hd:].detach().requires_grad_()
+    else:
+        qkv = torch.randn(B, Sq, 3 * H * hd)
+        qg = qkv.to(dev).requires_grad_()
+        og = self_attention(qg, H, mode)
+        t = qkv.double().reshape(B, Sq, H, 3 * hd).permute(0, 2, 1, 3)
+        qh, kh, vh = (t[..., :hd].detach().requires_grad_(), t[..., hd:2 * hd].detach().requires_grad_(),
+                      t[..., 2 * hd:].detach().requires_grad_())
+    assert og.dtype == torch.float32
+    mcode = {"none": 0, "reference": 1, "causal": 2}[mode]
+    s = (qh @ kh.transpose(-1, -2)) / math.sqrt(hd)
+    qi = torch.arange(Sq)[:, None]
+    kj = torch.arange(Sk)[None, :]
+    if mcode == 1:
+        s = s + (kj < qi).double()
+    elif mcode == 2:
+        s = s.masked_fill(kj > qi, float("-inf"))
+    if kpad is not None:
+        s = s.masked_fill(kpad[:, None, None, :], float("-inf"))
+    oc = torch.nan_to_num(torch.softmax(s, -1), nan=0.0) @ vh
+    oc_m = oc.permute(0, 2, 1, 3).reshape(B, Sq, H * hd)
+    _close(og, oc_m, 2e-5, 1e-5, f"attn f32 fwd {mode}")
+    do = torch.randn(B, Sq, H * hd)
+    og.backward(do.to(dev))
+    dq, dk, dv = torch.autograd.grad(oc_m, (qh, kh, vh), do.double())
+    if cross:
+        _close(qg.grad, dq.permute(0, 2, 1, 3).reshape(B, Sq, -1), 5e-5, 1e-5, "dq")
+        dkv = torch.cat([dk, dv], -1).permute(0, 2, 1, 3).reshape(B, Sk, -1)
+        _close(kvg.grad, dkv, 5e-5, 1e-5, "dkv")
+    else:
+        dqkv = torch.cat([dq, dk, dv], -1).permute(0, 2, 1, 3).reshape(B, Sq, -1)
+        _close(qg.grad, dqkv, 5e-5, 1e-5, f"dqkv {mode}")
+
+
+@pytest.mark.parametrize("mode", ["none", "reference", "causal"])
+@pytest.mark.parametrize("S", [256, 200, 37])
+def test_self_attention_f32(mode, S):
+    _attn_f32(2, 4, S, S, mode, False, False)
+
+
+@pytest.mark.parametrize("mode,kp", [("none", False), ("none", True), ("reference", False)])
+def test_cross_attention_f32(mode, kp):
+    _attn_f32(2, 3, 130, 130 if mode == "reference" else 77, mode, True, kp)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_layernorm_f32(p):
+    from sparkmi.ops.layernorm import add_dropout_layernorm
+    torch.manual_seed(9)
+    M, D = 1000, 512
+    h, r = torch.randn(M, D), torch.randn(M, D)
+    gamma = torch.nn.Parameter(torch.randn(D) * 0.5 + 1)
+    beta = torch.nn.Parameter(torch.randn(D) * 0.1)
+    gg, bg = torch.nn.Parameter(gamma.detach().to(dev)), torch.nn.Parameter(beta.detach().to(dev))
+    hg, rg = h.to(dev).requires_grad_(), r.to(dev).requires_grad_()
+    hc, rc = h.clone().requires_grad_(), r.clone().requires_grad_()
+    yg = add_dropout_layernorm(hg, rg, gg, bg, p, R.DropoutRNG(3).to(dev), 55)
+    yc = add_dropout_layernorm(hc, rc, gamma, beta, p, R.DropoutRNG(3), 55)
+    assert yg.dtype == torch.float32
+    _close(yg, yc, 2e-5, 1e-5, "ln fwd")
+    dy = torch.randn(M, D)
+    yg.backward(dy.to(dev))
+    yc.backward(dy)
+    _close(hg.grad, hc.grad, 2e-5, 1e-5, "dh")
+    _close(rg.grad, rc.grad, 2e-5, 1e-5, "dres")
+    _close(gg.grad, gamma.grad, 2e-3, 1e-5, "dgamma")
+    _close(bg.grad, beta.grad, 2e-3, 1e-5, "dbeta")
+
+
+def test_embedding_f32():
+    from sparkmi.ops.embedding import embedding, sinusoid_table
+    torch.manual_seed(10)
+    V, D, B, S = 1000, 512, 4, 64
+    w = torch.nn.Parameter(torch.randn(V, D))
+    wg = torch.nn.Parameter(w.detach().to(dev))
+    ids = torch.randint(0, V, (B, S))
+    pe = sinusoid_table(S, D)
+    yg = embedding(ids.to(dev), wg, pe.to(dev), 0.1, R.DropoutRNG(4).to(dev), 11, out_dtype=torch.float32)
+    yc = embedding(ids, w, pe, 0.1, R.DropoutRNG(4), 11, out_dtype=torch.float32)
+    assert yg.dtype == torch.float32
+    _close(yg, yc, 1e-6, 1e-6, "emb fwd")
+    dy = torch.randn(B, S, D)
+    yg.backward(dy.to(dev))
+    yc.backward(dy)
+    _close(wg.grad, w.grad, 1e-5, 1e-5, "emb bwd")
+
+
+def _pair(L=2, S=32, V=96, seed=0):
+    from sparkmi.models.transformer import Transformer
+    torch.manual_seed(seed)
+    mc = Transformer(d_model=128, ffn_hidden=256, num_heads=2, num_layers=L, max_sequence_length=S,
+                     src_vocab_size=V, tgt_vocab_size=V, seed=5, dtype="fp32")
+    torch.manual_seed(seed)
+    mg = Transformer(d_model=128, ffn_hidden=256, num_heads=2, num_layers=L, max_sequence_length=S,
+                     src_vocab_size=V, tgt_vocab_size=V, seed=5, dtype="fp32").to(dev)
+    return mc, mg
+
+
+def test_transformer_f32_step_matches_cpu():
+    from sparkmi.data.synthetic import translation_pairs
+    mc, mg = _pair()
+    mc.train(); mg.train()
+    src, tgt = translation_pairs(4, 32, 96, 96, seed=3)
+    lc = mc.training_step_loss(src, tgt)
+    lg = mg.training_step_loss(src.to(dev), tgt.to(dev))
+    assert abs(float(lc) - float(lg)) < 1e-5 * max(1.0, abs(float(lc))), (float(lc), float(lg))
+    lc.backward()
+    lg.backward()
+    for (n, pc), (_, pg) in zip(mc.named_parameters(), mg.named_parameters()):
+        rel = (pg.grad.cpu().double() - pc.grad.double()).norm() / (pc.grad.double().norm() + 1e-12)
+        assert rel < 1e-4, (n, float(rel))
+
+
+def test_transformer_f32_loss_curve_matches_cpu():
+    """60 Adam steps (dropout on, identical counter-based masks): the GPU fp32 trajectory stays on
+    the CPU fp32 reference trajectory."""
+    from sparkmi.data.synthetic import translation_pairs
+    from sparkmi.optim import Adam
+    from sparkmi.utils.flat import FlatParams
+    mc, mg = _pair(L=1, S=32, V=64, seed=1)
+    mc.train(); mg.train()
+    fc, fg = FlatParams(mc), FlatParams(mg, shadow=False)
+    oc, og = Adam(fc, lr=1e-3), Adam(fg, lr=1e-3)
+    src, tgt = translation_pairs(8, 32, 64, 64, seed=4)
+    sg, tg = src.to(dev), tgt.to(dev)
+    lcs, lgs = [], []
+    for _ in range(60):
+        mc.rng.advance(); mg.rng.advance()
+        lc = mc.training_step_loss(src, tgt)
+        lg = mg.training_step_loss(sg, tg)
+        lc.backward(); lg.backward()
+        oc.step(); og.step()
+        lcs.append(float(lc)); lgs.append(float(lg))
+    assert lcs[-1] < lcs[0] - 0.5, lcs  # it learns
+    for i, (a, b) in enumerate(zip(lcs, lgs)):
+        assert abs(a - b) <= 2e-3 * abs(a) + 1e-4, (i, a, b)
