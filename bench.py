@@ -118,6 +118,9 @@ def _sync(device):
 def time_steps(runner, batches, steps, warmup, device, world):
     import torch
     from sparkmi.parallel import barrier
+    # the HIP-graph capture must happen inside the untimed warm-up: eager steps first, the
+    # capture on the last warm-up step (StepRunner captures on step warmup_eager + 1)
+    runner.warmup_eager = max(0, min(runner.warmup_eager, warmup - 1))
     n = len(batches)
     loss = None
     for i in range(warmup):

@@ -58,6 +58,28 @@ __device__ __forceinline__ void f32_gload(const float* __restrict__ base, long l
   }
 }
 
+// Branch-free global -> register staging through a buffer descriptor: out-of-range rows / k read
+// 0 because their offset is pushed past the descriptor's extent (the range check returns zeros),
+// so a k-loop body stays ONE basic block and sched_group_barrier can interleave it.
+#define F32_OOB 0x7FFFFFF0
+template <bool KMAJ, int R>
+__device__ __forceinline__ void f32_bload(__amdgpu_buffer_rsrc_t rs, long ld, int r0, int rlim, int k0, int klim,
+                                          float4 (&v)[F32Tile<KMAJ, R>::NV], int tid) {
+#pragma unroll
+  for (int i = 0; i < F32Tile<KMAJ, R>::NV; ++i) {
+    const int f = tid + 256 * i;
+    int off;
+    if (!KMAJ) {
+      const int gr = r0 + (f >> 3), gk = k0 + (f & 7) * 4;
+      off = (gr < rlim && gk < klim) ? (int)(((long)gr * ld + gk) * 4) : F32_OOB;
+    } else {
+      const int gk = k0 + f / (R / 4), gc = r0 + (f % (R / 4)) * 4;
+      off = (gk < klim && gc < rlim) ? (int)(((long)gk * ld + gc) * 4) : F32_OOB;
+    }
+    v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+  }
+}
+
 template <bool KMAJ, int R>
 __device__ __forceinline__ void f32_lstore(float* __restrict__ lds, const float4 (&v)[F32Tile<KMAJ, R>::NV], int tid) {
 #pragma unroll
@@ -93,74 +115,13 @@ __device__ __forceinline__ int f32_tile_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
-// One output tile (all its k-tiles of split `split` and the epilogue).
-template <bool AK, bool BKM, int FM>
-__device__ __forceinline__ void gemm_f32_tile(const GemmF32Args& g, int tile, int split, float* smem) {
+// Fused epilogue of one output tile (acc = this wave's FM x 2 32x32 accumulators):
+// FWD + bias, activation, dropout; DGRAD + residual, relu'/dropout mask; WGRAD accumulate (+ the
+// bias-gradient row sums of A).  Each store instruction writes two full 128-B row segments.
+template <bool AK, int FM>
+__device__ __forceinline__ void f32_epilogue(const GemmF32Args& g, f32x16_t (&acc)[FM][2], float (&bsum)[FM], int m0,
+                                             int n0, int wm, int wn, int lane, bool do_bias) {
   constexpr int BMT = 64 * FM;
-  using TA = F32Tile<AK, BMT>;
-  using TB = F32Tile<BKM, FBN>;
-  constexpr int STAGE = TA::ELEMS + TB::ELEMS;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 1, wn = w & 1;
-  const int ntn = (g.N + FBN - 1) / FBN;
-  const int m0 = (tile / ntn) * BMT, n0 = (tile % ntn) * FBN;
-  const int kbeg = split * g.k_per_split;
-  const int kend = min(g.K, kbeg + g.k_per_split);
-  const int nk = (kend - kbeg + FBK - 1) / FBK;
-
-  f32x16_t acc[FM][2];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  const bool do_bias = AK && g.bias_grad && n0 == 0 && wn == 0;
-  float bsum[FM];
-#pragma unroll
-  for (int i = 0; i < FM; ++i) bsum[i] = 0.f;
-
-  float4 va[TA::NV], vb[TB::NV];
-  f32_gload<AK, BMT>(g.A, g.lda, m0, g.M, kbeg, kend, va, tid);
-  f32_gload<BKM, FBN>(g.B, g.ldb, n0, g.N, kbeg, kend, vb, tid);
-  f32_lstore<AK, BMT>(smem, va, tid);
-  f32_lstore<BKM, FBN>(smem + TA::ELEMS, vb, tid);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const bool more = kt + 1 < nk;
-    if (more) {  // next k-tile's loads fly under this k-tile's MFMAs
-      f32_gload<AK, BMT>(g.A, g.lda, m0, g.M, kbeg + (kt + 1) * FBK, kend, va, tid);
-      f32_gload<BKM, FBN>(g.B, g.ldb, n0, g.N, kbeg + (kt + 1) * FBK, kend, vb, tid);
-    }
-    const float* ta = smem + (kt & 1) * STAGE;
-    const float* tb = ta + TA::ELEMS;
-    float af[FM][16], bf[2][16];
-#pragma unroll
-    for (int i = 0; i < FM; ++i) f32_frag<AK, BMT>(ta, wm * BMT / 2 + i * 32, lane, af[i]);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) f32_frag<BKM, FBN>(tb, wn * 64 + j * 32, lane, bf[j]);
-#pragma unroll
-    for (int s = 0; s < 16; ++s)
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
-    if (do_bias) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int s = 0; s < 16; ++s) bsum[i] += af[i][s];
-    }
-    if (more) {
-      float* nx = smem + ((kt + 1) & 1) * STAGE;
-      f32_lstore<AK, BMT>(nx, va, tid);
-      f32_lstore<BKM, FBN>(nx + TA::ELEMS, vb, tid);
-    }
-    __syncthreads();
-  }
-
-  // ---------------- epilogue ----------------
   const uint32_t seed = g.thresh ? smi_seed(g.seedp, g.salt) : 0u;
   const int h = lane >> 5;
 #pragma unroll
@@ -205,14 +166,254 @@ __device__ __forceinline__ void gemm_f32_tile(const GemmF32Args& g, int tile, in
   }
 }
 
-template <bool AK, bool BKM, int FM>
+// One output tile (all its k-tiles of split `split` and the epilogue).
+template <bool AK, bool BKM, int FM, int PF>
+__device__ __forceinline__ void gemm_f32_tile(const GemmF32Args& g, int tile, int split, float* smem) {
+  constexpr int BMT = 64 * FM;
+  using TA = F32Tile<AK, BMT>;
+  using TB = F32Tile<BKM, FBN>;
+  constexpr int STAGE = TA::ELEMS + TB::ELEMS;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int ntn = (g.N + FBN - 1) / FBN;
+  const int m0 = (tile / ntn) * BMT, n0 = (tile % ntn) * FBN;
+  const int kbeg = split * g.k_per_split;
+  const int kend = min(g.K, kbeg + g.k_per_split);
+  const int nk = (kend - kbeg + FBK - 1) / FBK;
+
+  f32x16_t acc[FM][2];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const bool do_bias = AK && g.bias_grad && n0 == 0 && wn == 0;
+  float bsum[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) bsum[i] = 0.f;
+
+  // one k-tile of MFMAs on LDS stage `st` (and the fused bias-gradient row sums)
+  auto compute = [&](int st) {
+    const float* ta = smem + st * STAGE;
+    const float* tb = ta + TA::ELEMS;
+    float af[FM][16], bf[2][16];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) f32_frag<AK, BMT>(ta, wm * BMT / 2 + i * 32, lane, af[i]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) f32_frag<BKM, FBN>(tb, wn * 64 + j * 32, lane, bf[j]);
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+    if (do_bias) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int s = 0; s < 16; ++s) bsum[i] += af[i][s];
+    }
+  };
+  float4 va[TA::NV], vb[TB::NV];
+  f32_gload<AK, BMT>(g.A, g.lda, m0, g.M, kbeg, kend, va, tid);
+  f32_gload<BKM, FBN>(g.B, g.ldb, n0, g.N, kbeg, kend, vb, tid);
+  if constexpr (PF == 1) {
+    f32_lstore<AK, BMT>(smem, va, tid);
+    f32_lstore<BKM, FBN>(smem + TA::ELEMS, vb, tid);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more = kt + 1 < nk;
+      if (more) {  // next k-tile's loads fly under this k-tile's MFMAs
+        f32_gload<AK, BMT>(g.A, g.lda, m0, g.M, kbeg + (kt + 1) * FBK, kend, va, tid);
+        f32_gload<BKM, FBN>(g.B, g.ldb, n0, g.N, kbeg + (kt + 1) * FBK, kend, vb, tid);
+      }
+      compute(kt & 1);
+      if (more) {
+        float* nx = smem + ((kt + 1) & 1) * STAGE;
+        f32_lstore<AK, BMT>(nx, va, tid);
+        f32_lstore<BKM, FBN>(nx + TA::ELEMS, vb, tid);
+      }
+      __syncthreads();
+    }
+  } else {
+    // prefetch distance 2: two register sets (unrolled by 2), a k-tile's loads are issued two
+    // k-tiles of MFMAs before they are stored to LDS — HBM / MALL latency under load exceeds one
+    // k-tile of MFMAs at 64-row tiles (~2k cycles per wave)
+    float4 va1[TA::NV], vb1[TB::NV];
+    if (nk > 1) {
+      f32_gload<AK, BMT>(g.A, g.lda, m0, g.M, kbeg + FBK, kend, va1, tid);
+      f32_gload<BKM, FBN>(g.B, g.ldb, n0, g.N, kbeg + FBK, kend, vb1, tid);
+    }
+    f32_lstore<AK, BMT>(smem, va, tid);
+    f32_lstore<BKM, FBN>(smem + TA::ELEMS, vb, tid);
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt += 2) {
+      if (kt + 2 < nk) {
+        f32_gload<AK, BMT>(g.A, g.lda, m0, g.M, kbeg + (kt + 2) * FBK, kend, va, tid);
+        f32_gload<BKM, FBN>(g.B, g.ldb, n0, g.N, kbeg + (kt + 2) * FBK, kend, vb, tid);
+      }
+      compute(0);
+      if (kt + 1 < nk) {
+        f32_lstore<AK, BMT>(smem + STAGE, va1, tid);
+        f32_lstore<BKM, FBN>(smem + STAGE + TA::ELEMS, vb1, tid);
+      }
+      __syncthreads();
+      if (kt + 1 >= nk) break;
+      if (kt + 3 < nk) {
+        f32_gload<AK, BMT>(g.A, g.lda, m0, g.M, kbeg + (kt + 3) * FBK, kend, va1, tid);
+        f32_gload<BKM, FBN>(g.B, g.ldb, n0, g.N, kbeg + (kt + 3) * FBK, kend, vb1, tid);
+      }
+      compute(1);
+      if (kt + 2 < nk) {
+        f32_lstore<AK, BMT>(smem, va, tid);
+        f32_lstore<BKM, FBN>(smem + TA::ELEMS, vb, tid);
+      }
+      __syncthreads();
+    }
+  }
+
+  f32_epilogue<AK, FM>(g, acc, bsum, m0, n0, wm, wn, lane, do_bias);
+}
+
+
+// Software-pipelined form (one workgroup = one wave per SIMD, 128 x 128 tile, 3-stage LDS ring):
+// measured on the two-workgroups-per-CU form, the matrix pipe idled ~37 % of the time — the two
+// waves of a SIMD drift into lock-step (both in their load / barrier phase at once).  Here one
+// wave per SIMD keeps the pipe busy by itself: every k-tile's 64 MFMAs are issued back to back
+// while, in their shadow (an f32 32x32x2 MFMA occupies the pipe 64 cycles), the wave
+//   * issues the global loads of k-tile t+3 (register set R[t&1]),
+//   * reads k-tile t+1's fragments from LDS stage (t+1)%3 into the idle fragment set,
+//   * writes k-tile t+2 (loaded one iteration earlier) into LDS stage (t+2)%3,
+// interleaved one-per-MFMA by sched_group_barrier; one barrier per k-tile.
+#define SGB(mask, n) __builtin_amdgcn_sched_group_barrier((mask), (n), 0)
+#define SG_MFMA 0x008
+#define SG_VMEM_RD 0x020
+#define SG_DS_RD 0x100
+#define SG_DS_WR 0x200
+template <bool AK, bool BKM>
+__device__ __forceinline__ void gemm_f32_tile_pipe(const GemmF32Args& g, int tile, int split, float* smem) {
+  constexpr int FM = 2, BMT = 128;
+  using TA = F32Tile<AK, BMT>;
+  using TB = F32Tile<BKM, FBN>;
+  constexpr int STAGE = TA::ELEMS + TB::ELEMS;
+  constexpr int NRD = (AK ? 32 : 8) + (BKM ? 32 : 8);  // LDS fragment reads per k-tile per wave
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int ntn = (g.N + FBN - 1) / FBN;
+  const int m0 = (tile / ntn) * BMT, n0 = (tile % ntn) * FBN;
+  const int kbeg = split * g.k_per_split;
+  const int kend = min(g.K, kbeg + g.k_per_split);
+  const int nk = (kend - kbeg + FBK - 1) / FBK;
+  f32x16_t acc[FM][2];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const bool do_bias = AK && g.bias_grad && n0 == 0 && wn == 0;
+  float bsum[FM] = {0.f, 0.f};
+  float af0[FM][16], bf0[2][16], af1[FM][16], bf1[2][16];
+  float4 ra0[TA::NV], rb0[TB::NV], ra1[TA::NV], rb1[TB::NV];
+  const long a_bytes = 4 * (AK ? (long)(g.K - 1) * g.lda + g.M : (long)(g.M - 1) * g.lda + g.K);
+  const long b_bytes = 4 * (BKM ? (long)(g.K - 1) * g.ldb + g.N : (long)(g.N - 1) * g.ldb + g.K);
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, 0, (int)a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, 0, (int)b_bytes, 0x00020000);
+  // every step is unconditional (tiles past nk load zeros into stages nobody reads): no branches
+  auto ld = [&](int t, float4 (&ra)[TA::NV], float4 (&rb)[TB::NV]) {
+    f32_bload<AK, BMT>(rA, g.lda, m0, g.M, kbeg + t * FBK, kend, ra, tid);
+    f32_bload<BKM, FBN>(rB, g.ldb, n0, g.N, kbeg + t * FBK, kend, rb, tid);
+  };
+  auto st = [&](int t, const float4 (&ra)[TA::NV], const float4 (&rb)[TB::NV]) {
+    float* d = smem + (t % 3) * STAGE;
+    f32_lstore<AK, BMT>(d, ra, tid);
+    f32_lstore<BKM, FBN>(d + TA::ELEMS, rb, tid);
+  };
+  auto rd = [&](int t, float (&af)[FM][16], float (&bf)[2][16]) {
+    const float* ta = smem + (t % 3) * STAGE;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) f32_frag<AK, BMT>(ta, wm * BMT / 2 + i * 32, lane, af[i]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) f32_frag<BKM, FBN>(ta + TA::ELEMS, wn * 64 + j * 32, lane, bf[j]);
+  };
+  auto mma = [&](float (&af)[FM][16], float (&bf)[2][16]) {
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s2], bf[j][s2], acc[i][j], 0, 0, 0);
+    if constexpr (AK) {  // bias-gradient row sums (kept only by the column-block-0 waves)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) bsum[i] += af[i][s2];
+    }
+  };
+  // the interleave of one iteration: 8 x (MFMA, global load), reads, 8 x (MFMA, LDS write), rest
+  auto schedule = [&]() {
+#pragma unroll
+    for (int i = 0; i < TA::NV + TB::NV; ++i) { SGB(SG_MFMA, 1); SGB(SG_VMEM_RD, 1); }
+    if constexpr (NRD <= 40) {
+#pragma unroll
+      for (int i = 0; i < NRD; ++i) { SGB(SG_MFMA, 1); SGB(SG_DS_RD, 1); }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NRD / 2; ++i) { SGB(SG_MFMA, 1); SGB(SG_DS_RD, 2); }
+    }
+#pragma unroll
+    for (int i = 0; i < TA::NV + TB::NV; ++i) { SGB(SG_MFMA, 1); SGB(SG_DS_WR, 1); }
+    SGB(SG_MFMA, 64);
+  };
+  // prologue: k-tiles 0, 1 in LDS; k-tile 2 in R1; k-tile 0's fragments in F0
+  ld(0, ra0, rb0);
+  ld(1, ra1, rb1);
+  st(0, ra0, rb0);
+  st(1, ra1, rb1);
+  ld(2, ra1, rb1);
+  __syncthreads();
+  rd(0, af0, bf0);
+  // k-tiles in pairs with NO exit between the halves (an odd nk runs one extra all-zero k-tile:
+  // tiles past nk load zeros): a mid-pair exit made the compiler keep the accumulators in two
+  // register sets and copy 64 AGPRs per k-tile
+  const int nk2 = (nk + 1) & ~1;
+  for (int kt = 0; kt < nk2; kt += 2) {
+    ld(kt + 3, ra0, rb0);
+    rd(kt + 1, af1, bf1);
+    st(kt + 2, ra1, rb1);
+    mma(af0, bf0);
+    schedule();
+    __syncthreads();
+    ld(kt + 4, ra1, rb1);
+    rd(kt + 2, af0, bf0);
+    st(kt + 3, ra0, rb0);
+    mma(af1, bf1);
+    schedule();
+    __syncthreads();
+  }
+  f32_epilogue<AK, FM>(g, acc, bsum, m0, n0, wm, wn, lane, do_bias);
+}
+
+template <bool AK, bool BKM>
+__global__ __launch_bounds__(256, 1) void gemm_f32_pipe_kernel(GemmF32Args g) {
+  __shared__ __attribute__((aligned(16))) float smem[3 * (F32Tile<AK, 128>::ELEMS + F32Tile<BKM, FBN>::ELEMS)];
+  const int nwg = ((g.M + 127) / 128) * ((g.N + FBN - 1) / FBN);
+  const int split = blockIdx.x / nwg;
+  const int tile = f32_tile_remap(blockIdx.x - split * nwg, nwg);
+  gemm_f32_tile_pipe<AK, BKM>(g, tile, split, smem);
+}
+
+template <bool AK, bool BKM, int FM, int PF>
 __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmF32Args g) {
   constexpr int BMT = 64 * FM;
   __shared__ __attribute__((aligned(16))) float smem[2 * (F32Tile<AK, BMT>::ELEMS + F32Tile<BKM, FBN>::ELEMS)];
   const int nwg = ((g.M + BMT - 1) / BMT) * ((g.N + FBN - 1) / FBN);
   const int split = blockIdx.x / nwg;
   const int tile = f32_tile_remap(blockIdx.x - split * nwg, nwg);
-  gemm_f32_tile<AK, BKM, FM>(g, tile, split, smem);
+  gemm_f32_tile<AK, BKM, FM, PF>(g, tile, split, smem);
 }
 
 static int f32_ok(const GemmF32Args& g) {
@@ -246,15 +447,32 @@ extern "C" int smi_gemm_f32(const GemmF32Args* args, hipStream_t st) {
   g.k_per_split = kps;
   g.splits = (g.K + kps - 1) / kps;
   const dim3 grid((unsigned)(nwg * g.splits)), block(256);
-  if (g.mode == 0) {
-    if (bm == 64) hipLaunchKernelGGL((gemm_f32_kernel<false, false, 1>), grid, block, 0, st, g);
-    else hipLaunchKernelGGL((gemm_f32_kernel<false, false, 2>), grid, block, 0, st, g);
-  } else if (g.mode == 1) {
-    if (bm == 64) hipLaunchKernelGGL((gemm_f32_kernel<false, true, 1>), grid, block, 0, st, g);
-    else hipLaunchKernelGGL((gemm_f32_kernel<false, true, 2>), grid, block, 0, st, g);
-  } else {
-    hipLaunchKernelGGL((gemm_f32_kernel<true, true, 2>), grid, block, 0, st, g);
+  static int pf_env = -1;
+  if (pf_env < 0) {
+    // 0 = software-pipelined one-wave-per-SIMD kernel (default), 1 / 2 = two-workgroups-per-CU
+    // kernel with prefetch distance 1 / 2
+    const char* e = getenv("SMI_GEMM_F32_PF");
+    pf_env = e ? atoi(e) : 0;
   }
+  if (pf_env == 0) {
+    const int nwg128 = ((g.M + 127) / 128) * ((g.N + FBN - 1) / FBN);
+    const dim3 grid2((unsigned)(nwg128 * g.splits));
+    if (g.mode == 0) hipLaunchKernelGGL((gemm_f32_pipe_kernel<false, false>), grid2, block, 0, st, g);
+    else if (g.mode == 1) hipLaunchKernelGGL((gemm_f32_pipe_kernel<false, true>), grid2, block, 0, st, g);
+    else hipLaunchKernelGGL((gemm_f32_pipe_kernel<true, true>), grid2, block, 0, st, g);
+    SMI_CHECK_LAUNCH();
+  }
+#define F32K(AKV, BKV, FMV)                                                                          \
+  if (pf_env == 1) hipLaunchKernelGGL((gemm_f32_kernel<AKV, BKV, FMV, 1>), grid, block, 0, st, g); \
+  else hipLaunchKernelGGL((gemm_f32_kernel<AKV, BKV, FMV, 2>), grid, block, 0, st, g)
+  if (g.mode == 0) {
+    if (bm == 64) { F32K(false, false, 1); } else { F32K(false, false, 2); }
+  } else if (g.mode == 1) {
+    if (bm == 64) { F32K(false, true, 1); } else { F32K(false, true, 2); }
+  } else {
+    F32K(true, true, 2);
+  }
+#undef F32K
   SMI_CHECK_LAUNCH();
 }
 
@@ -264,14 +482,17 @@ extern "C" int smi_gemm_f32(const GemmF32Args* args, hipStream_t st) {
 // tiles start at t0[e], a multiple of 8 (same XCD pattern as a standalone launch).  Queued by
 // sparkmi/ops/_grad.py during the backward and flushed per gradient bucket / at its end.
 #define WGF_MAX 40
+#ifndef WGF_PF
+#define WGF_PF 1
+#endif
 struct WgradGroupF32 {
   const float* A[WGF_MAX]; const float* B[WGF_MAX];
   float* C[WGF_MAX]; float* bias[WGF_MAX];
   int lda[WGF_MAX], ldb[WGF_MAX], n[WGF_MAX], k[WGF_MAX], T[WGF_MAX];
   int t0[WGF_MAX + 1]; int count;
 };
-__global__ __launch_bounds__(256, 2) void gemm_f32_wgrad_group_kernel(WgradGroupF32 gr) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * (F32Tile<true, 128>::ELEMS + F32Tile<true, FBN>::ELEMS)];
+__global__ __launch_bounds__(256, 1) void gemm_f32_wgrad_group_kernel(WgradGroupF32 gr) {
+  __shared__ __attribute__((aligned(16))) float smem[3 * (F32Tile<true, 128>::ELEMS + F32Tile<true, FBN>::ELEMS)];
   const int t = blockIdx.x;
   int e = 0;
   while (e + 1 < gr.count && t >= gr.t0[e + 1]) ++e;  // uniform scan over <= WGF_MAX entries
@@ -282,7 +503,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_wgrad_group_kernel(WgradGroup
   g.bias_grad = gr.bias[e];
   const int nwg = ((g.M + 127) / 128) * ((g.N + FBN - 1) / FBN);
   const int lt = t - gr.t0[e];
-  if (lt < nwg) gemm_f32_tile<true, true, 2>(g, f32_tile_remap(lt, nwg), 0, smem);  // lt >= nwg: padding
+  if (lt < nwg) gemm_f32_tile_pipe<true, true>(g, f32_tile_remap(lt, nwg), 0, smem);  // lt >= nwg: padding
 }
 
 extern "C" int smi_gemm_f32_wgrad_group(const void* const* A, const long* lda, const void* const* B, const long* ldb,

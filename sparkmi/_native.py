@@ -1,7 +1,8 @@
 """Loader for sparkmi's in-tree native extensions.
 
 ``sparkmi._C`` holds the HIP/CDNA4 kernels (built for gfx950 by ``tools/build_native.py``);
-``sparkmi._runtime`` holds the host C++ runtime (libsvm parser, tokenizer, vocab encoder).
+``sparkmi._runtime`` holds the host C++ runtime (libsvm parser, tokenizer, vocab encoder);
+``sparkmi._comm`` the native communication layer (RCCL communicator, xGMI IPC all-reduce).
 
 torch is imported first on purpose: torch ships its own ``libamdhip64.so.7`` and ``_C``
 declares the same SONAME, so the dynamic linker binds ``_C`` to torch's already-loaded HIP
@@ -79,6 +80,30 @@ def RT():
     if _RT is None:
         raise ImportError(f"sparkmi._runtime unavailable: {_RT_err}; run python tools/build_native.py")
     return _RT
+
+
+_COMM = None
+_COMM_err = None
+
+
+def comm():
+    """The native communication module (RCCL communicator + IPC one-shot all-reduce)."""
+    global _COMM, _COMM_err
+    if _COMM is not None:
+        return _COMM
+    with _lock:
+        if _COMM is None and _COMM_err is None:
+            try:
+                _COMM = _load("_comm")
+            except ImportError:
+                _try_build()
+                try:
+                    _COMM = _load("_comm")
+                except ImportError as e:  # pragma: no cover
+                    _COMM_err = e
+    if _COMM is None:
+        raise ImportError(f"sparkmi._comm unavailable: {_COMM_err}; run python tools/build_native.py")
+    return _COMM
 
 
 def has_native():

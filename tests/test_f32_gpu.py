@@ -252,13 +252,13 @@ def test_embedding_f32():
 
 
 def _pair(L=2, S=32, V=96, seed=0):
+    """The same model twice (deepcopy keeps the dropout salts, so both draw identical masks)."""
+    import copy
     from sparkmi.models.transformer import Transformer
     torch.manual_seed(seed)
     mc = Transformer(d_model=128, ffn_hidden=256, num_heads=2, num_layers=L, max_sequence_length=S,
                      src_vocab_size=V, tgt_vocab_size=V, seed=5, dtype="fp32")
-    torch.manual_seed(seed)
-    mg = Transformer(d_model=128, ffn_hidden=256, num_heads=2, num_layers=L, max_sequence_length=S,
-                     src_vocab_size=V, tgt_vocab_size=V, seed=5, dtype="fp32").to(dev)
+    mg = copy.deepcopy(mc).to(dev)
     return mc, mg
 
 

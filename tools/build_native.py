@@ -5,6 +5,8 @@
                               pybind11 launch bindings (csrc/kernels/*.hip, csrc/bindings.cpp).
 * ``sparkmi/_runtime*.so``  — host C++ runtime: libsvm parser, basic_english tokenizer and
                               vocab encoder, batch padding, shuffling (csrc/runtime/*.cpp), g++.
+* ``sparkmi/_comm*.so``     — native communication layer: RCCL communicator + xGMI IPC one-shot
+                              all-reduce (csrc/comm/*.hip, *.cpp), hipcc, linked against librccl.
 
 Incremental: an object is rebuilt when its source or any header under csrc/include changes.
 Usage: python tools/build_native.py [--force] [--jobs N] [--asan-runtime]
@@ -95,6 +97,20 @@ def build(force=False, jobs=8, verbose=True):
         if _needs(s, o, hdr_t, force):
             jobs_list.append(["g++", "-O3", "-std=c++17", "-fPIC", "-c", s, "-o", o, "-fvisibility=hidden",
                               "-pthread"] + inc + py_inc)
+    comm_dir = os.path.join(CSRC, "comm")
+    comm_objs = []
+    for f in sorted(os.listdir(comm_dir)):
+        s = os.path.join(comm_dir, f)
+        o = os.path.join(OBJ, "comm_" + f + ".o")
+        if f.endswith(".hip"):
+            comm_objs.append(o)
+            if _needs(s, o, hdr_t, force):
+                jobs_list.append([HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-c", s, "-o", o] + inc)
+        elif f.endswith(".cpp"):
+            comm_objs.append(o)
+            if _needs(s, o, hdr_t, force):
+                jobs_list.append([HIPCC, "-O2", "-std=c++17", "-fPIC", "-c", s, "-o", o, "-fvisibility=hidden",
+                                  "-I/opt/rocm/include"] + inc + py_inc)
     if jobs_list:
         with ThreadPoolExecutor(max_workers=jobs) as ex:
             for cmd, _ in zip(jobs_list, ex.map(_run, jobs_list)):
@@ -106,6 +122,13 @@ def build(force=False, jobs=8, verbose=True):
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", c_so] + objs)
         if verbose:
             print("[link]", os.path.relpath(c_so, ROOT), flush=True)
+    comm_so = os.path.join(PKG, "_comm" + suffix)
+    if comm_objs and (force or not os.path.exists(comm_so) or
+                      any(os.path.getmtime(o) > os.path.getmtime(comm_so) for o in comm_objs)):
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", comm_so] + comm_objs +
+             ["-L/opt/rocm/lib", "-lrccl"])
+        if verbose:
+            print("[link]", os.path.relpath(comm_so, ROOT), flush=True)
     rt_so = os.path.join(PKG, "_runtime" + suffix)
     if rt_objs and (force or not os.path.exists(rt_so) or
                     any(os.path.getmtime(o) > os.path.getmtime(rt_so) for o in rt_objs)):
