@@ -79,6 +79,8 @@ int smi_adam(float*, float*, float*, float*, void*, long, const float*, float*, 
              int, int, hipStream_t);
 int smi_sgd(float*, float*, float*, void*, long, const float*, float*, unsigned*, float, float, float, int, float, int,
             hipStream_t);
+int smi_adam_multi(float* const*, float* const*, float* const*, float* const*, void* const*, const long*, int, const float*,
+                   float*, unsigned*, float, float, float, float, float, int, int, hipStream_t);
 int smi_multi_copy(void* const*, const void* const*, const long*, int, hipStream_t);
 }
 
@@ -233,6 +235,20 @@ PYBIND11_MODULE(_C, m) {
                    float gscale, int adamw, int zero_grad, u st) {
     chk(smi_adam(PF(p), PF(g), PF(mm), PF(v), P(pbf), n, PF(lr), PF(step), reinterpret_cast<unsigned*>(done), b1, b2,
                  eps, wd, gscale, adamw, zero_grad, S(st)), "adam");
+  });
+  // Adam over several disjoint ranges, one launch, one step advance (ZeRO-1 shard update)
+  m.def("adam_multi", [](std::vector<u> p, std::vector<u> g, std::vector<u> mm, std::vector<u> v, std::vector<u> pbf,
+                         std::vector<long> n, u lr, u step, u done, float b1, float b2, float eps, float wd, float gscale,
+                         int adamw, int zero_grad, u st) {
+    const size_t c = p.size();
+    if (g.size() != c || mm.size() != c || v.size() != c || pbf.size() != c || n.size() != c)
+      throw std::runtime_error("adam_multi: list sizes differ");
+    std::vector<float*> a(c), b(c), d(c), e(c);
+    std::vector<void*> f(c);
+    for (size_t i = 0; i < c; ++i) { a[i] = PF(p[i]); b[i] = PF(g[i]); d[i] = PF(mm[i]); e[i] = PF(v[i]); f[i] = P(pbf[i]); }
+    chk(smi_adam_multi(a.data(), b.data(), d.data(), e.data(), f.data(), n.data(), (int)c, PF(lr), PF(step),
+                       reinterpret_cast<unsigned*>(done), b1, b2, eps, wd, gscale, adamw, zero_grad, S(st)),
+        "adam_multi");
   });
   m.def("sgd", [](u p, u g, u buf, u pbf, long n, u lr, u step, u done, float mom, float damp, float wd, int nesterov,
                   float gscale, int zero_grad, u st) {

@@ -31,7 +31,8 @@ struct IpcArgs {
   unsigned* sig[IPC_MAX_RANKS];
   long cap;
   int rank, world;
-  unsigned epoch;
+  unsigned* ep;
+  unsigned* done;
   int* err;
 };
 extern "C" int smi_ipc_allreduce(const IpcArgs* args, int blocks, hipStream_t st);
@@ -161,12 +162,14 @@ PYBIND11_MODULE(_comm, m) {
   });
   m.def("ipc_close", [](u p) { hchk(hipIpcCloseMemHandle((void*)p), "hipIpcCloseMemHandle"); });
   m.def("ipc_free", [](u p) { hchk(hipFree((void*)p), "hipFree"); });
-  m.def("ipc_allreduce", [](u buf, long n, std::vector<u> data, std::vector<u> sig, long cap, int rank, unsigned epoch,
+  // ctr: device uint32[2] = {epoch, ticket}, zero-initialised
+  m.def("ipc_allreduce", [](u buf, long n, std::vector<u> data, std::vector<u> sig, long cap, int rank, u ctr,
                             u err, int blocks, u st) {
     if (data.size() != sig.size() || data.empty() || data.size() > IPC_MAX_RANKS)
       throw std::runtime_error("sparkmi._comm.ipc_allreduce: bad peer lists");
     IpcArgs a{};
-    a.buf = (float*)buf; a.n = n; a.cap = cap; a.rank = rank; a.world = (int)data.size(); a.epoch = epoch;
+    a.buf = (float*)buf; a.n = n; a.cap = cap; a.rank = rank; a.world = (int)data.size();
+    a.ep = (unsigned*)ctr; a.done = (unsigned*)ctr + 1;
     a.err = (int*)err;
     for (size_t i = 0; i < data.size(); ++i) { a.data[i] = (float*)data[i]; a.sig[i] = (unsigned*)sig[i]; }
     const int rc = smi_ipc_allreduce(&a, blocks, (hipStream_t)st);

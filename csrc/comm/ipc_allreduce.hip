@@ -4,7 +4,10 @@
 // ring protocol's per-hop latency; here every rank reads every peer's bucket directly over xGMI
 // (7 point-to-point links: all peers at once, one hop) and reduces locally.
 //
-// Protocol (one launch per all-reduce, stream-ordered on every rank; `epoch` increments per call):
+// Protocol (one launch per all-reduce, stream-ordered on every rank).  The epoch lives in device
+// memory (*ep, advanced by the launch's last block, like the optimizers' step counter), so the
+// launch can be captured in a HIP graph and replayed — a small model's whole data-parallel step
+// (forward, backward, this all-reduce, optimizer) is then ONE graph replay.
 //  1. block b copies its chunk of the local bucket into this rank's staging region, half
 //     (epoch & 1) — double-buffered so a fast rank's next call never overwrites data a slow
 //     peer is still reading (a rank can only reach epoch+2 after every peer signalled epoch+1,
@@ -31,7 +34,8 @@ struct IpcArgs {
   unsigned* sig[IPC_MAX_RANKS];        // every rank's signal region: [IPC_MAX_BLOCKS][IPC_MAX_RANKS]
   long cap;                            // floats per staging half
   int rank, world;
-  unsigned epoch;
+  unsigned* ep;                        // device epoch counter (read at entry, advanced at exit)
+  unsigned* done;                      // zeroed ticket word of the exit advance
   int* err;                            // set to 1 on a poll timeout
 };
 
@@ -40,7 +44,8 @@ __global__ __launch_bounds__(256) void ipc_allreduce_kernel(IpcArgs a) {
   const long n4 = a.n / 4;
   const long per = (n4 + nb - 1) / nb;
   const long lo = (long)b * per, hi = lo + per < n4 ? lo + per : n4;
-  const long half = (long)(a.epoch & 1u) * a.cap;
+  const unsigned epoch = a.ep[0] + 1u;
+  const long half = (long)(epoch & 1u) * a.cap;
   float4* mine = (float4*)(a.data[a.rank] + half);
   const float4* src = (const float4*)a.buf;
   for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = src[i];
@@ -48,11 +53,11 @@ __global__ __launch_bounds__(256) void ipc_allreduce_kernel(IpcArgs a) {
   __syncthreads();
   if ((int)threadIdx.x < a.world) {
     __atomic_thread_fence(__ATOMIC_RELEASE);  // system scope: the staging stores are visible first
-    __hip_atomic_store(a.sig[threadIdx.x] + b * IPC_MAX_RANKS + a.rank, a.epoch, __ATOMIC_RELEASE,
+    __hip_atomic_store(a.sig[threadIdx.x] + b * IPC_MAX_RANKS + a.rank, epoch, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
     const unsigned* f = a.sig[a.rank] + b * IPC_MAX_RANKS + threadIdx.x;
     long spins = 0;
-    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - a.epoch) < 0) {
+    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
       if (++spins > (1L << 24)) {  // ~4 s of s_sleep back-off: a peer is gone
         __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
@@ -70,6 +75,12 @@ __global__ __launch_bounds__(256) void ipc_allreduce_kernel(IpcArgs a) {
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
     out[i] = acc;
+  }
+  // advance the epoch: every block read ep[0] on entry; the last block to finish stores it
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(a.done, 1u) == gridDim.x - 1) {
+    a.ep[0] = epoch;
+    a.done[0] = 0u;
   }
 }
 

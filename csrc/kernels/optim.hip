@@ -77,6 +77,56 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
   finish_step(step_p, done, t);
 }
 
+// Adam over several disjoint ranges in ONE launch with ONE step advance: the ZeRO-1 update of
+// a data-parallel rank, which owns one piece of every gradient bucket (sparkmi/parallel/ddp.py)
+// and keeps the moments of its pieces only (compact m / v).  Range e owns blocks
+// [blk0[e], blk0[e+1]); float4 body (every piece is a multiple of 4 floats, 16-B aligned).
+#define ADAM_MULTI_MAX 64
+struct AdamMulti {
+  float* p[ADAM_MULTI_MAX]; float* g[ADAM_MULTI_MAX]; float* m[ADAM_MULTI_MAX]; float* v[ADAM_MULTI_MAX];
+  unsigned short* pbf[ADAM_MULTI_MAX]; long n[ADAM_MULTI_MAX]; int blk0[ADAM_MULTI_MAX + 1]; int count;
+};
+__global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a, const float* __restrict__ lr_p,
+                                                         float* __restrict__ step_p, unsigned* __restrict__ done, float b1,
+                                                         float b2, float eps, float wd, float gscale, int adamw,
+                                                         int zero_grad) {
+  const float t = step_p[0] + 1.f;
+  const float lr = lr_p[0];
+  const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
+  const float step_size = lr / bc1;
+  const float rbc2 = 1.f / sqrtf(bc2);
+  int e = 0;
+  while (e + 1 < a.count && (int)blockIdx.x >= a.blk0[e + 1]) ++e;  // wave-uniform scan
+  const long lb = blockIdx.x - a.blk0[e], nb = a.blk0[e + 1] - a.blk0[e];
+  float* p = a.p[e]; float* g = a.g[e]; float* m = a.m[e]; float* v = a.v[e]; unsigned short* pbf = a.pbf[e];
+  const long n4 = a.n[e] / 4;
+  for (long i = lb * blockDim.x + threadIdx.x; i < n4; i += nb * blockDim.x) {
+    float4 pp = ((float4*)p)[i], gg = ((float4*)g)[i], mm = ((float4*)m)[i], vv = ((float4*)v)[i];
+    float* pa = &pp.x; float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
+    unsigned short ob[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gr = ga[j] * gscale;
+      if (wd != 0.f) {
+        if (adamw) pa[j] *= (1.f - lr * wd);
+        else gr += wd * pa[j];
+      }
+      ma[j] = b1 * ma[j] + (1.f - b1) * gr;
+      va[j] = b2 * va[j] + (1.f - b2) * gr * gr;
+      const float denom = sqrtf(va[j]) * rbc2 + eps;
+      pa[j] -= step_size * ma[j] / denom;
+      ob[j] = f2bf(pa[j]);
+    }
+    ((float4*)p)[i] = pp; ((float4*)m)[i] = mm; ((float4*)v)[i] = vv;
+    if (zero_grad) ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (pbf) {
+      uint2 w; w.x = ob[0] | ((unsigned)ob[1] << 16); w.y = ob[2] | ((unsigned)ob[3] << 16);
+      ((uint2*)pbf)[i] = w;
+    }
+  }
+  finish_step(step_p, done, t);
+}
+
 // p -= lr * (g*gscale + wd*p) with optional (heavy-ball, torch-style) momentum buffer
 __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ buf,
                                                   unsigned short* __restrict__ pbf, long n, const float* __restrict__ lr_p,
@@ -117,6 +167,33 @@ extern "C" int smi_adam(float* p, float* g, float* m, float* v, void* pbf, long 
                         hipStream_t st) {
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, st, p, g, m, v, (unsigned short*)pbf, n, lr,
                      step, done, b1, b2, eps, wd, gscale, adamw, zero_grad);
+  SMI_CHECK_LAUNCH();
+}
+
+extern "C" int smi_adam_multi(float* const* p, float* const* g, float* const* m, float* const* v, void* const* pbf,
+                              const long* n, int count, const float* lr, float* step, unsigned* done, float b1, float b2,
+                              float eps, float wd, float gscale, int adamw, int zero_grad, hipStream_t st) {
+  if (count < 1 || count > ADAM_MULTI_MAX) return -1;
+  AdamMulti a{};
+  long total4 = 0;
+  for (int i = 0; i < count; ++i) {
+    if (n[i] % 4 || ((((uintptr_t)p[i]) | ((uintptr_t)g[i]) | ((uintptr_t)m[i]) | ((uintptr_t)v[i])) & 15)) return -1;
+    total4 += n[i] / 4;
+  }
+  int tot = 0;
+  for (int i = 0; i < count; ++i) {
+    a.p[i] = p[i]; a.g[i] = g[i]; a.m[i] = m[i]; a.v[i] = v[i]; a.pbf[i] = (unsigned short*)pbf[i]; a.n[i] = n[i];
+    // blocks proportional to the range's share of a <= 4096-block launch
+    long b = total4 ? (long)((double)(n[i] / 4) / (double)total4 * 4096.0) : 1;
+    if (b > (n[i] / 4 + 255) / 256) b = (n[i] / 4 + 255) / 256;
+    if (b < 1) b = 1;
+    a.blk0[i] = tot;
+    tot += (int)b;
+  }
+  a.blk0[count] = tot;
+  a.count = count;
+  hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)tot), dim3(256), 0, st, a, lr, step, done, b1, b2, eps, wd, gscale,
+                     adamw, zero_grad);
   SMI_CHECK_LAUNCH();
 }
 

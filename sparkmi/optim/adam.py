@@ -49,9 +49,57 @@ class Adam(_FlatOptimizer):
         self.weight_decay = weight_decay
         self.m = torch.zeros_like(flat.master)
         self.v = torch.zeros_like(flat.master)
+        self.ranges = None
+
+    def shard(self, ranges):
+        """ZeRO-1: update only the [start, end) ranges of the flat buffer (this data-parallel
+        rank's pieces, sparkmi/parallel/ddp.py); the moments are kept for those ranges only, in
+        one compact buffer, and the update is ONE multi-range launch with one step advance."""
+        self.ranges = [(int(s), int(e)) for s, e in ranges]
+        offs, o = [], 0
+        for s, e in self.ranges:
+            offs.append(o)
+            o += e - s
+        self._moff = offs
+        self.m = torch.zeros(o, dtype=torch.float32, device=self.flat.device)
+        self.v = torch.zeros(o, dtype=torch.float32, device=self.flat.device)
+        return self
+
+    def _step_shard(self):
+        f = self.flat
+        if _native.use_native(f.master):
+            C = _native.C()
+            mp, gp, sp = f.master.data_ptr(), f.grad.data_ptr(), _native.ptr(f.shadow)
+            C.adam_multi([mp + 4 * s for s, _ in self.ranges], [gp + 4 * s for s, _ in self.ranges],
+                         [self.m.data_ptr() + 4 * o for o in self._moff], [self.v.data_ptr() + 4 * o for o in self._moff],
+                         [sp + 2 * s if sp else 0 for s, _ in self.ranges], [e - s for s, e in self.ranges],
+                         self.lr_t.data_ptr(), self.step_t.data_ptr(), self.done_t.data_ptr(), self.b1, self.b2,
+                         self.eps, self.weight_decay, self.grad_scale, int(self.adamw), int(self.zero_grad_after_step),
+                         _native.stream())
+            return
+        with torch.no_grad():
+            self.step_t.add_(1)
+            t = float(self.step_t.item())
+            lr = float(self.lr_t.item())
+            bc1, bc2 = 1 - self.b1 ** t, 1 - self.b2 ** t
+            for (s, e), o in zip(self.ranges, self._moff):
+                p, g = f.master[s:e], f.grad[s:e] * self.grad_scale
+                m, v = self.m[o:o + e - s], self.v[o:o + e - s]
+                if self.weight_decay:
+                    if self.adamw:
+                        p.mul_(1 - lr * self.weight_decay)
+                    else:
+                        g = g + self.weight_decay * p
+                m.mul_(self.b1).add_(g, alpha=1 - self.b1)
+                v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+                p.addcdiv_(m, v.sqrt() / (bc2 ** 0.5) + self.eps, value=-lr / bc1)
+                if self.zero_grad_after_step:
+                    f.grad[s:e].zero_()
 
     def step(self):
         f = self.flat
+        if self.ranges is not None:
+            return self._step_shard()
         if _native.use_native(f.master):
             C = _native.C()
             st = _native.stream()

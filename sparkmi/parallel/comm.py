@@ -9,7 +9,8 @@ pointers on the current HIP stream, and ``abort()`` for the failure path.
 latency-bound buckets (< ~256 KB: the MLP's 256 B, the CNN's 31 KB gradients,
 distributed_multilayer_perceptron.py:103-106, distributed_cnn.py:152-156): every rank reads every
 peer's bucket directly over xGMI in one hop and sums in rank order (bit-identical results on
-every rank).  Handles are exchanged once through torch.distributed (any backend, gloo included),
+every rank).  The epoch counter lives on the device, so the call can sit inside a captured HIP
+graph (the small models' whole data-parallel step is one replay).  Handles are exchanged once through torch.distributed (any backend, gloo included),
 so two processes sharing one GPU can exercise it too.
 """
 import torch
@@ -102,15 +103,14 @@ class IpcAllReduce:
                 self.data.append(pd)
                 self.sig.append(ps)
         self.err = torch.zeros(1, dtype=torch.int32, device="cuda")
-        self.epoch = 0
+        self.ctr = torch.zeros(2, dtype=torch.int32, device="cuda")  # {epoch, ticket}: advanced by the kernel
         dist.barrier(group=group)
 
     def __call__(self, t):
         if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() % 4 or t.numel() > self.cap:
             raise ValueError("IpcAllReduce: contiguous fp32 tensor, numel % 4 == 0, <= capacity")
-        self.epoch += 1
         blocks = self.blocks or max(1, min(self.C.IPC_MAX_BLOCKS, (t.numel() // 4 + 1023) // 1024))
-        self.C.ipc_allreduce(t.data_ptr(), t.numel(), self.data, self.sig, self.cap, self.rank, self.epoch & 0xFFFFFFFF,
+        self.C.ipc_allreduce(t.data_ptr(), t.numel(), self.data, self.sig, self.cap, self.rank, self.ctr.data_ptr(),
                              self.err.data_ptr(), blocks, torch.cuda.current_stream().cuda_stream)
         return t
 

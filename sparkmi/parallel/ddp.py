@@ -14,13 +14,26 @@ module was called, so gradients were never synchronised).  Design for MI355X + R
 * buckets are large (default 64 MiB): an 8-GPU ring over xGMI is per-link bandwidth bound, and
   fewer, larger collectives amortise the per-call latency;
 * averaging is folded into the optimizer (``grad_scale = 1/world``) instead of a division
-  pass over the buffer.
+  pass over the buffer;
+* ``zero=True`` (ZeRO-1): each bucket is REDUCE-SCATTERED instead of all-reduced — rank r owns
+  piece r of every bucket — the optimizer updates only the owned pieces (compact moments,
+  one multi-range launch: sparkmi.optim.adam.Adam.shard) and the updated fp32 master pieces are
+  all-gathered in place; per-rank optimizer work and state drop by 1/world and the gradient
+  moves (w-1)/w instead of 2(w-1)/w of the buffer before the update;
+* ``ipc=True`` (default for small models on one node, <= 1 MiB of gradients): buckets are
+  summed by the one-shot xGMI IPC kernel (csrc/comm/ipc_allreduce.hip) — no ring latency, and
+  since it is a stream-ordered kernel with a device-side epoch, the whole data-parallel step
+  (forward, backward, all-reduce, optimizer) is captured as ONE HIP graph (``graph_safe``).
 The CPU/gloo path runs the identical logic (multi-process CPU tests).
 """
+import os
+
 import torch
 import torch.distributed as dist
 
 from ..ops import _grad
+
+IPC_LIMIT_BYTES = 1 << 20
 
 
 def broadcast_flat(flat, src=0, group=None):
@@ -30,13 +43,29 @@ def broadcast_flat(flat, src=0, group=None):
         flat.refresh_shadow()
 
 
+def _single_node(world):
+    lw = os.environ.get("LOCAL_WORLD_SIZE")
+    return lw is None or int(lw) == world
+
+
 class DataParallel:
-    def __init__(self, flat, group=None, bucket_mb=64.0, overlap=True, broadcast=True):
+    def __init__(self, flat, group=None, bucket_mb=64.0, overlap=True, broadcast=True, zero=False, ipc=None):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.overlap = overlap
         self._limit = int(bucket_mb * (1 << 20) / 4)
+        self.zero = bool(zero) and self.world > 1
+        if self.zero and 64 % self.world:
+            raise ValueError("zero=True needs a world size dividing 64 (buckets are 64-element aligned)")
+        self.ipc = None
+        if ipc is None:
+            ipc = os.environ.get("SPARKMI_IPC_AR", "1") != "0"
+        if (ipc and not self.zero and self.world > 1 and flat.grad.is_cuda and flat.numel * 4 <= IPC_LIMIT_BYTES
+                and self.world <= 8 and _single_node(self.world)):
+            from .comm import IpcAllReduce
+            self.ipc = IpcAllReduce(cap_floats=flat.numel, group=group)
         self._build_buckets()
         self._pending = None
         self._works = []
@@ -102,6 +131,21 @@ class DataParallel:
         self._works = []
         self.early_flushes = 0
 
+    @property
+    def graph_safe(self):
+        """True when the gradient reduction is a plain kernel (IPC path): the whole DP step can
+        be captured into one HIP graph."""
+        return self.ipc is not None
+
+    def piece(self, b):
+        """[start, end) of this rank's piece of bucket ``b`` (ZeRO-1 ownership)."""
+        s, e, _ = self.buckets[b]
+        n = (e - s) // self.world
+        return s + self.rank * n, s + (self.rank + 1) * n
+
+    def shard_ranges(self):
+        return [self.piece(b) for b in range(len(self.buckets))] if self.zero else [(0, self.flat.numel)]
+
     def _launch(self, b):
         if self._launched[b]:
             return
@@ -109,8 +153,49 @@ class DataParallel:
         self._launched[b] = True
         if self.flat.grad.is_cuda:
             _grad.join(self.flat.grad.device.index)  # weight grads may still be in flight on the side stream
-        w = dist.all_reduce(self.flat.grad[s:e], group=self.group, async_op=True)
+        g = self.flat.grad[s:e]
+        if self.ipc is not None:
+            self.ipc(g)  # stream-ordered kernel: nothing to wait for
+            return
+        if self.zero:
+            ps, pe = self.piece(b)
+            w = dist.reduce_scatter_tensor(self.flat.grad[ps:pe], g, group=self.group, async_op=True)
+        else:
+            w = dist.all_reduce(g, group=self.group, async_op=True)
         self._works.append(w)
+
+    def reshard_optimizer(self, opt, old_ranges):
+        """Carry a sharded optimizer's moments over a bucket re-cut (the split-graph capture aligns
+        buckets to backward pieces after the eager warm-up steps): every rank scatters its compact
+        moments into a full-size buffer, one all-reduce assembles them, each rank keeps its new
+        pieces."""
+        if not self.zero:
+            return
+        full = torch.zeros(2, self.flat.numel, dtype=torch.float32, device=self.flat.master.device)
+        o = 0
+        for s, e in old_ranges:
+            full[0, s:e] = opt.m[o:o + e - s]
+            full[1, s:e] = opt.v[o:o + e - s]
+            o += e - s
+        dist.all_reduce(full, group=self.group)
+        opt.shard(self.shard_ranges())
+        for (s, e), off in zip(opt.ranges, opt._moff):
+            opt.m[off:off + e - s] = full[0, s:e]
+            opt.v[off:off + e - s] = full[1, s:e]
+
+    def gather_params(self):
+        """ZeRO-1 epilogue of a step: all-gather every bucket's updated fp32 master pieces (in
+        place), refresh the bf16 shadow, and clear the gradient buffer (only the owned pieces
+        were consumed by the update)."""
+        if not self.zero:
+            return
+        m = self.flat.master
+        for b in range(len(self.buckets)):
+            s, e, _ = self.buckets[b]
+            ps, pe = self.piece(b)
+            dist.all_gather_into_tensor(m[s:e], m[ps:pe], group=self.group)
+        self.flat.refresh_shadow()
+        self.flat.grad.zero_()
 
     def launch(self, b):
         """Start bucket ``b``'s all-reduce now (idempotent within a step)."""
@@ -167,6 +252,10 @@ class DataParallel:
         return 1.0 / self.world
 
     def close(self):
+        if self.ipc is not None:
+            self.ipc.check()
+            self.ipc.close()
+            self.ipc = None
         if self._listener is not None:
             _grad.remove_listener(self._listener)
             self._listener = None

@@ -42,6 +42,8 @@ class StepRunner:
         self.steps = 0
         if ddp is not None:
             optimizer.grad_scale = ddp.grad_scale
+            if ddp.zero:
+                optimizer.shard(ddp.shard_ranges())
 
     @property
     def _dp(self):
@@ -83,6 +85,8 @@ class StepRunner:
         if self.ddp is not None:
             self.ddp.finish()
         self.opt.step()
+        if self.ddp is not None:
+            self.ddp.gather_params()  # ZeRO-1: all-gather the updated master pieces (no-op otherwise)
         return loss
 
     def _fwd_bwd_split(self, *batch):
@@ -131,7 +135,10 @@ class StepRunner:
                 ready[i] -= later
         self._split_keep = segments  # later graphs read leaf.grad / roots' saved tensors at fixed addresses
         self.graph, self.graph2 = graphs[0], graphs[1:]
+        old_ranges = self.ddp.shard_ranges()
         self.ddp.align_buckets(ready)
+        if self.ddp.zero:
+            self.ddp.reshard_optimizer(self.opt, old_ranges)
         self.bucket_waves = [self.ddp.complete_buckets(r) for r in ready]
 
     def _capture(self, batch):
@@ -146,11 +153,13 @@ class StepRunner:
             self.ddp.set_overlap(False)
             self._capture_split()
             return
-        if self._dp:
+        if self._dp and not self.ddp.graph_safe:
             self.ddp.set_overlap(False)  # no collective may be enqueued during capture
             with torch.cuda.graph(g):
                 self.static_loss = self._fwd_bwd(*self.static_in)
         else:
+            # one executor, or data-parallel over the IPC all-reduce kernel: the WHOLE step
+            # (forward, backward, gradient reduction, optimizer) is one graph
             with torch.cuda.graph(g):
                 self.static_loss = self._eager(*self.static_in)
         self.graph = g
@@ -170,7 +179,8 @@ class StepRunner:
                 for b in wave:
                     self.ddp.launch(b)
                 g.replay()
-        if self._dp:
+        if self._dp and not self.ddp.graph_safe:
             self.ddp.finish()   # bucketed RCCL all-reduce of the flat gradient buffer
             self.opt.step()
+            self.ddp.gather_params()
         return self.static_loss

@@ -78,3 +78,43 @@ def test_native_rccl_world1():
                              timeout=300).run(_rccl_fn)
     ref = torch.arange(16, dtype=torch.float32)
     assert torch.equal(x, ref) and torch.equal(o, ref) and torch.equal(r, ref) and e == 0
+
+
+def _mlp_dp(steps, use_dp):
+    import torch
+    from sparkmi.models.mlp import MultilayerPerceptron
+    from sparkmi.optim import SGD
+    from sparkmi.parallel import DataParallel, destroy, init_distributed
+    from sparkmi.train.runner import StepRunner
+    from sparkmi.utils.flat import FlatParams
+    rank, world, dev = init_distributed()
+    torch.manual_seed(0)
+    model = MultilayerPerceptron((4, 5, 4, 3)).to(dev).train()
+    flat = FlatParams(model, shadow=False)
+    opt = SGD(flat, lr=0.1)
+    ddp = DataParallel(flat) if use_dp else None
+    info = {"ipc": ddp is not None and ddp.ipc is not None, "graph_safe": ddp is not None and ddp.graph_safe}
+    runner = StepRunner(model, lambda m, x, y: m.loss(x, y), opt, ddp, graph=True)
+    g = torch.Generator().manual_seed(5)
+    X = torch.rand(steps, 60, 4, generator=g) * 2 - 1
+    Y = torch.randint(0, 3, (steps, 60), generator=g)
+    per = 60 // world
+    for i in range(steps):
+        runner.step(X[i, rank * per:(rank + 1) * per].to(dev), Y[i, rank * per:(rank + 1) * per].to(dev))
+    torch.cuda.synchronize()
+    out = flat.master.cpu().clone()
+    if ddp is not None:
+        ddp.close()
+    destroy()
+    return out, info
+
+
+def test_ipc_data_parallel_whole_step_graph():
+    """MLP data parallelism over the IPC all-reduce with the WHOLE step in one HIP graph (two
+    processes sharing the GPU) == one process at twice the batch."""
+    from sparkmi.api import Distributor
+    dp, info = Distributor(num_processes=2, use_gpu=True, env={"SPARKMI_DIST_BACKEND": "gloo"}, log_sink=None,
+                           timeout=300).run(_mlp_dp, 12, True)
+    assert info["ipc"] and info["graph_safe"]
+    single, _ = Distributor(num_processes=1, use_gpu=True, log_sink=None, timeout=300).run(_mlp_dp, 12, False)
+    torch.testing.assert_close(dp, single, atol=1e-5, rtol=1e-5)
