@@ -131,6 +131,8 @@ class DataParallel:
         self._works = []
         self.early_flushes = 0
 
+    bytes_reduced = 0  # cumulative gradient bytes handed to the collectives (metrics)
+
     @property
     def graph_safe(self):
         """True when the gradient reduction is a plain kernel (IPC path): the whole DP step can
@@ -154,6 +156,7 @@ class DataParallel:
         if self.flat.grad.is_cuda:
             _grad.join(self.flat.grad.device.index)  # weight grads may still be in flight on the side stream
         g = self.flat.grad[s:e]
+        self.bytes_reduced += g.numel() * g.element_size()
         if self.ipc is not None:
             self.ipc(g)  # stream-ordered kernel: nothing to wait for
             return

@@ -25,6 +25,7 @@ from .common import evaluate_classifier, run, shard
 @dataclasses.dataclass
 class CNNConfig(TrainConfig):
     """FashionMNIST CNN (distributed_cnn.py / pytorch_cnn.py)."""
+    local_mode: bool = False       # TorchDistributor(local_mode=False), distributed_cnn.py:227-230
     epochs: int = 3
     batch_size: int = 32
     lr: float = 0.01

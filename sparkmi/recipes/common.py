@@ -12,7 +12,9 @@ def run(train_fn, cfg):
     if cfg.world <= 1:
         return train_fn(cfg)
     use_gpu = cfg.device != "cpu" and torch.cuda.device_count() > 0
-    return Distributor(num_processes=cfg.world, local_mode=True, use_gpu=use_gpu).run(train_fn, cfg)
+    return Distributor(num_processes=cfg.world, local_mode=getattr(cfg, "local_mode", True), use_gpu=use_gpu,
+                       max_restarts=getattr(cfg, "max_restarts", 0),
+                       progress_timeout=getattr(cfg, "progress_timeout", 0.0) or None).run(train_fn, cfg)
 
 
 def shard(n, rank, world, seed=0):

@@ -32,6 +32,7 @@ SPECIALS = ["<pad>", "<sos>", "<eos>", "<unk>"]
 @dataclasses.dataclass
 class LSTMConfig(TrainConfig):
     """AG_NEWS LSTM classifier (distributed_lstm.py / pytorch_lstm.py)."""
+    local_mode: bool = False       # TorchDistributor(local_mode=False), distributed_lstm.py:211-214
     epochs: int = 3
     batch_size: int = 32
     lr: float = 1e-3

@@ -32,6 +32,10 @@ class TrainConfig:
     n_train: int = 0               # synthetic dataset size (0: reference size)
     n_test: int = 0
     bucket_mb: float = 64.0        # data-parallel gradient bucket size
+    zero: bool = False             # ZeRO-1: reduce-scatter + sharded optimizer + all-gather
+    local_mode: bool = True        # TorchDistributor local_mode (False: barrier-task cluster mode)
+    progress_timeout: float = 0.0  # s without step progress on a rank -> group failure (0: off)
+    max_restarts: int = 0          # group restarts from the last checkpoint after a failure
     verbose: bool = True
 
     def to_json(self):

@@ -40,6 +40,10 @@ class StepRunner:
         self.static_in = None
         self.static_loss = None
         self.steps = 0
+        # per-phase device timing: HIP events around forward+backward, gradient
+        # reduction and the optimizer, read back (one sync) by pop_phases() every log interval
+        self.phase_timing = False
+        self._phase_events = []
         if ddp is not None:
             optimizer.grad_scale = ddp.grad_scale
             if ddp.zero:
@@ -80,14 +84,40 @@ class StepRunner:
         for dst, src in zip(st, batch):
             dst.copy_(src, non_blocking=True)
 
+    def _event(self):
+        if not self.phase_timing or not torch.cuda.is_available() or torch.cuda.is_current_stream_capturing():
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
     def _eager(self, *batch):
+        e0 = self._event()
         loss = self._fwd_bwd(*batch)
+        e1 = self._event()
         if self.ddp is not None:
             self.ddp.finish()
+        e2 = self._event()
         self.opt.step()
         if self.ddp is not None:
             self.ddp.gather_params()  # ZeRO-1: all-gather the updated master pieces (no-op otherwise)
+        e3 = self._event()
+        if e0 is not None:
+            self._phase_events.append((e0, e1, e2, e3))
         return loss
+
+    def pop_phases(self):
+        """Mean device seconds per phase over the eager steps since the last call:
+        {fwd_bwd_s, allreduce_s, optim_s} (empty when no step was timed, e.g. graph replays,
+        whose phases live inside one graph)."""
+        ev, self._phase_events = self._phase_events, []
+        if not ev:
+            return {}
+        ev[-1][3].synchronize()
+        n = len(ev)
+        return {"fwd_bwd_s": sum(a.elapsed_time(b) for a, b, _, _ in ev) / n / 1e3,
+                "allreduce_s": sum(b.elapsed_time(c) for _, b, c, _ in ev) / n / 1e3,
+                "optim_s": sum(c.elapsed_time(d) for _, _, c, d in ev) / n / 1e3}
 
     def _fwd_bwd_split(self, *batch):
         _grad.reset_deferred()

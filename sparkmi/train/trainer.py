@@ -17,6 +17,7 @@ import torch
 
 from ..parallel import DataParallel, init_distributed
 from ..runtime.fault import fault_point
+from ..runtime.heartbeat import progress
 from ..utils import trace
 from ..utils.checkpoint import CheckpointManager
 from ..utils.flat import FlatParams
@@ -42,7 +43,7 @@ class Trainer:
         self.rank, self.world = rank, world
         self.flat = FlatParams(self.model, device=self.device, shadow=shadow)
         self.opt = make_optimizer(self.flat)
-        self.ddp = DataParallel(self.flat, bucket_mb=cfg.bucket_mb) if world > 1 else None
+        self.ddp = DataParallel(self.flat, bucket_mb=cfg.bucket_mb, zero=getattr(cfg, "zero", False)) if world > 1 else None
         use_graph = bool(cfg.graph) and self.device.type == "cuda"
         self.runner = StepRunner(self.model, loss_fn, self.opt, ddp=self.ddp, graph=use_graph)
         path = f"{cfg.metrics}.rank{rank}.jsonl" if cfg.metrics else None
@@ -79,20 +80,38 @@ class Trainer:
         t0 = time.perf_counter()
         steps_run, last = 0, None
         done = False
+        data_s, bytes0 = 0.0, 0
+        self.runner.phase_timing = bool(getattr(cfg, "phase_timing", True))
         while self.epoch < epochs and not done:
             if hasattr(loader, "set_epoch"):
                 loader.set_epoch(self.epoch)
             if hasattr(loader, "skip"):
                 loader.skip = self.cursor
             i = self.cursor
-            for batch in loader:
+            it = iter(loader)
+            while True:
+                td = time.perf_counter()
+                with trace.range("data"):
+                    batch = next(it, None)
+                if batch is None:
+                    break
+                data_s += time.perf_counter() - td
                 n = samples_per_batch or int(batch[0].shape[0])
                 with trace.range("step"):
                     last = self.runner.step(*batch)
                 self.step += 1
                 steps_run += 1
                 i += 1
-                self.metrics.step(last, n * self.world)
+                progress(self.step)  # heartbeat progress: a stuck collective stops this counter
+                if self.metrics.due():
+                    ph = self.runner.pop_phases()
+                    ddp_bytes = self.ddp.bytes_reduced if self.ddp is not None else 0
+                    extra = dict(ph, data_s=data_s / max(1, self.metrics.pending() + 1),
+                                 bytes_reduced=ddp_bytes - bytes0)
+                    bytes0, data_s = ddp_bytes, 0.0
+                    self.metrics.step(last, n * self.world, **extra)
+                else:
+                    self.metrics.step(last, n * self.world)
                 fault_point(self.step)
                 if self.ckpt is not None and cfg.ckpt_every and self.step % cfg.ckpt_every == 0:
                     self.cursor = i

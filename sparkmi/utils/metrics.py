@@ -3,7 +3,9 @@
 ``MetricsLogger.step(loss, n_samples)`` accumulates the loss ON DEVICE (no host sync per step,
 so a HIP-graph step loop is not stalled) and every ``every`` steps synchronises once and appends
 one JSON line: step, mean loss over the interval, samples/s and ms/step over the interval, plus
-any extra scalars given to ``log``.  ``aggregate()`` (driver side) combines per-rank files into
+the phase breakdown the Trainer passes (data_s: host time waiting for the batch;
+fwd_bwd_s / allreduce_s / optim_s: device time per phase from HIP events of eager steps;
+bytes_reduced: gradient bytes handed to the collectives in the interval).  ``aggregate()`` (driver side) combines per-rank files into
 whole-job samples/s, the BASELINE metric.
 """
 import json
@@ -36,6 +38,14 @@ class MetricsLogger:
     def _sync(self, t):
         if t is not None and t.is_cuda:
             torch.cuda.synchronize(t.device)
+
+    def due(self):
+        """True when the next step() call writes a record."""
+        return (self._step + 1) % self.every == 0
+
+    def pending(self):
+        """Steps accumulated since the last record."""
+        return self._n
 
     def step(self, loss=None, n_samples=0, **scalars):
         if self._t0 is None:

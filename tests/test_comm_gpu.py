@@ -41,7 +41,7 @@ def _ipc_fn():
 
 def test_ipc_allreduce_two_processes_one_gpu():
     from sparkmi.api import Distributor
-    res = Distributor(num_processes=2, use_gpu=True, env={"SPARKMI_DIST_BACKEND": "gloo"}, log_sink=None,
+    res = Distributor(num_processes=2, use_gpu=True, share_gpus=True, env={"SPARKMI_DIST_BACKEND": "gloo"}, log_sink=None,
                       timeout=300).run(_ipc_fn)
     k = 0
     for it in range(3):
@@ -113,7 +113,7 @@ def test_ipc_data_parallel_whole_step_graph():
     """MLP data parallelism over the IPC all-reduce with the WHOLE step in one HIP graph (two
     processes sharing the GPU) == one process at twice the batch."""
     from sparkmi.api import Distributor
-    dp, info = Distributor(num_processes=2, use_gpu=True, env={"SPARKMI_DIST_BACKEND": "gloo"}, log_sink=None,
+    dp, info = Distributor(num_processes=2, use_gpu=True, share_gpus=True, env={"SPARKMI_DIST_BACKEND": "gloo"}, log_sink=None,
                            timeout=300).run(_mlp_dp, 12, True)
     assert info["ipc"] and info["graph_safe"]
     single, _ = Distributor(num_processes=1, use_gpu=True, log_sink=None, timeout=300).run(_mlp_dp, 12, False)

@@ -164,3 +164,57 @@ def test_align_buckets_to_backward_segments():
     w0, w1 = ddp.complete_buckets(top), ddp.complete_buckets(mid)
     assert w0 and w1 and not set(w0) & set(w1)
     assert {i for b in w0 for i in ddp.buckets[b][2]} == {i for i, p in enumerate(flat.params) if id(p) in top}
+
+
+def _cluster_env():
+    import os
+    return {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "NODE_RANK",
+                                           "GROUP_RANK", "MASTER_ADDR", "SPARKMI_TASK_ADDRS", "SPARKMI_CLUSTER")}
+
+
+def test_cluster_mode_barrier_tasks():
+    """local_mode=False (distributed_cnn.py:227-231): each executor is a barrier task with its own
+    node rank and LOCAL_RANK 0; addresses are all-gathered before the run, task 0's is MASTER_ADDR."""
+    env = Distributor(num_processes=3, local_mode=False, use_gpu=False, log_sink=None).run(_cluster_env)
+    assert env["SPARKMI_CLUSTER"] == "1" and env["RANK"] == "0" and env["WORLD_SIZE"] == "3"
+    assert env["LOCAL_RANK"] == "0" and env["LOCAL_WORLD_SIZE"] == "1" and env["NODE_RANK"] == "0"
+    addrs = env["SPARKMI_TASK_ADDRS"].split(",")
+    assert len(addrs) == 3 and env["MASTER_ADDR"] == addrs[0]
+
+
+def _cluster_dp():
+    import torch
+    import torch.distributed as dist
+    from sparkmi.parallel import init_distributed
+    rank, world, _ = init_distributed()
+    t = torch.full((4,), float(rank + 1))
+    dist.all_reduce(t)
+    return t.tolist(), world
+
+
+def test_cluster_mode_collectives():
+    vals, world = Distributor(num_processes=2, local_mode=False, use_gpu=False, log_sink=None).run(_cluster_dp)
+    assert world == 2 and vals == [3.0] * 4
+
+
+def _collective_hang():
+    import time
+    import torch
+    import torch.distributed as dist
+    from sparkmi.parallel import init_distributed
+    from sparkmi.runtime import progress
+    rank, world, _ = init_distributed(timeout_s=3600)
+    for step in range(1, 1000):
+        progress(step)
+        if rank == 1 and step == 3:
+            while True:  # rank 1 wedges: rank 0 blocks INSIDE all_reduce, its heartbeat thread still beats
+                time.sleep(1)
+        dist.all_reduce(torch.ones(4))
+        time.sleep(0.05)
+
+
+def test_hang_inside_collective_detected_by_progress():
+    d = Distributor(num_processes=2, use_gpu=False, progress_timeout=3.0, log_sink=None, timeout=120)
+    with pytest.raises(LaunchError) as e:
+        d.run(_collective_hang)
+    assert "progress stalled" in str(e.value)
