@@ -278,6 +278,117 @@ __device__ __forceinline__ void gemm_f32_tile(const GemmF32Args& g, int tile, in
 }
 
 
+// Compile-time epilogue feature set of the pipelined kernel (EPI < 0: generic runtime flags).
+// Measured: the runtime-generic epilogue was ~9,700 instructions per wave (per-element mode /
+// flag branches, 64-bit address math, scalar loads of the C operand) = the ~20 us fixed cost of
+// every launch in the K scan (tools/f32_kscan.py); the specialised, LDS-staged one below is a
+// few hundred.
+enum : int { FE_BIAS = 1, FE_RELU = 2, FE_SIG = 4, FE_DROP = 8, FE_RESID = 16, FE_DACT = 32, FE_ACC = 64, FE_ATOMIC = 128 };
+#define FE_PITCH 132  // LDS pitch of the staged 128 x 128 fp32 tile (conflict-free both passes)
+
+template <int EPI>
+__device__ __forceinline__ bool fe_has(const GemmF32Args& g, int f) {
+  if constexpr (EPI >= 0) return (EPI & f) != 0;
+  switch (f) {
+    case FE_BIAS: return g.mode == 0 && g.bias;
+    case FE_RELU: return g.mode == 0 && g.relu == 1;
+    case FE_SIG: return g.mode == 0 && g.relu == 2;
+    case FE_DROP: return g.mode == 0 && g.thresh;
+    case FE_RESID: return g.mode == 1 && g.resid;
+    case FE_DACT: return g.mode == 1 && g.dact_y;
+    case FE_ACC: return g.beta_acc && !g.atomic;
+    case FE_ATOMIC: return g.atomic;
+  }
+  return false;
+}
+
+// The accumulators go through LDS once ([128][132] image, 66 KiB of the idle stage ring) so each
+// thread then owns 4 consecutive columns of 16 rows: float4 operand loads (bias once, residual /
+// mask / C per row) and float4 stores of whole 512-B row segments, no per-element addressing.
+template <bool AK, int EPI>
+__device__ __forceinline__ void f32_epilogue_lds(const GemmF32Args& g, f32x16_t (&acc)[2][2], float (&bsum)[2], int m0,
+                                                 int n0, int wm, int wn, int lane, bool do_bias, float* smem) {
+  const int tid = threadIdx.x, h = lane >> 5;
+  __syncthreads();  // every wave is done reading the k-loop's LDS stages
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        smem[(wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * FE_PITCH + wn * 64 + j * 32 + (lane & 31)] = acc[i][j][r];
+  __syncthreads();
+  const int c4 = (tid & 31) * 4, col = n0 + c4;
+  const bool full_cols = col + 3 < g.N;
+  const uint32_t seed = fe_has<EPI>(g, FE_DROP) ? smi_seed(g.seedp, g.salt) : 0u;
+  float4 bia = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (fe_has<EPI>(g, FE_BIAS)) {
+    if (full_cols) bia = *(const float4*)(g.bias + col);
+    else {
+      if (col < g.N) bia.x = g.bias[col];
+      if (col + 1 < g.N) bia.y = g.bias[col + 1];
+      if (col + 2 < g.N) bia.z = g.bias[col + 2];
+    }
+  }
+  const float bb[4] = {bia.x, bia.y, bia.z, bia.w};
+#pragma unroll 4
+  for (int q = 0; q < 16; ++q) {
+    const int rl = (tid >> 5) + 8 * q, row = m0 + rl;
+    if (row >= g.M || col >= g.N) continue;
+    const float4 t = *(const float4*)(smem + rl * FE_PITCH + c4);
+    float v[4] = {t.x, t.y, t.z, t.w};
+    const long cidx = (long)row * g.ldc + col;
+    if (full_cols) {
+      float4 rs, dy, cc;
+      if (fe_has<EPI>(g, FE_RESID)) rs = *(const float4*)(g.resid + (long)row * g.ldr + col);
+      if (fe_has<EPI>(g, FE_DACT)) dy = *(const float4*)(g.dact_y + (long)row * g.ldy + col);
+      if (fe_has<EPI>(g, FE_ACC)) cc = *(const float4*)(g.C + cidx);
+      const float rv[4] = {rs.x, rs.y, rs.z, rs.w}, dv[4] = {dy.x, dy.y, dy.z, dy.w}, cv[4] = {cc.x, cc.y, cc.z, cc.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x = v[e] + bb[e];
+        if (fe_has<EPI>(g, FE_RELU)) x = fmaxf(x, 0.f);
+        if (fe_has<EPI>(g, FE_SIG)) x = 1.f / (1.f + __expf(-x));
+        if (fe_has<EPI>(g, FE_DROP)) x = smi_keep(seed, (uint32_t)(cidx + e), g.thresh) ? x * g.dscale : 0.f;
+        if (fe_has<EPI>(g, FE_RESID)) x += rv[e];
+        if (fe_has<EPI>(g, FE_DACT)) x = dv[e] > 0.f ? x * g.dscale : 0.f;
+        if (fe_has<EPI>(g, FE_ACC)) x += cv[e];
+        v[e] = x;
+      }
+      if (fe_has<EPI>(g, FE_ATOMIC)) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) atomicAdd(g.C + cidx + e, v[e]);
+      } else {
+        *(float4*)(g.C + cidx) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    } else {
+      for (int e = 0; e < 4 && col + e < g.N; ++e) {
+        float x = v[e] + bb[e];
+        if (fe_has<EPI>(g, FE_RELU)) x = fmaxf(x, 0.f);
+        if (fe_has<EPI>(g, FE_SIG)) x = 1.f / (1.f + __expf(-x));
+        if (fe_has<EPI>(g, FE_DROP)) x = smi_keep(seed, (uint32_t)(cidx + e), g.thresh) ? x * g.dscale : 0.f;
+        if (fe_has<EPI>(g, FE_RESID)) x += g.resid[(long)row * g.ldr + col + e];
+        if (fe_has<EPI>(g, FE_DACT)) x = g.dact_y[(long)row * g.ldy + col + e] > 0.f ? x * g.dscale : 0.f;
+        if (fe_has<EPI>(g, FE_ATOMIC)) atomicAdd(g.C + cidx + e, x);
+        else g.C[cidx + e] = fe_has<EPI>(g, FE_ACC) ? g.C[cidx + e] + x : x;
+      }
+    }
+  }
+  if (AK && do_bias) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      // lanes l and l + 32 hold the two k-halves of row (l & 31)
+      auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(bsum[i]), __float_as_uint(bsum[i]), false, false);
+      const float tot = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+      const int row = m0 + wm * 64 + i * 32 + (lane & 31);
+      if (h == 0 && row < g.M) {
+        if (fe_has<EPI>(g, FE_ATOMIC)) atomicAdd(g.bias_grad + row, tot);
+        else g.bias_grad[row] = fe_has<EPI>(g, FE_ACC) ? g.bias_grad[row] + tot : tot;
+      }
+    }
+  }
+}
+
 // Software-pipelined form (one workgroup = one wave per SIMD, 128 x 128 tile, 3-stage LDS ring):
 // measured on the two-workgroups-per-CU form, the matrix pipe idled ~37 % of the time — the two
 // waves of a SIMD drift into lock-step (both in their load / barrier phase at once).  Here one
@@ -292,7 +403,7 @@ __device__ __forceinline__ void gemm_f32_tile(const GemmF32Args& g, int tile, in
 #define SG_VMEM_RD 0x020
 #define SG_DS_RD 0x100
 #define SG_DS_WR 0x200
-template <bool AK, bool BKM>
+template <bool AK, bool BKM, int EPI>
 __device__ __forceinline__ void gemm_f32_tile_pipe(const GemmF32Args& g, int tile, int split, float* smem) {
   constexpr int FM = 2, BMT = 128;
   using TA = F32Tile<AK, BMT>;
@@ -394,16 +505,16 @@ __device__ __forceinline__ void gemm_f32_tile_pipe(const GemmF32Args& g, int til
     schedule();
     __syncthreads();
   }
-  f32_epilogue<AK, FM>(g, acc, bsum, m0, n0, wm, wn, lane, do_bias);
+  f32_epilogue_lds<AK, EPI>(g, acc, bsum, m0, n0, wm, wn, lane, do_bias, smem);
 }
 
-template <bool AK, bool BKM>
+template <bool AK, bool BKM, int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_f32_pipe_kernel(GemmF32Args g) {
   __shared__ __attribute__((aligned(16))) float smem[3 * (F32Tile<AK, 128>::ELEMS + F32Tile<BKM, FBN>::ELEMS)];
   const int nwg = ((g.M + 127) / 128) * ((g.N + FBN - 1) / FBN);
   const int split = blockIdx.x / nwg;
   const int tile = f32_tile_remap(blockIdx.x - split * nwg, nwg);
-  gemm_f32_tile_pipe<AK, BKM>(g, tile, split, smem);
+  gemm_f32_tile_pipe<AK, BKM, EPI>(g, tile, split, smem);
 }
 
 template <bool AK, bool BKM, int FM, int PF>
@@ -457,9 +568,36 @@ extern "C" int smi_gemm_f32(const GemmF32Args* args, hipStream_t st) {
   if (pf_env == 0) {
     const int nwg128 = ((g.M + 127) / 128) * ((g.N + FBN - 1) / FBN);
     const dim3 grid2((unsigned)(nwg128 * g.splits));
-    if (g.mode == 0) hipLaunchKernelGGL((gemm_f32_pipe_kernel<false, false>), grid2, block, 0, st, g);
-    else if (g.mode == 1) hipLaunchKernelGGL((gemm_f32_pipe_kernel<false, true>), grid2, block, 0, st, g);
-    else hipLaunchKernelGGL((gemm_f32_pipe_kernel<true, true>), grid2, block, 0, st, g);
+    // specialised epilogues for the feature sets the models use; anything else -> generic (-1)
+    int fe = 0;
+    if (g.mode == 0) {
+      fe = (g.bias ? FE_BIAS : 0) | (g.relu == 1 ? FE_RELU : 0) | (g.relu == 2 ? FE_SIG : 0) | (g.thresh ? FE_DROP : 0);
+    } else if (g.mode == 1) {
+      fe = (g.resid ? FE_RESID : 0) | (g.dact_y ? FE_DACT : 0);
+    }
+    fe |= (g.atomic ? FE_ATOMIC : (g.beta_acc ? FE_ACC : 0));
+#define F32P(AKV, BKV, E) hipLaunchKernelGGL((gemm_f32_pipe_kernel<AKV, BKV, E>), grid2, block, 0, st, g)
+    if (g.mode == 0) {
+      switch (fe) {
+        case 0: F32P(false, false, 0); break;
+        case FE_BIAS: F32P(false, false, FE_BIAS); break;
+        case FE_BIAS | FE_RELU: F32P(false, false, FE_BIAS | FE_RELU); break;
+        case FE_BIAS | FE_RELU | FE_DROP: F32P(false, false, FE_BIAS | FE_RELU | FE_DROP); break;
+        default: F32P(false, false, -1); break;
+      }
+    } else if (g.mode == 1) {
+      switch (fe) {
+        case 0: F32P(false, true, 0); break;
+        case FE_RESID: F32P(false, true, FE_RESID); break;
+        case FE_DACT: F32P(false, true, FE_DACT); break;
+        default: F32P(false, true, -1); break;
+      }
+    } else {
+      if (fe == FE_ACC) F32P(true, true, FE_ACC);
+      else if (fe == FE_ATOMIC) F32P(true, true, FE_ATOMIC);
+      else F32P(true, true, -1);
+    }
+#undef F32P
     SMI_CHECK_LAUNCH();
   }
 #define F32K(AKV, BKV, FMV)                                                                          \
@@ -503,7 +641,7 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_wgrad_group_kernel(WgradGroup
   g.bias_grad = gr.bias[e];
   const int nwg = ((g.M + 127) / 128) * ((g.N + FBN - 1) / FBN);
   const int lt = t - gr.t0[e];
-  if (lt < nwg) gemm_f32_tile_pipe<true, true>(g, f32_tile_remap(lt, nwg), 0, smem);  // lt >= nwg: padding
+  if (lt < nwg) gemm_f32_tile_pipe<true, true, FE_ACC>(g, f32_tile_remap(lt, nwg), 0, smem);  // lt >= nwg: padding
 }
 
 extern "C" int smi_gemm_f32_wgrad_group(const void* const* A, const long* lda, const void* const* B, const long* ldb,
