@@ -57,6 +57,7 @@ int smi_colsum_bf16(const void*, long, int, float*, int, float*, int, hipStream_
 int smi_cast_f32_bf16(const float*, void*, long, hipStream_t);
 int smi_add_bf16(const void*, const void*, void*, long, hipStream_t);
 int smi_step_inc(float*, hipStream_t);
+int smi_seed_inc(int*, hipStream_t);
 int smi_mlp_fwd(const MLPArgs*, hipStream_t);
 int smi_gemm(const GemmArgs*, hipStream_t);
 int smi_gemm_f32(const GemmF32Args*, hipStream_t);
@@ -230,6 +231,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("cast_f32_bf16", [](u x, u y, long n, u st) { chk(smi_cast_f32_bf16(PF(x), P(y), n, S(st)), "cast_f32_bf16"); });
   m.def("add_bf16", [](u a, u b, u y, long n, u st) { chk(smi_add_bf16(P(a), P(b), P(y), n, S(st)), "add_bf16"); });
   m.def("step_inc", [](u step, u st) { chk(smi_step_inc(PF(step), S(st)), "step_inc"); });
+  m.def("seed_inc", [](u seed, u st) { chk(smi_seed_inc(reinterpret_cast<int*>(seed), S(st)), "seed_inc"); });
   // step: device step counter (advanced by the kernel); done: zeroed uint32 ticket word
   m.def("adam", [](u p, u g, u mm, u v, u pbf, long n, u lr, u step, u done, float b1, float b2, float eps, float wd,
                    float gscale, int adamw, int zero_grad, u st) {

@@ -36,51 +36,51 @@ __global__ void bias_act_drop_fwd_kernel(const unsigned short* __restrict__ x, c
 // dx = dy * dact(y) * dropmask*scale.  For relu the saved output y decides (y > 0 implies kept
 // and positive); for sigmoid y must be the pre-dropout activation (dropout unsupported there);
 // for identity the mask is recomputed from the seed.
+__device__ __forceinline__ float adb_one(float g, float yv, long idx, int act, uint32_t seed, uint32_t thresh,
+                                         float dscale) {
+  if (act == 1) return yv > 0.f ? g * (thresh ? dscale : 1.f) : 0.f;
+  if (act == 2) g *= yv * (1.f - yv);
+  if (thresh) g = smi_keep(seed, (uint32_t)idx, thresh) ? g * dscale : 0.f;
+  return g;
+}
+
 __global__ void act_drop_bwd_kernel(const unsigned short* __restrict__ dy, const unsigned short* __restrict__ y,
                                     unsigned short* __restrict__ dx, long total, int act,
                                     const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale) {
   const uint32_t seed = smi_seed(seedp, salt);
   const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
   if (i >= total) return;
+  if (i + 8 > total) {  // ragged tail (total % 8 != 0)
+    for (long j = i; j < total; ++j)
+      dx[j] = f2bf(adb_one(bf2f(dy[j]), act ? bf2f(y[j]) : 0.f, j, act, seed, thresh, dscale));
+    return;
+  }
   u16x8_t d = *(const u16x8_t*)(dy + i);
   u16x8_t yy;
   if (act) yy = *(const u16x8_t*)(y + i);
   u16x8_t o;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float g = bf2f(d[j]);
-    if (act == 1) g = bf2f(yy[j]) > 0.f ? g * (thresh ? dscale : 1.f) : 0.f;
-    else {
-      if (act == 2) { const float s = bf2f(yy[j]); g *= s * (1.f - s); }
-      if (thresh) g = smi_keep(seed, (uint32_t)(i + j), thresh) ? g * dscale : 0.f;
-    }
-    o[j] = f2bf(g);
-  }
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(adb_one(bf2f(d[j]), act ? bf2f(yy[j]) : 0.f, i + j, act, seed, thresh, dscale));
   *(u16x8_t*)(dx + i) = o;
 }
 
-// fp32 form of act_drop_bwd (reference-precision path): 4 floats per lane, 16-B accesses.
 __global__ void act_drop_bwd_f32_kernel(const float* __restrict__ dy, const float* __restrict__ y,
                                         float* __restrict__ dx, long total, int act,
                                         const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale) {
   const uint32_t seed = smi_seed(seedp, salt);
   const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i >= total) return;
+  if (i + 4 > total) {  // ragged tail (total % 4 != 0)
+    for (long j = i; j < total; ++j) dx[j] = adb_one(dy[j], act ? y[j] : 0.f, j, act, seed, thresh, dscale);
+    return;
+  }
   const float4 d = *(const float4*)(dy + i);
   float4 yy = make_float4(0.f, 0.f, 0.f, 0.f);
   if (act) yy = *(const float4*)(y + i);
   const float dv[4] = {d.x, d.y, d.z, d.w}, yv[4] = {yy.x, yy.y, yy.z, yy.w};
   float o[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    float g = dv[j];
-    if (act == 1) g = yv[j] > 0.f ? g * (thresh ? dscale : 1.f) : 0.f;
-    else {
-      if (act == 2) g *= yv[j] * (1.f - yv[j]);
-      if (thresh) g = smi_keep(seed, (uint32_t)(i + j), thresh) ? g * dscale : 0.f;
-    }
-    o[j] = g;
-  }
+  for (int j = 0; j < 4; ++j) o[j] = adb_one(dv[j], yv[j], i + j, act, seed, thresh, dscale);
   *(float4*)(dx + i) = make_float4(o[0], o[1], o[2], o[3]);
 }
 
@@ -138,7 +138,7 @@ __global__ void add_bf16_kernel(const unsigned short* __restrict__ a, const unsi
   *(u16x8_t*)(y + i) = o;
 }
 
-static inline unsigned nblk8(long total) { return (unsigned)((total / 8 + 255) / 256); }
+static inline unsigned nblk8(long total) { return (unsigned)(((total + 7) / 8 + 255) / 256); }
 
 extern "C" int smi_bias_act_drop_fwd(const void* x, const float* bias, void* y, long total, int N, int act,
                                      const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, hipStream_t st) {
@@ -150,7 +150,7 @@ extern "C" int smi_bias_act_drop_fwd(const void* x, const float* bias, void* y, 
 
 extern "C" int smi_act_drop_bwd(const void* dy, const void* y, void* dx, long total, int act, const uint32_t* seedp, uint32_t salt,
                                 uint32_t thresh, float dscale, hipStream_t st) {
-  if (total % 8) return -1;
+  if (total < 1) return 0;
   hipLaunchKernelGGL(act_drop_bwd_kernel, dim3(nblk8(total)), dim3(256), 0, st, (const unsigned short*)dy,
                      (const unsigned short*)y, (unsigned short*)dx, total, act, seedp, salt, thresh, dscale);
   SMI_CHECK_LAUNCH();
@@ -158,8 +158,8 @@ extern "C" int smi_act_drop_bwd(const void* dy, const void* y, void* dx, long to
 
 extern "C" int smi_act_drop_bwd_f32(const float* dy, const float* y, float* dx, long total, int act, const uint32_t* seedp,
                                     uint32_t salt, uint32_t thresh, float dscale, hipStream_t st) {
-  if (total % 4) return -1;
-  hipLaunchKernelGGL(act_drop_bwd_f32_kernel, dim3((unsigned)((total / 4 + 255) / 256)), dim3(256), 0, st, dy, y, dx, total,
+  if (total < 1) return 0;
+  hipLaunchKernelGGL(act_drop_bwd_f32_kernel, dim3((unsigned)(((total + 3) / 4 + 255) / 256)), dim3(256), 0, st, dy, y, dx, total,
                      act, seedp, salt, thresh, dscale);
   SMI_CHECK_LAUNCH();
 }

@@ -319,7 +319,9 @@ __device__ __forceinline__ void f32_epilogue_lds(const GemmF32Args& g, f32x16_t 
         smem[(wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * FE_PITCH + wn * 64 + j * 32 + (lane & 31)] = acc[i][j][r];
   __syncthreads();
   const int c4 = (tid & 31) * 4, col = n0 + c4;
-  const bool full_cols = col + 3 < g.N;
+  // float4 stores / loads need 16-B aligned rows: ragged leading dimensions take the scalar path
+  const bool vec = ((g.ldc | (fe_has<EPI>(g, FE_RESID) ? g.ldr : 0) | (fe_has<EPI>(g, FE_DACT) ? g.ldy : 0)) & 3) == 0;
+  const bool full_cols = vec && col + 3 < g.N;
   const uint32_t seed = fe_has<EPI>(g, FE_DROP) ? smi_seed(g.seedp, g.salt) : 0u;
   float4 bia = make_float4(0.f, 0.f, 0.f, 0.f);
   if (fe_has<EPI>(g, FE_BIAS)) {
@@ -328,6 +330,7 @@ __device__ __forceinline__ void f32_epilogue_lds(const GemmF32Args& g, f32x16_t 
       if (col < g.N) bia.x = g.bias[col];
       if (col + 1 < g.N) bia.y = g.bias[col + 1];
       if (col + 2 < g.N) bia.z = g.bias[col + 2];
+      if (col + 3 < g.N) bia.w = g.bias[col + 3];
     }
   }
   const float bb[4] = {bia.x, bia.y, bia.z, bia.w};

@@ -14,6 +14,8 @@
 #include "smi_common.h"
 
 __global__ void step_inc_kernel(float* step) { step[0] += 1.f; }
+// dropout step seed (sparkmi/ops/rng.py DropoutRNG.advance): one lane, captured in step graphs
+__global__ void seed_inc_kernel(int* seed) { seed[0] += 1; }
 
 // No __threadfence: nothing but the counter itself is published (the next launch sees it at the
 // kernel boundary), and an agent-scope release on gfx950 writes back L2 — once per block that
@@ -155,6 +157,11 @@ static inline unsigned grid_for(long n) {
   if (b > 4096) b = 4096;
   if (b < 1) b = 1;
   return (unsigned)b;
+}
+
+extern "C" int smi_seed_inc(int* seed, hipStream_t st) {
+  hipLaunchKernelGGL(seed_inc_kernel, dim3(1), dim3(1), 0, st, seed);
+  return (int)hipGetLastError();
 }
 
 extern "C" int smi_step_inc(float* step, hipStream_t st) {

@@ -19,6 +19,7 @@ Mask semantics:
   strictly-past keys.  mask_mode="causal" is the corrected semantics: key-padding masking in
   the encoder and cross attention, true causal masking in decoder self-attention.
 """
+import functools
 from dataclasses import dataclass
 
 import torch
@@ -27,7 +28,8 @@ from torch import nn
 from ..ops import (DropoutRNG, add_dropout_layernorm, cross_attention, embedding, linear, self_attention,
                    sinusoid_table)
 from ..ops._grad import ResidualGrad
-from ..ops.linear import ffn
+from ..ops._grad import SharedGrad
+from ..ops.linear import concat_linear, ffn
 from ..ops.loss import cross_entropy
 from ..ops.rng import new_salt
 
@@ -51,6 +53,11 @@ class TransformerConfig:
     mask_mode: str = "reference"      # or "causal"
     pad_id: int = 0
     dtype: str = "bf16"               # GPU activation dtype: "bf16" (fp32 master) or "fp32" (reference precision)
+
+
+def _native_path(x):
+    from .. import _native
+    return _native.use_native(x)
 
 
 def _share(obj, name, value):
@@ -115,10 +122,15 @@ class MultiHeadCrossAttention(nn.Module):
         self.q_layer = nn.Linear(d_model, d_model)
         self.linear_layer = nn.Linear(d_model, d_model)
 
-    def forward(self, x, y, mode="none", key_padding=None, y_slot=None):
-        kv = linear(x, self.kv_layer.weight, self.kv_layer.bias)
+    def forward(self, x, y, mode="none", key_padding=None, y_slot=None, kv=None):
+        """``kv``: optional (kv_all, column, SharedGrad) — this layer's k/v projection already
+        computed inside the decoder's concatenated kv GEMM (Decoder._shared_kv)."""
+        if kv is None:
+            kv_all, col, shared = linear(x, self.kv_layer.weight, self.kv_layer.bias), 0, None
+        else:
+            kv_all, col, shared = kv
         q = linear(y, self.q_layer.weight, self.q_layer.bias, x_slot=y_slot)
-        values = cross_attention(q, kv, self.num_heads, mode, key_padding)
+        values = cross_attention(q, kv_all, self.num_heads, mode, key_padding, col, shared)
         return linear(values, self.linear_layer.weight, self.linear_layer.bias)
 
 
@@ -210,12 +222,12 @@ class DecoderLayer(nn.Module):
         _share(self, "_rng", rng)
         self.salts = (new_salt(), new_salt(), new_salt())
 
-    def forward(self, x, y, self_mode="none", cross_mode="none", key_padding=None):
+    def forward(self, x, y, self_mode="none", cross_mode="none", key_padding=None, kv=None):
         ps = [d.p if self.training else 0.0 for d in (self.dropout1, self.dropout2, self.dropout3)]
         s1, s2, s3 = ResidualGrad(), ResidualGrad(), ResidualGrad()
         a = self.self_attention(y, self_mode, x_slot=s1)
         y = self.layer_norm1(a, y, ps[0], self._rng, self.salts[0], r_slot=s1)
-        c = self.encoder_decoder_attention(x, y, cross_mode, key_padding, y_slot=s2)
+        c = self.encoder_decoder_attention(x, y, cross_mode, key_padding, y_slot=s2, kv=kv)
         y = self.layer_norm2(c, y, ps[1], self._rng, self.salts[1], r_slot=s2)
         f = self.ffn(y, x_slot=s3)
         return self.layer_norm3(f, y, ps[2], self._rng, self.salts[2], r_slot=s3)
@@ -223,9 +235,10 @@ class DecoderLayer(nn.Module):
 
 class SequentialDecoder(nn.Sequential):
     def forward(self, *inputs):
-        x, y, self_mode, cross_mode, key_padding = inputs
-        for module in self._modules.values():
-            y = module(x, y, self_mode, cross_mode, key_padding)
+        x, y, self_mode, cross_mode, key_padding = inputs[:5]
+        kvs = inputs[5] if len(inputs) > 5 and inputs[5] is not None else [None] * len(self._modules)
+        for module, kv in zip(self._modules.values(), kvs):
+            y = module(x, y, self_mode, cross_mode, key_padding, kv)
         return y
 
 
@@ -237,9 +250,30 @@ class Decoder(nn.Module):
         self.layers = SequentialDecoder(*[DecoderLayer(d_model, ffn_hidden, num_heads, drop_prob, rng)
                                           for _ in range(num_layers)])
 
-    def forward(self, x, y, self_mode="none", cross_mode="none", key_padding=None):
+    def forward(self, x, y, self_mode="none", cross_mode="none", key_padding=None, flat=None):
         y = self.sentence_embedding(y)
-        return self.layers(x, y, self_mode, cross_mode, key_padding)
+        return self.layers(x, y, self_mode, cross_mode, key_padding, self._shared_kv(x, flat))
+
+    def kv_linears(self):
+        return [l.encoder_decoder_attention.kv_layer for l in self.layers]
+
+    def _shared_kv(self, x, flat):
+        """Every decoder layer projects the SAME encoder output to k/v (transformer.py:175-182):
+        on the GPU, with the kv weights stored back to back (Transformer._smi_flat_groups), that is
+        ONE GEMM of width L*2D; each layer's cross attention reads its column block and writes its
+        k/v gradient into the shared buffer, so the backward is one dgrad GEMM (K = L*2D, the sum
+        over layers done in the accumulators) and one weight-gradient GEMM."""
+        lins = self.kv_linears()
+        if flat is None or len(lins) < 2 or not _native_path(x):
+            return None
+        shared = SharedGrad()
+        kv_all = concat_linear(x, flat, lins, shared)
+        if kv_all is None:
+            return None
+        cols = [0]
+        for l in lins[:-1]:
+            cols.append(cols[-1] + l.weight.shape[0])
+        return [(kv_all, c, shared) for c in cols]
 
 
 class Transformer(nn.Module):
@@ -262,29 +296,45 @@ class Transformer(nn.Module):
                                tgt_vocab_size, self.rng, emb_dropout, dtype)
         self.linear = nn.Linear(d_model, tgt_vocab_size)
 
+    def _smi_flat_groups(self):
+        """FlatParams layout hint: the decoder's kv projections back to back (Decoder._shared_kv)."""
+        lins = self.decoder.kv_linears()
+        return [[l.weight for l in lins], [l.bias for l in lins]]
+
     @classmethod
     def from_config(cls, cfg: TransformerConfig, seed=0):
         return cls(cfg.d_model, cfg.ffn_hidden, cfg.num_heads, cfg.drop_prob, cfg.num_layers,
                    cfg.max_sequence_length, cfg.tgt_vocab_size, cfg.src_vocab_size, cfg.tgt_vocab_size,
                    cfg.mask_mode, cfg.emb_dropout, cfg.pad_id, seed, cfg.dtype)
 
-    def _modes(self, x, encoder_self_attention_mask, decoder_self_attention_mask, decoder_cross_attention_mask):
+    def _modes(self, x, encoder_self_attention_mask, decoder_self_attention_mask, decoder_cross_attention_mask,
+               y=None):
         if self.config.mask_mode == "reference":
-            # Q6: padding mask -> no-op; any look-ahead mask -> +1.0 on strictly-past keys
-            self_mode = "reference" if decoder_self_attention_mask is not None else "none"
-            cross_mode = "reference" if decoder_cross_attention_mask is not None else "none"
-            return "none", self_mode, cross_mode, None
+            # the masks are read by value, as the reference adds them (transformer.py:17-19)
+            Ss = x.shape[1]
+            St = y.shape[1] if y is not None else Ss
+            enc_mode, kp = interpret_mask(encoder_self_attention_mask, Ss, Ss)
+            self_mode, kp_self = interpret_mask(decoder_self_attention_mask, St, St)
+            cross_mode, kp_cross = interpret_mask(decoder_cross_attention_mask, St, Ss)
+            if kp_self is not None:
+                raise ValueError("decoder self-attention: key-padding masks are not supported by the fused kernels")
+            if kp is not None and kp_cross is not None and not torch.equal(kp, kp_cross):
+                raise ValueError("encoder and cross-attention key-padding masks must agree")
+            kp = kp if kp is not None else kp_cross
+            if kp is not None:
+                kp = kp.to(x.device)
+            return enc_mode, self_mode, cross_mode, kp
         key_padding = (x == self.config.pad_id)
         return "none", "causal", "none", key_padding
 
     def forward(self, x, y, encoder_self_attention_mask=None, decoder_self_attention_mask=None,
                 decoder_cross_attention_mask=None, enc_key_padding=None):
         enc_mode, self_mode, cross_mode, kp = self._modes(x, encoder_self_attention_mask,
-                                                          decoder_self_attention_mask, decoder_cross_attention_mask)
+                                                          decoder_self_attention_mask, decoder_cross_attention_mask, y)
         if enc_key_padding is not None:
             kp = enc_key_padding
         x = self.encoder(x, enc_mode, kp)
-        out = self.decoder(x, y, self_mode, cross_mode, kp)
+        out = self.decoder(x, y, self_mode, cross_mode, kp, getattr(self, "_smi_flat", None))
         return linear(out, self.linear.weight, self.linear.bias)
 
     def loss(self, logits, target):
@@ -297,7 +347,7 @@ class Transformer(nn.Module):
             dec_in, target = tgt[:, :-1], tgt[:, 1:]
         else:
             dec_in, target = tgt, tgt
-        la = torch.ones(1, dtype=torch.bool)  # marker: look-ahead mask present
+        la = create_look_ahead_mask(dec_in.shape[1])  # the reference's decoder masks (host, cached)
         logits = self(src, dec_in, None, la, la)
         return self.loss(logits, target)
 
@@ -314,8 +364,8 @@ class Transformer(nn.Module):
             dec_in, target = tgt[:, :-1], tgt[:, 1:]
         else:
             dec_in, target = tgt, tgt
-        la = torch.ones(1, dtype=torch.bool)
-        enc_mode, self_mode, cross_mode, kp = self._modes(src, None, la, la)
+        la = create_look_ahead_mask(dec_in.shape[1])
+        enc_mode, self_mode, cross_mode, kp = self._modes(src, None, la, la, dec_in)
         layers = list(self.encoder.layers)
         n = len(layers)
         cuts = sorted({c for c in (enc_cuts if enc_cuts is not None else [n // 2]) if 0 < c < n})
@@ -327,12 +377,87 @@ class Transformer(nn.Module):
             leaf = x.detach().requires_grad_()
             segments.append((leaf, x))
             x, start = leaf, c
-        out = self.decoder(x, dec_in, self_mode, cross_mode, kp)
+        out = self.decoder(x, dec_in, self_mode, cross_mode, kp, getattr(self, "_smi_flat", None))
         logits = linear(out, self.linear.weight, self.linear.bias)
         return self.loss(logits, target), segments[::-1]
 
 
+@functools.lru_cache(maxsize=16)
 def create_look_ahead_mask(size):
-    """pytorch_machine_translator.py:102-104."""
+    """pytorch_machine_translator.py:102-104 (bool [1,1,S,S], True above the diagonal); cached
+    host tensor, so the per-step mask costs nothing and is interpreted once."""
     mask = torch.tril(torch.ones(size, size)) == 0
     return mask.unsqueeze(0).unsqueeze(0)
+
+
+_NEG = -1e4  # an additive bias at or below this is a "masked out" key
+_mask_cache = {}
+
+
+def interpret_mask(mask, Sq, Sk):
+    """What the fused attention kernels must do for a reference-style mask tensor.
+
+    The reference ADDS ``mask.permute(0, 1, 3, 2)`` to the [B, H, Sq, Sk] scores
+    (transformer.py:17-19); bool masks add 1.0 where True.  Returns ``(mode, key_padding)``:
+      * None, or a bias constant along each score row (e.g. the [B,1,1,S] padding mask, which
+        becomes [B,1,S,1]): softmax is shift-invariant -> "none";
+      * +1.0 exactly on strictly-past keys (the look-ahead mask of
+        pytorch_machine_translator.py:102-104 after the permute) -> "reference";
+      * large negative (<= -1e4 or -inf) on future keys and row-constant elsewhere -> "causal";
+      * large negative on a per-(batch, key) set, row-constant elsewhere -> key padding [B, Sk]
+        (optionally with the causal pattern);
+    anything else raises ValueError: there is no general additive-bias attention kernel.
+    Device masks are read once per distinct tensor version (cached)."""
+    if mask is None:
+        return "none", None
+    if not torch.is_tensor(mask) or mask.dim() != 4:
+        raise ValueError("attention masks must be 4-D tensors added to the scores after permute(0, 1, 3, 2) "
+                         f"(transformer.py:17-19); got {type(mask).__name__} "
+                         f"{tuple(mask.shape) if torch.is_tensor(mask) else ''}")
+    B, H, Kd, Qd = mask.shape  # after the permute: [B, H, Qd, Kd]
+    if Qd not in (1, Sq) or Kd not in (1, Sk):
+        raise ValueError(f"mask of shape {tuple(mask.shape)} does not broadcast over scores [.., {Sq}, {Sk}]")
+    if Kd == 1:  # constant along every score row: a softmax no-op, decided from the shape alone
+        return "none", None
+    key = (mask.data_ptr(), mask._version, tuple(mask.shape), mask.dtype, str(mask.device), Sq, Sk)
+    hit = _mask_cache.get(key)
+    if hit is not None:
+        return hit
+    b = mask.detach().to("cpu", torch.float64).permute(0, 1, 3, 2)
+    if H > 1 and not torch.equal(b, b[:, :1].expand_as(b)):
+        raise ValueError("per-head attention masks are not supported by the fused kernels")
+    b = b[:, 0].expand(B, Sq, Sk)
+    q = torch.arange(Sq).view(Sq, 1)
+    k = torch.arange(Sk).view(1, Sk)
+    past = (k < q).to(torch.float64)
+    neg = b <= _NEG
+
+    def row_const(t, where):
+        t = torch.where(where, t, t.new_full((), float("nan")))
+        hi = torch.nan_to_num(t, nan=-float("inf")).amax(-1)
+        lo = torch.nan_to_num(t, nan=float("inf")).amin(-1)
+        return bool(((hi == lo) | torch.isinf(hi)).all())
+
+    out = None
+    every = torch.ones_like(neg)
+    if not neg.any():
+        if row_const(b, every):
+            out = ("none", None)
+        elif row_const(b - past, every):
+            out = ("reference", None)
+    elif row_const(b, ~neg):
+        future = (k > q).expand(B, Sq, Sk)
+        kp = neg.all(1)  # keys masked for every query row: key padding [B, Sk]
+        rest = neg & ~kp[:, None, :]
+        kpo = kp if bool(kp.any()) else None
+        if not rest.any():
+            out = ("none", kpo)
+        elif torch.equal(rest, future & ~kp[:, None, :]):
+            out = ("causal", kpo)
+    if out is None:
+        raise ValueError("unsupported attention mask: the fused kernels implement no-op (row-constant), the "
+                         "reference look-ahead (+1 on past keys), causal and key-padding masks")
+    if len(_mask_cache) > 64:
+        _mask_cache.clear()
+    _mask_cache[key] = out
+    return out

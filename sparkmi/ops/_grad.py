@@ -117,6 +117,26 @@ def needs_input_grad(ctx, i):
 
 
 
+class SharedGrad:
+    """Gradient buffer of a tensor whose consumers write their slices of dX in place (and return
+    None to autograd): the producer's backward then reads the whole gradient at once, e.g. one
+    dgrad GEMM over the six decoder kv projections (ops.linear.concat_linear)."""
+
+    __slots__ = ("buf",)
+
+    def __init__(self):
+        self.buf = None
+
+    def get(self, like: torch.Tensor) -> torch.Tensor:
+        if self.buf is None:
+            self.buf = torch.empty_like(like)
+        return self.buf
+
+    def take(self):
+        b, self.buf = self.buf, None
+        return b
+
+
 class ResidualGrad:
     """Routes a residual branch's gradient into the dgrad GEMM of the sibling consumer.
 

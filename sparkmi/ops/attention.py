@@ -78,10 +78,13 @@ class _AttnCore(torch.autograd.Function):
     """Shared autograd core.  ``views`` describe (base tensor, offset, (sb, ss, sh)) for q/k/v."""
 
     @staticmethod
-    def forward(ctx, qsrc, kvsrc, H, mode, key_padding, cross):
+    def forward(ctx, qsrc, kvsrc, H, mode, key_padding, cross, kv_col=0, shared=None):
         ctx.H, ctx.mode, ctx.cross = H, mode, cross
         ctx.native = _native.use_native(qsrc)
+        ctx.kv_col, ctx.shared = kv_col, shared
         if not ctx.native:
+            if shared is not None or kv_col:
+                raise ValueError("column-sliced kv with a shared gradient is a GPU-kernel path")
             if cross:
                 qh, kh, vh = _split_cross(qsrc, kvsrc, H)
             else:
@@ -102,9 +105,11 @@ class _AttnCore(torch.autograd.Function):
             if kvsrc.dtype != qsrc.dtype:
                 raise TypeError(f"cross attention: q dtype {qsrc.dtype} != kv dtype {kvsrc.dtype}")
             hd = qsrc.shape[2] // H
-            Sk = kvsrc.shape[1]
+            Sk, W = kvsrc.shape[1], kvsrc.shape[2]  # W: 2*H*hd, or the width of a concatenated kv
+            if kv_col < 0 or kv_col + 2 * H * hd > W:
+                raise ValueError(f"cross attention: kv columns [{kv_col}, {kv_col + 2 * H * hd}) outside width {W}")
             qp, qs = qsrc.data_ptr(), (Sq * H * hd, H * hd, hd)
-            kp, ks = kvsrc.data_ptr(), (Sk * 2 * H * hd, 2 * H * hd, 2 * hd)
+            kp, ks = kvsrc.data_ptr() + kv_col * es, (Sk * W, W, 2 * hd)
             vp, vs = kp + hd * es, ks
         else:
             hd = qsrc.shape[2] // (3 * H)
@@ -136,9 +141,9 @@ class _AttnCore(torch.autograd.Function):
             if ctx.cross:
                 dqs = _merge(dq)
                 dkv = torch.cat([dk, dv], dim=-1).permute(0, 2, 1, 3).reshape(B, kh.shape[2], -1)
-                return dqs.to(do.dtype), dkv.to(do.dtype), None, None, None, None
+                return dqs.to(do.dtype), dkv.to(do.dtype), None, None, None, None, None, None
             dqkv = torch.cat([dq, dk, dv], dim=-1).permute(0, 2, 1, 3).reshape(B, S, -1)
-            return dqkv.to(do.dtype), None, None, None, None, None
+            return dqkv.to(do.dtype), None, None, None, None, None, None, None
         C = _native.C()
         qsrc, kvsrc, o, lse = ctx.saved_tensors
         B, Sq, Sk, hd, qs, ks, vs, os_ = ctx.geom
@@ -150,10 +155,10 @@ class _AttnCore(torch.autograd.Function):
         delta = torch.empty(B, H, Sq, device=do.device, dtype=torch.float32)
         if ctx.cross:
             dq = torch.empty_like(qsrc)
-            dkv = torch.empty_like(kvsrc)
-            qp, kp = qsrc.data_ptr(), kvsrc.data_ptr()
+            dkv = ctx.shared.get(kvsrc) if ctx.shared is not None else torch.empty_like(kvsrc)
+            qp, kp = qsrc.data_ptr(), kvsrc.data_ptr() + ctx.kv_col * es
             vp = kp + hd * es
-            dqp, dkp = dq.data_ptr(), dkv.data_ptr()
+            dqp, dkp = dq.data_ptr(), dkv.data_ptr() + ctx.kv_col * es
             dvp = dkp + hd * es
         else:
             dqkv = torch.empty_like(qsrc)
@@ -166,16 +171,20 @@ class _AttnCore(torch.autograd.Function):
             dkp, dvp, _native.ptr(ctx.kpad), B, H, Sq, Sk, ctx.mode, _LOG2E / math.sqrt(hd),
             1.0 / math.sqrt(hd), _native.stream())
         if ctx.cross:
-            return dq, dkv, None, None, None, None
-        return dqkv, None, None, None, None, None
+            # a shared kv gradient is read by its producer (ops.linear.ConcatLinearFn)
+            return dq, (None if ctx.shared is not None else dkv), None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None
 
 
 def self_attention(qkv, num_heads, mode="none", key_padding=None):
     """qkv [B,S,H*3*hd] (per-head interleaved) -> [B,S,H*hd]."""
     return _AttnCore.apply(qkv, None, num_heads, MODES[mode] if not isinstance(mode, int) else mode, key_padding,
-                           False)
+                           False, 0, None)
 
 
-def cross_attention(q, kv, num_heads, mode="none", key_padding=None):
-    """q [B,Sq,H*hd], kv [B,Sk,H*2*hd] (per-head [k|v]) -> [B,Sq,H*hd]."""
-    return _AttnCore.apply(q, kv, num_heads, MODES[mode] if not isinstance(mode, int) else mode, key_padding, True)
+def cross_attention(q, kv, num_heads, mode="none", key_padding=None, kv_col=0, shared=None):
+    """q [B,Sq,H*hd], kv [B,Sk,H*2*hd] (per-head [k|v]) -> [B,Sq,H*hd].  GPU: ``kv`` may be a wider
+    concatenated projection [B,Sk,W] read from column ``kv_col``; with ``shared`` (a SharedGrad)
+    the kv gradient is written into ``shared``'s buffer at the same columns."""
+    return _AttnCore.apply(q, kv, num_heads, MODES[mode] if not isinstance(mode, int) else mode, key_padding, True,
+                           int(kv_col), shared)

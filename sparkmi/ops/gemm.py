@@ -5,7 +5,9 @@ Three entry points, one per GEMM of a linear layer, each with its fused epilogue
   dgrad(dy, w)     -> dx = (dy @ w) [+ resid] [* relu'/dropout mask]  bf16 out
   wgrad(dy, x, gw) -> gw += dy^T @ x                                  fp32 accumulate (split-K)
 ``supported(...)`` says whether a shape can run on the kernel (K multiple of 64, dims multiple
-of 8, 16-B aligned rows); callers fall back to hipBLASLt otherwise.
+of 8, 16-B aligned rows); other shapes run on the fp32 kernel (csrc/kernels/gemm_f32.hip, K % 4)
+with upcast operands.  Every GEMM of the training step is one of these two hand-written kernels
+(no vendor-library dispatch).
 """
 import os
 
@@ -13,40 +15,6 @@ import torch
 
 from .. import _native
 from . import _grad
-
-# Per-shape implementation choice between sparkmi's MFMA kernel (with its fused epilogue) and
-# hipBLASLt (+ a separate HIP epilogue kernel), measured once per (op, shape, epilogue) on the
-# live device with HIP events and cached; never measured during graph capture.
-_POLICY = os.environ.get("SPARKMI_GEMM_POLICY", "auto")  # auto | smi | blaslt
-_choices = {}
-
-
-def choose(key, run_smi, run_blaslt, iters=5):
-    """Return 'smi' or 'blaslt' for this call site/shape (autotuned once)."""
-    if _POLICY in ("smi", "blaslt"):
-        return _POLICY
-    c = _choices.get(key)
-    if c is not None:
-        return c
-    if torch.cuda.is_current_stream_capturing():
-        return "smi"
-    times = {}
-    for name, fn in (("smi", run_smi), ("blaslt", run_blaslt)):
-        fn()
-        start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        start.record()
-        for _ in range(iters):
-            fn()
-        end.record()
-        end.synchronize()
-        times[name] = start.elapsed_time(end) / iters
-    c = min(times, key=times.get)
-    _choices[key] = c
-    return c
-
-
-def choices():
-    return dict(_choices)
 
 _DISABLE = os.environ.get("SPARKMI_GEMM", "1") == "0"
 NUM_CU = 256

@@ -10,7 +10,8 @@ GPU paths, chosen by the activation dtype:
   * fp32 (reference precision): csrc/kernels/gemm_f32.hip on the fp32-input matrix cores
     (v_mfma_f32_32x32x2_f32), fp32 master weights used directly, the same fused epilogues;
   * bf16 (bf16 weight shadow, fp32 master/grad): csrc/kernels/gemm.hip (16x16x32 bf16 MFMA)
-    whenever the shape fits (K % 64 == 0, rows 16-B aligned), hipBLASLt through torch otherwise.
+    whenever the shape fits (K % 64 == 0, rows 16-B aligned), the fp32 kernel on upcast
+    operands otherwise (no vendor-library GEMM anywhere).
   * forward: ONE kernel = GEMM + bias + ReLU + dropout epilogue (counter-based mask, nothing
     saved but the output);
   * backward: dgrad GEMM (bf16 out), wgrad GEMM accumulating fp32 straight into the flat
@@ -30,18 +31,65 @@ from ._grad import bf16_weight, grad_buf, grad_ready
 ACTS = {None: 0, "none": 0, "relu": 1, "sigmoid": 2}
 
 
-def _blaslt_wgrad(gw, dy2, x2):
-    try:
-        torch.addmm(gw, dy2.t(), x2, out_dtype=torch.float32, out=gw)
-    except (TypeError, RuntimeError):
-        gw.add_(torch.mm(dy2.t(), x2).float())
-
-
 _GROUP_LIMIT = 1 << 31  # descriptor / 32-bit offset range of the grouped wgrad launches
 
 
 def _groupable(*ts):
     return all(t.numel() * t.element_size() < _GROUP_LIMIT for t in ts)
+
+
+def _r4(n):
+    return (n + 3) // 4 * 4
+
+
+def _pad2(t, rows, cols):
+    """Zero-padded copy of a 2-D tensor (or the tensor itself when already that shape)."""
+    if t is None or tuple(t.shape) == (rows, cols):
+        return t
+    out = t.new_zeros(rows, cols)
+    out[:t.shape[0], :t.shape[1]] = t
+    return out
+
+
+def _fwd32_any(x2, w, bias, act, rng, salt, p):
+    """fp32 forward for any shape: the kernel needs K % 4 (float4 k-loads); a ragged K is
+    zero-padded (zeros add nothing).  Ragged N is handled by the kernel's scalar epilogue."""
+    M, K = x2.shape
+    N = w.shape[0]
+    if not G.supported32(M, N, K, x2, w, mode=0):
+        x2, w = _pad2(x2.contiguous(), M, _r4(K)), _pad2(w.contiguous(), N, _r4(K))
+    return G.fwd32(x2, w, bias, act, rng, salt, _rng.threshold(p), _rng.scale(p))
+
+
+def _dgrad32_any(g2, w, resid=None, dact_y=None, dscale=1.0):
+    """fp32 dgrad for any shape: the reduction dim N (dy's columns, W's rows) and the output
+    dim K need multiples of 4 for the kernel's float4 loads; ragged ones are zero-padded."""
+    M, N = g2.shape
+    K = w.shape[1]
+    if G.supported32(M, K, N, g2, w, resid, dact_y, mode=1):
+        return G.dgrad32(g2, w, resid=resid, dact_y=dact_y, dscale=dscale)
+    N4, K4 = _r4(N), _r4(K)
+    dx = G.dgrad32(_pad2(g2.contiguous(), M, N4), _pad2(w.contiguous(), N4, K4),
+                   resid=_pad2(resid.contiguous(), M, K4) if resid is not None else None,
+                   dact_y=_pad2(dact_y.contiguous(), M, K4) if dact_y is not None else None, dscale=dscale)
+    return dx[:, :K] if K4 != K else dx
+
+
+def _wgrad32_any(gw, dy2, x2, gb=None):
+    """gw[N,K] (+)= dy^T x, gb += colsum(dy), fp32, any shape (ragged dims zero-padded into a
+    temporary that is then added)."""
+    N, K = gw.shape
+    M = dy2.shape[0]
+    if G.supported32(N, K, M, dy2, x2, mode=2) and gw.is_contiguous():
+        G.wgrad32(dy2, x2, gw, gb=gb)
+        return
+    M4, N4, K4 = _r4(M), _r4(N), _r4(K)
+    t = torch.zeros(N4, K4, device=gw.device, dtype=torch.float32)
+    tb = torch.zeros(N4, device=gw.device, dtype=torch.float32) if gb is not None else None
+    G.wgrad32(_pad2(dy2.contiguous(), M4, N4), _pad2(x2.contiguous(), M4, K4), t, gb=tb)
+    gw.add_(t[:N, :K])
+    if gb is not None:
+        gb.add_(tb[:N])
 
 
 def _wgrad_accumulate(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, gb=None, ready=None):
@@ -52,12 +100,11 @@ def _wgrad_accumulate(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, gb=
     N, K = gw.shape
     M = dy2.shape[0]
     if dy2.dtype == torch.float32:
-        if not G.supported32(N, K, M, dy2, x2, mode=2) or not gw.is_contiguous():
-            raise RuntimeError(f"fp32 wgrad: unsupported shape/layout N={N} K={K} M={M}")
-        if ready is not None and _grad.WGRAD_GROUP and _groupable(dy2, x2) and (gb is None or gb.is_contiguous()):
+        if (ready is not None and _grad.WGRAD_GROUP and G.supported32(N, K, M, dy2, x2, mode=2)
+                and gw.is_contiguous() and _groupable(dy2, x2) and (gb is None or gb.is_contiguous())):
             _grad.defer_wgrad_group(dy2, x2, gw, gb, ready, _native.stream())
             return True
-        G.wgrad32(dy2, x2, gw, gb=gb)
+        _wgrad32_any(gw, dy2, x2, gb)
         return False
     if (ready is not None and _grad.WGRAD_GROUP and G.supported(N, K, M, dy2, x2, mode=2) and gw.is_contiguous()
             and (gb is None or gb.is_contiguous()) and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
@@ -65,66 +112,21 @@ def _wgrad_accumulate(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, gb=
         _grad.defer_wgrad_group(dy2, x2, gw, gb, ready, _native.stream())
         return True
     if G.supported(N, K, M, dy2, x2, mode=2) and gw.is_contiguous():
-        key = ("wgrad", N, K, M, gb is not None)
-        if key not in G._choices and not torch.cuda.is_current_stream_capturing():
-            scratch = torch.zeros_like(gw)  # the timing runs must not touch the real gradients
-            bscr = torch.zeros_like(gb) if gb is not None else None
-
-            def run_blaslt():
-                _blaslt_wgrad(scratch, dy2, x2)
-                if bscr is not None:
-                    _colsum(dy2, bscr)
-            G.choose(key, lambda: G.wgrad(dy2, x2, scratch, gb=bscr), run_blaslt)
-        if G.choose(key, None, None) == "smi":
-            return G.wgrad(dy2, x2, gw, gb=gb, ready=ready) is True
-    _blaslt_wgrad(gw, dy2, x2)
-    if gb is not None:
-        _colsum(dy2, gb)
+        return G.wgrad(dy2, x2, gw, gb=gb, ready=ready) is True
+    # shapes outside the bf16 kernel's tiling: the fp32 kernel on upcast operands
+    _wgrad32_any(gw, dy2.float(), x2.float(), gb)
     return False
-
-
-def _blaslt_dgrad(g2, w_bf, resid, dact_y, dscale):
-    dx = torch.mm(g2, w_bf)
-    if resid is not None:
-        dx = dx + resid
-    if dact_y is not None:
-        C = _native.C()
-        C.act_drop_bwd(dx.data_ptr(), dact_y.data_ptr(), dx.data_ptr(), dx.numel(), 1, 0, 0,
-                       1 if dscale != 1.0 else 0, dscale, _native.stream())
-    return dx
 
 
 def _dgrad(g2, w_bf, resid=None, dact_y=None, dscale=1.0):
     M, N = g2.shape
     K = w_bf.shape[1]
     if g2.dtype == torch.float32:
-        if not G.supported32(M, K, N, g2, w_bf, resid, dact_y, mode=1):
-            raise RuntimeError(f"fp32 dgrad: unsupported shape/layout M={M} K={K} N={N}")
-        return G.dgrad32(g2, w_bf, resid=resid, dact_y=dact_y, dscale=dscale)
+        return _dgrad32_any(g2, w_bf, resid, dact_y, dscale)
     if G.supported(M, K, N, g2, w_bf, resid, dact_y, mode=1):
-        key = ("dgrad", M, K, N, resid is not None, dact_y is not None)
-        c = G.choose(key, lambda: G.dgrad(g2, w_bf, resid=resid, dact_y=dact_y, dscale=dscale),
-                     lambda: _blaslt_dgrad(g2, w_bf, resid, dact_y, dscale))
-        if c == "smi":
-            return G.dgrad(g2, w_bf, resid=resid, dact_y=dact_y, dscale=dscale)
-    return _blaslt_dgrad(g2, w_bf, resid, dact_y, dscale)
-
-
-def _colsum(dy2: torch.Tensor, out: torch.Tensor):
-    """out (fp32 [N]) += column sums of dy2 (bf16 [M,N]); one HIP launch, fp32 atomics per block."""
-    M, N = dy2.shape
-    col_blocks = (N + 255) // 256
-    rpb = max(64, min(1024, (M // 32 + 7) // 8 * 8))  # <= 32 adders per column (atomic contention)
-    _native.C().colsum_bf16(dy2.data_ptr(), M, N, 0, rpb, out.data_ptr(), 1, _native.stream())
-
-
-def _blaslt_fwd(x2, weight, w, bias, act, p, rng, salt):
-    N = weight.shape[0]
-    y2 = torch.addmm(bf16_weight(bias), x2, w.t()) if bias is not None else torch.mm(x2, w.t())
-    if act or p > 0:
-        _native.C().bias_act_drop_fwd(y2.data_ptr(), 0, y2.data_ptr(), y2.numel(), N, act, rng.ptr(), salt,
-                                      _rng.threshold(p), _rng.scale(p), _native.stream())
-    return y2
+        return G.dgrad(g2, w_bf, resid=resid, dact_y=dact_y, dscale=dscale)
+    f32 = [t.float() if t is not None else None for t in (g2, w_bf, resid, dact_y)]
+    return _dgrad32_any(*f32[:2], f32[2], f32[3], dscale).to(g2.dtype)
 
 
 def compute_weight(p: torch.Tensor, dtype) -> torch.Tensor:
@@ -132,22 +134,16 @@ def compute_weight(p: torch.Tensor, dtype) -> torch.Tensor:
     return p.detach() if dtype == torch.float32 else bf16_weight(p)
 
 
-def _fwd_native(x2, weight, bias, act, p, rng, salt):
+def _fwd_native(x2, weight, bias, act, p, rng, salt, w_bf=None):
     N, K = weight.shape
     M = x2.shape[0]
     if x2.dtype == torch.float32:
-        w = weight.detach()
-        if not G.supported32(M, N, K, x2, w, mode=0):
-            raise RuntimeError(f"fp32 linear: unsupported shape/layout M={M} N={N} K={K}")
-        return G.fwd32(x2, w, bias, act, rng, salt, _rng.threshold(p), _rng.scale(p))
-    w = bf16_weight(weight)
+        return _fwd32_any(x2, weight.detach(), bias, act, rng, salt, p)
+    w = w_bf if w_bf is not None else bf16_weight(weight)
     if G.supported(M, N, K, x2, w, mode=0) and act in (0, 1):
-        key = ("fwd", M, N, K, bias is not None, act, p > 0)
-        c = G.choose(key, lambda: G.fwd(x2, w, bias, act, rng, salt, _rng.threshold(p), _rng.scale(p)),
-                     lambda: _blaslt_fwd(x2, weight, w, bias, act, p, rng, salt))
-        if c == "smi":
-            return G.fwd(x2, w, bias, act, rng, salt, _rng.threshold(p), _rng.scale(p))
-    return _blaslt_fwd(x2, weight, w, bias, act, p, rng, salt)
+        return G.fwd(x2, w, bias, act, rng, salt, _rng.threshold(p), _rng.scale(p))
+    # shapes outside the bf16 kernel's tiling (or sigmoid): the fp32 kernel on upcast operands
+    return _fwd32_any(x2.float(), weight.detach(), bias, act, rng, salt, p).to(x2.dtype)
 
 
 def _ref_fwd(x2, weight, bias, act, p, seed, salt):
@@ -317,6 +313,62 @@ class FFNFn(torch.autograd.Function):
         if dx is not None:
             dx = dx.reshape(dy.shape)
         return dx, None, None, None, None, None, None, None, None
+
+
+class ConcatLinearFn(torch.autograd.Function):
+    """y = x @ W^T + b over linears stored back to back in the flat buffer (FlatParams.concat):
+    one GEMM in place of several on the same input.  The consumers read column slices of y and
+    write their gradients into ``shared`` (a SharedGrad) instead of returning them, so the
+    backward is ONE dgrad GEMM with K = the summed widths (the sum over consumers happens in the
+    MFMA accumulators, no elementwise adds) and ONE weight-gradient GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, wviews, bviews, shape, params, shared):
+        ctx.set_materialize_grads(False)
+        N, K = shape
+        wm, wg, ws = wviews
+        bm, bg = bviews[0], bviews[1]
+        x2 = x.reshape(-1, K).contiguous()
+        w = wm.view(N, K)
+        y2 = _fwd_native(x2, w, bm, 0, 0.0, None, 0, w_bf=ws.view(N, K) if ws is not None else None)
+        ctx.wviews, ctx.bg, ctx.shape, ctx.params, ctx.shared = wviews, bg, shape, params, shared
+        ctx.save_for_backward(x2)
+        return y2.reshape(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, _unused):
+        (x2,) = ctx.saved_tensors
+        N, K = ctx.shape
+        wm, wg, ws = ctx.wviews
+        g = ctx.shared.take()
+        if g is None:  # no consumer produced a gradient
+            grad_ready(*ctx.params)
+            return None, None, None, None, None, None
+        g2 = g.reshape(-1, N)
+        w = wm.view(N, K) if g2.dtype == torch.float32 else ws.view(N, K)
+        dx = _dgrad(g2, w) if ctx.needs_input_grad[0] else None
+        with _grad.side(g2.device, g2, x2):
+            if not _wgrad_accumulate(wg.view(N, K), g2, x2, ctx.bg, ready=ctx.params):
+                grad_ready(*ctx.params)
+        if dx is not None:
+            dx = dx.reshape(*g.shape[:-1], K)
+        return dx, None, None, None, None, None
+
+
+def concat_linear(x, flat, linears, shared):
+    """One GEMM for several nn.Linear on the same input whose weights (and biases) FlatParams
+    stored back to back; returns y [.., sum N_i] or None when the layout does not allow it.
+    Consumers must route their gradient through ``shared`` (see ConcatLinearFn)."""
+    ws = [l.weight for l in linears]
+    bs = [l.bias for l in linears]
+    if any(b is None for b in bs) or len({tuple(w.shape[1:]) for w in ws}) != 1:
+        return None
+    wv, bv = flat.concat(ws), flat.concat(bs)
+    if wv is None or bv is None or (x.dtype == torch.bfloat16 and wv[2] is None):
+        return None
+    N, K = sum(w.shape[0] for w in ws), ws[0].shape[1]
+    params = tuple(p for pair in zip(ws, bs) for p in pair)
+    return ConcatLinearFn.apply(x, wv, bv, (N, K), params, shared)
 
 
 def ffn(x, linear1, linear2, p=0.0, rng=None, salt=0, x_slot=None):

@@ -68,7 +68,11 @@ class DropoutRNG(torch.nn.Module):
         self.register_buffer("seed", torch.tensor([int(seed) & 0x7FFFFFFF], dtype=torch.int32), persistent=False)
 
     def advance(self):
-        self.seed.add_(1)
+        from .. import _native
+        if _native.use_native(self.seed):
+            _native.C().seed_inc(self.seed.data_ptr(), _native.stream())
+        else:
+            self.seed.add_(1)
 
     def current(self) -> int:
         return int(self.seed.item())

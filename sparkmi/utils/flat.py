@@ -10,6 +10,11 @@ compute shadow is kept in a third buffer (``p._smi_bf16``).  Consequences on MI3
   * parameters are laid out in REVERSE registration order, so the backward pass finishes the
     front of the buffer first and bucket 0 can be all-reduced while backward continues.
 Each parameter starts on a 64-element boundary (256-B aligned fp32, 128-B aligned bf16).
+
+A module may list parameter groups to be stored back to back (``_smi_flat_groups()``): e.g. the
+six decoder kv projections, which all read the encoder output, then form ONE [6*2D, D] weight
+view and run as one GEMM (``concat``).  A group sits where its first-registered member would
+(its gradients complete together, at the end of the decoder backward).
 """
 import torch
 
@@ -32,6 +37,7 @@ class FlatParams:
                 params.append((name, p))
         if reverse:
             params = params[::-1]
+        params = self._place_groups(module, params)
         device = torch.device(device) if device is not None else (params[0][1].device if params else torch.device("cpu"))
         self.device = device
         self.names = [n for n, _ in params]
@@ -57,6 +63,38 @@ class FlatParams:
         self.index = {id(p): i for i, p in enumerate(self.params)}
         object.__setattr__(module, "_smi_flat", self)  # checkpoint loads refresh the bf16 shadow
         self.refresh_shadow()
+
+    @staticmethod
+    def _place_groups(module, params):
+        fn = getattr(module, "_smi_flat_groups", None)
+        if fn is None:
+            return params
+        for group in fn():
+            ids = [id(p) for p in group]
+            pos = {id(p): i for i, (_, p) in enumerate(params)}
+            if len(group) < 2 or any(i not in pos for i in ids) or len(set(ids)) != len(ids):
+                continue
+            if any(p.numel() % ALIGN for p in group[:-1]):  # padding would break the concat view
+                continue
+            members = {i: params[pos[i]] for i in ids}
+            anchor = max(pos[i] for i in ids)
+            before = [e for e in params[:anchor + 1] if id(e[1]) not in members]
+            after = [e for e in params[anchor + 1:] if id(e[1]) not in members]
+            params = before + [members[i] for i in ids] + after
+        return params
+
+    def concat(self, params):
+        """(master, grad, shadow) views spanning ``params`` stored back to back in this order, as
+        flat 1-D tensors; None when they are not contiguous here."""
+        if not params or any(id(p) not in self.index for p in params):
+            return None
+        o0, _ = self.param_range(params[0])
+        o = o0
+        for p in params:
+            if self.param_range(p)[0] != o:
+                return None
+            o += p.numel()
+        return (self.master[o0:o], self.grad[o0:o], self.shadow[o0:o] if self.shadow is not None else None)
 
     def refresh_shadow(self):
         if self.shadow is None:

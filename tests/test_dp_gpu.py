@@ -47,7 +47,7 @@ def _train(graph, steps, split=False):
 
 @pytest.mark.gpu
 def test_graph_dp_matches_eager_dp():
-    env = {"SPARKMI_DIST_BACKEND": "gloo", "SPARKMI_GEMM_POLICY": "smi"}  # same kernels in both runs
+    env = {"SPARKMI_DIST_BACKEND": "gloo"}
     pg, sg, _ = launch(_train, (True, 6), {}, num_processes=2, use_gpu=True, env=env, log_sink=None, timeout=300)
     pe, se, _ = launch(_train, (False, 6), {}, num_processes=2, use_gpu=True, env=env, log_sink=None, timeout=300)
     assert sg and se
@@ -58,7 +58,7 @@ def test_graph_dp_matches_eager_dp():
 def test_split_graph_dp_matches_eager_dp():
     """Three-graph step (decoder backward, upper-encoder backward, lower-encoder backward, with
     each piece's final buckets all-reduced while the next runs) == eager DP."""
-    env = {"SPARKMI_DIST_BACKEND": "gloo", "SPARKMI_GEMM_POLICY": "smi"}
+    env = {"SPARKMI_DIST_BACKEND": "gloo"}
     ps, ss, info = launch(_train, (True, 6, True), {}, num_processes=2, use_gpu=True, env=env, log_sink=None,
                           timeout=300)
     pe, se, _ = launch(_train, (False, 6), {}, num_processes=2, use_gpu=True, env=env, log_sink=None, timeout=300)

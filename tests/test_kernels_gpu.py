@@ -245,7 +245,8 @@ def test_transformer_gpu_vs_cpu():
     m.load_state_dict(sd)
     m = m.to(dev).eval()
     FlatParams(m)
-    la = torch.ones(1, dtype=torch.bool)
+    from sparkmi.models.transformer import create_look_ahead_mask
+    la = create_look_ahead_mask(gold["tgt"].shape[1])
     logits = m(gold["src"].to(dev), gold["tgt"].to(dev), None, la, la)
     _close(logits, gold["logits"], 0.15, 0.05, "logits")
     loss = m.loss(logits, gold["tgt"].to(dev))

@@ -8,10 +8,14 @@
 * ``sparkmi/_comm*.so``     — native communication layer: RCCL communicator + xGMI IPC one-shot
                               all-reduce (csrc/comm/*.hip, *.cpp), hipcc, linked against librccl.
 
-Incremental: an object is rebuilt when its source or any header under csrc/include changes.
+Incremental by CONTENT, not mtime: every object carries a stamp (sha256 of its compile command,
+its source and every header under csrc/include) and every library a stamp of its link command
+and its objects' stamps; anything whose stamp differs is rebuilt.  Copied trees whose mtimes
+say "up to date" while the sources changed (or the reverse) therefore build correctly.
 Usage: python tools/build_native.py [--force] [--jobs N] [--asan-runtime]
 """
 import argparse
+import hashlib
 import os
 import subprocess
 import sys
@@ -43,20 +47,44 @@ def _pybind_includes():
     return [pybind11.get_include(), sysconfig.get_paths()["include"]]
 
 
-def _headers_mtime():
-    t = 0.0
-    for d in ("include",):
-        p = os.path.join(CSRC, d)
-        for f in os.listdir(p):
-            t = max(t, os.path.getmtime(os.path.join(p, f)))
-    return t
+def _headers_digest():
+    h = hashlib.sha256()
+    p = os.path.join(CSRC, "include")
+    for f in sorted(os.listdir(p)):
+        h.update(f.encode())
+        with open(os.path.join(p, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
 
 
-def _needs(src, obj, hdr_t, force):
-    if force or not os.path.exists(obj):
-        return True
-    ot = os.path.getmtime(obj)
-    return os.path.getmtime(src) > ot or hdr_t > ot
+def _stamp_path(target):
+    return os.path.join(OBJ, os.path.basename(target) + ".sha256")
+
+
+def _read_stamp(target):
+    try:
+        with open(_stamp_path(target)) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def _write_stamp(target, digest):
+    with open(_stamp_path(target), "w") as f:
+        f.write(digest + "\n")
+
+
+def _obj_digest(src, cmd, hdr):
+    h = hashlib.sha256()
+    h.update("\0".join(cmd).encode())
+    h.update(hdr.encode())
+    with open(src, "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()
+
+
+def _needs(target, digest, force):
+    return force or not os.path.exists(target) or _read_stamp(target) != digest
 
 
 def _run(cmd):
@@ -68,73 +96,74 @@ def _run(cmd):
 
 def build(force=False, jobs=8, verbose=True):
     os.makedirs(OBJ, exist_ok=True)
-    hdr_t = _headers_mtime()
+    hdr = _headers_digest()
     inc = ["-I" + os.path.join(CSRC, "include")]
     py_inc = ["-I" + p for p in _pybind_includes()]
+    jobs_list = []  # (cmd, object, digest)
+
+    def obj(src, o, cmd):
+        d = _obj_digest(src, cmd, hdr)
+        if _needs(o, d, force):
+            jobs_list.append((cmd, o, d))
+        return o, d
+
     kern_dir = os.path.join(CSRC, "kernels")
-    hip_srcs = sorted(os.path.join(kern_dir, f) for f in os.listdir(kern_dir) if f.endswith(".hip"))
-    jobs_list = []
     objs = []
-    for s in hip_srcs:
+    for s in sorted(os.path.join(kern_dir, f) for f in os.listdir(kern_dir) if f.endswith(".hip")):
         o = os.path.join(OBJ, os.path.basename(s) + ".o")
-        objs.append(o)
-        if _needs(s, o, hdr_t, force):
-            extra = KERNEL_FLAGS.get(os.path.basename(s), [])
-            jobs_list.append([HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-c", s, "-o", o,
-                              "-munsafe-fp-atomics"] + extra + inc)
+        extra = KERNEL_FLAGS.get(os.path.basename(s), [])
+        objs.append(obj(s, o, [HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-c", s, "-o", o,
+                               "-munsafe-fp-atomics"] + extra + inc))
     bind_src = os.path.join(CSRC, "bindings.cpp")
     bind_obj = os.path.join(OBJ, "bindings.o")
-    objs.append(bind_obj)
-    if _needs(bind_src, bind_obj, hdr_t, force):
-        jobs_list.append(["g++", "-O2", "-std=c++17", "-fPIC", "-c", bind_src, "-o", bind_obj,
-                          "-fvisibility=hidden", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"] + inc + py_inc)
+    objs.append(obj(bind_src, bind_obj, ["g++", "-O2", "-std=c++17", "-fPIC", "-c", bind_src, "-o", bind_obj,
+                                         "-fvisibility=hidden", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"] +
+                    inc + py_inc))
     rt_dir = os.path.join(CSRC, "runtime")
-    rt_srcs = sorted(os.path.join(rt_dir, f) for f in os.listdir(rt_dir) if f.endswith(".cpp"))
     rt_objs = []
-    for s in rt_srcs:
+    for s in sorted(os.path.join(rt_dir, f) for f in os.listdir(rt_dir) if f.endswith(".cpp")):
         o = os.path.join(OBJ, "rt_" + os.path.basename(s) + ".o")
-        rt_objs.append(o)
-        if _needs(s, o, hdr_t, force):
-            jobs_list.append(["g++", "-O3", "-std=c++17", "-fPIC", "-c", s, "-o", o, "-fvisibility=hidden",
-                              "-pthread"] + inc + py_inc)
+        rt_objs.append(obj(s, o, ["g++", "-O3", "-std=c++17", "-fPIC", "-c", s, "-o", o, "-fvisibility=hidden",
+                                  "-pthread"] + inc + py_inc))
     comm_dir = os.path.join(CSRC, "comm")
     comm_objs = []
     for f in sorted(os.listdir(comm_dir)):
         s = os.path.join(comm_dir, f)
         o = os.path.join(OBJ, "comm_" + f + ".o")
         if f.endswith(".hip"):
-            comm_objs.append(o)
-            if _needs(s, o, hdr_t, force):
-                jobs_list.append([HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-c", s, "-o", o] + inc)
+            comm_objs.append(obj(s, o, [HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-c", s, "-o",
+                                        o] + inc))
         elif f.endswith(".cpp"):
-            comm_objs.append(o)
-            if _needs(s, o, hdr_t, force):
-                jobs_list.append([HIPCC, "-O2", "-std=c++17", "-fPIC", "-c", s, "-o", o, "-fvisibility=hidden",
-                                  "-I/opt/rocm/include"] + inc + py_inc)
+            comm_objs.append(obj(s, o, [HIPCC, "-O2", "-std=c++17", "-fPIC", "-c", s, "-o", o, "-fvisibility=hidden",
+                                        "-I/opt/rocm/include"] + inc + py_inc))
     if jobs_list:
         with ThreadPoolExecutor(max_workers=jobs) as ex:
-            for cmd, _ in zip(jobs_list, ex.map(_run, jobs_list)):
+            for (cmd, o, d), _ in zip(jobs_list, ex.map(lambda j: _run(j[0]), jobs_list)):
+                _write_stamp(o, d)
                 if verbose:
                     print("[build]", os.path.basename(cmd[cmd.index("-c") + 1]), flush=True)
+
+    def link(so, objs_, cmd):
+        h = hashlib.sha256("\0".join(cmd).encode())
+        for _, d in objs_:
+            h.update(d.encode())
+        d = h.hexdigest()
+        if _needs(so, d, force):
+            _run(cmd)
+            _write_stamp(so, d)
+            if verbose:
+                print("[link]", os.path.relpath(so, ROOT), flush=True)
+
     suffix = _ext_suffix()
     c_so = os.path.join(PKG, "_C" + suffix)
-    if force or not os.path.exists(c_so) or any(os.path.getmtime(o) > os.path.getmtime(c_so) for o in objs):
-        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", c_so] + objs)
-        if verbose:
-            print("[link]", os.path.relpath(c_so, ROOT), flush=True)
+    link(c_so, objs, [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", c_so] + [o for o, _ in objs])
     comm_so = os.path.join(PKG, "_comm" + suffix)
-    if comm_objs and (force or not os.path.exists(comm_so) or
-                      any(os.path.getmtime(o) > os.path.getmtime(comm_so) for o in comm_objs)):
-        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", comm_so] + comm_objs +
-             ["-L/opt/rocm/lib", "-lrccl"])
-        if verbose:
-            print("[link]", os.path.relpath(comm_so, ROOT), flush=True)
+    if comm_objs:
+        link(comm_so, comm_objs, [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", comm_so] +
+             [o for o, _ in comm_objs] + ["-L/opt/rocm/lib", "-lrccl"])
     rt_so = os.path.join(PKG, "_runtime" + suffix)
-    if rt_objs and (force or not os.path.exists(rt_so) or
-                    any(os.path.getmtime(o) > os.path.getmtime(rt_so) for o in rt_objs)):
-        _run(["g++", "-shared", "-fPIC", "-pthread", "-o", rt_so] + rt_objs)
-        if verbose:
-            print("[link]", os.path.relpath(rt_so, ROOT), flush=True)
+    if rt_objs:
+        link(rt_so, rt_objs, ["g++", "-shared", "-fPIC", "-pthread", "-o", rt_so] + [o for o, _ in rt_objs])
     return c_so, rt_so
 
 
