@@ -240,7 +240,10 @@ def bench_mlp(args, rank, world, device):
     flat = FlatParams(model, shadow=False)
     opt = SGD(flat, lr=0.01)
     ddp = DataParallel(flat) if world > 1 else None
-    runner = StepRunner(model, lambda m, x, y: m.loss(x, y), opt, ddp, graph=device.type == "cuda" and args.graph != "off")
+    # one executor: the whole step (forward, CE, backward, SGD) is ONE kernel launch
+    fused = (lambda m, o, x, y: m.fused_sgd_step(o, x, y)) if world == 1 else None
+    runner = StepRunner(model, lambda m, x, y: m.loss(x, y), opt, ddp, graph=device.type == "cuda" and args.graph != "off",
+                        fused_step=fused)
     g = torch.Generator().manual_seed(31 + rank)
     batches = [(torch.rand(30, 4, generator=g).to(device) * 2 - 1, torch.randint(0, 3, (30,), generator=g).to(device))
                for _ in range(8)]

@@ -58,7 +58,12 @@ int smi_cast_f32_bf16(const float*, void*, long, hipStream_t);
 int smi_add_bf16(const void*, const void*, void*, long, hipStream_t);
 int smi_step_inc(float*, hipStream_t);
 int smi_seed_inc(int*, hipStream_t);
-int smi_mlp_fwd(const MLPArgs*, hipStream_t);
+int smi_lbfgs_direction(const float*, const float*, const float*, int*, int, long, const float*, float*, float*, int,
+                        hipStream_t);
+int smi_lbfgs_update(float*, float*, float*, int*, int, long, const float*, float, const float*, const float*, float*,
+                     float, hipStream_t);
+int smi_mlp(const MLPArgs*, int, hipStream_t);
+int smi_mlp_grid(int);
 int smi_gemm(const GemmArgs*, hipStream_t);
 int smi_gemm_f32(const GemmF32Args*, hipStream_t);
 int smi_gemm_f32_wgrad_group(const void* const*, const long*, const void* const*, const long*, void* const*, void* const*,
@@ -73,7 +78,6 @@ int smi_cnn(const CNNArgs*, hipStream_t);
 int smi_cnn_reduce(const CNNArgs*, hipStream_t);
 int smi_gather_rows(const void*, const long long*, void*, long, long, hipStream_t);
 int smi_gather_u8_scale(const void*, const long long*, void*, long, long, float, int, hipStream_t);
-int smi_mlp_bwd(const MLPArgs*, hipStream_t);
 int smi_lstm(const LSTMArgs*, int, hipStream_t);
 int smi_lstm_supported(int, int, int, int);
 int smi_adam(float*, float*, float*, float*, void*, long, const float*, float*, unsigned*, float, float, float, float, float,
@@ -231,6 +235,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("cast_f32_bf16", [](u x, u y, long n, u st) { chk(smi_cast_f32_bf16(PF(x), P(y), n, S(st)), "cast_f32_bf16"); });
   m.def("add_bf16", [](u a, u b, u y, long n, u st) { chk(smi_add_bf16(P(a), P(b), P(y), n, S(st)), "add_bf16"); });
   m.def("step_inc", [](u step, u st) { chk(smi_step_inc(PF(step), S(st)), "step_inc"); });
+  // device L-BFGS (csrc/kernels/lbfgs.hip): st = int32 {head, count}; out = fp32 {g.d, |g|_1, |g|_2^2, pairs}
+  m.def("lbfgs_direction", [](u Sm, u Ym, u rho, u st, int mm, long n, u g, u d, u out, int reset, u stream) {
+    chk(smi_lbfgs_direction(PF(Sm), PF(Ym), PF(rho), reinterpret_cast<int*>(st), mm, n, PF(g), PF(d), PF(out), reset,
+                            S(stream)), "lbfgs_direction");
+  });
+  m.def("lbfgs_update", [](u Sm, u Ym, u rho, u st, int mm, long n, u d, float t, u gn, u go, u x, float eps, u stream) {
+    chk(smi_lbfgs_update(PF(Sm), PF(Ym), PF(rho), reinterpret_cast<int*>(st), mm, n, PF(d), t, PF(gn), PF(go), PF(x),
+                         eps, S(stream)), "lbfgs_update");
+  });
   m.def("seed_inc", [](u seed, u st) { chk(smi_seed_inc(reinterpret_cast<int*>(seed), S(st)), "seed_inc"); });
   // step: device step counter (advanced by the kernel); done: zeroed uint32 ticket word
   m.def("adam", [](u p, u g, u mm, u v, u pbf, long n, u lr, u step, u done, float b1, float b2, float eps, float wd,
@@ -266,8 +279,11 @@ PYBIND11_MODULE(_C, m) {
   });
 
   // MLP: dims list, per-layer pointer lists (weights torch [out,in] layout, fp32)
-  m.def("mlp", [](int backward, u x, u y, u row_w, int n, std::vector<int> dims, std::vector<u> W, std::vector<u> b,
-                  std::vector<u> gW, std::vector<u> gb, u logits, u loss, u dloss, int act, u st) {
+  // mode 0 forward (+loss/logits), 1 + backward into gW/gb (accumulate or overwrite), 2 + SGD
+  // update of W/b with lr (device scalar) * gscale and step += 1.  ws/ticket: grid reduction.
+  m.def("mlp", [](int mode, u x, u y, u row_w, int n, std::vector<int> dims, std::vector<u> W, std::vector<u> b,
+                  std::vector<u> gW, std::vector<u> gb, u logits, u loss, u dloss, int act, u ws, u ticket,
+                  int accumulate, u lr, u step, float gscale, u st) {
     MLPArgs a{};
     const int L = (int)dims.size() - 1;
     if (L < 1 || L > MLP_MAXL || (int)W.size() != L || (int)b.size() != L) throw std::runtime_error("mlp: bad layer lists");
@@ -275,11 +291,14 @@ PYBIND11_MODULE(_C, m) {
     for (int i = 0; i <= L; ++i) a.dims[i] = dims[i];
     for (int l = 0; l < L; ++l) {
       a.W[l] = (const float*)W[l]; a.b[l] = (const float*)b[l];
-      a.gW[l] = backward ? (float*)gW.at(l) : nullptr; a.gb[l] = backward ? (float*)gb.at(l) : nullptr;
+      a.gW[l] = mode == 1 ? (float*)gW.at(l) : nullptr; a.gb[l] = mode == 1 ? (float*)gb.at(l) : nullptr;
     }
     a.logits = (float*)logits; a.loss = (float*)loss; a.dloss = (const float*)dloss; a.act = act;
-    chk(backward ? smi_mlp_bwd(&a, S(st)) : smi_mlp_fwd(&a, S(st)), "mlp");
+    a.ws = (float*)ws; a.ticket = reinterpret_cast<unsigned*>(ticket); a.accumulate = accumulate;
+    a.lr = (const float*)lr; a.step = (float*)step; a.gscale = gscale;
+    chk(smi_mlp(&a, mode, S(st)), "mlp");
   });
+  m.def("mlp_grid", [](int n) { return smi_mlp_grid(n); });
 
   m.def("gemm", [](int mode, u A, long lda, u B, long ldb, int M, int N, int K, u C, long ldc, int out_f32, int atomic,
                    int beta_acc, float alpha, u bias, u resid, long ldr, int act, u dact_y, long ldy, u seedp,

@@ -19,5 +19,15 @@ struct MLPArgs {
   float* loss;               // scalar, written (mean loss of the whole batch)
   const float* dloss;        // scalar upstream gradient (bwd)
   int act;                   // 1 relu, 2 sigmoid
+  // deterministic cross-block reduction (grid > 1): per-block partials [grid][total + 1] and a
+  // zeroed ticket word that the last block re-arms
+  float* ws;
+  unsigned* ticket;
+  int accumulate;            // bwd: gW/gb += gradient (else =)
+  // fused SGD (mode 2): params -= lr * gscale * gradient, step += 1; gradients are not stored
+  const float* lr;
+  float* step;
+  float gscale;
 };
+#define MLP_MAX_GRID 256
 

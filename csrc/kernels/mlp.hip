@@ -5,12 +5,15 @@
 // SURVEY App. A.1), which is the same model.
 //
 // The whole network is a few dozen parameters, so the GPU cost is launch latency, not FLOPs:
-// one kernel does the full-batch (or minibatch) forward + loss, one does forward-recompute +
-// backward + gradient accumulation; each wave64 handles 64 rows (one row per lane), per-lane
-// activations and pre-activation gradients live in LDS rows with an odd pitch (an even
-// multiple-of-32 pitch put all 64 lanes on one bank: 74 us per backward at batch 30), and each
-// weight-gradient entry is summed over the 64 rows by one lane (no LDS atomics, fixed order),
-// then flushed with one global atomic per parameter per block.  Row weights implement MLlib's per-block
+// ONE kernel does a whole training step — forward, softmax-CE, backward and the SGD update
+// (mode 2; the reference's optimizer.step(), distributed_multilayer_perceptron.py:108-111) — or
+// forward + loss (mode 0) or forward + backward into gradient buffers (mode 1, autograd and
+// data-parallel paths).  Each wave64 handles 64 rows (one row per lane); per-lane activations and
+// pre-activation gradients live in LDS rows with an odd pitch (an even multiple-of-32 pitch put
+// all 64 lanes on one bank: 74 us per backward at batch 30); each weight-gradient entry is summed
+// over the 64 rows by one lane in row order.  Across blocks nothing is atomic but a ticket: every
+// block publishes its partial gradient + loss, and the last block to arrive sums them in block
+// order, so gradients are bit-reproducible run to run.  Row weights implement MLlib's per-block
 // loss averaging (or 1/n for the torch-style mean).
 #include "smi_common.h"
 
@@ -50,98 +53,129 @@ __device__ __forceinline__ float mlp_forward_row(const MLPArgs& a, int row, floa
   return lse - z[lab];
 }
 
-__device__ unsigned mlp_loss_ticket = 0u;
-__device__ float mlp_loss_part[1024];  // per-block partial losses (grid <= 1024, mlp_grid)
-
 #define MLP_ACT_LD (MLP_ACT_STRIDE + 1)        // odd LDS pitch: lane-private rows on distinct banks
 #define MLP_DEL_LD (MLP_MAXW * MLP_MAXL + 1)
+#define MLP_MAXT 8192                          // parameters (weights + biases)
 
-__global__ __launch_bounds__(64) void mlp_fwd_kernel(MLPArgs a) {
-  __shared__ float acts[64 * MLP_ACT_LD];
-  float* act_s = acts + threadIdx.x * MLP_ACT_LD;
-  float lsum = 0.f;
-  for (int row = blockIdx.x * 64 + threadIdx.x; row < a.n; row += gridDim.x * 64) {
-    const float l = mlp_forward_row(a, row, act_s);
-    const float w = a.row_w ? a.row_w[row] : 1.f / (float)a.n;
-    lsum += w * l;
-    if (a.logits) {
-      int off = 0;
-      for (int k = 0; k < a.nlayers; ++k) off += a.dims[k];
-      const int C = a.dims[a.nlayers];
-      for (int c = 0; c < C; ++c) a.logits[(long)row * C + c] = act_s[off + c];
-    }
-  }
-  lsum = wave_sum(lsum);
-  if (!a.loss) return;
-  // mean loss without a zeroed accumulator (one fill launch per step): per-block partials, the
-  // last block (atomic ticket) adds them in block order and re-arms the ticket
-  __shared__ int last;
-  if (threadIdx.x == 0) {
-    mlp_loss_part[blockIdx.x] = lsum;
-    __threadfence();
-    last = atomicAdd(&mlp_loss_ticket, 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (last) {
-    __threadfence();
-    float s = 0.f;
-    for (int i = threadIdx.x; i < (int)gridDim.x; i += 64)
-      s += __hip_atomic_load(mlp_loss_part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s = wave_sum(s);
-    if (threadIdx.x == 0) {
-      a.loss[0] = s;
-      mlp_loss_ticket = 0u;
-    }
-  }
+__device__ __forceinline__ int mlp_total(const MLPArgs& a) {
+  int t = 0;
+  for (int l = 0; l < a.nlayers; ++l) t += a.dims[l + 1] * (a.dims[l] + 1);
+  return t;
 }
 
-__global__ __launch_bounds__(64) void mlp_bwd_kernel(MLPArgs a) {
+// Last step of every mode: the block-order sum of the per-block partials (entries 0..T-1 the
+// gradient, entry T the loss) — identical bits for any run with the same grid, no float atomics
+// — then the loss / gradient / SGD-updated parameters are written.  With one block the partials
+// are its own LDS values.
+__device__ void mlp_finalize(const MLPArgs& a, int mode, int T, const float* gacc, float lsum) {
+  const int lane = threadIdx.x;
+  const bool multi = gridDim.x > 1;
+  const int W = T + 1;
+  if (mode == 0) {
+    float s = lsum;
+    if (multi) {
+      s = 0.f;
+      for (int i = lane; i < (int)gridDim.x; i += 64)
+        s += __hip_atomic_load(a.ws + (long)i * W + T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s = wave_sum(s);
+    }
+    if (lane == 0 && a.loss) a.loss[0] = s;
+    return;
+  }
+  // loss: lane 0 sums the block losses in block order
+  if (lane == 0 && a.loss) {
+    float s = lsum;
+    if (multi) {
+      s = 0.f;
+      for (int i = 0; i < (int)gridDim.x; ++i)
+        s += __hip_atomic_load(a.ws + (long)i * W + T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    a.loss[0] = s;
+  }
+  const float lr = mode == 2 ? a.lr[0] * a.gscale : 0.f;
+  for (int l = 0, base = 0; l < a.nlayers; ++l) {
+    const int din = a.dims[l], dout = a.dims[l + 1], nl = dout * (din + 1);
+    for (int r = lane; r < nl; r += 64) {
+      float g = 0.f;
+      if (multi) {
+        for (int i = 0; i < (int)gridDim.x; ++i)
+          g += __hip_atomic_load(a.ws + (long)i * W + base + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        g = gacc[base + r];
+      }
+      const bool bias = r >= dout * din;
+      if (mode == 2) {
+        float* p = bias ? const_cast<float*>(a.b[l]) + (r - dout * din) : const_cast<float*>(a.W[l]) + r;
+        *p -= lr * g;
+      } else {
+        float* q = bias ? a.gb[l] + (r - dout * din) : a.gW[l] + r;
+        *q = a.accumulate ? *q + g : g;
+      }
+    }
+    base += nl;
+  }
+  if (mode == 2 && lane == 0 && a.step) a.step[0] += 1.f;
+}
+
+// mode 0: forward + loss (+ logits); 1: + backward, gradients to gW/gb; 2: + SGD update of W/b.
+// One wave64 per block, one row per lane; the grid-level sums are deterministic (block order).
+__global__ __launch_bounds__(64) void mlp_kernel(MLPArgs a, int mode) {
   __shared__ float acts[64 * MLP_ACT_LD];  // per row: layer inputs (dims[0..L-1]) + logits
   __shared__ float dls[64 * MLP_DEL_LD];   // per row: grad wrt each layer's pre-activation output
-  __shared__ float gacc[8192];
+  __shared__ float gacc[MLP_MAXT];
+  __shared__ int last;
   const int L = a.nlayers, lane = threadIdx.x;
   int offs[MLP_MAXL + 1];  // activation offsets (offs[l] = input of layer l)
   offs[0] = 0;
   for (int l = 0; l < L; ++l) offs[l + 1] = offs[l] + a.dims[l];
-  int total = 0;
-  for (int l = 0; l < L; ++l) total += a.dims[l + 1] * (a.dims[l] + 1);
-  for (int i = lane; i < total; i += 64) gacc[i] = 0.f;
+  const int T = mlp_total(a);
+  if (mode > 0)
+    for (int i = lane; i < T; i += 64) gacc[i] = 0.f;
   float* act_s = acts + lane * MLP_ACT_LD;
   float* del_s = dls + lane * MLP_DEL_LD;
   const float dl = a.dloss ? a.dloss[0] : 1.f;
   const int d0 = a.dims[0];
+  float lsum = 0.f;
   for (int chunk = blockIdx.x * 64; chunk < a.n; chunk += gridDim.x * 64) {
     const int row = chunk + lane;
     if (row < a.n) {
-      mlp_forward_row(a, row, act_s);
-      const float w = (a.row_w ? a.row_w[row] : 1.f / (float)a.n) * dl;
-      const int C = a.dims[L];
-      const float* z = act_s + offs[L];
-      float* dz = del_s + offs[L] - d0;
-      float m = z[0];
-      for (int c = 1; c < C; ++c) m = fmaxf(m, z[c]);
-      float se = 0.f;
-      for (int c = 0; c < C; ++c) se += __expf(z[c] - m);
-      const long long lab = a.y[row];
-      for (int c = 0; c < C; ++c) dz[c] = (__expf(z[c] - m) / se - (c == lab ? 1.f : 0.f)) * w;
-      for (int l = L - 1; l > 0; --l) {  // grad wrt layer l-1's pre-activation output
-        const int din = a.dims[l], dout = a.dims[l + 1];
-        const float* dcur = del_s + offs[l + 1] - d0;
-        float* dprev = del_s + offs[l] - d0;
-        const float* h = act_s + offs[l];
-        for (int i = 0; i < din; ++i) {
-          float s = 0.f;
-          for (int o = 0; o < dout; ++o) s += a.W[l][o * din + i] * dcur[o];
-          dprev[i] = a.act == 1 ? (h[i] > 0.f ? s : 0.f) : s * h[i] * (1.f - h[i]);
+      const float w = a.row_w ? a.row_w[row] : 1.f / (float)a.n;
+      lsum += w * mlp_forward_row(a, row, act_s);
+      if (a.logits) {
+        const int C = a.dims[L];
+        for (int c = 0; c < C; ++c) a.logits[(long)row * C + c] = act_s[offs[L] + c];
+      }
+      if (mode > 0) {
+        const int C = a.dims[L];
+        const float* z = act_s + offs[L];
+        float* dz = del_s + offs[L] - d0;
+        float m = z[0];
+        for (int c = 1; c < C; ++c) m = fmaxf(m, z[c]);
+        float se = 0.f;
+        for (int c = 0; c < C; ++c) se += __expf(z[c] - m);
+        const long long lab = a.y[row];
+        const float wd = w * dl;
+        for (int c = 0; c < C; ++c) dz[c] = (__expf(z[c] - m) / se - (c == lab ? 1.f : 0.f)) * wd;
+        for (int l = L - 1; l > 0; --l) {  // grad wrt layer l-1's pre-activation output
+          const int din = a.dims[l], dout = a.dims[l + 1];
+          const float* dcur = del_s + offs[l + 1] - d0;
+          float* dprev = del_s + offs[l] - d0;
+          const float* h = act_s + offs[l];
+          for (int i = 0; i < din; ++i) {
+            float s = 0.f;
+            for (int o = 0; o < dout; ++o) s += a.W[l][o * din + i] * dcur[o];
+            dprev[i] = a.act == 1 ? (h[i] > 0.f ? s : 0.f) : s * h[i] * (1.f - h[i]);
+          }
         }
       }
-    } else {  // rows past n contribute nothing
+    } else if (mode > 0) {  // rows past n contribute nothing
       for (int j = 0; j < offs[L] + a.dims[L] - d0; ++j) del_s[j] = 0.f;
       for (int j = 0; j < offs[L]; ++j) act_s[j] = 0.f;
     }
+    if (mode == 0) continue;
     __syncthreads();
     // gradient entry e (layer-major: W[o][i] then b[o]) summed over the chunk's 64 rows, in row order
-    for (int e = lane; e < total; e += 64) {
+    for (int e = lane; e < T; e += 64) {
       int l = 0, base = 0;
       while (e >= base + a.dims[l + 1] * (a.dims[l] + 1)) { base += a.dims[l + 1] * (a.dims[l] + 1); ++l; }
       const int din = a.dims[l], dout = a.dims[l + 1], r = e - base;
@@ -155,13 +189,24 @@ __global__ __launch_bounds__(64) void mlp_bwd_kernel(MLPArgs a) {
     }
     __syncthreads();
   }
-  for (int l = 0, base = 0; l < L; ++l) {
-    const int din = a.dims[l], dout = a.dims[l + 1];
-    const float* g = gacc + base;
-    for (int i = lane; i < dout * din; i += 64) atomicAdd(&a.gW[l][i], g[i]);
-    for (int i = lane; i < dout; i += 64) atomicAdd(&a.gb[l][i], g[dout * din + i]);
-    base += dout * (din + 1);
+  lsum = wave_sum(lsum);
+  if (gridDim.x == 1) {
+    mlp_finalize(a, mode, T, gacc, lsum);
+    return;
   }
+  // publish this block's partials, the last block to arrive reduces them in block order
+  float* part = a.ws + (long)blockIdx.x * (T + 1);
+  if (mode > 0)
+    for (int i = lane; i < T; i += 64) part[i] = gacc[i];
+  if (lane == 0) part[T] = lsum;
+  __threadfence();
+  __syncthreads();
+  if (lane == 0) last = atomicAdd(a.ticket, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  mlp_finalize(a, mode, T, gacc, lsum);
+  if (lane == 0) a.ticket[0] = 0u;  // re-arm for the next launch (stream-ordered)
 }
 
 static int mlp_check(const MLPArgs& a) {
@@ -169,23 +214,25 @@ static int mlp_check(const MLPArgs& a) {
   int total = 0;
   for (int l = 0; l <= a.nlayers; ++l) if (a.dims[l] < 1 || a.dims[l] > MLP_MAXW) return -1;
   for (int l = 0; l < a.nlayers; ++l) total += a.dims[l + 1] * (a.dims[l] + 1);
-  if (total > 8192) return -1;
+  if (total > MLP_MAXT) return -1;
   return 0;
 }
 
-static unsigned mlp_grid(int n) {
+extern "C" int smi_mlp_grid(int n) {
   int b = (n + 63) / 64;
-  return (unsigned)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
+  return b < 1 ? 1 : (b > MLP_MAX_GRID ? MLP_MAX_GRID : b);
 }
 
-extern "C" int smi_mlp_fwd(const MLPArgs* args, hipStream_t st) {
-  if (mlp_check(*args)) return -1;
-  hipLaunchKernelGGL(mlp_fwd_kernel, dim3(mlp_grid(args->n)), dim3(64), 0, st, *args);
-  SMI_CHECK_LAUNCH();
-}
-
-extern "C" int smi_mlp_bwd(const MLPArgs* args, hipStream_t st) {
-  if (mlp_check(*args)) return -1;
-  hipLaunchKernelGGL(mlp_bwd_kernel, dim3(mlp_grid(args->n)), dim3(64), 0, st, *args);
+// mode 0 forward/loss, 1 forward+backward (gradients), 2 forward+backward+SGD (one launch per
+// training step).  grid > 1 needs a.ws ([grid][total+1] floats) and a zeroed a.ticket.
+extern "C" int smi_mlp(const MLPArgs* args, int mode, hipStream_t st) {
+  const MLPArgs& a = *args;
+  if (mlp_check(a) || mode < 0 || mode > 2) return -1;
+  const int grid = smi_mlp_grid(a.n);
+  if (grid > 1 && (!a.ws || !a.ticket)) return -1;
+  if (mode > 0 && !a.y) return -1;
+  if (mode == 1) for (int l = 0; l < a.nlayers; ++l) if (!a.gW[l] || !a.gb[l]) return -1;
+  if (mode == 2 && !a.lr) return -1;
+  hipLaunchKernelGGL(mlp_kernel, dim3(grid), dim3(64), 0, st, a, mode);
   SMI_CHECK_LAUNCH();
 }

@@ -11,9 +11,14 @@ Semantics:
     per-block mean CE (per-row weights 1/(|block| * nblocks));
   * solver "l-bfgs" (memory 10, tol, maxIter) or "gd" (full-batch, step stepSize/sqrt(t));
   * default init (rand * 4.8 - 2.4)/sqrt(numIn) per layer from ``seed``.
-Compute: the objective and gradient come from the fused HIP MLP kernels (sparkmi/ops/mlp.py)
-on the executor's GPU when one is visible (the whole dataset resident in HBM), CPU torch
-otherwise.  ``transform`` appends rawPrediction / probability / prediction columns.
+Compute: ``fit`` runs on the session's executors (spark.executor.instances, or ``numExecutors``):
+one process per executor (Distributor), each holding its contiguous row partition resident on
+its device; every objective evaluation is the fused HIP MLP loss+gradient (sparkmi/ops/mlp.py)
+on the partition followed by ONE all-reduce of [gradient, loss] — Spark's treeAggregate — and
+every executor runs the identical device L-BFGS (sparkmi/optim/lbfgs.py, csrc/kernels/lbfgs.hip).
+CPU executors use float64 torch.  The objective is fixed on the global row order and reduced
+over fixed slabs of whole blocks in slab order (``reduction_slabs``), so a fit on N executors
+is bit-identical to the single-executor fit.  ``transform`` appends rawPrediction / probability / prediction columns.
 Persistence: ``write().overwrite().save(path)`` / ``load(path)`` in Spark's on-disk layout
 (metadata/part-00000 JSON + data/part-00000-*.parquet with a VectorUDT ``weights`` struct).
 """
@@ -103,7 +108,8 @@ class _MLPParams(HasFeaturesCol, HasLabelCol, HasPredictionCol, HasMaxIter, HasT
 class MultilayerPerceptronClassifier(Estimator, _MLPParams):
     def __init__(self, featuresCol="features", labelCol="label", predictionCol="prediction", maxIter=100, tol=1e-6,
                  seed=None, layers=None, blockSize=128, stepSize=0.03, solver="l-bfgs", initialWeights=None,
-                 probabilityCol="probability", rawPredictionCol="rawPrediction", device=None):
+                 probabilityCol="probability", rawPredictionCol="rawPrediction", device=None, numExecutors=None,
+                 fitTimeout=600):
         super().__init__()
         apply_mixin_defaults(self)
         self._setDefault(maxIter=100, tol=1e-6, blockSize=128, stepSize=0.03, solver="l-bfgs")
@@ -112,6 +118,8 @@ class MultilayerPerceptronClassifier(Estimator, _MLPParams):
                   initialWeights=initialWeights, probabilityCol=probabilityCol, rawPredictionCol=rawPredictionCol)
         self._set(**{k: v for k, v in kw.items() if v is not None})
         self.device = torch.device(device) if device else _device()
+        self.num_executors = numExecutors  # None: the dataset session's spark.executor.instances
+        self.fit_timeout = fitTimeout
 
     def setLayers(self, v):
         return self._set(layers=v)
@@ -120,8 +128,6 @@ class MultilayerPerceptronClassifier(Estimator, _MLPParams):
         return self._set(initialWeights=v)
 
     def _fit(self, dataset):
-        from ..optim.lbfgs import LBFGS
-        from ..ops.mlp import mlp_loss
         layers = self.getLayers()
         if not layers or len(layers) < 2:
             raise ValueError("layers must be set, e.g. [4, 5, 4, 3]")
@@ -133,53 +139,173 @@ class MultilayerPerceptronClassifier(Estimator, _MLPParams):
             raise ValueError(f"input layer size {layers[0]} != numFeatures {X.shape[1]}")
         if y.max() >= layers[-1] or y.min() < 0 or (y != np.round(y)).any():
             raise ValueError("labels must be integers in [0, numClasses)")
-        dev = self.device
-        xt = torch.as_tensor(X, dtype=torch.float32, device=dev)
-        yt = torch.as_tensor(y, dtype=torch.int64, device=dev)
-        rw = torch.as_tensor(block_row_weights(len(y), self.getBlockSize()), dtype=torch.float32, device=dev)
         if self.isDefined("initialWeights") and self.getOrDefault("initialWeights") is not None:
             w0 = np.asarray(self.getOrDefault("initialWeights").toArray(), dtype=np.float64)
             if w0.shape[0] != num_weights(layers):
                 raise ValueError("initialWeights has the wrong size")
         else:
             w0 = init_weights(layers, self.getSeed())
-        theta0 = torch.as_tensor(w0, dtype=torch.float32, device=dev)
+        # Spark's block-averaged objective, fixed on the GLOBAL row order: each executor's rows
+        # carry their global weights, so the executors' partial sums add up to the same
+        # objective whatever the partitioning
+        rw = block_row_weights(len(y), self.getBlockSize())
+        opts = dict(layers=list(layers), solver=solver, max_iter=self.getMaxIter(), tol=self.getTol(),
+                    step_size=self.getStepSize())
+        slabs = reduction_slabs(len(y), self.getBlockSize())
+        n_exec = self._executors(dataset, len(slabs) - 1)
+        t0 = time.time()
+        if n_exec <= 1:
+            theta, history, iters = _fit_arrays(X, y, rw, w0, opts, self.device, slabs)
+        else:
+            from ..api.distributor import Distributor
+            gpu = self.device.type == "cuda"
+            env = {}
+            if gpu and torch.cuda.device_count() < n_exec:
+                env["SPARKMI_DIST_BACKEND"] = "gloo"  # several executors share a device: no RCCL
+            theta, history, iters = Distributor(num_processes=n_exec, use_gpu=gpu, share_gpus=True, env=env,
+                                                log_sink=None, timeout=self.fit_timeout).run(
+                _fit_executor, X, y, rw, w0, opts, slabs)
+        model = MultilayerPerceptronClassificationModel(layers, np.asarray(theta, dtype=np.float64), device=self.device)
+        self._copyValues(model)
+        model._summary = TrainingSummary(history, iters, time.time() - t0)
+        model._num_executors = n_exec
+        return model
+
+    def _executors(self, dataset, n_slabs):
+        """Executors the fit runs on: ``numExecutors`` if given, else the dataset's session
+        (spark.executor.instances, mllib_multilayer_perceptron_classifier.py:12-19), at most one
+        per reduction slab."""
+        n = self.num_executors
+        if n is None:
+            sess = getattr(dataset, "session", None)
+            n = sess.num_executors if sess is not None else 1
+        return max(1, min(int(n), n_slabs))
+
+
+def _objective(X, y, rw, layers, device):
+    """fg(theta) -> (weighted CE sum over these rows [0-d tensor], flat gradient [new tensor]).
+    GPU: the fused HIP MLP kernels (fp32, sparkmi/ops/mlp.py); CPU: float64 torch."""
+    from ..ops.mlp import mlp_loss
+    if device.type == "cuda":
+        xt = torch.as_tensor(X, dtype=torch.float32, device=device)
+        yt = torch.as_tensor(y, dtype=torch.int64, device=device)
+        wt = torch.as_tensor(rw, dtype=torch.float32, device=device)
 
         def fg(theta):
             Ws, bs = unpack_weights(theta, layers)
             Ws = [W.contiguous().detach().requires_grad_() for W in Ws]
             bs = [b.contiguous().detach().requires_grad_() for b in bs]
-            for p in Ws + bs:
-                p.grad = None
-            loss = mlp_loss(xt, yt, Ws, bs, "sigmoid", rw)
+            loss = mlp_loss(xt, yt, Ws, bs, "sigmoid", wt)
             loss.backward()
-            g = pack_weights([W.grad for W in Ws], [b.grad for b in bs])
-            return float(loss.detach()), g
+            return loss.detach(), pack_weights([W.grad for W in Ws], [b.grad for b in bs])
+        return fg
+    xt = torch.as_tensor(X, dtype=torch.float64)
+    yt = torch.as_tensor(y, dtype=torch.int64)
+    wt = torch.as_tensor(rw, dtype=torch.float64)
 
-        t0 = time.time()
-        if solver == "l-bfgs":
-            opt = LBFGS(max_iter=self.getMaxIter(), m=10, tol=self.getTol())
-            theta = opt.minimize(fg, theta0)
-            history, iters = opt.objective_history, opt.iterations
-        else:
-            theta = theta0.clone()
+    def fg(theta):
+        th = theta.detach().requires_grad_()
+        Ws, bs = unpack_weights(th, layers)
+        h = xt
+        for i, (W, b) in enumerate(zip(Ws, bs)):
+            h = h @ W.t() + b
+            if i < len(Ws) - 1:
+                h = torch.sigmoid(h)
+        rl = torch.logsumexp(h, 1) - h.gather(1, yt[:, None]).squeeze(1)
+        loss = (rl * wt).sum()
+        (g,) = torch.autograd.grad(loss, th)
+        return loss.detach(), g
+    return fg
+
+
+MAX_SLABS = 64
+
+
+def reduction_slabs(n_rows, block_size, max_slabs=MAX_SLABS):
+    """Row boundaries of the objective's reduction slabs: whole Spark blocks grouped into at most
+    ``max_slabs`` contiguous slabs.  Each slab's loss/gradient is computed on its own and the
+    slabs are summed in slab order, so the result does not depend on how slabs are spread over
+    executors (floating-point sums are not associative; a plain all-reduce of per-executor
+    partial sums would make an N-executor fit differ from the 1-executor fit)."""
+    nb = max(1, (n_rows + block_size - 1) // block_size)
+    ns = min(nb, max_slabs)
+    return [min(n_rows, (s * nb // ns) * block_size) for s in range(ns)] + [n_rows]
+
+
+def _fit_arrays(X, y, rw, w0, opts, device, slabs, mine=None, reduce=None):
+    """Solve with the objective summed over reduction slabs.  ``slabs``: global row boundaries;
+    ``mine``: the slab indices whose rows are in X/y/rw (all of them by default, rows given
+    from the first of them on).  ``reduce(buf)`` sums the [slabs, n+1] partials over executors
+    in place — each slab is non-zero on exactly one executor, so that sum is exact (this is
+    Spark's treeAggregate, made order-independent) — and every executor then adds the slabs in
+    slab order and follows the identical trajectory."""
+    from ..optim.lbfgs import LBFGS
+    layers = opts["layers"]
+    dtype = torch.float32 if device.type == "cuda" else torch.float64
+    ns = len(slabs) - 1
+    mine = list(range(ns)) if mine is None else list(mine)
+    base = slabs[mine[0]] if mine else 0
+    objs = [(s, _objective(X[slabs[s] - base:slabs[s + 1] - base], y[slabs[s] - base:slabs[s + 1] - base],
+                           rw[slabs[s] - base:slabs[s + 1] - base], layers, device)) for s in mine]
+    n = num_weights(layers)
+
+    def fg(theta):
+        part = torch.zeros(ns, n + 1, dtype=dtype, device=device)
+        for s, obj in objs:
+            f, g = obj(theta)
+            part[s, :n] = g.reshape(-1)
+            part[s, n] = f
+        if reduce is not None:
+            reduce(part)
+        tot = part.sum(0)
+        return tot[n], tot[:n].clone()
+
+    theta0 = torch.as_tensor(w0, dtype=dtype, device=device)
+    if opts["solver"] == "l-bfgs":
+        opt = LBFGS(max_iter=opts["max_iter"], m=10, tol=opts["tol"])
+        theta = opt.minimize(fg, theta0)
+        history, iters = opt.objective_history, opt.iterations
+    else:
+        theta = theta0.clone()
+        f, g = fg(theta)
+        history = [float(f)]
+        iters = 0
+        for it in range(1, opts["max_iter"] + 1):
+            step = opts["step_size"] / np.sqrt(it)
+            new = theta - step * g
+            diff = float((new - theta).norm())
+            theta = new
             f, g = fg(theta)
-            history = [f]
-            iters = 0
-            for it in range(1, self.getMaxIter() + 1):
-                step = self.getStepSize() / np.sqrt(it)
-                new = theta - step * g
-                diff = float((new - theta).norm())
-                theta = new
-                f, g = fg(theta)
-                history.append(f)
-                iters = it
-                if diff < self.getTol() * max(float(theta.norm()), 1.0):
-                    break
-        model = MultilayerPerceptronClassificationModel(layers, theta.detach().double().cpu().numpy(), device=dev)
-        self._copyValues(model)
-        model._summary = TrainingSummary(history, iters, time.time() - t0)
-        return model
+            history.append(float(f))
+            iters = it
+            if diff < opts["tol"] * max(float(theta.norm()), 1.0):
+                break
+    return theta.detach().double().cpu().numpy(), history, iters
+
+
+def _fit_executor(X, y, rw, w0, opts, slabs):
+    """One executor of a distributed fit (run by Distributor): its contiguous run of reduction
+    slabs stays resident on its device; the slab partials are all-reduced every evaluation."""
+    import torch.distributed as dist
+    from ..parallel import init_distributed
+    rank, world, device = init_distributed()
+    ns = len(slabs) - 1
+    cut = np.linspace(0, ns, world + 1).round().astype(int)
+    mine = list(range(cut[rank], cut[rank + 1]))
+    lo, hi = (slabs[mine[0]], slabs[mine[-1] + 1]) if mine else (0, 0)
+    host = dist.get_backend() == "gloo" and device.type == "cuda"
+
+    def reduce(buf):
+        if host:  # gloo on shared devices: reduce through host memory
+            t = buf.cpu()
+            dist.all_reduce(t)
+            buf.copy_(t)
+        else:
+            dist.all_reduce(buf)
+
+    out = _fit_arrays(X[lo:hi], y[lo:hi], rw[lo:hi], w0, opts, device, slabs, mine, reduce=reduce)
+    dist.barrier()
+    return out
 
 
 class TrainingSummary:

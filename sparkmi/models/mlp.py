@@ -6,7 +6,7 @@ state_dicts load.  ``forward`` returns logits; ``loss`` runs the fused HIP MLP+C
 import torch
 from torch import nn
 
-from ..ops.mlp import mlp_logits, mlp_loss
+from ..ops.mlp import mlp_logits, mlp_loss, mlp_sgd_step
 
 
 class MultilayerPerceptron(nn.Module):
@@ -35,6 +35,23 @@ class MultilayerPerceptron(nn.Module):
     def loss(self, x, y, row_weight=None):
         lins = self.linears()
         return mlp_loss(x, y, [l.weight for l in lins], [l.bias for l in lins], self.activation, row_weight)
+
+
+    def fused_sgd_step(self, opt, x, y):
+        """The whole training step — forward, CE, backward, SGD update — as ONE HIP launch
+        (csrc/kernels/mlp.hip mode 2); the loss of the step is returned.  None when it does not
+        apply (CPU, an optimizer other than plain SGD, a bf16 shadow to refresh): the caller
+        then runs the usual forward/backward/step."""
+        from .. import _native
+        from ..optim.sgd import SGD
+        flat = getattr(opt, "flat", None)
+        if (not x.is_cuda or not isinstance(opt, SGD) or opt.momentum or opt.weight_decay
+                or getattr(opt, "ranges", None) is not None or (flat is not None and flat.shadow is not None)
+                or not _native.use_native(x)):
+            return None
+        lins = self.linears()
+        return mlp_sgd_step(x, y, [l.weight for l in lins], [l.bias for l in lins], opt.lr_t, opt.step_t,
+                            self.activation, grad_scale=opt.grad_scale)
 
 
 Multilayer_perceptor = MultilayerPerceptron  # reference class name

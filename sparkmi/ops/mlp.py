@@ -1,8 +1,9 @@
 """Fused small-MLP (affine + sigmoid/relu hidden layers + affine logits + softmax-CE).
 
 One HIP launch computes the (weighted) mean cross-entropy of a whole minibatch or full batch;
-one launch recomputes the forward and accumulates every weight/bias gradient
-(csrc/kernels/mlp.hip).  Used by the reference MLP (distributed_multilayer_perceptron.py:44-53)
+one launch recomputes the forward and accumulates every weight/bias gradient; and
+``mlp_sgd_step`` is a whole training step (forward, CE, backward, SGD update) in ONE launch
+(csrc/kernels/mlp.hip).  Cross-block sums are deterministic (block-order reduction).  Used by the reference MLP (distributed_multilayer_perceptron.py:44-53)
 and by the MLlib-compatible MultilayerPerceptronClassifier's L-BFGS objective.
 ``row_weight`` implements MLlib's per-block loss averaging.
 """
@@ -12,6 +13,26 @@ from .. import _native
 from ._grad import grad_buf, grad_ready
 
 ACT = {"sigmoid": 2, "relu": 1}
+_ws = {}
+
+
+def _workspace(device, n, dims):
+    """(ws, ticket) device pointers for the kernel's cross-block reduction (0, 0 for one block).
+    Cached per (device, size) and never freed: captured graphs keep using the same buffers."""
+    grid = _native.C().mlp_grid(int(n))
+    if grid <= 1:
+        return 0, 0
+    T = sum(dims[i + 1] * (dims[i] + 1) for i in range(len(dims) - 1))
+    key = (str(device), grid * (T + 1))
+    e = _ws.get(key)
+    if e is None:
+        e = _ws[key] = (torch.empty(grid * (T + 1), device=device, dtype=torch.float32),
+                        torch.zeros(1, device=device, dtype=torch.int32))
+    return e[0].data_ptr(), e[1].data_ptr()
+
+
+def _dims(Ws):
+    return [Ws[0].shape[1]] + [W.shape[0] for W in Ws]
 
 
 def _ref_logits(x, Ws, bs, act):
@@ -34,10 +55,11 @@ class MLPLossFn(torch.autograd.Function):
         ctx.save_for_backward(x, y, row_weight, *params)
         if ctx.native:
             loss = torch.empty(1, device=x.device, dtype=torch.float32)  # written by the kernel
-            dims = [Ws[0].shape[1]] + [W.shape[0] for W in Ws]
+            dims = _dims(Ws)
+            ws, tk = _workspace(x.device, x.shape[0], dims)
             _native.C().mlp(0, x.data_ptr(), y.data_ptr(), _native.ptr(row_weight), x.shape[0], dims,
                             [W.data_ptr() for W in Ws], [b.data_ptr() for b in bs], [], [], 0, loss.data_ptr(), 0,
-                            act, _native.stream())
+                            act, ws, tk, 0, 0, 0, 1.0, _native.stream())
             return loss[0]
         z = _ref_logits(x, Ws, bs, act)
         rl = torch.logsumexp(z, 1) - z.gather(1, y[:, None]).squeeze(1)
@@ -50,12 +72,13 @@ class MLPLossFn(torch.autograd.Function):
         L = ctx.nlayers
         Ws, bs = params[:L], params[L:]
         if ctx.native:
-            dims = [Ws[0].shape[1]] + [W.shape[0] for W in Ws]
+            dims = _dims(Ws)
             dl = dloss.reshape(1).float().contiguous()
+            ws, tk = _workspace(x.device, x.shape[0], dims)
             _native.C().mlp(1, x.data_ptr(), y.data_ptr(), _native.ptr(row_weight), x.shape[0], dims,
                             [W.data_ptr() for W in Ws], [b.data_ptr() for b in bs],
                             [grad_buf(W).data_ptr() for W in Ws], [grad_buf(b).data_ptr() for b in bs], 0, 0,
-                            dl.data_ptr(), ctx.act, _native.stream())
+                            dl.data_ptr(), ctx.act, ws, tk, 1, 0, 0, 1.0, _native.stream())
         else:
             with torch.enable_grad():
                 ps = [p.detach().float().requires_grad_() for p in params]
@@ -76,6 +99,24 @@ def mlp_loss(x, y, weights, biases, act="sigmoid", row_weight=None):
     return MLPLossFn.apply(x, y, row_weight, a, len(weights), *weights, *biases)
 
 
+def mlp_sgd_step(x, y, weights, biases, lr_t, step_t=None, act="sigmoid", row_weight=None, grad_scale=1.0,
+                 loss_out=None):
+    """One training step in ONE launch: forward, weighted softmax-CE, backward and plain SGD
+    (params -= lr * grad_scale * grad, ``step_t`` += 1) on the GPU.  Parameters must be fp32
+    contiguous device tensors (updated in place); ``lr_t`` a device scalar.  Returns the loss
+    (device scalar) of the step's forward, i.e. before the update."""
+    a = ACT[act] if isinstance(act, str) else act
+    x = x.float().contiguous()
+    y = y.to(torch.int64).contiguous()
+    loss = loss_out if loss_out is not None else torch.empty(1, device=x.device, dtype=torch.float32)
+    dims = _dims(weights)
+    ws, tk = _workspace(x.device, x.shape[0], dims)
+    _native.C().mlp(2, x.data_ptr(), y.data_ptr(), _native.ptr(row_weight), x.shape[0], dims,
+                    [W.data_ptr() for W in weights], [b.data_ptr() for b in biases], [], [], 0, loss.data_ptr(), 0,
+                    a, ws, tk, 0, lr_t.data_ptr(), _native.ptr(step_t), float(grad_scale), _native.stream())
+    return loss[0]
+
+
 def mlp_logits(x, weights, biases, act="sigmoid"):
     """Inference logits [n, C] (fused kernel on GPU)."""
     a = ACT[act] if isinstance(act, str) else act
@@ -84,8 +125,10 @@ def mlp_logits(x, weights, biases, act="sigmoid"):
         C = weights[-1].shape[0]
         out = torch.empty(x.shape[0], C, device=x.device, dtype=torch.float32)
         dims = [weights[0].shape[1]] + [W.shape[0] for W in weights]
+        ws, tk = _workspace(x.device, x.shape[0], dims)
         _native.C().mlp(0, x.data_ptr(), 0, 0, x.shape[0], dims, [W.data_ptr() for W in weights],
-                        [b.data_ptr() for b in biases], [], [], out.data_ptr(), 0, 0, a, _native.stream())
+                        [b.data_ptr() for b in biases], [], [], out.data_ptr(), 0, 0, a, ws, tk, 0, 0, 0, 1.0,
+                        _native.stream())
         return out
     with torch.no_grad():
         return _ref_logits(x, weights, biases, a)

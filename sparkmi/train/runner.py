@@ -25,8 +25,12 @@ from ..ops import _grad
 
 
 class StepRunner:
-    def __init__(self, model, loss_fn, optimizer, ddp=None, graph=False, warmup_eager=3, split_fn=None):
+    def __init__(self, model, loss_fn, optimizer, ddp=None, graph=False, warmup_eager=3, split_fn=None,
+                 fused_step=None):
         self.model = model
+        # fused_step(model, optimizer, *batch) -> loss or None: a whole single-executor step in
+        # one kernel (e.g. MultilayerPerceptron.fused_sgd_step); None falls back to the chain
+        self.fused_step = fused_step
         self.loss_fn = loss_fn          # loss_fn(model, *batch) -> scalar loss tensor
         self.split_fn = split_fn        # split_fn(model, *batch) -> (loss, leaf, root), see module doc
         self.graph2 = None              # split mode: the lower segments' backward graphs
@@ -92,6 +96,10 @@ class StepRunner:
         return e
 
     def _eager(self, *batch):
+        if self.fused_step is not None and self.ddp is None:
+            loss = self.fused_step(self.model, self.opt, *batch)
+            if loss is not None:
+                return loss
         e0 = self._event()
         loss = self._fwd_bwd(*batch)
         e1 = self._event()

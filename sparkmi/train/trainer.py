@@ -36,7 +36,8 @@ def setup_executor(cfg):
 
 
 class Trainer:
-    def __init__(self, model, loss_fn, make_optimizer, cfg, device, rank=0, world=1, name="run", shadow=None):
+    def __init__(self, model, loss_fn, make_optimizer, cfg, device, rank=0, world=1, name="run", shadow=None,
+                 fused_step=None):
         self.model = model.to(device)
         self.cfg = cfg
         self.device = torch.device(device)
@@ -45,7 +46,8 @@ class Trainer:
         self.opt = make_optimizer(self.flat)
         self.ddp = DataParallel(self.flat, bucket_mb=cfg.bucket_mb, zero=getattr(cfg, "zero", False)) if world > 1 else None
         use_graph = bool(cfg.graph) and self.device.type == "cuda"
-        self.runner = StepRunner(self.model, loss_fn, self.opt, ddp=self.ddp, graph=use_graph)
+        self.runner = StepRunner(self.model, loss_fn, self.opt, ddp=self.ddp, graph=use_graph,
+                                 fused_step=fused_step if world == 1 else None)
         path = f"{cfg.metrics}.rank{rank}.jsonl" if cfg.metrics else None
         self.metrics = MetricsLogger(path, rank=rank, every=cfg.log_every, echo=cfg.verbose and rank == 0,
                                      extra={"run": name, "world": world})

@@ -172,3 +172,40 @@ def test_params_api():
     assert v.toArray().tolist() == [1.0, 2.0]
     sv = Vectors.sparse(4, [1, 3], [1.0, 2.0])
     assert sv.toArray().tolist() == [0.0, 1.0, 0.0, 2.0]
+
+
+@pytest.mark.parametrize("solver", ["l-bfgs", "gd"])
+def test_distributed_fit_equals_single_executor(iris, tmp_path, solver):
+    """Executor-parallel fit (2 processes, partitions resident per executor, [grad, loss]
+    all-reduced each evaluation = Spark's treeAggregate) lands on the single-executor weights."""
+    train, _ = iris.randomSplit([0.6, 0.4], 1234)
+    kw = dict(maxIter=60, layers=[4, 5, 4, 3], blockSize=30, seed=1234, solver=solver, device="cpu",
+              stepSize=0.03 if solver == "l-bfgs" else 5.0)
+    m2 = MultilayerPerceptronClassifier(numExecutors=2, **kw).fit(train)
+    m1 = MultilayerPerceptronClassifier(numExecutors=1, **kw).fit(train)
+    assert m2._num_executors == 2 and m1._num_executors == 1
+    assert m1.summary.totalIterations == m2.summary.totalIterations
+    np.testing.assert_allclose(m2.weights.toArray(), m1.weights.toArray(), atol=1e-6, rtol=0)
+    np.testing.assert_allclose(m2.summary.objectiveHistory, m1.summary.objectiveHistory, rtol=1e-9)
+    path = str(tmp_path / "dist_model")
+    m2.write().overwrite().save(path)
+    back = MultilayerPerceptronClassificationModel.load(path)
+    np.testing.assert_array_equal(back.weights.toArray(), m2.weights.toArray())
+    np.testing.assert_array_equal(back.transform(iris).column("prediction"), m2.transform(iris).column("prediction"))
+
+
+def test_lbfgs_minimises_quadratic_cpu():
+    """Device-memory L-BFGS (ring buffers + two-loop) on an ill-conditioned quadratic."""
+    from sparkmi.optim.lbfgs import LBFGS
+    torch.manual_seed(0)
+    n = 40
+    Q = torch.randn(n, n, dtype=torch.float64)
+    A = Q @ Q.t() / n + 0.05 * torch.eye(n, dtype=torch.float64)  # condition number ~100
+    b = torch.randn(n, dtype=torch.float64)
+
+    def fg(x):
+        return 0.5 * x @ A @ x - b @ x, A @ x - b
+    opt = LBFGS(max_iter=1000, m=10, tol=1e-15)
+    x = opt.minimize(fg, torch.zeros(n, dtype=torch.float64))
+    torch.testing.assert_close(x, torch.linalg.solve(A, b), atol=1e-5, rtol=1e-5)
+    assert 10 < opt.iterations < 1000

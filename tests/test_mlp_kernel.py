@@ -39,3 +39,49 @@ def test_mlp_kernel_vs_torch(n, layers, act, weighted):
     for (name, pg), pc in zip(mg.named_parameters(), mc.parameters()):
         rel = float((pg.grad.cpu() - pc.grad).norm() / (pc.grad.norm() + 1e-12))
         assert rel < 1e-4, (name, rel)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [30, 5000])
+def test_mlp_gradients_bit_reproducible(n):
+    """Cross-block sums are a block-order reduction, not float atomics: the same backward twice
+    gives bit-identical gradients (5000 rows = 79 blocks)."""
+    torch.manual_seed(1)
+    m = MultilayerPerceptron((8, 32, 16, 5)).cuda()
+    x = (torch.rand(n, 8) * 2 - 1).cuda()
+    y = torch.randint(0, 5, (n,)).cuda()
+    grads = []
+    for _ in range(2):
+        for p in m.parameters():
+            p.grad = None
+        m.loss(x, y).backward()
+        grads.append([p.grad.clone() for p in m.parameters()])
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [30, 700])
+def test_mlp_fused_sgd_step_equals_chain(n):
+    """ONE launch (forward + CE + backward + SGD) == loss kernel + backward kernel + SGD kernel."""
+    from sparkmi.optim import SGD
+    from sparkmi.utils.flat import FlatParams
+    torch.manual_seed(2)
+    a = MultilayerPerceptron((4, 5, 4, 3)).cuda()
+    b = MultilayerPerceptron((4, 5, 4, 3)).cuda()
+    b.load_state_dict(a.state_dict())
+    fa, fb = FlatParams(a, shadow=False), FlatParams(b, shadow=False)
+    oa, ob = SGD(fa, lr=0.05), SGD(fb, lr=0.05)
+    g = torch.Generator().manual_seed(3)
+    for _ in range(5):
+        x = (torch.rand(n, 4, generator=g) * 2 - 1).cuda()
+        y = torch.randint(0, 3, (n,), generator=g).cuda()
+        la = a.fused_sgd_step(oa, x, y)
+        assert la is not None
+        lb = b.loss(x, y)
+        lb.backward()
+        ob.step()
+        assert abs(float(la) - float(lb)) <= 1e-6 * abs(float(lb)), (float(la), float(lb))
+    torch.testing.assert_close(fa.master, fb.master, atol=1e-6, rtol=1e-6)
+    assert float(oa.step_t) == float(ob.step_t) == 5.0
+    assert torch.count_nonzero(fa.grad) == 0  # the fused step never materialises gradients
