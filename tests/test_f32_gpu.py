@@ -113,6 +113,8 @@ def test_linear_ragged_shapes(M, N, K, dtype):
     from sparkmi.ops.linear import linear
     torch.manual_seed(5)
     lin = torch.nn.Linear(K, N)
+    with torch.no_grad():  # bf16-representable weights: both sides see the same operands (ReLU masks agree)
+        lin.weight.copy_(lin.weight.to(dtype).float())
     ling = torch.nn.Linear(K, N).to(dev)
     ling.load_state_dict(lin.state_dict())
     x = torch.randn(M, K)
