@@ -37,7 +37,7 @@ int smi_ln_bwd_f32(const void*, const void*, const float*, const float*, const f
                    float*, int, float*, float*, int, int, int, const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
 int smi_emb_fwd_f32(const long long*, const void*, const float*, void*, long, int, int, const uint32_t*, uint32_t, uint32_t,
                     float, hipStream_t);
-int smi_emb_bwd_f32(const long long*, const void*, float*, long, int, long long, const uint32_t*, uint32_t, uint32_t, float,
+int smi_emb_bwd_f32(const long long*, const void*, float*, long, int, long long, const uint32_t*, uint32_t, uint32_t, float, long, void*,
                     hipStream_t);
 int smi_attn_fwd(const AttnFwdArgs*, hipStream_t);
 int smi_attn_f32_fwd(const AttnF32Args*, hipStream_t);
@@ -48,7 +48,9 @@ int smi_ce_bwd(const void*, int, const long long*, int, int, long long, const fl
                hipStream_t);
 int smi_emb_fwd(const long long*, const void*, const float*, void*, long, int, int, const uint32_t*, uint32_t, uint32_t, float,
                 hipStream_t);
-int smi_emb_bwd(const long long*, const void*, float*, long, int, long long, const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
+int smi_emb_bwd(const long long*, const void*, float*, long, int, long long, const uint32_t*, uint32_t, uint32_t, float, long,
+                void*, hipStream_t);
+long smi_emb_det_ws_bytes(long, long);
 int smi_bias_act_drop_fwd(const void*, const float*, void*, long, int, int, const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
 int smi_act_drop_bwd(const void*, const void*, void*, long, int, const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
 int smi_act_drop_bwd_f32(const float*, const float*, float*, long, int, const uint32_t*, uint32_t, uint32_t, float,
@@ -80,6 +82,7 @@ int smi_gather_rows(const void*, const long long*, void*, long, long, hipStream_
 int smi_gather_u8_scale(const void*, const long long*, void*, long, long, float, int, hipStream_t);
 int smi_lstm(const LSTMArgs*, int, hipStream_t);
 int smi_lstm_supported(int, int, int, int);
+long smi_lstm_slab_floats(int, int, int, int, int);
 int smi_adam(float*, float*, float*, float*, void*, long, const float*, float*, unsigned*, float, float, float, float, float,
              int, int, hipStream_t);
 int smi_sgd(float*, float*, float*, void*, long, const float*, float*, unsigned*, float, float, float, int, float, int,
@@ -125,9 +128,9 @@ PYBIND11_MODULE(_C, m) {
                         dscale, S(st)), "emb_fwd_f32");
   });
   m.def("emb_bwd_f32", [](u ids, u dout, u dtable, long T, int D, long long pad, u seedp, uint32_t salt, uint32_t thresh,
-                          float dscale, u st) {
+                          float dscale, long V, u ws, u st) {
     chk(smi_emb_bwd_f32((const long long*)ids, P(dout), PF(dtable), T, D, pad, (const uint32_t*)seedp, salt, thresh,
-                        dscale, S(st)), "emb_bwd_f32");
+                        dscale, V, P(ws), S(st)), "emb_bwd_f32");
   });
   m.def("ln_bwd_reduce_multi", [](std::vector<u> pg, std::vector<u> pb, std::vector<u> og, std::vector<u> ob,
                                   std::vector<int> nb, std::vector<int> D, int accumulate, u st) {
@@ -213,9 +216,12 @@ PYBIND11_MODULE(_C, m) {
                       u st) {
     chk(smi_emb_fwd((const long long*)ids, P(table), PF(pe), P(out), T, D, Sp, (const uint32_t*)seedp, salt, thresh, dscale, S(st)), "emb_fwd");
   });
+  // V: table rows; ws: emb_det_ws_bytes(T, V) scratch -> deterministic bucketed backward (0: fp32 atomics)
+  m.def("emb_det_ws_bytes", [](long T, long V) { return smi_emb_det_ws_bytes(T, V); });
   m.def("emb_bwd", [](u ids, u dout, u dtable, long T, int D, long long pad, u seedp, uint32_t salt, uint32_t thresh,
-                      float dscale, u st) {
-    chk(smi_emb_bwd((const long long*)ids, P(dout), PF(dtable), T, D, pad, (const uint32_t*)seedp, salt, thresh, dscale, S(st)), "emb_bwd");
+                      float dscale, long V, u ws, u st) {
+    chk(smi_emb_bwd((const long long*)ids, P(dout), PF(dtable), T, D, pad, (const uint32_t*)seedp, salt, thresh, dscale,
+                    V, P(ws), S(st)), "emb_bwd");
   });
   m.def("bias_act_drop_fwd", [](u x, u bias, u y, long total, int N, int act, u seedp, uint32_t salt, uint32_t thresh,
                                 float dscale, u st) {
@@ -419,13 +425,14 @@ PYBIND11_MODULE(_C, m) {
   });
 
   m.def("lstm_supported", [](int E, int H, int L, int C) { return smi_lstm_supported(E, H, L, C) != 0; });
+  m.def("lstm_slab_floats", [](int B, int E, int H, int L, int C) { return smi_lstm_slab_floats(B, E, H, L, C); });
   // LSTM: pointer lists per layer; dict-free flat signature (forward fills pred/hn/cn/ws,
   // backward reads ws + dpred/dhn/dcn and accumulates into the g_* buffers).
   m.def("lstm", [](int backward, u ids, int B, int T, int E, int H, int L, int C, long long pad_idx, u emb,
                    std::vector<u> w_ih, std::vector<u> w_hh, std::vector<u> b_ih, std::vector<u> b_hh, u w_fc, u b_fc,
                    u h0, u c0, u pred, u hn, u cn, u ws, u ws_da, u seedp, uint32_t salt, uint32_t thresh, float dscale,
                    u dpred, u dhn, u dcn, u g_emb, std::vector<u> g_w_ih, std::vector<u> g_w_hh, std::vector<u> g_b_ih,
-                   std::vector<u> g_b_hh, u g_w_fc, u g_b_fc, u dh0, u dc0, u st) {
+                   std::vector<u> g_b_hh, u g_w_fc, u g_b_fc, u dh0, u dc0, u g_slab, u g_xe, long V, u emb_ws, u st) {
     if (L < 1 || L > LSTM_MAXL || (int)w_ih.size() != L || (int)w_hh.size() != L || (int)b_ih.size() != L ||
         (int)b_hh.size() != L)
       throw std::runtime_error("lstm: need L pointers per weight list");
@@ -448,6 +455,7 @@ PYBIND11_MODULE(_C, m) {
     a.seedp = (const uint32_t*)seedp; a.salt = salt; a.thresh = thresh; a.dscale = dscale;
     a.dpred = (const float*)dpred; a.dhn = (const float*)dhn; a.dcn = (const float*)dcn;
     a.g_emb = (float*)g_emb; a.g_w_fc = (float*)g_w_fc; a.g_b_fc = (float*)g_b_fc; a.dh0 = (float*)dh0; a.dc0 = (float*)dc0;
+    a.g_slab = (float*)g_slab; a.g_xe = (float*)g_xe; a.V = V; a.emb_ws = (void*)emb_ws;
     chk(smi_lstm(&a, backward, S(st)), "lstm");
   });
 }

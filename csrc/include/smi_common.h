@@ -166,3 +166,12 @@ __device__ __forceinline__ bool smi_keep(uint32_t seed, uint32_t idx, uint32_t t
 }
 
 #define SMI_CHECK_LAUNCH() return (int)hipGetLastError()
+
+// Workgroup barrier that orders LDS only: waits for this wave's LDS ops (lgkmcnt) but leaves its
+// global loads / stores in flight (a plain __syncthreads() also drains vmcnt, which exposes the
+// latency of prefetches and of stores nobody in the workgroup reads until much later).
+__device__ __forceinline__ void smi_lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}

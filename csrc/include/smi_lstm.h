@@ -17,7 +17,7 @@ struct LSTMArgs {
   float* pred;                             // [B][T][C]
   float* hn; float* cn;                    // [L][B][H]
   float* ws;                               // saved activations [B][L][T][6H] (i,f,g,o,c,h)
-  float* ws_da;                            // layer-0 gate grads [B][T][4H] (backward scratch)
+  float* ws_da;                            // gate grads [B][L][T][4H] (backward scratch)
   const uint32_t* seedp; uint32_t salt; uint32_t thresh; float dscale;  // inter-layer dropout
   // backward
   const float* dpred; const float* dhn; const float* dcn;
@@ -25,4 +25,10 @@ struct LSTMArgs {
   float* g_b_ih[LSTM_MAXL]; float* g_b_hh[LSTM_MAXL];
   float* g_w_fc; float* g_b_fc;
   float* dh0; float* dc0;
+  // deterministic gradient reduction (backward): per-sequence gradient slab [B][P] (P =
+  // sum_l 4H*(In_l + H + 1) + C*H + C), per-token embedding-input gradients [B][T][E]; V =
+  // embedding rows (bucketed table backward)
+  float* g_slab; float* g_xe; long V; void* emb_ws;  // emb_ws: smi_emb_det_ws_bytes(B*T, V)
 };
+#define LSTM_MAXT 2048
+#define LSTM_TCH 64  // timesteps per LDS-staged chunk in the kernels' tail phases

@@ -5,9 +5,10 @@
 // PE table transformer.py:33-42, precomputed once here instead of per forward) and
 // the LSTM's plain nn.Embedding with padding_idx (distributed_lstm.py:115,128).
 // Forward: one thread per 8 contiguous features (16-B loads of the bf16 table copy), bf16 out.
-// Backward: fp32 atomic adds (runs of equal ids merged first) into the dense fp32 gradient
-// table, rows == padding_idx skipped
-// (that row's gradient stays zero like torch's padding_idx).  Dense semantics are kept on
+// Backward (deterministic): ids are bucketed into position-ordered lists and each id's rows are
+// summed in a fixed order (bit-reproducible, no float atomics; emb_det_* kernels).
+// An fp32-atomic variant (runs of equal ids merged first) is kept for comparison.  Rows ==
+// padding_idx are skipped (that row's gradient stays zero like torch's padding_idx).  Dense semantics are kept on
 // purpose: the reference's Adam decays every row.
 #include "smi_common.h"
 
@@ -97,6 +98,199 @@ __global__ __launch_bounds__(256) void emb_bwd_kernel(const long long* __restric
   }
 }
 
+// ---- deterministic backward: id buckets, position-ordered lists, fixed-order sums -------------
+// Bucket of id v = v % NB (NB chosen so a bucket holds <= EMB_SLOTS ids: slot = v / NB).
+//  1. emb_det_count: per 256-token tile, the token count of every bucket (LDS int histogram);
+//  2. emb_det_scan:  per bucket, exclusive offsets over tiles and the bucket's list start;
+//  3. emb_det_place: every token writes its position to its bucket's list at (tile offset +
+//     its rank among the tile's same-bucket tokens) — lists are in position order;
+//  4. emb_det_sum:   workgroup (bucket, 64-column chunk): wave w sums the list entries
+//     q = w (mod 8) per id slot in LDS (8 loads in flight per wave), the 8 wave partials are
+//     added in wave order, and rows that got tokens are added into the table.
+// Every element is a fixed-order fp32 sum (independent of scheduling): bit-reproducible, no
+// float atomics, and a long run of one id is spread over 8 waves.
+#define EMB_TILE 256
+#define EMB_SLOTS 24
+#define EMB_CW 64
+#define EMB_SW 8  // waves of the sum kernel
+
+struct EmbDet {
+  int tiles, NB;
+  int* counts;  // [tiles][NB]
+  int* offs;    // [tiles][NB]
+  int* bstart;  // [NB + 1]
+  int* list;    // [T]
+};
+
+__device__ __forceinline__ int emb_bucket(long long id, long long pad, int NB) {
+  return (id < 0 || id == pad) ? -1 : (int)(id % NB);
+}
+
+__global__ __launch_bounds__(EMB_TILE) void emb_det_count(const long long* __restrict__ ids, long T, long long pad,
+                                                          EmbDet d) {
+  extern __shared__ int hist[];
+  for (int i = threadIdx.x; i < d.NB; i += EMB_TILE) hist[i] = 0;
+  __syncthreads();
+  const long t = (long)blockIdx.x * EMB_TILE + threadIdx.x;
+  const int bk = t < T ? emb_bucket(ids[t], pad, d.NB) : -1;
+  if (bk >= 0) atomicAdd(&hist[bk], 1);  // integer counts: order-independent
+  __syncthreads();
+  for (int i = threadIdx.x; i < d.NB; i += EMB_TILE) d.counts[(size_t)blockIdx.x * d.NB + i] = hist[i];
+}
+
+__global__ __launch_bounds__(1024) void emb_det_scan(EmbDet d) {
+  __shared__ int wtot[16];
+  __shared__ int carry;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry = 0;
+  for (int b0 = 0; b0 < d.NB; b0 += 1024) {
+    const int b = b0 + threadIdx.x;
+    int run = 0;
+    if (b < d.NB) {
+      int t = 0;
+      for (; t + 8 <= d.tiles; t += 8) {  // 8 independent loads in flight
+        int c[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) c[u] = d.counts[(size_t)(t + u) * d.NB + b];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          d.offs[(size_t)(t + u) * d.NB + b] = run;
+          run += c[u];
+        }
+      }
+      for (; t < d.tiles; ++t) {
+        d.offs[(size_t)t * d.NB + b] = run;
+        run += d.counts[(size_t)t * d.NB + b];
+      }
+    }
+    // block-wide exclusive scan of the bucket totals (wave shuffles, then the 16 wave totals)
+    int inc = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += v;
+    }
+    if (lane == 63) wtot[w] = inc;
+    __syncthreads();
+    int wbase = carry;
+    for (int i = 0; i < w; ++i) wbase += wtot[i];
+    if (b < d.NB) d.bstart[b] = wbase + inc - run;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int c = carry;
+      for (int i = 0; i < 16; ++i) c += wtot[i];
+      carry = c;
+      if (b0 + 1024 >= d.NB) d.bstart[d.NB] = c;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(EMB_TILE) void emb_det_place(const long long* __restrict__ ids, long T, long long pad,
+                                                          EmbDet d) {
+  __shared__ int sb[EMB_TILE];
+  const long t = (long)blockIdx.x * EMB_TILE + threadIdx.x;
+  const int bk = t < T ? emb_bucket(ids[t], pad, d.NB) : -1;
+  sb[threadIdx.x] = bk;
+  __syncthreads();
+  if (bk < 0) return;
+  int rank = 0;
+  for (int i = 0; i < (int)threadIdx.x; ++i) rank += sb[i] == bk;
+  d.list[d.bstart[bk] + d.offs[(size_t)blockIdx.x * d.NB + bk] + rank] = (int)t;
+}
+
+template <typename TS>
+__global__ __launch_bounds__(64 * EMB_SW) void emb_det_sum(const long long* __restrict__ ids,
+                                                           const TS* __restrict__ dout, float* __restrict__ dtable,
+                                                           int D, EmbDet d, const uint32_t* seedp, uint32_t salt,
+                                                           uint32_t thresh, float dscale) {
+  __shared__ float acc[EMB_SW][EMB_SLOTS][EMB_CW];
+  __shared__ unsigned s_mask[EMB_SW];
+  const int bkt = blockIdx.x, c0 = blockIdx.y * EMB_CW, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int beg = d.bstart[bkt], n = d.bstart[bkt + 1] - beg;
+  if (n == 0) return;  // uniform per workgroup
+  const uint32_t seed = thresh ? smi_seed(seedp, salt) : 0u;
+  const int c = c0 + lane;
+  const bool cok = c < D;
+  unsigned mask = 0u;  // slots this wave touched (wave-uniform): rows are zeroed on first touch
+  for (int q0 = w; q0 < n; q0 += 8 * EMB_SW) {  // this wave's entries q0, q0+8, ..., 8 at a time
+    long tt[8];
+    float g[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int q = q0 + u * EMB_SW;
+      tt[u] = q < n ? d.list[beg + q] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) g[u] = (tt[u] >= 0 && cok) ? emb_ld(dout + tt[u] * D + c) : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (tt[u] < 0) break;
+      float v = g[u];
+      if (thresh) v = smi_keep(seed, (uint32_t)(tt[u] * D + c), thresh) ? v * dscale : 0.f;
+      const int slot = (int)(ids[tt[u]] / d.NB);
+      if (!((mask >> slot) & 1u)) {
+        mask |= 1u << slot;
+        acc[w][slot][lane] = v;
+      } else {
+        acc[w][slot][lane] += v;
+      }
+    }
+  }
+  if (lane == 0) s_mask[w] = mask;
+  __syncthreads();
+  unsigned any = 0u;
+#pragma unroll
+  for (int ww = 0; ww < EMB_SW; ++ww) any |= s_mask[ww];
+  // wave w adds the touched slots w, w + 8, ... (partials in wave order) into the table
+  for (int slot = w; slot < EMB_SLOTS; slot += EMB_SW) {
+    if (!((any >> slot) & 1u) || !cok) continue;
+    float s = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < EMB_SW; ++ww)
+      if ((s_mask[ww] >> slot) & 1u) s += acc[ww][slot][lane];
+    dtable[((long)slot * d.NB + bkt) * D + c] += s;
+  }
+}
+
+static int emb_det_nb(long V) {
+  int NB = 1;
+  while ((V + NB - 1) / NB > EMB_SLOTS) NB *= 2;
+  return NB;
+}
+
+extern "C" long smi_emb_det_ws_bytes(long T, long V) {
+  const long tiles = (T + EMB_TILE - 1) / EMB_TILE;
+  const long NB = emb_det_nb(V);
+  return 4 * (2 * tiles * NB + NB + 1 + T) + 64;
+}
+
+template <typename TS>
+static int emb_bwd_launch(const long long* ids, const void* dout, float* dtable, long T, int D, long long padding_idx,
+                          const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, long V, void* ws,
+                          hipStream_t st) {
+  if (ws && V > 0 && T > 0) {
+    EmbDet d{};
+    d.tiles = (int)((T + EMB_TILE - 1) / EMB_TILE);
+    d.NB = emb_det_nb(V);
+    int* p = (int*)ws;
+    d.counts = p; p += (size_t)d.tiles * d.NB;
+    d.offs = p; p += (size_t)d.tiles * d.NB;
+    d.bstart = p; p += d.NB + 1;
+    d.list = p;
+    hipLaunchKernelGGL(emb_det_count, dim3(d.tiles), dim3(EMB_TILE), (size_t)d.NB * 4, st, ids, T, padding_idx, d);
+    hipLaunchKernelGGL(emb_det_scan, dim3(1), dim3(1024), 0, st, d);
+    hipLaunchKernelGGL(emb_det_place, dim3(d.tiles), dim3(EMB_TILE), 0, st, ids, T, padding_idx, d);
+    hipLaunchKernelGGL(emb_det_sum<TS>, dim3(d.NB, (D + EMB_CW - 1) / EMB_CW), dim3(64 * EMB_SW), 0, st, ids,
+                       (const TS*)dout, dtable, D, d, seedp, salt, thresh, dscale);
+    return (int)hipGetLastError();
+  }
+  const long waves = (T + EMB_RUN - 1) / EMB_RUN;
+  hipLaunchKernelGGL(emb_bwd_kernel<TS>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, ids, (const TS*)dout,
+                     dtable, T, D, padding_idx, seedp, salt, thresh, dscale);
+  return (int)hipGetLastError();
+}
+
 extern "C" int smi_emb_fwd(const long long* ids, const void* table, const float* pe, void* out, long T, int D, int S,
                            const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, hipStream_t st) {
   if (D % 8) return -1;
@@ -114,17 +308,15 @@ extern "C" int smi_emb_fwd_f32(const long long* ids, const void* table, const fl
   SMI_CHECK_LAUNCH();
 }
 
+// V: table rows; ws: smi_emb_det_ws_bytes(T, V) bytes of scratch -> deterministic bucketed
+// backward; null -> fp32 atomic adds
 extern "C" int smi_emb_bwd(const long long* ids, const void* dout, float* dtable, long T, int D, long long padding_idx,
-                           const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, hipStream_t st) {
-  const long waves = (T + EMB_RUN - 1) / EMB_RUN;
-  hipLaunchKernelGGL(emb_bwd_kernel<unsigned short>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, ids,
-                     (const unsigned short*)dout, dtable, T, D, padding_idx, seedp, salt, thresh, dscale);
-  SMI_CHECK_LAUNCH();
+                           const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, long V, void* ws,
+                           hipStream_t st) {
+  return emb_bwd_launch<unsigned short>(ids, dout, dtable, T, D, padding_idx, seedp, salt, thresh, dscale, V, ws, st);
 }
 extern "C" int smi_emb_bwd_f32(const long long* ids, const void* dout, float* dtable, long T, int D, long long padding_idx,
-                               const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, hipStream_t st) {
-  const long waves = (T + EMB_RUN - 1) / EMB_RUN;
-  hipLaunchKernelGGL(emb_bwd_kernel<float>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, ids,
-                     (const float*)dout, dtable, T, D, padding_idx, seedp, salt, thresh, dscale);
-  SMI_CHECK_LAUNCH();
+                               const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, long V, void* ws,
+                               hipStream_t st) {
+  return emb_bwd_launch<float>(ids, dout, dtable, T, D, padding_idx, seedp, salt, thresh, dscale, V, ws, st);
 }

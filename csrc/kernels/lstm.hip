@@ -14,13 +14,17 @@
 // layer -> barrier.  Gates, c and h are saved to a workspace for BPTT.
 //
 // Backward runs the ticks in reverse with the layers pipelined the other way (top layer
-// first).  Thread (l, r) accumulates dW_ih[r,:], dW_hh[r,:] and db[r] in registers over all
-// steps (no atomics inside the loop) and holds a slice of W columns for the transposed
-// products dh_{t-1} = W_hh^T da and dx_t = W_ih^T da (2 or 4 threads per output, combined
-// through LDS).  Layer-0 gate grads go to a scratch buffer and the embedding gradient is one
-// parallel W_ih0^T * da pass at the end, scattered into the fp32 table gradient with atomics
-// (rows == padding_idx skipped).  Weight gradients are added atomically into the caller's
-// (flat) fp32 gradient buffers once per sequence.
+// first).  A tick is the recurrence only: the cell backward of unit j (H threads per layer) on
+// terms prepared a tick ahead, then the transposed products dh_{t-1} = W_hh^T da and
+// dx_t = W_ih^T da (thread (l, r) holds a slice of W columns; 2 or 4 threads per output,
+// combined through LDS); two LDS-only barriers per tick.  No global load sits on the critical
+// path: the saved gates / cell state and the head's dpred are prefetched TWO ticks ahead into
+// rotating register sets.
+// The BPTT kernel runs only the recurrence (cell backward + transposed products) and saves every
+// layer's gate gradients; the weight gradients are then a split-K GEMM over all (b, t) with a
+// fixed-order combine (lstm_wgrad_partial / _combine, 128+ workgroups), and the embedding-table
+// gradient the position-ordered bucketed backward of csrc/kernels/embedding.hip over
+// lstm_xe_kernel's per-token W_ih0^T da0.  No float atomics anywhere: bit-reproducible.
 #include "smi_common.h"
 #include "smi_lstm.h"
 
@@ -30,6 +34,16 @@ __device__ __forceinline__ float smi_tanh(float x) {
   const float t = (1.0f - e) / (1.0f + e);
   return copysignf(t, x);
 }
+
+#ifdef LSTM_STAMPS  // diagnostic build only (tools/probes/lstm_probe.hip): per-phase cycle sums
+__device__ unsigned long long lstm_stamps[4][8];
+#define LSTAMP_T(v) do { (v) = clock64(); } while (0)
+#define LSTAMP_ADD(slot, i, t0, t1) do { if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) lstm_stamps[slot][i] += (t1) - (t0); } while (0)
+#else
+#define LSTAMP_T(v) do {} while (0)
+#define LSTAMP_ADD(slot, i, t0, t1) do {} while (0)
+#endif
+
 
 __device__ __forceinline__ uint32_t lstm_drop_idx(int b, int t, int l, int j, int T, int L, int H) {
   return (uint32_t)((((size_t)b * T + t) * L + l) * H + j);
@@ -46,6 +60,8 @@ __global__ __launch_bounds__(NT) void lstm_fwd_kernel(LSTMArgs a) {
   __shared__ __attribute__((aligned(16))) float s_in[LSTM_MAXL][MI];
   __shared__ __attribute__((aligned(16))) float s_h[LSTM_MAXL][H];
   __shared__ float s_g[LSTM_MAXL][G];
+  __shared__ long long s_ids[LSTM_MAXT];
+  for (int i = tid; i < T; i += blockDim.x) s_ids[i] = a.ids[(size_t)b * T + i];
 
   float wi[MI], wh[H], bias = 0.f;
 #pragma unroll
@@ -60,15 +76,20 @@ __global__ __launch_bounds__(NT) void lstm_fwd_kernel(LSTMArgs a) {
     c = a.c0 ? a.c0[((size_t)l * a.B + b) * H + r] : 0.f;
     s_h[l][r] = a.h0 ? a.h0[((size_t)l * a.B + b) * H + r] : 0.f;
   }
-  const long long* ids = a.ids + (size_t)b * T;
-  for (int e = tid; e < E; e += blockDim.x) s_in[0][e] = a.emb[(size_t)ids[0] * E + e];
+  __syncthreads();  // s_ids
+  // layer-0 input rows, prefetched two ticks ahead (thread e < E owns feature e)
+  auto emb_at = [&](int t) { return (tid < E && t < T) ? a.emb[(size_t)s_ids[t] * E + tid] : 0.f; };
+  if (tid < E) s_in[0][tid] = emb_at(0);
+  // next-tick inputs rotate through three registers (X[(k+1)%3] is written at tick k, X[k%3]
+  // reloaded): no register copies, so no wait on a load issued in the same tick
+  float x0 = 0.f, x1 = emb_at(1), x2 = emb_at(2);
   __syncthreads();
 
   const uint32_t seed = smi_seed(a.seedp, a.salt);
   const int gate = r / H;  // 0 i, 1 f, 2 g, 3 o
   float* wsb = a.ws + (size_t)b * L * T * 6 * H;
   const int nt = T + L - 1;
-  for (int k = 0; k < nt; ++k) {
+  auto tick = [&](int k, float& xnext, float& xload) {
     const int t = k - l;
     const bool on = act && t >= 0 && t < T;
     if (on) {
@@ -86,7 +107,7 @@ __global__ __launch_bounds__(NT) void lstm_fwd_kernel(LSTMArgs a) {
       const float z = (s0 + s1) + (s2 + s3);
       s_g[l][r] = gate == 2 ? smi_tanh(z) : smi_sigmoid(z);
     }
-    __syncthreads();
+    smi_lds_barrier();
     if (on && r < H) {
       const float ig = s_g[l][r], fg = s_g[l][H + r], gg = s_g[l][2 * H + r], og = s_g[l][3 * H + r];
       c = fg * c + ig * gg;
@@ -100,28 +121,62 @@ __global__ __launch_bounds__(NT) void lstm_fwd_kernel(LSTMArgs a) {
         s_in[l + 1][r] = hd;
       }
     }
-    if (k + 1 < T)  // layer 0's input for the next tick (s_in[0] was consumed before the barrier)
-      for (int e = tid; e < E; e += blockDim.x) s_in[0][e] = a.emb[(size_t)ids[k + 1] * E + e];
-    __syncthreads();
+    if (tid < E) {  // layer 0's input for the next tick (s_in[0] was consumed before the barrier)
+      s_in[0][tid] = xnext;
+      xload = emb_at(k + 3);
+    }
+    smi_lds_barrier();
+  };
+  int k = 0;
+  for (; k + 3 <= nt; k += 3) {
+    tick(k, x1, x0);
+    tick(k + 1, x2, x1);
+    tick(k + 2, x0, x2);
   }
+  if (k < nt) tick(k, x1, x0);
+  if (k + 1 < nt) tick(k + 1, x2, x1);
+  __syncthreads();  // ws (global) written by every cell thread is read by the fc head below
   if (act && r < H) {
     if (a.hn) a.hn[((size_t)l * a.B + b) * H + r] = s_h[l][r];
     if (a.cn) a.cn[((size_t)l * a.B + b) * H + r] = c;
   }
-  // fc head at every step (reads this workgroup's own workspace writes, ordered by the barrier)
-  const float* top = wsb + (size_t)(L - 1) * T * 6 * H + 5 * H;
-  for (int o = tid; o < T * C; o += blockDim.x) {
-    const int t = o / C, cc = o % C;
-    float s = a.b_fc[cc];
-    const float* hv = top + (size_t)t * 6 * H;
-    const float* wv = a.w_fc + (size_t)cc * H;
-#pragma unroll 8
-    for (int j = 0; j < H; ++j) s += wv[j] * hv[j];
-    a.pred[((size_t)b * T + t) * C + cc] = s;
+  // fc head at every step, from LDS-staged chunks of the top layer's h (coalesced loads, many in
+  // flight; a per-output global dot product would serialise on load latency)
+  {
+    __shared__ float s_top[LSTM_TCH * H];
+    __shared__ float s_wfc[LSTM_MAXC * H];
+    const float* top = wsb + (size_t)(L - 1) * T * 6 * H + 5 * H;
+    for (int i = tid; i < C * H; i += blockDim.x) s_wfc[i] = a.w_fc[i];
+    for (int t0 = 0; t0 < T; t0 += LSTM_TCH) {
+      const int nc = min(LSTM_TCH, T - t0);
+      __syncthreads();
+      for (int i = tid; i < nc * H; i += blockDim.x) s_top[i] = top[(size_t)(t0 + i / H) * 6 * H + i % H];
+      __syncthreads();
+      for (int o = tid; o < nc * C; o += blockDim.x) {
+        const int t = o / C, cc = o % C;
+        float s0 = a.b_fc[cc], s1 = 0.f;
+#pragma unroll
+        for (int j = 0; j < H; j += 2) {
+          s0 += s_wfc[cc * H + j] * s_top[t * H + j];
+          s1 += s_wfc[cc * H + j + 1] * s_top[t * H + j + 1];
+        }
+        a.pred[((size_t)b * T + t0 + t) * C + cc] = s0 + s1;
+      }
+    }
   }
 }
 
-template <int H, int MI, int NT>
+// what a cell thread consumes at one backward tick, loaded two ticks ahead (CM >= C head outputs:
+// 4 for the reference's 4 classes, so three in-flight sets stay small — register pressure is
+// what bounds this kernel's tick)
+template <int CM>
+struct LstmBwdIn {
+  float ig, fg, gg, og, cc, cp;  // raw: loaded two ticks ahead
+  float dp[CM];
+  float A, Bo, gi, cf, ig2, fct, dm;  // derived one tick ahead (prep), off the dependent chain
+};
+
+template <int H, int MI, int NT, int CM>
 __global__ __launch_bounds__(NT) void lstm_bwd_kernel(LSTMArgs a) {
   constexpr int G = 4 * H;
   const int b = blockIdx.x, tid = threadIdx.x;
@@ -129,12 +184,11 @@ __global__ __launch_bounds__(NT) void lstm_bwd_kernel(LSTMArgs a) {
   const int l = tid / G, r = tid % G;
   const bool act = l < L;
   const int In = l == 0 ? E : H;
-  __shared__ __attribute__((aligned(16))) float s_x[LSTM_MAXL][MI];
-  __shared__ __attribute__((aligned(16))) float s_hp[LSTM_MAXL][H];
   __shared__ __attribute__((aligned(16))) float s_da[LSTM_MAXL][G];
   __shared__ float s_part[LSTM_MAXL][G];
   __shared__ float s_dhr[LSTM_MAXL][H];
-  __shared__ float s_dxu[LSTM_MAXL][H];
+  __shared__ long long s_ids[LSTM_MAXT];
+  for (int i = tid; i < T; i += blockDim.x) s_ids[i] = a.ids[(size_t)b * T + i];
 
   // transposed-product assignment: l >= 1: output o = r % 2H (o < H: dh via W_hh col o, else dx
   // via W_ih col o-H) over gate rows [part*2H, part*2H+2H); l == 0: o = r % H (dh only) over
@@ -151,134 +205,274 @@ __global__ __launch_bounds__(NT) void lstm_bwd_kernel(LSTMArgs a) {
     }
     wc[q] = v;
   }
-  float dWi[MI], dWh[H], db = 0.f;
+  const bool cell = act && r < H, top = l == L - 1;
+  float wfc[CM];  // head column j (top-layer cell threads)
 #pragma unroll
-  for (int i = 0; i < MI; ++i) dWi[i] = 0.f;
-#pragma unroll
-  for (int i = 0; i < H; ++i) dWh[i] = 0.f;
+  for (int q = 0; q < CM; ++q) wfc[q] = (cell && top && q < C) ? a.w_fc[(size_t)q * H + r] : 0.f;
 
-  for (int i = tid; i < LSTM_MAXL * MI; i += blockDim.x) (&s_x[0][0])[i] = 0.f;
   float dc = 0.f;
-  if (act && r < H) {
+  if (cell) {
     dc = a.dcn ? a.dcn[((size_t)l * a.B + b) * H + r] : 0.f;
     s_dhr[l][r] = a.dhn ? a.dhn[((size_t)l * a.B + b) * H + r] : 0.f;
-    s_dxu[l][r] = 0.f;
   }
-  __syncthreads();
+  __syncthreads();  // s_ids
 
   const uint32_t seed = smi_seed(a.seedp, a.salt);
-  const long long* ids = a.ids + (size_t)b * T;
   const float* wsb = a.ws + (size_t)b * L * T * 6 * H;
   const float* dpred = a.dpred + (size_t)b * T * C;
-  float* dab = a.ws_da + (size_t)b * T * G;
+  float* dab = a.ws_da + (size_t)b * L * T * G;  // gate gradients of every layer [L][T][4H]
   const int nt = T + L - 1;
-  for (int k = 0; k < nt; ++k) {
-    const int t = T - 1 - k + (L - 1 - l);
+  const int tl = T - 1 + (L - 1 - l);  // this layer's step at tick k is tl - k
+  auto load_in = [&](int t, LstmBwdIn<CM>& v) {
+    if (!cell || t < 0 || t >= T) return;
+    const int j = r;
+    const float* w = wsb + ((size_t)l * T + t) * 6 * H;
+    v.ig = w[j]; v.fg = w[H + j]; v.gg = w[2 * H + j]; v.og = w[3 * H + j]; v.cc = w[4 * H + j];
+    v.cp = t > 0 ? w[j - 2 * H] : (a.c0 ? a.c0[((size_t)l * a.B + b) * H + j] : 0.f);
+    if (top) {
+#pragma unroll
+      for (int q = 0; q < CM; ++q) v.dp[q] = q < C ? dpred[(size_t)t * C + q] : 0.f;
+    }
+  };
+  // everything of step t's cell backward that does not depend on the incoming dh / dc
+  auto prep = [&](int t, LstmBwdIn<CM>& v) {
+    if (!cell || t < 0 || t >= T) return;
+    const float tc = smi_tanh(v.cc);
+    v.A = v.og * (1.f - tc * tc);
+    v.Bo = tc * v.og * (1.f - v.og);
+    v.gi = v.gg * v.ig * (1.f - v.ig);
+    v.cf = v.cp * v.fg * (1.f - v.fg);
+    v.ig2 = v.ig * (1.f - v.gg * v.gg);
+    float f = 0.f;
+    if (top) {
+#pragma unroll
+      for (int q = 0; q < CM; ++q) f += wfc[q] * v.dp[q];
+    }
+    v.fct = f;
+    v.dm = top ? 0.f : (a.thresh ? (smi_keep(seed, lstm_drop_idx(b, t, l, r, T, L, H), a.thresh) ? a.dscale : 0.f) : 1.f);
+  };
+  // The tick is the recurrence only: cell backward -> da (LDS + global) -> transposed products.
+  // The weight gradients dW = sum_t da_t^T [x_t | h_{t-1}] are a GEMM over the saved da after
+  // the loop, off the serial critical path.  Per-tick inputs rotate through three register sets
+  // (no copies, no same-tick load waits); two LDS barriers per tick, the recurrent dh and the dx
+  // handed down by the layer above are read straight from s_part (the previous tick's products).
+  LstmBwdIn<CM> ia{}, ib{}, ic{};
+  load_in(tl, ia);
+  load_in(tl - 1, ib);
+  prep(tl, ia);
+  auto own_dh = [&](int j) {
+    return l >= 1 ? s_part[l][j] + s_part[l][2 * H + j]
+                  : (s_part[0][j] + s_part[0][H + j]) + (s_part[0][2 * H + j] + s_part[0][3 * H + j]);
+  };
+  auto tick = [&](int k, const LstmBwdIn<CM>& cv, LstmBwdIn<CM>& pv, LstmBwdIn<CM>& nv) {
+    const int t = tl - k;
     const bool on = act && t >= 0 && t < T;
-    if (on && r < H) {  // cell backward for unit j = r
+    long long c_0 = 0, c_1 = 0, c_2 = 0, c_3 = 0, c_4 = 0;
+    (void)c_0; (void)c_1; (void)c_2; (void)c_3; (void)c_4;
+    LSTAMP_T(c_0);
+    load_in(t - 2, nv);  // in flight during this tick and the next
+    if (on && r < H) {  // cell backward for unit j = r: a short chain on top of prep()'d terms
       const int j = r;
-      const float* w = wsb + ((size_t)l * T + t) * 6 * H;
-      const float ig = w[j], fg = w[H + j], gg = w[2 * H + j], og = w[3 * H + j], cc = w[4 * H + j];
-      float cp, hp;
-      if (t > 0) { cp = w[j + 4 * H - 6 * H]; hp = w[j + 5 * H - 6 * H]; }
-      else {
-        cp = a.c0 ? a.c0[((size_t)l * a.B + b) * H + j] : 0.f;
-        hp = a.h0 ? a.h0[((size_t)l * a.B + b) * H + j] : 0.f;
-      }
-      float dh = s_dhr[l][j];
-      if (l == L - 1) {
-        for (int q = 0; q < C; ++q) dh += a.w_fc[(size_t)q * H + j] * dpred[(size_t)t * C + q];
+      float dh = t == T - 1 ? s_dhr[l][j] : own_dh(j);
+      dh += top ? cv.fct : (s_part[l + 1][H + j] + s_part[l + 1][3 * H + j]) * cv.dm;  // head / dx from above
+      dc += dh * cv.A;
+      const float d0 = dc * cv.gi, d1 = dc * cv.cf, d2 = dc * cv.ig2, d3 = dh * cv.Bo;
+      s_da[l][j] = d0; s_da[l][H + j] = d1; s_da[l][2 * H + j] = d2; s_da[l][3 * H + j] = d3;
+      float* dg = dab + ((size_t)l * T + t) * G;
+      dg[j] = d0; dg[H + j] = d1; dg[2 * H + j] = d2; dg[3 * H + j] = d3;
+      dc *= cv.fg;
+    }
+    LSTAMP_T(c_1);
+    smi_lds_barrier();
+    LSTAMP_T(c_2);
+    prep(t - 1, pv);  // next tick's terms (loaded last tick): independent work the compiler
+                      // interleaves with the transposed products below
+    if (on) {  // transposed products, 8 independent partial sums (short FMA chains)
+      float p[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (l == 0) {
+#pragma unroll
+        for (int q = 0; q < H; q += 8) {
+          const float4 d4 = *(const float4*)&s_da[0][row0 + q];
+          const float4 e4 = *(const float4*)&s_da[0][row0 + q + 4];
+          p[0] += wc[q] * d4.x; p[1] += wc[q + 1] * d4.y; p[2] += wc[q + 2] * d4.z; p[3] += wc[q + 3] * d4.w;
+          p[4] += wc[q + 4] * e4.x; p[5] += wc[q + 5] * e4.y; p[6] += wc[q + 6] * e4.z; p[7] += wc[q + 7] * e4.w;
+        }
       } else {
-        dh += s_dxu[l][j];
-      }
-      const float tc = smi_tanh(cc);
-      const float d_o = dh * tc;
-      dc += dh * og * (1.f - tc * tc);
-      s_da[l][j] = dc * gg * ig * (1.f - ig);
-      s_da[l][H + j] = dc * cp * fg * (1.f - fg);
-      s_da[l][2 * H + j] = dc * ig * (1.f - gg * gg);
-      s_da[l][3 * H + j] = d_o * og * (1.f - og);
-      dc *= fg;
-      s_hp[l][j] = hp;
-      if (l >= 1) {
-        const float hx = wsb[((size_t)(l - 1) * T + t) * 6 * H + 5 * H + j];
-        s_x[l][j] = a.thresh ? (smi_keep(seed, lstm_drop_idx(b, t, l - 1, j, T, L, H), a.thresh) ? hx * a.dscale : 0.f)
-                             : hx;
-      }
-    }
-    if (on && l == 0)
-      for (int e = r; e < E; e += G) s_x[0][e] = a.emb[(size_t)ids[t] * E + e];
-    __syncthreads();
-    if (on) {
-      const float da = s_da[l][r];
 #pragma unroll
-      for (int i = 0; i < MI; i += 4) {
-        const float4 x = *(const float4*)&s_x[l][i];
-        dWi[i] += da * x.x; dWi[i + 1] += da * x.y; dWi[i + 2] += da * x.z; dWi[i + 3] += da * x.w;
+        for (int q = 0; q < 2 * H; q += 8) {
+          const float4 d4 = *(const float4*)&s_da[l][row0 + q];
+          const float4 e4 = *(const float4*)&s_da[l][row0 + q + 4];
+          p[0] += wc[q] * d4.x; p[1] += wc[q + 1] * d4.y; p[2] += wc[q + 2] * d4.z; p[3] += wc[q + 3] * d4.w;
+          p[4] += wc[q + 4] * e4.x; p[5] += wc[q + 5] * e4.y; p[6] += wc[q + 6] * e4.z; p[7] += wc[q + 7] * e4.w;
+        }
       }
-#pragma unroll
-      for (int i = 0; i < H; i += 4) {
-        const float4 x = *(const float4*)&s_hp[l][i];
-        dWh[i] += da * x.x; dWh[i + 1] += da * x.y; dWh[i + 2] += da * x.z; dWh[i + 3] += da * x.w;
-      }
-      db += da;
-      float p0 = 0.f, p1 = 0.f;
-#pragma unroll
-      for (int q = 0; q < 2 * H; q += 2) {
-        if (q < nq) { p0 += wc[q] * s_da[l][row0 + q]; p1 += wc[q + 1] * s_da[l][row0 + q + 1]; }
-      }
-      s_part[l][r] = p0 + p1;
-      if (l == 0) dab[(size_t)t * G + r] = da;
+      s_part[l][r] = ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
     }
-    __syncthreads();
-    if (on && r < H) {
-      const int j = r;
-      if (l >= 1) {
-        s_dhr[l][j] = s_part[l][j] + s_part[l][2 * H + j];
-        const float dx = s_part[l][H + j] + s_part[l][3 * H + j];
-        s_dxu[l - 1][j] = a.thresh ? (smi_keep(seed, lstm_drop_idx(b, t, l - 1, j, T, L, H), a.thresh) ? dx * a.dscale : 0.f)
-                                   : dx;
-      } else {
-        s_dhr[0][j] = (s_part[0][j] + s_part[0][H + j]) + (s_part[0][2 * H + j] + s_part[0][3 * H + j]);
-      }
-    }
-    __syncthreads();
+    LSTAMP_T(c_3);
+    smi_lds_barrier();
+    LSTAMP_T(c_4);
+    LSTAMP_ADD(threadIdx.x >> 6, 0, c_0, c_1);
+    LSTAMP_ADD(threadIdx.x >> 6, 1, c_1, c_2);
+    LSTAMP_ADD(threadIdx.x >> 6, 2, c_2, c_3);
+    LSTAMP_ADD(threadIdx.x >> 6, 3, c_3, c_4);
+  };
+  long long cl0 = 0, cl1 = 0;
+  (void)cl0; (void)cl1;
+  LSTAMP_T(cl0);
+  int k = 0;
+  for (; k + 3 <= nt; k += 3) {
+    tick(k, ia, ib, ic);
+    tick(k + 1, ib, ic, ia);
+    tick(k + 2, ic, ia, ib);
   }
-  if (act && r < H) {
-    if (a.dh0) a.dh0[((size_t)l * a.B + b) * H + r] = s_dhr[l][r];
+  if (k < nt) tick(k, ia, ib, ic);
+  if (k + 1 < nt) tick(k + 1, ib, ic, ia);
+  __syncthreads();  // dab (global) is read across threads below
+  LSTAMP_T(cl1);
+  LSTAMP_ADD(threadIdx.x >> 6, 4, cl0, cl1);
+  if (cell) {
+    if (a.dh0) a.dh0[((size_t)l * a.B + b) * H + r] = own_dh(r);  // W_hh^T da at t = 0
     if (a.dc0) a.dc0[((size_t)l * a.B + b) * H + r] = dc;
   }
-  if (act) {
-    float* gwi = a.g_w_ih[l] + (size_t)r * In;
+
+}
+
+// ---- weight gradients, off the recurrence: for every layer l,
+//   [dW_ih | dW_hh | db][r, :] = sum_{b,t} da[b,l,t,r] * [x_t | h_{t-1} | 1]
+// and for the head [dW_fc | db_fc][c, :] = sum_{b,t} dpred[b,t,c] * [h_top(t) | 1].
+// The B*T (b,t) reduction is split into LSTM_KS fixed chunks; workgroup (chunk, row block, layer)
+// writes its partial tile, lstm_wgrad_combine sums the chunks in order (bit-reproducible) into
+// the gradient buffers.  128+ workgroups instead of the recurrence kernel's 32 doing it serially.
+#define LSTM_KS 64
+#define LSTM_RB 32    // gate rows per workgroup
+#define LSTM_WC 72    // padded columns (In + H + 1 <= 129 handled in column passes)
+#define LSTM_KSUB 64  // (b,t) rows staged per LDS round
+
+__host__ __device__ __forceinline__ int lstm_cols(const LSTMArgs& a, int l) {
+  return l < a.L ? (l == 0 ? a.E : a.H) + a.H + 1 : a.H + 1;
+}
+__host__ __device__ __forceinline__ int lstm_rows(const LSTMArgs& a, int l) { return l < a.L ? 4 * a.H : a.C; }
+// partial-tile scratch offset of (layer l, chunk s): [l][s][rows][cols]
+__host__ __device__ __forceinline__ long lstm_part_off(const LSTMArgs& a, int l, int s) {
+  long off = 0;
+  for (int i = 0; i < l; ++i) off += (long)LSTM_KS * lstm_rows(a, i) * lstm_cols(a, i);
+  return off + (long)s * lstm_rows(a, l) * lstm_cols(a, l);
+}
+
+__global__ __launch_bounds__(256) void lstm_wgrad_partial(LSTMArgs a) {
+  const int s = blockIdx.x, rb = blockIdx.y, l = blockIdx.z;
+  const int L = a.L, T = a.T, H = a.H, E = a.E, C = a.C, G = 4 * H;
+  const int rows = lstm_rows(a, l), cols = lstm_cols(a, l);
+  const int r0 = rb * LSTM_RB;
+  if (r0 >= rows) return;  // uniform per workgroup
+  const int nr = min(LSTM_RB, rows - r0);
+  const long BT = (long)a.B * T, kc = (BT + LSTM_KS - 1) / LSTM_KS;
+  const long k0 = (long)s * kc, k1 = min(BT, k0 + kc);
+  __shared__ float s_d[LSTM_KSUB][LSTM_RB];
+  __shared__ float s_x[LSTM_KSUB][LSTM_WC + 1];
+  const int tid = threadIdx.x, ri = tid >> 3, cg = tid & 7;
+  const uint32_t seed = smi_seed(a.seedp, a.salt);
+  for (int c0 = 0; c0 < cols; c0 += LSTM_WC) {  // column passes of LSTM_WC
+    const int ncol = min(LSTM_WC, cols - c0);
+    float acc[LSTM_WC / 8];
 #pragma unroll
-    for (int i = 0; i < MI; ++i) if (i < In) atomicAdd(gwi + i, dWi[i]);
-    float* gwh = a.g_w_hh[l] + (size_t)r * H;
+    for (int m = 0; m < LSTM_WC / 8; ++m) acc[m] = 0.f;
+    for (long kb = k0; kb < k1; kb += LSTM_KSUB) {
+      const int nk = (int)min((long)LSTM_KSUB, k1 - kb);
+      __syncthreads();
+      for (int i = tid; i < nk * LSTM_RB; i += 256) {
+        const int kk = i / LSTM_RB, rr = i % LSTM_RB;
+        const long bt = kb + kk;
+        const int b = (int)(bt / T), t = (int)(bt % T);
+        float v = 0.f;
+        if (rr < nr) v = l < L ? a.ws_da[(((size_t)b * L + l) * T + t) * G + r0 + rr]
+                               : a.dpred[((size_t)b * T + t) * C + r0 + rr];
+        s_d[kk][rr] = v;
+      }
+      for (int i = tid; i < nk * LSTM_WC; i += 256) {
+        const int kk = i / LSTM_WC, cc = i % LSTM_WC, c = c0 + cc;
+        const long bt = kb + kk;
+        const int b = (int)(bt / T), t = (int)(bt % T);
+        const float* wsb = a.ws + (size_t)b * L * T * 6 * H;
+        float v = 0.f;
+        if (c < cols) {
+          if (l == L) {  // head: [h_top(t) | 1]
+            v = c < H ? wsb[((size_t)(L - 1) * T + t) * 6 * H + 5 * H + c] : 1.f;
+          } else {
+            const int In = l == 0 ? E : H;
+            if (c < In) {  // x_t: embedding row, or the (dropped-out) output of the layer below
+              if (l == 0) v = a.emb[(size_t)a.ids[(size_t)b * T + t] * E + c];
+              else {
+                const float hx = wsb[((size_t)(l - 1) * T + t) * 6 * H + 5 * H + c];
+                v = a.thresh ? (smi_keep(seed, lstm_drop_idx(b, t, l - 1, c, T, L, H), a.thresh) ? hx * a.dscale : 0.f)
+                             : hx;
+              }
+            } else if (c < In + H) {  // h_{t-1}
+              const int j = c - In;
+              v = t > 0 ? wsb[((size_t)l * T + t - 1) * 6 * H + 5 * H + j] : (a.h0 ? a.h0[((size_t)l * a.B + b) * H + j] : 0.f);
+            } else {
+              v = 1.f;  // bias column
+            }
+          }
+        }
+        s_x[kk][cc] = v;
+      }
+      __syncthreads();
+      for (int kk = 0; kk < nk; ++kk) {
+        const float d = s_d[kk][ri];
 #pragma unroll
-    for (int i = 0; i < H; ++i) atomicAdd(gwh + i, dWh[i]);
-    atomicAdd(a.g_b_ih[l] + r, db);
-    atomicAdd(a.g_b_hh[l] + r, db);
-  }
-  // fc head grads: dW_fc[c][j] = sum_t dpred[t][c] * h_top(t)[j]; db_fc[c] = sum_t dpred[t][c]
-  const float* top = wsb + (size_t)(L - 1) * T * 6 * H + 5 * H;
-  for (int q = tid; q < C * (H + 1); q += blockDim.x) {
-    const int cc = q / (H + 1), j = q % (H + 1);
-    float s = 0.f;
-    if (j < H) { for (int t = 0; t < T; ++t) s += dpred[(size_t)t * C + cc] * top[(size_t)t * 6 * H + j]; atomicAdd(a.g_w_fc + (size_t)cc * H + j, s); }
-    else { for (int t = 0; t < T; ++t) s += dpred[(size_t)t * C + cc]; atomicAdd(a.g_b_fc + cc, s); }
-  }
-  // embedding grads: d emb[ids[t]] += W_ih0^T da0(t)   (scratch written above by this workgroup)
-  if (a.g_emb) {
-    for (int q = tid; q < T * E; q += blockDim.x) {
-      const int t = q / E, e = q % E;
-      const long long id = ids[t];
-      if (id == a.pad_idx) continue;
-      const float* dv = dab + (size_t)t * G;
-      const float* wv = a.w_ih[0] + e;
-      float s0 = 0.f, s1 = 0.f;
-      for (int rr = 0; rr < G; rr += 2) { s0 += wv[(size_t)rr * E] * dv[rr]; s1 += wv[(size_t)(rr + 1) * E] * dv[rr + 1]; }
-      atomicAdd(a.g_emb + (size_t)id * E + e, s0 + s1);
+        for (int m = 0; m < LSTM_WC / 8; ++m) acc[m] += d * s_x[kk][cg + 8 * m];
+      }
+    }
+    if (ri < nr) {
+      float* out = a.g_slab + lstm_part_off(a, l, s) + (size_t)(r0 + ri) * cols + c0;
+#pragma unroll
+      for (int m = 0; m < LSTM_WC / 8; ++m)
+        if (cg + 8 * m < ncol) out[cg + 8 * m] = acc[m];
     }
   }
+}
+
+__global__ __launch_bounds__(256) void lstm_wgrad_combine(LSTMArgs a) {
+  const int l = blockIdx.y;
+  const int rows = lstm_rows(a, l), cols = lstm_cols(a, l);
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= (long)rows * cols) return;
+  const int r = (int)(p / cols), c = (int)(p % cols);
+  float v = 0.f;
+  for (int s = 0; s < LSTM_KS; ++s) v += a.g_slab[lstm_part_off(a, l, s) + p];  // chunk order
+  if (l == a.L) {
+    if (c < a.H) a.g_w_fc[(size_t)r * a.H + c] += v;
+    else a.g_b_fc[r] += v;
+    return;
+  }
+  const int In = l == 0 ? a.E : a.H;
+  if (c < In) a.g_w_ih[l][(size_t)r * In + c] += v;
+  else if (c < In + a.H) a.g_w_hh[l][(size_t)r * a.H + (c - In)] += v;
+  else {
+    a.g_b_ih[l][r] += v;
+    a.g_b_hh[l][r] += v;
+  }
+}
+
+// per-token embedding-input gradients xe[b,t,:] = W_ih0^T da0[b,t,:] (the table gradient is their
+// position-ordered per-id sum, csrc/kernels/embedding.hip)
+__global__ __launch_bounds__(256) void lstm_xe_kernel(LSTMArgs a) {
+  const long q = (long)blockIdx.x * 256 + threadIdx.x;
+  const long BT = (long)a.B * a.T;
+  if (q >= BT * a.E) return;
+  const long bt = q / a.E;
+  const int e = (int)(q % a.E), b = (int)(bt / a.T), t = (int)(bt % a.T), G = 4 * a.H;
+  const float* d = a.ws_da + (((size_t)b * a.L) * a.T + t) * G;  // layer 0
+  const float* w = a.w_ih[0] + e;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  for (int r = 0; r < G; r += 4) {
+    s0 += w[(size_t)r * a.E] * d[r];
+    s1 += w[(size_t)(r + 1) * a.E] * d[r + 1];
+    s2 += w[(size_t)(r + 2) * a.E] * d[r + 2];
+    s3 += w[(size_t)(r + 3) * a.E] * d[r + 3];
+  }
+  a.g_xe[q] = (s0 + s1) + (s2 + s3);
 }
 
 // 4*H*L <= 256 threads: one wave per SIMD, so the backward's register-resident gradient rows
@@ -287,10 +481,16 @@ template <int H, int MI>
 static int lstm_launch(const LSTMArgs* a, int backward, hipStream_t st) {
   const int threads = ((4 * H * a->L + 63) / 64) * 64;
   if (threads <= 256) {
-    if (backward) hipLaunchKernelGGL((lstm_bwd_kernel<H, MI, 256>), dim3(a->B), dim3(threads), 0, st, *a);
+    if (backward) {
+      if (a->C <= 4) hipLaunchKernelGGL((lstm_bwd_kernel<H, MI, 256, 4>), dim3(a->B), dim3(threads), 0, st, *a);
+      else hipLaunchKernelGGL((lstm_bwd_kernel<H, MI, 256, LSTM_MAXC>), dim3(a->B), dim3(threads), 0, st, *a);
+    }
     else hipLaunchKernelGGL((lstm_fwd_kernel<H, MI, 256>), dim3(a->B), dim3(threads), 0, st, *a);
   } else {
-    if (backward) hipLaunchKernelGGL((lstm_bwd_kernel<H, MI, 512>), dim3(a->B), dim3(threads), 0, st, *a);
+    if (backward) {
+      if (a->C <= 4) hipLaunchKernelGGL((lstm_bwd_kernel<H, MI, 512, 4>), dim3(a->B), dim3(threads), 0, st, *a);
+      else hipLaunchKernelGGL((lstm_bwd_kernel<H, MI, 512, LSTM_MAXC>), dim3(a->B), dim3(threads), 0, st, *a);
+    }
     else hipLaunchKernelGGL((lstm_fwd_kernel<H, MI, 512>), dim3(a->B), dim3(threads), 0, st, *a);
   }
   return (int)hipGetLastError();
@@ -305,11 +505,41 @@ extern "C" int smi_lstm_supported(int E, int H, int L, int C) {
   return 1;
 }
 
+extern "C" int smi_emb_bwd_f32(const long long* ids, const void* dout, float* dtable, long T, int D, long long padding_idx,
+                               const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, long V, void* ws,
+                               hipStream_t st);
+
+extern "C" long smi_lstm_slab_floats(int B, int E, int H, int L, int C) {
+  LSTMArgs a{};
+  a.B = B; a.E = E; a.H = H; a.L = L; a.C = C;
+  return lstm_part_off(a, L + 1, 0);  // partial tiles of every layer and the head
+}
+
 extern "C" int smi_lstm(const LSTMArgs* a, int backward, hipStream_t st) {
-  if (!smi_lstm_supported(a->E, a->H, a->L, a->C) || a->B < 1 || a->T < 1) return -1;
+  if (!smi_lstm_supported(a->E, a->H, a->L, a->C) || a->B < 1 || a->T < 1 || a->T > LSTM_MAXT) return -1;
+  if (backward && (!a->g_slab || (a->g_emb && (!a->g_xe || a->V < 1 || !a->emb_ws)))) return -1;
   const int H = a->H;
   const bool wide = a->E > H;
-  if (H == 16) return wide ? lstm_launch<16, 32>(a, backward, st) : lstm_launch<16, 16>(a, backward, st);
-  if (H == 32) return wide ? lstm_launch<32, 64>(a, backward, st) : lstm_launch<32, 32>(a, backward, st);
-  return lstm_launch<64, 64>(a, backward, st);
+  int rc;
+  if (H == 16) rc = wide ? lstm_launch<16, 32>(a, backward, st) : lstm_launch<16, 16>(a, backward, st);
+  else if (H == 32) rc = wide ? lstm_launch<32, 64>(a, backward, st) : lstm_launch<32, 32>(a, backward, st);
+  else rc = lstm_launch<64, 64>(a, backward, st);
+  if (rc || !backward) return rc;
+  const int maxrows = 4 * H > a->C ? 4 * H : a->C;
+  hipLaunchKernelGGL(lstm_wgrad_partial, dim3(LSTM_KS, (maxrows + LSTM_RB - 1) / LSTM_RB, a->L + 1), dim3(256), 0, st,
+                     *a);
+  int maxout = 0;
+  for (int l = 0; l <= a->L; ++l) {
+    const int n = lstm_rows(*a, l) * lstm_cols(*a, l);
+    if (n > maxout) maxout = n;
+  }
+  hipLaunchKernelGGL(lstm_wgrad_combine, dim3((maxout + 255) / 256, a->L + 1), dim3(256), 0, st, *a);
+  if ((rc = (int)hipGetLastError())) return rc;
+  if (a->g_emb) {
+    const long n = (long)a->B * a->T * a->E;
+    hipLaunchKernelGGL(lstm_xe_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, *a);
+    return smi_emb_bwd_f32(a->ids, a->g_xe, a->g_emb, (long)a->B * a->T, a->E, a->pad_idx, nullptr, 0, 0, 1.f, a->V,
+                           a->emb_ws, st);
+  }
+  return (int)hipGetLastError();
 }

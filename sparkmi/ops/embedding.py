@@ -24,6 +24,7 @@ def sinusoid_table(max_len: int, d_model: int) -> torch.Tensor:
     return torch.stack([even_pe, odd_pe], dim=2).flatten(start_dim=1, end_dim=2)
 
 
+
 class EmbeddingFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ids, weight, pe, p, rng, salt, padding_idx, out_dtype):
@@ -66,8 +67,11 @@ class EmbeddingFn(torch.autograd.Function):
             C = _native.C()
             dout = dout.contiguous()
             bwd = C.emb_bwd_f32 if dout.dtype == torch.float32 else C.emb_bwd
+            # deterministic bucketed backward: bit-reproducible, no float atomics
+            V = weight.shape[0]
+            ws = torch.empty(C.emb_det_ws_bytes(T, V), device=dout.device, dtype=torch.uint8)
             bwd(ids.data_ptr(), dout.data_ptr(), gw.data_ptr(), T, D, ctx.pad, ctx.rng.ptr(), ctx.salt,
-                _rng.threshold(ctx.p), _rng.scale(ctx.p), _native.stream())
+                _rng.threshold(ctx.p), _rng.scale(ctx.p), V, ws.data_ptr(), _native.stream())
         else:
             g = dout.float()
             if ctx.p > 0:

@@ -3,9 +3,10 @@
 ``lstm_classifier(ids, h0, c0, params, ...)`` returns ``(pred [B,T,C], h_n [L,B,H], c_n)`` —
 exactly ``fc_out(lstm(embedding(ids), (h0, c0))[0])`` of the reference model
 (distributed_lstm.py:110-135), including nn.LSTM's inter-layer dropout.  GPU: one persistent
-workgroup per sequence for the forward, one for BPTT; weight gradients are accumulated in fp32
-straight into ``param.grad`` (flat buffers), the embedding rows equal to ``padding_idx`` get no
-gradient.  CPU: the identical math written with torch ops (same counter-hash dropout masks),
+workgroup per sequence for the forward, one for BPTT; each sequence's weight gradients go to a
+slab that one kernel sums in sequence order into ``param.grad`` (flat fp32 buffers), and the
+embedding-table gradient is a sorted segment sum — bit-reproducible, no float atomics; the
+embedding rows equal to ``padding_idx`` get no gradient.  CPU: the identical math written with torch ops (same counter-hash dropout masks),
 which is what the GPU kernel is tested against.
 """
 import torch
@@ -80,7 +81,7 @@ class LSTMFn(torch.autograd.Function):
                          [lw[2].data_ptr() for lw in layers], [lw[3].data_ptr() for lw in layers],
                          w_fc.data_ptr(), b_fc.data_ptr(), _native.ptr(h0c), _native.ptr(c0c), pred.data_ptr(),
                          hn.data_ptr(), cn.data_ptr(), ws.data_ptr(), 0, rng.ptr() if rng is not None else 0, salt,
-                         thresh, _rng.scale(p), 0, 0, 0, 0, [], [], [], [], 0, 0, 0, 0, _native.stream())
+                         thresh, _rng.scale(p), 0, 0, 0, 0, [], [], [], [], 0, 0, 0, 0, 0, 0, 0, 0, _native.stream())
         ctx.meta = (L, p, rng, salt, pad_idx, B, T, E, H, C)
         ctx.has_h0, ctx.has_c0 = h0 is not None, c0 is not None
         ctx.save_for_backward(ids, ws, h0c, c0c, *params)
@@ -95,12 +96,17 @@ class LSTMFn(torch.autograd.Function):
         dpred = dpred.float().contiguous() if dpred is not None else torch.zeros(B, T, C, device=dev)
         dhn = dhn.float().contiguous() if dhn is not None else None
         dcn = dcn.float().contiguous() if dcn is not None else None
-        ws_da = torch.empty(B, T, 4 * H, device=dev, dtype=torch.float32)
+        ws_da = torch.empty(B, L, T, 4 * H, device=dev, dtype=torch.float32)
         dh0 = torch.empty(L, B, H, device=dev) if ctx.needs_input_grad[1] else None
         dc0 = torch.empty(L, B, H, device=dev) if ctx.needs_input_grad[2] else None
         orig = params
         g = [grad_buf(t) for t in orig]
         g_emb, g_layers, g_fc, g_bfc = unpack(g, L)
+        C_ = _native.C()
+        slab = torch.empty(C_.lstm_slab_floats(B, E, H, L, C), device=dev, dtype=torch.float32)
+        want_emb = orig[0].requires_grad
+        xe = torch.empty(B, T, E, device=dev, dtype=torch.float32) if want_emb else None
+        ews = torch.empty(C_.emb_det_ws_bytes(B * T, emb.shape[0]), device=dev, dtype=torch.uint8) if want_emb else None
         _native.C().lstm(1, ids.data_ptr(), B, T, E, H, L, C, pad_idx, emb.data_ptr(),
                          [lw[0].data_ptr() for lw in layers], [lw[1].data_ptr() for lw in layers],
                          [lw[2].data_ptr() for lw in layers], [lw[3].data_ptr() for lw in layers],
@@ -110,7 +116,8 @@ class LSTMFn(torch.autograd.Function):
                          g_emb.data_ptr() if orig[0].requires_grad else 0,
                          [lw[0].data_ptr() for lw in g_layers], [lw[1].data_ptr() for lw in g_layers],
                          [lw[2].data_ptr() for lw in g_layers], [lw[3].data_ptr() for lw in g_layers],
-                         g_fc.data_ptr(), g_bfc.data_ptr(), _native.ptr(dh0), _native.ptr(dc0), _native.stream())
+                         g_fc.data_ptr(), g_bfc.data_ptr(), _native.ptr(dh0), _native.ptr(dc0), slab.data_ptr(),
+                         _native.ptr(xe), emb.shape[0], _native.ptr(ews), _native.stream())
         grad_ready(*orig)
         return (None, dh0 if ctx.has_h0 else None, dc0 if ctx.has_c0 else None, None) + (None,) * len(params)
 

@@ -14,6 +14,13 @@ _M32 = 0xFFFFFFFF
 _salts = itertools.count(1)
 
 
+def reset_salts():
+    """Restart the per-call-site salt sequence (a run's entry point: models built after this get
+    the same dropout streams as in a fresh process)."""
+    global _salts
+    _salts = itertools.count(1)
+
+
 def new_salt() -> int:
     """A fresh static per-call-site salt (deterministic construction order)."""
     return (next(_salts) * 0x2545F491) & _M32

@@ -32,6 +32,8 @@ def setup_executor(cfg):
         os.environ["SPARKMI_FORCE_CPU"] = "1"
     rank, world, device = init_distributed()
     torch.manual_seed(cfg.seed)
+    from ..ops.rng import reset_salts
+    reset_salts()  # same dropout salts as a fresh process: runs are reproducible in-process too
     return rank, world, device
 
 

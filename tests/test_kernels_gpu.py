@@ -143,6 +143,28 @@ def test_embedding():
     assert float(wg.grad[7].abs().sum()) == 0.0
 
 
+@pytest.mark.parametrize("n_tok", [8192, 20000])
+def test_embedding_backward_deterministic(n_tok):
+    """Id-bucketed, position-ordered backward: bit-reproducible and equal to the fp64 index_add
+    reference up to fp32 rounding, also with a 600-token run of one id."""
+    torch.manual_seed(4)
+    V, D = 300, 512  # few ids -> long runs of repeated ids
+    ids = torch.randint(0, V, (n_tok,))
+    ids[:600] = 11  # a long run (the padding-tail shape)
+    w = torch.nn.Parameter(torch.randn(V, D, device=dev, dtype=torch.float32))
+    do = torch.randn(n_tok, D, device=dev)
+    grads = []
+    for _ in range(2):
+        w.grad = None
+        out = embedding(ids.to(dev), w, None, 0.0, R.DropoutRNG(1).to(dev), 5, padding_idx=None,
+                        out_dtype=torch.float32)
+        out.backward(do)
+        grads.append(w.grad.clone())
+    ref = torch.zeros(V, D, dtype=torch.float64).index_add_(0, ids, do.cpu().double())
+    _close(grads[0], ref, 1e-4, 1e-5, "emb grad")
+    assert torch.equal(grads[0], grads[1])
+
+
 @pytest.mark.parametrize("act,p", [(None, 0.0), ("relu", 0.1), ("relu", 0.0)])
 def test_linear(act, p):
     torch.manual_seed(4)

@@ -30,14 +30,19 @@ def test_cnn_recipe_gpu_resume_exact(tmp_path):
 
 
 @pytest.mark.gpu
-def test_lstm_recipe_gpu_learns():
+def test_lstm_recipe_gpu_deterministic_and_learns():
+    """The LSTM step has no float atomics (slab + fixed-order reductions, position-ordered
+    embedding backward), so two identical runs are bit-identical; and training beats chance
+    (4 classes) by a wide margin."""
     from sparkmi.recipes import lstm
-    # The weight / embedding gradients are summed with fp32 atomics (like PyTorch's GPU LSTM and
-    # embedding backward), so identical runs take different trajectories through this small
-    # LSTM's loss plateau: at 2 epochs test accuracy ranged 23-74 %, at 4 epochs 73.7-99.7 %
-    # (tools/lstm_check.py).  4 epochs and a bar well above chance (25 %) keep the test stable.
-    r = lstm.main(GPU + ["--n-train", "8000", "--n-test", "800", "--epochs", "4", "--lr", "0.01"])
-    assert r["test_acc"] > 55.0
+    # deterministic trajectories (tools/lstm_sweep.py): lr 0.005 x 6 epochs reached 99.6 % / 100 %
+    # with two different (fixed) reduction orders; some (lr, epochs) settings stay on this small
+    # LSTM's loss plateau for a given summation order, so the setting is the robust one
+    args = GPU + ["--n-train", "8000", "--n-test", "800", "--epochs", "6", "--lr", "0.005"]
+    r1 = lstm.main(args)
+    r2 = lstm.main(args)
+    assert r1["final_loss"] == r2["final_loss"] and r1["test_acc"] == r2["test_acc"]
+    assert r1["test_acc"] > 90.0
 
 
 @pytest.mark.gpu
