@@ -105,14 +105,16 @@ __global__ __launch_bounds__(256) void emb_bwd_kernel(const long long* __restric
 //  3. emb_det_place: every token writes its position to its bucket's list at (tile offset +
 //     its rank among the tile's same-bucket tokens) — lists are in position order;
 //  4. emb_det_sum:   workgroup (bucket, 64-column chunk): wave w sums the list entries
-//     q = w (mod 8) per id slot in LDS (8 loads in flight per wave), the 8 wave partials are
-//     added in wave order, and rows that got tokens are added into the table.
+//     q = w (mod 8), 16 loads in flight, consecutive entries of one id in a register and other
+//     ids per slot in LDS; the 8 wave partials are added in wave order, and rows that got tokens
+//     are added into the table.  List entries carry the slot, so no id is loaded per token.
 // Every element is a fixed-order fp32 sum (independent of scheduling): bit-reproducible, no
 // float atomics, and a long run of one id is spread over 8 waves.
 #define EMB_TILE 256
 #define EMB_SLOTS 24
 #define EMB_CW 64
 #define EMB_SW 8  // waves of the sum kernel
+#define EMB_POS_BITS 26  // list entry: token position (< 2^26) | slot << 26
 
 struct EmbDet {
   int tiles, NB;
@@ -196,7 +198,9 @@ __global__ __launch_bounds__(EMB_TILE) void emb_det_place(const long long* __res
   if (bk < 0) return;
   int rank = 0;
   for (int i = 0; i < (int)threadIdx.x; ++i) rank += sb[i] == bk;
-  d.list[d.bstart[bk] + d.offs[(size_t)blockIdx.x * d.NB + bk] + rank] = (int)t;
+  // entry = position | slot << 26 (slot = id / NB < EMB_SLOTS): the sum kernel needs no id loads
+  d.list[d.bstart[bk] + d.offs[(size_t)blockIdx.x * d.NB + bk] + rank] =
+      (int)t | ((int)(ids[t] / d.NB) << EMB_POS_BITS);
 }
 
 template <typename TS>
@@ -213,30 +217,57 @@ __global__ __launch_bounds__(64 * EMB_SW) void emb_det_sum(const long long* __re
   const int c = c0 + lane;
   const bool cok = c < D;
   unsigned mask = 0u;  // slots this wave touched (wave-uniform): rows are zeroed on first touch
-  for (int q0 = w; q0 < n; q0 += 8 * EMB_SW) {  // this wave's entries q0, q0+8, ..., 8 at a time
-    long tt[8];
-    float g[8];
+  // a run of one slot accumulates in a register (a long run of one id — a padding tail — would
+  // otherwise be a chain of dependent LDS read-modify-writes); flushed when the slot changes
+  int rslot = -1;
+  float racc = 0.f;
+  auto flush = [&]() {
+    if (rslot < 0) return;
+    if (!((mask >> rslot) & 1u)) {
+      mask |= 1u << rslot;
+      acc[w][rslot][lane] = racc;
+    } else {
+      acc[w][rslot][lane] += racc;
+    }
+  };
+  // this wave's entries q0, q0 + EMB_SW, ... (16 per round); the next round's list entries are
+  // loaded while this round's rows are in flight
+  int en[16], nx[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int q = q0 + u * EMB_SW;
-      tt[u] = q < n ? d.list[beg + q] : -1;
+  for (int u = 0; u < 16; ++u) {
+    const int q = w + u * EMB_SW;
+    nx[u] = q < n ? d.list[beg + q] : -1;
+  }
+  for (int q0 = w; q0 < n; q0 += 16 * EMB_SW) {
+    float g[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) en[u] = nx[u];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const long tt = en[u] >= 0 ? (long)(en[u] & ((1 << EMB_POS_BITS) - 1)) : 0;
+      g[u] = (en[u] >= 0 && cok) ? emb_ld(dout + tt * D + c) : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) g[u] = (tt[u] >= 0 && cok) ? emb_ld(dout + tt[u] * D + c) : 0.f;
+    for (int u = 0; u < 16; ++u) {
+      const int q = q0 + 16 * EMB_SW + u * EMB_SW;
+      nx[u] = q < n ? d.list[beg + q] : -1;
+    }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if (tt[u] < 0) break;
+    for (int u = 0; u < 16; ++u) {
+      if (en[u] < 0) break;
+      const long tt = (long)(en[u] & ((1 << EMB_POS_BITS) - 1));
       float v = g[u];
-      if (thresh) v = smi_keep(seed, (uint32_t)(tt[u] * D + c), thresh) ? v * dscale : 0.f;
-      const int slot = (int)(ids[tt[u]] / d.NB);
-      if (!((mask >> slot) & 1u)) {
-        mask |= 1u << slot;
-        acc[w][slot][lane] = v;
-      } else {
-        acc[w][slot][lane] += v;
+      if (thresh) v = smi_keep(seed, (uint32_t)(tt * D + c), thresh) ? v * dscale : 0.f;
+      const int slot = en[u] >> EMB_POS_BITS;
+      if (slot != rslot) {
+        flush();
+        rslot = slot;
+        racc = 0.f;
       }
+      racc += v;
     }
   }
+  flush();
   if (lane == 0) s_mask[w] = mask;
   __syncthreads();
   unsigned any = 0u;
