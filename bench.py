@@ -166,7 +166,7 @@ def time_allreduce(flat, device, world, iters=10):
     return round(float(t.item()) * 1000, 3)
 
 
-def bench_cnn(args, rank, world, device):
+def bench_cnn(args, rank, world, device, dtype="fp32"):
     """distributed_cnn.py workload: FashionMNISTModel, batch 32/GPU, SGD lr 0.01, mean CE."""
     import torch
     from sparkmi.data.synthetic import fashion_mnist_like
@@ -176,7 +176,7 @@ def bench_cnn(args, rank, world, device):
     from sparkmi.train.runner import StepRunner
     from sparkmi.utils.flat import FlatParams
     torch.manual_seed(4321)
-    model = FashionMNISTModel(1, 10, 10).to(device).train()
+    model = FashionMNISTModel(1, 10, 10, dtype=dtype).to(device).train()
     flat = FlatParams(model)
     opt = SGD(flat, lr=0.01)
     ddp = DataParallel(flat) if world > 1 else None
@@ -192,9 +192,10 @@ def bench_cnn(args, rank, world, device):
     v = world * args.cnn_batch * args.cnn_steps / elapsed
     return {"samples_per_s": round(v, 1), "ms_per_step": round(elapsed / args.cnn_steps * 1000, 4),
             "vs_baseline": round(v / BASELINE_CNN, 2), "final_loss": round(float(loss), 4),
-            "dtype": "fp32", "global_batch": world * args.cnn_batch, "steps": args.cnn_steps,
+            "dtype": dtype, "global_batch": world * args.cnn_batch, "steps": args.cnn_steps,
             "allreduce_ms": ar, "grad_bytes": flat.numel * 4,
-            "config": f"FashionMNISTModel fused HIP kernel, batch {args.cnn_batch}/GPU, SGD lr0.01, dp{world}",
+            "config": f"FashionMNISTModel fused HIP kernel ({'bf16 MFMA' if dtype == 'bf16' else 'fp32'} convs), "
+                      f"batch {args.cnn_batch}/GPU, SGD lr0.01, dp{world}",
             "baseline_ref": "BASELINE.md §2 CNN CPU proxy 5,655 samples/s (1 proc x 8 threads)"}
 
 
@@ -321,9 +322,11 @@ def main():
         dtypes = ["fp32", "bf16"]
     else:
         dtypes = [args.dtype]
-    cnn = lstm = mlp = None
+    cnn = cnn32 = lstm = mlp = None
     if args.model in ("all", "cnn"):
-        cnn = bench_cnn(args, rank, world, device)
+        # BASELINE's CNN config is bf16 (Conv2d on matrix cores); the fp32 kernel is reported too
+        cnn32 = bench_cnn(args, rank, world, device, "fp32")
+        cnn = bench_cnn(args, rank, world, device, "bf16") if device.type == "cuda" else cnn32
     if args.model in ("all", "aux") and not args.no_aux:
         lstm = bench_lstm(args, rank, world, device)
         mlp = bench_mlp(args, rank, world, device)
@@ -340,7 +343,8 @@ def main():
                               "higher_is_better": True, "scaling": "weak", "vs_baseline": cnn["vs_baseline"],
                               "dtype": cnn["dtype"], "data": "synthetic",
                               "config": {"model": "FashionMNISTModel", "global_batch": cnn["global_batch"],
-                                         "seq_len": None, "parallelism": f"dp{world}"}, "cnn": cnn}))
+                                         "seq_len": None, "parallelism": f"dp{world}"}, "cnn": cnn,
+                              "cnn_fp32": cnn32}))
         destroy()
         return
     tr = {dt: bench_transformer(args, rank, world, device, dt) for dt in dtypes}
@@ -376,6 +380,7 @@ def main():
             out[f"transformer_{dt}"] = tr[dt]
         if cnn is not None:
             out["cnn"] = cnn
+            out["cnn_fp32"] = cnn32
         if lstm is not None:
             out["extra"] = {"lstm": lstm, "mlp": mlp,
                             "aux_baseline_ref": "BASELINE.md §2 best CPU proxy: LSTM 1,365, MLP 130,476 samples/s"}

@@ -407,8 +407,9 @@ PYBIND11_MODULE(_C, m) {
   // fused CNN: phase 0 = fwd(+bwd if train), 1 = gradient reduce
   m.def("cnn", [](int phase, u x, int x_u8, float x_scale, u y, int B, int cin, int C, int classes, std::vector<u> w,
                   std::vector<u> b, std::vector<u> gw, std::vector<u> gb, u slab, u row_loss, u pred, u logits,
-                  u loss, float loss_scale, u dloss, int train, u st) {
+                  u loss, float loss_scale, u dloss, int train, int bf16, u st) {
     CNNArgs a{};
+    a.bf16 = bf16;
     if (w.size() != 5 || b.size() != 5) throw std::runtime_error("cnn: need 5 weight and 5 bias pointers");
     a.x = (const void*)x; a.x_u8 = x_u8; a.x_scale = x_scale; a.y = (const long long*)y;
     a.B = B; a.cin = cin; a.C = C; a.classes = classes;

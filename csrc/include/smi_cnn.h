@@ -12,4 +12,5 @@ struct CNNArgs {
   float loss_scale;                          // 1/B for a mean loss
   const float* dloss;                        // upstream grad of the loss (reduce kernel)
   int train;
+  int bf16;                                  // convolutions on bf16 matrix cores (fp32 accumulate)
 };

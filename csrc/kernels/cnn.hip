@@ -326,8 +326,83 @@ __device__ __forceinline__ void conv_dgrad(const float* __restrict__ dz, int cou
   }
 }
 
+// ---- bf16 matrix-core convolutions (the BASELINE CNN config's precision; fp32 accumulation) --
+// A 3x3/pad-1 conv over an H x H LDS plane set is an implicit GEMM on v_mfma_f32_16x16x32_bf16:
+//   forward  D[pos][co] = sum_{k = ci*9 + ky*3 + kx} in[ci][pos + (ky-1, kx-1)] * W[co][ci][ky][kx]
+//   dgrad    D[pos][ci] = sum_{k = co*9 + ky*3 + kx} dz[co][pos + (1-ky, 1-kx)] * W[co][ci][ky][kx]
+// M = 16 positions per tile, N = 16 channels (C <= 16), K = 9 * channels padded to 32-steps.
+// Lane l gathers A[row l&15][k = 32s + 8(l>>4) + j] straight from the zero-halo fp32 planes
+// (per-lane offsets precomputed once per layer, so a k-step is 8 LDS reads + 4 packs + 1 MFMA)
+// and holds B[k][col l&15] = the weights for its (k, channel), converted to bf16 once per layer.
+// D: col = channel l&15, rows = positions 4(l>>4) + r.  Tiles are spread over the 16 waves.
+
+__device__ __forceinline__ bf16x8_t cnn_pack8(const float (&v)[8]) {
+  const unsigned p0 = pack2bf(v[0], v[1]), p1 = pack2bf(v[2], v[3]), p2 = pack2bf(v[4], v[5]), p3 = pack2bf(v[6], v[7]);
+  typedef __attribute__((ext_vector_type(4))) unsigned u4;
+  return __builtin_bit_cast(bf16x8_t, (u4){p0, p1, p2, p3});
+}
+
+// DG = false: forward (+bias, ReLU) into `out`; DG = true: transposed conv into `out` in place of
+// the forward activation, times relu'(out) when RELU (dz of the layer below), plain otherwise.
+// `tab` (LDS scratch): the layer's k -> plane-offset table and the bf16 B fragments of every
+// k-step, built once per call so the per-tile loop keeps almost nothing in registers (the
+// kernel runs 16 waves: 128 VGPRs per lane).
+template <int H, int PP, bool DG, bool RELU>
+__device__ __forceinline__ void conv_mfma(const float* __restrict__ in, int nin, float* __restrict__ out, int nout,
+                                          const float* __restrict__ wg, const float* __restrict__ bg,
+                                          float* __restrict__ tab) {
+  constexpr int NT = (H * H + 15) / 16;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int K = nin * 9, ks = (K + 31) / 32;
+  int* otab = (int*)tab;                          // [ks * 32] plane offsets (-1: padding k)
+  bf16x8_t* wtab = (bf16x8_t*)(tab + 256);        // [ks][64 lanes] B fragments
+  for (int k = threadIdx.x; k < ks * 32; k += blockDim.x) {
+    const int c = k / 9, kk = k - c * 9, ky = kk / 3, kx = kk - ky * 3;
+    otab[k] = k < K ? (DG ? c * PP * PP + (2 - ky) * PP + (2 - kx) : c * PP * PP + ky * PP + kx) : -1;
+  }
+  for (int e = threadIdx.x; e < ks * 64; e += blockDim.x) {
+    const int s = e >> 6, l = e & 63, col = l & 15;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 32 * s + 8 * (l >> 4) + j;
+      const int c = k / 9, kk = k - c * 9;
+      v[j] = (k < K && col < nout) ? wg[DG ? (c * nout + col) * 9 + kk : (col * nin + c) * 9 + kk] : 0.f;
+    }
+    wtab[e] = cnn_pack8(v);
+  }
+  __syncthreads();
+  const int col = lane & 15, kq = lane >> 4;
+  const float bias = (!DG && col < nout) ? bg[col] : 0.f;
+  for (int t = wv; t < NT; t += nw) {
+    const int p = t * 16 + col;  // this lane's A row (position)
+    const bool pv = p < H * H;
+    const int base = pv ? (p / H) * PP + (p % H) : 0;
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < ks; ++s) {
+      const int4 o0 = *(const int4*)(otab + 32 * s + 8 * kq), o1 = *(const int4*)(otab + 32 * s + 8 * kq + 4);
+      const int o[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (pv && o[j] >= 0) ? in[base + o[j]] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cnn_pack8(v), wtab[s * 64 + lane], acc, 0, 0, 0);
+    }
+    if (col < nout) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = t * 16 + 4 * kq + r;
+        if (q < H * H) {
+          float* o = out + col * PP * PP + (q / H + 1) * PP + (q % H + 1);
+          if (!DG) *o = fmaxf(acc[r] + bias, 0.f);
+          else *o = RELU ? (*o > 0.f ? acc[r] : 0.f) : acc[r];
+        }
+      }
+    }
+  }
+}
+
 // CC: channel capacity; EX: g.C == CC exactly (compile-time channel count, no clamps)
-template <int CC, bool EX>
+template <int CC, bool EX, bool BF>
 __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int C = EX ? CC : g.C, CI = g.cin, NC = g.classes;
@@ -357,19 +432,23 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   }
   __syncthreads();
   STAMP(1);
-  conv_fwd<28, P28, CC, EX>(xin, CI, a1, C, g.w[0], g.b[0]);
+  if (BF) conv_mfma<28, P28, false, false>(xin, CI, a1, C, g.w[0], g.b[0], wscr);
+  else conv_fwd<28, P28, CC, EX>(xin, CI, a1, C, g.w[0], g.b[0]);
   __syncthreads();
   STAMP(2);
-  conv_fwd<28, P28, CC, EX>(a1, C, a2, C, g.w[1], g.b[1]);
+  if (BF) conv_mfma<28, P28, false, false>(a1, C, a2, C, g.w[1], g.b[1], wscr);
+  else conv_fwd<28, P28, CC, EX>(a1, C, a2, C, g.w[1], g.b[1]);
   __syncthreads();
   STAMP(3);
   pool_fwd<28, P28, P14, 1>(a2, p1, C);
   __syncthreads();
   STAMP(4);
-  conv_fwd<14, P14, CC, EX>(p1, C, a3, C, g.w[2], g.b[2]);
+  if (BF) conv_mfma<14, P14, false, false>(p1, C, a3, C, g.w[2], g.b[2], wscr);
+  else conv_fwd<14, P14, CC, EX>(p1, C, a3, C, g.w[2], g.b[2]);
   __syncthreads();
   STAMP(5);
-  conv_fwd<14, P14, CC, EX>(a3, C, a4, C, g.w[3], g.b[3]);
+  if (BF) conv_mfma<14, P14, false, false>(a3, C, a4, C, g.w[3], g.b[3], wscr);
+  else conv_fwd<14, P14, CC, EX>(a3, C, a4, C, g.w[3], g.b[3]);
   __syncthreads();
   STAMP(6);
   pool_fwd<14, P14, 7, 0>(a4, p2, C);
@@ -453,7 +532,8 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
     gs[(e < C * C * 9 ? g.off[6] + e : g.off[7] + e - C * C * 9)] = wacc[e];
     wacc[e] = 0.f;
   }
-  conv_dgrad<14, P14, CC, EX>(a4, C, g.w[3], C, a3, true);
+  if (BF) conv_mfma<14, P14, true, true>(a4, C, a3, C, g.w[3], nullptr, wscr);
+  else conv_dgrad<14, P14, CC, EX>(a4, C, g.w[3], C, a3, true);
   __syncthreads();
   STAMP(14);
   // conv3: dW3 (dz3, p1); dp1 = convT(dz3) into p1 (no relu: p1 is a pool output)
@@ -464,7 +544,8 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
     gs[(e < C * C * 9 ? g.off[4] + e : g.off[5] + e - C * C * 9)] = wacc[e];
     wacc[e] = 0.f;
   }
-  conv_dgrad<14, P14, CC, EX>(a3, C, g.w[2], C, p1, false);
+  if (BF) conv_mfma<14, P14, true, false>(a3, C, p1, C, g.w[2], nullptr, wscr);
+  else conv_dgrad<14, P14, CC, EX>(a3, C, g.w[2], C, p1, false);
   __syncthreads();
   STAMP(16);
   // pool1 backward + relu'(a2): dz2 in a2
@@ -479,7 +560,8 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
     gs[(e < C * C * 9 ? g.off[2] + e : g.off[3] + e - C * C * 9)] = wacc[e];
     wacc[e] = 0.f;
   }
-  conv_dgrad<28, P28, CC, EX>(a2, C, g.w[1], C, a1, true);
+  if (BF) conv_mfma<28, P28, true, true>(a2, C, a1, C, g.w[1], nullptr, wscr);
+  else conv_dgrad<28, P28, CC, EX>(a2, C, g.w[1], C, a1, true);
   __syncthreads();
   STAMP(19);
   // conv1: dW1 (dz1, x)
@@ -528,7 +610,8 @@ extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
   if (lds > 160 * 1024) return -1;
   // channel capacity 10 (the reference model's hidden_units) gets exact compile-time groups
   // (LDS residency caps C at 13 for 1-channel input, so no exact instance above 10)
-  auto kern = g.C == 10 ? cnn_kernel<10, true> : cnn_kernel<CNN_MAXC, false>;
+  auto kern = g.bf16 ? (g.C == 10 ? cnn_kernel<10, true, true> : cnn_kernel<CNN_MAXC, false, true>)
+                     : (g.C == 10 ? cnn_kernel<10, true, false> : cnn_kernel<CNN_MAXC, false, false>);
   hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(g.B), dim3(CNN_THREADS), lds, st, g);
   SMI_CHECK_LAUNCH();

@@ -2,6 +2,8 @@
 same module names (block_1 / block_2 / classifier, nn.Sequential indices) so reference
 state_dicts load.  ``loss(x, y)`` runs the fused whole-network HIP kernel (sparkmi/ops/cnn.py);
 ``forward(x)`` returns logits (fused inference kernel on GPU, torch ops on CPU).
+``dtype="bf16"`` (the BASELINE CNN config) runs the four convolutions on bf16 matrix cores
+(implicit GEMM on v_mfma_f32_16x16x32_bf16, fp32 accumulation) inside the same fused kernel.
 """
 import torch
 from torch import nn
@@ -10,8 +12,11 @@ from ..ops.cnn import cnn_logits, cnn_loss
 
 
 class FashionMNISTModel(nn.Module):
-    def __init__(self, input_shape: int = 1, hidden_units: int = 10, output_shape: int = 10):
+    def __init__(self, input_shape: int = 1, hidden_units: int = 10, output_shape: int = 10, dtype: str = "fp32"):
         super().__init__()
+        if dtype not in ("fp32", "bf16"):
+            raise ValueError(f"dtype must be 'fp32' or 'bf16', got {dtype!r}")
+        self.conv_dtype = dtype  # GPU: "bf16" runs the convolutions on bf16 matrix cores
         self.block_1 = nn.Sequential(
             nn.Conv2d(input_shape, hidden_units, kernel_size=3, stride=1, padding=1), nn.ReLU(),
             nn.Conv2d(hidden_units, hidden_units, kernel_size=3, stride=1, padding=1), nn.ReLU(),
@@ -30,11 +35,11 @@ class FashionMNISTModel(nn.Module):
         return out
 
     def forward(self, x):
-        return cnn_logits(x, self.param_list())
+        return cnn_logits(x, self.param_list(), self.conv_dtype == "bf16")
 
     def loss(self, x, y):
         """Mean CE over the batch (distributed_cnn.py:141,177)."""
-        return cnn_loss(x, y, self.param_list())
+        return cnn_loss(x, y, self.param_list(), self.conv_dtype == "bf16")
 
 
 CNN = FashionMNISTModel

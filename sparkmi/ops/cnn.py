@@ -28,7 +28,7 @@ def reference_logits(x, params, x_scale=None):
     return F.linear(h.flatten(1), wf, bf)
 
 
-def _launch(phase, x, y, params, grads, slab, row_loss, pred, logits, loss, loss_scale, dloss, train):
+def _launch(phase, x, y, params, grads, slab, row_loss, pred, logits, loss, loss_scale, dloss, train, bf16=False):
     w = [params[i] for i in (0, 2, 4, 6, 8)]
     b = [params[i] for i in (1, 3, 5, 7, 9)]
     B, cin = x.shape[0], x.shape[1]
@@ -38,7 +38,7 @@ def _launch(phase, x, y, params, grads, slab, row_loss, pred, logits, loss, loss
     _native.C().cnn(phase, x.data_ptr(), int(x.dtype == torch.uint8), 1.0 / 255.0, _native.ptr(y), B, cin, C, classes,
                     [t.data_ptr() for t in w], [t.data_ptr() for t in b], gw, gb, _native.ptr(slab),
                     _native.ptr(row_loss), _native.ptr(pred), _native.ptr(logits), _native.ptr(loss), loss_scale,
-                    _native.ptr(dloss), int(train), _native.stream())
+                    _native.ptr(dloss), int(train), int(bf16), _native.stream())
 
 
 def num_params(params):
@@ -47,7 +47,7 @@ def num_params(params):
 
 class CNNLossFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, y, *params):
+    def forward(ctx, x, y, bf16, *params):
         ctx.native = _native.use_native(x)
         B = x.shape[0]
         if ctx.native:
@@ -58,7 +58,7 @@ class CNNLossFn(torch.autograd.Function):
             row_loss = torch.empty(B, device=x.device, dtype=torch.float32)
             pred = torch.empty(B, device=x.device, dtype=torch.int32)
             loss = torch.empty(1, device=x.device, dtype=torch.float32)
-            _launch(0, x, y, params, None, slab, row_loss, pred, None, loss, 1.0 / B, None, True)
+            _launch(0, x, y, params, None, slab, row_loss, pred, None, loss, 1.0 / B, None, True, bf16)
             ctx.save_for_backward(slab, *params)
             ctx.pred = pred
             return loss[0]
@@ -79,7 +79,7 @@ class CNNLossFn(torch.autograd.Function):
                             [t.data_ptr() for t in w], [params[i].data_ptr() for i in (1, 3, 5, 7, 9)],
                             [grads[i].data_ptr() for i in (0, 2, 4, 6, 8)],
                             [grads[i].data_ptr() for i in (1, 3, 5, 7, 9)], slab.data_ptr(), 0, 0, 0, 0, 0.0,
-                            dl.data_ptr(), 1, _native.stream())
+                            dl.data_ptr(), 1, 0, _native.stream())
             del x_dummy
         else:
             x, y, *params = ctx.saved_tensors
@@ -90,19 +90,22 @@ class CNNLossFn(torch.autograd.Function):
             for p, g in zip(params, gs):
                 grad_buf(p).add_(g)
         grad_ready(*params)
-        return (None, None) + (None,) * len(params)
+        return (None, None, None) + (None,) * len(params)
 
 
-def cnn_loss(x, y, params):
-    return CNNLossFn.apply(x, y, *params)
+def cnn_loss(x, y, params, bf16=False):
+    """Mean CE of the fused CNN step; ``bf16``: the convolutions run on bf16 matrix cores
+    (fp32 accumulation and fp32 activations / gradients elsewhere) on the GPU."""
+    return CNNLossFn.apply(x, y, bool(bf16), *params)
 
 
-def cnn_logits(x, params):
+def cnn_logits(x, params, bf16=False):
     if _native.use_native(x):
         x = x.contiguous()
         B = x.shape[0]
         logits = torch.empty(B, params[8].shape[0], device=x.device, dtype=torch.float32)
-        _launch(0, x, None, [p.contiguous() for p in params], None, None, None, None, logits, None, 1.0, None, False)
+        _launch(0, x, None, [p.contiguous() for p in params], None, None, None, None, logits, None, 1.0, None, False,
+                bf16)
         return logits
     with torch.no_grad():
         return reference_logits(x, [p.float() for p in params])

@@ -30,6 +30,7 @@ class CNNConfig(TrainConfig):
     batch_size: int = 32
     lr: float = 0.01
     hidden_units: int = 10
+    conv_dtype: str = "fp32"       # "bf16": convolutions on bf16 matrix cores (BASELINE's CNN config)
     n_train: int = 60000
     n_test: int = 10000
 
@@ -52,7 +53,7 @@ def train_fn(cfg):
     loader = DeviceLoader([xtr[idx], ytr[idx]], cfg.batch_size, device, shuffle=True, drop_last=True,
                           seed=cfg.seed + 1000 * rank)
     torch.manual_seed(cfg.seed)
-    model = FashionMNISTModel(1, cfg.hidden_units, 10)
+    model = FashionMNISTModel(1, cfg.hidden_units, 10, dtype=cfg.conv_dtype)
     trainer = Trainer(model, lambda m, x, y: m.loss(x, y), lambda flat: SGD(flat, lr=cfg.lr), cfg, device, rank,
                       world, "cnn", shadow=False)
     stats = trainer.fit(loader, cfg.epochs)

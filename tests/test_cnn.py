@@ -80,3 +80,66 @@ def test_fused_cnn_kernel_channel_counts(cin, hidden):
     for (n, pg), pc in zip(mg.named_parameters(), mc.parameters()):
         rel = float((pg.grad.cpu() - pc.grad).norm() / (pc.grad.norm() + 1e-12))
         assert rel < 1e-4, (n, rel)
+
+
+def _bf16_ref_logits(x, params):
+    """fp32 CNN with every convolution's operands rounded to bf16 (what the matrix-core path
+    multiplies; products and sums in fp32)."""
+    import torch.nn.functional as F
+    r = lambda t: t.bfloat16().float()  # noqa: E731
+    w1, b1, w2, b2, w3, b3, w4, b4, wf, bf = params
+    h = x.float() / 255.0 if x.dtype == torch.uint8 else x.float()
+    h = F.relu(F.conv2d(r(h), r(w1), b1, padding=1))
+    h = F.relu(F.conv2d(r(h), r(w2), b2, padding=1))
+    h = F.max_pool2d(h, 2)
+    h = F.relu(F.conv2d(r(h), r(w3), b3, padding=1))
+    h = F.relu(F.conv2d(r(h), r(w4), b4, padding=1))
+    h = F.max_pool2d(h, 2)
+    return F.linear(h.flatten(1), wf, bf)
+
+
+@pytest.mark.gpu
+def test_fused_cnn_bf16_mfma_vs_reference():
+    """bf16 matrix-core convolutions: forward equals the bf16-operand fp32 reference to fp32
+    summation error; gradients follow the fp32 reference to bf16 precision."""
+    torch.manual_seed(3)
+    B = 32
+    mc = FashionMNISTModel()
+    mg = FashionMNISTModel(dtype="bf16").cuda()
+    mg.load_state_dict(mc.state_dict())
+    x = torch.rand(B, 1, 28, 28)
+    y = torch.randint(0, 10, (B,))
+    zg = mg(x.cuda()).cpu()
+    zr = _bf16_ref_logits(x, [p.detach() for p in mc.param_list()])
+    assert float((zg - zr).abs().max()) < 2e-3, float((zg - zr).abs().max())
+    lg = mg.loss(x.cuda(), y.cuda())
+    lc = mc.loss(x, y)
+    assert abs(float(lg) - float(lc)) < 2e-2, (float(lg), float(lc))
+    lg.backward()
+    lc.backward()
+    # bf16 operands in three chained dgrads: the first conv's weight gradient (a sum over
+    # 25k cancelling terms) is ~10 % off the fp32 one, the later layers ~1-3 %
+    for (n, pg), pc in zip(mg.named_parameters(), mc.parameters()):
+        a, b = pg.grad.cpu().flatten(), pc.grad.flatten()
+        rel = float((a - b).norm() / (b.norm() + 1e-12))
+        cos = float(torch.nn.functional.cosine_similarity(a, b, dim=0))
+        assert rel < 0.15 and cos > 0.99, (n, rel, cos)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_fused_cnn_gradients_bit_reproducible(dtype):
+    """Per-image slabs + fixed-order reductions (no float atomics): identical backwards give
+    bit-identical gradients."""
+    torch.manual_seed(4)
+    m = FashionMNISTModel(dtype=dtype).cuda()
+    x = torch.rand(32, 1, 28, 28, device="cuda")
+    y = torch.randint(0, 10, (32,), device="cuda")
+    out = []
+    for _ in range(2):
+        for p in m.parameters():
+            p.grad = None
+        m.loss(x, y).backward()
+        out.append([p.grad.clone() for p in m.parameters()])
+    for a, b in zip(*out):
+        assert torch.equal(a, b)

@@ -13,6 +13,13 @@ def test_cnn_recipe_gpu_learns():
 
 
 @pytest.mark.gpu
+def test_cnn_recipe_gpu_bf16_learns():
+    from sparkmi.recipes import cnn
+    r = cnn.main(GPU + ["--n-train", "6400", "--n-test", "1000", "--epochs", "2", "--lr", "0.1", "--conv-dtype", "bf16"])
+    assert r["steps"] == 400 and r["test_acc"] > 90.0
+
+
+@pytest.mark.gpu
 def test_cnn_recipe_gpu_resume_exact(tmp_path):
     from sparkmi.recipes import cnn
     base = GPU + ["--n-train", "640", "--n-test", "64", "--epochs", "2"]
@@ -21,12 +28,11 @@ def test_cnn_recipe_gpu_resume_exact(tmp_path):
     cnn.main(base + ["--ckpt-dir", str(tmp_path / "b"), "--max-steps", "25", "--ckpt-every", "25"])
     rest = cnn.main(base + ["--ckpt-dir", str(tmp_path / "b")])
     assert rest["steps"] == 40 - 25
-    # the fused CNN kernel's weight-gradient reduction uses LDS float atomics (summation order is
-    # not deterministic), so even two uninterrupted runs differ in the last bits and the
-    # difference grows over training; a resumed run must be as close as that run-to-run noise
+    # no float atomics anywhere in the CNN step (per-image slabs, fixed-order reductions): two
+    # uninterrupted runs are bit-identical, and so is a run resumed from a checkpoint
     for k, v in full["state_dict"].items():
-        noise = (full2["state_dict"][k] - v).abs().max().item()
-        torch.testing.assert_close(rest["state_dict"][k], v, rtol=0, atol=max(5e-4, 4 * noise))
+        assert torch.equal(full2["state_dict"][k], v), k
+        assert torch.equal(rest["state_dict"][k], v), k
 
 
 @pytest.mark.gpu
@@ -35,10 +41,10 @@ def test_lstm_recipe_gpu_deterministic_and_learns():
     embedding backward), so two identical runs are bit-identical; and training beats chance
     (4 classes) by a wide margin."""
     from sparkmi.recipes import lstm
-    # deterministic trajectories (tools/lstm_sweep.py): lr 0.005 x 6 epochs reached 99.6 % / 100 %
-    # with two different (fixed) reduction orders; some (lr, epochs) settings stay on this small
-    # LSTM's loss plateau for a given summation order, so the setting is the robust one
-    args = GPU + ["--n-train", "8000", "--n-test", "800", "--epochs", "6", "--lr", "0.005"]
+    # deterministic trajectories (tools/lstm_sweep.py): this small LSTM's loss plateau makes some
+    # (lr, epochs) settings succeed or stall depending on the (fixed) summation order of a given
+    # build; lr 0.03 x 4 epochs reached 99.7 / 98.0 / 99.1 % across three reduction orders
+    args = GPU + ["--n-train", "8000", "--n-test", "800", "--epochs", "4", "--lr", "0.03"]
     r1 = lstm.main(args)
     r2 = lstm.main(args)
     assert r1["final_loss"] == r2["final_loss"] and r1["test_acc"] == r2["test_acc"]

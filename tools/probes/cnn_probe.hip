@@ -5,10 +5,10 @@
 #include <cstdio>
 #include <vector>
 
-int main() {
+int main(int argc, char** argv) {
   const int B = 32, C = 10, CI = 1, NC = 10;
   CNNArgs g{};
-  g.B = B; g.cin = CI; g.C = C; g.classes = NC; g.x_u8 = 1; g.x_scale = 1.f / 255.f; g.train = 1; g.loss_scale = 1.f / B;
+  g.B = B; g.cin = CI; g.C = C; g.classes = NC; g.x_u8 = 1; g.x_scale = 1.f / 255.f; g.train = 1; g.loss_scale = 1.f / B; g.bf16 = argc > 1;
   unsigned char* x; long long* y; float *w[5], *b[5], *slab, *rl, *loss; int* pred;
   (void)hipMalloc(&x, B * 784); (void)hipMemset(x, 7, B * 784);
   (void)hipMalloc(&y, B * 8); (void)hipMemset(y, 0, B * 8);
