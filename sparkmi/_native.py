@@ -2,7 +2,8 @@
 
 ``sparkmi._C`` holds the HIP/CDNA4 kernels (built for gfx950 by ``tools/build_native.py``);
 ``sparkmi._runtime`` holds the host C++ runtime (libsvm parser, tokenizer, vocab encoder);
-``sparkmi._comm`` the native communication layer (RCCL communicator, xGMI IPC all-reduce).
+``sparkmi._comm`` the native communication layer (RCCL communicator, xGMI IPC all-reduce),
+``sparkmi._io`` the native input pipeline (pinned host ring, threaded gather, async H2D).
 
 torch is imported first on purpose: torch ships its own ``libamdhip64.so.7`` and ``_C``
 declares the same SONAME, so the dynamic linker binds ``_C`` to torch's already-loaded HIP
@@ -104,6 +105,30 @@ def comm():
     if _COMM is None:
         raise ImportError(f"sparkmi._comm unavailable: {_COMM_err}; run python tools/build_native.py")
     return _COMM
+
+
+_IO = None
+_IO_err = None
+
+
+def io():
+    """The native input-pipeline module (pinned host ring, threaded gather, async H2D)."""
+    global _IO, _IO_err
+    if _IO is not None:
+        return _IO
+    with _lock:
+        if _IO is None and _IO_err is None:
+            try:
+                _IO = _load("_io")
+            except ImportError:
+                _try_build()
+                try:
+                    _IO = _load("_io")
+                except ImportError as e:  # pragma: no cover
+                    _IO_err = e
+    if _IO is None:
+        raise ImportError(f"sparkmi._io unavailable: {_IO_err}; run python tools/build_native.py")
+    return _IO
 
 
 def has_native():

@@ -176,44 +176,95 @@ class DeviceLoader:
 
 
 class PinnedStreamLoader:
-    """Streams host minibatches to the GPU through pinned staging buffers on a side stream,
-    double-buffered so the H2D copy of batch i+1 overlaps compute on batch i (for datasets that
-    do not fit in HBM)."""
+    """Streams host minibatches to the GPU for datasets that do not fit in HBM (SURVEY §5.8 item 6,
+    §2.3 pinned_ring): the native ring (csrc/io/pinned_ring.cpp, ``sparkmi._io``) owns
+    ``nslots`` page-locked host slots; each batch's rows are gathered into a slot by C++ threads
+    (GIL released), shipped to a ring of device buffers with hipMemcpyAsync on a dedicated copy
+    stream, and guarded by HIP events: the compute stream waits on the slot's event (no host
+    sync), a slot is refilled only after its previous copy landed, and a device buffer only
+    after the compute that used it was queued past.  Batch i+1 is gathered and copied while
+    batch i computes.  CPU: plain gathers."""
 
-    def __init__(self, arrays, batch_size, device, shuffle=False, drop_last=True, seed=0):
-        self.arrays = [torch.as_tensor(np.asarray(a)) for a in arrays]
+    def __init__(self, arrays, batch_size, device, shuffle=False, drop_last=True, seed=0, nslots=3, threads=4):
+        self.arrays = [np.ascontiguousarray(a.numpy() if torch.is_tensor(a) else np.asarray(a)) for a in arrays]
         self.n = len(self.arrays[0])
         self.batch_size, self.shuffle, self.drop_last, self.seed = batch_size, shuffle, drop_last, seed
         self.device = torch.device(device)
-        self.stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
         self.epoch = 0
+        self.ring = None
+        if self.device.type == "cuda":
+            from .. import _native
+            if nslots < 3:  # batch b+1 is issued before batch b is handed out: 3 slots in flight
+                raise ValueError("PinnedStreamLoader needs nslots >= 3")
+            self.row_bytes = [a.itemsize * int(np.prod(a.shape[1:], dtype=np.int64)) for a in self.arrays]
+            self.offs, off = [], 0
+            for rb in self.row_bytes:
+                self.offs.append(off)
+                off += (rb * batch_size + 255) // 256 * 256
+            dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
+            self.ring = _native.io().PinnedRing(off, nslots, dev, threads)
+            self.nslots = nslots
+            tdt = [torch.from_numpy(a[:1]).dtype for a in self.arrays]
+            self.dev_bufs = [[torch.empty((batch_size,) + a.shape[1:], dtype=t, device=self.device)
+                              for a, t in zip(self.arrays, tdt)] for _ in range(nslots)]
+            self.released = [None] * nslots  # compute-stream events: the slot's device buffers are free
+            self._last = None                # slot handed out most recently
 
     def __len__(self):
         return self.n // self.batch_size if self.drop_last else math.ceil(self.n / self.batch_size)
 
-    def _host_batches(self):
-        order = np.random.default_rng(self.seed + self.epoch).permutation(self.n) if self.shuffle else np.arange(self.n)
-        for b in range(len(self)):
-            idx = torch.as_tensor(order[b * self.batch_size:(b + 1) * self.batch_size])
-            yield [a[idx].pin_memory() if self.stream is not None else a[idx] for a in self.arrays]
+    def _order(self):
+        return (np.random.default_rng(self.seed + self.epoch).permutation(self.n) if self.shuffle
+                else np.arange(self.n)).astype(np.int64)
+
+    def _issue(self, s, idx):
+        """Gather batch rows into slot s and queue its H2D copies; returns the device views."""
+        r = self.ring
+        r.acquire(s)  # the previous copy out of this host slot has landed
+        k = len(idx)
+        rel = self.released[s]
+        outs = []
+        for a, rb, off, buf in zip(self.arrays, self.row_bytes, self.offs, self.dev_bufs[s]):
+            r.gather(s, off, a.ctypes.data, rb, idx.ctypes.data, k)
+            r.copy_async(s, off, rb * k, buf.data_ptr(), rel.cuda_event if rel is not None else 0)
+            outs.append(buf[:k])
+        r.commit(s)
+        return outs
 
     def __iter__(self):
-        if self.stream is None:
-            for hb in self._host_batches():
-                yield tuple(hb)
+        order = self._order()
+        nb = len(self)
+        if self.ring is not None:
+            self._release_last()
+        if self.ring is None:
+            for b in range(nb):
+                idx = order[b * self.batch_size:(b + 1) * self.batch_size]
+                yield tuple(torch.from_numpy(a[idx]) for a in self.arrays)
             self.epoch += 1
             return
-        pending = None
-        for hb in self._host_batches():
-            with torch.cuda.stream(self.stream):
-                db = [t.to(self.device, non_blocking=True) for t in hb]
-                ev = torch.cuda.Event()
-                ev.record(self.stream)
+        pending = None  # (slot, device views) issued but not yet handed out
+        for b in range(nb):
+            idx = np.ascontiguousarray(order[b * self.batch_size:(b + 1) * self.batch_size])
+            s = b % self.nslots
+            views = self._issue(s, idx)
             if pending is not None:
-                torch.cuda.current_stream().wait_event(pending[1])
-                yield tuple(pending[0])
-            pending = (db, ev)
+                yield self._hand_out(*pending)
+            pending = (s, views)
         if pending is not None:
-            torch.cuda.current_stream().wait_event(pending[1])
-            yield tuple(pending[0])
+            yield self._hand_out(*pending)
         self.epoch += 1
+
+    def _release_last(self):
+        """The consumer asked for another batch, so everything it does with the previous one is
+        queued on the compute stream: an event there frees that slot's device buffers."""
+        if self._last is not None:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self.released[self._last] = ev
+            self._last = None
+
+    def _hand_out(self, s, views):
+        self._release_last()
+        self.ring.wait(s, torch.cuda.current_stream(self.device).cuda_stream)  # no host sync
+        self._last = s
+        return tuple(views)

@@ -129,3 +129,17 @@ def test_trace_ranges_noop_and_enabled():
             trace.mark("z")
     finally:
         trace.enable(False)
+
+
+def test_pinned_stream_loader_cpu_order():
+    """PinnedStreamLoader's CPU path: shuffled epochs cover every row once, in the seeded order."""
+    import numpy as np
+    from sparkmi.data.dataset import PinnedStreamLoader
+    a = np.arange(50 * 3, dtype=np.float32).reshape(50, 3)
+    y = np.arange(50)
+    loader = PinnedStreamLoader([a, y], 8, "cpu", shuffle=True, seed=2)
+    for epoch in range(2):
+        order = np.random.default_rng(2 + epoch).permutation(50)
+        got = [b[1].numpy() for b in loader]
+        assert len(got) == 6
+        np.testing.assert_array_equal(np.concatenate(got), order[:48])

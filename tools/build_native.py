@@ -7,6 +7,8 @@
                               vocab encoder, batch padding, shuffling (csrc/runtime/*.cpp), g++.
 * ``sparkmi/_comm*.so``     — native communication layer: RCCL communicator + xGMI IPC one-shot
                               all-reduce (csrc/comm/*.hip, *.cpp), hipcc, linked against librccl.
+* ``sparkmi/_io*.so``       — native input pipeline: pinned host ring, threaded row gather,
+                              async H2D on a copy stream (csrc/io/*.cpp), hipcc.
 
 Incremental by CONTENT, not mtime: every object carries a stamp (sha256 of its compile command,
 its source and every header under csrc/include) and every library a stamp of its link command
@@ -136,6 +138,14 @@ def build(force=False, jobs=8, verbose=True):
         elif f.endswith(".cpp"):
             comm_objs.append(obj(s, o, [HIPCC, "-O2", "-std=c++17", "-fPIC", "-c", s, "-o", o, "-fvisibility=hidden",
                                         "-I/opt/rocm/include"] + inc + py_inc))
+    io_dir = os.path.join(CSRC, "io")
+    io_objs = []
+    for f in sorted(os.listdir(io_dir)) if os.path.isdir(io_dir) else []:
+        if f.endswith(".cpp"):
+            s = os.path.join(io_dir, f)
+            o = os.path.join(OBJ, "io_" + f + ".o")
+            io_objs.append(obj(s, o, [HIPCC, "-O2", "-std=c++17", "-fPIC", "-c", s, "-o", o, "-fvisibility=hidden",
+                                      "-I/opt/rocm/include"] + inc + py_inc))
     if jobs_list:
         with ThreadPoolExecutor(max_workers=jobs) as ex:
             for (cmd, o, d), _ in zip(jobs_list, ex.map(lambda j: _run(j[0]), jobs_list)):
@@ -161,6 +171,9 @@ def build(force=False, jobs=8, verbose=True):
     if comm_objs:
         link(comm_so, comm_objs, [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", comm_so] +
              [o for o, _ in comm_objs] + ["-L/opt/rocm/lib", "-lrccl"])
+    io_so = os.path.join(PKG, "_io" + suffix)
+    if io_objs:
+        link(io_so, io_objs, [HIPCC, "-shared", "-fPIC", "-o", io_so] + [o for o, _ in io_objs] + ["-pthread"])
     rt_so = os.path.join(PKG, "_runtime" + suffix)
     if rt_objs:
         link(rt_so, rt_objs, ["g++", "-shared", "-fPIC", "-pthread", "-o", rt_so] + [o for o, _ in rt_objs])
