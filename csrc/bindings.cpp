@@ -50,7 +50,7 @@ int smi_emb_fwd(const long long*, const void*, const float*, void*, long, int, i
                 hipStream_t);
 int smi_emb_bwd(const long long*, const void*, float*, long, int, long long, const uint32_t*, uint32_t, uint32_t, float, long,
                 void*, hipStream_t);
-long smi_emb_det_ws_bytes(long, long);
+long smi_emb_det_ws_bytes(long, long, long);
 int smi_bias_act_drop_fwd(const void*, const float*, void*, long, int, int, const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
 int smi_act_drop_bwd(const void*, const void*, void*, long, int, const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
 int smi_act_drop_bwd_f32(const float*, const float*, float*, long, int, const uint32_t*, uint32_t, uint32_t, float,
@@ -216,8 +216,8 @@ PYBIND11_MODULE(_C, m) {
                       u st) {
     chk(smi_emb_fwd((const long long*)ids, P(table), PF(pe), P(out), T, D, Sp, (const uint32_t*)seedp, salt, thresh, dscale, S(st)), "emb_fwd");
   });
-  // V: table rows; ws: emb_det_ws_bytes(T, V) scratch -> deterministic bucketed backward (0: fp32 atomics)
-  m.def("emb_det_ws_bytes", [](long T, long V) { return smi_emb_det_ws_bytes(T, V); });
+  // V: table rows; ws: emb_det_ws_bytes(T, V, D) scratch -> deterministic bucketed backward (0: fp32 atomics)
+  m.def("emb_det_ws_bytes", [](long T, long V, long D) { return smi_emb_det_ws_bytes(T, V, D); });
   m.def("emb_bwd", [](u ids, u dout, u dtable, long T, int D, long long pad, u seedp, uint32_t salt, uint32_t thresh,
                       float dscale, long V, u ws, u st) {
     chk(smi_emb_bwd((const long long*)ids, P(dout), PF(dtable), T, D, pad, (const uint32_t*)seedp, salt, thresh, dscale,

@@ -69,7 +69,7 @@ class EmbeddingFn(torch.autograd.Function):
             bwd = C.emb_bwd_f32 if dout.dtype == torch.float32 else C.emb_bwd
             # deterministic bucketed backward: bit-reproducible, no float atomics
             V = weight.shape[0]
-            ws = torch.empty(C.emb_det_ws_bytes(T, V), device=dout.device, dtype=torch.uint8)
+            ws = torch.empty(C.emb_det_ws_bytes(T, V, D), device=dout.device, dtype=torch.uint8)
             bwd(ids.data_ptr(), dout.data_ptr(), gw.data_ptr(), T, D, ctx.pad, ctx.rng.ptr(), ctx.salt,
                 _rng.threshold(ctx.p), _rng.scale(ctx.p), V, ws.data_ptr(), _native.stream())
         else:

@@ -106,7 +106,7 @@ class LSTMFn(torch.autograd.Function):
         slab = torch.empty(C_.lstm_slab_floats(B, E, H, L, C), device=dev, dtype=torch.float32)
         want_emb = orig[0].requires_grad
         xe = torch.empty(B, T, E, device=dev, dtype=torch.float32) if want_emb else None
-        ews = torch.empty(C_.emb_det_ws_bytes(B * T, emb.shape[0]), device=dev, dtype=torch.uint8) if want_emb else None
+        ews = torch.empty(C_.emb_det_ws_bytes(B * T, emb.shape[0], emb.shape[1]), device=dev, dtype=torch.uint8) if want_emb else None
         _native.C().lstm(1, ids.data_ptr(), B, T, E, H, L, C, pad_idx, emb.data_ptr(),
                          [lw[0].data_ptr() for lw in layers], [lw[1].data_ptr() for lw in layers],
                          [lw[2].data_ptr() for lw in layers], [lw[3].data_ptr() for lw in layers],

@@ -165,6 +165,31 @@ def test_embedding_backward_deterministic(n_tok):
     assert torch.equal(grads[0], grads[1])
 
 
+@pytest.mark.parametrize("D", [512, 96])
+def test_embedding_backward_heavy_buckets(D):
+    """Padded-batch shape: ~95 % of the tokens are one id (split over EMB_SPLIT segment
+    workgroups + ordered combine), a second heavy id, a light tail; bf16 dout, dropout."""
+    torch.manual_seed(5)
+    V, T = 10000, 8192
+    ids = torch.randint(0, V, (T,))
+    ids[torch.randperm(T)[:7700]] = 1
+    ids[torch.randperm(T)[:1200]] = 10001 % V  # same bucket family as id 1 for small NB, other slot
+    w = torch.nn.Parameter(torch.zeros(V, D, device=dev))
+    do = torch.randn(T, D, device=dev).bfloat16()
+    grads = []
+    for _ in range(2):
+        w.grad = None
+        out = embedding(ids.to(dev), w, None, 0.1, R.DropoutRNG(2).to(dev), 9, padding_idx=None,
+                        out_dtype=torch.bfloat16)
+        out.backward(do)
+        grads.append(w.grad.clone())
+    assert torch.equal(grads[0], grads[1])
+    wc = torch.nn.Parameter(torch.zeros(V, D))
+    oc = embedding(ids, wc, None, 0.1, R.DropoutRNG(2), 9, padding_idx=None, out_dtype=torch.float32)
+    oc.backward(do.float().cpu())
+    _close(grads[0], wc.grad, 1e-3, 1e-4, "emb heavy grad")
+
+
 @pytest.mark.parametrize("act,p", [(None, 0.0), ("relu", 0.1), ("relu", 0.0)])
 def test_linear(act, p):
     torch.manual_seed(4)

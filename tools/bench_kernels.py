@@ -112,7 +112,7 @@ def main():
                                  seed.data_ptr(), 3, thr, 1.1, st()))
     print(f"emb_fwd     {t:8.1f} us")
     dt = torch.zeros(V, D, device=dev)
-    ews = torch.empty(C.emb_det_ws_bytes(M, V), device=dev, dtype=torch.uint8)
+    ews = torch.empty(C.emb_det_ws_bytes(M, V, D), device=dev, dtype=torch.uint8)
     for det in (0, 1):
         t = timeit(lambda: C.emb_bwd(ids.data_ptr(), eo.data_ptr(), dt.data_ptr(), M, D, -1, seed.data_ptr(), 3, thr,
                                      1.1, V, ews.data_ptr() if det else 0, st()))
