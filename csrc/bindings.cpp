@@ -68,6 +68,7 @@ int smi_mlp(const MLPArgs*, int, hipStream_t);
 int smi_mlp_grid(int);
 int smi_gemm(const GemmArgs*, hipStream_t);
 int smi_gemm_f32(const GemmF32Args*, hipStream_t);
+int smi_gemm_f32_algo(int);
 int smi_gemm_f32_wgrad_group(const void* const*, const long*, const void* const*, const long*, void* const*, void* const*,
                              const int*, const int*, const int*, int, hipStream_t);
 int smi_splitk_reduce(const float*, int, long, float*, long, float*, int, hipStream_t);
@@ -383,6 +384,8 @@ PYBIND11_MODULE(_C, m) {
     g.thresh = thresh; g.dscale = dscale; g.splits = splits; g.bias_grad = (float*)bias_grad;
     chk(smi_gemm_f32(&g, S(st)), "gemm_f32");
   });
+  m.def("gemm_f32_algo", [](int set) { return smi_gemm_f32_algo(set); },
+        "fp32 GEMM product algorithm: 0 = f32 MFMA, 6 = 3-way bf16 split (6 terms); set < 0 queries");
   m.def("gemm_f32_wgrad_group", [](std::vector<u> A, std::vector<long> lda, std::vector<u> B, std::vector<long> ldb,
                                    std::vector<u> C, std::vector<u> bias, std::vector<int> n, std::vector<int> k,
                                    std::vector<int> T, u st) {

@@ -115,6 +115,36 @@ __device__ __forceinline__ int f32_tile_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
+// ---- fp32 products on the bf16 matrix cores (3-way split, 6 product terms) ----
+// x = hi + mid + lo exactly (three bf16 slices of 8 significant bits each, round-to-nearest-even
+// at every step, so each residual is exact in fp32), and every slice product is exact in the
+// fp32 accumulator.  a.b = hi.hi + (hi.mid + mid.hi + hi.lo + mid.mid + lo.hi) + O(2^-24 |a||b|):
+// the dropped terms (mid.lo, lo.mid, lo.lo) are below one fp32 rounding of the product, and the
+// big term is accumulated in its OWN fp32 chain (same rounding sequence as the f32 MFMA path) with
+// the five correction terms in a second accumulator added once at the end.  Rate: 6 x
+// v_mfma_f32_32x32x16_bf16 (32 cycles each) per 32x32x16 block vs 8 x v_mfma_f32_32x32x2_f32
+// (64 cycles each) — 2.7x the f32 matrix-core rate for the same exact-product fp32 arithmetic.
+struct Split3 { bf16x8_t h, m, l; };
+__device__ __forceinline__ void split3_pair(float x0, float x1, uint32_t& h, uint32_t& m, uint32_t& l) {
+  h = pack2bf(x0, x1);
+  const float r0 = x0 - __uint_as_float(h << 16), r1 = x1 - __uint_as_float(h & 0xFFFF0000u);
+  m = pack2bf(r0, r1);
+  const float s0 = r0 - __uint_as_float(m << 16), s1 = r1 - __uint_as_float(m & 0xFFFF0000u);
+  l = pack2bf(s0, s1);
+}
+// 8 consecutive fragment values f[o..o+7] -> the three bf16x8 MFMA operands
+__device__ __forceinline__ Split3 split3_8(const float* f) {
+  uint32_t h[4], m[4], l[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) split3_pair(f[2 * q], f[2 * q + 1], h[q], m[q], l[q]);
+  Split3 r;
+  r.h = __builtin_bit_cast(bf16x8_t, (uint4){h[0], h[1], h[2], h[3]});
+  r.m = __builtin_bit_cast(bf16x8_t, (uint4){m[0], m[1], m[2], m[3]});
+  r.l = __builtin_bit_cast(bf16x8_t, (uint4){l[0], l[1], l[2], l[3]});
+  return r;
+}
+#define MF32X16(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
+
 // Fused epilogue of one output tile (acc = this wave's FM x 2 32x32 accumulators):
 // FWD + bias, activation, dropout; DGRAD + residual, relu'/dropout mask; WGRAD accumulate (+ the
 // bias-gradient row sums of A).  Each store instruction writes two full 128-B row segments.
@@ -402,11 +432,12 @@ __device__ __forceinline__ void f32_epilogue_lds(const GemmF32Args& g, f32x16_t 
 //   * writes k-tile t+2 (loaded one iteration earlier) into LDS stage (t+2)%3,
 // interleaved one-per-MFMA by sched_group_barrier; one barrier per k-tile.
 #define SGB(mask, n) __builtin_amdgcn_sched_group_barrier((mask), (n), 0)
+#define SG_VALU 0x002
 #define SG_MFMA 0x008
 #define SG_VMEM_RD 0x020
 #define SG_DS_RD 0x100
 #define SG_DS_WR 0x200
-template <bool AK, bool BKM, int EPI>
+template <bool AK, bool BKM, int EPI, int XS = 0>
 __device__ __forceinline__ void gemm_f32_tile_pipe(const GemmF32Args& g, int tile, int split, float* smem) {
   constexpr int FM = 2, BMT = 128;
   using TA = F32Tile<AK, BMT>;
@@ -421,13 +452,13 @@ __device__ __forceinline__ void gemm_f32_tile_pipe(const GemmF32Args& g, int til
   const int kbeg = split * g.k_per_split;
   const int kend = min(g.K, kbeg + g.k_per_split);
   const int nk = (kend - kbeg + FBK - 1) / FBK;
-  f32x16_t acc[FM][2];
+  f32x16_t acc[FM][2], cacc[FM][2];  // cacc: correction terms of the split-bf16 path (XS)
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = cacc[i][j][r] = 0.f;
   const bool do_bias = AK && g.bias_grad && n0 == 0 && wn == 0;
   float bsum[FM] = {0.f, 0.f};
   float af0[FM][16], bf0[2][16], af1[FM][16], bf1[2][16];
@@ -454,12 +485,36 @@ __device__ __forceinline__ void gemm_f32_tile_pipe(const GemmF32Args& g, int til
     for (int j = 0; j < 2; ++j) f32_frag<BKM, FBN>(ta + TA::ELEMS, wn * 64 + j * 32, lane, bf[j]);
   };
   auto mma = [&](float (&af)[FM][16], float (&bf)[2][16]) {
+    if constexpr (XS == 6) {
+      // k-block b of the 32-deep tile: lane half h feeds k = 16h + 8b + e (e = 0..7) — the same
+      // k <-> (lane, slot) permutation for A and B, so the fp32 fragments are reused as read
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        Split3 sa[FM], sb[2];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) sa[i] = split3_8(&af[i][8 * b]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) sb[j] = split3_8(&bf[j][8 * b]);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            acc[i][j] = MF32X16(sa[i].h, sb[j].h, acc[i][j]);
+            cacc[i][j] = MF32X16(sa[i].l, sb[j].h, cacc[i][j]);
+            cacc[i][j] = MF32X16(sa[i].m, sb[j].m, cacc[i][j]);
+            cacc[i][j] = MF32X16(sa[i].h, sb[j].l, cacc[i][j]);
+            cacc[i][j] = MF32X16(sa[i].m, sb[j].h, cacc[i][j]);
+            cacc[i][j] = MF32X16(sa[i].h, sb[j].m, cacc[i][j]);
+          }
+      }
+    } else {
 #pragma unroll
     for (int s2 = 0; s2 < 16; ++s2)
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s2], bf[j][s2], acc[i][j], 0, 0, 0);
+    }
     if constexpr (AK) {  // bias-gradient row sums (kept only by the column-block-0 waves)
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -467,8 +522,69 @@ __device__ __forceinline__ void gemm_f32_tile_pipe(const GemmF32Args& g, int til
         for (int s2 = 0; s2 < 16; ++s2) bsum[i] += af[i][s2];
     }
   };
+  // ---- split-bf16 path (XS): block-pipelined — while block 0's MFMAs run, block 1 of the same
+  // k-tile is split; while block 1's run, block 0 of the NEXT k-tile (its fragments were read
+  // from LDS at the top of this half-iteration) is split; so the split VALU work issues in the
+  // shadow of the matrix pipe instead of in front of it
+  auto xsplit = [&](const float (&af)[FM][16], const float (&bf)[2][16], int b, Split3 (&sa)[FM], Split3 (&sb)[2]) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) sa[i] = split3_8(&af[i][8 * b]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) sb[j] = split3_8(&bf[j][8 * b]);
+  };
+  auto xmma = [&](const Split3 (&sa)[FM], const Split3 (&sb)[2]) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        acc[i][j] = MF32X16(sa[i].h, sb[j].h, acc[i][j]);
+        cacc[i][j] = MF32X16(sa[i].l, sb[j].h, cacc[i][j]);
+        cacc[i][j] = MF32X16(sa[i].m, sb[j].m, cacc[i][j]);
+        cacc[i][j] = MF32X16(sa[i].h, sb[j].l, cacc[i][j]);
+        cacc[i][j] = MF32X16(sa[i].m, sb[j].h, cacc[i][j]);
+        cacc[i][j] = MF32X16(sa[i].h, sb[j].m, cacc[i][j]);
+      }
+  };
+  // one k-tile: block 0 from the carried planes (p*), block 1 split from (af, bf); the next
+  // k-tile's block 0 split from (afn, bfn) into p*
+  auto xtile = [&](float (&af)[FM][16], float (&bf)[2][16], float (&afn)[FM][16], float (&bfn)[2][16],
+                   Split3 (&pa)[FM], Split3 (&pb)[2]) {
+    Split3 qa[FM], qb[2];
+    xsplit(af, bf, 1, qa, qb);
+    xmma(pa, pb);
+    if constexpr (AK) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) bsum[i] += af[i][s2];
+    }
+    xsplit(afn, bfn, 0, pa, pb);
+    xmma(qa, qb);
+  };
+  // interleave of one split-path half-iteration: phase A = block 0's 24 MFMAs with the global
+  // loads, the LDS fragment reads, block 1's split VALU and the LDS writes; phase B = block 1's
+  // 24 MFMAs with the next k-tile's block-0 split VALU
+  auto xschedule = [&]() {
+    constexpr int NMF = FM * 2 * 6;  // MFMAs per block
+    constexpr int NV = TA::NV + TB::NV;
+    constexpr int RDPM = (NRD + NMF - 1) / NMF;
+#pragma unroll
+    for (int i = 0; i < NMF; ++i) {
+      SGB(SG_MFMA, 1);
+      if (i < NV) SGB(SG_VMEM_RD, 1);
+      SGB(SG_DS_RD, RDPM);
+      SGB(SG_VALU, 6);
+      if (i >= NMF - NV) SGB(SG_DS_WR, 1);
+    }
+#pragma unroll
+    for (int i = 0; i < NMF; ++i) {
+      SGB(SG_MFMA, 1);
+      SGB(SG_VALU, 7);
+    }
+  };
   // the interleave of one iteration: 8 x (MFMA, global load), reads, 8 x (MFMA, LDS write), rest
   auto schedule = [&]() {
+    if constexpr (XS != 0) return;  // split path: compiler-scheduled (VALU splits between MFMAs)
 #pragma unroll
     for (int i = 0; i < TA::NV + TB::NV; ++i) { SGB(SG_MFMA, 1); SGB(SG_VMEM_RD, 1); }
     if constexpr (NRD <= 40) {
@@ -494,6 +610,24 @@ __device__ __forceinline__ void gemm_f32_tile_pipe(const GemmF32Args& g, int til
   // tiles past nk load zeros): a mid-pair exit made the compiler keep the accumulators in two
   // register sets and copy 64 AGPRs per k-tile
   const int nk2 = (nk + 1) & ~1;
+  if constexpr (XS != 0) {
+    Split3 pa[FM], pb[2];
+    xsplit(af0, bf0, 0, pa, pb);
+    for (int kt = 0; kt < nk2; kt += 2) {
+      ld(kt + 3, ra0, rb0);
+      rd(kt + 1, af1, bf1);
+      st(kt + 2, ra1, rb1);
+      xtile(af0, bf0, af1, bf1, pa, pb);
+      xschedule();
+      __syncthreads();
+      ld(kt + 4, ra1, rb1);
+      rd(kt + 2, af0, bf0);
+      st(kt + 3, ra0, rb0);
+      xtile(af1, bf1, af0, bf0, pa, pb);
+      xschedule();
+      __syncthreads();
+    }
+  } else
   for (int kt = 0; kt < nk2; kt += 2) {
     ld(kt + 3, ra0, rb0);
     rd(kt + 1, af1, bf1);
@@ -508,16 +642,22 @@ __device__ __forceinline__ void gemm_f32_tile_pipe(const GemmF32Args& g, int til
     schedule();
     __syncthreads();
   }
+  if constexpr (XS != 0) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] += cacc[i][j];
+  }
   f32_epilogue_lds<AK, EPI>(g, acc, bsum, m0, n0, wm, wn, lane, do_bias, smem);
 }
 
-template <bool AK, bool BKM, int EPI>
+template <bool AK, bool BKM, int EPI, int XS>
 __global__ __launch_bounds__(256, 1) void gemm_f32_pipe_kernel(GemmF32Args g) {
   __shared__ __attribute__((aligned(16))) float smem[3 * (F32Tile<AK, 128>::ELEMS + F32Tile<BKM, FBN>::ELEMS)];
   const int nwg = ((g.M + 127) / 128) * ((g.N + FBN - 1) / FBN);
   const int split = blockIdx.x / nwg;
   const int tile = f32_tile_remap(blockIdx.x - split * nwg, nwg);
-  gemm_f32_tile_pipe<AK, BKM, EPI>(g, tile, split, smem);
+  gemm_f32_tile_pipe<AK, BKM, EPI, XS>(g, tile, split, smem);
 }
 
 template <bool AK, bool BKM, int FM, int PF>
@@ -528,6 +668,21 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmF32Args g) {
   const int split = blockIdx.x / nwg;
   const int tile = f32_tile_remap(blockIdx.x - split * nwg, nwg);
   gemm_f32_tile<AK, BKM, FM, PF>(g, tile, split, smem);
+}
+
+// fp32 product algorithm: 0 = f32 MFMA (v_mfma_f32_32x32x2_f32), 6 = 3-way bf16 split, 6 terms
+// (SMI_F32_ALGO; see split3_8)
+static int g_f32_algo = -1;
+static int smi_f32_algo() {
+  if (g_f32_algo < 0) {
+    const char* e = getenv("SMI_F32_ALGO");
+    g_f32_algo = (e && atoi(e) == 6) ? 6 : 0;
+  }
+  return g_f32_algo;
+}
+extern "C" int smi_gemm_f32_algo(int set) {  // set < 0: query only
+  if (set == 0 || set == 6) g_f32_algo = set;
+  return smi_f32_algo();
 }
 
 static int f32_ok(const GemmF32Args& g) {
@@ -579,7 +734,11 @@ extern "C" int smi_gemm_f32(const GemmF32Args* args, hipStream_t st) {
       fe = (g.resid ? FE_RESID : 0) | (g.dact_y ? FE_DACT : 0);
     }
     fe |= (g.atomic ? FE_ATOMIC : (g.beta_acc ? FE_ACC : 0));
-#define F32P(AKV, BKV, E) hipLaunchKernelGGL((gemm_f32_pipe_kernel<AKV, BKV, E>), grid2, block, 0, st, g)
+#define F32P(AKV, BKV, E)                                                                          \
+  do {                                                                                             \
+    if (smi_f32_algo() == 6) hipLaunchKernelGGL((gemm_f32_pipe_kernel<AKV, BKV, E, 6>), grid2, block, 0, st, g); \
+    else hipLaunchKernelGGL((gemm_f32_pipe_kernel<AKV, BKV, E, 0>), grid2, block, 0, st, g);      \
+  } while (0)
     if (g.mode == 0) {
       switch (fe) {
         case 0: F32P(false, false, 0); break;
@@ -632,6 +791,7 @@ struct WgradGroupF32 {
   int lda[WGF_MAX], ldb[WGF_MAX], n[WGF_MAX], k[WGF_MAX], T[WGF_MAX];
   int t0[WGF_MAX + 1]; int count;
 };
+template <int XS>
 __global__ __launch_bounds__(256, 1) void gemm_f32_wgrad_group_kernel(WgradGroupF32 gr) {
   __shared__ __attribute__((aligned(16))) float smem[3 * (F32Tile<true, 128>::ELEMS + F32Tile<true, FBN>::ELEMS)];
   const int t = blockIdx.x;
@@ -644,7 +804,7 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_wgrad_group_kernel(WgradGroup
   g.bias_grad = gr.bias[e];
   const int nwg = ((g.M + 127) / 128) * ((g.N + FBN - 1) / FBN);
   const int lt = t - gr.t0[e];
-  if (lt < nwg) gemm_f32_tile_pipe<true, true, FE_ACC>(g, f32_tile_remap(lt, nwg), 0, smem);  // lt >= nwg: padding
+  if (lt < nwg) gemm_f32_tile_pipe<true, true, FE_ACC, XS>(g, f32_tile_remap(lt, nwg), 0, smem);  // lt >= nwg: padding
 }
 
 extern "C" int smi_gemm_f32_wgrad_group(const void* const* A, const long* lda, const void* const* B, const long* ldb,
@@ -666,6 +826,7 @@ extern "C" int smi_gemm_f32_wgrad_group(const void* const* A, const long* lda, c
   }
   gr.t0[count] = tot;
   gr.count = count;
-  hipLaunchKernelGGL(gemm_f32_wgrad_group_kernel, dim3(tot), dim3(256), 0, st, gr);
+  if (smi_f32_algo() == 6) hipLaunchKernelGGL(gemm_f32_wgrad_group_kernel<6>, dim3(tot), dim3(256), 0, st, gr);
+  else hipLaunchKernelGGL(gemm_f32_wgrad_group_kernel<0>, dim3(tot), dim3(256), 0, st, gr);
   SMI_CHECK_LAUNCH();
 }

@@ -73,6 +73,10 @@ class NativeComm:
         self.comm.destroy()
 
 
+class IpcUnavailable(RuntimeError):
+    """IPC mapping or the all-reduce self-test failed on at least one rank (all ranks agree)."""
+
+
 class IpcAllReduce:
     """Sum-all-reduce of fp32 tensors of up to ``cap_floats`` elements among the ranks of
     ``group`` (one node), in place, on the current stream."""
@@ -93,17 +97,40 @@ class IpcAllReduce:
         handles = [None] * self.world
         dist.all_gather_object(handles, (hdata, hsig), group=group)
         self.data, self.sig, self._opened = [], [], []
+        opened = True
         for r, (hd, hs) in enumerate(handles):
             if r == self.rank:
                 self.data.append(data)
                 self.sig.append(sig)
-            else:
-                pd, ps = C.ipc_open(hd), C.ipc_open(hs)
+            elif opened:
+                try:
+                    pd, ps = C.ipc_open(hd), C.ipc_open(hs)
+                except RuntimeError:
+                    opened = False
+                    continue
                 self._opened += [pd, ps]
                 self.data.append(pd)
                 self.sig.append(ps)
         self.err = torch.zeros(1, dtype=torch.int32, device="cuda")
         self.ctr = torch.zeros(2, dtype=torch.int32, device="cuda")  # {epoch, ticket}: advanced by the kernel
+        # every rank must be able to map every peer AND the kernel must produce the exact sum on
+        # this topology (peer reads over xGMI, system-scope flags): a one-call self-test whose
+        # verdict all ranks agree on through the regular process group; on failure the caller
+        # keeps the RCCL path (IpcUnavailable) instead of risking a hang or a wrong gradient
+        ok = opened
+        if opened:
+            probe = torch.full((self.cap if self.cap < 4096 else 4096,), float(self.rank + 1), device="cuda")
+            self(probe)
+            torch.cuda.synchronize()
+            want = float(self.world * (self.world + 1) // 2)
+            ok = bool(int(self.err.item()) == 0 and bool((probe == want).all()))
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                            device="cuda" if dist.get_backend(group) == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+        if not int(flag.item()):
+            self.close()
+            raise IpcUnavailable("IPC all-reduce self-test failed on some rank; using the collective path")
+        self.err.zero_()
         dist.barrier(group=group)
 
     def __call__(self, t):

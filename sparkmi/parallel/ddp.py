@@ -64,8 +64,11 @@ class DataParallel:
             ipc = os.environ.get("SPARKMI_IPC_AR", "1") != "0"
         if (ipc and not self.zero and self.world > 1 and flat.grad.is_cuda and flat.numel * 4 <= IPC_LIMIT_BYTES
                 and self.world <= 8 and _single_node(self.world)):
-            from .comm import IpcAllReduce
-            self.ipc = IpcAllReduce(cap_floats=flat.numel, group=group)
+            from .comm import IpcAllReduce, IpcUnavailable
+            try:
+                self.ipc = IpcAllReduce(cap_floats=flat.numel, group=group)
+            except IpcUnavailable:
+                self.ipc = None  # every rank agreed: buckets go through the process group
         self._build_buckets()
         self._pending = None
         self._works = []
