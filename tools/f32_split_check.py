@@ -29,8 +29,32 @@ def err(y, ref):
     return float(d.abs().max() / ref.abs().max()), float(d.norm() / ref.norm())
 
 
+ALGOS = (0, 6)
+
+
+def group_time(C, algo, iters):
+    M = 8192
+    probs = [(1536, 512), (512, 512), (1024, 512), (512, 512), (512, 512), (1024, 512), (512, 1024)]
+    dys = [torch.randn(M, n, device="cuda") for n, _ in probs]
+    xs = [torch.randn(M, k, device="cuda") for _, k in probs]
+    gws = [torch.zeros(n, k, device="cuda") for n, k in probs]
+    gbs = [torch.zeros(n, device="cuda") for n, _ in probs]
+    C.gemm_f32_algo(algo)
+
+    def grp():
+        C.gemm_f32_wgrad_group([d.data_ptr() for d in dys], [d.stride(0) for d in dys], [x.data_ptr() for x in xs],
+                               [x.stride(0) for x in xs], [g.data_ptr() for g in gws], [b.data_ptr() for b in gbs],
+                               [n for n, _ in probs], [k for _, k in probs], [M] * len(probs), _native.stream())
+    t = timeit(grp, max(3, iters // 4))
+    fl = sum(2 * M * n * k for n, k in probs)
+    return t, fl / t / 1e6
+
+
 def main(iters=20):
     C = _native.C()
+    for a in ALGOS:
+        t, tf = group_time(C, a, iters)
+        print(f"algo{a}: wgrad group (decoder layer) {t:8.1f} us {tf:6.1f} TF/s", flush=True)
     dev = "cuda"
     M = 8192
     torch.manual_seed(0)
@@ -41,7 +65,7 @@ def main(iters=20):
         ref_d = dy.double() @ w.double()
         ref_w = dy.double().t() @ x.double()
         line = []
-        for algo in (0, 6):
+        for algo in ALGOS:
             C.gemm_f32_algo(algo)
             yf = G.fwd32(x, w)
             yd = G.dgrad32(dy, w)
