@@ -63,6 +63,8 @@ def parse(argv=None):
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--split", type=int, default=1, help="multi-graph backward with overlapped all-reduce (DP)")
     ap.add_argument("--no-aux", action="store_true", help="skip the LSTM / MLP extras")
+    ap.add_argument("--no-f32-compare", action="store_true",
+                    help="skip the f32-MFMA comparison run of the fp32 transformer step")
     return ap.parse_args(argv)
 
 
@@ -356,7 +358,7 @@ def main():
     tr = {dt: bench_transformer(args, rank, world, device, dt) for dt in dtypes}
     head = tr[dtypes[0]]
     f32mfma = None
-    if "fp32" in dtypes and device.type == "cuda":
+    if "fp32" in dtypes and device.type == "cuda" and not args.no_f32_compare:
         # the same fp32 step with every GEMM product on v_mfma_f32_32x32x2_f32 instead of the
         # exact-product bf16 split (both fp32 in / out / accumulate), for comparison
         from sparkmi import _native

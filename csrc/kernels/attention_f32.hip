@@ -28,6 +28,7 @@
 #include "smi_common.h"
 #include "smi_attention.h"
 #include "smi_attn_mask.h"
+#include "smi_split3.h"
 
 #define FCH 32    // rows per streamed chunk (= one 32-row MFMA block)
 #define FPR 68    // padded pitch (floats) of row-fragment images
@@ -88,7 +89,7 @@ __device__ __forceinline__ int fa_kl(int r, int h) { return (r & 3) + 8 * (r >> 
 
 // ---------------------------------------------------------------------------------------------
 // Forward: S^T = K Q^T (query on the lane), online softmax, O^T += V^T P^T.
-template <int MODE, bool KPAD>
+template <int MODE, bool KPAD, int XS>
 __global__ __launch_bounds__(256, 2) void attn_f32_fwd_kernel(AttnF32Args a) {
   __shared__ __attribute__((aligned(16))) float Ks[2][FCH * FPR];
   __shared__ __attribute__((aligned(16))) float Vs[2][FCH * 64];
@@ -134,8 +135,7 @@ __global__ __launch_bounds__(256, 2) void attn_f32_fwd_kernel(AttnF32Args a) {
       {
         float kf[32];
         fa_rowfrag(Ks[buf], kb, lane, kf);
-#pragma unroll
-        for (int t = 0; t < 32; ++t) s = MF32(kf[t], qf[t], s);
+        s = f32_chain<XS, 32>(kf, qf, s);
       }
       float cmax = -INFINITY;
       if (uni) {
@@ -166,13 +166,15 @@ __global__ __launch_bounds__(256, 2) void attn_f32_fwd_kernel(AttnF32Args a) {
       psum = smi_row32_swap_sum(psum);
       l = l * alpha + psum;
       m = mnew;
+      float sv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sv[r] = s[r];
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
         o[dt] *= alpha;
         float vf[16];
         fa_colfrag<64>(Vs[buf], kb, dt * 32, lane, vf);
-#pragma unroll
-        for (int t = 0; t < 16; ++t) o[dt] = MF32(vf[t], s[t], o[dt]);
+        o[dt] = f32_chain<XS, 16>(vf, sv, o[dt]);
       }
     } while (0);
     if (more) { fa_store_chunk<FPR>(Ks[buf ^ 1], pk); fa_store_chunk<64>(Vs[buf ^ 1], pv); }
@@ -192,8 +194,8 @@ __global__ __launch_bounds__(256, 2) void attn_f32_fwd_kernel(AttnF32Args a) {
 
 // dQ: S^T = K Q^T, dP^T = V dO^T, dS^T = P^T o (dP^T - delta), dQ^T += K^T dS^T; also writes
 // delta = rowsum(dO * O) for the dK/dV kernel.
-template <int MODE, bool KPAD>
-__global__ __launch_bounds__(256, 2) void attn_f32_dq_kernel(AttnF32Args a) {
+template <int MODE, bool KPAD, int XS>
+__global__ __launch_bounds__(256, XS ? 1 : 2) void attn_f32_dq_kernel(AttnF32Args a) {
   __shared__ __attribute__((aligned(16))) float Ks[2][FCH * FPR];
   __shared__ __attribute__((aligned(16))) float Vs[2][FCH * FPR];
   const int hh = blockIdx.y, b = blockIdx.z;
@@ -252,14 +254,12 @@ __global__ __launch_bounds__(256, 2) void attn_f32_dq_kernel(AttnF32Args a) {
       {
         float kf[32];
         fa_rowfrag(Ks[buf], kb, lane, kf);
-#pragma unroll
-        for (int t = 0; t < 32; ++t) s = MF32(kf[t], qf[t], s);
+        s = f32_chain<XS, 32>(kf, qf, s);
       }
       {
         float vf[32];
         fa_rowfrag(Vs[buf], kb, lane, vf);
-#pragma unroll
-        for (int t = 0; t < 32; ++t) dp = MF32(vf[t], df[t], dp);
+        dp = f32_chain<XS, 32>(vf, df, dp);
       }
       if (uni) {
         const float off = ub - lse;
@@ -273,12 +273,14 @@ __global__ __launch_bounds__(256, 2) void attn_f32_dq_kernel(AttnF32Args a) {
           s[r] = __builtin_amdgcn_exp2f(x - lse) * (dp[r] - dl);  // exp2(-inf) = 0 for masked entries
         }
       }
+      float sv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sv[r] = s[r];
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
         float kc[16];
         fa_colfrag<FPR>(Ks[buf], kb, dt * 32, lane, kc);
-#pragma unroll
-        for (int t = 0; t < 16; ++t) acc[dt] = MF32(kc[t], s[t], acc[dt]);
+        acc[dt] = f32_chain<XS, 16>(kc, sv, acc[dt]);
       }
     } while (0);
     if (more) { fa_store_chunk<FPR>(Ks[buf ^ 1], pk); fa_store_chunk<FPR>(Vs[buf ^ 1], pv); }
@@ -293,8 +295,8 @@ __global__ __launch_bounds__(256, 2) void attn_f32_dq_kernel(AttnF32Args a) {
 
 // dK, dV: key on the lane.  S = Q K^T, dP = dO V^T, P = exp2(S' - lse), dS = P o (dP - delta),
 // dV^T += dO^T P, dK^T += Q^T dS.
-template <int MODE, bool KPAD>
-__global__ __launch_bounds__(256, 2) void attn_f32_dkdv_kernel(AttnF32Args a) {
+template <int MODE, bool KPAD, int XS>
+__global__ __launch_bounds__(256, XS ? 1 : 2) void attn_f32_dkdv_kernel(AttnF32Args a) {
   __shared__ __attribute__((aligned(16))) float Qs[2][FCH * FPR];
   __shared__ __attribute__((aligned(16))) float Ds[2][FCH * FPR];
   __shared__ float lse_s[2][FCH], dl_s[2][FCH];
@@ -357,14 +359,12 @@ __global__ __launch_bounds__(256, 2) void attn_f32_dkdv_kernel(AttnF32Args a) {
       {
         float qr[32];
         fa_rowfrag(Qs[buf], qb, lane, qr);
-#pragma unroll
-        for (int t = 0; t < 32; ++t) s = MF32(qr[t], kf[t], s);
+        s = f32_chain<XS, 32>(qr, kf, s);
       }
       {
         float dr[32];
         fa_rowfrag(Ds[buf], qb, lane, dr);
-#pragma unroll
-        for (int t = 0; t < 32; ++t) dp = MF32(dr[t], vf[t], dp);
+        dp = f32_chain<XS, 32>(dr, vf, dp);
       }
       // s[r]: query q0 + qb + fa_kl(r, h), key kj.  Rows past Sq carry lse = +inf (p = 0).
 #pragma unroll
@@ -378,16 +378,20 @@ __global__ __launch_bounds__(256, 2) void attn_f32_dkdv_kernel(AttnF32Args a) {
         s[r] = p;
         dp[r] = p * (dp[r] - dl_s[buf][ql]);
       }
+      float sv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sv[r] = s[r];
+      float dpv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dpv[r] = dp[r];
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
         float dc[16];
         fa_colfrag<FPR>(Ds[buf], qb, dt * 32, lane, dc);
-#pragma unroll
-        for (int t = 0; t < 16; ++t) dv[dt] = MF32(dc[t], s[t], dv[dt]);
+        dv[dt] = f32_chain<XS, 16>(dc, sv, dv[dt]);
         float qc[16];
         fa_colfrag<FPR>(Qs[buf], qb, dt * 32, lane, qc);
-#pragma unroll
-        for (int t = 0; t < 16; ++t) dk[dt] = MF32(qc[t], dp[t], dk[dt]);
+        dk[dt] = f32_chain<XS, 16>(qc, dpv, dk[dt]);
       }
     } while (0);
     if (more) {
@@ -408,18 +412,24 @@ __global__ __launch_bounds__(256, 2) void attn_f32_dkdv_kernel(AttnF32Args a) {
   }
 }
 
+// product algorithm shared with the fp32 GEMM (csrc/kernels/gemm_f32.hip:smi_gemm_f32_algo):
+// 0 = f32 MFMA chains, otherwise the exact-product bf16 split (smi_split3.h)
+extern "C" int smi_gemm_f32_algo(int);
+#define SMI_ATTN_F32_MODES(KERNEL, XSV, GRID, ARGS)                                                        \
+  switch ((ARGS).mode) {                                                                                   \
+    case 0: if (kp_) hipLaunchKernelGGL((KERNEL<0, true, XSV>), GRID, dim3(256), 0, st, ARGS);             \
+            else hipLaunchKernelGGL((KERNEL<0, false, XSV>), GRID, dim3(256), 0, st, ARGS); break;         \
+    case 1: if (kp_) hipLaunchKernelGGL((KERNEL<1, true, XSV>), GRID, dim3(256), 0, st, ARGS);             \
+            else hipLaunchKernelGGL((KERNEL<1, false, XSV>), GRID, dim3(256), 0, st, ARGS); break;         \
+    case 2: if (kp_) hipLaunchKernelGGL((KERNEL<2, true, XSV>), GRID, dim3(256), 0, st, ARGS);             \
+            else hipLaunchKernelGGL((KERNEL<2, false, XSV>), GRID, dim3(256), 0, st, ARGS); break;         \
+    default: return -1;                                                                                    \
+  }
 #define SMI_ATTN_F32_DISPATCH(KERNEL, GRID, ARGS)                                                           \
   do {                                                                                                     \
     const bool kp_ = (ARGS).kpad != nullptr;                                                               \
-    switch ((ARGS).mode) {                                                                                 \
-      case 0: if (kp_) hipLaunchKernelGGL((KERNEL<0, true>), GRID, dim3(256), 0, st, ARGS);                \
-              else hipLaunchKernelGGL((KERNEL<0, false>), GRID, dim3(256), 0, st, ARGS); break;            \
-      case 1: if (kp_) hipLaunchKernelGGL((KERNEL<1, true>), GRID, dim3(256), 0, st, ARGS);                \
-              else hipLaunchKernelGGL((KERNEL<1, false>), GRID, dim3(256), 0, st, ARGS); break;            \
-      case 2: if (kp_) hipLaunchKernelGGL((KERNEL<2, true>), GRID, dim3(256), 0, st, ARGS);                \
-              else hipLaunchKernelGGL((KERNEL<2, false>), GRID, dim3(256), 0, st, ARGS); break;            \
-      default: return -1;                                                                                  \
-    }                                                                                                      \
+    if (smi_gemm_f32_algo(-1) == 0) { SMI_ATTN_F32_MODES(KERNEL, 0, GRID, ARGS) }                         \
+    else { SMI_ATTN_F32_MODES(KERNEL, 1, GRID, ARGS) }                                                     \
   } while (0)
 
 static int fa_ok(const AttnF32Args& a) {

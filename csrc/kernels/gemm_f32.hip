@@ -26,6 +26,7 @@
 // store instruction two full 128-B row segments.
 #include "smi_common.h"
 #include "smi_gemm_f32.h"
+#include "smi_split3.h"
 
 #define FBN 128
 #define FBK 32
@@ -124,26 +125,6 @@ __device__ __forceinline__ int f32_tile_remap(int orig, int nwg) {
 // the five correction terms in a second accumulator added once at the end.  Rate: 6 x
 // v_mfma_f32_32x32x16_bf16 (32 cycles each) per 32x32x16 block vs 8 x v_mfma_f32_32x32x2_f32
 // (64 cycles each) — 2.7x the f32 matrix-core rate for the same exact-product fp32 arithmetic.
-struct Split3 { bf16x8_t h, m, l; };
-__device__ __forceinline__ void split3_pair(float x0, float x1, uint32_t& h, uint32_t& m, uint32_t& l) {
-  h = pack2bf(x0, x1);
-  const float r0 = x0 - __uint_as_float(h << 16), r1 = x1 - __uint_as_float(h & 0xFFFF0000u);
-  m = pack2bf(r0, r1);
-  const float s0 = r0 - __uint_as_float(m << 16), s1 = r1 - __uint_as_float(m & 0xFFFF0000u);
-  l = pack2bf(s0, s1);
-}
-// 8 consecutive fragment values f[o..o+7] -> the three bf16x8 MFMA operands
-__device__ __forceinline__ Split3 split3_8(const float* f) {
-  uint32_t h[4], m[4], l[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) split3_pair(f[2 * q], f[2 * q + 1], h[q], m[q], l[q]);
-  Split3 r;
-  r.h = __builtin_bit_cast(bf16x8_t, (uint4){h[0], h[1], h[2], h[3]});
-  r.m = __builtin_bit_cast(bf16x8_t, (uint4){m[0], m[1], m[2], m[3]});
-  r.l = __builtin_bit_cast(bf16x8_t, (uint4){l[0], l[1], l[2], l[3]});
-  return r;
-}
-#define MF32X16(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
 
 // Fused epilogue of one output tile (acc = this wave's FM x 2 32x32 accumulators):
 // FWD + bias, activation, dropout; DGRAD + residual, relu'/dropout mask; WGRAD accumulate (+ the

@@ -17,6 +17,18 @@ from sparkmi.ops.attention import attention_reference, cross_attention, self_att
 dev = "cuda"
 
 
+@pytest.fixture(autouse=True, params=[6, 0], ids=["split", "f32mfma"])
+def f32_algo(request):
+    """Every fp32 kernel test runs on both product algorithms: the exact-product bf16 split
+    (default) and the v_mfma_f32_32x32x2_f32 chains (csrc/kernels/gemm_f32.hip:smi_gemm_f32_algo,
+    shared by attention_f32.hip)."""
+    C = _native.C()
+    prev = C.gemm_f32_algo(-1)
+    C.gemm_f32_algo(request.param)
+    yield request.param
+    C.gemm_f32_algo(prev)
+
+
 def _close(a, b, atol, rtol, msg=""):
     a, b = a.double().cpu(), b.double().cpu()
     err = (a - b).abs()
