@@ -47,3 +47,35 @@ __device__ __forceinline__ f32x16_t f32_chain(const float (&x)[T], const float (
   }
   return acc;
 }
+
+// the same chain with y already split (an operand reused across chunks: split once per kernel)
+template <int XS, int T>
+struct F32Pre {
+  Split3 s[XS ? T / 8 : 1];
+  __device__ __forceinline__ void set(const float (&y)[T]) {
+    if constexpr (XS != 0) {
+#pragma unroll
+      for (int j = 0; j < T / 8; ++j) s[j] = split3_8(&y[8 * j]);
+    }
+  }
+};
+template <int XS, int T>
+__device__ __forceinline__ f32x16_t f32_chain_pre(const float (&x)[T], const float (&y)[T], const F32Pre<XS, T>& ys,
+                                                  f32x16_t acc) {
+  if constexpr (XS == 0) {
+    return f32_chain<0, T>(x, y, acc);
+  } else {
+#pragma unroll
+    for (int j = 0; j < T / 8; ++j) {
+      const Split3 a = split3_8(&x[8 * j]);
+      const Split3& b = ys.s[j];
+      acc = MF32X16(a.l, b.h, acc);
+      acc = MF32X16(a.m, b.m, acc);
+      acc = MF32X16(a.h, b.l, acc);
+      acc = MF32X16(a.m, b.h, acc);
+      acc = MF32X16(a.h, b.m, acc);
+      acc = MF32X16(a.h, b.h, acc);
+    }
+    return acc;
+  }
+}

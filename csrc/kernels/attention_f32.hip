@@ -109,6 +109,8 @@ __global__ __launch_bounds__(256, 2) void attn_f32_fwd_kernel(AttnF32Args a) {
   fa_load_chunk(V, a.v_ss, 0, a.Sk, pv);
   float qf[32];
   fa_ownrow(Q, a.q_ss, qi, a.Sq, lane, qf);
+  F32Pre<XS, 32> qs;  // the owned Q row split once (reused by every chunk)
+  qs.set(qf);
   fa_store_chunk<FPR>(Ks[0], pk);
   fa_store_chunk<64>(Vs[0], pv);
   __syncthreads();
@@ -135,7 +137,7 @@ __global__ __launch_bounds__(256, 2) void attn_f32_fwd_kernel(AttnF32Args a) {
       {
         float kf[32];
         fa_rowfrag(Ks[buf], kb, lane, kf);
-        s = f32_chain<XS, 32>(kf, qf, s);
+        s = f32_chain_pre<XS, 32>(kf, qf, qs, s);
       }
       float cmax = -INFINITY;
       if (uni) {
@@ -217,6 +219,9 @@ __global__ __launch_bounds__(256, XS ? 1 : 2) void attn_f32_dq_kernel(AttnF32Arg
   float qf[32], df[32];
   fa_ownrow(Q, a.q_ss, qi, a.Sq, lane, qf);
   fa_ownrow(dO, a.o_ss, qi, a.Sq, lane, df);
+  F32Pre<XS, 32> qs, ds;  // owned Q / dO rows split once
+  qs.set(qf);
+  ds.set(df);
   float dl;
   {
     float of[32];
@@ -254,12 +259,12 @@ __global__ __launch_bounds__(256, XS ? 1 : 2) void attn_f32_dq_kernel(AttnF32Arg
       {
         float kf[32];
         fa_rowfrag(Ks[buf], kb, lane, kf);
-        s = f32_chain<XS, 32>(kf, qf, s);
+        s = f32_chain_pre<XS, 32>(kf, qf, qs, s);
       }
       {
         float vf[32];
         fa_rowfrag(Vs[buf], kb, lane, vf);
-        dp = f32_chain<XS, 32>(vf, df, dp);
+        dp = f32_chain_pre<XS, 32>(vf, df, ds, dp);
       }
       if (uni) {
         const float off = ub - lse;
@@ -325,6 +330,9 @@ __global__ __launch_bounds__(256, XS ? 1 : 2) void attn_f32_dkdv_kernel(AttnF32A
   float kf[32], vf[32];
   fa_ownrow(K, a.k_ss, kj, a.Sk, lane, kf);
   fa_ownrow(V, a.v_ss, kj, a.Sk, lane, vf);
+  F32Pre<XS, 32> ks, vs;  // owned K / V rows split once
+  ks.set(kf);
+  vs.set(vf);
   const bool kok = kj < a.Sk && !(KPAD && a.kpad[(long)b * a.Sk + kj]);
   const float kbias = kok ? 0.f : -INFINITY;
   f32x16_t dk[2], dv[2];
@@ -359,12 +367,12 @@ __global__ __launch_bounds__(256, XS ? 1 : 2) void attn_f32_dkdv_kernel(AttnF32A
       {
         float qr[32];
         fa_rowfrag(Qs[buf], qb, lane, qr);
-        s = f32_chain<XS, 32>(qr, kf, s);
+        s = f32_chain_pre<XS, 32>(qr, kf, ks, s);
       }
       {
         float dr[32];
         fa_rowfrag(Ds[buf], qb, lane, dr);
-        dp = f32_chain<XS, 32>(dr, vf, dp);
+        dp = f32_chain_pre<XS, 32>(dr, vf, vs, dp);
       }
       // s[r]: query q0 + qb + fa_kl(r, h), key kj.  Rows past Sq carry lse = +inf (p = 0).
 #pragma unroll

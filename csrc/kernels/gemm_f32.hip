@@ -572,26 +572,30 @@ __device__ __forceinline__ int xs_off(int row, int k) {  // bf16 offset of (row,
   return row * 32 + ((((k >> 3) ^ (row >> 2)) & 3) << 3) + (k & 7);
 }
 
+// k-major operand image: [32 k][128 rows] bf16 per plane (256-B k-rows), 16-B chunk ch of k-row r
+// stored at chunk ch ^ (((r & 3) << 2) | ((r >> 2) & 3)) — conflict-free for both the staging
+// writes and ds_read_b64_tr_b16 (cdna_hip_programming.md T10 image (b))
+__device__ __forceinline__ int xs_koff(int k, int col) {  // col % 4 == 0
+  return k * 128 + ((((col >> 3) ^ (((k & 3) << 2) | ((k >> 2) & 3))) & 15) << 3) + (col & 7);
+}
+
+// staging map: k-contiguous operand: thread f = tid + 256 i holds row f >> 3, k (f & 7) * 4 .. + 3
+// (one float4); k-major: k-row (f >> 5), rows (f & 31) * 4 .. + 3 (one float4 of the natural layout)
 template <bool KMAJ>
 __device__ __forceinline__ void xs_bload(__amdgpu_buffer_rsrc_t rs, long ld, int r0, int rlim, int k0, int klim,
                                          float4 (&v)[4], int tid) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
+    const int f = tid + 256 * i;
+    int off;
     if (!KMAJ) {
-      const int f = tid + 256 * i, gr = r0 + (f >> 3), gk = k0 + (f & 7) * 4;
-      const int off = (gr < rlim && gk < klim) ? (int)(((long)gr * ld + gk) * 4) : F32_OOB;
-      v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      const int gr = r0 + (f >> 3), gk = k0 + (f & 7) * 4;
+      off = (gr < rlim && gk < klim) ? (int)(((long)gr * ld + gk) * 4) : F32_OOB;
     } else {
-      // row = tid & 127, k = 4 * ((tid >> 7) + 2 i) + e
-      const int gr = r0 + (tid & 127), gk = k0 + 4 * ((tid >> 7) + 2 * i);
-      float e4[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int off = (gr < rlim && gk + e < klim) ? (int)(((long)(gk + e) * ld + gr) * 4) : F32_OOB;
-        e4[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
-      }
-      v[i] = make_float4(e4[0], e4[1], e4[2], e4[3]);
+      const int gk = k0 + (f >> 5), gc = r0 + (f & 31) * 4;
+      off = (gk < klim && gc < rlim) ? (int)(((long)gk * ld + gc) * 4) : F32_OOB;
     }
+    v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
   }
 }
 
@@ -600,27 +604,45 @@ template <bool KMAJ>
 __device__ __forceinline__ void xs_lstore(unsigned short* __restrict__ dst, const float4 (&v)[4], int tid) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    int row, k;
-    if (!KMAJ) { const int f = tid + 256 * i; row = f >> 3; k = (f & 7) * 4; }
-    else { row = tid & 127; k = 4 * ((tid >> 7) + 2 * i); }
+    const int f = tid + 256 * i;
+    const int o = KMAJ ? xs_koff(f >> 5, (f & 31) * 4) : xs_off(f >> 3, (f & 7) * 4);
     uint32_t h0, m0, l0, h1, m1, l1;
     split3_pair(v[i].x, v[i].y, h0, m0, l0);
     split3_pair(v[i].z, v[i].w, h1, m1, l1);
-    const int o = xs_off(row, k);
     *(uint2*)(dst + o) = make_uint2(h0, h1);
     *(uint2*)(dst + XS_PLANE + o) = make_uint2(m0, m1);
     *(uint2*)(dst + 2 * XS_PLANE + o) = make_uint2(l0, l1);
   }
 }
 
-// the three bf16x8 planes of a 32-row fragment (rows c0 + (lane & 31)) for k-block b
+// the three bf16x8 planes of a 32-row fragment (rows c0 + (lane & 31), k = 16 b + 8 h + e)
+typedef __attribute__((ext_vector_type(4))) short xs_s16x4_t;
+template <bool KMAJ>
 __device__ __forceinline__ Split3 xs_frag(const unsigned short* __restrict__ op, int c0, int b, int lane) {
-  const int row = c0 + (lane & 31), k = 16 * b + 8 * (lane >> 5);
-  const int o = xs_off(row, k);
   Split3 r;
-  r.h = *(const bf16x8_t*)(op + o);
-  r.m = *(const bf16x8_t*)(op + XS_PLANE + o);
-  r.l = *(const bf16x8_t*)(op + 2 * XS_PLANE + o);
+  if (!KMAJ) {
+    const int row = c0 + (lane & 31), k = 16 * b + 8 * (lane >> 5);
+    const int o = xs_off(row, k);
+    r.h = *(const bf16x8_t*)(op + o);
+    r.m = *(const bf16x8_t*)(op + XS_PLANE + o);
+    r.l = *(const bf16x8_t*)(op + 2 * XS_PLANE + o);
+  } else {
+    // ds_read_b64_tr_b16 per 16-lane group g: lane 4q + p addresses k-row q of the 4 x 16 block
+    // (columns 4p .. 4p + 3); lane i receives column i.  Group g: rows c0 + 16 (g & 1) + i,
+    // k-half h = g >> 1; two reads give k = 16 b + 8 h + 0..3 and + 4..7.
+    const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4;
+    const int col = c0 + 16 * (g & 1) + 4 * p;
+    const int kb = 16 * b + 8 * (g >> 1) + q;
+    const int o0 = xs_koff(kb, col), o1 = xs_koff(kb + 4, col);
+    bf16x8_t* outs[3] = {&r.h, &r.m, &r.l};
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+      const unsigned short* base = op + pl * XS_PLANE;
+      const xs_s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) xs_s16x4_t*)(base + o0));
+      const xs_s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) xs_s16x4_t*)(base + o1));
+      *outs[pl] = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+  }
   return r;
 }
 
@@ -644,7 +666,7 @@ __device__ __forceinline__ void gemm_xs_tile(const GemmF32Args& g, int tile, int
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = cacc[i][j][r] = 0.f;
   const bool do_bias = AK && g.bias_grad && n0 == 0;
-  float bsum = 0.f;  // AK: partial row sum of A for row tid & 127 (k-major staging map)
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};  // AK: partial row sums of A rows (tid & 31) * 4 + j
   const long a_bytes = 4 * (AK ? (long)(g.K - 1) * g.lda + g.M : (long)(g.M - 1) * g.lda + g.K);
   const long b_bytes = 4 * (BKM ? (long)(g.K - 1) * g.ldb + g.N : (long)(g.N - 1) * g.ldb + g.K);
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, 0, (int)a_bytes, 0x00020000);
@@ -660,15 +682,15 @@ __device__ __forceinline__ void gemm_xs_tile(const GemmF32Args& g, int tile, int
     xs_lstore<BKM>(d + XS_OPER, rb, tid);
     if constexpr (AK) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) bsum += (ra[i].x + ra[i].y) + (ra[i].z + ra[i].w);
+      for (int i = 0; i < 4; ++i) { bsum[0] += ra[i].x; bsum[1] += ra[i].y; bsum[2] += ra[i].z; bsum[3] += ra[i].w; }
     }
   };
   auto rd = [&](int t, int b, Split3 (&fa)[FM], Split3 (&fb)[2]) {
     const unsigned short* d = lds + (t % 3) * XS_STAGE;
 #pragma unroll
-    for (int i = 0; i < FM; ++i) fa[i] = xs_frag(d, wm * 64 + i * 32, b, lane);
+    for (int i = 0; i < FM; ++i) fa[i] = xs_frag<AK>(d, wm * 64 + i * 32, b, lane);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) fb[j] = xs_frag(d + XS_OPER, wn * 64 + j * 32, b, lane);
+    for (int j = 0; j < 2; ++j) fb[j] = xs_frag<BKM>(d + XS_OPER, wn * 64 + j * 32, b, lane);
   };
   auto mma = [&](const Split3 (&sa)[FM], const Split3 (&sb)[2]) {
 #pragma unroll
@@ -737,11 +759,15 @@ __device__ __forceinline__ void gemm_xs_tile(const GemmF32Args& g, int tile, int
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] += cacc[i][j];
   float bias_tot = 0.f;
-  if (do_bias) {  // the two staging threads of a row (tid, tid + 128) combine through LDS
+  if (do_bias) {  // the 8 staging threads of a row group (tid & 31) combine through LDS in order
     __syncthreads();
-    if (tid >= 128) smem[tid - 128] = bsum;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) smem[(tid >> 5) * 128 + (tid & 31) * 4 + j] = bsum[j];
     __syncthreads();
-    if (tid < 128) bias_tot = bsum + smem[tid];
+    if (tid < 128) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) bias_tot += smem[q * 128 + tid];
+    }
   }
   float nob[2] = {0.f, 0.f};
   f32_epilogue_lds<AK, EPI>(g, acc, nob, m0, n0, wm, wn, lane, false, smem);
@@ -837,13 +863,13 @@ extern "C" int smi_gemm_f32(const GemmF32Args* args, hipStream_t st) {
       fe = (g.resid ? FE_RESID : 0) | (g.dact_y ? FE_DACT : 0);
     }
     fe |= (g.atomic ? FE_ATOMIC : (g.beta_acc ? FE_ACC : 0));
-// split path per operand layout (measured, tools/f32_split_check.py): FWD (both operands
-// k-contiguous) splits once at staging (XS 2); DGRAD / WGRAD (k-major operands, whose staging
-// would need dword gathers) split the fp32 fragments per wave (XS 1)
+// split path per mode (measured, tools/f32_split_check.py): FWD and DGRAD split once at staging
+// into LDS bf16 planes (XS 2; the k-major DGRAD weight through ds_read_b64_tr_b16), WGRAD splits
+// the fp32 fragments per wave (XS 1: 520 vs 563 us for a decoder layer's grouped launch)
 #define F32P(AKV, BKV, E)                                                                          \
   do {                                                                                             \
     if (smi_f32_algo() == 0) hipLaunchKernelGGL((gemm_f32_pipe_kernel<AKV, BKV, E, 0>), grid2, block, 0, st, g); \
-    else hipLaunchKernelGGL((gemm_f32_pipe_kernel<AKV, BKV, E, (BKV ? 1 : 2)>), grid2, block, 0, st, g); \
+    else hipLaunchKernelGGL((gemm_f32_pipe_kernel<AKV, BKV, E, (AKV ? 1 : 2)>), grid2, block, 0, st, g); \
   } while (0)
     if (g.mode == 0) {
       switch (fe) {

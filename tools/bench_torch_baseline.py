@@ -162,6 +162,8 @@ def main():
     ap.add_argument("--seq", type=int, default=256)
     ap.add_argument("--layers", type=int, default=6)
     ap.add_argument("--vocab", type=int, default=10000)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="bf16 autocast (fp32 master) or plain fp32 (the reference precision)")
     a = ap.parse_args()
     if a.model != "transformer":
         return small_model(a)
@@ -172,8 +174,11 @@ def main():
     src = torch.randint(1, a.vocab, (a.batch, a.seq), device=dev)
     tgt = torch.randint(1, a.vocab, (a.batch, a.seq), device=dev)
 
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+
     def step():
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=a.dtype == "bf16"):
             logits = m(src, tgt)
             loss = F.cross_entropy(logits.float().view(-1, a.vocab), tgt.view(-1), ignore_index=0)
         opt.zero_grad(set_to_none=True)
@@ -191,7 +196,8 @@ def main():
     dt = time.perf_counter() - t0
     print(json.dumps({"metric": "stock PyTorch eager transformer samples/s (1 GPU)", "value": round(a.batch * a.steps / dt, 2),
                       "ms_per_step": round(dt / a.steps * 1000, 3), "batch": a.batch, "seq": a.seq, "layers": a.layers,
-                      "dtype": "bf16 autocast, fp32 master", "final_loss": round(float(loss), 4),
+                      "dtype": "bf16 autocast, fp32 master" if a.dtype == "bf16" else "fp32",
+                      "final_loss": round(float(loss), 4),
                       "torch": torch.__version__}))
 
 
