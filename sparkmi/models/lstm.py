@@ -18,6 +18,7 @@ from torch import nn
 
 from ..ops import rng as _rng
 from ..ops.lstm import lstm_classifier
+from ..ops.loss import cross_entropy
 
 
 class LSTM(nn.Module):
@@ -54,7 +55,9 @@ class LSTM(nn.Module):
         """CE on the last step's prediction (distributed_lstm.py:186-189); returns (loss, pred)."""
         pred, _, _ = self(input_seq, hidden_in, mem_in)
         last = pred[:, -1, :]
-        return nn.functional.cross_entropy(last, labels), last
+        # sparkmi's CE kernel (csrc/kernels/cross_entropy.hip: fixed-order loss sum) instead of the
+        # ATen softmax / nll_loss launches; the CPU path falls back to the same math in torch
+        return cross_entropy(last.contiguous(), labels), last
 
 
 TextClassifierLSTM = LSTM
