@@ -7,10 +7,14 @@ lr 1e-3, dropout 0.1, reference mask semantics — a full training step (forward
 CE, backward, gradient all-reduce, optimizer) per iteration, synthetic Multi30k-shaped data
 resident in HBM, random-init weights.  ``value`` is measured at the REFERENCE precision: fp32
 activations, fp32 weights, fp32 accumulation, exactly as the reference trains
-(pytorch_machine_translator.py:120-137, default fp32 modules).  GEMM products are exact: each fp32
-operand is split into three bf16 slices and the six significant slice products run on the bf16
-matrix cores (csrc/kernels/gemm_f32.hip:split3_8; measured error against fp64 is 3x BELOW the
-v_mfma_f32_32x32x2_f32 kernel, which is reported beside it as ``transformer_fp32_f32mfma``).  The bf16
+(pytorch_machine_translator.py:120-137, default fp32 modules).  GEMM products are exact: every fp32
+operand is carried as three bf16 planes (hi + mid + lo, split once where it is produced) and the
+six significant plane products run on the bf16 matrix cores (csrc/kernels/gemm_sp*.hip; measured
+error against fp64 at or below the v_mfma_f32_32x32x2_f32 kernel, tests/test_gemm_sp_gpu.py; the
+same step on that f32-MFMA kernel is reported beside it as ``transformer_fp32_f32mfma``).  Every
+model is built after resetting the dropout salt sequence and the torch seed, so its trajectory
+does not depend on which models ran before it in the process; the headline run's per-step losses
+are in ``losses``.  The bf16
 (fp32-master) variant of the same step and the distributed_cnn workload (the other half of the
 BASELINE metric) are reported beside it for the same N, plus the LSTM / MLP workloads.
 
@@ -39,8 +43,10 @@ BASELINE_LSTM = 1365.0    # 1 proc x 8 threads
 BASELINE_MLP = 130476.0   # world 1, 1 thread
 METRIC = "samples/sec (whole node) distributed_cnn + transformer at 1/2/4/8 MI355X"
 F32_PRECISION = ("fp32 activations/weights/gradients/accumulators (reference precision); GEMM products exact: "
-                 "fp32 operands split into 3 bf16 slices on v_mfma_f32_32x32x16_bf16 (6 terms, error vs fp64 "
-                 "below the f32-MFMA kernel: tests/test_gemm_f32_split_gpu.py); fp32 attention on f32 MFMA")
+                 "fp32 operands carried as 3 bf16 planes (hi+mid+lo, split once where produced), 6 plane products "
+                 "on v_mfma_f32_32x32x16_bf16 (error vs fp64 at or below the f32-MFMA kernel: "
+                 "tests/test_gemm_sp_gpu.py); fp32 attention products on the same exact 3-way bf16 split")
+SPLIT_PEAK_TF = 2500.0 / 6  # 6 bf16 products per fp32 product on the 2.5 PF bf16 matrix cores
 
 
 def parse(argv=None):
@@ -123,7 +129,17 @@ def _sync(device):
         torch.cuda.synchronize()
 
 
-def time_steps(runner, batches, steps, warmup, device, world):
+def fresh_model_state(seed):
+    """Reset the process-global dropout salt sequence and the torch seed before building a model:
+    its masks and init then do not depend on the models built before it in this process."""
+    import torch
+    from sparkmi.ops.rng import reset_salts
+    reset_salts()
+    torch.manual_seed(seed)
+
+
+def time_steps(runner, batches, steps, warmup, device, world, record=None):
+    """``record``: a list that receives each timed step's loss (a device copy, read after timing)."""
     import torch
     from sparkmi.parallel import barrier
     # the HIP-graph capture must happen inside the untimed warm-up: eager steps first, the
@@ -139,6 +155,8 @@ def time_steps(runner, batches, steps, warmup, device, world):
     t0 = time.perf_counter()
     for i in range(steps):
         loss = runner.step(*batches[i % n])
+        if record is not None:
+            record.append(loss.detach().clone())
     _sync(device)
     barrier()
     _sync(device)
@@ -183,7 +201,7 @@ def bench_cnn(args, rank, world, device, dtype="fp32"):
     from sparkmi.parallel.ddp import DataParallel
     from sparkmi.train.runner import StepRunner
     from sparkmi.utils.flat import FlatParams
-    torch.manual_seed(4321)
+    fresh_model_state(4321)
     model = FashionMNISTModel(1, 10, 10, dtype=dtype).to(device).train()
     flat = FlatParams(model)
     opt = SGD(flat, lr=0.01)
@@ -217,7 +235,7 @@ def bench_lstm(args, rank, world, device):
     from sparkmi.train.runner import StepRunner
     from sparkmi.utils.flat import FlatParams
     V, B, T = 95812, 32, 129
-    torch.manual_seed(11)
+    fresh_model_state(11)
     model = LSTM(V, 32, 32, 4, num_layers=2, padding_idx=7).to(device).train()
     flat = FlatParams(model, shadow=False)
     opt = Adam(flat, lr=1e-3)
@@ -244,7 +262,7 @@ def bench_mlp(args, rank, world, device):
     from sparkmi.parallel.ddp import DataParallel
     from sparkmi.train.runner import StepRunner
     from sparkmi.utils.flat import FlatParams
-    torch.manual_seed(5)
+    fresh_model_state(5)
     model = MultilayerPerceptron((4, 5, 4, 3)).to(device).train()
     flat = FlatParams(model, shadow=False)
     opt = SGD(flat, lr=0.01)
@@ -275,7 +293,7 @@ def bench_transformer(args, rank, world, device, dtype):
     from sparkmi.parallel.ddp import DataParallel
     from sparkmi.train.runner import StepRunner
     from sparkmi.utils.flat import FlatParams
-    torch.manual_seed(1234)
+    fresh_model_state(1234)
     model = Transformer(d_model=512, ffn_hidden=1024, num_heads=8, drop_prob=0.1, num_layers=args.layers,
                         max_sequence_length=args.seq, src_vocab_size=args.vocab, tgt_vocab_size=args.vocab,
                         mask_mode="reference", seed=1234 + rank, dtype=dtype).to(device)
@@ -294,7 +312,8 @@ def bench_transformer(args, rank, world, device, dtype):
     src = src.view(pool, args.batch, args.seq)
     tgt = tgt.view(pool, args.batch, args.seq)
     batches = [(src[i], tgt[i]) for i in range(pool)]
-    elapsed, loss = time_steps(runner, batches, args.steps, args.warmup, device, world)
+    losses = []
+    elapsed, loss = time_steps(runner, batches, args.steps, args.warmup, device, world, record=losses)
     final_loss = float(loss.float().item()) if loss is not None else float("nan")
     ar = time_allreduce(flat, device, world)
     if ddp is not None:
@@ -303,11 +322,15 @@ def bench_transformer(args, rank, world, device, dtype):
     tflops = transformer_flops_per_sample(args.layers, args.seq, args.vocab) * value / world / 1e12
     peak = 157.3 if dtype == "fp32" else 2500.0
     res = {"samples_per_s": round(value, 2), "ms_per_step": round(elapsed / args.steps * 1000, 3),
-           "final_loss": round(final_loss, 4), "model_tflops_per_gpu": round(tflops, 1),
+           "final_loss": round(final_loss, 4), "losses": [round(float(l), 4) for l in losses],
+           "model_tflops_per_gpu": round(tflops, 1),
            f"mfu_vs_{'157tf_fp32' if dtype == 'fp32' else '2.5pf_bf16'}_dense": round(tflops / peak, 3),
            "allreduce_ms": ar, "grad_bytes": flat.numel * 4, "dtype": dtype,
            "overlap": "finished buckets all-reduced under the rest of the backward" if split_fn else None,
            "hip_graph": use_graph}
+    if dtype == "fp32":
+        # the algorithm the step actually runs: 6 bf16 products per fp32 product
+        res["mfu_vs_417tf_split3_ceiling"] = round(tflops / SPLIT_PEAK_TF, 3)
     del runner, opt, flat, model, ddp, batches, src, tgt
     if device.type == "cuda":
         torch.cuda.empty_cache()
@@ -362,11 +385,16 @@ def main():
         # the same fp32 step with every GEMM product on v_mfma_f32_32x32x2_f32 instead of the
         # exact-product bf16 split (both fp32 in / out / accumulate), for comparison
         from sparkmi import _native
+        from sparkmi.ops import gemm as G
         C = _native.C()
-        prev = C.gemm_f32_algo(-1)
+        prev, prev_sp = C.gemm_f32_algo(-1), G.SP
         C.gemm_f32_algo(0)
-        f32mfma = bench_transformer(args, rank, world, device, "fp32")
-        C.gemm_f32_algo(prev)
+        G.SP = False
+        try:
+            f32mfma = bench_transformer(args, rank, world, device, "fp32")
+        finally:
+            C.gemm_f32_algo(prev)
+            G.SP = prev_sp
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -393,6 +421,7 @@ def main():
                 "baseline_ref": "BASELINE.md §2 transformer L6/S256 CPU proxy 4.79 samples/s",
             },
             "allreduce_ms": head["allreduce_ms"],
+            "losses": head.get("losses"),
         }
         for dt in dtypes:
             out[f"transformer_{dt}"] = tr[dt]

@@ -18,6 +18,7 @@ using u = uintptr_t;
 #include "smi_mlp.h"
 #include "smi_gemm.h"
 #include "smi_gemm_f32.h"
+#include "smi_gemm_sp.h"
 #include "smi_cnn.h"
 #include "smi_lstm.h"
 #include <pybind11/stl.h>
@@ -71,6 +72,12 @@ int smi_gemm_f32(const GemmF32Args*, hipStream_t);
 int smi_gemm_f32_algo(int);
 int smi_gemm_f32_wgrad_group(const void* const*, const long*, const void* const*, const long*, void* const*, void* const*,
                              const int*, const int*, const int*, int, hipStream_t);
+int smi_gemm_sp(const GemmSpArgs*, hipStream_t);
+int smi_gemm_sp_wgrad_group(const void* const*, const long*, const long*, const void* const*, const long*, const long*,
+                            void* const*, void* const*, const int*, const int*, const int*, int, hipStream_t);
+int smi_split3(const float*, long, int, long, void*, long, long, hipStream_t);
+int smi_gemm_sp_waves(int);
+int smi_gemm_sp_tm(int);
 int smi_splitk_reduce(const float*, int, long, float*, long, float*, int, hipStream_t);
 int smi_splitk_fold_multi(const float* const*, float* const*, float* const*, const long*, const int*, const int*, int,
                           hipStream_t);
@@ -85,11 +92,11 @@ int smi_lstm(const LSTMArgs*, int, hipStream_t);
 int smi_lstm_supported(int, int, int, int);
 long smi_lstm_slab_floats(int, int, int, int, int);
 int smi_adam(float*, float*, float*, float*, void*, long, const float*, float*, unsigned*, float, float, float, float, float,
-             int, int, hipStream_t);
+             int, int, void*, long, hipStream_t);
 int smi_sgd(float*, float*, float*, void*, long, const float*, float*, unsigned*, float, float, float, int, float, int,
-            hipStream_t);
+            void*, long, hipStream_t);
 int smi_adam_multi(float* const*, float* const*, float* const*, float* const*, void* const*, const long*, int, const float*,
-                   float*, unsigned*, float, float, float, float, float, int, int, hipStream_t);
+                   float*, unsigned*, float, float, float, float, float, int, int, void* const*, long, hipStream_t);
 int smi_multi_copy(void* const*, const void* const*, const long*, int, hipStream_t);
 }
 
@@ -252,30 +259,36 @@ PYBIND11_MODULE(_C, m) {
                          eps, S(stream)), "lbfgs_update");
   });
   m.def("seed_inc", [](u seed, u st) { chk(smi_seed_inc(reinterpret_cast<int*>(seed), S(st)), "seed_inc"); });
-  // step: device step counter (advanced by the kernel); done: zeroed uint32 ticket word
+  // step: device step counter (advanced by the kernel); done: zeroed uint32 ticket word;
+  // pl / ps: optional split planes of the updated weights (plane stride ps elements)
   m.def("adam", [](u p, u g, u mm, u v, u pbf, long n, u lr, u step, u done, float b1, float b2, float eps, float wd,
-                   float gscale, int adamw, int zero_grad, u st) {
+                   float gscale, int adamw, int zero_grad, u pl, long ps, u st) {
     chk(smi_adam(PF(p), PF(g), PF(mm), PF(v), P(pbf), n, PF(lr), PF(step), reinterpret_cast<unsigned*>(done), b1, b2,
-                 eps, wd, gscale, adamw, zero_grad, S(st)), "adam");
+                 eps, wd, gscale, adamw, zero_grad, P(pl), ps, S(st)), "adam");
   });
   // Adam over several disjoint ranges, one launch, one step advance (ZeRO-1 shard update)
   m.def("adam_multi", [](std::vector<u> p, std::vector<u> g, std::vector<u> mm, std::vector<u> v, std::vector<u> pbf,
                          std::vector<long> n, u lr, u step, u done, float b1, float b2, float eps, float wd, float gscale,
-                         int adamw, int zero_grad, u st) {
+                         int adamw, int zero_grad, std::vector<u> pl, long ps, u st) {
     const size_t c = p.size();
-    if (g.size() != c || mm.size() != c || v.size() != c || pbf.size() != c || n.size() != c)
+    if (g.size() != c || mm.size() != c || v.size() != c || pbf.size() != c || n.size() != c ||
+        (!pl.empty() && pl.size() != c))
       throw std::runtime_error("adam_multi: list sizes differ");
     std::vector<float*> a(c), b(c), d(c), e(c);
-    std::vector<void*> f(c);
-    for (size_t i = 0; i < c; ++i) { a[i] = PF(p[i]); b[i] = PF(g[i]); d[i] = PF(mm[i]); e[i] = PF(v[i]); f[i] = P(pbf[i]); }
+    std::vector<void*> f(c), q(c);
+    for (size_t i = 0; i < c; ++i) {
+      a[i] = PF(p[i]); b[i] = PF(g[i]); d[i] = PF(mm[i]); e[i] = PF(v[i]); f[i] = P(pbf[i]);
+      q[i] = pl.empty() ? nullptr : P(pl[i]);
+    }
     chk(smi_adam_multi(a.data(), b.data(), d.data(), e.data(), f.data(), n.data(), (int)c, PF(lr), PF(step),
-                       reinterpret_cast<unsigned*>(done), b1, b2, eps, wd, gscale, adamw, zero_grad, S(st)),
+                       reinterpret_cast<unsigned*>(done), b1, b2, eps, wd, gscale, adamw, zero_grad,
+                       pl.empty() ? nullptr : q.data(), ps, S(st)),
         "adam_multi");
   });
   m.def("sgd", [](u p, u g, u buf, u pbf, long n, u lr, u step, u done, float mom, float damp, float wd, int nesterov,
-                  float gscale, int zero_grad, u st) {
+                  float gscale, int zero_grad, u pl, long ps, u st) {
     chk(smi_sgd(PF(p), PF(g), PF(buf), P(pbf), n, PF(lr), PF(step), reinterpret_cast<unsigned*>(done), mom, damp, wd,
-                nesterov, gscale, zero_grad, S(st)), "sgd");
+                nesterov, gscale, zero_grad, P(pl), ps, S(st)), "sgd");
   });
   m.def("multi_copy", [](std::vector<u> dst, std::vector<u> src, std::vector<long> bytes, u st) {
     if (dst.size() != src.size() || dst.size() != bytes.size()) throw std::runtime_error("multi_copy: list sizes differ");
@@ -384,6 +397,44 @@ PYBIND11_MODULE(_C, m) {
     g.thresh = thresh; g.dscale = dscale; g.splits = splits; g.bias_grad = (float*)bias_grad;
     chk(smi_gemm_f32(&g, S(st)), "gemm_f32");
   });
+  // split-plane fp32 GEMM (csrc/kernels/gemm_sp*.hip): operands as bf16 planes [3][rows][ld]
+  // (plane stride aps / bps), optional plane output P of the epilogue result
+  m.def("gemm_sp", [](int mode, u A, long lda, long aps, u B, long ldb, long bps, int M, int N, int K, int kpad, u C,
+                      long ldc, u Pp, long ldp, long pps, int beta_acc, u bias, int relu, u resid, long ldr, u dact_y,
+                      long ldy, u seedp, uint32_t salt, uint32_t thresh, float dscale, u bias_grad, u st) {
+    GemmSpArgs g{};
+    g.mode = mode; g.A = (const unsigned short*)A; g.lda = lda; g.aps = aps;
+    g.B = (const unsigned short*)B; g.ldb = ldb; g.bps = bps; g.M = M; g.N = N; g.K = K; g.kpad = kpad;
+    g.C = (float*)C; g.ldc = ldc; g.P = (unsigned short*)Pp; g.ldp = ldp; g.pps = pps; g.beta_acc = beta_acc;
+    g.bias = (const float*)bias; g.relu = relu; g.resid = (const float*)resid; g.ldr = ldr;
+    g.dact_y = (const float*)dact_y; g.ldy = ldy; g.seedp = (const uint32_t*)seedp; g.salt = salt;
+    g.thresh = thresh; g.dscale = dscale; g.bias_grad = (float*)bias_grad;
+    const int rc = smi_gemm_sp(&g, S(st));  // < 0: shape / feature set not covered (caller falls back)
+    if (rc > 0) chk(rc, "gemm_sp");
+    return rc == 0;
+  });
+  m.def("gemm_sp_wgrad_group", [](std::vector<u> A, std::vector<long> lda, std::vector<long> aps, std::vector<u> B,
+                                  std::vector<long> ldb, std::vector<long> bps, std::vector<u> C, std::vector<u> bias,
+                                  std::vector<int> n, std::vector<int> k, std::vector<int> T, u st) {
+    const size_t c = A.size();
+    if (lda.size() != c || aps.size() != c || B.size() != c || ldb.size() != c || bps.size() != c || C.size() != c ||
+        bias.size() != c || n.size() != c || k.size() != c || T.size() != c)
+      throw std::runtime_error("gemm_sp_wgrad_group: list sizes differ");
+    std::vector<const void*> a(c), b(c);
+    std::vector<void*> o(c), bo(c);
+    for (size_t i = 0; i < c; ++i) { a[i] = (const void*)A[i]; b[i] = (const void*)B[i]; o[i] = (void*)C[i]; bo[i] = (void*)bias[i]; }
+    chk(smi_gemm_sp_wgrad_group(a.data(), lda.data(), aps.data(), b.data(), ldb.data(), bps.data(), o.data(), bo.data(),
+                                n.data(), k.data(), T.data(), (int)c, S(st)),
+        "gemm_sp_wgrad_group");
+  });
+  // x[rows][cols] fp32 -> bf16 planes P[3][rows][ldp] (x = hi + mid + lo exactly; pad columns zeroed)
+  m.def("split3", [](u x, long rows, int cols, long ldx, u Pp, long ldp, long ps, u st) {
+    chk(smi_split3(PF(x), rows, cols, ldx, P(Pp), ldp, ps, S(st)), "split3");
+  });
+  m.def("gemm_sp_waves", [](int set) { return smi_gemm_sp_waves(set); },
+        "split-plane GEMM waves per 128x128 tile (4 | 8); other values query");
+  m.def("gemm_sp_tm", [](int set) { return smi_gemm_sp_tm(set); },
+        "split-plane GEMM tile height for large problems (128 | 256); other values query");
   m.def("gemm_f32_algo", [](int set) { return smi_gemm_f32_algo(set); },
         "fp32 GEMM product algorithm: 0 = f32 MFMA, 6 = 3-way bf16 split (6 terms); set < 0 queries");
   m.def("gemm_f32_wgrad_group", [](std::vector<u> A, std::vector<long> lda, std::vector<u> B, std::vector<long> ldb,

@@ -22,19 +22,7 @@
 namespace py = pybind11;
 using u = uintptr_t;
 
-#define IPC_MAX_RANKS 8
-#define IPC_MAX_BLOCKS 128
-struct IpcArgs {
-  float* buf;
-  long n;
-  float* data[IPC_MAX_RANKS];
-  unsigned* sig[IPC_MAX_RANKS];
-  long cap;
-  int rank, world;
-  unsigned* ep;
-  unsigned* done;
-  int* err;
-};
+#include "smi_ipc.h"
 extern "C" int smi_ipc_allreduce(const IpcArgs* args, int blocks, hipStream_t st);
 
 static void hchk(hipError_t e, const char* what) {
@@ -163,14 +151,16 @@ PYBIND11_MODULE(_comm, m) {
   m.def("ipc_close", [](u p) { hchk(hipIpcCloseMemHandle((void*)p), "hipIpcCloseMemHandle"); });
   m.def("ipc_free", [](u p) { hchk(hipFree((void*)p), "hipFree"); });
   // ctr: device uint32[2] = {epoch, ticket}, zero-initialised
+  // spins: poll bound before a peer counts as lost (the bucket is then NaN-poisoned, *err set)
   m.def("ipc_allreduce", [](u buf, long n, std::vector<u> data, std::vector<u> sig, long cap, int rank, u ctr,
-                            u err, int blocks, u st) {
+                            u err, int blocks, u st, long spins) {
     if (data.size() != sig.size() || data.empty() || data.size() > IPC_MAX_RANKS)
       throw std::runtime_error("sparkmi._comm.ipc_allreduce: bad peer lists");
     IpcArgs a{};
     a.buf = (float*)buf; a.n = n; a.cap = cap; a.rank = rank; a.world = (int)data.size();
     a.ep = (unsigned*)ctr; a.done = (unsigned*)ctr + 1;
     a.err = (int*)err;
+    a.spins = spins > 0 ? spins : IPC_DEFAULT_SPINS;
     for (size_t i = 0; i < data.size(); ++i) { a.data[i] = (float*)data[i]; a.sig[i] = (unsigned*)sig[i]; }
     const int rc = smi_ipc_allreduce(&a, blocks, (hipStream_t)st);
     if (rc != 0) throw std::runtime_error("sparkmi._comm.ipc_allreduce failed: " +
@@ -178,4 +168,5 @@ PYBIND11_MODULE(_comm, m) {
   });
   m.attr("IPC_MAX_RANKS") = IPC_MAX_RANKS;
   m.attr("IPC_MAX_BLOCKS") = IPC_MAX_BLOCKS;
+  m.attr("IPC_DEFAULT_SPINS") = IPC_DEFAULT_SPINS;
 }

@@ -15,29 +15,19 @@
 //  2. every storing wave drains its stores (vmcnt(0)), the block barriers, and thread r stores
 //     `epoch` into rank r's signal slot [b][my rank] with a system-scope release;
 //  3. thread r polls this rank's signal slot [b][r] (system-scope acquire loads, s_sleep
-//     back-off, BOUNDED: after ~4 s it records a timeout in *err and gives up, so a dead peer
-//     can never hang the GPU);
+//     back-off, BOUNDED: after `spins` polls (~4 s by default) it records a timeout in *err and
+//     gives up, so a dead peer can never hang the GPU);
 //  4. block b sums chunk b of all ranks' staging regions in rank order 0..world-1 — every rank
-//     computes bit-identical results — and writes it back to the local bucket.
+//     computes bit-identical results — and writes it back to the local bucket.  If any peer
+//     timed out, the block writes NaN instead: a lost peer never turns into a finite, silently
+//     wrong gradient; *err stays set (sticky) for the host-side health check
+//     (sparkmi/parallel/ddp.py DataParallel.check) that fails the group.
 // Staging and signal regions are allocated uncached (hipDeviceMallocUncached), so peer reads
 // over xGMI and polls never see stale cache lines.  Only vector memory instructions are used.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define IPC_MAX_RANKS 8
-#define IPC_MAX_BLOCKS 128
-
-struct IpcArgs {
-  float* buf;                          // local bucket (in / out), 16-B aligned, n % 4 == 0
-  long n;                              // floats
-  float* data[IPC_MAX_RANKS];          // every rank's staging region: [2][cap] floats
-  unsigned* sig[IPC_MAX_RANKS];        // every rank's signal region: [IPC_MAX_BLOCKS][IPC_MAX_RANKS]
-  long cap;                            // floats per staging half
-  int rank, world;
-  unsigned* ep;                        // device epoch counter (read at entry, advanced at exit)
-  unsigned* done;                      // zeroed ticket word of the exit advance
-  int* err;                            // set to 1 on a poll timeout
-};
+#include "smi_ipc.h"
 
 __global__ __launch_bounds__(256) void ipc_allreduce_kernel(IpcArgs a) {
   const int b = blockIdx.x, nb = gridDim.x;
@@ -50,6 +40,8 @@ __global__ __launch_bounds__(256) void ipc_allreduce_kernel(IpcArgs a) {
   const float4* src = (const float4*)a.buf;
   for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = src[i];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __shared__ int timed_out;
+  if (threadIdx.x == 0) timed_out = 0;
   __syncthreads();
   if ((int)threadIdx.x < a.world) {
     __atomic_thread_fence(__ATOMIC_RELEASE);  // system scope: the staging stores are visible first
@@ -58,8 +50,9 @@ __global__ __launch_bounds__(256) void ipc_allreduce_kernel(IpcArgs a) {
     const unsigned* f = a.sig[a.rank] + b * IPC_MAX_RANKS + threadIdx.x;
     long spins = 0;
     while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
-      if (++spins > (1L << 24)) {  // ~4 s of s_sleep back-off: a peer is gone
+      if (++spins > a.spins) {  // a peer is gone
         __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        atomicOr(&timed_out, 1);
         break;
       }
       __builtin_amdgcn_s_sleep(8);
@@ -68,6 +61,10 @@ __global__ __launch_bounds__(256) void ipc_allreduce_kernel(IpcArgs a) {
   }
   __syncthreads();
   float4* out = (float4*)a.buf;
+  if (timed_out) {  // poison: the bucket must not carry a finite partial sum
+    const float nan = __builtin_nanf("");
+    for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) out[i] = make_float4(nan, nan, nan, nan);
+  } else
   for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
     float4 acc = ((const float4*)(a.data[0] + half))[i];
     for (int r = 1; r < a.world; ++r) {
@@ -88,6 +85,7 @@ extern "C" int smi_ipc_allreduce(const IpcArgs* args, int blocks, hipStream_t st
   const IpcArgs& a = *args;
   if (a.world < 1 || a.world > IPC_MAX_RANKS || a.rank < 0 || a.rank >= a.world) return -1;
   if (a.n % 4 || a.n > a.cap || ((uintptr_t)a.buf & 15)) return -1;
+  if (args->spins < 1) return -1;
   if (blocks < 1) blocks = 1;
   if (blocks > IPC_MAX_BLOCKS) blocks = IPC_MAX_BLOCKS;
   hipLaunchKernelGGL(ipc_allreduce_kernel, dim3(blocks), dim3(256), 0, st, a);

@@ -12,6 +12,7 @@
 // block computes t = step[0] + 1 on entry, and the last block to finish (atomic ticket on the
 // `done` word) stores t and re-arms the ticket — all other blocks have read step[0] by then.
 #include "smi_common.h"
+#include "smi_split3.h"
 
 __global__ void step_inc_kernel(float* step) { step[0] += 1.f; }
 // dropout step seed (sparkmi/ops/rng.py DropoutRNG.advance): one lane, captured in step graphs
@@ -29,11 +30,31 @@ __device__ __forceinline__ void finish_step(float* step, unsigned* done, float t
   }
 }
 
+// Split planes of the updated weights (the operand format of the fp32 GEMM,
+// csrc/include/smi_gemm_sp.h): hi / mid / lo at pl, pl + ps, pl + 2 ps.
+__device__ __forceinline__ void store_planes4(unsigned short* __restrict__ pl, long ps, long i4, const float* pa) {
+  uint32_t h0, m0, l0, h1, m1, l1;
+  split3_pair(pa[0], pa[1], h0, m0, l0);
+  split3_pair(pa[2], pa[3], h1, m1, l1);
+  ((uint2*)pl)[i4] = make_uint2(h0, h1);
+  ((uint2*)(pl + ps))[i4] = make_uint2(m0, m1);
+  ((uint2*)(pl + 2 * ps))[i4] = make_uint2(l0, l1);
+}
+__device__ __forceinline__ void store_planes1(unsigned short* __restrict__ pl, long ps, long i, float x) {
+  const unsigned short hh = f2bf(x);
+  const float r = x - bf2f(hh);
+  const unsigned short mm = f2bf(r);
+  pl[i] = hh;
+  pl[ps + i] = mm;
+  pl[2 * ps + i] = f2bf(r - bf2f(mm));
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                                                    float* __restrict__ v, unsigned short* __restrict__ pbf, long n,
                                                    const float* __restrict__ lr_p, float* __restrict__ step_p,
                                                    unsigned* __restrict__ done, float b1, float b2, float eps, float wd,
-                                                   float gscale, int adamw, int zero_grad) {
+                                                   float gscale, int adamw, int zero_grad, unsigned short* __restrict__ pl,
+                                                   long ps) {
   const float t = step_p[0] + 1.f;
   const float lr = lr_p[0];
   const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
@@ -63,6 +84,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
       uint2 w; w.x = ob[0] | ((unsigned)ob[1] << 16); w.y = ob[2] | ((unsigned)ob[3] << 16);
       ((uint2*)pbf)[i] = w;
     }
+    if (pl) store_planes4(pl, ps, i, pa);
   }
   // tail
   if (blockIdx.x == 0) {
@@ -74,6 +96,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
       p[i] -= step_size * m[i] / (sqrtf(v[i]) * rbc2 + eps);
       if (zero_grad) g[i] = 0.f;
       if (pbf) pbf[i] = f2bf(p[i]);
+      if (pl) store_planes1(pl, ps, i, p[i]);
     }
   }
   finish_step(step_p, done, t);
@@ -86,7 +109,8 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
 #define ADAM_MULTI_MAX 64
 struct AdamMulti {
   float* p[ADAM_MULTI_MAX]; float* g[ADAM_MULTI_MAX]; float* m[ADAM_MULTI_MAX]; float* v[ADAM_MULTI_MAX];
-  unsigned short* pbf[ADAM_MULTI_MAX]; long n[ADAM_MULTI_MAX]; int blk0[ADAM_MULTI_MAX + 1]; int count;
+  unsigned short* pbf[ADAM_MULTI_MAX]; unsigned short* pl[ADAM_MULTI_MAX]; long n[ADAM_MULTI_MAX];
+  int blk0[ADAM_MULTI_MAX + 1]; int count; long ps;
 };
 __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a, const float* __restrict__ lr_p,
                                                          float* __restrict__ step_p, unsigned* __restrict__ done, float b1,
@@ -101,6 +125,7 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a, const floa
   while (e + 1 < a.count && (int)blockIdx.x >= a.blk0[e + 1]) ++e;  // wave-uniform scan
   const long lb = blockIdx.x - a.blk0[e], nb = a.blk0[e + 1] - a.blk0[e];
   float* p = a.p[e]; float* g = a.g[e]; float* m = a.m[e]; float* v = a.v[e]; unsigned short* pbf = a.pbf[e];
+  unsigned short* pl = a.pl[e];
   const long n4 = a.n[e] / 4;
   for (long i = lb * blockDim.x + threadIdx.x; i < n4; i += nb * blockDim.x) {
     float4 pp = ((float4*)p)[i], gg = ((float4*)g)[i], mm = ((float4*)m)[i], vv = ((float4*)v)[i];
@@ -125,6 +150,7 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a, const floa
       uint2 w; w.x = ob[0] | ((unsigned)ob[1] << 16); w.y = ob[2] | ((unsigned)ob[3] << 16);
       ((uint2*)pbf)[i] = w;
     }
+    if (pl) store_planes4(pl, a.ps, i, pa);
   }
   finish_step(step_p, done, t);
 }
@@ -133,7 +159,8 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a, const floa
 __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ buf,
                                                   unsigned short* __restrict__ pbf, long n, const float* __restrict__ lr_p,
                                                   float* __restrict__ step_p, unsigned* __restrict__ done, float momentum,
-                                                  float dampening, float wd, int nesterov, float gscale, int zero_grad) {
+                                                  float dampening, float wd, int nesterov, float gscale, int zero_grad,
+                                                  unsigned short* __restrict__ pl, long ps) {
   const float lr = lr_p[0];
   const float t = step_p[0] + 1.f;
   const bool first = t <= 1.f;
@@ -148,6 +175,7 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, float* 
     p[i] -= lr * d;
     if (zero_grad) g[i] = 0.f;
     if (pbf) pbf[i] = f2bf(p[i]);
+    if (pl) store_planes1(pl, ps, i, p[i]);
   }
   finish_step(step_p, done, t);
 }
@@ -171,15 +199,17 @@ extern "C" int smi_step_inc(float* step, hipStream_t st) {
 
 extern "C" int smi_adam(float* p, float* g, float* m, float* v, void* pbf, long n, const float* lr, float* step,
                         unsigned* done, float b1, float b2, float eps, float wd, float gscale, int adamw, int zero_grad,
-                        hipStream_t st) {
+                        void* pl, long ps, hipStream_t st) {
+  if (pl && (((uintptr_t)pl & 7) || ps % 4 || ps < n)) return -1;
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, st, p, g, m, v, (unsigned short*)pbf, n, lr,
-                     step, done, b1, b2, eps, wd, gscale, adamw, zero_grad);
+                     step, done, b1, b2, eps, wd, gscale, adamw, zero_grad, (unsigned short*)pl, ps);
   SMI_CHECK_LAUNCH();
 }
 
 extern "C" int smi_adam_multi(float* const* p, float* const* g, float* const* m, float* const* v, void* const* pbf,
                               const long* n, int count, const float* lr, float* step, unsigned* done, float b1, float b2,
-                              float eps, float wd, float gscale, int adamw, int zero_grad, hipStream_t st) {
+                              float eps, float wd, float gscale, int adamw, int zero_grad, void* const* pl, long ps,
+                              hipStream_t st) {
   if (count < 1 || count > ADAM_MULTI_MAX) return -1;
   AdamMulti a{};
   long total4 = 0;
@@ -190,6 +220,7 @@ extern "C" int smi_adam_multi(float* const* p, float* const* g, float* const* m,
   int tot = 0;
   for (int i = 0; i < count; ++i) {
     a.p[i] = p[i]; a.g[i] = g[i]; a.m[i] = m[i]; a.v[i] = v[i]; a.pbf[i] = (unsigned short*)pbf[i]; a.n[i] = n[i];
+    a.pl[i] = pl ? (unsigned short*)pl[i] : nullptr;
     // blocks proportional to the range's share of a <= 4096-block launch
     long b = total4 ? (long)((double)(n[i] / 4) / (double)total4 * 4096.0) : 1;
     if (b > (n[i] / 4 + 255) / 256) b = (n[i] / 4 + 255) / 256;
@@ -199,16 +230,18 @@ extern "C" int smi_adam_multi(float* const* p, float* const* g, float* const* m,
   }
   a.blk0[count] = tot;
   a.count = count;
+  a.ps = ps;
   hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)tot), dim3(256), 0, st, a, lr, step, done, b1, b2, eps, wd, gscale,
                      adamw, zero_grad);
   SMI_CHECK_LAUNCH();
 }
 
 extern "C" int smi_sgd(float* p, float* g, float* buf, void* pbf, long n, const float* lr, float* step, unsigned* done,
-                       float momentum, float dampening, float wd, int nesterov, float gscale, int zero_grad,
-                       hipStream_t st) {
+                       float momentum, float dampening, float wd, int nesterov, float gscale, int zero_grad, void* pl,
+                       long ps, hipStream_t st) {
+  if (pl && ps < n) return -1;
   hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, g, buf, (unsigned short*)pbf, n, lr, step,
-                     done, momentum, dampening, wd, nesterov, gscale, zero_grad);
+                     done, momentum, dampening, wd, nesterov, gscale, zero_grad, (unsigned short*)pl, ps);
   SMI_CHECK_LAUNCH();
 }
 

@@ -275,6 +275,31 @@ def defer_wgrad_group(dy, x, gw, gb, params, stream):
         flush_deferred()
 
 
+def _kind(e):
+    """Operand format of a queued wgrad: 'planes' (fp32 as [3, T, ld] bf16 split planes), 'bf16', 'f32'."""
+    return "planes" if e[0].dim() == 3 else ("bf16" if e[0].dtype == torch.bfloat16 else "f32")
+
+
+def _launch_group(C, batch, st):
+    kind = _kind(batch[0])
+    if kind == "planes":
+        C.gemm_sp_wgrad_group([b[0].data_ptr() for b in batch], [b[0].stride(1) for b in batch],
+                              [b[0].stride(0) for b in batch], [b[1].data_ptr() for b in batch],
+                              [b[1].stride(1) for b in batch], [b[1].stride(0) for b in batch],
+                              [b[2].data_ptr() for b in batch],
+                              [b[3].data_ptr() if b[3] is not None else 0 for b in batch],
+                              [b[2].shape[0] for b in batch], [b[2].shape[1] for b in batch],
+                              [b[0].shape[1] for b in batch], st)
+        return
+    fn = C.gemm_wgrad_group if kind == "bf16" else C.gemm_f32_wgrad_group
+    fn([b[0].data_ptr() for b in batch], [b[0].stride(0) for b in batch],
+       [b[1].data_ptr() for b in batch], [b[1].stride(0) for b in batch],
+       [b[2].data_ptr() for b in batch],
+       [b[3].data_ptr() if b[3] is not None else 0 for b in batch],
+       [b[2].shape[0] for b in batch], [b[2].shape[1] for b in batch],
+       [b[0].shape[0] for b in batch], st)
+
+
 def _flush_groups(C, gq):
     by_stream = {}
     for e in gq:
@@ -282,17 +307,12 @@ def _flush_groups(C, gq):
     for st, es in by_stream.items():
         batch, outs = [], set()
         for e in es + [None]:
-            # one batch's tiles run concurrently and add without atomics: outputs must be distinct
+            # one batch's tiles run concurrently and add without atomics: outputs must be distinct;
+            # a batch holds one operand format
             if e is None or len(batch) == GROUP_MAX or e[2].data_ptr() in outs or (
-                    e[3] is not None and e[3].data_ptr() in outs):
+                    e[3] is not None and e[3].data_ptr() in outs) or (batch and _kind(e) != _kind(batch[0])):
                 if batch:
-                    fn = C.gemm_wgrad_group if batch[0][0].dtype == torch.bfloat16 else C.gemm_f32_wgrad_group
-                    fn([b[0].data_ptr() for b in batch], [b[0].stride(0) for b in batch],
-                       [b[1].data_ptr() for b in batch], [b[1].stride(0) for b in batch],
-                       [b[2].data_ptr() for b in batch],
-                       [b[3].data_ptr() if b[3] is not None else 0 for b in batch],
-                       [b[2].shape[0] for b in batch], [b[2].shape[1] for b in batch],
-                       [b[0].shape[0] for b in batch], st)
+                    _launch_group(C, batch, st)
                 batch, outs = [], set()
             if e is not None:
                 batch.append(e)

@@ -166,3 +166,63 @@ def wgrad32(dy, x, gw, gb=None, splits=None):
                          gw.stride(0), 1, int(s > 1), 0, 0, 0, 0, 0, 0, 0, 0, 0, 1.0, s, _native.ptr(gb),
                          _native.stream())
     return gw
+
+
+# ---- split-plane fp32 GEMM: csrc/kernels/gemm_sp*.hip (operands as bf16 hi/mid/lo planes) ----
+# The reference-precision path of the fp32 Linear layers (sparkmi/ops/planes.py): six exact bf16
+# slice products per fp32 product on v_mfma_f32_32x32x16_bf16, no splitting inside the k-loop.
+# SPARKMI_F32_PLANES=0 falls back to csrc/kernels/gemm_f32.hip (split inside the GEMM).
+SP = os.environ.get("SPARKMI_F32_PLANES", "1") != "0" and not _DISABLE
+
+
+def _sp_ok(*ts):
+    return all(t is None or (t.dtype == torch.float32 and t.stride(-1) == 1 and t.data_ptr() % 16 == 0
+                             and (t.dim() < 2 or t.stride(-2) % 4 == 0)) for t in ts)
+
+
+def sp_fwd(xp, wp, M, N, K, bias=None, act=0, rng=None, salt=0, thresh=0, dscale=1.0, out_planes=False):
+    """y[M,N] = dropout(act(x @ w^T + bias)) from planes xp [3,M,>=K], wp [3,N,>=K].  Returns
+    (y, y_planes or None), or None when the kernel does not cover the case (caller falls back)."""
+    if not SP or act not in (0, 1) or not _sp_ok(bias):
+        return None
+    y = torch.empty(M, N, device=xp.device, dtype=torch.float32)
+    yp = None
+    if out_planes and N % 32 == 0:
+        yp = torch.empty(3, M, N, device=xp.device, dtype=torch.bfloat16)
+    ok = _native.C().gemm_sp(0, xp.data_ptr(), xp.stride(1), xp.stride(0), wp.data_ptr(), wp.stride(1), wp.stride(0),
+                             M, N, K, 0, y.data_ptr(), y.stride(0), _native.ptr(yp), N, yp.stride(0) if yp is not None
+                             else 0, 0, _native.ptr(bias), int(act), 0, 0, 0, 0, rng.ptr() if rng is not None else 0,
+                             salt, thresh, dscale, 0, _native.stream())
+    return (y, yp) if ok else None
+
+
+def sp_dgrad(dyp, wp, M, K, N, resid=None, dact_y=None, dscale=1.0, out_planes=False, need_f32=True):
+    """dx[M,K] = (dy @ w) (+ resid) (* [dact_y > 0] dscale) from planes dyp [3,M,>=N] (zero-padded
+    to a multiple of 32 when N is not), wp [3,N,K].  Returns (dx or None, dx_planes or None)."""
+    if not SP or not _sp_ok(resid, dact_y):
+        return None
+    dx = torch.empty(M, K, device=dyp.device, dtype=torch.float32) if need_f32 else None
+    dxp = None
+    if out_planes and K % 32 == 0:
+        dxp = torch.empty(3, M, K, device=dyp.device, dtype=torch.bfloat16)
+    if dx is None and dxp is None:
+        return None
+    ok = _native.C().gemm_sp(1, dyp.data_ptr(), dyp.stride(1), dyp.stride(0), wp.data_ptr(), wp.stride(1),
+                             wp.stride(0), M, K, N, int(dyp.stride(1) >= (N + 31) // 32 * 32), _native.ptr(dx),
+                             dx.stride(0) if dx is not None else 0, _native.ptr(dxp), K,
+                             dxp.stride(0) if dxp is not None else 0, 0, 0, 0, _native.ptr(resid),
+                             resid.stride(0) if resid is not None else 0, _native.ptr(dact_y),
+                             dact_y.stride(0) if dact_y is not None else 0, 0, 0, 0, dscale, 0, _native.stream())
+    return (dx, dxp) if ok else None
+
+
+def sp_wgrad(dyp, xp, gw, gb=None):
+    """gw[N,K] += dy^T x (and gb[N] += colsum dy) from planes dyp [3,M,>=N], xp [3,M,>=K]; one
+    launch, full token reduction per tile.  Returns False when not covered."""
+    if not SP or not gw.is_contiguous() or (gb is not None and not gb.is_contiguous()):
+        return False
+    N, K = gw.shape
+    M = dyp.shape[1]
+    return bool(_native.C().gemm_sp(2, dyp.data_ptr(), dyp.stride(1), dyp.stride(0), xp.data_ptr(), xp.stride(1),
+                                    xp.stride(0), N, K, M, 0, gw.data_ptr(), gw.stride(0), 0, 0, 0, 1, 0, 0, 0, 0, 0,
+                                    0, 0, 0, 0, 1.0, _native.ptr(gb), _native.stream()))

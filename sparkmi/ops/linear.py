@@ -7,8 +7,11 @@ y = dropout_p(act(x @ W^T + b)).  Reference call sites: every nn.Linear of trans
 (distributed_cnn.py:74-78).
 
 GPU paths, chosen by the activation dtype:
-  * fp32 (reference precision): csrc/kernels/gemm_f32.hip on the fp32-input matrix cores
-    (v_mfma_f32_32x32x2_f32), fp32 master weights used directly, the same fused epilogues;
+  * fp32 (reference precision): csrc/kernels/gemm_sp*.hip — every operand as three exact bf16
+    planes (sparkmi/ops/planes.py: weights split by the optimizer, activations split once where
+    produced and shared by the forward and weight-gradient GEMMs), six bf16 products per fp32
+    product on v_mfma_f32_32x32x16_bf16, the same fused epilogues; shapes outside its tiling run
+    csrc/kernels/gemm_f32.hip on the fp32 operands;
   * bf16 (bf16 weight shadow, fp32 master/grad): csrc/kernels/gemm.hip (16x16x32 bf16 MFMA)
     whenever the shape fits (K % 64 == 0, rows 16-B aligned), the fp32 kernel on upcast
     operands otherwise (no vendor-library GEMM anywhere).
@@ -24,6 +27,7 @@ import torch
 
 from .. import _native
 from . import gemm as G
+from . import planes as _pl
 from . import rng as _rng
 from . import _grad
 from ._grad import bf16_weight, grad_buf, grad_ready
@@ -99,6 +103,15 @@ def _wgrad_accumulate(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, gb=
     end-of-backward flush, sparkmi/ops/_grad.py); otherwise the caller reports it."""
     N, K = gw.shape
     M = dy2.shape[0]
+    if dy2.dtype == torch.float32 and G.SP and gw.is_contiguous() and N % 8 == 0 and K % 8 == 0 and (
+            gb is None or gb.is_contiguous()):
+        dyp, xp = _pl.cached(dy2), _pl.cached(x2)
+        if dyp is not None and xp is not None:
+            if ready is not None and _grad.WGRAD_GROUP and _groupable(dyp, xp):
+                _grad.defer_wgrad_group(dyp, xp, gw, gb, ready, _native.stream())
+                return True
+            if G.sp_wgrad(dyp, xp, gw, gb):
+                return False
     if dy2.dtype == torch.float32:
         if (ready is not None and _grad.WGRAD_GROUP and G.supported32(N, K, M, dy2, x2, mode=2)
                 and gw.is_contiguous() and _groupable(dy2, x2) and (gb is None or gb.is_contiguous())):
@@ -118,10 +131,18 @@ def _wgrad_accumulate(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, gb=
     return False
 
 
-def _dgrad(g2, w_bf, resid=None, dact_y=None, dscale=1.0):
+def _dgrad(g2, w_bf, resid=None, dact_y=None, dscale=1.0, wp=None, out_planes=False):
     M, N = g2.shape
     K = w_bf.shape[1]
     if g2.dtype == torch.float32:
+        if wp is not None and G.SP and G._sp_ok(g2):
+            r = G.sp_dgrad(_pl.of(g2, kpad=N % 32 != 0), wp, M, K, N, resid=resid, dact_y=dact_y, dscale=dscale,
+                           out_planes=out_planes)
+            if r is not None:
+                dx, dxp = r
+                if dxp is not None:
+                    _pl.attach(dx, dxp)
+                return dx
         return _dgrad32_any(g2, w_bf, resid, dact_y, dscale)
     if G.supported(M, K, N, g2, w_bf, resid, dact_y, mode=1):
         return G.dgrad(g2, w_bf, resid=resid, dact_y=dact_y, dscale=dscale)
@@ -134,10 +155,32 @@ def compute_weight(p: torch.Tensor, dtype) -> torch.Tensor:
     return p.detach() if dtype == torch.float32 else bf16_weight(p)
 
 
-def _fwd_native(x2, weight, bias, act, p, rng, salt, w_bf=None):
+def _fwd_sp(x2, wp, N, bias, act, p, rng, salt, out_planes=False):
+    """fp32 forward on the split-plane GEMM (x2's planes: cached or split now); None if not covered."""
+    M, K = x2.shape
+    if wp is None or not G.SP or not G._sp_ok(x2) or act not in (0, 1):
+        return None
+    r = G.sp_fwd(_pl.of(x2), wp, M, N, K, bias, act, rng, salt, _rng.threshold(p), _rng.scale(p),
+                 out_planes=out_planes)
+    if r is None:
+        return None
+    y, yp = r
+    if yp is not None:
+        _pl.attach(y, yp)
+    return y
+
+
+def _wplanes(weight):
+    return _pl.weight(weight) if G.SP and weight.dim() == 2 and weight.shape[1] % 8 == 0 else None
+
+
+def _fwd_native(x2, weight, bias, act, p, rng, salt, w_bf=None, out_planes=False, wp=None):
     N, K = weight.shape
     M = x2.shape[0]
     if x2.dtype == torch.float32:
+        y = _fwd_sp(x2, wp if wp is not None else _wplanes(weight), N, bias, act, p, rng, salt, out_planes)
+        if y is not None:
+            return y
         return _fwd32_any(x2, weight.detach(), bias, act, rng, salt, p)
     w = w_bf if w_bf is not None else bf16_weight(weight)
     if G.supported(M, N, K, x2, w, mode=0) and act in (0, 1):
@@ -182,6 +225,7 @@ class LinearFn(torch.autograd.Function):
         if ctx.native:
             x2 = x2.contiguous()
             y2 = _fwd_native(x2, weight, bias, act, p, rng, salt)
+            ctx.x_planes = _pl.cached(x2)  # kept for the weight-gradient GEMM
             ctx.seed = 0
         else:
             ctx.seed = rng.current() if p > 0 else 0
@@ -208,8 +252,13 @@ class LinearFn(torch.autograd.Function):
             else:
                 g2 = dy2
             resid = _slot_grad(ctx.x_slot, g2.shape[0])
-            dx = _dgrad(g2, compute_weight(weight, g2.dtype), resid=resid) if ctx.needs_input_grad[0] else None
+            f32 = g2.dtype == torch.float32
+            wp = _wplanes(weight) if f32 else None
+            dx = _dgrad(g2, compute_weight(weight, g2.dtype), resid=resid, wp=wp) if ctx.needs_input_grad[0] else None
             bgrad = grad_buf(bias) if bias is not None else None
+            if f32 and G.SP and ctx.x_planes is not None:
+                _pl.attach(x2, ctx.x_planes)
+                _pl.of(g2, kpad=g2.shape[1] % 32 != 0)
             with _grad.side(g2.device, g2, x2):
                 deferred = _wgrad_accumulate(gw, g2, x2, bgrad, ready=(weight, bias))
         else:
@@ -264,8 +313,9 @@ class FFNFn(torch.autograd.Function):
         ctx.native = _native.use_native(x)
         if ctx.native:
             x2 = x2.contiguous()
-            h = _fwd_native(x2, w1, b1, 1, p, rng, salt)
+            h = _fwd_native(x2, w1, b1, 1, p, rng, salt, out_planes=True)
             y = _fwd_native(h, w2, b2, 0, 0.0, rng, 0)
+            ctx.x_planes, ctx.h_planes = _pl.cached(x2), _pl.cached(h)
             ctx.seed = 0
         else:
             ctx.seed = rng.current() if p > 0 else 0
@@ -283,14 +333,23 @@ class FFNFn(torch.autograd.Function):
         p = ctx.p
         if ctx.native:
             dy2 = dy2.contiguous()
+            f32 = dy2.dtype == torch.float32
+            if f32 and G.SP:
+                if ctx.x_planes is not None:
+                    _pl.attach(x2, ctx.x_planes)
+                if ctx.h_planes is not None:
+                    _pl.attach(h, ctx.h_planes)
             # dh_pre = (dy @ W2) * relu'/dropout mask (from the saved output h), fused epilogue
-            dh = _dgrad(dy2, compute_weight(w2, dy2.dtype), dact_y=h, dscale=_rng.scale(p))
+            # (fp32: its planes written by the same epilogue, for linear1's dgrad and wgrad)
+            dh = _dgrad(dy2, compute_weight(w2, dy2.dtype), dact_y=h, dscale=_rng.scale(p),
+                        wp=_wplanes(w2) if f32 else None, out_planes=True)
             gw2, gb2, gw1, gb1 = grad_buf(w2), grad_buf(b2), grad_buf(w1), grad_buf(b1)
             with _grad.side(dy2.device, dy2, h):
                 if not _wgrad_accumulate(gw2, dy2, h, gb2, ready=(w2, b2)):
                     grad_ready(w2, b2)
             resid = _slot_grad(ctx.x_slot, dh.shape[0])
-            dx = _dgrad(dh, compute_weight(w1, dh.dtype), resid=resid) if ctx.needs_input_grad[0] else None
+            dx = _dgrad(dh, compute_weight(w1, dh.dtype), resid=resid,
+                        wp=_wplanes(w1) if f32 else None) if ctx.needs_input_grad[0] else None
             with _grad.side(dh.device, dh, x2):
                 if not _wgrad_accumulate(gw1, dh, x2, gb1, ready=(w1, b1)):
                     grad_ready(w1, b1)
@@ -326,12 +385,14 @@ class ConcatLinearFn(torch.autograd.Function):
     def forward(ctx, x, wviews, bviews, shape, params, shared):
         ctx.set_materialize_grads(False)
         N, K = shape
-        wm, wg, ws = wviews
+        wm, wg, ws = wviews[:3]
         bm, bg = bviews[0], bviews[1]
         x2 = x.reshape(-1, K).contiguous()
         w = wm.view(N, K)
-        y2 = _fwd_native(x2, w, bm, 0, 0.0, None, 0, w_bf=ws.view(N, K) if ws is not None else None)
+        wp = wviews[3] if len(wviews) > 3 and x2.dtype == torch.float32 and G.SP else None
+        y2 = _fwd_native(x2, w, bm, 0, 0.0, None, 0, w_bf=ws.view(N, K) if ws is not None else None, wp=wp)
         ctx.wviews, ctx.bg, ctx.shape, ctx.params, ctx.shared = wviews, bg, shape, params, shared
+        ctx.x_planes, ctx.wp = _pl.cached(x2), wp
         ctx.save_for_backward(x2)
         return y2.reshape(*x.shape[:-1], N)
 
@@ -339,14 +400,17 @@ class ConcatLinearFn(torch.autograd.Function):
     def backward(ctx, _unused):
         (x2,) = ctx.saved_tensors
         N, K = ctx.shape
-        wm, wg, ws = ctx.wviews
+        wm, wg, ws = ctx.wviews[:3]
         g = ctx.shared.take()
         if g is None:  # no consumer produced a gradient
             grad_ready(*ctx.params)
             return None, None, None, None, None, None
         g2 = g.reshape(-1, N)
         w = wm.view(N, K) if g2.dtype == torch.float32 else ws.view(N, K)
-        dx = _dgrad(g2, w) if ctx.needs_input_grad[0] else None
+        dx = _dgrad(g2, w, wp=ctx.wp) if ctx.needs_input_grad[0] else None
+        if ctx.wp is not None and ctx.x_planes is not None:
+            _pl.attach(x2, ctx.x_planes)
+            _pl.of(g2, kpad=N % 32 != 0)
         with _grad.side(g2.device, g2, x2):
             if not _wgrad_accumulate(wg.view(N, K), g2, x2, ctx.bg, ready=ctx.params):
                 grad_ready(*ctx.params)
@@ -366,6 +430,8 @@ def concat_linear(x, flat, linears, shared):
     wv, bv = flat.concat(ws), flat.concat(bs)
     if wv is None or bv is None or (x.dtype == torch.bfloat16 and wv[2] is None):
         return None
+    if x.dtype == torch.float32 and x.is_cuda and G.SP:
+        wv = tuple(wv) + (flat.concat_planes(ws),)
     N, K = sum(w.shape[0] for w in ws), ws[0].shape[1]
     params = tuple(p for pair in zip(ws, bs) for p in pair)
     return ConcatLinearFn.apply(x, wv, bv, (N, K), params, shared)

@@ -75,7 +75,8 @@ class Adam(_FlatOptimizer):
                          [sp + 2 * s if sp else 0 for s, _ in self.ranges], [e - s for s, e in self.ranges],
                          self.lr_t.data_ptr(), self.step_t.data_ptr(), self.done_t.data_ptr(), self.b1, self.b2,
                          self.eps, self.weight_decay, self.grad_scale, int(self.adamw), int(self.zero_grad_after_step),
-                         _native.stream())
+                         [_native.ptr(f.planes) + 2 * s for s, _ in self.ranges] if f.planes is not None else [],
+                         f.plane_stride(), _native.stream())
             return
         with torch.no_grad():
             self.step_t.add_(1)
@@ -95,6 +96,7 @@ class Adam(_FlatOptimizer):
                 p.addcdiv_(m, v.sqrt() / (bc2 ** 0.5) + self.eps, value=-lr / bc1)
                 if self.zero_grad_after_step:
                     f.grad[s:e].zero_()
+            f.refresh_planes()
 
     def step(self):
         f = self.flat
@@ -105,7 +107,8 @@ class Adam(_FlatOptimizer):
             st = _native.stream()
             C.adam(f.master.data_ptr(), f.grad.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), _native.ptr(f.shadow),
                    f.numel, self.lr_t.data_ptr(), self.step_t.data_ptr(), self.done_t.data_ptr(), self.b1, self.b2, self.eps,
-                   self.weight_decay, self.grad_scale, int(self.adamw), int(self.zero_grad_after_step), st)
+                   self.weight_decay, self.grad_scale, int(self.adamw), int(self.zero_grad_after_step),
+                   _native.ptr(f.planes), f.plane_stride(), st)
             return
         with torch.no_grad():
             self.step_t.add_(1)
@@ -128,6 +131,7 @@ class Adam(_FlatOptimizer):
                 f.grad.zero_()
             if f.shadow is not None:
                 f.shadow.copy_(p.to(torch.bfloat16))
+            f.refresh_planes()
 
     def state_dict(self):
         sd = super().state_dict()

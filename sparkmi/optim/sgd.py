@@ -19,7 +19,8 @@ class SGD(_FlatOptimizer):
             st = _native.stream()
             C.sgd(f.master.data_ptr(), f.grad.data_ptr(), _native.ptr(self.buf), _native.ptr(f.shadow), f.numel,
                   self.lr_t.data_ptr(), self.step_t.data_ptr(), self.done_t.data_ptr(), self.momentum, self.dampening, self.weight_decay,
-                  int(self.nesterov), self.grad_scale, int(self.zero_grad_after_step), st)
+                  int(self.nesterov), self.grad_scale, int(self.zero_grad_after_step), _native.ptr(f.planes),
+                  f.plane_stride(), st)
             return
         with torch.no_grad():
             self.step_t.add_(1)
@@ -38,6 +39,7 @@ class SGD(_FlatOptimizer):
                 f.grad.zero_()
             if f.shadow is not None:
                 f.shadow.copy_(f.master.to(torch.bfloat16))
+            f.refresh_planes()
 
     def state_dict(self):
         sd = super().state_dict()

@@ -77,13 +77,24 @@ class IpcUnavailable(RuntimeError):
     """IPC mapping or the all-reduce self-test failed on at least one rank (all ranks agree)."""
 
 
+class IpcPeerLost(RuntimeError):
+    """An IPC all-reduce timed out waiting for a peer: the bucket of that call was NaN-poisoned
+    (never a finite partial sum) and the group must fail (the launcher restarts it from the last
+    checkpoint)."""
+
+
 class IpcAllReduce:
     """Sum-all-reduce of fp32 tensors of up to ``cap_floats`` elements among the ranks of
     ``group`` (one node), in place, on the current stream."""
 
-    def __init__(self, cap_floats=1 << 18, group=None, blocks=None):
+    def __init__(self, cap_floats=1 << 18, group=None, blocks=None, timeout_s=None):
         C = _native.comm()
         self.C = C
+        if timeout_s is None:
+            import os
+            timeout_s = float(os.environ.get("SPARKMI_IPC_TIMEOUT_S", "4"))
+        # the kernel's poll bound: ~2^24 polls with s_sleep back-off take ~4 s
+        self.spins = max(1, int(float(timeout_s) * (1 << 24) / 4.0))
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -138,13 +149,18 @@ class IpcAllReduce:
             raise ValueError("IpcAllReduce: contiguous fp32 tensor, numel % 4 == 0, <= capacity")
         blocks = self.blocks or max(1, min(self.C.IPC_MAX_BLOCKS, (t.numel() // 4 + 1023) // 1024))
         self.C.ipc_allreduce(t.data_ptr(), t.numel(), self.data, self.sig, self.cap, self.rank, self.ctr.data_ptr(),
-                             self.err.data_ptr(), blocks, torch.cuda.current_stream().cuda_stream)
+                             self.err.data_ptr(), blocks, torch.cuda.current_stream().cuda_stream, self.spins)
         return t
 
+    def failed(self):
+        """True once any call timed out waiting for a peer (sticky; synchronises)."""
+        return bool(int(self.err.item()))
+
     def check(self):
-        """Raise if any call timed out waiting for a peer (synchronises)."""
-        if int(self.err.item()):
-            raise RuntimeError("IPC all-reduce: a peer did not signal within the timeout")
+        """Raise IpcPeerLost if any call timed out waiting for a peer (synchronises)."""
+        if self.failed():
+            raise IpcPeerLost("IPC all-reduce: a peer did not signal within the timeout; the affected gradient "
+                              "bucket was NaN-poisoned")
 
     def close(self):
         torch.cuda.synchronize()

@@ -127,12 +127,28 @@ class DataParallel:
         self.overlap = bool(on)
 
     def reset(self):
+        # gradient-readiness bookkeeping of one backward.  A parameter reused in one forward
+        # (e.g. a module applied twice) reports ready / queued once per contribution: its bucket
+        # may only go to the collective after the LAST one.  The first backward learns which
+        # parameters are reused (no early flush or launch at all during it); afterwards buckets
+        # holding a reused parameter are reduced in finish() only.
+        counts = getattr(self, "_rcount", None)
+        if counts is not None and self._learning and any(counts):
+            self._reused = {i for i, c in enumerate(counts) if c > 1}
+            self._learning = False
+        self._rcount = [0] * len(self.flat.params)
         self._pending = [len(idx) for (_, _, idx) in self.buckets]
         self._unsettled = [len(idx) for (_, _, idx) in self.buckets]
         self._settled = set()
         self._launched = [False] * len(self.buckets)
         self._works = []
         self.early_flushes = 0
+
+    _learning = True
+    _reused = frozenset()
+
+    def _early_ok(self, b):
+        return not self._learning and not any(i in self._reused for i in self.buckets[b][2])
 
     bytes_reduced = 0  # cumulative gradient bytes handed to the collectives (metrics)
 
@@ -226,7 +242,7 @@ class DataParallel:
         if i is None or self._pending is None:
             return
         b = self._settle(i)
-        if b is not None and self._pending[b] > 0:
+        if b is not None and self._pending[b] > 0 and self._early_ok(b):
             # every parameter of bucket b is queued or final: launch the queued weight-gradient
             # work now (its completion reports the parameters ready -> _on_ready launches b)
             self.early_flushes += 1
@@ -236,9 +252,13 @@ class DataParallel:
         i = self.flat.index.get(id(p))
         if i is None or self._pending is None:
             return
+        self._rcount[i] += 1
         self._settle(i)
         b = self.bucket_of[i]
+        if self._rcount[i] > 1 or not self._early_ok(b):
+            return  # a reused parameter (or the learning step): the bucket waits for finish()
         self._pending[b] -= 1
+        assert self._pending[b] >= 0, "gradient bucket bookkeeping went negative"
         if self._pending[b] == 0:
             self._launch(b)
 
@@ -256,6 +276,13 @@ class DataParallel:
     @property
     def grad_scale(self):
         return 1.0 / self.world
+
+    def check(self):
+        """Fail loudly if the gradient reduction lost a peer (IPC path: a poll timed out, the
+        bucket was NaN-poisoned; sparkmi.parallel.comm.IpcPeerLost).  Synchronises: call it every
+        log interval (Trainer) — inside a replayed HIP graph nothing else looks."""
+        if self.ipc is not None:
+            self.ipc.check()
 
     def close(self):
         if self.ipc is not None:

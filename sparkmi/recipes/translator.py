@@ -7,7 +7,10 @@ Reference: d_model 512, ffn 1024, 8 heads, dropout 0.1, 1 layer, S = 200 (Trunca
 masked mean, decoder input == target (no shift, Q7), the reference's mask semantics (Q6:
 padding mask no-op, look-ahead mask adds +1.0 to strictly-past keys).  ``--shift-targets`` and
 ``--mask-mode causal`` select the textbook variants instead.  spaCy tokenizers are unavailable
-offline, so both sides use basic_english (X14).
+offline, so both sides use basic_english (X14).  ``--dtype fp32`` (default) trains at the
+reference's precision (fp32 modules, pytorch_machine_translator.py:120-137); ``--dtype bf16``
+runs bf16 activations with fp32 master weights.  Data-parallel runs capture the backward as
+several graphs so finished gradient buckets are reduced under the rest of the backward.
 """
 import dataclasses
 
@@ -38,9 +41,20 @@ class TranslatorConfig(TrainConfig):
     num_layers: int = 1
     max_sequence_length: int = 200
     mask_mode: str = "reference"
+    dtype: str = "fp32"            # "fp32" (reference precision) | "bf16" (bf16 activations, fp32 master)
     shift_targets: bool = False
     n_train: int = 29000
     log_every: int = 100
+
+
+def transformer_flops_per_sample(layers, seq, vocab, d=512, ffn=1024):
+    """Matmul FLOPs of one training sample (forward + backward = 3x forward): the GEMMs of every
+    encoder / decoder layer, the vocab projection, QK^T and PV of the 3 attention sites per layer
+    pair (63.4 GFLOP at L6 S256 V10k)."""
+    enc = 2 * d * (3 * d + d + 2 * ffn)
+    dec = 2 * d * (3 * d + d + d + 2 * d + d + 2 * ffn)
+    attn = 3 * 4 * seq * d
+    return 3 * (layers * (enc + dec + attn) + 2 * d * vocab) * seq
 
 
 def build_corpus(cfg):
@@ -65,12 +79,19 @@ def train_fn(cfg):
     loader = DeviceLoader([src[idx], tgt[idx]], cfg.batch_size, device, shuffle=True, drop_last=True,
                           seed=cfg.seed + 1000 * rank)
     torch.manual_seed(cfg.seed)
+    if cfg.dtype not in ("fp32", "bf16"):
+        raise ValueError(f"--dtype must be fp32 or bf16, got {cfg.dtype!r}")
     model = Transformer(cfg.d_model, cfg.ffn_hidden, cfg.num_heads, cfg.drop_prob, cfg.num_layers,
                         cfg.max_sequence_length, len(de_vocab), len(en_vocab), len(de_vocab), mask_mode=cfg.mask_mode,
-                        seed=cfg.seed + rank)
+                        seed=cfg.seed + rank, dtype=cfg.dtype)
     shift = cfg.shift_targets
+    S = cfg.max_sequence_length - (1 if shift else 0)
+    flops = transformer_flops_per_sample(cfg.num_layers, S, len(de_vocab), cfg.d_model, cfg.ffn_hidden)
     trainer = Trainer(model, lambda m, s, t: m.training_step_loss(s, t, shift_targets=shift),
-                      lambda flat: Adam(flat, lr=cfg.lr), cfg, device, rank, world, "translator")
+                      lambda flat: Adam(flat, lr=cfg.lr), cfg, device, rank, world, "translator",
+                      shadow=(cfg.dtype == "bf16" and torch.device(device).type == "cuda"),
+                      split_fn=lambda m, s, t: m.training_step_split(s, t, shift_targets=shift),
+                      flops_per_sample=flops)
     stats = trainer.fit(loader, cfg.epochs)
     trainer.close()
     out = dict(stats, world=world, en_vocab=len(en_vocab), de_vocab=len(de_vocab))

@@ -48,9 +48,13 @@ class StepRunner:
         # reduction and the optimizer, read back (one sync) by pop_phases() every log interval
         self.phase_timing = False
         self._phase_events = []
+        self._opt_in_graph = False      # the captured graph holds the gradient reduction + optimizer
         if ddp is not None:
             optimizer.grad_scale = ddp.grad_scale
             if ddp.zero:
+                if not hasattr(optimizer, "shard"):
+                    raise ValueError(f"zero=True (ZeRO-1) needs an optimizer with sharded state; "
+                                     f"{type(optimizer).__name__} has none (use Adam/AdamW or zero=False)")
                 optimizer.shard(ddp.shard_ranges())
 
     @property
@@ -115,9 +119,10 @@ class StepRunner:
         return loss
 
     def pop_phases(self):
-        """Mean device seconds per phase over the eager steps since the last call:
-        {fwd_bwd_s, allreduce_s, optim_s} (empty when no step was timed, e.g. graph replays,
-        whose phases live inside one graph)."""
+        """Mean device seconds per phase over the steps since the last call: {fwd_bwd_s,
+        allreduce_s, optim_s} (eager steps: events between the phases; graph steps: the step is
+        captured as separate phase graphs while ``phase_timing`` is on, events between their
+        replays)."""
         ev, self._phase_events = self._phase_events, []
         if not ev:
             return {}
@@ -195,11 +200,28 @@ class StepRunner:
             self.ddp.set_overlap(False)  # no collective may be enqueued during capture
             with torch.cuda.graph(g):
                 self.static_loss = self._fwd_bwd(*self.static_in)
+        elif self.phase_timing and self.fused_step is None:
+            # phase-timed graph step: forward + backward, gradient reduction (IPC kernel) and the
+            # optimizer as three graphs replayed back to back, events between them (one more
+            # replay per phase than the single-graph step: timing, not the fastest path)
+            if self._dp:
+                self.ddp.set_overlap(False)
+            with torch.cuda.graph(g):
+                self.static_loss = self._fwd_bwd(*self.static_in)
+            self._phase_graphs = []
+            for fn in ((lambda: self.ddp.finish()) if self._dp else (lambda: None),
+                       lambda: (self.opt.step(), self.ddp.gather_params() if self._dp else None)):
+                pg = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(pg, pool=g.pool()):
+                    fn()
+                self._phase_graphs.append(pg)
+            self._opt_in_graph = True
         else:
             # one executor, or data-parallel over the IPC all-reduce kernel: the WHOLE step
             # (forward, backward, gradient reduction, optimizer) is one graph
             with torch.cuda.graph(g):
                 self.static_loss = self._eager(*self.static_in)
+            self._opt_in_graph = True
         self.graph = g
 
     def step(self, *batch):
@@ -210,15 +232,40 @@ class StepRunner:
         if self.graph is None:
             self._capture(batch)  # then replayed below for this step
         self._refresh_inputs(batch)
+        phased = getattr(self, "_phase_graphs", None)
+        e0 = self._event()
         self.graph.replay()
+        if phased is not None:
+            e1 = self._event()
+            phased[0].replay()
+            e2 = self._event()
+            phased[1].replay()
+            e3 = self._event()
+            if e0 is not None:
+                self._phase_events.append((e0, e1, e2, e3))
+            if self._dp:
+                self.ddp.bytes_reduced += self.ddp.flat.grad.numel() * 4
+            return self.static_loss
         if self.graph2 is not None:
             # after each backward piece, its final buckets go to RCCL while the next piece runs
             for g, wave in zip(self.graph2, self.bucket_waves):
                 for b in wave:
                     self.ddp.launch(b)
                 g.replay()
-        if self._dp and not self.ddp.graph_safe:
-            self.ddp.finish()   # bucketed RCCL all-reduce of the flat gradient buffer
+        if not self._opt_in_graph:
+            # the graphs hold forward + backward only (data-parallel over RCCL, or split-graph
+            # capture over either backend): reduce the remaining buckets, then the optimizer
+            if self._dp:
+                self.ddp.finish()
             self.opt.step()
-            self.ddp.gather_params()
+            if self._dp:
+                self.ddp.gather_params()
+        elif self._dp:
+            # the replayed graph reduced every bucket (IPC kernel): account its bytes
+            self.ddp.bytes_reduced += self.ddp.flat.grad.numel() * 4
         return self.static_loss
+
+    def check(self):
+        """Raise if the data-parallel reduction lost a peer (synchronises; call per log interval)."""
+        if self.ddp is not None:
+            self.ddp.check()

@@ -39,7 +39,7 @@ def setup_executor(cfg):
 
 class Trainer:
     def __init__(self, model, loss_fn, make_optimizer, cfg, device, rank=0, world=1, name="run", shadow=None,
-                 fused_step=None):
+                 fused_step=None, split_fn=None, flops_per_sample=None):
         self.model = model.to(device)
         self.cfg = cfg
         self.device = torch.device(device)
@@ -48,11 +48,14 @@ class Trainer:
         self.opt = make_optimizer(self.flat)
         self.ddp = DataParallel(self.flat, bucket_mb=cfg.bucket_mb, zero=getattr(cfg, "zero", False)) if world > 1 else None
         use_graph = bool(cfg.graph) and self.device.type == "cuda"
+        # split_fn (data-parallel): the backward as several graphs, finished gradient buckets
+        # reduced while the rest of the backward runs (StepRunner)
         self.runner = StepRunner(self.model, loss_fn, self.opt, ddp=self.ddp, graph=use_graph,
-                                 fused_step=fused_step if world == 1 else None)
+                                 fused_step=fused_step if world == 1 else None,
+                                 split_fn=split_fn if (world > 1 and use_graph) else None)
         path = f"{cfg.metrics}.rank{rank}.jsonl" if cfg.metrics else None
         self.metrics = MetricsLogger(path, rank=rank, every=cfg.log_every, echo=cfg.verbose and rank == 0,
-                                     extra={"run": name, "world": world})
+                                     extra={"run": name, "world": world}, flops_per_sample=flops_per_sample)
         self.ckpt = CheckpointManager(cfg.ckpt_dir, rank=rank) if cfg.ckpt_dir else None
         self.step = 0
         self.epoch = 0
@@ -71,6 +74,7 @@ class Trainer:
 
     def _save(self, cursor):
         if self.ckpt is not None:
+            self.runner.check()  # never checkpoint a model updated from a poisoned gradient
             with trace.range("checkpoint"):
                 self.ckpt.save(self.step, self.model, self.opt, self.epoch, cursor)
             if self.world > 1:
@@ -108,6 +112,7 @@ class Trainer:
                 i += 1
                 progress(self.step)  # heartbeat progress: a stuck collective stops this counter
                 if self.metrics.due():
+                    self.runner.check()  # a lost data-parallel peer fails the group here
                     ph = self.runner.pop_phases()
                     ddp_bytes = self.ddp.bytes_reduced if self.ddp is not None else 0
                     extra = dict(ph, data_s=data_s / max(1, self.metrics.pending() + 1),

@@ -11,6 +11,12 @@ compute shadow is kept in a third buffer (``p._smi_bf16``).  Consequences on MI3
     front of the buffer first and bucket 0 can be all-reduced while backward continues.
 Each parameter starts on a 64-element boundary (256-B aligned fp32, 128-B aligned bf16).
 
+Reference-precision (fp32) models keep a fourth buffer on GPU, created on first use: the weights
+split into three bf16 planes (``planes`` [3, numel], hi / mid / lo with p = hi + mid + lo
+exactly; sparkmi/ops/planes.py), the operand format of the fp32 GEMM.  The optimizer kernel
+rewrites the planes of every parameter it updates, and ``refresh_shadow`` (checkpoint loads,
+data-parallel broadcasts / ZeRO gathers) re-splits them.
+
 A module may list parameter groups to be stored back to back (``_smi_flat_groups()``): e.g. the
 six decoder kv projections, which all read the encoder output, then form ONE [6*2D, D] weight
 view and run as one GEMM (``concat``).  A group sits where its first-registered member would
@@ -61,8 +67,50 @@ class FlatParams:
                 if self.shadow is not None:
                     p._smi_bf16 = self.shadow[o:o + n].view(p.shape)
         self.index = {id(p): i for i, p in enumerate(self.params)}
+        self.planes = None  # [3, numel] bf16 split planes, created by the first weight_planes()
+        for p, o in zip(self.params, self.offsets):
+            if device.type == "cuda" and p.dim() == 2:
+                p._smi_planes_fn = self._planes_fn(p, o)
         object.__setattr__(module, "_smi_flat", self)  # checkpoint loads refresh the bf16 shadow
         self.refresh_shadow()
+
+    def _planes_fn(self, p, o):
+        rows, cols = p.shape
+        return lambda: self.ensure_planes()[:, o:o + rows * cols].view(3, rows, cols)
+
+    def ensure_planes(self):
+        """The [3, numel] split-plane buffer (allocated and split from the master on first use)."""
+        if self.planes is None:
+            self.planes = torch.empty(3, self.numel, dtype=torch.bfloat16, device=self.device)
+            self.refresh_planes()
+        return self.planes
+
+    def plane_stride(self):
+        return self.planes.stride(0) if self.planes is not None else 0
+
+    def refresh_planes(self):
+        """Re-split the planes from the fp32 master (after anything but the optimizer wrote it)."""
+        if self.planes is None:
+            return
+        if _native.use_native(self.master):
+            _native.C().split3(self.master.data_ptr(), 1, self.numel, self.numel, self.planes.data_ptr(), self.numel,
+                               self.planes.stride(0), _native.stream())
+        else:
+            hi = self.master.to(torch.bfloat16)
+            r = self.master - hi.float()
+            mid = r.to(torch.bfloat16)
+            self.planes[0].copy_(hi)
+            self.planes[1].copy_(mid)
+            self.planes[2].copy_((r - mid.float()).to(torch.bfloat16))
+
+    def concat_planes(self, params):
+        """[3, sum rows, cols] plane view of 2-D ``params`` stored back to back (see ``concat``)."""
+        if self.concat(params) is None:
+            return None
+        o0, _ = self.param_range(params[0])
+        rows = sum(p.shape[0] for p in params)
+        cols = params[0].shape[1]
+        return self.ensure_planes()[:, o0:o0 + rows * cols].view(3, rows, cols)
 
     @staticmethod
     def _place_groups(module, params):
@@ -97,6 +145,7 @@ class FlatParams:
         return (self.master[o0:o], self.grad[o0:o], self.shadow[o0:o] if self.shadow is not None else None)
 
     def refresh_shadow(self):
+        self.refresh_planes()
         if self.shadow is None:
             return
         if _native.use_native(self.master):

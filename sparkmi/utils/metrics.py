@@ -5,8 +5,9 @@ so a HIP-graph step loop is not stalled) and every ``every`` steps synchronises 
 one JSON line: step, mean loss over the interval, samples/s and ms/step over the interval, plus
 the phase breakdown the Trainer passes (data_s: host time waiting for the batch;
 fwd_bwd_s / allreduce_s / optim_s: device time per phase from HIP events of eager steps;
-bytes_reduced: gradient bytes handed to the collectives in the interval).  ``aggregate()`` (driver side) combines per-rank files into
-whole-job samples/s, the BASELINE metric.
+bytes_reduced: gradient bytes handed to the collectives in the interval; with ``flops_per_sample``
+also tflops: achieved model TFLOP/s of this rank).  ``aggregate()`` (driver side) combines
+per-rank files into whole-job samples/s, the BASELINE metric.
 """
 import json
 import os
@@ -16,8 +17,9 @@ import torch
 
 
 class MetricsLogger:
-    def __init__(self, path=None, rank=0, every=50, echo=False, extra=None):
+    def __init__(self, path=None, rank=0, every=50, echo=False, extra=None, flops_per_sample=None):
         self.path = path
+        self.flops_per_sample = flops_per_sample
         self.rank = rank
         self.every = max(1, int(every))
         self.echo = echo
@@ -69,6 +71,8 @@ class MetricsLogger:
         rec = {"step": self._step, "rank": self.rank, "time": time.time(),
                "loss": float(self._acc.item()) / self._n if self._acc is not None else None,
                "samples_per_s": self._samples / dt, "ms_per_step": dt * 1e3 / self._n}
+        if self.flops_per_sample:
+            rec["tflops"] = self._samples * self.flops_per_sample / dt / 1e12
         rec.update(self.extra)
         rec.update({k: (float(v) if isinstance(v, (int, float)) or torch.is_tensor(v) else v) for k, v in scalars.items()})
         self.log_record(rec)

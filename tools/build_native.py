@@ -49,12 +49,34 @@ def _pybind_includes():
     return [pybind11.get_include(), sysconfig.get_paths()["include"]]
 
 
-def _headers_digest():
+_INC_RE = __import__("re").compile(r'^\s*#\s*include\s+"([^"]+)"', __import__("re").M)
+
+
+def _headers_digest(src=None):
+    """Digest of the csrc/include headers ``src`` includes (transitively), or of all of them: a
+    header edit rebuilds only the translation units that see it."""
+    inc_dir = os.path.join(CSRC, "include")
+    if src is None:
+        names = sorted(os.listdir(inc_dir))
+    else:
+        seen, todo = set(), [src]
+        while todo:
+            f = todo.pop()
+            try:
+                with open(f) as fh:
+                    text = fh.read()
+            except OSError:
+                continue
+            for name in _INC_RE.findall(text):
+                path = os.path.join(inc_dir, name)
+                if name not in seen and os.path.exists(path):
+                    seen.add(name)
+                    todo.append(path)
+        names = sorted(seen)
     h = hashlib.sha256()
-    p = os.path.join(CSRC, "include")
-    for f in sorted(os.listdir(p)):
+    for f in names:
         h.update(f.encode())
-        with open(os.path.join(p, f), "rb") as fh:
+        with open(os.path.join(inc_dir, f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()
 
@@ -98,13 +120,12 @@ def _run(cmd):
 
 def build(force=False, jobs=8, verbose=True):
     os.makedirs(OBJ, exist_ok=True)
-    hdr = _headers_digest()
     inc = ["-I" + os.path.join(CSRC, "include")]
     py_inc = ["-I" + p for p in _pybind_includes()]
     jobs_list = []  # (cmd, object, digest)
 
     def obj(src, o, cmd):
-        d = _obj_digest(src, cmd, hdr)
+        d = _obj_digest(src, cmd, _headers_digest(src))
         if _needs(o, d, force):
             jobs_list.append((cmd, o, d))
         return o, d
