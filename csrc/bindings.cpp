@@ -33,9 +33,10 @@ int smi_ln_bwd_reduce(const float*, const float*, int, int, float*, float*, int,
 int smi_ln_bwd_reduce_multi(const float* const*, const float* const*, float* const*, float* const*, const int*, const int*,
                             int, int, hipStream_t);
 int smi_ln_fwd_f32(const void*, const void*, const float*, const float*, void*, void*, float*, float*, int, int, float,
-                   const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
+                   const uint32_t*, uint32_t, uint32_t, float, void*, long, hipStream_t);
 int smi_ln_bwd_f32(const void*, const void*, const float*, const float*, const float*, void*, void*, const void*, float*,
-                   float*, int, float*, float*, int, int, int, const uint32_t*, uint32_t, uint32_t, float, hipStream_t);
+                   float*, int, float*, float*, int, int, int, const uint32_t*, uint32_t, uint32_t, float, void*, long,
+                   hipStream_t);
 int smi_emb_fwd_f32(const long long*, const void*, const float*, void*, long, int, int, const uint32_t*, uint32_t, uint32_t,
                     float, hipStream_t);
 int smi_emb_bwd_f32(const long long*, const void*, float*, long, int, long long, const uint32_t*, uint32_t, uint32_t, float, long, void*,
@@ -119,15 +120,18 @@ PYBIND11_MODULE(_C, m) {
     chk(smi_ln_bwd(P(dy), P(xs), PF(mean), PF(rstd), PF(gamma), P(dres), P(dh), P(dres_add), PF(pg), PF(pb), nblocks,
                    PF(dgamma), PF(dbeta), accumulate, M, D, (const uint32_t*)seedp, salt, thresh, dscale, S(st)), "ln_bwd");
   });
+  // planes / pps: optional bf16 hi/mid/lo planes [3][M][D] of the output y (fwd) / dh (bwd), 0 for none
   m.def("ln_fwd_f32", [](u h, u r, u gamma, u beta, u y, u xsave, u mean, u rstd, int M, int D, float eps, u seedp,
-                         uint32_t salt, uint32_t thresh, float dscale, u st) {
+                         uint32_t salt, uint32_t thresh, float dscale, u planes, long pps, u st) {
     chk(smi_ln_fwd_f32(P(h), P(r), PF(gamma), PF(beta), P(y), P(xsave), PF(mean), PF(rstd), M, D, eps,
-                       (const uint32_t*)seedp, salt, thresh, dscale, S(st)), "ln_fwd_f32");
+                       (const uint32_t*)seedp, salt, thresh, dscale, P(planes), pps, S(st)), "ln_fwd_f32");
   });
   m.def("ln_bwd_f32", [](u dy, u xs, u mean, u rstd, u gamma, u dres, u dh, u dres_add, u pg, u pb, int nblocks, u dgamma,
-                         u dbeta, int accumulate, int M, int D, u seedp, uint32_t salt, uint32_t thresh, float dscale, u st) {
+                         u dbeta, int accumulate, int M, int D, u seedp, uint32_t salt, uint32_t thresh, float dscale,
+                         u planes, long pps, u st) {
     chk(smi_ln_bwd_f32(P(dy), P(xs), PF(mean), PF(rstd), PF(gamma), P(dres), P(dh), P(dres_add), PF(pg), PF(pb), nblocks,
-                       PF(dgamma), PF(dbeta), accumulate, M, D, (const uint32_t*)seedp, salt, thresh, dscale, S(st)),
+                       PF(dgamma), PF(dbeta), accumulate, M, D, (const uint32_t*)seedp, salt, thresh, dscale, P(planes),
+                       pps, S(st)),
         "ln_bwd_f32");
   });
   m.def("emb_fwd_f32", [](u ids, u table, u pe, u out, long T, int D, int Sp, u seedp, uint32_t salt, uint32_t thresh,
@@ -183,8 +187,9 @@ PYBIND11_MODULE(_C, m) {
     chk(smi_attn_bwd(&a, P(o), PF(delta), S(st)), "attn_bwd");
   });
   // fp32 attention: (q, k, v) pointers + (batch, seq, head) strides; o/lse written by the forward
+  // op / op_ps (fwd), dqp / dkp / dvp / dq_ps / dkv_ps (bwd): optional split planes of the outputs
   m.def("attn_f32_fwd", [](u q, u k, u v, py::tuple qs, py::tuple ks, py::tuple vs, u o, py::tuple os, u lse, u kpad,
-                           int B, int H, int Sq, int Sk, int mode, float scale_log2, u st) {
+                           int B, int H, int Sq, int Sk, int mode, float scale_log2, u op, long op_ps, u st) {
     AttnF32Args a{};
     a.q = (const float*)q; a.k = (const float*)k; a.v = (const float*)v;
     a.q_sb = qs[0].cast<long>(); a.q_ss = qs[1].cast<long>(); a.q_sh = qs[2].cast<long>();
@@ -193,12 +198,15 @@ PYBIND11_MODULE(_C, m) {
     a.o = (float*)o; a.o_sb = os[0].cast<long>(); a.o_ss = os[1].cast<long>(); a.o_sh = os[2].cast<long>();
     a.lse = (float*)lse; a.kpad = (const unsigned char*)kpad;
     a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk; a.mode = mode; a.scale_log2 = scale_log2;
+    a.op = (unsigned short*)op; a.op_ps = op_ps;
     chk(smi_attn_f32_fwd(&a, S(st)), "attn_f32_fwd");
   });
   m.def("attn_f32_bwd", [](u q, u k, u v, py::tuple qs, py::tuple ks, py::tuple vs, u o, u dout, py::tuple os, u lse,
                            u delta, u dq, u dk, u dv, u kpad, int B, int H, int Sq, int Sk, int mode, float scale_log2,
-                           float scale, u st) {
+                           float scale, u dqp, u dkp, u dvp, long dq_ps, long dkv_ps, u st) {
     AttnF32Args a{};
+    a.dqp = (unsigned short*)dqp; a.dkp = (unsigned short*)dkp; a.dvp = (unsigned short*)dvp;
+    a.dq_ps = dq_ps; a.dkv_ps = dkv_ps;
     a.q = (const float*)q; a.k = (const float*)k; a.v = (const float*)v;
     a.q_sb = qs[0].cast<long>(); a.q_ss = qs[1].cast<long>(); a.q_sh = qs[2].cast<long>();
     a.k_sb = ks[0].cast<long>(); a.k_ss = ks[1].cast<long>(); a.k_sh = ks[2].cast<long>();

@@ -34,4 +34,8 @@ struct AttnF32Args {
   const unsigned char* kpad;         // [B,Sk] or null
   int B, H, Sq, Sk, mode;
   float scale_log2, scale;           // log2(e)/sqrt(hd), 1/sqrt(hd)
+  // optional bf16 hi/mid/lo planes of the outputs for the split-plane GEMMs that consume them
+  // (sparkmi/ops/planes.py): same element offsets as O / dQ / dK,dV, planes op_ps / dq_ps / dkv_ps apart
+  unsigned short* op; unsigned short* dqp; unsigned short* dkp; unsigned short* dvp;
+  long op_ps, dq_ps, dkv_ps;
 };

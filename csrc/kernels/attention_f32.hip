@@ -1,6 +1,9 @@
 // Fused scaled-dot-product attention at the REFERENCE precision: fp32 Q/K/V/O, fp32 scores,
-// softmax and accumulation, on the fp32-input matrix cores (v_mfma_f32_32x32x2_f32, exact f32
-// products).  head_dim = 64.  Forward + dQ + dK/dV, no S x S tensor in HBM.
+// softmax and accumulation, exact fp32 products.  Products run on the bf16 matrix cores through
+// the exact 3-way bf16 split (XS = 1, smi_split3.h: six v_mfma_f32_32x32x16_bf16 slice products
+// per fp32 product; the owned rows are split once) — the default — or on the fp32-input matrix
+// cores (XS = 0, v_mfma_f32_32x32x2_f32; smi_gemm_f32_algo(0)).  head_dim = 64.  Forward + dQ +
+// dK/dV, no S x S tensor in HBM; outputs optionally also as split planes for the next GEMM.
 //
 // Reference semantics: transformer.py:12-25 (scaled_dot_product) as called by MultiHeadAttention
 // (:74-83) and MultiHeadCrossAttention (:177-191), run in fp32 by pytorch_machine_translator.py
@@ -84,6 +87,21 @@ __device__ __forceinline__ void fa_store_rowT(float* __restrict__ dst, const f32
 #pragma unroll
   for (int g = 0; g < 4; ++g)
     *(float4*)(dst + 8 * g + 4 * h) = make_float4(a[4 * g] * sc, a[4 * g + 1] * sc, a[4 * g + 2] * sc, a[4 * g + 3] * sc);
+}
+// the same tile as split planes (P: plane-0 element matching dst, planes ps apart)
+__device__ __forceinline__ void fa_store_rowT_planes(unsigned short* __restrict__ P, long ps, const f32x16_t& a, int lane,
+                                                     float sc) {
+  const int h = lane >> 5;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    uint32_t h0, m0, l0, h1, m1, l1;
+    split3_pair(a[4 * g] * sc, a[4 * g + 1] * sc, h0, m0, l0);
+    split3_pair(a[4 * g + 2] * sc, a[4 * g + 3] * sc, h1, m1, l1);
+    unsigned short* q = P + 8 * g + 4 * h;
+    *(uint2*)q = make_uint2(h0, h1);
+    *(uint2*)(q + ps) = make_uint2(m0, m1);
+    *(uint2*)(q + 2 * ps) = make_uint2(l0, l1);
+  }
 }
 __device__ __forceinline__ int fa_kl(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
@@ -187,6 +205,10 @@ __global__ __launch_bounds__(256, 2) void attn_f32_fwd_kernel(AttnF32Args a) {
     const float inv = l > 0.f ? 1.0f / l : 0.f;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) fa_store_rowT(O + dt * 32, o[dt], lane, inv);
+    if (a.op) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) fa_store_rowT_planes(a.op + (O - a.o) + dt * 32, a.op_ps, o[dt], lane, inv);
+    }
     if (h == 0) {
       const float mref = (m == -INFINITY) ? 0.f : m;
       a.lse[((long)b * a.H + hh) * a.Sq + qi] = l > 0.f ? mref + log2f(l) : INFINITY;
@@ -295,6 +317,10 @@ __global__ __launch_bounds__(256, XS ? 1 : 2) void attn_f32_dq_kernel(AttnF32Arg
     float* dQ = a.dq + b * a.q_sb + hh * a.q_sh + (long)qi * a.q_ss;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) fa_store_rowT(dQ + dt * 32, acc[dt], lane, a.scale);
+    if (a.dqp) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) fa_store_rowT_planes(a.dqp + (dQ - a.dq) + dt * 32, a.dq_ps, acc[dt], lane, a.scale);
+    }
   }
 }
 
@@ -417,6 +443,13 @@ __global__ __launch_bounds__(256, XS ? 1 : 2) void attn_f32_dkdv_kernel(AttnF32A
       fa_store_rowT(dK + dt * 32, dk[dt], lane, a.scale);
       fa_store_rowT(dV + dt * 32, dv[dt], lane, 1.0f);
     }
+    if (a.dkp) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        fa_store_rowT_planes(a.dkp + (dK - a.dk) + dt * 32, a.dkv_ps, dk[dt], lane, a.scale);
+        fa_store_rowT_planes(a.dvp + (dV - a.dv) + dt * 32, a.dkv_ps, dv[dt], lane, 1.0f);
+      }
+    }
   }
 }
 
@@ -446,6 +479,9 @@ static int fa_ok(const AttnF32Args& a) {
   for (long s : st)
     if (s % 4) return 0;
   if ((((uintptr_t)a.q) | ((uintptr_t)a.k) | ((uintptr_t)a.v) | ((uintptr_t)a.o)) & 15) return 0;
+  // plane outputs: 8-B stores of 4 consecutive head-dim values
+  if ((((uintptr_t)a.op) | ((uintptr_t)a.dqp) | ((uintptr_t)a.dkp) | ((uintptr_t)a.dvp)) & 7) return 0;
+  if ((a.dkp != nullptr) != (a.dvp != nullptr)) return 0;
   return a.B > 0 && a.H > 0 && a.Sq > 0 && a.Sk > 0;
 }
 

@@ -17,12 +17,14 @@ static int g_sp_tm = 0;
 int smi_sp_tm() {
   if (g_sp_tm == 0) {
     const char* e = getenv("SMI_SP_TM");
-    g_sp_tm = (e && atoi(e) == 128) ? 128 : 256;
+    const int v = e ? atoi(e) : 0;
+    g_sp_tm = (v == 128 || v == 4) ? v : 256;
   }
   return g_sp_tm;
 }
-extern "C" int smi_gemm_sp_tm(int set) {  // set 128 / 256 (A/B runs in one process); other values query
-  if (set == 128 || set == 256) g_sp_tm = set;
+// set 128 / 256 / 4 (256 x 128 tiles on 4 pipelined waves) for A/B runs in one process; other values query
+extern "C" int smi_gemm_sp_tm(int set) {
+  if (set == 128 || set == 256 || set == 4) g_sp_tm = set;
   return smi_sp_tm();
 }
 extern "C" int smi_gemm_sp_waves(int set) {  // set 4 / 8 (A/B runs in one process); other values query
@@ -91,7 +93,8 @@ extern "C" int smi_gemm_sp(const GemmSpArgs* args, hipStream_t st) {
   if (g.relu > 1 || !g.C) return -1;
 #define SPF(E, O)                                                                                   \
   do {                                                                                              \
-    if (t256) hipLaunchKernelGGL((gemm_sp256_kernel<false, false, E, O>), grid, dim3(512), 0, st, g); \
+    if (t256 && smi_sp_tm() == 4) hipLaunchKernelGGL((gemm_sp4w_kernel<false, false, E, O>), grid, dim3(256), 0, st, g); \
+    else if (t256) hipLaunchKernelGGL((gemm_sp256_kernel<false, false, E, O>), grid, dim3(512), 0, st, g); \
     else if (w8) hipLaunchKernelGGL((gemm_sp_kernel<8, false, false, E, O>), grid, dim3(512), 0, st, g); \
     else hipLaunchKernelGGL((gemm_sp_kernel<4, false, false, E, O>), grid, dim3(256), 0, st, g);    \
   } while (0)

@@ -7,6 +7,18 @@
 // Statistics are fp32; the pre-norm sum is saved in the activation dtype for the backward. dgamma/dbeta are reduced per block into fp32 partial slabs and summed
 // by a second kernel that accumulates into the caller's (flat) fp32 gradient buffer.
 #include "smi_common.h"
+#include "smi_split3.h"
+
+// fp32 path: the output's bf16 hi/mid/lo planes ([3][M][D], plane stride pps) for the split-plane
+// GEMM that consumes it (sparkmi/ops/planes.py), written beside the fp32 store
+__device__ __forceinline__ void ln_store_planes(unsigned short* P, long pps, const float (&v)[8]) {
+  uint32_t h[4], m[4], l[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) split3_pair(v[2 * e], v[2 * e + 1], h[e], m[e], l[e]);
+  *(uint4*)P = make_uint4(h[0], h[1], h[2], h[3]);
+  *(uint4*)(P + pps) = make_uint4(m[0], m[1], m[2], m[3]);
+  *(uint4*)(P + 2 * pps) = make_uint4(l[0], l[1], l[2], l[3]);
+}
 
 // Every global load a row needs (h, r, gamma, beta; the dropout seed) is issued before the
 // first reduction: a load that depends on a reduction result serialises two memory latencies
@@ -18,7 +30,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
     const float* __restrict__ gamma, const float* __restrict__ beta,
     T* __restrict__ y, T* __restrict__ xsave,
     float* __restrict__ mean_out, float* __restrict__ rstd_out,
-    int M, int D, float eps, const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale) {
+    int M, int D, float eps, const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale,
+    unsigned short* __restrict__ yp, long pps) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (row >= M) return;
@@ -71,6 +84,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) out[j] = (x[v][j] - mean) * rstd * gg[j] + bb[j];
     V8<T>::store(y + base + col, out);
+    if (yp) ln_store_planes(yp + base + col, pps, out);
     if (xsave) V8<T>::store(xsave + base + col, x[v]);
   }
   if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
@@ -87,7 +101,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     T* __restrict__ dres, T* __restrict__ dh,
     const T* __restrict__ dres_add,
     float* __restrict__ part_g, float* __restrict__ part_b,
-    int M, int D, const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale) {
+    int M, int D, const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale,
+    unsigned short* __restrict__ dhp, long pps) {
   const float invD = 1.0f / (float)D;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -166,6 +181,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       }
       if (dres) V8<T>::store(dres + base + col, o1);
       if (dh) V8<T>::store(dh + base + col, o2);
+      if (dhp) ln_store_planes(dhp + base + col, pps, o2);
     }
   }
   __shared__ float red[2][4][VPL * 512];
@@ -215,28 +231,34 @@ __global__ __launch_bounds__(256) void colsum2_kernel(const float* __restrict__ 
 template <typename T>
 static int ln_fwd_launch(const void* h, const void* r, const float* gamma, const float* beta, void* y, void* xsave,
                          float* mean, float* rstd, int M, int D, float eps, const uint32_t* seedp, uint32_t salt,
-                         uint32_t thresh, float dscale, hipStream_t st) {
+                         uint32_t thresh, float dscale, void* planes, long pps, hipStream_t st) {
   dim3 grid((M + 3) / 4), block(256);
+  unsigned short* yp = (unsigned short*)planes;
   const T* hh = (const T*)h; const T* rr = (const T*)r;
   T* yy = (T*)y; T* xx = (T*)xsave;
   if (D % 8 || D > 4096) return -1;
   const int vpl = (D + 511) / 512;
-  if (vpl == 1) hipLaunchKernelGGL((ln_fwd_kernel<1, T>), grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale);
-  else if (vpl == 2) hipLaunchKernelGGL((ln_fwd_kernel<2, T>), grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale);
-  else if (vpl <= 4) hipLaunchKernelGGL((ln_fwd_kernel<4, T>), grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale);
-  else hipLaunchKernelGGL((ln_fwd_kernel<8, T>), grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale);
+  if (vpl == 1) hipLaunchKernelGGL((ln_fwd_kernel<1, T>), grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale, yp, pps);
+  else if (vpl == 2) hipLaunchKernelGGL((ln_fwd_kernel<2, T>), grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale, yp, pps);
+  else if (vpl <= 4) hipLaunchKernelGGL((ln_fwd_kernel<4, T>), grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale, yp, pps);
+  else hipLaunchKernelGGL((ln_fwd_kernel<8, T>), grid, block, 0, st, hh, rr, gamma, beta, yy, xx, mean, rstd, M, D, eps, seedp, salt, thresh, dscale, yp, pps);
   SMI_CHECK_LAUNCH();
 }
 
 extern "C" int smi_ln_fwd(const void* h, const void* r, const float* gamma, const float* beta, void* y,
                           void* xsave, float* mean, float* rstd, int M, int D, float eps,
                           const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, hipStream_t st) {
-  return ln_fwd_launch<unsigned short>(h, r, gamma, beta, y, xsave, mean, rstd, M, D, eps, seedp, salt, thresh, dscale, st);
+  return ln_fwd_launch<unsigned short>(h, r, gamma, beta, y, xsave, mean, rstd, M, D, eps, seedp, salt, thresh, dscale,
+                                       nullptr, 0, st);
 }
 extern "C" int smi_ln_fwd_f32(const void* h, const void* r, const float* gamma, const float* beta, void* y,
                               void* xsave, float* mean, float* rstd, int M, int D, float eps,
-                              const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, hipStream_t st) {
-  return ln_fwd_launch<float>(h, r, gamma, beta, y, xsave, mean, rstd, M, D, eps, seedp, salt, thresh, dscale, st);
+                              const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, void* planes,
+                              long pps, hipStream_t st) {
+  // planes: [3][M][D] bf16 of y (or null); D % 8 == 0 keeps every 16-B plane store aligned
+  if (planes && (((uintptr_t)planes & 15) || pps < (long)M * D)) return -1;
+  return ln_fwd_launch<float>(h, r, gamma, beta, y, xsave, mean, rstd, M, D, eps, seedp, salt, thresh, dscale, planes,
+                              pps, st);
 }
 
 template <typename T>
@@ -244,7 +266,8 @@ static int ln_bwd_launch(const void* dy, const void* xs, const float* mean, cons
                          const float* gamma, void* dres, void* dh, const void* dres_add,
                          float* part_g, float* part_b, int nblocks, float* dgamma, float* dbeta,
                          int accumulate, int M, int D, const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale,
-                         hipStream_t st) {
+                         void* planes, long pps, hipStream_t st) {
+  unsigned short* dhp = (unsigned short*)planes;
   // nblocks = capacity (rows) of the partial slabs; the kernel needs ceil(M / (4 * RPW)) of them
   const T* a = (const T*)dy; const T* b = (const T*)xs;
   T* o1 = (T*)dres; T* o2 = (T*)dh;
@@ -255,9 +278,9 @@ static int ln_bwd_launch(const void* dy, const void* xs, const float* mean, cons
   const int nb = (M + 4 * rpw - 1) / (4 * rpw);
   if (nb > nblocks) return -1;
   dim3 grid(nb), block(256);
-  if (vpl == 1) hipLaunchKernelGGL((ln_bwd_kernel<1, 2, T>), grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, D, seedp, salt, thresh, dscale);
-  else if (vpl == 2) hipLaunchKernelGGL((ln_bwd_kernel<2, 2, T>), grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, D, seedp, salt, thresh, dscale);
-  else hipLaunchKernelGGL((ln_bwd_kernel<4, 1, T>), grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, D, seedp, salt, thresh, dscale);
+  if (vpl == 1) hipLaunchKernelGGL((ln_bwd_kernel<1, 2, T>), grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, D, seedp, salt, thresh, dscale, dhp, pps);
+  else if (vpl == 2) hipLaunchKernelGGL((ln_bwd_kernel<2, 2, T>), grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, D, seedp, salt, thresh, dscale, dhp, pps);
+  else hipLaunchKernelGGL((ln_bwd_kernel<4, 1, T>), grid, block, 0, st, a, b, mean, rstd, gamma, o1, o2, ad, part_g, part_b, M, D, seedp, salt, thresh, dscale, dhp, pps);
   if (dgamma) {  // else the caller reduces the partials itself (smi_ln_bwd_reduce, e.g. on a side stream)
     const int groups = accumulate ? (nb >= 1024 ? 16 : (nb >= 256 ? 8 : (nb >= 64 ? 4 : 1))) : 1;
     hipLaunchKernelGGL(colsum2_kernel, dim3((D + 63) / 64, groups), dim3(256), 0, st, part_g, part_b, nb, D, dgamma, dbeta,
@@ -272,15 +295,17 @@ extern "C" int smi_ln_bwd(const void* dy, const void* xs, const float* mean, con
                           int accumulate, int M, int D, const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale,
                           hipStream_t st) {
   return ln_bwd_launch<unsigned short>(dy, xs, mean, rstd, gamma, dres, dh, dres_add, part_g, part_b, nblocks, dgamma,
-                                       dbeta, accumulate, M, D, seedp, salt, thresh, dscale, st);
+                                       dbeta, accumulate, M, D, seedp, salt, thresh, dscale, nullptr, 0, st);
 }
 extern "C" int smi_ln_bwd_f32(const void* dy, const void* xs, const float* mean, const float* rstd,
                               const float* gamma, void* dres, void* dh, const void* dres_add,
                               float* part_g, float* part_b, int nblocks, float* dgamma, float* dbeta,
                               int accumulate, int M, int D, const uint32_t* seedp, uint32_t salt, uint32_t thresh,
-                              float dscale, hipStream_t st) {
+                              float dscale, void* planes, long pps, hipStream_t st) {
+  // planes: [3][M][D] bf16 of dh (or null)
+  if (planes && (((uintptr_t)planes & 15) || pps < (long)M * D || !dh)) return -1;
   return ln_bwd_launch<float>(dy, xs, mean, rstd, gamma, dres, dh, dres_add, part_g, part_b, nblocks, dgamma, dbeta,
-                              accumulate, M, D, seedp, salt, thresh, dscale, st);
+                              accumulate, M, D, seedp, salt, thresh, dscale, planes, pps, st);
 }
 
 // dgamma/dbeta (+)= column sums of the nb partial rows written by smi_ln_bwd

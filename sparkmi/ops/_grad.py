@@ -122,18 +122,31 @@ class SharedGrad:
     None to autograd): the producer's backward then reads the whole gradient at once, e.g. one
     dgrad GEMM over the six decoder kv projections (ops.linear.concat_linear)."""
 
-    __slots__ = ("buf",)
+    __slots__ = ("buf", "planes")
 
     def __init__(self):
         self.buf = None
+        self.planes = None
 
     def get(self, like: torch.Tensor) -> torch.Tensor:
         if self.buf is None:
             self.buf = torch.empty_like(like)
         return self.buf
 
+    def get_planes(self, buf: torch.Tensor) -> torch.Tensor:
+        """bf16 split planes [3, rows, W] of the buffer (fp32 path), filled by the same writers;
+        attached to the buffer on take() for the producer's split-plane GEMMs."""
+        if self.planes is None:
+            W = buf.shape[-1]
+            self.planes = torch.empty(3, buf.numel() // W, W, device=buf.device, dtype=torch.bfloat16)
+        return self.planes
+
     def take(self):
         b, self.buf = self.buf, None
+        p, self.planes = self.planes, None
+        if b is not None and p is not None:
+            from . import planes as _pl
+            _pl.attach(b, p)
         return b
 
 

@@ -22,6 +22,7 @@ import math
 import torch
 
 from .. import _native
+from . import planes as _pl
 
 MODES = {"none": 0, None: 0, "reference": 1, "causal": 2}
 _LOG2E = 1.4426950408889634
@@ -74,6 +75,16 @@ def _merge(o):
     return o.permute(0, 2, 1, 3).reshape(B, S, H * hd)
 
 
+def _planes_like(t):
+    """Planes [3, rows, W] for an fp32 [.., W] attention output / gradient (None: planes off or W
+    not a multiple of 32, the split-plane GEMM's k granularity)."""
+    from . import gemm as G
+    W = t.shape[-1]
+    if t.dtype != torch.float32 or not G.SP or W % 32 or not t.is_contiguous():
+        return None
+    return torch.empty(3, t.numel() // W, W, device=t.device, dtype=torch.bfloat16)
+
+
 class _AttnCore(torch.autograd.Function):
     """Shared autograd core.  ``views`` describe (base tensor, offset, (sb, ss, sh)) for q/k/v."""
 
@@ -123,9 +134,16 @@ class _AttnCore(torch.autograd.Function):
         lse = torch.empty(B, H, Sq, device=qsrc.device, dtype=torch.float32)
         os_ = (Sq * H * hd, H * hd, hd)
         kpad = key_padding.to(torch.uint8).contiguous() if key_padding is not None else None
-        fwd = C.attn_f32_fwd if f32 else C.attn_fwd
-        fwd(qp, kp, vp, qs, ks, vs, o.data_ptr(), os_, lse.data_ptr(), _native.ptr(kpad), B, H, Sq, Sk, mode,
-            _LOG2E / math.sqrt(hd), _native.stream())
+        if f32:
+            opl = _planes_like(o)  # the out-projection's operand, written by the same epilogue
+            C.attn_f32_fwd(qp, kp, vp, qs, ks, vs, o.data_ptr(), os_, lse.data_ptr(), _native.ptr(kpad), B, H, Sq, Sk,
+                           mode, _LOG2E / math.sqrt(hd), _native.ptr(opl), opl.stride(0) if opl is not None else 0,
+                           _native.stream())
+            if opl is not None:
+                _pl.attach(o, opl)
+        else:
+            C.attn_fwd(qp, kp, vp, qs, ks, vs, o.data_ptr(), os_, lse.data_ptr(), _native.ptr(kpad), B, H, Sq, Sk, mode,
+                       _LOG2E / math.sqrt(hd), _native.stream())
         ctx.geom = (B, Sq, Sk, hd, qs, ks, vs, os_)
         ctx.kpad = kpad
         ctx.save_for_backward(qsrc, kvsrc if cross else None, o, lse)
@@ -153,6 +171,11 @@ class _AttnCore(torch.autograd.Function):
             do = do.to(o.dtype)
         es = qsrc.element_size()
         delta = torch.empty(B, H, Sq, device=do.device, dtype=torch.float32)
+        f32 = qsrc.dtype == torch.float32
+        # split planes of the gradients (fp32): the dY operands of the projections' dgrad / wgrad
+        # GEMMs, at the same element offsets as the fp32 gradients (2 B per element per plane)
+        pq = pk = pv = 0
+        q_ps = kv_ps = 0
         if ctx.cross:
             dq = torch.empty_like(qsrc)
             dkv = ctx.shared.get(kvsrc) if ctx.shared is not None else torch.empty_like(kvsrc)
@@ -160,16 +183,36 @@ class _AttnCore(torch.autograd.Function):
             vp = kp + hd * es
             dqp, dkp = dq.data_ptr(), dkv.data_ptr() + ctx.kv_col * es
             dvp = dkp + hd * es
+            if f32:
+                qpl = _planes_like(dq)
+                kvpl = (ctx.shared.get_planes(dkv) if ctx.shared is not None else _planes_like(dkv))
+                if qpl is not None and kvpl is not None:
+                    _pl.attach(dq, qpl)
+                    if ctx.shared is None:
+                        _pl.attach(dkv, kvpl)
+                    pq, q_ps = qpl.data_ptr(), qpl.stride(0)
+                    pk, kv_ps = kvpl.data_ptr() + ctx.kv_col * 2, kvpl.stride(0)
+                    pv = pk + hd * 2
         else:
             dqkv = torch.empty_like(qsrc)
             qp = qsrc.data_ptr()
             kp, vp = qp + hd * es, qp + 2 * hd * es
             dqp = dqkv.data_ptr()
             dkp, dvp = dqp + hd * es, dqp + 2 * hd * es
-        bwd = C.attn_f32_bwd if qsrc.dtype == torch.float32 else C.attn_bwd
-        bwd(qp, kp, vp, qs, ks, vs, o.data_ptr(), do.data_ptr(), os_, lse.data_ptr(), delta.data_ptr(), dqp,
-            dkp, dvp, _native.ptr(ctx.kpad), B, H, Sq, Sk, ctx.mode, _LOG2E / math.sqrt(hd),
-            1.0 / math.sqrt(hd), _native.stream())
+            if f32:
+                pl = _planes_like(dqkv)
+                if pl is not None:
+                    _pl.attach(dqkv, pl)
+                    pq, q_ps = pl.data_ptr(), pl.stride(0)
+                    pk, pv, kv_ps = pq + hd * 2, pq + 2 * hd * 2, q_ps
+        if f32:
+            C.attn_f32_bwd(qp, kp, vp, qs, ks, vs, o.data_ptr(), do.data_ptr(), os_, lse.data_ptr(), delta.data_ptr(),
+                           dqp, dkp, dvp, _native.ptr(ctx.kpad), B, H, Sq, Sk, ctx.mode, _LOG2E / math.sqrt(hd),
+                           1.0 / math.sqrt(hd), pq, pk, pv, q_ps, kv_ps, _native.stream())
+        else:
+            C.attn_bwd(qp, kp, vp, qs, ks, vs, o.data_ptr(), do.data_ptr(), os_, lse.data_ptr(), delta.data_ptr(), dqp,
+                       dkp, dvp, _native.ptr(ctx.kpad), B, H, Sq, Sk, ctx.mode, _LOG2E / math.sqrt(hd),
+                       1.0 / math.sqrt(hd), _native.stream())
         if ctx.cross:
             # a shared kv gradient is read by its producer (ops.linear.ConcatLinearFn)
             return dq, (None if ctx.shared is not None else dkv), None, None, None, None, None, None

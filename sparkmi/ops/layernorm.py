@@ -11,7 +11,17 @@ import torch
 from .. import _native
 from . import rng as _rng
 from . import _grad
+from . import planes as _pl
 from ._grad import grad_buf, grad_ready
+
+
+def _planes_for(t, D, M):
+    """bf16 hi/mid/lo planes [3, M, D] for an fp32 output the split-plane GEMM will consume
+    (sparkmi/ops/planes.py), or None (bf16 path, planes disabled, or a width the GEMM pads)."""
+    from . import gemm as G
+    if t.dtype != torch.float32 or not G.SP or D % 32:
+        return None
+    return torch.empty(3, M, D, device=t.device, dtype=torch.bfloat16)
 
 
 
@@ -46,10 +56,15 @@ class AddDropoutLayerNorm(torch.autograd.Function):
             rstd = torch.empty(M, device=h.device, dtype=torch.float32)
             if r is not None and r.dtype != h.dtype:
                 raise TypeError(f"layernorm: residual dtype {r.dtype} != input dtype {h.dtype}")
-            fwd = C.ln_fwd_f32 if h.dtype == torch.float32 else C.ln_fwd
-            fwd(h.data_ptr(), _native.ptr(r), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(), xs.data_ptr(),
-                     mean.data_ptr(), rstd.data_ptr(), M, D, eps, rng.ptr(), salt, _rng.threshold(p), _rng.scale(p),
-                     _native.stream())
+            args = (h.data_ptr(), _native.ptr(r), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(), xs.data_ptr(),
+                    mean.data_ptr(), rstd.data_ptr(), M, D, eps, rng.ptr(), salt, _rng.threshold(p), _rng.scale(p))
+            if h.dtype == torch.float32:
+                yp = _planes_for(y, D, M)  # the next Linear's operand, written beside y
+                C.ln_fwd_f32(*args, _native.ptr(yp), yp.stride(0) if yp is not None else 0, _native.stream())
+                if yp is not None:
+                    _pl.attach(y, yp)
+            else:
+                C.ln_fwd(*args, _native.stream())
             ctx.native = True
         else:
             seed = rng.current()
@@ -74,10 +89,16 @@ class AddDropoutLayerNorm(torch.autograd.Function):
             rows_per_block = 4 * (2 if vpl <= 2 else 1)  # ln_bwd_kernel<VPL, RPW>
             nb = (M + rows_per_block - 1) // rows_per_block
             part = torch.empty(2, nb, D, device=dy.device, dtype=torch.float32)
-            bwd = C.ln_bwd_f32 if dy.dtype == torch.float32 else C.ln_bwd
-            bwd(dy.data_ptr(), xs.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(),
-                     _native.ptr(dres), dh.data_ptr(), 0, part[0].data_ptr(), part[1].data_ptr(), nb,
-                     0, 0, 1, M, D, ctx.rng.ptr(), ctx.salt, _rng.threshold(p), _rng.scale(p), _native.stream())
+            args = (dy.data_ptr(), xs.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(),
+                    _native.ptr(dres), dh.data_ptr(), 0, part[0].data_ptr(), part[1].data_ptr(), nb,
+                    0, 0, 1, M, D, ctx.rng.ptr(), ctx.salt, _rng.threshold(p), _rng.scale(p))
+            if dy.dtype == torch.float32:
+                dhp = _planes_for(dh, D, M)  # dY operand of the sublayer's last Linear (dgrad + wgrad)
+                C.ln_bwd_f32(*args, _native.ptr(dhp), dhp.stride(0) if dhp is not None else 0, _native.stream())
+                if dhp is not None:
+                    _pl.attach(dh, dhp)
+            else:
+                C.ln_bwd(*args, _native.stream())
             if _grad.LN_DEFER:  # folded with every other LayerNorm's at the end of the backward
                 _grad.defer_ln_fold(part[0], part[1], nb, D, gg, gb, (gamma, beta), _native.stream())
             else:

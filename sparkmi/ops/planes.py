@@ -31,6 +31,12 @@ def attach(t, planes):
 
 def cached(t, kpad=False):
     e = getattr(t, "_smi_planes", None)
+    if e is None:
+        # a reshape view of a tensor the producer split (shares its storage and version counter)
+        b = t._base
+        if b is not None and b.data_ptr() == t.data_ptr() and b.numel() == t.numel() and b.is_contiguous() \
+                and t.is_contiguous():
+            e = getattr(b, "_smi_planes", None)
     if e is None or e[1] != t._version:
         return None
     p = e[0]

@@ -17,6 +17,18 @@ def _sum3(P, cols):
     return (P[0].float() + P[1].float() + P[2].float())[:, :cols]
 
 
+@pytest.fixture(params=[256, 4, 128], ids=["tile256w8", "tile256w4", "tile128"])
+def tile(request):
+    """Every tile form of the plane GEMM (C.gemm_sp_tm: 8-wave 256 x 128, 4-wave pipelined 256 x 128,
+    8-wave 128 x 128)."""
+    from sparkmi import _native
+    C = _native.C()
+    prev = C.gemm_sp_tm(0)
+    C.gemm_sp_tm(request.param)
+    yield request.param
+    C.gemm_sp_tm(prev)
+
+
 @pytest.fixture
 def algo():
     from sparkmi import _native
@@ -42,7 +54,7 @@ def test_split3_exact():
 
 @pytest.mark.parametrize("M,N,K", [(1024, 512, 512), (8192, 1536, 512), (300, 264, 160), (4096, 10000, 512),
                                    (512, 1024, 1024)])
-def test_sp_matches_f32_precision(algo, M, N, K):
+def test_sp_matches_f32_precision(algo, tile, M, N, K):
     from sparkmi.ops import gemm as G
     from sparkmi.ops import planes
     torch.manual_seed(3)
@@ -74,7 +86,7 @@ def test_sp_matches_f32_precision(algo, M, N, K):
         assert torch.equal(_sum3(yp, N), y)
 
 
-def test_sp_dgrad_dact_planes_and_dropout():
+def test_sp_dgrad_dact_planes_and_dropout(tile):
     """FFN pattern: h = dropout(relu(x W1^T + b1)) with planes out; dh = (dy W2) * [h > 0] * s
     written as planes only (no fp32 copy)."""
     from sparkmi.ops import gemm as G
@@ -104,7 +116,7 @@ def test_sp_dgrad_dact_planes_and_dropout():
     assert _err(_sum3(dhp, F), ref) < 1e-6
 
 
-def test_sp_wgrad_group():
+def test_sp_wgrad_group(tile):
     from sparkmi import _native
     from sparkmi.ops import planes
     torch.manual_seed(2)
