@@ -27,6 +27,7 @@ elapsed over ranks is used; rank 0 prints one JSON line.  ``value`` = whole-job 
 N * batch * K / max_elapsed (weak scaling).
 """
 import argparse
+import math
 import json
 import os
 import subprocess
@@ -69,6 +70,9 @@ def parse(argv=None):
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--split", type=int, default=1, help="multi-graph backward with overlapped all-reduce (DP)")
     ap.add_argument("--no-aux", action="store_true", help="skip the LSTM / MLP extras")
+    ap.add_argument("--data", default="random", choices=["random", "copy"],
+                    help="transformer batches: random = independent uniform src/tgt (Multi30k-shaped; loss floor "
+                         "ln(V-4)), copy = tgt a fixed permutation of src (learnable, same shapes)")
     ap.add_argument("--no-f32-compare", action="store_true",
                     help="skip the f32-MFMA comparison run of the fp32 transformer step")
     return ap.parse_args(argv)
@@ -287,7 +291,7 @@ def bench_transformer(args, rank, world, device, dtype):
     """One full training step of the BASELINE transformer at ``dtype`` ('fp32' = reference
     precision, or 'bf16' = bf16 activations/weights with fp32 master weights and fp32 accumulate)."""
     import torch
-    from sparkmi.data.synthetic import translation_pairs
+    from sparkmi.data.synthetic import copy_pairs, translation_pairs
     from sparkmi.models.transformer import Transformer
     from sparkmi.optim import Adam
     from sparkmi.parallel.ddp import DataParallel
@@ -308,7 +312,11 @@ def bench_transformer(args, rank, world, device, dtype):
     runner = StepRunner(model, lambda m, s, t: m.training_step_loss(s, t), opt, ddp, graph=use_graph,
                         split_fn=split_fn)
     pool = 8
-    src, tgt = translation_pairs(pool * args.batch, args.seq, args.vocab, args.vocab, seed=100 + rank, device=device)
+    if args.data == "copy":
+        src, tgt = copy_pairs(pool * args.batch, args.seq, args.vocab, seed=100 + rank, device=device)
+    else:
+        src, tgt = translation_pairs(pool * args.batch, args.seq, args.vocab, args.vocab, seed=100 + rank,
+                                     device=device)
     src = src.view(pool, args.batch, args.seq)
     tgt = tgt.view(pool, args.batch, args.seq)
     batches = [(src[i], tgt[i]) for i in range(pool)]
@@ -323,6 +331,8 @@ def bench_transformer(args, rank, world, device, dtype):
     peak = 157.3 if dtype == "fp32" else 2500.0
     res = {"samples_per_s": round(value, 2), "ms_per_step": round(elapsed / args.steps * 1000, 3),
            "final_loss": round(final_loss, 4), "losses": [round(float(l), 4) for l in losses],
+           # random data: src / tgt independent and uniform over V - 4 content tokens -> no model beats ln(V - 4)
+           "loss_floor": round(math.log(args.vocab - 4), 4) if args.data == "random" else 0.0, "data": args.data,
            "model_tflops_per_gpu": round(tflops, 1),
            f"mfu_vs_{'157tf_fp32' if dtype == 'fp32' else '2.5pf_bf16'}_dense": round(tflops / peak, 3),
            "allreduce_ms": ar, "grad_bytes": flat.numel * 4, "dtype": dtype,

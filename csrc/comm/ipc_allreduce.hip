@@ -1,40 +1,81 @@
-// One-shot all-reduce over IPC-mapped device memory for latency-bound gradient buckets
-// (SURVEY §5.8 item 3): the MLP's 256-B and the CNN's 31-KB gradients
-// (distributed_multilayer_perceptron.py:103-106, distributed_cnn.py:152-156) cannot absorb a
-// ring protocol's per-hop latency; here every rank reads every peer's bucket directly over xGMI
-// (7 point-to-point links: all peers at once, one hop) and reduces locally.
+// All-reduce over IPC-mapped device memory, one node: every rank reads its
+// peers' staging regions directly over xGMI (7 point-to-point links: all peers at once, one hop)
+// instead of a ring's 2 (w - 1) latency-bound hops.
+//  * ONE-SHOT (latency-bound buckets: the MLP's 256 B, the CNN's 31 KB gradients,
+//    distributed_multilayer_perceptron.py:103-106, distributed_cnn.py:152-156): every rank reads
+//    every peer's whole bucket and sums it — (w - 1) n floats over xGMI per rank, one signal round.
+//  * TWO-SHOT (31 KB .. tens of MB, e.g. the LSTM's 12.3 MB dense embedding gradient): reduce-
+//    scatter then all-gather — rank r sums chunk r of every peer's bucket (reading its 1/w slice
+//    from all peers at once), publishes the sum in place, then every rank gathers the w reduced
+//    chunks: 2 (w - 1) / w n floats per rank, two signal rounds.
 //
-// Protocol (one launch per all-reduce, stream-ordered on every rank).  The epoch lives in device
-// memory (*ep, advanced by the launch's last block, like the optimizers' step counter), so the
-// launch can be captured in a HIP graph and replayed — a small model's whole data-parallel step
-// (forward, backward, this all-reduce, optimizer) is then ONE graph replay.
-//  1. block b copies its chunk of the local bucket into this rank's staging region, half
-//     (epoch & 1) — double-buffered so a fast rank's next call never overwrites data a slow
-//     peer is still reading (a rank can only reach epoch+2 after every peer signalled epoch+1,
-//     i.e. finished reading epoch);
-//  2. every storing wave drains its stores (vmcnt(0)), the block barriers, and thread r stores
-//     `epoch` into rank r's signal slot [b][my rank] with a system-scope release;
-//  3. thread r polls this rank's signal slot [b][r] (system-scope acquire loads, s_sleep
-//     back-off, BOUNDED: after `spins` polls (~4 s by default) it records a timeout in *err and
-//     gives up, so a dead peer can never hang the GPU);
-//  4. block b sums chunk b of all ranks' staging regions in rank order 0..world-1 — every rank
-//     computes bit-identical results — and writes it back to the local bucket.  If any peer
-//     timed out, the block writes NaN instead: a lost peer never turns into a finite, silently
-//     wrong gradient; *err stays set (sticky) for the host-side health check
-//     (sparkmi/parallel/ddp.py DataParallel.check) that fails the group.
-// Staging and signal regions are allocated uncached (hipDeviceMallocUncached), so peer reads
-// over xGMI and polls never see stale cache lines.  Only vector memory instructions are used.
+// Protocol (one launch per all-reduce, stream-ordered on every rank).  Device state ctr =
+// {epoch, done ticket, signal value} advanced by each launch's last block (like the optimizers'
+// step counter), so launches can sit in a captured HIP graph and replay — a small model's whole
+// data-parallel step (forward, backward, this all-reduce, optimizer) is ONE graph replay.
+//  1. block b copies its share of the local bucket into this rank's staging half (epoch & 1):
+//     double-buffered, so a fast rank's next call never overwrites data a slow peer still reads
+//     (a rank only starts call e + 1 after every peer signalled call e's first round, i.e.
+//     finished call e - 1);
+//  2. drain the stores (vmcnt(0)), barrier, thread q stores the round's signal value into slot
+//     [b][my rank] of rank q (system-scope release) and polls slot [b][q] of its own region
+//     (system-scope acquire, s_sleep back-off, BOUNDED: after `spins` polls (~4 s by default) the
+//     block records a timeout in *err and gives up — a dead peer never hangs the GPU);
+//  3. one-shot: block b sums its share of every rank's staging in rank order 0..w-1 (bit-identical
+//     on every rank).  Two-shot: block b sums its share of chunk `rank` in rank order, writes it
+//     back into its own staging (only this rank reads chunk `rank` there) and to the bucket,
+//     signals round 2, then copies its share of every peer's reduced chunk into the bucket.
+//  4. a timed-out wait poisons: the block writes NaN (and, two-shot, publishes NaN as its reduced
+//     chunk) — a lost peer never becomes a finite, silently wrong gradient; *err stays set
+//     (sticky) for the host-side check (sparkmi/parallel/ddp.py DataParallel.check).
+// Signal values increase monotonically over all launches of both kernels (one per round), so the
+// two kernels, any block counts and both rounds share one slot array.  Staging and signal regions
+// are uncached (hipDeviceMallocUncached): peer reads over xGMI and polls never see stale lines.
+// Only vector memory instructions are used.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "smi_ipc.h"
+
+// signal round: publish `val` to every peer's slot [b][rank], wait for every peer's slot [b][q]
+// to reach `val`; returns (block-uniform) whether some peer timed out
+__device__ __forceinline__ bool ipc_round(const IpcArgs& a, int b, unsigned val, int* timed_out) {
+  if ((int)threadIdx.x < a.world) {
+    __atomic_thread_fence(__ATOMIC_RELEASE);  // system scope: this block's stores are visible first
+    __hip_atomic_store(a.sig[threadIdx.x] + b * IPC_MAX_RANKS + a.rank, val, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned* f = a.sig[a.rank] + b * IPC_MAX_RANKS + threadIdx.x;
+    long spins = 0;
+    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - val) < 0) {
+      if (++spins > a.spins) {  // a peer is gone
+        __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        atomicOr(timed_out, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  }
+  __syncthreads();
+  return *timed_out != 0;
+}
+
+// the last block to finish advances the device state for the next launch
+__device__ __forceinline__ void ipc_advance(const IpcArgs& a, unsigned epoch, unsigned sval) {
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(a.done, 1u) == gridDim.x - 1) {
+    a.ep[0] = epoch;
+    a.sv[0] = sval;
+    a.done[0] = 0u;
+  }
+}
 
 __global__ __launch_bounds__(256) void ipc_allreduce_kernel(IpcArgs a) {
   const int b = blockIdx.x, nb = gridDim.x;
   const long n4 = a.n / 4;
   const long per = (n4 + nb - 1) / nb;
   const long lo = (long)b * per, hi = lo + per < n4 ? lo + per : n4;
-  const unsigned epoch = a.ep[0] + 1u;
+  const unsigned epoch = a.ep[0] + 1u, sval = a.sv[0] + 1u;
   const long half = (long)(epoch & 1u) * a.cap;
   float4* mine = (float4*)(a.data[a.rank] + half);
   const float4* src = (const float4*)a.buf;
@@ -43,51 +84,95 @@ __global__ __launch_bounds__(256) void ipc_allreduce_kernel(IpcArgs a) {
   __shared__ int timed_out;
   if (threadIdx.x == 0) timed_out = 0;
   __syncthreads();
-  if ((int)threadIdx.x < a.world) {
-    __atomic_thread_fence(__ATOMIC_RELEASE);  // system scope: the staging stores are visible first
-    __hip_atomic_store(a.sig[threadIdx.x] + b * IPC_MAX_RANKS + a.rank, epoch, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-    const unsigned* f = a.sig[a.rank] + b * IPC_MAX_RANKS + threadIdx.x;
-    long spins = 0;
-    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
-      if (++spins > a.spins) {  // a peer is gone
-        __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        atomicOr(&timed_out, 1);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(8);
-    }
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);
-  }
-  __syncthreads();
+  const bool lost = ipc_round(a, b, sval, &timed_out);
   float4* out = (float4*)a.buf;
-  if (timed_out) {  // poison: the bucket must not carry a finite partial sum
+  if (lost) {  // poison: the bucket must not carry a finite partial sum
     const float nan = __builtin_nanf("");
     for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) out[i] = make_float4(nan, nan, nan, nan);
-  } else
-  for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    float4 acc = ((const float4*)(a.data[0] + half))[i];
-    for (int r = 1; r < a.world; ++r) {
-      const float4 v = ((const float4*)(a.data[r] + half))[i];
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  } else {
+    for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+      float4 acc = ((const float4*)(a.data[0] + half))[i];
+      for (int r = 1; r < a.world; ++r) {
+        const float4 v = ((const float4*)(a.data[r] + half))[i];
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+      out[i] = acc;
     }
-    out[i] = acc;
   }
-  // advance the epoch: every block read ep[0] on entry; the last block to finish stores it
-  __syncthreads();
-  if (threadIdx.x == 0 && atomicAdd(a.done, 1u) == gridDim.x - 1) {
-    a.ep[0] = epoch;
-    a.done[0] = 0u;
-  }
+  ipc_advance(a, epoch, sval);
 }
 
-extern "C" int smi_ipc_allreduce(const IpcArgs* args, int blocks, hipStream_t st) {
+__global__ __launch_bounds__(256) void ipc_allreduce2_kernel(IpcArgs a) {
+  const int b = blockIdx.x, nb = gridDim.x;
+  const long n4 = a.n / 4;
+  const long C = (n4 + a.world - 1) / a.world;  // float4 per chunk (the last one may be short)
+  const long per = (C + nb - 1) / nb;           // float4 per block per chunk
+  const unsigned epoch = a.ep[0] + 1u, s1 = a.sv[0] + 1u, s2 = s1 + 1u;
+  const long half = (long)(epoch & 1u) * a.cap;
+  float4* mine = (float4*)(a.data[a.rank] + half);
+  float4* out = (float4*)a.buf;
+  auto range = [&](int c, long& lo, long& hi) {  // block b's share of chunk c
+    const long c0 = (long)c * C, c1 = c0 + C < n4 ? c0 + C : n4;
+    lo = c0 + (long)b * per;
+    hi = lo + per < c1 ? lo + per : c1;
+  };
+  // 1. stage block b's share of every chunk
+  for (int c = 0; c < a.world; ++c) {
+    long lo, hi;
+    range(c, lo, hi);
+    for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = out[i];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __shared__ int timed_out;
+  if (threadIdx.x == 0) timed_out = 0;
+  __syncthreads();
+  const float nan = __builtin_nanf("");
+  // 2. reduce-scatter: sum this rank's chunk over all ranks (rank order), publish it in place
+  bool lost = ipc_round(a, b, s1, &timed_out);
+  {
+    long lo, hi;
+    range(a.rank, lo, hi);
+    for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+      float4 acc = make_float4(nan, nan, nan, nan);
+      if (!lost) {
+        acc = ((const float4*)(a.data[0] + half))[i];
+        for (int r = 1; r < a.world; ++r) {
+          const float4 v = ((const float4*)(a.data[r] + half))[i];
+          acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
+      }
+      mine[i] = acc;
+      out[i] = acc;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // 3. all-gather every peer's reduced chunk
+  lost = ipc_round(a, b, s2, &timed_out);
+  for (int q = 0; q < a.world; ++q) {
+    if (q == a.rank) continue;
+    long lo, hi;
+    range(q, lo, hi);
+    const float4* peer = (const float4*)(a.data[q] + half);
+    for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) out[i] = lost ? make_float4(nan, nan, nan, nan) : peer[i];
+  }
+  if (lost) {  // this rank's own chunk too
+    long lo, hi;
+    range(a.rank, lo, hi);
+    for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) out[i] = make_float4(nan, nan, nan, nan);
+  }
+  ipc_advance(a, epoch, s2);
+}
+
+// algo 1: one-shot, 2: two-shot
+extern "C" int smi_ipc_allreduce(const IpcArgs* args, int blocks, int algo, hipStream_t st) {
   const IpcArgs& a = *args;
   if (a.world < 1 || a.world > IPC_MAX_RANKS || a.rank < 0 || a.rank >= a.world) return -1;
   if (a.n % 4 || a.n > a.cap || ((uintptr_t)a.buf & 15)) return -1;
-  if (args->spins < 1) return -1;
+  if (args->spins < 1 || (algo != 1 && algo != 2)) return -1;
   if (blocks < 1) blocks = 1;
   if (blocks > IPC_MAX_BLOCKS) blocks = IPC_MAX_BLOCKS;
-  hipLaunchKernelGGL(ipc_allreduce_kernel, dim3(blocks), dim3(256), 0, st, a);
+  if (algo == 1) hipLaunchKernelGGL(ipc_allreduce_kernel, dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(ipc_allreduce2_kernel, dim3(blocks), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }

@@ -1,5 +1,5 @@
-// Argument block of the IPC one-shot all-reduce (csrc/comm/ipc_allreduce.hip), shared with the
-// host bindings (csrc/comm/comm.cpp).
+// Argument block of the IPC one-shot / two-shot all-reduce (csrc/comm/ipc_allreduce.hip), shared
+// with the host bindings (csrc/comm/comm.cpp).
 #pragma once
 #define IPC_MAX_RANKS 8
 #define IPC_MAX_BLOCKS 128
@@ -14,6 +14,7 @@ struct IpcArgs {
   int rank, world;
   unsigned* ep;                        // device epoch counter (read at entry, advanced at exit)
   unsigned* done;                      // zeroed ticket word of the exit advance
+  unsigned* sv;                        // device signal value: the last value stored into signal slots
   int* err;                            // set to 1 on a poll timeout (sticky)
   long spins;                          // poll bound (s_sleep 8 back-off per poll)
 };

@@ -80,6 +80,18 @@ def translation_pairs(n, seq_len, src_vocab, tgt_vocab, seed=0, device="cpu"):
             token_sequences(n, seq_len, tgt_vocab, seed=seed + 1, device=device))
 
 
+def copy_pairs(n, seq_len, vocab, seed=0, device="cpu"):
+    """A LEARNABLE parallel corpus of the same shape: tgt = a fixed permutation of the source
+    tokens (same lengths and specials).  ``translation_pairs`` draws src and tgt independently
+    and uniformly, so no model can beat the token entropy there (cross-entropy floor ln(vocab - 4),
+    9.21 at vocab 10000); here the loss can fall to zero."""
+    src = token_sequences(n, seq_len, vocab, seed=seed, device=device)
+    g = _gen(seed + 11, device)
+    perm = torch.arange(vocab, device=device)
+    perm[len(SPECIALS):] = len(SPECIALS) + torch.randperm(vocab - len(SPECIALS), generator=g, device=device)
+    return src, perm[src]
+
+
 def ag_news_like(n, seq_len, vocab_size, num_classes=4, seed=0, device="cpu"):
     """AG_NEWS-like classification: padded ids [n, seq_len] and labels [n] in 0..3 where the label
     is weakly encoded in the token distribution (so training makes progress)."""

@@ -1,76 +1,29 @@
-"""Native communication layer: sparkmi._comm from Python.
+"""Native communication layer: the xGMI IPC all-reduce of sparkmi._comm.
 
-``NativeComm`` — an RCCL communicator owned by sparkmi (not torch's process group): bootstrapped
-from an ncclUniqueId published by rank 0 through the job's c10d TCPStore (the same rendezvous the
-reference's ``init_process_group`` used, distributed_cnn.py:152), collectives on raw device
-pointers on the current HIP stream, and ``abort()`` for the failure path.
-
-``IpcAllReduce`` — one-shot all-reduce over IPC-mapped uncached device memory for
-latency-bound buckets (< ~256 KB: the MLP's 256 B, the CNN's 31 KB gradients,
-distributed_multilayer_perceptron.py:103-106, distributed_cnn.py:152-156): every rank reads every
-peer's bucket directly over xGMI in one hop and sums in rank order (bit-identical results on
-every rank).  The epoch counter lives on the device, so the call can sit inside a captured HIP
-graph (the small models' whole data-parallel step is one replay).  Handles are exchanged once through torch.distributed (any backend, gloo included),
-so two processes sharing one GPU can exercise it too.
+``IpcAllReduce`` — all-reduce over IPC-mapped uncached device memory, one node, every rank
+reading its peers directly over xGMI (one hop on the 7 point-to-point links) instead of a ring:
+  * one-shot (buckets <= ``ONE_SHOT_MAX_BYTES`` or 2 ranks): every rank reads every peer's
+    bucket and sums it — the latency path for the MLP's 256 B and the CNN's 31 KB gradients
+    (distributed_multilayer_perceptron.py:103-106, distributed_cnn.py:152-156);
+  * two-shot (larger buckets, e.g. the LSTM's 12.3 MB dense embedding gradient): reduce-scatter
+    (rank r sums chunk r, reading its 1/w slice from all peers at once) then all-gather —
+    2 (w - 1) / w of the bucket over xGMI per rank instead of (w - 1).
+Both sum in rank order (bit-identical results on every rank) and keep their epoch on the device,
+so a call can sit inside a captured HIP graph (a small model's whole data-parallel step is one
+replay).  A peer that stops signalling is detected by a bounded poll: the bucket is NaN-poisoned,
+a sticky device flag is set, and ``check()`` raises ``IpcPeerLost``.  Handles are exchanged once
+through torch.distributed (any backend, gloo included), so two processes sharing one GPU can
+exercise it too.  Bulk collectives (the transformer's 188 MB gradient) go through RCCL — torch's
+"nccl" process group — in sparkmi/parallel/ddp.py.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
 from .. import _native
 
-_DT = {torch.float32: "float32", torch.bfloat16: "bfloat16", torch.float16: "float16", torch.int32: "int32",
-       torch.int64: "int64", torch.uint8: "uint8"}
-
-
-def _store():
-    return dist.distributed_c10d._get_default_store()
-
-
-class NativeComm:
-    def __init__(self, rank=None, world=None, device=None, store=None, tag="sparkmi_rccl"):
-        init = dist.is_available() and dist.is_initialized()
-        self.rank = (dist.get_rank() if init else 0) if rank is None else rank
-        self.world = (dist.get_world_size() if init else 1) if world is None else world
-        dev = torch.cuda.current_device() if device is None else device
-        C = _native.comm()
-        if self.world == 1:
-            uid = C.unique_id()
-        else:
-            st = store if store is not None else _store()
-            key = f"{tag}_uid"
-            if self.rank == 0:
-                st.set(key, C.unique_id())
-            uid = st.get(key)
-        self.comm = C.Comm(uid, self.rank, self.world, dev)
-
-    @staticmethod
-    def _s():
-        return torch.cuda.current_stream().cuda_stream
-
-    def all_reduce(self, t, op="sum"):
-        self.comm.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], op, self._s())
-        return t
-
-    def reduce_scatter(self, out, inp, op="sum"):
-        self.comm.reduce_scatter(inp.data_ptr(), out.data_ptr(), out.numel(), _DT[out.dtype], op, self._s())
-        return out
-
-    def all_gather(self, out, inp):
-        self.comm.all_gather(inp.data_ptr(), out.data_ptr(), inp.numel(), _DT[inp.dtype], self._s())
-        return out
-
-    def broadcast(self, t, root=0):
-        self.comm.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], root, self._s())
-        return t
-
-    def async_error(self):
-        return self.comm.async_error()
-
-    def abort(self):
-        self.comm.abort()
-
-    def destroy(self):
-        self.comm.destroy()
+ONE_SHOT_MAX_BYTES = 256 << 10
 
 
 class IpcUnavailable(RuntimeError):
@@ -91,7 +44,6 @@ class IpcAllReduce:
         C = _native.comm()
         self.C = C
         if timeout_s is None:
-            import os
             timeout_s = float(os.environ.get("SPARKMI_IPC_TIMEOUT_S", "4"))
         # the kernel's poll bound: ~2^24 polls with s_sleep back-off take ~4 s
         self.spins = max(1, int(float(timeout_s) * (1 << 24) / 4.0))
@@ -123,18 +75,20 @@ class IpcAllReduce:
                 self.data.append(pd)
                 self.sig.append(ps)
         self.err = torch.zeros(1, dtype=torch.int32, device="cuda")
-        self.ctr = torch.zeros(2, dtype=torch.int32, device="cuda")  # {epoch, ticket}: advanced by the kernel
+        # {epoch, ticket, signal value, pad}: advanced by the kernels' last block
+        self.ctr = torch.zeros(4, dtype=torch.int32, device="cuda")
         # every rank must be able to map every peer AND the kernel must produce the exact sum on
         # this topology (peer reads over xGMI, system-scope flags): a one-call self-test whose
         # verdict all ranks agree on through the regular process group; on failure the caller
         # keeps the RCCL path (IpcUnavailable) instead of risking a hang or a wrong gradient
         ok = opened
         if opened:
-            probe = torch.full((self.cap if self.cap < 4096 else 4096,), float(self.rank + 1), device="cuda")
-            self(probe)
-            torch.cuda.synchronize()
             want = float(self.world * (self.world + 1) // 2)
-            ok = bool(int(self.err.item()) == 0 and bool((probe == want).all()))
+            for algo in (1, 2):  # both kernels must produce the exact sum on this topology
+                probe = torch.full((self.cap if self.cap < 4096 else 4096,), float(self.rank + 1), device="cuda")
+                self(probe, algo=algo)
+                torch.cuda.synchronize()
+                ok = ok and bool(int(self.err.item()) == 0 and bool((probe == want).all()))
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
                             device="cuda" if dist.get_backend(group) == "nccl" else "cpu")
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
@@ -144,12 +98,24 @@ class IpcAllReduce:
         self.err.zero_()
         dist.barrier(group=group)
 
-    def __call__(self, t):
+    def algo_for(self, numel):
+        """1 = one-shot, 2 = two-shot: two-shot moves 2 (w - 1) / w of the bucket per rank instead of
+        (w - 1), at the price of a second signal round — worth it past the latency-bound sizes."""
+        return 1 if self.world <= 2 or numel * 4 <= ONE_SHOT_MAX_BYTES else 2
+
+    def __call__(self, t, algo=None):
         if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() % 4 or t.numel() > self.cap:
             raise ValueError("IpcAllReduce: contiguous fp32 tensor, numel % 4 == 0, <= capacity")
-        blocks = self.blocks or max(1, min(self.C.IPC_MAX_BLOCKS, (t.numel() // 4 + 1023) // 1024))
+        algo = algo or self.algo_for(t.numel())
+        n4 = t.numel() // 4
+        if self.blocks:
+            blocks = self.blocks
+        elif algo == 1:
+            blocks = max(1, min(self.C.IPC_MAX_BLOCKS, (n4 + 1023) // 1024))
+        else:  # >= 512 float4 of every chunk per block
+            blocks = max(1, min(self.C.IPC_MAX_BLOCKS, ((n4 + self.world - 1) // self.world + 511) // 512))
         self.C.ipc_allreduce(t.data_ptr(), t.numel(), self.data, self.sig, self.cap, self.rank, self.ctr.data_ptr(),
-                             self.err.data_ptr(), blocks, torch.cuda.current_stream().cuda_stream, self.spins)
+                             self.err.data_ptr(), blocks, torch.cuda.current_stream().cuda_stream, self.spins, algo)
         return t
 
     def failed(self):

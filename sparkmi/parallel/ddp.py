@@ -20,10 +20,14 @@ module was called, so gradients were never synchronised).  Design for MI355X + R
   one multi-range launch: sparkmi.optim.adam.Adam.shard) and the updated fp32 master pieces are
   all-gathered in place; per-rank optimizer work and state drop by 1/world and the gradient
   moves (w-1)/w instead of 2(w-1)/w of the buffer before the update;
-* ``ipc=True`` (default for small models on one node, <= 1 MiB of gradients): buckets are
-  summed by the one-shot xGMI IPC kernel (csrc/comm/ipc_allreduce.hip) — no ring latency, and
-  since it is a stream-ordered kernel with a device-side epoch, the whole data-parallel step
-  (forward, backward, all-reduce, optimizer) is captured as ONE HIP graph (``graph_safe``).
+* comm path by size (``SPARKMI_DP_COMM`` = auto | ipc | rccl; auto by default): gradients of
+  up to ``IPC_LIMIT_BYTES`` (32 MiB: the MLP's 256 B, the CNN's 31 KB, the LSTM's 12.3 MB) on one
+  node go through the xGMI IPC all-reduce (csrc/comm/ipc_allreduce.hip; one-shot for buckets
+  <= 256 KB, two-shot reduce-scatter + all-gather above) — no ring latency, and since it is a
+  stream-ordered kernel with a device-side epoch, the whole data-parallel step (forward,
+  backward, all-reduce, optimizer) is captured as ONE HIP graph (``graph_safe``).  Larger
+  gradients (the transformer's 188 MB) go through RCCL on its own stream, overlapped with the
+  backward; ``ipc`` forces the IPC kernels for them too (stream-ordered on the compute stream).
 The CPU/gloo path runs the identical logic (multi-process CPU tests).
 """
 import os
@@ -33,7 +37,7 @@ import torch.distributed as dist
 
 from ..ops import _grad
 
-IPC_LIMIT_BYTES = 1 << 20
+IPC_LIMIT_BYTES = 32 << 20
 
 
 def broadcast_flat(flat, src=0, group=None):
@@ -60,16 +64,22 @@ class DataParallel:
         if self.zero and 64 % self.world:
             raise ValueError("zero=True needs a world size dividing 64 (buckets are 64-element aligned)")
         self.ipc = None
+        mode = os.environ.get("SPARKMI_DP_COMM", "auto")
+        if mode not in ("auto", "ipc", "rccl"):
+            raise ValueError(f"SPARKMI_DP_COMM={mode!r}: auto | ipc | rccl")
         if ipc is None:
-            ipc = os.environ.get("SPARKMI_IPC_AR", "1") != "0"
-        if (ipc and not self.zero and self.world > 1 and flat.grad.is_cuda and flat.numel * 4 <= IPC_LIMIT_BYTES
-                and self.world <= 8 and _single_node(self.world)):
+            ipc = os.environ.get("SPARKMI_IPC_AR", "1") != "0" and mode != "rccl"
+        if ipc and mode == "auto" and flat.numel * 4 > IPC_LIMIT_BYTES:
+            ipc = False
+        self._build_buckets()
+        if (ipc and not self.zero and self.world > 1 and flat.grad.is_cuda and self.world <= 8
+                and _single_node(self.world)):
             from .comm import IpcAllReduce, IpcUnavailable
             try:
-                self.ipc = IpcAllReduce(cap_floats=flat.numel, group=group)
+                # any bucket cut (align_buckets re-cuts) stays within the bucket limit
+                self.ipc = IpcAllReduce(cap_floats=min(self._limit, flat.numel), group=group)
             except IpcUnavailable:
                 self.ipc = None  # every rank agreed: buckets go through the process group
-        self._build_buckets()
         self._pending = None
         self._works = []
         self._listener = None

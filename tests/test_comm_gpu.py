@@ -1,10 +1,11 @@
-"""T6 on one MI355X: the native comm layer (csrc/comm).
+"""T6 on one MI355X: the native comm layer (csrc/comm/ipc_allreduce.hip).
 
-* IPC one-shot all-reduce with TWO processes sharing the GPU (IPC handles work across processes
-  on one device): results equal the rank-ordered fp32 sum bit for bit, over
-  several epochs (both staging halves) and sizes, including a bucket that does not fill a block.
-* The native RCCL communicator (world 1 on one GPU — RCCL refuses two ranks on one device):
-  bootstrap through the TCPStore, every collective entry point, async-error query, abort.
+* IPC one-shot AND two-shot all-reduce with TWO processes sharing the GPU (IPC handles work
+  across processes on one device): results equal the rank-ordered fp32 sum bit
+  for bit, over several epochs (both staging halves), both kernels interleaved on one signal
+  array, and sizes from 16 B to 16 MB (ragged chunks, buckets that do not fill a block).
+* Peer loss: rank 1 skips one all-reduce -> rank 0's kernel times out within the configured
+  bound, its bucket is NaN (never a finite partial sum) and check() raises IpcPeerLost.
 """
 import sys
 
@@ -16,7 +17,9 @@ pytestmark = pytest.mark.gpu
 
 cloudpickle.register_pickle_by_value(sys.modules[__name__])
 
-SIZES = [4, 256, 7744, 65536]  # floats: MLP-sized, CNN-sized (7,740 params padded), 256 KB
+# floats: MLP-sized, CNN-sized (7,740 params padded), 256 KB, a ragged 1.2 MB, LSTM-sized 12.3 MB
+SIZES = [4, 256, 7744, 65536, 300004, 3075008]
+CAP = 1 << 22
 
 
 def _ipc_fn():
@@ -24,14 +27,15 @@ def _ipc_fn():
     from sparkmi.parallel import init_distributed, destroy
     from sparkmi.parallel.comm import IpcAllReduce
     rank, world, dev = init_distributed()
-    ar = IpcAllReduce(cap_floats=1 << 16)
+    ar = IpcAllReduce(cap_floats=CAP)
     out = []
     for it in range(3):
         for n in SIZES:
-            g = torch.Generator().manual_seed(1000 * it + n + rank)
-            x = torch.randn(n, generator=g).to(dev)
-            ar(x)
-            out.append(x.cpu())
+            for algo in (1, 2):
+                g = torch.Generator().manual_seed(1000 * it + n + rank)
+                x = torch.randn(n, generator=g).to(dev)
+                ar(x, algo=algo)
+                out.append(x.cpu())
     torch.cuda.synchronize()
     ar.check()
     ar.close()
@@ -48,73 +52,47 @@ def test_ipc_allreduce_two_processes_one_gpu():
         for n in SIZES:
             a = torch.randn(n, generator=torch.Generator().manual_seed(1000 * it + n))
             b = torch.randn(n, generator=torch.Generator().manual_seed(1000 * it + n + 1))
-            assert torch.equal(res[k], a + b), (it, n)
-            k += 1
+            for algo in (1, 2):
+                assert torch.equal(res[k], a + b), (it, n, algo)
+                k += 1
 
 
-def _rccl_fn():
+def _lost_fn():
+    import time
     import torch
     from sparkmi.parallel import init_distributed, destroy
-    from sparkmi.parallel.comm import NativeComm
+    from sparkmi.parallel.comm import IpcAllReduce, IpcPeerLost
     rank, world, dev = init_distributed()
-    c = NativeComm()
-    x = torch.arange(16, dtype=torch.float32, device=dev)
-    c.all_reduce(x)
-    o = torch.empty(16, device=dev)
-    c.all_gather(o, x)
-    r = torch.empty(16, device=dev)
-    c.reduce_scatter(r, x)
-    c.broadcast(x, 0)
-    torch.cuda.synchronize()
-    e = c.async_error()
-    c.abort()
+    ar = IpcAllReduce(cap_floats=1 << 16, timeout_s=1.0)
+    res = {}
+    for algo in (1, 2):
+        x = torch.ones(4096, device=dev)
+        ar(x, algo=algo)  # healthy call
+        torch.cuda.synchronize()
+        res[f"ok{algo}"] = float(x[0])
+    if rank == 0:
+        x = torch.ones(65536, device=dev)
+        t0 = time.time()
+        ar(x, algo=2)  # rank 1 never joins this one
+        torch.cuda.synchronize()
+        res["wait_s"] = time.time() - t0
+        res["finite"] = int(torch.isfinite(x).sum())
+        try:
+            ar.check()
+            res["raised"] = False
+        except IpcPeerLost:
+            res["raised"] = True
+    allr = [None] * world
+    torch.distributed.all_gather_object(allr, res)  # Distributor.run returns rank 0's value
     destroy()
-    return x.cpu(), o.cpu(), r.cpu(), e
+    return allr
 
 
-def test_native_rccl_world1():
+def test_ipc_peer_lost_poisons_and_raises():
     from sparkmi.api import Distributor
-    x, o, r, e = Distributor(num_processes=1, use_gpu=True, log_sink=None,
-                             timeout=300).run(_rccl_fn)
-    ref = torch.arange(16, dtype=torch.float32)
-    assert torch.equal(x, ref) and torch.equal(o, ref) and torch.equal(r, ref) and e == 0
-
-
-def _mlp_dp(steps, use_dp):
-    import torch
-    from sparkmi.models.mlp import MultilayerPerceptron
-    from sparkmi.optim import SGD
-    from sparkmi.parallel import DataParallel, destroy, init_distributed
-    from sparkmi.train.runner import StepRunner
-    from sparkmi.utils.flat import FlatParams
-    rank, world, dev = init_distributed()
-    torch.manual_seed(0)
-    model = MultilayerPerceptron((4, 5, 4, 3)).to(dev).train()
-    flat = FlatParams(model, shadow=False)
-    opt = SGD(flat, lr=0.1)
-    ddp = DataParallel(flat) if use_dp else None
-    info = {"ipc": ddp is not None and ddp.ipc is not None, "graph_safe": ddp is not None and ddp.graph_safe}
-    runner = StepRunner(model, lambda m, x, y: m.loss(x, y), opt, ddp, graph=True)
-    g = torch.Generator().manual_seed(5)
-    X = torch.rand(steps, 60, 4, generator=g) * 2 - 1
-    Y = torch.randint(0, 3, (steps, 60), generator=g)
-    per = 60 // world
-    for i in range(steps):
-        runner.step(X[i, rank * per:(rank + 1) * per].to(dev), Y[i, rank * per:(rank + 1) * per].to(dev))
-    torch.cuda.synchronize()
-    out = flat.master.cpu().clone()
-    if ddp is not None:
-        ddp.close()
-    destroy()
-    return out, info
-
-
-def test_ipc_data_parallel_whole_step_graph():
-    """MLP data parallelism over the IPC all-reduce with the WHOLE step in one HIP graph (two
-    processes sharing the GPU) == one process at twice the batch."""
-    from sparkmi.api import Distributor
-    dp, info = Distributor(num_processes=2, use_gpu=True, share_gpus=True, env={"SPARKMI_DIST_BACKEND": "gloo"}, log_sink=None,
-                           timeout=300).run(_mlp_dp, 12, True)
-    assert info["ipc"] and info["graph_safe"]
-    single, _ = Distributor(num_processes=1, use_gpu=True, log_sink=None, timeout=300).run(_mlp_dp, 12, False)
-    torch.testing.assert_close(dp, single, atol=1e-5, rtol=1e-5)
+    res = Distributor(num_processes=2, use_gpu=True, share_gpus=True, env={"SPARKMI_DIST_BACKEND": "gloo"}, log_sink=None,
+                      timeout=300).run(_lost_fn)
+    r0, r1 = res
+    assert r0["ok1"] == r0["ok2"] == r1["ok1"] == r1["ok2"] == 2.0
+    assert r0["raised"] and r0["finite"] == 0, r0  # poisoned, loud
+    assert r0["wait_s"] < 30.0, r0  # bounded by the configured timeout (1 s of polling)
