@@ -1,5 +1,7 @@
 """Shared recipe plumbing: executor launch (sequential in-process or Distributor), data sharding,
 evaluation helpers."""
+import os
+
 import numpy as np
 import torch
 
@@ -12,7 +14,10 @@ def run(train_fn, cfg):
     if cfg.world <= 1:
         return train_fn(cfg)
     use_gpu = cfg.device != "cpu" and torch.cuda.device_count() > 0
+    # SPARKMI_SHARE_GPUS=1: several executors per device (tests on a one-GPU box; gloo backend)
+    share = os.environ.get("SPARKMI_SHARE_GPUS", "0") == "1"
     return Distributor(num_processes=cfg.world, local_mode=getattr(cfg, "local_mode", True), use_gpu=use_gpu,
+                       share_gpus=share,
                        max_restarts=getattr(cfg, "max_restarts", 0),
                        progress_timeout=getattr(cfg, "progress_timeout", 0.0) or None).run(train_fn, cfg)
 

@@ -94,7 +94,7 @@ def train_fn(cfg):
                       flops_per_sample=flops)
     stats = trainer.fit(loader, cfg.epochs)
     trainer.close()
-    out = dict(stats, world=world, en_vocab=len(en_vocab), de_vocab=len(de_vocab))
+    out = dict(stats, world=world, en_vocab=len(en_vocab), de_vocab=len(de_vocab), dtype=cfg.dtype)
     if rank == 0:
         out["train_samples_per_s"] = stats["steps"] * cfg.batch_size * world / max(stats["time_s"], 1e-9)
     return out if rank == 0 else None

@@ -254,12 +254,19 @@ class StepRunner:
                 g.replay()
         if not self._opt_in_graph:
             # the graphs hold forward + backward only (data-parallel over RCCL, or split-graph
-            # capture over either backend): reduce the remaining buckets, then the optimizer
+            # capture over either backend): reduce the remaining buckets, then the optimizer.
+            # Phase events: fwd_bwd = the replays, allreduce = what finish() still waits for
+            # (the part of the reduction not hidden under the backward), optim = the update
+            e1 = self._event()
             if self._dp:
                 self.ddp.finish()
+            e2 = self._event()
             self.opt.step()
             if self._dp:
                 self.ddp.gather_params()
+            e3 = self._event()
+            if e0 is not None:
+                self._phase_events.append((e0, e1, e2, e3))
         elif self._dp:
             # the replayed graph reduced every bucket (IPC kernel): account its bytes
             self.ddp.bytes_reduced += self.ddp.flat.grad.numel() * 4

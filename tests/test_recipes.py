@@ -66,6 +66,23 @@ def test_translator_recipe_small():
     assert r["steps"] == 2 and r["final_loss"] > 0
 
 
+def test_translator_recipe_dtype_and_metrics(tmp_path):
+    """--dtype: fp32 by default (the reference's precision), bf16 on request, anything else
+    refused; the metrics records carry the model TFLOP/s of the step."""
+    from sparkmi.recipes import translator
+    small = CPU + ["--n-train", "64", "--max-steps", "2", "--d-model", "64", "--ffn-hidden", "128", "--num-heads", "2",
+                   "--max-sequence-length", "32", "--log-every", "1"]
+    assert translator.parse(translator.TranslatorConfig, small).dtype == "fp32"
+    r = translator.main(small + ["--metrics", str(tmp_path / "m")])
+    assert r["steps"] == 2 and r["dtype"] == "fp32"
+    recs = read_jsonl(str(tmp_path / "m.rank0.jsonl"))
+    assert recs and all(rec["tflops"] > 0 for rec in recs)
+    rb = translator.main(small + ["--dtype", "bf16"])
+    assert rb["steps"] == 2 and rb["dtype"] == "bf16" and rb["final_loss"] > 0
+    with pytest.raises(ValueError):
+        translator.main(small + ["--dtype", "fp16"])
+
+
 def test_mllib_recipe(tmp_path):
     from sparkmi.recipes import mllib_mlp
     r = mllib_mlp.run(save_path=str(tmp_path / "model"), verbose=False)

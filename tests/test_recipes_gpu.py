@@ -64,3 +64,41 @@ def test_mlp_recipe_gpu():
     from sparkmi.recipes import mlp
     r = mlp.main(GPU + ["--epochs", "100", "--lr", "2.0"])
     assert r["test_acc"] > 85.0
+
+
+def _phase_recs(path):
+    from sparkmi.utils.metrics import read_jsonl
+    recs = read_jsonl(path)
+    return [r for r in recs if "fwd_bwd_s" in r]
+
+
+@pytest.mark.gpu
+def test_translator_graph_metrics_phases(tmp_path):
+    """A HIP-graph training run (fp32 default) writes metrics records with the per-phase device
+    times (fwd_bwd_s / allreduce_s / optim_s from events between the phase graphs) and TFLOP/s."""
+    from sparkmi.recipes import translator
+    r = translator.main(GPU + ["--n-train", "640", "--max-steps", "12", "--d-model", "128", "--ffn-hidden", "256",
+                               "--num-heads", "2", "--max-sequence-length", "64", "--log-every", "4",
+                               "--metrics", str(tmp_path / "m")])
+    assert r["steps"] == 12 and r["dtype"] == "fp32"
+    recs = _phase_recs(str(tmp_path / "m.rank0.jsonl"))
+    assert recs, "no phase record"
+    last = recs[-1]
+    assert last["fwd_bwd_s"] > 0 and last["optim_s"] > 0 and last["allreduce_s"] >= 0 and last["tflops"] > 0, last
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_translator_graph_dp_metrics_phases(tmp_path, monkeypatch):
+    """The same from a 2-executor data-parallel graph run (split-graph backward, gloo on the
+    shared GPU): the allreduce phase is what finish() still waits for after the replays."""
+    from sparkmi.recipes import translator
+    monkeypatch.setenv("SPARKMI_DIST_BACKEND", "gloo")  # RCCL needs one device per rank
+    monkeypatch.setenv("SPARKMI_SHARE_GPUS", "1")       # both executors on the box's one GPU
+    monkeypatch.setenv("SPARKMI_DP_COMM", "rccl")      # the process-group path, not the IPC kernel
+    r = translator.main(GPU + ["--world", "2", "--n-train", "640", "--max-steps", "12", "--d-model", "128",
+                               "--ffn-hidden", "256", "--num-heads", "2", "--max-sequence-length", "64",
+                               "--log-every", "4", "--metrics", str(tmp_path / "m")])
+    assert r["steps"] == 12 and r["world"] == 2
+    recs = _phase_recs(str(tmp_path / "m.rank0.jsonl"))
+    assert recs and recs[-1]["fwd_bwd_s"] > 0 and recs[-1]["allreduce_s"] >= 0 and recs[-1]["optim_s"] > 0, recs
