@@ -38,7 +38,7 @@ int smi_ln_bwd_f32(const void*, const void*, const float*, const float*, const f
                    float*, int, float*, float*, int, int, int, const uint32_t*, uint32_t, uint32_t, float, void*, long,
                    hipStream_t);
 int smi_emb_fwd_f32(const long long*, const void*, const float*, void*, long, int, int, const uint32_t*, uint32_t, uint32_t,
-                    float, hipStream_t);
+                    float, void*, long, hipStream_t);
 int smi_emb_bwd_f32(const long long*, const void*, float*, long, int, long long, const uint32_t*, uint32_t, uint32_t, float, long, void*,
                     hipStream_t);
 int smi_attn_fwd(const AttnFwdArgs*, hipStream_t);
@@ -47,7 +47,7 @@ int smi_attn_f32_bwd(const AttnF32Args*, hipStream_t);
 int smi_attn_bwd(const AttnBwdArgs*, const void*, float*, hipStream_t);
 int smi_ce_fwd(const void*, int, const long long*, int, int, long long, float*, float*, float*, float*, hipStream_t);
 int smi_ce_bwd(const void*, int, const long long*, int, int, long long, const float*, const float*, const float*, void*,
-               hipStream_t);
+               void*, long, long, hipStream_t);
 int smi_emb_fwd(const long long*, const void*, const float*, void*, long, int, int, const uint32_t*, uint32_t, uint32_t, float,
                 hipStream_t);
 int smi_emb_bwd(const long long*, const void*, float*, long, int, long long, const uint32_t*, uint32_t, uint32_t, float, long,
@@ -79,6 +79,7 @@ int smi_gemm_sp_wgrad_group(const void* const*, const long*, const long*, const 
 int smi_split3(const float*, long, int, long, void*, long, long, hipStream_t);
 int smi_gemm_sp_waves(int);
 int smi_gemm_sp_tm(int);
+int smi_gemm_sp_wg_tm(int);
 int smi_splitk_reduce(const float*, int, long, float*, long, float*, int, hipStream_t);
 int smi_splitk_fold_multi(const float* const*, float* const*, float* const*, const long*, const int*, const int*, int,
                           hipStream_t);
@@ -135,9 +136,9 @@ PYBIND11_MODULE(_C, m) {
         "ln_bwd_f32");
   });
   m.def("emb_fwd_f32", [](u ids, u table, u pe, u out, long T, int D, int Sp, u seedp, uint32_t salt, uint32_t thresh,
-                          float dscale, u st) {
+                          float dscale, u planes, long pps, u st) {
     chk(smi_emb_fwd_f32((const long long*)ids, P(table), PF(pe), P(out), T, D, Sp, (const uint32_t*)seedp, salt, thresh,
-                        dscale, S(st)), "emb_fwd_f32");
+                        dscale, P(planes), pps, S(st)), "emb_fwd_f32");
   });
   m.def("emb_bwd_f32", [](u ids, u dout, u dtable, long T, int D, long long pad, u seedp, uint32_t salt, uint32_t thresh,
                           float dscale, long V, u ws, u st) {
@@ -223,10 +224,11 @@ PYBIND11_MODULE(_C, m) {
     chk(smi_ce_fwd(P(logits), is_bf16, (const long long*)labels, M, V, ignore, PF(lse), PF(count), PF(loss),
                    PF(row_loss), S(st)), "ce_fwd");
   });
+  // planes / ldp / pps: optional split planes of the fp32 gradient (0 for none)
   m.def("ce_bwd", [](u logits, int is_bf16, u labels, int M, int V, long long ignore, u lse, u count, u dloss, u grad,
-                     u st) {
+                     u planes, long ldp, long pps, u st) {
     chk(smi_ce_bwd(P(logits), is_bf16, (const long long*)labels, M, V, ignore, PF(lse), PF(count), PF(dloss), P(grad),
-                   S(st)), "ce_bwd");
+                   P(planes), ldp, pps, S(st)), "ce_bwd");
   });
   m.def("emb_fwd", [](u ids, u table, u pe, u out, long T, int D, int Sp, u seedp, uint32_t salt, uint32_t thresh, float dscale,
                       u st) {
@@ -442,7 +444,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_sp_waves", [](int set) { return smi_gemm_sp_waves(set); },
         "split-plane GEMM waves per 128x128 tile (4 | 8); other values query");
   m.def("gemm_sp_tm", [](int set) { return smi_gemm_sp_tm(set); },
-        "split-plane GEMM tile height for large problems (128 | 256); other values query");
+        "split-plane GEMM tile form for large problems (16: 256x128 on 16x16x32 MFMA | 256 | 4 | 128); other values query");
+  m.def("gemm_sp_wg_tm", [](int set) { return smi_gemm_sp_wg_tm(set); },
+        "tile form of the grouped weight-gradient launch (128 | 256 | 16 | 4; -1 follows gemm_sp_tm); other values query");
   m.def("gemm_f32_algo", [](int set) { return smi_gemm_f32_algo(set); },
         "fp32 GEMM product algorithm: 0 = f32 MFMA, 6 = 3-way bf16 split (6 terms); set < 0 queries");
   m.def("gemm_f32_wgrad_group", [](std::vector<u> A, std::vector<long> lda, std::vector<u> B, std::vector<long> ldb,

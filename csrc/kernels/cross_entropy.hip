@@ -6,9 +6,12 @@
 // (distributed_cnn.py:141, distributed_lstm.py:142,189).
 // Forward: one 256-thread block per row, online (max, sum) pass over V with 16-B loads (4 in
 // flight per thread); stores the row logsumexp and row loss; a one-block finalize sums them.
-// Backward: grad = (softmax - onehot) * dloss / count, written in place or out of place.
+// Backward: grad = (softmax - onehot) * dloss / count, written in place or out of place; fp32
+// path: optionally also its bf16 hi/mid/lo planes [3][M][ldp] (ldp >= V, zero columns V..ldp-1),
+// the dY operand of the vocab projection's split-plane dgrad / wgrad (no separate split pass).
 // The valid-row count lives on the device, so the whole loss is graph-capturable.
 #include "smi_common.h"
+#include "smi_split3.h"
 
 // Sums the per-row losses and counts the valid rows (one block): a single-address atomic per row
 // from 8192 blocks serialises at the L2 (~120 us measured), this is one pass over 32 KiB.
@@ -120,7 +123,8 @@ template <bool BF16>
 __global__ __launch_bounds__(256) void ce_bwd_kernel(const void* __restrict__ logits, const long long* __restrict__ labels,
                                                      int V, long long ignore, const float* __restrict__ lse_in,
                                                      const float* __restrict__ count, const float* __restrict__ dloss,
-                                                     void* __restrict__ grad) {
+                                                     void* __restrict__ grad, unsigned short* __restrict__ P, long ldp,
+                                                     long pps) {
   const int row = blockIdx.x;
   const long base = (long)row * V;
   const long long lab = labels[row];
@@ -145,6 +149,15 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const void* __restrict__ lo
     } else {
       *(float4*)((float*)grad + base + (long)i * 8) = make_float4(gq[0], gq[1], gq[2], gq[3]);
       *(float4*)((float*)grad + base + (long)i * 8 + 4) = make_float4(gq[4], gq[5], gq[6], gq[7]);
+      if (P) {
+        uint32_t h[4], m[4], l[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) split3_pair(gq[2 * e], gq[2 * e + 1], h[e], m[e], l[e]);
+        unsigned short* q = P + (long)row * ldp + (long)i * 8;
+        *(uint4*)q = make_uint4(h[0], h[1], h[2], h[3]);
+        *(uint4*)(q + pps) = make_uint4(m[0], m[1], m[2], m[3]);
+        *(uint4*)(q + 2 * pps) = make_uint4(l[0], l[1], l[2], l[3]);
+      }
     }
   }
   for (int i = nvec * 8 + threadIdx.x; i < V; i += 256) {
@@ -152,6 +165,19 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const void* __restrict__ lo
     const float gq = (__expf(x - lse) - (i == lab ? 1.f : 0.f)) * scale;
     if (BF16) ((unsigned short*)grad)[base + i] = f2bf(gq);
     else ((float*)grad)[base + i] = gq;
+    if (!BF16 && P) {
+      unsigned short* q = P + (long)row * ldp + i;
+      const unsigned short hb = f2bf(gq);
+      const float r = gq - bf2f(hb);
+      const unsigned short mb = f2bf(r);
+      q[0] = hb; q[pps] = mb; q[2 * pps] = f2bf(r - bf2f(mb));
+    }
+  }
+  if (!BF16 && P) {  // the k padding of the GEMM operand
+    for (long i = V + threadIdx.x; i < ldp; i += 256) {
+      unsigned short* q = P + (long)row * ldp + i;
+      q[0] = 0; q[pps] = 0; q[2 * pps] = 0;
+    }
   }
 }
 
@@ -167,10 +193,15 @@ extern "C" int smi_ce_fwd(const void* logits, int is_bf16, const long long* labe
 }
 
 extern "C" int smi_ce_bwd(const void* logits, int is_bf16, const long long* labels, int M, int V, long long ignore,
-                          const float* lse, const float* count, const float* dloss, void* grad, hipStream_t st) {
+                          const float* lse, const float* count, const float* dloss, void* grad, void* planes, long ldp,
+                          long pps, hipStream_t st) {
+  unsigned short* P = (unsigned short*)planes;
+  if (P && (is_bf16 || ldp < V || ldp % 8 || pps < (long)M * ldp || ((uintptr_t)P & 15))) return -1;
   if (is_bf16)
-    hipLaunchKernelGGL(ce_bwd_kernel<true>, dim3(M), dim3(256), 0, st, logits, labels, V, ignore, lse, count, dloss, grad);
+    hipLaunchKernelGGL(ce_bwd_kernel<true>, dim3(M), dim3(256), 0, st, logits, labels, V, ignore, lse, count, dloss, grad,
+                       nullptr, 0L, 0L);
   else
-    hipLaunchKernelGGL(ce_bwd_kernel<false>, dim3(M), dim3(256), 0, st, logits, labels, V, ignore, lse, count, dloss, grad);
+    hipLaunchKernelGGL(ce_bwd_kernel<false>, dim3(M), dim3(256), 0, st, logits, labels, V, ignore, lse, count, dloss, grad,
+                       P, ldp, pps);
   SMI_CHECK_LAUNCH();
 }

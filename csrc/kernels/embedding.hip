@@ -11,13 +11,15 @@
 // padding_idx are skipped (that row's gradient stays zero like torch's padding_idx).  Dense semantics are kept on
 // purpose: the reference's Adam decays every row.
 #include "smi_common.h"
+#include "smi_split3.h"
 
 // T = storage of the table copy and the output: unsigned short (bf16 shadow) or float (fp32
 // reference-precision path: the fp32 master table itself).
 template <typename T>
 __global__ void emb_fwd_kernel(const long long* __restrict__ ids, const T* __restrict__ table,
                                const float* __restrict__ pe, T* __restrict__ out, long Tn, int D, int S,
-                               const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale) {
+                               const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale,
+                               unsigned short* __restrict__ P, long pps) {
   const uint32_t seed = smi_seed(seedp, salt);
   const int vpr = D / 8;
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -36,6 +38,15 @@ __global__ void emb_fwd_kernel(const long long* __restrict__ ids, const T* __res
     o[j] = x;
   }
   V8<T>::store(out + t * D + c, o);
+  if (P) {  // fp32 path: split planes [3][Tn][D] for the first layer's split-plane GEMMs
+    uint32_t h[4], m[4], l[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split3_pair(o[2 * e], o[2 * e + 1], h[e], m[e], l[e]);
+    unsigned short* q = P + t * D + c;
+    *(uint4*)q = make_uint4(h[0], h[1], h[2], h[3]);
+    *(uint4*)(q + pps) = make_uint4(m[0], m[1], m[2], m[3]);
+    *(uint4*)(q + 2 * pps) = make_uint4(l[0], l[1], l[2], l[3]);
+  }
 }
 
 // One wave per run of EMB_RUN consecutive tokens, lane = column (a wave-instruction covers 64
@@ -406,15 +417,19 @@ extern "C" int smi_emb_fwd(const long long* ids, const void* table, const float*
   if (D % 8) return -1;
   const long n = T * (D / 8);
   hipLaunchKernelGGL(emb_fwd_kernel<unsigned short>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ids,
-                     (const unsigned short*)table, pe, (unsigned short*)out, T, D, S, seedp, salt, thresh, dscale);
+                     (const unsigned short*)table, pe, (unsigned short*)out, T, D, S, seedp, salt, thresh, dscale,
+                     nullptr, 0L);
   SMI_CHECK_LAUNCH();
 }
+// planes / pps: optional split planes [3][T][D] of the output (0 for none)
 extern "C" int smi_emb_fwd_f32(const long long* ids, const void* table, const float* pe, void* out, long T, int D, int S,
-                               const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, hipStream_t st) {
-  if (D % 8) return -1;
+                               const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, void* planes,
+                               long pps, hipStream_t st) {
+  if (D % 8 || (planes && (((uintptr_t)planes & 15) || pps < T * D))) return -1;
   const long n = T * (D / 8);
   hipLaunchKernelGGL(emb_fwd_kernel<float>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ids,
-                     (const float*)table, pe, (float*)out, T, D, S, seedp, salt, thresh, dscale);
+                     (const float*)table, pe, (float*)out, T, D, S, seedp, salt, thresh, dscale,
+                     (unsigned short*)planes, pps);
   SMI_CHECK_LAUNCH();
 }
 

@@ -42,9 +42,18 @@ class EmbeddingFn(torch.autograd.Function):
             if pe is not None and pe.shape[0] < S:
                 raise ValueError(f"sequence length {S} exceeds positional table {pe.shape[0]}")
             table = weight.detach() if f32 else bf16_weight(weight)
-            (C.emb_fwd_f32 if f32 else C.emb_fwd)(ids_c.data_ptr(), table.data_ptr(), _native.ptr(pe), out.data_ptr(),
-                                                  T, D, S if pe is not None else 1, rng.ptr(), salt,
-                                                  _rng.threshold(p), _rng.scale(p), _native.stream())
+            args = (ids_c.data_ptr(), table.data_ptr(), _native.ptr(pe), out.data_ptr(), T, D,
+                    S if pe is not None else 1, rng.ptr(), salt, _rng.threshold(p), _rng.scale(p))
+            if f32:
+                from . import gemm as G
+                from . import planes as _pl
+                # the first layer's GEMM operand, split by the same kernel (D % 32: no k padding)
+                op = torch.empty(3, T, D, device=ids.device, dtype=torch.bfloat16) if (G.SP and D % 32 == 0) else None
+                C.emb_fwd_f32(*args, _native.ptr(op), op.stride(0) if op is not None else 0, _native.stream())
+                if op is not None:
+                    _pl.attach(out, op)
+            else:
+                C.emb_fwd(*args, _native.stream())
             ctx.seed = 0
         else:
             x = weight.float()[ids_c]

@@ -50,8 +50,16 @@ class CrossEntropyFn(torch.autograd.Function):
             C = _native.C()
             grad = torch.empty_like(x2)
             dl = dloss.reshape(1).to(torch.float32).contiguous()
+            # fp32: the gradient's split planes (k-padded: V is the K of the vocab projection's
+            # dgrad) for the split-plane GEMMs, written by the same kernel
+            from . import gemm as G
+            from . import planes as _pl
+            gp = _pl.new(M, V, x2.device, kpad=True) if (x2.dtype == torch.float32 and G.SP) else None
             C.ce_bwd(x2.data_ptr(), int(x2.dtype == torch.bfloat16), lab.data_ptr(), M, V, ctx.ignore, lse.data_ptr(),
-                     stats[0:1].data_ptr(), dl.data_ptr(), grad.data_ptr(), _native.stream())
+                     stats[0:1].data_ptr(), dl.data_ptr(), grad.data_ptr(), _native.ptr(gp),
+                     gp.stride(1) if gp is not None else 0, gp.stride(0) if gp is not None else 0, _native.stream())
+            if gp is not None:
+                _pl.attach(grad, gp)
             return grad.reshape(ctx.shape), None, None
         count = stats[0].clamp_min(1.0)
         p = torch.exp(x2.float() - lse[:, None])

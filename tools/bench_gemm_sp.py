@@ -41,7 +41,7 @@ def main():
         fl = 2.0 * M * N * K
         r = {"N": N, "K": K}
         gw = torch.zeros(N, K, device="cuda")
-        for tm in (4, 256, 128):
+        for tm in (16, 256, 128):
             C.gemm_sp_tm(tm)
             r[f"sp{tm}_fwd_us"] = timeit(lambda: G.sp_fwd(xp, wp, M, N, K, bias=b))
             r[f"sp{tm}_dgrad_us"] = timeit(lambda: G.sp_dgrad(dyp, wp, M, K, N))
@@ -74,7 +74,7 @@ def main():
                               [g.data_ptr() for g in gws], [g.data_ptr() for g in gbs], [n for n, _ in shp],
                               [k for _, k in shp], [T] * len(shp), _native.stream())
     fl = sum(2.0 * T * n * k for n, k in shp)
-    for tm in (4, 256, 128):
+    for tm in (16, 256, 128):
         C.gemm_sp_tm(tm)
         t = timeit(grp)
         print(json.dumps({f"sp{tm}_wgrad_group_dec_layer_us": round(t, 1), "tf": round(fl / (t * 1e-6) / 1e12, 1)}),

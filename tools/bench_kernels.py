@@ -94,7 +94,7 @@ def main():
     grad = torch.empty_like(logits)
     dl = torch.ones(1, device=dev)
     t = timeit(lambda: C.ce_bwd(logits.data_ptr(), 1, lab.data_ptr(), M, V, 0, lse2.data_ptr(), stats.data_ptr(),
-                                dl.data_ptr(), grad.data_ptr(), st()))
+                                dl.data_ptr(), grad.data_ptr(), 0, 0, 0, st()))
     print(f"ce_bwd      {t:8.1f} us  {2 * M * V * 2 / t / 1e3:7.0f} GB/s")
     n = 47_000_000
     p_, g_, m_, v_ = (torch.randn(n, device=dev) for _ in range(4))
