@@ -80,6 +80,7 @@ int smi_split3(const float*, long, int, long, void*, long, long, hipStream_t);
 int smi_gemm_sp_waves(int);
 int smi_gemm_sp_tm(int);
 int smi_gemm_sp_wg_tm(int);
+int smi_attn_f32_sp(int);
 int smi_splitk_reduce(const float*, int, long, float*, long, float*, int, hipStream_t);
 int smi_splitk_fold_multi(const float* const*, float* const*, float* const*, const long*, const int*, const int*, int,
                           hipStream_t);
@@ -445,6 +446,8 @@ PYBIND11_MODULE(_C, m) {
         "split-plane GEMM waves per 128x128 tile (4 | 8); other values query");
   m.def("gemm_sp_tm", [](int set) { return smi_gemm_sp_tm(set); },
         "split-plane GEMM tile form for large problems (16: 256x128 on 16x16x32 MFMA | 256 | 4 | 128); other values query");
+  m.def("attn_f32_sp", [](int set) { return smi_attn_f32_sp(set); },
+        "fp32 attention kernels: 1 staged-plane (default), 0 per-wave split; other values query");
   m.def("gemm_sp_wg_tm", [](int set) { return smi_gemm_sp_wg_tm(set); },
         "tile form of the grouped weight-gradient launch (128 | 256 | 16 | 4; -1 follows gemm_sp_tm); other values query");
   m.def("gemm_f32_algo", [](int set) { return smi_gemm_f32_algo(set); },

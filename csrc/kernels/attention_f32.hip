@@ -28,6 +28,8 @@
 // LDS images: [32 rows][68 floats] for row-fragment (ds_read_b128, conflict-free at pitch 68)
 // operands, [32][64] for column-only operands (ds_read_b32 rows, conflict-free at any pitch).
 // 32-row chunks keep the staging registers at 16 per thread (64-row chunks spilled dK/dV).
+#include <stdlib.h>
+
 #include "smi_common.h"
 #include "smi_attention.h"
 #include "smi_attn_mask.h"
@@ -453,6 +455,431 @@ __global__ __launch_bounds__(256, XS ? 1 : 2) void attn_f32_dkdv_kernel(AttnF32A
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// STAGED-PLANE kernels (the default; smi_attn_f32_sp): the same three passes and accumulation
+// order, but every streamed 32-row chunk is split into bf16 hi / mid / lo planes ONCE, while it
+// is staged into LDS (each thread splits the 8 values it loads), instead of every wave splitting
+// every fragment it reads (the XS = 1 kernels re-split each streamed value per wave and per use:
+// VALU-bound at ~40 % of the split ceiling).  Fragments then come out of LDS as ready bf16
+// operands: row fragments (k = head dim) by ds_read_b128, column fragments (k = the streamed
+// rows) by ds_read_b64_tr_b16; six v_mfma_f32_32x32x16_bf16 per fragment pair.  Only the
+// per-block P / dS values (computed in registers) are split in the loop.
+//
+// LDS image per operand plane: [32 rows][64] bf16, 128-B rows, 16-B chunk c stored at
+// c ^ as_sw(row), as_sw(r) = ((r >> 1) & 1) << 2 | ((r >> 2) & 3): conflict-free both for the
+// row-fragment reads (each 16-lane ds_read_b128 group reads one chunk of 16 rows: same-parity
+// rows get 8 distinct swizzles) and for the column-fragment reads (each 32-lane transpose group
+// reads 4 consecutive rows x 4 chunks: rows r and r + 2 land in opposite chunk halves).
+// Column fragments take the streamed rows in the ACCUMULATOR's order: k-step t, lane half h,
+// slot j <-> row 16 t + (j & 3) + 8 (j >> 2) + 4 h — the rows lane (n, h) holds in registers
+// 8 t .. 8 t + 7 of a 32 x 32 accumulator — so P / dS feed the second product straight from
+// registers.
+#define AS_PL (32 * 64)
+#define AS_OP (3 * AS_PL)
+typedef __attribute__((ext_vector_type(4))) short as_s16x4_t;
+
+__device__ __forceinline__ int as_sw(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
+__device__ __forceinline__ int as_off(int r, int c) { return r * 64 + ((((c >> 3) ^ as_sw(r)) & 7) << 3) + (c & 7); }
+
+struct AStage { float4 v[2]; };
+// thread t loads 8 consecutive floats: row t >> 3, columns 8 (t & 7) .. + 7 (rows >= rmax: zero)
+__device__ __forceinline__ void as_load(const float* __restrict__ base, long ss, int r0, int rmax, AStage& p) {
+  const int r = threadIdx.x >> 3, c = (threadIdx.x & 7) * 8;
+  if (r0 + r < rmax) {
+    const float* q = base + (long)(r0 + r) * ss + c;
+    p.v[0] = *(const float4*)q;
+    p.v[1] = *(const float4*)(q + 4);
+  } else {
+    p.v[0] = p.v[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+__device__ __forceinline__ void as_store(unsigned short* img, const AStage& p) {
+  const int r = threadIdx.x >> 3, c = (threadIdx.x & 7) * 8;
+  const float f[8] = {p.v[0].x, p.v[0].y, p.v[0].z, p.v[0].w, p.v[1].x, p.v[1].y, p.v[1].z, p.v[1].w};
+  const Split3 sp = split3_8(f);
+  const int o = as_off(r, c);
+  *(bf16x8_t*)(img + o) = sp.h;
+  *(bf16x8_t*)(img + AS_PL + o) = sp.m;
+  *(bf16x8_t*)(img + 2 * AS_PL + o) = sp.l;
+}
+// A operand, rows = streamed rows (lane & 31), k-step j: head dims 32 h + 8 j .. + 7 (the owned
+// operand's F32Pre order)
+__device__ __forceinline__ Split3 as_rowfrag(const unsigned short* img, int lane, int j) {
+  const int o = as_off(lane & 31, 32 * (lane >> 5) + 8 * j);
+  Split3 r;
+  r.h = *(const bf16x8_t*)(img + o);
+  r.m = *(const bf16x8_t*)(img + AS_PL + o);
+  r.l = *(const bf16x8_t*)(img + 2 * AS_PL + o);
+  return r;
+}
+// A operand, rows = head dims 32 dt + (lane & 31), k-step t over the streamed rows (accumulator order)
+__device__ __forceinline__ Split3 as_colfrag(const unsigned short* img, int lane, int dt, int t) {
+  const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4;
+  const int col = 32 * dt + 16 * (g & 1) + 4 * p;
+  const int r0 = 16 * t + 4 * (g >> 1) + q;
+  const int o0 = as_off(r0, col), o1 = as_off(r0 + 8, col);
+  Split3 r;
+  bf16x8_t* outs[3] = {&r.h, &r.m, &r.l};
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) {
+    const unsigned short* b = img + pl * AS_PL;
+    const as_s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) as_s16x4_t*)(b + o0));
+    const as_s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) as_s16x4_t*)(b + o1));
+    *outs[pl] = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+  return r;
+}
+// acc += a . b, six slice products smallest first (the XS = 1 chains' order)
+__device__ __forceinline__ f32x16_t as_mma(const Split3& a, const Split3& b, f32x16_t acc) {
+  acc = MF32X16(a.l, b.h, acc);
+  acc = MF32X16(a.m, b.m, acc);
+  acc = MF32X16(a.h, b.l, acc);
+  acc = MF32X16(a.m, b.h, acc);
+  acc = MF32X16(a.h, b.m, acc);
+  return MF32X16(a.h, b.h, acc);
+}
+// rows x owned: sum over the 64 head dims of (streamed row-fragment) x (owned split row)
+__device__ __forceinline__ f32x16_t as_rows_dot(const unsigned short* img, int lane, const F32Pre<1, 32>& own,
+                                                f32x16_t acc) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc = as_mma(as_rowfrag(img, lane, j), own.s[j], acc);
+  return acc;
+}
+// acc[dt] += (streamed columns)^T . v, v = the 16 per-lane accumulator values (split here)
+__device__ __forceinline__ void as_cols_acc(const unsigned short* img, int lane, const float (&v)[16], f32x16_t (&acc)[2]) {
+  const Split3 b0 = split3_8(&v[0]), b1 = split3_8(&v[8]);
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    acc[dt] = as_mma(as_colfrag(img, lane, dt, 0), b0, acc[dt]);
+    acc[dt] = as_mma(as_colfrag(img, lane, dt, 1), b1, acc[dt]);
+  }
+}
+
+template <int MODE, bool KPAD>
+__global__ __launch_bounds__(256, 2) void attn_sp_fwd_kernel(AttnF32Args a) {
+  __shared__ __attribute__((aligned(16))) unsigned short Ks[2][AS_OP];
+  __shared__ __attribute__((aligned(16))) unsigned short Vs[2][AS_OP];
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int qwave = blockIdx.x * 128 + w * 32;
+  const int qi = qwave + (lane & 31);
+  const float* Q = a.q + b * a.q_sb + hh * a.q_sh;
+  const float* K = a.k + b * a.k_sb + hh * a.k_sh;
+  const float* V = a.v + b * a.v_sb + hh * a.v_sh;
+  const unsigned char* kp = a.kpad ? a.kpad + (long)b * a.Sk : nullptr;
+  int kend = a.Sk;
+  if (MODE == 2) kend = min(a.Sk, blockIdx.x * 128 + 128);
+  const int nchunks = (kend + FCH - 1) / FCH;
+  AStage pk, pv;
+  as_load(K, a.k_ss, 0, a.Sk, pk);
+  as_load(V, a.v_ss, 0, a.Sk, pv);
+  F32Pre<1, 32> qs;
+  {
+    float qf[32];
+    fa_ownrow(Q, a.q_ss, qi, a.Sq, lane, qf);
+    qs.set(qf);
+  }
+  as_store(Ks[0], pk);
+  as_store(Vs[0], pv);
+  __syncthreads();
+  float m = -INFINITY, l = 0.f;
+  f32x16_t o[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1;
+    const bool more = c + 1 < nchunks;
+    if (more) { as_load(K, a.k_ss, (c + 1) * FCH, a.Sk, pk); as_load(V, a.v_ss, (c + 1) * FCH, a.Sk, pv); }
+    const unsigned long long kmask = KPAD ? chunk_pad_mask(kp, c * FCH, a.Sk) : 0ull;
+    do {
+      const int k0 = c * FCH;
+      float ub;
+      const bool full = k0 + 32 <= a.Sk;
+      const bool uni = uniform_bias<MODE, KPAD, 32>(k0, qwave, qwave + 31, full, ub);
+      if (uni && ub == -INFINITY) break;
+      f32x16_t s;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[r] = 0.f;
+      s = as_rows_dot(Ks[buf], lane, qs, s);  // S^T = K Q^T: key rows, query on the lane
+      float cmax = -INFINITY;
+      if (uni) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cmax = fmaxf(cmax, s[r]);
+        cmax = cmax * a.scale_log2 + ub;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kl = fa_kl(r, h);
+          s[r] = score_adj<MODE, KPAD>(s[r], qi, k0 + kl, kl, full, a.Sk, kmask, a.scale_log2);
+          cmax = fmaxf(cmax, s[r]);
+        }
+      }
+      cmax = smi_row32_swap_max(cmax);
+      const float mnew = fmaxf(m, cmax);
+      const float mref = (mnew == -INFINITY) ? 0.f : mnew;
+      const float alpha = __builtin_amdgcn_exp2f(m - mref);
+      float psum = 0.f;
+      float pv16[16];
+      if (uni) {
+        const float off = ub - mref;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { pv16[r] = __builtin_amdgcn_exp2f(fmaf(s[r], a.scale_log2, off)); psum += pv16[r]; }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { pv16[r] = __builtin_amdgcn_exp2f(s[r] - mref); psum += pv16[r]; }
+      }
+      psum = smi_row32_swap_sum(psum);
+      l = l * alpha + psum;
+      m = mnew;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) o[dt] *= alpha;
+      as_cols_acc(Vs[buf], lane, pv16, o);  // O^T += V^T P^T
+    } while (0);
+    if (more) { as_store(Ks[buf ^ 1], pk); as_store(Vs[buf ^ 1], pv); }
+    __syncthreads();
+  }
+  if (qi < a.Sq) {
+    float* O = a.o + b * a.o_sb + hh * a.o_sh + (long)qi * a.o_ss;
+    const float inv = l > 0.f ? 1.0f / l : 0.f;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) fa_store_rowT(O + dt * 32, o[dt], lane, inv);
+    if (a.op) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) fa_store_rowT_planes(a.op + (O - a.o) + dt * 32, a.op_ps, o[dt], lane, inv);
+    }
+    if (h == 0) {
+      const float mref = (m == -INFINITY) ? 0.f : m;
+      a.lse[((long)b * a.H + hh) * a.Sq + qi] = l > 0.f ? mref + log2f(l) : INFINITY;
+    }
+  }
+}
+
+template <int MODE, bool KPAD>
+__global__ __launch_bounds__(256, 2) void attn_sp_dq_kernel(AttnF32Args a) {
+  __shared__ __attribute__((aligned(16))) unsigned short Ks[2][AS_OP];
+  __shared__ __attribute__((aligned(16))) unsigned short Vs[2][AS_OP];
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int qwave = blockIdx.x * 128 + w * 32;
+  const int qi = qwave + (lane & 31);
+  const float* Q = a.q + b * a.q_sb + hh * a.q_sh;
+  const float* K = a.k + b * a.k_sb + hh * a.k_sh;
+  const float* V = a.v + b * a.v_sb + hh * a.v_sh;
+  const float* dO = a.dout + b * a.o_sb + hh * a.o_sh;
+  const float* Og = a.o + b * a.o_sb + hh * a.o_sh;
+  const unsigned char* kp = a.kpad ? a.kpad + (long)b * a.Sk : nullptr;
+  int kend = a.Sk;
+  if (MODE == 2) kend = min(a.Sk, blockIdx.x * 128 + 128);
+  const int nchunks = (kend + FCH - 1) / FCH;
+  AStage pk, pv;
+  as_load(K, a.k_ss, 0, a.Sk, pk);
+  as_load(V, a.v_ss, 0, a.Sk, pv);
+  F32Pre<1, 32> qs, ds;
+  float dl;
+  {
+    float qf[32], df[32], of[32];
+    fa_ownrow(Q, a.q_ss, qi, a.Sq, lane, qf);
+    fa_ownrow(dO, a.o_ss, qi, a.Sq, lane, df);
+    fa_ownrow(Og, a.o_ss, qi, a.Sq, lane, of);
+    qs.set(qf);
+    ds.set(df);
+    float sacc = 0.f;
+#pragma unroll
+    for (int t = 0; t < 32; ++t) sacc = fmaf(df[t], of[t], sacc);
+    dl = smi_row32_swap_sum(sacc);
+  }
+  const long rbase = ((long)b * a.H + hh) * a.Sq;
+  if (h == 0 && qi < a.Sq) a.delta[rbase + qi] = dl;
+  const float lse = qi < a.Sq ? a.lse[rbase + qi] : INFINITY;
+  as_store(Ks[0], pk);
+  as_store(Vs[0], pv);
+  __syncthreads();
+  f32x16_t acc[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[dt][r] = 0.f;
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1;
+    const bool more = c + 1 < nchunks;
+    if (more) { as_load(K, a.k_ss, (c + 1) * FCH, a.Sk, pk); as_load(V, a.v_ss, (c + 1) * FCH, a.Sk, pv); }
+    const unsigned long long kmask = KPAD ? chunk_pad_mask(kp, c * FCH, a.Sk) : 0ull;
+    do {
+      const int k0 = c * FCH;
+      float ub;
+      const bool full = k0 + 32 <= a.Sk;
+      const bool uni = uniform_bias<MODE, KPAD, 32>(k0, qwave, qwave + 31, full, ub);
+      if (uni && ub == -INFINITY) break;
+      f32x16_t s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+      s = as_rows_dot(Ks[buf], lane, qs, s);   // S^T = K Q^T
+      dp = as_rows_dot(Vs[buf], lane, ds, dp);  // dP^T = V dO^T
+      float dsv[16];
+      if (uni) {
+        const float off = ub - lse;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dsv[r] = __builtin_amdgcn_exp2f(fmaf(s[r], a.scale_log2, off)) * (dp[r] - dl);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kl = fa_kl(r, h);
+          const float x = score_adj<MODE, KPAD>(s[r], qi, k0 + kl, kl, full, a.Sk, kmask, a.scale_log2);
+          dsv[r] = __builtin_amdgcn_exp2f(x - lse) * (dp[r] - dl);  // exp2(-inf) = 0 for masked entries
+        }
+      }
+      as_cols_acc(Ks[buf], lane, dsv, acc);  // dQ^T += K^T dS^T
+    } while (0);
+    if (more) { as_store(Ks[buf ^ 1], pk); as_store(Vs[buf ^ 1], pv); }
+    __syncthreads();
+  }
+  if (qi < a.Sq) {
+    float* dQ = a.dq + b * a.q_sb + hh * a.q_sh + (long)qi * a.q_ss;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) fa_store_rowT(dQ + dt * 32, acc[dt], lane, a.scale);
+    if (a.dqp) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) fa_store_rowT_planes(a.dqp + (dQ - a.dq) + dt * 32, a.dq_ps, acc[dt], lane, a.scale);
+    }
+  }
+}
+
+// one workgroup per CU: owned K and V splits (96 registers) + two accumulator pairs + the P / dS
+// splits exceed 256 registers (two workgroups per CU spilled 34)
+template <int MODE, bool KPAD>
+__global__ __launch_bounds__(256, 1) void attn_sp_dkdv_kernel(AttnF32Args a) {
+  __shared__ __attribute__((aligned(16))) unsigned short Qs[2][AS_OP];
+  __shared__ __attribute__((aligned(16))) unsigned short Ds[2][AS_OP];
+  __shared__ float lse_s[2][FCH], dl_s[2][FCH];
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int kwave = blockIdx.x * 128 + w * 32;
+  const int kj = kwave + (lane & 31);
+  const float* Q = a.q + b * a.q_sb + hh * a.q_sh;
+  const float* K = a.k + b * a.k_sb + hh * a.k_sh;
+  const float* V = a.v + b * a.v_sb + hh * a.v_sh;
+  const float* dO = a.dout + b * a.o_sb + hh * a.o_sh;
+  const long rbase = ((long)b * a.H + hh) * a.Sq;
+  int qstart = 0;
+  if (MODE == 2) qstart = (blockIdx.x * 128) & ~(FCH - 1);
+  const int nchunks = qstart < a.Sq ? (a.Sq - qstart + FCH - 1) / FCH : 0;
+  AStage pq, pd;
+  float lse_r = INFINITY, dl_r = 0.f;
+  if (nchunks) {
+    as_load(Q, a.q_ss, qstart, a.Sq, pq);
+    as_load(dO, a.o_ss, qstart, a.Sq, pd);
+    if (threadIdx.x < FCH && qstart + (int)threadIdx.x < a.Sq) {
+      lse_r = a.lse[rbase + qstart + threadIdx.x];
+      dl_r = a.delta[rbase + qstart + threadIdx.x];
+    }
+  }
+  F32Pre<1, 32> ks, vs;
+  {
+    float kf[32], vf[32];
+    fa_ownrow(K, a.k_ss, kj, a.Sk, lane, kf);
+    fa_ownrow(V, a.v_ss, kj, a.Sk, lane, vf);
+    ks.set(kf);
+    vs.set(vf);
+  }
+  const bool kok = kj < a.Sk && !(KPAD && a.kpad[(long)b * a.Sk + kj]);
+  const float kbias = kok ? 0.f : -INFINITY;
+  f32x16_t dk[2], dv[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
+  if (nchunks) {
+    as_store(Qs[0], pq);
+    as_store(Ds[0], pd);
+    if (threadIdx.x < FCH) { lse_s[0][threadIdx.x] = lse_r; dl_s[0][threadIdx.x] = dl_r; }
+  }
+  __syncthreads();
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1, q0 = qstart + c * FCH;
+    const bool more = c + 1 < nchunks;
+    if (more) {
+      as_load(Q, a.q_ss, q0 + FCH, a.Sq, pq);
+      as_load(dO, a.o_ss, q0 + FCH, a.Sq, pd);
+      lse_r = INFINITY; dl_r = 0.f;
+      if (threadIdx.x < FCH && q0 + FCH + (int)threadIdx.x < a.Sq) {
+        lse_r = a.lse[rbase + q0 + FCH + threadIdx.x];
+        dl_r = a.delta[rbase + q0 + FCH + threadIdx.x];
+      }
+    }
+    do {
+      if (MODE == 2 && q0 + 31 < kwave) break;  // every query of the block before every key
+      f32x16_t s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+      s = as_rows_dot(Qs[buf], lane, ks, s);   // S = Q K^T: query rows, key on the lane
+      dp = as_rows_dot(Ds[buf], lane, vs, dp);  // dP = dO V^T
+      float pvv[16], dsv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ql = fa_kl(r, h);
+        const int qq = q0 + ql;
+        float x = fmaf(s[r], a.scale_log2, kbias);
+        if (MODE == 1) x += (kj < qq) ? LOG2E_F : 0.f;
+        if (MODE == 2) x = (kj > qq) ? -INFINITY : x;
+        const float pr = __builtin_amdgcn_exp2f(x - lse_s[buf][ql]);  // rows past Sq: lse = +inf -> 0
+        pvv[r] = pr;
+        dsv[r] = pr * (dp[r] - dl_s[buf][ql]);
+      }
+      as_cols_acc(Ds[buf], lane, pvv, dv);  // dV^T += dO^T P
+      as_cols_acc(Qs[buf], lane, dsv, dk);  // dK^T += Q^T dS
+    } while (0);
+    if (more) {
+      as_store(Qs[buf ^ 1], pq);
+      as_store(Ds[buf ^ 1], pd);
+      if (threadIdx.x < FCH) { lse_s[buf ^ 1][threadIdx.x] = lse_r; dl_s[buf ^ 1][threadIdx.x] = dl_r; }
+    }
+    __syncthreads();
+  }
+  if (kj < a.Sk) {
+    float* dK = a.dk + b * a.k_sb + hh * a.k_sh + (long)kj * a.k_ss;
+    float* dV = a.dv + b * a.v_sb + hh * a.v_sh + (long)kj * a.v_ss;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      fa_store_rowT(dK + dt * 32, dk[dt], lane, a.scale);
+      fa_store_rowT(dV + dt * 32, dv[dt], lane, 1.0f);
+    }
+    if (a.dkp) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        fa_store_rowT_planes(a.dkp + (dK - a.dk) + dt * 32, a.dkv_ps, dk[dt], lane, a.scale);
+        fa_store_rowT_planes(a.dvp + (dV - a.dv) + dt * 32, a.dkv_ps, dv[dt], lane, 1.0f);
+      }
+    }
+  }
+}
+
+// staged-plane kernels on (default) / off (SMI_ATTN_SP=0: the XS kernels above)
+static int g_attn_sp = -1;
+extern "C" int smi_attn_f32_sp(int set) {
+  if (set == 0 || set == 1) g_attn_sp = set;
+  if (g_attn_sp < 0) {
+    const char* e = getenv("SMI_ATTN_SP");
+    g_attn_sp = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_attn_sp;
+}
+#define SMI_ATTN_SP_MODES(KERNEL, GRID, ARGS)                                                            \
+  do {                                                                                                   \
+    const bool kp_ = (ARGS).kpad != nullptr;                                                             \
+    switch ((ARGS).mode) {                                                                               \
+      case 0: if (kp_) hipLaunchKernelGGL((KERNEL<0, true>), GRID, dim3(256), 0, st, ARGS);              \
+              else hipLaunchKernelGGL((KERNEL<0, false>), GRID, dim3(256), 0, st, ARGS); break;          \
+      case 1: if (kp_) hipLaunchKernelGGL((KERNEL<1, true>), GRID, dim3(256), 0, st, ARGS);              \
+              else hipLaunchKernelGGL((KERNEL<1, false>), GRID, dim3(256), 0, st, ARGS); break;          \
+      case 2: if (kp_) hipLaunchKernelGGL((KERNEL<2, true>), GRID, dim3(256), 0, st, ARGS);              \
+              else hipLaunchKernelGGL((KERNEL<2, false>), GRID, dim3(256), 0, st, ARGS); break;          \
+      default: return -1;                                                                                \
+    }                                                                                                    \
+  } while (0)
+
 // product algorithm shared with the fp32 GEMM (csrc/kernels/gemm_f32.hip:smi_gemm_f32_algo):
 // 0 = f32 MFMA chains, otherwise the exact-product bf16 split (smi_split3.h)
 extern "C" int smi_gemm_f32_algo(int);
@@ -489,7 +916,8 @@ extern "C" int smi_attn_f32_fwd(const AttnF32Args* args, hipStream_t st) {
   const AttnF32Args& a = *args;
   if (!fa_ok(a)) return -1;
   dim3 grid((a.Sq + 127) / 128, a.H, a.B);
-  SMI_ATTN_F32_DISPATCH(attn_f32_fwd_kernel, grid, a);
+  if (smi_gemm_f32_algo(-1) != 0 && smi_attn_f32_sp(-1)) SMI_ATTN_SP_MODES(attn_sp_fwd_kernel, grid, a);
+  else SMI_ATTN_F32_DISPATCH(attn_f32_fwd_kernel, grid, a);
   SMI_CHECK_LAUNCH();
 }
 
@@ -497,7 +925,12 @@ extern "C" int smi_attn_f32_bwd(const AttnF32Args* args, hipStream_t st) {
   const AttnF32Args& a = *args;
   if (!fa_ok(a) || !a.dout || !a.delta || (((uintptr_t)a.dout | (uintptr_t)a.dq | (uintptr_t)a.dk | (uintptr_t)a.dv) & 15))
     return -1;
-  SMI_ATTN_F32_DISPATCH(attn_f32_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), a);
-  SMI_ATTN_F32_DISPATCH(attn_f32_dkdv_kernel, dim3((a.Sk + 127) / 128, a.H, a.B), a);
+  if (smi_gemm_f32_algo(-1) != 0 && smi_attn_f32_sp(-1)) {
+    SMI_ATTN_SP_MODES(attn_sp_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), a);
+    SMI_ATTN_SP_MODES(attn_sp_dkdv_kernel, dim3((a.Sk + 127) / 128, a.H, a.B), a);
+  } else {
+    SMI_ATTN_F32_DISPATCH(attn_f32_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), a);
+    SMI_ATTN_F32_DISPATCH(attn_f32_dkdv_kernel, dim3((a.Sk + 127) / 128, a.H, a.B), a);
+  }
   SMI_CHECK_LAUNCH();
 }

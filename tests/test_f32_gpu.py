@@ -238,14 +238,25 @@ def _attn_f32(B, H, Sq, Sk, mode, cross, kp):
         _close(qg.grad, dqkv, 5e-5, 1e-5, f"dqkv {mode}")
 
 
+@pytest.fixture(params=[1, 0], ids=["staged_planes", "wave_split"])
+def attn_kernel(request):
+    """The split-product attention kernels: streamed chunks split once at LDS staging (default)
+    or per wave per fragment (C.attn_f32_sp(0)); irrelevant under the f32-MFMA algorithm."""
+    C = _native.C()
+    prev = C.attn_f32_sp(-1)
+    C.attn_f32_sp(request.param)
+    yield request.param
+    C.attn_f32_sp(prev)
+
+
 @pytest.mark.parametrize("mode", ["none", "reference", "causal"])
 @pytest.mark.parametrize("S", [256, 200, 37])
-def test_self_attention_f32(mode, S):
+def test_self_attention_f32(attn_kernel, mode, S):
     _attn_f32(2, 4, S, S, mode, False, False)
 
 
 @pytest.mark.parametrize("mode,kp", [("none", False), ("none", True), ("reference", False)])
-def test_cross_attention_f32(mode, kp):
+def test_cross_attention_f32(attn_kernel, mode, kp):
     _attn_f32(2, 3, 130, 130 if mode == "reference" else 77, mode, True, kp)
 
 
