@@ -15,12 +15,14 @@ struct LSTMArgs {
   const float* w_fc; const float* b_fc;    // [C][H], [C]
   const float* h0; const float* c0;        // [L][B][H] (null: zeros)
   float* pred;                             // [B][T][C]
+  float* pred_last;                        // [B][C]: the last step's prediction again (or null)
   float* hn; float* cn;                    // [L][B][H]
   float* ws;                               // saved activations [B][L][T][6H] (i,f,g,o,c,h)
   float* ws_da;                            // gate grads [B][L][T][4H] (backward scratch)
   const uint32_t* seedp; uint32_t salt; uint32_t thresh; float dscale;  // inter-layer dropout
   // backward
   const float* dpred; const float* dhn; const float* dcn;
+  int dpred_last;                          // 1: dpred is [B][C], the last step's only (others zero)
   float* g_emb; float* g_w_ih[LSTM_MAXL]; float* g_w_hh[LSTM_MAXL];
   float* g_b_ih[LSTM_MAXL]; float* g_b_hh[LSTM_MAXL];
   float* g_w_fc; float* g_b_fc;

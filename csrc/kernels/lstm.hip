@@ -161,6 +161,7 @@ __global__ __launch_bounds__(NT) void lstm_fwd_kernel(LSTMArgs a) {
           s1 += s_wfc[cc * H + j + 1] * s_top[t * H + j + 1];
         }
         a.pred[((size_t)b * T + t0 + t) * C + cc] = s0 + s1;
+        if (a.pred_last && t0 + t == T - 1) a.pred_last[(size_t)b * C + cc] = s0 + s1;
       }
     }
   }
@@ -219,7 +220,8 @@ __global__ __launch_bounds__(NT) void lstm_bwd_kernel(LSTMArgs a) {
 
   const uint32_t seed = smi_seed(a.seedp, a.salt);
   const float* wsb = a.ws + (size_t)b * L * T * 6 * H;
-  const float* dpred = a.dpred + (size_t)b * T * C;
+  // dpred_last: only the last step's head gradient exists ([B][C]; the loss reads pred[:, -1])
+  const float* dpred = a.dpred + (size_t)b * (a.dpred_last ? 1 : T) * C;
   float* dab = a.ws_da + (size_t)b * L * T * G;  // gate gradients of every layer [L][T][4H]
   const int nt = T + L - 1;
   const int tl = T - 1 + (L - 1 - l);  // this layer's step at tick k is tl - k
@@ -231,7 +233,8 @@ __global__ __launch_bounds__(NT) void lstm_bwd_kernel(LSTMArgs a) {
     v.cp = t > 0 ? w[j - 2 * H] : (a.c0 ? a.c0[((size_t)l * a.B + b) * H + j] : 0.f);
     if (top) {
 #pragma unroll
-      for (int q = 0; q < CM; ++q) v.dp[q] = q < C ? dpred[(size_t)t * C + q] : 0.f;
+      for (int q = 0; q < CM; ++q)
+        v.dp[q] = (q < C && (!a.dpred_last || t == T - 1)) ? dpred[(size_t)(a.dpred_last ? 0 : t) * C + q] : 0.f;
     }
   };
   // everything of step t's cell backward that does not depend on the incoming dh / dc
@@ -385,8 +388,11 @@ __global__ __launch_bounds__(256) void lstm_wgrad_partial(LSTMArgs a) {
         const long bt = kb + kk;
         const int b = (int)(bt / T), t = (int)(bt % T);
         float v = 0.f;
-        if (rr < nr) v = l < L ? a.ws_da[(((size_t)b * L + l) * T + t) * G + r0 + rr]
-                               : a.dpred[((size_t)b * T + t) * C + r0 + rr];
+        if (rr < nr) {
+          if (l < L) v = a.ws_da[(((size_t)b * L + l) * T + t) * G + r0 + rr];
+          else if (!a.dpred_last) v = a.dpred[((size_t)b * T + t) * C + r0 + rr];
+          else v = t == T - 1 ? a.dpred[(size_t)b * C + r0 + rr] : 0.f;
+        }
         s_d[kk][rr] = v;
       }
       for (int i = tid; i < nk * LSTM_WC; i += 256) {

@@ -17,7 +17,7 @@ import torch
 from torch import nn
 
 from ..ops import rng as _rng
-from ..ops.lstm import lstm_classifier
+from ..ops.lstm import lstm_classifier, lstm_classifier_last
 from ..ops.loss import cross_entropy
 
 
@@ -53,11 +53,12 @@ class LSTM(nn.Module):
 
     def loss(self, input_seq, labels, hidden_in=None, mem_in=None):
         """CE on the last step's prediction (distributed_lstm.py:186-189); returns (loss, pred)."""
-        pred, _, _ = self(input_seq, hidden_in, mem_in)
-        last = pred[:, -1, :]
+        last, _, _, _ = lstm_classifier_last(input_seq, hidden_in, mem_in, self.param_list(), self.num_layers,
+                                             dropout=self.dropout_p, training=self.training, rng=self.rng,
+                                             salt=self.salt, padding_idx=self.padding_idx)
         # sparkmi's CE kernel (csrc/kernels/cross_entropy.hip: fixed-order loss sum) instead of the
         # ATen softmax / nll_loss launches; the CPU path falls back to the same math in torch
-        return cross_entropy(last.contiguous(), labels), last
+        return cross_entropy(last, labels), last
 
 
 TextClassifierLSTM = LSTM

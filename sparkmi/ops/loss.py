@@ -24,14 +24,14 @@ class CrossEntropyFn(torch.autograd.Function):
             C = _native.C()
             x2 = x2.contiguous()
             lse = torch.empty(M, device=x2.device, dtype=torch.float32)
-            stats = torch.empty(2, device=x2.device, dtype=torch.float32)  # [count, loss]
+            stats = torch.empty(1, device=x2.device, dtype=torch.float32)  # valid-row count
+            loss = torch.empty((), device=x2.device, dtype=torch.float32)  # its own buffer: no copy kernel
             row_loss = torch.empty(M, device=x2.device, dtype=torch.float32)
             C.ce_fwd(x2.data_ptr(), int(x2.dtype == torch.bfloat16), lab.data_ptr(), M, V, ignore_index,
-                     lse.data_ptr(), stats[0:1].data_ptr(), stats[1:2].data_ptr(), row_loss.data_ptr(),
-                     _native.stream())
+                     lse.data_ptr(), stats.data_ptr(), loss.data_ptr(), row_loss.data_ptr(), _native.stream())
             ctx.save_for_backward(x2, lab, lse, stats)
             ctx.shape = logits.shape
-            return stats[1].clone()
+            return loss
         xf = x2.float()
         lse = torch.logsumexp(xf, dim=-1)
         valid = lab != ignore_index

@@ -61,6 +61,7 @@ def supported(E, H, L, C):
 class LSTMFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ids, h0, c0, meta, *params):
+        ctx.set_materialize_grads(False)  # unused outputs get no zero-filled gradients
         L, p, rng, salt, pad_idx = meta
         emb, layers, w_fc, b_fc = unpack(params, L)
         B, T = ids.shape
@@ -70,6 +71,7 @@ class LSTMFn(torch.autograd.Function):
         if not all(t.is_contiguous() and t.dtype == torch.float32 for t in params):
             raise ValueError("LSTM parameters must be contiguous fp32")
         pred = torch.empty(B, T, C, device=dev, dtype=torch.float32)
+        last = torch.empty(B, C, device=dev, dtype=torch.float32)  # pred[:, -1] written by the kernel too
         hn = torch.empty(L, B, H, device=dev, dtype=torch.float32)
         cn = torch.empty_like(hn)
         ws = torch.empty(B, L, T, 6 * H, device=dev, dtype=torch.float32)
@@ -81,19 +83,31 @@ class LSTMFn(torch.autograd.Function):
                          [lw[2].data_ptr() for lw in layers], [lw[3].data_ptr() for lw in layers],
                          w_fc.data_ptr(), b_fc.data_ptr(), _native.ptr(h0c), _native.ptr(c0c), pred.data_ptr(),
                          hn.data_ptr(), cn.data_ptr(), ws.data_ptr(), 0, rng.ptr() if rng is not None else 0, salt,
-                         thresh, _rng.scale(p), 0, 0, 0, 0, [], [], [], [], 0, 0, 0, 0, 0, 0, 0, 0, _native.stream())
+                         thresh, _rng.scale(p), 0, 0, 0, 0, [], [], [], [], 0, 0, 0, 0, 0, 0, 0, 0,
+                         last.data_ptr(), 0, _native.stream())
         ctx.meta = (L, p, rng, salt, pad_idx, B, T, E, H, C)
         ctx.has_h0, ctx.has_c0 = h0 is not None, c0 is not None
         ctx.save_for_backward(ids, ws, h0c, c0c, *params)
-        return pred, hn, cn
+        return pred, hn, cn, last
 
     @staticmethod
-    def backward(ctx, dpred, dhn, dcn):
+    def backward(ctx, dpred, dhn, dcn, dlast):
         L, p, rng, salt, pad_idx, B, T, E, H, C = ctx.meta
         ids, ws, h0c, c0c, *params = ctx.saved_tensors
         emb, layers, w_fc, b_fc = unpack(params, L)
         dev = ids.device
-        dpred = dpred.float().contiguous() if dpred is not None else torch.zeros(B, T, C, device=dev)
+        # the classifier's loss reads only the last step: hand the kernel that [B, C] gradient
+        # (no zero-filled [B, T, C] tensor, no scatter); a full dpred (+ dlast) takes the general path
+        last_only = 0
+        if dpred is None and dlast is not None:
+            dpred, last_only = dlast.float().contiguous(), 1
+        elif dpred is None:
+            dpred = torch.zeros(B, T, C, device=dev)
+        else:
+            dpred = dpred.float().contiguous()
+            if dlast is not None:
+                dpred = dpred.clone()
+                dpred[:, -1] += dlast.float()
         dhn = dhn.float().contiguous() if dhn is not None else None
         dcn = dcn.float().contiguous() if dcn is not None else None
         ws_da = torch.empty(B, L, T, 4 * H, device=dev, dtype=torch.float32)
@@ -117,7 +131,7 @@ class LSTMFn(torch.autograd.Function):
                          [lw[0].data_ptr() for lw in g_layers], [lw[1].data_ptr() for lw in g_layers],
                          [lw[2].data_ptr() for lw in g_layers], [lw[3].data_ptr() for lw in g_layers],
                          g_fc.data_ptr(), g_bfc.data_ptr(), _native.ptr(dh0), _native.ptr(dc0), slab.data_ptr(),
-                         _native.ptr(xe), emb.shape[0], _native.ptr(ews), _native.stream())
+                         _native.ptr(xe), emb.shape[0], _native.ptr(ews), 0, last_only, _native.stream())
         grad_ready(*orig)
         return (None, dh0 if ctx.has_h0 else None, dc0 if ctx.has_c0 else None, None) + (None,) * len(params)
 
@@ -133,6 +147,22 @@ def lstm_classifier(ids, h0, c0, params, num_layers, dropout=0.0, training=True,
             raise NotImplementedError(f"sparkmi LSTM kernel: unsupported shape E={E} H={H} L={num_layers} C={C} "
                                       "(H in {16,32,64}, 4*H*L <= 512, E <= 2H and <= 64, C <= 16)")
         pad = -1 if padding_idx is None else int(padding_idx)
-        return LSTMFn.apply(ids, h0, c0, (num_layers, p, rng, salt, pad), *params)
+        pred, hn, cn, _ = LSTMFn.apply(ids, h0, c0, (num_layers, p, rng, salt, pad), *params)
+        return pred, hn, cn
     seed = rng.current() if (rng is not None and p > 0) else 0
     return reference_forward(ids, h0, c0, params, num_layers, p, seed, salt, padding_idx)
+
+
+def lstm_classifier_last(ids, h0, c0, params, num_layers, dropout=0.0, training=True, rng=None, salt=0,
+                         padding_idx=None):
+    """(pred[:, -1] contiguous, pred, h_n, c_n): the GPU kernel writes the last step's prediction
+    as its own output, so a loss on it needs no slice copy and its backward no zero-filled dpred."""
+    p = dropout if training else 0.0
+    emb, layers, w_fc, _ = unpack(params, num_layers)
+    E, H, C = emb.shape[1], layers[0][1].shape[1], w_fc.shape[0]
+    if ids.is_cuda and _native.use_native(ids) and supported(E, H, num_layers, C):
+        pad = -1 if padding_idx is None else int(padding_idx)
+        pred, hn, cn, last = LSTMFn.apply(ids, h0, c0, (num_layers, p, rng, salt, pad), *params)
+        return last, pred, hn, cn
+    pred, hn, cn = lstm_classifier(ids, h0, c0, params, num_layers, dropout, training, rng, salt, padding_idx)
+    return pred[:, -1, :].contiguous(), pred, hn, cn
