@@ -401,6 +401,74 @@ __device__ __forceinline__ void conv_mfma(const float* __restrict__ in, int nin,
   }
 }
 
+
+// bf16 weight gradient (the bf16 path): the same GEMM D[co][n] = sum_pos dz[co][pos] X[pos][n] on
+// v_mfma_f32_16x16x32_bf16 (fp32 accumulation), summed over the PADDED position index q (rows of
+// the halo plane, halo columns included: dz is zero there), so a lane's 8 positions of a 32-deep
+// k-step are 8 CONSECUTIVE floats — dz by 4 ds_read_b64, the im2col column by 8 ds_read_b32 at one
+// base — instead of one scalar gather per position (the fp32 16x16x4 form: 2 gathers per 4
+// positions, LDS-issue bound).  q covers [PP, PP + 32 KS) — every interior position; an im2col
+// index below 0 (the first position, a halo one: dz = 0 there) is clamped to 0, indices past the
+// plane read the next buffer's finite values (times dz = 0).
+template <int H, int PP>
+__device__ __forceinline__ void conv_wgrad_bf16(const float* __restrict__ dz, const float* __restrict__ in, int cin, int cout,
+                                                float* __restrict__ acc, float* __restrict__ scratch) {
+  constexpr int KS = (H * PP + H - PP + 1 + 31) / 32;  // 32-position k-steps
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
+  const int ncol = cin * 9 + 1;
+  const int nt = (ncol + 15) >> 4;
+  const int nch = max(1, min(min(nw, WG_SCRATCH / 256) / nt, KS));
+  const int units = nt * nch;
+  const int i = lane & 15, g = lane >> 4;
+  const bool aok = i < cout;
+  const float* pa = dz + (aok ? i : 0) * PP * PP;
+  for (int u = wv; u < units; u += nw) {
+    const int t = u % nt, ch = u / nt;
+    const int n = t * 16 + i;  // this lane's B column
+    const int mode = n < cin * 9 ? 0 : (n == cin * 9 ? 1 : 2);  // gather / bias ones / padding zeros
+    int boff = 0;
+    if (mode == 0) {
+      const int ci = n / 9, k = n - ci * 9;
+      boff = ci * PP * PP + (k / 3 - 1) * PP + (k % 3 - 1);
+    }
+    const int s0 = ch * KS / nch, s1 = (ch + 1) * KS / nch;
+    f32x4_t d = {0.f, 0.f, 0.f, 0.f};
+    for (int s = s0; s < s1; ++s) {
+      const int q = PP + 32 * s + 8 * g;
+      float av[8], bv[8];
+      if (aok) {
+        const f2* ap = (const f2*)(pa + q);  // q even, plane bases 8-B aligned
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { const f2 v = ap[e]; av[2 * e] = v.x; av[2 * e + 1] = v.y; }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) av[e] = 0.f;
+      }
+      if (mode == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bv[e] = in[max(boff + q + e, 0)];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bv[e] = mode == 1 ? 1.f : 0.f;
+      }
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cnn_pack8(av), cnn_pack8(bv), d, 0, 0, 0);
+    }
+    float* row = scratch + u * 256;  // [co 16][col 16]: lane holds rows 4 g + r, column i
+#pragma unroll
+    for (int r = 0; r < 4; ++r) row[(g * 4 + r) * 16 + i] = d[r];
+  }
+  __syncthreads();
+  const int nwt = cout * cin * 9;
+  for (int e = threadIdx.x; e < nwt + cout; e += blockDim.x) {
+    const int co = e < nwt ? e / (cin * 9) : e - nwt;
+    const int col = e < nwt ? e - co * cin * 9 : cin * 9;
+    const int tt = col >> 4, j = col & 15;
+    float v = 0.f;
+    for (int c = 0; c < nch; ++c) v += scratch[(c * nt + tt) * 256 + co * 16 + j];
+    acc[e] = v;
+  }
+}
+
 // CC: channel capacity; EX: g.C == CC exactly (compile-time channel count, no clamps)
 template <int CC, bool EX, bool BF>
 __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
@@ -525,7 +593,8 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   __syncthreads();
   STAMP(12);
   // conv4: dW4, db4 (from dz4, a3); then dz3 = convT(dz4) * relu'(a3) in a3
-  conv_wgrad<14, P14>(a4, a3, C, C, wacc, wscr, 25);
+  if (BF) conv_wgrad_bf16<14, P14>(a4, a3, C, C, wacc, wscr);
+  else conv_wgrad<14, P14>(a4, a3, C, C, wacc, wscr, 25);
   __syncthreads();
   STAMP(13);
   for (int e = threadIdx.x; e < C * C * 9 + C; e += blockDim.x) {
@@ -537,7 +606,8 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   __syncthreads();
   STAMP(14);
   // conv3: dW3 (dz3, p1); dp1 = convT(dz3) into p1 (no relu: p1 is a pool output)
-  conv_wgrad<14, P14>(a3, p1, C, C, wacc, wscr);
+  if (BF) conv_wgrad_bf16<14, P14>(a3, p1, C, C, wacc, wscr);
+  else conv_wgrad<14, P14>(a3, p1, C, C, wacc, wscr);
   __syncthreads();
   STAMP(15);
   for (int e = threadIdx.x; e < C * C * 9 + C; e += blockDim.x) {
@@ -553,7 +623,8 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   __syncthreads();
   STAMP(17);
   // conv2: dW2 (dz2, a1); dz1 = convT(dz2) * relu'(a1) in a1
-  conv_wgrad<28, P28>(a2, a1, C, C, wacc, wscr, 21);
+  if (BF) conv_wgrad_bf16<28, P28>(a2, a1, C, C, wacc, wscr);
+  else conv_wgrad<28, P28>(a2, a1, C, C, wacc, wscr, 21);
   __syncthreads();
   STAMP(18);
   for (int e = threadIdx.x; e < C * C * 9 + C; e += blockDim.x) {
@@ -565,7 +636,8 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   __syncthreads();
   STAMP(19);
   // conv1: dW1 (dz1, x)
-  conv_wgrad<28, P28>(a1, xin, CI, C, wacc, wscr, 23);
+  if (BF) conv_wgrad_bf16<28, P28>(a1, xin, CI, C, wacc, wscr);
+  else conv_wgrad<28, P28>(a1, xin, CI, C, wacc, wscr, 23);
   __syncthreads();
   STAMP(20);
   for (int e = threadIdx.x; e < C * CI * 9 + C; e += blockDim.x)
