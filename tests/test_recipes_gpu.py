@@ -96,7 +96,7 @@ def test_translator_graph_dp_metrics_phases(tmp_path, monkeypatch):
     monkeypatch.setenv("SPARKMI_DIST_BACKEND", "gloo")  # RCCL needs one device per rank
     monkeypatch.setenv("SPARKMI_SHARE_GPUS", "1")       # both executors on the box's one GPU
     monkeypatch.setenv("SPARKMI_DP_COMM", "rccl")      # the process-group path, not the IPC kernel
-    r = translator.main(GPU + ["--world", "2", "--n-train", "640", "--max-steps", "12", "--d-model", "128",
+    r = translator.main(GPU + ["--world", "2", "--n-train", "640", "--epochs", "3", "--max-steps", "12", "--d-model", "128",
                                "--ffn-hidden", "256", "--num-heads", "2", "--max-sequence-length", "64",
                                "--log-every", "4", "--metrics", str(tmp_path / "m")])
     assert r["steps"] == 12 and r["world"] == 2
