@@ -78,6 +78,8 @@ def parse(argv=None):
     ap.add_argument("--data", default="random", choices=["random", "copy"],
                     help="transformer batches: random = independent uniform src/tgt (Multi30k-shaped; loss floor "
                          "ln(V-4)), copy = tgt a fixed permutation of src (learnable, same shapes)")
+    ap.add_argument("--no-zero-compare", action="store_true",
+                    help="skip the ZeRO-1 variant of the fp32 transformer step (measured only when N > 1)")
     ap.add_argument("--no-f32-compare", action="store_true",
                     help="skip the f32-MFMA comparison run of the fp32 transformer step")
     return ap.parse_args(argv)
@@ -292,7 +294,7 @@ def bench_mlp(args, rank, world, device):
             "vs_baseline": round(v / BASELINE_MLP, 2), "config": f"MLP 4-5-4-3 sigmoid, batch 30/GPU, SGD, fp32, dp{world}"}
 
 
-def bench_transformer(args, rank, world, device, dtype):
+def bench_transformer(args, rank, world, device, dtype, zero=False):
     """One full training step of the BASELINE transformer at ``dtype`` ('fp32' = reference
     precision, or 'bf16' = bf16 activations/weights with fp32 master weights and fp32 accumulate)."""
     import torch
@@ -309,7 +311,7 @@ def bench_transformer(args, rank, world, device, dtype):
     model.train()
     flat = FlatParams(model, shadow=(dtype == "bf16" and device.type == "cuda"))
     opt = Adam(flat, lr=1e-3)
-    ddp = DataParallel(flat, bucket_mb=args.bucket_mb) if world > 1 else None
+    ddp = DataParallel(flat, bucket_mb=args.bucket_mb, zero=zero) if world > 1 else None
     use_graph = args.graph != "off" and device.type == "cuda"
     # data-parallel: backward in several graphs (decoder, then encoder halves) so the finished
     # gradient buckets are all-reduced while the rest of the backward runs (sparkmi/train/runner.py)
@@ -342,7 +344,7 @@ def bench_transformer(args, rank, world, device, dtype):
            f"mfu_vs_{'157tf_fp32' if dtype == 'fp32' else '2.5pf_bf16'}_dense": round(tflops / peak, 3),
            "allreduce_ms": ar, "grad_bytes": flat.numel * 4, "dtype": dtype,
            "overlap": "finished buckets all-reduced under the rest of the backward" if split_fn else None,
-           "hip_graph": use_graph}
+           "hip_graph": use_graph, "zero1": bool(zero and world > 1)}
     if dtype == "fp32":
         # the algorithm the step actually runs: 6 bf16 products per fp32 product
         res["mfu_vs_417tf_split3_ceiling"] = round(tflops / SPLIT_PEAK_TF, 3)
@@ -413,6 +415,11 @@ def main():
         finally:
             C.gemm_f32_algo(prev)
             G.SP = prev_sp
+    zero1 = None
+    if world > 1 and "fp32" in dtypes and not args.no_zero_compare:
+        # ZeRO-1 beside the headline (reduce-scatter under the backward, sharded Adam, parameter
+        # all-gather after it): measured at every N so the replicated-vs-sharded choice rests on data
+        zero1 = bench_transformer(args, rank, world, device, "fp32", zero=True)
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -445,6 +452,8 @@ def main():
             out[f"transformer_{dt}"] = tr[dt]
         if f32mfma is not None:
             out["transformer_fp32_f32mfma"] = f32mfma
+        if zero1 is not None:
+            out["transformer_fp32_zero1"] = zero1
         if cnn is not None:
             out["cnn"] = cnn
             out["cnn_fp32"] = cnn32
