@@ -340,6 +340,290 @@ __global__ __launch_bounds__(NT) void lstm_bwd_kernel(LSTMArgs a) {
 
 }
 
+// ---- two-wave recurrence (L * H <= 64 and In + H <= 64: the reference's H = 32, L = 2) --------
+//
+// The tick above costs ~2.5k cycles, almost all of it LDS round trips behind TWO workgroup
+// barriers (gate exchange, then the cell update's h exchange).  Here lane (l, j) of a 64-lane
+// wave owns unit j of layer l, and the workgroup is just two waves: wave w owns the gate pair
+// {2w, 2w + 1} (w = 0: i, f; w = 1: g, o), i.e. 2 x (In + H) <= 128 fp32 weights per lane, held in
+// VGPRs and accumulated with packed v_pk_fma_f32.  After the single barrier that exchanges the
+// gate pairs BOTH waves run the (cheap) cell update redundantly and write h / the dropped-out
+// layer input into their OWN LDS copy, which only the same wave reads at the next tick — in-order
+// LDS within a wave needs no barrier — so a tick has exactly one barrier.  The backward is the
+// same shape: both waves run the cell backward redundantly into their own da copy; wave 0 forms
+// dh_{t-1} = W_hh^T da (its lane holds W_hh column j), wave 1 forms dx_t = W_ih^T da for the
+// layer below (column j of W_ih), one barrier hands them over.
+//
+// Why not MFMA for the gate products: per tick and layer they are [32 seq x 64] x [64 x 128];
+// fp32-exact through the 3-plane bf16 split that is 6 x 4 k-steps x 4 tiles = 96
+// v_mfma_f32_32x32x16_bf16 per layer per tick (~1.5k cycles on one CU for the batch), while the
+// same products spread over one CU per sequence are ~128 cycles of packed fp32 VALU.  The
+// recurrence is a latency chain; batching it onto the matrix cores lengthens the chain.
+typedef float smi_f2 __attribute__((ext_vector_type(2)));
+#define SMI_WAVE_LDS_ORDER() asm volatile("" ::: "memory")  // compiler order only: LDS is in-order per wave
+
+template <int H, int MI>
+__global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
+  const int b = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int L = a.L, T = a.T, E = a.E, C = a.C;
+  const int l = lane / H, j = lane % H;
+  const bool act = l < L;
+  const int In = l == 0 ? E : H;
+  constexpr int SI = MI + 4, SH = H + 4;  // padded rows: the L broadcast rows of a read hit distinct banks
+  __shared__ __attribute__((aligned(16))) float s_in[2][2][LSTM_MAXL * SI];  // [wave][buf][layer row]
+  __shared__ __attribute__((aligned(16))) float s_h[2][2][LSTM_MAXL * SH];
+  __shared__ float s_g[2][LSTM_MAXL][4][H];                                // [buf][layer][gate][unit]
+  __shared__ long long s_ids[LSTM_MAXT];
+  for (int i = tid; i < T; i += blockDim.x) s_ids[i] = a.ids[(size_t)b * T + i];
+
+  const int g0 = 2 * w, g1 = 2 * w + 1;
+  smi_f2 wi0[MI / 2], wi1[MI / 2], wh0[H / 2], wh1[H / 2];
+#pragma unroll
+  for (int i = 0; i < MI; i += 2) {
+    const float* r0 = a.w_ih[act ? l : 0] + (size_t)(g0 * H + j) * In;
+    const float* r1 = a.w_ih[act ? l : 0] + (size_t)(g1 * H + j) * In;
+    wi0[i / 2] = smi_f2{(act && i < In) ? r0[i] : 0.f, (act && i + 1 < In) ? r0[i + 1] : 0.f};
+    wi1[i / 2] = smi_f2{(act && i < In) ? r1[i] : 0.f, (act && i + 1 < In) ? r1[i + 1] : 0.f};
+  }
+#pragma unroll
+  for (int i = 0; i < H; i += 2) {
+    const float* r0 = a.w_hh[act ? l : 0] + (size_t)(g0 * H + j) * H;
+    const float* r1 = a.w_hh[act ? l : 0] + (size_t)(g1 * H + j) * H;
+    wh0[i / 2] = act ? smi_f2{r0[i], r0[i + 1]} : smi_f2{0.f, 0.f};
+    wh1[i / 2] = act ? smi_f2{r1[i], r1[i + 1]} : smi_f2{0.f, 0.f};
+  }
+  const float bias0 = act ? a.b_ih[l][g0 * H + j] + a.b_hh[l][g0 * H + j] : 0.f;
+  const float bias1 = act ? a.b_ih[l][g1 * H + j] + a.b_hh[l][g1 * H + j] : 0.f;
+  for (int i = tid; i < 2 * 2 * LSTM_MAXL * SI; i += blockDim.x) (&s_in[0][0][0])[i] = 0.f;
+  float c = 0.f, hl = 0.f;
+  __syncthreads();
+  if (act) {
+    c = a.c0 ? a.c0[((size_t)l * a.B + b) * H + j] : 0.f;
+    hl = a.h0 ? a.h0[((size_t)l * a.B + b) * H + j] : 0.f;
+    s_h[w][0][l * SH + j] = hl;  // a layer reads h_{-1} from the buffer of its first tick: both
+    s_h[w][1][l * SH + j] = hl;
+  }
+  __syncthreads();  // s_ids
+  auto emb_at = [&](int t) { return (lane < E && t < T) ? a.emb[(size_t)s_ids[t] * E + lane] : 0.f; };
+  if (lane < E) s_in[w][0][lane] = emb_at(0);
+  float x0 = 0.f, x1 = emb_at(1), x2 = emb_at(2);
+  __syncthreads();
+
+  const uint32_t seed = smi_seed(a.seedp, a.salt);
+  float* wsb = a.ws + (size_t)b * L * T * 6 * H;
+  const int nt = T + L - 1;
+  auto tick = [&](int k, float& xnext, float& xload) {
+    const int t = k - l;
+    const bool on = act && t >= 0 && t < T;
+    const int rb = k & 1, wb = rb ^ 1;
+    if (on) {
+      smi_f2 p0 = {bias0, 0.f}, q0 = {0.f, 0.f}, p1 = {bias1, 0.f}, q1 = {0.f, 0.f};
+      const float* xin = &s_in[w][rb][l * SI];
+      const float* hin = &s_h[w][rb][l * SH];
+#pragma unroll
+      for (int i = 0; i < MI; i += 4) {
+        const float4 x = *(const float4*)&xin[i];
+        const smi_f2 xa = {x.x, x.y}, xb = {x.z, x.w};
+        p0 = __builtin_elementwise_fma(wi0[i / 2], xa, p0);
+        q0 = __builtin_elementwise_fma(wi0[i / 2 + 1], xb, q0);
+        p1 = __builtin_elementwise_fma(wi1[i / 2], xa, p1);
+        q1 = __builtin_elementwise_fma(wi1[i / 2 + 1], xb, q1);
+      }
+#pragma unroll
+      for (int i = 0; i < H; i += 4) {
+        const float4 x = *(const float4*)&hin[i];
+        const smi_f2 xa = {x.x, x.y}, xb = {x.z, x.w};
+        p0 = __builtin_elementwise_fma(wh0[i / 2], xa, p0);
+        q0 = __builtin_elementwise_fma(wh0[i / 2 + 1], xb, q0);
+        p1 = __builtin_elementwise_fma(wh1[i / 2], xa, p1);
+        q1 = __builtin_elementwise_fma(wh1[i / 2 + 1], xb, q1);
+      }
+      const float z0 = (p0.x + p0.y) + (q0.x + q0.y), z1 = (p1.x + p1.y) + (q1.x + q1.y);
+      s_g[rb][l][g0][j] = w == 1 ? smi_tanh(z0) : smi_sigmoid(z0);  // gate 2 (g) is the tanh one
+      s_g[rb][l][g1][j] = smi_sigmoid(z1);
+    }
+    smi_lds_barrier();
+    if (on) {
+      const float ig = s_g[rb][l][0][j], fg = s_g[rb][l][1][j], gg = s_g[rb][l][2][j], og = s_g[rb][l][3][j];
+      c = fg * c + ig * gg;
+      hl = og * smi_tanh(c);
+      s_h[w][wb][l * SH + j] = hl;
+      float* ws = wsb + ((size_t)l * T + t) * 6 * H;
+      if (w == 0) { ws[j] = ig; ws[H + j] = fg; ws[2 * H + j] = gg; }
+      else { ws[3 * H + j] = og; ws[4 * H + j] = c; ws[5 * H + j] = hl; }
+      if (l + 1 < L) {
+        float hd = hl;
+        if (a.thresh) hd = smi_keep(seed, lstm_drop_idx(b, t, l, j, T, L, H), a.thresh) ? hl * a.dscale : 0.f;
+        s_in[w][wb][(l + 1) * SI + j] = hd;
+      }
+    }
+    if (lane < E) {  // layer 0's input for the next tick
+      s_in[w][wb][lane] = xnext;
+      xload = emb_at(k + 3);
+    }
+    SMI_WAVE_LDS_ORDER();
+  };
+  int k = 0;
+  for (; k + 3 <= nt; k += 3) {
+    tick(k, x1, x0);
+    tick(k + 1, x2, x1);
+    tick(k + 2, x0, x2);
+  }
+  if (k < nt) tick(k, x1, x0);
+  if (k + 1 < nt) tick(k + 1, x2, x1);
+  __syncthreads();  // ws (global) written by both waves is read by the fc head below
+  if (act && w == 0) {
+    if (a.hn) a.hn[((size_t)l * a.B + b) * H + j] = hl;
+    if (a.cn) a.cn[((size_t)l * a.B + b) * H + j] = c;
+  }
+  {
+    __shared__ float s_top[LSTM_TCH * H];
+    __shared__ float s_wfc[LSTM_MAXC * H];
+    const float* top = wsb + (size_t)(L - 1) * T * 6 * H + 5 * H;
+    for (int i = tid; i < C * H; i += blockDim.x) s_wfc[i] = a.w_fc[i];
+    for (int t0 = 0; t0 < T; t0 += LSTM_TCH) {
+      const int nc = min(LSTM_TCH, T - t0);
+      __syncthreads();
+      for (int i = tid; i < nc * H; i += blockDim.x) s_top[i] = top[(size_t)(t0 + i / H) * 6 * H + i % H];
+      __syncthreads();
+      for (int o = tid; o < nc * C; o += blockDim.x) {
+        const int t = o / C, cc = o % C;
+        float s0 = a.b_fc[cc], s1 = 0.f;
+#pragma unroll
+        for (int q = 0; q < H; q += 2) {
+          s0 += s_wfc[cc * H + q] * s_top[t * H + q];
+          s1 += s_wfc[cc * H + q + 1] * s_top[t * H + q + 1];
+        }
+        a.pred[((size_t)b * T + t0 + t) * C + cc] = s0 + s1;
+        if (a.pred_last && t0 + t == T - 1) a.pred_last[(size_t)b * C + cc] = s0 + s1;
+      }
+    }
+  }
+}
+
+template <int H, int MI, int CM>
+__global__ __launch_bounds__(128) void lstm_bwd_w2_kernel(LSTMArgs a) {
+  constexpr int G = 4 * H;
+  const int b = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int L = a.L, T = a.T, C = a.C;
+  const int l = lane / H, j = lane % H;
+  const bool act = l < L, top = l == L - 1;
+  __shared__ __attribute__((aligned(16))) float s_da[2][LSTM_MAXL][G + 4];  // per-wave copy
+  __shared__ float s_dh[2][LSTM_MAXL][H];  // [buf]: W_hh^T da (wave 0)
+  __shared__ float s_dx[2][LSTM_MAXL][H];  // [buf]: W_ih^T da, the layer below's input gradient (wave 1)
+  // wave 0: column j of W_hh[l]; wave 1: column j of W_ih[l] (l >= 1: In = H; layer 0's input
+  // gradient is lstm_xe_kernel's job after the loop)
+  const bool prod = act && (w == 0 || l >= 1);
+  smi_f2 wc[G / 2];
+#pragma unroll
+  for (int q = 0; q < G; q += 2) {
+    const float* m = w == 0 ? a.w_hh[act ? l : 0] : a.w_ih[act ? l : 0];
+    wc[q / 2] = prod ? smi_f2{m[(size_t)q * H + j], m[(size_t)(q + 1) * H + j]} : smi_f2{0.f, 0.f};
+  }
+  float wfc[CM];
+#pragma unroll
+  for (int q = 0; q < CM; ++q) wfc[q] = (act && top && q < C) ? a.w_fc[(size_t)q * H + j] : 0.f;
+  float dc = 0.f, dhn = 0.f;
+  if (act) {
+    dc = a.dcn ? a.dcn[((size_t)l * a.B + b) * H + j] : 0.f;
+    dhn = a.dhn ? a.dhn[((size_t)l * a.B + b) * H + j] : 0.f;
+  }
+  for (int i = tid; i < 2 * LSTM_MAXL * H; i += blockDim.x) (&s_dx[0][0][0])[i] = 0.f;
+  __syncthreads();
+
+  const uint32_t seed = smi_seed(a.seedp, a.salt);
+  const float* wsb = a.ws + (size_t)b * L * T * 6 * H;
+  const float* dpred = a.dpred + (size_t)b * (a.dpred_last ? 1 : T) * C;
+  float* dab = a.ws_da + (size_t)b * L * T * G;
+  const int nt = T + L - 1;
+  const int tl = T - 1 + (L - 1 - l);
+  auto load_in = [&](int t, LstmBwdIn<CM>& v) {
+    if (!act || t < 0 || t >= T) return;
+    const float* ws = wsb + ((size_t)l * T + t) * 6 * H;
+    v.ig = ws[j]; v.fg = ws[H + j]; v.gg = ws[2 * H + j]; v.og = ws[3 * H + j]; v.cc = ws[4 * H + j];
+    v.cp = t > 0 ? ws[j - 2 * H] : (a.c0 ? a.c0[((size_t)l * a.B + b) * H + j] : 0.f);
+    if (top) {
+#pragma unroll
+      for (int q = 0; q < CM; ++q)
+        v.dp[q] = (q < C && (!a.dpred_last || t == T - 1)) ? dpred[(size_t)(a.dpred_last ? 0 : t) * C + q] : 0.f;
+    }
+  };
+  auto prep = [&](int t, LstmBwdIn<CM>& v) {
+    if (!act || t < 0 || t >= T) return;
+    const float tc = smi_tanh(v.cc);
+    v.A = v.og * (1.f - tc * tc);
+    v.Bo = tc * v.og * (1.f - v.og);
+    v.gi = v.gg * v.ig * (1.f - v.ig);
+    v.cf = v.cp * v.fg * (1.f - v.fg);
+    v.ig2 = v.ig * (1.f - v.gg * v.gg);
+    float f = 0.f;
+    if (top) {
+#pragma unroll
+      for (int q = 0; q < CM; ++q) f += wfc[q] * v.dp[q];
+    }
+    v.fct = f;
+    v.dm = top ? 0.f : (a.thresh ? (smi_keep(seed, lstm_drop_idx(b, t, l, j, T, L, H), a.thresh) ? a.dscale : 0.f) : 1.f);
+  };
+  LstmBwdIn<CM> ia{}, ib{}, ic{};
+  load_in(tl, ia);
+  load_in(tl - 1, ib);
+  prep(tl, ia);
+  float dh_first = 0.f;  // W_hh^T da at t = 0 (wave 0): the gradient of h0
+  auto tick = [&](int k, const LstmBwdIn<CM>& cv, LstmBwdIn<CM>& pv, LstmBwdIn<CM>& nv) {
+    const int t = tl - k;
+    const bool on = act && t >= 0 && t < T;
+    const int rb = k & 1, wb = rb ^ 1;
+    load_in(t - 2, nv);
+    if (on) {  // cell backward (both waves, bit-identical) on terms prep()'d a tick ahead
+      float dh = t == T - 1 ? dhn : s_dh[rb][l][j];
+      dh += top ? cv.fct : s_dx[rb][l + 1][j] * cv.dm;
+      dc += dh * cv.A;
+      const float d0 = dc * cv.gi, d1 = dc * cv.cf, d2 = dc * cv.ig2, d3 = dh * cv.Bo;
+      s_da[w][l][j] = d0; s_da[w][l][H + j] = d1; s_da[w][l][2 * H + j] = d2; s_da[w][l][3 * H + j] = d3;
+      float* dg = dab + ((size_t)l * T + t) * G;
+      if (w == 0) { dg[j] = d0; dg[H + j] = d1; }
+      else { dg[2 * H + j] = d2; dg[3 * H + j] = d3; }
+      dc *= cv.fg;
+    }
+    SMI_WAVE_LDS_ORDER();
+    prep(t - 1, pv);
+    if (on && prod) {  // this wave's transposed product over the layer's 4H gate gradients
+      smi_f2 p0 = {0.f, 0.f}, p1 = {0.f, 0.f}, p2 = {0.f, 0.f}, p3 = {0.f, 0.f};
+      const float* da = &s_da[w][l][0];
+#pragma unroll
+      for (int q = 0; q < G; q += 8) {
+        const float4 d4 = *(const float4*)&da[q];
+        const float4 e4 = *(const float4*)&da[q + 4];
+        p0 = __builtin_elementwise_fma(wc[q / 2], smi_f2{d4.x, d4.y}, p0);
+        p1 = __builtin_elementwise_fma(wc[q / 2 + 1], smi_f2{d4.z, d4.w}, p1);
+        p2 = __builtin_elementwise_fma(wc[q / 2 + 2], smi_f2{e4.x, e4.y}, p2);
+        p3 = __builtin_elementwise_fma(wc[q / 2 + 3], smi_f2{e4.z, e4.w}, p3);
+      }
+      const float s = ((p0.x + p0.y) + (p1.x + p1.y)) + ((p2.x + p2.y) + (p3.x + p3.y));
+      if (w == 0) {
+        s_dh[wb][l][j] = s;
+        if (t == 0) dh_first = s;
+      } else {
+        s_dx[wb][l][j] = s;
+      }
+    }
+    smi_lds_barrier();
+  };
+  int k = 0;
+  for (; k + 3 <= nt; k += 3) {
+    tick(k, ia, ib, ic);
+    tick(k + 1, ib, ic, ia);
+    tick(k + 2, ic, ia, ib);
+  }
+  if (k < nt) tick(k, ia, ib, ic);
+  if (k + 1 < nt) tick(k + 1, ib, ic, ia);
+  __syncthreads();  // dab (global) is read across workgroups by the weight-gradient kernels (next launch)
+  if (act && w == 0) {
+    if (a.dh0) a.dh0[((size_t)l * a.B + b) * H + j] = dh_first;
+    if (a.dc0) a.dc0[((size_t)l * a.B + b) * H + j] = dc;
+  }
+}
+
 // ---- weight gradients, off the recurrence: for every layer l,
 //   [dW_ih | dW_hh | db][r, :] = sum_{b,t} da[b,l,t,r] * [x_t | h_{t-1} | 1]
 // and for the head [dW_fc | db_fc][c, :] = sum_{b,t} dpred[b,t,c] * [h_top(t) | 1].
@@ -483,8 +767,28 @@ __global__ __launch_bounds__(256) void lstm_xe_kernel(LSTMArgs a) {
 
 // 4*H*L <= 256 threads: one wave per SIMD, so the backward's register-resident gradient rows
 // and W column slices get the full 512-entry (VGPR + AGPR) file.
+static int lstm_w2_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SMI_LSTM_W2");
+    v = e ? atoi(e) != 0 : 1;
+  }
+  return v;
+}
+
 template <int H, int MI>
 static int lstm_launch(const LSTMArgs* a, int backward, hipStream_t st) {
+  if constexpr (MI + H <= 64) {
+    if (a->L * H <= 64 && lstm_w2_enabled()) {
+      if (backward) {
+        if (a->C <= 4) hipLaunchKernelGGL((lstm_bwd_w2_kernel<H, MI, 4>), dim3(a->B), dim3(128), 0, st, *a);
+        else hipLaunchKernelGGL((lstm_bwd_w2_kernel<H, MI, LSTM_MAXC>), dim3(a->B), dim3(128), 0, st, *a);
+      } else {
+        hipLaunchKernelGGL((lstm_fwd_w2_kernel<H, MI>), dim3(a->B), dim3(128), 0, st, *a);
+      }
+      return (int)hipGetLastError();
+    }
+  }
   const int threads = ((4 * H * a->L + 63) / 64) * 64;
   if (threads <= 256) {
     if (backward) {
