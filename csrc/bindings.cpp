@@ -48,6 +48,8 @@ int smi_attn_bwd(const AttnBwdArgs*, const void*, float*, hipStream_t);
 int smi_ce_fwd(const void*, int, const long long*, int, int, long long, float*, float*, float*, float*, hipStream_t);
 int smi_ce_bwd(const void*, int, const long long*, int, int, long long, const float*, const float*, const float*, void*,
                void*, long, long, hipStream_t);
+int smi_ce_fwd_part(const void*, int, const float*, const long long*, int, int, long long, float*, float*, float*, float*,
+                    hipStream_t);
 int smi_emb_fwd(const long long*, const void*, const float*, void*, long, int, int, const uint32_t*, uint32_t, uint32_t, float,
                 hipStream_t);
 int smi_emb_bwd(const long long*, const void*, float*, long, int, long long, const uint32_t*, uint32_t, uint32_t, float, long,
@@ -81,6 +83,7 @@ int smi_gemm_sp_waves(int);
 int smi_gemm_sp_tm(int);
 int smi_gemm_sp_wg_tm(int);
 int smi_attn_f32_sp(int);
+int smi_attn_dkdv8(int);
 int smi_splitk_reduce(const float*, int, long, float*, long, float*, int, hipStream_t);
 int smi_splitk_fold_multi(const float* const*, float* const*, float* const*, const long*, const int*, const int*, int,
                           hipStream_t);
@@ -191,8 +194,11 @@ PYBIND11_MODULE(_C, m) {
   // fp32 attention: (q, k, v) pointers + (batch, seq, head) strides; o/lse written by the forward
   // op / op_ps (fwd), dqp / dkp / dvp / dq_ps / dkv_ps (bwd): optional split planes of the outputs
   m.def("attn_f32_fwd", [](u q, u k, u v, py::tuple qs, py::tuple ks, py::tuple vs, u o, py::tuple os, u lse, u kpad,
-                           int B, int H, int Sq, int Sk, int mode, float scale_log2, u op, long op_ps, u st) {
+                           int B, int H, int Sq, int Sk, int mode, float scale_log2, u op, long op_ps, u qpi, u kpi,
+                           u vpi, long qi_ps, long kvi_ps, u st) {
     AttnF32Args a{};
+    a.qpi = (const unsigned short*)qpi; a.kpi = (const unsigned short*)kpi; a.vpi = (const unsigned short*)vpi;
+    a.qi_ps = qi_ps; a.kvi_ps = kvi_ps;
     a.q = (const float*)q; a.k = (const float*)k; a.v = (const float*)v;
     a.q_sb = qs[0].cast<long>(); a.q_ss = qs[1].cast<long>(); a.q_sh = qs[2].cast<long>();
     a.k_sb = ks[0].cast<long>(); a.k_ss = ks[1].cast<long>(); a.k_sh = ks[2].cast<long>();
@@ -205,8 +211,12 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("attn_f32_bwd", [](u q, u k, u v, py::tuple qs, py::tuple ks, py::tuple vs, u o, u dout, py::tuple os, u lse,
                            u delta, u dq, u dk, u dv, u kpad, int B, int H, int Sq, int Sk, int mode, float scale_log2,
-                           float scale, u dqp, u dkp, u dvp, long dq_ps, long dkv_ps, u st) {
+                           float scale, u dqp, u dkp, u dvp, long dq_ps, long dkv_ps, u qpi, u kpi, u vpi, u dopi,
+                           long qi_ps, long kvi_ps, long doi_ps, int no_f32_grad, u st) {
     AttnF32Args a{};
+    a.no_f32_grad = no_f32_grad;
+    a.qpi = (const unsigned short*)qpi; a.kpi = (const unsigned short*)kpi; a.vpi = (const unsigned short*)vpi;
+    a.dopi = (const unsigned short*)dopi; a.qi_ps = qi_ps; a.kvi_ps = kvi_ps; a.doi_ps = doi_ps;
     a.dqp = (unsigned short*)dqp; a.dkp = (unsigned short*)dkp; a.dvp = (unsigned short*)dvp;
     a.dq_ps = dq_ps; a.dkv_ps = dkv_ps;
     a.q = (const float*)q; a.k = (const float*)k; a.v = (const float*)v;
@@ -224,6 +234,12 @@ PYBIND11_MODULE(_C, m) {
                      u row_loss, u st) {
     chk(smi_ce_fwd(P(logits), is_bf16, (const long long*)labels, M, V, ignore, PF(lse), PF(count), PF(loss),
                    PF(row_loss), S(st)), "ce_fwd");
+  });
+  // the loss from the vocab projection's epilogue statistics (gemm_sp lse_part): no logits pass
+  m.def("ce_fwd_part", [](u part, int nt, u logits, u labels, int M, int V, long long ignore, u lse, u count, u loss,
+                          u row_loss, u st) {
+    chk(smi_ce_fwd_part(P(part), nt, PF(logits), (const long long*)labels, M, V, ignore, PF(lse), PF(count), PF(loss),
+                        PF(row_loss), S(st)), "ce_fwd_part");
   });
   // planes / ldp / pps: optional split planes of the fp32 gradient (0 for none)
   m.def("ce_bwd", [](u logits, int is_bf16, u labels, int M, int V, long long ignore, u lse, u count, u dloss, u grad,
@@ -412,8 +428,9 @@ PYBIND11_MODULE(_C, m) {
   // (plane stride aps / bps), optional plane output P of the epilogue result
   m.def("gemm_sp", [](int mode, u A, long lda, long aps, u B, long ldb, long bps, int M, int N, int K, int kpad, u C,
                       long ldc, u Pp, long ldp, long pps, int beta_acc, u bias, int relu, u resid, long ldr, u dact_y,
-                      long ldy, u seedp, uint32_t salt, uint32_t thresh, float dscale, u bias_grad, u st) {
+                      long ldy, u seedp, uint32_t salt, uint32_t thresh, float dscale, u bias_grad, u lse_part, u st) {
     GemmSpArgs g{};
+    g.lse_part = (float*)lse_part;
     g.mode = mode; g.A = (const unsigned short*)A; g.lda = lda; g.aps = aps;
     g.B = (const unsigned short*)B; g.ldb = ldb; g.bps = bps; g.M = M; g.N = N; g.K = K; g.kpad = kpad;
     g.C = (float*)C; g.ldc = ldc; g.P = (unsigned short*)Pp; g.ldp = ldp; g.pps = pps; g.beta_acc = beta_acc;
@@ -446,6 +463,8 @@ PYBIND11_MODULE(_C, m) {
         "split-plane GEMM waves per 128x128 tile (4 | 8); other values query");
   m.def("gemm_sp_tm", [](int set) { return smi_gemm_sp_tm(set); },
         "split-plane GEMM tile form for large problems (16: 256x128 on 16x16x32 MFMA | 256 | 4 | 128); other values query");
+  m.def("attn_dkdv8", [](int set) { return smi_attn_dkdv8(set); },
+        "fp32 attention dK/dV: 1 = 8-wave workgroups with owned V in LDS (default), 0 = 4-wave; other values query");
   m.def("attn_f32_sp", [](int set) { return smi_attn_f32_sp(set); },
         "fp32 attention kernels: 1 staged-plane (default), 0 per-wave split; other values query");
   m.def("gemm_sp_wg_tm", [](int set) { return smi_gemm_sp_wg_tm(set); },

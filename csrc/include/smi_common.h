@@ -83,6 +83,21 @@ __device__ __forceinline__ float smi_row32_swap_max(float v) {
   auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
 }
+// reductions over each 32-lane half of the wave (quad / mirror DPP steps + the row16 swap)
+__device__ __forceinline__ float half_wave_sum(float v) {
+  v += smi_dpp<SMI_DPP_QP1032>(v);
+  v += smi_dpp<SMI_DPP_QP2301>(v);
+  v += smi_dpp<SMI_DPP_HMIRROR>(v);
+  v += smi_dpp<SMI_DPP_MIRROR>(v);
+  return smi_row16_swap_sum(v);
+}
+__device__ __forceinline__ float half_wave_max(float v) {
+  v = fmaxf(v, smi_dpp<SMI_DPP_QP1032>(v));
+  v = fmaxf(v, smi_dpp<SMI_DPP_QP2301>(v));
+  v = fmaxf(v, smi_dpp<SMI_DPP_HMIRROR>(v));
+  v = fmaxf(v, smi_dpp<SMI_DPP_MIRROR>(v));
+  return smi_row16_swap_max(v);
+}
 __device__ __forceinline__ float wave_sum(float v) {
   v += smi_dpp<SMI_DPP_QP1032>(v);
   v += smi_dpp<SMI_DPP_QP2301>(v);

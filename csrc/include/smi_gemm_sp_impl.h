@@ -66,7 +66,7 @@ __device__ unsigned long long* g_sp_stamps;
 #define SP_STAMP(slot) do {} while (0)
 #endif
 
-enum : int { SE_BIAS = 1, SE_RELU = 2, SE_DROP = 8, SE_RESID = 16, SE_DACT = 32, SE_ACC = 64 };
+enum : int { SE_BIAS = 1, SE_RELU = 2, SE_DROP = 8, SE_RESID = 16, SE_DACT = 32, SE_ACC = 64, SE_LSE = 128 };
 enum : int { SO_C = 1, SO_P = 2 };  // epilogue outputs: fp32 C, planes P
 
 typedef __attribute__((address_space(3))) void sp_lds_void;
@@ -188,11 +188,14 @@ __device__ __forceinline__ void sp_store_tile(const GemmSpArgs& g, const float* 
 #pragma unroll 4
   for (int q = 0; q < TM / RS; ++q) {
     const int rl = (tid >> 5) + RS * q, row = m0 + rl;
-    if (row >= g.M || col >= g.N) continue;
+    if (row >= g.M) continue;  // uniform over the 32 lanes that share the row
+    if (!(EPI & SE_LSE) && col >= g.N) continue;
     const float4 t = *(const float4*)(ep + rl * SP_EPI_PITCH + c4);
     float v[4] = {t.x, t.y, t.z, t.w};
     const long cidx = (long)row * g.ldc + col;
-    if (full_cols) {
+    if ((EPI & SE_LSE) && col >= g.N) {
+      // past the last column: only joins the row statistics below
+    } else if (full_cols) {
       float4 rs = make_float4(0.f, 0.f, 0.f, 0.f), dy = rs, cc = rs;
       if (EPI & SE_RESID) rs = *(const float4*)(g.resid + (long)row * g.ldr + col);
       if (EPI & SE_DACT) dy = *(const float4*)(g.dact_y + (long)row * g.ldy + col);
@@ -220,7 +223,23 @@ __device__ __forceinline__ void sp_store_tile(const GemmSpArgs& g, const float* 
         if ((EPI & SE_ACC) && hasC) x += g.C[cidx + e];
         if (hasC) g.C[cidx + e] = x;
         if (OUT & SO_P) sp_store1(g.P + (long)row * g.ldp + col + e, g.pps, x);
+        v[e] = x;
       }
+    }
+    if constexpr ((EPI & SE_LSE) != 0) {
+      // the row's (max, sum exp) over this tile's 128 columns: the 32 lanes of the half-wave hold
+      // the row's 4-column groups; one lane stores the pair (fp32, natural-log units)
+      float lm = -INFINITY;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (col + e < g.N) lm = fmaxf(lm, v[e]);
+      const float rm = half_wave_max(lm);  // DPP: no LDS-crossbar round trips
+      float ls = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (col + e < g.N) ls += __expf(v[e] - rm);
+      const float rsum = half_wave_sum(ls);
+      if ((tid & 31) == 0) ((float2*)g.lse_part)[(long)(n0 >> 7) * g.M + row] = make_float2(rm, rsum);
     }
   }
 }
@@ -1091,8 +1110,16 @@ int smi_sp_waves();
 // 256-row tiles where they fill the chip: SMI_SP_TM = 16 (default: 8 waves on the 16x16x32 MFMA),
 // 256 (8 waves, 32x32x16), 4 (4 waves, pipelined), 128 (128-row tiles only)
 int smi_sp_tm();
+// 256 x 128 tiles when they fill the chip and do not lose a partial wave against 128 x 128 tiles:
+// (M, N) = (8192, 1536) is 384 tiles of 256 rows (1.5 waves of 256 CUs) but 768 of 128 rows
+// (3 full waves) — measured 87 vs 78 us (profiles/r3_gemm_sp_tiles_bench.log).
 static inline bool sp_use256(int M, int N) {
-  return smi_sp_tm() != 128 && ((M + 255) / 256) * ((N + 127) / 128) >= SP_NUM_CU;
+  if (smi_sp_tm() == 128) return false;
+  const long t256 = (long)((M + 255) / 256) * ((N + 127) / 128);
+  const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
+  if (t256 < SP_NUM_CU) return false;
+  const long w256 = (t256 + SP_NUM_CU - 1) / SP_NUM_CU, w128 = (t128 + SP_NUM_CU - 1) / SP_NUM_CU;
+  return 2 * w256 <= w128 || smi_sp_tm() == 256;
 }
 
 // Host-side checks shared by the launchers: 16-B aligned plane rows, descriptor-addressable

@@ -317,8 +317,10 @@ __global__ __launch_bounds__(256, XS ? 1 : 2) void attn_f32_dq_kernel(AttnF32Arg
   }
   if (qi < a.Sq) {
     float* dQ = a.dq + b * a.q_sb + hh * a.q_sh + (long)qi * a.q_ss;
+    if (!a.no_f32_grad) {
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt) fa_store_rowT(dQ + dt * 32, acc[dt], lane, a.scale);
+      for (int dt = 0; dt < 2; ++dt) fa_store_rowT(dQ + dt * 32, acc[dt], lane, a.scale);
+    }
     if (a.dqp) {
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) fa_store_rowT_planes(a.dqp + (dQ - a.dq) + dt * 32, a.dq_ps, acc[dt], lane, a.scale);
@@ -440,10 +442,12 @@ __global__ __launch_bounds__(256, XS ? 1 : 2) void attn_f32_dkdv_kernel(AttnF32A
   if (kj < a.Sk) {
     float* dK = a.dk + b * a.k_sb + hh * a.k_sh + (long)kj * a.k_ss;
     float* dV = a.dv + b * a.v_sb + hh * a.v_sh + (long)kj * a.v_ss;
+    if (!a.no_f32_grad) {
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
-      fa_store_rowT(dK + dt * 32, dk[dt], lane, a.scale);
-      fa_store_rowT(dV + dt * 32, dv[dt], lane, 1.0f);
+      for (int dt = 0; dt < 2; ++dt) {
+        fa_store_rowT(dK + dt * 32, dk[dt], lane, a.scale);
+        fa_store_rowT(dV + dt * 32, dv[dt], lane, 1.0f);
+      }
     }
     if (a.dkp) {
 #pragma unroll
@@ -483,9 +487,11 @@ __device__ __forceinline__ int as_sw(int r) { return (((r >> 1) & 1) << 2) | ((r
 __device__ __forceinline__ int as_off(int r, int c) { return r * 64 + ((((c >> 3) ^ as_sw(r)) & 7) << 3) + (c & 7); }
 
 struct AStage { float4 v[2]; };
-// thread t loads 8 consecutive floats: row t >> 3, columns 8 (t & 7) .. + 7 (rows >= rmax: zero)
-__device__ __forceinline__ void as_load(const float* __restrict__ base, long ss, int r0, int rmax, AStage& p) {
-  const int r = threadIdx.x >> 3, c = (threadIdx.x & 7) * 8;
+// thread t (< 256) loads 8 consecutive floats: row t >> 3, columns 8 (t & 7) .. + 7 (rows >= rmax: zero)
+__device__ __forceinline__ void as_load(const float* __restrict__ base, long ss, int r0, int rmax, AStage& p,
+                                        int ti = -1) {
+  if (ti < 0) ti = threadIdx.x;
+  const int r = ti >> 3, c = (ti & 7) * 8;
   if (r0 + r < rmax) {
     const float* q = base + (long)(r0 + r) * ss + c;
     p.v[0] = *(const float4*)q;
@@ -494,8 +500,9 @@ __device__ __forceinline__ void as_load(const float* __restrict__ base, long ss,
     p.v[0] = p.v[1] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
-__device__ __forceinline__ void as_store(unsigned short* img, const AStage& p) {
-  const int r = threadIdx.x >> 3, c = (threadIdx.x & 7) * 8;
+__device__ __forceinline__ void as_store(unsigned short* img, const AStage& p, int ti = -1) {
+  if (ti < 0) ti = threadIdx.x;
+  const int r = ti >> 3, c = (ti & 7) * 8;
   const float f[8] = {p.v[0].x, p.v[0].y, p.v[0].z, p.v[0].w, p.v[1].x, p.v[1].y, p.v[1].z, p.v[1].w};
   const Split3 sp = split3_8(f);
   const int o = as_off(r, c);
@@ -503,6 +510,74 @@ __device__ __forceinline__ void as_store(unsigned short* img, const AStage& p) {
   *(bf16x8_t*)(img + AS_PL + o) = sp.m;
   *(bf16x8_t*)(img + 2 * AS_PL + o) = sp.l;
 }
+// PLANE INPUTS (PI): when the producer of Q / K / V (the projection GEMM's epilogue) or of dO (the
+// out-projection's dgrad epilogue) already wrote the operand's hi / mid / lo planes, a chunk is
+// staged as three 16-B loads + three 16-B LDS stores per thread and the owned rows are loaded as
+// ready MFMA operands: no split arithmetic left outside the per-block P / dS values.
+struct APStage { uint4 h, m, l; };
+template <bool PI> struct AStageT { using T = AStage; };
+template <> struct AStageT<true> { using T = APStage; };
+__device__ __forceinline__ void as_load(const unsigned short* __restrict__ base, long ps, long ss, int r0, int rmax,
+                                        APStage& p, int ti = -1) {
+  if (ti < 0) ti = threadIdx.x;
+  const int r = ti >> 3, c = (ti & 7) * 8;
+  if (r0 + r < rmax) {
+    const unsigned short* q = base + (long)(r0 + r) * ss + c;
+    p.h = *(const uint4*)q;
+    p.m = *(const uint4*)(q + ps);
+    p.l = *(const uint4*)(q + 2 * ps);
+  } else {
+    p.h = p.m = p.l = make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+__device__ __forceinline__ void as_store(unsigned short* img, const APStage& p, int ti = -1) {
+  if (ti < 0) ti = threadIdx.x;
+  const int o = as_off(ti >> 3, (ti & 7) * 8);
+  *(uint4*)(img + o) = p.h;
+  *(uint4*)(img + AS_PL + o) = p.m;
+  *(uint4*)(img + 2 * AS_PL + o) = p.l;
+}
+// one operand's fp32 source or its planes: staged loads / owned rows / reconstructed fp32 rows
+template <bool PI>
+struct AsSrc {
+  const float* f; const unsigned short* p; long ps, ss;
+  __device__ __forceinline__ void load(int r0, int rmax, typename AStageT<PI>::T& st, int ti = -1) const {
+    if constexpr (PI) as_load(p, ps, ss, r0, rmax, st, ti);
+    else as_load(f, ss, r0, rmax, st, ti);
+  }
+  // the owned row as ready operands (F32Pre order: s[j] = head dims 32 h + 8 j .. + 7)
+  __device__ __forceinline__ void own(int row, int rmax, int lane, F32Pre<1, 32>& o) const {
+    if constexpr (PI) {
+      const bool ok = row < rmax;
+      const unsigned short* q = p + (long)row * ss + 32 * (lane >> 5);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+        o.s[j].h = __builtin_bit_cast(bf16x8_t, ok ? *(const uint4*)(q + 8 * j) : z);
+        o.s[j].m = __builtin_bit_cast(bf16x8_t, ok ? *(const uint4*)(q + ps + 8 * j) : z);
+        o.s[j].l = __builtin_bit_cast(bf16x8_t, ok ? *(const uint4*)(q + 2 * ps + 8 * j) : z);
+      }
+    } else {
+      float v[32];
+      fa_ownrow(f, ss, row, rmax, lane, v);
+      o.set(v);
+    }
+  }
+  // the owned row's fp32 values (planes: h + m + l, exact)
+  __device__ __forceinline__ void own_f32(const F32Pre<1, 32>& o, int row, int rmax, int lane, float (&v)[32]) const {
+    if constexpr (PI) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          v[8 * j + e] = (bf2f((unsigned short)o.s[j].h[e]) + bf2f((unsigned short)o.s[j].m[e])) +
+                         bf2f((unsigned short)o.s[j].l[e]);
+    } else {
+      fa_ownrow(f, ss, row, rmax, lane, v);
+    }
+  }
+};
+
 // A operand, rows = streamed rows (lane & 31), k-step j: head dims 32 h + 8 j .. + 7 (the owned
 // operand's F32Pre order)
 __device__ __forceinline__ Split3 as_rowfrag(const unsigned short* img, int lane, int j) {
@@ -556,7 +631,11 @@ __device__ __forceinline__ void as_cols_acc(const unsigned short* img, int lane,
   }
 }
 
-template <int MODE, bool KPAD>
+// operand sources of batch b, head hh (fp32 base + plane base at the same element offset)
+#define AS_SRC(NAME, FP, PP, PS, SB, SH, SS)                                                         \
+  const AsSrc<PI> NAME{(FP) + b * (SB) + hh * (SH), PI ? (PP) + b * (SB) + hh * (SH) : nullptr, (PS), (SS)}
+
+template <int MODE, bool KPAD, bool PI>
 __global__ __launch_bounds__(256, 2) void attn_sp_fwd_kernel(AttnF32Args a) {
   __shared__ __attribute__((aligned(16))) unsigned short Ks[2][AS_OP];
   __shared__ __attribute__((aligned(16))) unsigned short Vs[2][AS_OP];
@@ -564,22 +643,18 @@ __global__ __launch_bounds__(256, 2) void attn_sp_fwd_kernel(AttnF32Args a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
   const int qwave = blockIdx.x * 128 + w * 32;
   const int qi = qwave + (lane & 31);
-  const float* Q = a.q + b * a.q_sb + hh * a.q_sh;
-  const float* K = a.k + b * a.k_sb + hh * a.k_sh;
-  const float* V = a.v + b * a.v_sb + hh * a.v_sh;
+  AS_SRC(Q, a.q, a.qpi, a.qi_ps, a.q_sb, a.q_sh, a.q_ss);
+  AS_SRC(K, a.k, a.kpi, a.kvi_ps, a.k_sb, a.k_sh, a.k_ss);
+  AS_SRC(V, a.v, a.vpi, a.kvi_ps, a.v_sb, a.v_sh, a.v_ss);
   const unsigned char* kp = a.kpad ? a.kpad + (long)b * a.Sk : nullptr;
   int kend = a.Sk;
   if (MODE == 2) kend = min(a.Sk, blockIdx.x * 128 + 128);
   const int nchunks = (kend + FCH - 1) / FCH;
-  AStage pk, pv;
-  as_load(K, a.k_ss, 0, a.Sk, pk);
-  as_load(V, a.v_ss, 0, a.Sk, pv);
+  typename AStageT<PI>::T pk, pv;
+  K.load(0, a.Sk, pk);
+  V.load(0, a.Sk, pv);
   F32Pre<1, 32> qs;
-  {
-    float qf[32];
-    fa_ownrow(Q, a.q_ss, qi, a.Sq, lane, qf);
-    qs.set(qf);
-  }
+  Q.own(qi, a.Sq, lane, qs);
   as_store(Ks[0], pk);
   as_store(Vs[0], pv);
   __syncthreads();
@@ -592,7 +667,7 @@ __global__ __launch_bounds__(256, 2) void attn_sp_fwd_kernel(AttnF32Args a) {
   for (int c = 0; c < nchunks; ++c) {
     const int buf = c & 1;
     const bool more = c + 1 < nchunks;
-    if (more) { as_load(K, a.k_ss, (c + 1) * FCH, a.Sk, pk); as_load(V, a.v_ss, (c + 1) * FCH, a.Sk, pv); }
+    if (more) { K.load((c + 1) * FCH, a.Sk, pk); V.load((c + 1) * FCH, a.Sk, pv); }
     const unsigned long long kmask = KPAD ? chunk_pad_mask(kp, c * FCH, a.Sk) : 0ull;
     do {
       const int k0 = c * FCH;
@@ -657,7 +732,7 @@ __global__ __launch_bounds__(256, 2) void attn_sp_fwd_kernel(AttnF32Args a) {
   }
 }
 
-template <int MODE, bool KPAD>
+template <int MODE, bool KPAD, bool PI>
 __global__ __launch_bounds__(256, 2) void attn_sp_dq_kernel(AttnF32Args a) {
   __shared__ __attribute__((aligned(16))) unsigned short Ks[2][AS_OP];
   __shared__ __attribute__((aligned(16))) unsigned short Vs[2][AS_OP];
@@ -665,27 +740,26 @@ __global__ __launch_bounds__(256, 2) void attn_sp_dq_kernel(AttnF32Args a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
   const int qwave = blockIdx.x * 128 + w * 32;
   const int qi = qwave + (lane & 31);
-  const float* Q = a.q + b * a.q_sb + hh * a.q_sh;
-  const float* K = a.k + b * a.k_sb + hh * a.k_sh;
-  const float* V = a.v + b * a.v_sb + hh * a.v_sh;
-  const float* dO = a.dout + b * a.o_sb + hh * a.o_sh;
+  AS_SRC(Q, a.q, a.qpi, a.qi_ps, a.q_sb, a.q_sh, a.q_ss);
+  AS_SRC(K, a.k, a.kpi, a.kvi_ps, a.k_sb, a.k_sh, a.k_ss);
+  AS_SRC(V, a.v, a.vpi, a.kvi_ps, a.v_sb, a.v_sh, a.v_ss);
+  AS_SRC(dO, a.dout, a.dopi, a.doi_ps, a.o_sb, a.o_sh, a.o_ss);
   const float* Og = a.o + b * a.o_sb + hh * a.o_sh;
   const unsigned char* kp = a.kpad ? a.kpad + (long)b * a.Sk : nullptr;
   int kend = a.Sk;
   if (MODE == 2) kend = min(a.Sk, blockIdx.x * 128 + 128);
   const int nchunks = (kend + FCH - 1) / FCH;
-  AStage pk, pv;
-  as_load(K, a.k_ss, 0, a.Sk, pk);
-  as_load(V, a.v_ss, 0, a.Sk, pv);
+  typename AStageT<PI>::T pk, pv;
+  K.load(0, a.Sk, pk);
+  V.load(0, a.Sk, pv);
   F32Pre<1, 32> qs, ds;
   float dl;
   {
-    float qf[32], df[32], of[32];
-    fa_ownrow(Q, a.q_ss, qi, a.Sq, lane, qf);
-    fa_ownrow(dO, a.o_ss, qi, a.Sq, lane, df);
+    float df[32], of[32];
+    Q.own(qi, a.Sq, lane, qs);
+    dO.own(qi, a.Sq, lane, ds);
+    dO.own_f32(ds, qi, a.Sq, lane, df);
     fa_ownrow(Og, a.o_ss, qi, a.Sq, lane, of);
-    qs.set(qf);
-    ds.set(df);
     float sacc = 0.f;
 #pragma unroll
     for (int t = 0; t < 32; ++t) sacc = fmaf(df[t], of[t], sacc);
@@ -705,7 +779,7 @@ __global__ __launch_bounds__(256, 2) void attn_sp_dq_kernel(AttnF32Args a) {
   for (int c = 0; c < nchunks; ++c) {
     const int buf = c & 1;
     const bool more = c + 1 < nchunks;
-    if (more) { as_load(K, a.k_ss, (c + 1) * FCH, a.Sk, pk); as_load(V, a.v_ss, (c + 1) * FCH, a.Sk, pv); }
+    if (more) { K.load((c + 1) * FCH, a.Sk, pk); V.load((c + 1) * FCH, a.Sk, pv); }
     const unsigned long long kmask = KPAD ? chunk_pad_mask(kp, c * FCH, a.Sk) : 0ull;
     do {
       const int k0 = c * FCH;
@@ -738,8 +812,10 @@ __global__ __launch_bounds__(256, 2) void attn_sp_dq_kernel(AttnF32Args a) {
   }
   if (qi < a.Sq) {
     float* dQ = a.dq + b * a.q_sb + hh * a.q_sh + (long)qi * a.q_ss;
+    if (!a.no_f32_grad) {
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt) fa_store_rowT(dQ + dt * 32, acc[dt], lane, a.scale);
+      for (int dt = 0; dt < 2; ++dt) fa_store_rowT(dQ + dt * 32, acc[dt], lane, a.scale);
+    }
     if (a.dqp) {
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) fa_store_rowT_planes(a.dqp + (dQ - a.dq) + dt * 32, a.dq_ps, acc[dt], lane, a.scale);
@@ -749,7 +825,7 @@ __global__ __launch_bounds__(256, 2) void attn_sp_dq_kernel(AttnF32Args a) {
 
 // one workgroup per CU: owned K and V splits (96 registers) + two accumulator pairs + the P / dS
 // splits exceed 256 registers (two workgroups per CU spilled 34)
-template <int MODE, bool KPAD>
+template <int MODE, bool KPAD, bool PI>
 __global__ __launch_bounds__(256, 1) void attn_sp_dkdv_kernel(AttnF32Args a) {
   __shared__ __attribute__((aligned(16))) unsigned short Qs[2][AS_OP];
   __shared__ __attribute__((aligned(16))) unsigned short Ds[2][AS_OP];
@@ -758,32 +834,27 @@ __global__ __launch_bounds__(256, 1) void attn_sp_dkdv_kernel(AttnF32Args a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
   const int kwave = blockIdx.x * 128 + w * 32;
   const int kj = kwave + (lane & 31);
-  const float* Q = a.q + b * a.q_sb + hh * a.q_sh;
-  const float* K = a.k + b * a.k_sb + hh * a.k_sh;
-  const float* V = a.v + b * a.v_sb + hh * a.v_sh;
-  const float* dO = a.dout + b * a.o_sb + hh * a.o_sh;
+  AS_SRC(Q, a.q, a.qpi, a.qi_ps, a.q_sb, a.q_sh, a.q_ss);
+  AS_SRC(K, a.k, a.kpi, a.kvi_ps, a.k_sb, a.k_sh, a.k_ss);
+  AS_SRC(V, a.v, a.vpi, a.kvi_ps, a.v_sb, a.v_sh, a.v_ss);
+  AS_SRC(dO, a.dout, a.dopi, a.doi_ps, a.o_sb, a.o_sh, a.o_ss);
   const long rbase = ((long)b * a.H + hh) * a.Sq;
   int qstart = 0;
   if (MODE == 2) qstart = (blockIdx.x * 128) & ~(FCH - 1);
   const int nchunks = qstart < a.Sq ? (a.Sq - qstart + FCH - 1) / FCH : 0;
-  AStage pq, pd;
+  typename AStageT<PI>::T pq, pd;
   float lse_r = INFINITY, dl_r = 0.f;
   if (nchunks) {
-    as_load(Q, a.q_ss, qstart, a.Sq, pq);
-    as_load(dO, a.o_ss, qstart, a.Sq, pd);
+    Q.load(qstart, a.Sq, pq);
+    dO.load(qstart, a.Sq, pd);
     if (threadIdx.x < FCH && qstart + (int)threadIdx.x < a.Sq) {
       lse_r = a.lse[rbase + qstart + threadIdx.x];
       dl_r = a.delta[rbase + qstart + threadIdx.x];
     }
   }
   F32Pre<1, 32> ks, vs;
-  {
-    float kf[32], vf[32];
-    fa_ownrow(K, a.k_ss, kj, a.Sk, lane, kf);
-    fa_ownrow(V, a.v_ss, kj, a.Sk, lane, vf);
-    ks.set(kf);
-    vs.set(vf);
-  }
+  K.own(kj, a.Sk, lane, ks);
+  V.own(kj, a.Sk, lane, vs);
   const bool kok = kj < a.Sk && !(KPAD && a.kpad[(long)b * a.Sk + kj]);
   const float kbias = kok ? 0.f : -INFINITY;
   f32x16_t dk[2], dv[2];
@@ -801,8 +872,8 @@ __global__ __launch_bounds__(256, 1) void attn_sp_dkdv_kernel(AttnF32Args a) {
     const int buf = c & 1, q0 = qstart + c * FCH;
     const bool more = c + 1 < nchunks;
     if (more) {
-      as_load(Q, a.q_ss, q0 + FCH, a.Sq, pq);
-      as_load(dO, a.o_ss, q0 + FCH, a.Sq, pd);
+      Q.load(q0 + FCH, a.Sq, pq);
+      dO.load(q0 + FCH, a.Sq, pd);
       lse_r = INFINITY; dl_r = 0.f;
       if (threadIdx.x < FCH && q0 + FCH + (int)threadIdx.x < a.Sq) {
         lse_r = a.lse[rbase + q0 + FCH + threadIdx.x];
@@ -841,10 +912,12 @@ __global__ __launch_bounds__(256, 1) void attn_sp_dkdv_kernel(AttnF32Args a) {
   if (kj < a.Sk) {
     float* dK = a.dk + b * a.k_sb + hh * a.k_sh + (long)kj * a.k_ss;
     float* dV = a.dv + b * a.v_sb + hh * a.v_sh + (long)kj * a.v_ss;
+    if (!a.no_f32_grad) {
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
-      fa_store_rowT(dK + dt * 32, dk[dt], lane, a.scale);
-      fa_store_rowT(dV + dt * 32, dv[dt], lane, 1.0f);
+      for (int dt = 0; dt < 2; ++dt) {
+        fa_store_rowT(dK + dt * 32, dk[dt], lane, a.scale);
+        fa_store_rowT(dV + dt * 32, dv[dt], lane, 1.0f);
+      }
     }
     if (a.dkp) {
 #pragma unroll
@@ -854,6 +927,140 @@ __global__ __launch_bounds__(256, 1) void attn_sp_dkdv_kernel(AttnF32Args a) {
       }
     }
   }
+}
+
+// dK / dV with EIGHT waves per workgroup (256 keys: a whole head at S = 256), two waves per SIMD.
+// The 4-wave kernel above needs > 256 registers per lane (owned K and V splits, dK / dV
+// accumulators, P / dS splits), so it runs one wave per SIMD with every LDS / MFMA / exp latency
+// exposed, in two rounds of 256 workgroups.  Here the owned V rows live in LDS instead (a [32 keys]
+// [64] plane image per wave, read back as the dP product's B fragments exactly like a staged
+// chunk's row fragments: 12 extra ds_read_b128 per chunk), which fits two waves per SIMD, and each
+// staged Q / dO chunk serves 256 keys instead of 128 (threads 0-255 stage Q, 256-511 dO).
+// LDS: 2 x 2 x 12 KiB staging + 8 x 12 KiB owned V = 144 KiB.
+#define AS_DKDV8_KEYS 256
+template <int MODE, bool KPAD, bool PI>
+__global__ __launch_bounds__(512, 1) void attn_sp_dkdv8_kernel(AttnF32Args a) {
+  __shared__ __attribute__((aligned(16))) unsigned short Qs[2][AS_OP];
+  __shared__ __attribute__((aligned(16))) unsigned short Ds[2][AS_OP];
+  __shared__ __attribute__((aligned(16))) unsigned short Vo[8][AS_OP];
+  __shared__ float lse_s[2][FCH], dl_s[2][FCH];
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  const int kb0 = blockIdx.x * AS_DKDV8_KEYS;
+  const int kwave = kb0 + w * 32;
+  const int kj = kwave + (lane & 31);
+  const bool stq = tid < 256;  // this thread stages Q (waves 0-3) or dO (waves 4-7)
+  const int ti = tid & 255;
+  AS_SRC(Q, a.q, a.qpi, a.qi_ps, a.q_sb, a.q_sh, a.q_ss);
+  AS_SRC(K, a.k, a.kpi, a.kvi_ps, a.k_sb, a.k_sh, a.k_ss);
+  AS_SRC(V, a.v, a.vpi, a.kvi_ps, a.v_sb, a.v_sh, a.v_ss);
+  AS_SRC(dO, a.dout, a.dopi, a.doi_ps, a.o_sb, a.o_sh, a.o_ss);
+  const AsSrc<PI>& SQ = stq ? Q : dO;
+  const long rbase = ((long)b * a.H + hh) * a.Sq;
+  int qstart = 0;
+  if (MODE == 2) qstart = kb0 & ~(FCH - 1);
+  const int nchunks = qstart < a.Sq ? (a.Sq - qstart + FCH - 1) / FCH : 0;
+  typename AStageT<PI>::T ps;
+  float lse_r = INFINITY, dl_r = 0.f;
+  if (nchunks) {
+    SQ.load(qstart, a.Sq, ps, ti);
+    if (tid < FCH && qstart + tid < a.Sq) {
+      lse_r = a.lse[rbase + qstart + tid];
+      dl_r = a.delta[rbase + qstart + tid];
+    }
+  }
+  // owned V rows of the block -> the eight per-wave plane images (four 32-row passes of 512 threads)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = tid + 512 * i, blk = idx >> 8;
+    typename AStageT<PI>::T pv;
+    V.load(kb0 + 32 * blk, a.Sk, pv, idx & 255);
+    as_store(Vo[blk], pv, idx & 255);
+  }
+  F32Pre<1, 32> ks;
+  K.own(kj, a.Sk, lane, ks);
+  const bool kok = kj < a.Sk && !(KPAD && a.kpad[(long)b * a.Sk + kj]);
+  const float kbias = kok ? 0.f : -INFINITY;
+  f32x16_t dk[2], dv[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
+  if (nchunks) {
+    as_store(stq ? Qs[0] : Ds[0], ps, ti);
+    if (tid < FCH) { lse_s[0][tid] = lse_r; dl_s[0][tid] = dl_r; }
+  }
+  __syncthreads();
+  const unsigned short* vimg = Vo[w];
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1, q0 = qstart + c * FCH;
+    const bool more = c + 1 < nchunks;
+    if (more) {
+      SQ.load(q0 + FCH, a.Sq, ps, ti);
+      lse_r = INFINITY; dl_r = 0.f;
+      if (tid < FCH && q0 + FCH + tid < a.Sq) {
+        lse_r = a.lse[rbase + q0 + FCH + tid];
+        dl_r = a.delta[rbase + q0 + FCH + tid];
+      }
+    }
+    do {
+      if (MODE == 2 && q0 + 31 < kwave) break;  // every query of the chunk before every key of the wave
+      f32x16_t s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+      s = as_rows_dot(Qs[buf], lane, ks, s);  // S = Q K^T: query rows, key on the lane
+#pragma unroll
+      for (int j = 0; j < 4; ++j)  // dP = dO V^T, V's fragments from the wave's LDS image
+        dp = as_mma(as_rowfrag(Ds[buf], lane, j), as_rowfrag(vimg, lane, j), dp);
+      float pvv[16], dsv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ql = fa_kl(r, h);
+        const int qq = q0 + ql;
+        float x = fmaf(s[r], a.scale_log2, kbias);
+        if (MODE == 1) x += (kj < qq) ? LOG2E_F : 0.f;
+        if (MODE == 2) x = (kj > qq) ? -INFINITY : x;
+        const float pr = __builtin_amdgcn_exp2f(x - lse_s[buf][ql]);  // rows past Sq: lse = +inf -> 0
+        pvv[r] = pr;
+        dsv[r] = pr * (dp[r] - dl_s[buf][ql]);
+      }
+      as_cols_acc(Ds[buf], lane, pvv, dv);  // dV^T += dO^T P
+      as_cols_acc(Qs[buf], lane, dsv, dk);  // dK^T += Q^T dS
+    } while (0);
+    if (more) {
+      as_store(stq ? Qs[buf ^ 1] : Ds[buf ^ 1], ps, ti);
+      if (tid < FCH) { lse_s[buf ^ 1][tid] = lse_r; dl_s[buf ^ 1][tid] = dl_r; }
+    }
+    __syncthreads();
+  }
+  if (kj < a.Sk) {
+    float* dK = a.dk + b * a.k_sb + hh * a.k_sh + (long)kj * a.k_ss;
+    float* dV = a.dv + b * a.v_sb + hh * a.v_sh + (long)kj * a.v_ss;
+    if (!a.no_f32_grad) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        fa_store_rowT(dK + dt * 32, dk[dt], lane, a.scale);
+        fa_store_rowT(dV + dt * 32, dv[dt], lane, 1.0f);
+      }
+    }
+    if (a.dkp) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        fa_store_rowT_planes(a.dkp + (dK - a.dk) + dt * 32, a.dkv_ps, dk[dt], lane, a.scale);
+        fa_store_rowT_planes(a.dvp + (dV - a.dv) + dt * 32, a.dkv_ps, dv[dt], lane, 1.0f);
+      }
+    }
+  }
+}
+
+static int g_attn_dkdv8 = -1;  // SMI_ATTN_DKDV8=0: the 4-wave dK/dV kernel
+extern "C" int smi_attn_dkdv8(int set) {
+  if (set == 0 || set == 1) g_attn_dkdv8 = set;
+  if (g_attn_dkdv8 < 0) {
+    const char* e = getenv("SMI_ATTN_DKDV8");
+    g_attn_dkdv8 = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_attn_dkdv8;
 }
 
 // staged-plane kernels on (default) / off (SMI_ATTN_SP=0: the XS kernels above)
@@ -866,18 +1073,38 @@ extern "C" int smi_attn_f32_sp(int set) {
   }
   return g_attn_sp;
 }
-#define SMI_ATTN_SP_MODES(KERNEL, GRID, ARGS)                                                            \
+#define SMI_ATTN_SP_PI(KERNEL, PI, GRID, ARGS)                                                           \
+  switch ((ARGS).mode) {                                                                                 \
+    case 0: if (kp_) hipLaunchKernelGGL((KERNEL<0, true, PI>), GRID, dim3(256), 0, st, ARGS);            \
+            else hipLaunchKernelGGL((KERNEL<0, false, PI>), GRID, dim3(256), 0, st, ARGS); break;        \
+    case 1: if (kp_) hipLaunchKernelGGL((KERNEL<1, true, PI>), GRID, dim3(256), 0, st, ARGS);            \
+            else hipLaunchKernelGGL((KERNEL<1, false, PI>), GRID, dim3(256), 0, st, ARGS); break;        \
+    case 2: if (kp_) hipLaunchKernelGGL((KERNEL<2, true, PI>), GRID, dim3(256), 0, st, ARGS);            \
+            else hipLaunchKernelGGL((KERNEL<2, false, PI>), GRID, dim3(256), 0, st, ARGS); break;        \
+    default: return -1;                                                                                  \
+  }
+#define SMI_ATTN_SP_PI8(KERNEL, PI, GRID, ARGS)                                                          \
+  switch ((ARGS).mode) {                                                                                 \
+    case 0: if (kp_) hipLaunchKernelGGL((KERNEL<0, true, PI>), GRID, dim3(512), 0, st, ARGS);            \
+            else hipLaunchKernelGGL((KERNEL<0, false, PI>), GRID, dim3(512), 0, st, ARGS); break;        \
+    case 1: if (kp_) hipLaunchKernelGGL((KERNEL<1, true, PI>), GRID, dim3(512), 0, st, ARGS);            \
+            else hipLaunchKernelGGL((KERNEL<1, false, PI>), GRID, dim3(512), 0, st, ARGS); break;        \
+    case 2: if (kp_) hipLaunchKernelGGL((KERNEL<2, true, PI>), GRID, dim3(512), 0, st, ARGS);            \
+            else hipLaunchKernelGGL((KERNEL<2, false, PI>), GRID, dim3(512), 0, st, ARGS); break;        \
+    default: return -1;                                                                                  \
+  }
+#define SMI_ATTN_SP_MODES8(KERNEL, GRID, ARGS, PI_)                                                      \
   do {                                                                                                   \
     const bool kp_ = (ARGS).kpad != nullptr;                                                             \
-    switch ((ARGS).mode) {                                                                               \
-      case 0: if (kp_) hipLaunchKernelGGL((KERNEL<0, true>), GRID, dim3(256), 0, st, ARGS);              \
-              else hipLaunchKernelGGL((KERNEL<0, false>), GRID, dim3(256), 0, st, ARGS); break;          \
-      case 1: if (kp_) hipLaunchKernelGGL((KERNEL<1, true>), GRID, dim3(256), 0, st, ARGS);              \
-              else hipLaunchKernelGGL((KERNEL<1, false>), GRID, dim3(256), 0, st, ARGS); break;          \
-      case 2: if (kp_) hipLaunchKernelGGL((KERNEL<2, true>), GRID, dim3(256), 0, st, ARGS);              \
-              else hipLaunchKernelGGL((KERNEL<2, false>), GRID, dim3(256), 0, st, ARGS); break;          \
-      default: return -1;                                                                                \
-    }                                                                                                    \
+    if (PI_) { SMI_ATTN_SP_PI8(KERNEL, true, GRID, ARGS) }                                               \
+    else { SMI_ATTN_SP_PI8(KERNEL, false, GRID, ARGS) }                                                  \
+  } while (0)
+// PI_: the inputs' planes are present (every operand the kernel reads: see fa_pi)
+#define SMI_ATTN_SP_MODES(KERNEL, GRID, ARGS, PI_)                                                       \
+  do {                                                                                                   \
+    const bool kp_ = (ARGS).kpad != nullptr;                                                             \
+    if (PI_) { SMI_ATTN_SP_PI(KERNEL, true, GRID, ARGS) }                                                \
+    else { SMI_ATTN_SP_PI(KERNEL, false, GRID, ARGS) }                                                   \
   } while (0)
 
 // product algorithm shared with the fp32 GEMM (csrc/kernels/gemm_f32.hip:smi_gemm_f32_algo):
@@ -912,11 +1139,22 @@ static int fa_ok(const AttnF32Args& a) {
   return a.B > 0 && a.H > 0 && a.Sq > 0 && a.Sk > 0;
 }
 
+// input planes usable: all of Q / K / V (and dO for the backward) present, 16-B aligned rows
+static bool fa_pi(const AttnF32Args& a, bool bwd) {
+  if (!a.qpi || !a.kpi || !a.vpi || (bwd && !a.dopi)) return false;
+  const uintptr_t al = (uintptr_t)a.qpi | (uintptr_t)a.kpi | (uintptr_t)a.vpi | (bwd ? (uintptr_t)a.dopi : 0);
+  const long st[] = {a.q_ss, a.k_ss, a.v_ss, a.q_sh, a.k_sh, a.v_sh, a.q_sb, a.k_sb, a.v_sb, a.qi_ps, a.kvi_ps,
+                     bwd ? a.o_ss : 0, bwd ? a.o_sh : 0, bwd ? a.o_sb : 0, bwd ? a.doi_ps : 0};
+  for (long s : st)
+    if (s % 8) return false;
+  return (al & 15) == 0;
+}
+
 extern "C" int smi_attn_f32_fwd(const AttnF32Args* args, hipStream_t st) {
   const AttnF32Args& a = *args;
   if (!fa_ok(a)) return -1;
   dim3 grid((a.Sq + 127) / 128, a.H, a.B);
-  if (smi_gemm_f32_algo(-1) != 0 && smi_attn_f32_sp(-1)) SMI_ATTN_SP_MODES(attn_sp_fwd_kernel, grid, a);
+  if (smi_gemm_f32_algo(-1) != 0 && smi_attn_f32_sp(-1)) SMI_ATTN_SP_MODES(attn_sp_fwd_kernel, grid, a, fa_pi(a, false));
   else SMI_ATTN_F32_DISPATCH(attn_f32_fwd_kernel, grid, a);
   SMI_CHECK_LAUNCH();
 }
@@ -925,9 +1163,14 @@ extern "C" int smi_attn_f32_bwd(const AttnF32Args* args, hipStream_t st) {
   const AttnF32Args& a = *args;
   if (!fa_ok(a) || !a.dout || !a.delta || (((uintptr_t)a.dout | (uintptr_t)a.dq | (uintptr_t)a.dk | (uintptr_t)a.dv) & 15))
     return -1;
+  if (a.no_f32_grad && (!a.dqp || !a.dkp || !a.dvp)) return -1;  // planes-only needs every plane output
   if (smi_gemm_f32_algo(-1) != 0 && smi_attn_f32_sp(-1)) {
-    SMI_ATTN_SP_MODES(attn_sp_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), a);
-    SMI_ATTN_SP_MODES(attn_sp_dkdv_kernel, dim3((a.Sk + 127) / 128, a.H, a.B), a);
+    const bool pi = fa_pi(a, true);
+    SMI_ATTN_SP_MODES(attn_sp_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), a, pi);
+    if (smi_attn_dkdv8(-1))
+      SMI_ATTN_SP_MODES8(attn_sp_dkdv8_kernel, dim3((a.Sk + AS_DKDV8_KEYS - 1) / AS_DKDV8_KEYS, a.H, a.B), a, pi);
+    else
+      SMI_ATTN_SP_MODES(attn_sp_dkdv_kernel, dim3((a.Sk + 127) / 128, a.H, a.B), a, pi);
   } else {
     SMI_ATTN_F32_DISPATCH(attn_f32_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), a);
     SMI_ATTN_F32_DISPATCH(attn_f32_dkdv_kernel, dim3((a.Sk + 127) / 128, a.H, a.B), a);

@@ -18,6 +18,10 @@ int smi_sp_launch_dgrad(const GemmSpArgs& g, int epi, int out, dim3 grid, bool t
   // the FFN's hidden gradient dh feeds only linear1's dgrad / wgrad: planes (+ fp32 on request)
   else if (epi == SE_DACT && out == SO_P) SPD(SE_DACT, SO_P);
   else if (epi == SE_DACT && out == (SO_C | SO_P)) SPD(SE_DACT, SO_C | SO_P);
+  // the attention output's gradient dO (out-projection dgrad): planes for the attention backward
+  // kernels (+ fp32 when a kernel without plane inputs reads it)
+  else if (epi == 0 && out == SO_P) SPD(0, SO_P);
+  else if (epi == 0 && out == (SO_C | SO_P)) SPD(0, SO_C | SO_P);
   else return -1;
 #undef SPD
   SMI_CHECK_LAUNCH();

@@ -303,7 +303,9 @@ extern "C" int smi_ln_bwd_f32(const void* dy, const void* xs, const float* mean,
                               int accumulate, int M, int D, const uint32_t* seedp, uint32_t salt, uint32_t thresh,
                               float dscale, void* planes, long pps, hipStream_t st) {
   // planes: [3][M][D] bf16 of dh (or null)
-  if (planes && (((uintptr_t)planes & 15) || pps < (long)M * D || !dh)) return -1;
+  // dh null with planes: the sublayer's last Linear reads dh's planes only (planes-only output)
+  if (planes && (((uintptr_t)planes & 15) || pps < (long)M * D)) return -1;
+  if (!planes && !dh) return -1;
   return ln_bwd_launch<float>(dy, xs, mean, rstd, gamma, dres, dh, dres_add, part_g, part_b, nblocks, dgamma, dbeta,
                               accumulate, M, D, seedp, salt, thresh, dscale, planes, pps, st);
 }

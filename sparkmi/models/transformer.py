@@ -22,6 +22,8 @@ Mask semantics:
 import functools
 from dataclasses import dataclass
 
+import os
+
 import torch
 from torch import nn
 
@@ -30,6 +32,7 @@ from ..ops import (DropoutRNG, add_dropout_layernorm, cross_attention, embedding
 from ..ops._grad import ResidualGrad
 from ..ops._grad import SharedGrad
 from ..ops.linear import concat_linear, ffn
+from ..ops import planes as _pl
 from ..ops.loss import cross_entropy
 from ..ops.rng import new_salt
 
@@ -97,6 +100,18 @@ class SentenceEmbedding(nn.Module):
                          out_dtype=dtype)
 
 
+def _gp(t):
+    """A sublayer-internal tensor with one consumer (attention core / LayerNorm / loss): its
+    gradient may come back as split planes only (sparkmi/ops/planes.py, SMI_PLANES_ONLY)."""
+    return _pl.mark_grad_planes_ok(t)
+
+
+# fp32 GPU path: feed the attention kernels producer-written q/k/v/dO planes (SMI_ATTN_PLANES=1)
+ATTN_PLANES = os.environ.get("SMI_ATTN_PLANES", "0") == "1"
+# fp32 GPU path: the vocab projection's epilogue computes the cross-entropy row statistics
+CE_FUSED = os.environ.get("SMI_CE_FUSED", "1") != "0"
+
+
 class MultiHeadAttention(nn.Module):
     def __init__(self, d_model, num_heads):
         super().__init__()
@@ -107,9 +122,12 @@ class MultiHeadAttention(nn.Module):
         self.linear_layer = nn.Linear(d_model, d_model)
 
     def forward(self, x, mode="none", key_padding=None, x_slot=None):
-        qkv = linear(x, self.qkv_layer.weight, self.qkv_layer.bias, x_slot=x_slot)
+        # ATTN_PLANES: the projection writes q/k/v planes and the out-projection's dgrad writes dO
+        # planes, read by the attention kernels instead of splitting at staging (off by default:
+        # measured slower, docs/PERF_NOTES.md)
+        qkv = _gp(linear(x, self.qkv_layer.weight, self.qkv_layer.bias, x_slot=x_slot, out_planes=ATTN_PLANES))
         values = self_attention(qkv, self.num_heads, mode, key_padding)
-        return linear(values, self.linear_layer.weight, self.linear_layer.bias)
+        return _gp(linear(values, self.linear_layer.weight, self.linear_layer.bias, dx_planes=ATTN_PLANES))
 
 
 class MultiHeadCrossAttention(nn.Module):
@@ -126,12 +144,13 @@ class MultiHeadCrossAttention(nn.Module):
         """``kv``: optional (kv_all, column, SharedGrad) — this layer's k/v projection already
         computed inside the decoder's concatenated kv GEMM (Decoder._shared_kv)."""
         if kv is None:
-            kv_all, col, shared = linear(x, self.kv_layer.weight, self.kv_layer.bias), 0, None
+            kv_all = _gp(linear(x, self.kv_layer.weight, self.kv_layer.bias, out_planes=ATTN_PLANES))
+            col, shared = 0, None
         else:
             kv_all, col, shared = kv
-        q = linear(y, self.q_layer.weight, self.q_layer.bias, x_slot=y_slot)
+        q = _gp(linear(y, self.q_layer.weight, self.q_layer.bias, x_slot=y_slot, out_planes=ATTN_PLANES))
         values = cross_attention(q, kv_all, self.num_heads, mode, key_padding, col, shared)
-        return linear(values, self.linear_layer.weight, self.linear_layer.bias)
+        return _gp(linear(values, self.linear_layer.weight, self.linear_layer.bias, dx_planes=ATTN_PLANES))
 
 
 class LayerNormalization(nn.Module):
@@ -160,7 +179,7 @@ class PositionwiseFeedForward(nn.Module):
 
     def forward(self, x, x_slot=None):
         p = self.dropout.p if self.training else 0.0
-        return ffn(x, self.linear1, self.linear2, p, self._rng, self.salt, x_slot)
+        return _gp(ffn(x, self.linear1, self.linear2, p, self._rng, self.salt, x_slot))
 
 
 class EncoderLayer(nn.Module):
@@ -335,7 +354,9 @@ class Transformer(nn.Module):
             kp = enc_key_padding
         x = self.encoder(x, enc_mode, kp)
         out = self.decoder(x, y, self_mode, cross_mode, kp, getattr(self, "_smi_flat", None))
-        return linear(out, self.linear.weight, self.linear.bias)
+        # fp32 GPU: the epilogue also reduces each logits row (softmax statistics per 128 columns),
+        # so the cross-entropy forward never re-reads the logits (sparkmi/ops/loss.py)
+        return linear(out, self.linear.weight, self.linear.bias, lse_stats=CE_FUSED)
 
     def loss(self, logits, target):
         """Token CE ignoring pad, mean over non-pad targets (pytorch_machine_translator.py:182-188)."""
@@ -348,7 +369,7 @@ class Transformer(nn.Module):
         else:
             dec_in, target = tgt, tgt
         la = create_look_ahead_mask(dec_in.shape[1])  # the reference's decoder masks (host, cached)
-        logits = self(src, dec_in, None, la, la)
+        logits = _gp(self(src, dec_in, None, la, la))  # consumed by the loss only
         return self.loss(logits, target)
 
     def training_step_split(self, src, tgt, shift_targets=False, enc_cuts=None):
@@ -378,7 +399,7 @@ class Transformer(nn.Module):
             segments.append((leaf, x))
             x, start = leaf, c
         out = self.decoder(x, dec_in, self_mode, cross_mode, kp, getattr(self, "_smi_flat", None))
-        logits = linear(out, self.linear.weight, self.linear.bias)
+        logits = _gp(linear(out, self.linear.weight, self.linear.bias, lse_stats=CE_FUSED))
         return self.loss(logits, target), segments[::-1]
 
 

@@ -122,11 +122,12 @@ class SharedGrad:
     None to autograd): the producer's backward then reads the whole gradient at once, e.g. one
     dgrad GEMM over the six decoder kv projections (ops.linear.concat_linear)."""
 
-    __slots__ = ("buf", "planes")
+    __slots__ = ("buf", "planes", "planes_only")
 
     def __init__(self):
         self.buf = None
         self.planes = None
+        self.planes_only = False  # every writer wrote planes only (sparkmi/ops/planes.py)
 
     def get(self, like: torch.Tensor) -> torch.Tensor:
         if self.buf is None:
@@ -144,9 +145,11 @@ class SharedGrad:
     def take(self):
         b, self.buf = self.buf, None
         p, self.planes = self.planes, None
+        only, self.planes_only = self.planes_only, False
         if b is not None and p is not None:
             from . import planes as _pl
             _pl.attach(b, p)
+            b._smi_planes_only = only
         return b
 
 

@@ -180,9 +180,12 @@ def _sp_ok(*ts):
                              and (t.dim() < 2 or t.stride(-2) % 4 == 0)) for t in ts)
 
 
-def sp_fwd(xp, wp, M, N, K, bias=None, act=0, rng=None, salt=0, thresh=0, dscale=1.0, out_planes=False):
+def sp_fwd(xp, wp, M, N, K, bias=None, act=0, rng=None, salt=0, thresh=0, dscale=1.0, out_planes=False,
+           lse_part=None):
     """y[M,N] = dropout(act(x @ w^T + bias)) from planes xp [3,M,>=K], wp [3,N,>=K].  Returns
-    (y, y_planes or None), or None when the kernel does not cover the case (caller falls back)."""
+    (y, y_planes or None), or None when the kernel does not cover the case (caller falls back).
+    ``lse_part``: fp32 [ceil(N/128), M, 2] filled with each row's per-128-column softmax
+    statistics (max, sum exp(y - max)) by the epilogue (the fused cross-entropy forward)."""
     if not SP or act not in (0, 1) or not _sp_ok(bias):
         return None
     y = torch.empty(M, N, device=xp.device, dtype=torch.float32)
@@ -192,7 +195,7 @@ def sp_fwd(xp, wp, M, N, K, bias=None, act=0, rng=None, salt=0, thresh=0, dscale
     ok = _native.C().gemm_sp(0, xp.data_ptr(), xp.stride(1), xp.stride(0), wp.data_ptr(), wp.stride(1), wp.stride(0),
                              M, N, K, 0, y.data_ptr(), y.stride(0), _native.ptr(yp), N, yp.stride(0) if yp is not None
                              else 0, 0, _native.ptr(bias), int(act), 0, 0, 0, 0, rng.ptr() if rng is not None else 0,
-                             salt, thresh, dscale, 0, _native.stream())
+                             salt, thresh, dscale, 0, _native.ptr(lse_part), _native.stream())
     return (y, yp) if ok else None
 
 
@@ -212,7 +215,7 @@ def sp_dgrad(dyp, wp, M, K, N, resid=None, dact_y=None, dscale=1.0, out_planes=F
                              dx.stride(0) if dx is not None else 0, _native.ptr(dxp), K,
                              dxp.stride(0) if dxp is not None else 0, 0, 0, 0, _native.ptr(resid),
                              resid.stride(0) if resid is not None else 0, _native.ptr(dact_y),
-                             dact_y.stride(0) if dact_y is not None else 0, 0, 0, 0, dscale, 0, _native.stream())
+                             dact_y.stride(0) if dact_y is not None else 0, 0, 0, 0, dscale, 0, 0, _native.stream())
     return (dx, dxp) if ok else None
 
 
@@ -225,4 +228,4 @@ def sp_wgrad(dyp, xp, gw, gb=None):
     M = dyp.shape[1]
     return bool(_native.C().gemm_sp(2, dyp.data_ptr(), dyp.stride(1), dyp.stride(0), xp.data_ptr(), xp.stride(1),
                                     xp.stride(0), N, K, M, 0, gw.data_ptr(), gw.stride(0), 0, 0, 0, 1, 0, 0, 0, 0, 0,
-                                    0, 0, 0, 0, 1.0, _native.ptr(gb), _native.stream()))
+                                    0, 0, 0, 0, 1.0, _native.ptr(gb), 0, _native.stream()))

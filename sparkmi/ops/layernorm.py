@@ -46,6 +46,7 @@ class AddDropoutLayerNorm(torch.autograd.Function):
         ctx.p, ctx.rng, ctx.salt, ctx.D, ctx.M = p, rng, salt, D, M
         ctx.has_r = r is not None
         ctx.r_slot = r_slot
+        ctx.h_gplanes = _pl.grad_planes_ok(h)  # dh may be handed back as planes only
         if _native.use_native(h):
             C = _native.C()
             h = h.contiguous()
@@ -94,9 +95,13 @@ class AddDropoutLayerNorm(torch.autograd.Function):
                     0, 0, 1, M, D, ctx.rng.ptr(), ctx.salt, _rng.threshold(p), _rng.scale(p))
             if dy.dtype == torch.float32:
                 dhp = _planes_for(dh, D, M)  # dY operand of the sublayer's last Linear (dgrad + wgrad)
+                only = dhp is not None and ctx.h_gplanes  # ... which reads nothing else: planes only
+                if only:
+                    args = args[:6] + (0,) + args[7:]
                 C.ln_bwd_f32(*args, _native.ptr(dhp), dhp.stride(0) if dhp is not None else 0, _native.stream())
                 if dhp is not None:
                     _pl.attach(dh, dhp)
+                    dh._smi_planes_only = only
             else:
                 C.ln_bwd(*args, _native.stream())
             if _grad.LN_DEFER:  # folded with every other LayerNorm's at the end of the backward

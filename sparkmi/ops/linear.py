@@ -113,6 +113,7 @@ def _wgrad_accumulate(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, gb=
             if G.sp_wgrad(dyp, xp, gw, gb):
                 return False
     if dy2.dtype == torch.float32:
+        _pl.f32(dy2)  # a planes-only gradient on a path that reads fp32
         if (ready is not None and _grad.WGRAD_GROUP and G.supported32(N, K, M, dy2, x2, mode=2)
                 and gw.is_contiguous() and _groupable(dy2, x2) and (gb is None or gb.is_contiguous())):
             _grad.defer_wgrad_group(dy2, x2, gw, gb, ready, _native.stream())
@@ -131,19 +132,23 @@ def _wgrad_accumulate(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, gb=
     return False
 
 
-def _dgrad(g2, w_bf, resid=None, dact_y=None, dscale=1.0, wp=None, out_planes=False):
+def _dgrad(g2, w_bf, resid=None, dact_y=None, dscale=1.0, wp=None, out_planes=False, need_f32=True):
+    """dX = dY W (+resid) (x relu'/dropout mask); fp32: on the split-plane GEMM from dY's planes.
+    ``need_f32=False`` with ``out_planes``: dX as planes only (a placeholder fp32 tensor)."""
     M, N = g2.shape
     K = w_bf.shape[1]
     if g2.dtype == torch.float32:
         if wp is not None and G.SP and G._sp_ok(g2):
             r = G.sp_dgrad(_pl.of(g2, kpad=N % 32 != 0), wp, M, K, N, resid=resid, dact_y=dact_y, dscale=dscale,
-                           out_planes=out_planes)
+                           out_planes=out_planes, need_f32=need_f32 or not out_planes)
             if r is not None:
                 dx, dxp = r
+                if dx is None:
+                    return _pl.placeholder((M, K), dxp, g2.device)
                 if dxp is not None:
                     _pl.attach(dx, dxp)
                 return dx
-        return _dgrad32_any(g2, w_bf, resid, dact_y, dscale)
+        return _dgrad32_any(_pl.f32(g2), w_bf, resid, dact_y, dscale)
     if G.supported(M, K, N, g2, w_bf, resid, dact_y, mode=1):
         return G.dgrad(g2, w_bf, resid=resid, dact_y=dact_y, dscale=dscale)
     f32 = [t.float() if t is not None else None for t in (g2, w_bf, resid, dact_y)]
@@ -155,18 +160,29 @@ def compute_weight(p: torch.Tensor, dtype) -> torch.Tensor:
     return p.detach() if dtype == torch.float32 else bf16_weight(p)
 
 
-def _fwd_sp(x2, wp, N, bias, act, p, rng, salt, out_planes=False):
-    """fp32 forward on the split-plane GEMM (x2's planes: cached or split now); None if not covered."""
+def _fwd_sp(x2, wp, N, bias, act, p, rng, salt, out_planes=False, lse_stats=False):
+    """fp32 forward on the split-plane GEMM (x2's planes: cached or split now); None if not covered.
+    ``lse_stats``: the epilogue also writes per-row softmax statistics, attached to y for the
+    cross-entropy that consumes it (sparkmi/ops/loss.py)."""
     M, K = x2.shape
     if wp is None or not G.SP or not G._sp_ok(x2) or act not in (0, 1):
         return None
+    part = None
+    if lse_stats and bias is not None and act == 0 and p == 0 and not out_planes:
+        part = torch.empty((N + 127) // 128, M, 2, device=x2.device, dtype=torch.float32)
     r = G.sp_fwd(_pl.of(x2), wp, M, N, K, bias, act, rng, salt, _rng.threshold(p), _rng.scale(p),
-                 out_planes=out_planes)
+                 out_planes=out_planes, lse_part=part)
+    if r is None and part is not None:  # the statistics epilogue not covered: plain forward
+        part = None
+        r = G.sp_fwd(_pl.of(x2), wp, M, N, K, bias, act, rng, salt, _rng.threshold(p), _rng.scale(p),
+                     out_planes=out_planes)
     if r is None:
         return None
     y, yp = r
     if yp is not None:
         _pl.attach(y, yp)
+    if part is not None:
+        y._smi_lse = (part, y._version)
     return y
 
 
@@ -174,11 +190,12 @@ def _wplanes(weight):
     return _pl.weight(weight) if G.SP and weight.dim() == 2 and weight.shape[1] % 8 == 0 else None
 
 
-def _fwd_native(x2, weight, bias, act, p, rng, salt, w_bf=None, out_planes=False, wp=None):
+def _fwd_native(x2, weight, bias, act, p, rng, salt, w_bf=None, out_planes=False, wp=None, lse_stats=False):
     N, K = weight.shape
     M = x2.shape[0]
     if x2.dtype == torch.float32:
-        y = _fwd_sp(x2, wp if wp is not None else _wplanes(weight), N, bias, act, p, rng, salt, out_planes)
+        y = _fwd_sp(x2, wp if wp is not None else _wplanes(weight), N, bias, act, p, rng, salt, out_planes,
+                    lse_stats)
         if y is not None:
             return y
         return _fwd32_any(x2, weight.detach(), bias, act, rng, salt, p)
@@ -215,7 +232,7 @@ def _ref_act_bwd(g2, y2, act, p, seed, salt):
 
 class LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, act, p, rng, salt, x_slot=None):
+    def forward(ctx, x, weight, bias, act, p, rng, salt, x_slot=None, planes=0):
         shp = x.shape
         K = shp[-1]
         N = weight.shape[0]
@@ -224,13 +241,14 @@ class LinearFn(torch.autograd.Function):
         ctx.native = _native.use_native(x)
         if ctx.native:
             x2 = x2.contiguous()
-            y2 = _fwd_native(x2, weight, bias, act, p, rng, salt)
+            y2 = _fwd_native(x2, weight, bias, act, p, rng, salt, out_planes=bool(planes & 1),
+                             lse_stats=bool(planes & 4))
             ctx.x_planes = _pl.cached(x2)  # kept for the weight-gradient GEMM
             ctx.seed = 0
         else:
             ctx.seed = rng.current() if p > 0 else 0
             y2 = _ref_fwd(x2, weight, bias, act, p, ctx.seed, salt).to(x.dtype)
-        ctx.x_slot = x_slot
+        ctx.x_slot, ctx.dx_planes = x_slot, bool(planes & 2)
         ctx.save_for_backward(x2, weight, bias, y2 if act else None)
         return y2.reshape(*shp[:-1], N)
 
@@ -243,6 +261,8 @@ class LinearFn(torch.autograd.Function):
         gw = grad_buf(weight)
         if ctx.native:
             C = _native.C()
+            if act or p > 0 or not dy2.is_contiguous():
+                _pl.f32(dy2)  # read as fp32 below
             dy2 = dy2.contiguous()
             if act or p > 0:
                 g2 = torch.empty_like(dy2)
@@ -254,7 +274,8 @@ class LinearFn(torch.autograd.Function):
             resid = _slot_grad(ctx.x_slot, g2.shape[0])
             f32 = g2.dtype == torch.float32
             wp = _wplanes(weight) if f32 else None
-            dx = _dgrad(g2, compute_weight(weight, g2.dtype), resid=resid, wp=wp) if ctx.needs_input_grad[0] else None
+            dx = _dgrad(g2, compute_weight(weight, g2.dtype), resid=resid, wp=wp,
+                        out_planes=ctx.dx_planes) if ctx.needs_input_grad[0] else None
             bgrad = grad_buf(bias) if bias is not None else None
             if f32 and G.SP and ctx.x_planes is not None:
                 _pl.attach(x2, ctx.x_planes)
@@ -278,7 +299,7 @@ class LinearFn(torch.autograd.Function):
             grad_ready(weight, bias)
         if dx is not None:
             dx = dx.reshape(*dy.shape[:-1], K)
-        return dx, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None
 
 
 def _slot_grad(slot, rows):
@@ -289,16 +310,21 @@ def _slot_grad(slot, rows):
     return g.reshape(rows, -1).contiguous() if g is not None else None
 
 
-def linear(x, weight, bias=None, act=None, p=0.0, rng=None, salt=0, x_slot=None):
+def linear(x, weight, bias=None, act=None, p=0.0, rng=None, salt=0, x_slot=None, out_planes=False, dx_planes=False,
+           lse_stats=False):
     """y = dropout_p(act(x @ weight^T + bias)); act in {None, 'relu', 'sigmoid'}.  ``x_slot``:
-    a ResidualGrad whose parked gradient is added to dX in the dgrad epilogue."""
+    a ResidualGrad whose parked gradient is added to dX in the dgrad epilogue.  fp32 GPU path:
+    ``out_planes`` / ``dx_planes`` make the forward / dgrad epilogue also write the split planes of
+    y / dX (sparkmi/ops/planes.py) for a consumer that reads planes (the attention kernels);
+    ``lse_stats``: per-row softmax statistics of y for a cross-entropy on it (sparkmi/ops/loss.py)."""
     a = ACTS[act] if not isinstance(act, int) else act
     if a == 2 and p > 0:
         raise ValueError("sigmoid + dropout epilogue is not supported")
     if rng is None:
         from .layernorm import _NULL_RNG
         rng, p = _NULL_RNG, 0.0
-    return LinearFn.apply(x, weight, bias, a, float(p), rng, int(salt), x_slot)
+    return LinearFn.apply(x, weight, bias, a, float(p), rng, int(salt), x_slot,
+                          (1 if out_planes else 0) | (2 if dx_planes else 0) | (4 if lse_stats else 0))
 
 
 class FFNFn(torch.autograd.Function):
@@ -341,8 +367,11 @@ class FFNFn(torch.autograd.Function):
                     _pl.attach(h, ctx.h_planes)
             # dh_pre = (dy @ W2) * relu'/dropout mask (from the saved output h), fused epilogue
             # (fp32: its planes written by the same epilogue, for linear1's dgrad and wgrad)
+            if not dy2.is_contiguous():
+                _pl.f32(dy2)
+            # dh feeds only linear1's dgrad / wgrad, both on its planes: planes only
             dh = _dgrad(dy2, compute_weight(w2, dy2.dtype), dact_y=h, dscale=_rng.scale(p),
-                        wp=_wplanes(w2) if f32 else None, out_planes=True)
+                        wp=_wplanes(w2) if f32 else None, out_planes=True, need_f32=not _pl.PLANES_ONLY)
             gw2, gb2, gw1, gb1 = grad_buf(w2), grad_buf(b2), grad_buf(w1), grad_buf(b1)
             with _grad.side(dy2.device, dy2, h):
                 if not _wgrad_accumulate(gw2, dy2, h, gb2, ready=(w2, b2)):
@@ -390,7 +419,10 @@ class ConcatLinearFn(torch.autograd.Function):
         x2 = x.reshape(-1, K).contiguous()
         w = wm.view(N, K)
         wp = wviews[3] if len(wviews) > 3 and x2.dtype == torch.float32 and G.SP else None
-        y2 = _fwd_native(x2, w, bm, 0, 0.0, None, 0, w_bf=ws.view(N, K) if ws is not None else None, wp=wp)
+        # fp32 + SMI_ATTN_PLANES: the planes of y too, read by the cross-attention kernels
+        from ..models import transformer as _tm
+        y2 = _fwd_native(x2, w, bm, 0, 0.0, None, 0, w_bf=ws.view(N, K) if ws is not None else None, wp=wp,
+                         out_planes=wp is not None and _tm.ATTN_PLANES)
         ctx.wviews, ctx.bg, ctx.shape, ctx.params, ctx.shared = wviews, bg, shape, params, shared
         ctx.x_planes, ctx.wp = _pl.cached(x2), wp
         ctx.save_for_backward(x2)

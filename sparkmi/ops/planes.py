@@ -14,9 +14,17 @@ operand ONCE, where it is produced:
 A k-contiguous GEMM operand whose k extent is not a multiple of 32 (the vocabulary dimension in
 the vocab projection's dgrad) is stored with ``ld`` rounded up and zero padding.
 """
+import os
+
 import torch
 
 from .. import _native
+
+# Planes-only gradients: a gradient whose every consumer reads split planes (the dY operand of a
+# dgrad / wgrad GEMM pair) is written by its producer as planes alone — its fp32 tensor is a
+# placeholder that is never filled unless a fallback path asks for it (f32() below).  The FFN
+# hidden gradient, dlogits, the LayerNorm dh and the attention dQ/dK/dV skip 4 B per element.
+PLANES_ONLY = os.environ.get("SMI_PLANES_ONLY", "1") != "0"
 
 
 def r32(n):
@@ -77,3 +85,50 @@ def weight(w):
     if fn is not None:
         return fn()
     return split(w.detach().reshape(w.shape[0], -1))
+
+
+def placeholder(like_shape, planes, device):
+    """An fp32 tensor standing for the values held in ``planes`` (not filled: planes-only)."""
+    t = torch.empty(like_shape, device=device, dtype=torch.float32)
+    attach(t, planes)
+    t._smi_planes_only = True
+    return t
+
+
+def mark_grad_planes_ok(t):
+    """Declare that t's gradient may be planes-only: t was produced by a sparkmi Linear / FFN
+    (whose backward reads dY through planes) and has exactly ONE differentiable consumer (autograd
+    would otherwise add a second gradient to the placeholder).  The model code marks such tensors
+    (sparkmi/models/transformer.py); user tensors are never marked, so a .grad stays real."""
+    if t.dtype == torch.float32 and t.is_cuda:
+        t._smi_gplanes = True
+    return t
+
+
+def grad_planes_ok(t):
+    """A planes-only gradient for t is allowed: PLANES_ONLY is on and t came from a producer that
+    reads planes (never a user tensor, whose .grad must hold real values)."""
+    return PLANES_ONLY and any(b is not None and getattr(b, "_smi_gplanes", False) for b in (t, t._base))
+
+
+def planes_only(t):
+    """True when t (or the tensor t is a view of) holds its values in planes only."""
+    return any(b is not None and getattr(b, "_smi_planes_only", False) for b in (t, t._base))
+
+
+def f32(t):
+    """Fill a planes-only tensor's fp32 values from its planes (hi + mid + lo, exact) so that a
+    path that reads fp32 sees them; a no-op for ordinary tensors.  Returns t."""
+    for b in (t, t._base):
+        if b is None or not getattr(b, "_smi_planes_only", False):
+            continue
+        p = cached(b)
+        if p is None:
+            raise RuntimeError("planes-only tensor lost its planes")
+        W = b.shape[-1]
+        b2 = b.view(-1, W)
+        torch.add(p[0, :, :W].float(), p[1, :, :W].float(), out=b2)
+        b2.add_(p[2, :, :W].float())
+        b._smi_planes_only = False
+        attach(b, p)
+    return t

@@ -238,15 +238,18 @@ def _attn_f32(B, H, Sq, Sk, mode, cross, kp):
         _close(qg.grad, dqkv, 5e-5, 1e-5, f"dqkv {mode}")
 
 
-@pytest.fixture(params=[1, 0], ids=["staged_planes", "wave_split"])
+@pytest.fixture(params=[1, 2, 0], ids=["staged_planes", "staged_planes_dkdv4", "wave_split"])
 def attn_kernel(request):
-    """The split-product attention kernels: streamed chunks split once at LDS staging (default)
-    or per wave per fragment (C.attn_f32_sp(0)); irrelevant under the f32-MFMA algorithm."""
+    """The split-product attention kernels: streamed chunks split once at LDS staging (default;
+    dK/dV on 8-wave workgroups, or the 4-wave kernel: C.attn_dkdv8(0)) or per wave per fragment
+    (C.attn_f32_sp(0)); irrelevant under the f32-MFMA algorithm."""
     C = _native.C()
-    prev = C.attn_f32_sp(-1)
-    C.attn_f32_sp(request.param)
+    prev, prev8 = C.attn_f32_sp(-1), C.attn_dkdv8(-1)
+    C.attn_f32_sp(1 if request.param else 0)
+    C.attn_dkdv8(0 if request.param == 2 else 1)
     yield request.param
     C.attn_f32_sp(prev)
+    C.attn_dkdv8(prev8)
 
 
 @pytest.mark.parametrize("mode", ["none", "reference", "causal"])
@@ -258,6 +261,74 @@ def test_self_attention_f32(attn_kernel, mode, S):
 @pytest.mark.parametrize("mode,kp", [("none", False), ("none", True), ("reference", False)])
 def test_cross_attention_f32(attn_kernel, mode, kp):
     _attn_f32(2, 3, 130, 130 if mode == "reference" else 77, mode, True, kp)
+
+
+@pytest.mark.parametrize("cross", [False, True])
+@pytest.mark.parametrize("mode,S", [("none", 256), ("reference", 256), ("causal", 200), ("reference", 37)])
+def test_attention_f32_plane_inputs(f32_algo, mode, S, cross):
+    """Q/K/V (and dO) as producer-written split planes (sparkmi/ops/attention.py:_in_planes):
+    bitwise the fp32-input kernels' results (the planes are exactly the split the kernels make at
+    staging); planes of a DIFFERENT tensor change the result (the planes are what is read)."""
+    from sparkmi.ops import planes as PL
+    torch.manual_seed(11)
+    B, H, hd = 2, 3, 64
+    if cross:  # kv read from column 128 of a wider concatenated projection, like the decoder's
+        Sk = S + 5 if mode == "none" else S
+        q0, kv0 = torch.randn(B, S, H * hd, device=dev), torch.randn(B, Sk, 128 + 2 * H * hd, device=dev)
+        ins = (q0, kv0)
+    else:
+        ins = (torch.randn(B, S, 3 * H * hd, device=dev),)
+    do0 = torch.randn(B, S, H * hd, device=dev)
+
+    def run(planes, scale=1.0):
+        xs = [t.clone().requires_grad_() for t in ins]
+        if planes:
+            for t in xs:
+                PL.attach(t, PL.split((t.detach() * scale).reshape(-1, t.shape[-1])))
+        o = (cross_attention(xs[0], xs[1], H, mode, kv_col=128) if cross else self_attention(xs[0], H, mode))
+        do = do0.clone()
+        if planes:
+            PL.attach(do, PL.split((do0 * scale).reshape(-1, do0.shape[-1])))
+        o.backward(do)
+        g = [t.grad for t in xs]
+        if cross:  # kv_col = 128: the kv gradient's first 128 columns are not this op's
+            g[1] = g[1][..., 128:]
+        return [o.detach()] + g
+
+    ref, pin = run(False), run(True)
+    for a, b in zip(ref, pin):
+        assert torch.equal(a, b)
+    if f32_algo != 0:  # the split-product kernels read the planes (the f32-MFMA kernels never do)
+        other = run(True, 2.0)
+        assert not torch.equal(other[0], ref[0])
+        assert not torch.equal(other[1], ref[1])
+
+
+@pytest.mark.parametrize("M,V", [(8192, 10000), (300, 10000), (77, 45), (256, 384)])
+def test_vocab_linear_ce_fused_stats(M, V):
+    """The vocab projection's epilogue reduces each logits row per 128 columns (max, sum exp) and
+    the cross-entropy forward merges those (ce_fwd_part) instead of re-reading the logits: the
+    loss and its gradients equal the standalone ce_fwd path (a clone of the logits carries no
+    statistics) to fp32 rounding; ignored rows stay out of the mean."""
+    from sparkmi.ops.linear import linear
+    from sparkmi.ops.loss import _lse_part, cross_entropy
+    torch.manual_seed(12)
+    K = 512
+    x = torch.randn(M, K, device=dev) * 0.5
+    lin = torch.nn.Linear(K, V).to(dev)
+    lab = torch.randint(0, V, (M,), device=dev)
+    lab[::7] = 0
+    outs = []
+    for fused in (True, False):
+        xg = x.clone().requires_grad_()
+        logits = linear(xg, lin.weight, lin.bias, lse_stats=True)
+        if fused and G.SP and V % 8 == 0:
+            assert _lse_part(logits.reshape(-1, V)) is not None
+        loss = cross_entropy(logits if fused else logits.clone(), lab, ignore_index=0)
+        loss.backward()
+        outs.append((loss.detach(), xg.grad))
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=2e-6, atol=2e-6)
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-4, atol=1e-7)
 
 
 @pytest.mark.parametrize("p", [0.0, 0.1])
@@ -326,6 +397,27 @@ def test_transformer_f32_step_matches_cpu():
     for (n, pc), (_, pg) in zip(mc.named_parameters(), mg.named_parameters()):
         rel = (pg.grad.cpu().double() - pc.grad.double()).norm() / (pc.grad.double().norm() + 1e-12)
         assert rel < 1e-4, (n, float(rel))
+
+
+def test_transformer_f32_attention_plane_inputs_bitwise(monkeypatch):
+    """SMI_ATTN_PLANES: the projections / out-projection dgrad emit q/k/v/dO planes and the
+    attention kernels read them instead of splitting at staging — the whole step (loss and every
+    gradient) is bitwise the default path's."""
+    from sparkmi.data.synthetic import translation_pairs
+    from sparkmi.models import transformer as T
+    src, tgt = translation_pairs(4, 32, 96, 96, seed=3)
+    _, mg = _pair()
+    mg.train()
+    out = []
+    for planes in (False, True):
+        monkeypatch.setattr(T, "ATTN_PLANES", planes)
+        for p in mg.parameters():
+            p.grad = None
+        lg = mg.training_step_loss(src.to(dev), tgt.to(dev))
+        lg.backward()
+        out.append([lg.detach()] + [p.grad.clone() for p in mg.parameters()])
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
 
 
 def test_transformer_f32_loss_curve_matches_cpu():
