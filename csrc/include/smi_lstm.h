@@ -34,3 +34,4 @@ struct LSTMArgs {
 };
 #define LSTM_MAXT 2048
 #define LSTM_TCH 64  // timesteps per LDS-staged chunk in the kernels' tail phases
+#define LSTM_WCH 16  // ticks of per-tick outputs staged in LDS between burst stores (power of 2)

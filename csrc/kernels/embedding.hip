@@ -169,7 +169,16 @@ __global__ __launch_bounds__(1024) void emb_det_scan(EmbDet d) {
   for (int b0 = 0; b0 < d.NB; b0 += 1024) {
     const int b = b0 + threadIdx.x;
     int run = 0;
-    if (b < d.NB) {
+    if (b < d.NB && d.tiles <= 32) {  // every tile's count in flight at once: one load latency
+      int c[32];
+#pragma unroll
+      for (int t = 0; t < 32; ++t) c[t] = t < d.tiles ? d.counts[(size_t)t * d.NB + b] : 0;
+#pragma unroll
+      for (int t = 0; t < 32; ++t) {
+        if (t < d.tiles) d.offs[(size_t)t * d.NB + b] = run;
+        run += c[t];
+      }
+    } else if (b < d.NB) {
       int t = 0;
       for (; t + 8 <= d.tiles; t += 8) {  // 8 independent loads in flight
         int c[8];
@@ -207,20 +216,37 @@ __global__ __launch_bounds__(1024) void emb_det_scan(EmbDet d) {
     }
     __syncthreads();
   }
-  // heavy buckets (>= EMB_HEAVY tokens), in bucket order; at most T / EMB_HEAVY of them
-  if (threadIdx.x < 64) {
+  // heavy buckets (>= EMB_HEAVY tokens), in bucket order; at most T / EMB_HEAVY of them.  All 16
+  // waves: wave w counts its contiguous slice of buckets, the slices' counts are prefix-summed in
+  // LDS, then every wave writes its heavy buckets at its offset (one wave walking 4096 buckets in
+  // 64-bucket steps was a chain of 64 dependent global-load latencies)
+  if (d.hmax > 0) {
+    __shared__ int hcnt[16];
+    const int per = ((d.NB + 15) / 16 + 63) / 64 * 64;
+    const int lo = w * per, hi = min(d.NB, lo + per);
+    auto heavy = [&](int b) { return b < hi && d.bstart[b + 1] - d.bstart[b] >= EMB_HEAVY; };
     int cnt = 0;
-    for (int b0 = 0; b0 < d.NB; b0 += 64) {
+    for (int b0 = lo; b0 < hi; b0 += 64) cnt += __popcll(__ballot(heavy(b0 + lane)));
+    if (lane == 0) hcnt[w] = cnt;
+    __syncthreads();
+    int base = 0, tot = 0;
+    for (int i = 0; i < 16; ++i) {
+      base += i < w ? hcnt[i] : 0;
+      tot += hcnt[i];
+    }
+    for (int b0 = lo; b0 < hi; b0 += 64) {
       const int b = b0 + lane;
-      const bool h = b < d.NB && d.bstart[b + 1] - d.bstart[b] >= EMB_HEAVY;
+      const bool h = heavy(b);
       const unsigned long long bal = __ballot(h);
       if (h) {
-        const int r = cnt + __popcll(bal & ((1ull << lane) - 1ull));
+        const int r = base + __popcll(bal & ((1ull << lane) - 1ull));
         if (r < d.hmax) d.heavy[1 + r] = b;
       }
-      cnt += __popcll(bal);
+      base += __popcll(bal);
     }
-    if (lane == 0) d.heavy[0] = min(cnt, d.hmax);
+    if (threadIdx.x == 0) d.heavy[0] = min(tot, d.hmax);
+  } else if (threadIdx.x == 0) {
+    d.heavy[0] = 0;
   }
 }
 

@@ -28,10 +28,12 @@
 #include "smi_common.h"
 #include "smi_lstm.h"
 
-__device__ __forceinline__ float smi_sigmoid(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// v_rcp_f32 (1 ulp) instead of the IEEE division sequence (~10 dependent instructions): the
+// activations sit on the recurrence's serial chain three times per tick
+__device__ __forceinline__ float smi_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 __device__ __forceinline__ float smi_tanh(float x) {
   const float e = __expf(-2.0f * fabsf(x));
-  const float t = (1.0f - e) / (1.0f + e);
+  const float t = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
   return copysignf(t, x);
 }
 
@@ -374,6 +376,10 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
   __shared__ __attribute__((aligned(16))) float s_h[2][2][LSTM_MAXL * SH];
   __shared__ float s_g[2][LSTM_MAXL][4][H];                                // [buf][layer][gate][unit]
   __shared__ long long s_ids[LSTM_MAXT];
+  // saved activations of the last LSTM_WCH ticks, [tick % LSTM_WCH][layer][i f g o c h][unit],
+  // flushed to the workspace in bursts (a global store inside the tick shares vmcnt with the
+  // prefetched embedding loads: every tick waited for its stores' round trip)
+  __shared__ __attribute__((aligned(16))) float s_ws[LSTM_WCH][(64 / H) * 6 * H];
   for (int i = tid; i < T; i += blockDim.x) s_ids[i] = a.ids[(size_t)b * T + i];
 
   const int g0 = 2 * w, g1 = 2 * w + 1;
@@ -404,7 +410,10 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
     s_h[w][1][l * SH + j] = hl;
   }
   __syncthreads();  // s_ids
-  auto emb_at = [&](int t) { return (lane < E && t < T) ? a.emb[(size_t)s_ids[t] * E + lane] : 0.f; };
+  // unconditional (clamped) load with no select on its value: a load inside a branch, or a mask
+  // applied right after it, makes the compiler wait for it in the same tick.  Rows past T are
+  // only ever read by layer 0 at ticks where it is off; lanes >= E never write them.
+  auto emb_at = [&](int t) { return a.emb[(size_t)s_ids[min(t, T - 1)] * E + min(lane, E - 1)]; };
   if (lane < E) s_in[w][0][lane] = emb_at(0);
   float x0 = 0.f, x1 = emb_at(1), x2 = emb_at(2);
   __syncthreads();
@@ -412,6 +421,8 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
   const uint32_t seed = smi_seed(a.seedp, a.salt);
   float* wsb = a.ws + (size_t)b * L * T * 6 * H;
   const int nt = T + L - 1;
+  // every prologue load (weights, h0 / c0) retired here, so the tick loop's wait counts are exact
+  __builtin_amdgcn_s_waitcnt(0);
   auto tick = [&](int k, float& xnext, float& xload) {
     const int t = k - l;
     const bool on = act && t >= 0 && t < T;
@@ -448,7 +459,7 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
       c = fg * c + ig * gg;
       hl = og * smi_tanh(c);
       s_h[w][wb][l * SH + j] = hl;
-      float* ws = wsb + ((size_t)l * T + t) * 6 * H;
+      float* ws = &s_ws[k & (LSTM_WCH - 1)][l * 6 * H];
       if (w == 0) { ws[j] = ig; ws[H + j] = fg; ws[2 * H + j] = gg; }
       else { ws[3 * H + j] = og; ws[4 * H + j] = c; ws[5 * H + j] = hl; }
       if (l + 1 < L) {
@@ -457,11 +468,19 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
         s_in[w][wb][(l + 1) * SI + j] = hd;
       }
     }
-    if (lane < E) {  // layer 0's input for the next tick
-      s_in[w][wb][lane] = xnext;
-      xload = emb_at(k + 3);
-    }
+    if (lane < E) s_in[w][wb][lane] = xnext;  // layer 0's input for the next tick
+    xload = emb_at(k + 3);
     SMI_WAVE_LDS_ORDER();
+    if ((k & (LSTM_WCH - 1)) == LSTM_WCH - 1 || k == nt - 1) {  // burst the staged ticks to ws
+      __syncthreads();
+      const int k0 = k & ~(LSTM_WCH - 1), rows = (k - k0 + 1) * L;
+      constexpr int R4 = 6 * H / 4;  // float4 per (tick, layer) row
+      for (int e = tid; e < rows * R4; e += blockDim.x) {
+        const int r = e / R4, c4 = e - r * R4, kk = k0 + r / L, ll = r % L, tt = kk - ll;
+        if (tt >= 0 && tt < T)
+          *(float4*)(wsb + ((size_t)ll * T + tt) * 6 * H + 4 * c4) = *(const float4*)&s_ws[kk & (LSTM_WCH - 1)][ll * 6 * H + 4 * c4];
+      }
+    }
   };
   int k = 0;
   for (; k + 3 <= nt; k += 3) {
@@ -511,6 +530,9 @@ __global__ __launch_bounds__(128) void lstm_bwd_w2_kernel(LSTMArgs a) {
   __shared__ __attribute__((aligned(16))) float s_da[2][LSTM_MAXL][G + 4];  // per-wave copy
   __shared__ float s_dh[2][LSTM_MAXL][H];  // [buf]: W_hh^T da (wave 0)
   __shared__ float s_dx[2][LSTM_MAXL][H];  // [buf]: W_ih^T da, the layer below's input gradient (wave 1)
+  // gate gradients of the last LSTM_WCH ticks [tick % LSTM_WCH][layer][4H], burst-stored (no global
+  // store inside the tick: it would share vmcnt with the prefetched workspace loads)
+  __shared__ __attribute__((aligned(16))) float s_dab[LSTM_WCH][(64 / H) * G];
   // wave 0: column j of W_hh[l]; wave 1: column j of W_ih[l] (l >= 1: In = H; layer 0's input
   // gradient is lstm_xe_kernel's job after the loop)
   const bool prod = act && (w == 0 || l >= 1);
@@ -537,15 +559,19 @@ __global__ __launch_bounds__(128) void lstm_bwd_w2_kernel(LSTMArgs a) {
   float* dab = a.ws_da + (size_t)b * L * T * G;
   const int nt = T + L - 1;
   const int tl = T - 1 + (L - 1 - l);
+  const float c0v = (act && a.c0) ? a.c0[((size_t)l * a.B + b) * H + j] : 0.f;
+  // every lane loads every value at clamped indices (no branch around a load: the compiler can
+  // then count vmcnt exactly instead of waiting for everything in flight)
   auto load_in = [&](int t, LstmBwdIn<CM>& v) {
-    if (!act || t < 0 || t >= T) return;
-    const float* ws = wsb + ((size_t)l * T + t) * 6 * H;
+    const int tc = min(max(t, 0), T - 1);
+    const float* ws = wsb + ((size_t)(act ? l : L - 1) * T + tc) * 6 * H;
     v.ig = ws[j]; v.fg = ws[H + j]; v.gg = ws[2 * H + j]; v.og = ws[3 * H + j]; v.cc = ws[4 * H + j];
-    v.cp = t > 0 ? ws[j - 2 * H] : (a.c0 ? a.c0[((size_t)l * a.B + b) * H + j] : 0.f);
-    if (top) {
+    const float cpv = ws[(tc > 0 ? -2 * H : 4 * H) + j];  // c at t - 1 (t = 0: c0)
+    v.cp = t > 0 ? cpv : c0v;
 #pragma unroll
-      for (int q = 0; q < CM; ++q)
-        v.dp[q] = (q < C && (!a.dpred_last || t == T - 1)) ? dpred[(size_t)(a.dpred_last ? 0 : t) * C + q] : 0.f;
+    for (int q = 0; q < CM; ++q) {
+      const float d = dpred[(size_t)(a.dpred_last ? 0 : tc) * C + min(q, C - 1)];
+      v.dp[q] = (top && q < C && (!a.dpred_last || t == T - 1)) ? d : 0.f;
     }
   };
   auto prep = [&](int t, LstmBwdIn<CM>& v) {
@@ -568,6 +594,7 @@ __global__ __launch_bounds__(128) void lstm_bwd_w2_kernel(LSTMArgs a) {
   load_in(tl, ia);
   load_in(tl - 1, ib);
   prep(tl, ia);
+  __builtin_amdgcn_s_waitcnt(0);  // prologue loads retired: exact wait counts in the tick loop
   float dh_first = 0.f;  // W_hh^T da at t = 0 (wave 0): the gradient of h0
   auto tick = [&](int k, const LstmBwdIn<CM>& cv, LstmBwdIn<CM>& pv, LstmBwdIn<CM>& nv) {
     const int t = tl - k;
@@ -580,7 +607,7 @@ __global__ __launch_bounds__(128) void lstm_bwd_w2_kernel(LSTMArgs a) {
       dc += dh * cv.A;
       const float d0 = dc * cv.gi, d1 = dc * cv.cf, d2 = dc * cv.ig2, d3 = dh * cv.Bo;
       s_da[w][l][j] = d0; s_da[w][l][H + j] = d1; s_da[w][l][2 * H + j] = d2; s_da[w][l][3 * H + j] = d3;
-      float* dg = dab + ((size_t)l * T + t) * G;
+      float* dg = &s_dab[k & (LSTM_WCH - 1)][l * G];
       if (w == 0) { dg[j] = d0; dg[H + j] = d1; }
       else { dg[2 * H + j] = d2; dg[3 * H + j] = d3; }
       dc *= cv.fg;
@@ -608,6 +635,16 @@ __global__ __launch_bounds__(128) void lstm_bwd_w2_kernel(LSTMArgs a) {
       }
     }
     smi_lds_barrier();
+    if ((k & (LSTM_WCH - 1)) == LSTM_WCH - 1 || k == nt - 1) {  // burst the staged gate gradients
+      const int k0 = k & ~(LSTM_WCH - 1), rows = (k - k0 + 1) * L;
+      constexpr int R4 = G / 4;
+      for (int e = tid; e < rows * R4; e += blockDim.x) {
+        const int r = e / R4, c4 = e - r * R4, kk = k0 + r / L, ll = r % L, tt = T - 1 + (L - 1 - ll) - kk;
+        if (tt >= 0 && tt < T)
+          *(float4*)(dab + ((size_t)ll * T + tt) * G + 4 * c4) = *(const float4*)&s_dab[kk & (LSTM_WCH - 1)][ll * G + 4 * c4];
+      }
+      __syncthreads();  // the next tick overwrites slot 0
+    }
   };
   int k = 0;
   for (; k + 3 <= nt; k += 3) {

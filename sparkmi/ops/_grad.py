@@ -221,7 +221,7 @@ def _queued(params):
 
 def pending():
     """True when deferred work is queued or a flush is scheduled."""
-    return bool(_cb[0] or _ln_queue or _fold_queue or _group_queue)
+    return bool(_cb[0] or _ln_queue or _fold_queue or _group_queue or _async["main"] is not None)
 
 
 def reset_deferred():
@@ -229,6 +229,8 @@ def reset_deferred():
     work leaves the queues filled and the flush flag set (autograd discards its final callbacks);
     without this reset every later backward would queue work that is never flushed."""
     stale = pending()
+    if _async["main"] is not None:
+        _join_async()
     _ln_queue.clear()
     _fold_queue.clear()
     _group_queue.clear()
@@ -380,10 +382,59 @@ def _flush_folds(C, fq):
                     outs.add(e[5].data_ptr())
 
 
+# ---- overlapped weight-gradient group ----
+# The queued weight gradients of the part of the backward that is already done (the decoder's,
+# once the backward reaches the encoder) do not depend on anything that follows, so they can run
+# on a side stream while the rest of the backward runs: compute-bound wgrad tiles fill the CUs
+# the bandwidth-bound LayerNorms and the latency-bound attention kernels leave idle.  ONE fork
+# and ONE join per backward (a side stream per Linear cost 15-20 us per cross-queue dependency,
+# see _SIDE_ENABLED above).  The launched operands stay referenced until the join; their
+# parameters are reported final only after it.  Single-process only (no defer listeners: the
+# data-parallel engine runs its own early flushes).  SMI_WGRAD_OVERLAP=0 disables it.
+WGRAD_OVERLAP = os.environ.get("SMI_WGRAD_OVERLAP", "1") != "0" and not _SIDE_ENABLED
+_async = {"main": None, "dev": None, "hold": []}
+
+
+def flush_groups_async(device):
+    """Launch the queued grouped weight-gradient GEMMs now on the side stream of ``device``."""
+    if not (WGRAD_OVERLAP and WGRAD_GROUP and _group_queue) or _defer_listeners or device.type != "cuda":
+        return False
+    from .. import _native
+    dev = device.index if device.index is not None else torch.cuda.current_device()
+    if _async["main"] is not None and _async["dev"] != dev:
+        return False
+    gq = list(_group_queue)
+    _group_queue.clear()
+    _group_bytes.clear()
+    main = torch.cuda.current_stream(dev)
+    side = _side_stream(dev)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        st = _native.stream()
+        _flush_groups(_native.C(), [e[:5] + (st,) for e in gq])
+    if _async["main"] is None:
+        _async["main"], _async["dev"] = main, dev
+    _async["hold"].extend(gq)
+    _queue_flush()  # the end-of-backward flush joins the side stream
+    return True
+
+
+def _join_async():
+    main = _async["main"]
+    if main is None:
+        return []
+    main.wait_stream(_side_streams[_async["dev"]])
+    held = _async["hold"]
+    _async["main"], _async["dev"], _async["hold"] = None, None, []
+    return held
+
+
 def flush_deferred():
     """Launch every queued weight-gradient GEMM / fold, then report the parameters final.
     The queues are emptied first (try/finally): a launch that raises leaves no stale entries."""
     from .. import _native
+    for e in _join_async():  # overlapped groups: joined into the main stream, now final
+        grad_ready(*e[4])
     gq, lq, fq = list(_group_queue), list(_ln_queue), list(_fold_queue)
     _group_queue.clear()
     _group_bytes.clear()

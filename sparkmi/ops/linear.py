@@ -437,6 +437,9 @@ class ConcatLinearFn(torch.autograd.Function):
         if g is None:  # no consumer produced a gradient
             grad_ready(*ctx.params)
             return None, None, None, None, None, None
+        # every consumer of this projection (the decoder) has finished its backward: its queued
+        # weight gradients run on a side stream beside the rest (the encoder's backward)
+        _grad.flush_groups_async(g.device)
         g2 = g.reshape(-1, N)
         w = wm.view(N, K) if g2.dtype == torch.float32 else ws.view(N, K)
         dx = _dgrad(g2, w, wp=ctx.wp) if ctx.needs_input_grad[0] else None

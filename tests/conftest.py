@@ -22,3 +22,14 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _fresh_dropout_salts():
+    """Every test builds its models from the first dropout salt (sparkmi/ops/rng.py: salts are a
+    process-global counter), so a test's dropout masks — its problem instance — do not depend on
+    how many models earlier tests built (a trajectory test with a loss spike passed alone and
+    failed after the rest of its file)."""
+    from sparkmi.ops import rng
+    rng.reset_salts()
+    yield

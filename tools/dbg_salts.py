@@ -1,0 +1,30 @@
+"""Does the GPU-vs-CPU gradient check depend on the dropout salt values (process-global counter)?"""
+import os, sys, torch
+sys.path.insert(0, os.getcwd())
+from sparkmi import _native
+import tests.test_f32_gpu as T
+from sparkmi.ops import rng as R
+from sparkmi.data.synthetic import translation_pairs
+from sparkmi.utils.flat import FlatParams
+C = _native.C()
+for burn in range(0, 400, 23):
+    R.reset_salts()
+    for _ in range(burn):
+        R.new_salt()
+    for algo in (6, 0):
+        C.gemm_f32_algo(algo)
+        mc, mg = T._pair(L=3)
+        mc.train(); mg.train()
+        fc, fg = FlatParams(mc), FlatParams(mg, shadow=False)
+        src, tgt = translation_pairs(4, 32, 96, 96, seed=3)
+        fg.zero_grad()
+        lc = mc.training_step_loss(src, tgt)
+        lg = mg.training_step_loss(src.to('cuda'), tgt.to('cuda'))
+        lc.backward(); lg.backward(); torch.cuda.synchronize()
+        bad = []
+        for (n, pc), (_, pg) in zip(mc.named_parameters(), mg.named_parameters()):
+            rel = float((pg.grad.cpu().double() - pc.grad.double()).norm() / (pc.grad.double().norm() + 1e-12))
+            if not (rel < 1e-4): bad.append((n, round(rel, 5)))
+        if bad:
+            print("burn", burn, "algo", algo, "bad", len(bad), bad[:4], flush=True)
+print("done", flush=True)
