@@ -428,9 +428,11 @@ PYBIND11_MODULE(_C, m) {
   // (plane stride aps / bps), optional plane output P of the epilogue result
   m.def("gemm_sp", [](int mode, u A, long lda, long aps, u B, long ldb, long bps, int M, int N, int K, int kpad, u C,
                       long ldc, u Pp, long ldp, long pps, int beta_acc, u bias, int relu, u resid, long ldr, u dact_y,
-                      long ldy, u seedp, uint32_t salt, uint32_t thresh, float dscale, u bias_grad, u lse_part, u st) {
+                      long ldy, u seedp, uint32_t salt, uint32_t thresh, float dscale, u bias_grad, u lse_part, u mask,
+                      long ldm, u st) {
     GemmSpArgs g{};
     g.lse_part = (float*)lse_part;
+    g.mask = (unsigned char*)mask; g.ldm = ldm;
     g.mode = mode; g.A = (const unsigned short*)A; g.lda = lda; g.aps = aps;
     g.B = (const unsigned short*)B; g.ldb = ldb; g.bps = bps; g.M = M; g.N = N; g.K = K; g.kpad = kpad;
     g.C = (float*)C; g.ldc = ldc; g.P = (unsigned short*)Pp; g.ldp = ldp; g.pps = pps; g.beta_acc = beta_acc;

@@ -66,8 +66,9 @@ __device__ unsigned long long* g_sp_stamps;
 #define SP_STAMP(slot) do {} while (0)
 #endif
 
-enum : int { SE_BIAS = 1, SE_RELU = 2, SE_DROP = 8, SE_RESID = 16, SE_DACT = 32, SE_ACC = 64, SE_LSE = 128 };
-enum : int { SO_C = 1, SO_P = 2 };  // epilogue outputs: fp32 C, planes P
+enum : int { SE_BIAS = 1, SE_RELU = 2, SE_DROP = 8, SE_RESID = 16, SE_DACT = 32, SE_ACC = 64, SE_LSE = 128,
+              SE_DMASK = 256 };
+enum : int { SO_C = 1, SO_P = 2, SO_M = 4 };  // epilogue outputs: fp32 C, planes P, positivity mask
 
 typedef __attribute__((address_space(3))) void sp_lds_void;
 typedef __attribute__((ext_vector_type(4))) short sp_s16x4_t;
@@ -200,7 +201,9 @@ __device__ __forceinline__ void sp_store_tile(const GemmSpArgs& g, const float* 
       if (EPI & SE_RESID) rs = *(const float4*)(g.resid + (long)row * g.ldr + col);
       if (EPI & SE_DACT) dy = *(const float4*)(g.dact_y + (long)row * g.ldy + col);
       if ((EPI & SE_ACC) && hasC) cc = *(const float4*)(g.C + cidx);
+      const unsigned mk = (EPI & SE_DMASK) ? g.mask[(long)row * g.ldm + (col >> 2)] : 0u;
       const float rv[4] = {rs.x, rs.y, rs.z, rs.w}, dv[4] = {dy.x, dy.y, dy.z, dy.w}, cv[4] = {cc.x, cc.y, cc.z, cc.w};
+      unsigned bits = 0u;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float x = v[e] + bb[e];
@@ -208,23 +211,31 @@ __device__ __forceinline__ void sp_store_tile(const GemmSpArgs& g, const float* 
         if (EPI & SE_DROP) x = smi_keep(seed, (uint32_t)(cidx + e), g.thresh) ? x * g.dscale : 0.f;
         if (EPI & SE_RESID) x += rv[e];
         if (EPI & SE_DACT) x = dv[e] > 0.f ? x * g.dscale : 0.f;
+        if (EPI & SE_DMASK) x = ((mk >> e) & 1u) ? x * g.dscale : 0.f;
         if (EPI & SE_ACC) x += cv[e];
+        bits |= (x > 0.f ? 1u : 0u) << e;
         v[e] = x;
       }
       if (hasC) *(float4*)(g.C + cidx) = make_float4(v[0], v[1], v[2], v[3]);
       if (OUT & SO_P) sp_store4(g.P + (long)row * g.ldp + col, g.pps, v);
+      if (OUT & SO_M) g.mask[(long)row * g.ldm + (col >> 2)] = (unsigned char)bits;
     } else {
+      const unsigned mk = (EPI & SE_DMASK) ? g.mask[(long)row * g.ldm + (col >> 2)] : 0u;
+      unsigned bits = 0u;
       for (int e = 0; e < 4 && col + e < g.N; ++e) {
         float x = v[e] + bb[e];
         if (EPI & SE_RELU) x = fmaxf(x, 0.f);
         if (EPI & SE_DROP) x = smi_keep(seed, (uint32_t)(cidx + e), g.thresh) ? x * g.dscale : 0.f;
         if (EPI & SE_RESID) x += g.resid[(long)row * g.ldr + col + e];
         if (EPI & SE_DACT) x = g.dact_y[(long)row * g.ldy + col + e] > 0.f ? x * g.dscale : 0.f;
+        if (EPI & SE_DMASK) x = ((mk >> e) & 1u) ? x * g.dscale : 0.f;
         if ((EPI & SE_ACC) && hasC) x += g.C[cidx + e];
         if (hasC) g.C[cidx + e] = x;
         if (OUT & SO_P) sp_store1(g.P + (long)row * g.ldp + col + e, g.pps, x);
+        bits |= (x > 0.f ? 1u : 0u) << e;
         v[e] = x;
       }
+      if (OUT & SO_M) g.mask[(long)row * g.ldm + (col >> 2)] = (unsigned char)bits;
     }
     if constexpr ((EPI & SE_LSE) != 0) {
       // the row's (max, sum exp) over this tile's 128 columns: the 32 lanes of the half-wave hold

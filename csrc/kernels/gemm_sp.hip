@@ -94,21 +94,22 @@ extern "C" int smi_gemm_sp(const GemmSpArgs* args, hipStream_t st) {
   if (g.P && (((uintptr_t)g.P & 7) || g.ldp % 4 || g.pps % 4)) return -1;
   if (!g.C && !g.P) return -1;
   if (g.mode == 2 && g.P) return -1;
-  const int out = (g.C ? SO_C : 0) | (g.P ? SO_P : 0);
+  const int out = (g.C ? SO_C : 0) | (g.P ? SO_P : 0) | (g.mode == 0 && g.mask ? SO_M : 0);
+  if (g.mask && (g.ldm < (g.N + 3) / 4 || (g.mode == 1 && g.dact_y))) return -1;
   const bool t256 = sp_use256(g.M, g.N);
   const int nwg = t256 ? ((g.M + 255) / 256) * ((g.N + 127) / 128) : ((g.M + 127) / 128) * ((g.N + 127) / 128);
   const dim3 grid((unsigned)nwg);
   int epi = 0;
   if (g.mode == 0) epi = (g.bias ? SE_BIAS : 0) | (g.relu == 1 ? SE_RELU : 0) | (g.thresh ? SE_DROP : 0) |
                         (g.lse_part ? SE_LSE : 0);
-  else if (g.mode == 1) epi = (g.resid ? SE_RESID : 0) | (g.dact_y ? SE_DACT : 0);
+  else if (g.mode == 1) epi = (g.resid ? SE_RESID : 0) | (g.dact_y ? SE_DACT : 0) | (g.mask ? SE_DMASK : 0);
   if (g.beta_acc) epi |= SE_ACC;
   if (g.mode == 1) return smi_sp_launch_dgrad(g, epi, out, grid, t256, st);  // csrc/kernels/gemm_sp_dgrad.hip
   if (g.mode == 2) return smi_sp_launch_wgrad(g, epi, grid, st);       // csrc/kernels/gemm_sp_wgrad.hip
   const bool w8 = smi_sp_waves() == 8;
   // the feature sets the models use (anything else: the caller falls back to gemm_f32):
   // fp32 output, or fp32 output + planes (the FFN hidden activation, consumed by linear2)
-  if (g.relu > 1 || !g.C) return -1;
+  if (g.relu > 1 || (!g.C && out != (SO_P | SO_M))) return -1;
 #define SPF(E, O)                                                                                   \
   do {                                                                                              \
     if (t256 && smi_sp_tm() == 4) hipLaunchKernelGGL((gemm_sp4w_kernel<false, false, E, O>), grid, dim3(256), 0, st, g); \
@@ -120,8 +121,17 @@ extern "C" int smi_gemm_sp(const GemmSpArgs* args, hipStream_t st) {
 #define SPF_OUT(E)                  \
   do {                              \
     if (out == SO_C) SPF(E, SO_C);  \
-    else SPF(E, SO_C | SO_P);       \
+    else if (out == (SO_C | SO_P)) SPF(E, SO_C | SO_P); \
+    else return -1;                 \
   } while (0)
+  // the FFN hidden activation: planes for linear2's GEMMs + the positivity mask for its dgrad
+  // epilogue, no fp32 tensor (sparkmi/ops/linear.py FFNFn)
+  if (out == (SO_P | SO_M)) {
+    if (epi == (SE_BIAS | SE_RELU | SE_DROP)) SPF(SE_BIAS | SE_RELU | SE_DROP, SO_P | SO_M);
+    else if (epi == (SE_BIAS | SE_RELU)) SPF(SE_BIAS | SE_RELU, SO_P | SO_M);
+    else return -1;
+    SMI_CHECK_LAUNCH();
+  }
   switch (epi) {
     case 0: SPF_OUT(0); break;
     case SE_BIAS: SPF_OUT(SE_BIAS); break;

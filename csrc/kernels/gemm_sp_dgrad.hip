@@ -20,6 +20,9 @@ int smi_sp_launch_dgrad(const GemmSpArgs& g, int epi, int out, dim3 grid, bool t
   else if (epi == SE_DACT && out == (SO_C | SO_P)) SPD(SE_DACT, SO_C | SO_P);
   // the attention output's gradient dO (out-projection dgrad): planes for the attention backward
   // kernels (+ fp32 when a kernel without plane inputs reads it)
+  // linear2's dgrad on the FFN hidden mask instead of the fp32 activation
+  else if (epi == SE_DMASK && out == SO_P) SPD(SE_DMASK, SO_P);
+  else if (epi == SE_DMASK && out == (SO_C | SO_P)) SPD(SE_DMASK, SO_C | SO_P);
   else if (epi == 0 && out == SO_P) SPD(0, SO_P);
   else if (epi == 0 && out == (SO_C | SO_P)) SPD(0, SO_C | SO_P);
   else return -1;

@@ -39,6 +39,7 @@ __device__ __forceinline__ float smi_tanh(float x) {
 
 #ifdef LSTM_STAMPS  // diagnostic build only (tools/probes/lstm_probe.hip): per-phase cycle sums
 __device__ unsigned long long lstm_stamps[4][8];
+__device__ unsigned long long lstm_rt[4];  // [0..1] s_memrealtime / [2..3] s_memtime around the fwd tick loop
 #define LSTAMP_T(v) do { (v) = clock64(); } while (0)
 #define LSTAMP_ADD(slot, i, t0, t1) do { if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) lstm_stamps[slot][i] += (t1) - (t0); } while (0)
 #else
@@ -427,6 +428,9 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
     const int t = k - l;
     const bool on = act && t >= 0 && t < T;
     const int rb = k & 1, wb = rb ^ 1;
+    long long c_0 = 0, c_1 = 0, c_2 = 0, c_3 = 0;
+    (void)c_0; (void)c_1; (void)c_2; (void)c_3;
+    LSTAMP_T(c_0);
     if (on) {
       smi_f2 p0 = {bias0, 0.f}, q0 = {0.f, 0.f}, p1 = {bias1, 0.f}, q1 = {0.f, 0.f};
       const float* xin = &s_in[w][rb][l * SI];
@@ -453,7 +457,9 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
       s_g[rb][l][g0][j] = w == 1 ? smi_tanh(z0) : smi_sigmoid(z0);  // gate 2 (g) is the tanh one
       s_g[rb][l][g1][j] = smi_sigmoid(z1);
     }
+    LSTAMP_T(c_1);
     smi_lds_barrier();
+    LSTAMP_T(c_2);
     if (on) {
       const float ig = s_g[rb][l][0][j], fg = s_g[rb][l][1][j], gg = s_g[rb][l][2][j], og = s_g[rb][l][3][j];
       c = fg * c + ig * gg;
@@ -471,6 +477,10 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
     if (lane < E) s_in[w][wb][lane] = xnext;  // layer 0's input for the next tick
     xload = emb_at(k + 3);
     SMI_WAVE_LDS_ORDER();
+    LSTAMP_T(c_3);
+    LSTAMP_ADD(w, 0, c_0, c_1);  // gates: LDS reads, packed FMAs, activations
+    LSTAMP_ADD(w, 1, c_1, c_2);  // the barrier
+    LSTAMP_ADD(w, 2, c_2, c_3);  // cell update, LDS writes, prefetch
     if ((k & (LSTM_WCH - 1)) == LSTM_WCH - 1 || k == nt - 1) {  // burst the staged ticks to ws
       __syncthreads();
       const int k0 = k & ~(LSTM_WCH - 1), rows = (k - k0 + 1) * L;
@@ -483,6 +493,9 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
     }
   };
   int k = 0;
+#ifdef LSTM_STAMPS
+  unsigned long long rt0 = __builtin_amdgcn_s_memrealtime(), ct0 = __builtin_amdgcn_s_memtime();
+#endif
   for (; k + 3 <= nt; k += 3) {
     tick(k, x1, x0);
     tick(k + 1, x2, x1);
@@ -490,6 +503,12 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
   }
   if (k < nt) tick(k, x1, x0);
   if (k + 1 < nt) tick(k + 1, x2, x1);
+#ifdef LSTM_STAMPS
+  if (tid == 0 && b == 0) {
+    lstm_rt[0] += __builtin_amdgcn_s_memrealtime() - rt0;
+    lstm_rt[2] += __builtin_amdgcn_s_memtime() - ct0;
+  }
+#endif
   __syncthreads();  // ws (global) written by both waves is read by the fc head below
   if (act && w == 0) {
     if (a.hn) a.hn[((size_t)l * a.B + b) * H + j] = hl;

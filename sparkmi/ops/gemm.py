@@ -181,28 +181,36 @@ def _sp_ok(*ts):
 
 
 def sp_fwd(xp, wp, M, N, K, bias=None, act=0, rng=None, salt=0, thresh=0, dscale=1.0, out_planes=False,
-           lse_part=None):
+           lse_part=None, mask=None):
     """y[M,N] = dropout(act(x @ w^T + bias)) from planes xp [3,M,>=K], wp [3,N,>=K].  Returns
     (y, y_planes or None), or None when the kernel does not cover the case (caller falls back).
     ``lse_part``: fp32 [ceil(N/128), M, 2] filled with each row's per-128-column softmax
-    statistics (max, sum exp(y - max)) by the epilogue (the fused cross-entropy forward)."""
+    statistics (max, sum exp(y - max)) by the epilogue (the fused cross-entropy forward).
+    ``mask``: uint8 [M, ceil(N/4)] receiving bit e of column group c = (y[:, 4c + e] > 0) INSTEAD
+    of the fp32 y (returned None; planes required) — the FFN hidden activation's sign for the
+    linear2 dgrad epilogue."""
     if not SP or act not in (0, 1) or not _sp_ok(bias):
         return None
-    y = torch.empty(M, N, device=xp.device, dtype=torch.float32)
+    if mask is not None and not (out_planes and N % 32 == 0):
+        return None
+    y = torch.empty(M, N, device=xp.device, dtype=torch.float32) if mask is None else None
     yp = None
     if out_planes and N % 32 == 0:
         yp = torch.empty(3, M, N, device=xp.device, dtype=torch.bfloat16)
     ok = _native.C().gemm_sp(0, xp.data_ptr(), xp.stride(1), xp.stride(0), wp.data_ptr(), wp.stride(1), wp.stride(0),
-                             M, N, K, 0, y.data_ptr(), y.stride(0), _native.ptr(yp), N, yp.stride(0) if yp is not None
-                             else 0, 0, _native.ptr(bias), int(act), 0, 0, 0, 0, rng.ptr() if rng is not None else 0,
-                             salt, thresh, dscale, 0, _native.ptr(lse_part), _native.stream())
+                             # ldc = N without an fp32 output: the dropout hash index is row * ldc + col
+                             M, N, K, 0, _native.ptr(y), y.stride(0) if y is not None else N, _native.ptr(yp), N,
+                             yp.stride(0) if yp is not None else 0, 0, _native.ptr(bias), int(act), 0, 0, 0, 0,
+                             rng.ptr() if rng is not None else 0, salt, thresh, dscale, 0, _native.ptr(lse_part),
+                             _native.ptr(mask), mask.stride(0) if mask is not None else 0, _native.stream())
     return (y, yp) if ok else None
 
 
-def sp_dgrad(dyp, wp, M, K, N, resid=None, dact_y=None, dscale=1.0, out_planes=False, need_f32=True):
+def sp_dgrad(dyp, wp, M, K, N, resid=None, dact_y=None, dscale=1.0, out_planes=False, need_f32=True, dmask=None):
     """dx[M,K] = (dy @ w) (+ resid) (* [dact_y > 0] dscale) from planes dyp [3,M,>=N] (zero-padded
-    to a multiple of 32 when N is not), wp [3,N,K].  Returns (dx or None, dx_planes or None)."""
-    if not SP or not _sp_ok(resid, dact_y):
+    to a multiple of 32 when N is not), wp [3,N,K].  ``dmask`` (uint8 [M, ceil(K/4)], sp_fwd's
+    ``mask``) stands in for dact_y.  Returns (dx or None, dx_planes or None)."""
+    if not SP or not _sp_ok(resid, dact_y) or (dmask is not None and dact_y is not None):
         return None
     dx = torch.empty(M, K, device=dyp.device, dtype=torch.float32) if need_f32 else None
     dxp = None
@@ -212,10 +220,11 @@ def sp_dgrad(dyp, wp, M, K, N, resid=None, dact_y=None, dscale=1.0, out_planes=F
         return None
     ok = _native.C().gemm_sp(1, dyp.data_ptr(), dyp.stride(1), dyp.stride(0), wp.data_ptr(), wp.stride(1),
                              wp.stride(0), M, K, N, int(dyp.stride(1) >= (N + 31) // 32 * 32), _native.ptr(dx),
-                             dx.stride(0) if dx is not None else 0, _native.ptr(dxp), K,
+                             dx.stride(0) if dx is not None else K, _native.ptr(dxp), K,
                              dxp.stride(0) if dxp is not None else 0, 0, 0, 0, _native.ptr(resid),
                              resid.stride(0) if resid is not None else 0, _native.ptr(dact_y),
-                             dact_y.stride(0) if dact_y is not None else 0, 0, 0, 0, dscale, 0, 0, _native.stream())
+                             dact_y.stride(0) if dact_y is not None else 0, 0, 0, 0, dscale, 0, 0,
+                             _native.ptr(dmask), dmask.stride(0) if dmask is not None else 0, _native.stream())
     return (dx, dxp) if ok else None
 
 
@@ -228,4 +237,4 @@ def sp_wgrad(dyp, xp, gw, gb=None):
     M = dyp.shape[1]
     return bool(_native.C().gemm_sp(2, dyp.data_ptr(), dyp.stride(1), dyp.stride(0), xp.data_ptr(), xp.stride(1),
                                     xp.stride(0), N, K, M, 0, gw.data_ptr(), gw.stride(0), 0, 0, 0, 1, 0, 0, 0, 0, 0,
-                                    0, 0, 0, 0, 1.0, _native.ptr(gb), 0, _native.stream()))
+                                    0, 0, 0, 0, 1.0, _native.ptr(gb), 0, 0, 0, _native.stream()))

@@ -55,6 +55,10 @@ def _pad2(t, rows, cols):
     return out
 
 
+# FFN hidden activation as planes + positivity mask (no fp32 tensor); SMI_FFN_MASK=0 keeps fp32
+_FFN_MASK = __import__("os").environ.get("SMI_FFN_MASK", "1") != "0"
+
+
 def _fwd32_any(x2, w, bias, act, rng, salt, p):
     """fp32 forward for any shape: the kernel needs K % 4 (float4 k-loads); a ragged K is
     zero-padded (zeros add nothing).  Ragged N is handled by the kernel's scalar epilogue."""
@@ -113,7 +117,8 @@ def _wgrad_accumulate(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, gb=
             if G.sp_wgrad(dyp, xp, gw, gb):
                 return False
     if dy2.dtype == torch.float32:
-        _pl.f32(dy2)  # a planes-only gradient on a path that reads fp32
+        _pl.f32(dy2)  # a planes-only gradient / activation on a path that reads fp32
+        _pl.f32(x2)
         if (ready is not None and _grad.WGRAD_GROUP and G.supported32(N, K, M, dy2, x2, mode=2)
                 and gw.is_contiguous() and _groupable(dy2, x2) and (gb is None or gb.is_contiguous())):
             _grad.defer_wgrad_group(dy2, x2, gw, gb, ready, _native.stream())
@@ -132,15 +137,18 @@ def _wgrad_accumulate(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, gb=
     return False
 
 
-def _dgrad(g2, w_bf, resid=None, dact_y=None, dscale=1.0, wp=None, out_planes=False, need_f32=True):
+def _dgrad(g2, w_bf, resid=None, dact_y=None, dscale=1.0, wp=None, out_planes=False, need_f32=True, dmask=None):
     """dX = dY W (+resid) (x relu'/dropout mask); fp32: on the split-plane GEMM from dY's planes.
-    ``need_f32=False`` with ``out_planes``: dX as planes only (a placeholder fp32 tensor)."""
+    ``need_f32=False`` with ``out_planes``: dX as planes only (a placeholder fp32 tensor).
+    ``dmask``: the positivity mask written by the producing forward epilogue, used instead of
+    ``dact_y`` when that is a planes-only placeholder (filled here if a fallback needs it)."""
     M, N = g2.shape
     K = w_bf.shape[1]
     if g2.dtype == torch.float32:
         if wp is not None and G.SP and G._sp_ok(g2):
-            r = G.sp_dgrad(_pl.of(g2, kpad=N % 32 != 0), wp, M, K, N, resid=resid, dact_y=dact_y, dscale=dscale,
-                           out_planes=out_planes, need_f32=need_f32 or not out_planes)
+            r = G.sp_dgrad(_pl.of(g2, kpad=N % 32 != 0), wp, M, K, N, resid=resid,
+                           dact_y=dact_y if dmask is None else None, dscale=dscale, out_planes=out_planes,
+                           need_f32=need_f32 or not out_planes, dmask=dmask)
             if r is not None:
                 dx, dxp = r
                 if dx is None:
@@ -148,7 +156,7 @@ def _dgrad(g2, w_bf, resid=None, dact_y=None, dscale=1.0, wp=None, out_planes=Fa
                 if dxp is not None:
                     _pl.attach(dx, dxp)
                 return dx
-        return _dgrad32_any(_pl.f32(g2), w_bf, resid, dact_y, dscale)
+        return _dgrad32_any(_pl.f32(g2), w_bf, resid, _pl.f32(dact_y) if dact_y is not None else None, dscale)
     if G.supported(M, K, N, g2, w_bf, resid, dact_y, mode=1):
         return G.dgrad(g2, w_bf, resid=resid, dact_y=dact_y, dscale=dscale)
     f32 = [t.float() if t is not None else None for t in (g2, w_bf, resid, dact_y)]
@@ -160,7 +168,7 @@ def compute_weight(p: torch.Tensor, dtype) -> torch.Tensor:
     return p.detach() if dtype == torch.float32 else bf16_weight(p)
 
 
-def _fwd_sp(x2, wp, N, bias, act, p, rng, salt, out_planes=False, lse_stats=False):
+def _fwd_sp(x2, wp, N, bias, act, p, rng, salt, out_planes=False, lse_stats=False, relu_mask=None):
     """fp32 forward on the split-plane GEMM (x2's planes: cached or split now); None if not covered.
     ``lse_stats``: the epilogue also writes per-row softmax statistics, attached to y for the
     cross-entropy that consumes it (sparkmi/ops/loss.py)."""
@@ -170,6 +178,11 @@ def _fwd_sp(x2, wp, N, bias, act, p, rng, salt, out_planes=False, lse_stats=Fals
     part = None
     if lse_stats and bias is not None and act == 0 and p == 0 and not out_planes:
         part = torch.empty((N + 127) // 128, M, 2, device=x2.device, dtype=torch.float32)
+    if relu_mask is not None:  # planes + positivity mask, no fp32 tensor (FFNFn)
+        r = G.sp_fwd(_pl.of(x2), wp, M, N, K, bias, act, rng, salt, _rng.threshold(p), _rng.scale(p),
+                     out_planes=True, mask=relu_mask)
+        if r is not None:
+            return _pl.placeholder((M, N), r[1], x2.device)
     r = G.sp_fwd(_pl.of(x2), wp, M, N, K, bias, act, rng, salt, _rng.threshold(p), _rng.scale(p),
                  out_planes=out_planes, lse_part=part)
     if r is None and part is not None:  # the statistics epilogue not covered: plain forward
@@ -190,15 +203,16 @@ def _wplanes(weight):
     return _pl.weight(weight) if G.SP and weight.dim() == 2 and weight.shape[1] % 8 == 0 else None
 
 
-def _fwd_native(x2, weight, bias, act, p, rng, salt, w_bf=None, out_planes=False, wp=None, lse_stats=False):
+def _fwd_native(x2, weight, bias, act, p, rng, salt, w_bf=None, out_planes=False, wp=None, lse_stats=False,
+                relu_mask=None):
     N, K = weight.shape
     M = x2.shape[0]
     if x2.dtype == torch.float32:
         y = _fwd_sp(x2, wp if wp is not None else _wplanes(weight), N, bias, act, p, rng, salt, out_planes,
-                    lse_stats)
+                    lse_stats, relu_mask)
         if y is not None:
             return y
-        return _fwd32_any(x2, weight.detach(), bias, act, rng, salt, p)
+        return _fwd32_any(_pl.f32(x2), weight.detach(), bias, act, rng, salt, p)
     w = w_bf if w_bf is not None else bf16_weight(weight)
     if G.supported(M, N, K, x2, w, mode=0) and act in (0, 1):
         return G.fwd(x2, w, bias, act, rng, salt, _rng.threshold(p), _rng.scale(p))
@@ -339,7 +353,13 @@ class FFNFn(torch.autograd.Function):
         ctx.native = _native.use_native(x)
         if ctx.native:
             x2 = x2.contiguous()
-            h = _fwd_native(x2, w1, b1, 1, p, rng, salt, out_planes=True)
+            # the hidden activation feeds linear2's GEMMs (planes) and linear2's dgrad epilogue (only
+            # its sign): planes + a 4-bit-per-4-columns positivity mask, no fp32 tensor
+            H = w1.shape[0]
+            mask = (torch.empty(x2.shape[0], (H + 3) // 4, device=x2.device, dtype=torch.uint8)
+                    if _pl.PLANES_ONLY and _FFN_MASK and x2.dtype == torch.float32 and G.SP else None)
+            h = _fwd_native(x2, w1, b1, 1, p, rng, salt, out_planes=True, relu_mask=mask)
+            ctx.h_mask = mask if (mask is not None and _pl.planes_only(h)) else None
             y = _fwd_native(h, w2, b2, 0, 0.0, rng, 0)
             ctx.x_planes, ctx.h_planes = _pl.cached(x2), _pl.cached(h)
             ctx.seed = 0
@@ -371,7 +391,8 @@ class FFNFn(torch.autograd.Function):
                 _pl.f32(dy2)
             # dh feeds only linear1's dgrad / wgrad, both on its planes: planes only
             dh = _dgrad(dy2, compute_weight(w2, dy2.dtype), dact_y=h, dscale=_rng.scale(p),
-                        wp=_wplanes(w2) if f32 else None, out_planes=True, need_f32=not _pl.PLANES_ONLY)
+                        wp=_wplanes(w2) if f32 else None, out_planes=True, need_f32=not _pl.PLANES_ONLY,
+                        dmask=getattr(ctx, "h_mask", None))
             gw2, gb2, gw1, gb1 = grad_buf(w2), grad_buf(b2), grad_buf(w1), grad_buf(b1)
             with _grad.side(dy2.device, dy2, h):
                 if not _wgrad_accumulate(gw2, dy2, h, gb2, ready=(w2, b2)):
