@@ -34,4 +34,5 @@ struct LSTMArgs {
 };
 #define LSTM_MAXT 2048
 #define LSTM_TCH 64  // timesteps per LDS-staged chunk in the kernels' tail phases
-#define LSTM_WCH 16  // ticks of per-tick outputs staged in LDS between burst stores (power of 2)
+#define LSTM_WCH 16  // backward: ticks of per-tick outputs staged in LDS between burst stores (power of 2)
+#define LSTM_XW 64   // two-wave forward: ticks per LDS window of layer-0 inputs

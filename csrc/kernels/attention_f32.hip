@@ -41,6 +41,33 @@
 
 struct FStage { float4 v[2]; };  // one 32 x 64 fp32 chunk = 2 float4 per thread
 
+// Diagnostic build (-DATTN_STAMPS, tools/probes/attn_fwd_probe.hip): per-phase shader-clock sums
+// of the staged forward, kept in registers and added once per wave at exit, plus each wave's
+// s_memrealtime start / end (dispatch ramp and drain).
+#ifdef ATTN_STAMPS
+__device__ unsigned long long attn_stamps[8 * 4096];  // [wave][phase]: plain stores (same-address atomics
+                                                     // from every wave queued at one L2 channel: 4x slower)
+__device__ unsigned long long attn_wave_rt[2 * 4096];
+#define AST_DECL long long ast_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; const unsigned long long ast_rt0 = __builtin_amdgcn_s_memrealtime()
+#define AST_T(v) long long v = clock64()
+#define AST_ADD(i, t0, t1) (ast_[i] += (t1) - (t0))
+#define AST_END()                                                                                      \
+  do {                                                                                               \
+    if ((threadIdx.x & 63) == 0) {                                                                   \
+      const int wid_ = ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6); \
+      if (wid_ < 4096) {                                                                             \
+        for (int i_ = 0; i_ < 8; ++i_) attn_stamps[8 * wid_ + i_] = (unsigned long long)ast_[i_];   \
+        attn_wave_rt[2 * wid_] = ast_rt0; attn_wave_rt[2 * wid_ + 1] = __builtin_amdgcn_s_memrealtime(); \
+      }                                                                                              \
+    }                                                                                                \
+  } while (0)
+#else
+#define AST_DECL
+#define AST_T(v)
+#define AST_ADD(i, t0, t1)
+#define AST_END() do {} while (0)
+#endif
+
 __device__ __forceinline__ void fa_load_chunk(const float* __restrict__ base, long ss, int r0, int rmax, FStage& p) {
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -635,29 +662,50 @@ __device__ __forceinline__ void as_cols_acc(const unsigned short* img, int lane,
 #define AS_SRC(NAME, FP, PP, PS, SB, SH, SS)                                                         \
   const AsSrc<PI> NAME{(FP) + b * (SB) + hh * (SH), PI ? (PP) + b * (SB) + hh * (SH) : nullptr, (PS), (SS)}
 
-template <int MODE, bool KPAD, bool PI>
-__global__ __launch_bounds__(256, 2) void attn_sp_fwd_kernel(AttnF32Args a) {
+// NW = waves per workgroup, 32 queries each.  NW = 8 (opt-in, smi_attn_fwd8; at S = 256 a whole
+// head per workgroup, one workgroup per CU, still two waves per SIMD): each streamed K / V chunk is staged
+// once for 256 queries instead of 128 — half the staging loads, splits and LDS stores per wave
+// (threads 0-255 stage K, 256-511 V) and half the K / V reads from L2 / HBM.  Per-wave arithmetic
+// and its order are those of NW = 4 (bitwise-identical output).
+template <int MODE, bool KPAD, bool PI, int NW>
+__device__ __forceinline__ void attn_sp_fwd_body(const AttnF32Args& a) {
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  constexpr int QW = 32 * NW;  // queries per workgroup
   __shared__ __attribute__((aligned(16))) unsigned short Ks[2][AS_OP];
   __shared__ __attribute__((aligned(16))) unsigned short Vs[2][AS_OP];
+  AST_DECL;
+  AST_T(tk0);
   const int hh = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
-  const int qwave = blockIdx.x * 128 + w * 32;
+  const int qwave = blockIdx.x * QW + w * 32;
   const int qi = qwave + (lane & 31);
   AS_SRC(Q, a.q, a.qpi, a.qi_ps, a.q_sb, a.q_sh, a.q_ss);
   AS_SRC(K, a.k, a.kpi, a.kvi_ps, a.k_sb, a.k_sh, a.k_ss);
   AS_SRC(V, a.v, a.vpi, a.kvi_ps, a.v_sb, a.v_sh, a.v_ss);
   const unsigned char* kp = a.kpad ? a.kpad + (long)b * a.Sk : nullptr;
   int kend = a.Sk;
-  if (MODE == 2) kend = min(a.Sk, blockIdx.x * 128 + 128);
+  if (MODE == 2) kend = min(a.Sk, blockIdx.x * QW + QW);
   const int nchunks = (kend + FCH - 1) / FCH;
+  // chunk staging: NW = 4 every thread stages 8 values of K and 8 of V; NW = 8 one operand per
+  // half of the workgroup (wave-uniform)
+  const bool kside = NW == 4 || threadIdx.x < 256;
+  const int ti = threadIdx.x & 255;
   typename AStageT<PI>::T pk, pv;
-  K.load(0, a.Sk, pk);
-  V.load(0, a.Sk, pv);
+  auto stage_load = [&](int r0) {
+    if constexpr (NW == 4) { K.load(r0, a.Sk, pk); V.load(r0, a.Sk, pv); }
+    else { if (kside) K.load(r0, a.Sk, pk, ti); else V.load(r0, a.Sk, pk, ti); }
+  };
+  auto stage_store = [&](int bf) {
+    if constexpr (NW == 4) { as_store(Ks[bf], pk); as_store(Vs[bf], pv); }
+    else as_store(kside ? Ks[bf] : Vs[bf], pk, ti);
+  };
+  stage_load(0);
   F32Pre<1, 32> qs;
   Q.own(qi, a.Sq, lane, qs);
-  as_store(Ks[0], pk);
-  as_store(Vs[0], pv);
+  stage_store(0);
   __syncthreads();
+  AST_T(tk1);
+  AST_ADD(0, tk0, tk1);  // prologue
   float m = -INFINITY, l = 0.f;
   f32x16_t o[2];
 #pragma unroll
@@ -667,8 +715,11 @@ __global__ __launch_bounds__(256, 2) void attn_sp_fwd_kernel(AttnF32Args a) {
   for (int c = 0; c < nchunks; ++c) {
     const int buf = c & 1;
     const bool more = c + 1 < nchunks;
-    if (more) { K.load((c + 1) * FCH, a.Sk, pk); V.load((c + 1) * FCH, a.Sk, pv); }
+    AST_T(tc0);
+    if (more) stage_load((c + 1) * FCH);
     const unsigned long long kmask = KPAD ? chunk_pad_mask(kp, c * FCH, a.Sk) : 0ull;
+    AST_T(tc1);
+    AST_ADD(1, tc0, tc1);  // next chunk's load issue
     do {
       const int k0 = c * FCH;
       float ub;
@@ -709,13 +760,23 @@ __global__ __launch_bounds__(256, 2) void attn_sp_fwd_kernel(AttnF32Args a) {
       psum = smi_row32_swap_sum(psum);
       l = l * alpha + psum;
       m = mnew;
+      AST_T(tc2);
+      AST_ADD(2, tc1, tc2);  // S chain + online softmax
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) o[dt] *= alpha;
       as_cols_acc(Vs[buf], lane, pv16, o);  // O^T += V^T P^T
+      AST_T(tc3);
+      AST_ADD(3, tc2, tc3);  // rescale (waits for the previous PV) + P split + PV issue
     } while (0);
-    if (more) { as_store(Ks[buf ^ 1], pk); as_store(Vs[buf ^ 1], pv); }
+    AST_T(tc4);
+    if (more) stage_store(buf ^ 1);
+    AST_T(tc5);
+    AST_ADD(4, tc4, tc5);  // wait for the chunk's loads, split, LDS stores
     __syncthreads();
+    AST_T(tc6);
+    AST_ADD(5, tc5, tc6);  // barrier
   }
+  AST_T(tk2);
   if (qi < a.Sq) {
     float* O = a.o + b * a.o_sb + hh * a.o_sh + (long)qi * a.o_ss;
     const float inv = l > 0.f ? 1.0f / l : 0.f;
@@ -730,7 +791,15 @@ __global__ __launch_bounds__(256, 2) void attn_sp_fwd_kernel(AttnF32Args a) {
       a.lse[((long)b * a.H + hh) * a.Sq + qi] = l > 0.f ? mref + log2f(l) : INFINITY;
     }
   }
+  AST_T(tk3);
+  AST_ADD(6, tk2, tk3);  // epilogue stores
+  AST_ADD(7, tk0, tk3);  // wave lifetime
+  AST_END();
 }
+template <int MODE, bool KPAD, bool PI>
+__global__ __launch_bounds__(256, 2) void attn_sp_fwd4(AttnF32Args a) { attn_sp_fwd_body<MODE, KPAD, PI, 4>(a); }
+template <int MODE, bool KPAD, bool PI>
+__global__ __launch_bounds__(512, 1) void attn_sp_fwd8(AttnF32Args a) { attn_sp_fwd_body<MODE, KPAD, PI, 8>(a); }
 
 template <int MODE, bool KPAD, bool PI>
 __global__ __launch_bounds__(256, 2) void attn_sp_dq_kernel(AttnF32Args a) {
@@ -1063,6 +1132,18 @@ extern "C" int smi_attn_dkdv8(int set) {
   return g_attn_dkdv8;
 }
 
+// forward on 4-wave workgroups (default) / 8-wave (SMI_ATTN_FWD8=1): -3 us per call on one box,
+// +2..5 us on another (tools/probes/attn_fwd_probe.hip) — opt-in
+static int g_attn_fwd8 = -1;
+extern "C" int smi_attn_fwd8(int set) {
+  if (set == 0 || set == 1) g_attn_fwd8 = set;
+  if (g_attn_fwd8 < 0) {
+    const char* e = getenv("SMI_ATTN_FWD8");
+    g_attn_fwd8 = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_attn_fwd8;
+}
+
 // staged-plane kernels on (default) / off (SMI_ATTN_SP=0: the XS kernels above)
 static int g_attn_sp = -1;
 extern "C" int smi_attn_f32_sp(int set) {
@@ -1154,8 +1235,15 @@ extern "C" int smi_attn_f32_fwd(const AttnF32Args* args, hipStream_t st) {
   const AttnF32Args& a = *args;
   if (!fa_ok(a)) return -1;
   dim3 grid((a.Sq + 127) / 128, a.H, a.B);
-  if (smi_gemm_f32_algo(-1) != 0 && smi_attn_f32_sp(-1)) SMI_ATTN_SP_MODES(attn_sp_fwd_kernel, grid, a, fa_pi(a, false));
-  else SMI_ATTN_F32_DISPATCH(attn_f32_fwd_kernel, grid, a);
+  if (smi_gemm_f32_algo(-1) != 0 && smi_attn_f32_sp(-1)) {
+    if (smi_attn_fwd8(-1)) {
+      SMI_ATTN_SP_MODES8(attn_sp_fwd8, dim3((a.Sq + 255) / 256, a.H, a.B), a, fa_pi(a, false));
+    } else {
+      SMI_ATTN_SP_MODES(attn_sp_fwd4, grid, a, fa_pi(a, false));
+    }
+  } else {
+    SMI_ATTN_F32_DISPATCH(attn_f32_fwd_kernel, grid, a);
+  }
   SMI_CHECK_LAUNCH();
 }
 

@@ -40,11 +40,17 @@ __device__ __forceinline__ float smi_tanh(float x) {
 #ifdef LSTM_STAMPS  // diagnostic build only (tools/probes/lstm_probe.hip): per-phase cycle sums
 __device__ unsigned long long lstm_stamps[4][8];
 __device__ unsigned long long lstm_rt[4];  // [0..1] s_memrealtime / [2..3] s_memtime around the fwd tick loop
+// sums kept in registers, added to lstm_stamps once per wave at exit (a global read-modify-write
+// per tick waited on its load every tick and slowed the stamped workgroup)
+#define LSTAMP_DECL long long lst_[8] = {0, 0, 0, 0, 0, 0, 0, 0}
 #define LSTAMP_T(v) do { (v) = clock64(); } while (0)
-#define LSTAMP_ADD(slot, i, t0, t1) do { if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) lstm_stamps[slot][i] += (t1) - (t0); } while (0)
+#define LSTAMP_ADD(slot, i, t0, t1) (lst_[i] += (t1) - (t0))
+#define LSTAMP_FLUSH(slot) do { if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) for (int i_ = 0; i_ < 8; ++i_) lstm_stamps[slot][i_] += lst_[i_]; } while (0)
 #else
+#define LSTAMP_DECL
 #define LSTAMP_T(v) do {} while (0)
 #define LSTAMP_ADD(slot, i, t0, t1) do {} while (0)
+#define LSTAMP_FLUSH(slot) do {} while (0)
 #endif
 
 
@@ -182,6 +188,7 @@ struct LstmBwdIn {
 
 template <int H, int MI, int NT, int CM>
 __global__ __launch_bounds__(NT) void lstm_bwd_kernel(LSTMArgs a) {
+  LSTAMP_DECL;
   constexpr int G = 4 * H;
   const int b = blockIdx.x, tid = threadIdx.x;
   const int L = a.L, T = a.T, E = a.E, C = a.C;
@@ -336,6 +343,7 @@ __global__ __launch_bounds__(NT) void lstm_bwd_kernel(LSTMArgs a) {
   __syncthreads();  // dab (global) is read across threads below
   LSTAMP_T(cl1);
   LSTAMP_ADD(threadIdx.x >> 6, 4, cl0, cl1);
+  LSTAMP_FLUSH(threadIdx.x >> 6);
   if (cell) {
     if (a.dh0) a.dh0[((size_t)l * a.B + b) * H + r] = own_dh(r);  // W_hh^T da at t = 0
     if (a.dc0) a.dc0[((size_t)l * a.B + b) * H + r] = dc;
@@ -367,6 +375,7 @@ typedef float smi_f2 __attribute__((ext_vector_type(2)));
 
 template <int H, int MI>
 __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
+  LSTAMP_DECL;
   const int b = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int L = a.L, T = a.T, E = a.E, C = a.C;
   const int l = lane / H, j = lane % H;
@@ -377,10 +386,12 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
   __shared__ __attribute__((aligned(16))) float s_h[2][2][LSTM_MAXL * SH];
   __shared__ float s_g[2][LSTM_MAXL][4][H];                                // [buf][layer][gate][unit]
   __shared__ long long s_ids[LSTM_MAXT];
-  // saved activations of the last LSTM_WCH ticks, [tick % LSTM_WCH][layer][i f g o c h][unit],
-  // flushed to the workspace in bursts (a global store inside the tick shares vmcnt with the
-  // prefetched embedding loads: every tick waited for its stores' round trip)
-  __shared__ __attribute__((aligned(16))) float s_ws[LSTM_WCH][(64 / H) * 6 * H];
+  // layer 0's inputs (embedding rows) for two windows of LSTM_XW ticks, refilled half a window
+  // ahead: the tick loop issues no per-tick global load, so its per-tick stores of the saved
+  // activations never sit in front of a load the tick waits for (gfx9 vmcnt counts both, in order)
+  constexpr int XW = LSTM_XW, NX = XW * MI / 128;  // window ticks, values per thread per window
+  static_assert((XW * MI) % 128 == 0, "whole window per 128 threads");
+  __shared__ __attribute__((aligned(16))) float s_x[2][XW][SI];
   for (int i = tid; i < T; i += blockDim.x) s_ids[i] = a.ids[(size_t)b * T + i];
 
   const int g0 = 2 * w, g1 = 2 * w + 1;
@@ -411,12 +422,26 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
     s_h[w][1][l * SH + j] = hl;
   }
   __syncthreads();  // s_ids
-  // unconditional (clamped) load with no select on its value: a load inside a branch, or a mask
-  // applied right after it, makes the compiler wait for it in the same tick.  Rows past T are
-  // only ever read by layer 0 at ticks where it is off; lanes >= E never write them.
-  auto emb_at = [&](int t) { return a.emb[(size_t)s_ids[min(t, T - 1)] * E + min(lane, E - 1)]; };
-  if (lane < E) s_in[w][0][lane] = emb_at(0);
-  float x0 = 0.f, x1 = emb_at(1), x2 = emb_at(2);
+  // window loads: unconditional (clamped) so that no select waits on them at issue; the mask
+  // (columns >= E, ticks >= T) is applied when the window is written to LDS, half a window later
+  float xr[NX];
+  auto win_load = [&](int t0) {
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int e = (tid + 128 * i) % MI, tt = (tid + 128 * i) / MI;
+      xr[i] = a.emb[(size_t)s_ids[min(t0 + tt, T - 1)] * E + min(e, E - 1)];
+    }
+  };
+  auto win_store = [&](int t0, int buf) {
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int e = (tid + 128 * i) % MI, tt = (tid + 128 * i) / MI;
+      s_x[buf][tt][e] = (e < E && t0 + tt < T) ? xr[i] : 0.f;
+    }
+  };
+  win_load(0);
+  win_store(0, 0);
+  if (XW < T) win_load(XW);
   __syncthreads();
 
   const uint32_t seed = smi_seed(a.seedp, a.salt);
@@ -424,7 +449,7 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
   const int nt = T + L - 1;
   // every prologue load (weights, h0 / c0) retired here, so the tick loop's wait counts are exact
   __builtin_amdgcn_s_waitcnt(0);
-  auto tick = [&](int k, float& xnext, float& xload) {
+  auto tick = [&](int k) {
     const int t = k - l;
     const bool on = act && t >= 0 && t < T;
     const int rb = k & 1, wb = rb ^ 1;
@@ -433,7 +458,7 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
     LSTAMP_T(c_0);
     if (on) {
       smi_f2 p0 = {bias0, 0.f}, q0 = {0.f, 0.f}, p1 = {bias1, 0.f}, q1 = {0.f, 0.f};
-      const float* xin = &s_in[w][rb][l * SI];
+      const float* xin = l == 0 ? &s_x[(t / XW) & 1][t % XW][0] : &s_in[w][rb][l * SI];
       const float* hin = &s_h[w][rb][l * SH];
 #pragma unroll
       for (int i = 0; i < MI; i += 4) {
@@ -465,50 +490,46 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
       c = fg * c + ig * gg;
       hl = og * smi_tanh(c);
       s_h[w][wb][l * SH + j] = hl;
-      float* ws = &s_ws[k & (LSTM_WCH - 1)][l * 6 * H];
-      if (w == 0) { ws[j] = ig; ws[H + j] = fg; ws[2 * H + j] = gg; }
-      else { ws[3 * H + j] = og; ws[4 * H + j] = c; ws[5 * H + j] = hl; }
       if (l + 1 < L) {
         float hd = hl;
         if (a.thresh) hd = smi_keep(seed, lstm_drop_idx(b, t, l, j, T, L, H), a.thresh) ? hl * a.dscale : 0.f;
         s_in[w][wb][(l + 1) * SI + j] = hd;
       }
+      float* ws = wsb + ((size_t)l * T + t) * 6 * H;  // saved activations: i f g (wave 0), o c h (wave 1)
+      if (w == 0) { ws[j] = ig; ws[H + j] = fg; ws[2 * H + j] = gg; }
+      else { ws[3 * H + j] = og; ws[4 * H + j] = c; ws[5 * H + j] = hl; }
     }
-    if (lane < E) s_in[w][wb][lane] = xnext;  // layer 0's input for the next tick
-    xload = emb_at(k + 3);
     SMI_WAVE_LDS_ORDER();
     LSTAMP_T(c_3);
     LSTAMP_ADD(w, 0, c_0, c_1);  // gates: LDS reads, packed FMAs, activations
     LSTAMP_ADD(w, 1, c_1, c_2);  // the barrier
     LSTAMP_ADD(w, 2, c_2, c_3);  // cell update, LDS writes, prefetch
-    if ((k & (LSTM_WCH - 1)) == LSTM_WCH - 1 || k == nt - 1) {  // burst the staged ticks to ws
-      __syncthreads();
-      const int k0 = k & ~(LSTM_WCH - 1), rows = (k - k0 + 1) * L;
-      constexpr int R4 = 6 * H / 4;  // float4 per (tick, layer) row
-      for (int e = tid; e < rows * R4; e += blockDim.x) {
-        const int r = e / R4, c4 = e - r * R4, kk = k0 + r / L, ll = r % L, tt = kk - ll;
-        if (tt >= 0 && tt < T)
-          *(float4*)(wsb + ((size_t)ll * T + tt) * 6 * H + 4 * c4) = *(const float4*)&s_ws[kk & (LSTM_WCH - 1)][ll * 6 * H + 4 * c4];
+    long long c_4 = 0, c_5 = 0;
+    (void)c_4; (void)c_5;
+    LSTAMP_T(c_4);
+    if (k % XW == XW / 2) {  // mid-window: window w + 1 into LDS (its buffer last held w - 1), load w + 2
+      const int wn = k / XW + 1;
+      if (wn * XW < T) {
+        win_store(wn * XW, wn & 1);  // read from tick wn * XW on: many barriers later
+        if ((wn + 1) * XW < T) win_load((wn + 1) * XW);
       }
     }
+    LSTAMP_T(c_5);
+    LSTAMP_ADD(w, 3, c_3, c_4);  // stamp bookkeeping
+    LSTAMP_ADD(w, 4, c_4, c_5);  // window refill (every LSTM_XW ticks)
   };
   int k = 0;
 #ifdef LSTM_STAMPS
   unsigned long long rt0 = __builtin_amdgcn_s_memrealtime(), ct0 = __builtin_amdgcn_s_memtime();
 #endif
-  for (; k + 3 <= nt; k += 3) {
-    tick(k, x1, x0);
-    tick(k + 1, x2, x1);
-    tick(k + 2, x0, x2);
-  }
-  if (k < nt) tick(k, x1, x0);
-  if (k + 1 < nt) tick(k + 1, x2, x1);
+  for (; k < nt; ++k) tick(k);
 #ifdef LSTM_STAMPS
   if (tid == 0 && b == 0) {
     lstm_rt[0] += __builtin_amdgcn_s_memrealtime() - rt0;
     lstm_rt[2] += __builtin_amdgcn_s_memtime() - ct0;
   }
 #endif
+  LSTAMP_FLUSH(w);
   __syncthreads();  // ws (global) written by both waves is read by the fc head below
   if (act && w == 0) {
     if (a.hn) a.hn[((size_t)l * a.B + b) * H + j] = hl;

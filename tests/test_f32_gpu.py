@@ -238,18 +238,21 @@ def _attn_f32(B, H, Sq, Sk, mode, cross, kp):
         _close(qg.grad, dqkv, 5e-5, 1e-5, f"dqkv {mode}")
 
 
-@pytest.fixture(params=[1, 2, 0], ids=["staged_planes", "staged_planes_dkdv4", "wave_split"])
+@pytest.fixture(params=[1, 2, 0], ids=["staged_planes", "staged_planes_4wave", "wave_split"])
 def attn_kernel(request):
     """The split-product attention kernels: streamed chunks split once at LDS staging (default;
-    dK/dV on 8-wave workgroups, or the 4-wave kernel: C.attn_dkdv8(0)) or per wave per fragment
-    (C.attn_f32_sp(0)); irrelevant under the f32-MFMA algorithm."""
+    forward on 8-wave (opt-in) and dK/dV on 8-wave workgroups (default), or both 4-wave:
+    C.attn_fwd8(0), C.attn_dkdv8(0)) or per wave per fragment (C.attn_f32_sp(0)); irrelevant under
+    the f32-MFMA algorithm."""
     C = _native.C()
-    prev, prev8 = C.attn_f32_sp(-1), C.attn_dkdv8(-1)
+    prev, prev8, prevf8 = C.attn_f32_sp(-1), C.attn_dkdv8(-1), C.attn_fwd8(-1)
     C.attn_f32_sp(1 if request.param else 0)
     C.attn_dkdv8(0 if request.param == 2 else 1)
+    C.attn_fwd8(0 if request.param == 2 else 1)
     yield request.param
     C.attn_f32_sp(prev)
     C.attn_dkdv8(prev8)
+    C.attn_fwd8(prevf8)
 
 
 @pytest.mark.parametrize("mode", ["none", "reference", "causal"])

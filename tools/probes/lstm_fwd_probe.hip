@@ -33,10 +33,10 @@ int main() {
   std::vector<unsigned long long> st(32), rt(4);
   (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(lstm_stamps), 32 * 8);
   (void)hipMemcpyFromSymbol(rt.data(), HIP_SYMBOL(lstm_rt), 4 * 8);
-  const char* nm[3] = {"gates", "barrier", "cell+writes"};
+  const char* nm[5] = {"gates", "barrier", "cell+writes", "stamps", "flush"};
   for (int w = 0; w < 2; ++w) {
     printf("wave %d:", w);
-    for (int i = 0; i < 3; ++i) printf("  %s %.0f", nm[i], (double)st[w * 8 + i] / R / (T + L - 1));
+    for (int i = 0; i < 5; ++i) printf("  %s %.0f", nm[i], (double)st[w * 8 + i] / R / (T + L - 1));
     printf("  (cycles per tick)\n");
   }
   const double us = (double)rt[0] / R / 100.0, cyc = (double)rt[2] / R;
