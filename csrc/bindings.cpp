@@ -85,6 +85,7 @@ int smi_gemm_sp_wg_tm(int);
 int smi_attn_f32_sp(int);
 int smi_attn_dkdv8(int);
 int smi_attn_fwd8(int);
+int smi_adam_wide(int);
 int smi_splitk_reduce(const float*, int, long, float*, long, float*, int, hipStream_t);
 int smi_splitk_fold_multi(const float* const*, float* const*, float* const*, const long*, const int*, const int*, int,
                           hipStream_t);
@@ -468,6 +469,8 @@ PYBIND11_MODULE(_C, m) {
         "split-plane GEMM tile form for large problems (16: 256x128 on 16x16x32 MFMA | 256 | 4 | 128); other values query");
   m.def("attn_dkdv8", [](int set) { return smi_attn_dkdv8(set); },
         "fp32 attention dK/dV: 1 = 8-wave workgroups with owned V in LDS (default), 0 = 4-wave; other values query");
+  m.def("adam_wide", [](int set) { return smi_adam_wide(set); },
+        "Adam launch: 1 = 1024-thread blocks, <= 512 (default), 0 = 256-thread blocks, <= 4096; other values query");
   m.def("attn_fwd8", [](int set) { return smi_attn_fwd8(set); },
         "fp32 attention forward: 1 = 8-wave workgroups (a whole head per workgroup), 0 = 4-wave (default); other values query");
   m.def("attn_f32_sp", [](int set) { return smi_attn_f32_sp(set); },

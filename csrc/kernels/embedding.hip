@@ -161,11 +161,19 @@ __global__ __launch_bounds__(EMB_TILE) void emb_det_count(const long long* __res
   for (int i = threadIdx.x; i < d.NB; i += EMB_TILE) d.counts[(size_t)blockIdx.x * d.NB + i] = hist[i];
 }
 
+#define EMB_HBITS 2048  // LDS heavy-bucket bitmask words: NB <= 65,536 (V <= ~1.5M ids)
 __global__ __launch_bounds__(1024) void emb_det_scan(EmbDet d) {
   __shared__ int wtot[16];
   __shared__ int carry;
+  // heavy-bucket flags, set from the bucket totals this pass already holds in registers (the heavy
+  // pass below re-read every bucket's start from global memory: a chain of dependent load
+  // latencies per wave, ~60 % of this kernel)
+  __shared__ unsigned hbits[EMB_HBITS];
+  const bool lds_flags = d.NB <= 32 * EMB_HBITS;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (threadIdx.x == 0) carry = 0;
+  for (int i = threadIdx.x; i < EMB_HBITS; i += 1024) hbits[i] = 0u;
+  __syncthreads();
   for (int b0 = 0; b0 < d.NB; b0 += 1024) {
     const int b = b0 + threadIdx.x;
     int run = 0;
@@ -195,6 +203,7 @@ __global__ __launch_bounds__(1024) void emb_det_scan(EmbDet d) {
         run += d.counts[(size_t)t * d.NB + b];
       }
     }
+    if (lds_flags && b < d.NB && run >= EMB_HEAVY) atomicOr(&hbits[b >> 5], 1u << (b & 31));  // LDS
     // block-wide exclusive scan of the bucket totals (wave shuffles, then the 16 wave totals)
     int inc = run;
 #pragma unroll
@@ -224,7 +233,11 @@ __global__ __launch_bounds__(1024) void emb_det_scan(EmbDet d) {
     __shared__ int hcnt[16];
     const int per = ((d.NB + 15) / 16 + 63) / 64 * 64;
     const int lo = w * per, hi = min(d.NB, lo + per);
-    auto heavy = [&](int b) { return b < hi && d.bstart[b + 1] - d.bstart[b] >= EMB_HEAVY; };
+    auto heavy = [&](int b) {
+      if (b >= hi) return false;
+      if (lds_flags) return ((hbits[b >> 5] >> (b & 31)) & 1u) != 0u;
+      return d.bstart[b + 1] - d.bstart[b] >= EMB_HEAVY;
+    };
     int cnt = 0;
     for (int b0 = lo; b0 < hi; b0 += 64) cnt += __popcll(__ballot(heavy(b0 + lane)));
     if (lane == 0) hcnt[w] = cnt;

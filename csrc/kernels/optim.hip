@@ -11,6 +11,8 @@
 // The step counter advances inside the update kernel (no separate increment launch): every
 // block computes t = step[0] + 1 on entry, and the last block to finish (atomic ticket on the
 // `done` word) stores t and re-arms the ticket — all other blocks have read step[0] by then.
+#include <stdlib.h>
+
 #include "smi_common.h"
 #include "smi_split3.h"
 
@@ -49,7 +51,8 @@ __device__ __forceinline__ void store_planes1(unsigned short* __restrict__ pl, l
   pl[2 * ps + i] = f2bf(r - bf2f(mm));
 }
 
-__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
+template <int NT>
+__global__ __launch_bounds__(NT) void adam_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                                                    float* __restrict__ v, unsigned short* __restrict__ pbf, long n,
                                                    const float* __restrict__ lr_p, float* __restrict__ step_p,
                                                    unsigned* __restrict__ done, float b1, float b2, float eps, float wd,
@@ -197,12 +200,36 @@ extern "C" int smi_step_inc(float* step, hipStream_t st) {
   SMI_CHECK_LAUNCH();
 }
 
+// Adam launch shape: 1024-thread blocks, <= 512 of them (default) / 256-thread blocks, <= 4096
+// (SMI_ADAM_WIDE=0)
+static int g_adam_wide = -1;
+extern "C" int smi_adam_wide(int set) {
+  if (set == 0 || set == 1) g_adam_wide = set;
+  if (g_adam_wide < 0) {
+    const char* e = getenv("SMI_ADAM_WIDE");
+    g_adam_wide = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_adam_wide;
+}
+static int adam_wide() { return smi_adam_wide(-1); }
+
 extern "C" int smi_adam(float* p, float* g, float* m, float* v, void* pbf, long n, const float* lr, float* step,
                         unsigned* done, float b1, float b2, float eps, float wd, float gscale, int adamw, int zero_grad,
                         void* pl, long ps, hipStream_t st) {
   if (pl && (((uintptr_t)pl & 7) || ps % 4 || ps < n)) return -1;
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, st, p, g, m, v, (unsigned short*)pbf, n, lr,
-                     step, done, b1, b2, eps, wd, gscale, adamw, zero_grad, (unsigned short*)pl, ps);
+  if (adam_wide()) {
+    // 1024-thread blocks, at most two per CU: every block takes one ticket on the shared `done`
+    // word at its end, and same-address atomics serialise at one L2 channel (~10 ns each) — the
+    // 3,000-block launch of a 3M-parameter model spent most of its 40 us in that ticket queue
+    long b = (n / 4 + 1023) / 1024;
+    if (b > 512) b = 512;
+    if (b < 1) b = 1;
+    hipLaunchKernelGGL(adam_kernel<1024>, dim3((unsigned)b), dim3(1024), 0, st, p, g, m, v, (unsigned short*)pbf, n,
+                       lr, step, done, b1, b2, eps, wd, gscale, adamw, zero_grad, (unsigned short*)pl, ps);
+  } else {
+    hipLaunchKernelGGL(adam_kernel<256>, dim3(grid_for(n / 4 + 1)), dim3(256), 0, st, p, g, m, v, (unsigned short*)pbf,
+                       n, lr, step, done, b1, b2, eps, wd, gscale, adamw, zero_grad, (unsigned short*)pl, ps);
+  }
   SMI_CHECK_LAUNCH();
 }
 
