@@ -562,6 +562,7 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
 
 template <int H, int MI, int CM>
 __global__ __launch_bounds__(128) void lstm_bwd_w2_kernel(LSTMArgs a) {
+  LSTAMP_DECL;
   constexpr int G = 4 * H;
   const int b = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int L = a.L, T = a.T, C = a.C;
@@ -600,6 +601,9 @@ __global__ __launch_bounds__(128) void lstm_bwd_w2_kernel(LSTMArgs a) {
   const int nt = T + L - 1;
   const int tl = T - 1 + (L - 1 - l);
   const float c0v = (act && a.c0) ? a.c0[((size_t)l * a.B + b) * H + j] : 0.f;
+  float dpl[CM];
+#pragma unroll
+  for (int q = 0; q < CM; ++q) dpl[q] = (a.dpred_last && top && q < C) ? dpred[min(q, C - 1)] : 0.f;
   // every lane loads every value at clamped indices (no branch around a load: the compiler can
   // then count vmcnt exactly instead of waiting for everything in flight)
   auto load_in = [&](int t, LstmBwdIn<CM>& v) {
@@ -608,10 +612,15 @@ __global__ __launch_bounds__(128) void lstm_bwd_w2_kernel(LSTMArgs a) {
     v.ig = ws[j]; v.fg = ws[H + j]; v.gg = ws[2 * H + j]; v.og = ws[3 * H + j]; v.cc = ws[4 * H + j];
     const float cpv = ws[(tc > 0 ? -2 * H : 4 * H) + j];  // c at t - 1 (t = 0: c0)
     v.cp = t > 0 ? cpv : c0v;
+    if (a.dpred_last) {  // the last step's dpred only: loaded once before the loop
 #pragma unroll
-    for (int q = 0; q < CM; ++q) {
-      const float d = dpred[(size_t)(a.dpred_last ? 0 : tc) * C + min(q, C - 1)];
-      v.dp[q] = (top && q < C && (!a.dpred_last || t == T - 1)) ? d : 0.f;
+      for (int q = 0; q < CM; ++q) v.dp[q] = t == T - 1 ? dpl[q] : 0.f;
+    } else {
+#pragma unroll
+      for (int q = 0; q < CM; ++q) {
+        const float d = dpred[(size_t)tc * C + min(q, C - 1)];
+        v.dp[q] = (top && q < C) ? d : 0.f;
+      }
     }
   };
   auto prep = [&](int t, LstmBwdIn<CM>& v) {
@@ -640,6 +649,9 @@ __global__ __launch_bounds__(128) void lstm_bwd_w2_kernel(LSTMArgs a) {
     const int t = tl - k;
     const bool on = act && t >= 0 && t < T;
     const int rb = k & 1, wb = rb ^ 1;
+    long long c_0 = 0, c_1 = 0, c_2 = 0, c_3 = 0, c_4 = 0;
+    (void)c_0; (void)c_1; (void)c_2; (void)c_3; (void)c_4;
+    LSTAMP_T(c_0);
     load_in(t - 2, nv);
     if (on) {  // cell backward (both waves, bit-identical) on terms prep()'d a tick ahead
       float dh = t == T - 1 ? dhn : s_dh[rb][l][j];
@@ -653,6 +665,7 @@ __global__ __launch_bounds__(128) void lstm_bwd_w2_kernel(LSTMArgs a) {
       dc *= cv.fg;
     }
     SMI_WAVE_LDS_ORDER();
+    LSTAMP_T(c_1);
     prep(t - 1, pv);
     if (on && prod) {  // this wave's transposed product over the layer's 4H gate gradients
       smi_f2 p0 = {0.f, 0.f}, p1 = {0.f, 0.f}, p2 = {0.f, 0.f}, p3 = {0.f, 0.f};
@@ -674,7 +687,9 @@ __global__ __launch_bounds__(128) void lstm_bwd_w2_kernel(LSTMArgs a) {
         s_dx[wb][l][j] = s;
       }
     }
+    LSTAMP_T(c_2);
     smi_lds_barrier();
+    LSTAMP_T(c_3);
     if ((k & (LSTM_WCH - 1)) == LSTM_WCH - 1 || k == nt - 1) {  // burst the staged gate gradients
       const int k0 = k & ~(LSTM_WCH - 1), rows = (k - k0 + 1) * L;
       constexpr int R4 = G / 4;
@@ -685,6 +700,11 @@ __global__ __launch_bounds__(128) void lstm_bwd_w2_kernel(LSTMArgs a) {
       }
       __syncthreads();  // the next tick overwrites slot 0
     }
+    LSTAMP_T(c_4);
+    LSTAMP_ADD(w, 5, c_0, c_1);  // load issue (waits on the loads of two ticks ago) + cell backward
+    LSTAMP_ADD(w, 6, c_1, c_2);  // prep of the next tick + transposed product
+    LSTAMP_ADD(w, 7, c_2, c_3);  // barrier
+    LSTAMP_ADD(w, 3, c_3, c_4);  // burst flush (every LSTM_WCH ticks)
   };
   int k = 0;
   for (; k + 3 <= nt; k += 3) {
@@ -694,6 +714,7 @@ __global__ __launch_bounds__(128) void lstm_bwd_w2_kernel(LSTMArgs a) {
   }
   if (k < nt) tick(k, ia, ib, ic);
   if (k + 1 < nt) tick(k + 1, ib, ic, ia);
+  LSTAMP_FLUSH(2 + w);
   __syncthreads();  // dab (global) is read across workgroups by the weight-gradient kernels (next launch)
   if (act && w == 0) {
     if (a.dh0) a.dh0[((size_t)l * a.B + b) * H + j] = dh_first;
