@@ -670,14 +670,22 @@ __global__ __launch_bounds__(128) void lstm_bwd_w2_kernel(LSTMArgs a) {
     if (on && prod) {  // this wave's transposed product over the layer's 4H gate gradients
       smi_f2 p0 = {0.f, 0.f}, p1 = {0.f, 0.f}, p2 = {0.f, 0.f}, p3 = {0.f, 0.f};
       const float* da = &s_da[w][l][0];
+      // two rounds of G / 8 LDS reads issued back to back before their FMAs (the interleaved form
+      // kept 2-3 reads in flight: ~32 exposed LDS latencies, most of the 1.3k-cycle product);
+      // same accumulation order
 #pragma unroll
-      for (int q = 0; q < G; q += 8) {
-        const float4 d4 = *(const float4*)&da[q];
-        const float4 e4 = *(const float4*)&da[q + 4];
-        p0 = __builtin_elementwise_fma(wc[q / 2], smi_f2{d4.x, d4.y}, p0);
-        p1 = __builtin_elementwise_fma(wc[q / 2 + 1], smi_f2{d4.z, d4.w}, p1);
-        p2 = __builtin_elementwise_fma(wc[q / 2 + 2], smi_f2{e4.x, e4.y}, p2);
-        p3 = __builtin_elementwise_fma(wc[q / 2 + 3], smi_f2{e4.z, e4.w}, p3);
+      for (int hq = 0; hq < G; hq += G / 2) {
+        float4 dv[G / 8];
+#pragma unroll
+        for (int i = 0; i < G / 8; ++i) dv[i] = *(const float4*)&da[hq + 4 * i];
+#pragma unroll
+        for (int i = 0; i < G / 8; i += 2) {
+          const int q = hq + 4 * i;
+          p0 = __builtin_elementwise_fma(wc[q / 2], smi_f2{dv[i].x, dv[i].y}, p0);
+          p1 = __builtin_elementwise_fma(wc[q / 2 + 1], smi_f2{dv[i].z, dv[i].w}, p1);
+          p2 = __builtin_elementwise_fma(wc[q / 2 + 2], smi_f2{dv[i + 1].x, dv[i + 1].y}, p2);
+          p3 = __builtin_elementwise_fma(wc[q / 2 + 3], smi_f2{dv[i + 1].z, dv[i + 1].w}, p3);
+        }
       }
       const float s = ((p0.x + p0.y) + (p1.x + p1.y)) + ((p2.x + p2.y) + (p3.x + p3.y));
       if (w == 0) {
