@@ -457,7 +457,10 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
     (void)c_0; (void)c_1; (void)c_2; (void)c_3;
     LSTAMP_T(c_0);
     if (on) {
+      // eight independent packed-FMA chains (two per gate and input half, input rows and h rows
+      // apart): four chains of 16 dependent v_pk_fma_f32 left the gate phase latency-bound
       smi_f2 p0 = {bias0, 0.f}, q0 = {0.f, 0.f}, p1 = {bias1, 0.f}, q1 = {0.f, 0.f};
+      smi_f2 r0 = {0.f, 0.f}, u0 = {0.f, 0.f}, r1 = {0.f, 0.f}, u1 = {0.f, 0.f};
       const float* xin = l == 0 ? &s_x[(t / XW) & 1][t % XW][0] : &s_in[w][rb][l * SI];
       const float* hin = &s_h[w][rb][l * SH];
 #pragma unroll
@@ -473,12 +476,13 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
       for (int i = 0; i < H; i += 4) {
         const float4 x = *(const float4*)&hin[i];
         const smi_f2 xa = {x.x, x.y}, xb = {x.z, x.w};
-        p0 = __builtin_elementwise_fma(wh0[i / 2], xa, p0);
-        q0 = __builtin_elementwise_fma(wh0[i / 2 + 1], xb, q0);
-        p1 = __builtin_elementwise_fma(wh1[i / 2], xa, p1);
-        q1 = __builtin_elementwise_fma(wh1[i / 2 + 1], xb, q1);
+        r0 = __builtin_elementwise_fma(wh0[i / 2], xa, r0);
+        u0 = __builtin_elementwise_fma(wh0[i / 2 + 1], xb, u0);
+        r1 = __builtin_elementwise_fma(wh1[i / 2], xa, r1);
+        u1 = __builtin_elementwise_fma(wh1[i / 2 + 1], xb, u1);
       }
-      const float z0 = (p0.x + p0.y) + (q0.x + q0.y), z1 = (p1.x + p1.y) + (q1.x + q1.y);
+      const float z0 = ((p0.x + p0.y) + (q0.x + q0.y)) + ((r0.x + r0.y) + (u0.x + u0.y));
+      const float z1 = ((p1.x + p1.y) + (q1.x + q1.y)) + ((r1.x + r1.y) + (u1.x + u1.y));
       s_g[rb][l][g0][j] = w == 1 ? smi_tanh(z0) : smi_sigmoid(z0);  // gate 2 (g) is the tanh one
       s_g[rb][l][g1][j] = smi_sigmoid(z1);
     }
