@@ -42,6 +42,30 @@ int main() {
   const double us = (double)rt[0] / R / 100.0, cyc = (double)rt[2] / R;
   printf("tick loop: %.1f us, %.0f shader cycles -> %.2f GHz, %.0f cycles / %.3f us per tick\n", us, cyc,
          cyc / us / 1000.0, cyc / (T + L - 1), us / (T + L - 1));
+  // backward recurrence kernel alone (last-step dpred), stamped: slots 2 + wave
+  {
+    float *dpred = zalloc((size_t)B * C), *wsda = zalloc((size_t)B * L * T * 4 * H);
+    a.dpred = dpred; a.dpred_last = 1; a.ws_da = wsda;
+    for (int it = 0; it < 3; ++it) hipLaunchKernelGGL((lstm_bwd_w2_kernel<32, 32, 4>), dim3(B), dim3(128), 0, 0, a);
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(lstm_stamps), z.data(), 32 * 8);
+    for (int it = 0; it < R; ++it) hipLaunchKernelGGL((lstm_bwd_w2_kernel<32, 32, 4>), dim3(B), dim3(128), 0, 0, a);
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(lstm_stamps), 32 * 8);
+    const char* bn[4] = {"flush", "load+cell", "prep+product", "barrier"};
+    const int bi[4] = {3, 5, 6, 7};
+    for (int w = 0; w < 2; ++w) {
+      printf("bwd wave %d:", w);
+      for (int i = 0; i < 4; ++i) printf("  %s %.0f", bn[i], (double)st[(2 + w) * 8 + bi[i]] / R / (T + L - 1));
+      printf("  (cycles per tick)\n");
+    }
+    hipEvent_t f0, f1; (void)hipEventCreate(&f0); (void)hipEventCreate(&f1);
+    (void)hipEventRecord(f0);
+    for (int it = 0; it < 20; ++it) hipLaunchKernelGGL((lstm_bwd_w2_kernel<32, 32, 4>), dim3(B), dim3(128), 0, 0, a);
+    (void)hipEventRecord(f1); (void)hipEventSynchronize(f1);
+    float bms; (void)hipEventElapsedTime(&bms, f0, f1);
+    printf("bwd recurrence: %.1f us per call\n", bms * 1000 / 20);
+  }
   hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
   (void)hipEventRecord(e0);
   for (int it = 0; it < 20; ++it) smi_lstm(&a, 0, 0);
