@@ -45,7 +45,7 @@ BASELINE_MLP = 130476.0   # world 1, 1 thread
 METRIC = "samples/sec (whole node) distributed_cnn + transformer at 1/2/4/8 MI355X"
 F32_PRECISION = ("fp32 activations/weights/gradients/accumulators (reference precision); GEMM products exact: "
                  "fp32 operands carried as 3 bf16 planes (hi+mid+lo, split once where produced), 6 plane products "
-                 "on v_mfma_f32_32x32x16_bf16 (error vs fp64 at or below the f32-MFMA kernel: "
+                 "on v_mfma_f32_16x16x32_bf16 (error vs fp64 at or below the f32-MFMA kernel: "
                  "tests/test_gemm_sp_gpu.py); fp32 attention products on the same exact 3-way bf16 split")
 SPLIT_PEAK_TF = 2500.0 / 6  # 6 bf16 products per fp32 product on the 2.5 PF (spec) bf16 matrix cores
 # measured on this MI355X (profiles/r3_bf16_peak_rate.log, tools/bench_bf16_peak.py): hipBLASLt bf16
@@ -180,6 +180,20 @@ def time_steps(runner, batches, steps, warmup, device, world, record=None):
     return elapsed, loss
 
 
+def ranks_in_sync(flat, world):
+    """After the timed steps every rank must hold bit-identical parameters (synchronous data
+    parallelism): rank 0's master weights broadcast and compared on every rank (None at N = 1)."""
+    if world <= 1:
+        return None
+    import torch
+    import torch.distributed as dist
+    ref = flat.master.clone()
+    dist.broadcast(ref, 0)
+    ok = torch.tensor([1 if torch.equal(ref, flat.master) else 0], dtype=torch.int32, device=ref.device)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    return bool(int(ok.item()))
+
+
 def time_allreduce(flat, device, world, iters=10):
     """Isolated cost of the step's gradient all-reduce (the whole flat fp32 gradient buffer,
     same buckets and backend as the step): the communication phase, in ms, max over ranks."""
@@ -201,6 +215,59 @@ def time_allreduce(flat, device, world, iters=10):
     t = torch.tensor([el], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return round(float(t.item()) * 1000, 3)
+
+
+def time_comm_paths(device, world, bucket_mb, iters=5):
+    """The bulk-gradient collective options at one bucket (``--bucket-mb``), ms per all-reduce,
+    max over ranks: RCCL with its default channels, RCCL on a communicator created with
+    min_ctas = 32 (more channels over the 7 xGMI links), and the IPC two-shot kernel
+    (csrc/comm/ipc_allreduce.hip).  DataParallel's start-up probe makes the same IPC-vs-RCCL
+    choice for the run (``comm_probe`` of the step result)."""
+    if world <= 1 or device.type != "cuda":
+        return None
+    import torch
+    import torch.distributed as dist
+    n = int(bucket_mb * (1 << 20) / 4) // 4 * 4
+    x = torch.zeros(n, dtype=torch.float32, device=device)
+
+    def timed(fn):
+        for _ in range(2):
+            fn()
+        _sync(device)
+        dist.all_reduce(torch.zeros(1, device=device))
+        _sync(device)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        _sync(device)
+        t = torch.tensor([(time.perf_counter() - t0) / iters * 1e3], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return round(float(t.item()), 3)
+
+    out = {"bucket_bytes": n * 4}
+    out["rccl_ms"] = timed(lambda: dist.all_reduce(x))
+    if dist.get_backend() == "nccl":
+        try:
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.config.min_ctas = 32
+            g = dist.new_group(list(range(world)), backend="nccl", pg_options=opts)
+            out["rccl_min_ctas32_ms"] = timed(lambda: dist.all_reduce(x, group=g))
+            dist.destroy_process_group(g)
+        except Exception as e:  # noqa: BLE001 — reported, not fatal
+            out["rccl_min_ctas32_ms"] = f"unavailable: {type(e).__name__}"
+    try:
+        from sparkmi.parallel.comm import IpcAllReduce
+        ar = IpcAllReduce(cap_floats=n)
+        out["ipc_two_shot_ms"] = timed(lambda: ar(x, algo=2))
+        ar.check()
+        ar.close()
+    except Exception as e:  # noqa: BLE001
+        out["ipc_two_shot_ms"] = f"unavailable: {type(e).__name__}"
+    for k in ("rccl_ms", "rccl_min_ctas32_ms", "ipc_two_shot_ms"):
+        v = out.get(k)
+        if isinstance(v, float) and v > 0:
+            out[k.replace("_ms", "_GBps_busbw")] = round(2 * (world - 1) / world * n * 4 / (v * 1e-3) / 1e9, 1)
+    return out
 
 
 def bench_cnn(args, rank, world, device, dtype="fp32"):
@@ -330,9 +397,14 @@ def bench_transformer(args, rank, world, device, dtype, zero=False):
     losses = []
     elapsed, loss = time_steps(runner, batches, args.steps, args.warmup, device, world, record=losses)
     final_loss = float(loss.float().item()) if loss is not None else float("nan")
+    in_sync = ranks_in_sync(flat, world)
     ar = time_allreduce(flat, device, world)
+    comm = None
     if ddp is not None:
+        comm = {"path": ddp.comm, "probe": ddp.comm_probe}
         ddp.close()
+        if dtype == "fp32" and not zero:
+            comm["paths"] = time_comm_paths(device, world, args.bucket_mb)
     value = world * args.batch * args.steps / elapsed
     tflops = transformer_flops_per_sample(args.layers, args.seq, args.vocab) * value / world / 1e12
     peak = 157.3 if dtype == "fp32" else 2500.0
@@ -344,7 +416,8 @@ def bench_transformer(args, rank, world, device, dtype, zero=False):
            f"mfu_vs_{'157tf_fp32' if dtype == 'fp32' else '2.5pf_bf16'}_dense": round(tflops / peak, 3),
            "allreduce_ms": ar, "grad_bytes": flat.numel * 4, "dtype": dtype,
            "overlap": "finished buckets all-reduced under the rest of the backward" if split_fn else None,
-           "hip_graph": use_graph, "zero1": bool(zero and world > 1)}
+           "hip_graph": use_graph, "zero1": bool(zero and world > 1), "comm": comm,
+           "ranks_in_sync": in_sync}
     if dtype == "fp32":
         # the algorithm the step actually runs: 6 bf16 products per fp32 product
         res["mfu_vs_417tf_split3_ceiling"] = round(tflops / SPLIT_PEAK_TF, 3)

@@ -38,15 +38,20 @@
 #include "smi_ipc.h"
 
 // signal round: publish `val` to every peer's slot [b][rank], wait for every peer's slot [b][q]
-// to reach `val`; returns (block-uniform) whether some peer timed out
+// to reach `val`; returns (block-uniform) whether some peer timed out.  A block that already knows
+// of a loss (a sticky error from an earlier call, or this call's first round: `*timed_out` set
+// before the round) still publishes its signal, so live peers are not kept waiting, but does not
+// poll again: after a loss every later call poisons at once instead of spending the timeout.
 __device__ __forceinline__ bool ipc_round(const IpcArgs& a, int b, unsigned val, int* timed_out) {
+  const bool known = *timed_out != 0;  // block-uniform: written before the caller's last barrier
+  __syncthreads();
   if ((int)threadIdx.x < a.world) {
     __atomic_thread_fence(__ATOMIC_RELEASE);  // system scope: this block's stores are visible first
     __hip_atomic_store(a.sig[threadIdx.x] + b * IPC_MAX_RANKS + a.rank, val, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
     const unsigned* f = a.sig[a.rank] + b * IPC_MAX_RANKS + threadIdx.x;
     long spins = 0;
-    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - val) < 0) {
+    while (!known && (int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - val) < 0) {
       if (++spins > a.spins) {  // a peer is gone
         __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         atomicOr(timed_out, 1);
@@ -58,6 +63,12 @@ __device__ __forceinline__ bool ipc_round(const IpcArgs& a, int b, unsigned val,
   }
   __syncthreads();
   return *timed_out != 0;
+}
+// a loss recorded by an earlier call (sticky *err): this call poisons without polling
+__device__ __forceinline__ void ipc_init_lost(const IpcArgs& a, int* timed_out) {
+  if (threadIdx.x == 0)
+    *timed_out = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ? 1 : 0;
+  __syncthreads();
 }
 
 // the last block to finish advances the device state for the next launch
@@ -82,8 +93,7 @@ __global__ __launch_bounds__(256) void ipc_allreduce_kernel(IpcArgs a) {
   for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = src[i];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __shared__ int timed_out;
-  if (threadIdx.x == 0) timed_out = 0;
-  __syncthreads();
+  ipc_init_lost(a, &timed_out);
   const bool lost = ipc_round(a, b, sval, &timed_out);
   float4* out = (float4*)a.buf;
   if (lost) {  // poison: the bucket must not carry a finite partial sum
@@ -124,8 +134,7 @@ __global__ __launch_bounds__(256) void ipc_allreduce2_kernel(IpcArgs a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __shared__ int timed_out;
-  if (threadIdx.x == 0) timed_out = 0;
-  __syncthreads();
+  ipc_init_lost(a, &timed_out);
   const float nan = __builtin_nanf("");
   // 2. reduce-scatter: sum this rank's chunk over all ranks (rank order), publish it in place
   bool lost = ipc_round(a, b, s1, &timed_out);

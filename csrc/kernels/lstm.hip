@@ -855,6 +855,146 @@ __global__ __launch_bounds__(256) void lstm_wgrad_combine(LSTMArgs a) {
   }
 }
 
+// ONE launch for every weight gradient of the stack (layers + head) AND the embedding-input
+// gradients xe, on the fp32 matrix cores: v_mfma_f32_16x16x4_f32 (exact fp32 products, an fmaf
+// chain per accumulator — the reference's fp32 precision).
+//   dW_l[r][c] = sum over all B*T (b,t) of da_l[b,t][r] * x_l[b,t][c]   (x = [input | h_{t-1} | 1])
+//   xe[b,t][e] = sum_r da_0[b,t][r] * W_ih0[r][e]
+// A weight-gradient workgroup owns one 16 x 16 output tile; its 8 waves split the (b,t) reduction
+// into 8 fixed ranges, and the 8 partial tiles are summed in wave order through LDS: bit-
+// reproducible without a second launch, a slab or float atomics (lstm_wgrad_partial + _combine
+// did the same reduction on the VALU in two launches).  Workgroups past the weight tiles compute
+// xe: each wave one 16 x 16 tile (K = 4H).  Operand layouts (16x16x4 f32): lane l holds A row /
+// B column l & 15 at k = l >> 4; the accumulator's register j of lane l is row 4 (l >> 4) + j,
+// column l & 15.
+#define LW_WAVES 8
+__device__ __forceinline__ float lw_d(const LSTMArgs& a, int l, long bt, int r, int rows) {
+  if (r >= rows) return 0.f;
+  const int b = (int)(bt / a.T), t = (int)(bt % a.T);
+  if (l < a.L) return a.ws_da[(((size_t)b * a.L + l) * a.T + t) * 4 * a.H + r];
+  if (!a.dpred_last) return a.dpred[((size_t)b * a.T + t) * a.C + r];
+  return t == a.T - 1 ? a.dpred[(size_t)b * a.C + r] : 0.f;
+}
+__device__ __forceinline__ float lw_x(const LSTMArgs& a, int l, long bt, int c, int cols, uint32_t seed) {
+  if (c >= cols) return 0.f;
+  const int b = (int)(bt / a.T), t = (int)(bt % a.T), H = a.H, L = a.L, T = a.T;
+  const float* wsb = a.ws + (size_t)b * L * T * 6 * H;
+  if (l == L) return c < H ? wsb[((size_t)(L - 1) * T + t) * 6 * H + 5 * H + c] : 1.f;
+  const int In = l == 0 ? a.E : H;
+  if (c < In) {
+    if (l == 0) return a.emb[(size_t)a.ids[(size_t)b * T + t] * a.E + c];
+    const float hx = wsb[((size_t)(l - 1) * T + t) * 6 * H + 5 * H + c];
+    return a.thresh ? (smi_keep(seed, lstm_drop_idx(b, t, l - 1, c, T, L, H), a.thresh) ? hx * a.dscale : 0.f) : hx;
+  }
+  if (c < In + H) {
+    const int j = c - In;
+    return t > 0 ? wsb[((size_t)l * T + t - 1) * 6 * H + 5 * H + j] : (a.h0 ? a.h0[((size_t)l * a.B + b) * H + j] : 0.f);
+  }
+  return 1.f;
+}
+__host__ __device__ __forceinline__ int lw_tiles(const LSTMArgs& a, int l) {
+  return ((lstm_rows(a, l) + 15) / 16) * ((lstm_cols(a, l) + 15) / 16);
+}
+__host__ __device__ __forceinline__ int lw_wgrad_blocks(const LSTMArgs& a) {
+  int n = 0;
+  for (int l = 0; l <= a.L; ++l) n += lw_tiles(a, l);
+  return n;
+}
+#define MF16F32(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
+
+__global__ __launch_bounds__(64 * LW_WAVES) void lstm_wgrad_mfma(LSTMArgs a) {
+  __shared__ float part[LW_WAVES][256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+  const long BT = (long)a.B * a.T;
+  int tile = blockIdx.x;
+  const int nw = lw_wgrad_blocks(a);
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  if (tile >= nw) {
+    // xe tiles: one per wave (uniform per wave)
+    if (!a.g_xe) return;
+    const int G = 4 * a.H, E = a.E;
+    const int ecols = (E + 15) / 16;
+    const long xt = (long)(tile - nw) * LW_WAVES + w;
+    const long bt0 = (xt / ecols) * 16;
+    const int e0 = (int)(xt % ecols) * 16;
+    if (bt0 >= BT) return;
+    const long bt = bt0 + li;
+    const int b = (int)(bt / a.T), t = (int)(bt % a.T);
+    const float* d = a.ws_da + (((size_t)b * a.L) * a.T + t) * G;  // layer 0
+    const bool okr = bt < BT, okc = e0 + li < E;
+    const float* wcol = a.w_ih[0] + e0 + li;
+#pragma unroll 4
+    for (int k0 = 0; k0 < G; k0 += 4) {
+      const int k = k0 + lk;
+      const float av = okr ? d[k] : 0.f;
+      const float bv = okc ? wcol[(size_t)k * E] : 0.f;
+      acc = MF16F32(av, bv, acc);
+    }
+    if (okc) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const long r = bt0 + 4 * lk + j;
+        if (r < BT) a.g_xe[r * E + e0 + li] = acc[j];
+      }
+    }
+    return;
+  }
+  int l = 0;
+  while (tile >= lw_tiles(a, l)) tile -= lw_tiles(a, l++);
+  const int rows = lstm_rows(a, l), cols = lstm_cols(a, l);
+  const int ctn = (cols + 15) / 16;
+  const int r0 = (tile / ctn) * 16, c0 = (tile % ctn) * 16;
+  const uint32_t seed = smi_seed(a.seedp, a.salt);
+  // wave w reduces (b,t) rows [k_begin, k_end), 4 per MFMA
+  const long kc = ((BT + LW_WAVES - 1) / LW_WAVES + 3) / 4 * 4;
+  const long kb = w * kc, ke = min(BT, kb + kc);
+  for (long k0 = kb; k0 < ke; k0 += 16) {
+    float av[4], bv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long k = k0 + 4 * u + lk;
+      const bool ok = k < ke;
+      av[u] = ok ? lw_d(a, l, k, r0 + li, rows) : 0.f;
+      bv[u] = ok ? lw_x(a, l, k, c0 + li, cols, seed) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = MF16F32(av[u], bv[u], acc);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) part[w][(4 * lk + j) * 16 + li] = acc[j];
+  __syncthreads();
+  if (threadIdx.x >= 256) return;
+  const int rr = threadIdx.x >> 4, cc = threadIdx.x & 15;
+  const int r = r0 + rr, c = c0 + cc;
+  if (r >= rows || c >= cols) return;
+  float v = 0.f;
+#pragma unroll
+  for (int q = 0; q < LW_WAVES; ++q) v += part[q][threadIdx.x];  // wave (= (b,t) range) order
+  if (l == a.L) {
+    if (c < a.H) a.g_w_fc[(size_t)r * a.H + c] += v;
+    else a.g_b_fc[r] += v;
+    return;
+  }
+  const int In = l == 0 ? a.E : a.H;
+  if (c < In) a.g_w_ih[l][(size_t)r * In + c] += v;
+  else if (c < In + a.H) a.g_w_hh[l][(size_t)r * a.H + (c - In)] += v;
+  else {
+    a.g_b_ih[l][r] += v;
+    a.g_b_hh[l][r] += v;
+  }
+}
+
+// SMI_LSTM_WGRAD=valu: the two-launch VALU split-K reduction above (+ lstm_xe_kernel)
+static int lstm_wgrad_mfma_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SMI_LSTM_WGRAD");
+    v = (e && e[0] == 'v') ? 0 : 1;
+  }
+  return v;
+}
+
 // per-token embedding-input gradients xe[b,t,:] = W_ih0^T da0[b,t,:] (the table gradient is their
 // position-ordered per-id sum, csrc/kernels/embedding.hip)
 __global__ __launch_bounds__(256) void lstm_xe_kernel(LSTMArgs a) {
@@ -945,6 +1085,16 @@ extern "C" int smi_lstm(const LSTMArgs* a, int backward, hipStream_t st) {
   else if (H == 32) rc = wide ? lstm_launch<32, 64>(a, backward, st) : lstm_launch<32, 32>(a, backward, st);
   else rc = lstm_launch<64, 64>(a, backward, st);
   if (rc || !backward) return rc;
+  if (lstm_wgrad_mfma_enabled()) {
+    const long xtiles = a->g_emb ? ((long)a->B * a->T + 15) / 16 * ((a->E + 15) / 16) : 0;
+    const long nblk = lw_wgrad_blocks(*a) + (xtiles + LW_WAVES - 1) / LW_WAVES;
+    hipLaunchKernelGGL(lstm_wgrad_mfma, dim3((unsigned)nblk), dim3(64 * LW_WAVES), 0, st, *a);
+    if ((rc = (int)hipGetLastError())) return rc;
+    if (a->g_emb)
+      return smi_emb_bwd_f32(a->ids, a->g_xe, a->g_emb, (long)a->B * a->T, a->E, a->pad_idx, nullptr, 0, 0, 1.f, a->V,
+                             a->emb_ws, st);
+    return 0;
+  }
   const int maxrows = 4 * H > a->C ? 4 * H : a->C;
   hipLaunchKernelGGL(lstm_wgrad_partial, dim3(LSTM_KS, (maxrows + LSTM_RB - 1) / LSTM_RB, a->L + 1), dim3(256), 0, st,
                      *a);

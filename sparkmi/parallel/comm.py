@@ -54,6 +54,8 @@ class IpcAllReduce:
             raise ValueError(f"IPC all-reduce supports <= {C.IPC_MAX_RANKS} ranks")
         self.cap = (int(cap_floats) + 3) // 4 * 4
         self.blocks = blocks
+        # 1 | 2: every call uses that kernel (tests; SPARKMI_IPC_ALGO), else algo_for(size)
+        self.force_algo = int(os.environ.get("SPARKMI_IPC_ALGO", "0")) or None
         data, hdata = C.ipc_alloc(2 * self.cap * 4)
         sig, hsig = C.ipc_alloc(C.IPC_MAX_BLOCKS * C.IPC_MAX_RANKS * 4)
         self._own = (data, sig)
@@ -103,10 +105,10 @@ class IpcAllReduce:
         (w - 1), at the price of a second signal round — worth it past the latency-bound sizes."""
         return 1 if self.world <= 2 or numel * 4 <= ONE_SHOT_MAX_BYTES else 2
 
-    def __call__(self, t, algo=None):
+    def __call__(self, t, algo=None, stream=None):
         if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() % 4 or t.numel() > self.cap:
             raise ValueError("IpcAllReduce: contiguous fp32 tensor, numel % 4 == 0, <= capacity")
-        algo = algo or self.algo_for(t.numel())
+        algo = algo or self.force_algo or self.algo_for(t.numel())
         n4 = t.numel() // 4
         if self.blocks:
             blocks = self.blocks
@@ -115,7 +117,8 @@ class IpcAllReduce:
         else:  # >= 512 float4 of every chunk per block
             blocks = max(1, min(self.C.IPC_MAX_BLOCKS, ((n4 + self.world - 1) // self.world + 511) // 512))
         self.C.ipc_allreduce(t.data_ptr(), t.numel(), self.data, self.sig, self.cap, self.rank, self.ctr.data_ptr(),
-                             self.err.data_ptr(), blocks, torch.cuda.current_stream().cuda_stream, self.spins, algo)
+                             self.err.data_ptr(), blocks, (stream or torch.cuda.current_stream()).cuda_stream,
+                             self.spins, algo)
         return t
 
     def failed(self):

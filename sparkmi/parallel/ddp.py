@@ -20,14 +20,17 @@ module was called, so gradients were never synchronised).  Design for MI355X + R
   one multi-range launch: sparkmi.optim.adam.Adam.shard) and the updated fp32 master pieces are
   all-gathered in place; per-rank optimizer work and state drop by 1/world and the gradient
   moves (w-1)/w instead of 2(w-1)/w of the buffer before the update;
-* comm path by size (``SPARKMI_DP_COMM`` = auto | ipc | rccl; auto by default): gradients of
-  up to ``IPC_LIMIT_BYTES`` (32 MiB: the MLP's 256 B, the CNN's 31 KB, the LSTM's 12.3 MB) on one
+* comm path (``SPARKMI_DP_COMM`` = auto | ipc | rccl; auto by default): gradients of up to
+  ``IPC_LIMIT_BYTES`` (32 MiB: the MLP's 256 B, the CNN's 31 KB, the LSTM's 12.3 MB) on one
   node go through the xGMI IPC all-reduce (csrc/comm/ipc_allreduce.hip; one-shot for buckets
   <= 256 KB, two-shot reduce-scatter + all-gather above) — no ring latency, and since it is a
   stream-ordered kernel with a device-side epoch, the whole data-parallel step (forward,
-  backward, all-reduce, optimizer) is captured as ONE HIP graph (``graph_safe``).  Larger
-  gradients (the transformer's 188 MB) go through RCCL on its own stream, overlapped with the
-  backward; ``ipc`` forces the IPC kernels for them too (stream-ordered on the compute stream).
+  backward, all-reduce, optimizer) is captured as ONE HIP graph (``graph_safe``).  For larger
+  gradients (the transformer's 188 MB) auto MEASURES both paths at start-up on the largest
+  bucket (``comm_probe``: IPC two-shot vs the RCCL process group, max over ranks) and keeps the
+  faster; ``SPARKMI_DP_PROBE=0`` sends them to RCCL without measuring.  Either way a bucket's
+  reduction runs on a side stream (RCCL's own, or the IPC comm stream forked from the compute
+  stream at launch and joined in ``finish()``), overlapped with the rest of the backward.
 The CPU/gloo path runs the identical logic (multi-process CPU tests).
 """
 import os
@@ -37,7 +40,18 @@ import torch.distributed as dist
 
 from ..ops import _grad
 
-IPC_LIMIT_BYTES = 32 << 20
+IPC_LIMIT_BYTES = 32 << 20  # auto without a measurement: IPC kernels up to this gradient size
+
+
+def choose_comm(ipc_ms, rccl_ms):
+    """The auto path for a bulk gradient from a measured all-reduce of its largest bucket (max over
+    ranks): the IPC two-shot when it is at least as fast as RCCL, else RCCL.  Both run on a side
+    stream overlapped with the backward, so the isolated bucket time is the right comparison."""
+    if ipc_ms is None:
+        return "rccl"
+    if rccl_ms is None:
+        return "ipc"
+    return "ipc" if ipc_ms <= rccl_ms else "rccl"
 
 
 def broadcast_flat(flat, src=0, group=None):
@@ -69,17 +83,33 @@ class DataParallel:
             raise ValueError(f"SPARKMI_DP_COMM={mode!r}: auto | ipc | rccl")
         if ipc is None:
             ipc = os.environ.get("SPARKMI_IPC_AR", "1") != "0" and mode != "rccl"
-        if ipc and mode == "auto" and flat.numel * 4 > IPC_LIMIT_BYTES:
-            ipc = False
+        # bulk gradients in auto mode: measure both paths on the largest bucket and keep the faster
+        # (SPARKMI_DP_PROBE=0: the fixed IPC_LIMIT_BYTES rule instead)
+        probe = (ipc and mode == "auto" and flat.numel * 4 > IPC_LIMIT_BYTES)
+        if probe and os.environ.get("SPARKMI_DP_PROBE", "1") == "0":
+            ipc = probe = False
         self._build_buckets()
+        self.comm_probe = None
         if (ipc and not self.zero and self.world > 1 and flat.grad.is_cuda and self.world <= 8
                 and _single_node(self.world)):
             from .comm import IpcAllReduce, IpcUnavailable
             try:
-                # any bucket cut (align_buckets re-cuts) stays within the bucket limit
-                self.ipc = IpcAllReduce(cap_floats=min(self._limit, flat.numel), group=group)
+                self.ipc = IpcAllReduce(cap_floats=self._ipc_capacity(), group=group)
             except IpcUnavailable:
                 self.ipc = None  # every rank agreed: buckets go through the process group
+            if self.ipc is not None and probe:
+                n = max(e - s for s, e, _ in self.buckets)
+                ipc_ms, rccl_ms = self._probe(n)
+                choice = choose_comm(ipc_ms, rccl_ms)
+                self.comm_probe = {"bucket_bytes": n * 4, "ipc_ms": ipc_ms, "rccl_ms": rccl_ms, "choice": choice}
+                if choice != "ipc":
+                    self.ipc.close()
+                    self.ipc = None
+        # the IPC kernels run on a comm stream forked from the compute stream at each bucket
+        # launch (joined in finish()): buckets reduce while the rest of the backward runs, as
+        # RCCL's do on its own stream
+        self._cs = torch.cuda.Stream(device=flat.grad.device) if self.ipc is not None else None
+        self._cs_used = False
         self._pending = None
         self._works = []
         self._listener = None
@@ -91,6 +121,43 @@ class DataParallel:
                 self._listener = _grad.add_listener(self._on_ready)
                 self._dlistener = _grad.add_defer_listener(self._on_queued)
         self.reset()
+
+    @property
+    def comm(self):
+        return "ipc" if self.ipc is not None else ("rccl" if self.world > 1 else "none")
+
+    def _probe(self, n, iters=3):
+        """(IPC two-shot ms, process-group ms) of an n-float all-reduce, max over ranks."""
+        import time
+        x = torch.zeros(n, dtype=torch.float32, device=self.flat.grad.device)
+
+        def timed(fn):
+            for _ in range(2):
+                fn()
+            torch.cuda.synchronize()
+            dist.all_reduce(torch.zeros(1, device=x.device), group=self.group)  # line the ranks up
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                fn()
+            torch.cuda.synchronize()
+            t = torch.tensor([(time.perf_counter() - t0) / iters * 1e3], dtype=torch.float64, device=x.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            return round(float(t.item()), 3)
+
+        ipc_ms = timed(lambda: self.ipc(x))
+        rccl_ms = timed(lambda: dist.all_reduce(x, group=self.group))
+        self.ipc.check()
+        return ipc_ms, rccl_ms
+
+    def _ipc_capacity(self):
+        """Staging floats for the IPC kernels: any bucket _build_buckets can cut (for any set of
+        re-cuts by align_buckets) is either within the bucket limit or ONE parameter larger than
+        it (a parameter is never split), so the largest of those bounds every bucket."""
+        flat = self.flat
+        sizes = [(flat.offsets[i + 1] if i + 1 < len(flat.params) else flat.numel) - flat.offsets[i]
+                 for i in range(len(flat.params))]
+        return max([min(self._limit, flat.numel)] + sizes)
 
     def _build_buckets(self, cuts=()):
         """Contiguous buckets of <= bucket_mb over the flat gradient buffer; a bucket never spans
@@ -187,7 +254,9 @@ class DataParallel:
         g = self.flat.grad[s:e]
         self.bytes_reduced += g.numel() * g.element_size()
         if self.ipc is not None:
-            self.ipc(g)  # stream-ordered kernel: nothing to wait for
+            self._cs.wait_stream(torch.cuda.current_stream(g.device))  # the bucket's gradients are written
+            self.ipc(g, stream=self._cs)
+            self._cs_used = True
             return
         if self.zero:
             ps, pe = self.piece(b)
@@ -281,6 +350,9 @@ class DataParallel:
             self._launch(b)
         for w in self._works:
             w.wait()
+        if self._cs_used:
+            torch.cuda.current_stream(self.flat.grad.device).wait_stream(self._cs)
+            self._cs_used = False
         self.reset()
 
     @property

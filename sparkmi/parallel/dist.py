@@ -32,16 +32,21 @@ def init_distributed(backend=None, timeout_s=600):
     """Initialise the default process group from env vars; returns (rank, world, device)."""
     ws = int(os.environ.get("WORLD_SIZE", 1))
     use_gpu = torch.cuda.is_available() and os.environ.get("SPARKMI_FORCE_CPU", "0") != "1"
+    backend = backend or os.environ.get("SPARKMI_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     if use_gpu:
-        lr = local_rank()
-        torch.cuda.set_device(lr % max(1, torch.cuda.device_count()))
+        lr, ndev = local_rank(), max(1, torch.cuda.device_count())
+        if lr >= ndev and ws > 1 and backend == "nccl":
+            # RCCL needs one device per rank (several ranks per GPU only over gloo, in tests)
+            raise RuntimeError(f"LOCAL_RANK {lr} but only {ndev} visible GPU(s): RCCL runs one executor per "
+                               f"MI355X (launch at most {ndev} ranks per node, or use the gloo backend to "
+                               f"share devices in tests)")
+        torch.cuda.set_device(lr % ndev)
         device = torch.device("cuda", torch.cuda.current_device())
     else:
         device = torch.device("cpu")
     if ws > 1 and not is_dist():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
-        backend = backend or os.environ.get("SPARKMI_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         kw = {}
         if backend == "nccl":
             kw["device_id"] = device

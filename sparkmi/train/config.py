@@ -36,6 +36,7 @@ class TrainConfig:
     local_mode: bool = True        # TorchDistributor local_mode (False: barrier-task cluster mode)
     progress_timeout: float = 0.0  # s without step progress on a rank -> group failure (0: off)
     max_restarts: int = 0          # group restarts from the last checkpoint after a failure
+    phase_timing: bool = False     # graph steps as separate phase graphs + events (timing, slower)
     verbose: bool = True
 
     def to_json(self):

@@ -204,17 +204,25 @@ class StepRunner:
             # phase-timed graph step: forward + backward, gradient reduction (IPC kernel) and the
             # optimizer as three graphs replayed back to back, events between them (one more
             # replay per phase than the single-graph step: timing, not the fastest path)
+            # (single executor: no reduction phase, so no empty middle graph is captured)
             if self._dp:
                 self.ddp.set_overlap(False)
+                reduced0 = self.ddp.bytes_reduced  # capture records, it reduces nothing
             with torch.cuda.graph(g):
                 self.static_loss = self._fwd_bwd(*self.static_in)
             self._phase_graphs = []
-            for fn in ((lambda: self.ddp.finish()) if self._dp else (lambda: None),
-                       lambda: (self.opt.step(), self.ddp.gather_params() if self._dp else None)):
+            fns = [lambda: self.ddp.finish()] if self._dp else [None]
+            fns.append(lambda: (self.opt.step(), self.ddp.gather_params() if self._dp else None))
+            for fn in fns:
+                if fn is None:
+                    self._phase_graphs.append(None)
+                    continue
                 pg = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(pg, pool=g.pool()):
                     fn()
                 self._phase_graphs.append(pg)
+            if self._dp:
+                self.ddp.bytes_reduced = reduced0
             self._opt_in_graph = True
         else:
             # one executor, or data-parallel over the IPC all-reduce kernel: the WHOLE step
@@ -237,7 +245,8 @@ class StepRunner:
         self.graph.replay()
         if phased is not None:
             e1 = self._event()
-            phased[0].replay()
+            if phased[0] is not None:
+                phased[0].replay()
             e2 = self._event()
             phased[1].replay()
             e3 = self._event()

@@ -89,7 +89,7 @@ class Trainer:
         steps_run, last = 0, None
         done = False
         data_s, bytes0 = 0.0, 0
-        self.runner.phase_timing = bool(getattr(cfg, "phase_timing", True))
+        self.runner.phase_timing = bool(getattr(cfg, "phase_timing", False))
         while self.epoch < epochs and not done:
             if hasattr(loader, "set_epoch"):
                 loader.set_epoch(self.epoch)

@@ -47,6 +47,20 @@ def test_bench_spawns_ranks():
     out = _run([sys.executable, "bench.py", "--gpus", "2"] + TINY)
     _check(out, 2)
     assert out["allreduce_ms"] is not None and out["transformer_fp32"]["grad_bytes"] > 0
+    assert out["transformer_fp32"]["ranks_in_sync"] is True
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_bench_two_ranks_on_the_gpu():
+    """bench.py --gpus 2 on the box's one MI355X (gloo between the two ranks sharing it): the
+    fp32 transformer step through the GPU kernels, split-graph backward with the overlapped
+    bucket reduction, and bit-identical parameters on both ranks after the timed steps."""
+    out = _run([sys.executable, "bench.py", "--gpus", "2", "--model", "transformer", "--dtype", "fp32", "--layers", "2",
+                "--steps", "4", "--warmup", "3", "--no-f32-compare", "--no-zero-compare"],
+               env={"SPARKMI_DIST_BACKEND": "gloo"})
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 64 and out["value"] > 0
+    assert out["transformer_fp32"]["ranks_in_sync"] is True, out["transformer_fp32"]
 
 
 @pytest.mark.slow

@@ -1,6 +1,6 @@
 """T6 on one MI355X: the native comm layer (csrc/comm/ipc_allreduce.hip).
 
-* IPC one-shot AND two-shot all-reduce with TWO processes sharing the GPU (IPC handles work
+* IPC one-shot AND two-shot all-reduce with 2, 4 and 8 processes sharing the GPU (IPC handles work
   across processes on one device): results equal the rank-ordered fp32 sum bit
   for bit, over several epochs (both staging halves), both kernels interleaved on one signal
   array, and sizes from 16 B to 16 MB (ragged chunks, buckets that do not fill a block).
@@ -43,17 +43,22 @@ def _ipc_fn():
     return out
 
 
-def test_ipc_allreduce_two_processes_one_gpu():
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_ipc_allreduce_processes_one_gpu(world):
+    """2, 4 and 8 ranks sharing the GPU: the 8-rank signal slots, the 4- and 8-chunk two-shot
+    ranges (ragged last chunks) and the rank-order sums the node's 8-GPU run relies on."""
     from sparkmi.api import Distributor
-    res = Distributor(num_processes=2, use_gpu=True, share_gpus=True, env={"SPARKMI_DIST_BACKEND": "gloo"}, log_sink=None,
-                      timeout=300).run(_ipc_fn)
+    res = Distributor(num_processes=world, use_gpu=True, share_gpus=True, env={"SPARKMI_DIST_BACKEND": "gloo"},
+                      log_sink=None, timeout=380).run(_ipc_fn)
     k = 0
     for it in range(3):
         for n in SIZES:
-            a = torch.randn(n, generator=torch.Generator().manual_seed(1000 * it + n))
-            b = torch.randn(n, generator=torch.Generator().manual_seed(1000 * it + n + 1))
+            want = torch.randn(n, generator=torch.Generator().manual_seed(1000 * it + n))
+            for r in range(1, world):  # rank order, as the kernels sum
+                want = want + torch.randn(n, generator=torch.Generator().manual_seed(1000 * it + n + r))
             for algo in (1, 2):
-                assert torch.equal(res[k], a + b), (it, n, algo)
+                assert torch.equal(res[k], want), (world, it, n, algo)
                 k += 1
 
 
@@ -82,17 +87,27 @@ def _lost_fn():
             res["raised"] = False
         except IpcPeerLost:
             res["raised"] = True
+        # once a loss is recorded (sticky), a later call poisons at once, no polling
+        y = torch.ones(65536, device=dev)
+        t0 = time.time()
+        ar(y, algo=2)
+        torch.cuda.synchronize()
+        res["wait2_s"] = time.time() - t0
+        res["finite2"] = int(torch.isfinite(y).sum())
     allr = [None] * world
     torch.distributed.all_gather_object(allr, res)  # Distributor.run returns rank 0's value
     destroy()
     return allr
 
 
-def test_ipc_peer_lost_poisons_and_raises():
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 4])
+def test_ipc_peer_lost_poisons_and_raises(world):
     from sparkmi.api import Distributor
-    res = Distributor(num_processes=2, use_gpu=True, share_gpus=True, env={"SPARKMI_DIST_BACKEND": "gloo"}, log_sink=None,
-                      timeout=300).run(_lost_fn)
-    r0, r1 = res
-    assert r0["ok1"] == r0["ok2"] == r1["ok1"] == r1["ok2"] == 2.0
+    res = Distributor(num_processes=world, use_gpu=True, share_gpus=True, env={"SPARKMI_DIST_BACKEND": "gloo"},
+                      log_sink=None, timeout=280).run(_lost_fn)
+    r0, r1 = res[0], res[1]
+    assert r0["ok1"] == r0["ok2"] == r1["ok1"] == r1["ok2"] == float(world)
     assert r0["raised"] and r0["finite"] == 0, r0  # poisoned, loud
     assert r0["wait_s"] < 30.0, r0  # bounded by the configured timeout (1 s of polling)
+    assert r0["finite2"] == 0 and r0["wait2_s"] < 0.5, r0  # poisoned without another timeout

@@ -81,10 +81,15 @@ _CFGS = [  # name, optimizer, zero, graph, split, ipc
     ("adam_zero_graph", "adam", True, True, False, False),
     ("adam_split", "adam", False, True, True, False),
     ("adam_zero_split", "adam", True, True, True, False),
+    # the IPC kernels on their comm stream under the split-graph backward (buckets reduced while
+    # the next backward piece replays), two-shot forced (2 ranks would pick one-shot)
+    ("sgd_ipc2_eager", "sgd", False, False, False, 2),
+    ("sgd_ipc2_split", "sgd", False, True, True, 2),
+    ("adam_ipc2_split", "adam", False, True, True, 2),
 ]
 
 
-def _dp_grid(steps):
+def _dp_grid(steps, only=None):
     import torch
     from sparkmi.models.transformer import Transformer
     from sparkmi.ops.rng import reset_salts
@@ -100,15 +105,19 @@ def _dp_grid(steps):
     for name, ok, zero, graph, split, ipc in _CFGS:
         if world == 1 and name not in ("sgd_eager", "adam_eager"):
             continue
+        if only is not None and name not in only:
+            continue
         reset_salts()
         torch.manual_seed(0)
         m = Transformer(d_model=128, ffn_hidden=256, num_heads=2, drop_prob=0.0, num_layers=2, max_sequence_length=64,
                         src_vocab_size=300, tgt_vocab_size=300, emb_dropout=0.0, dtype="fp32").to(device)
         flat = FlatParams(m, shadow=False)
         opt = SGD(flat, lr=0.05) if ok == "sgd" else Adam(flat, lr=1e-3)
-        ddp = DataParallel(flat, bucket_mb=0.5, zero=zero, ipc=ipc) if world > 1 else None
+        ddp = DataParallel(flat, bucket_mb=0.5, zero=zero, ipc=bool(ipc)) if world > 1 else None
         if ddp is not None:
-            assert (ddp.ipc is not None) == ipc, name
+            assert (ddp.ipc is not None) == bool(ipc), name
+            if ipc == 2:
+                ddp.ipc.force_algo = 2
         split_fn = (lambda mm, s, t: mm.training_step_split(s, t)) if split else None
         runner = StepRunner(m, lambda mm, s, t: mm.training_step_loss(s, t), opt, ddp, graph=graph, warmup_eager=2,
                             split_fn=split_fn)
@@ -151,3 +160,32 @@ def test_transformer_dp_parity_grid():
     assert (a["adam_eager"] - r1["adam_eager"]).abs().max() < 5 * 1e-3 * 5
     for mode in ("eager", "graph", "split"):
         assert torch.equal(a[f"adam_zero_{mode}"], a[f"adam_{mode}"]), mode
+    # IPC two-shot on the comm stream: the split-graph step equals the eager step bit for bit
+    # (same rank-order sums), and both agree with the process-group path to fp32 tolerance
+    assert torch.equal(a["sgd_ipc2_split"], a["sgd_ipc2_eager"])
+    torch.testing.assert_close(a["sgd_ipc2_eager"], r1["sgd_eager"], rtol=1e-4, atol=1e-5)
+    assert (a["adam_ipc2_split"] - r1["adam_eager"]).abs().max() < 5 * 1e-3 * 5
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_transformer_dp_parity_grid_world4():
+    """The same grid at FOUR ranks sharing the GPU (batch 2 each == one rank at batch 8): the
+    4-chunk two-shot ranges, the 4-way ZeRO-1 pieces and the IPC split-graph path, which the
+    2-rank grid cannot reach."""
+    env = {"SPARKMI_DIST_BACKEND": "gloo"}
+    only = ("sgd_eager", "sgd_split", "sgd_ipc_eager", "sgd_ipc2_split", "adam_eager", "adam_zero_eager",
+            "adam_zero_split", "adam_split")
+    r4 = launch(_dp_grid, (4, only), {}, num_processes=4, use_gpu=True, env=env, log_sink=None, timeout=380)
+    (r1,) = launch(_dp_grid, (4,), {}, num_processes=1, use_gpu=True, env=env, log_sink=None, timeout=380)
+    for name in r4[0]:
+        for q in r4[1:]:
+            assert torch.equal(r4[0][name], q[name]), f"{name}: ranks disagree"
+    a = r4[0]
+    for name in ("sgd_eager", "sgd_split", "sgd_ipc_eager", "sgd_ipc2_split"):
+        torch.testing.assert_close(a[name], r1["sgd_eager"], rtol=1e-4, atol=1e-5, msg=name)
+    # 4-operand sums: the reduce-scatter and the all-reduce may associate differently, and Adam's
+    # sign-like first steps amplify last-bit differences on ~zero gradients (bound as above)
+    assert (a["adam_zero_eager"] - a["adam_eager"]).abs().max() < 5 * 1e-3 * 4
+    assert (a["adam_zero_split"] - a["adam_split"]).abs().max() < 5 * 1e-3 * 4
+    assert (a["adam_eager"] - r1["adam_eager"]).abs().max() < 5 * 1e-3 * 4

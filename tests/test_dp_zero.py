@@ -156,3 +156,43 @@ def test_deferred_queue_recovers_after_failed_backward():
     _grad._cb[0] = True
     assert _grad.reset_deferred() is True
     assert not _grad.pending()
+
+
+def test_ipc_capacity_covers_oversized_parameter_buckets():
+    """a parameter larger than the bucket limit gets a bucket of its own that exceeds
+    the limit; the IPC staging capacity must cover it (and every re-cut by align_buckets)."""
+    from sparkmi.parallel.ddp import DataParallel
+    from sparkmi.utils.flat import FlatParams
+    m = torch.nn.Sequential(torch.nn.Embedding(5000, 32), torch.nn.Linear(32, 4))  # 160k-float embedding
+    flat = FlatParams(m, device="cpu", shadow=False)
+    dp = DataParallel.__new__(DataParallel)
+    dp.flat, dp._limit = flat, 1000          # bucket limit far below the embedding
+    dp._build_buckets()
+    cap = dp._ipc_capacity()
+    assert max(e - s for s, e, _ in dp.buckets) <= cap
+    for cuts in ([1], [1, 2], [0, 1, 2]):
+        dp._build_buckets(cuts)
+        assert max(e - s for s, e, _ in dp.buckets) <= cap
+    assert cap >= 5000 * 32
+
+
+def test_choose_comm_prefers_the_measured_faster_path():
+    """Bulk-gradient path selection from the start-up measurement."""
+    from sparkmi.parallel.ddp import choose_comm
+    assert choose_comm(1.0, 2.0) == "ipc"
+    assert choose_comm(2.0, 1.0) == "rccl"
+    assert choose_comm(1.5, 1.5) == "ipc"        # a tie keeps the graph-capturable kernel
+    assert choose_comm(None, 1.0) == "rccl"      # IPC unavailable
+    assert choose_comm(1.0, None) == "ipc"
+
+
+def test_dp_probe_disabled_uses_rccl_for_bulk(monkeypatch):
+    """SPARKMI_DP_PROBE=0: a bulk gradient (> IPC_LIMIT_BYTES) goes to the process group without
+    building the IPC path; world 1 never probes."""
+    from sparkmi.parallel import ddp
+    from sparkmi.utils.flat import FlatParams
+    monkeypatch.setenv("SPARKMI_DP_PROBE", "0")
+    monkeypatch.setattr(ddp, "IPC_LIMIT_BYTES", 16)
+    flat = FlatParams(torch.nn.Linear(8, 8), device="cpu", shadow=False)
+    dp = ddp.DataParallel(flat)
+    assert dp.ipc is None and dp.comm_probe is None and dp.comm == "none"

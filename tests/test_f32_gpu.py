@@ -512,6 +512,39 @@ def test_transformer_f32_concat_kv_matches_cpu():
         assert rel < 1e-4, (n, float(rel))
 
 
+@pytest.mark.timeout(600)
+def test_transformer_f32_gradients_match_cpu_across_salts():
+    """the one-step GPU-vs-CPU gradient check must not depend on which dropout
+    salts the models drew (salts are a process counter, so 16 offsets = 16 different mask sets on
+    the L=3 concat-kv model).  Every parameter of every offset is checked (not only the first in
+    iteration order) against the same 1e-4 relative bound; the failure message lists them all."""
+    from sparkmi.data.synthetic import translation_pairs
+    from sparkmi.utils.flat import FlatParams
+    bad = []
+    for burn in range(0, 400, 25):
+        R.reset_salts()
+        for _ in range(burn):
+            R.new_salt()
+        mc, mg = _pair(L=3)
+        mc.train(); mg.train()
+        FlatParams(mc)
+        fg = FlatParams(mg, shadow=False)
+        src, tgt = translation_pairs(4, 32, 96, 96, seed=3)
+        fg.zero_grad()
+        lc = mc.training_step_loss(src, tgt)
+        lg = mg.training_step_loss(src.to(dev), tgt.to(dev))
+        if abs(float(lc) - float(lg)) >= 1e-5 * max(1.0, abs(float(lc))):
+            bad.append((burn, "loss", float(lc), float(lg)))
+        lc.backward()
+        lg.backward()
+        torch.cuda.synchronize()
+        for (n, pc), (_, pg) in zip(mc.named_parameters(), mg.named_parameters()):
+            rel = float((pg.grad.cpu().double() - pc.grad.double()).norm() / (pc.grad.double().norm() + 1e-12))
+            if not rel < 1e-4:
+                bad.append((burn, n, rel))
+    assert not bad, f"{len(bad)} mismatches: {bad}"
+
+
 def test_transformer_f32_flagship_trajectory(f32_algo, monkeypatch):
     """The BASELINE.json model at full shape (L6, d512, h8, ffn1024, S256, V10000; dropout 0.1,
     reference mask mode), batch 2, 10 Adam steps at the reference's lr 1e-3 on flat parameters:

@@ -79,7 +79,7 @@ def test_translator_graph_metrics_phases(tmp_path):
     from sparkmi.recipes import translator
     r = translator.main(GPU + ["--n-train", "640", "--max-steps", "12", "--d-model", "128", "--ffn-hidden", "256",
                                "--num-heads", "2", "--max-sequence-length", "64", "--log-every", "4",
-                               "--metrics", str(tmp_path / "m")])
+                               "--phase-timing", "--metrics", str(tmp_path / "m")])
     assert r["steps"] == 12 and r["dtype"] == "fp32"
     recs = _phase_recs(str(tmp_path / "m.rank0.jsonl"))
     assert recs, "no phase record"
@@ -98,7 +98,7 @@ def test_translator_graph_dp_metrics_phases(tmp_path, monkeypatch):
     monkeypatch.setenv("SPARKMI_DP_COMM", "rccl")      # the process-group path, not the IPC kernel
     r = translator.main(GPU + ["--world", "2", "--n-train", "640", "--epochs", "3", "--max-steps", "12", "--d-model", "128",
                                "--ffn-hidden", "256", "--num-heads", "2", "--max-sequence-length", "64",
-                               "--log-every", "4", "--metrics", str(tmp_path / "m")])
+                               "--log-every", "4", "--phase-timing", "--metrics", str(tmp_path / "m")])
     assert r["steps"] == 12 and r["world"] == 2
     recs = _phase_recs(str(tmp_path / "m.rank0.jsonl"))
     assert recs and recs[-1]["fwd_bwd_s"] > 0 and recs[-1]["allreduce_s"] >= 0 and recs[-1]["optim_s"] > 0, recs
