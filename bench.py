@@ -285,7 +285,9 @@ def bench_cnn(args, rank, world, device, dtype="fp32"):
     opt = SGD(flat, lr=0.01)
     ddp = DataParallel(flat) if world > 1 else None
     use_graph = device.type == "cuda" and args.graph != "off"
-    runner = StepRunner(model, lambda m, x, y: m.loss(x, y), opt, ddp, graph=use_graph)
+    # one executor: the whole step (forward, backward, batch gradient sum, SGD) is ONE launch
+    fused = (lambda m, o, x, y: m.fused_sgd_step(o, x, y)) if world == 1 else None
+    runner = StepRunner(model, lambda m, x, y: m.loss(x, y), opt, ddp, graph=use_graph, fused_step=fused)
     imgs, labels = fashion_mnist_like(16 * args.cnn_batch, seed=7 + rank, device=device)
     batches = [(imgs[i * args.cnn_batch:(i + 1) * args.cnn_batch], labels[i * args.cnn_batch:(i + 1) * args.cnn_batch])
                for i in range(16)]

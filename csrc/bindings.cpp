@@ -93,6 +93,7 @@ void smi_gemm_set_bm(int);
 int smi_gemm_wgrad_group(const void* const*, const long*, const void* const*, const long*, void* const*, void* const*,
                          const int*, const int*, const int*, int, hipStream_t);
 int smi_cnn(const CNNArgs*, hipStream_t);
+int smi_cnn_fused_ok(int, int, int);
 int smi_cnn_reduce(const CNNArgs*, hipStream_t);
 int smi_gather_rows(const void*, const long long*, void*, long, long, hipStream_t);
 int smi_gather_u8_scale(const void*, const long long*, void*, long, long, float, int, hipStream_t);
@@ -520,6 +521,29 @@ PYBIND11_MODULE(_C, m) {
     a.loss = (float*)loss; a.loss_scale = loss_scale; a.dloss = (const float*)dloss; a.train = train;
     chk(phase == 0 ? smi_cnn(&a, S(st)) : smi_cnn_reduce(&a, S(st)), "cnn");
   });
+
+  // the whole single-executor CNN training step in ONE launch: forward + backward per image and
+  // the fused slab reduction + SGD update in the kernel's tail (CNNArgs::fused)
+  m.def("cnn_sgd_step", [](u x, int x_u8, float x_scale, u y, int B, int cin, int C, int classes, std::vector<u> w,
+                           std::vector<u> b, std::vector<u> shadow, u slab, u part, u row_loss, u loss,
+                           float loss_scale, u lr, u step, u tick, int bf16, u st) {
+    CNNArgs a{};
+    a.bf16 = bf16;
+    if (w.size() != 5 || b.size() != 5) throw std::runtime_error("cnn_sgd_step: need 5 weight and 5 bias pointers");
+    if (!shadow.empty() && shadow.size() != 10) throw std::runtime_error("cnn_sgd_step: 0 or 10 shadow pointers");
+    a.x = (const void*)x; a.x_u8 = x_u8; a.x_scale = x_scale; a.y = (const long long*)y;
+    a.B = B; a.cin = cin; a.C = C; a.classes = classes;
+    for (int i = 0; i < 5; ++i) { a.w[i] = (const float*)w[i]; a.b[i] = (const float*)b[i]; }
+    for (int i = 0; i < 10; ++i) a.shadow[i] = shadow.empty() ? nullptr : (unsigned short*)shadow[i];
+    const int sz[10] = {C * cin * 9, C, C * C * 9, C, C * C * 9, C, C * C * 9, C, classes * C * 49, classes};
+    int o = 0;
+    for (int i = 0; i < 10; ++i) { a.off[i] = o; o += sz[i]; }
+    a.P = o; a.slab = (float*)slab; a.part = (float*)part; a.row_loss = (float*)row_loss; a.loss = (float*)loss;
+    a.loss_scale = loss_scale; a.train = 1; a.fused = 1;
+    a.lr = (const float*)lr; a.step = (float*)step; a.tick = (unsigned*)tick;
+    chk(smi_cnn(&a, S(st)), "cnn_sgd_step");
+  });
+  m.def("cnn_fused_ok", [](int C, int cin, int classes) { return smi_cnn_fused_ok(C, cin, classes) != 0; });
 
   m.def("lstm_supported", [](int E, int H, int L, int C) { return smi_lstm_supported(E, H, L, C) != 0; });
   m.def("lstm_slab_floats", [](int B, int E, int H, int L, int C) { return smi_lstm_slab_floats(B, E, H, L, C); });

@@ -44,4 +44,6 @@ struct AttnF32Args {
   const unsigned short* qpi; const unsigned short* kpi; const unsigned short* vpi; const unsigned short* dopi;
   long qi_ps, kvi_ps, doi_ps;
   int no_f32_grad;                   // backward: write dQ / dK / dV as planes only (dqp / dkp / dvp set)
+  int ae16;                          // set by the launcher: outputs and their planes admit whole-row
+                                     // 16-B stores (row-coalesced LDS epilogue, attention_f32.hip)
 };

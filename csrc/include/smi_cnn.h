@@ -13,4 +13,13 @@ struct CNNArgs {
   const float* dloss;                        // upstream grad of the loss (reduce kernel)
   int train;
   int bf16;                                  // convolutions on bf16 matrix cores (fp32 accumulate)
+  // fused SGD step (cnn_kernel's tail, one launch per training step): the per-image slabs are
+  // summed in two ticketed levels (groups of CNN_GRP images, then the groups) and the LAST
+  // workgroup applies p -= lr * g to the parameters (+ their bf16 shadows), the mean loss and the
+  // step counter.  part: [ceil(B / CNN_GRP)][P] group sums; tick: CNN_GRP + 1 zeroed counters
+  // (re-armed by the kernel), owned by the model.
+  int fused;
+  float* part; unsigned* tick; const float* lr; float* step;
+  unsigned short* shadow[10];                // per-parameter bf16 shadows (slab order) or null
 };
+#define CNN_GRP 8

@@ -658,6 +658,52 @@ __device__ __forceinline__ void as_cols_acc(const unsigned short* img, int lane,
   }
 }
 
+// Row-coalesced epilogue (the kernels' transposed outputs O^T / dQ^T / dK^T / dV^T): lane (row
+// l & 31, half h) holds head dims 32 dt + 8 g + 4 h + e in register 4 g + e of acc[dt], so a direct
+// store writes one 16-B piece of 32 different rows per instruction (row stride apart: every
+// store touches 32-64 cache lines, and the all-CU store burst at the end of the kernel is
+// issue-bound).  Instead the wave stages its 32 x 64 tile in a private LDS image (pitch 68:
+// conflict-free float4 rows) and stores whole rows: fp32 as 256-B row segments (4 rows per wave
+// instruction), planes as 128-B row segments (8 rows per instruction, each lane splitting 8
+// consecutive values).  Bitwise the same values as the direct stores.
+#define AE_PITCH 68
+#define AE_FLOATS (32 * AE_PITCH)
+__device__ __forceinline__ void ae_stage(float* img, const f32x16_t (&acc)[2], int lane, float sc) {
+  const int row = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *(float4*)(img + row * AE_PITCH + 32 * dt + 8 * g + 4 * h) =
+          make_float4(acc[dt][4 * g] * sc, acc[dt][4 * g + 1] * sc, acc[dt][4 * g + 2] * sc, acc[dt][4 * g + 3] * sc);
+}
+// dst / P: row 0 of the wave's 32 rows (fp32 output / plane 0, either may be null), rows ss apart
+__device__ __forceinline__ void ae_store(const float* img, float* __restrict__ dst, unsigned short* __restrict__ P, long ss,
+                                         long ps, int nrows, int lane) {
+  if (dst) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int row = 4 * k + (lane >> 4), c = 4 * (lane & 15);
+      if (row < nrows) *(float4*)(dst + (long)row * ss + c) = *(const float4*)(img + row * AE_PITCH + c);
+    }
+  }
+  if (P) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int row = 8 * k + (lane >> 3), c = 8 * (lane & 7);
+      if (row < nrows) {
+        const float4 v0 = *(const float4*)(img + row * AE_PITCH + c), v1 = *(const float4*)(img + row * AE_PITCH + c + 4);
+        const float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        const Split3 sp = split3_8(f);
+        unsigned short* q = P + (long)row * ss + c;
+        *(bf16x8_t*)q = sp.h;
+        *(bf16x8_t*)(q + ps) = sp.m;
+        *(bf16x8_t*)(q + 2 * ps) = sp.l;
+      }
+    }
+  }
+}
+
 // operand sources of batch b, head hh (fp32 base + plane base at the same element offset)
 #define AS_SRC(NAME, FP, PP, PS, SB, SH, SS)                                                         \
   const AsSrc<PI> NAME{(FP) + b * (SB) + hh * (SH), PI ? (PP) + b * (SB) + hh * (SH) : nullptr, (PS), (SS)}
@@ -777,19 +823,26 @@ __device__ __forceinline__ void attn_sp_fwd_body(const AttnF32Args& a) {
     AST_ADD(5, tc5, tc6);  // barrier
   }
   AST_T(tk2);
-  if (qi < a.Sq) {
+  const float inv = l > 0.f ? 1.0f / l : 0.f;
+  if (NW == 4 && a.ae16) {
+    // row-coalesced stores through the (now free) K / V staging buffers: 4 x 8.5 KiB of 48 KiB
+    float* img = (float*)(w < 2 ? &Ks[0][0] : &Vs[0][0]) + (w & 1) * AE_FLOATS;  // 2 x 8.5 of 24 KiB each
+    ae_stage(img, o, lane, inv);
+    __syncthreads();
+    const long r0 = (long)b * a.o_sb + hh * a.o_sh + (long)qwave * a.o_ss;
+    ae_store(img, a.o + r0, a.op ? a.op + r0 : nullptr, a.o_ss, a.op_ps, a.Sq - qwave, lane);
+  } else if (qi < a.Sq) {
     float* O = a.o + b * a.o_sb + hh * a.o_sh + (long)qi * a.o_ss;
-    const float inv = l > 0.f ? 1.0f / l : 0.f;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) fa_store_rowT(O + dt * 32, o[dt], lane, inv);
     if (a.op) {
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) fa_store_rowT_planes(a.op + (O - a.o) + dt * 32, a.op_ps, o[dt], lane, inv);
     }
-    if (h == 0) {
-      const float mref = (m == -INFINITY) ? 0.f : m;
-      a.lse[((long)b * a.H + hh) * a.Sq + qi] = l > 0.f ? mref + log2f(l) : INFINITY;
-    }
+  }
+  if (qi < a.Sq && h == 0) {
+    const float mref = (m == -INFINITY) ? 0.f : m;
+    a.lse[((long)b * a.H + hh) * a.Sq + qi] = l > 0.f ? mref + log2f(l) : INFINITY;
   }
   AST_T(tk3);
   AST_ADD(6, tk2, tk3);  // epilogue stores
@@ -879,7 +932,15 @@ __global__ __launch_bounds__(256, 2) void attn_sp_dq_kernel(AttnF32Args a) {
     if (more) { as_store(Ks[buf ^ 1], pk); as_store(Vs[buf ^ 1], pv); }
     __syncthreads();
   }
-  if (qi < a.Sq) {
+  if (a.ae16) {
+    // staging buffers free after the loop's last barrier: waves 0-1 in Ks, 2-3 in Vs (2 x 8.5 of 24 KiB)
+    float* img = (float*)(w < 2 ? &Ks[0][0] : &Vs[0][0]) + (w & 1) * AE_FLOATS;
+    ae_stage(img, acc, lane, a.scale);
+    __syncthreads();
+    const long r0 = (long)b * a.q_sb + hh * a.q_sh + (long)qwave * a.q_ss;
+    ae_store(img, a.no_f32_grad ? nullptr : a.dq + r0, a.dqp ? a.dqp + r0 : nullptr, a.q_ss, a.dq_ps, a.Sq - qwave,
+             lane);
+  } else if (qi < a.Sq) {
     float* dQ = a.dq + b * a.q_sb + hh * a.q_sh + (long)qi * a.q_ss;
     if (!a.no_f32_grad) {
 #pragma unroll
@@ -1102,7 +1163,21 @@ __global__ __launch_bounds__(512, 1) void attn_sp_dkdv8_kernel(AttnF32Args a) {
     }
     __syncthreads();
   }
-  if (kj < a.Sk) {
+  if (a.ae16) {
+    // every wave's dK and dV tiles through the (free) owned-V images: 2 x 8.5 KiB of its 12 KiB
+    float* img = (float*)&Vo[w][0];
+    ae_stage(img, dk, lane, a.scale);
+    __syncthreads();
+    const long rk = (long)b * a.k_sb + hh * a.k_sh + (long)kwave * a.k_ss;
+    const long rv = (long)b * a.v_sb + hh * a.v_sh + (long)kwave * a.v_ss;
+    ae_store(img, a.no_f32_grad ? nullptr : a.dk + rk, a.dkp ? a.dkp + rk : nullptr, a.k_ss, a.dkv_ps, a.Sk - kwave,
+             lane);
+    __syncthreads();
+    ae_stage(img, dv, lane, 1.0f);
+    __syncthreads();
+    ae_store(img, a.no_f32_grad ? nullptr : a.dv + rv, a.dvp ? a.dvp + rv : nullptr, a.v_ss, a.dkv_ps, a.Sk - kwave,
+             lane);
+  } else if (kj < a.Sk) {
     float* dK = a.dk + b * a.k_sb + hh * a.k_sh + (long)kj * a.k_ss;
     float* dV = a.dv + b * a.v_sb + hh * a.v_sh + (long)kj * a.v_ss;
     if (!a.no_f32_grad) {
@@ -1231,9 +1306,24 @@ static bool fa_pi(const AttnF32Args& a, bool bwd) {
   return (al & 15) == 0;
 }
 
+// whole-row 16-B stores of an output (fp32: float4 rows, already required by fa_ok) and of its
+// planes (8 bf16 per store): 16-B plane base and strides that are multiples of 8 elements
+static bool fa_ae16(const unsigned short* p, long sb, long sh, long ss) {
+  return !p || ((((uintptr_t)p) & 15) == 0 && sb % 8 == 0 && sh % 8 == 0 && ss % 8 == 0);
+}
+static int g_attn_ae = -1;  // SMI_ATTN_AE=0: the per-lane transposed stores
+static bool fa_ae_enabled() {
+  if (g_attn_ae < 0) {
+    const char* e = getenv("SMI_ATTN_AE");
+    g_attn_ae = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_attn_ae != 0;
+}
+
 extern "C" int smi_attn_f32_fwd(const AttnF32Args* args, hipStream_t st) {
-  const AttnF32Args& a = *args;
+  AttnF32Args a = *args;
   if (!fa_ok(a)) return -1;
+  a.ae16 = fa_ae_enabled() && fa_ae16(a.op, a.o_sb, a.o_sh, a.o_ss);
   dim3 grid((a.Sq + 127) / 128, a.H, a.B);
   if (smi_gemm_f32_algo(-1) != 0 && smi_attn_f32_sp(-1)) {
     if (smi_attn_fwd8(-1)) {
@@ -1248,9 +1338,11 @@ extern "C" int smi_attn_f32_fwd(const AttnF32Args* args, hipStream_t st) {
 }
 
 extern "C" int smi_attn_f32_bwd(const AttnF32Args* args, hipStream_t st) {
-  const AttnF32Args& a = *args;
+  AttnF32Args a = *args;
   if (!fa_ok(a) || !a.dout || !a.delta || (((uintptr_t)a.dout | (uintptr_t)a.dq | (uintptr_t)a.dk | (uintptr_t)a.dv) & 15))
     return -1;
+  a.ae16 = fa_ae_enabled() && fa_ae16(a.dqp, a.q_sb, a.q_sh, a.q_ss) && fa_ae16(a.dkp, a.k_sb, a.k_sh, a.k_ss) &&
+           fa_ae16(a.dvp, a.v_sb, a.v_sh, a.v_ss);
   if (a.no_f32_grad && (!a.dqp || !a.dkp || !a.dvp)) return -1;  // planes-only needs every plane output
   if (smi_gemm_f32_algo(-1) != 0 && smi_attn_f32_sp(-1)) {
     const bool pi = fa_pi(a, true);

@@ -469,6 +469,79 @@ __device__ __forceinline__ void conv_wgrad_bf16(const float* __restrict__ dz, co
   }
 }
 
+// Fused SGD tail (CNNArgs::fused): the step's remaining work without a second launch.  Level 1:
+// the last image of each group of CNN_GRP to finish (ticket; release / acquire fences around it)
+// sums the group's slabs in image order into part[group]; level 2: the last group to finish sums
+// the group partials in group order and applies torch SGD (p -= lr * g) to every parameter, then
+// the mean loss (image order) and the step counter.  Float4 passes (P % 4 == 0, checked by the
+// launcher) keep enough loads in flight for one workgroup to read a group's 8 x 31 KB slabs in a
+// few microseconds.  Deterministic: every sum has a fixed order.  No spinning: a workgroup that
+// is not the last simply exits.
+__device__ __noinline__ void cnn_fused_tail(const CNNArgs& g, int img) {
+  __shared__ int last;
+  const int ngrp = (g.B + CNN_GRP - 1) / CNN_GRP;
+  const int grp = img / CNN_GRP, g0 = grp * CNN_GRP, g1 = min(g.B, g0 + CNN_GRP);
+  __syncthreads();  // every thread's slab stores issued
+  if (threadIdx.x == 0) {
+    __threadfence();  // release this image's slab
+    last = atomicAdd(g.tick + grp, 1u) == (unsigned)(g1 - g0 - 1);
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();  // acquire the group's slabs
+  const int P4 = g.P / 4;
+  const float4* slab4 = (const float4*)g.slab;
+  float4* part4 = (float4*)(g.part + (long)grp * g.P);
+  for (int q = threadIdx.x; q < P4; q += blockDim.x) {
+    float4 acc = slab4[(long)g0 * P4 + q];
+#pragma unroll 8
+    for (int i = g0 + 1; i < g1; ++i) {
+      const float4 v = slab4[(long)i * P4 + q];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    part4[q] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();  // release the group sum
+    g.tick[grp] = 0u;  // re-arm (every image of the group has taken its ticket)
+    last = atomicAdd(g.tick + CNN_GRP, 1u) == (unsigned)(ngrp - 1);
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();  // acquire every group sum
+  const float lr = g.lr[0];
+  const float4* pall = (const float4*)g.part;
+  for (int q = threadIdx.x; q < P4; q += blockDim.x) {
+    float4 s = pall[q];
+    for (int k = 1; k < ngrp; ++k) {
+      const float4 v = pall[(long)k * P4 + q];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    const float sv[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int p = 4 * q + e;
+      int seg = 0;
+      while (seg < 9 && p >= g.off[seg + 1]) ++seg;
+      float* dst = (float*)(seg % 2 == 0 ? g.w[seg / 2] : g.b[seg / 2]) + (p - g.off[seg]);
+      const float np = *dst - lr * sv[e];
+      *dst = np;
+      if (g.shadow[seg]) g.shadow[seg][p - g.off[seg]] = f2bf(np);
+    }
+  }
+  if (threadIdx.x < 64) {
+    float ls = 0.f;
+    for (int i = threadIdx.x; i < g.B; i += 64) ls += g.row_loss[i];
+    ls = wave_sum(ls);
+    if (threadIdx.x == 0) {
+      if (g.loss) g.loss[0] = ls * g.loss_scale;
+      if (g.step) g.step[0] += 1.f;
+      g.tick[CNN_GRP] = 0u;
+    }
+  }
+}
+
 // CC: channel capacity; EX: g.C == CC exactly (compile-time channel count, no clamps)
 template <int CC, bool EX, bool BF>
 __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
@@ -552,7 +625,7 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   }
   // mean loss without a second launch: the last workgroup to get here (atomic ticket) sums
   // row_loss in image order with wave 0 and re-arms the ticket
-  if (g.loss && g.row_loss) {
+  if (g.loss && g.row_loss && !g.fused) {
     __shared__ int cnn_last;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -642,6 +715,7 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   STAMP(20);
   for (int e = threadIdx.x; e < C * CI * 9 + C; e += blockDim.x)
     gs[(e < C * CI * 9 ? g.off[0] + e : g.off[1] + e - C * CI * 9)] = wacc[e];
+  if (g.fused) cnn_fused_tail(g, img);
 }
 
 // grad[p] (+)= dloss * sum_img slab[img][p], scattered to the 10 parameter tensors; also the mean
@@ -677,6 +751,7 @@ static size_t cnn_lds_bytes(const CNNArgs& g) {
 
 extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
   CNNArgs g = *args;
+  if (g.fused && (g.P % 4 || !g.part || !g.tick || !g.lr || !g.slab || !g.row_loss || !g.train)) return -1;
   if (g.C < 1 || g.C > CNN_MAXC || g.cin < 1 || g.cin > 4 || g.classes < 1 || g.classes > 16) return -1;
   const size_t lds = cnn_lds_bytes(g);
   if (lds > 160 * 1024) return -1;
@@ -687,6 +762,11 @@ extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
   hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(g.B), dim3(CNN_THREADS), lds, st, g);
   SMI_CHECK_LAUNCH();
+}
+
+extern "C" int smi_cnn_fused_ok(int C, int cin, int classes) {
+  const int P = C * cin * 9 + C + 3 * (C * C * 9 + C) + classes * C * 49 + classes;
+  return P % 4 == 0;
 }
 
 extern "C" int smi_cnn_reduce(const CNNArgs* args, hipStream_t st) {

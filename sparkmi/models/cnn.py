@@ -8,7 +8,7 @@ state_dicts load.  ``loss(x, y)`` runs the fused whole-network HIP kernel (spark
 import torch
 from torch import nn
 
-from ..ops.cnn import cnn_logits, cnn_loss
+from ..ops.cnn import cnn_logits, cnn_loss, cnn_sgd_step
 
 
 class FashionMNISTModel(nn.Module):
@@ -26,6 +26,9 @@ class FashionMNISTModel(nn.Module):
             nn.Conv2d(hidden_units, hidden_units, 3, padding=1), nn.ReLU(),
             nn.MaxPool2d(2))
         self.classifier = nn.Sequential(nn.Flatten(), nn.Linear(hidden_units * 7 * 7, output_shape))
+        # fused-step tickets (CNN_GRP + 1 counters, re-armed by the kernel): per model, so two
+        # models never share them; not part of the state_dict (reference key parity)
+        self.register_buffer("_step_tick", torch.zeros(9, dtype=torch.int32), persistent=False)
 
     def param_list(self):
         c = [self.block_1[0], self.block_1[2], self.block_2[0], self.block_2[2], self.classifier[1]]
@@ -36,6 +39,27 @@ class FashionMNISTModel(nn.Module):
 
     def forward(self, x):
         return cnn_logits(x, self.param_list(), self.conv_dtype == "bf16")
+
+    def fused_sgd_step(self, opt, x, y):
+        """The whole single-executor training step (forward, CE, backward, batch gradient sum,
+        SGD update) as ONE HIP launch (csrc/kernels/cnn.hip, fused tail); returns the loss.  None
+        when it does not apply (CPU, data parallelism, an optimizer other than plain SGD, an odd
+        parameter count): the caller runs the usual forward / backward / step."""
+        from .. import _native
+        from ..optim.sgd import SGD
+        flat = getattr(opt, "flat", None)
+        params = self.param_list()
+        if (not x.is_cuda or not _native.use_native(x) or not isinstance(opt, SGD) or opt.momentum
+                or opt.weight_decay or opt.grad_scale != 1.0 or getattr(opt, "ranges", None) is not None
+                or flat is None or getattr(flat, "planes", None) is not None or x.dim() != 4
+                or not _native.C().cnn_fused_ok(params[0].shape[0], params[0].shape[1], params[8].shape[0])):
+            return None
+        shadows = None
+        if flat.shadow is not None:
+            offs = [flat.offsets[flat.index[id(p)]] for p in params]
+            shadows = [flat.shadow[o:o + p.numel()] for p, o in zip(params, offs)]
+        return cnn_sgd_step(x.contiguous(), y.to(torch.int64).contiguous(), params, opt.lr_t, opt.step_t,
+                            self._step_tick, shadows, self.conv_dtype == "bf16")
 
     def loss(self, x, y):
         """Mean CE over the batch (distributed_cnn.py:141,177)."""

@@ -109,3 +109,26 @@ def cnn_logits(x, params, bf16=False):
         return logits
     with torch.no_grad():
         return reference_logits(x, [p.float() for p in params])
+
+
+def cnn_sgd_step(x, y, params, lr_t, step_t, tick, shadows=None, bf16=False):
+    """The whole training step — forward, mean CE, backward, gradient reduction over the batch
+    and the SGD update — as ONE launch (csrc/kernels/cnn.hip, CNNArgs::fused): the per-image
+    slabs are summed in the kernel's ticketed tail, which then updates ``params`` in place
+    (p -= lr * g; ``lr_t`` / ``step_t`` are the optimizer's device scalars) and their bf16
+    ``shadows`` (10 tensors or None).  Returns the step's mean loss (device scalar).  ``tick``:
+    CNN_GRP + 1 zeroed int32 counters owned by the model (the kernel re-arms them)."""
+    B = x.shape[0]
+    w = [params[i] for i in (0, 2, 4, 6, 8)]
+    b = [params[i] for i in (1, 3, 5, 7, 9)]
+    P = num_params(params)
+    slab = torch.empty(B, P, device=x.device, dtype=torch.float32)
+    part = torch.empty((B + 7) // 8, P, device=x.device, dtype=torch.float32)
+    row_loss = torch.empty(B, device=x.device, dtype=torch.float32)
+    loss = torch.empty(1, device=x.device, dtype=torch.float32)
+    _native.C().cnn_sgd_step(x.data_ptr(), int(x.dtype == torch.uint8), 1.0 / 255.0, y.data_ptr(), B, x.shape[1],
+                             w[0].shape[0], w[4].shape[0], [t.data_ptr() for t in w], [t.data_ptr() for t in b],
+                             [t.data_ptr() for t in shadows] if shadows else [], slab.data_ptr(), part.data_ptr(),
+                             row_loss.data_ptr(), loss.data_ptr(), 1.0 / B, lr_t.data_ptr(), step_t.data_ptr(),
+                             tick.data_ptr(), int(bf16), _native.stream())
+    return loss[0]

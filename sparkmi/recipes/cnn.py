@@ -55,7 +55,7 @@ def train_fn(cfg):
     torch.manual_seed(cfg.seed)
     model = FashionMNISTModel(1, cfg.hidden_units, 10, dtype=cfg.conv_dtype)
     trainer = Trainer(model, lambda m, x, y: m.loss(x, y), lambda flat: SGD(flat, lr=cfg.lr), cfg, device, rank,
-                      world, "cnn", shadow=False)
+                      world, "cnn", shadow=False, fused_step=lambda m, o, x, y: m.fused_sgd_step(o, x, y))
     stats = trainer.fit(loader, cfg.epochs)
     trainer.close()
     out = dict(stats, data=source, world=world, train_samples_per_rank=len(idx))

@@ -143,3 +143,53 @@ def test_fused_cnn_gradients_bit_reproducible(dtype):
         out.append([p.grad.clone() for p in m.parameters()])
     for a, b in zip(*out):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,B", [("fp32", 32), ("bf16", 32), ("fp32", 20)])
+def test_fused_sgd_step_matches_unfused(dtype, B):
+    """The one-launch CNN step (fused slab reduction + SGD in the kernel's ticketed tail) follows
+    the three-launch path (kernel -> batch gradient reduce -> SGD kernel) step for step, keeps the
+    bf16 shadow in sync, is bit-reproducible, and replays identically inside a HIP graph
+    (StepRunner's single-executor fused_step path).  B = 20: a ragged last group of images."""
+    from sparkmi.optim import SGD
+    from sparkmi.train.runner import StepRunner
+    from sparkmi.utils.flat import FlatParams
+    g = torch.Generator().manual_seed(3)
+    xs = (torch.rand(6, B, 1, 28, 28, generator=g) * 255).to(torch.uint8).cuda()
+    ys = torch.randint(0, 10, (6, B), generator=g).cuda()
+
+    def run(mode):
+        torch.manual_seed(0)
+        m = FashionMNISTModel(1, 10, 10, dtype=dtype).cuda().train()
+        flat = FlatParams(m, shadow=True)
+        opt = SGD(flat, lr=0.05)
+        losses = []
+        if mode == "graph":
+            r = StepRunner(m, lambda mm, x, y: mm.loss(x, y), opt, graph=True, warmup_eager=2,
+                           fused_step=lambda mm, o, x, y: mm.fused_sgd_step(o, x, y))
+        for i in range(6):
+            if mode == "fused":
+                loss = m.fused_sgd_step(opt, xs[i], ys[i])
+                assert loss is not None
+            elif mode == "graph":
+                loss = r.step(xs[i], ys[i])
+            else:
+                loss = m.loss(xs[i], ys[i])
+                loss.backward()
+                opt.step()
+            losses.append(float(loss))
+        torch.cuda.synchronize()
+        return losses, flat.master.clone(), flat.shadow.clone(), float(opt.step_t.item())
+
+    lf, pf, sf, tf = run("fused")
+    lf2, pf2, _, _ = run("fused")
+    lg, pg, _, _ = run("graph")
+    lu, pu, _, tu = run("unfused")
+    assert lf == lf2 and torch.equal(pf, pf2)           # deterministic
+    assert lg == lf and torch.equal(pg, pf)             # graph replay == eager fused
+    assert torch.equal(sf, pf.to(torch.bfloat16))       # shadow refreshed
+    assert tf == tu == 6.0                              # step counter advanced per step
+    for a, b in zip(lf, lu):
+        assert abs(a - b) <= 1e-5 * abs(b) + 1e-6, (lf, lu)
+    torch.testing.assert_close(pf, pu, rtol=1e-5, atol=2e-6)
