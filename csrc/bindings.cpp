@@ -554,7 +554,8 @@ PYBIND11_MODULE(_C, m) {
                    u h0, u c0, u pred, u hn, u cn, u ws, u ws_da, u seedp, uint32_t salt, uint32_t thresh, float dscale,
                    u dpred, u dhn, u dcn, u g_emb, std::vector<u> g_w_ih, std::vector<u> g_w_hh, std::vector<u> g_b_ih,
                    std::vector<u> g_b_hh, u g_w_fc, u g_b_fc, u dh0, u dc0, u g_slab, u g_xe, long V, u emb_ws,
-                   u pred_last, int dpred_last, u st) {
+                   u pred_last, int dpred_last, u ce_labels, u ce_row, u ce_dlast, u ce_loss, u ce_tick,
+                   u dpred_scale, u st) {
     if (L < 1 || L > LSTM_MAXL || (int)w_ih.size() != L || (int)w_hh.size() != L || (int)b_ih.size() != L ||
         (int)b_hh.size() != L)
       throw std::runtime_error("lstm: need L pointers per weight list");
@@ -579,6 +580,10 @@ PYBIND11_MODULE(_C, m) {
     a.g_emb = (float*)g_emb; a.g_w_fc = (float*)g_w_fc; a.g_b_fc = (float*)g_b_fc; a.dh0 = (float*)dh0; a.dc0 = (float*)dc0;
     a.g_slab = (float*)g_slab; a.g_xe = (float*)g_xe; a.V = V; a.emb_ws = (void*)emb_ws;
     a.pred_last = (float*)pred_last; a.dpred_last = dpred_last;
+    a.ce_labels = (const long long*)ce_labels; a.ce_row = (float*)ce_row; a.ce_dlast = (float*)ce_dlast;
+    a.ce_loss = (float*)ce_loss; a.ce_tick = (unsigned*)ce_tick; a.dpred_scale = (const float*)dpred_scale;
+    if (a.ce_labels && (!a.ce_row || !a.ce_dlast || !a.ce_loss || !a.ce_tick || a.C > LSTM_MAXC))
+      throw std::runtime_error("lstm: fused CE needs row, dlast, loss and ticket buffers");
     chk(smi_lstm(&a, backward, S(st)), "lstm");
   });
 }

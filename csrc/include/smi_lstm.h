@@ -31,6 +31,11 @@ struct LSTMArgs {
   // sum_l 4H*(In_l + H + 1) + C*H + C), per-token embedding-input gradients [B][T][E]; V =
   // embedding rows (bucketed table backward)
   float* g_slab; float* g_xe; long V; void* emb_ws;  // emb_ws: smi_emb_det_ws_bytes(B*T, V)
+  // fused cross-entropy on the last step (forward; labels non-null): per-sequence loss, the head
+  // gradient dlast = (softmax - onehot) / B, and the mean loss through a last-workgroup ticket
+  // (ce_tick: one zeroed counter, re-armed by the kernel)
+  const long long* ce_labels; float* ce_row; float* ce_dlast; float* ce_loss; unsigned* ce_tick;
+  const float* dpred_scale;                // backward: dpred x this device scalar (the loss's dloss)
 };
 #define LSTM_MAXT 2048
 #define LSTM_TCH 64  // timesteps per LDS-staged chunk in the kernels' tail phases

@@ -58,6 +58,41 @@ __device__ __forceinline__ uint32_t lstm_drop_idx(int b, int t, int l, int j, in
   return (uint32_t)((((size_t)b * T + t) * L + l) * H + j);
 }
 
+// Fused CE on the last step's prediction (LSTMArgs::ce_labels; distributed_lstm.py:189
+// CrossEntropyLoss(pred[:, -1, :], labels - 1) with its mean): thread 0 of sequence b's workgroup
+// computes the row loss and the head gradient (softmax - onehot) / B from the logits in LDS; the
+// last workgroup to finish (ticket, release / acquire fences) sums the row losses in sequence
+// order.  Replaces three launches (CE forward, finalize, backward) per step.
+__device__ __noinline__ void lstm_ce_tail(const LSTMArgs& a, int b, const float* s_plast) {
+  __shared__ int s_lastwg;
+  __syncthreads();  // s_plast complete
+  if (threadIdx.x == 0) {
+    const int C = a.C;
+    float m = s_plast[0];
+    for (int c = 1; c < C; ++c) m = fmaxf(m, s_plast[c]);
+    float se = 0.f;
+    for (int c = 0; c < C; ++c) se += __expf(s_plast[c] - m);
+    const float lse = m + __logf(se);
+    const long long lab = a.ce_labels[b];
+    a.ce_row[b] = lse - s_plast[lab];
+    const float inv = 1.0f / (float)a.B;
+    for (int c = 0; c < C; ++c) a.ce_dlast[(size_t)b * C + c] = (__expf(s_plast[c] - lse) - (c == lab ? 1.f : 0.f)) * inv;
+    __threadfence();
+    s_lastwg = atomicAdd(a.ce_tick, 1u) == (unsigned)a.B - 1;
+  }
+  __syncthreads();
+  if (s_lastwg && threadIdx.x < 64) {
+    __threadfence();
+    float sum = 0.f;
+    for (int i = threadIdx.x; i < a.B; i += 64) sum += __hip_atomic_load(a.ce_row + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sum = wave_sum(sum);
+    if (threadIdx.x == 0) {
+      a.ce_loss[0] = sum / (float)a.B;
+      a.ce_tick[0] = 0u;
+    }
+  }
+}
+
 template <int H, int MI, int NT>  // hidden size, padded input width (>= E, >= H), block threads
 __global__ __launch_bounds__(NT) void lstm_fwd_kernel(LSTMArgs a) {
   constexpr int G = 4 * H;
@@ -154,6 +189,7 @@ __global__ __launch_bounds__(NT) void lstm_fwd_kernel(LSTMArgs a) {
   {
     __shared__ float s_top[LSTM_TCH * H];
     __shared__ float s_wfc[LSTM_MAXC * H];
+    __shared__ float s_plast[LSTM_MAXC];
     const float* top = wsb + (size_t)(L - 1) * T * 6 * H + 5 * H;
     for (int i = tid; i < C * H; i += blockDim.x) s_wfc[i] = a.w_fc[i];
     for (int t0 = 0; t0 < T; t0 += LSTM_TCH) {
@@ -171,8 +207,10 @@ __global__ __launch_bounds__(NT) void lstm_fwd_kernel(LSTMArgs a) {
         }
         a.pred[((size_t)b * T + t0 + t) * C + cc] = s0 + s1;
         if (a.pred_last && t0 + t == T - 1) a.pred_last[(size_t)b * C + cc] = s0 + s1;
+        if (t0 + t == T - 1) s_plast[cc] = s0 + s1;
       }
     }
+    if (a.ce_labels) lstm_ce_tail(a, b, s_plast);
   }
 }
 
@@ -232,6 +270,7 @@ __global__ __launch_bounds__(NT) void lstm_bwd_kernel(LSTMArgs a) {
   const float* wsb = a.ws + (size_t)b * L * T * 6 * H;
   // dpred_last: only the last step's head gradient exists ([B][C]; the loss reads pred[:, -1])
   const float* dpred = a.dpred + (size_t)b * (a.dpred_last ? 1 : T) * C;
+  const float dps = a.dpred_scale ? a.dpred_scale[0] : 1.f;
   float* dab = a.ws_da + (size_t)b * L * T * G;  // gate gradients of every layer [L][T][4H]
   const int nt = T + L - 1;
   const int tl = T - 1 + (L - 1 - l);  // this layer's step at tick k is tl - k
@@ -244,7 +283,7 @@ __global__ __launch_bounds__(NT) void lstm_bwd_kernel(LSTMArgs a) {
     if (top) {
 #pragma unroll
       for (int q = 0; q < CM; ++q)
-        v.dp[q] = (q < C && (!a.dpred_last || t == T - 1)) ? dpred[(size_t)(a.dpred_last ? 0 : t) * C + q] : 0.f;
+        v.dp[q] = (q < C && (!a.dpred_last || t == T - 1)) ? dpred[(size_t)(a.dpred_last ? 0 : t) * C + q] * dps : 0.f;
     }
   };
   // everything of step t's cell backward that does not depend on the incoming dh / dc
@@ -542,6 +581,7 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
   {
     __shared__ float s_top[LSTM_TCH * H];
     __shared__ float s_wfc[LSTM_MAXC * H];
+    __shared__ float s_plast[LSTM_MAXC];
     const float* top = wsb + (size_t)(L - 1) * T * 6 * H + 5 * H;
     for (int i = tid; i < C * H; i += blockDim.x) s_wfc[i] = a.w_fc[i];
     for (int t0 = 0; t0 < T; t0 += LSTM_TCH) {
@@ -559,8 +599,10 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
         }
         a.pred[((size_t)b * T + t0 + t) * C + cc] = s0 + s1;
         if (a.pred_last && t0 + t == T - 1) a.pred_last[(size_t)b * C + cc] = s0 + s1;
+        if (t0 + t == T - 1) s_plast[cc] = s0 + s1;
       }
     }
+    if (a.ce_labels) lstm_ce_tail(a, b, s_plast);
   }
 }
 
@@ -606,8 +648,9 @@ __global__ __launch_bounds__(128) void lstm_bwd_w2_kernel(LSTMArgs a) {
   const int tl = T - 1 + (L - 1 - l);
   const float c0v = (act && a.c0) ? a.c0[((size_t)l * a.B + b) * H + j] : 0.f;
   float dpl[CM];
+  const float dps = a.dpred_scale ? a.dpred_scale[0] : 1.f;
 #pragma unroll
-  for (int q = 0; q < CM; ++q) dpl[q] = (a.dpred_last && top && q < C) ? dpred[min(q, C - 1)] : 0.f;
+  for (int q = 0; q < CM; ++q) dpl[q] = (a.dpred_last && top && q < C) ? dpred[min(q, C - 1)] * dps : 0.f;
   // every lane loads every value at clamped indices (no branch around a load: the compiler can
   // then count vmcnt exactly instead of waiting for everything in flight)
   auto load_in = [&](int t, LstmBwdIn<CM>& v) {
@@ -622,7 +665,7 @@ __global__ __launch_bounds__(128) void lstm_bwd_w2_kernel(LSTMArgs a) {
     } else {
 #pragma unroll
       for (int q = 0; q < CM; ++q) {
-        const float d = dpred[(size_t)tc * C + min(q, C - 1)];
+        const float d = dpred[(size_t)tc * C + min(q, C - 1)] * dps;
         v.dp[q] = (top && q < C) ? d : 0.f;
       }
     }
@@ -786,6 +829,7 @@ __global__ __launch_bounds__(256) void lstm_wgrad_partial(LSTMArgs a) {
           if (l < L) v = a.ws_da[(((size_t)b * L + l) * T + t) * G + r0 + rr];
           else if (!a.dpred_last) v = a.dpred[((size_t)b * T + t) * C + r0 + rr];
           else v = t == T - 1 ? a.dpred[(size_t)b * C + r0 + rr] : 0.f;
+          if (l == L && a.dpred_scale) v *= a.dpred_scale[0];
         }
         s_d[kk][rr] = v;
       }
@@ -872,8 +916,9 @@ __device__ __forceinline__ float lw_d(const LSTMArgs& a, int l, long bt, int r, 
   if (r >= rows) return 0.f;
   const int b = (int)(bt / a.T), t = (int)(bt % a.T);
   if (l < a.L) return a.ws_da[(((size_t)b * a.L + l) * a.T + t) * 4 * a.H + r];
-  if (!a.dpred_last) return a.dpred[((size_t)b * a.T + t) * a.C + r];
-  return t == a.T - 1 ? a.dpred[(size_t)b * a.C + r] : 0.f;
+  const float ds = a.dpred_scale ? a.dpred_scale[0] : 1.f;
+  if (!a.dpred_last) return a.dpred[((size_t)b * a.T + t) * a.C + r] * ds;
+  return t == a.T - 1 ? a.dpred[(size_t)b * a.C + r] * ds : 0.f;
 }
 __device__ __forceinline__ float lw_x(const LSTMArgs& a, int l, long bt, int c, int cols, uint32_t seed) {
   if (c >= cols) return 0.f;

@@ -17,7 +17,7 @@ import torch
 from torch import nn
 
 from ..ops import rng as _rng
-from ..ops.lstm import lstm_classifier, lstm_classifier_last
+from ..ops.lstm import lstm_classifier, lstm_classifier_ce, lstm_classifier_last
 from ..ops.loss import cross_entropy
 
 
@@ -53,6 +53,12 @@ class LSTM(nn.Module):
 
     def loss(self, input_seq, labels, hidden_in=None, mem_in=None):
         """CE on the last step's prediction (distributed_lstm.py:186-189); returns (loss, pred)."""
+        if input_seq.is_cuda and labels.dim() == 1:
+            # GPU: the CE of the last step is fused into the LSTM forward kernel's tail (row loss,
+            # head gradient, fixed-order mean through a ticket): no separate CE launches
+            return lstm_classifier_ce(input_seq, labels, hidden_in, mem_in, self.param_list(), self.num_layers,
+                                      dropout=self.dropout_p, training=self.training, rng=self.rng, salt=self.salt,
+                                      padding_idx=self.padding_idx)
         last, _, _, _ = lstm_classifier_last(input_seq, hidden_in, mem_in, self.param_list(), self.num_layers,
                                              dropout=self.dropout_p, training=self.training, rng=self.rng,
                                              salt=self.salt, padding_idx=self.padding_idx)

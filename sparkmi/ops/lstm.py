@@ -61,6 +61,11 @@ def supported(E, H, L, C):
 class LSTMFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ids, h0, c0, meta, *params):
+        return LSTMFn._forward(ctx, ids, h0, c0, meta, params, None)
+
+    @staticmethod
+    def _forward(ctx, ids, h0, c0, meta, params, labels):
+        """The forward launch; ``labels``: also the fused last-step CE (returns its extra outputs)."""
         ctx.set_materialize_grads(False)  # unused outputs get no zero-filled gradients
         L, p, rng, salt, pad_idx = meta
         emb, layers, w_fc, b_fc = unpack(params, L)
@@ -78,20 +83,35 @@ class LSTMFn(torch.autograd.Function):
         h0c = h0.float().contiguous() if h0 is not None else None
         c0c = c0.float().contiguous() if c0 is not None else None
         thresh = _rng.threshold(p)
+        ce = None
+        if labels is not None:
+            labels = labels.to(torch.int64).contiguous()
+            ce = (torch.empty(B, device=dev, dtype=torch.float32), torch.empty(B, C, device=dev, dtype=torch.float32),
+                  torch.empty((), device=dev, dtype=torch.float32), _ce_ticket(dev))
         _native.C().lstm(0, ids.data_ptr(), B, T, E, H, L, C, pad_idx, emb.data_ptr(),
                          [lw[0].data_ptr() for lw in layers], [lw[1].data_ptr() for lw in layers],
                          [lw[2].data_ptr() for lw in layers], [lw[3].data_ptr() for lw in layers],
                          w_fc.data_ptr(), b_fc.data_ptr(), _native.ptr(h0c), _native.ptr(c0c), pred.data_ptr(),
                          hn.data_ptr(), cn.data_ptr(), ws.data_ptr(), 0, rng.ptr() if rng is not None else 0, salt,
                          thresh, _rng.scale(p), 0, 0, 0, 0, [], [], [], [], 0, 0, 0, 0, 0, 0, 0, 0,
-                         last.data_ptr(), 0, _native.stream())
+                         last.data_ptr(), 0, labels.data_ptr() if ce else 0, ce[0].data_ptr() if ce else 0,
+                         ce[1].data_ptr() if ce else 0, ce[2].data_ptr() if ce else 0, ce[3].data_ptr() if ce else 0,
+                         0, _native.stream())
         ctx.meta = (L, p, rng, salt, pad_idx, B, T, E, H, C)
         ctx.has_h0, ctx.has_c0 = h0 is not None, c0 is not None
         ctx.save_for_backward(ids, ws, h0c, c0c, *params)
+        if ce is not None:
+            ctx.ce_dlast = ce[1]
+            return ce[2], last
         return pred, hn, cn, last
 
     @staticmethod
     def backward(ctx, dpred, dhn, dcn, dlast):
+        return LSTMFn._backward(ctx, dpred, dhn, dcn, dlast, None)
+
+    @staticmethod
+    def _backward(ctx, dpred, dhn, dcn, dlast, dscale):
+        """dscale: a device scalar the kernels multiply dpred by (the fused CE's dloss), or None."""
         L, p, rng, salt, pad_idx, B, T, E, H, C = ctx.meta
         ids, ws, h0c, c0c, *params = ctx.saved_tensors
         emb, layers, w_fc, b_fc = unpack(params, L)
@@ -111,8 +131,9 @@ class LSTMFn(torch.autograd.Function):
         dhn = dhn.float().contiguous() if dhn is not None else None
         dcn = dcn.float().contiguous() if dcn is not None else None
         ws_da = torch.empty(B, L, T, 4 * H, device=dev, dtype=torch.float32)
-        dh0 = torch.empty(L, B, H, device=dev) if ctx.needs_input_grad[1] else None
-        dc0 = torch.empty(L, B, H, device=dev) if ctx.needs_input_grad[2] else None
+        i0 = getattr(ctx, "h0_input", 1)  # position of h0 among the Function's inputs
+        dh0 = torch.empty(L, B, H, device=dev) if ctx.needs_input_grad[i0] else None
+        dc0 = torch.empty(L, B, H, device=dev) if ctx.needs_input_grad[i0 + 1] else None
         orig = params
         g = [grad_buf(t) for t in orig]
         g_emb, g_layers, g_fc, g_bfc = unpack(g, L)
@@ -131,9 +152,57 @@ class LSTMFn(torch.autograd.Function):
                          [lw[0].data_ptr() for lw in g_layers], [lw[1].data_ptr() for lw in g_layers],
                          [lw[2].data_ptr() for lw in g_layers], [lw[3].data_ptr() for lw in g_layers],
                          g_fc.data_ptr(), g_bfc.data_ptr(), _native.ptr(dh0), _native.ptr(dc0), slab.data_ptr(),
-                         _native.ptr(xe), emb.shape[0], _native.ptr(ews), 0, last_only, _native.stream())
+                         _native.ptr(xe), emb.shape[0], _native.ptr(ews), 0, last_only, 0, 0, 0, 0, 0,
+                         _native.ptr(dscale), _native.stream())
         grad_ready(*orig)
         return (None, dh0 if ctx.has_h0 else None, dc0 if ctx.has_c0 else None, None) + (None,) * len(params)
+
+
+_CE_TICKETS = {}
+
+
+def _ce_ticket(dev):
+    """The fused CE's ticket counter (zeroed once, re-armed by the kernel); one per device — a
+    step's forward completes its ticket round before the next forward on the stream starts."""
+    t = _CE_TICKETS.get(dev)
+    if t is None:
+        t = _CE_TICKETS[dev] = torch.zeros(1, device=dev, dtype=torch.int32)
+    return t
+
+
+class LSTMCEFn(torch.autograd.Function):
+    """The LSTM classifier with the mean cross-entropy of its last step fused into the forward
+    kernel's tail (csrc/kernels/lstm.hip lstm_ce_tail): returns (loss, pred[:, -1]); the backward
+    feeds the precomputed head gradient (softmax - onehot) / B, times dloss, to the BPTT kernel."""
+
+    @staticmethod
+    def forward(ctx, ids, labels, h0, c0, meta, *params):
+        ctx.h0_input = 2
+        loss, last = LSTMFn._forward(ctx, ids, h0, c0, meta, params, labels)
+        ctx.mark_non_differentiable(last)
+        return loss, last
+
+    @staticmethod
+    def backward(ctx, dloss, dlast_unused):
+        if dloss is None:
+            return (None,) * (5 + len(ctx.saved_tensors) - 4)
+        ds = dloss.reshape(1).float().contiguous()
+        grads = LSTMFn._backward(ctx, None, None, None, ctx.ce_dlast, ds)
+        return (None, None) + grads[1:3] + (None,) + grads[4:]
+
+
+def lstm_classifier_ce(ids, labels, h0, c0, params, num_layers, dropout=0.0, training=True, rng=None, salt=0,
+                       padding_idx=None):
+    """(mean CE of pred[:, -1] against ``labels``, pred[:, -1]) — the classifier's training loss
+    (distributed_lstm.py:186-189) with the CE fused into the GPU kernel; CPU: torch reference."""
+    p = dropout if training else 0.0
+    emb, layers, w_fc, _ = unpack(params, num_layers)
+    E, H, C = emb.shape[1], layers[0][1].shape[1], w_fc.shape[0]
+    if ids.is_cuda and _native.use_native(ids) and supported(E, H, num_layers, C):
+        pad = -1 if padding_idx is None else int(padding_idx)
+        return LSTMCEFn.apply(ids, labels, h0, c0, (num_layers, p, rng, salt, pad), *params)
+    last, _, _, _ = lstm_classifier_last(ids, h0, c0, params, num_layers, dropout, training, rng, salt, padding_idx)
+    return torch.nn.functional.cross_entropy(last, labels), last
 
 
 def lstm_classifier(ids, h0, c0, params, num_layers, dropout=0.0, training=True, rng=None, salt=0,

@@ -72,6 +72,18 @@ class FlatParams:
             if device.type == "cuda" and p.dim() == 2:
                 p._smi_planes_fn = self._planes_fn(p, o)
         object.__setattr__(module, "_smi_flat", self)  # checkpoint loads refresh the bf16 shadow
+        # module.load_state_dict writes the master through p.data: re-derive the bf16 shadow and
+        # the weight planes the fp32 GEMMs read.  Other in-place weight edits
+        # (nn.init, p.data.copy_) must call refresh_shadow() themselves.
+        import weakref
+        ref = weakref.ref(self)
+
+        def _refresh_after_load(mod, incompatible):
+            f = ref()
+            if f is not None and getattr(mod, "_smi_flat", None) is f:
+                f.refresh_shadow()
+
+        self._load_hook = module.register_load_state_dict_post_hook(_refresh_after_load)
         self.refresh_shadow()
 
     def _planes_fn(self, p, o):

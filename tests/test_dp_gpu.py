@@ -189,3 +189,73 @@ def test_transformer_dp_parity_grid_world4():
     assert (a["adam_zero_eager"] - a["adam_eager"]).abs().max() < 5 * 1e-3 * 4
     assert (a["adam_zero_split"] - a["adam_split"]).abs().max() < 5 * 1e-3 * 4
     assert (a["adam_eager"] - r1["adam_eager"]).abs().max() < 5 * 1e-3 * 4
+
+
+# ---- small models over the IPC kernels: the whole-step graph and the two-shot path ----
+def _small_dp(kind, steps, graph):
+    import torch
+    from sparkmi.models.lstm import LSTM
+    from sparkmi.models.mlp import MultilayerPerceptron
+    from sparkmi.optim import SGD
+    from sparkmi.parallel import DataParallel, init_distributed
+    from sparkmi.train.runner import StepRunner
+    from sparkmi.utils.flat import FlatParams
+    rank, world, device = init_distributed()
+    torch.manual_seed(0)
+    g = torch.Generator().manual_seed(5)
+    GB = 8  # global batch
+    if kind == "mlp":
+        m = MultilayerPerceptron((4, 5, 4, 3)).to(device)
+        xs = torch.randn(steps, GB, 4, generator=g).to(device)
+        ys = torch.randint(0, 3, (steps, GB), generator=g).to(device)
+        loss_fn = lambda mm, x, y: mm.loss(x, y)  # noqa: E731
+    else:
+        # 5000 x 32 embedding: a 640 KB gradient bucket (two-shot at 4 ranks, auto-selected)
+        m = LSTM(5000, 32, 32, 4, num_layers=2, dropout=0.0).to(device)
+        xs = torch.randint(4, 5000, (steps, GB, 24), generator=g).to(device)
+        ys = torch.randint(0, 4, (steps, GB), generator=g).to(device)
+        loss_fn = lambda mm, x, y: mm.loss(x, y)[0]  # noqa: E731
+    flat = FlatParams(m, shadow=False)
+    opt = SGD(flat, lr=0.1)
+    ddp = DataParallel(flat, bucket_mb=64.0) if world > 1 else None
+    info = None
+    if ddp is not None:
+        assert ddp.ipc is not None, "small gradients take the IPC kernels in auto mode"
+        n = max(e - s for s, e, _ in ddp.buckets)
+        info = ddp.ipc.algo_for(n)
+    runner = StepRunner(m, loss_fn, opt, ddp, graph=graph, warmup_eager=2)
+    per = GB // world
+    for i in range(steps):
+        runner.step(xs[i, rank * per:(rank + 1) * per].contiguous(), ys[i, rank * per:(rank + 1) * per].contiguous())
+    torch.cuda.synchronize()
+    if ddp is not None:
+        ddp.check()
+        ddp.close()
+    return flat.master.cpu().clone(), info
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_mlp_ipc_whole_step_graph_matches_single_process():
+    """MLP data parallelism with the WHOLE step (forward, backward, IPC all-reduce, SGD) as one
+    HIP graph == one process at twice the batch (restored from round 2)."""
+    env = {"SPARKMI_DIST_BACKEND": "gloo"}
+    p2, algo = launch(_small_dp, ("mlp", 8, True), {}, num_processes=2, use_gpu=True, env=env, log_sink=None,
+                      timeout=280)
+    p1, _ = launch(_small_dp, ("mlp", 8, False), {}, num_processes=1, use_gpu=True, env=env, log_sink=None, timeout=280)
+    assert algo == 1
+    torch.testing.assert_close(p2, p1, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_lstm_dp_auto_two_shot_matches_single_process():
+    """A 640 KB LSTM gradient at 4 ranks: auto mode picks the IPC TWO-shot kernel; 4 ranks x batch
+    2 == one process x batch 8 (graph-captured steps)."""
+    env = {"SPARKMI_DIST_BACKEND": "gloo"}
+    p4, algo = launch(_small_dp, ("lstm", 5, True), {}, num_processes=4, use_gpu=True, env=env, log_sink=None,
+                      timeout=380)
+    p1, _ = launch(_small_dp, ("lstm", 5, False), {}, num_processes=1, use_gpu=True, env=env, log_sink=None,
+                   timeout=380)
+    assert algo == 2
+    torch.testing.assert_close(p4, p1, rtol=1e-4, atol=1e-5)

@@ -75,3 +75,20 @@ def test_cpu_training_unchanged_by_grouping():
     assert torch.equal(la, lb)
     for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
         torch.testing.assert_close(pa.grad, pb.grad, rtol=0, atol=0, msg=n)
+
+
+def test_load_state_dict_refreshes_shadow_and_planes():
+    """a direct module.load_state_dict (not through the checkpoint manager) re-derives
+    the bf16 shadow and the fp32 GEMMs' weight planes from the new master weights."""
+    import torch
+    from sparkmi.utils.flat import FlatParams
+    torch.manual_seed(0)
+    m = torch.nn.Linear(16, 8)
+    flat = FlatParams(m, device="cpu", shadow=True)
+    flat.ensure_planes()
+    sd = {k: torch.randn_like(v) for k, v in m.state_dict().items()}
+    m.load_state_dict(sd)
+    assert torch.equal(m.weight.detach(), sd["weight"])
+    assert torch.equal(flat.shadow, flat.master.to(torch.bfloat16))
+    p = flat.planes
+    assert torch.equal(p[0].float() + p[1].float() + p[2].float(), flat.master)

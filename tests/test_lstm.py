@@ -106,3 +106,38 @@ def test_lstm_gradients_bit_reproducible():
         out.append(_grads(m))
     for a, b in zip(*out):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("L,H,B", [(2, 32, 32), (3, 16, 7)])
+def test_lstm_fused_ce_matches_reference(L, H, B):
+    """LSTM.loss on the GPU: the last step's mean CE fused into the forward kernel's tail (row
+    loss, head gradient, ticketed fixed-order mean), the backward scaled by dloss — against the
+    torch reference (reference_forward + F.cross_entropy); a scaled loss scales every gradient;
+    the fused path is bit-reproducible."""
+    torch.manual_seed(4)
+    V, C, T, pad = 61, 4, 33, 3
+    m = LSTM(V, H, H, C, num_layers=L, padding_idx=pad, dropout=0.3).cuda().train()
+    ids = torch.randint(0, V, (B, T), device="cuda")
+    y = torch.randint(0, C, (B,), device="cuda")
+    params = m.param_list()
+    seed = m.rng.current()
+    loss, last = m.loss(ids, y)
+    (2.5 * loss).backward()
+    gk = _grads(m)
+    for q in params:
+        q.grad = None
+    pr, _, _ = LS.reference_forward(ids, None, None, params, L, 0.3, seed, m.salt, pad)
+    ref = torch.nn.functional.cross_entropy(pr[:, -1], y)
+    (2.5 * ref).backward()
+    assert abs(float(loss) - float(ref)) <= 1e-5 * abs(float(ref)) + 1e-6
+    torch.testing.assert_close(last, pr[:, -1].detach(), rtol=1e-4, atol=1e-4)
+    for a, b in zip(gk, _grads(m)):
+        torch.testing.assert_close(a, b, rtol=2e-3, atol=2e-4)
+    for q in params:
+        q.grad = None
+    loss2, _ = m.loss(ids, y)
+    (2.5 * loss2).backward()
+    assert float(loss2) == float(loss)
+    for a, b in zip(gk, _grads(m)):
+        assert torch.equal(a, b)
