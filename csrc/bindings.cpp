@@ -94,6 +94,7 @@ int smi_gemm_wgrad_group(const void* const*, const long*, const void* const*, co
                          const int*, const int*, const int*, int, hipStream_t);
 int smi_cnn(const CNNArgs*, hipStream_t);
 int smi_cnn_fused_ok(int, int, int);
+int smi_emb_pair(int);
 int smi_cnn_reduce(const CNNArgs*, hipStream_t);
 int smi_gather_rows(const void*, const long long*, void*, long, long, hipStream_t);
 int smi_gather_u8_scale(const void*, const long long*, void*, long, long, float, int, hipStream_t);
@@ -543,6 +544,8 @@ PYBIND11_MODULE(_C, m) {
     a.lr = (const float*)lr; a.step = (float*)step; a.tick = (unsigned*)tick;
     chk(smi_cnn(&a, S(st)), "cnn_sgd_step");
   });
+  m.def("emb_pair", [](int set) { return smi_emb_pair(set); },
+        "deterministic embedding backward: 1 = pair-compare (<= 8192 tokens), 0 = bucketed lists; -1 queries");
   m.def("cnn_fused_ok", [](int C, int cin, int classes) { return smi_cnn_fused_ok(C, cin, classes) != 0; });
 
   m.def("lstm_supported", [](int E, int H, int L, int C) { return smi_lstm_supported(E, H, L, C) != 0; });

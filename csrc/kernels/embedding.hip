@@ -398,6 +398,180 @@ __global__ __launch_bounds__(256) void emb_det_combine(float* __restrict__ dtabl
   }
 }
 
+// ---- pair-compare backward for batches of up to EMB_PAIR_MAX tokens (3 launches) --------------
+// The bucketed path above spends 5-6 launches (and a scan over every bucket of the vocabulary) on
+// the ordering; for a step's few thousand tokens the ordering is cheaper as an all-pairs id
+// comparison spread over the chip:
+//  1. emb_pair_rank (one 1024-thread workgroup per 64 tokens, its 16 waves splitting the earlier
+//     positions): for every token p, rank = # earlier tokens with its id and first = the id's first
+//     position (-1: padding token, no gradient) — exact integer results, no atomics;
+//  2. emb_pair_plan (one workgroup, all tokens in LDS): group sizes per first position (LDS integer
+//     adds: order-independent), exclusive scans, member lists in position order
+//     (list[off[first] + rank] = p), and chunks of at most EMB_CH members per group;
+//  3. emb_pair_sum (one workgroup per chunk): the chunk's member rows summed in position order;
+//     a one-chunk group adds its sum to its table row, a longer group's chunks write partials and
+//     the group's last chunk to finish (ticket) adds them in chunk order.
+// Every table row is one fixed-order fp32 sum: bit-reproducible, and long groups (a frequent word)
+// are spread over several workgroups.
+#define EMB_PAIR_MAX 8192
+#define EMB_CH 32
+struct EmbPair {
+  int* rank; int* first; int* list;
+  int* ch_owner; int* ch_start; int* ch_len; int* ch_g0; int* ch_gn;  // per chunk
+  unsigned* tick;   // per group (indexed by its first chunk), zeroed by emb_pair_plan
+  int* nchunks;
+  float* part;      // [T][D] chunk partials of multi-chunk groups
+};
+
+__global__ __launch_bounds__(1024) void emb_pair_rank(const long long* __restrict__ ids, long T, long long pad, EmbPair e) {
+  __shared__ __attribute__((aligned(16))) int s_id[EMB_PAIR_MAX];
+  __shared__ int s_cnt[16][64], s_min[16][64];
+  const int p0 = blockIdx.x * 64;
+  const int n = (int)min((long)p0 + 64, T);  // positions 0 .. n - 1 compared
+  const int n4 = (n + 3) & ~3;
+  for (int i = threadIdx.x; i < n4; i += 1024) s_id[i] = i < n ? (int)ids[i] : -2;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int p = p0 + lane;
+  const int myid = p < n ? s_id[p] : -3;
+  const bool live = p < n && (long long)myid != pad && myid >= 0;
+  const int per = ((n4 / 4 + 15) / 16) * 4;  // positions per wave (multiple of 4)
+  const int q0 = w * per, q1 = min(q0 + per, n4);
+  int cnt = 0, fmin = p;
+  for (int q = q0; q < q1; q += 4) {
+    const int4 v = *(const int4*)(s_id + q);  // same address on every lane: a broadcast read
+    const int vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool eq = vv[k] == myid && q + k < p;
+      cnt += eq ? 1 : 0;
+      fmin = eq ? min(fmin, q + k) : fmin;
+    }
+  }
+  s_cnt[w][lane] = cnt;
+  s_min[w][lane] = fmin;
+  __syncthreads();
+  if (threadIdx.x < 64 && p < T) {
+    int c = 0, f = p;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { c += s_cnt[k][lane]; f = min(f, s_min[k][lane]); }
+    e.rank[p] = c;
+    e.first[p] = live ? f : -1;
+  }
+}
+
+__global__ __launch_bounds__(1024) void emb_pair_plan(long T, EmbPair e) {
+  __shared__ int s_f[EMB_PAIR_MAX], s_off[EMB_PAIR_MAX], s_coff[EMB_PAIR_MAX];
+  __shared__ int s_wsum[2][16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n = (int)T;
+  for (int i = tid; i < n; i += 1024) { s_f[i] = e.first[i]; s_off[i] = 0; }
+  __syncthreads();
+  for (int i = tid; i < n; i += 1024)
+    if (s_f[i] >= 0) atomicAdd(&s_off[s_f[i]], 1);  // group sizes (integer adds: order-free)
+  __syncthreads();
+  // chunks per group, then exclusive scans of sizes and chunk counts over the positions: thread
+  // tid owns the contiguous range [tid * per, ...) — serial inside, wave / block prefix outside
+  const int per = (n + 1023) / 1024, a0 = min(n, tid * per), a1 = min(n, a0 + per);
+  int ssum = 0, csum = 0;
+  for (int i = a0; i < a1; ++i) {
+    const int c = s_off[i];
+    s_coff[i] = (c + EMB_CH - 1) / EMB_CH;
+    ssum += c;
+    csum += s_coff[i];
+  }
+  int sx = ssum, cx = csum;  // inclusive wave scans
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int ys = __shfl_up(sx, d, 64), yc = __shfl_up(cx, d, 64);
+    if (lane >= d) { sx += ys; cx += yc; }
+  }
+  if (lane == 63) { s_wsum[0][w] = sx; s_wsum[1][w] = cx; }
+  __syncthreads();
+  int sb = 0, cb = 0;
+  for (int k = 0; k < w; ++k) { sb += s_wsum[0][k]; cb += s_wsum[1][k]; }
+  int so = sb + sx - ssum, co = cb + cx - csum;  // exclusive prefix of this thread's range
+  for (int i = a0; i < a1; ++i) {
+    const int c = s_off[i], nc = s_coff[i];
+    s_off[i] = so;
+    s_coff[i] = co;
+    // chunk table of the group first at position i
+    for (int k = 0; k < nc; ++k) {
+      e.ch_owner[co + k] = i;
+      e.ch_start[co + k] = so + k * EMB_CH;
+      e.ch_len[co + k] = min(EMB_CH, c - k * EMB_CH);
+      e.ch_g0[co + k] = co;
+      e.ch_gn[co + k] = nc;
+      e.tick[co + k] = 0u;
+    }
+    so += c;
+    co += nc;
+  }
+  if (tid == 1023) *e.nchunks = co;
+  __syncthreads();
+  for (int i = tid; i < n; i += 1024)
+    if (s_f[i] >= 0) e.list[s_off[s_f[i]] + e.rank[i]] = i;  // position order within the group
+}
+
+template <typename TS>
+__global__ __launch_bounds__(128) void emb_pair_sum(const long long* __restrict__ ids, const TS* __restrict__ dout,
+                                                    float* __restrict__ dtable, int D, EmbPair e,
+                                                    const uint32_t* seedp, uint32_t salt, uint32_t thresh,
+                                                    float dscale) {
+  const int k = blockIdx.x;
+  if (k >= *e.nchunks) return;
+  __shared__ int s_mem[EMB_CH];
+  __shared__ int s_last;
+  const int start = e.ch_start[k], len = e.ch_len[k], g0 = e.ch_g0[k], gn = e.ch_gn[k];
+  if (threadIdx.x < len) s_mem[threadIdx.x] = e.list[start + threadIdx.x];
+  __syncthreads();
+  const long long id = ids[e.ch_owner[k]];
+  const uint32_t seed = thresh ? smi_seed(seedp, salt) : 0u;
+  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+    float acc = 0.f;
+    int m = 0;
+    for (; m + 4 <= len; m += 4) {  // four rows in flight, added in position order
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long t = s_mem[m + u];
+        v[u] = emb_ld(dout + t * D + c);
+        if (thresh) v[u] = smi_keep(seed, (uint32_t)(t * D + c), thresh) ? v[u] * dscale : 0.f;
+      }
+      acc += v[0];
+      acc += v[1];
+      acc += v[2];
+      acc += v[3];
+    }
+    for (; m < len; ++m) {
+      const long t = s_mem[m];
+      float v = emb_ld(dout + t * D + c);
+      if (thresh) v = smi_keep(seed, (uint32_t)(t * D + c), thresh) ? v * dscale : 0.f;
+      acc += v;
+    }
+    if (gn == 1) dtable[id * D + c] += acc;
+    else e.part[(long)k * D + c] = acc;
+  }
+  if (gn == 1) return;
+  __threadfence();  // release every thread's partial
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(e.tick + g0, 1u) == (unsigned)gn - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+    float acc = 0.f;
+    for (int j = 0; j < gn; ++j) acc += __hip_atomic_load(e.part + (long)(g0 + j) * D + c, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+    dtable[id * D + c] += acc;
+  }
+  if (threadIdx.x == 0) e.tick[g0] = 0u;
+}
+
+static long emb_pair_ws_bytes(long T, long D) {
+  return 4 * (9 * T + 4) + 4 * T * D + 64;
+}
+
 static int emb_det_nb(long V) {
   int NB = 1;
   while ((V + NB - 1) / NB > EMB_SLOTS) NB *= 2;
@@ -412,13 +586,47 @@ static long emb_det_ints(long T, long NB, long hmax) {
 }
 extern "C" long smi_emb_det_ws_bytes(long T, long V, long D) {
   const long hmax = T / EMB_HEAVY;
-  return 4 * emb_det_ints(T, emb_det_nb(V), hmax) + 4 * hmax * EMB_SPLIT * EMB_SLOTS * D + 64;
+  const long det = 4 * emb_det_ints(T, emb_det_nb(V), hmax) + 4 * hmax * EMB_SPLIT * EMB_SLOTS * D + 64;
+  const long pair = T <= EMB_PAIR_MAX ? emb_pair_ws_bytes(T, D) : 0;
+  return det > pair ? det : pair;
+}
+
+// deterministic backward algorithm: 1 = pair-compare (<= EMB_PAIR_MAX tokens, default), 0 = the
+// bucketed lists (SMI_EMB_BWD=det)
+static int g_emb_pair = -1;
+extern "C" int smi_emb_pair(int set) {
+  if (set == 0 || set == 1) g_emb_pair = set;
+  if (g_emb_pair < 0) {
+    const char* ev = getenv("SMI_EMB_BWD");
+    g_emb_pair = (ev && ev[0] == 'd') ? 0 : 1;
+  }
+  return g_emb_pair;
 }
 
 template <typename TS>
 static int emb_bwd_launch(const long long* ids, const void* dout, float* dtable, long T, int D, long long padding_idx,
                           const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, long V, void* ws,
                           hipStream_t st) {
+  if (ws && V > 0 && T > 0 && T <= EMB_PAIR_MAX && smi_emb_pair(-1)) {
+    EmbPair e{};
+    int* p = (int*)ws;
+    e.rank = p; p += T;
+    e.first = p; p += T;
+    e.list = p; p += T;
+    e.ch_owner = p; p += T;
+    e.ch_start = p; p += T;
+    e.ch_len = p; p += T;
+    e.ch_g0 = p; p += T;
+    e.ch_gn = p; p += T;
+    e.tick = (unsigned*)p; p += T;
+    e.nchunks = p; p += 4;
+    e.part = (float*)p;
+    hipLaunchKernelGGL(emb_pair_rank, dim3((unsigned)((T + 63) / 64)), dim3(1024), 0, st, ids, T, padding_idx, e);
+    hipLaunchKernelGGL(emb_pair_plan, dim3(1), dim3(1024), 0, st, T, e);
+    hipLaunchKernelGGL(emb_pair_sum<TS>, dim3((unsigned)T), dim3(128), 0, st, ids, (const TS*)dout, dtable, D, e, seedp,
+                       salt, thresh, dscale);
+    return (int)hipGetLastError();
+  }
   if (ws && V > 0 && T > 0) {
     EmbDet d{};
     d.tiles = (int)((T + EMB_TILE - 1) / EMB_TILE);

@@ -331,3 +331,34 @@ def test_ffn_fused():
                     (g2.bias, l2.bias, "b2")):
         rel = (a.grad.cpu() - b.grad).norm() / b.grad.norm()
         assert rel < 2e-2, (n, float(rel))
+
+
+@pytest.mark.parametrize("T,V,D,pad", [(4128, 95812, 32, 0), (8192, 10000, 512, 3), (8192, 50, 96, None)])
+def test_embedding_backward_pair_vs_bucketed(T, V, D, pad):
+    """The 3-launch pair-compare backward (<= 8192 tokens: the LSTM's 32 x 129 and the
+    transformer's 32 x 256 batches) against the bucketed-list one: equal to fp32 rounding, both
+    bit-reproducible, padding rows untouched; V = 50: groups of ~160 tokens (5 chunks each)."""
+    torch.manual_seed(6)
+    C = _native.C()
+    ids = torch.randint(0, V, (T,))
+    ids[: T // 4] = pad if pad is not None else 1
+    do = torch.randn(T, D, device=dev)
+    prev = C.emb_pair(-1)
+    out = {}
+    try:
+        for algo in (1, 0):
+            C.emb_pair(algo)
+            gs = []
+            for _ in range(2):
+                w = torch.nn.Parameter(torch.zeros(V, D, device=dev))
+                o = embedding(ids.to(dev), w, None, 0.1, R.DropoutRNG(2).to(dev), 9, padding_idx=pad,
+                              out_dtype=torch.float32)
+                o.backward(do)
+                gs.append(w.grad.clone())
+            assert torch.equal(gs[0], gs[1]), algo
+            out[algo] = gs[0]
+    finally:
+        C.emb_pair(prev)
+    _close(out[1], out[0], 1e-5, 1e-5, "pair vs bucketed")
+    if pad is not None:
+        assert float(out[1][pad].abs().sum()) == 0.0
