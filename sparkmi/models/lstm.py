@@ -23,7 +23,7 @@ from ..ops.loss import cross_entropy
 
 class LSTM(nn.Module):
     def __init__(self, vocab_size, embedding_dim, hidden_size, output_size, num_layers=2, padding_idx=None,
-                 dropout=0.5, seed=0):
+                 dropout=0.5, seed=0, salt_base=1):
         super().__init__()
         self.embedding = nn.Embedding(num_embeddings=vocab_size, embedding_dim=hidden_size, padding_idx=padding_idx)
         self.lstm = nn.LSTM(input_size=embedding_dim, hidden_size=hidden_size, num_layers=num_layers,
@@ -32,7 +32,8 @@ class LSTM(nn.Module):
         self.num_layers, self.hidden_size, self.dropout_p = num_layers, hidden_size, dropout
         self.padding_idx = padding_idx
         self.rng = _rng.DropoutRNG(seed)
-        self.salt = _rng.new_salt()
+        with _rng.salt_scope(salt_base):  # the model's own salt stream: masks independent of other models
+            self.salt = _rng.new_salt()
 
     def param_list(self):
         ps = [self.embedding.weight]

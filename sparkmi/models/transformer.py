@@ -34,7 +34,7 @@ from ..ops._grad import SharedGrad
 from ..ops.linear import concat_linear, ffn
 from ..ops import planes as _pl
 from ..ops.loss import cross_entropy
-from ..ops.rng import new_salt
+from ..ops.rng import new_salt, salt_scope
 
 
 def get_device():
@@ -303,7 +303,7 @@ class Transformer(nn.Module):
 
     def __init__(self, d_model=512, ffn_hidden=1024, num_heads=8, drop_prob=0.1, num_layers=1,
                  max_sequence_length=200, de_vocab_size=10000, src_vocab_size=None, tgt_vocab_size=None,
-                 mask_mode="reference", emb_dropout=0.1, pad_id=0, seed=0, dtype="bf16"):
+                 mask_mode="reference", emb_dropout=0.1, pad_id=0, seed=0, dtype="bf16", salt_base=1):
         super().__init__()
         if dtype not in ("bf16", "fp32"):
             raise ValueError(f"dtype must be 'bf16' or 'fp32', got {dtype!r}")
@@ -312,10 +312,11 @@ class Transformer(nn.Module):
         self.config = TransformerConfig(d_model, ffn_hidden, num_heads, drop_prob, num_layers, max_sequence_length,
                                         src_vocab_size, tgt_vocab_size, emb_dropout, mask_mode, pad_id, dtype)
         self.rng = DropoutRNG(seed)
-        self.encoder = Encoder(d_model, ffn_hidden, num_heads, drop_prob, num_layers, max_sequence_length,
-                               src_vocab_size, self.rng, emb_dropout, dtype)
-        self.decoder = Decoder(d_model, ffn_hidden, num_heads, drop_prob, num_layers, max_sequence_length,
-                               tgt_vocab_size, self.rng, emb_dropout, dtype)
+        with salt_scope(salt_base):  # the model's own dropout-salt stream (sparkmi/ops/rng.py)
+            self.encoder = Encoder(d_model, ffn_hidden, num_heads, drop_prob, num_layers, max_sequence_length,
+                                   src_vocab_size, self.rng, emb_dropout, dtype)
+            self.decoder = Decoder(d_model, ffn_hidden, num_heads, drop_prob, num_layers, max_sequence_length,
+                                   tgt_vocab_size, self.rng, emb_dropout, dtype)
         self.linear = nn.Linear(d_model, tgt_vocab_size)
 
     def _smi_flat_groups(self):

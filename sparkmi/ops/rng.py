@@ -6,6 +6,7 @@ replayed HIP graph draws a fresh mask each step; ``salt`` is a static per-call-s
 handed out at module construction.  Masks are never stored: the backward recomputes them.
 Mirrors ``smi_hash``/``smi_seed`` in csrc/include/smi_common.h.
 """
+import contextlib
 import itertools
 
 import torch
@@ -19,6 +20,22 @@ def reset_salts():
     the same dropout streams as in a fresh process)."""
     global _salts
     _salts = itertools.count(1)
+
+
+@contextlib.contextmanager
+def salt_scope(base: int = 1):
+    """Modules built inside draw the salts base, base + 1, ... of a stream of their own; the
+    process-wide sequence is restored afterwards.  The root models (Transformer, LSTM) build their
+    submodules in one, so a model's dropout masks depend only on its own structure and ``salt_base``
+    — not on how many models the process built before it (an eval model beside a training model,
+    an MLlib Pipeline's stages, a test suite)."""
+    global _salts
+    saved = _salts
+    _salts = itertools.count(int(base))
+    try:
+        yield
+    finally:
+        _salts = saved
 
 
 def new_salt() -> int:
