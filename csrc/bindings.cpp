@@ -85,6 +85,8 @@ int smi_gemm_sp_wg_tm(int);
 int smi_attn_f32_sp(int);
 int smi_attn_dkdv8(int);
 int smi_attn_fwd8(int);
+int smi_attn_stagger(int);
+int smi_attn_ae(int);
 int smi_adam_wide(int);
 int smi_splitk_reduce(const float*, int, long, float*, long, float*, int, hipStream_t);
 int smi_splitk_fold_multi(const float* const*, float* const*, float* const*, const long*, const int*, const int*, int,
@@ -544,6 +546,10 @@ PYBIND11_MODULE(_C, m) {
     a.lr = (const float*)lr; a.step = (float*)step; a.tick = (unsigned*)tick;
     chk(smi_cnn(&a, S(st)), "cnn_sgd_step");
   });
+  m.def("attn_ae", [](int set) { return smi_attn_ae(set); },
+        "fp32 attention outputs: 1 = whole-row stores through LDS (default), 0 = per-lane stores; -1 queries");
+  m.def("attn_stagger", [](int set) { return smi_attn_stagger(set); },
+        "fp32 attention dK/dV: 1 = staggered 8-wave kernel (default), 0 = lockstep; -1 queries");
   m.def("emb_pair", [](int set) { return smi_emb_pair(set); },
         "deterministic embedding backward: 1 = pair-compare (<= 8192 tokens), 0 = bucketed lists; -1 queries");
   m.def("cnn_fused_ok", [](int C, int cin, int classes) { return smi_cnn_fused_ok(C, cin, classes) != 0; });

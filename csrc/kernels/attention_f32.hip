@@ -1197,6 +1197,166 @@ __global__ __launch_bounds__(512, 1) void attn_sp_dkdv8_kernel(AttnF32Args a) {
   }
 }
 
+// dK / dV, 8 waves, STAGGERED: the two halves of the workgroup (waves 0-3 = A, 4-7 = B; each
+// SIMD hosts one wave of each) run half a chunk apart, so on every SIMD one wave's pure-MFMA
+// segment X (S = Q K^T and dP = dO V^T: 48 MFMAs) pairs with its partner's VALU-heavy segment Y
+// (P, dS, their splits, then dV^T += dO^T P and dK^T += Q^T dS: ~300 VALU + 48 MFMAs).  In the
+// lockstep kernel above both waves of a SIMD reach their softmax VALU together and the matrix
+// pipe idles for it once per chunk.  Slot t: A runs X(t/2) (t even) or Y((t-1)/2); B runs
+// X((t-1)/2) (t odd) or Y(t/2 - 1); one barrier per slot.  Chunk c lives in buffer c & 1 from
+// slot 2c to 2c + 2; chunk c + 1 is written by B in slot 2c + 1 into the buffer chunk c - 1
+// left (its last reader, B's Y(c - 1), ended with slot 2c), its global loads issued one slot
+// earlier.  Per-wave arithmetic and its order are the lockstep kernel's (bitwise-identical).
+template <int MODE, bool KPAD, bool PI>
+__global__ __launch_bounds__(512, 1) void attn_sp_dkdv8s_kernel(AttnF32Args a) {
+  __shared__ __attribute__((aligned(16))) unsigned short Qs[2][AS_OP];
+  __shared__ __attribute__((aligned(16))) unsigned short Ds[2][AS_OP];
+  __shared__ __attribute__((aligned(16))) unsigned short Vo[8][AS_OP];
+  __shared__ float lse_s[2][FCH], dl_s[2][FCH];
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  const int kb0 = blockIdx.x * AS_DKDV8_KEYS;
+  const int kwave = kb0 + w * 32;
+  const int kj = kwave + (lane & 31);
+  const bool grpB = __builtin_amdgcn_readfirstlane(w) >= 4;  // wave-uniform: the late half, and the stager
+  const int tb = tid & 255;
+  AS_SRC(Q, a.q, a.qpi, a.qi_ps, a.q_sb, a.q_sh, a.q_ss);
+  AS_SRC(K, a.k, a.kpi, a.kvi_ps, a.k_sb, a.k_sh, a.k_ss);
+  AS_SRC(V, a.v, a.vpi, a.kvi_ps, a.v_sb, a.v_sh, a.v_ss);
+  AS_SRC(dO, a.dout, a.dopi, a.doi_ps, a.o_sb, a.o_sh, a.o_ss);
+  const long rbase = ((long)b * a.H + hh) * a.Sq;
+  int qstart = 0;
+  if (MODE == 2) qstart = kb0 & ~(FCH - 1);
+  const int nchunks = qstart < a.Sq ? (a.Sq - qstart + FCH - 1) / FCH : 0;
+  typename AStageT<PI>::T pq, pd;
+  float lse_r = INFINITY, dl_r = 0.f;
+  // group B stages both operands of a chunk: 8 values of Q and 8 of dO per thread
+  auto stage_load = [&](int c) {
+    const int q0 = qstart + c * FCH;
+    Q.load(q0, a.Sq, pq, tb);
+    dO.load(q0, a.Sq, pd, tb);
+    lse_r = INFINITY; dl_r = 0.f;
+    if (tb < FCH && q0 + tb < a.Sq) {
+      lse_r = a.lse[rbase + q0 + tb];
+      dl_r = a.delta[rbase + q0 + tb];
+    }
+  };
+  auto stage_store = [&](int bf) {
+    as_store(Qs[bf], pq, tb);
+    as_store(Ds[bf], pd, tb);
+    if (tb < FCH) { lse_s[bf][tb] = lse_r; dl_s[bf][tb] = dl_r; }
+  };
+  if (grpB && nchunks) stage_load(0);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = tid + 512 * i, blk = idx >> 8;
+    typename AStageT<PI>::T pv;
+    V.load(kb0 + 32 * blk, a.Sk, pv, idx & 255);
+    as_store(Vo[blk], pv, idx & 255);
+  }
+  F32Pre<1, 32> ks;
+  K.own(kj, a.Sk, lane, ks);
+  const bool kok = kj < a.Sk && !(KPAD && a.kpad[(long)b * a.Sk + kj]);
+  const float kbias = kok ? 0.f : -INFINITY;
+  f32x16_t dk[2], dv[2], s, dp;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+  if (grpB && nchunks) {
+    stage_store(0);
+    if (nchunks > 1) stage_load(1);
+  }
+  __syncthreads();
+  const unsigned short* vimg = Vo[w];
+  const int nslots = nchunks ? 2 * nchunks + 1 : 0;
+  for (int t = 0; t < nslots; ++t) {
+    int cx = -1, cy = -1;
+    if (!grpB) { if ((t & 1) == 0) cx = t >> 1; else cy = t >> 1; }
+    else { if (t & 1) cx = t >> 1; else if (t > 0) cy = (t >> 1) - 1; }
+    if (cx >= nchunks) cx = -1;
+    if (cy >= nchunks) cy = -1;
+    if (cx >= 0) {  // X: S = Q K^T, dP = dO V^T
+      const int buf = cx & 1, q0 = qstart + cx * FCH;
+      if (!(MODE == 2 && q0 + 31 < kwave)) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+        s = as_rows_dot(Qs[buf], lane, ks, s);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dp = as_mma(as_rowfrag(Ds[buf], lane, j), as_rowfrag(vimg, lane, j), dp);
+      }
+    }
+    if (cy >= 0) {  // Y: P, dS, dV^T += dO^T P, dK^T += Q^T dS
+      const int buf = cy & 1, q0 = qstart + cy * FCH;
+      if (!(MODE == 2 && q0 + 31 < kwave)) {
+        float pvv[16], dsv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ql = fa_kl(r, h);
+          const int qq = q0 + ql;
+          float x = fmaf(s[r], a.scale_log2, kbias);
+          if (MODE == 1) x += (kj < qq) ? LOG2E_F : 0.f;
+          if (MODE == 2) x = (kj > qq) ? -INFINITY : x;
+          const float pr = __builtin_amdgcn_exp2f(x - lse_s[buf][ql]);
+          pvv[r] = pr;
+          dsv[r] = pr * (dp[r] - dl_s[buf][ql]);
+        }
+        as_cols_acc(Ds[buf], lane, pvv, dv);
+        as_cols_acc(Qs[buf], lane, dsv, dk);
+      }
+    }
+    if (grpB && (t & 1)) {  // slot 2c + 1: chunk c + 1 into the buffer chunk c - 1 left, loads of c + 2
+      const int c = t >> 1;
+      if (c + 1 < nchunks) stage_store((c + 1) & 1);
+      if (c + 2 < nchunks) stage_load(c + 2);
+    }
+    __syncthreads();
+  }
+  if (a.ae16) {
+    float* img = (float*)&Vo[w][0];
+    ae_stage(img, dk, lane, a.scale);
+    __syncthreads();
+    const long rk = (long)b * a.k_sb + hh * a.k_sh + (long)kwave * a.k_ss;
+    const long rv = (long)b * a.v_sb + hh * a.v_sh + (long)kwave * a.v_ss;
+    ae_store(img, a.no_f32_grad ? nullptr : a.dk + rk, a.dkp ? a.dkp + rk : nullptr, a.k_ss, a.dkv_ps, a.Sk - kwave,
+             lane);
+    __syncthreads();
+    ae_stage(img, dv, lane, 1.0f);
+    __syncthreads();
+    ae_store(img, a.no_f32_grad ? nullptr : a.dv + rv, a.dvp ? a.dvp + rv : nullptr, a.v_ss, a.dkv_ps, a.Sk - kwave,
+             lane);
+  } else if (kj < a.Sk) {
+    float* dK = a.dk + b * a.k_sb + hh * a.k_sh + (long)kj * a.k_ss;
+    float* dV = a.dv + b * a.v_sb + hh * a.v_sh + (long)kj * a.v_ss;
+    if (!a.no_f32_grad) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        fa_store_rowT(dK + dt * 32, dk[dt], lane, a.scale);
+        fa_store_rowT(dV + dt * 32, dv[dt], lane, 1.0f);
+      }
+    }
+    if (a.dkp) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        fa_store_rowT_planes(a.dkp + (dK - a.dk) + dt * 32, a.dkv_ps, dk[dt], lane, a.scale);
+        fa_store_rowT_planes(a.dvp + (dV - a.dv) + dt * 32, a.dkv_ps, dv[dt], lane, 1.0f);
+      }
+    }
+  }
+}
+
+static int g_attn_stagger = -1;  // SMI_ATTN_STAGGER=0: the lockstep dK/dV kernel
+extern "C" int smi_attn_stagger(int set) {
+  if (set == 0 || set == 1) g_attn_stagger = set;
+  if (g_attn_stagger < 0) {
+    const char* e = getenv("SMI_ATTN_STAGGER");
+    g_attn_stagger = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_attn_stagger;
+}
+
 static int g_attn_dkdv8 = -1;  // SMI_ATTN_DKDV8=0: the 4-wave dK/dV kernel
 extern "C" int smi_attn_dkdv8(int set) {
   if (set == 0 || set == 1) g_attn_dkdv8 = set;
@@ -1312,13 +1472,15 @@ static bool fa_ae16(const unsigned short* p, long sb, long sh, long ss) {
   return !p || ((((uintptr_t)p) & 15) == 0 && sb % 8 == 0 && sh % 8 == 0 && ss % 8 == 0);
 }
 static int g_attn_ae = -1;  // SMI_ATTN_AE=0: the per-lane transposed stores
-static bool fa_ae_enabled() {
+extern "C" int smi_attn_ae(int set) {
+  if (set == 0 || set == 1) g_attn_ae = set;
   if (g_attn_ae < 0) {
     const char* e = getenv("SMI_ATTN_AE");
     g_attn_ae = (e && e[0] == '0') ? 0 : 1;
   }
-  return g_attn_ae != 0;
+  return g_attn_ae;
 }
+static bool fa_ae_enabled() { return smi_attn_ae(-1) != 0; }
 
 extern "C" int smi_attn_f32_fwd(const AttnF32Args* args, hipStream_t st) {
   AttnF32Args a = *args;
@@ -1347,7 +1509,9 @@ extern "C" int smi_attn_f32_bwd(const AttnF32Args* args, hipStream_t st) {
   if (smi_gemm_f32_algo(-1) != 0 && smi_attn_f32_sp(-1)) {
     const bool pi = fa_pi(a, true);
     SMI_ATTN_SP_MODES(attn_sp_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), a, pi);
-    if (smi_attn_dkdv8(-1))
+    if (smi_attn_dkdv8(-1) && smi_attn_stagger(-1))
+      SMI_ATTN_SP_MODES8(attn_sp_dkdv8s_kernel, dim3((a.Sk + AS_DKDV8_KEYS - 1) / AS_DKDV8_KEYS, a.H, a.B), a, pi);
+    else if (smi_attn_dkdv8(-1))
       SMI_ATTN_SP_MODES8(attn_sp_dkdv8_kernel, dim3((a.Sk + AS_DKDV8_KEYS - 1) / AS_DKDV8_KEYS, a.H, a.B), a, pi);
     else
       SMI_ATTN_SP_MODES(attn_sp_dkdv_kernel, dim3((a.Sk + 127) / 128, a.H, a.B), a, pi);

@@ -598,3 +598,44 @@ def test_transformer_f32_flagship_trajectory(f32_algo, monkeypatch):
         if i < 5:
             assert d <= 2e-3 * abs(lc[i]) + 1e-4, (i, d, worst, lc, lp, lg)
     assert lc[-1] < lc[0] - 1.0, lc  # the copy task is learnable (the random-pair floor is ln(V - 4))
+
+
+@pytest.mark.parametrize("cross", [False, True])
+@pytest.mark.parametrize("mode,S", [("none", 256), ("reference", 256), ("causal", 200), ("reference", 37)])
+def test_attention_f32_stagger_and_row_epilogue_bitwise(f32_algo, mode, S, cross):
+    """Round-4 kernel variants are scheduling changes only: the staggered 8-wave dK/dV kernel
+    (two half-workgroups half a chunk apart) and the whole-row LDS epilogue give BITWISE the
+    lockstep kernel's / the per-lane stores' outputs, gradients and planes."""
+    if f32_algo == 0:
+        pytest.skip("split-product kernels only")
+    from sparkmi.ops import planes as PL
+    C = _native.C()
+    torch.manual_seed(13)
+    B, H, hd = 2, 3, 64
+    if cross:
+        Sk = S + 5 if mode == "none" else S
+        ins = (torch.randn(B, S, H * hd, device=dev), torch.randn(B, Sk, 128 + 2 * H * hd, device=dev))
+    else:
+        ins = (torch.randn(B, S, 3 * H * hd, device=dev),)
+    do0 = torch.randn(B, S, H * hd, device=dev)
+
+    def run():
+        xs = [t.clone().requires_grad_() for t in ins]
+        o = (cross_attention(xs[0], xs[1], H, mode, kv_col=128) if cross else self_attention(xs[0], H, mode))
+        o.backward(do0)
+        out = [o.detach()] + [t.grad.clone() for t in xs]
+        op = PL.cached(o.detach().reshape(-1, o.shape[-1]))
+        return out, (op.clone() if op is not None else None)
+
+    prev_s, prev_a = C.attn_stagger(-1), C.attn_ae(-1)
+    try:
+        C.attn_stagger(1); C.attn_ae(1)
+        new, newp = run()
+        C.attn_stagger(0); C.attn_ae(0)
+        old, oldp = run()
+    finally:
+        C.attn_stagger(prev_s); C.attn_ae(prev_a)
+    for a, b in zip(new, old):
+        assert torch.equal(a, b)
+    if newp is not None and oldp is not None:
+        assert torch.equal(newp, oldp)
