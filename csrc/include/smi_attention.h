@@ -46,4 +46,7 @@ struct AttnF32Args {
   int no_f32_grad;                   // backward: write dQ / dK / dV as planes only (dqp / dkp / dvp set)
   int ae16;                          // set by the launcher: outputs and their planes admit whole-row
                                      // 16-B stores (row-coalesced LDS epilogue, attention_f32.hip)
+  int skew;                          // set by the launcher (SMI_ATTN_SKEW): the second workgroup of
+                                     // each CU starts skew x 512 cycles late (desynchronises the two
+                                     // resident workgroups' MFMA and softmax phases)
 };

@@ -704,6 +704,16 @@ __device__ __forceinline__ void ae_store(const float* img, float* __restrict__ d
   }
 }
 
+// the second resident workgroup of each CU (linear block id >= one per CU) sleeps a.skew x 512
+// cycles before its prologue (wave-uniform)
+__device__ __forceinline__ void fa_skew(const AttnF32Args& a) {
+  if (a.skew > 0) {
+    const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    if (lin >= 256)
+      for (int i = 0; i < a.skew; ++i) __builtin_amdgcn_s_sleep(8);
+  }
+}
+
 // operand sources of batch b, head hh (fp32 base + plane base at the same element offset)
 #define AS_SRC(NAME, FP, PP, PS, SB, SH, SS)                                                         \
   const AsSrc<PI> NAME{(FP) + b * (SB) + hh * (SH), PI ? (PP) + b * (SB) + hh * (SH) : nullptr, (PS), (SS)}
@@ -721,6 +731,7 @@ __device__ __forceinline__ void attn_sp_fwd_body(const AttnF32Args& a) {
   __shared__ __attribute__((aligned(16))) unsigned short Vs[2][AS_OP];
   AST_DECL;
   AST_T(tk0);
+  fa_skew(a);
   const int hh = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
   const int qwave = blockIdx.x * QW + w * 32;
@@ -858,6 +869,7 @@ template <int MODE, bool KPAD, bool PI>
 __global__ __launch_bounds__(256, 2) void attn_sp_dq_kernel(AttnF32Args a) {
   __shared__ __attribute__((aligned(16))) unsigned short Ks[2][AS_OP];
   __shared__ __attribute__((aligned(16))) unsigned short Vs[2][AS_OP];
+  fa_skew(a);
   const int hh = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
   const int qwave = blockIdx.x * 128 + w * 32;
@@ -1481,11 +1493,23 @@ extern "C" int smi_attn_ae(int set) {
   return g_attn_ae;
 }
 static bool fa_ae_enabled() { return smi_attn_ae(-1) != 0; }
+// SMI_ATTN_SKEW = n: the forward / dQ kernels' second workgroup per CU starts n x 512 cycles late
+static int g_attn_skew = -1;
+extern "C" int smi_attn_skew(int set) {
+  if (set >= 0) g_attn_skew = set;
+  if (g_attn_skew < 0) {
+    const char* e = getenv("SMI_ATTN_SKEW");
+    g_attn_skew = e ? atoi(e) : 0;
+  }
+  return g_attn_skew;
+}
+static int fa_skew_units() { return smi_attn_skew(-1); }
 
 extern "C" int smi_attn_f32_fwd(const AttnF32Args* args, hipStream_t st) {
   AttnF32Args a = *args;
   if (!fa_ok(a)) return -1;
   a.ae16 = fa_ae_enabled() && fa_ae16(a.op, a.o_sb, a.o_sh, a.o_ss);
+  a.skew = fa_skew_units();
   dim3 grid((a.Sq + 127) / 128, a.H, a.B);
   if (smi_gemm_f32_algo(-1) != 0 && smi_attn_f32_sp(-1)) {
     if (smi_attn_fwd8(-1)) {
@@ -1505,6 +1529,7 @@ extern "C" int smi_attn_f32_bwd(const AttnF32Args* args, hipStream_t st) {
     return -1;
   a.ae16 = fa_ae_enabled() && fa_ae16(a.dqp, a.q_sb, a.q_sh, a.q_ss) && fa_ae16(a.dkp, a.k_sb, a.k_sh, a.k_ss) &&
            fa_ae16(a.dvp, a.v_sb, a.v_sh, a.v_ss);
+  a.skew = fa_skew_units();
   if (a.no_f32_grad && (!a.dqp || !a.dkp || !a.dvp)) return -1;  // planes-only needs every plane output
   if (smi_gemm_f32_algo(-1) != 0 && smi_attn_f32_sp(-1)) {
     const bool pi = fa_pi(a, true);

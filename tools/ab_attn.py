@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""A/B of the fp32 attention kernel variants at the flagship shape (B 32, S 256, H 8, hd 64,
+reference mask, planes out as in the model): whole-row LDS epilogue on/off (C.attn_ae), staggered
+dK/dV on/off (C.attn_stagger), start skew of the second workgroup per CU (C.attn_skew).  Each
+variant is timed in interleaved rounds (forward alone, then forward + backward) so clock drift
+hits every variant alike; one JSON line per variant with the median over rounds."""
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from sparkmi import _native  # noqa: E402
+from sparkmi.ops import planes as PL  # noqa: E402
+from sparkmi.ops.attention import self_attention  # noqa: E402
+
+
+def timeit(fn, n=30):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1000.0 / n
+
+
+def main():
+    C = _native.C()
+    B, S, H, hd = 32, 256, 8, 64
+    torch.manual_seed(0)
+    qkv = torch.randn(B, S, 3 * H * hd, device="cuda", requires_grad=True)
+    do = torch.randn(B, S, H * hd, device="cuda")
+    PL.attach(do, PL.split(do.reshape(-1, H * hd)))
+    variants = [("base", 0, 0, 0), ("ae", 1, 0, 0), ("ae+stagger", 1, 1, 0), ("ae+stagger+skew4", 1, 1, 4),
+                ("ae+stagger+skew8", 1, 1, 8)]
+    res = {v[0]: ([], []) for v in variants}
+    for _ in range(5):
+        for name, ae, st, sk in variants:
+            C.attn_ae(ae)
+            C.attn_stagger(st)
+            C.attn_skew(sk)
+            f = timeit(lambda: self_attention(qkv.detach(), H, "reference"))
+
+            def fb():
+                o = self_attention(qkv, H, "reference")
+                o.backward(do)
+            t = timeit(fb)
+            res[name][0].append(f)
+            res[name][1].append(t - f)
+    fl = 4.0 * B * H * S * S * hd
+    for name, (fs, bs) in res.items():
+        f, b = statistics.median(fs), statistics.median(bs)
+        print(json.dumps({"variant": name, "fwd_us": round(f, 1), "bwd_us": round(b, 1),
+                          "fwd_tf": round(fl / f / 1e6, 1), "bwd_tf": round(2.5 * fl / b / 1e6, 1)}), flush=True)
+    C.attn_ae(1)
+    C.attn_stagger(1)
+    C.attn_skew(0)
+
+
+if __name__ == "__main__":
+    main()
