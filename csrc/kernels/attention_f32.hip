@@ -965,6 +965,133 @@ __global__ __launch_bounds__(256, 2) void attn_sp_dq_kernel(AttnF32Args a) {
   }
 }
 
+// dQ on EIGHT waves (256 queries: a whole head at S = 256), staggered like attn_sp_dkdv8s_kernel:
+// each staged K / V chunk serves 256 queries (the 4-wave kernel stages it twice per head), and the
+// two half-workgroups run half a chunk apart so one wave's X segment (S^T = K Q^T, dP^T = V dO^T:
+// 48 MFMAs) pairs on its SIMD with the partner's Y segment (the dS values, their split and
+// dQ^T += K^T dS^T: ~150 VALU + 24 MFMAs).  Group B stages both operands of every chunk.  Per-wave
+// arithmetic and order are the 4-wave kernel's (bitwise-identical dQ, delta).
+template <int MODE, bool KPAD, bool PI>
+__global__ __launch_bounds__(512, 1) void attn_sp_dq8s_kernel(AttnF32Args a) {
+  __shared__ __attribute__((aligned(16))) unsigned short Ks[2][AS_OP];
+  __shared__ __attribute__((aligned(16))) unsigned short Vs[2][AS_OP];
+  __shared__ __attribute__((aligned(16))) float epi[8][AE_FLOATS];
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  const int qwave = blockIdx.x * 256 + w * 32;
+  const int qi = qwave + (lane & 31);
+  const bool grpB = __builtin_amdgcn_readfirstlane(w) >= 4;
+  const int tb = tid & 255;
+  AS_SRC(Q, a.q, a.qpi, a.qi_ps, a.q_sb, a.q_sh, a.q_ss);
+  AS_SRC(K, a.k, a.kpi, a.kvi_ps, a.k_sb, a.k_sh, a.k_ss);
+  AS_SRC(V, a.v, a.vpi, a.kvi_ps, a.v_sb, a.v_sh, a.v_ss);
+  AS_SRC(dO, a.dout, a.dopi, a.doi_ps, a.o_sb, a.o_sh, a.o_ss);
+  const float* Og = a.o + b * a.o_sb + hh * a.o_sh;
+  const unsigned char* kp = a.kpad ? a.kpad + (long)b * a.Sk : nullptr;
+  int kend = a.Sk;
+  if (MODE == 2) kend = min(a.Sk, blockIdx.x * 256 + 256);
+  const int nchunks = (kend + FCH - 1) / FCH;
+  typename AStageT<PI>::T pk, pv;
+  auto stage_load = [&](int c) { K.load(c * FCH, a.Sk, pk, tb); V.load(c * FCH, a.Sk, pv, tb); };
+  auto stage_store = [&](int bf) { as_store(Ks[bf], pk, tb); as_store(Vs[bf], pv, tb); };
+  if (grpB && nchunks) stage_load(0);
+  F32Pre<1, 32> qs, ds;
+  float dl;
+  {
+    float df[32], of[32];
+    Q.own(qi, a.Sq, lane, qs);
+    dO.own(qi, a.Sq, lane, ds);
+    dO.own_f32(ds, qi, a.Sq, lane, df);
+    fa_ownrow(Og, a.o_ss, qi, a.Sq, lane, of);
+    float sacc = 0.f;
+#pragma unroll
+    for (int t = 0; t < 32; ++t) sacc = fmaf(df[t], of[t], sacc);
+    dl = smi_row32_swap_sum(sacc);
+  }
+  const long rbase = ((long)b * a.H + hh) * a.Sq;
+  if (h == 0 && qi < a.Sq) a.delta[rbase + qi] = dl;
+  const float lse = qi < a.Sq ? a.lse[rbase + qi] : INFINITY;
+  if (grpB && nchunks) {
+    stage_store(0);
+    if (nchunks > 1) stage_load(1);
+  }
+  __syncthreads();
+  f32x16_t acc[2], s, dp;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[dt][r] = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+  const int nslots = nchunks ? 2 * nchunks + 1 : 0;
+  for (int t = 0; t < nslots; ++t) {
+    int cx = -1, cy = -1;
+    if (!grpB) { if ((t & 1) == 0) cx = t >> 1; else cy = t >> 1; }
+    else { if (t & 1) cx = t >> 1; else if (t > 0) cy = (t >> 1) - 1; }
+    if (cx >= nchunks) cx = -1;
+    if (cy >= nchunks) cy = -1;
+    if (cx >= 0) {  // X: S^T = K Q^T, dP^T = V dO^T
+      const int buf = cx & 1, k0 = cx * FCH;
+      float ub;
+      const bool full = k0 + 32 <= a.Sk;
+      const bool uni = uniform_bias<MODE, KPAD, 32>(k0, qwave, qwave + 31, full, ub);
+      if (!(uni && ub == -INFINITY)) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+        s = as_rows_dot(Ks[buf], lane, qs, s);
+        dp = as_rows_dot(Vs[buf], lane, ds, dp);
+      }
+    }
+    if (cy >= 0) {  // Y: dS, dQ^T += K^T dS^T
+      const int buf = cy & 1, k0 = cy * FCH;
+      float ub;
+      const bool full = k0 + 32 <= a.Sk;
+      const bool uni = uniform_bias<MODE, KPAD, 32>(k0, qwave, qwave + 31, full, ub);
+      if (!(uni && ub == -INFINITY)) {
+        const unsigned long long kmask = KPAD ? chunk_pad_mask(kp, k0, a.Sk) : 0ull;
+        float dsv[16];
+        if (uni) {
+          const float off = ub - lse;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dsv[r] = __builtin_amdgcn_exp2f(fmaf(s[r], a.scale_log2, off)) * (dp[r] - dl);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int kl = fa_kl(r, h);
+            const float x = score_adj<MODE, KPAD>(s[r], qi, k0 + kl, kl, full, a.Sk, kmask, a.scale_log2);
+            dsv[r] = __builtin_amdgcn_exp2f(x - lse) * (dp[r] - dl);
+          }
+        }
+        as_cols_acc(Ks[buf], lane, dsv, acc);
+      }
+    }
+    if (grpB && (t & 1)) {
+      const int c = t >> 1;
+      if (c + 1 < nchunks) stage_store((c + 1) & 1);
+      if (c + 2 < nchunks) stage_load(c + 2);
+    }
+    __syncthreads();
+  }
+  if (a.ae16) {
+    float* img = &epi[w][0];
+    ae_stage(img, acc, lane, a.scale);
+    __syncthreads();
+    const long r0 = (long)b * a.q_sb + hh * a.q_sh + (long)qwave * a.q_ss;
+    ae_store(img, a.no_f32_grad ? nullptr : a.dq + r0, a.dqp ? a.dqp + r0 : nullptr, a.q_ss, a.dq_ps, a.Sq - qwave,
+             lane);
+  } else if (qi < a.Sq) {
+    float* dQ = a.dq + b * a.q_sb + hh * a.q_sh + (long)qi * a.q_ss;
+    if (!a.no_f32_grad) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) fa_store_rowT(dQ + dt * 32, acc[dt], lane, a.scale);
+    }
+    if (a.dqp) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) fa_store_rowT_planes(a.dqp + (dQ - a.dq) + dt * 32, a.dq_ps, acc[dt], lane, a.scale);
+    }
+  }
+}
+
 // one workgroup per CU: owned K and V splits (96 registers) + two accumulator pairs + the P / dS
 // splits exceed 256 registers (two workgroups per CU spilled 34)
 template <int MODE, bool KPAD, bool PI>
@@ -1455,6 +1582,8 @@ extern "C" int smi_gemm_f32_algo(int);
     else { SMI_ATTN_F32_MODES(KERNEL, 1, GRID, ARGS) }                                                     \
   } while (0)
 
+extern "C" int smi_attn_stagger(int);
+
 static int fa_ok(const AttnF32Args& a) {
   // float4 access to every row: 16-B aligned bases and strides that are multiples of 4 floats
   const long st[] = {a.q_ss, a.k_ss, a.v_ss, a.o_ss, a.q_sh, a.k_sh, a.v_sh, a.o_sh, a.q_sb, a.k_sb, a.v_sb, a.o_sb};
@@ -1533,7 +1662,10 @@ extern "C" int smi_attn_f32_bwd(const AttnF32Args* args, hipStream_t st) {
   if (a.no_f32_grad && (!a.dqp || !a.dkp || !a.dvp)) return -1;  // planes-only needs every plane output
   if (smi_gemm_f32_algo(-1) != 0 && smi_attn_f32_sp(-1)) {
     const bool pi = fa_pi(a, true);
-    SMI_ATTN_SP_MODES(attn_sp_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), a, pi);
+    if (smi_attn_dkdv8(-1) && smi_attn_stagger(-1))
+      SMI_ATTN_SP_MODES8(attn_sp_dq8s_kernel, dim3((a.Sq + 255) / 256, a.H, a.B), a, pi);
+    else
+      SMI_ATTN_SP_MODES(attn_sp_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), a, pi);
     if (smi_attn_dkdv8(-1) && smi_attn_stagger(-1))
       SMI_ATTN_SP_MODES8(attn_sp_dkdv8s_kernel, dim3((a.Sk + AS_DKDV8_KEYS - 1) / AS_DKDV8_KEYS, a.H, a.B), a, pi);
     else if (smi_attn_dkdv8(-1))
