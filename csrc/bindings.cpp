@@ -88,6 +88,7 @@ int smi_attn_fwd8(int);
 int smi_attn_stagger(int);
 int smi_attn_ae(int);
 int smi_attn_skew(int);
+int smi_attn_fwd_stagger(int);
 int smi_adam_wide(int);
 int smi_splitk_reduce(const float*, int, long, float*, long, float*, int, hipStream_t);
 int smi_splitk_fold_multi(const float* const*, float* const*, float* const*, const long*, const int*, const int*, int,
@@ -547,6 +548,8 @@ PYBIND11_MODULE(_C, m) {
     a.lr = (const float*)lr; a.step = (float*)step; a.tick = (unsigned*)tick;
     chk(smi_cnn(&a, S(st)), "cnn_sgd_step");
   });
+  m.def("attn_fwd_stagger", [](int set) { return smi_attn_fwd_stagger(set); },
+        "fp32 attention forward: 1 = staggered 8-wave kernel, 0 = 4-wave (default); -1 queries");
   m.def("attn_skew", [](int set) { return smi_attn_skew(set); },
         "fp32 attention forward / dQ: the second workgroup per CU starts set x 512 cycles late; -1 queries");
   m.def("attn_ae", [](int set) { return smi_attn_ae(set); },

@@ -860,6 +860,137 @@ __device__ __forceinline__ void attn_sp_fwd_body(const AttnF32Args& a) {
   AST_ADD(7, tk0, tk3);  // wave lifetime
   AST_END();
 }
+// Forward on EIGHT waves (a whole head per workgroup at S = 256), staggered like the backward
+// kernels: X = S^T = K Q^T (24 MFMAs) of one wave pairs on its SIMD with the partner's Y = online
+// softmax, the P split and O^T += V^T P^T (~230 VALU + 24 MFMAs); group B stages every K / V chunk
+// (once per 256 queries).  Per-wave arithmetic and order are the 4-wave kernel's (bitwise-identical
+// O, LSE).
+template <int MODE, bool KPAD, bool PI>
+__global__ __launch_bounds__(512, 1) void attn_sp_fwd8s_kernel(AttnF32Args a) {
+  __shared__ __attribute__((aligned(16))) unsigned short Ks[2][AS_OP];
+  __shared__ __attribute__((aligned(16))) unsigned short Vs[2][AS_OP];
+  __shared__ __attribute__((aligned(16))) float epi[8][AE_FLOATS];
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  const int qwave = blockIdx.x * 256 + w * 32;
+  const int qi = qwave + (lane & 31);
+  const bool grpB = __builtin_amdgcn_readfirstlane(w) >= 4;
+  const int tb = tid & 255;
+  AS_SRC(Q, a.q, a.qpi, a.qi_ps, a.q_sb, a.q_sh, a.q_ss);
+  AS_SRC(K, a.k, a.kpi, a.kvi_ps, a.k_sb, a.k_sh, a.k_ss);
+  AS_SRC(V, a.v, a.vpi, a.kvi_ps, a.v_sb, a.v_sh, a.v_ss);
+  const unsigned char* kp = a.kpad ? a.kpad + (long)b * a.Sk : nullptr;
+  int kend = a.Sk;
+  if (MODE == 2) kend = min(a.Sk, blockIdx.x * 256 + 256);
+  const int nchunks = (kend + FCH - 1) / FCH;
+  typename AStageT<PI>::T pk, pv;
+  auto stage_load = [&](int c) { K.load(c * FCH, a.Sk, pk, tb); V.load(c * FCH, a.Sk, pv, tb); };
+  auto stage_store = [&](int bf) { as_store(Ks[bf], pk, tb); as_store(Vs[bf], pv, tb); };
+  if (grpB && nchunks) stage_load(0);
+  F32Pre<1, 32> qs;
+  Q.own(qi, a.Sq, lane, qs);
+  if (grpB && nchunks) {
+    stage_store(0);
+    if (nchunks > 1) stage_load(1);
+  }
+  __syncthreads();
+  float m = -INFINITY, l = 0.f;
+  f32x16_t o[2], s;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s[r] = 0.f;
+  const int nslots = nchunks ? 2 * nchunks + 1 : 0;
+  for (int t = 0; t < nslots; ++t) {
+    int cx = -1, cy = -1;
+    if (!grpB) { if ((t & 1) == 0) cx = t >> 1; else cy = t >> 1; }
+    else { if (t & 1) cx = t >> 1; else if (t > 0) cy = (t >> 1) - 1; }
+    if (cx >= nchunks) cx = -1;
+    if (cy >= nchunks) cy = -1;
+    if (cx >= 0) {  // X: S^T = K Q^T
+      const int buf = cx & 1, k0 = cx * FCH;
+      float ub;
+      const bool full = k0 + 32 <= a.Sk;
+      const bool uni = uniform_bias<MODE, KPAD, 32>(k0, qwave, qwave + 31, full, ub);
+      if (!(uni && ub == -INFINITY)) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = 0.f;
+        s = as_rows_dot(Ks[buf], lane, qs, s);
+      }
+    }
+    if (cy >= 0) {  // Y: online softmax, O^T += V^T P^T
+      const int buf = cy & 1, k0 = cy * FCH;
+      float ub;
+      const bool full = k0 + 32 <= a.Sk;
+      const bool uni = uniform_bias<MODE, KPAD, 32>(k0, qwave, qwave + 31, full, ub);
+      if (!(uni && ub == -INFINITY)) {
+        const unsigned long long kmask = KPAD ? chunk_pad_mask(kp, k0, a.Sk) : 0ull;
+        float cmax = -INFINITY;
+        if (uni) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) cmax = fmaxf(cmax, s[r]);
+          cmax = cmax * a.scale_log2 + ub;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int kl = fa_kl(r, h);
+            s[r] = score_adj<MODE, KPAD>(s[r], qi, k0 + kl, kl, full, a.Sk, kmask, a.scale_log2);
+            cmax = fmaxf(cmax, s[r]);
+          }
+        }
+        cmax = smi_row32_swap_max(cmax);
+        const float mnew = fmaxf(m, cmax);
+        const float mref = (mnew == -INFINITY) ? 0.f : mnew;
+        const float alpha = __builtin_amdgcn_exp2f(m - mref);
+        float psum = 0.f;
+        float pv16[16];
+        if (uni) {
+          const float off = ub - mref;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) { pv16[r] = __builtin_amdgcn_exp2f(fmaf(s[r], a.scale_log2, off)); psum += pv16[r]; }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) { pv16[r] = __builtin_amdgcn_exp2f(s[r] - mref); psum += pv16[r]; }
+        }
+        psum = smi_row32_swap_sum(psum);
+        l = l * alpha + psum;
+        m = mnew;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) o[dt] *= alpha;
+        as_cols_acc(Vs[buf], lane, pv16, o);
+      }
+    }
+    if (grpB && (t & 1)) {
+      const int c = t >> 1;
+      if (c + 1 < nchunks) stage_store((c + 1) & 1);
+      if (c + 2 < nchunks) stage_load(c + 2);
+    }
+    __syncthreads();
+  }
+  const float inv = l > 0.f ? 1.0f / l : 0.f;
+  if (a.ae16) {
+    float* img = &epi[w][0];
+    ae_stage(img, o, lane, inv);
+    __syncthreads();
+    const long r0 = (long)b * a.o_sb + hh * a.o_sh + (long)qwave * a.o_ss;
+    ae_store(img, a.o + r0, a.op ? a.op + r0 : nullptr, a.o_ss, a.op_ps, a.Sq - qwave, lane);
+  } else if (qi < a.Sq) {
+    float* O = a.o + b * a.o_sb + hh * a.o_sh + (long)qi * a.o_ss;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) fa_store_rowT(O + dt * 32, o[dt], lane, inv);
+    if (a.op) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) fa_store_rowT_planes(a.op + (O - a.o) + dt * 32, a.op_ps, o[dt], lane, inv);
+    }
+  }
+  if (qi < a.Sq && h == 0) {
+    const float mref = (m == -INFINITY) ? 0.f : m;
+    a.lse[((long)b * a.H + hh) * a.Sq + qi] = l > 0.f ? mref + log2f(l) : INFINITY;
+  }
+}
+
 template <int MODE, bool KPAD, bool PI>
 __global__ __launch_bounds__(256, 2) void attn_sp_fwd4(AttnF32Args a) { attn_sp_fwd_body<MODE, KPAD, PI, 4>(a); }
 template <int MODE, bool KPAD, bool PI>
@@ -1584,6 +1715,17 @@ extern "C" int smi_gemm_f32_algo(int);
 
 extern "C" int smi_attn_stagger(int);
 
+// the staggered 8-wave forward (SMI_ATTN_FWD_STAGGER=1; default off until measured)
+static int g_attn_fwd_stagger = -1;
+extern "C" int smi_attn_fwd_stagger(int set) {
+  if (set == 0 || set == 1) g_attn_fwd_stagger = set;
+  if (g_attn_fwd_stagger < 0) {
+    const char* e = getenv("SMI_ATTN_FWD_STAGGER");
+    g_attn_fwd_stagger = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_attn_fwd_stagger;
+}
+
 static int fa_ok(const AttnF32Args& a) {
   // float4 access to every row: 16-B aligned bases and strides that are multiples of 4 floats
   const long st[] = {a.q_ss, a.k_ss, a.v_ss, a.o_ss, a.q_sh, a.k_sh, a.v_sh, a.o_sh, a.q_sb, a.k_sb, a.v_sb, a.o_sb};
@@ -1643,6 +1785,8 @@ extern "C" int smi_attn_f32_fwd(const AttnF32Args* args, hipStream_t st) {
   if (smi_gemm_f32_algo(-1) != 0 && smi_attn_f32_sp(-1)) {
     if (smi_attn_fwd8(-1)) {
       SMI_ATTN_SP_MODES8(attn_sp_fwd8, dim3((a.Sq + 255) / 256, a.H, a.B), a, fa_pi(a, false));
+    } else if (smi_attn_fwd_stagger(-1)) {
+      SMI_ATTN_SP_MODES8(attn_sp_fwd8s_kernel, dim3((a.Sq + 255) / 256, a.H, a.B), a, fa_pi(a, false));
     } else {
       SMI_ATTN_SP_MODES(attn_sp_fwd4, grid, a, fa_pi(a, false));
     }

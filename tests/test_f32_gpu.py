@@ -603,9 +603,9 @@ def test_transformer_f32_flagship_trajectory(f32_algo, monkeypatch):
 @pytest.mark.parametrize("cross", [False, True])
 @pytest.mark.parametrize("mode,S", [("none", 256), ("reference", 256), ("causal", 200), ("reference", 37)])
 def test_attention_f32_stagger_and_row_epilogue_bitwise(f32_algo, mode, S, cross):
-    """Round-4 kernel variants are scheduling changes only: the staggered 8-wave dK/dV kernel
-    (two half-workgroups half a chunk apart) and the whole-row LDS epilogue give BITWISE the
-    lockstep kernel's / the per-lane stores' outputs, gradients and planes."""
+    """Round-4 kernel variants are scheduling changes only: the staggered 8-wave forward, dQ and
+    dK/dV kernels (two half-workgroups half a chunk apart) and the whole-row LDS epilogue give
+    BITWISE the 4-wave / lockstep kernels' outputs, gradients and planes."""
     if f32_algo == 0:
         pytest.skip("split-product kernels only")
     from sparkmi.ops import planes as PL
@@ -627,14 +627,14 @@ def test_attention_f32_stagger_and_row_epilogue_bitwise(f32_algo, mode, S, cross
         op = PL.cached(o.detach().reshape(-1, o.shape[-1]))
         return out, (op.clone() if op is not None else None)
 
-    prev_s, prev_a = C.attn_stagger(-1), C.attn_ae(-1)
+    prev_s, prev_a, prev_f = C.attn_stagger(-1), C.attn_ae(-1), C.attn_fwd_stagger(-1)
     try:
-        C.attn_stagger(1); C.attn_ae(1)
+        C.attn_stagger(1); C.attn_ae(1); C.attn_fwd_stagger(1)
         new, newp = run()
-        C.attn_stagger(0); C.attn_ae(0)
+        C.attn_stagger(0); C.attn_ae(0); C.attn_fwd_stagger(0)
         old, oldp = run()
     finally:
-        C.attn_stagger(prev_s); C.attn_ae(prev_a)
+        C.attn_stagger(prev_s); C.attn_ae(prev_a); C.attn_fwd_stagger(prev_f)
     for a, b in zip(new, old):
         assert torch.equal(a, b)
     if newp is not None and oldp is not None:

@@ -36,14 +36,15 @@ def main():
     qkv = torch.randn(B, S, 3 * H * hd, device="cuda", requires_grad=True)
     do = torch.randn(B, S, H * hd, device="cuda")
     PL.attach(do, PL.split(do.reshape(-1, H * hd)))
-    variants = [("base", 0, 0, 0), ("ae", 1, 0, 0), ("ae+stagger", 1, 1, 0), ("ae+stagger+skew4", 1, 1, 4),
-                ("ae+stagger+skew8", 1, 1, 8)]
+    variants = [("base", 0, 0, 0, 0), ("ae", 1, 0, 0, 0), ("ae+stagger", 1, 1, 0, 0), ("ae+skew8", 1, 0, 8, 0),
+                ("ae+stagger+fwd8s", 1, 1, 0, 1)]
     res = {v[0]: ([], []) for v in variants}
     for _ in range(5):
-        for name, ae, st, sk in variants:
+        for name, ae, st, sk, fs in variants:
             C.attn_ae(ae)
             C.attn_stagger(st)
             C.attn_skew(sk)
+            C.attn_fwd_stagger(fs)
             f = timeit(lambda: self_attention(qkv.detach(), H, "reference"))
 
             def fb():
@@ -60,6 +61,7 @@ def main():
     C.attn_ae(1)
     C.attn_stagger(1)
     C.attn_skew(0)
+    C.attn_fwd_stagger(0)
 
 
 if __name__ == "__main__":
