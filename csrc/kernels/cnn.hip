@@ -481,9 +481,14 @@ __device__ __noinline__ void cnn_fused_tail(const CNNArgs& g, int img) {
   __shared__ int last;
   const int ngrp = (g.B + CNN_GRP - 1) / CNN_GRP;
   const int grp = img / CNN_GRP, g0 = grp * CNN_GRP, g1 = min(g.B, g0 + CNN_GRP);
-  __threadfence();  // release: every thread's slab stores are visible device-wide ...
-  __syncthreads();  // ... before thread 0 takes the ticket
-  if (threadIdx.x == 0) last = atomicAdd(g.tick + grp, 1u) == (unsigned)(g1 - g0 - 1);
+  // every wave's slab stores complete (workgroup-scope release in the barrier), then ONE agent-
+  // scope release by thread 0 (it writes the CU's L2 back: cumulative over the workgroup's stores)
+  // before the ticket — a release per wave (16 per workgroup) made the step 2x slower
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(g.tick + grp, 1u) == (unsigned)(g1 - g0 - 1);
+  }
   __syncthreads();
   if (!last) return;
   __threadfence();  // acquire the group's slabs
@@ -499,9 +504,9 @@ __device__ __noinline__ void cnn_fused_tail(const CNNArgs& g, int img) {
     }
     part4[q] = acc;
   }
-  __threadfence();  // release the group sum (every thread's part of it)
-  __syncthreads();
+  __syncthreads();  // the group sum stored by every wave (then released by thread 0)
   if (threadIdx.x == 0) {
+    __threadfence();
     g.tick[grp] = 0u;  // re-arm (every image of the group has taken its ticket)
     last = atomicAdd(g.tick + CNN_GRP, 1u) == (unsigned)(ngrp - 1);
   }

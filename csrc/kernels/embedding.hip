@@ -553,9 +553,11 @@ __global__ __launch_bounds__(128) void emb_pair_sum(const long long* __restrict_
     else e.part[(long)k * D + c] = acc;
   }
   if (gn == 1) return;
-  __threadfence();  // release every thread's partial
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(e.tick + g0, 1u) == (unsigned)gn - 1;
+  __syncthreads();  // every wave's partial stored; thread 0's agent release covers the workgroup
+  if (threadIdx.x == 0) {
+    __threadfence();
+    s_last = atomicAdd(e.tick + g0, 1u) == (unsigned)gn - 1;
+  }
   __syncthreads();
   if (!s_last) return;
   __threadfence();

@@ -912,17 +912,16 @@ __global__ __launch_bounds__(256) void lstm_wgrad_combine(LSTMArgs a) {
 // B column l & 15 at k = l >> 4; the accumulator's register j of lane l is row 4 (l >> 4) + j,
 // column l & 15.
 #define LW_WAVES 8
-__device__ __forceinline__ float lw_d(const LSTMArgs& a, int l, long bt, int r, int rows) {
+__device__ __forceinline__ float lw_d(const LSTMArgs& a, int l, int b, int t, int r, int rows) {
   if (r >= rows) return 0.f;
-  const int b = (int)(bt / a.T), t = (int)(bt % a.T);
   if (l < a.L) return a.ws_da[(((size_t)b * a.L + l) * a.T + t) * 4 * a.H + r];
   const float ds = a.dpred_scale ? a.dpred_scale[0] : 1.f;
   if (!a.dpred_last) return a.dpred[((size_t)b * a.T + t) * a.C + r] * ds;
   return t == a.T - 1 ? a.dpred[(size_t)b * a.C + r] * ds : 0.f;
 }
-__device__ __forceinline__ float lw_x(const LSTMArgs& a, int l, long bt, int c, int cols, uint32_t seed) {
+__device__ __forceinline__ float lw_x(const LSTMArgs& a, int l, int b, int t, int c, int cols, uint32_t seed) {
   if (c >= cols) return 0.f;
-  const int b = (int)(bt / a.T), t = (int)(bt % a.T), H = a.H, L = a.L, T = a.T;
+  const int H = a.H, L = a.L, T = a.T;
   const float* wsb = a.ws + (size_t)b * L * T * 6 * H;
   if (l == L) return c < H ? wsb[((size_t)(L - 1) * T + t) * 6 * H + 5 * H + c] : 1.f;
   const int In = l == 0 ? a.E : H;
@@ -994,17 +993,29 @@ __global__ __launch_bounds__(64 * LW_WAVES) void lstm_wgrad_mfma(LSTMArgs a) {
   // wave w reduces (b,t) rows [k_begin, k_end), 4 per MFMA
   const long kc = ((BT + LW_WAVES - 1) / LW_WAVES + 3) / 4 * 4;
   const long kb = w * kc, ke = min(BT, kb + kc);
+  // (b, t) of this lane's k = k0 + 4u + lk, advanced by 16 per step without dividing (an integer
+  // division by the runtime T per element made the gather VALU-bound)
+  int bu[4], tu[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const long k = kb + 4 * u + lk;
+    bu[u] = (int)(k / a.T);
+    tu[u] = (int)(k - (long)bu[u] * a.T);
+  }
   for (long k0 = kb; k0 < ke; k0 += 16) {
     float av[4], bv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const long k = k0 + 4 * u + lk;
-      const bool ok = k < ke;
-      av[u] = ok ? lw_d(a, l, k, r0 + li, rows) : 0.f;
-      bv[u] = ok ? lw_x(a, l, k, c0 + li, cols, seed) : 0.f;
+      const bool ok = k0 + 4 * u + lk < ke;
+      av[u] = ok ? lw_d(a, l, bu[u], tu[u], r0 + li, rows) : 0.f;
+      bv[u] = ok ? lw_x(a, l, bu[u], tu[u], c0 + li, cols, seed) : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc = MF16F32(av[u], bv[u], acc);
+    for (int u = 0; u < 4; ++u) {
+      acc = MF16F32(av[u], bv[u], acc);
+      tu[u] += 16;
+      while (tu[u] >= a.T) { tu[u] -= a.T; ++bu[u]; }
+    }
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) part[w][(4 * lk + j) * 16 + li] = acc[j];

@@ -38,6 +38,9 @@ def main():
     PL.attach(do, PL.split(do.reshape(-1, H * hd)))
     variants = [("base", 0, 0, 0, 0), ("ae", 1, 0, 0, 0), ("ae+stagger", 1, 1, 0, 0), ("ae+skew8", 1, 0, 8, 0),
                 ("ae+stagger+fwd8s", 1, 1, 0, 1)]
+    if "--only" in sys.argv:
+        only = sys.argv[sys.argv.index("--only") + 1]
+        variants = [v for v in variants if v[0] == only]
     res = {v[0]: ([], []) for v in variants}
     for _ in range(5):
         for name, ae, st, sk, fs in variants:
