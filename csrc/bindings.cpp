@@ -87,6 +87,7 @@ int smi_attn_dkdv8(int);
 int smi_attn_fwd8(int);
 int smi_attn_stagger(int);
 int smi_attn_ae(int);
+int smi_attn_ae_bwd(int);
 int smi_attn_skew(int);
 int smi_attn_fwd_stagger(int);
 int smi_adam_wide(int);
@@ -552,6 +553,8 @@ PYBIND11_MODULE(_C, m) {
         "fp32 attention forward: 1 = staggered 8-wave kernel, 0 = 4-wave (default); -1 queries");
   m.def("attn_skew", [](int set) { return smi_attn_skew(set); },
         "fp32 attention forward / dQ: the second workgroup per CU starts set x 512 cycles late; -1 queries");
+  m.def("attn_ae_bwd", [](int set) { return smi_attn_ae_bwd(set); },
+        "fp32 attention backward outputs through LDS: 1 = on, 0 = per-lane stores (default); -1 queries");
   m.def("attn_ae", [](int set) { return smi_attn_ae(set); },
         "fp32 attention outputs: 1 = whole-row stores through LDS (default), 0 = per-lane stores; -1 queries");
   m.def("attn_stagger", [](int set) { return smi_attn_stagger(set); },

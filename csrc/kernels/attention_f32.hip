@@ -1617,12 +1617,14 @@ __global__ __launch_bounds__(512, 1) void attn_sp_dkdv8s_kernel(AttnF32Args a) {
   }
 }
 
-static int g_attn_stagger = -1;  // SMI_ATTN_STAGGER=0: the lockstep dK/dV kernel
+// SMI_ATTN_STAGGER=1: the staggered 8-wave dQ and dK/dV kernels (bitwise the same results; measured
+// no faster than the 4-wave dQ + lockstep 8-wave dK/dV pair, tools/ab_attn.py — opt-in)
+static int g_attn_stagger = -1;
 extern "C" int smi_attn_stagger(int set) {
   if (set == 0 || set == 1) g_attn_stagger = set;
   if (g_attn_stagger < 0) {
     const char* e = getenv("SMI_ATTN_STAGGER");
-    g_attn_stagger = (e && e[0] == '0') ? 0 : 1;
+    g_attn_stagger = (e && e[0] == '1') ? 1 : 0;
   }
   return g_attn_stagger;
 }
@@ -1764,6 +1766,17 @@ extern "C" int smi_attn_ae(int set) {
   return g_attn_ae;
 }
 static bool fa_ae_enabled() { return smi_attn_ae(-1) != 0; }
+// the backward kernels' dQ / dK / dV through LDS too (SMI_ATTN_AE_BWD=1): measured +3..5 us per
+// call against the per-lane stores (tools/ab_attn.py: the forward gains 5..13 us) — off by default
+static int g_attn_ae_bwd = -1;
+extern "C" int smi_attn_ae_bwd(int set) {
+  if (set == 0 || set == 1) g_attn_ae_bwd = set;
+  if (g_attn_ae_bwd < 0) {
+    const char* e = getenv("SMI_ATTN_AE_BWD");
+    g_attn_ae_bwd = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_attn_ae_bwd;
+}
 // SMI_ATTN_SKEW = n: the forward / dQ kernels' second workgroup per CU starts n x 512 cycles late
 static int g_attn_skew = -1;
 extern "C" int smi_attn_skew(int set) {
@@ -1800,7 +1813,7 @@ extern "C" int smi_attn_f32_bwd(const AttnF32Args* args, hipStream_t st) {
   AttnF32Args a = *args;
   if (!fa_ok(a) || !a.dout || !a.delta || (((uintptr_t)a.dout | (uintptr_t)a.dq | (uintptr_t)a.dk | (uintptr_t)a.dv) & 15))
     return -1;
-  a.ae16 = fa_ae_enabled() && fa_ae16(a.dqp, a.q_sb, a.q_sh, a.q_ss) && fa_ae16(a.dkp, a.k_sb, a.k_sh, a.k_ss) &&
+  a.ae16 = smi_attn_ae_bwd(-1) && fa_ae16(a.dqp, a.q_sb, a.q_sh, a.q_ss) && fa_ae16(a.dkp, a.k_sb, a.k_sh, a.k_ss) &&
            fa_ae16(a.dvp, a.v_sb, a.v_sh, a.v_ss);
   a.skew = fa_skew_units();
   if (a.no_f32_grad && (!a.dqp || !a.dkp || !a.dvp)) return -1;  // planes-only needs every plane output

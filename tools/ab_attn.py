@@ -37,14 +37,15 @@ def main():
     do = torch.randn(B, S, H * hd, device="cuda")
     PL.attach(do, PL.split(do.reshape(-1, H * hd)))
     variants = [("base", 0, 0, 0, 0), ("ae", 1, 0, 0, 0), ("ae+stagger", 1, 1, 0, 0), ("ae+skew8", 1, 0, 8, 0),
-                ("ae+stagger+fwd8s", 1, 1, 0, 1)]
+                ("ae+stagger+fwd8s", 1, 1, 0, 1), ("ae_both", 2, 0, 0, 0)]
     if "--only" in sys.argv:
         only = sys.argv[sys.argv.index("--only") + 1]
         variants = [v for v in variants if v[0] == only]
     res = {v[0]: ([], []) for v in variants}
     for _ in range(5):
         for name, ae, st, sk, fs in variants:
-            C.attn_ae(ae)
+            C.attn_ae(1 if ae else 0)
+            C.attn_ae_bwd(1 if ae == 2 else 0)
             C.attn_stagger(st)
             C.attn_skew(sk)
             C.attn_fwd_stagger(fs)
@@ -62,7 +63,8 @@ def main():
         print(json.dumps({"variant": name, "fwd_us": round(f, 1), "bwd_us": round(b, 1),
                           "fwd_tf": round(fl / f / 1e6, 1), "bwd_tf": round(2.5 * fl / b / 1e6, 1)}), flush=True)
     C.attn_ae(1)
-    C.attn_stagger(1)
+    C.attn_ae_bwd(0)
+    C.attn_stagger(0)
     C.attn_skew(0)
     C.attn_fwd_stagger(0)
 
