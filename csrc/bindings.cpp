@@ -99,6 +99,7 @@ int smi_gemm_wgrad_group(const void* const*, const long*, const void* const*, co
                          const int*, const int*, const int*, int, hipStream_t);
 int smi_cnn(const CNNArgs*, hipStream_t);
 int smi_cnn_fused_ok(int, int, int);
+long smi_emb_pair_max(long);
 int smi_emb_pair(int);
 int smi_cnn_reduce(const CNNArgs*, hipStream_t);
 int smi_gather_rows(const void*, const long long*, void*, long, long, hipStream_t);
@@ -559,6 +560,8 @@ PYBIND11_MODULE(_C, m) {
         "fp32 attention outputs: 1 = whole-row stores through LDS (default), 0 = per-lane stores; -1 queries");
   m.def("attn_stagger", [](int set) { return smi_attn_stagger(set); },
         "fp32 attention dK/dV: 1 = staggered 8-wave kernel (default), 0 = lockstep; -1 queries");
+  m.def("emb_pair_max", [](long set) { return smi_emb_pair_max(set); },
+        "largest token batch the pair-compare embedding backward takes (set < 0 queries)");
   m.def("emb_pair", [](int set) { return smi_emb_pair(set); },
         "deterministic embedding backward: 1 = pair-compare (<= 8192 tokens), 0 = bucketed lists; -1 queries");
   m.def("cnn_fused_ok", [](int C, int cin, int classes) { return smi_cnn_fused_ok(C, cin, classes) != 0; });

@@ -190,3 +190,29 @@ __device__ __forceinline__ void smi_lds_barrier() {
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
+
+// ---- hand-off between workgroups of ONE launch (ticketed last-workgroup reductions) ----
+// Each XCD has its own L2, not coherent with the others, so an agent-scope fence is L2 maintenance
+// of the whole XCD cache: release = buffer_wbl2 (write back every dirty line), acquire = buffer_inv
+// (measured: the CNN step 52 -> 84 us with one fence pair per workgroup).  Instead
+// (MI355X_MICROARCH "publish-large", "splitk-seam"): the producer writes what it hands off with
+// device-scope (sc1) stores, which write through to the coherence point, drains them
+// (smi_wt_drain, before the workgroup barrier that precedes the ticket; device atomics are
+// coherent) and the consumer reads them with device-scope (sc1) loads.  No fences.
+__device__ __forceinline__ void smi_wt_store(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float smi_cc_load(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// two floats as one 8-B granule (p 8-B aligned)
+__device__ __forceinline__ void smi_wt_store2(float* p, float a, float b) {
+  const unsigned long long v = (unsigned long long)__float_as_uint(a) | ((unsigned long long)__float_as_uint(b) << 32);
+  __hip_atomic_store((unsigned long long*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float2 smi_cc_load2(const float* p) {
+  const unsigned long long v = __hip_atomic_load((unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return make_float2(__uint_as_float((unsigned)v), __uint_as_float((unsigned)(v >> 32)));
+}
+__device__ __forceinline__ void smi_wt_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+

@@ -34,6 +34,7 @@ struct LSTMArgs {
   // fused cross-entropy on the last step (forward; labels non-null): per-sequence loss, the head
   // gradient dlast = (softmax - onehot) / B, and the mean loss through a last-workgroup ticket
   // (ce_tick: one zeroed counter, re-armed by the kernel)
+  // backward: ce_tick = the weight-gradient kernel's (L + 1) x 8 per-column-tile tickets (zeroed, re-armed)
   const long long* ce_labels; float* ce_row; float* ce_dlast; float* ce_loss; unsigned* ce_tick;
   const float* dpred_scale;                // backward: dpred x this device scalar (the loss's dloss)
 };

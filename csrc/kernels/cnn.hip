@@ -470,61 +470,53 @@ __device__ __forceinline__ void conv_wgrad_bf16(const float* __restrict__ dz, co
 }
 
 // Fused SGD tail (CNNArgs::fused): the step's remaining work without a second launch.  Level 1:
-// the last image of each group of CNN_GRP to finish (ticket; release / acquire fences around it)
-// sums the group's slabs in image order into part[group]; level 2: the last group to finish sums
-// the group partials in group order and applies torch SGD (p -= lr * g) to every parameter, then
-// the mean loss (image order) and the step counter.  Float4 passes (P % 4 == 0, checked by the
-// launcher) keep enough loads in flight for one workgroup to read a group's 8 x 31 KB slabs in a
-// few microseconds.  Deterministic: every sum has a fixed order.  No spinning: a workgroup that
-// is not the last simply exits.
+// the last image of each group of CNN_GRP to finish (ticket) sums the group's slabs in image order
+// into part[group]; level 2: the last group to finish sums the group partials in group order and
+// applies torch SGD (p -= lr * g) to every parameter, then the mean loss (image order) and the
+// step counter.  Hand-offs are write-through stores + device-scope loads (smi_common.h), no L2
+// fences; 8-B granules with every load of a thread's sum in flight together.  Deterministic:
+// every sum has a fixed order.  No spinning: a workgroup that is not the last simply exits.
 __device__ __noinline__ void cnn_fused_tail(const CNNArgs& g, int img) {
   __shared__ int last;
   const int ngrp = (g.B + CNN_GRP - 1) / CNN_GRP;
   const int grp = img / CNN_GRP, g0 = grp * CNN_GRP, g1 = min(g.B, g0 + CNN_GRP);
-  // every wave's slab stores complete (workgroup-scope release in the barrier), then ONE agent-
-  // scope release by thread 0 (it writes the CU's L2 back: cumulative over the workgroup's stores)
-  // before the ticket — a release per wave (16 per workgroup) made the step 2x slower
+  smi_wt_drain();  // this wave's slab stores reached the coherence point
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(g.tick + grp, 1u) == (unsigned)(g1 - g0 - 1);
-  }
+  if (threadIdx.x == 0) last = atomicAdd(g.tick + grp, 1u) == (unsigned)(g1 - g0 - 1);
   __syncthreads();
   if (!last) return;
-  __threadfence();  // acquire the group's slabs
-  const int P4 = g.P / 4;
-  const float4* slab4 = (const float4*)g.slab;
-  float4* part4 = (float4*)(g.part + (long)grp * g.P);
-  for (int q = threadIdx.x; q < P4; q += blockDim.x) {
-    float4 acc = slab4[(long)g0 * P4 + q];
-#pragma unroll 8
-    for (int i = g0 + 1; i < g1; ++i) {
-      const float4 v = slab4[(long)i * P4 + q];
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-    }
-    part4[q] = acc;
+  const int P2 = g.P / 2;
+  float* part = g.part + (long)grp * g.P;
+  for (int q = threadIdx.x; q < P2; q += blockDim.x) {
+    float2 v[CNN_GRP];
+#pragma unroll
+    for (int i = 0; i < CNN_GRP; ++i)
+      if (g0 + i < g1) v[i] = smi_cc_load2(g.slab + (long)(g0 + i) * g.P + 2 * q);
+    float2 acc = v[0];
+#pragma unroll
+    for (int i = 1; i < CNN_GRP; ++i)
+      if (g0 + i < g1) { acc.x += v[i].x; acc.y += v[i].y; }
+    smi_wt_store2(part + 2 * q, acc.x, acc.y);
   }
-  __syncthreads();  // the group sum stored by every wave (then released by thread 0)
+  smi_wt_drain();
+  __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();
     g.tick[grp] = 0u;  // re-arm (every image of the group has taken its ticket)
     last = atomicAdd(g.tick + CNN_GRP, 1u) == (unsigned)(ngrp - 1);
   }
   __syncthreads();
   if (!last) return;
-  __threadfence();  // acquire every group sum
   const float lr = g.lr[0];
-  const float4* pall = (const float4*)g.part;
-  for (int q = threadIdx.x; q < P4; q += blockDim.x) {
-    float4 s = pall[q];
+  for (int q = threadIdx.x; q < P2; q += blockDim.x) {
+    float2 s = smi_cc_load2(g.part + 2 * q);
     for (int k = 1; k < ngrp; ++k) {
-      const float4 v = pall[(long)k * P4 + q];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      const float2 v = smi_cc_load2(g.part + (long)k * g.P + 2 * q);
+      s.x += v.x; s.y += v.y;
     }
-    const float sv[4] = {s.x, s.y, s.z, s.w};
+    const float sv[2] = {s.x, s.y};
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int p = 4 * q + e;
+    for (int e = 0; e < 2; ++e) {
+      const int p = 2 * q + e;
       int seg = 0;
       while (seg < 9 && p >= g.off[seg + 1]) ++seg;
       float* dst = (float*)(seg % 2 == 0 ? g.w[seg / 2] : g.b[seg / 2]) + (p - g.off[seg]);
@@ -535,7 +527,7 @@ __device__ __noinline__ void cnn_fused_tail(const CNNArgs& g, int img) {
   }
   if (threadIdx.x < 64) {
     float ls = 0.f;
-    for (int i = threadIdx.x; i < g.B; i += 64) ls += g.row_loss[i];
+    for (int i = threadIdx.x; i < g.B; i += 64) ls += smi_cc_load(g.row_loss + i);
     ls = wave_sum(ls);
     if (threadIdx.x == 0) {
       if (g.loss) g.loss[0] = ls * g.loss_scale;
@@ -617,7 +609,7 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
     for (int o = 0; o < NC; ++o) se += __expf(lg[o] - m);
     const float lse = m + __logf(se);
     const long long lab = g.y ? g.y[img] : 0;
-    if (g.row_loss) g.row_loss[img] = lse - lg[lab];
+    if (g.row_loss) smi_wt_store(g.row_loss + img, lse - lg[lab]);  // read by the last workgroup
     if (g.pred) g.pred[img] = am;
     if (g.logits)
       for (int o = 0; o < NC; ++o) g.logits[(long)img * NC + o] = lg[o];
@@ -630,14 +622,11 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   // row_loss in image order with wave 0 and re-arms the ticket
   if (g.loss && g.row_loss && !g.fused) {
     __shared__ int cnn_last;
+    smi_wt_drain();
     __syncthreads();
-    if (threadIdx.x == 0) {
-      __threadfence();
-      cnn_last = atomicAdd(&cnn_loss_ticket, 1u) == gridDim.x - 1;
-    }
+    if (threadIdx.x == 0) cnn_last = atomicAdd(&cnn_loss_ticket, 1u) == gridDim.x - 1;
     __syncthreads();
     if (cnn_last && threadIdx.x < 64) {
-      __threadfence();
       float s = 0.f;
       for (int i = threadIdx.x; i < g.B; i += 64)
         s += __hip_atomic_load(g.row_loss + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -653,8 +642,8 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   STAMP(9);
   float* gs = g.slab + (long)img * g.P;  // this image's gradient slab
   // fc grads: gW[o][i] = dl[o] * p2[i]; gb[o] = dl[o]; dp2[i] = sum_o W[o][i] dl[o] (into p2 buffer after)
-  for (int e = threadIdx.x; e < NC * F; e += blockDim.x) gs[g.off[8] + e] = lg[e / F] * p2[e % F];
-  for (int o = threadIdx.x; o < NC; o += blockDim.x) gs[g.off[9] + o] = lg[o];
+  for (int e = threadIdx.x; e < NC * F; e += blockDim.x) smi_wt_store(gs + g.off[8] + e, lg[e / F] * p2[e % F]);
+  for (int o = threadIdx.x; o < NC; o += blockDim.x) smi_wt_store(gs + g.off[9] + o, lg[o]);
   __syncthreads();
   STAMP(10);
   for (int i = threadIdx.x; i < F; i += blockDim.x) {
@@ -674,7 +663,7 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   __syncthreads();
   STAMP(13);
   for (int e = threadIdx.x; e < C * C * 9 + C; e += blockDim.x) {
-    gs[(e < C * C * 9 ? g.off[6] + e : g.off[7] + e - C * C * 9)] = wacc[e];
+    smi_wt_store(gs + (e < C * C * 9 ? g.off[6] + e : g.off[7] + e - C * C * 9), wacc[e]);
     wacc[e] = 0.f;
   }
   if (BF) conv_mfma<14, P14, true, true>(a4, C, a3, C, g.w[3], nullptr, wscr);
@@ -687,7 +676,7 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   __syncthreads();
   STAMP(15);
   for (int e = threadIdx.x; e < C * C * 9 + C; e += blockDim.x) {
-    gs[(e < C * C * 9 ? g.off[4] + e : g.off[5] + e - C * C * 9)] = wacc[e];
+    smi_wt_store(gs + (e < C * C * 9 ? g.off[4] + e : g.off[5] + e - C * C * 9), wacc[e]);
     wacc[e] = 0.f;
   }
   if (BF) conv_mfma<14, P14, true, false>(a3, C, p1, C, g.w[2], nullptr, wscr);
@@ -704,7 +693,7 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   __syncthreads();
   STAMP(18);
   for (int e = threadIdx.x; e < C * C * 9 + C; e += blockDim.x) {
-    gs[(e < C * C * 9 ? g.off[2] + e : g.off[3] + e - C * C * 9)] = wacc[e];
+    smi_wt_store(gs + (e < C * C * 9 ? g.off[2] + e : g.off[3] + e - C * C * 9), wacc[e]);
     wacc[e] = 0.f;
   }
   if (BF) conv_mfma<28, P28, true, true>(a2, C, a1, C, g.w[1], nullptr, wscr);
@@ -717,7 +706,7 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   __syncthreads();
   STAMP(20);
   for (int e = threadIdx.x; e < C * CI * 9 + C; e += blockDim.x)
-    gs[(e < C * CI * 9 ? g.off[0] + e : g.off[1] + e - C * CI * 9)] = wacc[e];
+    smi_wt_store(gs + (e < C * CI * 9 ? g.off[0] + e : g.off[1] + e - C * CI * 9), wacc[e]);
   if (g.fused) cnn_fused_tail(g, img);
 }
 

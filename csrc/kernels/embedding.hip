@@ -408,7 +408,7 @@ __global__ __launch_bounds__(256) void emb_det_combine(float* __restrict__ dtabl
 //  2. emb_pair_plan (one workgroup, all tokens in LDS): group sizes per first position (LDS integer
 //     adds: order-independent), exclusive scans, member lists in position order
 //     (list[off[first] + rank] = p), and chunks of at most EMB_CH members per group;
-//  3. emb_pair_sum (one workgroup per chunk): the chunk's member rows summed in position order;
+//  3. emb_pair_sum (one wave per chunk): the chunk's member rows summed in position order;
 //     a one-chunk group adds its sum to its table row, a longer group's chunks write partials and
 //     the group's last chunk to finish (ticket) adds them in chunk order.
 // Every table row is one fixed-order fp32 sum: bit-reproducible, and long groups (a frequent word)
@@ -514,27 +514,28 @@ __global__ __launch_bounds__(1024) void emb_pair_plan(long T, EmbPair e) {
 }
 
 template <typename TS>
-__global__ __launch_bounds__(128) void emb_pair_sum(const long long* __restrict__ ids, const TS* __restrict__ dout,
-                                                    float* __restrict__ dtable, int D, EmbPair e,
-                                                    const uint32_t* seedp, uint32_t salt, uint32_t thresh,
-                                                    float dscale) {
-  const int k = blockIdx.x;
-  if (k >= *e.nchunks) return;
-  __shared__ int s_mem[EMB_CH];
-  __shared__ int s_last;
+__global__ __launch_bounds__(1024) void emb_pair_sum(const long long* __restrict__ ids, const TS* __restrict__ dout,
+                                                     float* __restrict__ dtable, int D, EmbPair e,
+                                                     const uint32_t* seedp, uint32_t salt, uint32_t thresh,
+                                                     float dscale) {
+  // one WAVE per chunk (16 per workgroup): a workgroup per chunk left the chip latency-bound on
+  // thousands of one- or two-row chunks (transformer batch: 135 us per call); member positions
+  // held one per lane and broadcast by __shfl — no LDS, no workgroup barrier
+  const int lane = threadIdx.x & 63;
+  const int k = blockIdx.x * 16 + (threadIdx.x >> 6);
+  if (k >= *e.nchunks) return;  // wave-uniform
   const int start = e.ch_start[k], len = e.ch_len[k], g0 = e.ch_g0[k], gn = e.ch_gn[k];
-  if (threadIdx.x < len) s_mem[threadIdx.x] = e.list[start + threadIdx.x];
-  __syncthreads();
+  const int mine = lane < len ? e.list[start + lane] : 0;
   const long long id = ids[e.ch_owner[k]];
   const uint32_t seed = thresh ? smi_seed(seedp, salt) : 0u;
-  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+  for (int c = lane; c < D; c += 64) {
     float acc = 0.f;
     int m = 0;
     for (; m + 4 <= len; m += 4) {  // four rows in flight, added in position order
       float v[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const long t = s_mem[m + u];
+        const long t = __shfl(mine, m + u, 64);
         v[u] = emb_ld(dout + t * D + c);
         if (thresh) v[u] = smi_keep(seed, (uint32_t)(t * D + c), thresh) ? v[u] * dscale : 0.f;
       }
@@ -544,30 +545,25 @@ __global__ __launch_bounds__(128) void emb_pair_sum(const long long* __restrict_
       acc += v[3];
     }
     for (; m < len; ++m) {
-      const long t = s_mem[m];
+      const long t = __shfl(mine, m, 64);
       float v = emb_ld(dout + t * D + c);
       if (thresh) v = smi_keep(seed, (uint32_t)(t * D + c), thresh) ? v * dscale : 0.f;
       acc += v;
     }
     if (gn == 1) dtable[id * D + c] += acc;
-    else e.part[(long)k * D + c] = acc;
+    else smi_wt_store(e.part + (long)k * D + c, acc);  // write-through hand-off (smi_common.h)
   }
   if (gn == 1) return;
-  __syncthreads();  // every wave's partial stored; thread 0's agent release covers the workgroup
-  if (threadIdx.x == 0) {
-    __threadfence();
-    s_last = atomicAdd(e.tick + g0, 1u) == (unsigned)gn - 1;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();
-  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+  smi_wt_drain();  // this wave's partial reached the coherence point
+  int last = 0;
+  if (lane == 0) last = atomicAdd(e.tick + g0, 1u) == (unsigned)gn - 1;
+  if (!__shfl(last, 0, 64)) return;
+  for (int c = lane; c < D; c += 64) {
     float acc = 0.f;
-    for (int j = 0; j < gn; ++j) acc += __hip_atomic_load(e.part + (long)(g0 + j) * D + c, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT);
+    for (int j = 0; j < gn; ++j) acc += smi_cc_load(e.part + (long)(g0 + j) * D + c);  // chunk order
     dtable[id * D + c] += acc;
   }
-  if (threadIdx.x == 0) e.tick[g0] = 0u;
+  if (lane == 0) e.tick[g0] = 0u;
 }
 
 static long emb_pair_ws_bytes(long T, long D) {
@@ -595,6 +591,20 @@ extern "C" long smi_emb_det_ws_bytes(long T, long V, long D) {
 
 // deterministic backward algorithm: 1 = pair-compare (<= EMB_PAIR_MAX tokens, default), 0 = the
 // bucketed lists (SMI_EMB_BWD=det)
+// batches the pair path takes by default: the all-pairs rank grows as T^2 — at the transformer's
+// 8192 tokens it measured 40 us per call against the bucketed path's ~70 us for everything
+// (profiles/r4e_fp32_step.txt); the LSTM's 4128 tokens gain (SMI_EMB_PAIR_MAX overrides, <= 8192)
+static long g_emb_pair_sel = -1;
+extern "C" long smi_emb_pair_max(long set) {  // set < 0: query
+  if (set >= 0) g_emb_pair_sel = set > EMB_PAIR_MAX ? EMB_PAIR_MAX : set;
+  if (g_emb_pair_sel < 0) {
+    const char* ev = getenv("SMI_EMB_PAIR_MAX");
+    g_emb_pair_sel = ev ? atol(ev) : 4608;
+    if (g_emb_pair_sel > EMB_PAIR_MAX) g_emb_pair_sel = EMB_PAIR_MAX;
+  }
+  return g_emb_pair_sel;
+}
+static long emb_pair_sel() { return smi_emb_pair_max(-1); }
 static int g_emb_pair = -1;
 extern "C" int smi_emb_pair(int set) {
   if (set == 0 || set == 1) g_emb_pair = set;
@@ -609,7 +619,7 @@ template <typename TS>
 static int emb_bwd_launch(const long long* ids, const void* dout, float* dtable, long T, int D, long long padding_idx,
                           const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, long V, void* ws,
                           hipStream_t st) {
-  if (ws && V > 0 && T > 0 && T <= EMB_PAIR_MAX && smi_emb_pair(-1)) {
+  if (ws && V > 0 && T > 0 && T <= emb_pair_sel() && smi_emb_pair(-1)) {
     EmbPair e{};
     int* p = (int*)ws;
     e.rank = p; p += T;
@@ -625,7 +635,7 @@ static int emb_bwd_launch(const long long* ids, const void* dout, float* dtable,
     e.part = (float*)p;
     hipLaunchKernelGGL(emb_pair_rank, dim3((unsigned)((T + 63) / 64)), dim3(1024), 0, st, ids, T, padding_idx, e);
     hipLaunchKernelGGL(emb_pair_plan, dim3(1), dim3(1024), 0, st, T, e);
-    hipLaunchKernelGGL(emb_pair_sum<TS>, dim3((unsigned)T), dim3(128), 0, st, ids, (const TS*)dout, dtable, D, e, seedp,
+    hipLaunchKernelGGL(emb_pair_sum<TS>, dim3((unsigned)((T + 15) / 16)), dim3(1024), 0, st, ids, (const TS*)dout, dtable, D, e, seedp,
                        salt, thresh, dscale);
     return (int)hipGetLastError();
   }

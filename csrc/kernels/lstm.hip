@@ -61,7 +61,7 @@ __device__ __forceinline__ uint32_t lstm_drop_idx(int b, int t, int l, int j, in
 // Fused CE on the last step's prediction (LSTMArgs::ce_labels; distributed_lstm.py:189
 // CrossEntropyLoss(pred[:, -1, :], labels - 1) with its mean): thread 0 of sequence b's workgroup
 // computes the row loss and the head gradient (softmax - onehot) / B from the logits in LDS; the
-// last workgroup to finish (ticket, release / acquire fences) sums the row losses in sequence
+// last workgroup to finish (ticket; write-through hand-off) sums the row losses in sequence
 // order.  Replaces three launches (CE forward, finalize, backward) per step.
 __device__ __noinline__ void lstm_ce_tail(const LSTMArgs& a, int b, const float* s_plast) {
   __shared__ int s_lastwg;
@@ -74,15 +74,14 @@ __device__ __noinline__ void lstm_ce_tail(const LSTMArgs& a, int b, const float*
     for (int c = 0; c < C; ++c) se += __expf(s_plast[c] - m);
     const float lse = m + __logf(se);
     const long long lab = a.ce_labels[b];
-    a.ce_row[b] = lse - s_plast[lab];
+    smi_wt_store(a.ce_row + b, lse - s_plast[lab]);  // read by the last workgroup (smi_common.h)
     const float inv = 1.0f / (float)a.B;
     for (int c = 0; c < C; ++c) a.ce_dlast[(size_t)b * C + c] = (__expf(s_plast[c] - lse) - (c == lab ? 1.f : 0.f)) * inv;
-    __threadfence();
+    smi_wt_drain();
     s_lastwg = atomicAdd(a.ce_tick, 1u) == (unsigned)a.B - 1;
   }
   __syncthreads();
   if (s_lastwg && threadIdx.x < 64) {
-    __threadfence();
     float sum = 0.f;
     for (int i = threadIdx.x; i < a.B; i += 64) sum += __hip_atomic_load(a.ce_row + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sum = wave_sum(sum);
@@ -904,14 +903,18 @@ __global__ __launch_bounds__(256) void lstm_wgrad_combine(LSTMArgs a) {
 // chain per accumulator — the reference's fp32 precision).
 //   dW_l[r][c] = sum over all B*T (b,t) of da_l[b,t][r] * x_l[b,t][c]   (x = [input | h_{t-1} | 1])
 //   xe[b,t][e] = sum_r da_0[b,t][r] * W_ih0[r][e]
-// A weight-gradient workgroup owns one 16 x 16 output tile; its 8 waves split the (b,t) reduction
-// into 8 fixed ranges, and the 8 partial tiles are summed in wave order through LDS: bit-
-// reproducible without a second launch, a slab or float atomics (lstm_wgrad_partial + _combine
-// did the same reduction on the VALU in two launches).  Workgroups past the weight tiles compute
-// xe: each wave one 16 x 16 tile (K = 4H).  Operand layouts (16x16x4 f32): lane l holds A row /
-// B column l & 15 at k = l >> 4; the accumulator's register j of lane l is row 4 (l >> 4) + j,
-// column l & 15.
+// Workgroup (chunk s, column tile ct, layer l): its (b,t) range is staged through LDS in rounds of
+// LW_KR rows with every load of a round in flight at once (a per-lane gather loop was latency-
+// bound: 117 us), wave w accumulates row tile w of the 16-column slice over the whole range, the
+// partial tile goes to the slab, and the LAST of the nch chunk workgroups of (l, ct) — a ticket
+// per column tile — sums the nch partials in chunk order (bit-reproducible, no float atomics, no
+// second launch).  The (chunk, ct = 0, l = 0) workgroups also turn their staged da_0 rows into xe
+// rows against W_ih0 (staged once).  Operand layouts (16x16x4 f32): lane l holds A row / B column
+// l & 15 at k = l >> 4; the accumulator's register j of lane l is row 4 (l >> 4) + j, column l & 15.
 #define LW_WAVES 8
+#define LW_KR 64    // (b,t) rows per LDS round
+#define LW_PD 144   // s_d pitch: >= 4H (128); == 16 mod 64 -> the 4 k-rows of an A read hit distinct banks
+#define LW_PW 48    // s_w pitch (E <= 32)
 __device__ __forceinline__ float lw_d(const LSTMArgs& a, int l, int b, int t, int r, int rows) {
   if (r >= rows) return 0.f;
   if (l < a.L) return a.ws_da[(((size_t)b * a.L + l) * a.T + t) * 4 * a.H + r];
@@ -936,109 +939,142 @@ __device__ __forceinline__ float lw_x(const LSTMArgs& a, int l, int b, int t, in
   }
   return 1.f;
 }
-__host__ __device__ __forceinline__ int lw_tiles(const LSTMArgs& a, int l) {
-  return ((lstm_rows(a, l) + 15) / 16) * ((lstm_cols(a, l) + 15) / 16);
+// chunks of the (b,t) reduction: one per ~2 LDS rounds, at most LSTM_KS (the slab's capacity)
+static inline int lw_chunks(const LSTMArgs& a) {
+  const long BT = (long)a.B * a.T;
+  const long n = (BT + 2 * LW_KR - 1) / (2 * LW_KR);
+  return (int)(n < 1 ? 1 : (n > LSTM_KS ? LSTM_KS : n));
 }
-__host__ __device__ __forceinline__ int lw_wgrad_blocks(const LSTMArgs& a) {
-  int n = 0;
-  for (int l = 0; l <= a.L; ++l) n += lw_tiles(a, l);
-  return n;
+static inline int lw_ctiles(const LSTMArgs& a) {
+  int m = 0;
+  for (int l = 0; l <= a.L; ++l) m = max(m, (lstm_cols(a, l) + 15) / 16);
+  return m;
 }
+#define LW_TICKS 8  // ticket slots per layer (column tiles; cols <= 128)
 #define MF16F32(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
 
 __global__ __launch_bounds__(64 * LW_WAVES) void lstm_wgrad_mfma(LSTMArgs a) {
-  __shared__ float part[LW_WAVES][256];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __shared__ float s_d[LW_KR * LW_PD];
+  __shared__ float s_x[LW_KR * 16];
+  __shared__ float s_w[128 * LW_PW];
+  __shared__ int s_last;
+  const int s = blockIdx.x, ct = blockIdx.y, l = blockIdx.z;
+  const int rows = lstm_rows(a, l), cols = lstm_cols(a, l);
+  if (ct * 16 >= cols) return;  // uniform per workgroup; never counted by the ticket
+  const int c0 = ct * 16;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int li = lane & 15, lk = lane >> 4;
-  const long BT = (long)a.B * a.T;
-  int tile = blockIdx.x;
-  const int nw = lw_wgrad_blocks(a);
+  const int T = a.T, L = a.L, G = 4 * a.H, E = a.E;
+  const int nch = gridDim.x;
+  const long BT = (long)a.B * T, kc = (BT + nch - 1) / nch;
+  const long kb = (long)s * kc, ke = min(BT, kb + kc);
+  const int rt = (rows + 15) / 16, rp = rt * 16;  // row tiles (<= LW_WAVES), padded rows
+  const uint32_t seed = smi_seed(a.seedp, a.salt);
+  const bool do_xe = l == 0 && ct == 0 && a.g_xe;
+  if (do_xe)
+    for (int i = tid; i < G * E; i += 64 * LW_WAVES) s_w[(i / E) * LW_PW + i % E] = a.w_ih[0][i];
   f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-  if (tile >= nw) {
-    // xe tiles: one per wave (uniform per wave)
-    if (!a.g_xe) return;
-    const int G = 4 * a.H, E = a.E;
-    const int ecols = (E + 15) / 16;
-    const long xt = (long)(tile - nw) * LW_WAVES + w;
-    const long bt0 = (xt / ecols) * 16;
-    const int e0 = (int)(xt % ecols) * 16;
-    if (bt0 >= BT) return;
-    const long bt = bt0 + li;
-    const int b = (int)(bt / a.T), t = (int)(bt % a.T);
-    const float* d = a.ws_da + (((size_t)b * a.L) * a.T + t) * G;  // layer 0
-    const bool okr = bt < BT, okc = e0 + li < E;
-    const float* wcol = a.w_ih[0] + e0 + li;
-#pragma unroll 4
-    for (int k0 = 0; k0 < G; k0 += 4) {
-      const int k = k0 + lk;
-      const float av = okr ? d[k] : 0.f;
-      const float bv = okc ? wcol[(size_t)k * E] : 0.f;
-      acc = MF16F32(av, bv, acc);
-    }
-    if (okc) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const long r = bt0 + 4 * lk + j;
-        if (r < BT) a.g_xe[r * E + e0 + li] = acc[j];
+  for (long k = kb; k < ke; k += LW_KR) {
+    const int nk = (int)min((long)LW_KR, ke - k), nk4 = (nk + 3) & ~3;
+    __syncthreads();  // the previous round's LDS reads are done
+    if (l < L) {  // da rows: 16-B loads, every one of the round in flight together
+      const int q4 = rp / 4;
+      for (int i = tid; i < nk4 * q4; i += 64 * LW_WAVES) {
+        const int kk = i / q4, q = i - kk * q4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (kk < nk) {
+          const long bt = k + kk;
+          const int b = (int)(bt / T), t = (int)(bt - (long)b * T);
+          v = *(const float4*)(a.ws_da + (((size_t)b * L + l) * T + t) * G + 4 * q);
+        }
+        *(float4*)(s_d + kk * LW_PD + 4 * q) = v;
+      }
+    } else {
+      for (int i = tid; i < nk4 * rp; i += 64 * LW_WAVES) {
+        const int kk = i / rp, r = i - kk * rp;
+        float v = 0.f;
+        if (kk < nk) {
+          const long bt = k + kk;
+          const int b = (int)(bt / T), t = (int)(bt - (long)b * T);
+          v = lw_d(a, l, b, t, r, rows);
+        }
+        s_d[kk * LW_PD + r] = v;
       }
     }
-    return;
-  }
-  int l = 0;
-  while (tile >= lw_tiles(a, l)) tile -= lw_tiles(a, l++);
-  const int rows = lstm_rows(a, l), cols = lstm_cols(a, l);
-  const int ctn = (cols + 15) / 16;
-  const int r0 = (tile / ctn) * 16, c0 = (tile % ctn) * 16;
-  const uint32_t seed = smi_seed(a.seedp, a.salt);
-  // wave w reduces (b,t) rows [k_begin, k_end), 4 per MFMA
-  const long kc = ((BT + LW_WAVES - 1) / LW_WAVES + 3) / 4 * 4;
-  const long kb = w * kc, ke = min(BT, kb + kc);
-  // (b, t) of this lane's k = k0 + 4u + lk, advanced by 16 per step without dividing (an integer
-  // division by the runtime T per element made the gather VALU-bound)
-  int bu[4], tu[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const long k = kb + 4 * u + lk;
-    bu[u] = (int)(k / a.T);
-    tu[u] = (int)(k - (long)bu[u] * a.T);
-  }
-  for (long k0 = kb; k0 < ke; k0 += 16) {
-    float av[4], bv[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const bool ok = k0 + 4 * u + lk < ke;
-      av[u] = ok ? lw_d(a, l, bu[u], tu[u], r0 + li, rows) : 0.f;
-      bv[u] = ok ? lw_x(a, l, bu[u], tu[u], c0 + li, cols, seed) : 0.f;
+    for (int i = tid; i < nk4 * 16; i += 64 * LW_WAVES) {
+      const int kk = i >> 4, cc = i & 15;
+      float v = 0.f;
+      if (kk < nk) {
+        const long bt = k + kk;
+        const int b = (int)(bt / T), t = (int)(bt - (long)b * T);
+        v = lw_x(a, l, b, t, c0 + cc, cols, seed);
+      }
+      s_x[kk * 16 + cc] = v;
     }
+    __syncthreads();
+    if (w < rt) {
+#pragma unroll 4
+      for (int k0 = 0; k0 < nk4; k0 += 4)
+        acc = MF16F32(s_d[(k0 + lk) * LW_PD + w * 16 + li], s_x[(k0 + lk) * 16 + li], acc);
+    }
+    if (do_xe) {  // xe rows of this round: (row tile, 16-column group) per wave
+      const int et = (E + 15) / 16, xt = ((nk + 15) / 16) * et;
+      for (int x = w; x < xt; x += LW_WAVES) {
+        const int r16 = (x / et) * 16, e0 = (x % et) * 16;
+        f32x4_t xa = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+        for (int kr = 0; kr < G; kr += 4) {
+          const float av = r16 + li < nk ? s_d[(r16 + li) * LW_PD + kr + lk] : 0.f;
+          xa = MF16F32(av, s_w[(kr + lk) * LW_PW + e0 + li], xa);
+        }
+        if (e0 + li < E) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      acc = MF16F32(av[u], bv[u], acc);
-      tu[u] += 16;
-      while (tu[u] >= a.T) { tu[u] -= a.T; ++bu[u]; }
+          for (int j = 0; j < 4; ++j) {
+            const int rr = r16 + 4 * lk + j;
+            if (rr < nk) a.g_xe[(k + rr) * E + e0 + li] = xa[j];
+          }
+        }
+      }
     }
   }
+  // this chunk's partial of the slice: [rows][cols] tile s of layer l in the slab
+  float* part = a.g_slab + lstm_part_off(a, l, s);
+  if (w < rt && c0 + li < cols) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) part[w][(4 * lk + j) * 16 + li] = acc[j];
+    for (int j = 0; j < 4; ++j) {
+      const int r = w * 16 + 4 * lk + j;
+      if (r < rows) smi_wt_store(part + (size_t)r * cols + c0 + li, acc[j]);  // write-through hand-off
+    }
+  }
+  smi_wt_drain();
   __syncthreads();
-  if (threadIdx.x >= 256) return;
-  const int rr = threadIdx.x >> 4, cc = threadIdx.x & 15;
-  const int r = r0 + rr, c = c0 + cc;
-  if (r >= rows || c >= cols) return;
-  float v = 0.f;
-#pragma unroll
-  for (int q = 0; q < LW_WAVES; ++q) v += part[q][threadIdx.x];  // wave (= (b,t) range) order
-  if (l == a.L) {
-    if (c < a.H) a.g_w_fc[(size_t)r * a.H + c] += v;
-    else a.g_b_fc[r] += v;
-    return;
+  if (tid == 0) s_last = atomicAdd(a.ce_tick + l * LW_TICKS + ct, 1u) == (unsigned)nch - 1;
+  __syncthreads();
+  if (!s_last) return;
+  const int In = l < L ? (l == 0 ? E : a.H) : 0;
+  for (int p = tid; p < rows * 16; p += 64 * LW_WAVES) {
+    const int r = p >> 4, c = c0 + (p & 15);
+    if (c >= cols) continue;
+    const size_t o = (size_t)r * cols + c;
+    float v = 0.f;
+#pragma unroll 8
+    for (int q = 0; q < nch; ++q) v += smi_cc_load(a.g_slab + lstm_part_off(a, l, q) + o);  // chunk order
+    if (l == L) {
+      if (c < a.H) a.g_w_fc[(size_t)r * a.H + c] += v;
+      else a.g_b_fc[r] += v;
+    } else if (c < In) a.g_w_ih[l][(size_t)r * In + c] += v;
+    else if (c < In + a.H) a.g_w_hh[l][(size_t)r * a.H + (c - In)] += v;
+    else {
+      a.g_b_ih[l][r] += v;
+      a.g_b_hh[l][r] += v;
+    }
   }
-  const int In = l == 0 ? a.E : a.H;
-  if (c < In) a.g_w_ih[l][(size_t)r * In + c] += v;
-  else if (c < In + a.H) a.g_w_hh[l][(size_t)r * a.H + (c - In)] += v;
-  else {
-    a.g_b_ih[l][r] += v;
-    a.g_b_hh[l][r] += v;
-  }
+  if (tid == 0) a.ce_tick[l * LW_TICKS + ct] = 0u;  // re-armed for the next step (graph replay)
+}
+
+// the MFMA form's limits: 4H (and C) <= 128 rows, E <= 32, column tiles <= LW_TICKS
+static bool lw_fits(const LSTMArgs& a) {
+  return 4 * a.H <= 128 && a.C <= 128 && a.E <= 32 && lw_ctiles(a) <= LW_TICKS && a.ce_tick != nullptr;
 }
 
 // SMI_LSTM_WGRAD=valu: the two-launch VALU split-K reduction above (+ lstm_xe_kernel)
@@ -1141,10 +1177,9 @@ extern "C" int smi_lstm(const LSTMArgs* a, int backward, hipStream_t st) {
   else if (H == 32) rc = wide ? lstm_launch<32, 64>(a, backward, st) : lstm_launch<32, 32>(a, backward, st);
   else rc = lstm_launch<64, 64>(a, backward, st);
   if (rc || !backward) return rc;
-  if (lstm_wgrad_mfma_enabled()) {
-    const long xtiles = a->g_emb ? ((long)a->B * a->T + 15) / 16 * ((a->E + 15) / 16) : 0;
-    const long nblk = lw_wgrad_blocks(*a) + (xtiles + LW_WAVES - 1) / LW_WAVES;
-    hipLaunchKernelGGL(lstm_wgrad_mfma, dim3((unsigned)nblk), dim3(64 * LW_WAVES), 0, st, *a);
+  if (lstm_wgrad_mfma_enabled() && lw_fits(*a)) {
+    // ce_tick (backward): (L + 1) x LW_TICKS zeroed counters, re-armed by the kernel
+    hipLaunchKernelGGL(lstm_wgrad_mfma, dim3(lw_chunks(*a), lw_ctiles(*a), a->L + 1), dim3(64 * LW_WAVES), 0, st, *a);
     if ((rc = (int)hipGetLastError())) return rc;
     if (a->g_emb)
       return smi_emb_bwd_f32(a->ids, a->g_xe, a->g_emb, (long)a->B * a->T, a->E, a->pad_idx, nullptr, 0, 0, 1.f, a->V,

@@ -196,15 +196,14 @@ __global__ __launch_bounds__(64) void mlp_kernel(MLPArgs a, int mode) {
   }
   // publish this block's partials, the last block to arrive reduces them in block order
   float* part = a.ws + (long)blockIdx.x * (T + 1);
-  if (mode > 0)
-    for (int i = lane; i < T; i += 64) part[i] = gacc[i];
-  if (lane == 0) part[T] = lsum;
-  __threadfence();
+  if (mode > 0)  // write-through hand-off to the last block (smi_common.h), no L2 fences
+    for (int i = lane; i < T; i += 64) smi_wt_store(part + i, gacc[i]);
+  if (lane == 0) smi_wt_store(part + T, lsum);
+  smi_wt_drain();
   __syncthreads();
   if (lane == 0) last = atomicAdd(a.ticket, 1u) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
-  __threadfence();
   mlp_finalize(a, mode, T, gacc, lsum);
   if (lane == 0) a.ticket[0] = 0u;  // re-arm for the next launch (stream-ordered)
 }

@@ -152,8 +152,8 @@ class LSTMFn(torch.autograd.Function):
                          [lw[0].data_ptr() for lw in g_layers], [lw[1].data_ptr() for lw in g_layers],
                          [lw[2].data_ptr() for lw in g_layers], [lw[3].data_ptr() for lw in g_layers],
                          g_fc.data_ptr(), g_bfc.data_ptr(), _native.ptr(dh0), _native.ptr(dc0), slab.data_ptr(),
-                         _native.ptr(xe), emb.shape[0], _native.ptr(ews), 0, last_only, 0, 0, 0, 0, 0,
-                         _native.ptr(dscale), _native.stream())
+                         _native.ptr(xe), emb.shape[0], _native.ptr(ews), 0, last_only, 0, 0, 0, 0,
+                         _ce_ticket(dev)[8:].data_ptr(), _native.ptr(dscale), _native.stream())
         grad_ready(*orig)
         return (None, dh0 if ctx.has_h0 else None, dc0 if ctx.has_c0 else None, None) + (None,) * len(params)
 
@@ -162,11 +162,12 @@ _CE_TICKETS = {}
 
 
 def _ce_ticket(dev):
-    """The fused CE's ticket counter (zeroed once, re-armed by the kernel); one per device — a
-    step's forward completes its ticket round before the next forward on the stream starts."""
+    """Ticket counters (zeroed once, re-armed by the kernels), one block per device: [0] the fused
+    CE of the forward, [8:] the backward weight-gradient kernel's (L + 1) x 8 column-tile tickets —
+    each launch completes its ticket rounds before the next one on the stream starts."""
     t = _CE_TICKETS.get(dev)
     if t is None:
-        t = _CE_TICKETS[dev] = torch.zeros(1, device=dev, dtype=torch.int32)
+        t = _CE_TICKETS[dev] = torch.zeros(8 + 8 * 5, device=dev, dtype=torch.int32)
     return t
 
 

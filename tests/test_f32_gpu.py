@@ -523,7 +523,7 @@ def test_transformer_f32_gradients_match_cpu_across_salts():
     from sparkmi.utils.flat import FlatParams
     import copy
     from sparkmi.models.transformer import Transformer
-    bad = []
+    bad, ties = [], []
     for burn in range(0, 1024, 16):
         torch.manual_seed(0)
         mc = Transformer(d_model=128, ffn_hidden=256, num_heads=2, num_layers=3, max_sequence_length=32,
@@ -534,8 +534,13 @@ def test_transformer_f32_gradients_match_cpu_across_salts():
         fg = FlatParams(mg, shadow=False)
         src, tgt = translation_pairs(4, 32, 96, 96, seed=3)
         fg.zero_grad()
-        lc = mc.training_step_loss(src, tgt)
-        lg = mg.training_step_loss(src.to(dev), tgt.to(dev))
+        with _relu_ties_follow_gpu() as tie:
+            lg = mg.training_step_loss(src.to(dev), tgt.to(dev))
+            tie.replay()
+            lc = mc.training_step_loss(src, tgt)
+        if tie.flips:
+            ties.append((burn, tie.flips))
+        bad += [(burn, "relu tie", m) for m in tie.bad]
         if abs(float(lc) - float(lg)) >= 1e-5 * max(1.0, abs(float(lc))):
             bad.append((burn, "loss", float(lc), float(lg)))
         lc.backward()
@@ -545,7 +550,58 @@ def test_transformer_f32_gradients_match_cpu_across_salts():
             rel = float((pg.grad.cpu().double() - pc.grad.double()).norm() / (pc.grad.double().norm() + 1e-12))
             if not rel < 1e-4:
                 bad.append((burn, n, rel))
+    print("relu ties decided differently on the GPU (salt offset, count):", ties)
     assert not bad, f"{len(bad)} mismatches: {bad}"
+
+
+class _relu_ties_follow_gpu:
+    """Root cause of the salt-dependent mismatch: ReLU(z) is discontinuous in
+    its derivative, and an FFN pre-activation z within rounding of 0 can land on opposite sides
+    on the GPU and the CPU (their fp32 sums differ in the last bits: different reduction orders).
+    The gradient of that hidden unit then flows on one device and not the other — a 1e-2 error in
+    linear1's weight gradient that every earlier layer inherits (tools/dbg_salt81.py: at salt base
+    81 every individual GEMM call matches its own inputs to 1.5e-7, tools/dbg_salt81b.py).  Here
+    the CPU reference takes the GPU's side of every such tie: the GPU's FFN hidden activations are
+    recorded, and where the CPU's sign disagrees the CPU uses the GPU value — allowed only when
+    both are rounding-level (|h| <= 1e-5 max|h|); anything larger is reported as a mismatch."""
+
+    def __enter__(self):
+        from sparkmi.ops import linear as LIN
+        from sparkmi.ops import planes as PL
+        self.LIN, self.flips, self.bad, self.rec, self.i = LIN, 0, [], [], None
+        self.nat, self.ref = LIN._fwd_native, LIN._ref_fwd
+
+        def nat(x2, w, b, act, *a, **k):
+            y = self.nat(x2, w, b, act, *a, **k)
+            if act == 1 and self.i is None:  # fp32 values without touching the GPU path's state
+                pl = PL.cached(y) if PL.planes_only(y) else None
+                W = y.shape[-1]
+                hv = y.detach() if pl is None else (pl[0, :, :W].float() + pl[1, :, :W].float()) + pl[2, :, :W].float()
+                self.rec.append(hv.cpu().clone())
+            return y
+
+        def ref(x2, w, b, act, p, seed, salt):
+            y = self.ref(x2, w, b, act, p, seed, salt)
+            if act == 1 and self.i is not None and self.i < len(self.rec):
+                hg = self.rec[self.i].reshape(y.shape).to(y.dtype)
+                self.i += 1
+                dis = (y > 0) != (hg > 0)
+                if bool(dis.any()):
+                    self.flips += int(dis.sum())
+                    big = float(torch.maximum(y[dis].abs(), hg[dis].abs()).max())
+                    if big > 1e-5 * float(y.abs().max()):
+                        self.bad.append(big)
+                    y = torch.where(dis, hg, y)
+            return y
+        LIN._fwd_native, LIN._ref_fwd = nat, ref
+        return self
+
+    def replay(self):
+        self.i = 0
+
+    def __exit__(self, *exc):
+        self.LIN._fwd_native, self.LIN._ref_fwd = self.nat, self.ref
+        return False
 
 
 def test_transformer_f32_flagship_trajectory(f32_algo, monkeypatch):

@@ -343,7 +343,8 @@ def test_embedding_backward_pair_vs_bucketed(T, V, D, pad):
     ids = torch.randint(0, V, (T,))
     ids[: T // 4] = pad if pad is not None else 1
     do = torch.randn(T, D, device=dev)
-    prev = C.emb_pair(-1)
+    prev, prev_max = C.emb_pair(-1), C.emb_pair_max(-1)
+    C.emb_pair_max(8192)
     out = {}
     try:
         for algo in (1, 0):
@@ -359,6 +360,7 @@ def test_embedding_backward_pair_vs_bucketed(T, V, D, pad):
             out[algo] = gs[0]
     finally:
         C.emb_pair(prev)
+        C.emb_pair_max(prev_max)
     _close(out[1], out[0], 1e-5, 1e-5, "pair vs bucketed")
     if pad is not None:
         assert float(out[1][pad].abs().sum()) == 0.0

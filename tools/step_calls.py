@@ -19,7 +19,7 @@ def main():
     want = ["name", "start", "end"]
     extra = [x for x in ("grid_size_x", "grid_size_y", "grid_size_z", "workgroup_size_x") if x in cols]
     rows = c.execute(f"select {', '.join(want + extra)} from kernels order by start").fetchall()
-    marks = [i for i, r in enumerate(rows) if r[0].startswith(a.marker)]
+    marks = [i for i, r in enumerate(rows) if r[0].removeprefix("void ").startswith(a.marker)]
     steps = list(zip(marks[:-1], marks[1:]))
     lo, hi = steps[a.step]
     tot = 0.0

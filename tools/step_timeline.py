@@ -26,7 +26,7 @@ def main():
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end, queue_id, stream_id from kernels order by start").fetchall()
-    marks = [i for i, r in enumerate(rows) if r[0].startswith(a.marker)]
+    marks = [i for i, r in enumerate(rows) if r[0].removeprefix("void ").startswith(a.marker)]
     if len(marks) < a.steps + 1:
         raise SystemExit(f"only {len(marks)} marker kernels found")
     lo, hi = marks[-a.steps - 1], marks[-1]
