@@ -476,7 +476,7 @@ __device__ __forceinline__ void conv_wgrad_bf16(const float* __restrict__ dz, co
 // step counter.  Hand-offs are write-through stores + device-scope loads (smi_common.h), no L2
 // fences; 8-B granules with every load of a thread's sum in flight together.  Deterministic:
 // every sum has a fixed order.  No spinning: a workgroup that is not the last simply exits.
-__device__ __noinline__ void cnn_fused_tail(const CNNArgs& g, int img) {
+__device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img) {
   __shared__ int last;
   const int ngrp = (g.B + CNN_GRP - 1) / CNN_GRP;
   const int grp = img / CNN_GRP, g0 = grp * CNN_GRP, g1 = min(g.B, g0 + CNN_GRP);

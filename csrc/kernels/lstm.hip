@@ -63,7 +63,7 @@ __device__ __forceinline__ uint32_t lstm_drop_idx(int b, int t, int l, int j, in
 // computes the row loss and the head gradient (softmax - onehot) / B from the logits in LDS; the
 // last workgroup to finish (ticket; write-through hand-off) sums the row losses in sequence
 // order.  Replaces three launches (CE forward, finalize, backward) per step.
-__device__ __noinline__ void lstm_ce_tail(const LSTMArgs& a, int b, const float* s_plast) {
+__device__ __forceinline__ void lstm_ce_tail(const LSTMArgs& a, int b, const float* s_plast) {
   __shared__ int s_lastwg;
   __syncthreads();  // s_plast complete
   if (threadIdx.x == 0) {

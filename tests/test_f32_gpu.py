@@ -566,8 +566,9 @@ class _relu_ties_follow_gpu:
     both are rounding-level (|h| <= 1e-5 max|h|); anything larger is reported as a mismatch."""
 
     def __enter__(self):
-        from sparkmi.ops import linear as LIN
-        from sparkmi.ops import planes as PL
+        import importlib
+        LIN = importlib.import_module("sparkmi.ops.linear")  # the module (sparkmi.ops.linear is also a function)
+        PL = importlib.import_module("sparkmi.ops.planes")
         self.LIN, self.flips, self.bad, self.rec, self.i = LIN, 0, [], [], None
         self.nat, self.ref = LIN._fwd_native, LIN._ref_fwd
 

@@ -17,7 +17,7 @@ def main():
     c = sqlite3.connect(a.db)
     cols = [r[1] for r in c.execute("pragma table_info(kernels)").fetchall()]
     want = ["name", "start", "end"]
-    extra = [x for x in ("grid_size_x", "grid_size_y", "grid_size_z", "workgroup_size_x") if x in cols]
+    extra = [x for x in ("grid_size_x", "grid_size_y", "grid_size_z", "workgroup_size_x", "grid_x", "grid_y", "grid_z", "workgroup_x", "queue_id") if x in cols]
     rows = c.execute(f"select {', '.join(want + extra)} from kernels order by start").fetchall()
     marks = [i for i, r in enumerate(rows) if r[0].removeprefix("void ").startswith(a.marker)]
     steps = list(zip(marks[:-1], marks[1:]))
