@@ -100,6 +100,7 @@ int smi_gemm_wgrad_group(const void* const*, const long*, const void* const*, co
 int smi_cnn(const CNNArgs*, hipStream_t);
 int smi_cnn_fused_ok(int, int, int);
 long smi_emb_pair_max(long);
+int smi_emb_pair_plan(const long long*, long, long long, long, void*, hipStream_t);
 int smi_emb_pair(int);
 int smi_cnn_reduce(const CNNArgs*, hipStream_t);
 int smi_gather_rows(const void*, const long long*, void*, long, long, hipStream_t);
@@ -562,6 +563,9 @@ PYBIND11_MODULE(_C, m) {
         "fp32 attention dK/dV: 1 = staggered 8-wave kernel (default), 0 = lockstep; -1 queries");
   m.def("emb_pair_max", [](long set) { return smi_emb_pair_max(set); },
         "largest token batch the pair-compare embedding backward takes (set < 0 queries)");
+  m.def("emb_pair_plan", [](u ids, long T, long long pad, long V, u ws, u st) {
+        return smi_emb_pair_plan((const long long*)ids, T, pad, V, (void*)ws, S(st)); },
+        "pair-path ordering of ids into ws (rank + plan launches); 1 planned, 0 path not applicable");
   m.def("emb_pair", [](int set) { return smi_emb_pair(set); },
         "deterministic embedding backward: 1 = pair-compare (<= 8192 tokens), 0 = bucketed lists; -1 queries");
   m.def("cnn_fused_ok", [](int C, int cin, int classes) { return smi_cnn_fused_ok(C, cin, classes) != 0; });
@@ -576,7 +580,7 @@ PYBIND11_MODULE(_C, m) {
                    u dpred, u dhn, u dcn, u g_emb, std::vector<u> g_w_ih, std::vector<u> g_w_hh, std::vector<u> g_b_ih,
                    std::vector<u> g_b_hh, u g_w_fc, u g_b_fc, u dh0, u dc0, u g_slab, u g_xe, long V, u emb_ws,
                    u pred_last, int dpred_last, u ce_labels, u ce_row, u ce_dlast, u ce_loss, u ce_tick,
-                   u dpred_scale, u st) {
+                   u dpred_scale, int emb_planned, u st) {
     if (L < 1 || L > LSTM_MAXL || (int)w_ih.size() != L || (int)w_hh.size() != L || (int)b_ih.size() != L ||
         (int)b_hh.size() != L)
       throw std::runtime_error("lstm: need L pointers per weight list");
@@ -603,6 +607,7 @@ PYBIND11_MODULE(_C, m) {
     a.pred_last = (float*)pred_last; a.dpred_last = dpred_last;
     a.ce_labels = (const long long*)ce_labels; a.ce_row = (float*)ce_row; a.ce_dlast = (float*)ce_dlast;
     a.ce_loss = (float*)ce_loss; a.ce_tick = (unsigned*)ce_tick; a.dpred_scale = (const float*)dpred_scale;
+    a.emb_planned = emb_planned;
     if (a.ce_labels && (!a.ce_row || !a.ce_dlast || !a.ce_loss || !a.ce_tick || a.C > LSTM_MAXC))
       throw std::runtime_error("lstm: fused CE needs row, dlast, loss and ticket buffers");
     chk(smi_lstm(&a, backward, S(st)), "lstm");

@@ -508,10 +508,21 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img) {
   if (!last) return;
   const float lr = g.lr[0];
   for (int q = threadIdx.x; q < P2; q += blockDim.x) {
-    float2 s = smi_cc_load2(g.part + 2 * q);
-    for (int k = 1; k < ngrp; ++k) {
-      const float2 v = smi_cc_load2(g.part + (long)k * g.P + 2 * q);
-      s.x += v.x; s.y += v.y;
+    float2 s;
+    if (ngrp <= 16) {  // every group's load in flight at once, then the group-order sum
+      float2 v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] = k < ngrp ? smi_cc_load2(g.part + (long)k * g.P + 2 * q) : make_float2(0.f, 0.f);
+      s = v[0];
+#pragma unroll
+      for (int k = 1; k < 16; ++k)
+        if (k < ngrp) { s.x += v[k].x; s.y += v[k].y; }
+    } else {
+      s = smi_cc_load2(g.part + 2 * q);
+      for (int k = 1; k < ngrp; ++k) {
+        const float2 v = smi_cc_load2(g.part + (long)k * g.P + 2 * q);
+        s.x += v.x; s.y += v.y;
+      }
     }
     const float sv[2] = {s.x, s.y};
 #pragma unroll

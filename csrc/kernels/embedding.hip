@@ -615,24 +615,48 @@ extern "C" int smi_emb_pair(int set) {
   return g_emb_pair;
 }
 
+static EmbPair emb_pair_layout(void* ws, long T) {
+  EmbPair e{};
+  int* p = (int*)ws;
+  e.rank = p; p += T;
+  e.first = p; p += T;
+  e.list = p; p += T;
+  e.ch_owner = p; p += T;
+  e.ch_start = p; p += T;
+  e.ch_len = p; p += T;
+  e.ch_g0 = p; p += T;
+  e.ch_gn = p; p += T;
+  e.tick = (unsigned*)p; p += T;
+  e.nchunks = p; p += 4;
+  e.part = (float*)p;
+  return e;
+}
+
+// The pair path's ordering depends on the ids alone: a caller that knows them early (the LSTM's
+// forward) runs rank + plan on a side stream beside the recurrence (32 of 256 CUs busy) and calls
+// smi_emb_pair_sum_f32 in the backward.  Returns 1 when planned, 0 when the pair path does not
+// apply (the caller keeps the full smi_emb_bwd_f32 launch sequence).
+extern "C" int smi_emb_pair_plan(const long long* ids, long T, long long padding_idx, long V, void* ws, hipStream_t st) {
+  if (!ws || V < 1 || T < 1 || T > emb_pair_sel() || !smi_emb_pair(-1)) return 0;
+  EmbPair e = emb_pair_layout(ws, T);
+  hipLaunchKernelGGL(emb_pair_rank, dim3((unsigned)((T + 63) / 64)), dim3(1024), 0, st, ids, T, padding_idx, e);
+  hipLaunchKernelGGL(emb_pair_plan, dim3(1), dim3(1024), 0, st, T, e);
+  return hipGetLastError() == hipSuccess ? 1 : -1;
+}
+extern "C" int smi_emb_pair_sum_f32(const long long* ids, const float* dout, float* dtable, long T, int D, void* ws,
+                                    hipStream_t st) {
+  EmbPair e = emb_pair_layout(ws, T);
+  hipLaunchKernelGGL(emb_pair_sum<float>, dim3((unsigned)((T + 15) / 16)), dim3(1024), 0, st, ids, dout, dtable, D, e,
+                     nullptr, 0u, 0u, 1.f);
+  return (int)hipGetLastError();
+}
+
 template <typename TS>
 static int emb_bwd_launch(const long long* ids, const void* dout, float* dtable, long T, int D, long long padding_idx,
                           const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, long V, void* ws,
                           hipStream_t st) {
   if (ws && V > 0 && T > 0 && T <= emb_pair_sel() && smi_emb_pair(-1)) {
-    EmbPair e{};
-    int* p = (int*)ws;
-    e.rank = p; p += T;
-    e.first = p; p += T;
-    e.list = p; p += T;
-    e.ch_owner = p; p += T;
-    e.ch_start = p; p += T;
-    e.ch_len = p; p += T;
-    e.ch_g0 = p; p += T;
-    e.ch_gn = p; p += T;
-    e.tick = (unsigned*)p; p += T;
-    e.nchunks = p; p += 4;
-    e.part = (float*)p;
+    EmbPair e = emb_pair_layout(ws, T);
     hipLaunchKernelGGL(emb_pair_rank, dim3((unsigned)((T + 63) / 64)), dim3(1024), 0, st, ids, T, padding_idx, e);
     hipLaunchKernelGGL(emb_pair_plan, dim3(1), dim3(1024), 0, st, T, e);
     hipLaunchKernelGGL(emb_pair_sum<TS>, dim3((unsigned)((T + 15) / 16)), dim3(1024), 0, st, ids, (const TS*)dout, dtable, D, e, seedp,

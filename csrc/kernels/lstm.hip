@@ -1052,13 +1052,21 @@ __global__ __launch_bounds__(64 * LW_WAVES) void lstm_wgrad_mfma(LSTMArgs a) {
   __syncthreads();
   if (!s_last) return;
   const int In = l < L ? (l == 0 ? E : a.H) : 0;
+  const long pstride = (long)rows * cols;  // consecutive chunks' partial tiles of layer l
+  const float* pbase = a.g_slab + lstm_part_off(a, l, 0);
   for (int p = tid; p < rows * 16; p += 64 * LW_WAVES) {
     const int r = p >> 4, c = c0 + (p & 15);
     if (c >= cols) continue;
     const size_t o = (size_t)r * cols + c;
+    // every chunk's load in flight at once (device-scope loads reach memory: a serial chain of
+    // them made the reduction the kernel's long pole), then the fixed chunk-order sum
+    float pv[LSTM_KS];
+#pragma unroll
+    for (int q = 0; q < LSTM_KS; ++q) pv[q] = q < nch ? smi_cc_load(pbase + q * pstride + o) : 0.f;
     float v = 0.f;
-#pragma unroll 8
-    for (int q = 0; q < nch; ++q) v += smi_cc_load(a.g_slab + lstm_part_off(a, l, q) + o);  // chunk order
+#pragma unroll
+    for (int q = 0; q < LSTM_KS; ++q)
+      if (q < nch) v += pv[q];
     if (l == L) {
       if (c < a.H) a.g_w_fc[(size_t)r * a.H + c] += v;
       else a.g_b_fc[r] += v;
@@ -1160,6 +1168,8 @@ extern "C" int smi_lstm_supported(int E, int H, int L, int C) {
 extern "C" int smi_emb_bwd_f32(const long long* ids, const void* dout, float* dtable, long T, int D, long long padding_idx,
                                const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, long V, void* ws,
                                hipStream_t st);
+extern "C" int smi_emb_pair_sum_f32(const long long* ids, const float* dout, float* dtable, long T, int D, void* ws,
+                                    hipStream_t st);
 
 extern "C" long smi_lstm_slab_floats(int B, int E, int H, int L, int C) {
   LSTMArgs a{};
@@ -1181,6 +1191,8 @@ extern "C" int smi_lstm(const LSTMArgs* a, int backward, hipStream_t st) {
     // ce_tick (backward): (L + 1) x LW_TICKS zeroed counters, re-armed by the kernel
     hipLaunchKernelGGL(lstm_wgrad_mfma, dim3(lw_chunks(*a), lw_ctiles(*a), a->L + 1), dim3(64 * LW_WAVES), 0, st, *a);
     if ((rc = (int)hipGetLastError())) return rc;
+    if (a->g_emb && a->emb_planned)
+      return smi_emb_pair_sum_f32(a->ids, a->g_xe, a->g_emb, (long)a->B * a->T, a->E, a->emb_ws, st);
     if (a->g_emb)
       return smi_emb_bwd_f32(a->ids, a->g_xe, a->g_emb, (long)a->B * a->T, a->E, a->pad_idx, nullptr, 0, 0, 1.f, a->V,
                              a->emb_ws, st);

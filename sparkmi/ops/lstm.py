@@ -96,7 +96,10 @@ class LSTMFn(torch.autograd.Function):
                          thresh, _rng.scale(p), 0, 0, 0, 0, [], [], [], [], 0, 0, 0, 0, 0, 0, 0, 0,
                          last.data_ptr(), 0, labels.data_ptr() if ce else 0, ce[0].data_ptr() if ce else 0,
                          ce[1].data_ptr() if ce else 0, ce[2].data_ptr() if ce else 0, ce[3].data_ptr() if ce else 0,
-                         0, _native.stream())
+                         0, 0, _native.stream())
+        ctx.emb_plan = None
+        if emb.requires_grad and torch.is_grad_enabled():
+            ctx.emb_plan = _plan_embedding(ids, B * T, pad_idx, emb)
         ctx.meta = (L, p, rng, salt, pad_idx, B, T, E, H, C)
         ctx.has_h0, ctx.has_c0 = h0 is not None, c0 is not None
         ctx.save_for_backward(ids, ws, h0c, c0c, *params)
@@ -141,7 +144,13 @@ class LSTMFn(torch.autograd.Function):
         slab = torch.empty(C_.lstm_slab_floats(B, E, H, L, C), device=dev, dtype=torch.float32)
         want_emb = orig[0].requires_grad
         xe = torch.empty(B, T, E, device=dev, dtype=torch.float32) if want_emb else None
-        ews = torch.empty(C_.emb_det_ws_bytes(B * T, emb.shape[0], emb.shape[1]), device=dev, dtype=torch.uint8) if want_emb else None
+        plan = getattr(ctx, "emb_plan", None) if want_emb else None
+        if plan is not None:  # the ordering ran beside the forward: join it, sum only
+            torch.cuda.current_stream(dev).wait_stream(plan[1])
+            ews = plan[0]
+        else:
+            ews = torch.empty(C_.emb_det_ws_bytes(B * T, emb.shape[0], emb.shape[1]), device=dev,
+                              dtype=torch.uint8) if want_emb else None
         _native.C().lstm(1, ids.data_ptr(), B, T, E, H, L, C, pad_idx, emb.data_ptr(),
                          [lw[0].data_ptr() for lw in layers], [lw[1].data_ptr() for lw in layers],
                          [lw[2].data_ptr() for lw in layers], [lw[3].data_ptr() for lw in layers],
@@ -153,12 +162,37 @@ class LSTMFn(torch.autograd.Function):
                          [lw[2].data_ptr() for lw in g_layers], [lw[3].data_ptr() for lw in g_layers],
                          g_fc.data_ptr(), g_bfc.data_ptr(), _native.ptr(dh0), _native.ptr(dc0), slab.data_ptr(),
                          _native.ptr(xe), emb.shape[0], _native.ptr(ews), 0, last_only, 0, 0, 0, 0,
-                         _ce_ticket(dev)[8:].data_ptr(), _native.ptr(dscale), _native.stream())
+                         _ce_ticket(dev)[8:].data_ptr(), _native.ptr(dscale), int(plan is not None), _native.stream())
+        ctx.emb_plan = None
         grad_ready(*orig)
         return (None, dh0 if ctx.has_h0 else None, dc0 if ctx.has_c0 else None, None) + (None,) * len(params)
 
 
 _CE_TICKETS = {}
+_PLAN_STREAMS = {}
+
+
+def _plan_embedding(ids, T, pad_idx, emb):
+    """Order the step's token ids for the deterministic embedding backward (pair path: rank +
+    plan, csrc/kernels/embedding.hip) on a side stream forked here, beside the forward recurrence
+    that keeps only 32 of the 256 CUs busy; the backward joins it.  (ws, stream) or None when the
+    pair path does not apply to this batch (the backward then runs the whole sequence itself)."""
+    dev = ids.device
+    C_ = _native.C()
+    ws = torch.empty(C_.emb_det_ws_bytes(T, emb.shape[0], emb.shape[1]), device=dev, dtype=torch.uint8)
+    main = torch.cuda.current_stream(dev)
+    s = _PLAN_STREAMS.get(dev)
+    if s is None:
+        s = _PLAN_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    s.wait_stream(main)
+    ws.record_stream(s)
+    ids.record_stream(s)
+    with torch.cuda.stream(s):
+        ok = C_.emb_pair_plan(ids.data_ptr(), T, pad_idx, emb.shape[0], ws.data_ptr(), s.cuda_stream)
+    if ok != 1:
+        main.wait_stream(s)  # nothing was launched; keep the fork joined
+        return None
+    return ws, s
 
 
 def _ce_ticket(dev):
