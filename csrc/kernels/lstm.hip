@@ -983,8 +983,8 @@ __global__ __launch_bounds__(64 * LW_WAVES) void lstm_wgrad_mfma(LSTMArgs a) {
         const int kk = i / q4, q = i - kk * q4;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (kk < nk) {
-          const long bt = k + kk;
-          const int b = (int)(bt / T), t = (int)(bt - (long)b * T);
+          const int bt = (int)k + kk;  // B * T < 2^31 (LSTM_MAXT): 32-bit division
+          const int b = bt / T, t = bt - b * T;
           v = *(const float4*)(a.ws_da + (((size_t)b * L + l) * T + t) * G + 4 * q);
         }
         *(float4*)(s_d + kk * LW_PD + 4 * q) = v;
@@ -994,8 +994,8 @@ __global__ __launch_bounds__(64 * LW_WAVES) void lstm_wgrad_mfma(LSTMArgs a) {
         const int kk = i / rp, r = i - kk * rp;
         float v = 0.f;
         if (kk < nk) {
-          const long bt = k + kk;
-          const int b = (int)(bt / T), t = (int)(bt - (long)b * T);
+          const int bt = (int)k + kk;  // B * T < 2^31 (LSTM_MAXT): 32-bit division
+          const int b = bt / T, t = bt - b * T;
           v = lw_d(a, l, b, t, r, rows);
         }
         s_d[kk * LW_PD + r] = v;
@@ -1005,8 +1005,8 @@ __global__ __launch_bounds__(64 * LW_WAVES) void lstm_wgrad_mfma(LSTMArgs a) {
       const int kk = i >> 4, cc = i & 15;
       float v = 0.f;
       if (kk < nk) {
-        const long bt = k + kk;
-        const int b = (int)(bt / T), t = (int)(bt - (long)b * T);
+        const int bt = (int)k + kk;
+        const int b = bt / T, t = bt - b * T;
         v = lw_x(a, l, b, t, c0 + cc, cols, seed);
       }
       s_x[kk * 16 + cc] = v;

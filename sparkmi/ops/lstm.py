@@ -98,7 +98,9 @@ class LSTMFn(torch.autograd.Function):
                          ce[1].data_ptr() if ce else 0, ce[2].data_ptr() if ce else 0, ce[3].data_ptr() if ce else 0,
                          0, 0, _native.stream())
         ctx.emb_plan = None
-        if emb.requires_grad and torch.is_grad_enabled():
+        # (inside Function.forward grad mode is off: the embedding's needs_input_grad says whether
+        # a backward will want the table gradient; the inputs before it: ids, [labels,] h0, c0, meta)
+        if ctx.needs_input_grad[3 + getattr(ctx, "h0_input", 1)]:
             ctx.emb_plan = _plan_embedding(ids, B * T, pad_idx, emb)
         ctx.meta = (L, p, rng, salt, pad_idx, B, T, E, H, C)
         ctx.has_h0, ctx.has_c0 = h0 is not None, c0 is not None
