@@ -100,7 +100,9 @@ int smi_gemm_wgrad_group(const void* const*, const long*, const void* const*, co
 int smi_cnn(const CNNArgs*, hipStream_t);
 int smi_cnn_fused_ok(int, int, int);
 long smi_emb_pair_max(long);
-int smi_emb_pair_plan(const long long*, long, long long, long, void*, hipStream_t);
+int smi_emb_plan(const long long*, long, long long, long, void*, hipStream_t);
+int smi_emb_sum(int, int, const long long*, const void*, float*, long, int, long long, const uint32_t*, uint32_t,
+                uint32_t, float, long, void*, hipStream_t);
 int smi_emb_pair(int);
 int smi_cnn_reduce(const CNNArgs*, hipStream_t);
 int smi_gather_rows(const void*, const long long*, void*, long, long, hipStream_t);
@@ -563,9 +565,14 @@ PYBIND11_MODULE(_C, m) {
         "fp32 attention dK/dV: 1 = staggered 8-wave kernel (default), 0 = lockstep; -1 queries");
   m.def("emb_pair_max", [](long set) { return smi_emb_pair_max(set); },
         "largest token batch the pair-compare embedding backward takes (set < 0 queries)");
-  m.def("emb_pair_plan", [](u ids, long T, long long pad, long V, u ws, u st) {
-        return smi_emb_pair_plan((const long long*)ids, T, pad, V, (void*)ws, S(st)); },
-        "pair-path ordering of ids into ws (rank + plan launches); 1 planned, 0 path not applicable");
+  m.def("emb_plan", [](u ids, long T, long long pad, long V, u ws, u st) {
+        return smi_emb_plan((const long long*)ids, T, pad, V, (void*)ws, S(st)); },
+        "ordering half of the deterministic embedding backward (ids only); returns the algorithm for emb_sum");
+  m.def("emb_sum", [](int algo, int bf16, u ids, u dout, u dtable, long T, int D, long long pad, u seedp,
+                      uint32_t salt, uint32_t thresh, float dscale, long V, u ws, u st) {
+        chk(smi_emb_sum(algo, bf16, (const long long*)ids, (const void*)dout, (float*)dtable, T, D, pad,
+                        (const uint32_t*)seedp, salt, thresh, dscale, V, (void*)ws, S(st)), "emb_sum"); },
+        "summing half of the embedding backward after emb_plan");
   m.def("emb_pair", [](int set) { return smi_emb_pair(set); },
         "deterministic embedding backward: 1 = pair-compare (<= 8192 tokens), 0 = bucketed lists; -1 queries");
   m.def("cnn_fused_ok", [](int C, int cin, int classes) { return smi_cnn_fused_ok(C, cin, classes) != 0; });

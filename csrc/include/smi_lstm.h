@@ -37,8 +37,8 @@ struct LSTMArgs {
   // backward: ce_tick = the weight-gradient kernel's (L + 1) x 8 per-column-tile tickets (zeroed, re-armed)
   const long long* ce_labels; float* ce_row; float* ce_dlast; float* ce_loss; unsigned* ce_tick;
   const float* dpred_scale;                // backward: dpred x this device scalar (the loss's dloss)
-  int emb_planned;                         // backward: emb_ws already holds the pair-path plan of ids
-                                           // (smi_emb_pair_plan, run beside the forward): sum only
+  int emb_planned;                         // backward: emb_ws already holds the ordering of ids
+                                           // (smi_emb_plan's algorithm, run beside the forward): sum only
 };
 #define LSTM_MAXT 2048
 #define LSTM_TCH 64  // timesteps per LDS-staged chunk in the kernels' tail phases

@@ -632,54 +632,53 @@ static EmbPair emb_pair_layout(void* ws, long T) {
   return e;
 }
 
-// The pair path's ordering depends on the ids alone: a caller that knows them early (the LSTM's
-// forward) runs rank + plan on a side stream beside the recurrence (32 of 256 CUs busy) and calls
-// smi_emb_pair_sum_f32 in the backward.  Returns 1 when planned, 0 when the pair path does not
-// apply (the caller keeps the full smi_emb_bwd_f32 launch sequence).
-extern "C" int smi_emb_pair_plan(const long long* ids, long T, long long padding_idx, long V, void* ws, hipStream_t st) {
-  if (!ws || V < 1 || T < 1 || T > emb_pair_sel() || !smi_emb_pair(-1)) return 0;
-  EmbPair e = emb_pair_layout(ws, T);
-  hipLaunchKernelGGL(emb_pair_rank, dim3((unsigned)((T + 63) / 64)), dim3(1024), 0, st, ids, T, padding_idx, e);
-  hipLaunchKernelGGL(emb_pair_plan, dim3(1), dim3(1024), 0, st, T, e);
-  return hipGetLastError() == hipSuccess ? 1 : -1;
-}
-extern "C" int smi_emb_pair_sum_f32(const long long* ids, const float* dout, float* dtable, long T, int D, void* ws,
-                                    hipStream_t st) {
-  EmbPair e = emb_pair_layout(ws, T);
-  hipLaunchKernelGGL(emb_pair_sum<float>, dim3((unsigned)((T + 15) / 16)), dim3(1024), 0, st, ids, dout, dtable, D, e,
-                     nullptr, 0u, 0u, 1.f);
-  return (int)hipGetLastError();
+static EmbDet emb_det_layout(void* ws, long T, long V) {
+  EmbDet d{};
+  d.tiles = (int)((T + EMB_TILE - 1) / EMB_TILE);
+  d.NB = emb_det_nb(V);
+  d.hmax = (int)(T / EMB_HEAVY);
+  int* p = (int*)ws;
+  d.counts = p; p += (size_t)d.tiles * d.NB;
+  d.offs = p; p += (size_t)d.tiles * d.NB;
+  d.bstart = p; p += d.NB + 1;
+  d.list = p; p += T;
+  d.heavy = p; p += d.hmax + 1;
+  d.pmask = (unsigned*)p;
+  d.part = (float*)ws + emb_det_ints(T, d.NB, d.hmax);
+  return d;
 }
 
-template <typename TS>
-static int emb_bwd_launch(const long long* ids, const void* dout, float* dtable, long T, int D, long long padding_idx,
-                          const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, long V, void* ws,
-                          hipStream_t st) {
-  if (ws && V > 0 && T > 0 && T <= emb_pair_sel() && smi_emb_pair(-1)) {
+// The ordering half of the deterministic backward depends on the ids alone, so a caller that
+// knows them early (the forward) can run it beside other work: returns the algorithm the sum half
+// must use (1 = pair-compare, 2 = bucketed lists, 0 = no scratch: fp32 atomics in the sum half).
+static int emb_plan_launch(const long long* ids, long T, long long padding_idx, long V, void* ws, hipStream_t st) {
+  if (!ws || V <= 0 || T <= 0) return 0;
+  if (T <= emb_pair_sel() && smi_emb_pair(-1)) {
     EmbPair e = emb_pair_layout(ws, T);
     hipLaunchKernelGGL(emb_pair_rank, dim3((unsigned)((T + 63) / 64)), dim3(1024), 0, st, ids, T, padding_idx, e);
     hipLaunchKernelGGL(emb_pair_plan, dim3(1), dim3(1024), 0, st, T, e);
-    hipLaunchKernelGGL(emb_pair_sum<TS>, dim3((unsigned)((T + 15) / 16)), dim3(1024), 0, st, ids, (const TS*)dout, dtable, D, e, seedp,
-                       salt, thresh, dscale);
+    return 1;
+  }
+  EmbDet d = emb_det_layout(ws, T, V);
+  hipLaunchKernelGGL(emb_det_count, dim3(d.tiles), dim3(EMB_TILE), (size_t)d.NB * 4, st, ids, T, padding_idx, d);
+  hipLaunchKernelGGL(emb_det_scan, dim3(1), dim3(1024), 0, st, d);
+  hipLaunchKernelGGL(emb_det_place, dim3(d.tiles), dim3(EMB_TILE), 0, st, ids, T, padding_idx, d);
+  return 2;
+}
+
+template <typename TS>
+static int emb_sum_launch(int algo, const long long* ids, const void* dout, float* dtable, long T, int D,
+                          long long padding_idx, const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale,
+                          long V, void* ws, hipStream_t st) {
+  if (algo == 1) {
+    EmbPair e = emb_pair_layout(ws, T);
+    hipLaunchKernelGGL(emb_pair_sum<TS>, dim3((unsigned)((T + 15) / 16)), dim3(1024), 0, st, ids, (const TS*)dout,
+                       dtable, D, e, seedp, salt, thresh, dscale);
     return (int)hipGetLastError();
   }
-  if (ws && V > 0 && T > 0) {
-    EmbDet d{};
-    d.tiles = (int)((T + EMB_TILE - 1) / EMB_TILE);
-    d.NB = emb_det_nb(V);
-    d.hmax = (int)(T / EMB_HEAVY);
-    int* p = (int*)ws;
-    d.counts = p; p += (size_t)d.tiles * d.NB;
-    d.offs = p; p += (size_t)d.tiles * d.NB;
-    d.bstart = p; p += d.NB + 1;
-    d.list = p; p += T;
-    d.heavy = p; p += d.hmax + 1;
-    d.pmask = (unsigned*)p;
-    d.part = (float*)ws + emb_det_ints(T, d.NB, d.hmax);
+  if (algo == 2) {
+    EmbDet d = emb_det_layout(ws, T, V);
     const dim3 cg((D + EMB_CW - 1) / EMB_CW);
-    hipLaunchKernelGGL(emb_det_count, dim3(d.tiles), dim3(EMB_TILE), (size_t)d.NB * 4, st, ids, T, padding_idx, d);
-    hipLaunchKernelGGL(emb_det_scan, dim3(1), dim3(1024), 0, st, d);
-    hipLaunchKernelGGL(emb_det_place, dim3(d.tiles), dim3(EMB_TILE), 0, st, ids, T, padding_idx, d);
     hipLaunchKernelGGL((emb_det_sum<TS, false>), dim3(d.NB, cg.x), dim3(64 * EMB_SW), 0, st, ids, (const TS*)dout,
                        dtable, D, d, seedp, salt, thresh, dscale);
     if (d.hmax > 0) {
@@ -693,6 +692,27 @@ static int emb_bwd_launch(const long long* ids, const void* dout, float* dtable,
   hipLaunchKernelGGL(emb_bwd_kernel<TS>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, ids, (const TS*)dout,
                      dtable, T, D, padding_idx, seedp, salt, thresh, dscale);
   return (int)hipGetLastError();
+}
+
+template <typename TS>
+static int emb_bwd_launch(const long long* ids, const void* dout, float* dtable, long T, int D, long long padding_idx,
+                          const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, long V, void* ws,
+                          hipStream_t st) {
+  const int algo = emb_plan_launch(ids, T, padding_idx, V, ws, st);
+  return emb_sum_launch<TS>(algo, ids, dout, dtable, T, D, padding_idx, seedp, salt, thresh, dscale, V, ws, st);
+}
+
+extern "C" int smi_emb_plan(const long long* ids, long T, long long padding_idx, long V, void* ws, hipStream_t st) {
+  return emb_plan_launch(ids, T, padding_idx, V, ws, st);
+}
+// the sum half after smi_emb_plan (algo = its return value); bf16: dout in bf16
+extern "C" int smi_emb_sum(int algo, int bf16, const long long* ids, const void* dout, float* dtable, long T, int D,
+                           long long padding_idx, const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale,
+                           long V, void* ws, hipStream_t st) {
+  if (bf16)
+    return emb_sum_launch<unsigned short>(algo, ids, dout, dtable, T, D, padding_idx, seedp, salt, thresh, dscale, V,
+                                          ws, st);
+  return emb_sum_launch<float>(algo, ids, dout, dtable, T, D, padding_idx, seedp, salt, thresh, dscale, V, ws, st);
 }
 
 extern "C" int smi_emb_fwd(const long long* ids, const void* table, const float* pe, void* out, long T, int D, int S,

@@ -1168,8 +1168,9 @@ extern "C" int smi_lstm_supported(int E, int H, int L, int C) {
 extern "C" int smi_emb_bwd_f32(const long long* ids, const void* dout, float* dtable, long T, int D, long long padding_idx,
                                const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale, long V, void* ws,
                                hipStream_t st);
-extern "C" int smi_emb_pair_sum_f32(const long long* ids, const float* dout, float* dtable, long T, int D, void* ws,
-                                    hipStream_t st);
+extern "C" int smi_emb_sum(int algo, int bf16, const long long* ids, const void* dout, float* dtable, long T, int D,
+                           long long padding_idx, const uint32_t* seedp, uint32_t salt, uint32_t thresh, float dscale,
+                           long V, void* ws, hipStream_t st);
 
 extern "C" long smi_lstm_slab_floats(int B, int E, int H, int L, int C) {
   LSTMArgs a{};
@@ -1192,7 +1193,8 @@ extern "C" int smi_lstm(const LSTMArgs* a, int backward, hipStream_t st) {
     hipLaunchKernelGGL(lstm_wgrad_mfma, dim3(lw_chunks(*a), lw_ctiles(*a), a->L + 1), dim3(64 * LW_WAVES), 0, st, *a);
     if ((rc = (int)hipGetLastError())) return rc;
     if (a->g_emb && a->emb_planned)
-      return smi_emb_pair_sum_f32(a->ids, a->g_xe, a->g_emb, (long)a->B * a->T, a->E, a->emb_ws, st);
+      return smi_emb_sum(a->emb_planned, 0, a->ids, a->g_xe, a->g_emb, (long)a->B * a->T, a->E, a->pad_idx, nullptr, 0,
+                         0, 1.f, a->V, a->emb_ws, st);
     if (a->g_emb)
       return smi_emb_bwd_f32(a->ids, a->g_xe, a->g_emb, (long)a->B * a->T, a->E, a->pad_idx, nullptr, 0, 0, 1.f, a->V,
                              a->emb_ws, st);

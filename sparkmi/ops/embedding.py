@@ -25,9 +25,34 @@ def sinusoid_table(max_len: int, d_model: int) -> torch.Tensor:
 
 
 
+_PLAN_STREAMS = {}
+
+
+def plan_backward(ids, T, pad_idx, weight):
+    """Run the ordering half of the deterministic embedding backward (it depends on the ids only:
+    pair-compare rank + plan, or the bucketed count / scan / place; csrc/kernels/embedding.hip
+    smi_emb_plan) NOW, on a side stream forked from the current one, so that it overlaps the
+    forward instead of sitting on the backward's critical path.  Returns (ws, stream, algo); the
+    backward joins the stream and launches only the summing half.  Called from inside
+    Function.forward, so only when a weight gradient will be wanted (needs_input_grad)."""
+    dev = ids.device
+    C = _native.C()
+    ws = torch.empty(C.emb_det_ws_bytes(T, weight.shape[0], weight.shape[1]), device=dev, dtype=torch.uint8)
+    main = torch.cuda.current_stream(dev)
+    s = _PLAN_STREAMS.get(dev)
+    if s is None:
+        s = _PLAN_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    s.wait_stream(main)
+    ws.record_stream(s)
+    ids.record_stream(s)
+    with torch.cuda.stream(s):
+        algo = C.emb_plan(ids.data_ptr(), T, pad_idx, weight.shape[0], ws.data_ptr(), s.cuda_stream)
+    return ws, s, algo
+
+
 class EmbeddingFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, ids, weight, pe, p, rng, salt, padding_idx, out_dtype):
+    def forward(ctx, ids, weight, pe, p, rng, salt, padding_idx, out_dtype, plan=False):
         B = ids.shape
         D = weight.shape[1]
         T = ids.numel()
@@ -63,6 +88,9 @@ class EmbeddingFn(torch.autograd.Function):
             if p > 0:
                 x = x * _rng.keep_mask(x.shape, p, ctx.seed, salt, x.device).to(x.dtype) * _rng.scale(p)
             out = x.to(out_dtype)
+        ctx.plan = None
+        if ctx.native and plan and ctx.needs_input_grad[1]:  # plan: grad mode was on at the call
+            ctx.plan = plan_backward(ids_c, T, ctx.pad, weight)
         ctx.save_for_backward(ids_c, weight)
         return out
 
@@ -75,12 +103,20 @@ class EmbeddingFn(torch.autograd.Function):
         if ctx.native:
             C = _native.C()
             dout = dout.contiguous()
-            bwd = C.emb_bwd_f32 if dout.dtype == torch.float32 else C.emb_bwd
-            # deterministic bucketed backward: bit-reproducible, no float atomics
             V = weight.shape[0]
-            ws = torch.empty(C.emb_det_ws_bytes(T, V, D), device=dout.device, dtype=torch.uint8)
-            bwd(ids.data_ptr(), dout.data_ptr(), gw.data_ptr(), T, D, ctx.pad, ctx.rng.ptr(), ctx.salt,
-                _rng.threshold(ctx.p), _rng.scale(ctx.p), V, ws.data_ptr(), _native.stream())
+            # deterministic backward (bit-reproducible, no float atomics): the ordering ran beside
+            # the forward (plan_backward); join it and sum
+            plan, ctx.plan = ctx.plan, None
+            if plan is not None:
+                torch.cuda.current_stream(dout.device).wait_stream(plan[1])
+                C.emb_sum(plan[2], int(dout.dtype != torch.float32), ids.data_ptr(), dout.data_ptr(), gw.data_ptr(), T,
+                          D, ctx.pad, ctx.rng.ptr(), ctx.salt, _rng.threshold(ctx.p), _rng.scale(ctx.p), V,
+                          plan[0].data_ptr(), _native.stream())
+            else:
+                bwd = C.emb_bwd_f32 if dout.dtype == torch.float32 else C.emb_bwd
+                ws = torch.empty(C.emb_det_ws_bytes(T, V, D), device=dout.device, dtype=torch.uint8)
+                bwd(ids.data_ptr(), dout.data_ptr(), gw.data_ptr(), T, D, ctx.pad, ctx.rng.ptr(), ctx.salt,
+                    _rng.threshold(ctx.p), _rng.scale(ctx.p), V, ws.data_ptr(), _native.stream())
         else:
             g = dout.float()
             if ctx.p > 0:
@@ -92,11 +128,11 @@ class EmbeddingFn(torch.autograd.Function):
                 g, idf = g[keep], idf[keep]
             gw.index_add_(0, idf, g)
         grad_ready(weight)
-        return None, None, None, None, None, None, None, None
+        return None, None, None, None, None, None, None, None, None
 
 
 def embedding(ids, weight, pe=None, p=0.0, rng=None, salt=0, padding_idx=None, out_dtype=torch.float32):
     if rng is None:
         from .layernorm import _NULL_RNG
         rng, p = _NULL_RNG, 0.0
-    return EmbeddingFn.apply(ids, weight, pe, float(p), rng, int(salt), padding_idx, out_dtype)
+    return EmbeddingFn.apply(ids, weight, pe, float(p), rng, int(salt), padding_idx, out_dtype, torch.is_grad_enabled())

@@ -67,7 +67,7 @@ class LSTMFn(torch.autograd.Function):
     def _forward(ctx, ids, h0, c0, meta, params, labels):
         """The forward launch; ``labels``: also the fused last-step CE (returns its extra outputs)."""
         ctx.set_materialize_grads(False)  # unused outputs get no zero-filled gradients
-        L, p, rng, salt, pad_idx = meta
+        L, p, rng, salt, pad_idx = meta[:5]
         emb, layers, w_fc, b_fc = unpack(params, L)
         B, T = ids.shape
         E, H, C = emb.shape[1], layers[0][1].shape[1], w_fc.shape[0]
@@ -100,7 +100,7 @@ class LSTMFn(torch.autograd.Function):
         ctx.emb_plan = None
         # (inside Function.forward grad mode is off: the embedding's needs_input_grad says whether
         # a backward will want the table gradient; the inputs before it: ids, [labels,] h0, c0, meta)
-        if ctx.needs_input_grad[3 + getattr(ctx, "h0_input", 1)]:
+        if ctx.needs_input_grad[3 + getattr(ctx, "h0_input", 1)] and len(meta) > 5 and meta[5]:
             ctx.emb_plan = _plan_embedding(ids, B * T, pad_idx, emb)
         ctx.meta = (L, p, rng, salt, pad_idx, B, T, E, H, C)
         ctx.has_h0, ctx.has_c0 = h0 is not None, c0 is not None
@@ -164,37 +164,20 @@ class LSTMFn(torch.autograd.Function):
                          [lw[2].data_ptr() for lw in g_layers], [lw[3].data_ptr() for lw in g_layers],
                          g_fc.data_ptr(), g_bfc.data_ptr(), _native.ptr(dh0), _native.ptr(dc0), slab.data_ptr(),
                          _native.ptr(xe), emb.shape[0], _native.ptr(ews), 0, last_only, 0, 0, 0, 0,
-                         _ce_ticket(dev)[8:].data_ptr(), _native.ptr(dscale), int(plan is not None), _native.stream())
+                         _ce_ticket(dev)[8:].data_ptr(), _native.ptr(dscale), plan[2] if plan is not None else 0,
+                         _native.stream())
         ctx.emb_plan = None
         grad_ready(*orig)
         return (None, dh0 if ctx.has_h0 else None, dc0 if ctx.has_c0 else None, None) + (None,) * len(params)
 
 
 _CE_TICKETS = {}
-_PLAN_STREAMS = {}
 
 
 def _plan_embedding(ids, T, pad_idx, emb):
-    """Order the step's token ids for the deterministic embedding backward (pair path: rank +
-    plan, csrc/kernels/embedding.hip) on a side stream forked here, beside the forward recurrence
-    that keeps only 32 of the 256 CUs busy; the backward joins it.  (ws, stream) or None when the
-    pair path does not apply to this batch (the backward then runs the whole sequence itself)."""
-    dev = ids.device
-    C_ = _native.C()
-    ws = torch.empty(C_.emb_det_ws_bytes(T, emb.shape[0], emb.shape[1]), device=dev, dtype=torch.uint8)
-    main = torch.cuda.current_stream(dev)
-    s = _PLAN_STREAMS.get(dev)
-    if s is None:
-        s = _PLAN_STREAMS[dev] = torch.cuda.Stream(device=dev)
-    s.wait_stream(main)
-    ws.record_stream(s)
-    ids.record_stream(s)
-    with torch.cuda.stream(s):
-        ok = C_.emb_pair_plan(ids.data_ptr(), T, pad_idx, emb.shape[0], ws.data_ptr(), s.cuda_stream)
-    if ok != 1:
-        main.wait_stream(s)  # nothing was launched; keep the fork joined
-        return None
-    return ws, s
+    """See sparkmi.ops.embedding.plan_backward (the recurrence keeps only 32 of 256 CUs busy)."""
+    from .embedding import plan_backward
+    return plan_backward(ids, T, pad_idx, emb)
 
 
 def _ce_ticket(dev):
@@ -237,7 +220,7 @@ def lstm_classifier_ce(ids, labels, h0, c0, params, num_layers, dropout=0.0, tra
     E, H, C = emb.shape[1], layers[0][1].shape[1], w_fc.shape[0]
     if ids.is_cuda and _native.use_native(ids) and supported(E, H, num_layers, C):
         pad = -1 if padding_idx is None else int(padding_idx)
-        return LSTMCEFn.apply(ids, labels, h0, c0, (num_layers, p, rng, salt, pad), *params)
+        return LSTMCEFn.apply(ids, labels, h0, c0, (num_layers, p, rng, salt, pad, torch.is_grad_enabled()), *params)
     last, _, _, _ = lstm_classifier_last(ids, h0, c0, params, num_layers, dropout, training, rng, salt, padding_idx)
     return torch.nn.functional.cross_entropy(last, labels), last
 
@@ -253,7 +236,7 @@ def lstm_classifier(ids, h0, c0, params, num_layers, dropout=0.0, training=True,
             raise NotImplementedError(f"sparkmi LSTM kernel: unsupported shape E={E} H={H} L={num_layers} C={C} "
                                       "(H in {16,32,64}, 4*H*L <= 512, E <= 2H and <= 64, C <= 16)")
         pad = -1 if padding_idx is None else int(padding_idx)
-        pred, hn, cn, _ = LSTMFn.apply(ids, h0, c0, (num_layers, p, rng, salt, pad), *params)
+        pred, hn, cn, _ = LSTMFn.apply(ids, h0, c0, (num_layers, p, rng, salt, pad, torch.is_grad_enabled()), *params)
         return pred, hn, cn
     seed = rng.current() if (rng is not None and p > 0) else 0
     return reference_forward(ids, h0, c0, params, num_layers, p, seed, salt, padding_idx)
@@ -268,7 +251,7 @@ def lstm_classifier_last(ids, h0, c0, params, num_layers, dropout=0.0, training=
     E, H, C = emb.shape[1], layers[0][1].shape[1], w_fc.shape[0]
     if ids.is_cuda and _native.use_native(ids) and supported(E, H, num_layers, C):
         pad = -1 if padding_idx is None else int(padding_idx)
-        pred, hn, cn, last = LSTMFn.apply(ids, h0, c0, (num_layers, p, rng, salt, pad), *params)
+        pred, hn, cn, last = LSTMFn.apply(ids, h0, c0, (num_layers, p, rng, salt, pad, torch.is_grad_enabled()), *params)
         return last, pred, hn, cn
     pred, hn, cn = lstm_classifier(ids, h0, c0, params, num_layers, dropout, training, rng, salt, padding_idx)
     return pred[:, -1, :].contiguous(), pred, hn, cn
