@@ -1766,14 +1766,17 @@ extern "C" int smi_attn_ae(int set) {
   return g_attn_ae;
 }
 static bool fa_ae_enabled() { return smi_attn_ae(-1) != 0; }
-// the backward kernels' dQ / dK / dV through LDS too (SMI_ATTN_AE_BWD=1): measured +3..5 us per
-// call against the per-lane stores (tools/ab_attn.py: the forward gains 5..13 us) — off by default
+// the backward kernels' dQ / dK / dV through LDS too (SMI_ATTN_AE_BWD=0: per-lane stores).  In
+// isolation (tools/ab_attn.py: self-attention, compact layouts) it measured +3..5 us per call, but
+// inside the step the cross-attention dK / dV go to the 6-layer concatenated kv gradient (row
+// stride 6144) and the per-lane stores touched 32-64 rows per instruction: dK/dV 98 -> 57 us,
+// the fp32 step 15.59 -> 15.11 ms (same box, gpurun_out/r4j_*)
 static int g_attn_ae_bwd = -1;
 extern "C" int smi_attn_ae_bwd(int set) {
   if (set == 0 || set == 1) g_attn_ae_bwd = set;
   if (g_attn_ae_bwd < 0) {
     const char* e = getenv("SMI_ATTN_AE_BWD");
-    g_attn_ae_bwd = (e && e[0] == '1') ? 1 : 0;
+    g_attn_ae_bwd = (e && e[0] == '0') ? 0 : 1;
   }
   return g_attn_ae_bwd;
 }

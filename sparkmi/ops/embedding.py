@@ -41,7 +41,8 @@ def plan_backward(ids, T, pad_idx, weight):
     main = torch.cuda.current_stream(dev)
     s = _PLAN_STREAMS.get(dev)
     if s is None:
-        s = _PLAN_STREAMS[dev] = torch.cuda.Stream(device=dev)
+        # high priority: the ordering is tiny and should not queue behind the forward's kernels
+        s = _PLAN_STREAMS[dev] = torch.cuda.Stream(device=dev, priority=-1)
     s.wait_stream(main)
     ws.record_stream(s)
     ids.record_stream(s)
