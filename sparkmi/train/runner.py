@@ -5,7 +5,8 @@ buffer) -> gradient all-reduce (data-parallel) -> fused optimizer launch.
 With ``graph=True`` the step's kernels are captured once into a hipGraph after a few eager
 warm-up steps and then replayed: one host launch per step instead of hundreds, which matters
 at the reference's small per-GPU batches.  Inputs are copied into static
-device buffers before each replay.
+device buffers before each replay (or, with ``bind_inputs``, read in place by a graph captured per
+batch when the batches live at fixed device addresses).
   * one executor: the whole step (optimizer included) is one graph;
   * data-parallel: the graph holds forward + backward; the gradient buckets are then
     all-reduced by RCCL (a few large collectives over the flat buffer) and the optimizer runs
@@ -26,8 +27,16 @@ from ..ops import _grad
 
 class StepRunner:
     def __init__(self, model, loss_fn, optimizer, ddp=None, graph=False, warmup_eager=3, split_fn=None,
-                 fused_step=None):
+                 fused_step=None, bind_inputs=False, max_bound=32):
         self.model = model
+        # bind_inputs: batches that live at fixed device addresses (an HBM-resident dataset's
+        # batch views) are read IN PLACE by a graph captured per batch (shared memory pool, at
+        # most max_bound of them) instead of being copied into static buffers before every
+        # replay: single-executor whole-step graphs only; other modes copy as before
+        self.bind_inputs = bind_inputs
+        self.max_bound = max_bound
+        self._bound = {}
+        self._bound_pool = None
         # fused_step(model, optimizer, *batch) -> loss or None: a whole single-executor step in
         # one kernel (e.g. MultilayerPerceptron.fused_sgd_step); None falls back to the chain
         self.fused_step = fused_step
@@ -232,11 +241,38 @@ class StepRunner:
             self._opt_in_graph = True
         self.graph = g
 
+    def _bind_ok(self):
+        return (self.bind_inputs and not self._dp and self.split_fn is None and not self.phase_timing
+                and not torch.cuda.is_current_stream_capturing())
+
+    def _step_bound(self, batch):
+        """Replay the graph captured for exactly these input tensors (capture it first if new);
+        None when the cache is full (the caller takes the copying path)."""
+        key = tuple((b.data_ptr(), tuple(b.shape), b.dtype) for b in batch)
+        ent = self._bound.get(key)
+        if ent is None:
+            if len(self._bound) >= self.max_bound:
+                return None
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self._bound_pool):
+                loss = self._eager(*batch)
+            if self._bound_pool is None:
+                self._bound_pool = g.pool()
+            self._opt_in_graph = True
+            ent = self._bound[key] = (g, loss, batch)  # the batch stays referenced: its memory is the input
+        ent[0].replay()
+        return ent[1]
+
     def step(self, *batch):
         self.steps += 1
         use_graph = self.graph_requested and batch[0].is_cuda
         if not use_graph or self.steps <= self.warmup_eager:
             return self._eager(*batch)
+        if self._bind_ok():
+            loss = self._step_bound(batch)
+            if loss is not None:
+                return loss
         if self.graph is None:
             self._capture(batch)  # then replayed below for this step
         self._refresh_inputs(batch)
