@@ -953,7 +953,9 @@ static inline int lw_ctiles(const LSTMArgs& a) {
 #define LW_TICKS 8  // ticket slots per layer (column tiles; cols <= 128)
 #define MF16F32(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
 
-__global__ __launch_bounds__(64 * LW_WAVES) void lstm_wgrad_mfma(LSTMArgs a) {
+// two 512-thread workgroups per CU (<= 128 VGPRs, 2 x 64 KB LDS): the whole grid (33 chunks x 5
+// column tiles x 3 layers at the reference shape) is resident at once
+__global__ __launch_bounds__(64 * LW_WAVES, 2) void lstm_wgrad_mfma(LSTMArgs a) {
   __shared__ float s_d[LW_KR * LW_PD];
   __shared__ float s_x[LW_KR * 16];
   __shared__ float s_w[128 * LW_PW];
@@ -1060,13 +1062,15 @@ __global__ __launch_bounds__(64 * LW_WAVES) void lstm_wgrad_mfma(LSTMArgs a) {
     const size_t o = (size_t)r * cols + c;
     // every chunk's load in flight at once (device-scope loads reach memory: a serial chain of
     // them made the reduction the kernel's long pole), then the fixed chunk-order sum
-    float pv[LSTM_KS];
-#pragma unroll
-    for (int q = 0; q < LSTM_KS; ++q) pv[q] = q < nch ? smi_cc_load(pbase + q * pstride + o) : 0.f;
     float v = 0.f;
+    for (int q0 = 0; q0 < nch; q0 += 16) {
+      float pv[16];
 #pragma unroll
-    for (int q = 0; q < LSTM_KS; ++q)
-      if (q < nch) v += pv[q];
+      for (int j = 0; j < 16; ++j) pv[j] = q0 + j < nch ? smi_cc_load(pbase + (q0 + j) * pstride + o) : 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (q0 + j < nch) v += pv[j];
+    }
     if (l == L) {
       if (c < a.H) a.g_w_fc[(size_t)r * a.H + c] += v;
       else a.g_b_fc[r] += v;
