@@ -23,8 +23,10 @@ __device__ __forceinline__ float mlp_act(float v, int act) {
   return act == 1 ? fmaxf(v, 0.f) : 1.f / (1.f + __expf(-v));
 }
 
-// forward one row; activations of every layer stored in a (lane-private) LDS slab
-__device__ __forceinline__ float mlp_forward_row(const MLPArgs& a, int row, float* act_s) {
+// forward one row; activations of every layer stored in a (lane-private) LDS slab; Wp / bp: the
+// layer parameters (an LDS copy when they fit, else the global tensors)
+__device__ __forceinline__ float mlp_forward_row(const MLPArgs& a, int row, float* act_s, const float* const* Wp,
+                                                 const float* const* bp) {
   int off = 0;
   const int d0 = a.dims[0];
   for (int i = 0; i < d0; ++i) act_s[i] = a.x[(long)row * d0 + i];
@@ -34,8 +36,8 @@ __device__ __forceinline__ float mlp_forward_row(const MLPArgs& a, int row, floa
     float* out = act_s + off + din;
     const bool last = l == a.nlayers - 1;
     for (int o = 0; o < dout; ++o) {
-      float s = a.b[l][o];
-      const float* w = a.W[l] + o * din;
+      float s = bp[l][o];
+      const float* w = Wp[l] + o * din;
       for (int i = 0; i < din; ++i) s += w[i] * in[i];
       out[o] = last ? s : mlp_act(s, a.act);
     }
@@ -56,6 +58,7 @@ __device__ __forceinline__ float mlp_forward_row(const MLPArgs& a, int row, floa
 #define MLP_ACT_LD (MLP_ACT_STRIDE + 1)        // odd LDS pitch: lane-private rows on distinct banks
 #define MLP_DEL_LD (MLP_MAXW * MLP_MAXL + 1)
 #define MLP_MAXT 8192                          // parameters (weights + biases)
+#define MLP_WLDS 2048                          // parameters staged in LDS (fits beside the slabs)
 
 __device__ __forceinline__ int mlp_total(const MLPArgs& a) {
   int t = 0;
@@ -123,12 +126,32 @@ __global__ __launch_bounds__(64) void mlp_kernel(MLPArgs a, int mode) {
   __shared__ float acts[64 * MLP_ACT_LD];  // per row: layer inputs (dims[0..L-1]) + logits
   __shared__ float dls[64 * MLP_DEL_LD];   // per row: grad wrt each layer's pre-activation output
   __shared__ float gacc[MLP_MAXT];
+  __shared__ float wts[MLP_WLDS];          // the parameters (layer-major), when they fit
   __shared__ int last;
   const int L = a.nlayers, lane = threadIdx.x;
   int offs[MLP_MAXL + 1];  // activation offsets (offs[l] = input of layer l)
   offs[0] = 0;
   for (int l = 0; l < L; ++l) offs[l + 1] = offs[l] + a.dims[l];
   const int T = mlp_total(a);
+  // every parameter read of the row loops from LDS: one round of global loads up front instead
+  // of a dependent global load per multiply-add (the kernel is latency-bound at these sizes)
+  const float* Wp[MLP_MAXL];
+  const float* bp[MLP_MAXL];
+  const bool wl = T <= MLP_WLDS;
+  for (int l = 0, base = 0; l < L; ++l) {
+    const int din = a.dims[l], dout = a.dims[l + 1];
+    if (wl) {
+      for (int i = lane; i < dout * din; i += 64) wts[base + i] = a.W[l][i];
+      for (int i = lane; i < dout; i += 64) wts[base + dout * din + i] = a.b[l][i];
+      Wp[l] = wts + base;
+      bp[l] = wts + base + dout * din;
+    } else {
+      Wp[l] = a.W[l];
+      bp[l] = a.b[l];
+    }
+    base += dout * (din + 1);
+  }
+  if (wl) __syncthreads();
   if (mode > 0)
     for (int i = lane; i < T; i += 64) gacc[i] = 0.f;
   float* act_s = acts + lane * MLP_ACT_LD;
@@ -140,7 +163,7 @@ __global__ __launch_bounds__(64) void mlp_kernel(MLPArgs a, int mode) {
     const int row = chunk + lane;
     if (row < a.n) {
       const float w = a.row_w ? a.row_w[row] : 1.f / (float)a.n;
-      lsum += w * mlp_forward_row(a, row, act_s);
+      lsum += w * mlp_forward_row(a, row, act_s, Wp, bp);
       if (a.logits) {
         const int C = a.dims[L];
         for (int c = 0; c < C; ++c) a.logits[(long)row * C + c] = act_s[offs[L] + c];
@@ -163,7 +186,7 @@ __global__ __launch_bounds__(64) void mlp_kernel(MLPArgs a, int mode) {
           const float* h = act_s + offs[l];
           for (int i = 0; i < din; ++i) {
             float s = 0.f;
-            for (int o = 0; o < dout; ++o) s += a.W[l][o * din + i] * dcur[o];
+            for (int o = 0; o < dout; ++o) s += Wp[l][o * din + i] * dcur[o];
             dprev[i] = a.act == 1 ? (h[i] > 0.f ? s : 0.f) : s * h[i] * (1.f - h[i]);
           }
         }
