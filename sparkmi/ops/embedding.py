@@ -26,15 +26,36 @@ def sinusoid_table(max_len: int, d_model: int) -> torch.Tensor:
 
 
 _PLAN_STREAMS = {}
+_PENDING = []  # forked plans not yet joined: [ws, stream, algo, joined]
+
+
+def join_plans():
+    """Make the current stream wait for every forked, not yet joined plan.  A caller that ends a
+    HIP-graph capture before the backward that would join them (the data-parallel split-graph
+    step: forward in the first graph, the encoder embedding's backward in the last) calls this
+    at the end of that capture, so no capture ends with an unjoined side branch."""
+    while _PENDING:
+        plan = _PENDING.pop()
+        if not plan[3]:
+            torch.cuda.current_stream(plan[1].device).wait_stream(plan[1])
+            plan[3] = True
+
+
+def _join(plan):
+    if not plan[3]:
+        torch.cuda.current_stream(plan[1].device).wait_stream(plan[1])
+        plan[3] = True
+    if plan in _PENDING:
+        _PENDING.remove(plan)
 
 
 def plan_backward(ids, T, pad_idx, weight):
     """Run the ordering half of the deterministic embedding backward (it depends on the ids only:
     pair-compare rank + plan, or the bucketed count / scan / place; csrc/kernels/embedding.hip
     smi_emb_plan) NOW, on a side stream forked from the current one, so that it overlaps the
-    forward instead of sitting on the backward's critical path.  Returns (ws, stream, algo); the
-    backward joins the stream and launches only the summing half.  Called from inside
-    Function.forward, so only when a weight gradient will be wanted (needs_input_grad)."""
+    forward instead of sitting on the backward's critical path.  Returns [ws, stream, algo,
+    joined]; the backward joins the stream (``_join``, once) and launches only the summing half.
+    Called from inside Function.forward, only when a weight gradient will be wanted."""
     dev = ids.device
     C = _native.C()
     ws = torch.empty(C.emb_det_ws_bytes(T, weight.shape[0], weight.shape[1]), device=dev, dtype=torch.uint8)
@@ -48,7 +69,11 @@ def plan_backward(ids, T, pad_idx, weight):
     ids.record_stream(s)
     with torch.cuda.stream(s):
         algo = C.emb_plan(ids.data_ptr(), T, pad_idx, weight.shape[0], ws.data_ptr(), s.cuda_stream)
-    return ws, s, algo
+    plan = [ws, s, algo, False]
+    _PENDING.append(plan)
+    if len(_PENDING) > 64:  # forwards without a backward (grad mode on, no .backward()): bounded
+        _join(_PENDING[0])
+    return plan
 
 
 class EmbeddingFn(torch.autograd.Function):
@@ -109,7 +134,7 @@ class EmbeddingFn(torch.autograd.Function):
             # the forward (plan_backward); join it and sum
             plan, ctx.plan = ctx.plan, None
             if plan is not None:
-                torch.cuda.current_stream(dout.device).wait_stream(plan[1])
+                _join(plan)
                 C.emb_sum(plan[2], int(dout.dtype != torch.float32), ids.data_ptr(), dout.data_ptr(), gw.data_ptr(), T,
                           D, ctx.pad, ctx.rng.ptr(), ctx.salt, _rng.threshold(ctx.p), _rng.scale(ctx.p), V,
                           plan[0].data_ptr(), _native.stream())

@@ -148,7 +148,8 @@ class LSTMFn(torch.autograd.Function):
         xe = torch.empty(B, T, E, device=dev, dtype=torch.float32) if want_emb else None
         plan = getattr(ctx, "emb_plan", None) if want_emb else None
         if plan is not None:  # the ordering ran beside the forward: join it, sum only
-            torch.cuda.current_stream(dev).wait_stream(plan[1])
+            from .embedding import _join
+            _join(plan)
             ews = plan[0]
         else:
             ews = torch.empty(C_.emb_det_ws_bytes(B * T, emb.shape[0], emb.shape[1]), device=dev,

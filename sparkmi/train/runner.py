@@ -23,6 +23,7 @@ batch when the batches live at fixed device addresses).
 import torch
 
 from ..ops import _grad
+from ..ops.embedding import join_plans
 
 
 class StepRunner:
@@ -78,6 +79,7 @@ class StepRunner:
         loss = self.loss_fn(self.model, *batch)
         loss.backward(self._seed(loss))
         _grad.join()
+        join_plans()  # a forward whose embedding backward did not run (frozen table): joined here
         return loss.detach()
 
     def _seed(self, loss):
@@ -165,6 +167,7 @@ class StepRunner:
         try:
             with torch.cuda.graph(g1):
                 self.static_loss, segments = self._fwd_bwd_split(*self.static_in)
+                join_plans()  # embedding orderings forked in this forward, joined before G1 ends
         finally:
             _grad.remove_listener(listener)
         ready.append(first)
