@@ -17,7 +17,7 @@ from sparkmi import _native  # noqa: E402
 from sparkmi.data.synthetic import translation_pairs  # noqa: E402
 from sparkmi.models.transformer import Transformer  # noqa: E402
 from sparkmi.ops import _grad  # noqa: E402
-from sparkmi.ops import linear as LIN  # noqa: E402
+LIN = importlib.import_module("sparkmi.ops.linear")  # the module (sparkmi.ops.linear is also a function)
 from sparkmi.utils.flat import FlatParams  # noqa: E402
 
 C = _native.C()
