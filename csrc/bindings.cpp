@@ -100,6 +100,7 @@ int smi_gemm_wgrad_group(const void* const*, const long*, const void* const*, co
 int smi_cnn(const CNNArgs*, hipStream_t);
 int smi_cnn_fused_ok(int, int, int);
 long smi_emb_pair_max(long);
+int smi_emb_plan_algo(long, long);
 int smi_emb_plan(const long long*, long, long long, long, void*, hipStream_t);
 int smi_emb_sum(int, int, const long long*, const void*, float*, long, int, long long, const uint32_t*, uint32_t,
                 uint32_t, float, long, void*, hipStream_t);
@@ -565,6 +566,8 @@ PYBIND11_MODULE(_C, m) {
         "fp32 attention dK/dV: 1 = staggered 8-wave kernel (default), 0 = lockstep; -1 queries");
   m.def("emb_pair_max", [](long set) { return smi_emb_pair_max(set); },
         "largest token batch the pair-compare embedding backward takes (set < 0 queries)");
+  m.def("emb_plan_algo", [](long T, long V) { return smi_emb_plan_algo(T, V); },
+        "the ordering algorithm emb_plan picks for T tokens over V rows (1 pair, 2 bucketed, 0 none)");
   m.def("emb_plan", [](u ids, long T, long long pad, long V, u ws, u st) {
         return smi_emb_plan((const long long*)ids, T, pad, V, (void*)ws, S(st)); },
         "ordering half of the deterministic embedding backward (ids only); returns the algorithm for emb_sum");
@@ -587,7 +590,7 @@ PYBIND11_MODULE(_C, m) {
                    u dpred, u dhn, u dcn, u g_emb, std::vector<u> g_w_ih, std::vector<u> g_w_hh, std::vector<u> g_b_ih,
                    std::vector<u> g_b_hh, u g_w_fc, u g_b_fc, u dh0, u dc0, u g_slab, u g_xe, long V, u emb_ws,
                    u pred_last, int dpred_last, u ce_labels, u ce_row, u ce_dlast, u ce_loss, u ce_tick,
-                   u dpred_scale, int emb_planned, u st) {
+                   u dpred_scale, int emb_planned, int emb_side, u emb_tick, u st) {
     if (L < 1 || L > LSTM_MAXL || (int)w_ih.size() != L || (int)w_hh.size() != L || (int)b_ih.size() != L ||
         (int)b_hh.size() != L)
       throw std::runtime_error("lstm: need L pointers per weight list");
@@ -615,6 +618,7 @@ PYBIND11_MODULE(_C, m) {
     a.ce_labels = (const long long*)ce_labels; a.ce_row = (float*)ce_row; a.ce_dlast = (float*)ce_dlast;
     a.ce_loss = (float*)ce_loss; a.ce_tick = (unsigned*)ce_tick; a.dpred_scale = (const float*)dpred_scale;
     a.emb_planned = emb_planned;
+    a.emb_side = emb_side; a.emb_tick = (unsigned*)emb_tick; a.emb_V = V;
     if (a.ce_labels && (!a.ce_row || !a.ce_dlast || !a.ce_loss || !a.ce_tick || a.C > LSTM_MAXC))
       throw std::runtime_error("lstm: fused CE needs row, dlast, loss and ticket buffers");
     chk(smi_lstm(&a, backward, S(st)), "lstm");

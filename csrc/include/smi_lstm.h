@@ -38,9 +38,14 @@ struct LSTMArgs {
   const long long* ce_labels; float* ce_row; float* ce_dlast; float* ce_loss; unsigned* ce_tick;
   const float* dpred_scale;                // backward: dpred x this device scalar (the loss's dloss)
   int emb_planned;                         // backward: emb_ws already holds the ordering of ids
-                                           // (smi_emb_plan's algorithm, run beside the forward): sum only
+                                           // (the algorithm the forward planned with): sum only
+  // forward: order the ids for the embedding backward into emb_ws during this launch (pair path:
+  // extra workgroups beside the recurrence's B, on CUs it leaves idle; emb_tick: one zeroed
+  // counter, re-armed); else smi_emb_plan on the stream first
+  int emb_side; unsigned* emb_tick; long emb_V;
 };
 #define LSTM_MAXT 2048
 #define LSTM_TCH 64  // timesteps per LDS-staged chunk in the kernels' tail phases
 #define LSTM_WCH 16  // backward: ticks of per-tick outputs staged in LDS between burst stores (power of 2)
 #define LSTM_XW 64   // two-wave forward: ticks per LDS window of layer-0 inputs
+#define LSTM_EMB_MAX 4608  // tokens (B x T) the forward launch orders itself (LDS-resident plan)

@@ -12,6 +12,7 @@
 // purpose: the reference's Adam decays every row.
 #include "smi_common.h"
 #include "smi_split3.h"
+#include "smi_emb_pair.h"
 
 // T = storage of the table copy and the output: unsigned short (bf16 shadow) or float (fp32
 // reference-precision path: the fp32 master table itself).
@@ -413,104 +414,16 @@ __global__ __launch_bounds__(256) void emb_det_combine(float* __restrict__ dtabl
 //     the group's last chunk to finish (ticket) adds them in chunk order.
 // Every table row is one fixed-order fp32 sum: bit-reproducible, and long groups (a frequent word)
 // are spread over several workgroups.
-#define EMB_PAIR_MAX 8192
-#define EMB_CH 32
-struct EmbPair {
-  int* rank; int* first; int* list;
-  int* ch_owner; int* ch_start; int* ch_len; int* ch_g0; int* ch_gn;  // per chunk
-  unsigned* tick;   // per group (indexed by its first chunk), zeroed by emb_pair_plan
-  int* nchunks;
-  float* part;      // [T][D] chunk partials of multi-chunk groups
-};
-
 __global__ __launch_bounds__(1024) void emb_pair_rank(const long long* __restrict__ ids, long T, long long pad, EmbPair e) {
   __shared__ __attribute__((aligned(16))) int s_id[EMB_PAIR_MAX];
   __shared__ int s_cnt[16][64], s_min[16][64];
-  const int p0 = blockIdx.x * 64;
-  const int n = (int)min((long)p0 + 64, T);  // positions 0 .. n - 1 compared
-  const int n4 = (n + 3) & ~3;
-  for (int i = threadIdx.x; i < n4; i += 1024) s_id[i] = i < n ? (int)ids[i] : -2;
-  __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int p = p0 + lane;
-  const int myid = p < n ? s_id[p] : -3;
-  const bool live = p < n && (long long)myid != pad && myid >= 0;
-  const int per = ((n4 / 4 + 15) / 16) * 4;  // positions per wave (multiple of 4)
-  const int q0 = w * per, q1 = min(q0 + per, n4);
-  int cnt = 0, fmin = p;
-  for (int q = q0; q < q1; q += 4) {
-    const int4 v = *(const int4*)(s_id + q);  // same address on every lane: a broadcast read
-    const int vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const bool eq = vv[k] == myid && q + k < p;
-      cnt += eq ? 1 : 0;
-      fmin = eq ? min(fmin, q + k) : fmin;
-    }
-  }
-  s_cnt[w][lane] = cnt;
-  s_min[w][lane] = fmin;
-  __syncthreads();
-  if (threadIdx.x < 64 && p < T) {
-    int c = 0, f = p;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) { c += s_cnt[k][lane]; f = min(f, s_min[k][lane]); }
-    e.rank[p] = c;
-    e.first[p] = live ? f : -1;
-  }
+  emb_pair_rank_tile<1024, false>(ids, T, pad, e, blockIdx.x * 64, s_id, s_cnt, s_min);
 }
 
 __global__ __launch_bounds__(1024) void emb_pair_plan(long T, EmbPair e) {
   __shared__ int s_f[EMB_PAIR_MAX], s_off[EMB_PAIR_MAX], s_coff[EMB_PAIR_MAX];
   __shared__ int s_wsum[2][16];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int n = (int)T;
-  for (int i = tid; i < n; i += 1024) { s_f[i] = e.first[i]; s_off[i] = 0; }
-  __syncthreads();
-  for (int i = tid; i < n; i += 1024)
-    if (s_f[i] >= 0) atomicAdd(&s_off[s_f[i]], 1);  // group sizes (integer adds: order-free)
-  __syncthreads();
-  // chunks per group, then exclusive scans of sizes and chunk counts over the positions: thread
-  // tid owns the contiguous range [tid * per, ...) — serial inside, wave / block prefix outside
-  const int per = (n + 1023) / 1024, a0 = min(n, tid * per), a1 = min(n, a0 + per);
-  int ssum = 0, csum = 0;
-  for (int i = a0; i < a1; ++i) {
-    const int c = s_off[i];
-    s_coff[i] = (c + EMB_CH - 1) / EMB_CH;
-    ssum += c;
-    csum += s_coff[i];
-  }
-  int sx = ssum, cx = csum;  // inclusive wave scans
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int ys = __shfl_up(sx, d, 64), yc = __shfl_up(cx, d, 64);
-    if (lane >= d) { sx += ys; cx += yc; }
-  }
-  if (lane == 63) { s_wsum[0][w] = sx; s_wsum[1][w] = cx; }
-  __syncthreads();
-  int sb = 0, cb = 0;
-  for (int k = 0; k < w; ++k) { sb += s_wsum[0][k]; cb += s_wsum[1][k]; }
-  int so = sb + sx - ssum, co = cb + cx - csum;  // exclusive prefix of this thread's range
-  for (int i = a0; i < a1; ++i) {
-    const int c = s_off[i], nc = s_coff[i];
-    s_off[i] = so;
-    s_coff[i] = co;
-    // chunk table of the group first at position i
-    for (int k = 0; k < nc; ++k) {
-      e.ch_owner[co + k] = i;
-      e.ch_start[co + k] = so + k * EMB_CH;
-      e.ch_len[co + k] = min(EMB_CH, c - k * EMB_CH);
-      e.ch_g0[co + k] = co;
-      e.ch_gn[co + k] = nc;
-      e.tick[co + k] = 0u;
-    }
-    so += c;
-    co += nc;
-  }
-  if (tid == 1023) *e.nchunks = co;
-  __syncthreads();
-  for (int i = tid; i < n; i += 1024)
-    if (s_f[i] >= 0) e.list[s_off[s_f[i]] + e.rank[i]] = i;  // position order within the group
+  emb_pair_plan_body<1024, false>(T, e, s_f, s_off, s_coff, s_wsum);
 }
 
 template <typename TS>
@@ -615,22 +528,6 @@ extern "C" int smi_emb_pair(int set) {
   return g_emb_pair;
 }
 
-static EmbPair emb_pair_layout(void* ws, long T) {
-  EmbPair e{};
-  int* p = (int*)ws;
-  e.rank = p; p += T;
-  e.first = p; p += T;
-  e.list = p; p += T;
-  e.ch_owner = p; p += T;
-  e.ch_start = p; p += T;
-  e.ch_len = p; p += T;
-  e.ch_g0 = p; p += T;
-  e.ch_gn = p; p += T;
-  e.tick = (unsigned*)p; p += T;
-  e.nchunks = p; p += 4;
-  e.part = (float*)p;
-  return e;
-}
 
 static EmbDet emb_det_layout(void* ws, long T, long V) {
   EmbDet d{};
@@ -702,6 +599,11 @@ static int emb_bwd_launch(const long long* ids, const void* dout, float* dtable,
   return emb_sum_launch<TS>(algo, ids, dout, dtable, T, D, padding_idx, seedp, salt, thresh, dscale, V, ws, st);
 }
 
+// the algorithm smi_emb_plan picks for T tokens over V rows (ws given)
+extern "C" int smi_emb_plan_algo(long T, long V) {
+  if (V <= 0 || T <= 0) return 0;
+  return T <= emb_pair_sel() && smi_emb_pair(-1) ? 1 : 2;
+}
 extern "C" int smi_emb_plan(const long long* ids, long T, long long padding_idx, long V, void* ws, hipStream_t st) {
   return emb_plan_launch(ids, T, padding_idx, V, ws, st);
 }

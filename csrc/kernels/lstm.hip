@@ -27,6 +27,7 @@
 // lstm_xe_kernel's per-token W_ih0^T da0.  No float atomics anywhere: bit-reproducible.
 #include "smi_common.h"
 #include "smi_lstm.h"
+#include "smi_emb_pair.h"
 
 // v_rcp_f32 (1 ulp) instead of the IEEE division sequence (~10 dependent instructions): the
 // activations sit on the recurrence's serial chain three times per tick
@@ -411,8 +412,35 @@ __global__ __launch_bounds__(NT) void lstm_bwd_kernel(LSTMArgs a) {
 typedef float smi_f2 __attribute__((ext_vector_type(2)));
 #define SMI_WAVE_LDS_ORDER() asm volatile("" ::: "memory")  // compiler order only: LDS is in-order per wave
 
+// Workgroups B .. of the forward launch (LSTMArgs::emb_side): the pair-compare ordering of the
+// B x T ids for the embedding backward, on CUs the B recurrence workgroups leave idle (it ran
+// serialised after the forward as its own launches, 24 us of the step).  Each takes a tile of 64
+// tokens; the last to finish (ticket, write-through hand-off) builds the plan in LDS.
+__device__ __forceinline__ void lstm_emb_side(const LSTMArgs& a) {
+  __shared__ __attribute__((aligned(16))) int s_id[LSTM_EMB_MAX];
+  __shared__ int s_cnt[2][64], s_min[2][64];
+  __shared__ int s_f[LSTM_EMB_MAX], s_off[LSTM_EMB_MAX], s_coff[LSTM_EMB_MAX];
+  __shared__ int s_wsum[2][2];
+  __shared__ int s_last;
+  const long T = (long)a.B * a.T;
+  const EmbPair e = emb_pair_layout(a.emb_ws, T);
+  const int ntile = (int)((T + 63) / 64);
+  emb_pair_rank_tile<128, true>(a.ids, T, a.pad_idx, e, (blockIdx.x - a.B) * 64, s_id, s_cnt, s_min);
+  smi_wt_drain();
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(a.emb_tick, 1u) == (unsigned)ntile - 1;
+  __syncthreads();
+  if (!s_last) return;
+  emb_pair_plan_body<128, true>(T, e, s_f, s_off, s_coff, s_wsum);
+  if (threadIdx.x == 0) a.emb_tick[0] = 0u;
+}
+
 template <int H, int MI>
 __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
+  if ((int)blockIdx.x >= a.B) {  // the embedding-backward ordering workgroups (uniform)
+    lstm_emb_side(a);
+    return;
+  }
   LSTAMP_DECL;
   const int b = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int L = a.L, T = a.T, E = a.E, C = a.C;
@@ -1138,7 +1166,8 @@ static int lstm_launch(const LSTMArgs* a, int backward, hipStream_t st) {
         if (a->C <= 4) hipLaunchKernelGGL((lstm_bwd_w2_kernel<H, MI, 4>), dim3(a->B), dim3(128), 0, st, *a);
         else hipLaunchKernelGGL((lstm_bwd_w2_kernel<H, MI, LSTM_MAXC>), dim3(a->B), dim3(128), 0, st, *a);
       } else {
-        hipLaunchKernelGGL((lstm_fwd_w2_kernel<H, MI>), dim3(a->B), dim3(128), 0, st, *a);
+        const int side = a->emb_side == 1 ? (int)(((long)a->B * a->T + 63) / 64) : 0;
+        hipLaunchKernelGGL((lstm_fwd_w2_kernel<H, MI>), dim3(a->B + side), dim3(128), 0, st, *a);
       }
       return (int)hipGetLastError();
     }
@@ -1182,8 +1211,28 @@ extern "C" long smi_lstm_slab_floats(int B, int E, int H, int L, int C) {
   return lstm_part_off(a, L + 1, 0);  // partial tiles of every layer and the head
 }
 
-extern "C" int smi_lstm(const LSTMArgs* a, int backward, hipStream_t st) {
+extern "C" int smi_emb_plan(const long long* ids, long T, long long padding_idx, long V, void* ws, hipStream_t st);
+extern "C" int smi_emb_plan_algo(long T, long V);
+
+extern "C" int smi_lstm(const LSTMArgs* args, int backward, hipStream_t st) {
+  LSTMArgs ab = *args;
+  const LSTMArgs* a = &ab;
   if (!smi_lstm_supported(a->E, a->H, a->L, a->C) || a->B < 1 || a->T < 1 || a->T > LSTM_MAXT) return -1;
+  if (!backward && a->emb_side) {
+    // order the ids for the embedding backward in this launch (pair path, w2 kernel) or, when
+    // that does not apply, with the standalone ordering launches first
+    const long T = (long)a->B * a->T;
+    const int algo = smi_emb_plan_algo(T, a->emb_V);
+    const bool w2 = a->L * a->H <= 64 && lstm_w2_enabled() && (a->H == 16 || a->H == 32) &&
+                    (a->E <= a->H ? a->H : 2 * a->H) + a->H <= 64;
+    if (!a->emb_ws || !a->emb_tick || algo == 0) return -1;  // the caller counts on a plan
+    if (algo == 1 && T <= LSTM_EMB_MAX && w2) {
+      ab.emb_side = 1;
+    } else {
+      if (smi_emb_plan(a->ids, T, a->pad_idx, a->emb_V, a->emb_ws, st) != algo) return -1;
+      ab.emb_side = 2;  // planned already: no side workgroups
+    }
+  }
   if (backward && (!a->g_slab || (a->g_emb && (!a->g_xe || a->V < 1 || !a->emb_ws)))) return -1;
   const int H = a->H;
   const bool wide = a->E > H;

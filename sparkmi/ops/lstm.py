@@ -88,20 +88,28 @@ class LSTMFn(torch.autograd.Function):
             labels = labels.to(torch.int64).contiguous()
             ce = (torch.empty(B, device=dev, dtype=torch.float32), torch.empty(B, C, device=dev, dtype=torch.float32),
                   torch.empty((), device=dev, dtype=torch.float32), _ce_ticket(dev))
+        # the embedding backward's id ordering, made by this launch on CUs the recurrence leaves
+        # idle (csrc/kernels/lstm.hip lstm_emb_side); the backward only sums
+        plan_ws = None
+        if ctx.needs_input_grad[3 + getattr(ctx, "h0_input", 1)] and len(meta) > 5 and meta[5]:
+            C_ = _native.C()
+            plan_ws = torch.empty(C_.emb_det_ws_bytes(B * T, emb.shape[0], E), device=dev, dtype=torch.uint8)
         _native.C().lstm(0, ids.data_ptr(), B, T, E, H, L, C, pad_idx, emb.data_ptr(),
                          [lw[0].data_ptr() for lw in layers], [lw[1].data_ptr() for lw in layers],
                          [lw[2].data_ptr() for lw in layers], [lw[3].data_ptr() for lw in layers],
                          w_fc.data_ptr(), b_fc.data_ptr(), _native.ptr(h0c), _native.ptr(c0c), pred.data_ptr(),
                          hn.data_ptr(), cn.data_ptr(), ws.data_ptr(), 0, rng.ptr() if rng is not None else 0, salt,
-                         thresh, _rng.scale(p), 0, 0, 0, 0, [], [], [], [], 0, 0, 0, 0, 0, 0, 0, 0,
+                         thresh, _rng.scale(p), 0, 0, 0, 0, [], [], [], [], 0, 0, 0, 0, 0, 0,
+                         emb.shape[0] if plan_ws is not None else 0, _native.ptr(plan_ws),
                          last.data_ptr(), 0, labels.data_ptr() if ce else 0, ce[0].data_ptr() if ce else 0,
                          ce[1].data_ptr() if ce else 0, ce[2].data_ptr() if ce else 0, ce[3].data_ptr() if ce else 0,
-                         0, 0, _native.stream())
-        ctx.emb_plan = None
+                         0, 0, int(plan_ws is not None), _ce_ticket(dev)[1:].data_ptr(), _native.stream())
         # (inside Function.forward grad mode is off: the embedding's needs_input_grad says whether
-        # a backward will want the table gradient; the inputs before it: ids, [labels,] h0, c0, meta)
-        if ctx.needs_input_grad[3 + getattr(ctx, "h0_input", 1)] and len(meta) > 5 and meta[5]:
-            ctx.emb_plan = _plan_embedding(ids, B * T, pad_idx, emb)
+        # a backward will want the table gradient; the inputs before it: ids, [labels,] h0, c0, meta;
+        # meta[5]: grad mode at the call)
+        ctx.emb_plan = None
+        if plan_ws is not None:
+            ctx.emb_plan = (plan_ws, _native.C().emb_plan_algo(B * T, emb.shape[0]))
         ctx.meta = (L, p, rng, salt, pad_idx, B, T, E, H, C)
         ctx.has_h0, ctx.has_c0 = h0 is not None, c0 is not None
         ctx.save_for_backward(ids, ws, h0c, c0c, *params)
@@ -147,9 +155,7 @@ class LSTMFn(torch.autograd.Function):
         want_emb = orig[0].requires_grad
         xe = torch.empty(B, T, E, device=dev, dtype=torch.float32) if want_emb else None
         plan = getattr(ctx, "emb_plan", None) if want_emb else None
-        if plan is not None:  # the ordering ran beside the forward: join it, sum only
-            from .embedding import _join
-            _join(plan)
+        if plan is not None:  # the forward launch ordered the ids already: sum only
             ews = plan[0]
         else:
             ews = torch.empty(C_.emb_det_ws_bytes(B * T, emb.shape[0], emb.shape[1]), device=dev,
@@ -165,8 +171,8 @@ class LSTMFn(torch.autograd.Function):
                          [lw[2].data_ptr() for lw in g_layers], [lw[3].data_ptr() for lw in g_layers],
                          g_fc.data_ptr(), g_bfc.data_ptr(), _native.ptr(dh0), _native.ptr(dc0), slab.data_ptr(),
                          _native.ptr(xe), emb.shape[0], _native.ptr(ews), 0, last_only, 0, 0, 0, 0,
-                         _ce_ticket(dev)[8:].data_ptr(), _native.ptr(dscale), plan[2] if plan is not None else 0,
-                         _native.stream())
+                         _ce_ticket(dev)[8:].data_ptr(), _native.ptr(dscale), plan[1] if plan is not None else 0,
+                         0, 0, _native.stream())
         ctx.emb_plan = None
         grad_ready(*orig)
         return (None, dh0 if ctx.has_h0 else None, dc0 if ctx.has_c0 else None, None) + (None,) * len(params)
@@ -175,10 +181,6 @@ class LSTMFn(torch.autograd.Function):
 _CE_TICKETS = {}
 
 
-def _plan_embedding(ids, T, pad_idx, emb):
-    """See sparkmi.ops.embedding.plan_backward (the recurrence keeps only 32 of 256 CUs busy)."""
-    from .embedding import plan_backward
-    return plan_backward(ids, T, pad_idx, emb)
 
 
 def _ce_ticket(dev):
