@@ -25,6 +25,8 @@ def sinusoid_table(max_len: int, d_model: int) -> torch.Tensor:
 
 
 
+# SPARKMI_EMB_PLAN_AHEAD=0: the whole ordering + sum in the backward (A/B switch)
+PLAN_AHEAD = __import__("os").environ.get("SPARKMI_EMB_PLAN_AHEAD", "1") != "0"
 _PLAN_STREAMS = {}
 _PENDING = []  # forked plans not yet joined: [ws, stream, algo, joined]
 
@@ -115,7 +117,7 @@ class EmbeddingFn(torch.autograd.Function):
                 x = x * _rng.keep_mask(x.shape, p, ctx.seed, salt, x.device).to(x.dtype) * _rng.scale(p)
             out = x.to(out_dtype)
         ctx.plan = None
-        if ctx.native and plan and ctx.needs_input_grad[1]:  # plan: grad mode was on at the call
+        if ctx.native and plan and PLAN_AHEAD and ctx.needs_input_grad[1]:  # plan: grad mode on at the call
             ctx.plan = plan_backward(ids_c, T, ctx.pad, weight)
         ctx.save_for_backward(ids_c, weight)
         return out
