@@ -163,6 +163,18 @@ def test_embedding_backward_deterministic(n_tok):
     ref = torch.zeros(V, D, dtype=torch.float64).index_add_(0, ids, do.cpu().double())
     _close(grads[0], ref, 1e-4, 1e-5, "emb grad")
     assert torch.equal(grads[0], grads[1])
+    # the id ordering made in the backward (plan-ahead off) instead of beside the forward: same bits
+    import importlib
+    E = importlib.import_module("sparkmi.ops.embedding")
+    prev, E.PLAN_AHEAD = E.PLAN_AHEAD, False
+    try:
+        w.grad = None
+        out = embedding(ids.to(dev), w, None, 0.0, R.DropoutRNG(1).to(dev), 5, padding_idx=None,
+                        out_dtype=torch.float32)
+        out.backward(do)
+    finally:
+        E.PLAN_AHEAD = prev
+    assert torch.equal(grads[0], w.grad)
 
 
 @pytest.mark.parametrize("D", [512, 96])

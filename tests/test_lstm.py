@@ -106,6 +106,14 @@ def test_lstm_gradients_bit_reproducible():
         out.append(_grads(m))
     for a, b in zip(*out):
         assert torch.equal(a, b)
+    # the id ordering made by the forward launch's side workgroups (the path above) vs made by the
+    # backward itself (meta without the grad-mode flag: no plan): the same bits
+    for q in params:
+        q.grad = None
+    pred, _, _, _ = LS.LSTMFn.apply(ids, None, None, (L, 0.5, m.rng, m.salt, pad), *params)
+    pred[:, -1].square().sum().backward()
+    for a, b in zip(out[0], _grads(m)):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.gpu
