@@ -91,7 +91,8 @@ class LSTMFn(torch.autograd.Function):
         # the embedding backward's id ordering, made by this launch on CUs the recurrence leaves
         # idle (csrc/kernels/lstm.hip lstm_emb_side); the backward only sums
         plan_ws = None
-        if ctx.needs_input_grad[3 + getattr(ctx, "h0_input", 1)] and len(meta) > 5 and meta[5]:
+        if (EMB_IN_FORWARD and ctx.needs_input_grad[3 + getattr(ctx, "h0_input", 1)] and len(meta) > 5
+                and meta[5]):
             C_ = _native.C()
             plan_ws = torch.empty(C_.emb_det_ws_bytes(B * T, emb.shape[0], E), device=dev, dtype=torch.uint8)
         _native.C().lstm(0, ids.data_ptr(), B, T, E, H, L, C, pad_idx, emb.data_ptr(),
@@ -179,6 +180,9 @@ class LSTMFn(torch.autograd.Function):
 
 
 _CE_TICKETS = {}
+# the embedding backward's id ordering made by the forward launch (SMI_LSTM_EMB_SIDE=1) or by the
+# backward itself (0)
+EMB_IN_FORWARD = __import__("os").environ.get("SMI_LSTM_EMB_SIDE", "1") != "0"
 
 
 
