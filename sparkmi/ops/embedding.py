@@ -47,8 +47,10 @@ def _join(plan):
     if not plan[3]:
         torch.cuda.current_stream(plan[1].device).wait_stream(plan[1])
         plan[3] = True
-    if plan in _PENDING:
-        _PENDING.remove(plan)
+    for i, q in enumerate(_PENDING):  # by identity (the entries hold tensors)
+        if q is plan:
+            del _PENDING[i]
+            break
 
 
 def plan_backward(ids, T, pad_idx, weight):
