@@ -565,6 +565,22 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   float* wacc = lg + 16;                 // max(C, CI)*C*9 + C wgrad accumulators
   const int WC = C > CI ? C : CI;
   float* wscr = wacc + WC * C * 9 + C;   // conv_wgrad per-unit 16x16 partial tiles (WG_SCRATCH floats)
+  // the four conv layers' weights and biases, staged once: every conv table build / fp32 conv
+  // read them from global memory per layer (a dependent L2 round trip inside each phase)
+  float* wst = wscr + WG_SCRATCH + 2;
+  const float* lw[4];
+  const float* lb[4];
+  {
+    int o = 0;
+    for (int l = 0; l < 4; ++l) {
+      const int n = C * (l == 0 ? CI : C) * 9;
+      for (int i = threadIdx.x; i < n; i += blockDim.x) wst[o + i] = g.w[l][i];
+      for (int i = threadIdx.x; i < C; i += blockDim.x) wst[o + n + i] = g.b[l][i];
+      lw[l] = wst + o;
+      lb[l] = wst + o + n;
+      o += n + C;
+    }
+  }
   const int total = CI * PL28 + 2 * C * PL28 + 3 * C * PL14 + C * 49 + 16 + WC * C * 9 + C;
   for (int i = threadIdx.x; i < total; i += blockDim.x) sm[i] = 0.f;
   if (threadIdx.x == 0) { wscr[WG_SCRATCH] = 0.f; wscr[WG_SCRATCH + 1] = 1.f; }  // conv_wgrad pad cells
@@ -579,23 +595,23 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   }
   __syncthreads();
   STAMP(1);
-  if (BF) conv_mfma<28, P28, false, false>(xin, CI, a1, C, g.w[0], g.b[0], wscr);
-  else conv_fwd<28, P28, CC, EX>(xin, CI, a1, C, g.w[0], g.b[0]);
+  if (BF) conv_mfma<28, P28, false, false>(xin, CI, a1, C, lw[0], lb[0], wscr);
+  else conv_fwd<28, P28, CC, EX>(xin, CI, a1, C, lw[0], lb[0]);
   __syncthreads();
   STAMP(2);
-  if (BF) conv_mfma<28, P28, false, false>(a1, C, a2, C, g.w[1], g.b[1], wscr);
-  else conv_fwd<28, P28, CC, EX>(a1, C, a2, C, g.w[1], g.b[1]);
+  if (BF) conv_mfma<28, P28, false, false>(a1, C, a2, C, lw[1], lb[1], wscr);
+  else conv_fwd<28, P28, CC, EX>(a1, C, a2, C, lw[1], lb[1]);
   __syncthreads();
   STAMP(3);
   pool_fwd<28, P28, P14, 1>(a2, p1, C);
   __syncthreads();
   STAMP(4);
-  if (BF) conv_mfma<14, P14, false, false>(p1, C, a3, C, g.w[2], g.b[2], wscr);
-  else conv_fwd<14, P14, CC, EX>(p1, C, a3, C, g.w[2], g.b[2]);
+  if (BF) conv_mfma<14, P14, false, false>(p1, C, a3, C, lw[2], lb[2], wscr);
+  else conv_fwd<14, P14, CC, EX>(p1, C, a3, C, lw[2], lb[2]);
   __syncthreads();
   STAMP(5);
-  if (BF) conv_mfma<14, P14, false, false>(a3, C, a4, C, g.w[3], g.b[3], wscr);
-  else conv_fwd<14, P14, CC, EX>(a3, C, a4, C, g.w[3], g.b[3]);
+  if (BF) conv_mfma<14, P14, false, false>(a3, C, a4, C, lw[3], lb[3], wscr);
+  else conv_fwd<14, P14, CC, EX>(a3, C, a4, C, lw[3], lb[3]);
   __syncthreads();
   STAMP(6);
   pool_fwd<14, P14, 7, 0>(a4, p2, C);
@@ -677,8 +693,8 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
     smi_wt_store(gs + (e < C * C * 9 ? g.off[6] + e : g.off[7] + e - C * C * 9), wacc[e]);
     wacc[e] = 0.f;
   }
-  if (BF) conv_mfma<14, P14, true, true>(a4, C, a3, C, g.w[3], nullptr, wscr);
-  else conv_dgrad<14, P14, CC, EX>(a4, C, g.w[3], C, a3, true);
+  if (BF) conv_mfma<14, P14, true, true>(a4, C, a3, C, lw[3], nullptr, wscr);
+  else conv_dgrad<14, P14, CC, EX>(a4, C, lw[3], C, a3, true);
   __syncthreads();
   STAMP(14);
   // conv3: dW3 (dz3, p1); dp1 = convT(dz3) into p1 (no relu: p1 is a pool output)
@@ -690,8 +706,8 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
     smi_wt_store(gs + (e < C * C * 9 ? g.off[4] + e : g.off[5] + e - C * C * 9), wacc[e]);
     wacc[e] = 0.f;
   }
-  if (BF) conv_mfma<14, P14, true, false>(a3, C, p1, C, g.w[2], nullptr, wscr);
-  else conv_dgrad<14, P14, CC, EX>(a3, C, g.w[2], C, p1, false);
+  if (BF) conv_mfma<14, P14, true, false>(a3, C, p1, C, lw[2], nullptr, wscr);
+  else conv_dgrad<14, P14, CC, EX>(a3, C, lw[2], C, p1, false);
   __syncthreads();
   STAMP(16);
   // pool1 backward + relu'(a2): dz2 in a2
@@ -707,8 +723,8 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
     smi_wt_store(gs + (e < C * C * 9 ? g.off[2] + e : g.off[3] + e - C * C * 9), wacc[e]);
     wacc[e] = 0.f;
   }
-  if (BF) conv_mfma<28, P28, true, true>(a2, C, a1, C, g.w[1], nullptr, wscr);
-  else conv_dgrad<28, P28, CC, EX>(a2, C, g.w[1], C, a1, true);
+  if (BF) conv_mfma<28, P28, true, true>(a2, C, a1, C, lw[1], nullptr, wscr);
+  else conv_dgrad<28, P28, CC, EX>(a2, C, lw[1], C, a1, true);
   __syncthreads();
   STAMP(19);
   // conv1: dW1 (dz1, x)
@@ -748,8 +764,9 @@ static size_t cnn_lds_bytes(const CNNArgs& g) {
   const int C = g.C, CI = g.cin;
   // + conv_wgrad scratch (WG_SCRATCH floats)
   const int WC = C > CI ? C : CI;  // wgrad accumulators hold [C][max(C, CI)*9] + C
+  // + the staged conv weights and biases (C * CI * 9 + 3 * C * C * 9 + 4 * C)
   return sizeof(float) * (size_t)(CI * PL28 + 2 * C * PL28 + 3 * C * PL14 + C * 49 + 16 + WC * C * 9 + C + 4 +
-                                  WG_SCRATCH + 2);
+                                  WG_SCRATCH + 2 + C * CI * 9 + 3 * C * C * 9 + 4 * C);
 }
 
 extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
