@@ -98,7 +98,7 @@ void smi_gemm_set_bm(int);
 int smi_gemm_wgrad_group(const void* const*, const long*, const void* const*, const long*, void* const*, void* const*,
                          const int*, const int*, const int*, int, hipStream_t);
 int smi_cnn(const CNNArgs*, hipStream_t);
-int smi_cnn_fused_ok(int, int, int);
+int smi_cnn_fused_ok(int, int, int, int);
 long smi_emb_pair_max(long);
 int smi_emb_plan_algo(long, long);
 int smi_emb_plan(const long long*, long, long long, long, void*, hipStream_t);
@@ -578,7 +578,7 @@ PYBIND11_MODULE(_C, m) {
         "summing half of the embedding backward after emb_plan");
   m.def("emb_pair", [](int set) { return smi_emb_pair(set); },
         "deterministic embedding backward: 1 = pair-compare (<= 8192 tokens), 0 = bucketed lists; -1 queries");
-  m.def("cnn_fused_ok", [](int C, int cin, int classes) { return smi_cnn_fused_ok(C, cin, classes) != 0; });
+  m.def("cnn_fused_ok", [](int C, int cin, int classes, int B) { return smi_cnn_fused_ok(C, cin, classes, B) != 0; });
 
   m.def("lstm_supported", [](int E, int H, int L, int C) { return smi_lstm_supported(E, H, L, C) != 0; });
   m.def("lstm_slab_floats", [](int B, int E, int H, int L, int C) { return smi_lstm_slab_floats(B, E, H, L, C); });

@@ -19,6 +19,7 @@ struct CNNArgs {
   // step counter.  part: [ceil(B / CNN_GRP)][P] group sums; tick: CNN_GRP + 1 zeroed counters
   // (re-armed by the kernel), owned by the model.
   int fused;
+  int wstage;  // set by the launcher: the bf16 convs read LDS-staged weights (when they fit)
   float* part; unsigned* tick; const float* lr; float* step;
   unsigned short* shadow[10];                // per-parameter bf16 shadows (slab order) or null
 };

@@ -214,5 +214,19 @@ __device__ __forceinline__ float2 smi_cc_load2(const float* p) {
   const unsigned long long v = __hip_atomic_load((unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return make_float2(__uint_as_float((unsigned)v), __uint_as_float((unsigned)(v >> 32)));
 }
+// 16-B granules through a buffer resource (byte offset 16-B aligned), cache policy sc1 (aux bit
+// 4), the same device-scope policy as the atomics above.  A device-scope access is one memory
+// transaction per lane however wide it is (measured on the CNN tail: 4-B lanes ~17 GB/s per CU),
+// so the widest granule moves 4x the bytes per transaction.
+__device__ __forceinline__ float4 smi_cc_load4(__amdgpu_buffer_rsrc_t rs, int byte_off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 16));
+}
+__device__ __forceinline__ void smi_wt_store4(__amdgpu_buffer_rsrc_t rs, int byte_off, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), rs,
+                                         byte_off, 0, 16);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t smi_rsrc(const void* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, bytes, 0x00020000);
+}
 __device__ __forceinline__ void smi_wt_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 

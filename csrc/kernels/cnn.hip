@@ -17,6 +17,7 @@
 // bit-reproducible) and accumulates into the model's gradient buffers.
 #include "smi_common.h"
 #include "smi_cnn.h"
+#include <type_traits>
 
 // One workgroup per image; 1024 threads (16 waves) so every phase of the per-image pipeline has
 // enough independent work items (the batch of 32 images occupies only 32 CUs)
@@ -469,77 +470,246 @@ __device__ __forceinline__ void conv_wgrad_bf16(const float* __restrict__ dz, co
   }
 }
 
+// Compact slab row (P floats, P % 4 == 0): the conv layers' gradients at their parameter offsets
+// [0, off[8]), then from the 16-B aligned cnn_cs(g) the image's logit gradient dl [NC] and pooled
+// activations p2 [F] in place of the NC x F fc outer product (the reducers form the batch sum of
+// dl[o] * p2[i]: a third of the bytes to hand off).
+__device__ __forceinline__ int cnn_cs(const CNNArgs& g) { return (g.off[8] + 3) & ~3; }
+
+// Pin a loaded value in its register here: the compiler's wait for it happens at this point (with
+// the level's other loads in flight alongside) and not in front of a later store, where its
+// conservative count-to-zero wait also drains every store before (one round trip per store).
+#define CNN_PIN(x) asm volatile("" : "+v"(x))
+
 // Fused SGD tail (CNNArgs::fused): the step's remaining work without a second launch.  Level 1:
-// the last image of each group of CNN_GRP to finish (ticket) sums the group's slabs in image order
-// into part[group]; level 2: the last group to finish sums the group partials in group order and
-// applies torch SGD (p -= lr * g) to every parameter, then the mean loss (image order) and the
-// step counter.  Hand-offs are write-through stores + device-scope loads (smi_common.h), no L2
-// fences; 8-B granules with every load of a thread's sum in flight together.  Deterministic:
-// every sum has a fixed order.  No spinning: a workgroup that is not the last simply exits.
-__device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img) {
+// the last image of each group of CNN_GRP to finish (ticket) sums the group's conv slab parts in
+// image order into part[group]; level 2: the last group to finish stages every image's dl / p2 in
+// LDS, sums the group partials in group order, forms the fc gradient as the image-order batch sum
+// of dl[o] * p2[i], and applies torch SGD (p -= lr * g) to every parameter, then the mean loss
+// (image order) and the step counter.  Hand-offs are write-through stores + device-scope loads in
+// 16-B granules (smi_common.h), no L2 fences.  Deterministic: every sum has a fixed order.  No
+// spinning: a workgroup that is not the last simply exits.
+__device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float* sm) {
   __shared__ int last;
   const int ngrp = (g.B + CNN_GRP - 1) / CNN_GRP;
   const int grp = img / CNN_GRP, g0 = grp * CNN_GRP, g1 = min(g.B, g0 + CNN_GRP);
+  const int off8 = g.off[8], NC = g.classes, F = g.C * 49, nt = blockDim.x, P = g.P;
+  const int cs = cnn_cs(g), n4 = cs >> 2;  // conv part in 16-B granules
+  const __amdgpu_buffer_rsrc_t rslab = smi_rsrc(g.slab, g.B * P * 4);
+  const __amdgpu_buffer_rsrc_t rpart = smi_rsrc(g.part, ngrp * P * 4);
   smi_wt_drain();  // this wave's slab stores reached the coherence point
   __syncthreads();
   if (threadIdx.x == 0) last = atomicAdd(g.tick + grp, 1u) == (unsigned)(g1 - g0 - 1);
   __syncthreads();
   if (!last) return;
-  const int P2 = g.P / 2;
-  float* part = g.part + (long)grp * g.P;
-  for (int q = threadIdx.x; q < P2; q += blockDim.x) {
-    float2 v[CNN_GRP];
+  STAMP(26);
+  // Loads below are unconditional (a lane's or image's out-of-range granule reads 0 through the
+  // buffer resource's range check, or a clamped valid address): a load under a branch makes the
+  // compiler wait for EVERY outstanding memory operation, stores included, before its first use,
+  // which serialised one store round trip per parameter (measured: 6 us in the fc update).
+  // level 1: the group's conv gradients, the group's slabs of a granule all in flight together
+  for (int q4 = threadIdx.x; q4 < n4; q4 += nt) {
+    float4 v[CNN_GRP];
 #pragma unroll
-    for (int i = 0; i < CNN_GRP; ++i)
-      if (g0 + i < g1) v[i] = smi_cc_load2(g.slab + (long)(g0 + i) * g.P + 2 * q);
-    float2 acc = v[0];
+    for (int i = 0; i < CNN_GRP; ++i) v[i] = smi_cc_load4(rslab, ((g0 + i) * P + 4 * q4) * 4);  // >= B: 0
+    float4 acc = v[0];
 #pragma unroll
-    for (int i = 1; i < CNN_GRP; ++i)
-      if (g0 + i < g1) { acc.x += v[i].x; acc.y += v[i].y; }
-    smi_wt_store2(part + 2 * q, acc.x, acc.y);
+    for (int i = 1; i < CNN_GRP; ++i) acc = make_float4(acc.x + v[i].x, acc.y + v[i].y, acc.z + v[i].z, acc.w + v[i].w);
+    smi_wt_store4(rpart, (grp * P + 4 * q4) * 4, acc);
   }
   smi_wt_drain();
   __syncthreads();
+  STAMP(27);
   if (threadIdx.x == 0) {
     g.tick[grp] = 0u;  // re-arm (every image of the group has taken its ticket)
     last = atomicAdd(g.tick + CNN_GRP, 1u) == (unsigned)(ngrp - 1);
   }
   __syncthreads();
   if (!last) return;
+  STAMP(28);
+  // level 2.  Stage every image's dl / p2 row (R4 floats) in LDS (the activation planes are free),
+  // sum the conv group partials in group order and form the fc gradient from the staged rows
+  const int R4 = (NC + F + 3) & ~3, ns4 = g.B * (R4 >> 2);
   const float lr = g.lr[0];
-  for (int q = threadIdx.x; q < P2; q += blockDim.x) {
-    float2 s;
-    if (ngrp <= 16) {  // every group's load in flight at once, then the group-order sum
-      float2 v[16];
+  float rl = 0.f;  // lane i: row losses i, i + 64, ...
+  if (threadIdx.x < 64)
+    for (int i = threadIdx.x; i < g.B; i += 64) rl += smi_cc_load(g.row_loss + i);
+  // fc: thread t owns column i of the fc weight for the classes of its half h (two halves of 8
+  // classes, o4 granules ob, ob+1, when NC > 8 and two columns per thread fit: all 16 waves busy)
+  const int H = (NC > 8 && 2 * F <= nt) ? 2 : 1, no4 = (H == 2 || NC <= 8) ? 2 : 4;
+  const int h = H == 2 ? (int)threadIdx.x / F : 0, ob = H == 2 ? 2 * h : 0;
+  const int i0 = (int)threadIdx.x - h * F;
+  const bool fc_on = h < H && i0 < F;
+  float* fw = const_cast<float*>(g.w[4]);
+  auto fc_load = [&](int i, float* pv) {  // column i's parameters (clamped addresses: no branch)
 #pragma unroll
-      for (int k = 0; k < 16; ++k) v[k] = k < ngrp ? smi_cc_load2(g.part + (long)k * g.P + 2 * q) : make_float2(0.f, 0.f);
-      s = v[0];
+    for (int t = 0; t < 16; ++t) pv[t] = fw[min(4 * ob + t, NC - 1) * F + min(max(i, 0), F - 1)];
+  };
+  float pfc[16];  // the thread's first column, loaded with the level's other loads
+  fc_load(i0, pfc);
+  float* fb = const_cast<float*>(g.b[4]);
+  const float pb = fb[min((int)threadIdx.x, NC - 1)];
+  auto conv_seg = [&](int p, int& seg, int& r) {
+    seg = 0;
+    while (seg < 7 && p >= g.off[seg + 1]) ++seg;
+    r = p - g.off[seg];
+    return (float*)(seg % 2 == 0 ? g.w[seg / 2] : g.b[seg / 2]) + r;
+  };
+  struct Conv4 { float pv[4]; float4 c[4]; };  // group partials 0..3 (batches up to 32 images)
+  auto conv_load = [&](int q4, Conv4& k) {
 #pragma unroll
-      for (int k = 1; k < 16; ++k)
-        if (k < ngrp) { s.x += v[k].x; s.y += v[k].y; }
-    } else {
-      s = smi_cc_load2(g.part + 2 * q);
-      for (int k = 1; k < ngrp; ++k) {
-        const float2 v = smi_cc_load2(g.part + (long)k * g.P + 2 * q);
-        s.x += v.x; s.y += v.y;
-      }
+    for (int u = 0; u < 4; ++u) {
+      int seg, r;
+      k.pv[u] = *conv_seg(min(4 * q4 + u, off8 - 1), seg, r);
     }
-    const float sv[2] = {s.x, s.y};
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int p = 2 * q + e;
-      int seg = 0;
-      while (seg < 9 && p >= g.off[seg + 1]) ++seg;
-      float* dst = (float*)(seg % 2 == 0 ? g.w[seg / 2] : g.b[seg / 2]) + (p - g.off[seg]);
-      const float np = *dst - lr * sv[e];
-      *dst = np;
-      if (g.shadow[seg]) g.shadow[seg][p - g.off[seg]] = f2bf(np);
+    for (int j = 0; j < 4; ++j) k.c[j] = smi_cc_load4(rpart, (j * P + 4 * q4) * 4);  // j >= ngrp: 0
+  };
+  auto conv_apply = [&](int q4, const Conv4& k) {
+    float4 gsum = k.c[0];
+#pragma unroll
+    for (int j = 1; j < 4; ++j) gsum = make_float4(gsum.x + k.c[j].x, gsum.y + k.c[j].y, gsum.z + k.c[j].z, gsum.w + k.c[j].w);
+    for (int j = 4; j < ngrp; ++j) {  // batches above 32 images
+      const float4 cj = smi_cc_load4(rpart, (j * P + 4 * q4) * 4);
+      gsum = make_float4(gsum.x + cj.x, gsum.y + cj.y, gsum.z + cj.z, gsum.w + cj.w);
+    }
+    const float gv[4] = {gsum.x, gsum.y, gsum.z, gsum.w};
+    float np[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      np[u] = k.pv[u] - lr * gv[u];
+      CNN_PIN(np[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = 4 * q4 + u;
+      if (q4 >= n4 || p >= off8) continue;
+      int seg, r;
+      float* dst = conv_seg(p, seg, r);
+      *dst = np[u];
+      if (g.shadow[seg]) g.shadow[seg][r] = f2bf(np[u]);
+    }
+  };
+  auto stage_load = [&](int e4, float4* v) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e4 + u * nt, im = e / (R4 >> 2), j4 = e - im * (R4 >> 2);
+      v[u] = smi_cc_load4(rslab, (im * P + cs + 4 * j4) * 4);  // im >= B: 0
+    }
+  };
+  auto stage_store = [&](int e4, const float4* v) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (e4 + u * nt < ns4) reinterpret_cast<float4*>(sm)[e4 + u * nt] = v[u];
+  };
+  if (n4 <= nt && ns4 <= 4 * nt) {
+    // one round trip: every staging and partial-sum load of the thread issued before the first use
+    float4 v[4];
+    Conv4 k;
+    stage_load(threadIdx.x, v);
+    conv_load(threadIdx.x, k);
+    stage_store(threadIdx.x, v);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) CNN_PIN(pfc[t]);
+    STAMP(21);
+    conv_apply(threadIdx.x, k);
+    STAMP(22);
+  } else {
+    for (int e4 = threadIdx.x; e4 < ns4; e4 += 4 * nt) {
+      float4 v[4];
+      stage_load(e4, v);
+      stage_store(e4, v);
+    }
+    for (int q4 = threadIdx.x; q4 < n4; q4 += nt) {
+      Conv4 k;
+      conv_load(q4, k);
+      conv_apply(q4, k);
     }
   }
+  __syncthreads();
+  STAMP(30);
+  // gW[o][i] = sum_im dl[im][o] * p2[im][i] in image order (o = 4 * (ob + t4) + c)
+  // NO4 (compile time): the class granules of the thread's half.  Images in batches of IB with every
+  // LDS read of a batch issued before the FMAs (one LDS latency per batch, not per read)
+  auto fc_column_n = [&](auto no4c, int i, const float* pv) {
+    constexpr int NO4 = decltype(no4c)::value;
+    float gw[4 * NO4];
+#pragma unroll
+    for (int t = 0; t < 4 * NO4; ++t) gw[t] = 0.f;
+    constexpr int IB = 8 / NO4;  // images per batch: 32 registers of dl granules in flight
+    int im = 0;
+    for (; im + IB <= g.B; im += IB) {
+      float x[IB];
+      float4 d[IB][NO4];
+#pragma unroll
+      for (int u = 0; u < IB; ++u) {
+        const float* row = sm + (im + u) * R4;
+        x[u] = row[NC + i];
+#pragma unroll
+        for (int t4 = 0; t4 < NO4; ++t4) d[u][t4] = reinterpret_cast<const float4*>(row)[ob + t4];
+      }
+#pragma unroll
+      for (int u = 0; u < IB; ++u)
+#pragma unroll
+        for (int t4 = 0; t4 < NO4; ++t4) {
+          gw[4 * t4] += d[u][t4].x * x[u];
+          gw[4 * t4 + 1] += d[u][t4].y * x[u];
+          gw[4 * t4 + 2] += d[u][t4].z * x[u];
+          gw[4 * t4 + 3] += d[u][t4].w * x[u];
+        }
+    }
+    for (; im < g.B; ++im) {
+      const float* row = sm + im * R4;
+      const float x = row[NC + i];
+#pragma unroll
+      for (int t4 = 0; t4 < NO4; ++t4) {
+        const float4 d = reinterpret_cast<const float4*>(row)[ob + t4];
+        gw[4 * t4] += d.x * x;
+        gw[4 * t4 + 1] += d.y * x;
+        gw[4 * t4 + 2] += d.z * x;
+        gw[4 * t4 + 3] += d.w * x;
+      }
+    }
+    float np[4 * NO4];
+#pragma unroll
+    for (int t = 0; t < 4 * NO4; ++t) {
+      np[t] = pv[t] - lr * gw[t];
+      CNN_PIN(np[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < 4 * NO4; ++t) {
+      const int o = 4 * ob + t;
+      if (o >= NC) continue;
+      fw[o * F + i] = np[t];
+      if (g.shadow[8]) g.shadow[8][o * F + i] = f2bf(np[t]);
+    }
+  };
+  auto fc_column = [&](int i, const float* pv) {
+    if (no4 == 2) fc_column_n(std::integral_constant<int, 2>{}, i, pv);
+    else fc_column_n(std::integral_constant<int, 4>{}, i, pv);
+  };
+  if (H * F <= nt) {  // one column per thread: no loop (a loop's loads make every store wait)
+    if (fc_on) fc_column(i0, pfc);
+  } else {
+    for (int i = i0; i < F; i += nt) {
+      float pv[16];
+      fc_load(i, pv);
+      fc_column(i, pv);
+    }
+  }
+  STAMP(23);
+  if ((int)threadIdx.x < NC) {
+    const int o = threadIdx.x;
+    float gb = 0.f;
+#pragma unroll 8
+    for (int im = 0; im < g.B; ++im) gb += sm[im * R4 + o];
+    const float np = pb - lr * gb;
+    fb[o] = np;
+    if (g.shadow[9]) g.shadow[9][o] = f2bf(np);
+  }
+  STAMP(29);
   if (threadIdx.x < 64) {
-    float ls = 0.f;
-    for (int i = threadIdx.x; i < g.B; i += 64) ls += smi_cc_load(g.row_loss + i);
-    ls = wave_sum(ls);
+    const float ls = wave_sum(rl);
     if (threadIdx.x == 0) {
       if (g.loss) g.loss[0] = ls * g.loss_scale;
       if (g.step) g.step[0] += 1.f;
@@ -565,19 +735,25 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   float* wacc = lg + 16;                 // max(C, CI)*C*9 + C wgrad accumulators
   const int WC = C > CI ? C : CI;
   float* wscr = wacc + WC * C * 9 + C;   // conv_wgrad per-unit 16x16 partial tiles (WG_SCRATCH floats)
-  // the four conv layers' weights and biases, staged once: every conv table build / fp32 conv
-  // read them from global memory per layer (a dependent L2 round trip inside each phase)
+  // the four conv layers' weights and biases, staged once for the bf16 (MFMA) convs, whose per-
+  // layer fragment tables read them element-wise (the fp32 convs keep global weights: they read
+  // them through the constant address space as scalar loads)
   float* wst = wscr + WG_SCRATCH + 2;
-  const float* lw[4];
-  const float* lb[4];
+  const float* lw[4] = {};
+  const float* lb[4] = {};
   {
     int o = 0;
     for (int l = 0; l < 4; ++l) {
       const int n = C * (l == 0 ? CI : C) * 9;
-      for (int i = threadIdx.x; i < n; i += blockDim.x) wst[o + i] = g.w[l][i];
-      for (int i = threadIdx.x; i < C; i += blockDim.x) wst[o + n + i] = g.b[l][i];
-      lw[l] = wst + o;
-      lb[l] = wst + o + n;
+      if (BF && g.wstage) {
+        for (int i = threadIdx.x; i < n; i += blockDim.x) wst[o + i] = g.w[l][i];
+        for (int i = threadIdx.x; i < C; i += blockDim.x) wst[o + n + i] = g.b[l][i];
+        lw[l] = wst + o;
+        lb[l] = wst + o + n;
+      } else {
+        lw[l] = g.w[l];
+        lb[l] = g.b[l];
+      }
       o += n + C;
     }
   }
@@ -596,22 +772,22 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   __syncthreads();
   STAMP(1);
   if (BF) conv_mfma<28, P28, false, false>(xin, CI, a1, C, lw[0], lb[0], wscr);
-  else conv_fwd<28, P28, CC, EX>(xin, CI, a1, C, lw[0], lb[0]);
+  else conv_fwd<28, P28, CC, EX>(xin, CI, a1, C, g.w[0], g.b[0]);
   __syncthreads();
   STAMP(2);
   if (BF) conv_mfma<28, P28, false, false>(a1, C, a2, C, lw[1], lb[1], wscr);
-  else conv_fwd<28, P28, CC, EX>(a1, C, a2, C, lw[1], lb[1]);
+  else conv_fwd<28, P28, CC, EX>(a1, C, a2, C, g.w[1], g.b[1]);
   __syncthreads();
   STAMP(3);
   pool_fwd<28, P28, P14, 1>(a2, p1, C);
   __syncthreads();
   STAMP(4);
   if (BF) conv_mfma<14, P14, false, false>(p1, C, a3, C, lw[2], lb[2], wscr);
-  else conv_fwd<14, P14, CC, EX>(p1, C, a3, C, lw[2], lb[2]);
+  else conv_fwd<14, P14, CC, EX>(p1, C, a3, C, g.w[2], g.b[2]);
   __syncthreads();
   STAMP(5);
   if (BF) conv_mfma<14, P14, false, false>(a3, C, a4, C, lw[3], lb[3], wscr);
-  else conv_fwd<14, P14, CC, EX>(a3, C, a4, C, lw[3], lb[3]);
+  else conv_fwd<14, P14, CC, EX>(a3, C, a4, C, g.w[3], g.b[3]);
   __syncthreads();
   STAMP(6);
   pool_fwd<14, P14, 7, 0>(a4, p2, C);
@@ -668,9 +844,11 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   __syncthreads();
   STAMP(9);
   float* gs = g.slab + (long)img * g.P;  // this image's gradient slab
-  // fc grads: gW[o][i] = dl[o] * p2[i]; gb[o] = dl[o]; dp2[i] = sum_o W[o][i] dl[o] (into p2 buffer after)
-  for (int e = threadIdx.x; e < NC * F; e += blockDim.x) smi_wt_store(gs + g.off[8] + e, lg[e / F] * p2[e % F]);
-  for (int o = threadIdx.x; o < NC; o += blockDim.x) smi_wt_store(gs + g.off[9] + o, lg[o]);
+  // fc grads: the slab keeps this image's dl (NC) and p2 (F) in place of the NC x F outer product
+  // gW[o][i] = dl[o] * p2[i] (gb[o] = dl[o]): the reducers form the batch sum of products (a
+  // third of the bytes to reduce); dp2[i] = sum_o W[o][i] dl[o] goes into the p2 buffer after
+  for (int i = threadIdx.x; i < F; i += blockDim.x) smi_wt_store(gs + cnn_cs(g) + NC + i, p2[i]);
+  for (int o = threadIdx.x; o < NC; o += blockDim.x) smi_wt_store(gs + cnn_cs(g) + o, lg[o]);
   __syncthreads();
   STAMP(10);
   for (int i = threadIdx.x; i < F; i += blockDim.x) {
@@ -694,7 +872,7 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
     wacc[e] = 0.f;
   }
   if (BF) conv_mfma<14, P14, true, true>(a4, C, a3, C, lw[3], nullptr, wscr);
-  else conv_dgrad<14, P14, CC, EX>(a4, C, lw[3], C, a3, true);
+  else conv_dgrad<14, P14, CC, EX>(a4, C, g.w[3], C, a3, true);
   __syncthreads();
   STAMP(14);
   // conv3: dW3 (dz3, p1); dp1 = convT(dz3) into p1 (no relu: p1 is a pool output)
@@ -707,7 +885,7 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
     wacc[e] = 0.f;
   }
   if (BF) conv_mfma<14, P14, true, false>(a3, C, p1, C, lw[2], nullptr, wscr);
-  else conv_dgrad<14, P14, CC, EX>(a3, C, lw[2], C, p1, false);
+  else conv_dgrad<14, P14, CC, EX>(a3, C, g.w[2], C, p1, false);
   __syncthreads();
   STAMP(16);
   // pool1 backward + relu'(a2): dz2 in a2
@@ -724,7 +902,7 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
     wacc[e] = 0.f;
   }
   if (BF) conv_mfma<28, P28, true, true>(a2, C, a1, C, lw[1], nullptr, wscr);
-  else conv_dgrad<28, P28, CC, EX>(a2, C, lw[1], C, a1, true);
+  else conv_dgrad<28, P28, CC, EX>(a2, C, g.w[1], C, a1, true);
   __syncthreads();
   STAMP(19);
   // conv1: dW1 (dz1, x)
@@ -734,7 +912,7 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   STAMP(20);
   for (int e = threadIdx.x; e < C * CI * 9 + C; e += blockDim.x)
     smi_wt_store(gs + (e < C * CI * 9 ? g.off[0] + e : g.off[1] + e - C * CI * 9), wacc[e]);
-  if (g.fused) cnn_fused_tail(g, img);
+  if (g.fused) cnn_fused_tail(g, img, sm);
 }
 
 // grad[p] (+)= dloss * sum_img slab[img][p], scattered to the 10 parameter tensors; also the mean
@@ -743,15 +921,26 @@ __global__ void cnn_reduce_kernel(CNNArgs g) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   const float dl = g.dloss ? g.dloss[0] : 1.f;
   if (p < g.P) {
+    // the compact slab (cnn_cs): an fc weight gradient entry is the batch sum of dl[o] * p2[i]
+    const int off8 = g.off[8], F = g.C * 49, cs = cnn_cs(g);
+    int a = p, b = -1;  // slab entries: the value, or the product of two
+    if (p >= g.off[9]) a = cs + (p - g.off[9]);
+    else if (p >= off8) { const int o = (p - off8) / F; a = cs + o; b = cs + g.classes + (p - off8 - o * F); }
     // 8 independent partial sums: all 8 loads of a round are in flight together (a plain
     // serial loop waited one memory round trip per image: 10 us for 32 images), fixed order
     float q[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     int i = 0;
     for (; i + 8 <= g.B; i += 8) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) q[j] += g.slab[(long)(i + j) * g.P + p];
+      for (int j = 0; j < 8; ++j) {
+        const float* r = g.slab + (long)(i + j) * g.P;
+        q[j] += b < 0 ? r[a] : r[a] * r[b];
+      }
     }
-    for (int j = 0; i < g.B; ++i, ++j) q[j] += g.slab[(long)i * g.P + p];
+    for (int j = 0; i < g.B; ++i, ++j) {
+      const float* r = g.slab + (long)i * g.P;
+      q[j] += b < 0 ? r[a] : r[a] * r[b];
+    }
     const float s = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
     int seg = 0;
     while (seg < 9 && p >= g.off[seg + 1]) ++seg;
@@ -764,17 +953,21 @@ static size_t cnn_lds_bytes(const CNNArgs& g) {
   const int C = g.C, CI = g.cin;
   // + conv_wgrad scratch (WG_SCRATCH floats)
   const int WC = C > CI ? C : CI;  // wgrad accumulators hold [C][max(C, CI)*9] + C
-  // + the staged conv weights and biases (C * CI * 9 + 3 * C * C * 9 + 4 * C)
+  // + the staged conv weights and biases (C * CI * 9 + 3 * C * C * 9 + 4 * C) when wstage
   return sizeof(float) * (size_t)(CI * PL28 + 2 * C * PL28 + 3 * C * PL14 + C * 49 + 16 + WC * C * 9 + C + 4 +
-                                  WG_SCRATCH + 2 + C * CI * 9 + 3 * C * C * 9 + 4 * C);
+                                  WG_SCRATCH + 2 + (g.wstage ? C * CI * 9 + 3 * C * C * 9 + 4 * C : 0));
 }
 
 extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
   CNNArgs g = *args;
   if (g.fused && (g.P % 4 || !g.part || !g.tick || !g.lr || !g.slab || !g.row_loss || !g.train)) return -1;
   if (g.C < 1 || g.C > CNN_MAXC || g.cin < 1 || g.cin > 4 || g.classes < 1 || g.classes > 16) return -1;
+  g.wstage = g.bf16 ? 1 : 0;
+  if (g.wstage && cnn_lds_bytes(g) > 160 * 1024) g.wstage = 0;  // the weights then stay global
   const size_t lds = cnn_lds_bytes(g);
   if (lds > 160 * 1024) return -1;
+  // the fused tail stages every image's dl and p2 in the (then free) LDS planes
+  if (g.fused && (size_t)g.B * ((g.classes + g.C * 49 + 3) & ~3) * sizeof(float) > lds) return -1;
   // channel capacity 10 (the reference model's hidden_units) gets exact compile-time groups
   // (LDS residency caps C at 13 for 1-channel input, so no exact instance above 10)
   auto kern = g.bf16 ? (g.C == 10 ? cnn_kernel<10, true, true> : cnn_kernel<CNN_MAXC, false, true>)
@@ -784,9 +977,12 @@ extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
   SMI_CHECK_LAUNCH();
 }
 
-extern "C" int smi_cnn_fused_ok(int C, int cin, int classes) {
+extern "C" int smi_cnn_fused_ok(int C, int cin, int classes, int B) {
+  // the fused tail stages every image's dl and p2 in the kernel's LDS (see smi_cnn)
+  CNNArgs g{};
+  g.C = C; g.cin = cin; g.classes = classes;
   const int P = C * cin * 9 + C + 3 * (C * C * 9 + C) + classes * C * 49 + classes;
-  return P % 4 == 0;
+  return P % 4 == 0 && (size_t)B * ((classes + C * 49 + 3) & ~3) * sizeof(float) <= cnn_lds_bytes(g);
 }
 
 extern "C" int smi_cnn_reduce(const CNNArgs* args, hipStream_t st) {

@@ -43,8 +43,8 @@ class FashionMNISTModel(nn.Module):
     def fused_sgd_step(self, opt, x, y):
         """The whole single-executor training step (forward, CE, backward, batch gradient sum,
         SGD update) as ONE HIP launch (csrc/kernels/cnn.hip, fused tail); returns the loss.  None
-        when it does not apply (CPU, data parallelism, an optimizer other than plain SGD, an odd
-        parameter count): the caller runs the usual forward / backward / step."""
+        when it does not apply (CPU, data parallelism, an optimizer other than plain SGD, a batch
+        whose fc activations do not fit the kernel's LDS): the caller runs the usual forward / backward / step."""
         from .. import _native
         from ..optim.sgd import SGD
         flat = getattr(opt, "flat", None)
@@ -52,7 +52,8 @@ class FashionMNISTModel(nn.Module):
         if (not x.is_cuda or not _native.use_native(x) or not isinstance(opt, SGD) or opt.momentum
                 or opt.weight_decay or opt.grad_scale != 1.0 or getattr(opt, "ranges", None) is not None
                 or flat is None or getattr(flat, "planes", None) is not None or x.dim() != 4
-                or not _native.C().cnn_fused_ok(params[0].shape[0], params[0].shape[1], params[8].shape[0])):
+                or not _native.C().cnn_fused_ok(params[0].shape[0], params[0].shape[1], params[8].shape[0],
+                                                 x.shape[0])):
             return None
         shadows = None
         if flat.shadow is not None:

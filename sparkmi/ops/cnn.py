@@ -2,9 +2,10 @@
 
 ``cnn_loss(x, y, params)`` = mean cross-entropy of the reference CNN (distributed_cnn.py:47-86)
 over the batch.  GPU: ONE kernel launch runs forward AND backward for every image (one
-workgroup per image, activations in LDS) and leaves per-image gradients in a slab; the
-autograd backward is one reduce launch that sums the slab over images, scales by dloss and
-accumulates into the parameters' (flat) fp32 gradients.  CPU: the identical math with torch
+workgroup per image, activations in LDS) and leaves per-image gradients in a slab (the conv
+layers' gradients, then the image's logit gradient dl and pooled activations p2: the fc
+gradient is their outer product, formed by the reducer); the autograd backward is one reduce
+launch that sums the slab over images, scales by dloss and accumulates into the parameters' (flat) fp32 gradients.  CPU: the identical math with torch
 (conv2d / max_pool2d / linear), so the kernel is testable against it.
 """
 import torch

@@ -10,7 +10,13 @@ int main(int argc, char** argv) {
   CNNArgs g{};
   g.B = B; g.cin = CI; g.C = C; g.classes = NC; g.x_u8 = 1; g.x_scale = 1.f / 255.f; g.train = 1; g.loss_scale = 1.f / B; g.bf16 = argc > 1;
   unsigned char* x; long long* y; float *w[5], *b[5], *slab, *rl, *loss; int* pred;
-  (void)hipMalloc(&x, B * 784); (void)hipMemset(x, 7, B * 784);
+  (void)hipMalloc(&x, B * 784);
+  {  // random pixels and weights (zeros run at a higher clock and leave every ReLU off)
+    std::vector<unsigned char> hx(B * 784);
+    unsigned r = 12345u;
+    for (auto& v : hx) { r = r * 1664525u + 1013904223u; v = (unsigned char)(r >> 24); }
+    (void)hipMemcpy(x, hx.data(), hx.size(), hipMemcpyHostToDevice);
+  }
   (void)hipMalloc(&y, B * 8); (void)hipMemset(y, 0, B * 8);
   const int sz[5] = {C * CI * 9, C * C * 9, C * C * 9, C * C * 9, NC * C * 49};
   int off = 0;
@@ -18,12 +24,27 @@ int main(int argc, char** argv) {
   for (int i = 0; i < 10; ++i) { g.off[i] = off; off += bs[i]; }
   g.P = off;
   for (int i = 0; i < 5; ++i) {
-    (void)hipMalloc(&w[i], sz[i] * 4); (void)hipMemset(w[i], 0, sz[i] * 4);
+    (void)hipMalloc(&w[i], sz[i] * 4);
+    {
+      std::vector<float> hw(sz[i]);
+      unsigned r = 777u + i;
+      for (auto& v : hw) { r = r * 1664525u + 1013904223u; v = ((float)(r >> 8) / 16777216.f - 0.5f) * 0.3f; }
+      (void)hipMemcpy(w[i], hw.data(), hw.size() * 4, hipMemcpyHostToDevice);
+    }
     (void)hipMalloc(&b[i], 64); (void)hipMemset(b[i], 0, 64);
     g.w[i] = w[i]; g.b[i] = b[i];
   }
   (void)hipMalloc(&slab, (size_t)B * g.P * 4); (void)hipMalloc(&rl, B * 4); (void)hipMalloc(&loss, 4); (void)hipMalloc(&pred, B * 4);
   g.x = x; g.y = y; g.slab = slab; g.row_loss = rl; g.loss = loss; g.pred = pred;
+  if (argc > 2) {  // the fused single-executor SGD step (ticketed slab reduction + SGD in the tail)
+    float *part, *lr, *step; unsigned* tick;
+    (void)hipMalloc(&part, (size_t)((B + CNN_GRP - 1) / CNN_GRP) * g.P * 4);
+    (void)hipMalloc(&tick, (CNN_GRP + 1) * 4); (void)hipMemset(tick, 0, (CNN_GRP + 1) * 4);
+    (void)hipMalloc(&lr, 4); (void)hipMemset(lr, 0, 4);
+    (void)hipMalloc(&step, 4); (void)hipMemset(step, 0, 4);
+    g.fused = 1; g.part = part; g.tick = tick; g.lr = lr; g.step = step;
+  }
+  printf("mode: %s%s\n", g.bf16 ? "bf16" : "fp32", g.fused ? " fused" : "");
   for (int it = 0; it < 20; ++it) smi_cnn(&g, 0);
   (void)hipDeviceSynchronize();
   std::vector<unsigned long long> st(64 * 32);
@@ -50,6 +71,12 @@ int main(int argc, char** argv) {
     }
     printf("%s: wave0 units %8.0f, all units %8.0f, combine+write %8.0f ticks\n", nm[k], u0 / B, ua / B, cb / B);
   }
+  // fused tail stamps (slots 26-29: group sum start / done, final start / SGD done), relative to
+  // the same workgroup's body end (slot 20; s_memtime is per-XCD, so only same-WG differences)
+  for (int im = 0; im < B; ++im)
+    for (int k = (g.bf16 ? 21 : 26); k < 31; ++k)
+      if (st[im * 32 + k]) printf("img %2d slot %d: %+8lld ticks after its body end\n", im, k,
+                                  (long long)(st[im * 32 + k] - st[im * 32 + 20]));
   double tot = 0;
   for (int im = 0; im < B; ++im) tot += (double)(st[im * 32 + nph - 1] - st[im * 32]);
   printf("total %8.0f ticks\n", tot / B);
