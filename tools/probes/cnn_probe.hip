@@ -60,7 +60,19 @@ int main(int argc, char** argv) {
   // conv_wgrad sub-stamps (slot sb: wave 0's units done, sb+1: all units done; phase end = combine done)
   const int sub[3][3] = {{21, 17, 18}, {23, 19, 20}, {25, 12, 13}};
   const char* nm[3] = {"conv2 wgrad", "conv1 wgrad", "conv4 wgrad"};
-  for (int k = 0; k < 3; ++k) {
+  if (g.bf16) {  // bf16 build: slot 24 / 25 = conv2 forward / dgrad tables ready (conv_mfma sb)
+    const int tb[2][3] = {{24, 2, 3}, {25, 18, 19}};
+    const char* tn[2] = {"conv2 fwd", "conv2 dgrad"};
+    for (int k = 0; k < 2; ++k) {
+      double a = 0, b = 0;
+      for (int im = 0; im < B; ++im) {
+        a += (double)(st[im * 32 + tb[k][0]] - st[im * 32 + tb[k][1]]);
+        b += (double)(st[im * 32 + tb[k][2]] - st[im * 32 + tb[k][0]]);
+      }
+      printf("%s: tables %8.0f, tiles + barrier %8.0f ticks\n", tn[k], a / B, b / B);
+    }
+  }
+  for (int k = 0; k < 3 && !g.bf16; ++k) {
     const int sb = sub[k][0], p0 = sub[k][1], p1 = sub[k][2];
     if (!st[sb]) continue;
     double u0 = 0, ua = 0, cb = 0;
