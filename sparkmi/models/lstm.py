@@ -35,6 +35,11 @@ class LSTM(nn.Module):
         with _rng.salt_scope(salt_base):  # the model's own salt stream: masks independent of other models
             self.salt = _rng.new_salt()
 
+    def sparse_rows(self):
+        """{embedding weight: the last batch's token ids}: its gradient touches only those rows
+        (DataParallel(sparse_rows=...), the optional row-sparse exchange of SURVEY §5.8)."""
+        return {self.embedding.weight: lambda: self.last_ids}
+
     def param_list(self):
         ps = [self.embedding.weight]
         for i in range(self.num_layers):
@@ -48,12 +53,14 @@ class LSTM(nn.Module):
         return z, z.clone()
 
     def forward(self, input_seq, hidden_in=None, mem_in=None):
+        self.last_ids = input_seq
         return lstm_classifier(input_seq, hidden_in, mem_in, self.param_list(), self.num_layers,
                                dropout=self.dropout_p, training=self.training, rng=self.rng, salt=self.salt,
                                padding_idx=self.padding_idx)
 
     def loss(self, input_seq, labels, hidden_in=None, mem_in=None):
         """CE on the last step's prediction (distributed_lstm.py:186-189); returns (loss, pred)."""
+        self.last_ids = input_seq
         if input_seq.is_cuda and labels.dim() == 1:
             # GPU: the CE of the last step is fused into the LSTM forward kernel's tail (row loss,
             # head gradient, fixed-order mean through a ticket): no separate CE launches

@@ -31,6 +31,14 @@ module was called, so gradients were never synchronised).  Design for MI355X + R
   faster; ``SPARKMI_DP_PROBE=0`` sends them to RCCL without measuring.  Either way a bucket's
   reduction runs on a side stream (RCCL's own, or the IPC comm stream forked from the compute
   stream at launch and joined in ``finish()``), overlapped with the rest of the backward.
+* ``sparse_rows={param: ids_fn}`` (opt-in; SURVEY §5.8 item 5, the LSTM embedding of
+  /root/reference/distributed_lstm.py:115): a table whose gradient touches only the step's rows
+  is exchanged ROW-SPARSE instead of all-reduced dense — each rank de-duplicates its row ids
+  (``ids_fn()``, a device sort), all-gathers (ids, rows) padded to the largest rank's count and adds the
+  ranks' rows into the dense gradient in rank order (deterministic; untouched rows stay zero, so
+  any optimizer, Adam included, sees exactly the all-reduced gradient).  The LSTM's 12.3 MB table
+  moves B*T*(8 + 4*D) bytes per rank instead (4,128 rows: 0.56 MB).  Uses the process group, so a
+  DP step with sparse rows is not a single-graph (``graph_safe``) step.
 The CPU/gloo path runs the identical logic (multi-process CPU tests).
 """
 import os
@@ -67,8 +75,13 @@ def _single_node(world):
 
 
 class DataParallel:
-    def __init__(self, flat, group=None, bucket_mb=64.0, overlap=True, broadcast=True, zero=False, ipc=None):
+    def __init__(self, flat, group=None, bucket_mb=64.0, overlap=True, broadcast=True, zero=False, ipc=None,
+                 sparse_rows=None):
         self.flat = flat
+        # parameter index -> callable returning the step's touched row ids (row-sparse exchange)
+        self._sparse = {flat.index[id(p)]: fn for p, fn in (sparse_rows or {}).items()}
+        if self._sparse and zero:
+            raise ValueError("sparse_rows and zero=True do not combine (a sparse table has no owned piece)")
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -165,6 +178,8 @@ class DataParallel:
         flat = self.flat
         self.buckets = []  # (start, end, param indices)
         cut_set = set(cuts)
+        for i in getattr(self, "_sparse", ()):  # a row-sparse table is a bucket of its own
+            cut_set.update((i, i + 1))
         cur, start = [], 0
         for i, p in enumerate(flat.params):
             s = flat.offsets[i]
@@ -233,7 +248,7 @@ class DataParallel:
     def graph_safe(self):
         """True when the gradient reduction is a plain kernel (IPC path): the whole DP step can
         be captured into one HIP graph."""
-        return self.ipc is not None
+        return self.ipc is not None and not self._sparse
 
     def piece(self, b):
         """[start, end) of this rank's piece of bucket ``b`` (ZeRO-1 ownership)."""
@@ -247,10 +262,13 @@ class DataParallel:
     def _launch(self, b):
         if self._launched[b]:
             return
-        s, e, _ = self.buckets[b]
+        s, e, idx = self.buckets[b]
         self._launched[b] = True
         if self.flat.grad.is_cuda:
             _grad.join(self.flat.grad.device.index)  # weight grads may still be in flight on the side stream
+        if len(idx) == 1 and idx[0] in self._sparse:
+            self._sparse_exchange(s, e, idx[0])
+            return
         g = self.flat.grad[s:e]
         self.bytes_reduced += g.numel() * g.element_size()
         if self.ipc is not None:
@@ -264,6 +282,37 @@ class DataParallel:
         else:
             w = dist.all_reduce(g, group=self.group, async_op=True)
         self._works.append(w)
+
+    def _sparse_exchange(self, s, e, i):
+        """Row-sparse reduction of parameter ``i``'s gradient (flat slice [s, e), rows of the
+        parameter's first dimension): unique local row ids (sorted; duplicates -> the dummy row V),
+        all-gather of the fixed-size (ids, rows) pairs, rank-order scatter-add into the dense
+        gradient (id lists padded to the largest rank's with the dummy row)."""
+        p = self.flat.params[i]
+        nrow = p.shape[0]
+        d = p.numel() // nrow
+        g = self.flat.grad[s:s + p.numel()].view(nrow, d)  # (the slice may end in alignment padding)
+        ids = self._sparse[i]().reshape(-1).to(device=g.device, dtype=torch.int64)
+        srt = torch.sort(ids).values
+        first = torch.ones_like(srt, dtype=torch.bool)
+        first[1:] = srt[1:] != srt[:-1]
+        uid = torch.where(first, srt, torch.full_like(srt, nrow))
+        # ranks may hold different numbers of ids (per-batch padded lengths): pad to the largest
+        kt = torch.tensor([uid.numel()], dtype=torch.int64, device=g.device)
+        dist.all_reduce(kt, op=dist.ReduceOp.MAX, group=self.group)
+        k = int(kt.item())
+        if k > uid.numel():
+            uid = torch.cat([uid, uid.new_full((k - uid.numel(),), nrow)])
+        rows = torch.cat([g, g.new_zeros(1, d)])[uid]
+        all_ids = uid.new_empty(self.world * k)
+        all_rows = rows.new_empty(self.world * k, d)
+        dist.all_gather_into_tensor(all_ids, uid, group=self.group)
+        dist.all_gather_into_tensor(all_rows, rows, group=self.group)
+        dense = g.new_zeros(nrow + 1, d)
+        for r in range(self.world):  # rank order: ids are unique within a rank (but the dummy row)
+            dense.index_put_((all_ids[r * k:(r + 1) * k],), all_rows[r * k:(r + 1) * k], accumulate=True)
+        g.copy_(dense[:nrow])
+        self.bytes_reduced += k * (8 + 4 * d)  # bytes this rank contributed
 
     def reshard_optimizer(self, opt, old_ranges):
         """Carry a sharded optimizer's moments over a bucket re-cut (the split-graph capture aligns

@@ -46,7 +46,10 @@ class Trainer:
         self.rank, self.world = rank, world
         self.flat = FlatParams(self.model, device=self.device, shadow=shadow)
         self.opt = make_optimizer(self.flat)
-        self.ddp = DataParallel(self.flat, bucket_mb=cfg.bucket_mb, zero=getattr(cfg, "zero", False)) if world > 1 else None
+        sparse = (self.model.sparse_rows() if getattr(cfg, "sparse_embedding", False)
+                  and hasattr(self.model, "sparse_rows") else None)
+        self.ddp = DataParallel(self.flat, bucket_mb=cfg.bucket_mb, zero=getattr(cfg, "zero", False),
+                                sparse_rows=sparse) if world > 1 else None
         use_graph = bool(cfg.graph) and self.device.type == "cuda"
         # split_fn (data-parallel): the backward as several graphs, finished gradient buckets
         # reduced while the rest of the backward runs (StepRunner)

@@ -59,6 +59,14 @@ def test_lstm_recipe_small():
     assert r["steps"] == 3 and r["padding_idx"] >= 4
 
 
+def test_lstm_recipe_data_parallel_sparse_embedding_gloo():
+    """distributed_lstm on 2 executors with the row-sparse embedding-gradient exchange."""
+    from sparkmi.recipes import lstm
+    r = lstm.main(CPU + ["--world", "2", "--n-train", "256", "--n-test", "64", "--max-steps", "3",
+                         "--sparse-embedding"])
+    assert r["world"] == 2 and r["steps"] == 3
+
+
 def test_translator_recipe_small():
     from sparkmi.recipes import translator
     r = translator.main(CPU + ["--n-train", "128", "--max-steps", "2", "--d-model", "64", "--ffn-hidden", "128",
