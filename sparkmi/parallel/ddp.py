@@ -304,10 +304,15 @@ class DataParallel:
         if k > uid.numel():
             uid = torch.cat([uid, uid.new_full((k - uid.numel(),), nrow)])
         rows = torch.cat([g, g.new_zeros(1, d)])[uid]
-        all_ids = uid.new_empty(self.world * k)
-        all_rows = rows.new_empty(self.world * k, d)
-        dist.all_gather_into_tensor(all_ids, uid, group=self.group)
-        dist.all_gather_into_tensor(all_rows, rows, group=self.group)
+        # (gloo moves host tensors: device rows of a gloo group are staged through host memory)
+        host = g.is_cuda and dist.get_backend(self.group) == "gloo"
+        su, sr = (uid.cpu(), rows.cpu()) if host else (uid, rows)
+        all_ids = su.new_empty(self.world * k)
+        all_rows = sr.new_empty(self.world * k, d)
+        dist.all_gather_into_tensor(all_ids, su, group=self.group)
+        dist.all_gather_into_tensor(all_rows, sr, group=self.group)
+        if host:
+            all_ids, all_rows = all_ids.to(g.device), all_rows.to(g.device)
         dense = g.new_zeros(nrow + 1, d)
         for r in range(self.world):  # rank order: ids are unique within a rank (but the dummy row)
             dense.index_put_((all_ids[r * k:(r + 1) * k],), all_rows[r * k:(r + 1) * k], accumulate=True)

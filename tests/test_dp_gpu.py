@@ -192,7 +192,7 @@ def test_transformer_dp_parity_grid_world4():
 
 
 # ---- small models over the IPC kernels: the whole-step graph and the two-shot path ----
-def _small_dp(kind, steps, graph):
+def _small_dp(kind, steps, graph, sparse=False):
     import torch
     from sparkmi.models.lstm import LSTM
     from sparkmi.models.mlp import MultilayerPerceptron
@@ -217,9 +217,9 @@ def _small_dp(kind, steps, graph):
         loss_fn = lambda mm, x, y: mm.loss(x, y)[0]  # noqa: E731
     flat = FlatParams(m, shadow=False)
     opt = SGD(flat, lr=0.1)
-    ddp = DataParallel(flat, bucket_mb=64.0) if world > 1 else None
+    ddp = DataParallel(flat, bucket_mb=64.0, sparse_rows=m.sparse_rows() if sparse else None) if world > 1 else None
     info = None
-    if ddp is not None:
+    if ddp is not None and not sparse:
         assert ddp.ipc is not None, "small gradients take the IPC kernels in auto mode"
         n = max(e - s for s, e, _ in ddp.buckets)
         info = ddp.ipc.algo_for(n)
@@ -259,3 +259,17 @@ def test_lstm_dp_auto_two_shot_matches_single_process():
                    timeout=380)
     assert algo == 2
     torch.testing.assert_close(p4, p1, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_lstm_dp_sparse_embedding_matches_single_process():
+    """The row-sparse embedding-gradient exchange on device tensors (sort / dedup / rank-order
+    scatter-add on the GPU; the dense rest over IPC): 2 ranks x batch 4 == one process x batch 8,
+    forward + backward graph-captured."""
+    env = {"SPARKMI_DIST_BACKEND": "gloo"}
+    p2, _ = launch(_small_dp, ("lstm", 5, True, True), {}, num_processes=2, use_gpu=True, env=env, log_sink=None,
+                   timeout=280)
+    p1, _ = launch(_small_dp, ("lstm", 5, False), {}, num_processes=1, use_gpu=True, env=env, log_sink=None,
+                   timeout=280)
+    torch.testing.assert_close(p2, p1, rtol=1e-4, atol=1e-5)

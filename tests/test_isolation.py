@@ -16,9 +16,9 @@ from sparkmi.optim import Adam
 from sparkmi.utils.flat import FlatParams
 
 
-def _transformer(device, seed, d=64, salt_base=1):
-    torch.manual_seed(seed)
-    m = Transformer(d_model=d, ffn_hidden=2 * d, num_heads=2, num_layers=1, max_sequence_length=16,
+def _transformer(device, seed, d=128, salt_base=1):
+    torch.manual_seed(seed)  # head_dim 64 (the GPU attention kernels' head size)
+    m = Transformer(d_model=d, ffn_hidden=2 * d, num_heads=d // 64, num_layers=1, max_sequence_length=16,
                     src_vocab_size=48, tgt_vocab_size=48, seed=seed, dtype="fp32", salt_base=salt_base)
     return m.to(device).train()
 
@@ -49,7 +49,7 @@ def test_two_models_one_process_do_not_perturb_each_other(device):
     # A again, interleaved with a second transformer (other salts, other width) and an LSTM
     a2 = _transformer(device, seed=5)
     a2_step = _trainer(a2, tr_step)
-    b = _trainer(_transformer(device, seed=9, d=32, salt_base=101), tr_step)
+    b = _trainer(_transformer(device, seed=9, d=64, salt_base=101), tr_step)
     ids = torch.randint(1, 200, (4, 12), generator=torch.Generator().manual_seed(1)).to(device)
     lbl = torch.randint(0, 4, (4,), generator=torch.Generator().manual_seed(2)).to(device)
     lstm = LSTM(200, 32, 32, 4, num_layers=2, seed=3, salt_base=7).to(device).train()
