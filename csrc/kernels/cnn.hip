@@ -37,8 +37,20 @@ __device__ unsigned long long cnn_stamps[64 * 32];
 #endif
 #define P28 30   // 28x28 plane with 1-pixel zero halo
 #define P14 16   // 14x14 plane with 1-pixel zero halo
-#define PL28 (P28 * P28)
-#define PL14 (P14 * P14)
+// channel-plane stride: the halo plane plus CNN_PAD floats, so the same position of consecutive
+// channels lands in different LDS banks (a 16 x 16 plane is 256 floats: every channel started at
+// bank 0, and the weight-gradient / MFMA operand reads of 16 channels conflicted).  Swept with
+// tools/probes/cnn_probe.hip (-DCNN_PAD14 / -DCNN_PAD28): 0/0 94.8k clocks per image body, 4/8
+// 85.9k (14 x 14 weight gradients 6.4k -> 4.1k), a plateau beyond.
+#ifndef CNN_PAD14
+#define CNN_PAD14 4
+#endif
+#ifndef CNN_PAD28
+#define CNN_PAD28 8
+#endif
+#define CPL(pp) ((pp) * (pp) + ((pp) == P14 ? CNN_PAD14 : CNN_PAD28))
+#define PL28 CPL(P28)
+#define PL14 CPL(P14)
 
 __device__ __forceinline__ int i28(int c, int y, int x) { return c * PL28 + (y + 1) * P28 + (x + 1); }
 __device__ __forceinline__ int i14(int c, int y, int x) { return c * PL14 + (y + 1) * P14 + (x + 1); }
@@ -118,7 +130,7 @@ __device__ __forceinline__ void conv_fwd(const float* __restrict__ in, int cin, 
 #pragma unroll 1  // a full unroll (cin is compile-time with EX) hoists every weight into SGPRs and spills
     for (int ci = 0; ci < cin; ++ci) {
       f2 A[3], M[3], B[3];  // output x0 uses cols x0..x0+2, x0+1 uses x0+1..x0+3 (halo coords)
-      load_win<PP>(in + ci * PP * PP + y * PP + x0, A, M, B, PP);
+      load_win<PP>(in + ci * CPL(PP) + y * PP + x0, A, M, B, PP);
 #pragma unroll
       for (int c = 0; c < G::CG; ++c) {
         const cfp wp = w + (wrow[c] * cin + ci) * 9;
@@ -134,7 +146,7 @@ __device__ __forceinline__ void conv_fwd(const float* __restrict__ in, int cin, 
 #pragma unroll
       for (int c = 0; c < G::CG; ++c)
         if (base + c >= co0 && base + c < cout) {
-          float* op = out + (base + c) * PP * PP + (y + 1) * PP + (x0 + 1);
+          float* op = out + (base + c) * CPL(PP) + (y + 1) * PP + (x0 + 1);
           op[0] = fmaxf(acc[c].x, 0.f);
           op[1] = fmaxf(acc[c].y, 0.f);
         }
@@ -148,9 +160,9 @@ __device__ __forceinline__ void pool_fwd(const float* __restrict__ in, float* __
   constexpr int Ho = H / 2;
   for (int e = threadIdx.x; e < c * Ho * Ho; e += blockDim.x) {
     const int ch = e / (Ho * Ho), r = e % (Ho * Ho), py = r / Ho, px = r % Ho;
-    const float* p = in + ch * PPI * PPI + (2 * py + 1) * PPI + (2 * px + 1);
+    const float* p = in + ch * CPL(PPI) + (2 * py + 1) * PPI + (2 * px + 1);
     const float m = fmaxf(fmaxf(p[0], p[1]), fmaxf(p[PPI], p[PPI + 1]));
-    out[HO ? (ch * PPO * PPO + (py + 1) * PPO + (px + 1)) : (ch * Ho * Ho + py * Ho + px)] = m;
+    out[HO ? (ch * CPL(PPO) + (py + 1) * PPO + (px + 1)) : (ch * Ho * Ho + py * Ho + px)] = m;
   }
 }
 
@@ -162,8 +174,8 @@ __device__ __forceinline__ void unpool_relu_inplace(float* __restrict__ a, const
   constexpr int Ho = H / 2;
   for (int e = threadIdx.x; e < c * Ho * Ho; e += blockDim.x) {
     const int ch = e / (Ho * Ho), r = e % (Ho * Ho), py = r / Ho, px = r % Ho;
-    float* p = a + ch * PPI * PPI + (2 * py + 1) * PPI + (2 * px + 1);
-    const float gv = ghalo ? g[ch * gpitch * gpitch + (py + 1) * gpitch + (px + 1)] : g[ch * Ho * Ho + py * Ho + px];
+    float* p = a + ch * CPL(PPI) + (2 * py + 1) * PPI + (2 * px + 1);
+    const float gv = ghalo ? g[ch * CPL(gpitch) + (py + 1) * gpitch + (px + 1)] : g[ch * Ho * Ho + py * Ho + px];
     const float v0 = p[0], v1 = p[1], v2 = p[PPI], v3 = p[PPI + 1];
     int am = 0;
     float m = v0;
@@ -224,7 +236,7 @@ __device__ __forceinline__ void conv_wgrad(const float* __restrict__ dz, const f
     const bool bg = n < cin * 9;
     if (bg) {
       const int ci = n / 9, k = n - ci * 9;
-      bbase = in + ci * PP * PP + (k / 3) * PP + (k % 3);
+      bbase = in + ci * CPL(PP) + (k / 3) * PP + (k % 3);
       bstr = GROWS * PP;
     } else {
       bbase = n == cin * 9 ? one_cell : zero_cell;
@@ -234,7 +246,7 @@ __device__ __forceinline__ void conv_wgrad(const float* __restrict__ dz, const f
     const float* pb[GS];
 #pragma unroll
     for (int q = 0; q < GS; ++q) {
-      pa[q] = aok ? dz + i * PP * PP + PP + 1 + off[q] + g0 * astr : zero_cell;  // dz at (y+1, x+1)
+      pa[q] = aok ? dz + i * CPL(PP) + PP + 1 + off[q] + g0 * astr : zero_cell;  // dz at (y+1, x+1)
       pb[q] = bbase + (bg ? off[q] : 0) + g0 * bstr;
     }
     f4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};  // MFMA dependent latency 40 > issue 32
@@ -302,7 +314,7 @@ __device__ __forceinline__ void conv_dgrad(const float* __restrict__ dz, int cou
     for (int co = 0; co < cout; ++co) {
       // rows y+2-ky (ky = 0..2) of dz, cols x0..x0+3: output x0 takes col x0+2-kx, x0+1 takes x0+3-kx
       f2 A[3], M[3], B[3];
-      load_win<PP>(dz + co * PP * PP + (y + 2) * PP + x0, A, M, B, -PP);
+      load_win<PP>(dz + co * CPL(PP) + (y + 2) * PP + x0, A, M, B, -PP);
 #pragma unroll
       for (int c = 0; c < G::CG; ++c) {
         const cfp wp = w + (co * cin + wcol[c]) * 9;
@@ -318,7 +330,7 @@ __device__ __forceinline__ void conv_dgrad(const float* __restrict__ dz, int cou
 #pragma unroll
       for (int c = 0; c < G::CG; ++c) {
         if (base + c >= ci0 && base + c < cin) {
-          float* ap = a + (base + c) * PP * PP + (y + 1) * PP + (x0 + 1);
+          float* ap = a + (base + c) * CPL(PP) + (y + 1) * PP + (x0 + 1);
           ap[0] = relu ? (ap[0] > 0.f ? acc[c].x : 0.f) : acc[c].x;
           ap[1] = relu ? (ap[1] > 0.f ? acc[c].y : 0.f) : acc[c].y;
         }
@@ -359,7 +371,7 @@ __device__ __forceinline__ void conv_mfma(const float* __restrict__ in, int nin,
   bf16x8_t* wtab = (bf16x8_t*)(tab + 256);        // [ks][64 lanes] B fragments
   for (int k = threadIdx.x; k < ks * 32; k += blockDim.x) {
     const int c = k / 9, kk = k - c * 9, ky = kk / 3, kx = kk - ky * 3;
-    otab[k] = k < K ? (DG ? c * PP * PP + (2 - ky) * PP + (2 - kx) : c * PP * PP + ky * PP + kx) : -1;
+    otab[k] = k < K ? (DG ? c * CPL(PP) + (2 - ky) * PP + (2 - kx) : c * CPL(PP) + ky * PP + kx) : -1;
   }
   for (int e = threadIdx.x; e < ks * 64; e += blockDim.x) {
     const int s = e >> 6, l = e & 63, col = l & 15;
@@ -393,7 +405,7 @@ __device__ __forceinline__ void conv_mfma(const float* __restrict__ in, int nin,
       for (int r = 0; r < 4; ++r) {
         const int q = t * 16 + 4 * kq + r;
         if (q < H * H) {
-          float* o = out + col * PP * PP + (q / H + 1) * PP + (q % H + 1);
+          float* o = out + col * CPL(PP) + (q / H + 1) * PP + (q % H + 1);
           if (!DG) *o = fmaxf(acc[r] + bias, 0.f);
           else *o = RELU ? (*o > 0.f ? acc[r] : 0.f) : acc[r];
         }
@@ -422,7 +434,7 @@ __device__ __forceinline__ void conv_wgrad_bf16(const float* __restrict__ dz, co
   const int units = nt * nch;
   const int i = lane & 15, g = lane >> 4;
   const bool aok = i < cout;
-  const float* pa = dz + (aok ? i : 0) * PP * PP;
+  const float* pa = dz + (aok ? i : 0) * CPL(PP);
   for (int u = wv; u < units; u += nw) {
     const int t = u % nt, ch = u / nt;
     const int n = t * 16 + i;  // this lane's B column
@@ -430,7 +442,7 @@ __device__ __forceinline__ void conv_wgrad_bf16(const float* __restrict__ dz, co
     int boff = 0;
     if (mode == 0) {
       const int ci = n / 9, k = n - ci * 9;
-      boff = ci * PP * PP + (k / 3 - 1) * PP + (k % 3 - 1);
+      boff = ci * CPL(PP) + (k / 3 - 1) * PP + (k % 3 - 1);
     }
     const int s0 = ch * KS / nch, s1 = (ch + 1) * KS / nch;
     f32x4_t d = {0.f, 0.f, 0.f, 0.f};
