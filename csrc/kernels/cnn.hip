@@ -447,19 +447,29 @@ __device__ __forceinline__ void conv_wgrad_bf16(const float* __restrict__ dz, co
     const int s0 = ch * KS / nch, s1 = (ch + 1) * KS / nch;
     f32x4_t d = {0.f, 0.f, 0.f, 0.f};
     for (int s = s0; s < s1; ++s) {
-      const int q = PP + 32 * s + 8 * g;
+      // 28 x 28: lane group g takes positions q + g + 4 e — for one e the 64 lanes read 16
+      // channels x 4 consecutive positions (distinct banks at the 908-float plane stride) instead
+      // of 8-position runs (measured: conv2 / conv1 weight gradients -4 %, -5 %; at 14 x 14 the
+      // runs are faster)
+      constexpr int QS = H == 28 ? 4 : 1;
+      const int q = PP + 32 * s + (QS == 4 ? g : 8 * g);
       float av[8], bv[8];
       if (aok) {
-        const f2* ap = (const f2*)(pa + q);  // q even, plane bases 8-B aligned
+        if (QS == 1) {
+          const f2* ap = (const f2*)(pa + q);  // q even, plane bases 8-B aligned
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { const f2 v = ap[e]; av[2 * e] = v.x; av[2 * e + 1] = v.y; }
+          for (int e = 0; e < 4; ++e) { const f2 v = ap[e]; av[2 * e] = v.x; av[2 * e + 1] = v.y; }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) av[e] = pa[q + QS * e];
+        }
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e) av[e] = 0.f;
       }
       if (mode == 0) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) bv[e] = in[max(boff + q + e, 0)];
+        for (int e = 0; e < 8; ++e) bv[e] = in[max(boff + q + QS * e, 0)];
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e) bv[e] = mode == 1 ? 1.f : 0.f;
