@@ -49,6 +49,9 @@ __device__ unsigned long long cnn_stamps[64 * 32];
 #define CNN_PAD28 8
 #endif
 #define CPL(pp) ((pp) * (pp) + ((pp) == P14 ? CNN_PAD14 : CNN_PAD28))
+#ifndef CNN_CONV1_VALU_MAXC
+#define CNN_CONV1_VALU_MAXC 2
+#endif
 #define PL28 CPL(P28)
 #define PL14 CPL(P14)
 
@@ -793,7 +796,11 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   }
   __syncthreads();
   STAMP(1);
-  if (BF) conv_mfma<28, P28, false, false>(xin, CI, a1, C, lw[0], lb[0], wscr);
+  // conv1 on the VALU in both modes when the input has one or two channels: an MFMA k-step would
+  // be 9 (18) real taps of 32, and the fp32 sliding-window conv needs no fragment tables
+  // (measured at 1 channel: 6.4k -> 2.9k clocks; its weight gradient stays on the bf16 MFMA path,
+  // the fp32 one measured 4.7k -> 6.4k)
+  if (BF && CI > CNN_CONV1_VALU_MAXC) conv_mfma<28, P28, false, false>(xin, CI, a1, C, lw[0], lb[0], wscr);
   else conv_fwd<28, P28, CC, EX>(xin, CI, a1, C, g.w[0], g.b[0]);
   __syncthreads();
   STAMP(2);
