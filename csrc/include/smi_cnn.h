@@ -23,4 +23,6 @@ struct CNNArgs {
   float* part; unsigned* tick; const float* lr; float* step;
   unsigned short* shadow[10];                // per-parameter bf16 shadows (slab order) or null
 };
+#ifndef CNN_GRP
 #define CNN_GRP 8
+#endif
