@@ -579,6 +579,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("emb_pair", [](int set) { return smi_emb_pair(set); },
         "deterministic embedding backward: 1 = pair-compare (<= 8192 tokens), 0 = bucketed lists; -1 queries");
   m.def("cnn_fused_ok", [](int C, int cin, int classes, int B) { return smi_cnn_fused_ok(C, cin, classes, B) != 0; });
+  m.def("cnn_grp", []() { return (int)CNN_GRP; });  // images per fused-tail group (part rows, tickets)
 
   m.def("lstm_supported", [](int E, int H, int L, int C) { return smi_lstm_supported(E, H, L, C) != 0; });
   m.def("lstm_slab_floats", [](int B, int E, int H, int L, int C) { return smi_lstm_slab_floats(B, E, H, L, C); });

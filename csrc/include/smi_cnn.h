@@ -26,3 +26,4 @@ struct CNNArgs {
 #ifndef CNN_GRP
 #define CNN_GRP 8
 #endif
+static_assert(CNN_GRP >= 1 && CNN_GRP <= 32, "the model owns CNN_GRP + 1 <= 33 tickets");

@@ -994,7 +994,8 @@ static size_t cnn_lds_bytes(const CNNArgs& g) {
 
 extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
   CNNArgs g = *args;
-  if (g.fused && (g.P % 4 || !g.part || !g.tick || !g.lr || !g.slab || !g.row_loss || !g.train)) return -1;
+  // the fused tail's group tickets are tick[0 .. ngrp) below the level-2 ticket tick[CNN_GRP]
+  if (g.fused && (g.P % 4 || (g.B + CNN_GRP - 1) / CNN_GRP > CNN_GRP || !g.part || !g.tick || !g.lr || !g.slab || !g.row_loss || !g.train)) return -1;
   if (g.C < 1 || g.C > CNN_MAXC || g.cin < 1 || g.cin > 4 || g.classes < 1 || g.classes > 16) return -1;
   g.wstage = g.bf16 ? 1 : 0;
   if (g.wstage && cnn_lds_bytes(g) > 160 * 1024) g.wstage = 0;  // the weights then stay global
@@ -1016,7 +1017,8 @@ extern "C" int smi_cnn_fused_ok(int C, int cin, int classes, int B) {
   CNNArgs g{};
   g.C = C; g.cin = cin; g.classes = classes;
   const int P = C * cin * 9 + C + 3 * (C * C * 9 + C) + classes * C * 49 + classes;
-  return P % 4 == 0 && (size_t)B * ((classes + C * 49 + 3) & ~3) * sizeof(float) <= cnn_lds_bytes(g);
+  return P % 4 == 0 && B <= CNN_GRP * CNN_GRP &&
+         (size_t)B * ((classes + C * 49 + 3) & ~3) * sizeof(float) <= cnn_lds_bytes(g);
 }
 
 extern "C" int smi_cnn_reduce(const CNNArgs* args, hipStream_t st) {

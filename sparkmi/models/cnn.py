@@ -26,9 +26,9 @@ class FashionMNISTModel(nn.Module):
             nn.Conv2d(hidden_units, hidden_units, 3, padding=1), nn.ReLU(),
             nn.MaxPool2d(2))
         self.classifier = nn.Sequential(nn.Flatten(), nn.Linear(hidden_units * 7 * 7, output_shape))
-        # fused-step tickets (CNN_GRP + 1 counters, re-armed by the kernel): per model, so two
-        # models never share them; not part of the state_dict (reference key parity)
-        self.register_buffer("_step_tick", torch.zeros(9, dtype=torch.int32), persistent=False)
+        # fused-step tickets (CNN_GRP + 1 <= 33 counters, re-armed by the kernel): per model, so
+        # two models never share them; not part of the state_dict (reference key parity)
+        self.register_buffer("_step_tick", torch.zeros(33, dtype=torch.int32), persistent=False)
 
     def param_list(self):
         c = [self.block_1[0], self.block_1[2], self.block_2[0], self.block_2[2], self.classifier[1]]

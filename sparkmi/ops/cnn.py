@@ -124,7 +124,8 @@ def cnn_sgd_step(x, y, params, lr_t, step_t, tick, shadows=None, bf16=False):
     b = [params[i] for i in (1, 3, 5, 7, 9)]
     P = num_params(params)
     slab = torch.empty(B, P, device=x.device, dtype=torch.float32)
-    part = torch.empty((B + 7) // 8, P, device=x.device, dtype=torch.float32)
+    grp = _native.C().cnn_grp()
+    part = torch.empty((B + grp - 1) // grp, P, device=x.device, dtype=torch.float32)
     row_loss = torch.empty(B, device=x.device, dtype=torch.float32)
     loss = torch.empty(1, device=x.device, dtype=torch.float32)
     _native.C().cnn_sgd_step(x.data_ptr(), int(x.dtype == torch.uint8), 1.0 / 255.0, y.data_ptr(), B, x.shape[1],
