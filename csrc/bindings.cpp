@@ -82,14 +82,7 @@ int smi_split3(const float*, long, int, long, void*, long, long, hipStream_t);
 int smi_gemm_sp_waves(int);
 int smi_gemm_sp_tm(int);
 int smi_gemm_sp_wg_tm(int);
-int smi_attn_f32_sp(int);
-int smi_attn_dkdv8(int);
-int smi_attn_fwd8(int);
-int smi_attn_stagger(int);
 int smi_attn_ae(int);
-int smi_attn_ae_bwd(int);
-int smi_attn_skew(int);
-int smi_attn_fwd_stagger(int);
 int smi_adam_wide(int);
 int smi_splitk_reduce(const float*, int, long, float*, long, float*, int, hipStream_t);
 int smi_splitk_fold_multi(const float* const*, float* const*, float* const*, const long*, const int*, const int*, int,
@@ -208,11 +201,8 @@ PYBIND11_MODULE(_C, m) {
   // fp32 attention: (q, k, v) pointers + (batch, seq, head) strides; o/lse written by the forward
   // op / op_ps (fwd), dqp / dkp / dvp / dq_ps / dkv_ps (bwd): optional split planes of the outputs
   m.def("attn_f32_fwd", [](u q, u k, u v, py::tuple qs, py::tuple ks, py::tuple vs, u o, py::tuple os, u lse, u kpad,
-                           int B, int H, int Sq, int Sk, int mode, float scale_log2, u op, long op_ps, u qpi, u kpi,
-                           u vpi, long qi_ps, long kvi_ps, u st) {
+                           int B, int H, int Sq, int Sk, int mode, float scale_log2, u op, long op_ps, u st) {
     AttnF32Args a{};
-    a.qpi = (const unsigned short*)qpi; a.kpi = (const unsigned short*)kpi; a.vpi = (const unsigned short*)vpi;
-    a.qi_ps = qi_ps; a.kvi_ps = kvi_ps;
     a.q = (const float*)q; a.k = (const float*)k; a.v = (const float*)v;
     a.q_sb = qs[0].cast<long>(); a.q_ss = qs[1].cast<long>(); a.q_sh = qs[2].cast<long>();
     a.k_sb = ks[0].cast<long>(); a.k_ss = ks[1].cast<long>(); a.k_sh = ks[2].cast<long>();
@@ -225,12 +215,9 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("attn_f32_bwd", [](u q, u k, u v, py::tuple qs, py::tuple ks, py::tuple vs, u o, u dout, py::tuple os, u lse,
                            u delta, u dq, u dk, u dv, u kpad, int B, int H, int Sq, int Sk, int mode, float scale_log2,
-                           float scale, u dqp, u dkp, u dvp, long dq_ps, long dkv_ps, u qpi, u kpi, u vpi, u dopi,
-                           long qi_ps, long kvi_ps, long doi_ps, int no_f32_grad, u st) {
+                           float scale, u dqp, u dkp, u dvp, long dq_ps, long dkv_ps, int no_f32_grad, u st) {
     AttnF32Args a{};
     a.no_f32_grad = no_f32_grad;
-    a.qpi = (const unsigned short*)qpi; a.kpi = (const unsigned short*)kpi; a.vpi = (const unsigned short*)vpi;
-    a.dopi = (const unsigned short*)dopi; a.qi_ps = qi_ps; a.kvi_ps = kvi_ps; a.doi_ps = doi_ps;
     a.dqp = (unsigned short*)dqp; a.dkp = (unsigned short*)dkp; a.dvp = (unsigned short*)dvp;
     a.dq_ps = dq_ps; a.dkv_ps = dkv_ps;
     a.q = (const float*)q; a.k = (const float*)k; a.v = (const float*)v;
@@ -478,17 +465,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_sp_waves", [](int set) { return smi_gemm_sp_waves(set); },
         "split-plane GEMM waves per 128x128 tile (4 | 8); other values query");
   m.def("gemm_sp_tm", [](int set) { return smi_gemm_sp_tm(set); },
-        "split-plane GEMM tile form for large problems (16: 256x128 on 16x16x32 MFMA | 256 | 4 | 128); other values query");
-  m.def("attn_dkdv8", [](int set) { return smi_attn_dkdv8(set); },
-        "fp32 attention dK/dV: 1 = 8-wave workgroups with owned V in LDS (default), 0 = 4-wave; other values query");
+        "split-plane GEMM tile form for large problems (16: 256x128 on 16x16x32 MFMA | 256 | 128); other values query");
   m.def("adam_wide", [](int set) { return smi_adam_wide(set); },
         "Adam launch: 1 = 1024-thread blocks, <= 512 (default), 0 = 256-thread blocks, <= 4096; other values query");
-  m.def("attn_fwd8", [](int set) { return smi_attn_fwd8(set); },
-        "fp32 attention forward: 1 = 8-wave workgroups (a whole head per workgroup), 0 = 4-wave (default); other values query");
-  m.def("attn_f32_sp", [](int set) { return smi_attn_f32_sp(set); },
-        "fp32 attention kernels: 1 staged-plane (default), 0 per-wave split; other values query");
   m.def("gemm_sp_wg_tm", [](int set) { return smi_gemm_sp_wg_tm(set); },
-        "tile form of the grouped weight-gradient launch (128 | 256 | 16 | 4; -1 follows gemm_sp_tm); other values query");
+        "tile form of the grouped weight-gradient launch (128 | 256 | 16; -1 follows gemm_sp_tm); other values query");
   m.def("gemm_f32_algo", [](int set) { return smi_gemm_f32_algo(set); },
         "fp32 GEMM product algorithm: 0 = f32 MFMA, 6 = 3-way bf16 split (6 terms); set < 0 queries");
   m.def("gemm_f32_wgrad_group", [](std::vector<u> A, std::vector<long> lda, std::vector<u> B, std::vector<long> ldb,
@@ -554,16 +535,8 @@ PYBIND11_MODULE(_C, m) {
     a.lr = (const float*)lr; a.step = (float*)step; a.tick = (unsigned*)tick;
     chk(smi_cnn(&a, S(st)), "cnn_sgd_step");
   });
-  m.def("attn_fwd_stagger", [](int set) { return smi_attn_fwd_stagger(set); },
-        "fp32 attention forward: 1 = staggered 8-wave kernel, 0 = 4-wave (default); -1 queries");
-  m.def("attn_skew", [](int set) { return smi_attn_skew(set); },
-        "fp32 attention forward / dQ: the second workgroup per CU starts set x 512 cycles late; -1 queries");
-  m.def("attn_ae_bwd", [](int set) { return smi_attn_ae_bwd(set); },
-        "fp32 attention backward outputs through LDS: 1 = on, 0 = per-lane stores (default); -1 queries");
   m.def("attn_ae", [](int set) { return smi_attn_ae(set); },
-        "fp32 attention outputs: 1 = whole-row stores through LDS (default), 0 = per-lane stores; -1 queries");
-  m.def("attn_stagger", [](int set) { return smi_attn_stagger(set); },
-        "fp32 attention dK/dV: 1 = staggered 8-wave kernel (default), 0 = lockstep; -1 queries");
+        "fp32 attention outputs (forward and backward): 1 = whole-row stores through LDS (default), 0 = per-lane stores; -1 queries");
   m.def("emb_pair_max", [](long set) { return smi_emb_pair_max(set); },
         "largest token batch the pair-compare embedding backward takes (set < 0 queries)");
   m.def("emb_plan_algo", [](long T, long V) { return smi_emb_plan_algo(T, V); },

@@ -38,15 +38,7 @@ struct AttnF32Args {
   // (sparkmi/ops/planes.py): same element offsets as O / dQ / dK,dV, planes op_ps / dq_ps / dkv_ps apart
   unsigned short* op; unsigned short* dqp; unsigned short* dkp; unsigned short* dvp;
   long op_ps, dq_ps, dkv_ps;
-  // optional planes of the INPUTS, written by their producers' epilogues (the projection GEMMs,
-  // the out-projection's dgrad): same element offsets and strides as q / k / v / dout, planes
-  // qi_ps / kvi_ps / doi_ps apart.  All of q, k, v (and dout in the backward) or none.
-  const unsigned short* qpi; const unsigned short* kpi; const unsigned short* vpi; const unsigned short* dopi;
-  long qi_ps, kvi_ps, doi_ps;
   int no_f32_grad;                   // backward: write dQ / dK / dV as planes only (dqp / dkp / dvp set)
   int ae16;                          // set by the launcher: outputs and their planes admit whole-row
                                      // 16-B stores (row-coalesced LDS epilogue, attention_f32.hip)
-  int skew;                          // set by the launcher (SMI_ATTN_SKEW): the second workgroup of
-                                     // each CU starts skew x 512 cycles late (desynchronises the two
-                                     // resident workgroups' MFMA and softmax phases)
 };

@@ -44,25 +44,6 @@ struct F32Tile {
   static constexpr int NV = R / 32;  // float4 staging loads per thread
 };
 
-// Global -> registers: the operand tile at (row/col origin r0, k origin k0).  Out-of-range rows /
-// columns / k read as 0 (rlim, klim exclusive; float4 granularity: klim % 4 == 0 for k-contig,
-// rlim % 4 == 0 for k-major, checked by the launcher).
-template <bool KMAJ, int R>
-__device__ __forceinline__ void f32_gload(const float* __restrict__ base, long ld, int r0, int rlim, int k0, int klim,
-                                          float4 (&v)[F32Tile<KMAJ, R>::NV], int tid) {
-#pragma unroll
-  for (int i = 0; i < F32Tile<KMAJ, R>::NV; ++i) {
-    const int f = tid + 256 * i;
-    if (!KMAJ) {
-      const int row = f >> 3, gr = r0 + row, gk = k0 + (f & 7) * 4;
-      v[i] = (gr < rlim && gk < klim) ? *(const float4*)(base + (long)gr * ld + gk) : make_float4(0.f, 0.f, 0.f, 0.f);
-    } else {
-      const int kr = f / (R / 4), gk = k0 + kr, gc = r0 + (f % (R / 4)) * 4;
-      v[i] = (gk < klim && gc < rlim) ? *(const float4*)(base + (long)gk * ld + gc) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  }
-}
-
 // Branch-free global -> register staging through a buffer descriptor: out-of-range rows / k read
 // 0 because their offset is pushed past the descriptor's extent (the range check returns zeros),
 // so a k-loop body stays ONE basic block and sched_group_barrier can interleave it.
@@ -129,169 +110,6 @@ __device__ __forceinline__ int f32_tile_remap(int orig, int nwg) {
 // the five correction terms in a second accumulator added once at the end.  Rate: 6 x
 // v_mfma_f32_32x32x16_bf16 (32 cycles each) per 32x32x16 block vs 8 x v_mfma_f32_32x32x2_f32
 // (64 cycles each) — 2.7x the f32 matrix-core rate for the same exact-product fp32 arithmetic.
-
-// Fused epilogue of one output tile (acc = this wave's FM x 2 32x32 accumulators):
-// FWD + bias, activation, dropout; DGRAD + residual, relu'/dropout mask; WGRAD accumulate (+ the
-// bias-gradient row sums of A).  Each store instruction writes two full 128-B row segments.
-template <bool AK, int FM>
-__device__ __forceinline__ void f32_epilogue(const GemmF32Args& g, f32x16_t (&acc)[FM][2], float (&bsum)[FM], int m0,
-                                             int n0, int wm, int wn, int lane, bool do_bias) {
-  constexpr int BMT = 64 * FM;
-  const uint32_t seed = g.thresh ? smi_seed(g.seedp, g.salt) : 0u;
-  const int h = lane >> 5;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int col = n0 + wn * 64 + j * 32 + (lane & 31);
-    const bool cok = col < g.N;
-    const float bia = (g.bias && cok) ? g.bias[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * BMT / 2 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (!cok || row >= g.M) continue;
-        const long cidx = (long)row * g.ldc + col;
-        float v = acc[i][j][r];
-        if (g.mode == 0) {
-          v += bia;
-          if (g.relu == 1) v = fmaxf(v, 0.f);
-          else if (g.relu == 2) v = 1.f / (1.f + __expf(-v));
-          if (g.thresh) v = smi_keep(seed, (uint32_t)cidx, g.thresh) ? v * g.dscale : 0.f;
-        } else if (g.mode == 1) {
-          if (g.resid) v += g.resid[(long)row * g.ldr + col];
-          if (g.dact_y) v = g.dact_y[(long)row * g.ldy + col] > 0.f ? v * g.dscale : 0.f;
-        }
-        if (g.atomic) atomicAdd(g.C + cidx, v);
-        else g.C[cidx] = g.beta_acc ? g.C[cidx] + v : v;
-      }
-    }
-  }
-  if (do_bias) {
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      // lanes l and l + 32 hold the two k-halves of row (l & 31)
-      auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(bsum[i]), __float_as_uint(bsum[i]), false, false);
-      const float tot = __uint_as_float(a[0]) + __uint_as_float(a[1]);
-      const int row = m0 + wm * BMT / 2 + i * 32 + (lane & 31);
-      if (h == 0 && row < g.M) {
-        if (g.atomic) atomicAdd(g.bias_grad + row, tot);
-        else g.bias_grad[row] = g.beta_acc ? g.bias_grad[row] + tot : tot;
-      }
-    }
-  }
-}
-
-// One output tile (all its k-tiles of split `split` and the epilogue).
-template <bool AK, bool BKM, int FM, int PF>
-__device__ __forceinline__ void gemm_f32_tile(const GemmF32Args& g, int tile, int split, float* smem) {
-  constexpr int BMT = 64 * FM;
-  using TA = F32Tile<AK, BMT>;
-  using TB = F32Tile<BKM, FBN>;
-  constexpr int STAGE = TA::ELEMS + TB::ELEMS;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 1, wn = w & 1;
-  const int ntn = (g.N + FBN - 1) / FBN;
-  const int m0 = (tile / ntn) * BMT, n0 = (tile % ntn) * FBN;
-  const int kbeg = split * g.k_per_split;
-  const int kend = min(g.K, kbeg + g.k_per_split);
-  const int nk = (kend - kbeg + FBK - 1) / FBK;
-
-  f32x16_t acc[FM][2];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  const bool do_bias = AK && g.bias_grad && n0 == 0 && wn == 0;
-  float bsum[FM];
-#pragma unroll
-  for (int i = 0; i < FM; ++i) bsum[i] = 0.f;
-
-  // one k-tile of MFMAs on LDS stage `st` (and the fused bias-gradient row sums)
-  auto compute = [&](int st) {
-    const float* ta = smem + st * STAGE;
-    const float* tb = ta + TA::ELEMS;
-    float af[FM][16], bf[2][16];
-#pragma unroll
-    for (int i = 0; i < FM; ++i) f32_frag<AK, BMT>(ta, wm * BMT / 2 + i * 32, lane, af[i]);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) f32_frag<BKM, FBN>(tb, wn * 64 + j * 32, lane, bf[j]);
-#pragma unroll
-    for (int s = 0; s < 16; ++s)
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
-    if (do_bias) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int s = 0; s < 16; ++s) bsum[i] += af[i][s];
-    }
-  };
-  float4 va[TA::NV], vb[TB::NV];
-  f32_gload<AK, BMT>(g.A, g.lda, m0, g.M, kbeg, kend, va, tid);
-  f32_gload<BKM, FBN>(g.B, g.ldb, n0, g.N, kbeg, kend, vb, tid);
-  if constexpr (PF == 1) {
-    f32_lstore<AK, BMT>(smem, va, tid);
-    f32_lstore<BKM, FBN>(smem + TA::ELEMS, vb, tid);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      const bool more = kt + 1 < nk;
-      if (more) {  // next k-tile's loads fly under this k-tile's MFMAs
-        f32_gload<AK, BMT>(g.A, g.lda, m0, g.M, kbeg + (kt + 1) * FBK, kend, va, tid);
-        f32_gload<BKM, FBN>(g.B, g.ldb, n0, g.N, kbeg + (kt + 1) * FBK, kend, vb, tid);
-      }
-      compute(kt & 1);
-      if (more) {
-        float* nx = smem + ((kt + 1) & 1) * STAGE;
-        f32_lstore<AK, BMT>(nx, va, tid);
-        f32_lstore<BKM, FBN>(nx + TA::ELEMS, vb, tid);
-      }
-      __syncthreads();
-    }
-  } else {
-    // prefetch distance 2: two register sets (unrolled by 2), a k-tile's loads are issued two
-    // k-tiles of MFMAs before they are stored to LDS — HBM / MALL latency under load exceeds one
-    // k-tile of MFMAs at 64-row tiles (~2k cycles per wave)
-    float4 va1[TA::NV], vb1[TB::NV];
-    if (nk > 1) {
-      f32_gload<AK, BMT>(g.A, g.lda, m0, g.M, kbeg + FBK, kend, va1, tid);
-      f32_gload<BKM, FBN>(g.B, g.ldb, n0, g.N, kbeg + FBK, kend, vb1, tid);
-    }
-    f32_lstore<AK, BMT>(smem, va, tid);
-    f32_lstore<BKM, FBN>(smem + TA::ELEMS, vb, tid);
-    __syncthreads();
-    for (int kt = 0; kt < nk; kt += 2) {
-      if (kt + 2 < nk) {
-        f32_gload<AK, BMT>(g.A, g.lda, m0, g.M, kbeg + (kt + 2) * FBK, kend, va, tid);
-        f32_gload<BKM, FBN>(g.B, g.ldb, n0, g.N, kbeg + (kt + 2) * FBK, kend, vb, tid);
-      }
-      compute(0);
-      if (kt + 1 < nk) {
-        f32_lstore<AK, BMT>(smem + STAGE, va1, tid);
-        f32_lstore<BKM, FBN>(smem + STAGE + TA::ELEMS, vb1, tid);
-      }
-      __syncthreads();
-      if (kt + 1 >= nk) break;
-      if (kt + 3 < nk) {
-        f32_gload<AK, BMT>(g.A, g.lda, m0, g.M, kbeg + (kt + 3) * FBK, kend, va1, tid);
-        f32_gload<BKM, FBN>(g.B, g.ldb, n0, g.N, kbeg + (kt + 3) * FBK, kend, vb1, tid);
-      }
-      compute(1);
-      if (kt + 2 < nk) {
-        f32_lstore<AK, BMT>(smem, va, tid);
-        f32_lstore<BKM, FBN>(smem + TA::ELEMS, vb, tid);
-      }
-      __syncthreads();
-    }
-  }
-
-  f32_epilogue<AK, FM>(g, acc, bsum, m0, n0, wm, wn, lane, do_bias);
-}
-
 
 // Compile-time epilogue feature set of the pipelined kernel (EPI < 0: generic runtime flags).
 // Measured: the runtime-generic epilogue was ~9,700 instructions per wave (per-element mode /
@@ -791,16 +609,6 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_pipe_kernel(GemmF32Args g) {
   const int tile = f32_tile_remap(blockIdx.x - split * nwg, nwg);
   if constexpr (XS == 2) gemm_xs_tile<AK, BKM, EPI>(g, tile, split, smem);
   else gemm_f32_tile_pipe<AK, BKM, EPI, XS>(g, tile, split, smem);
-}
-
-template <bool AK, bool BKM, int FM, int PF>
-__global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmF32Args g) {
-  constexpr int BMT = 64 * FM;
-  __shared__ __attribute__((aligned(16))) float smem[2 * (F32Tile<AK, BMT>::ELEMS + F32Tile<BKM, FBN>::ELEMS)];
-  const int nwg = ((g.M + BMT - 1) / BMT) * ((g.N + FBN - 1) / FBN);
-  const int split = blockIdx.x / nwg;
-  const int tile = f32_tile_remap(blockIdx.x - split * nwg, nwg);
-  gemm_f32_tile<AK, BKM, FM, PF>(g, tile, split, smem);
 }
 
 // Grouped weight-gradient GEMMs (fp32): gw_e[n,k] += dY_e[T,n]^T X_e[T,k] (and gb_e[n] += dY_e^T 1)

@@ -537,71 +537,18 @@ __device__ __forceinline__ void as_store(unsigned short* img, const AStage& p, i
   *(bf16x8_t*)(img + AS_PL + o) = sp.m;
   *(bf16x8_t*)(img + 2 * AS_PL + o) = sp.l;
 }
-// PLANE INPUTS (PI): when the producer of Q / K / V (the projection GEMM's epilogue) or of dO (the
-// out-projection's dgrad epilogue) already wrote the operand's hi / mid / lo planes, a chunk is
-// staged as three 16-B loads + three 16-B LDS stores per thread and the owned rows are loaded as
-// ready MFMA operands: no split arithmetic left outside the per-block P / dS values.
-struct APStage { uint4 h, m, l; };
-template <bool PI> struct AStageT { using T = AStage; };
-template <> struct AStageT<true> { using T = APStage; };
-__device__ __forceinline__ void as_load(const unsigned short* __restrict__ base, long ps, long ss, int r0, int rmax,
-                                        APStage& p, int ti = -1) {
-  if (ti < 0) ti = threadIdx.x;
-  const int r = ti >> 3, c = (ti & 7) * 8;
-  if (r0 + r < rmax) {
-    const unsigned short* q = base + (long)(r0 + r) * ss + c;
-    p.h = *(const uint4*)q;
-    p.m = *(const uint4*)(q + ps);
-    p.l = *(const uint4*)(q + 2 * ps);
-  } else {
-    p.h = p.m = p.l = make_uint4(0u, 0u, 0u, 0u);
-  }
-}
-__device__ __forceinline__ void as_store(unsigned short* img, const APStage& p, int ti = -1) {
-  if (ti < 0) ti = threadIdx.x;
-  const int o = as_off(ti >> 3, (ti & 7) * 8);
-  *(uint4*)(img + o) = p.h;
-  *(uint4*)(img + AS_PL + o) = p.m;
-  *(uint4*)(img + 2 * AS_PL + o) = p.l;
-}
-// one operand's fp32 source or its planes: staged loads / owned rows / reconstructed fp32 rows
-template <bool PI>
+// one operand's fp32 source: staged loads / owned rows (split once per kernel)
 struct AsSrc {
-  const float* f; const unsigned short* p; long ps, ss;
-  __device__ __forceinline__ void load(int r0, int rmax, typename AStageT<PI>::T& st, int ti = -1) const {
-    if constexpr (PI) as_load(p, ps, ss, r0, rmax, st, ti);
-    else as_load(f, ss, r0, rmax, st, ti);
-  }
+  const float* f; long ss;
+  __device__ __forceinline__ void load(int r0, int rmax, AStage& st, int ti = -1) const { as_load(f, ss, r0, rmax, st, ti); }
   // the owned row as ready operands (F32Pre order: s[j] = head dims 32 h + 8 j .. + 7)
   __device__ __forceinline__ void own(int row, int rmax, int lane, F32Pre<1, 32>& o) const {
-    if constexpr (PI) {
-      const bool ok = row < rmax;
-      const unsigned short* q = p + (long)row * ss + 32 * (lane >> 5);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-        o.s[j].h = __builtin_bit_cast(bf16x8_t, ok ? *(const uint4*)(q + 8 * j) : z);
-        o.s[j].m = __builtin_bit_cast(bf16x8_t, ok ? *(const uint4*)(q + ps + 8 * j) : z);
-        o.s[j].l = __builtin_bit_cast(bf16x8_t, ok ? *(const uint4*)(q + 2 * ps + 8 * j) : z);
-      }
-    } else {
-      float v[32];
-      fa_ownrow(f, ss, row, rmax, lane, v);
-      o.set(v);
-    }
+    float v[32];
+    fa_ownrow(f, ss, row, rmax, lane, v);
+    o.set(v);
   }
-  // the owned row's fp32 values (planes: h + m + l, exact)
-  __device__ __forceinline__ void own_f32(const F32Pre<1, 32>& o, int row, int rmax, int lane, float (&v)[32]) const {
-    if constexpr (PI) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          v[8 * j + e] = (bf2f((unsigned short)o.s[j].h[e]) + bf2f((unsigned short)o.s[j].m[e])) +
-                         bf2f((unsigned short)o.s[j].l[e]);
-    } else {
-      fa_ownrow(f, ss, row, rmax, lane, v);
-    }
+  __device__ __forceinline__ void own_f32(int row, int rmax, int lane, float (&v)[32]) const {
+    fa_ownrow(f, ss, row, rmax, lane, v);
   }
 };
 
@@ -704,58 +651,34 @@ __device__ __forceinline__ void ae_store(const float* img, float* __restrict__ d
   }
 }
 
-// the second resident workgroup of each CU (linear block id >= one per CU) sleeps a.skew x 512
-// cycles before its prologue (wave-uniform)
-__device__ __forceinline__ void fa_skew(const AttnF32Args& a) {
-  if (a.skew > 0) {
-    const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-    if (lin >= 256)
-      for (int i = 0; i < a.skew; ++i) __builtin_amdgcn_s_sleep(8);
-  }
-}
+// operand source of batch b, head hh
+#define AS_SRC(NAME, FP, SB, SH, SS) const AsSrc NAME{(FP) + b * (SB) + hh * (SH), (SS)}
 
-// operand sources of batch b, head hh (fp32 base + plane base at the same element offset)
-#define AS_SRC(NAME, FP, PP, PS, SB, SH, SS)                                                         \
-  const AsSrc<PI> NAME{(FP) + b * (SB) + hh * (SH), PI ? (PP) + b * (SB) + hh * (SH) : nullptr, (PS), (SS)}
-
-// NW = waves per workgroup, 32 queries each.  NW = 8 (opt-in, smi_attn_fwd8; at S = 256 a whole
-// head per workgroup, one workgroup per CU, still two waves per SIMD): each streamed K / V chunk is staged
-// once for 256 queries instead of 128 — half the staging loads, splits and LDS stores per wave
-// (threads 0-255 stage K, 256-511 V) and half the K / V reads from L2 / HBM.  Per-wave arithmetic
-// and its order are those of NW = 4 (bitwise-identical output).
-template <int MODE, bool KPAD, bool PI, int NW>
-__device__ __forceinline__ void attn_sp_fwd_body(const AttnF32Args& a) {
-  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-  constexpr int QW = 32 * NW;  // queries per workgroup
+// Forward: four waves of 32 queries per workgroup, two workgroups per CU; K / V streamed in
+// 32-row chunks through double-buffered staged planes (an 8-wave variant with one staged chunk
+// per 256 queries, and a staggered one, measured no faster in the step: round 4).
+template <int MODE, bool KPAD>
+__global__ __launch_bounds__(256, 2) void attn_sp_fwd4(AttnF32Args a) {
+  constexpr int QW = 128;  // queries per workgroup
   __shared__ __attribute__((aligned(16))) unsigned short Ks[2][AS_OP];
   __shared__ __attribute__((aligned(16))) unsigned short Vs[2][AS_OP];
   AST_DECL;
   AST_T(tk0);
-  fa_skew(a);
   const int hh = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
   const int qwave = blockIdx.x * QW + w * 32;
   const int qi = qwave + (lane & 31);
-  AS_SRC(Q, a.q, a.qpi, a.qi_ps, a.q_sb, a.q_sh, a.q_ss);
-  AS_SRC(K, a.k, a.kpi, a.kvi_ps, a.k_sb, a.k_sh, a.k_ss);
-  AS_SRC(V, a.v, a.vpi, a.kvi_ps, a.v_sb, a.v_sh, a.v_ss);
+  AS_SRC(Q, a.q, a.q_sb, a.q_sh, a.q_ss);
+  AS_SRC(K, a.k, a.k_sb, a.k_sh, a.k_ss);
+  AS_SRC(V, a.v, a.v_sb, a.v_sh, a.v_ss);
   const unsigned char* kp = a.kpad ? a.kpad + (long)b * a.Sk : nullptr;
   int kend = a.Sk;
   if (MODE == 2) kend = min(a.Sk, blockIdx.x * QW + QW);
   const int nchunks = (kend + FCH - 1) / FCH;
-  // chunk staging: NW = 4 every thread stages 8 values of K and 8 of V; NW = 8 one operand per
-  // half of the workgroup (wave-uniform)
-  const bool kside = NW == 4 || threadIdx.x < 256;
-  const int ti = threadIdx.x & 255;
-  typename AStageT<PI>::T pk, pv;
-  auto stage_load = [&](int r0) {
-    if constexpr (NW == 4) { K.load(r0, a.Sk, pk); V.load(r0, a.Sk, pv); }
-    else { if (kside) K.load(r0, a.Sk, pk, ti); else V.load(r0, a.Sk, pk, ti); }
-  };
-  auto stage_store = [&](int bf) {
-    if constexpr (NW == 4) { as_store(Ks[bf], pk); as_store(Vs[bf], pv); }
-    else as_store(kside ? Ks[bf] : Vs[bf], pk, ti);
-  };
+  // chunk staging: every thread stages 8 values of K and 8 of V
+  AStage pk, pv;
+  auto stage_load = [&](int r0) { K.load(r0, a.Sk, pk); V.load(r0, a.Sk, pv); };
+  auto stage_store = [&](int bf) { as_store(Ks[bf], pk); as_store(Vs[bf], pv); };
   stage_load(0);
   F32Pre<1, 32> qs;
   Q.own(qi, a.Sq, lane, qs);
@@ -835,7 +758,7 @@ __device__ __forceinline__ void attn_sp_fwd_body(const AttnF32Args& a) {
   }
   AST_T(tk2);
   const float inv = l > 0.f ? 1.0f / l : 0.f;
-  if (NW == 4 && a.ae16) {
+  if (a.ae16) {
     // row-coalesced stores through the (now free) K / V staging buffers: 4 x 8.5 KiB of 48 KiB
     float* img = (float*)(w < 2 ? &Ks[0][0] : &Vs[0][0]) + (w & 1) * AE_FLOATS;  // 2 x 8.5 of 24 KiB each
     ae_stage(img, o, lane, inv);
@@ -860,161 +783,25 @@ __device__ __forceinline__ void attn_sp_fwd_body(const AttnF32Args& a) {
   AST_ADD(7, tk0, tk3);  // wave lifetime
   AST_END();
 }
-// Forward on EIGHT waves (a whole head per workgroup at S = 256), staggered like the backward
-// kernels: X = S^T = K Q^T (24 MFMAs) of one wave pairs on its SIMD with the partner's Y = online
-// softmax, the P split and O^T += V^T P^T (~230 VALU + 24 MFMAs); group B stages every K / V chunk
-// (once per 256 queries).  Per-wave arithmetic and order are the 4-wave kernel's (bitwise-identical
-// O, LSE).
-template <int MODE, bool KPAD, bool PI>
-__global__ __launch_bounds__(512, 1) void attn_sp_fwd8s_kernel(AttnF32Args a) {
-  __shared__ __attribute__((aligned(16))) unsigned short Ks[2][AS_OP];
-  __shared__ __attribute__((aligned(16))) unsigned short Vs[2][AS_OP];
-  __shared__ __attribute__((aligned(16))) float epi[8][AE_FLOATS];
-  const int hh = blockIdx.y, b = blockIdx.z;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-  const int qwave = blockIdx.x * 256 + w * 32;
-  const int qi = qwave + (lane & 31);
-  const bool grpB = __builtin_amdgcn_readfirstlane(w) >= 4;
-  const int tb = tid & 255;
-  AS_SRC(Q, a.q, a.qpi, a.qi_ps, a.q_sb, a.q_sh, a.q_ss);
-  AS_SRC(K, a.k, a.kpi, a.kvi_ps, a.k_sb, a.k_sh, a.k_ss);
-  AS_SRC(V, a.v, a.vpi, a.kvi_ps, a.v_sb, a.v_sh, a.v_ss);
-  const unsigned char* kp = a.kpad ? a.kpad + (long)b * a.Sk : nullptr;
-  int kend = a.Sk;
-  if (MODE == 2) kend = min(a.Sk, blockIdx.x * 256 + 256);
-  const int nchunks = (kend + FCH - 1) / FCH;
-  typename AStageT<PI>::T pk, pv;
-  auto stage_load = [&](int c) { K.load(c * FCH, a.Sk, pk, tb); V.load(c * FCH, a.Sk, pv, tb); };
-  auto stage_store = [&](int bf) { as_store(Ks[bf], pk, tb); as_store(Vs[bf], pv, tb); };
-  if (grpB && nchunks) stage_load(0);
-  F32Pre<1, 32> qs;
-  Q.own(qi, a.Sq, lane, qs);
-  if (grpB && nchunks) {
-    stage_store(0);
-    if (nchunks > 1) stage_load(1);
-  }
-  __syncthreads();
-  float m = -INFINITY, l = 0.f;
-  f32x16_t o[2], s;
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) s[r] = 0.f;
-  const int nslots = nchunks ? 2 * nchunks + 1 : 0;
-  for (int t = 0; t < nslots; ++t) {
-    int cx = -1, cy = -1;
-    if (!grpB) { if ((t & 1) == 0) cx = t >> 1; else cy = t >> 1; }
-    else { if (t & 1) cx = t >> 1; else if (t > 0) cy = (t >> 1) - 1; }
-    if (cx >= nchunks) cx = -1;
-    if (cy >= nchunks) cy = -1;
-    if (cx >= 0) {  // X: S^T = K Q^T
-      const int buf = cx & 1, k0 = cx * FCH;
-      float ub;
-      const bool full = k0 + 32 <= a.Sk;
-      const bool uni = uniform_bias<MODE, KPAD, 32>(k0, qwave, qwave + 31, full, ub);
-      if (!(uni && ub == -INFINITY)) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s[r] = 0.f;
-        s = as_rows_dot(Ks[buf], lane, qs, s);
-      }
-    }
-    if (cy >= 0) {  // Y: online softmax, O^T += V^T P^T
-      const int buf = cy & 1, k0 = cy * FCH;
-      float ub;
-      const bool full = k0 + 32 <= a.Sk;
-      const bool uni = uniform_bias<MODE, KPAD, 32>(k0, qwave, qwave + 31, full, ub);
-      if (!(uni && ub == -INFINITY)) {
-        const unsigned long long kmask = KPAD ? chunk_pad_mask(kp, k0, a.Sk) : 0ull;
-        float cmax = -INFINITY;
-        if (uni) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) cmax = fmaxf(cmax, s[r]);
-          cmax = cmax * a.scale_log2 + ub;
-        } else {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int kl = fa_kl(r, h);
-            s[r] = score_adj<MODE, KPAD>(s[r], qi, k0 + kl, kl, full, a.Sk, kmask, a.scale_log2);
-            cmax = fmaxf(cmax, s[r]);
-          }
-        }
-        cmax = smi_row32_swap_max(cmax);
-        const float mnew = fmaxf(m, cmax);
-        const float mref = (mnew == -INFINITY) ? 0.f : mnew;
-        const float alpha = __builtin_amdgcn_exp2f(m - mref);
-        float psum = 0.f;
-        float pv16[16];
-        if (uni) {
-          const float off = ub - mref;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) { pv16[r] = __builtin_amdgcn_exp2f(fmaf(s[r], a.scale_log2, off)); psum += pv16[r]; }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) { pv16[r] = __builtin_amdgcn_exp2f(s[r] - mref); psum += pv16[r]; }
-        }
-        psum = smi_row32_swap_sum(psum);
-        l = l * alpha + psum;
-        m = mnew;
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) o[dt] *= alpha;
-        as_cols_acc(Vs[buf], lane, pv16, o);
-      }
-    }
-    if (grpB && (t & 1)) {
-      const int c = t >> 1;
-      if (c + 1 < nchunks) stage_store((c + 1) & 1);
-      if (c + 2 < nchunks) stage_load(c + 2);
-    }
-    __syncthreads();
-  }
-  const float inv = l > 0.f ? 1.0f / l : 0.f;
-  if (a.ae16) {
-    float* img = &epi[w][0];
-    ae_stage(img, o, lane, inv);
-    __syncthreads();
-    const long r0 = (long)b * a.o_sb + hh * a.o_sh + (long)qwave * a.o_ss;
-    ae_store(img, a.o + r0, a.op ? a.op + r0 : nullptr, a.o_ss, a.op_ps, a.Sq - qwave, lane);
-  } else if (qi < a.Sq) {
-    float* O = a.o + b * a.o_sb + hh * a.o_sh + (long)qi * a.o_ss;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) fa_store_rowT(O + dt * 32, o[dt], lane, inv);
-    if (a.op) {
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) fa_store_rowT_planes(a.op + (O - a.o) + dt * 32, a.op_ps, o[dt], lane, inv);
-    }
-  }
-  if (qi < a.Sq && h == 0) {
-    const float mref = (m == -INFINITY) ? 0.f : m;
-    a.lse[((long)b * a.H + hh) * a.Sq + qi] = l > 0.f ? mref + log2f(l) : INFINITY;
-  }
-}
 
-template <int MODE, bool KPAD, bool PI>
-__global__ __launch_bounds__(256, 2) void attn_sp_fwd4(AttnF32Args a) { attn_sp_fwd_body<MODE, KPAD, PI, 4>(a); }
-template <int MODE, bool KPAD, bool PI>
-__global__ __launch_bounds__(512, 1) void attn_sp_fwd8(AttnF32Args a) { attn_sp_fwd_body<MODE, KPAD, PI, 8>(a); }
-
-template <int MODE, bool KPAD, bool PI>
+template <int MODE, bool KPAD>
 __global__ __launch_bounds__(256, 2) void attn_sp_dq_kernel(AttnF32Args a) {
   __shared__ __attribute__((aligned(16))) unsigned short Ks[2][AS_OP];
   __shared__ __attribute__((aligned(16))) unsigned short Vs[2][AS_OP];
-  fa_skew(a);
   const int hh = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
   const int qwave = blockIdx.x * 128 + w * 32;
   const int qi = qwave + (lane & 31);
-  AS_SRC(Q, a.q, a.qpi, a.qi_ps, a.q_sb, a.q_sh, a.q_ss);
-  AS_SRC(K, a.k, a.kpi, a.kvi_ps, a.k_sb, a.k_sh, a.k_ss);
-  AS_SRC(V, a.v, a.vpi, a.kvi_ps, a.v_sb, a.v_sh, a.v_ss);
-  AS_SRC(dO, a.dout, a.dopi, a.doi_ps, a.o_sb, a.o_sh, a.o_ss);
+  AS_SRC(Q, a.q, a.q_sb, a.q_sh, a.q_ss);
+  AS_SRC(K, a.k, a.k_sb, a.k_sh, a.k_ss);
+  AS_SRC(V, a.v, a.v_sb, a.v_sh, a.v_ss);
+  AS_SRC(dO, a.dout, a.o_sb, a.o_sh, a.o_ss);
   const float* Og = a.o + b * a.o_sb + hh * a.o_sh;
   const unsigned char* kp = a.kpad ? a.kpad + (long)b * a.Sk : nullptr;
   int kend = a.Sk;
   if (MODE == 2) kend = min(a.Sk, blockIdx.x * 128 + 128);
   const int nchunks = (kend + FCH - 1) / FCH;
-  typename AStageT<PI>::T pk, pv;
+  AStage pk, pv;
   K.load(0, a.Sk, pk);
   V.load(0, a.Sk, pv);
   F32Pre<1, 32> qs, ds;
@@ -1023,7 +810,7 @@ __global__ __launch_bounds__(256, 2) void attn_sp_dq_kernel(AttnF32Args a) {
     float df[32], of[32];
     Q.own(qi, a.Sq, lane, qs);
     dO.own(qi, a.Sq, lane, ds);
-    dO.own_f32(ds, qi, a.Sq, lane, df);
+    dO.own_f32(qi, a.Sq, lane, df);
     fa_ownrow(Og, a.o_ss, qi, a.Sq, lane, of);
     float sacc = 0.f;
 #pragma unroll
@@ -1096,239 +883,6 @@ __global__ __launch_bounds__(256, 2) void attn_sp_dq_kernel(AttnF32Args a) {
   }
 }
 
-// dQ on EIGHT waves (256 queries: a whole head at S = 256), staggered like attn_sp_dkdv8s_kernel:
-// each staged K / V chunk serves 256 queries (the 4-wave kernel stages it twice per head), and the
-// two half-workgroups run half a chunk apart so one wave's X segment (S^T = K Q^T, dP^T = V dO^T:
-// 48 MFMAs) pairs on its SIMD with the partner's Y segment (the dS values, their split and
-// dQ^T += K^T dS^T: ~150 VALU + 24 MFMAs).  Group B stages both operands of every chunk.  Per-wave
-// arithmetic and order are the 4-wave kernel's (bitwise-identical dQ, delta).
-template <int MODE, bool KPAD, bool PI>
-__global__ __launch_bounds__(512, 1) void attn_sp_dq8s_kernel(AttnF32Args a) {
-  __shared__ __attribute__((aligned(16))) unsigned short Ks[2][AS_OP];
-  __shared__ __attribute__((aligned(16))) unsigned short Vs[2][AS_OP];
-  __shared__ __attribute__((aligned(16))) float epi[8][AE_FLOATS];
-  const int hh = blockIdx.y, b = blockIdx.z;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-  const int qwave = blockIdx.x * 256 + w * 32;
-  const int qi = qwave + (lane & 31);
-  const bool grpB = __builtin_amdgcn_readfirstlane(w) >= 4;
-  const int tb = tid & 255;
-  AS_SRC(Q, a.q, a.qpi, a.qi_ps, a.q_sb, a.q_sh, a.q_ss);
-  AS_SRC(K, a.k, a.kpi, a.kvi_ps, a.k_sb, a.k_sh, a.k_ss);
-  AS_SRC(V, a.v, a.vpi, a.kvi_ps, a.v_sb, a.v_sh, a.v_ss);
-  AS_SRC(dO, a.dout, a.dopi, a.doi_ps, a.o_sb, a.o_sh, a.o_ss);
-  const float* Og = a.o + b * a.o_sb + hh * a.o_sh;
-  const unsigned char* kp = a.kpad ? a.kpad + (long)b * a.Sk : nullptr;
-  int kend = a.Sk;
-  if (MODE == 2) kend = min(a.Sk, blockIdx.x * 256 + 256);
-  const int nchunks = (kend + FCH - 1) / FCH;
-  typename AStageT<PI>::T pk, pv;
-  auto stage_load = [&](int c) { K.load(c * FCH, a.Sk, pk, tb); V.load(c * FCH, a.Sk, pv, tb); };
-  auto stage_store = [&](int bf) { as_store(Ks[bf], pk, tb); as_store(Vs[bf], pv, tb); };
-  if (grpB && nchunks) stage_load(0);
-  F32Pre<1, 32> qs, ds;
-  float dl;
-  {
-    float df[32], of[32];
-    Q.own(qi, a.Sq, lane, qs);
-    dO.own(qi, a.Sq, lane, ds);
-    dO.own_f32(ds, qi, a.Sq, lane, df);
-    fa_ownrow(Og, a.o_ss, qi, a.Sq, lane, of);
-    float sacc = 0.f;
-#pragma unroll
-    for (int t = 0; t < 32; ++t) sacc = fmaf(df[t], of[t], sacc);
-    dl = smi_row32_swap_sum(sacc);
-  }
-  const long rbase = ((long)b * a.H + hh) * a.Sq;
-  if (h == 0 && qi < a.Sq) a.delta[rbase + qi] = dl;
-  const float lse = qi < a.Sq ? a.lse[rbase + qi] : INFINITY;
-  if (grpB && nchunks) {
-    stage_store(0);
-    if (nchunks > 1) stage_load(1);
-  }
-  __syncthreads();
-  f32x16_t acc[2], s, dp;
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[dt][r] = 0.f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
-  const int nslots = nchunks ? 2 * nchunks + 1 : 0;
-  for (int t = 0; t < nslots; ++t) {
-    int cx = -1, cy = -1;
-    if (!grpB) { if ((t & 1) == 0) cx = t >> 1; else cy = t >> 1; }
-    else { if (t & 1) cx = t >> 1; else if (t > 0) cy = (t >> 1) - 1; }
-    if (cx >= nchunks) cx = -1;
-    if (cy >= nchunks) cy = -1;
-    if (cx >= 0) {  // X: S^T = K Q^T, dP^T = V dO^T
-      const int buf = cx & 1, k0 = cx * FCH;
-      float ub;
-      const bool full = k0 + 32 <= a.Sk;
-      const bool uni = uniform_bias<MODE, KPAD, 32>(k0, qwave, qwave + 31, full, ub);
-      if (!(uni && ub == -INFINITY)) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
-        s = as_rows_dot(Ks[buf], lane, qs, s);
-        dp = as_rows_dot(Vs[buf], lane, ds, dp);
-      }
-    }
-    if (cy >= 0) {  // Y: dS, dQ^T += K^T dS^T
-      const int buf = cy & 1, k0 = cy * FCH;
-      float ub;
-      const bool full = k0 + 32 <= a.Sk;
-      const bool uni = uniform_bias<MODE, KPAD, 32>(k0, qwave, qwave + 31, full, ub);
-      if (!(uni && ub == -INFINITY)) {
-        const unsigned long long kmask = KPAD ? chunk_pad_mask(kp, k0, a.Sk) : 0ull;
-        float dsv[16];
-        if (uni) {
-          const float off = ub - lse;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) dsv[r] = __builtin_amdgcn_exp2f(fmaf(s[r], a.scale_log2, off)) * (dp[r] - dl);
-        } else {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int kl = fa_kl(r, h);
-            const float x = score_adj<MODE, KPAD>(s[r], qi, k0 + kl, kl, full, a.Sk, kmask, a.scale_log2);
-            dsv[r] = __builtin_amdgcn_exp2f(x - lse) * (dp[r] - dl);
-          }
-        }
-        as_cols_acc(Ks[buf], lane, dsv, acc);
-      }
-    }
-    if (grpB && (t & 1)) {
-      const int c = t >> 1;
-      if (c + 1 < nchunks) stage_store((c + 1) & 1);
-      if (c + 2 < nchunks) stage_load(c + 2);
-    }
-    __syncthreads();
-  }
-  if (a.ae16) {
-    float* img = &epi[w][0];
-    ae_stage(img, acc, lane, a.scale);
-    __syncthreads();
-    const long r0 = (long)b * a.q_sb + hh * a.q_sh + (long)qwave * a.q_ss;
-    ae_store(img, a.no_f32_grad ? nullptr : a.dq + r0, a.dqp ? a.dqp + r0 : nullptr, a.q_ss, a.dq_ps, a.Sq - qwave,
-             lane);
-  } else if (qi < a.Sq) {
-    float* dQ = a.dq + b * a.q_sb + hh * a.q_sh + (long)qi * a.q_ss;
-    if (!a.no_f32_grad) {
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) fa_store_rowT(dQ + dt * 32, acc[dt], lane, a.scale);
-    }
-    if (a.dqp) {
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) fa_store_rowT_planes(a.dqp + (dQ - a.dq) + dt * 32, a.dq_ps, acc[dt], lane, a.scale);
-    }
-  }
-}
-
-// one workgroup per CU: owned K and V splits (96 registers) + two accumulator pairs + the P / dS
-// splits exceed 256 registers (two workgroups per CU spilled 34)
-template <int MODE, bool KPAD, bool PI>
-__global__ __launch_bounds__(256, 1) void attn_sp_dkdv_kernel(AttnF32Args a) {
-  __shared__ __attribute__((aligned(16))) unsigned short Qs[2][AS_OP];
-  __shared__ __attribute__((aligned(16))) unsigned short Ds[2][AS_OP];
-  __shared__ float lse_s[2][FCH], dl_s[2][FCH];
-  const int hh = blockIdx.y, b = blockIdx.z;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
-  const int kwave = blockIdx.x * 128 + w * 32;
-  const int kj = kwave + (lane & 31);
-  AS_SRC(Q, a.q, a.qpi, a.qi_ps, a.q_sb, a.q_sh, a.q_ss);
-  AS_SRC(K, a.k, a.kpi, a.kvi_ps, a.k_sb, a.k_sh, a.k_ss);
-  AS_SRC(V, a.v, a.vpi, a.kvi_ps, a.v_sb, a.v_sh, a.v_ss);
-  AS_SRC(dO, a.dout, a.dopi, a.doi_ps, a.o_sb, a.o_sh, a.o_ss);
-  const long rbase = ((long)b * a.H + hh) * a.Sq;
-  int qstart = 0;
-  if (MODE == 2) qstart = (blockIdx.x * 128) & ~(FCH - 1);
-  const int nchunks = qstart < a.Sq ? (a.Sq - qstart + FCH - 1) / FCH : 0;
-  typename AStageT<PI>::T pq, pd;
-  float lse_r = INFINITY, dl_r = 0.f;
-  if (nchunks) {
-    Q.load(qstart, a.Sq, pq);
-    dO.load(qstart, a.Sq, pd);
-    if (threadIdx.x < FCH && qstart + (int)threadIdx.x < a.Sq) {
-      lse_r = a.lse[rbase + qstart + threadIdx.x];
-      dl_r = a.delta[rbase + qstart + threadIdx.x];
-    }
-  }
-  F32Pre<1, 32> ks, vs;
-  K.own(kj, a.Sk, lane, ks);
-  V.own(kj, a.Sk, lane, vs);
-  const bool kok = kj < a.Sk && !(KPAD && a.kpad[(long)b * a.Sk + kj]);
-  const float kbias = kok ? 0.f : -INFINITY;
-  f32x16_t dk[2], dv[2];
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
-  if (nchunks) {
-    as_store(Qs[0], pq);
-    as_store(Ds[0], pd);
-    if (threadIdx.x < FCH) { lse_s[0][threadIdx.x] = lse_r; dl_s[0][threadIdx.x] = dl_r; }
-  }
-  __syncthreads();
-  for (int c = 0; c < nchunks; ++c) {
-    const int buf = c & 1, q0 = qstart + c * FCH;
-    const bool more = c + 1 < nchunks;
-    if (more) {
-      Q.load(q0 + FCH, a.Sq, pq);
-      dO.load(q0 + FCH, a.Sq, pd);
-      lse_r = INFINITY; dl_r = 0.f;
-      if (threadIdx.x < FCH && q0 + FCH + (int)threadIdx.x < a.Sq) {
-        lse_r = a.lse[rbase + q0 + FCH + threadIdx.x];
-        dl_r = a.delta[rbase + q0 + FCH + threadIdx.x];
-      }
-    }
-    do {
-      if (MODE == 2 && q0 + 31 < kwave) break;  // every query of the block before every key
-      f32x16_t s, dp;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
-      s = as_rows_dot(Qs[buf], lane, ks, s);   // S = Q K^T: query rows, key on the lane
-      dp = as_rows_dot(Ds[buf], lane, vs, dp);  // dP = dO V^T
-      float pvv[16], dsv[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ql = fa_kl(r, h);
-        const int qq = q0 + ql;
-        float x = fmaf(s[r], a.scale_log2, kbias);
-        if (MODE == 1) x += (kj < qq) ? LOG2E_F : 0.f;
-        if (MODE == 2) x = (kj > qq) ? -INFINITY : x;
-        const float pr = __builtin_amdgcn_exp2f(x - lse_s[buf][ql]);  // rows past Sq: lse = +inf -> 0
-        pvv[r] = pr;
-        dsv[r] = pr * (dp[r] - dl_s[buf][ql]);
-      }
-      as_cols_acc(Ds[buf], lane, pvv, dv);  // dV^T += dO^T P
-      as_cols_acc(Qs[buf], lane, dsv, dk);  // dK^T += Q^T dS
-    } while (0);
-    if (more) {
-      as_store(Qs[buf ^ 1], pq);
-      as_store(Ds[buf ^ 1], pd);
-      if (threadIdx.x < FCH) { lse_s[buf ^ 1][threadIdx.x] = lse_r; dl_s[buf ^ 1][threadIdx.x] = dl_r; }
-    }
-    __syncthreads();
-  }
-  if (kj < a.Sk) {
-    float* dK = a.dk + b * a.k_sb + hh * a.k_sh + (long)kj * a.k_ss;
-    float* dV = a.dv + b * a.v_sb + hh * a.v_sh + (long)kj * a.v_ss;
-    if (!a.no_f32_grad) {
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        fa_store_rowT(dK + dt * 32, dk[dt], lane, a.scale);
-        fa_store_rowT(dV + dt * 32, dv[dt], lane, 1.0f);
-      }
-    }
-    if (a.dkp) {
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        fa_store_rowT_planes(a.dkp + (dK - a.dk) + dt * 32, a.dkv_ps, dk[dt], lane, a.scale);
-        fa_store_rowT_planes(a.dvp + (dV - a.dv) + dt * 32, a.dkv_ps, dv[dt], lane, 1.0f);
-      }
-    }
-  }
-}
-
 // dK / dV with EIGHT waves per workgroup (256 keys: a whole head at S = 256), two waves per SIMD.
 // The 4-wave kernel above needs > 256 registers per lane (owned K and V splits, dK / dV
 // accumulators, P / dS splits), so it runs one wave per SIMD with every LDS / MFMA / exp latency
@@ -1338,7 +892,7 @@ __global__ __launch_bounds__(256, 1) void attn_sp_dkdv_kernel(AttnF32Args a) {
 // staged Q / dO chunk serves 256 keys instead of 128 (threads 0-255 stage Q, 256-511 dO).
 // LDS: 2 x 2 x 12 KiB staging + 8 x 12 KiB owned V = 144 KiB.
 #define AS_DKDV8_KEYS 256
-template <int MODE, bool KPAD, bool PI>
+template <int MODE, bool KPAD>
 __global__ __launch_bounds__(512, 1) void attn_sp_dkdv8_kernel(AttnF32Args a) {
   __shared__ __attribute__((aligned(16))) unsigned short Qs[2][AS_OP];
   __shared__ __attribute__((aligned(16))) unsigned short Ds[2][AS_OP];
@@ -1351,16 +905,16 @@ __global__ __launch_bounds__(512, 1) void attn_sp_dkdv8_kernel(AttnF32Args a) {
   const int kj = kwave + (lane & 31);
   const bool stq = tid < 256;  // this thread stages Q (waves 0-3) or dO (waves 4-7)
   const int ti = tid & 255;
-  AS_SRC(Q, a.q, a.qpi, a.qi_ps, a.q_sb, a.q_sh, a.q_ss);
-  AS_SRC(K, a.k, a.kpi, a.kvi_ps, a.k_sb, a.k_sh, a.k_ss);
-  AS_SRC(V, a.v, a.vpi, a.kvi_ps, a.v_sb, a.v_sh, a.v_ss);
-  AS_SRC(dO, a.dout, a.dopi, a.doi_ps, a.o_sb, a.o_sh, a.o_ss);
-  const AsSrc<PI>& SQ = stq ? Q : dO;
+  AS_SRC(Q, a.q, a.q_sb, a.q_sh, a.q_ss);
+  AS_SRC(K, a.k, a.k_sb, a.k_sh, a.k_ss);
+  AS_SRC(V, a.v, a.v_sb, a.v_sh, a.v_ss);
+  AS_SRC(dO, a.dout, a.o_sb, a.o_sh, a.o_ss);
+  const AsSrc& SQ = stq ? Q : dO;
   const long rbase = ((long)b * a.H + hh) * a.Sq;
   int qstart = 0;
   if (MODE == 2) qstart = kb0 & ~(FCH - 1);
   const int nchunks = qstart < a.Sq ? (a.Sq - qstart + FCH - 1) / FCH : 0;
-  typename AStageT<PI>::T ps;
+  AStage ps;
   float lse_r = INFINITY, dl_r = 0.f;
   if (nchunks) {
     SQ.load(qstart, a.Sq, ps, ti);
@@ -1373,7 +927,7 @@ __global__ __launch_bounds__(512, 1) void attn_sp_dkdv8_kernel(AttnF32Args a) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int idx = tid + 512 * i, blk = idx >> 8;
-    typename AStageT<PI>::T pv;
+    AStage pv;
     V.load(kb0 + 32 * blk, a.Sk, pv, idx & 255);
     as_store(Vo[blk], pv, idx & 255);
   }
@@ -1467,236 +1021,24 @@ __global__ __launch_bounds__(512, 1) void attn_sp_dkdv8_kernel(AttnF32Args a) {
   }
 }
 
-// dK / dV, 8 waves, STAGGERED: the two halves of the workgroup (waves 0-3 = A, 4-7 = B; each
-// SIMD hosts one wave of each) run half a chunk apart, so on every SIMD one wave's pure-MFMA
-// segment X (S = Q K^T and dP = dO V^T: 48 MFMAs) pairs with its partner's VALU-heavy segment Y
-// (P, dS, their splits, then dV^T += dO^T P and dK^T += Q^T dS: ~300 VALU + 48 MFMAs).  In the
-// lockstep kernel above both waves of a SIMD reach their softmax VALU together and the matrix
-// pipe idles for it once per chunk.  Slot t: A runs X(t/2) (t even) or Y((t-1)/2); B runs
-// X((t-1)/2) (t odd) or Y(t/2 - 1); one barrier per slot.  Chunk c lives in buffer c & 1 from
-// slot 2c to 2c + 2; chunk c + 1 is written by B in slot 2c + 1 into the buffer chunk c - 1
-// left (its last reader, B's Y(c - 1), ended with slot 2c), its global loads issued one slot
-// earlier.  Per-wave arithmetic and its order are the lockstep kernel's (bitwise-identical).
-template <int MODE, bool KPAD, bool PI>
-__global__ __launch_bounds__(512, 1) void attn_sp_dkdv8s_kernel(AttnF32Args a) {
-  __shared__ __attribute__((aligned(16))) unsigned short Qs[2][AS_OP];
-  __shared__ __attribute__((aligned(16))) unsigned short Ds[2][AS_OP];
-  __shared__ __attribute__((aligned(16))) unsigned short Vo[8][AS_OP];
-  __shared__ float lse_s[2][FCH], dl_s[2][FCH];
-  const int hh = blockIdx.y, b = blockIdx.z;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-  const int kb0 = blockIdx.x * AS_DKDV8_KEYS;
-  const int kwave = kb0 + w * 32;
-  const int kj = kwave + (lane & 31);
-  const bool grpB = __builtin_amdgcn_readfirstlane(w) >= 4;  // wave-uniform: the late half, and the stager
-  const int tb = tid & 255;
-  AS_SRC(Q, a.q, a.qpi, a.qi_ps, a.q_sb, a.q_sh, a.q_ss);
-  AS_SRC(K, a.k, a.kpi, a.kvi_ps, a.k_sb, a.k_sh, a.k_ss);
-  AS_SRC(V, a.v, a.vpi, a.kvi_ps, a.v_sb, a.v_sh, a.v_ss);
-  AS_SRC(dO, a.dout, a.dopi, a.doi_ps, a.o_sb, a.o_sh, a.o_ss);
-  const long rbase = ((long)b * a.H + hh) * a.Sq;
-  int qstart = 0;
-  if (MODE == 2) qstart = kb0 & ~(FCH - 1);
-  const int nchunks = qstart < a.Sq ? (a.Sq - qstart + FCH - 1) / FCH : 0;
-  typename AStageT<PI>::T pq, pd;
-  float lse_r = INFINITY, dl_r = 0.f;
-  // group B stages both operands of a chunk: 8 values of Q and 8 of dO per thread
-  auto stage_load = [&](int c) {
-    const int q0 = qstart + c * FCH;
-    Q.load(q0, a.Sq, pq, tb);
-    dO.load(q0, a.Sq, pd, tb);
-    lse_r = INFINITY; dl_r = 0.f;
-    if (tb < FCH && q0 + tb < a.Sq) {
-      lse_r = a.lse[rbase + q0 + tb];
-      dl_r = a.delta[rbase + q0 + tb];
-    }
-  };
-  auto stage_store = [&](int bf) {
-    as_store(Qs[bf], pq, tb);
-    as_store(Ds[bf], pd, tb);
-    if (tb < FCH) { lse_s[bf][tb] = lse_r; dl_s[bf][tb] = dl_r; }
-  };
-  if (grpB && nchunks) stage_load(0);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int idx = tid + 512 * i, blk = idx >> 8;
-    typename AStageT<PI>::T pv;
-    V.load(kb0 + 32 * blk, a.Sk, pv, idx & 255);
-    as_store(Vo[blk], pv, idx & 255);
-  }
-  F32Pre<1, 32> ks;
-  K.own(kj, a.Sk, lane, ks);
-  const bool kok = kj < a.Sk && !(KPAD && a.kpad[(long)b * a.Sk + kj]);
-  const float kbias = kok ? 0.f : -INFINITY;
-  f32x16_t dk[2], dv[2], s, dp;
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
-  if (grpB && nchunks) {
-    stage_store(0);
-    if (nchunks > 1) stage_load(1);
-  }
-  __syncthreads();
-  const unsigned short* vimg = Vo[w];
-  const int nslots = nchunks ? 2 * nchunks + 1 : 0;
-  for (int t = 0; t < nslots; ++t) {
-    int cx = -1, cy = -1;
-    if (!grpB) { if ((t & 1) == 0) cx = t >> 1; else cy = t >> 1; }
-    else { if (t & 1) cx = t >> 1; else if (t > 0) cy = (t >> 1) - 1; }
-    if (cx >= nchunks) cx = -1;
-    if (cy >= nchunks) cy = -1;
-    if (cx >= 0) {  // X: S = Q K^T, dP = dO V^T
-      const int buf = cx & 1, q0 = qstart + cx * FCH;
-      if (!(MODE == 2 && q0 + 31 < kwave)) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
-        s = as_rows_dot(Qs[buf], lane, ks, s);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) dp = as_mma(as_rowfrag(Ds[buf], lane, j), as_rowfrag(vimg, lane, j), dp);
-      }
-    }
-    if (cy >= 0) {  // Y: P, dS, dV^T += dO^T P, dK^T += Q^T dS
-      const int buf = cy & 1, q0 = qstart + cy * FCH;
-      if (!(MODE == 2 && q0 + 31 < kwave)) {
-        float pvv[16], dsv[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int ql = fa_kl(r, h);
-          const int qq = q0 + ql;
-          float x = fmaf(s[r], a.scale_log2, kbias);
-          if (MODE == 1) x += (kj < qq) ? LOG2E_F : 0.f;
-          if (MODE == 2) x = (kj > qq) ? -INFINITY : x;
-          const float pr = __builtin_amdgcn_exp2f(x - lse_s[buf][ql]);
-          pvv[r] = pr;
-          dsv[r] = pr * (dp[r] - dl_s[buf][ql]);
-        }
-        as_cols_acc(Ds[buf], lane, pvv, dv);
-        as_cols_acc(Qs[buf], lane, dsv, dk);
-      }
-    }
-    if (grpB && (t & 1)) {  // slot 2c + 1: chunk c + 1 into the buffer chunk c - 1 left, loads of c + 2
-      const int c = t >> 1;
-      if (c + 1 < nchunks) stage_store((c + 1) & 1);
-      if (c + 2 < nchunks) stage_load(c + 2);
-    }
-    __syncthreads();
-  }
-  if (a.ae16) {
-    float* img = (float*)&Vo[w][0];
-    ae_stage(img, dk, lane, a.scale);
-    __syncthreads();
-    const long rk = (long)b * a.k_sb + hh * a.k_sh + (long)kwave * a.k_ss;
-    const long rv = (long)b * a.v_sb + hh * a.v_sh + (long)kwave * a.v_ss;
-    ae_store(img, a.no_f32_grad ? nullptr : a.dk + rk, a.dkp ? a.dkp + rk : nullptr, a.k_ss, a.dkv_ps, a.Sk - kwave,
-             lane);
-    __syncthreads();
-    ae_stage(img, dv, lane, 1.0f);
-    __syncthreads();
-    ae_store(img, a.no_f32_grad ? nullptr : a.dv + rv, a.dvp ? a.dvp + rv : nullptr, a.v_ss, a.dkv_ps, a.Sk - kwave,
-             lane);
-  } else if (kj < a.Sk) {
-    float* dK = a.dk + b * a.k_sb + hh * a.k_sh + (long)kj * a.k_ss;
-    float* dV = a.dv + b * a.v_sb + hh * a.v_sh + (long)kj * a.v_ss;
-    if (!a.no_f32_grad) {
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        fa_store_rowT(dK + dt * 32, dk[dt], lane, a.scale);
-        fa_store_rowT(dV + dt * 32, dv[dt], lane, 1.0f);
-      }
-    }
-    if (a.dkp) {
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        fa_store_rowT_planes(a.dkp + (dK - a.dk) + dt * 32, a.dkv_ps, dk[dt], lane, a.scale);
-        fa_store_rowT_planes(a.dvp + (dV - a.dv) + dt * 32, a.dkv_ps, dv[dt], lane, 1.0f);
-      }
-    }
-  }
-}
-
-// SMI_ATTN_STAGGER=1: the staggered 8-wave dQ and dK/dV kernels (bitwise the same results; measured
-// no faster than the 4-wave dQ + lockstep 8-wave dK/dV pair, tools/ab_attn.py — opt-in)
-static int g_attn_stagger = -1;
-extern "C" int smi_attn_stagger(int set) {
-  if (set == 0 || set == 1) g_attn_stagger = set;
-  if (g_attn_stagger < 0) {
-    const char* e = getenv("SMI_ATTN_STAGGER");
-    g_attn_stagger = (e && e[0] == '1') ? 1 : 0;
-  }
-  return g_attn_stagger;
-}
-
-static int g_attn_dkdv8 = -1;  // SMI_ATTN_DKDV8=0: the 4-wave dK/dV kernel
-extern "C" int smi_attn_dkdv8(int set) {
-  if (set == 0 || set == 1) g_attn_dkdv8 = set;
-  if (g_attn_dkdv8 < 0) {
-    const char* e = getenv("SMI_ATTN_DKDV8");
-    g_attn_dkdv8 = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_attn_dkdv8;
-}
-
-// forward on 4-wave workgroups (default) / 8-wave (SMI_ATTN_FWD8=1): -3 us per call on one box,
-// +2..5 us on another (tools/probes/attn_fwd_probe.hip) — opt-in
-static int g_attn_fwd8 = -1;
-extern "C" int smi_attn_fwd8(int set) {
-  if (set == 0 || set == 1) g_attn_fwd8 = set;
-  if (g_attn_fwd8 < 0) {
-    const char* e = getenv("SMI_ATTN_FWD8");
-    g_attn_fwd8 = (e && e[0] == '1') ? 1 : 0;
-  }
-  return g_attn_fwd8;
-}
-
-// staged-plane kernels on (default) / off (SMI_ATTN_SP=0: the XS kernels above)
-static int g_attn_sp = -1;
-extern "C" int smi_attn_f32_sp(int set) {
-  if (set == 0 || set == 1) g_attn_sp = set;
-  if (g_attn_sp < 0) {
-    const char* e = getenv("SMI_ATTN_SP");
-    g_attn_sp = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_attn_sp;
-}
-#define SMI_ATTN_SP_PI(KERNEL, PI, GRID, ARGS)                                                           \
-  switch ((ARGS).mode) {                                                                                 \
-    case 0: if (kp_) hipLaunchKernelGGL((KERNEL<0, true, PI>), GRID, dim3(256), 0, st, ARGS);            \
-            else hipLaunchKernelGGL((KERNEL<0, false, PI>), GRID, dim3(256), 0, st, ARGS); break;        \
-    case 1: if (kp_) hipLaunchKernelGGL((KERNEL<1, true, PI>), GRID, dim3(256), 0, st, ARGS);            \
-            else hipLaunchKernelGGL((KERNEL<1, false, PI>), GRID, dim3(256), 0, st, ARGS); break;        \
-    case 2: if (kp_) hipLaunchKernelGGL((KERNEL<2, true, PI>), GRID, dim3(256), 0, st, ARGS);            \
-            else hipLaunchKernelGGL((KERNEL<2, false, PI>), GRID, dim3(256), 0, st, ARGS); break;        \
-    default: return -1;                                                                                  \
-  }
-#define SMI_ATTN_SP_PI8(KERNEL, PI, GRID, ARGS)                                                          \
-  switch ((ARGS).mode) {                                                                                 \
-    case 0: if (kp_) hipLaunchKernelGGL((KERNEL<0, true, PI>), GRID, dim3(512), 0, st, ARGS);            \
-            else hipLaunchKernelGGL((KERNEL<0, false, PI>), GRID, dim3(512), 0, st, ARGS); break;        \
-    case 1: if (kp_) hipLaunchKernelGGL((KERNEL<1, true, PI>), GRID, dim3(512), 0, st, ARGS);            \
-            else hipLaunchKernelGGL((KERNEL<1, false, PI>), GRID, dim3(512), 0, st, ARGS); break;        \
-    case 2: if (kp_) hipLaunchKernelGGL((KERNEL<2, true, PI>), GRID, dim3(512), 0, st, ARGS);            \
-            else hipLaunchKernelGGL((KERNEL<2, false, PI>), GRID, dim3(512), 0, st, ARGS); break;        \
-    default: return -1;                                                                                  \
-  }
-#define SMI_ATTN_SP_MODES8(KERNEL, GRID, ARGS, PI_)                                                      \
+// Launch over the compile-time (mask mode, key padding) instances of a kernel, NT threads
+#define SMI_ATTN_SP_MODES(KERNEL, GRID, NT, ARGS)                                                        \
   do {                                                                                                   \
     const bool kp_ = (ARGS).kpad != nullptr;                                                             \
-    if (PI_) { SMI_ATTN_SP_PI8(KERNEL, true, GRID, ARGS) }                                               \
-    else { SMI_ATTN_SP_PI8(KERNEL, false, GRID, ARGS) }                                                  \
-  } while (0)
-// PI_: the inputs' planes are present (every operand the kernel reads: see fa_pi)
-#define SMI_ATTN_SP_MODES(KERNEL, GRID, ARGS, PI_)                                                       \
-  do {                                                                                                   \
-    const bool kp_ = (ARGS).kpad != nullptr;                                                             \
-    if (PI_) { SMI_ATTN_SP_PI(KERNEL, true, GRID, ARGS) }                                                \
-    else { SMI_ATTN_SP_PI(KERNEL, false, GRID, ARGS) }                                                   \
+    switch ((ARGS).mode) {                                                                               \
+      case 0: if (kp_) hipLaunchKernelGGL((KERNEL<0, true>), GRID, dim3(NT), 0, st, ARGS);               \
+              else hipLaunchKernelGGL((KERNEL<0, false>), GRID, dim3(NT), 0, st, ARGS); break;           \
+      case 1: if (kp_) hipLaunchKernelGGL((KERNEL<1, true>), GRID, dim3(NT), 0, st, ARGS);               \
+              else hipLaunchKernelGGL((KERNEL<1, false>), GRID, dim3(NT), 0, st, ARGS); break;           \
+      case 2: if (kp_) hipLaunchKernelGGL((KERNEL<2, true>), GRID, dim3(NT), 0, st, ARGS);               \
+              else hipLaunchKernelGGL((KERNEL<2, false>), GRID, dim3(NT), 0, st, ARGS); break;           \
+      default: return -1;                                                                                \
+    }                                                                                                    \
   } while (0)
 
 // product algorithm shared with the fp32 GEMM (csrc/kernels/gemm_f32.hip:smi_gemm_f32_algo):
-// 0 = f32 MFMA chains, otherwise the exact-product bf16 split (smi_split3.h)
+// 0 = f32 MFMA chains (the XS = 0 kernels above), otherwise the exact-product bf16 split: the
+// staged-plane kernels
 extern "C" int smi_gemm_f32_algo(int);
 #define SMI_ATTN_F32_MODES(KERNEL, XSV, GRID, ARGS)                                                        \
   switch ((ARGS).mode) {                                                                                   \
@@ -1715,19 +1057,6 @@ extern "C" int smi_gemm_f32_algo(int);
     else { SMI_ATTN_F32_MODES(KERNEL, 1, GRID, ARGS) }                                                     \
   } while (0)
 
-extern "C" int smi_attn_stagger(int);
-
-// the staggered 8-wave forward (SMI_ATTN_FWD_STAGGER=1; default off until measured)
-static int g_attn_fwd_stagger = -1;
-extern "C" int smi_attn_fwd_stagger(int set) {
-  if (set == 0 || set == 1) g_attn_fwd_stagger = set;
-  if (g_attn_fwd_stagger < 0) {
-    const char* e = getenv("SMI_ATTN_FWD_STAGGER");
-    g_attn_fwd_stagger = (e && e[0] == '1') ? 1 : 0;
-  }
-  return g_attn_fwd_stagger;
-}
-
 static int fa_ok(const AttnF32Args& a) {
   // float4 access to every row: 16-B aligned bases and strides that are multiples of 4 floats
   const long st[] = {a.q_ss, a.k_ss, a.v_ss, a.o_ss, a.q_sh, a.k_sh, a.v_sh, a.o_sh, a.q_sb, a.k_sb, a.v_sb, a.o_sb};
@@ -1740,23 +1069,19 @@ static int fa_ok(const AttnF32Args& a) {
   return a.B > 0 && a.H > 0 && a.Sq > 0 && a.Sk > 0;
 }
 
-// input planes usable: all of Q / K / V (and dO for the backward) present, 16-B aligned rows
-static bool fa_pi(const AttnF32Args& a, bool bwd) {
-  if (!a.qpi || !a.kpi || !a.vpi || (bwd && !a.dopi)) return false;
-  const uintptr_t al = (uintptr_t)a.qpi | (uintptr_t)a.kpi | (uintptr_t)a.vpi | (bwd ? (uintptr_t)a.dopi : 0);
-  const long st[] = {a.q_ss, a.k_ss, a.v_ss, a.q_sh, a.k_sh, a.v_sh, a.q_sb, a.k_sb, a.v_sb, a.qi_ps, a.kvi_ps,
-                     bwd ? a.o_ss : 0, bwd ? a.o_sh : 0, bwd ? a.o_sb : 0, bwd ? a.doi_ps : 0};
-  for (long s : st)
-    if (s % 8) return false;
-  return (al & 15) == 0;
-}
-
 // whole-row 16-B stores of an output (fp32: float4 rows, already required by fa_ok) and of its
 // planes (8 bf16 per store): 16-B plane base and strides that are multiples of 8 elements
 static bool fa_ae16(const unsigned short* p, long sb, long sh, long ss) {
   return !p || ((((uintptr_t)p) & 15) == 0 && sb % 8 == 0 && sh % 8 == 0 && ss % 8 == 0);
 }
-static int g_attn_ae = -1;  // SMI_ATTN_AE=0: the per-lane transposed stores
+// The row-coalesced epilogue (ae_stage / ae_store) of all three staged-plane kernels; the one A/B
+// switch of this file: SMI_ATTN_AE=0 selects the per-lane transposed stores (also taken whenever an
+// output's alignment rules the 16-B row stores out).  In isolation (tools/ab_attn.py:
+// self-attention, compact layouts) the backward's measured +3..5 us per call, but inside the step
+// the cross-attention dK / dV go to the 6-layer concatenated kv gradient (row stride 6144), where
+// the per-lane stores touched 32-64 rows per instruction: dK/dV 98 -> 57 us, the fp32 step
+// 15.59 -> 15.11 ms (round 4, same box).
+static int g_attn_ae = -1;
 extern "C" int smi_attn_ae(int set) {
   if (set == 0 || set == 1) g_attn_ae = set;
   if (g_attn_ae < 0) {
@@ -1765,50 +1090,14 @@ extern "C" int smi_attn_ae(int set) {
   }
   return g_attn_ae;
 }
-static bool fa_ae_enabled() { return smi_attn_ae(-1) != 0; }
-// the backward kernels' dQ / dK / dV through LDS too (SMI_ATTN_AE_BWD=0: per-lane stores).  In
-// isolation (tools/ab_attn.py: self-attention, compact layouts) it measured +3..5 us per call, but
-// inside the step the cross-attention dK / dV go to the 6-layer concatenated kv gradient (row
-// stride 6144) and the per-lane stores touched 32-64 rows per instruction: dK/dV 98 -> 57 us,
-// the fp32 step 15.59 -> 15.11 ms (same box, gpurun_out/r4j_*)
-static int g_attn_ae_bwd = -1;
-extern "C" int smi_attn_ae_bwd(int set) {
-  if (set == 0 || set == 1) g_attn_ae_bwd = set;
-  if (g_attn_ae_bwd < 0) {
-    const char* e = getenv("SMI_ATTN_AE_BWD");
-    g_attn_ae_bwd = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_attn_ae_bwd;
-}
-// SMI_ATTN_SKEW = n: the forward / dQ kernels' second workgroup per CU starts n x 512 cycles late
-static int g_attn_skew = -1;
-extern "C" int smi_attn_skew(int set) {
-  if (set >= 0) g_attn_skew = set;
-  if (g_attn_skew < 0) {
-    const char* e = getenv("SMI_ATTN_SKEW");
-    g_attn_skew = e ? atoi(e) : 0;
-  }
-  return g_attn_skew;
-}
-static int fa_skew_units() { return smi_attn_skew(-1); }
 
 extern "C" int smi_attn_f32_fwd(const AttnF32Args* args, hipStream_t st) {
   AttnF32Args a = *args;
   if (!fa_ok(a)) return -1;
-  a.ae16 = fa_ae_enabled() && fa_ae16(a.op, a.o_sb, a.o_sh, a.o_ss);
-  a.skew = fa_skew_units();
+  a.ae16 = smi_attn_ae(-1) && fa_ae16(a.op, a.o_sb, a.o_sh, a.o_ss);
   dim3 grid((a.Sq + 127) / 128, a.H, a.B);
-  if (smi_gemm_f32_algo(-1) != 0 && smi_attn_f32_sp(-1)) {
-    if (smi_attn_fwd8(-1)) {
-      SMI_ATTN_SP_MODES8(attn_sp_fwd8, dim3((a.Sq + 255) / 256, a.H, a.B), a, fa_pi(a, false));
-    } else if (smi_attn_fwd_stagger(-1)) {
-      SMI_ATTN_SP_MODES8(attn_sp_fwd8s_kernel, dim3((a.Sq + 255) / 256, a.H, a.B), a, fa_pi(a, false));
-    } else {
-      SMI_ATTN_SP_MODES(attn_sp_fwd4, grid, a, fa_pi(a, false));
-    }
-  } else {
-    SMI_ATTN_F32_DISPATCH(attn_f32_fwd_kernel, grid, a);
-  }
+  if (smi_gemm_f32_algo(-1) != 0) SMI_ATTN_SP_MODES(attn_sp_fwd4, grid, 256, a);
+  else SMI_ATTN_F32_DISPATCH(attn_f32_fwd_kernel, grid, a);
   SMI_CHECK_LAUNCH();
 }
 
@@ -1816,22 +1105,12 @@ extern "C" int smi_attn_f32_bwd(const AttnF32Args* args, hipStream_t st) {
   AttnF32Args a = *args;
   if (!fa_ok(a) || !a.dout || !a.delta || (((uintptr_t)a.dout | (uintptr_t)a.dq | (uintptr_t)a.dk | (uintptr_t)a.dv) & 15))
     return -1;
-  a.ae16 = smi_attn_ae_bwd(-1) && fa_ae16(a.dqp, a.q_sb, a.q_sh, a.q_ss) && fa_ae16(a.dkp, a.k_sb, a.k_sh, a.k_ss) &&
+  a.ae16 = smi_attn_ae(-1) && fa_ae16(a.dqp, a.q_sb, a.q_sh, a.q_ss) && fa_ae16(a.dkp, a.k_sb, a.k_sh, a.k_ss) &&
            fa_ae16(a.dvp, a.v_sb, a.v_sh, a.v_ss);
-  a.skew = fa_skew_units();
   if (a.no_f32_grad && (!a.dqp || !a.dkp || !a.dvp)) return -1;  // planes-only needs every plane output
-  if (smi_gemm_f32_algo(-1) != 0 && smi_attn_f32_sp(-1)) {
-    const bool pi = fa_pi(a, true);
-    if (smi_attn_dkdv8(-1) && smi_attn_stagger(-1))
-      SMI_ATTN_SP_MODES8(attn_sp_dq8s_kernel, dim3((a.Sq + 255) / 256, a.H, a.B), a, pi);
-    else
-      SMI_ATTN_SP_MODES(attn_sp_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), a, pi);
-    if (smi_attn_dkdv8(-1) && smi_attn_stagger(-1))
-      SMI_ATTN_SP_MODES8(attn_sp_dkdv8s_kernel, dim3((a.Sk + AS_DKDV8_KEYS - 1) / AS_DKDV8_KEYS, a.H, a.B), a, pi);
-    else if (smi_attn_dkdv8(-1))
-      SMI_ATTN_SP_MODES8(attn_sp_dkdv8_kernel, dim3((a.Sk + AS_DKDV8_KEYS - 1) / AS_DKDV8_KEYS, a.H, a.B), a, pi);
-    else
-      SMI_ATTN_SP_MODES(attn_sp_dkdv_kernel, dim3((a.Sk + 127) / 128, a.H, a.B), a, pi);
+  if (smi_gemm_f32_algo(-1) != 0) {
+    SMI_ATTN_SP_MODES(attn_sp_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), 256, a);
+    SMI_ATTN_SP_MODES(attn_sp_dkdv8_kernel, dim3((a.Sk + AS_DKDV8_KEYS - 1) / AS_DKDV8_KEYS, a.H, a.B), 512, a);
   } else {
     SMI_ATTN_F32_DISPATCH(attn_f32_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), a);
     SMI_ATTN_F32_DISPATCH(attn_f32_dkdv_kernel, dim3((a.Sk + 127) / 128, a.H, a.B), a);

@@ -503,16 +503,15 @@ extern "C" long smi_emb_det_ws_bytes(long T, long V, long D) {
 }
 
 // deterministic backward algorithm: 1 = pair-compare (<= EMB_PAIR_MAX tokens, default), 0 = the
-// bucketed lists (SMI_EMB_BWD=det)
+// bucketed lists (emb_pair(0))
 // batches the pair path takes by default: the all-pairs rank grows as T^2 — at the transformer's
 // 8192 tokens it measured 40 us per call against the bucketed path's ~70 us for everything
-// (profiles/r4e_fp32_step.txt); the LSTM's 4128 tokens gain (SMI_EMB_PAIR_MAX overrides, <= 8192)
+// (profiles/r4e_fp32_step.txt); the LSTM's 4128 tokens gain (emb_pair_max overrides, <= 8192)
 static long g_emb_pair_sel = -1;
 extern "C" long smi_emb_pair_max(long set) {  // set < 0: query
   if (set >= 0) g_emb_pair_sel = set > EMB_PAIR_MAX ? EMB_PAIR_MAX : set;
   if (g_emb_pair_sel < 0) {
-    const char* ev = getenv("SMI_EMB_PAIR_MAX");
-    g_emb_pair_sel = ev ? atol(ev) : 4608;
+    g_emb_pair_sel = 4608;
     if (g_emb_pair_sel > EMB_PAIR_MAX) g_emb_pair_sel = EMB_PAIR_MAX;
   }
   return g_emb_pair_sel;
@@ -522,8 +521,7 @@ static int g_emb_pair = -1;
 extern "C" int smi_emb_pair(int set) {
   if (set == 0 || set == 1) g_emb_pair = set;
   if (g_emb_pair < 0) {
-    const char* ev = getenv("SMI_EMB_BWD");
-    g_emb_pair = (ev && ev[0] == 'd') ? 0 : 1;
+    g_emb_pair = 1;
   }
   return g_emb_pair;
 }

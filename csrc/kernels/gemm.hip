@@ -532,28 +532,15 @@ extern "C" int smi_gemm(const GemmArgs* args, hipStream_t st) {
   if (g.a_bytes >= (1L << 31) || g.b_bytes >= (1L << 31)) return -1;
   // tile height: 64 rows (up to 3 workgroups per CU whose load / MFMA / store phases overlap)
   // unless there are > 4 128-row tiles per CU anyway (the vocab projection); measured on the
-  // transformer shapes (tools/probes/run_gemm_probe3.sh).  SMI_GEMM_BM overrides (64 / 128).
-  static int bm_env = -1, ns_env = -1;
-  if (bm_env < 0) {
-    const char* e = getenv("SMI_GEMM_BM");
-    bm_env = e ? atoi(e) : 0;
-    const char* e2 = getenv("SMI_GEMM_NS");
-    ns_env = e2 ? atoi(e2) : 0;
-  }
+  // transformer shapes (tools/probes/run_gemm_probe3.sh).
   const int tiles128 = ((g.M + 127) / 128) * ((g.N + BN - 1) / BN) * g.splits;
   int bm = (ak || tiles128 > 1024) ? 128 : 64;
-  if (!ak && (bm_env == 64 || bm_env == 128)) bm = bm_env;
   if (!ak && (g_bm_force == 64 || g_bm_force == 128)) bm = g_bm_force;
   const int ntiles = ((g.M + bm - 1) / bm) * ((g.N + BN - 1) / BN) * g.splits;
   // pipeline depth: NS=2 (two workgroups per CU) or NS=4 (one per CU, three k-steps in flight)
   // ring depth: 2 stages (2-3 WGs per CU) everywhere by default — measured: 3 or 4 stages
-  // (fewer WGs per CU) were 3-5 % slower per step, for WGRAD too (SMI_GEMM_WGRAD_NS=4 / SMI_GEMM_NS).
-  static int wns_env = -1;
-  if (wns_env < 0) {
-    const char* e = getenv("SMI_GEMM_WGRAD_NS");
-    wns_env = e ? atoi(e) : 2;
-  }
-  const int ns = ak ? (wns_env == 4 ? 4 : 2) : (ns_env >= 2 && ns_env <= 4 ? ns_env : GEMM_NS);
+  // (fewer WGs per CU) were 3-5 % slower per step, for WGRAD too.
+  const int ns = ak ? 2 : GEMM_NS;
   const int maxg = NUM_CU * (ns == 2 ? (bm == 64 ? 3 : 2) : (ns == 3 && bm == 64 ? 2 : 1));
   const int grid = ntiles < maxg ? ntiles : maxg;
   const bool atomic = g.out_f32 && g.atomic;

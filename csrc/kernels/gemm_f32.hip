@@ -34,8 +34,7 @@ int smi_f32_launch_wgrad(const GemmF32Args& g, int fe, int algo, dim3 grid2, hip
 static int g_f32_algo = -1;
 static int smi_f32_algo() {
   if (g_f32_algo < 0) {
-    const char* e = getenv("SMI_F32_ALGO");
-    g_f32_algo = (e && atoi(e) == 0) ? 0 : 6;
+    g_f32_algo = 6;
   }
   return g_f32_algo;
 }
@@ -58,31 +57,14 @@ extern "C" int smi_gemm_f32(const GemmF32Args* args, hipStream_t st) {
   GemmF32Args g = *args;
   if (!f32_ok(g) || g.mode < 0 || g.mode > 2) return -1;
   const bool ak = g.mode == 2;
-  static int bm_env = -1;
-  if (bm_env < 0) {
-    const char* e = getenv("SMI_GEMM_F32_BM");
-    bm_env = e ? atoi(e) : 0;
-  }
-  const int t128 = ((g.M + 127) / 128) * ((g.N + FBN - 1) / FBN);
-  // 64-row tiles until there are >= 2 128-row tiles per CU (two co-resident workgroups per CU)
-  int bm = (ak || t128 >= 2 * NUM_CU) ? 128 : 64;
-  if (!ak && (bm_env == 64 || bm_env == 128)) bm = bm_env;
-  const int nwg = ((g.M + bm - 1) / bm) * ((g.N + FBN - 1) / FBN);
   if (g.splits < 1) g.splits = 1;
   if (g.splits > 1 && !g.atomic) return -1;
   int kps = (g.K / g.splits + FBK - 1) / FBK * FBK;
   if (kps < FBK) kps = FBK;
   g.k_per_split = kps;
   g.splits = (g.K + kps - 1) / kps;
-  const dim3 grid((unsigned)(nwg * g.splits)), block(256);
-  static int pf_env = -1;
-  if (pf_env < 0) {
-    // 0 = software-pipelined one-wave-per-SIMD kernel (default), 1 / 2 = two-workgroups-per-CU
-    // kernel with prefetch distance 1 / 2
-    const char* e = getenv("SMI_GEMM_F32_PF");
-    pf_env = e ? atoi(e) : 0;
-  }
-  if (pf_env == 0) {
+  const dim3 block(256);
+  {  // the software-pipelined one-wave-per-SIMD kernel
     const int nwg128 = ((g.M + 127) / 128) * ((g.N + FBN - 1) / FBN);
     const dim3 grid2((unsigned)(nwg128 * g.splits));
     // specialised epilogues for the feature sets the models use; anything else -> generic (-1)
@@ -117,17 +99,5 @@ extern "C" int smi_gemm_f32(const GemmF32Args* args, hipStream_t st) {
 #undef F32P
     SMI_CHECK_LAUNCH();
   }
-#define F32K(AKV, BKV, FMV)                                                                          \
-  if (pf_env == 1) hipLaunchKernelGGL((gemm_f32_kernel<AKV, BKV, FMV, 1>), grid, block, 0, st, g); \
-  else hipLaunchKernelGGL((gemm_f32_kernel<AKV, BKV, FMV, 2>), grid, block, 0, st, g)
-  if (g.mode == 0) {
-    if (bm == 64) { F32K(false, false, 1); } else { F32K(false, false, 2); }
-  } else if (g.mode == 1) {
-    if (bm == 64) { F32K(false, true, 1); } else { F32K(false, true, 2); }
-  } else {
-    F32K(true, true, 2);
-  }
-#undef F32K
-  SMI_CHECK_LAUNCH();
 }
 

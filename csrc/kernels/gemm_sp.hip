@@ -5,42 +5,27 @@
 
 #include <stdlib.h>
 
-static int g_sp_waves = 0;  // 0: not yet read from SMI_SP_WAVES
-int smi_sp_waves() {
-  if (g_sp_waves == 0) {
-    const char* e = getenv("SMI_SP_WAVES");
-    g_sp_waves = (e && atoi(e) == 4) ? 4 : 8;
-  }
-  return g_sp_waves;
-}
-static int g_sp_tm = 0;
-int smi_sp_tm() {
-  if (g_sp_tm == 0) {
-    const char* e = getenv("SMI_SP_TM");
-    const int v = e ? atoi(e) : 0;
-    g_sp_tm = (v == 128 || v == 4 || v == 256) ? v : 16;  // default: 256 x 128 on the 16x16x32 MFMA
-  }
-  return g_sp_tm;
-}
-// set 128 / 256 / 4 (256 x 128 tiles on 4 pipelined waves) for A/B runs in one process; other values query
+static int g_sp_waves = 8;  // waves per 128 x 128 tile (gemm_sp_waves sets 4 for A/B runs)
+int smi_sp_waves() { return g_sp_waves; }
+// tile form of the large problems: 16 = 256 x 128 on the 16x16x32 MFMA (default), 256 = the same
+// on 32x32x16, 128 = 128 x 128 tiles (a 4-wave software-pipelined 256 x 128 form measured 157 vs
+// 181-187 TF and was removed in round 5)
+static int g_sp_tm = 16;
+int smi_sp_tm() { return g_sp_tm; }
+// set 128 / 256 / 16 for A/B runs in one process; other values query
 extern "C" int smi_gemm_sp_tm(int set) {
-  if (set == 128 || set == 256 || set == 4 || set == 16) g_sp_tm = set;
+  if (set == 128 || set == 256 || set == 16) g_sp_tm = set;
   return smi_sp_tm();
 }
-// the grouped weight-gradient launch's tile (SMI_SP_WG_TM = 128 | 256 | 16 | 4; default: follow
+// the grouped weight-gradient launch's tile (gemm_sp_wg_tm = 128 | 256 | 16 | 4; default: follow
 // smi_sp_tm).  Per backward the group holds every layer's weight gradients, each a long
 // K = tokens reduction: fewer, larger tiles can leave CUs idle where 128-row tiles fill them.
-static int g_sp_wg_tm = 0;
+static int g_sp_wg_tm = -1;
 int smi_sp_wg_tm() {
-  if (g_sp_wg_tm == 0) {
-    const char* e = getenv("SMI_SP_WG_TM");
-    const int v = e ? atoi(e) : 0;
-    g_sp_wg_tm = (v == 128 || v == 256 || v == 16 || v == 4) ? v : -1;
-  }
   return g_sp_wg_tm > 0 ? g_sp_wg_tm : smi_sp_tm();
 }
 extern "C" int smi_gemm_sp_wg_tm(int set) {
-  if (set == 128 || set == 256 || set == 16 || set == 4) g_sp_wg_tm = set;
+  if (set == 128 || set == 256 || set == 16) g_sp_wg_tm = set;
   else if (set == -1) g_sp_wg_tm = -1;  // follow smi_sp_tm
   return smi_sp_wg_tm();
 }
@@ -112,8 +97,7 @@ extern "C" int smi_gemm_sp(const GemmSpArgs* args, hipStream_t st) {
   if (g.relu > 1 || (!g.C && out != (SO_P | SO_M))) return -1;
 #define SPF(E, O)                                                                                   \
   do {                                                                                              \
-    if (t256 && smi_sp_tm() == 4) hipLaunchKernelGGL((gemm_sp4w_kernel<false, false, E, O>), grid, dim3(256), 0, st, g); \
-    else if (t256 && smi_sp_tm() == 16) hipLaunchKernelGGL((gemm_sp256m_kernel<false, false, E, O>), grid, dim3(512), 0, st, g); \
+    if (t256 && smi_sp_tm() == 16) hipLaunchKernelGGL((gemm_sp256m_kernel<false, false, E, O>), grid, dim3(512), 0, st, g); \
     else if (t256) hipLaunchKernelGGL((gemm_sp256_kernel<false, false, E, O>), grid, dim3(512), 0, st, g); \
     else if (w8) hipLaunchKernelGGL((gemm_sp_kernel<8, false, false, E, O>), grid, dim3(512), 0, st, g); \
     else hipLaunchKernelGGL((gemm_sp_kernel<4, false, false, E, O>), grid, dim3(256), 0, st, g);    \

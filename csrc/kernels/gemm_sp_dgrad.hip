@@ -6,8 +6,7 @@ int smi_sp_launch_dgrad(const GemmSpArgs& g, int epi, int out, dim3 grid, bool t
   const bool w8 = smi_sp_waves() == 8;
 #define SPD(E, O)                                                                                  \
   do {                                                                                             \
-    if (t256 && smi_sp_tm() == 4) hipLaunchKernelGGL((gemm_sp4w_kernel<false, true, E, O>), grid, dim3(256), 0, st, g); \
-    else if (t256 && smi_sp_tm() == 16) hipLaunchKernelGGL((gemm_sp256m_kernel<false, true, E, O>), grid, dim3(512), 0, st, g); \
+    if (t256 && smi_sp_tm() == 16) hipLaunchKernelGGL((gemm_sp256m_kernel<false, true, E, O>), grid, dim3(512), 0, st, g); \
     else if (t256) hipLaunchKernelGGL((gemm_sp256_kernel<false, true, E, O>), grid, dim3(512), 0, st, g); \
     else if (w8) hipLaunchKernelGGL((gemm_sp_kernel<8, false, true, E, O>), grid, dim3(512), 0, st, g); \
     else hipLaunchKernelGGL((gemm_sp_kernel<4, false, true, E, O>), grid, dim3(256), 0, st, g);    \

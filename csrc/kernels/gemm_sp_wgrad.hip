@@ -20,7 +20,7 @@ struct SpWgradGroup {
   int t0[SPG_MAX + 1]; int count;
 };
 
-// 128-row form (SMI_SP_TM=128).  Column block 0 of an entry with a bias also reduces dY^T 1.
+// 128-row form (gemm_sp_tm 128).  Column block 0 of an entry with a bias also reduces dY^T 1.
 template <int NW, bool BIASG>
 __global__ __launch_bounds__(64 * NW, 1) void gemm_sp_wgrad_group_kernel(SpWgradGroup gr) {
   __shared__ __attribute__((aligned(16))) unsigned short lds[SP_NS * SP_ST];
@@ -64,7 +64,7 @@ __global__ __launch_bounds__(512, 1) void gemm_sp_wgrad_group256_kernel(SpWgradG
   else gemm_sp_tile256<true, true, SE_ACC, SO_C, false>(g, (l2 / ncb) * ntn + cb, lds);
 }
 
-// the same on the 16x16x32 MFMA (SMI_SP_TM=16, gemm_sp_tile256m)
+// the same on the 16x16x32 MFMA (gemm_sp_tm 16, gemm_sp_tile256m)
 __global__ __launch_bounds__(512, 1) void gemm_sp_wgrad_group256m_kernel(SpWgradGroup gr) {
   __shared__ __attribute__((aligned(16))) unsigned short lds[2 * SP_ST256];
   const int t = blockIdx.x;
@@ -85,27 +85,6 @@ __global__ __launch_bounds__(512, 1) void gemm_sp_wgrad_group256m_kernel(SpWgrad
   else gemm_sp_tile256m<true, true, SE_ACC, SO_C, false>(g, (l2 / ncb) * ntn + cb, lds);
 }
 
-// the same on 4 pipelined waves (SMI_SP_TM=4, gemm_sp_tile4w)
-__global__ __launch_bounds__(256, 1) void gemm_sp_wgrad_group4w_kernel(SpWgradGroup gr) {
-  __shared__ __attribute__((aligned(16))) unsigned short lds[SP4_NS * SP4_ST];
-  const int t = blockIdx.x;
-  int e = 0;
-  while (e + 1 < gr.count && t >= gr.t0[e + 1]) ++e;
-  GemmSpArgs g{};
-  g.mode = 2; g.A = gr.A[e]; g.lda = gr.lda[e]; g.aps = gr.aps[e]; g.B = gr.B[e]; g.ldb = gr.ldb[e];
-  g.bps = gr.bps[e]; g.M = gr.n[e]; g.N = gr.k[e]; g.K = gr.T[e]; g.C = gr.C[e]; g.ldc = gr.k[e];
-  g.beta_acc = 1; g.dscale = 1.f; g.bias_grad = gr.bias[e];
-  g.a_bytes = gr.a_bytes[e]; g.b_bytes = gr.b_bytes[e];
-  const int ncb = gr.ncb[e], ntn = (g.N + 127) / 128;
-  const int nwg = ((g.M + 255) / 256) * ncb;
-  const int lt = t - gr.t0[e];
-  if (lt >= nwg) return;
-  const int l2 = sp_tile_remap(lt, nwg);
-  const int cb = gr.cb0[e] + l2 % ncb;
-  if (g.bias_grad && cb == 0) gemm_sp_tile4w<true, true, SE_ACC, SO_C, true>(g, (l2 / ncb) * ntn + cb, lds);
-  else gemm_sp_tile4w<true, true, SE_ACC, SO_C, false>(g, (l2 / ncb) * ntn + cb, lds);
-}
-
 // A_e: dY planes [3][T][lda] (plane stride aps), B_e: X planes [3][T][ldb]; C_e = gW [n][k] (row
 // stride k), bias_e = gb [n] or null.
 extern "C" int smi_gemm_sp_wgrad_group(const void* const* A, const long* lda, const long* aps, const void* const* B,
@@ -115,7 +94,7 @@ extern "C" int smi_gemm_sp_wgrad_group(const void* const* A, const long* lda, co
   SpWgradGroup gm{}, gb{};
   int tm = 0, tb = 0, cm = 0, cb = 0;
   const int wtm = smi_sp_wg_tm();
-  const bool t4w = wtm == 4, t16 = wtm == 16, t256 = wtm == 256 || t4w || t16;
+  const bool t16 = wtm == 16, t256 = wtm == 256 || t16;
   for (int i = 0; i < count; ++i) {
     int ab = 0, bb = 0;
     if (!sp_operand_ok((const unsigned short*)A[i], lda[i], aps[i], n[i], n[i], true, 0, T[i], ab)) return -1;
@@ -139,8 +118,7 @@ extern "C" int smi_gemm_sp_wgrad_group(const void* const* A, const long* lda, co
   }
   (void)gb; (void)tb; (void)cb;
   gm.t0[cm] = tm; gm.count = cm;
-  if (t4w) hipLaunchKernelGGL(gemm_sp_wgrad_group4w_kernel, dim3((unsigned)tm), dim3(256), 0, st, gm);
-  else if (t16) hipLaunchKernelGGL(gemm_sp_wgrad_group256m_kernel, dim3((unsigned)tm), dim3(512), 0, st, gm);
+  if (t16) hipLaunchKernelGGL(gemm_sp_wgrad_group256m_kernel, dim3((unsigned)tm), dim3(512), 0, st, gm);
   else if (t256) hipLaunchKernelGGL(gemm_sp_wgrad_group256_kernel, dim3((unsigned)tm), dim3(512), 0, st, gm);
   else if (smi_sp_waves() == 8) hipLaunchKernelGGL((gemm_sp_wgrad_group_kernel<8, true>), dim3((unsigned)tm), dim3(512), 0, st, gm);
   else hipLaunchKernelGGL((gemm_sp_wgrad_group_kernel<4, true>), dim3((unsigned)tm), dim3(256), 0, st, gm);

@@ -1117,15 +1117,11 @@ static bool lw_fits(const LSTMArgs& a) {
   return 4 * a.H <= 128 && a.C <= 128 && a.E <= 32 && lw_ctiles(a) <= LW_TICKS && a.ce_tick != nullptr;
 }
 
-// SMI_LSTM_WGRAD=valu: the two-launch VALU split-K reduction above (+ lstm_xe_kernel)
-static int lstm_wgrad_mfma_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("SMI_LSTM_WGRAD");
-    v = (e && e[0] == 'v') ? 0 : 1;
-  }
-  return v;
-}
+// the MFMA weight gradient (default; 35 us for every weight gradient against 39 + 8 us for the
+// VALU split-K pair, docs/PERF_NOTES.md round 4); 0: the two-launch VALU split-K reduction above
+// (+ lstm_xe_kernel), still taken by the shapes outside lw_fits
+static int g_lstm_wgrad_mfma = 1;
+static int lstm_wgrad_mfma_enabled() { return g_lstm_wgrad_mfma; }
 
 // per-token embedding-input gradients xe[b,t,:] = W_ih0^T da0[b,t,:] (the table gradient is their
 // position-ordered per-id sum, csrc/kernels/embedding.hip)
@@ -1149,14 +1145,7 @@ __global__ __launch_bounds__(256) void lstm_xe_kernel(LSTMArgs a) {
 
 // 4*H*L <= 256 threads: one wave per SIMD, so the backward's register-resident gradient rows
 // and W column slices get the full 512-entry (VGPR + AGPR) file.
-static int lstm_w2_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("SMI_LSTM_W2");
-    v = e ? atoi(e) != 0 : 1;
-  }
-  return v;
-}
+static int lstm_w2_enabled() { return 1; }
 
 template <int H, int MI>
 static int lstm_launch(const LSTMArgs* a, int backward, hipStream_t st) {

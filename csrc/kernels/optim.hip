@@ -206,8 +206,7 @@ static int g_adam_wide = -1;
 extern "C" int smi_adam_wide(int set) {
   if (set == 0 || set == 1) g_adam_wide = set;
   if (g_adam_wide < 0) {
-    const char* e = getenv("SMI_ADAM_WIDE");
-    g_adam_wide = (e && e[0] == '0') ? 0 : 1;
+    g_adam_wide = 1;
   }
   return g_adam_wide;
 }

@@ -22,7 +22,6 @@ Mask semantics:
 import functools
 from dataclasses import dataclass
 
-import os
 
 import torch
 from torch import nn
@@ -106,13 +105,11 @@ def _gp(t):
     return _pl.mark_grad_planes_ok(t)
 
 
-# fp32 GPU path: feed the attention kernels producer-written q/k/v/dO planes (SMI_ATTN_PLANES=1)
-ATTN_PLANES = os.environ.get("SMI_ATTN_PLANES", "0") == "1"
 # fp32 GPU path: the vocab projection's epilogue computes the cross-entropy row statistics
-# (SMI_CE_FUSED=1).  Off by default: step-time neutral (-0.01 ms, profiles/r3b_ab_planes_only.txt)
-# and its tile-merged logsumexp moves the early flagship trajectory off the CPU reference by more
-# than the standalone pass (tests/test_f32_gpu.py::test_transformer_f32_flagship_trajectory)
-CE_FUSED = os.environ.get("SMI_CE_FUSED", "0") == "1"
+# (True).  Off: step-time neutral (-0.01 ms, profiles/r3b_ab_planes_only.txt), and its tile-merged
+# logsumexp moves the early flagship trajectory off the CPU reference by more than the standalone
+# pass (tests/test_f32_gpu.py::test_transformer_f32_flagship_trajectory); tests exercise it
+CE_FUSED = False
 
 
 class MultiHeadAttention(nn.Module):
@@ -125,12 +122,9 @@ class MultiHeadAttention(nn.Module):
         self.linear_layer = nn.Linear(d_model, d_model)
 
     def forward(self, x, mode="none", key_padding=None, x_slot=None):
-        # ATTN_PLANES: the projection writes q/k/v planes and the out-projection's dgrad writes dO
-        # planes, read by the attention kernels instead of splitting at staging (off by default:
-        # measured slower, docs/PERF_NOTES.md)
-        qkv = _gp(linear(x, self.qkv_layer.weight, self.qkv_layer.bias, x_slot=x_slot, out_planes=ATTN_PLANES))
+        qkv = _gp(linear(x, self.qkv_layer.weight, self.qkv_layer.bias, x_slot=x_slot))
         values = self_attention(qkv, self.num_heads, mode, key_padding)
-        return _gp(linear(values, self.linear_layer.weight, self.linear_layer.bias, dx_planes=ATTN_PLANES))
+        return _gp(linear(values, self.linear_layer.weight, self.linear_layer.bias))
 
 
 class MultiHeadCrossAttention(nn.Module):
@@ -147,13 +141,13 @@ class MultiHeadCrossAttention(nn.Module):
         """``kv``: optional (kv_all, column, SharedGrad) — this layer's k/v projection already
         computed inside the decoder's concatenated kv GEMM (Decoder._shared_kv)."""
         if kv is None:
-            kv_all = _gp(linear(x, self.kv_layer.weight, self.kv_layer.bias, out_planes=ATTN_PLANES))
+            kv_all = _gp(linear(x, self.kv_layer.weight, self.kv_layer.bias))
             col, shared = 0, None
         else:
             kv_all, col, shared = kv
-        q = _gp(linear(y, self.q_layer.weight, self.q_layer.bias, x_slot=y_slot, out_planes=ATTN_PLANES))
+        q = _gp(linear(y, self.q_layer.weight, self.q_layer.bias, x_slot=y_slot))
         values = cross_attention(q, kv_all, self.num_heads, mode, key_padding, col, shared)
-        return _gp(linear(values, self.linear_layer.weight, self.linear_layer.bias, dx_planes=ATTN_PLANES))
+        return _gp(linear(values, self.linear_layer.weight, self.linear_layer.bias))
 
 
 class LayerNormalization(nn.Module):

@@ -25,7 +25,7 @@ _listeners = []
 # the fork/join branches leaves the GPU idle 15-20 us at each cross-queue dependency (1.06 ms of
 # idle per transformer step in 108 such gaps) — more than the overlap wins; the single-stream
 # step has no idle gaps at all (profiles/timeline_*).
-_SIDE_ENABLED = os.environ.get("SPARKMI_WGRAD_STREAM", "0") != "0"
+_SIDE_ENABLED = False
 _side_streams = {}
 _pending = {}  # device -> the stream the side work was forked from (and must be joined back into)
 
@@ -179,7 +179,7 @@ class ResidualGrad:
 # launch at the end of the backward (autograd final callback), after which the parameters are
 # reported ready (DDP bucket hooks / split-graph ready sets see them at the end of their
 # backward piece).  SPARKMI_LN_DEFER=0 restores the per-LayerNorm fold.
-LN_DEFER = os.environ.get("SPARKMI_LN_DEFER", "1") != "0" and not _SIDE_ENABLED
+LN_DEFER = True
 _ln_queue = []
 _cb = [False]
 
@@ -249,7 +249,7 @@ def defer_ln_fold(part_g, part_b, nb, D, gg, gb, params, stream):
 # Same idea for the split-K slabs of the weight-gradient GEMMs (sparkmi/ops/gemm.py:wgrad):
 # one fold launch per Linear (66 per transformer step) becomes one batched launch per backward
 # piece; the slabs stay alive until then.  SPARKMI_FOLD_DEFER=0 folds each GEMM immediately.
-FOLD_DEFER = os.environ.get("SPARKMI_FOLD_DEFER", "1") != "0" and not _SIDE_ENABLED
+FOLD_DEFER = True
 _fold_queue = []
 
 
@@ -266,7 +266,7 @@ def defer_wgrad_fold(slab, splits, n, gw, nb, gb, params, stream):
 # end (csrc/kernels/gemm.hip:gemm_wgrad_group_kernel: no split-K, each tile reduces all tokens
 # and adds into the fp32 gradient).  The queued dY / X stay referenced until then (autograd
 # then never accumulates into them in place).  SPARKMI_WGRAD_GROUP=0 restores per-Linear GEMMs.
-WGRAD_GROUP = os.environ.get("SPARKMI_WGRAD_GROUP", "1") != "0" and not _SIDE_ENABLED
+WGRAD_GROUP = True
 _group_queue = []
 GROUP_MAX = 40  # csrc/kernels/gemm.hip WG_MAX
 
@@ -391,7 +391,7 @@ def _flush_folds(C, fq):
 # see _SIDE_ENABLED above).  The launched operands stay referenced until the join; their
 # parameters are reported final only after it.  Single-process only (no defer listeners: the
 # data-parallel engine runs its own early flushes).  SMI_WGRAD_OVERLAP=0 disables it.
-WGRAD_OVERLAP = os.environ.get("SMI_WGRAD_OVERLAP", "1") != "0" and not _SIDE_ENABLED
+WGRAD_OVERLAP = True
 _async = {"main": None, "dev": None, "hold": []}
 
 

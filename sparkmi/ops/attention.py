@@ -75,15 +75,6 @@ def _merge(o):
     return o.permute(0, 2, 1, 3).reshape(B, S, H * hd)
 
 
-def _in_planes(t, row_stride, off_elems=0):
-    """(pointer, plane stride) of the producer-written planes of an fp32 attention input ``t``
-    at element offset ``off_elems`` of each row, or None (no planes, or a layout that differs)."""
-    p = _pl.cached(t.reshape(-1, t.shape[-1]))
-    if p is None or p.stride(1) != row_stride or p.stride(2) != 1:
-        return None
-    return p.data_ptr() + 2 * off_elems, p.stride(0), p
-
-
 def _planes_like(t):
     """Planes [3, rows, W] for an fp32 [.., W] attention output / gradient (None: planes off or W
     not a multiple of 32, the split-plane GEMM's k granularity)."""
@@ -143,23 +134,11 @@ class _AttnCore(torch.autograd.Function):
         lse = torch.empty(B, H, Sq, device=qsrc.device, dtype=torch.float32)
         os_ = (Sq * H * hd, H * hd, hd)
         kpad = key_padding.to(torch.uint8).contiguous() if key_padding is not None else None
-        ctx.pin = None
         if f32:
-            # the projections' planes (q/k/v as ready MFMA operands), when their epilogue wrote them
-            if cross:  # q [B,Sq,H*hd]; kv head h = [k_h | v_h] from column kv_col
-                pq_ = _in_planes(qsrc, qs[1])
-                pkv_ = _in_planes(kvsrc, ks[1], kv_col)
-                kv_off = (0, hd)
-            else:  # qkv head h = [q_h | k_h | v_h]
-                pq_ = pkv_ = _in_planes(qsrc, qs[1])
-                kv_off = (hd, 2 * hd)
-            if pq_ is not None and pkv_ is not None:  # plane pointers in bytes (bf16 elements)
-                ctx.pin = (pq_[0], pkv_[0] + 2 * kv_off[0], pkv_[0] + 2 * kv_off[1], pq_[1], pkv_[1], pq_[2], pkv_[2])
-            pin = ctx.pin or (0, 0, 0, 0, 0)
             opl = _planes_like(o)  # the out-projection's operand, written by the same epilogue
             C.attn_f32_fwd(qp, kp, vp, qs, ks, vs, o.data_ptr(), os_, lse.data_ptr(), _native.ptr(kpad), B, H, Sq, Sk,
                            mode, _LOG2E / math.sqrt(hd), _native.ptr(opl), opl.stride(0) if opl is not None else 0,
-                           pin[0], pin[1], pin[2], pin[3], pin[4], _native.stream())
+                           _native.stream())
             if opl is not None:
                 _pl.attach(o, opl)
         else:
@@ -227,20 +206,13 @@ class _AttnCore(torch.autograd.Function):
                     pq, q_ps = pl.data_ptr(), pl.stride(0)
                     pk, pv, kv_ps = pq + hd * 2, pq + 2 * hd * 2, q_ps
         if f32:
-            # dO's planes from the out-projection's dgrad epilogue + the inputs' planes
-            pdo = _in_planes(do, os_[1]) if ctx.pin is not None else None
-            pin = ctx.pin if pdo is not None else (0, 0, 0, 0, 0)
-            if pdo is None:
-                _pl.f32(do)  # the kernels read dO's fp32 values
+            _pl.f32(do)  # the kernels read dO's fp32 values
             # dQ/dK/dV feed only the projections' dgrad / wgrad GEMMs (their planes): planes only
             only = bool(pq) and _pl.grad_planes_ok(qsrc) and (not ctx.cross or ctx.shared is not None
                                                                or _pl.grad_planes_ok(kvsrc))
             C.attn_f32_bwd(qp, kp, vp, qs, ks, vs, o.data_ptr(), do.data_ptr(), os_, lse.data_ptr(), delta.data_ptr(),
                            dqp, dkp, dvp, _native.ptr(ctx.kpad), B, H, Sq, Sk, ctx.mode, _LOG2E / math.sqrt(hd),
-                           1.0 / math.sqrt(hd), pq, pk, pv, q_ps, kv_ps, pin[0], pin[1], pin[2],
-                           pdo[0] if pdo is not None else 0, pin[3], pin[4], pdo[1] if pdo is not None else 0,
-                           int(only), _native.stream())
-            ctx.pin = None
+                           1.0 / math.sqrt(hd), pq, pk, pv, q_ps, kv_ps, int(only), _native.stream())
             if only:
                 if ctx.cross:
                     dq._smi_planes_only = True

@@ -25,8 +25,8 @@ def sinusoid_table(max_len: int, d_model: int) -> torch.Tensor:
 
 
 
-# SPARKMI_EMB_PLAN_AHEAD=0: the whole ordering + sum in the backward (A/B switch)
-PLAN_AHEAD = __import__("os").environ.get("SPARKMI_EMB_PLAN_AHEAD", "1") != "0"
+# False: the whole ordering + sum in the backward (tests)
+PLAN_AHEAD = True
 _PLAN_STREAMS = {}
 _PENDING = []  # forked plans not yet joined: [ws, stream, algo, joined]
 

@@ -16,7 +16,7 @@ import torch
 from .. import _native
 from . import _grad
 
-_DISABLE = os.environ.get("SPARKMI_GEMM", "1") == "0"
+_DISABLE = False  # True (tests): every Linear on torch ops
 NUM_CU = 256
 
 
@@ -61,7 +61,7 @@ def dgrad(dy, w, resid=None, dact_y=None, dscale=1.0, out=None):
 # split-K target (workgroups) for the weight-gradient GEMM: it runs on the side stream next to
 # the backward's critical path, so it need not fill the chip alone; fewer splits = fewer fp32
 # atomic partial sums (each split adds one full N x K slab).
-_WGRAD_TARGET = int(os.environ.get("SPARKMI_WGRAD_TARGET", str(NUM_CU)))
+_WGRAD_TARGET = NUM_CU
 
 
 def wgrad_splits(N, K, M):
@@ -72,7 +72,7 @@ def wgrad_splits(N, K, M):
     return s
 
 
-_WGRAD_MODE = os.environ.get("SPARKMI_WGRAD_MODE", "slab")  # slab | atomic
+_WGRAD_MODE = "slab"  # slab | atomic (tests)
 
 
 def _actual_splits(M, s):
@@ -171,8 +171,9 @@ def wgrad32(dy, x, gw, gb=None, splits=None):
 # ---- split-plane fp32 GEMM: csrc/kernels/gemm_sp*.hip (operands as bf16 hi/mid/lo planes) ----
 # The reference-precision path of the fp32 Linear layers (sparkmi/ops/planes.py): six exact bf16
 # slice products per fp32 product on v_mfma_f32_32x32x16_bf16, no splitting inside the k-loop.
-# SPARKMI_F32_PLANES=0 falls back to csrc/kernels/gemm_f32.hip (split inside the GEMM).
-SP = os.environ.get("SPARKMI_F32_PLANES", "1") != "0" and not _DISABLE
+# SP = False falls back to csrc/kernels/gemm_f32.hip (split inside the GEMM; the bench's f32-MFMA
+# comparison run).
+SP = not _DISABLE
 
 
 def _sp_ok(*ts):

@@ -55,8 +55,9 @@ def _pad2(t, rows, cols):
     return out
 
 
-# FFN hidden activation as planes + positivity mask (no fp32 tensor); SMI_FFN_MASK=0 keeps fp32
-_FFN_MASK = __import__("os").environ.get("SMI_FFN_MASK", "1") != "0"
+# FFN hidden activation as planes + positivity mask (no fp32 tensor; -400 MB of activations per
+# step, round 3c); False keeps fp32
+_FFN_MASK = True
 
 
 def _fwd32_any(x2, w, bias, act, rng, salt, p):
@@ -440,10 +441,7 @@ class ConcatLinearFn(torch.autograd.Function):
         x2 = x.reshape(-1, K).contiguous()
         w = wm.view(N, K)
         wp = wviews[3] if len(wviews) > 3 and x2.dtype == torch.float32 and G.SP else None
-        # fp32 + SMI_ATTN_PLANES: the planes of y too, read by the cross-attention kernels
-        from ..models import transformer as _tm
-        y2 = _fwd_native(x2, w, bm, 0, 0.0, None, 0, w_bf=ws.view(N, K) if ws is not None else None, wp=wp,
-                         out_planes=wp is not None and _tm.ATTN_PLANES)
+        y2 = _fwd_native(x2, w, bm, 0, 0.0, None, 0, w_bf=ws.view(N, K) if ws is not None else None, wp=wp)
         ctx.wviews, ctx.bg, ctx.shape, ctx.params, ctx.shared = wviews, bg, shape, params, shared
         ctx.x_planes, ctx.wp = _pl.cached(x2), wp
         ctx.save_for_backward(x2)

@@ -180,9 +180,9 @@ class LSTMFn(torch.autograd.Function):
 
 
 _CE_TICKETS = {}
-# the embedding backward's id ordering made by the forward launch (SMI_LSTM_EMB_SIDE=1) or by the
-# backward itself (0)
-EMB_IN_FORWARD = __import__("os").environ.get("SMI_LSTM_EMB_SIDE", "1") != "0"
+# the embedding backward's id ordering made by the forward launch (True; LSTM step 0.330 -> 0.294
+# ms, docs/PERF_NOTES.md round 4) or by the backward itself (False: tests)
+EMB_IN_FORWARD = True
 
 
 

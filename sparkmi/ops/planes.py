@@ -24,7 +24,7 @@ from .. import _native
 # dgrad / wgrad GEMM pair) is written by its producer as planes alone — its fp32 tensor is a
 # placeholder that is never filled unless a fallback path asks for it (f32() below).  The FFN
 # hidden gradient, dlogits, the LayerNorm dh and the attention dQ/dK/dV skip 4 B per element.
-PLANES_ONLY = os.environ.get("SMI_PLANES_ONLY", "1") != "0"
+PLANES_ONLY = True  # False (tests): every gradient also written in fp32
 
 
 def r32(n):

@@ -238,21 +238,16 @@ def _attn_f32(B, H, Sq, Sk, mode, cross, kp):
         _close(qg.grad, dqkv, 5e-5, 1e-5, f"dqkv {mode}")
 
 
-@pytest.fixture(params=[1, 2, 0], ids=["staged_planes", "staged_planes_4wave", "wave_split"])
+@pytest.fixture(params=[1, 0], ids=["staged_planes", "per_lane_epilogue"])
 def attn_kernel(request):
-    """The split-product attention kernels: streamed chunks split once at LDS staging (default;
-    forward on 8-wave (opt-in) and dK/dV on 8-wave workgroups (default), or both 4-wave:
-    C.attn_fwd8(0), C.attn_dkdv8(0)) or per wave per fragment (C.attn_f32_sp(0)); irrelevant under
-    the f32-MFMA algorithm."""
+    """The split-product attention kernels (forward 4-wave, dQ 4-wave, dK/dV 8-wave with owned V in
+    LDS), with the row-coalesced LDS epilogue (default) or the per-lane transposed stores
+    (C.attn_ae(0)); irrelevant under the f32-MFMA algorithm."""
     C = _native.C()
-    prev, prev8, prevf8 = C.attn_f32_sp(-1), C.attn_dkdv8(-1), C.attn_fwd8(-1)
-    C.attn_f32_sp(1 if request.param else 0)
-    C.attn_dkdv8(0 if request.param == 2 else 1)
-    C.attn_fwd8(0 if request.param == 2 else 1)
+    prev = C.attn_ae(-1)
+    C.attn_ae(request.param)
     yield request.param
-    C.attn_f32_sp(prev)
-    C.attn_dkdv8(prev8)
-    C.attn_fwd8(prevf8)
+    C.attn_ae(prev)
 
 
 @pytest.mark.parametrize("mode", ["none", "reference", "causal"])
@@ -400,27 +395,6 @@ def test_transformer_f32_step_matches_cpu():
     for (n, pc), (_, pg) in zip(mc.named_parameters(), mg.named_parameters()):
         rel = (pg.grad.cpu().double() - pc.grad.double()).norm() / (pc.grad.double().norm() + 1e-12)
         assert rel < 1e-4, (n, float(rel))
-
-
-def test_transformer_f32_attention_plane_inputs_bitwise(monkeypatch):
-    """SMI_ATTN_PLANES: the projections / out-projection dgrad emit q/k/v/dO planes and the
-    attention kernels read them instead of splitting at staging — the whole step (loss and every
-    gradient) is bitwise the default path's."""
-    from sparkmi.data.synthetic import translation_pairs
-    from sparkmi.models import transformer as T
-    src, tgt = translation_pairs(4, 32, 96, 96, seed=3)
-    _, mg = _pair()
-    mg.train()
-    out = []
-    for planes in (False, True):
-        monkeypatch.setattr(T, "ATTN_PLANES", planes)
-        for p in mg.parameters():
-            p.grad = None
-        lg = mg.training_step_loss(src.to(dev), tgt.to(dev))
-        lg.backward()
-        out.append([lg.detach()] + [p.grad.clone() for p in mg.parameters()])
-    for a, b in zip(*out):
-        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("graph", [False, True])
@@ -659,10 +633,9 @@ def test_transformer_f32_flagship_trajectory(f32_algo, monkeypatch):
 
 @pytest.mark.parametrize("cross", [False, True])
 @pytest.mark.parametrize("mode,S", [("none", 256), ("reference", 256), ("causal", 200), ("reference", 37)])
-def test_attention_f32_stagger_and_row_epilogue_bitwise(f32_algo, mode, S, cross):
-    """Round-4 kernel variants are scheduling changes only: the staggered 8-wave forward, dQ and
-    dK/dV kernels (two half-workgroups half a chunk apart) and the whole-row LDS epilogue give
-    BITWISE the 4-wave / lockstep kernels' outputs, gradients and planes."""
+def test_attention_f32_row_epilogue_bitwise(f32_algo, mode, S, cross):
+    """The whole-row LDS epilogue is a store-scheduling change only: BITWISE the per-lane
+    transposed stores' outputs, gradients and planes."""
     if f32_algo == 0:
         pytest.skip("split-product kernels only")
     from sparkmi.ops import planes as PL
@@ -686,7 +659,7 @@ def test_attention_f32_stagger_and_row_epilogue_bitwise(f32_algo, mode, S, cross
         op = PL.cached(o.detach().reshape(-1, o.shape[-1]))
         return out, (op.clone() if op is not None else None)
 
-    flags = (C.attn_stagger, C.attn_ae, C.attn_ae_bwd, C.attn_fwd_stagger)
+    flags = (C.attn_ae,)
     prev = [f(-1) for f in flags]
     try:
         for f in flags:

@@ -17,10 +17,10 @@ def _sum3(P, cols):
     return (P[0].float() + P[1].float() + P[2].float())[:, :cols]
 
 
-@pytest.fixture(params=[256, 16, 4, 128], ids=["tile256w8", "tile256m16", "tile256w4", "tile128"])
+@pytest.fixture(params=[256, 16, 128], ids=["tile256w8", "tile256m16", "tile128"])
 def tile(request):
     """Every tile form of the plane GEMM (C.gemm_sp_tm: 8-wave 256 x 128, the same on the 16x16x32
-    MFMA, 4-wave pipelined 256 x 128, 8-wave 128 x 128)."""
+    MFMA, 8-wave 128 x 128)."""
     from sparkmi import _native
     C = _native.C()
     prev = C.gemm_sp_tm(0)

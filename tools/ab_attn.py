@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
-"""A/B of the fp32 attention kernel variants at the flagship shape (B 32, S 256, H 8, hd 64,
-reference mask, planes out as in the model): whole-row LDS epilogue on/off (C.attn_ae), staggered
-dK/dV on/off (C.attn_stagger), start skew of the second workgroup per CU (C.attn_skew).  Each
+"""Timing / A/B of the fp32 attention kernels at the flagship shape (B 32, S 256, H 8, hd 64,
+reference mask, planes out as in the model): whole-row LDS epilogue on/off (C.attn_ae).  Each
 variant is timed in interleaved rounds (forward alone, then forward + backward) so clock drift
 hits every variant alike; one JSON line per variant with the median over rounds."""
 import json
@@ -36,19 +35,14 @@ def main():
     qkv = torch.randn(B, S, 3 * H * hd, device="cuda", requires_grad=True)
     do = torch.randn(B, S, H * hd, device="cuda")
     PL.attach(do, PL.split(do.reshape(-1, H * hd)))
-    variants = [("base", 0, 0, 0, 0), ("ae", 1, 0, 0, 0), ("ae+stagger", 1, 1, 0, 0), ("ae+skew8", 1, 0, 8, 0),
-                ("ae+stagger+fwd8s", 1, 1, 0, 1), ("ae_both", 2, 0, 0, 0)]
+    variants = [("ae", 1), ("per_lane", 0)]
     if "--only" in sys.argv:
         only = sys.argv[sys.argv.index("--only") + 1]
         variants = [v for v in variants if v[0] == only]
     res = {v[0]: ([], []) for v in variants}
     for _ in range(5):
-        for name, ae, st, sk, fs in variants:
-            C.attn_ae(1 if ae else 0)
-            C.attn_ae_bwd(1 if ae == 2 else 0)
-            C.attn_stagger(st)
-            C.attn_skew(sk)
-            C.attn_fwd_stagger(fs)
+        for name, ae in variants:
+            C.attn_ae(ae)
             f = timeit(lambda: self_attention(qkv.detach(), H, "reference"))
 
             def fb():
@@ -63,10 +57,6 @@ def main():
         print(json.dumps({"variant": name, "fwd_us": round(f, 1), "bwd_us": round(b, 1),
                           "fwd_tf": round(fl / f / 1e6, 1), "bwd_tf": round(2.5 * fl / b / 1e6, 1)}), flush=True)
     C.attn_ae(1)
-    C.attn_ae_bwd(0)
-    C.attn_stagger(0)
-    C.attn_skew(0)
-    C.attn_fwd_stagger(0)
 
 
 if __name__ == "__main__":

@@ -46,7 +46,7 @@ def main():
             r[f"sp{tm}_fwd_us"] = timeit(lambda: G.sp_fwd(xp, wp, M, N, K, bias=b))
             r[f"sp{tm}_dgrad_us"] = timeit(lambda: G.sp_dgrad(dyp, wp, M, K, N))
             r[f"sp{tm}_wgrad_us"] = timeit(lambda: G.sp_wgrad(dyp, xp, gw))
-        C.gemm_sp_tm(256)
+        C.gemm_sp_tm(16)
         r["split_x_us"] = timeit(lambda: planes.split(x))
         r["split_dy_us"] = timeit(lambda: planes.split(dy, kpad=N % 32 != 0))
         for a in ((6, 0) if "--f32" in sys.argv else ()):
@@ -79,7 +79,7 @@ def main():
         t = timeit(grp)
         print(json.dumps({f"sp{tm}_wgrad_group_dec_layer_us": round(t, 1), "tf": round(fl / (t * 1e-6) / 1e12, 1)}),
               flush=True)
-    C.gemm_sp_tm(256)
+    C.gemm_sp_tm(16)
 
 
 if __name__ == "__main__":
