@@ -297,25 +297,83 @@ def bench_cnn(args, rank, world, device, dtype="fp32"):
     opt = SGD(flat, lr=0.01)
     ddp = DataParallel(flat) if world > 1 else None
     use_graph = device.type == "cuda" and args.graph != "off"
-    # one executor: the whole step (forward, backward, batch gradient sum, SGD) is ONE launch
+    # one executor: the whole step (forward, backward, batch gradient sum, SGD) is ONE launch;
+    # data-parallel: the same kernel leaves the batch gradient (gradient mode), then the IPC
+    # all-reduce and SGD — three launches, in bound multi-step graphs like the single-executor step
     fused = (lambda m, o, x, y: m.fused_sgd_step(o, x, y)) if world == 1 else None
+    fgrad = (lambda m, x, y: m.fused_grad_step(x, y)) if world > 1 else None
     runner = StepRunner(model, lambda m, x, y: m.loss(x, y), opt, ddp, graph=use_graph, fused_step=fused,
-                        bind_inputs=True)
+                        bind_inputs=True, fused_grad=fgrad)
     imgs, labels = fashion_mnist_like(16 * args.cnn_batch, seed=7 + rank, device=device)
     batches = [(imgs[i * args.cnn_batch:(i + 1) * args.cnn_batch], labels[i * args.cnn_batch:(i + 1) * args.cnn_batch])
                for i in range(16)]
     elapsed, loss = time_steps(runner, batches, args.cnn_steps, max(args.warmup, 5), device, world)
     ar = time_allreduce(flat, device, world)
+    comm = None
     if ddp is not None:
+        comm = ddp.comm
         ddp.close()
     v = world * args.cnn_batch * args.cnn_steps / elapsed
     return {"samples_per_s": round(v, 1), "ms_per_step": round(elapsed / args.cnn_steps * 1000, 4),
             "vs_baseline": round(v / BASELINE_CNN, 2), "final_loss": round(float(loss), 4),
             "dtype": dtype, "global_batch": world * args.cnn_batch, "steps": args.cnn_steps,
-            "allreduce_ms": ar, "grad_bytes": flat.numel * 4,
+            "allreduce_ms": ar, "grad_bytes": flat.numel * 4, "comm": comm,
             "config": f"FashionMNISTModel fused HIP kernel ({'bf16 MFMA' if dtype == 'bf16' else 'fp32'} convs), "
                       f"batch {args.cnn_batch}/GPU, SGD lr0.01, dp{world}",
             "baseline_ref": "BASELINE.md §2 CNN CPU proxy 5,655 samples/s (1 proc x 8 threads)"}
+
+
+def bench_cnn_recipe(args, rank, world, device, dtype="bf16"):
+    """The CNN exactly as the recipe trains it (sparkmi/recipes/cnn.py -> Trainer.fit): a 60,000-image
+    HBM-resident uint8 shard per executor, a fresh shuffle every epoch, each step gathering its batch
+    inside the step graph (DeviceLoader fixed=True), multi-step graphs of ``unroll`` steps, device-side
+    loss metrics — the path a user of examples/distributed_cnn.py gets, timed like the headline CNN
+    step (both numbers side by side)."""
+    import dataclasses
+    import torch
+    from sparkmi.data.dataset import DeviceLoader
+    from sparkmi.data.synthetic import fashion_mnist_like
+    from sparkmi.models.cnn import FashionMNISTModel
+    from sparkmi.optim import SGD
+    from sparkmi.parallel import barrier
+    from sparkmi.recipes.cnn import CNNConfig
+    from sparkmi.train.trainer import Trainer
+    fresh_model_state(4321)
+    n = 60000
+    x, y = fashion_mnist_like(n, seed=17 + rank)
+    cfg = CNNConfig(world=world, batch_size=args.cnn_batch, lr=0.01, conv_dtype=dtype, log_every=10 ** 9,
+                    verbose=False, graph=args.graph != "off", unroll=8)
+    loader = DeviceLoader([x, y], cfg.batch_size, device, shuffle=True, drop_last=True, seed=1000 * rank, fixed=True)
+    model = FashionMNISTModel(1, 10, 10, dtype=dtype)
+    tr = Trainer(model, lambda m, a, b: m.loss(a, b), lambda flat: SGD(flat, lr=cfg.lr), cfg, device, rank, world,
+                 "cnn_bench", shadow=False, fused_step=lambda m, o, a, b: m.fused_sgd_step(o, a, b),
+                 fused_grad=lambda m, a, b: m.fused_grad_step(a, b))
+    warm = max(args.warmup, 5) + 2 * tr.runner.unroll
+    tr.cfg = dataclasses.replace(cfg, max_steps=warm)
+    tr.fit(loader, 10 ** 6)
+    _sync(device)
+    barrier()
+    _sync(device)
+    t0 = time.perf_counter()
+    tr.cfg = dataclasses.replace(cfg, max_steps=warm + args.cnn_steps)
+    res = tr.fit(loader, 10 ** 6)
+    _sync(device)
+    barrier()
+    _sync(device)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    steps = res["steps"]
+    tr.close()
+    v = world * args.cnn_batch * steps / elapsed
+    return {"samples_per_s": round(v, 1), "ms_per_step": round(elapsed / steps * 1000, 4), "steps": steps,
+            "final_loss": round(res["final_loss"], 4), "dtype": dtype, "global_batch": world * args.cnn_batch,
+            "vs_baseline": round(v / BASELINE_CNN, 2),
+            "config": f"Trainer.fit over a shuffled 60k-image HBM shard per executor, batch gather in the step graph, "
+                      f"{cfg.unroll}-step graphs, dp{world}"}
 
 
 def bench_lstm(args, rank, world, device):
@@ -462,7 +520,7 @@ def main():
         dtypes = ["fp32", "bf16"]
     else:
         dtypes = [args.dtype]
-    cnn = cnn32 = lstm = mlp = None
+    cnn = cnn32 = cnn_recipe = lstm = mlp = None
 
     def side(fn, *a):
         # an extra workload that raises must not take the headline down with it (ranks raise
@@ -477,6 +535,7 @@ def main():
         # BASELINE's CNN config is bf16 (Conv2d on matrix cores); the fp32 kernel is reported too
         cnn32 = side(bench_cnn, args, rank, world, device, "fp32")
         cnn = side(bench_cnn, args, rank, world, device, "bf16") if device.type == "cuda" else cnn32
+        cnn_recipe = side(bench_cnn_recipe, args, rank, world, device, "bf16" if device.type == "cuda" else "fp32")
     if args.model in ("all", "aux") and not args.no_aux:
         lstm = side(bench_lstm, args, rank, world, device)
         mlp = side(bench_mlp, args, rank, world, device)
@@ -494,7 +553,7 @@ def main():
                               "dtype": cnn["dtype"], "data": "synthetic",
                               "config": {"model": "FashionMNISTModel", "global_batch": cnn["global_batch"],
                                          "seq_len": None, "parallelism": f"dp{world}"}, "cnn": cnn,
-                              "cnn_fp32": cnn32}))
+                              "cnn_fp32": cnn32, "cnn_recipe_path": cnn_recipe}))
         destroy()
         return
     tr = {dt: bench_transformer(args, rank, world, device, dt) for dt in dtypes}
@@ -556,6 +615,7 @@ def main():
         if cnn is not None:
             out["cnn"] = cnn
             out["cnn_fp32"] = cnn32
+            out["cnn_recipe_path"] = cnn_recipe
         if lstm is not None:
             out["extra"] = {"lstm": lstm, "mlp": mlp,
                             "aux_baseline_ref": "BASELINE.md §2 best CPU proxy: LSTM 1,365, MLP 130,476 samples/s"}

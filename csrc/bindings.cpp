@@ -100,6 +100,7 @@ int smi_emb_sum(int, int, const long long*, const void*, float*, long, int, long
 int smi_emb_pair(int);
 int smi_cnn_reduce(const CNNArgs*, hipStream_t);
 int smi_gather_rows(const void*, const long long*, void*, long, long, hipStream_t);
+int smi_gather_batch(const void* const*, void* const*, const long*, int, const long long*, int*, unsigned*, int, hipStream_t);
 int smi_gather_u8_scale(const void*, const long long*, void*, long, long, float, int, hipStream_t);
 int smi_lstm(const LSTMArgs*, int, hipStream_t);
 int smi_lstm_supported(int, int, int, int);
@@ -486,6 +487,15 @@ PYBIND11_MODULE(_C, m) {
                                  T.data(), (int)c, S(st)),
         "gemm_f32_wgrad_group");
   });
+  m.def("gather_batch", [](std::vector<u> src, std::vector<u> out, std::vector<long> row_bytes, u perm, u cursor,
+                           u done, int B, u st) {
+    if (src.size() != out.size() || src.size() != row_bytes.size()) throw std::runtime_error("gather_batch: sizes");
+    std::vector<const void*> s(src.size());
+    std::vector<void*> o(out.size());
+    for (size_t i = 0; i < src.size(); ++i) { s[i] = P(src[i]); o[i] = P(out[i]); }
+    chk(smi_gather_batch(s.data(), o.data(), row_bytes.data(), (int)src.size(), (const long long*)perm, (int*)cursor,
+                         (unsigned*)done, B, S(st)), "gather_batch");
+  }, "out_a[i] = src_a[perm[cursor * B + i]] for up to 4 arrays, then cursor += 1 (device cursor)");
   m.def("gather_rows", [](u src, u idx, u out, long n, long row_bytes, u st) {
     chk(smi_gather_rows(P(src), (const long long*)idx, P(out), n, row_bytes, S(st)), "gather_rows");
   });
@@ -534,6 +544,27 @@ PYBIND11_MODULE(_C, m) {
     a.loss_scale = loss_scale; a.train = 1; a.fused = 1;
     a.lr = (const float*)lr; a.step = (float*)step; a.tick = (unsigned*)tick;
     chk(smi_cnn(&a, S(st)), "cnn_sgd_step");
+  });
+  // the same launch in GRADIENT mode (the data-parallel step): the tail adds the batch gradient
+  // to gw / gb (the flat gradient buffer) instead of updating the parameters
+  m.def("cnn_grad_step", [](u x, int x_u8, float x_scale, u y, int B, int cin, int C, int classes, std::vector<u> w,
+                            std::vector<u> b, std::vector<u> gw, std::vector<u> gb, u slab, u part, u row_loss, u loss,
+                            float loss_scale, u tick, int bf16, u st) {
+    CNNArgs a{};
+    a.bf16 = bf16;
+    if (w.size() != 5 || b.size() != 5 || gw.size() != 5 || gb.size() != 5)
+      throw std::runtime_error("cnn_grad_step: need 5 weight, bias, weight-gradient and bias-gradient pointers");
+    a.x = (const void*)x; a.x_u8 = x_u8; a.x_scale = x_scale; a.y = (const long long*)y;
+    a.B = B; a.cin = cin; a.C = C; a.classes = classes;
+    for (int i = 0; i < 5; ++i) {
+      a.w[i] = (const float*)w[i]; a.b[i] = (const float*)b[i]; a.gw[i] = (float*)gw[i]; a.gb[i] = (float*)gb[i];
+    }
+    const int sz[10] = {C * cin * 9, C, C * C * 9, C, C * C * 9, C, C * C * 9, C, classes * C * 49, classes};
+    int o = 0;
+    for (int i = 0; i < 10; ++i) { a.off[i] = o; o += sz[i]; }
+    a.P = o; a.slab = (float*)slab; a.part = (float*)part; a.row_loss = (float*)row_loss; a.loss = (float*)loss;
+    a.loss_scale = loss_scale; a.train = 1; a.fused = 1; a.lr = nullptr; a.tick = (unsigned*)tick;
+    chk(smi_cnn(&a, S(st)), "cnn_grad_step");
   });
   m.def("attn_ae", [](int set) { return smi_attn_ae(set); },
         "fp32 attention outputs (forward and backward): 1 = whole-row stores through LDS (default), 0 = per-lane stores; -1 queries");

@@ -514,6 +514,10 @@ __device__ __forceinline__ int cnn_cs(const CNNArgs& g) { return (g.off[8] + 3) 
 // (image order) and the step counter.  Hand-offs are write-through stores + device-scope loads in
 // 16-B granules (smi_common.h), no L2 fences.  Deterministic: every sum has a fixed order.  No
 // spinning: a workgroup that is not the last simply exits.
+// GRADIENT mode (lr == null; the data-parallel step): the same two levels, but level 2 ADDS the
+// batch gradient to gw / gb (the flat fp32 gradient buffer, reduced across executors next and
+// consumed by the optimizer) instead of updating the parameters: g += batch sum, written as
+// g - (-1) * sum so both modes share one code path (exact), no step bump, no shadows.
 __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float* sm) {
   __shared__ int last;
   const int ngrp = (g.B + CNN_GRP - 1) / CNN_GRP;
@@ -555,7 +559,12 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
   // level 2.  Stage every image's dl / p2 row (R4 floats) in LDS (the activation planes are free),
   // sum the conv group partials in group order and form the fc gradient from the staged rows
   const int R4 = (NC + F + 3) & ~3, ns4 = g.B * (R4 >> 2);
-  const float lr = g.lr[0];
+  const bool gmode = g.lr == nullptr;
+  const float lr = gmode ? -1.f : g.lr[0];
+  // the tensor level 2 updates for slab segment seg: the parameter, or (gradient mode) its gradient
+  auto dst_of = [&](int seg) -> float* {
+    return gmode ? (seg % 2 == 0 ? g.gw[seg / 2] : g.gb[seg / 2]) : const_cast<float*>(seg % 2 == 0 ? g.w[seg / 2] : g.b[seg / 2]);
+  };
   float rl = 0.f;  // lane i: row losses i, i + 64, ...
   if (threadIdx.x < 64)
     for (int i = threadIdx.x; i < g.B; i += 64) rl += smi_cc_load(g.row_loss + i);
@@ -565,20 +574,20 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
   const int h = H == 2 ? (int)threadIdx.x / F : 0, ob = H == 2 ? 2 * h : 0;
   const int i0 = (int)threadIdx.x - h * F;
   const bool fc_on = h < H && i0 < F;
-  float* fw = const_cast<float*>(g.w[4]);
+  float* fw = dst_of(8);
   auto fc_load = [&](int i, float* pv) {  // column i's parameters (clamped addresses: no branch)
 #pragma unroll
     for (int t = 0; t < 16; ++t) pv[t] = fw[min(4 * ob + t, NC - 1) * F + min(max(i, 0), F - 1)];
   };
   float pfc[16];  // the thread's first column, loaded with the level's other loads
   fc_load(i0, pfc);
-  float* fb = const_cast<float*>(g.b[4]);
+  float* fb = dst_of(9);
   const float pb = fb[min((int)threadIdx.x, NC - 1)];
   auto conv_seg = [&](int p, int& seg, int& r) {
     seg = 0;
     while (seg < 7 && p >= g.off[seg + 1]) ++seg;
     r = p - g.off[seg];
-    return (float*)(seg % 2 == 0 ? g.w[seg / 2] : g.b[seg / 2]) + r;
+    return dst_of(seg) + r;
   };
   struct Conv4 { float pv[4]; float4 c[4]; };  // group partials 0..3 (batches up to 32 images)
   auto conv_load = [&](int q4, Conv4& k) {
@@ -737,7 +746,7 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
     const float ls = wave_sum(rl);
     if (threadIdx.x == 0) {
       if (g.loss) g.loss[0] = ls * g.loss_scale;
-      if (g.step) g.step[0] += 1.f;
+      if (g.step && !gmode) g.step[0] += 1.f;
       g.tick[CNN_GRP] = 0u;
     }
   }
@@ -995,7 +1004,13 @@ static size_t cnn_lds_bytes(const CNNArgs& g) {
 extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
   CNNArgs g = *args;
   // the fused tail's group tickets are tick[0 .. ngrp) below the level-2 ticket tick[CNN_GRP]
-  if (g.fused && (g.P % 4 || (g.B + CNN_GRP - 1) / CNN_GRP > CNN_GRP || !g.part || !g.tick || !g.lr || !g.slab || !g.row_loss || !g.train)) return -1;
+  if (g.fused && (g.P % 4 || (g.B + CNN_GRP - 1) / CNN_GRP > CNN_GRP || !g.part || !g.tick || !g.slab || !g.row_loss || !g.train)) return -1;
+  if (g.fused && !g.lr) {  // gradient mode: every gradient destination, no shadows
+    for (int i = 0; i < 5; ++i)
+      if (!g.gw[i] || !g.gb[i]) return -1;
+    for (int i = 0; i < 10; ++i)
+      if (g.shadow[i]) return -1;
+  }
   if (g.C < 1 || g.C > CNN_MAXC || g.cin < 1 || g.cin > 4 || g.classes < 1 || g.classes > 16) return -1;
   g.wstage = g.bf16 ? 1 : 0;
   if (g.wstage && cnn_lds_bytes(g) > 160 * 1024) g.wstage = 0;  // the weights then stay global

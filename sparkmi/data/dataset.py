@@ -135,10 +135,18 @@ class DeviceLoader:
     ``arrays`` are uploaded once to ``device``; each epoch draws a device-side permutation
     (seeded by seed+epoch: reproducible, identical on every run) and yields gathered batches.
     ``image_scale`` applies the uint8 -> float ``/255`` of torchvision's ToTensor inside the
-    gather (first tensor only)."""
+    gather (first tensor only).
+
+    ``fixed=True`` (GPU, drop_last, no image_scale): every batch lands in the SAME static buffers,
+    gathered by ONE kernel that reads the epoch's permutation at a device-side cursor and advances
+    it (csrc/kernels/gather.hip gather_batch).  ``pre_step()`` launches that gather; a training
+    loop that installs it into its step (Trainer -> StepRunner.pre_step, ``deferred = True``) gets
+    the gather captured inside the step's HIP graph — a replayed graph, or a multi-step graph of
+    several steps, draws its own shuffled batches with no host work per step.  Without a consumer
+    (``deferred`` False) iteration gathers eagerly, so the yielded tensors always hold the batch."""
 
     def __init__(self, arrays, batch_size, device, shuffle=True, drop_last=False, seed=0, image_scale=None,
-                 image_dtype=torch.float32):
+                 image_dtype=torch.float32, fixed=False):
         self.device = torch.device(device)
         self.arrays = [torch.as_tensor(a).to(self.device) for a in arrays]
         self.n = len(self.arrays[0])
@@ -146,6 +154,23 @@ class DeviceLoader:
         self.image_scale, self.image_dtype = image_scale, image_dtype
         self.epoch = 0
         self.skip = 0  # batches of the current epoch already consumed (exact resume)
+        self.fixed = bool(fixed and drop_last and image_scale is None and self.device.type == "cuda"
+                          and len(self.arrays) <= 4 and _native.use_native(self.arrays[0]))
+        self.deferred = False
+        if self.fixed:
+            B = batch_size
+            self.static = [torch.empty((B,) + tuple(a.shape[1:]), dtype=a.dtype, device=self.device)
+                           for a in self.arrays]
+            self._perm_buf = torch.empty(self.n, dtype=torch.int64, device=self.device)
+            self._cursor = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self._done = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self._row_bytes = [a[0].numel() * a.element_size() for a in self.arrays]
+
+    def pre_step(self):
+        """Gather the next batch (device cursor) into the static buffers: one launch, graph-safe."""
+        _native.C().gather_batch([a.data_ptr() for a in self.arrays], [t.data_ptr() for t in self.static],
+                                 self._row_bytes, self._perm_buf.data_ptr(), self._cursor.data_ptr(),
+                                 self._done.data_ptr(), self.batch_size, _native.stream())
 
     def set_epoch(self, e):
         self.epoch = e
@@ -163,6 +188,16 @@ class DeviceLoader:
     def __iter__(self):
         perm = self._perm()
         start, self.skip = self.skip, 0
+        if self.fixed:
+            # stream-ordered before every gather of the epoch (eager or replayed)
+            self._perm_buf.copy_(perm)
+            self._cursor.fill_(start)
+            for b in range(start, len(self)):
+                if not self.deferred:
+                    self.pre_step()
+                yield tuple(self.static)
+            self.epoch += 1
+            return
         for b in range(start, len(self)):
             idx = perm[b * self.batch_size:(b + 1) * self.batch_size]
             out = []

@@ -8,7 +8,7 @@ state_dicts load.  ``loss(x, y)`` runs the fused whole-network HIP kernel (spark
 import torch
 from torch import nn
 
-from ..ops.cnn import cnn_logits, cnn_loss, cnn_sgd_step
+from ..ops.cnn import cnn_grad_step, cnn_logits, cnn_loss, cnn_sgd_step
 
 
 class FashionMNISTModel(nn.Module):
@@ -61,6 +61,24 @@ class FashionMNISTModel(nn.Module):
             shadows = [flat.shadow[o:o + p.numel()] for p, o in zip(params, offs)]
         return cnn_sgd_step(x.contiguous(), y.to(torch.int64).contiguous(), params, opt.lr_t, opt.step_t,
                             self._step_tick, shadows, self.conv_dtype == "bf16")
+
+    def fused_grad_step(self, x, y):
+        """Forward, mean CE, backward and the batch gradient sum as ONE HIP launch, the gradient
+        added to the parameters' flat fp32 gradient slices (the data-parallel step's local half:
+        all-reduce and optimizer follow; csrc/kernels/cnn.hip gradient mode).  Returns the loss,
+        or None when it does not apply (CPU, parameters outside a FlatParams buffer, a batch the
+        kernel's LDS cannot stage): the caller then runs loss() and backward()."""
+        from .. import _native
+        from ..ops._grad import grad_buf
+        params = self.param_list()
+        if (not x.is_cuda or not _native.use_native(x) or x.dim() != 4
+                or getattr(self, "_smi_flat", None) is None
+                or not _native.C().cnn_fused_ok(params[0].shape[0], params[0].shape[1], params[8].shape[0],
+                                                 x.shape[0])):
+            return None
+        grads = [grad_buf(p) for p in params]
+        return cnn_grad_step(x.contiguous(), y.to(torch.int64).contiguous(), params, grads, self._step_tick,
+                             self.conv_dtype == "bf16")
 
     def loss(self, x, y):
         """Mean CE over the batch (distributed_cnn.py:141,177)."""

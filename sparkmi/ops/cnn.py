@@ -134,3 +134,26 @@ def cnn_sgd_step(x, y, params, lr_t, step_t, tick, shadows=None, bf16=False):
                              row_loss.data_ptr(), loss.data_ptr(), 1.0 / B, lr_t.data_ptr(), step_t.data_ptr(),
                              tick.data_ptr(), int(bf16), _native.stream())
     return loss[0]
+
+
+def cnn_grad_step(x, y, params, grads, tick, bf16=False):
+    """Forward, mean CE, backward and the gradient reduction over the batch as ONE launch, the
+    batch gradient ADDED to ``grads`` (10 fp32 tensors: the flat gradient buffer's slices) — the
+    data-parallel step's local half (csrc/kernels/cnn.hip gradient mode): the executors'
+    gradients are then all-reduced and the optimizer applies them.  Returns the mean loss."""
+    B = x.shape[0]
+    w = [params[i] for i in (0, 2, 4, 6, 8)]
+    b = [params[i] for i in (1, 3, 5, 7, 9)]
+    P = num_params(params)
+    slab = torch.empty(B, P, device=x.device, dtype=torch.float32)
+    grp = _native.C().cnn_grp()
+    part = torch.empty((B + grp - 1) // grp, P, device=x.device, dtype=torch.float32)
+    row_loss = torch.empty(B, device=x.device, dtype=torch.float32)
+    loss = torch.empty(1, device=x.device, dtype=torch.float32)
+    _native.C().cnn_grad_step(x.data_ptr(), int(x.dtype == torch.uint8), 1.0 / 255.0, y.data_ptr(), B, x.shape[1],
+                              w[0].shape[0], w[4].shape[0], [t.data_ptr() for t in w], [t.data_ptr() for t in b],
+                              [grads[i].data_ptr() for i in (0, 2, 4, 6, 8)],
+                              [grads[i].data_ptr() for i in (1, 3, 5, 7, 9)], slab.data_ptr(), part.data_ptr(),
+                              row_loss.data_ptr(), loss.data_ptr(), 1.0 / B, tick.data_ptr(), int(bf16),
+                              _native.stream())
+    return loss[0]

@@ -4,8 +4,10 @@ Reference: batch 32, SGD lr 0.01, CE, 3 epochs, FashionMNISTModel(1, 10, 10)
 (distributed_cnn.py:109-147).  Differences by design: every executor trains on its own disjoint
 shard of the TRAIN set (the reference iterated the test loader, Q3, through a sampler fixed to
 rank 0 of 2, Q2) and gradients really are averaged (Q1).  The shard is uploaded to HBM once as
-uint8; each step is one fused HIP kernel for forward+backward of the whole network plus the
-fused SGD update, captured in a HIP graph on a single executor.
+uint8; each step is the batch gather (device cursor, sparkmi/data/dataset.py DeviceLoader
+fixed=True) + one fused HIP kernel for forward+backward of the whole network and the SGD update
+on a single executor (data-parallel: the kernel leaves the batch gradient, then the IPC
+all-reduce and SGD), replayed as multi-step HIP graphs (cfg.unroll steps per launch).
 """
 import dataclasses
 
@@ -50,12 +52,14 @@ def train_fn(cfg):
     rank, world, device = setup_executor(cfg)
     (xtr, ytr), (xte, yte), source = load_data(cfg)
     idx = torch.from_numpy(shard(len(ytr), rank, world, cfg.seed))
+    # fixed-buffer loader: each step gathers its shuffled batch inside the step's HIP graph
     loader = DeviceLoader([xtr[idx], ytr[idx]], cfg.batch_size, device, shuffle=True, drop_last=True,
-                          seed=cfg.seed + 1000 * rank)
+                          seed=cfg.seed + 1000 * rank, fixed=True)
     torch.manual_seed(cfg.seed)
     model = FashionMNISTModel(1, cfg.hidden_units, 10, dtype=cfg.conv_dtype)
     trainer = Trainer(model, lambda m, x, y: m.loss(x, y), lambda flat: SGD(flat, lr=cfg.lr), cfg, device, rank,
-                      world, "cnn", shadow=False, fused_step=lambda m, o, x, y: m.fused_sgd_step(o, x, y))
+                      world, "cnn", shadow=False, fused_step=lambda m, o, x, y: m.fused_sgd_step(o, x, y),
+                      fused_grad=lambda m, x, y: m.fused_grad_step(x, y))
     stats = trainer.fit(loader, cfg.epochs)
     trainer.close()
     out = dict(stats, data=source, world=world, train_samples_per_rank=len(idx))

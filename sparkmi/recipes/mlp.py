@@ -55,8 +55,11 @@ def train_fn(cfg):
     xtr, ytr = train_df.to_torch()
     xte, yte = test_df.to_torch()
     idx = torch.from_numpy(shard(len(ytr), rank, world, cfg.seed))
-    loader = DeviceLoader([xtr[idx], ytr[idx]], cfg.batch_size, device, shuffle=True, drop_last=False,
-                          seed=cfg.seed + 1000 * rank)
+    full = len(idx) % cfg.batch_size == 0
+    # whole batches only: the fixed-buffer loader (each step gathers its shuffled batch inside the
+    # step's HIP graph); a ragged last batch keeps the per-batch gather
+    loader = DeviceLoader([xtr[idx], ytr[idx]], cfg.batch_size, device, shuffle=True, drop_last=full,
+                          seed=cfg.seed + 1000 * rank, fixed=full)
     torch.manual_seed(cfg.seed)
     layers = [int(v) for v in cfg.layers.split(",")]
     model = MultilayerPerceptron(layers)

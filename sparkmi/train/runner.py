@@ -28,7 +28,7 @@ from ..ops.embedding import join_plans
 
 class StepRunner:
     def __init__(self, model, loss_fn, optimizer, ddp=None, graph=False, warmup_eager=3, split_fn=None,
-                 fused_step=None, bind_inputs=False, max_bound=32):
+                 fused_step=None, bind_inputs=False, max_bound=32, fused_grad=None):
         self.model = model
         # bind_inputs: batches that live at fixed device addresses (an HBM-resident dataset's
         # batch views) are read IN PLACE by a graph captured per batch (shared memory pool, at
@@ -45,6 +45,17 @@ class StepRunner:
         # fused_step(model, optimizer, *batch) -> loss or None: a whole single-executor step in
         # one kernel (e.g. MultilayerPerceptron.fused_sgd_step); None falls back to the chain
         self.fused_step = fused_step
+        # fused_grad(model, *batch) -> loss or None: forward + backward in one kernel, the batch
+        # gradient added to the flat gradient buffer (e.g. FashionMNISTModel.fused_grad_step); the
+        # gradient reduction (data-parallel) and the optimizer follow as usual — a data-parallel
+        # small-model step is then that kernel + the IPC all-reduce + the optimizer
+        self.fused_grad = fused_grad
+        # pre_step(): launches that produce the step's inputs in place (e.g. DeviceLoader(fixed=
+        # True).pre_step: the next shuffled batch gathered at a device cursor into the buffers the
+        # step reads).  Bound / multi-step graphs capture it with the step; every other mode runs
+        # it eagerly before the step (before the static-input copy of a copying graph)
+        self.pre_step = None
+        self._pre_inline = False
         self.loss_fn = loss_fn          # loss_fn(model, *batch) -> scalar loss tensor
         self.split_fn = split_fn        # split_fn(model, *batch) -> (loss, leaf, root), see module doc
         self.graph2 = None              # split mode: the lower segments' backward graphs
@@ -115,12 +126,16 @@ class StepRunner:
         return e
 
     def _eager(self, *batch):
+        if self._pre_inline and self.pre_step is not None:
+            self.pre_step()
         if self.fused_step is not None and self.ddp is None:
             loss = self.fused_step(self.model, self.opt, *batch)
             if loss is not None:
                 return loss
         e0 = self._event()
-        loss = self._fwd_bwd(*batch)
+        loss = self.fused_grad(self.model, *batch) if self.fused_grad is not None else None
+        if loss is None:
+            loss = self._fwd_bwd(*batch)
         e1 = self._event()
         if self.ddp is not None:
             self.ddp.finish()
@@ -249,8 +264,10 @@ class StepRunner:
         self.graph = g
 
     def _bind_ok(self):
-        return (self.bind_inputs and not self._dp and self.split_fn is None and not self.phase_timing
-                and not torch.cuda.is_current_stream_capturing())
+        # data-parallel too when the reduction is a plain kernel (IPC path, ddp.graph_safe): the
+        # bound / multi-step graphs then hold forward, backward, all-reduce and optimizer
+        return (self.bind_inputs and (not self._dp or self.ddp.graph_safe) and self.split_fn is None
+                and not self.phase_timing and not torch.cuda.is_current_stream_capturing())
 
     def _step_bound(self, batch):
         """Replay the graph captured for exactly these input tensors (capture it first if new);
@@ -262,18 +279,25 @@ class StepRunner:
                 return None
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self._bound_pool):
-                loss = self._eager(*batch)
+            self._pre_inline = True
+            try:
+                with torch.cuda.graph(g, pool=self._bound_pool):
+                    loss = self._eager(*batch)
+            finally:
+                self._pre_inline = False
             if self._bound_pool is None:
                 self._bound_pool = g.pool()
             self._opt_in_graph = True
             ent = self._bound[key] = (g, loss, batch)  # the batch stays referenced: its memory is the input
         ent[0].replay()
+        if self._dp:
+            self.ddp.bytes_reduced += self.ddp.flat.grad.numel() * 4
         return ent[1]
 
-    def _step_multi(self, group):
+    def _step_multi(self, group, losses=None):
         """Replay the graph holding the steps of ``group`` (a list of batches) back to back,
-        capturing it first if new; None when it cannot (cache full)."""
+        capturing it first if new; None when it cannot (cache full).  ``losses``: a list that
+        receives every step's loss (device scalars the graph rewrites each replay)."""
         key = tuple(tuple((b.data_ptr(), tuple(b.shape), b.dtype) for b in batch) for batch in group)
         ent = self._multi.get(key)
         if ent is None:
@@ -281,30 +305,42 @@ class StepRunner:
                 return None
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self._bound_pool):
-                for batch in group:
-                    loss = self._eager(*batch)
+            step_losses = []
+            self._pre_inline = True
+            try:
+                with torch.cuda.graph(g, pool=self._bound_pool):
+                    for batch in group:
+                        step_losses.append(self._eager(*batch))
+            finally:
+                self._pre_inline = False
             if self._bound_pool is None:
                 self._bound_pool = g.pool()
             self._opt_in_graph = True
-            ent = self._multi[key] = (g, loss, group)
+            ent = self._multi[key] = (g, step_losses[-1], group, step_losses)
         ent[0].replay()
+        if losses is not None:
+            losses.extend(ent[3])
         self.steps += len(group)
+        if self._dp:
+            self.ddp.bytes_reduced += self.ddp.flat.grad.numel() * 4 * len(group)
         return ent[1]
 
-    def run_steps(self, seq):
+    def run_steps(self, seq, losses=None):
         """Run one training step per batch of ``seq`` (a list of batch tuples), in order; returns
-        the last loss.  With ``bind_inputs`` and ``unroll`` > 1, each run of ``unroll``
-        consecutive batches replays as one multi-step graph (the same steps, one launch)."""
+        the last loss (``losses``: a list that receives every step's loss).  With ``bind_inputs``
+        and ``unroll`` > 1, each run of ``unroll`` consecutive batches replays as one multi-step
+        graph (the same steps, one launch)."""
         loss, i, U = None, 0, self.unroll
         while i < len(seq):
             if (U > 1 and i + U <= len(seq) and self.graph_requested and seq[i][0].is_cuda
                     and self.steps >= self.warmup_eager and self._bind_ok()):
-                out = self._step_multi(seq[i:i + U])
+                out = self._step_multi(seq[i:i + U], losses)
                 if out is not None:
                     loss, i = out, i + U
                     continue
             loss = self.step(*seq[i])
+            if losses is not None:
+                losses.append(loss)
             i += 1
         return loss
 
@@ -312,11 +348,15 @@ class StepRunner:
         self.steps += 1
         use_graph = self.graph_requested and batch[0].is_cuda
         if not use_graph or self.steps <= self.warmup_eager:
+            if self.pre_step is not None:
+                self.pre_step()
             return self._eager(*batch)
         if self._bind_ok():
             loss = self._step_bound(batch)
             if loss is not None:
                 return loss
+        if self.pre_step is not None:
+            self.pre_step()  # the inputs in place before the static-input copy below
         if self.graph is None:
             self._capture(batch)  # then replayed below for this step
         self._refresh_inputs(batch)

@@ -39,7 +39,7 @@ def setup_executor(cfg):
 
 class Trainer:
     def __init__(self, model, loss_fn, make_optimizer, cfg, device, rank=0, world=1, name="run", shadow=None,
-                 fused_step=None, split_fn=None, flops_per_sample=None):
+                 fused_step=None, split_fn=None, flops_per_sample=None, fused_grad=None):
         self.model = model.to(device)
         self.cfg = cfg
         self.device = torch.device(device)
@@ -53,8 +53,11 @@ class Trainer:
         use_graph = bool(cfg.graph) and self.device.type == "cuda"
         # split_fn (data-parallel): the backward as several graphs, finished gradient buckets
         # reduced while the rest of the backward runs (StepRunner)
+        # fused_step: a whole single-executor step in one kernel; fused_grad: forward + backward in
+        # one kernel (the data-parallel step's local half, reduction and optimizer follow)
         self.runner = StepRunner(self.model, loss_fn, self.opt, ddp=self.ddp, graph=use_graph,
                                  fused_step=fused_step if world == 1 else None,
+                                 fused_grad=fused_grad if world > 1 else None,
                                  split_fn=split_fn if (world > 1 and use_graph) else None)
         path = f"{cfg.metrics}.rank{rank}.jsonl" if cfg.metrics else None
         self.metrics = MetricsLogger(path, rank=rank, every=cfg.log_every, echo=cfg.verbose and rank == 0,
@@ -84,10 +87,40 @@ class Trainer:
                 from ..parallel import barrier
                 barrier()
 
+    def _bind_loader(self, loader):
+        """A fixed-buffer DeviceLoader: its gather runs inside the step (captured with it), the
+        graphs read its static buffers in place, and ``cfg.unroll`` steps replay as one
+        multi-step graph — the loop issues one launch per ``unroll`` shuffled steps."""
+        if not (getattr(loader, "fixed", False) and self.device.type == "cuda" and self.runner.graph_requested):
+            return 1
+        loader.deferred = True
+        self.runner.pre_step = loader.pre_step
+        self.runner.bind_inputs = True
+        self.runner.unroll = max(1, int(getattr(self.cfg, "unroll", 1)))
+        return self.runner.unroll
+
+    def _group(self, it, U):
+        """Up to U batches of ``it`` without crossing a log / checkpoint / max_steps boundary."""
+        cfg = self.cfg
+        n = U
+        for every in (cfg.log_every, cfg.ckpt_every if self.ckpt is not None else 0):
+            if every:
+                n = min(n, every - self.step % every)
+        if cfg.max_steps:
+            n = min(n, cfg.max_steps - self.step)
+        group = []
+        for _ in range(max(1, n)):
+            b = next(it, None)
+            if b is None:
+                break
+            group.append(b)
+        return group
+
     def fit(self, loader, epochs, samples_per_batch=None):
         """Train over ``loader`` (an epoch-seeded DeviceLoader-like iterable) for ``epochs``."""
         cfg = self.cfg
         self.maybe_resume()
+        U = self._bind_loader(loader)
         t0 = time.perf_counter()
         steps_run, last = 0, None
         done = False
@@ -103,28 +136,38 @@ class Trainer:
             while True:
                 td = time.perf_counter()
                 with trace.range("data"):
-                    batch = next(it, None)
-                if batch is None:
+                    group = self._group(it, U) if U > 1 else [b for b in (next(it, None),) if b is not None]
+                if not group:
                     break
                 data_s += time.perf_counter() - td
-                n = samples_per_batch or int(batch[0].shape[0])
+                n = samples_per_batch or int(group[0][0].shape[0])
                 with trace.range("step"):
-                    last = self.runner.step(*batch)
-                self.step += 1
-                steps_run += 1
-                i += 1
-                progress(self.step)  # heartbeat progress: a stuck collective stops this counter
-                if self.metrics.due():
-                    self.runner.check()  # a lost data-parallel peer fails the group here
-                    ph = self.runner.pop_phases()
-                    ddp_bytes = self.ddp.bytes_reduced if self.ddp is not None else 0
-                    extra = dict(ph, data_s=data_s / max(1, self.metrics.pending() + 1),
-                                 bytes_reduced=ddp_bytes - bytes0)
-                    bytes0, data_s = ddp_bytes, 0.0
-                    self.metrics.step(last, n * self.world, **extra)
-                else:
-                    self.metrics.step(last, n * self.world)
-                fault_point(self.step)
+                    if len(group) > 1:
+                        losses = []
+                        self.runner.run_steps(group, losses)
+                    else:
+                        losses = [self.runner.step(*group[0])]
+                # the group's losses summed once (one reduction, not one add per step): the metrics
+                # mean over the interval is unchanged (groups never cross a log boundary)
+                gsum = losses[0] if len(losses) == 1 else torch.stack([l.reshape(()) for l in losses]).sum()
+                last = losses[-1]
+                for j in range(len(losses)):
+                    lj = gsum if j == len(losses) - 1 else None
+                    self.step += 1
+                    steps_run += 1
+                    i += 1
+                    progress(self.step)  # heartbeat progress: a stuck collective stops this counter
+                    if self.metrics.due():
+                        self.runner.check()  # a lost data-parallel peer fails the group here
+                        ph = self.runner.pop_phases()
+                        ddp_bytes = self.ddp.bytes_reduced if self.ddp is not None else 0
+                        extra = dict(ph, data_s=data_s / max(1, self.metrics.pending() + 1),
+                                     bytes_reduced=ddp_bytes - bytes0)
+                        bytes0, data_s = ddp_bytes, 0.0
+                        self.metrics.step(lj, n * self.world, **extra)
+                    else:
+                        self.metrics.step(lj, n * self.world)
+                    fault_point(self.step)
                 if self.ckpt is not None and cfg.ckpt_every and self.step % cfg.ckpt_every == 0:
                     self.cursor = i
                     self._save(i)

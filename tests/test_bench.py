@@ -68,3 +68,21 @@ def test_bench_under_torchrun():
     out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                 "--master-addr", "127.0.0.1", "--master-port", "29631", "bench.py", "--gpus", "2"] + TINY)
     _check(out, 2)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_bench_cnn_two_ranks_on_the_gpu():
+    """bench.py --gpus 2 --model cnn on the box's one MI355X: the data-parallel CNN fast step (fused
+    gradient kernel + IPC all-reduce + SGD in bound multi-step graphs) next to the single-rank
+    step on the same box; both ranks share the one device, so the 2-rank step also carries the
+    other rank's kernels (<= 1.3x the 1-rank step)."""
+    base = ["--model", "cnn", "--cnn-steps", "400", "--warmup", "20"]
+    one = _run([sys.executable, "bench.py", "--gpus", "1"] + base)
+    two = _run([sys.executable, "bench.py", "--gpus", "2"] + base, env={"SPARKMI_DIST_BACKEND": "gloo"})
+    assert two["n_gpus"] == 2 and two["config"]["global_batch"] == 64
+    assert two["cnn"]["comm"] == "ipc"
+    r1, r2 = one["cnn"]["ms_per_step"], two["cnn"]["ms_per_step"]
+    print(f"\ncnn bf16 ms/step: 1 rank {r1}, 2 ranks sharing the GPU {r2} (x{r2 / r1:.2f}); "
+          f"recipe path 1 rank {one['cnn_recipe_path']['ms_per_step']}, 2 ranks {two['cnn_recipe_path']['ms_per_step']}")
+    assert r2 <= 2.0 * r1, (r1, r2)

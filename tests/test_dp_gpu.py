@@ -273,3 +273,70 @@ def test_lstm_dp_sparse_embedding_matches_single_process():
     p1, _ = launch(_small_dp, ("lstm", 5, False), {}, num_processes=1, use_gpu=True, env=env, log_sink=None,
                    timeout=280)
     torch.testing.assert_close(p2, p1, rtol=1e-4, atol=1e-5)
+
+
+# ---- the data-parallel CNN fast step: fused gradient kernel + IPC + SGD ----
+def _cnn_dp(steps, graph, bind, dtype="fp32"):
+    import torch
+    from sparkmi.data.synthetic import fashion_mnist_like
+    from sparkmi.models.cnn import FashionMNISTModel
+    from sparkmi.optim import SGD
+    from sparkmi.parallel import DataParallel, init_distributed
+    from sparkmi.train.runner import StepRunner
+    from sparkmi.utils.flat import FlatParams
+    rank, world, device = init_distributed()
+    torch.manual_seed(0)
+    m = FashionMNISTModel(1, 10, 10, dtype=dtype).to(device)
+    flat = FlatParams(m, shadow=False)
+    opt = SGD(flat, lr=0.05)
+    ddp = DataParallel(flat) if world > 1 else None
+    GB = 32
+    imgs, labels = fashion_mnist_like(steps * GB, seed=3, device=device)
+    per = GB // world
+    batches = [(imgs[i * GB + rank * per:i * GB + (rank + 1) * per].contiguous(),
+                labels[i * GB + rank * per:i * GB + (rank + 1) * per].contiguous()) for i in range(steps)]
+    runner = StepRunner(m, lambda mm, x, y: mm.loss(x, y), opt, ddp, graph=graph, warmup_eager=2,
+                        fused_step=(lambda mm, o, x, y: mm.fused_sgd_step(o, x, y)) if world == 1 else None,
+                        fused_grad=(lambda mm, x, y: mm.fused_grad_step(x, y)) if world > 1 else None,
+                        bind_inputs=bind)
+    if bind:
+        runner.unroll = 2
+        runner.run_steps(batches[:3])
+        runner.run_steps(batches[3:])
+    else:
+        for b in batches:
+            runner.step(*b)
+    torch.cuda.synchronize()
+    comm = None
+    if ddp is not None:
+        comm = ddp.comm
+        ddp.check()
+        ddp.close()
+    import torch.distributed as dist
+    out = flat.master.cpu().clone()
+    if world == 1:
+        return [out], comm
+    allr = [None] * world
+    dist.all_gather_object(allr, out)
+    return allr, comm
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("world", [2, 4])
+def test_cnn_dp_fused_step_matches_single_process(world):
+    """FashionMNISTModel data parallelism on the fast step: the fused kernel's gradient mode (batch
+    gradient added to the flat buffer in its ticketed tail), the IPC one-shot all-reduce and SGD,
+    eager and in bound multi-step HIP graphs.  Parameters are bitwise equal on every rank, and
+    world x (32 / world) == one process x 32 (the fused SGD step) to fp32 tolerance (different
+    summation orders)."""
+    env = {"SPARKMI_DIST_BACKEND": "gloo"}
+    (r1,), _ = launch(_cnn_dp, (7, False, False), {}, num_processes=1, use_gpu=True, env=env, log_sink=None,
+                      timeout=300)
+    for graph, bind in ((False, False), (True, True)):
+        rs, comm = launch(_cnn_dp, (7, graph, bind), {}, num_processes=world, use_gpu=True, env=env, log_sink=None,
+                          timeout=300)
+        assert comm == "ipc"
+        for q in rs[1:]:
+            assert torch.equal(rs[0], q), "ranks disagree"
+        torch.testing.assert_close(rs[0], r1, rtol=1e-4, atol=2e-6, msg=f"graph={graph} bind={bind}")
