@@ -523,14 +523,25 @@ def main():
     cnn = cnn32 = cnn_recipe = lstm = mlp = None
 
     def side(fn, *a):
-        # an extra workload that raises must not take the headline down with it (ranks raise
-        # together: every rank runs the same code on the same shapes); reported as its error
+        # an extra workload that raises must not take the headline down with it; reported as its
+        # error.  Every rank learns whether ANY rank failed (one MAX all-reduce of a flag) and all
+        # take the error branch together, so a rank that failed alone never walks into the next
+        # workload's collectives while its peers are still inside this one's
         if args.model != "all":
             return fn(*a)
+        out, err = None, None
         try:
-            return fn(*a)
+            out = fn(*a)
         except Exception as e:  # noqa: BLE001
-            return {"error": f"{type(e).__name__}: {e}"[:300]}
+            err = f"{type(e).__name__}: {e}"[:300]
+        if world > 1:
+            import torch.distributed as dist
+            flag = torch.tensor([1 if err else 0], dtype=torch.int32,
+                                device=device if dist.get_backend() == "nccl" else "cpu")
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+            if int(flag.item()) and err is None:
+                err = "failed on another rank"
+        return {"error": err} if err else out
     if args.model in ("all", "cnn"):
         # BASELINE's CNN config is bf16 (Conv2d on matrix cores); the fp32 kernel is reported too
         cnn32 = side(bench_cnn, args, rank, world, device, "fp32")

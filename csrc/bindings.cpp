@@ -100,6 +100,7 @@ int smi_emb_sum(int, int, const long long*, const void*, float*, long, int, long
 int smi_emb_pair(int);
 int smi_cnn_reduce(const CNNArgs*, hipStream_t);
 int smi_gather_rows(const void*, const long long*, void*, long, long, hipStream_t);
+int smi_sparse_rank_sum(const long long*, const float*, int*, float*, int, int, int, long, hipStream_t);
 int smi_gather_batch(const void* const*, void* const*, const long*, int, const long long*, int*, unsigned*, int, hipStream_t);
 int smi_gather_u8_scale(const void*, const long long*, void*, long, long, float, int, hipStream_t);
 int smi_lstm(const LSTMArgs*, int, hipStream_t);
@@ -496,6 +497,10 @@ PYBIND11_MODULE(_C, m) {
     chk(smi_gather_batch(s.data(), o.data(), row_bytes.data(), (int)src.size(), (const long long*)perm, (int*)cursor,
                          (unsigned*)done, B, S(st)), "gather_batch");
   }, "out_a[i] = src_a[perm[cursor * B + i]] for up to 4 arrays, then cursor += 1 (device cursor)");
+  m.def("sparse_rank_sum", [](u ids, u rows, u pos, u g, int W, int k, int d, long nrow, u st) {
+    chk(smi_sparse_rank_sum((const long long*)ids, (const float*)rows, (int*)pos, (float*)g, W, k, d, nrow, S(st)),
+        "sparse_rank_sum");
+  }, "g[v] = rank-order sum of the gathered (id, row) lists' rows of v (csrc/kernels/sparse_rows.hip)");
   m.def("gather_rows", [](u src, u idx, u out, long n, long row_bytes, u st) {
     chk(smi_gather_rows(P(src), (const long long*)idx, P(out), n, row_bytes, S(st)), "gather_rows");
   });

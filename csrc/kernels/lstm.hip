@@ -74,7 +74,8 @@ __device__ __forceinline__ void lstm_ce_tail(const LSTMArgs& a, int b, const flo
     float se = 0.f;
     for (int c = 0; c < C; ++c) se += __expf(s_plast[c] - m);
     const float lse = m + __logf(se);
-    const long long lab = a.ce_labels[b];
+    long long lab = a.ce_labels[b];
+    lab = lab < 0 ? 0 : (lab >= C ? C - 1 : lab);  // memory safety: the host passes ids in [0, C)
     smi_wt_store(a.ce_row + b, lse - s_plast[lab]);  // read by the last workgroup (smi_common.h)
     const float inv = 1.0f / (float)a.B;
     for (int c = 0; c < C; ++c) a.ce_dlast[(size_t)b * C + c] = (__expf(s_plast[c] - lse) - (c == lab ? 1.f : 0.f)) * inv;

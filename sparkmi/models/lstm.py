@@ -34,11 +34,25 @@ class LSTM(nn.Module):
         self.rng = _rng.DropoutRNG(seed)
         with _rng.salt_scope(salt_base):  # the model's own salt stream: masks independent of other models
             self.salt = _rng.new_salt()
+        # ticket counters of the fused kernels (forward CE, embedding side plan, weight-gradient
+        # column tiles; re-armed by the kernels): per model, so two models never share them; not
+        # part of the state_dict (reference key parity).  One launch of a model at a time: LSTM
+        # launches of ONE model on concurrent streams would share them.
+        self.register_buffer("_tick", torch.zeros(48, dtype=torch.int32), persistent=False)
+        self.last_ids = None
 
-    def sparse_rows(self):
-        """{embedding weight: the last batch's token ids}: its gradient touches only those rows
-        (DataParallel(sparse_rows=...), the optional row-sparse exchange of SURVEY §5.8)."""
-        return {self.embedding.weight: lambda: self.last_ids}
+    def sparse_rows(self, cap=None):
+        """{embedding weight: the last TRAINING batch's token ids}: its gradient touches only those
+        rows (DataParallel(sparse_rows=...), the optional row-sparse exchange of SURVEY §5.8).  The
+        ids are recorded only by a grad-enabled forward in training mode, so an evaluation pass
+        between training steps (no_grad or eval()) cannot redirect the exchange to its rows.
+        ``cap`` (e.g. batch * max sequence length): a fixed id-list capacity, no host sync."""
+        fn = lambda: self.last_ids  # noqa: E731
+        return {self.embedding.weight: (fn, int(cap)) if cap else fn}
+
+    def _record_ids(self, input_seq):
+        if self.training and torch.is_grad_enabled() and self.embedding.weight.requires_grad:
+            self.last_ids = input_seq
 
     def param_list(self):
         ps = [self.embedding.weight]
@@ -53,23 +67,26 @@ class LSTM(nn.Module):
         return z, z.clone()
 
     def forward(self, input_seq, hidden_in=None, mem_in=None):
-        self.last_ids = input_seq
+        self._record_ids(input_seq)
         return lstm_classifier(input_seq, hidden_in, mem_in, self.param_list(), self.num_layers,
                                dropout=self.dropout_p, training=self.training, rng=self.rng, salt=self.salt,
-                               padding_idx=self.padding_idx)
+                               padding_idx=self.padding_idx, tick=self._tick)
 
     def loss(self, input_seq, labels, hidden_in=None, mem_in=None):
         """CE on the last step's prediction (distributed_lstm.py:186-189); returns (loss, pred)."""
-        self.last_ids = input_seq
-        if input_seq.is_cuda and labels.dim() == 1:
+        self._record_ids(input_seq)
+        if (input_seq.is_cuda and labels.dim() == 1 and labels.is_cuda and labels.device == input_seq.device
+                and labels.dtype in (torch.int64, torch.int32)):
             # GPU: the CE of the last step is fused into the LSTM forward kernel's tail (row loss,
-            # head gradient, fixed-order mean through a ticket): no separate CE launches
+            # head gradient, fixed-order mean through a ticket): no separate CE launches.  Class
+            # ids must lie in [0, C) (the reference's labels - 1 of AG_NEWS, distributed_lstm.py:180;
+            # no ignore_index): the kernel clamps an out-of-range id rather than read out of bounds
             return lstm_classifier_ce(input_seq, labels, hidden_in, mem_in, self.param_list(), self.num_layers,
                                       dropout=self.dropout_p, training=self.training, rng=self.rng, salt=self.salt,
-                                      padding_idx=self.padding_idx)
+                                      padding_idx=self.padding_idx, tick=self._tick)
         last, _, _, _ = lstm_classifier_last(input_seq, hidden_in, mem_in, self.param_list(), self.num_layers,
                                              dropout=self.dropout_p, training=self.training, rng=self.rng,
-                                             salt=self.salt, padding_idx=self.padding_idx)
+                                             salt=self.salt, padding_idx=self.padding_idx, tick=self._tick)
         # sparkmi's CE kernel (csrc/kernels/cross_entropy.hip: fixed-order loss sum) instead of the
         # ATen softmax / nll_loss launches; the CPU path falls back to the same math in torch
         return cross_entropy(last, labels), last

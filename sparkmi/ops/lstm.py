@@ -68,6 +68,9 @@ class LSTMFn(torch.autograd.Function):
         """The forward launch; ``labels``: also the fused last-step CE (returns its extra outputs)."""
         ctx.set_materialize_grads(False)  # unused outputs get no zero-filled gradients
         L, p, rng, salt, pad_idx = meta[:5]
+        # the model's ticket block (meta[6]) or, for a bare op call, the per-device shared one
+        tick = meta[6] if len(meta) > 6 and meta[6] is not None else _ce_ticket(ids.device)
+        ctx.tick = tick
         emb, layers, w_fc, b_fc = unpack(params, L)
         B, T = ids.shape
         E, H, C = emb.shape[1], layers[0][1].shape[1], w_fc.shape[0]
@@ -87,7 +90,7 @@ class LSTMFn(torch.autograd.Function):
         if labels is not None:
             labels = labels.to(torch.int64).contiguous()
             ce = (torch.empty(B, device=dev, dtype=torch.float32), torch.empty(B, C, device=dev, dtype=torch.float32),
-                  torch.empty((), device=dev, dtype=torch.float32), _ce_ticket(dev))
+                  torch.empty((), device=dev, dtype=torch.float32), tick)
         # the embedding backward's id ordering, made by this launch on CUs the recurrence leaves
         # idle (csrc/kernels/lstm.hip lstm_emb_side); the backward only sums
         plan_ws = None
@@ -104,7 +107,7 @@ class LSTMFn(torch.autograd.Function):
                          emb.shape[0] if plan_ws is not None else 0, _native.ptr(plan_ws),
                          last.data_ptr(), 0, labels.data_ptr() if ce else 0, ce[0].data_ptr() if ce else 0,
                          ce[1].data_ptr() if ce else 0, ce[2].data_ptr() if ce else 0, ce[3].data_ptr() if ce else 0,
-                         0, 0, int(plan_ws is not None), _ce_ticket(dev)[1:].data_ptr(), _native.stream())
+                         0, 0, int(plan_ws is not None), tick[1:].data_ptr(), _native.stream())
         # (inside Function.forward grad mode is off: the embedding's needs_input_grad says whether
         # a backward will want the table gradient; the inputs before it: ids, [labels,] h0, c0, meta;
         # meta[5]: grad mode at the call)
@@ -172,7 +175,7 @@ class LSTMFn(torch.autograd.Function):
                          [lw[2].data_ptr() for lw in g_layers], [lw[3].data_ptr() for lw in g_layers],
                          g_fc.data_ptr(), g_bfc.data_ptr(), _native.ptr(dh0), _native.ptr(dc0), slab.data_ptr(),
                          _native.ptr(xe), emb.shape[0], _native.ptr(ews), 0, last_only, 0, 0, 0, 0,
-                         _ce_ticket(dev)[8:].data_ptr(), _native.ptr(dscale), plan[1] if plan is not None else 0,
+                         ctx.tick[8:].data_ptr(), _native.ptr(dscale), plan[1] if plan is not None else 0,
                          0, 0, _native.stream())
         ctx.emb_plan = None
         grad_ready(*orig)
@@ -188,9 +191,11 @@ EMB_IN_FORWARD = True
 
 
 def _ce_ticket(dev):
-    """Ticket counters (zeroed once, re-armed by the kernels), one block per device: [0] the fused
-    CE of the forward, [8:] the backward weight-gradient kernel's (L + 1) x 8 column-tile tickets —
-    each launch completes its ticket rounds before the next one on the stream starts."""
+    """Ticket counters (zeroed once, re-armed by the kernels) for op calls without a model's own
+    block (LSTM._tick): [0] the fused CE of the forward, [1] the embedding side plan, [8:] the
+    backward weight-gradient kernel's (L + 1) x 8 column-tile tickets.  Shared per device: such
+    calls must not run concurrently on different streams (each launch completes its ticket rounds
+    before the next one on its stream starts)."""
     t = _CE_TICKETS.get(dev)
     if t is None:
         t = _CE_TICKETS[dev] = torch.zeros(8 + 8 * 5, device=dev, dtype=torch.int32)
@@ -219,7 +224,7 @@ class LSTMCEFn(torch.autograd.Function):
 
 
 def lstm_classifier_ce(ids, labels, h0, c0, params, num_layers, dropout=0.0, training=True, rng=None, salt=0,
-                       padding_idx=None):
+                       padding_idx=None, tick=None):
     """(mean CE of pred[:, -1] against ``labels``, pred[:, -1]) — the classifier's training loss
     (distributed_lstm.py:186-189) with the CE fused into the GPU kernel; CPU: torch reference."""
     p = dropout if training else 0.0
@@ -227,13 +232,15 @@ def lstm_classifier_ce(ids, labels, h0, c0, params, num_layers, dropout=0.0, tra
     E, H, C = emb.shape[1], layers[0][1].shape[1], w_fc.shape[0]
     if ids.is_cuda and _native.use_native(ids) and supported(E, H, num_layers, C):
         pad = -1 if padding_idx is None else int(padding_idx)
-        return LSTMCEFn.apply(ids, labels, h0, c0, (num_layers, p, rng, salt, pad, torch.is_grad_enabled()), *params)
-    last, _, _, _ = lstm_classifier_last(ids, h0, c0, params, num_layers, dropout, training, rng, salt, padding_idx)
+        return LSTMCEFn.apply(ids, labels, h0, c0, (num_layers, p, rng, salt, pad, torch.is_grad_enabled(), tick),
+                              *params)
+    last, _, _, _ = lstm_classifier_last(ids, h0, c0, params, num_layers, dropout, training, rng, salt, padding_idx,
+                                         tick)
     return torch.nn.functional.cross_entropy(last, labels), last
 
 
 def lstm_classifier(ids, h0, c0, params, num_layers, dropout=0.0, training=True, rng=None, salt=0,
-                    padding_idx=None):
+                    padding_idx=None, tick=None):
     """pred, h_n, c_n of embedding -> LSTM(num_layers, dropout) -> linear head (every step)."""
     p = dropout if training else 0.0
     emb, layers, w_fc, _ = unpack(params, num_layers)
@@ -243,14 +250,15 @@ def lstm_classifier(ids, h0, c0, params, num_layers, dropout=0.0, training=True,
             raise NotImplementedError(f"sparkmi LSTM kernel: unsupported shape E={E} H={H} L={num_layers} C={C} "
                                       "(H in {16,32,64}, 4*H*L <= 512, E <= 2H and <= 64, C <= 16)")
         pad = -1 if padding_idx is None else int(padding_idx)
-        pred, hn, cn, _ = LSTMFn.apply(ids, h0, c0, (num_layers, p, rng, salt, pad, torch.is_grad_enabled()), *params)
+        pred, hn, cn, _ = LSTMFn.apply(ids, h0, c0, (num_layers, p, rng, salt, pad, torch.is_grad_enabled(), tick),
+                                       *params)
         return pred, hn, cn
     seed = rng.current() if (rng is not None and p > 0) else 0
     return reference_forward(ids, h0, c0, params, num_layers, p, seed, salt, padding_idx)
 
 
 def lstm_classifier_last(ids, h0, c0, params, num_layers, dropout=0.0, training=True, rng=None, salt=0,
-                         padding_idx=None):
+                         padding_idx=None, tick=None):
     """(pred[:, -1] contiguous, pred, h_n, c_n): the GPU kernel writes the last step's prediction
     as its own output, so a loss on it needs no slice copy and its backward no zero-filled dpred."""
     p = dropout if training else 0.0
@@ -258,7 +266,8 @@ def lstm_classifier_last(ids, h0, c0, params, num_layers, dropout=0.0, training=
     E, H, C = emb.shape[1], layers[0][1].shape[1], w_fc.shape[0]
     if ids.is_cuda and _native.use_native(ids) and supported(E, H, num_layers, C):
         pad = -1 if padding_idx is None else int(padding_idx)
-        pred, hn, cn, last = LSTMFn.apply(ids, h0, c0, (num_layers, p, rng, salt, pad, torch.is_grad_enabled()), *params)
+        pred, hn, cn, last = LSTMFn.apply(ids, h0, c0, (num_layers, p, rng, salt, pad, torch.is_grad_enabled(),
+                                                        tick), *params)
         return last, pred, hn, cn
-    pred, hn, cn = lstm_classifier(ids, h0, c0, params, num_layers, dropout, training, rng, salt, padding_idx)
+    pred, hn, cn = lstm_classifier(ids, h0, c0, params, num_layers, dropout, training, rng, salt, padding_idx, tick)
     return pred[:, -1, :].contiguous(), pred, hn, cn

@@ -31,14 +31,18 @@ module was called, so gradients were never synchronised).  Design for MI355X + R
   faster; ``SPARKMI_DP_PROBE=0`` sends them to RCCL without measuring.  Either way a bucket's
   reduction runs on a side stream (RCCL's own, or the IPC comm stream forked from the compute
   stream at launch and joined in ``finish()``), overlapped with the rest of the backward.
-* ``sparse_rows={param: ids_fn}`` (opt-in; SURVEY §5.8 item 5, the LSTM embedding of
-  /root/reference/distributed_lstm.py:115): a table whose gradient touches only the step's rows
-  is exchanged ROW-SPARSE instead of all-reduced dense — each rank de-duplicates its row ids
-  (``ids_fn()``, a device sort), all-gathers (ids, rows) padded to the largest rank's count and adds the
-  ranks' rows into the dense gradient in rank order (deterministic; untouched rows stay zero, so
-  any optimizer, Adam included, sees exactly the all-reduced gradient).  The LSTM's 12.3 MB table
-  moves B*T*(8 + 4*D) bytes per rank instead (4,128 rows: 0.56 MB).  Uses the process group, so a
-  DP step with sparse rows is not a single-graph (``graph_safe``) step.
+* ``sparse_rows={param: ids_fn or (ids_fn, cap)}`` (opt-in; SURVEY §5.8 item 5, the LSTM
+  embedding of /root/reference/distributed_lstm.py:115): a table whose gradient touches only the
+  step's rows is exchanged ROW-SPARSE instead of all-reduced dense — each rank de-duplicates its
+  row ids (``ids_fn()``, a device sort), gathers those rows (index_select, no table copy),
+  all-gathers the (ids, rows) lists and every rank sums each touched row's contributions IN RANK
+  ORDER into the gradient (csrc/kernels/sparse_rows.hip on the GPU: deterministic, only the touched
+  rows written; untouched rows stay zero, so any optimizer, Adam included, sees exactly the
+  all-reduced gradient).  The LSTM's 12.3 MB table moves B*T*(8 + 4*D) bytes per rank instead
+  (4,128 rows: 0.56 MB).  ``cap``: a fixed list length >= any rank's id count (e.g. B * max_len):
+  no host sync at all; without it the ranks agree on the longest list with one small all-reduce
+  read on the host each step.  Uses the process group, so a DP step with sparse rows is not a
+  single-graph (``graph_safe``) step.
 The CPU/gloo path runs the identical logic (multi-process CPU tests).
 """
 import os
@@ -78,8 +82,13 @@ class DataParallel:
     def __init__(self, flat, group=None, bucket_mb=64.0, overlap=True, broadcast=True, zero=False, ipc=None,
                  sparse_rows=None):
         self.flat = flat
-        # parameter index -> callable returning the step's touched row ids (row-sparse exchange)
-        self._sparse = {flat.index[id(p)]: fn for p, fn in (sparse_rows or {}).items()}
+        # parameter index -> callable returning the step's touched row ids (row-sparse exchange),
+        # and its optional fixed list capacity
+        self._sparse, self._sparse_cap, self._sparse_pos = {}, {}, {}
+        for p, fn in (sparse_rows or {}).items():
+            fn, cap = fn if isinstance(fn, tuple) else (fn, None)
+            self._sparse[flat.index[id(p)]] = fn
+            self._sparse_cap[flat.index[id(p)]] = cap
         if self._sparse and zero:
             raise ValueError("sparse_rows and zero=True do not combine (a sparse table has no owned piece)")
         self.group = group
@@ -285,9 +294,9 @@ class DataParallel:
 
     def _sparse_exchange(self, s, e, i):
         """Row-sparse reduction of parameter ``i``'s gradient (flat slice [s, e), rows of the
-        parameter's first dimension): unique local row ids (sorted; duplicates -> the dummy row V),
-        all-gather of the fixed-size (ids, rows) pairs, rank-order scatter-add into the dense
-        gradient (id lists padded to the largest rank's with the dummy row)."""
+        parameter's first dimension): unique local row ids (sorted; duplicates -> the dummy id
+        nrow), their rows gathered, an all-gather of the fixed-length (ids, rows) lists, and the
+        rank-order sum of every touched row written into the gradient."""
         p = self.flat.params[i]
         nrow = p.shape[0]
         d = p.numel() // nrow
@@ -297,13 +306,18 @@ class DataParallel:
         first = torch.ones_like(srt, dtype=torch.bool)
         first[1:] = srt[1:] != srt[:-1]
         uid = torch.where(first, srt, torch.full_like(srt, nrow))
-        # ranks may hold different numbers of ids (per-batch padded lengths): pad to the largest
-        kt = torch.tensor([uid.numel()], dtype=torch.int64, device=g.device)
-        dist.all_reduce(kt, op=dist.ReduceOp.MAX, group=self.group)
-        k = int(kt.item())
+        k = self._sparse_cap.get(i)
+        if k is None:
+            # ranks may hold different numbers of ids (per-batch padded lengths): the longest list
+            kt = torch.tensor([uid.numel()], dtype=torch.int64, device=g.device)
+            dist.all_reduce(kt, op=dist.ReduceOp.MAX, group=self.group)
+            k = int(kt.item())
+        elif uid.numel() > k:
+            raise ValueError(f"sparse_rows: {uid.numel()} ids exceed the list capacity {k}")
         if k > uid.numel():
             uid = torch.cat([uid, uid.new_full((k - uid.numel(),), nrow)])
-        rows = torch.cat([g, g.new_zeros(1, d)])[uid]
+        valid = uid < nrow
+        rows = g.index_select(0, uid.clamp(max=nrow - 1)) * valid[:, None].to(g.dtype)
         # (gloo moves host tensors: device rows of a gloo group are staged through host memory)
         host = g.is_cuda and dist.get_backend(self.group) == "gloo"
         su, sr = (uid.cpu(), rows.cpu()) if host else (uid, rows)
@@ -313,10 +327,22 @@ class DataParallel:
         dist.all_gather_into_tensor(all_rows, sr, group=self.group)
         if host:
             all_ids, all_rows = all_ids.to(g.device), all_rows.to(g.device)
-        dense = g.new_zeros(nrow + 1, d)
-        for r in range(self.world):  # rank order: ids are unique within a rank (but the dummy row)
-            dense.index_put_((all_ids[r * k:(r + 1) * k],), all_rows[r * k:(r + 1) * k], accumulate=True)
-        g.copy_(dense[:nrow])
+        from .. import _native
+        if g.is_cuda and _native.use_native(g):
+            pos = self._sparse_pos.get(i)
+            if pos is None or pos.shape[0] < self.world * nrow:
+                pos = self._sparse_pos[i] = torch.full((self.world * nrow,), -1, dtype=torch.int32, device=g.device)
+            _native.C().sparse_rank_sum(all_ids.data_ptr(), all_rows.contiguous().data_ptr(), pos.data_ptr(),
+                                        g.data_ptr(), self.world, k, d, nrow, _native.stream())
+        else:
+            # the same math in torch: touched rows zeroed, then each rank's rows added in rank order
+            # (ids unique within a rank: every index_add_ is collision-free, so the order is fixed)
+            touched = all_ids[all_ids < nrow]
+            g.index_fill_(0, touched, 0.0)
+            for r in range(self.world):
+                ir = all_ids[r * k:(r + 1) * k]
+                m = ir < nrow
+                g.index_add_(0, ir[m], all_rows[r * k:(r + 1) * k][m])
         self.bytes_reduced += k * (8 + 4 * d)  # bytes this rank contributed
 
     def reshard_optimizer(self, opt, old_ranges):

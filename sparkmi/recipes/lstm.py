@@ -107,8 +107,9 @@ def train_fn(cfg):
         loss, _ = m.loss(x, y)
         return loss
 
+    # sparse exchange list capacity: <sos> + at most max_len tokens + <eos> per sequence
     trainer = Trainer(model, loss_fn, lambda flat: Adam(flat, lr=cfg.lr), cfg, device, rank, world, "lstm",
-                      shadow=False)
+                      shadow=False, sparse_cap=cfg.batch_size * (cfg.max_len + 2))
     stats = trainer.fit(loader, cfg.epochs)
     trainer.close()
     out = dict(stats, world=world, vocab_size=len(vocab), padding_idx=pad)

@@ -39,14 +39,15 @@ def setup_executor(cfg):
 
 class Trainer:
     def __init__(self, model, loss_fn, make_optimizer, cfg, device, rank=0, world=1, name="run", shadow=None,
-                 fused_step=None, split_fn=None, flops_per_sample=None, fused_grad=None):
+                 fused_step=None, split_fn=None, flops_per_sample=None, fused_grad=None, sparse_cap=None):
         self.model = model.to(device)
         self.cfg = cfg
         self.device = torch.device(device)
         self.rank, self.world = rank, world
         self.flat = FlatParams(self.model, device=self.device, shadow=shadow)
         self.opt = make_optimizer(self.flat)
-        sparse = (self.model.sparse_rows() if getattr(cfg, "sparse_embedding", False)
+        # sparse_cap: a bound on the ids per step (fixed list length: no host sync in the exchange)
+        sparse = (self.model.sparse_rows(cap=sparse_cap) if getattr(cfg, "sparse_embedding", False)
                   and hasattr(self.model, "sparse_rows") else None)
         self.ddp = DataParallel(self.flat, bucket_mb=cfg.bucket_mb, zero=getattr(cfg, "zero", False),
                                 sparse_rows=sparse) if world > 1 else None

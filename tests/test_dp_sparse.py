@@ -19,7 +19,7 @@ cloudpickle.register_pickle_by_value(sys.modules[__name__])
 V, T, B = 300, 12, 4
 
 
-def _run(steps, sparse):
+def _run(steps, sparse, cap=None, eval_between=False):
     import torch
     from sparkmi.models.lstm import LSTM
     from sparkmi.optim import Adam
@@ -32,7 +32,7 @@ def _run(steps, sparse):
     flat = FlatParams(m)
     opt = Adam(flat, lr=1e-2)
     ws, r = world_size(), rank()
-    ddp = DataParallel(flat, bucket_mb=0.05, sparse_rows=m.sparse_rows() if sparse else None)
+    ddp = DataParallel(flat, bucket_mb=0.05, sparse_rows=m.sparse_rows(cap=cap) if sparse else None)
     runner = StepRunner(m, lambda mm, x, y: mm.loss(x, y)[0], opt, ddp, graph=False)
     g = torch.Generator().manual_seed(11)
     # a small id range so both ranks touch common rows and repeat ids within a batch
@@ -41,13 +41,20 @@ def _run(steps, sparse):
     lbl = torch.randint(0, 4, (steps, 2 * B), generator=g)
     for i in range(steps):
         runner.step(ids[i, r * B:(r + 1) * B], lbl[i, r * B:(r + 1) * B])
+        if eval_between:  # a validation pass between steps must not redirect the exchange
+            with torch.no_grad():
+                m(torch.randint(50, V, (B, T), generator=g))
+            m.eval()
+            m.loss(torch.randint(50, V, (B, T), generator=g), lbl[i, :B])
+            m.train()
     out = (flat.master.clone(), ddp.bytes_reduced)
     ddp.close()
     return out
 
 
-def _dp(sparse, steps=3):
-    return Distributor(num_processes=2, use_gpu=False, log_sink=None, timeout=300).run(_run, steps, sparse)
+def _dp(sparse, steps=3, cap=None, eval_between=False):
+    return Distributor(num_processes=2, use_gpu=False, log_sink=None, timeout=300).run(_run, steps, sparse, cap,
+                                                                                          eval_between)
 
 
 def test_sparse_embedding_exchange_matches_dense_allreduce():
@@ -56,3 +63,12 @@ def test_sparse_embedding_exchange_matches_dense_allreduce():
     assert torch.allclose(sparse, dense, rtol=1e-6, atol=1e-7), float((sparse - dense).abs().max())
     # the 300 x 32 table: 38,400 B dense per step vs B*T = 48 ids x (8 + 128) B = 6,528 B
     assert sparse_bytes < dense_bytes - 3 * (V * 32 * 4 - B * T * 136) + 1
+
+
+def test_sparse_exchange_fixed_capacity_and_eval_between_steps():
+    """A fixed id-list capacity (no host sync) gives the same parameters, and evaluation forwards
+    between the training steps (no_grad, eval mode) do not change which rows are exchanged
+    (the ids are recorded by grad-enabled training forwards only)."""
+    dense, _ = _dp(False, eval_between=True)
+    capped, _ = _dp(True, cap=B * T + 7, eval_between=True)
+    assert torch.allclose(capped, dense, rtol=1e-6, atol=1e-7), float((capped - dense).abs().max())

@@ -261,47 +261,6 @@ def test_cross_attention_f32(attn_kernel, mode, kp):
     _attn_f32(2, 3, 130, 130 if mode == "reference" else 77, mode, True, kp)
 
 
-@pytest.mark.parametrize("cross", [False, True])
-@pytest.mark.parametrize("mode,S", [("none", 256), ("reference", 256), ("causal", 200), ("reference", 37)])
-def test_attention_f32_plane_inputs(f32_algo, mode, S, cross):
-    """Q/K/V (and dO) as producer-written split planes (sparkmi/ops/attention.py:_in_planes):
-    bitwise the fp32-input kernels' results (the planes are exactly the split the kernels make at
-    staging); planes of a DIFFERENT tensor change the result (the planes are what is read)."""
-    from sparkmi.ops import planes as PL
-    torch.manual_seed(11)
-    B, H, hd = 2, 3, 64
-    if cross:  # kv read from column 128 of a wider concatenated projection, like the decoder's
-        Sk = S + 5 if mode == "none" else S
-        q0, kv0 = torch.randn(B, S, H * hd, device=dev), torch.randn(B, Sk, 128 + 2 * H * hd, device=dev)
-        ins = (q0, kv0)
-    else:
-        ins = (torch.randn(B, S, 3 * H * hd, device=dev),)
-    do0 = torch.randn(B, S, H * hd, device=dev)
-
-    def run(planes, scale=1.0):
-        xs = [t.clone().requires_grad_() for t in ins]
-        if planes:
-            for t in xs:
-                PL.attach(t, PL.split((t.detach() * scale).reshape(-1, t.shape[-1])))
-        o = (cross_attention(xs[0], xs[1], H, mode, kv_col=128) if cross else self_attention(xs[0], H, mode))
-        do = do0.clone()
-        if planes:
-            PL.attach(do, PL.split((do0 * scale).reshape(-1, do0.shape[-1])))
-        o.backward(do)
-        g = [t.grad for t in xs]
-        if cross:  # kv_col = 128: the kv gradient's first 128 columns are not this op's
-            g[1] = g[1][..., 128:]
-        return [o.detach()] + g
-
-    ref, pin = run(False), run(True)
-    for a, b in zip(ref, pin):
-        assert torch.equal(a, b)
-    if f32_algo != 0:  # the split-product kernels read the planes (the f32-MFMA kernels never do)
-        other = run(True, 2.0)
-        assert not torch.equal(other[0], ref[0])
-        assert not torch.equal(other[1], ref[1])
-
-
 @pytest.mark.parametrize("M,V", [(8192, 10000), (300, 10000), (77, 45), (256, 384)])
 def test_vocab_linear_ce_fused_stats(M, V):
     """The vocab projection's epilogue reduces each logits row per 128 columns (max, sum exp) and
