@@ -27,7 +27,8 @@ module was called, so gradients were never synchronised).  Design for MI355X + R
   stream-ordered kernel with a device-side epoch, the whole data-parallel step (forward,
   backward, all-reduce, optimizer) is captured as ONE HIP graph (``graph_safe``).  For larger
   gradients (the transformer's 188 MB) auto MEASURES both paths at start-up on the largest
-  bucket (``comm_probe``: IPC two-shot vs the RCCL process group, max over ranks) and keeps the
+  bucket (``comm_probe``: IPC two-shot vs the RCCL process group vs an RCCL communicator with
+  min_ctas = 32, i.e. more rings over the 7 xGMI links; max over ranks) and keeps the
   faster; ``SPARKMI_DP_PROBE=0`` sends them to RCCL without measuring.  Either way a bucket's
   reduction runs on a side stream (RCCL's own, or the IPC comm stream forked from the compute
   stream at launch and joined in ``finish()``), overlapped with the rest of the backward.
@@ -55,15 +56,34 @@ from ..ops import _grad
 IPC_LIMIT_BYTES = 32 << 20  # auto without a measurement: IPC kernels up to this gradient size
 
 
-def choose_comm(ipc_ms, rccl_ms):
+def choose_comm(ipc_ms, rccl_ms, rccl_mc_ms=None):
     """The auto path for a bulk gradient from a measured all-reduce of its largest bucket (max over
-    ranks): the IPC two-shot when it is at least as fast as RCCL, else RCCL.  Both run on a side
-    stream overlapped with the backward, so the isolated bucket time is the right comparison."""
-    if ipc_ms is None:
+    ranks): 'ipc' (the IPC two-shot kernel), 'rccl' (the process group's RCCL communicator) or
+    'rccl_mc' (an RCCL communicator created with min_ctas = 32: more channels, i.e. more rings
+    over the 7 point-to-point xGMI links of a node).  The fastest wins; a tie prefers that order
+    (the graph-capturable kernel first).  All run on a side stream overlapped with the backward,
+    so the isolated bucket time is the right comparison.  None = path unavailable."""
+    cands = [(name, ms) for name, ms in (("ipc", ipc_ms), ("rccl", rccl_ms), ("rccl_mc", rccl_mc_ms))
+             if ms is not None]
+    if not cands:
         return "rccl"
-    if rccl_ms is None:
-        return "ipc"
-    return "ipc" if ipc_ms <= rccl_ms else "rccl"
+    return min(cands, key=lambda c: c[1])[0]
+
+
+MIN_CTAS = 32  # RCCL channels of the multi-channel communicator the probe measures
+
+
+def multichannel_group(world, min_ctas=MIN_CTAS):
+    """A new RCCL communicator over all ranks with at least ``min_ctas`` channels (CTAs), or None
+    (not the nccl backend, or the option unavailable).  Collective: every rank calls it."""
+    if not dist.is_initialized() or dist.get_backend() != "nccl":
+        return None
+    try:
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.config.min_ctas = int(min_ctas)
+        return dist.new_group(list(range(world)), backend="nccl", pg_options=opts)
+    except Exception:  # noqa: BLE001 — an older RCCL / torch without the option: not a candidate
+        return None
 
 
 def broadcast_flat(flat, src=0, group=None):
@@ -105,13 +125,18 @@ class DataParallel:
             raise ValueError(f"SPARKMI_DP_COMM={mode!r}: auto | ipc | rccl")
         if ipc is None:
             ipc = os.environ.get("SPARKMI_IPC_AR", "1") != "0" and mode != "rccl"
-        # bulk gradients in auto mode: measure both paths on the largest bucket and keep the faster
-        # (SPARKMI_DP_PROBE=0: the fixed IPC_LIMIT_BYTES rule instead)
-        probe = (ipc and mode == "auto" and flat.numel * 4 > IPC_LIMIT_BYTES)
-        if probe and os.environ.get("SPARKMI_DP_PROBE", "1") == "0":
-            ipc = probe = False
+        # bulk gradients in auto mode: measure the paths on the largest bucket and keep the fastest
+        # (SPARKMI_DP_PROBE=0: the fixed IPC_LIMIT_BYTES rule instead, the default RCCL group)
+        probe = (mode == "auto" and flat.numel * 4 > IPC_LIMIT_BYTES and self.world > 1
+                 and os.environ.get("SPARKMI_DP_PROBE", "1") != "0")
+        if ipc and mode == "auto" and flat.numel * 4 > IPC_LIMIT_BYTES and not probe:
+            ipc = False
         self._build_buckets()
         self.comm_probe = None
+        # the communicator of the gradient-bucket collectives: the caller's group, or the
+        # multi-channel RCCL one when the probe measured it faster
+        self.bulk_group = group
+        self._mc_group = None
         if (ipc and not self.zero and self.world > 1 and flat.grad.is_cuda and self.world <= 8
                 and _single_node(self.world)):
             from .comm import IpcAllReduce, IpcUnavailable
@@ -119,14 +144,20 @@ class DataParallel:
                 self.ipc = IpcAllReduce(cap_floats=self._ipc_capacity(), group=group)
             except IpcUnavailable:
                 self.ipc = None  # every rank agreed: buckets go through the process group
-            if self.ipc is not None and probe:
-                n = max(e - s for s, e, _ in self.buckets)
-                ipc_ms, rccl_ms = self._probe(n)
-                choice = choose_comm(ipc_ms, rccl_ms)
-                self.comm_probe = {"bucket_bytes": n * 4, "ipc_ms": ipc_ms, "rccl_ms": rccl_ms, "choice": choice}
-                if choice != "ipc":
-                    self.ipc.close()
-                    self.ipc = None
+        if probe:
+            n = max(e - s for s, e, _ in self.buckets)
+            mc = multichannel_group(self.world) if group is None else None
+            ipc_ms, rccl_ms, mc_ms = self._probe(n, mc)
+            choice = choose_comm(ipc_ms, rccl_ms, mc_ms)
+            self.comm_probe = {"bucket_bytes": n * 4, "ipc_ms": ipc_ms, "rccl_ms": rccl_ms,
+                               f"rccl_min_ctas{MIN_CTAS}_ms": mc_ms, "choice": choice}
+            if choice != "ipc" and self.ipc is not None:
+                self.ipc.close()
+                self.ipc = None
+            if choice == "rccl_mc":
+                self.bulk_group = self._mc_group = mc
+            elif mc is not None:
+                dist.destroy_process_group(mc)
         # the IPC kernels run on a comm stream forked from the compute stream at each bucket
         # launch (joined in finish()): buckets reduce while the rest of the backward runs, as
         # RCCL's do on its own stream
@@ -146,31 +177,46 @@ class DataParallel:
 
     @property
     def comm(self):
-        return "ipc" if self.ipc is not None else ("rccl" if self.world > 1 else "none")
+        if self.ipc is not None:
+            return "ipc"
+        if self.world <= 1:
+            return "none"
+        return "rccl_mc" if self._mc_group is not None else "rccl"
 
-    def _probe(self, n, iters=3):
-        """(IPC two-shot ms, process-group ms) of an n-float all-reduce, max over ranks."""
+    def _probe(self, n, mc=None, iters=3):
+        """(IPC two-shot ms or None, process-group ms, multi-channel RCCL ms or None) of an n-float
+        all-reduce, max over ranks."""
         import time
-        x = torch.zeros(n, dtype=torch.float32, device=self.flat.grad.device)
+        dev = self.flat.grad.device
+        x = torch.zeros(n, dtype=torch.float32, device=dev)
+        cuda = dev.type == "cuda"
+        # a gloo group reduces host tensors: its flags live on the CPU
+        fdev = dev if (cuda and dist.get_backend(self.group) == "nccl") else torch.device("cpu")
+
+        def sync():
+            if cuda:
+                torch.cuda.synchronize(dev)
 
         def timed(fn):
             for _ in range(2):
                 fn()
-            torch.cuda.synchronize()
-            dist.all_reduce(torch.zeros(1, device=x.device), group=self.group)  # line the ranks up
-            torch.cuda.synchronize()
+            sync()
+            dist.all_reduce(torch.zeros(1, device=fdev), group=self.group)  # line the ranks up
+            sync()
             t0 = time.perf_counter()
             for _ in range(iters):
                 fn()
-            torch.cuda.synchronize()
-            t = torch.tensor([(time.perf_counter() - t0) / iters * 1e3], dtype=torch.float64, device=x.device)
+            sync()
+            t = torch.tensor([(time.perf_counter() - t0) / iters * 1e3], dtype=torch.float64, device=fdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
             return round(float(t.item()), 3)
 
-        ipc_ms = timed(lambda: self.ipc(x))
+        ipc_ms = timed(lambda: self.ipc(x)) if self.ipc is not None else None
         rccl_ms = timed(lambda: dist.all_reduce(x, group=self.group))
-        self.ipc.check()
-        return ipc_ms, rccl_ms
+        mc_ms = timed(lambda: dist.all_reduce(x, group=mc)) if mc is not None else None
+        if self.ipc is not None:
+            self.ipc.check()
+        return ipc_ms, rccl_ms, mc_ms
 
     def _ipc_capacity(self):
         """Staging floats for the IPC kernels: any bucket _build_buckets can cut (for any set of
@@ -287,9 +333,9 @@ class DataParallel:
             return
         if self.zero:
             ps, pe = self.piece(b)
-            w = dist.reduce_scatter_tensor(self.flat.grad[ps:pe], g, group=self.group, async_op=True)
+            w = dist.reduce_scatter_tensor(self.flat.grad[ps:pe], g, group=self.bulk_group, async_op=True)
         else:
-            w = dist.all_reduce(g, group=self.group, async_op=True)
+            w = dist.all_reduce(g, group=self.bulk_group, async_op=True)
         self._works.append(w)
 
     def _sparse_exchange(self, s, e, i):
@@ -451,6 +497,10 @@ class DataParallel:
             self.ipc.check()
             self.ipc.close()
             self.ipc = None
+        if self._mc_group is not None:
+            dist.destroy_process_group(self._mc_group)
+            self._mc_group = None
+            self.bulk_group = self.group
         if self._listener is not None:
             _grad.remove_listener(self._listener)
             self._listener = None

@@ -196,3 +196,39 @@ def test_dp_probe_disabled_uses_rccl_for_bulk(monkeypatch):
     flat = FlatParams(torch.nn.Linear(8, 8), device="cpu", shadow=False)
     dp = ddp.DataParallel(flat)
     assert dp.ipc is None and dp.comm_probe is None and dp.comm == "none"
+
+
+def test_choose_comm_three_paths():
+    """The probe's three candidates: IPC two-shot, the default RCCL
+    communicator and the min_ctas multi-channel one; fastest wins, ties prefer that order."""
+    from sparkmi.parallel.ddp import choose_comm
+    assert choose_comm(3.0, 2.0, 1.0) == "rccl_mc"
+    assert choose_comm(1.0, 2.0, 1.0) == "ipc"
+    assert choose_comm(None, 2.0, 2.0) == "rccl"
+    assert choose_comm(None, 2.0, 1.5) == "rccl_mc"
+    assert choose_comm(None, None, None) == "rccl"
+    assert choose_comm(None, 2.0, None) == "rccl"
+
+
+def _probe_run():
+    import torch
+    from sparkmi.parallel import ddp, init_distributed
+    from sparkmi.utils.flat import FlatParams
+    init_distributed()
+    ddp.IPC_LIMIT_BYTES = 1024  # a "bulk" gradient at test size
+    flat = FlatParams(torch.nn.Linear(64, 64), device="cpu", shadow=False)
+    dp = ddp.DataParallel(flat)
+    out = (dp.comm_probe, dp.comm, dp.bulk_group is None)
+    dp.close()
+    return out
+
+
+def test_dp_probe_lists_three_paths_gloo():
+    """Two CPU ranks over gloo: the start-up probe measures the process group, reports the IPC and
+    multi-channel RCCL candidates as unavailable (None) and keeps the default group."""
+    from sparkmi.api import Distributor
+    probe, comm, default_group = Distributor(num_processes=2, use_gpu=False, log_sink=None,
+                                             timeout=120).run(_probe_run)
+    assert set(probe) >= {"bucket_bytes", "ipc_ms", "rccl_ms", "rccl_min_ctas32_ms", "choice"}
+    assert probe["ipc_ms"] is None and probe["rccl_min_ctas32_ms"] is None and probe["rccl_ms"] > 0
+    assert probe["choice"] == "rccl" and comm == "rccl" and default_group
