@@ -419,10 +419,12 @@ def bench_mlp(args, rank, world, device):
     flat = FlatParams(model, shadow=False)
     opt = SGD(flat, lr=0.01)
     ddp = DataParallel(flat) if world > 1 else None
-    # one executor: the whole step (forward, CE, backward, SGD) is ONE kernel launch
+    # one executor: the whole step (forward, CE, backward, SGD) is ONE kernel launch; data-parallel:
+    # forward + backward in one kernel (gradients to the flat buffer), the IPC all-reduce and SGD
     fused = (lambda m, o, x, y: m.fused_sgd_step(o, x, y)) if world == 1 else None
+    fgrad = (lambda m, x, y: m.fused_grad_step(x, y)) if world > 1 else None
     runner = StepRunner(model, lambda m, x, y: m.loss(x, y), opt, ddp, graph=device.type == "cuda" and args.graph != "off",
-                        fused_step=fused, bind_inputs=True)
+                        fused_step=fused, bind_inputs=True, fused_grad=fgrad)
     g = torch.Generator().manual_seed(31 + rank)
     batches = [(torch.rand(30, 4, generator=g).to(device) * 2 - 1, torch.randint(0, 3, (30,), generator=g).to(device))
                for _ in range(8)]

@@ -70,6 +70,7 @@ int smi_lbfgs_update(float*, float*, float*, int*, int, long, const float*, floa
                      float, hipStream_t);
 int smi_mlp(const MLPArgs*, int, hipStream_t);
 int smi_mlp_grid(int);
+int smi_mlp_small(int);
 int smi_gemm(const GemmArgs*, hipStream_t);
 int smi_gemm_f32(const GemmF32Args*, hipStream_t);
 int smi_gemm_f32_algo(int);
@@ -349,6 +350,8 @@ PYBIND11_MODULE(_C, m) {
     chk(smi_mlp(&a, mode, S(st)), "mlp");
   });
   m.def("mlp_grid", [](int n) { return smi_mlp_grid(n); });
+  m.def("mlp_small", [](int set) { return smi_mlp_small(set); },
+        "MLP kernel: 1 = the compile-time 4-5-4-3 kernel for batches <= 64 (default), 0 = the generic one; -1 queries");
 
   m.def("gemm", [](int mode, u A, long lda, u B, long ldb, int M, int N, int K, u C, long ldc, int out_f32, int atomic,
                    int beta_acc, float alpha, u bias, u resid, long ldr, int act, u dact_y, long ldy, u seedp,

@@ -231,6 +231,158 @@ __global__ __launch_bounds__(64) void mlp_kernel(MLPArgs a, int mode) {
   if (lane == 0) a.ticket[0] = 0u;  // re-arm for the next launch (stream-ordered)
 }
 
+// Compile-time form for the reference topology (4-5-4-3 sigmoid, batch <= 64: one wave, one row
+// per lane; distributed_multilayer_perceptron.py:44-53, batch 30 at :93).  The generic kernel above
+// loops over runtime dims through dynamically indexed pointer / offset arrays and LDS rows (13.7 us
+// per step, latency-bound); here every activation and gradient lives in registers, the 64
+// parameters are uniform (scalar) loads, and the only LDS round trip is the per-parameter row sum:
+// each lane writes its row's T products, then lane e sums parameter e over the rows in row order.
+// Same modes as mlp_kernel (0 loss, 1 gradients, 2 fused SGD step).
+template <int D0, int D1, int D2, int D3>
+__global__ __launch_bounds__(64) void mlp_small_kernel(MLPArgs a, int mode) {
+  constexpr int T1 = D1 * (D0 + 1), T2 = D2 * (D1 + 1), T3 = D3 * (D2 + 1), T = T1 + T2 + T3;
+  constexpr int PT = T + 1;  // odd pitch: the 64 lanes' rows on distinct banks
+  __shared__ float prod[64 * PT];
+  const int lane = threadIdx.x;
+  const bool valid = lane < a.n;
+  const int row = valid ? lane : 0;
+  // parameters (uniform addresses: scalar loads, all in flight together)
+  float W1[D1][D0], b1[D1], W2[D2][D1], b2[D2], W3[D3][D2], b3[D3];
+#pragma unroll
+  for (int o = 0; o < D1; ++o) {
+    b1[o] = a.b[0][o];
+#pragma unroll
+    for (int i = 0; i < D0; ++i) W1[o][i] = a.W[0][o * D0 + i];
+  }
+#pragma unroll
+  for (int o = 0; o < D2; ++o) {
+    b2[o] = a.b[1][o];
+#pragma unroll
+    for (int i = 0; i < D1; ++i) W2[o][i] = a.W[1][o * D1 + i];
+  }
+#pragma unroll
+  for (int o = 0; o < D3; ++o) {
+    b3[o] = a.b[2][o];
+#pragma unroll
+    for (int i = 0; i < D2; ++i) W3[o][i] = a.W[2][o * D2 + i];
+  }
+  float x[D0];
+#pragma unroll
+  for (int i = 0; i < D0; ++i) x[i] = a.x[(long)row * D0 + i];
+  const long long lab0 = a.y ? a.y[row] : 0;
+  const int lab = lab0 < 0 ? 0 : (lab0 >= D3 ? D3 - 1 : (int)lab0);
+  const float w = valid ? (a.row_w ? a.row_w[row] : 1.f / (float)a.n) : 0.f;
+  const float dl = a.dloss ? a.dloss[0] : 1.f;
+  // forward
+  float h1[D1], h2[D2], z[D3];
+#pragma unroll
+  for (int o = 0; o < D1; ++o) {
+    float s = b1[o];
+#pragma unroll
+    for (int i = 0; i < D0; ++i) s += W1[o][i] * x[i];
+    h1[o] = mlp_act(s, a.act);
+  }
+#pragma unroll
+  for (int o = 0; o < D2; ++o) {
+    float s = b2[o];
+#pragma unroll
+    for (int i = 0; i < D1; ++i) s += W2[o][i] * h1[i];
+    h2[o] = mlp_act(s, a.act);
+  }
+#pragma unroll
+  for (int o = 0; o < D3; ++o) {
+    float s = b3[o];
+#pragma unroll
+    for (int i = 0; i < D2; ++i) s += W3[o][i] * h2[i];
+    z[o] = s;
+  }
+  float m = z[0];
+#pragma unroll
+  for (int c = 1; c < D3; ++c) m = fmaxf(m, z[c]);
+  float e[D3], se = 0.f;
+#pragma unroll
+  for (int c = 0; c < D3; ++c) { e[c] = __expf(z[c] - m); se += e[c]; }
+  const float lse = m + __logf(se);
+  float zl = z[0];
+#pragma unroll
+  for (int c = 1; c < D3; ++c) zl = c == lab ? z[c] : zl;
+  const float lsum = wave_sum(valid ? w * (lse - zl) : 0.f);
+  if (a.logits && valid) {
+#pragma unroll
+    for (int c = 0; c < D3; ++c) a.logits[(long)row * D3 + c] = z[c];
+  }
+  if (mode == 0) {
+    if (lane == 0 && a.loss) a.loss[0] = lsum;
+    return;
+  }
+  // backward (rows past n: w = 0, every product 0)
+  float dz[D3], d2[D2], d1[D1];
+  const float inv = 1.f / se, wd = w * dl;
+#pragma unroll
+  for (int c = 0; c < D3; ++c) dz[c] = (e[c] * inv - (c == lab ? 1.f : 0.f)) * wd;
+#pragma unroll
+  for (int i = 0; i < D2; ++i) {
+    float s = 0.f;
+#pragma unroll
+    for (int o = 0; o < D3; ++o) s += W3[o][i] * dz[o];
+    d2[i] = a.act == 1 ? (h2[i] > 0.f ? s : 0.f) : s * h2[i] * (1.f - h2[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < D1; ++i) {
+    float s = 0.f;
+#pragma unroll
+    for (int o = 0; o < D2; ++o) s += W2[o][i] * d2[o];
+    d1[i] = a.act == 1 ? (h1[i] > 0.f ? s : 0.f) : s * h1[i] * (1.f - h1[i]);
+  }
+  // the row's per-parameter products, layer-major (W[o][i] then b[o]) like mlp_kernel
+  float* pr = prod + lane * PT;
+#pragma unroll
+  for (int o = 0; o < D1; ++o) {
+#pragma unroll
+    for (int i = 0; i < D0; ++i) pr[o * D0 + i] = d1[o] * x[i];
+    pr[D1 * D0 + o] = d1[o];
+  }
+#pragma unroll
+  for (int o = 0; o < D2; ++o) {
+#pragma unroll
+    for (int i = 0; i < D1; ++i) pr[T1 + o * D1 + i] = d2[o] * h1[i];
+    pr[T1 + D2 * D1 + o] = d2[o];
+  }
+#pragma unroll
+  for (int o = 0; o < D3; ++o) {
+#pragma unroll
+    for (int i = 0; i < D2; ++i) pr[T1 + T2 + o * D2 + i] = dz[o] * h2[i];
+    pr[T1 + T2 + D3 * D2 + o] = dz[o];
+  }
+  __syncthreads();
+  const float lr = mode == 2 ? a.lr[0] * a.gscale : 0.f;
+  for (int q = lane; q < T; q += 64) {
+    float g = 0.f;
+#pragma unroll 16
+    for (int k = 0; k < 64; ++k) g += prod[k * PT + q];  // row order
+    const int l = q < T1 ? 0 : (q < T1 + T2 ? 1 : 2);
+    const int r = q - (l == 0 ? 0 : (l == 1 ? T1 : T1 + T2));
+    const int din = l == 0 ? D0 : (l == 1 ? D1 : D2), dout = l == 0 ? D1 : (l == 1 ? D2 : D3);
+    const bool bias = r >= dout * din;
+    if (mode == 2) {
+      float* p = bias ? const_cast<float*>(a.b[l]) + (r - dout * din) : const_cast<float*>(a.W[l]) + r;
+      *p -= lr * g;
+    } else {
+      float* p = bias ? a.gb[l] + (r - dout * din) : a.gW[l] + r;
+      *p = a.accumulate ? *p + g : g;
+    }
+  }
+  if (lane == 0) {
+    if (a.loss) a.loss[0] = lsum;
+    if (mode == 2 && a.step) a.step[0] += 1.f;
+  }
+}
+
+static bool mlp_small_ok(const MLPArgs& a) {
+  return a.nlayers == 3 && a.dims[0] == 4 && a.dims[1] == 5 && a.dims[2] == 4 && a.dims[3] == 3 && a.n >= 1 &&
+         a.n <= 64 && (a.act == 1 || a.act == 2);
+}
+
 static int mlp_check(const MLPArgs& a) {
   if (a.nlayers < 1 || a.nlayers > MLP_MAXL) return -1;
   int total = 0;
@@ -245,6 +397,14 @@ extern "C" int smi_mlp_grid(int n) {
   return b < 1 ? 1 : (b > MLP_MAX_GRID ? MLP_MAX_GRID : b);
 }
 
+// the compile-time 4-5-4-3 kernel for batches of <= 64 rows (1, default) or always the generic one
+// (0: tests compare the two)
+static int g_mlp_small = 1;
+extern "C" int smi_mlp_small(int set) {
+  if (set == 0 || set == 1) g_mlp_small = set;
+  return g_mlp_small;
+}
+
 // mode 0 forward/loss, 1 forward+backward (gradients), 2 forward+backward+SGD (one launch per
 // training step).  grid > 1 needs a.ws ([grid][total+1] floats) and a zeroed a.ticket.
 extern "C" int smi_mlp(const MLPArgs* args, int mode, hipStream_t st) {
@@ -255,6 +415,7 @@ extern "C" int smi_mlp(const MLPArgs* args, int mode, hipStream_t st) {
   if (mode > 0 && !a.y) return -1;
   if (mode == 1) for (int l = 0; l < a.nlayers; ++l) if (!a.gW[l] || !a.gb[l]) return -1;
   if (mode == 2 && !a.lr) return -1;
-  hipLaunchKernelGGL(mlp_kernel, dim3(grid), dim3(64), 0, st, a, mode);
+  if (mlp_small_ok(a) && g_mlp_small) hipLaunchKernelGGL((mlp_small_kernel<4, 5, 4, 3>), dim3(1), dim3(64), 0, st, a, mode);
+  else hipLaunchKernelGGL(mlp_kernel, dim3(grid), dim3(64), 0, st, a, mode);
   SMI_CHECK_LAUNCH();
 }

@@ -6,7 +6,7 @@ state_dicts load.  ``forward`` returns logits; ``loss`` runs the fused HIP MLP+C
 import torch
 from torch import nn
 
-from ..ops.mlp import mlp_logits, mlp_loss, mlp_sgd_step
+from ..ops.mlp import mlp_grad_step, mlp_logits, mlp_loss, mlp_sgd_step
 
 
 class MultilayerPerceptron(nn.Module):
@@ -52,6 +52,17 @@ class MultilayerPerceptron(nn.Module):
         lins = self.linears()
         return mlp_sgd_step(x, y, [l.weight for l in lins], [l.bias for l in lins], opt.lr_t, opt.step_t,
                             self.activation, grad_scale=opt.grad_scale)
+
+
+    def fused_grad_step(self, x, y):
+        """Forward, CE and backward as ONE HIP launch, the gradients added to the flat gradient
+        buffer (the data-parallel step's local half: the IPC all-reduce and SGD follow).  None when
+        it does not apply (CPU, parameters outside a FlatParams buffer)."""
+        from .. import _native
+        if not x.is_cuda or not _native.use_native(x) or getattr(self, "_smi_flat", None) is None:
+            return None
+        lins = self.linears()
+        return mlp_grad_step(x, y, [l.weight for l in lins], [l.bias for l in lins], self.activation)
 
 
 Multilayer_perceptor = MultilayerPerceptron  # reference class name

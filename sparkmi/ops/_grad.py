@@ -453,3 +453,27 @@ def flush_deferred():
         grad_ready(*e[6])
     for e in gq:
         grad_ready(*e[4])
+
+
+class _FlushPoint(torch.autograd.Function):
+    """Identity whose backward launches the weight gradients queued so far on the side stream
+    (flush_groups_async): placed at a layer's input, its backward runs once every consumer of the
+    input inside the layer has produced its gradient, i.e. when that layer's backward is done."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        if g is not None and g.is_cuda:
+            flush_groups_async(g.device)
+        return g
+
+
+def wgrad_flush_point(x):
+    """x unchanged; in the backward, the layer's queued weight-gradient GEMMs start on the side
+    stream beside the next layer's backward (GPU, grouped wgrads, single process)."""
+    if not (x.is_cuda and x.requires_grad and WGRAD_OVERLAP and WGRAD_GROUP and torch.is_grad_enabled()):
+        return x
+    return _FlushPoint.apply(x)

@@ -117,6 +117,23 @@ def mlp_sgd_step(x, y, weights, biases, lr_t, step_t=None, act="sigmoid", row_we
     return loss[0]
 
 
+def mlp_grad_step(x, y, weights, biases, act="sigmoid", row_weight=None):
+    """Forward, weighted softmax-CE and backward in ONE launch, the gradients ADDED to the
+    parameters' (flat) gradient buffers — the data-parallel step's local half (the all-reduce and
+    the optimizer follow).  Returns the loss (device scalar)."""
+    a = ACT[act] if isinstance(act, str) else act
+    x = x.float().contiguous()
+    y = y.to(torch.int64).contiguous()
+    loss = torch.empty(1, device=x.device, dtype=torch.float32)
+    dims = _dims(weights)
+    ws, tk = _workspace(x.device, x.shape[0], dims)
+    _native.C().mlp(1, x.data_ptr(), y.data_ptr(), _native.ptr(row_weight), x.shape[0], dims,
+                    [W.data_ptr() for W in weights], [b.data_ptr() for b in biases],
+                    [grad_buf(W).data_ptr() for W in weights], [grad_buf(b).data_ptr() for b in biases], 0,
+                    loss.data_ptr(), 0, a, ws, tk, 1, 0, 0, 1.0, _native.stream())
+    return loss[0]
+
+
 def mlp_logits(x, weights, biases, act="sigmoid"):
     """Inference logits [n, C] (fused kernel on GPU)."""
     a = ACT[act] if isinstance(act, str) else act

@@ -85,3 +85,43 @@ def test_mlp_fused_sgd_step_equals_chain(n):
     torch.testing.assert_close(fa.master, fb.master, atol=1e-6, rtol=1e-6)
     assert float(oa.step_t) == float(ob.step_t) == 5.0
     assert torch.count_nonzero(fa.grad) == 0  # the fused step never materialises gradients
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,act,weighted", [(30, "sigmoid", False), (64, "relu", True), (1, "sigmoid", False)])
+def test_mlp_small_kernel_matches_generic(n, act, weighted):
+    """The compile-time 4-5-4-3 kernel (registers, one wave; csrc/kernels/mlp.hip mlp_small_kernel)
+    against the generic kernel: loss, gradients (mode 1) and the fused SGD step (mode 2)."""
+    from sparkmi import _native
+    from sparkmi.ops.mlp import mlp_sgd_step
+    C = _native.C()
+    torch.manual_seed(3)
+    x = (torch.rand(n, 4) * 2 - 1).cuda()
+    y = torch.randint(0, 3, (n,)).cuda()
+    rw = (torch.rand(n) / n).cuda() if weighted else None
+    base = MultilayerPerceptron((4, 5, 4, 3), activation=act).cuda()
+    out = {}
+    prev = C.mlp_small(-1)
+    try:
+        for small in (1, 0):
+            C.mlp_small(small)
+            m = MultilayerPerceptron((4, 5, 4, 3), activation=act).cuda()
+            m.load_state_dict(base.state_dict())
+            loss = m.loss(x, y, rw)
+            loss.backward()
+            grads = [p.grad.clone() for p in m.parameters()]
+            lins = m.linears()
+            lr = torch.tensor([0.1], device="cuda")
+            step = torch.zeros(1, device="cuda")
+            l2 = mlp_sgd_step(x, y, [l.weight for l in lins], [l.bias for l in lins], lr, step, act, rw)
+            out[small] = (loss.detach(), grads, l2, [p.detach().clone() for p in m.parameters()], step.clone())
+    finally:
+        C.mlp_small(prev)
+    a, b = out[1], out[0]
+    torch.testing.assert_close(a[0], b[0], rtol=1e-6, atol=1e-7)
+    for ga, gb in zip(a[1], b[1]):
+        torch.testing.assert_close(ga, gb, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(a[2], b[2], rtol=1e-6, atol=1e-7)
+    for pa, pb in zip(a[3], b[3]):
+        torch.testing.assert_close(pa, pb, rtol=1e-6, atol=1e-7)
+    assert float(a[4]) == float(b[4]) == 1.0
