@@ -108,11 +108,11 @@ int smi_lstm(const LSTMArgs*, int, hipStream_t);
 int smi_lstm_supported(int, int, int, int);
 long smi_lstm_slab_floats(int, int, int, int, int);
 int smi_adam(float*, float*, float*, float*, void*, long, const float*, float*, unsigned*, float, float, float, float, float,
-             int, int, void*, long, hipStream_t);
+             int, int, void*, long, int*, hipStream_t);
 int smi_sgd(float*, float*, float*, void*, long, const float*, float*, unsigned*, float, float, float, int, float, int,
-            void*, long, hipStream_t);
+            void*, long, int*, hipStream_t);
 int smi_adam_multi(float* const*, float* const*, float* const*, float* const*, void* const*, const long*, int, const float*,
-                   float*, unsigned*, float, float, float, float, float, int, int, void* const*, long, hipStream_t);
+                   float*, unsigned*, float, float, float, float, float, int, int, void* const*, long, int*, hipStream_t);
 int smi_multi_copy(void* const*, const void* const*, const long*, int, hipStream_t);
 }
 
@@ -291,16 +291,17 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("seed_inc", [](u seed, u st) { chk(smi_seed_inc(reinterpret_cast<int*>(seed), S(st)), "seed_inc"); });
   // step: device step counter (advanced by the kernel); done: zeroed uint32 ticket word;
-  // pl / ps: optional split planes of the updated weights (plane stride ps elements)
+  // pl / ps: optional split planes of the updated weights (plane stride ps elements); seed: an
+  // optional int32 dropout step seed the update kernel advances for the next step (0: none)
   m.def("adam", [](u p, u g, u mm, u v, u pbf, long n, u lr, u step, u done, float b1, float b2, float eps, float wd,
-                   float gscale, int adamw, int zero_grad, u pl, long ps, u st) {
+                   float gscale, int adamw, int zero_grad, u pl, long ps, u seed, u st) {
     chk(smi_adam(PF(p), PF(g), PF(mm), PF(v), P(pbf), n, PF(lr), PF(step), reinterpret_cast<unsigned*>(done), b1, b2,
-                 eps, wd, gscale, adamw, zero_grad, P(pl), ps, S(st)), "adam");
+                 eps, wd, gscale, adamw, zero_grad, P(pl), ps, reinterpret_cast<int*>(seed), S(st)), "adam");
   });
   // Adam over several disjoint ranges, one launch, one step advance (ZeRO-1 shard update)
   m.def("adam_multi", [](std::vector<u> p, std::vector<u> g, std::vector<u> mm, std::vector<u> v, std::vector<u> pbf,
                          std::vector<long> n, u lr, u step, u done, float b1, float b2, float eps, float wd, float gscale,
-                         int adamw, int zero_grad, std::vector<u> pl, long ps, u st) {
+                         int adamw, int zero_grad, std::vector<u> pl, long ps, u seed, u st) {
     const size_t c = p.size();
     if (g.size() != c || mm.size() != c || v.size() != c || pbf.size() != c || n.size() != c ||
         (!pl.empty() && pl.size() != c))
@@ -313,13 +314,13 @@ PYBIND11_MODULE(_C, m) {
     }
     chk(smi_adam_multi(a.data(), b.data(), d.data(), e.data(), f.data(), n.data(), (int)c, PF(lr), PF(step),
                        reinterpret_cast<unsigned*>(done), b1, b2, eps, wd, gscale, adamw, zero_grad,
-                       pl.empty() ? nullptr : q.data(), ps, S(st)),
+                       pl.empty() ? nullptr : q.data(), ps, reinterpret_cast<int*>(seed), S(st)),
         "adam_multi");
   });
   m.def("sgd", [](u p, u g, u buf, u pbf, long n, u lr, u step, u done, float mom, float damp, float wd, int nesterov,
-                  float gscale, int zero_grad, u pl, long ps, u st) {
+                  float gscale, int zero_grad, u pl, long ps, u seed, u st) {
     chk(smi_sgd(PF(p), PF(g), PF(buf), P(pbf), n, PF(lr), PF(step), reinterpret_cast<unsigned*>(done), mom, damp, wd,
-                nesterov, gscale, zero_grad, P(pl), ps, S(st)), "sgd");
+                nesterov, gscale, zero_grad, P(pl), ps, reinterpret_cast<int*>(seed), S(st)), "sgd");
   });
   m.def("multi_copy", [](std::vector<u> dst, std::vector<u> src, std::vector<long> bytes, u st) {
     if (dst.size() != src.size() || dst.size() != bytes.size()) throw std::runtime_error("multi_copy: list sizes differ");

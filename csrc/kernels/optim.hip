@@ -24,10 +24,14 @@ __global__ void seed_inc_kernel(int* seed) { seed[0] += 1; }
 // kernel boundary), and an agent-scope release on gfx950 writes back L2 — once per block that
 // doubled the 47M-parameter Adam (0.27 -> 0.55 ms).  Every block has consumed its step[0] read
 // (bias corrections) before its ticket, so the last block's store cannot be seen early.
-__device__ __forceinline__ void finish_step(float* step, unsigned* done, float t) {
+// seed (optional): the model's dropout step seed (sparkmi/ops/rng.py DropoutRNG), advanced here
+// for the NEXT step instead of by a separate one-lane launch at the start of every step (the
+// training-step runner binds it: sparkmi/train/runner.py); no kernel of this launch reads it.
+__device__ __forceinline__ void finish_step(float* step, unsigned* done, float t, int* seed) {
   __syncthreads();
   if (threadIdx.x == 0 && atomicAdd(done, 1u) == gridDim.x - 1) {
     step[0] = t;
+    if (seed) seed[0] += 1;
     done[0] = 0u;
   }
 }
@@ -57,7 +61,7 @@ __global__ __launch_bounds__(NT) void adam_kernel(float* __restrict__ p, float* 
                                                    const float* __restrict__ lr_p, float* __restrict__ step_p,
                                                    unsigned* __restrict__ done, float b1, float b2, float eps, float wd,
                                                    float gscale, int adamw, int zero_grad, unsigned short* __restrict__ pl,
-                                                   long ps) {
+                                                   long ps, int* __restrict__ seed) {
   const float t = step_p[0] + 1.f;
   const float lr = lr_p[0];
   const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
@@ -102,7 +106,7 @@ __global__ __launch_bounds__(NT) void adam_kernel(float* __restrict__ p, float* 
       if (pl) store_planes1(pl, ps, i, p[i]);
     }
   }
-  finish_step(step_p, done, t);
+  finish_step(step_p, done, t, seed);
 }
 
 // Adam over several disjoint ranges in ONE launch with ONE step advance: the ZeRO-1 update of
@@ -118,7 +122,7 @@ struct AdamMulti {
 __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a, const float* __restrict__ lr_p,
                                                          float* __restrict__ step_p, unsigned* __restrict__ done, float b1,
                                                          float b2, float eps, float wd, float gscale, int adamw,
-                                                         int zero_grad) {
+                                                         int zero_grad, int* __restrict__ seed) {
   const float t = step_p[0] + 1.f;
   const float lr = lr_p[0];
   const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
@@ -155,7 +159,7 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a, const floa
     }
     if (pl) store_planes4(pl, a.ps, i, pa);
   }
-  finish_step(step_p, done, t);
+  finish_step(step_p, done, t, seed);
 }
 
 // p -= lr * (g*gscale + wd*p) with optional (heavy-ball, torch-style) momentum buffer
@@ -163,7 +167,7 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, float* 
                                                   unsigned short* __restrict__ pbf, long n, const float* __restrict__ lr_p,
                                                   float* __restrict__ step_p, unsigned* __restrict__ done, float momentum,
                                                   float dampening, float wd, int nesterov, float gscale, int zero_grad,
-                                                  unsigned short* __restrict__ pl, long ps) {
+                                                  unsigned short* __restrict__ pl, long ps, int* __restrict__ seed) {
   const float lr = lr_p[0];
   const float t = step_p[0] + 1.f;
   const bool first = t <= 1.f;
@@ -180,7 +184,7 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, float* 
     if (pbf) pbf[i] = f2bf(p[i]);
     if (pl) store_planes1(pl, ps, i, p[i]);
   }
-  finish_step(step_p, done, t);
+  finish_step(step_p, done, t, seed);
 }
 
 static inline unsigned grid_for(long n) {
@@ -214,7 +218,7 @@ static int adam_wide() { return smi_adam_wide(-1); }
 
 extern "C" int smi_adam(float* p, float* g, float* m, float* v, void* pbf, long n, const float* lr, float* step,
                         unsigned* done, float b1, float b2, float eps, float wd, float gscale, int adamw, int zero_grad,
-                        void* pl, long ps, hipStream_t st) {
+                        void* pl, long ps, int* seed, hipStream_t st) {
   if (pl && (((uintptr_t)pl & 7) || ps % 4 || ps < n)) return -1;
   if (adam_wide()) {
     // 1024-thread blocks, at most two per CU: every block takes one ticket on the shared `done`
@@ -224,10 +228,10 @@ extern "C" int smi_adam(float* p, float* g, float* m, float* v, void* pbf, long 
     if (b > 512) b = 512;
     if (b < 1) b = 1;
     hipLaunchKernelGGL(adam_kernel<1024>, dim3((unsigned)b), dim3(1024), 0, st, p, g, m, v, (unsigned short*)pbf, n,
-                       lr, step, done, b1, b2, eps, wd, gscale, adamw, zero_grad, (unsigned short*)pl, ps);
+                       lr, step, done, b1, b2, eps, wd, gscale, adamw, zero_grad, (unsigned short*)pl, ps, seed);
   } else {
     hipLaunchKernelGGL(adam_kernel<256>, dim3(grid_for(n / 4 + 1)), dim3(256), 0, st, p, g, m, v, (unsigned short*)pbf,
-                       n, lr, step, done, b1, b2, eps, wd, gscale, adamw, zero_grad, (unsigned short*)pl, ps);
+                       n, lr, step, done, b1, b2, eps, wd, gscale, adamw, zero_grad, (unsigned short*)pl, ps, seed);
   }
   SMI_CHECK_LAUNCH();
 }
@@ -235,7 +239,7 @@ extern "C" int smi_adam(float* p, float* g, float* m, float* v, void* pbf, long 
 extern "C" int smi_adam_multi(float* const* p, float* const* g, float* const* m, float* const* v, void* const* pbf,
                               const long* n, int count, const float* lr, float* step, unsigned* done, float b1, float b2,
                               float eps, float wd, float gscale, int adamw, int zero_grad, void* const* pl, long ps,
-                              hipStream_t st) {
+                              int* seed, hipStream_t st) {
   if (count < 1 || count > ADAM_MULTI_MAX) return -1;
   AdamMulti a{};
   long total4 = 0;
@@ -258,16 +262,16 @@ extern "C" int smi_adam_multi(float* const* p, float* const* g, float* const* m,
   a.count = count;
   a.ps = ps;
   hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)tot), dim3(256), 0, st, a, lr, step, done, b1, b2, eps, wd, gscale,
-                     adamw, zero_grad);
+                     adamw, zero_grad, seed);
   SMI_CHECK_LAUNCH();
 }
 
 extern "C" int smi_sgd(float* p, float* g, float* buf, void* pbf, long n, const float* lr, float* step, unsigned* done,
                        float momentum, float dampening, float wd, int nesterov, float gscale, int zero_grad, void* pl,
-                       long ps, hipStream_t st) {
+                       long ps, int* seed, hipStream_t st) {
   if (pl && ps < n) return -1;
   hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, g, buf, (unsigned short*)pbf, n, lr, step,
-                     done, momentum, dampening, wd, nesterov, gscale, zero_grad, (unsigned short*)pl, ps);
+                     done, momentum, dampening, wd, nesterov, gscale, zero_grad, (unsigned short*)pl, ps, seed);
   SMI_CHECK_LAUNCH();
 }
 

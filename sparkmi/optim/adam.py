@@ -20,6 +20,9 @@ class _FlatOptimizer:
         self.done_t = torch.zeros(1, dtype=torch.int32, device=dev)
         self.grad_scale = 1.0
         self.zero_grad_after_step = True
+        # the model's dropout step seed (an int32 device tensor), advanced by the update kernel for
+        # the next step (set by StepRunner; None: the runner advances it with its own launch)
+        self.bump_seed = None
 
     @property
     def lr(self):
@@ -76,10 +79,12 @@ class Adam(_FlatOptimizer):
                          self.lr_t.data_ptr(), self.step_t.data_ptr(), self.done_t.data_ptr(), self.b1, self.b2,
                          self.eps, self.weight_decay, self.grad_scale, int(self.adamw), int(self.zero_grad_after_step),
                          [_native.ptr(f.planes) + 2 * s for s, _ in self.ranges] if f.planes is not None else [],
-                         f.plane_stride(), _native.stream())
+                         f.plane_stride(), _native.ptr(self.bump_seed), _native.stream())
             return
         with torch.no_grad():
             self.step_t.add_(1)
+            if self.bump_seed is not None:
+                self.bump_seed.add_(1)
             t = float(self.step_t.item())
             lr = float(self.lr_t.item())
             bc1, bc2 = 1 - self.b1 ** t, 1 - self.b2 ** t
@@ -108,10 +113,12 @@ class Adam(_FlatOptimizer):
             C.adam(f.master.data_ptr(), f.grad.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), _native.ptr(f.shadow),
                    f.numel, self.lr_t.data_ptr(), self.step_t.data_ptr(), self.done_t.data_ptr(), self.b1, self.b2, self.eps,
                    self.weight_decay, self.grad_scale, int(self.adamw), int(self.zero_grad_after_step),
-                   _native.ptr(f.planes), f.plane_stride(), st)
+                   _native.ptr(f.planes), f.plane_stride(), _native.ptr(self.bump_seed), st)
             return
         with torch.no_grad():
             self.step_t.add_(1)
+            if self.bump_seed is not None:
+                self.bump_seed.add_(1)
             t = float(self.step_t.item())
             lr = float(self.lr_t.item())
             g = f.grad * self.grad_scale

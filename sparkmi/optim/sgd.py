@@ -20,10 +20,12 @@ class SGD(_FlatOptimizer):
             C.sgd(f.master.data_ptr(), f.grad.data_ptr(), _native.ptr(self.buf), _native.ptr(f.shadow), f.numel,
                   self.lr_t.data_ptr(), self.step_t.data_ptr(), self.done_t.data_ptr(), self.momentum, self.dampening, self.weight_decay,
                   int(self.nesterov), self.grad_scale, int(self.zero_grad_after_step), _native.ptr(f.planes),
-                  f.plane_stride(), st)
+                  f.plane_stride(), _native.ptr(self.bump_seed), st)
             return
         with torch.no_grad():
             self.step_t.add_(1)
+            if self.bump_seed is not None:
+                self.bump_seed.add_(1)
             lr = float(self.lr_t.item())
             d = f.grad * self.grad_scale
             if self.weight_decay:

@@ -86,11 +86,24 @@ class StepRunner:
     def _dp(self):
         return self.ddp is not None and self.ddp.world > 1
 
+    def _advance_seed(self):
+        """The dropout step seed for this step.  The first time, where the optimizer's update kernel
+        can advance it (a device seed and an optimizer with ``bump_seed``), the seed is advanced
+        once here and handed to the optimizer, which advances it at the end of every step for the
+        next one: one launch fewer per step, the same seed sequence.  Otherwise one bump launch."""
+        rng = getattr(self.model, "rng", None)
+        if rng is None:
+            return
+        if self.opt is not None and getattr(self.opt, "bump_seed", False) is rng.seed:
+            return  # advanced by the previous step's optimizer launch
+        rng.advance()
+        if (hasattr(self.opt, "bump_seed") and self.opt.bump_seed is None and rng.seed.is_cuda
+                and not torch.cuda.is_current_stream_capturing()):
+            self.opt.bump_seed = rng.seed
+
     def _fwd_bwd(self, *batch):
         _grad.reset_deferred()  # a previous backward that raised must not leave queued work behind
-        rng = getattr(self.model, "rng", None)
-        if rng is not None:
-            rng.advance()
+        self._advance_seed()
         loss = self.loss_fn(self.model, *batch)
         loss.backward(self._seed(loss))
         _grad.join()
@@ -164,9 +177,7 @@ class StepRunner:
 
     def _fwd_bwd_split(self, *batch):
         _grad.reset_deferred()
-        rng = getattr(self.model, "rng", None)
-        if rng is not None:
-            rng.advance()
+        self._advance_seed()
         loss, segments = self.split_fn(self.model, *batch)
         loss.backward(self._seed(loss))
         _grad.join()

@@ -102,7 +102,7 @@ def main():
     lr, stp = torch.full((1,), 1e-3, device=dev), torch.ones(1, device=dev)
     done = torch.zeros(1, device=dev, dtype=torch.int32)
     t = timeit(lambda: C.adam(p_.data_ptr(), g_.data_ptr(), m_.data_ptr(), v_.data_ptr(), pb.data_ptr(), n,
-                              lr.data_ptr(), stp.data_ptr(), done.data_ptr(), 0.9, 0.999, 1e-8, 0.0, 1.0, 0, 1, 0, 0, st()))
+                              lr.data_ptr(), stp.data_ptr(), done.data_ptr(), 0.9, 0.999, 1e-8, 0.0, 1.0, 0, 1, 0, 0, 0, st()))
     print(f"adam 47M    {t:8.1f} us  {n * (4 * 4 + 4 * 4 + 2) / t / 1e3:7.0f} GB/s")
     ids = torch.randint(0, V, (M,), device=dev)
     table = torch.randn(V, D, device=dev).bfloat16()
