@@ -342,7 +342,7 @@ def bench_cnn_recipe(args, rank, world, device, dtype="bf16"):
     n = 60000
     x, y = fashion_mnist_like(n, seed=17 + rank)
     cfg = CNNConfig(world=world, batch_size=args.cnn_batch, lr=0.01, conv_dtype=dtype, log_every=10 ** 9,
-                    verbose=False, graph=args.graph != "off", unroll=8)
+                    verbose=False, graph=args.graph != "off")
     loader = DeviceLoader([x, y], cfg.batch_size, device, shuffle=True, drop_last=True, seed=1000 * rank, fixed=True)
     model = FashionMNISTModel(1, 10, 10, dtype=dtype)
     tr = Trainer(model, lambda m, a, b: m.loss(a, b), lambda flat: SGD(flat, lr=cfg.lr), cfg, device, rank, world,

@@ -20,13 +20,14 @@ extern "C" int smi_gemm_sp_tm(int set) {
 // the grouped weight-gradient launch's tile (gemm_sp_wg_tm = 128 | 256 | 16 | 4; default: follow
 // smi_sp_tm).  Per backward the group holds every layer's weight gradients, each a long
 // K = tokens reduction: fewer, larger tiles can leave CUs idle where 128-row tiles fill them.
-static int g_sp_wg_tm = -1;
+// 0 (default): chosen per launch by wave quantization (gemm_sp_wgrad.hip sp_wg_auto); -1: follow
+// smi_sp_tm; 128 / 256 / 16: forced
+static int g_sp_wg_tm = 0;
 int smi_sp_wg_tm() {
-  return g_sp_wg_tm > 0 ? g_sp_wg_tm : smi_sp_tm();
+  return g_sp_wg_tm > 0 ? g_sp_wg_tm : (g_sp_wg_tm == 0 ? 0 : smi_sp_tm());
 }
 extern "C" int smi_gemm_sp_wg_tm(int set) {
-  if (set == 128 || set == 256 || set == 16) g_sp_wg_tm = set;
-  else if (set == -1) g_sp_wg_tm = -1;  // follow smi_sp_tm
+  if (set == 128 || set == 256 || set == 16 || set == 0 || set == -1) g_sp_wg_tm = set;
   return smi_sp_wg_tm();
 }
 extern "C" int smi_gemm_sp_waves(int set) {  // set 4 / 8 (A/B runs in one process); other values query

@@ -28,7 +28,7 @@ from torch import nn
 
 from ..ops import (DropoutRNG, add_dropout_layernorm, cross_attention, embedding, linear, self_attention,
                    sinusoid_table)
-from ..ops._grad import ResidualGrad, wgrad_flush_point
+from ..ops._grad import ResidualGrad
 from ..ops._grad import SharedGrad
 from ..ops.linear import concat_linear, ffn
 from ..ops import planes as _pl
@@ -110,10 +110,6 @@ def _gp(t):
 # logsumexp moves the early flagship trajectory off the CPU reference by more than the standalone
 # pass (tests/test_f32_gpu.py::test_transformer_f32_flagship_trajectory); tests exercise it
 CE_FUSED = False
-# layers whose backward ends with a launch of their queued weight-gradient GEMMs on the side stream
-# (sparkmi/ops/_grad.py wgrad_flush_point): "encoder" | "all" (decoder too) | "none" (the decoder's
-# queue is launched once the backward reaches the encoder, the encoder's at the end)
-WGRAD_FLUSH_LAYERS = "encoder"
 
 
 class MultiHeadAttention(nn.Module):
@@ -198,8 +194,6 @@ class EncoderLayer(nn.Module):
     def forward(self, x, mode="none", key_padding=None):
         p1 = self.dropout1.p if self.training else 0.0
         p2 = self.dropout2.p if self.training else 0.0
-        if WGRAD_FLUSH_LAYERS in ("encoder", "all"):
-            x = wgrad_flush_point(x)
         # residual gradients ride the dgrad epilogue of the block's first linear (ResidualGrad)
         s1, s2 = ResidualGrad(), ResidualGrad()
         a = self.attention(x, mode, key_padding, x_slot=s1)
@@ -246,8 +240,6 @@ class DecoderLayer(nn.Module):
 
     def forward(self, x, y, self_mode="none", cross_mode="none", key_padding=None, kv=None):
         ps = [d.p if self.training else 0.0 for d in (self.dropout1, self.dropout2, self.dropout3)]
-        if WGRAD_FLUSH_LAYERS == "all":
-            y = wgrad_flush_point(y)
         s1, s2, s3 = ResidualGrad(), ResidualGrad(), ResidualGrad()
         a = self.self_attention(y, self_mode, x_slot=s1)
         y = self.layer_norm1(a, y, ps[0], self._rng, self.salts[0], r_slot=s1)

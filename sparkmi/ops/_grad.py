@@ -390,7 +390,10 @@ def _flush_folds(C, fq):
 # and ONE join per backward (a side stream per Linear cost 15-20 us per cross-queue dependency,
 # see _SIDE_ENABLED above).  The launched operands stay referenced until the join; their
 # parameters are reported final only after it.  Single-process only (no defer listeners: the
-# data-parallel engine runs its own early flushes).  SMI_WGRAD_OVERLAP=0 disables it.
+# data-parallel engine runs its own early flushes).  False disables it.  A flush per layer (each
+# encoder / decoder layer's wgrads launched when its backward is done) measured +1.1 / +1.5 ms per
+# fp32 step (profiles/r5_ab_wgrad_flush_points.log): the side-stream wgrad workgroups (one per CU,
+# 147 KiB of LDS) take CUs from the critical dgrad chain.
 WGRAD_OVERLAP = True
 _async = {"main": None, "dev": None, "hold": []}
 
@@ -454,26 +457,3 @@ def flush_deferred():
     for e in gq:
         grad_ready(*e[4])
 
-
-class _FlushPoint(torch.autograd.Function):
-    """Identity whose backward launches the weight gradients queued so far on the side stream
-    (flush_groups_async): placed at a layer's input, its backward runs once every consumer of the
-    input inside the layer has produced its gradient, i.e. when that layer's backward is done."""
-
-    @staticmethod
-    def forward(ctx, x):
-        return x.view_as(x)
-
-    @staticmethod
-    def backward(ctx, g):
-        if g is not None and g.is_cuda:
-            flush_groups_async(g.device)
-        return g
-
-
-def wgrad_flush_point(x):
-    """x unchanged; in the backward, the layer's queued weight-gradient GEMMs start on the side
-    stream beside the next layer's backward (GPU, grouped wgrads, single process)."""
-    if not (x.is_cuda and x.requires_grad and WGRAD_OVERLAP and WGRAD_GROUP and torch.is_grad_enabled()):
-        return x
-    return _FlushPoint.apply(x)

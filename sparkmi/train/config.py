@@ -37,7 +37,7 @@ class TrainConfig:
     progress_timeout: float = 0.0  # s without step progress on a rank -> group failure (0: off)
     max_restarts: int = 0          # group restarts from the last checkpoint after a failure
     phase_timing: bool = False     # graph steps as separate phase graphs + events (timing, slower)
-    unroll: int = 8                # fixed-buffer loaders: steps per replayed multi-step graph
+    unroll: int = 16               # fixed-buffer loaders: steps per replayed multi-step graph
     sparse_embedding: bool = False  # DP: exchange the model's embedding gradient row-sparse
                                     # (models exposing ``sparse_rows()``, e.g. the LSTM)
     verbose: bool = True

@@ -56,6 +56,7 @@ class StepRunner:
         # it eagerly before the step (before the static-input copy of a copying graph)
         self.pre_step = None
         self._pre_inline = False
+        self.last_group_sum = None  # the summed loss of the last multi-step graph replay (run_steps)
         self.loss_fn = loss_fn          # loss_fn(model, *batch) -> scalar loss tensor
         self.split_fn = split_fn        # split_fn(model, *batch) -> (loss, leaf, root), see module doc
         self.graph2 = None              # split mode: the lower segments' backward graphs
@@ -322,13 +323,16 @@ class StepRunner:
                 with torch.cuda.graph(g, pool=self._bound_pool):
                     for batch in group:
                         step_losses.append(self._eager(*batch))
+                    # the group's summed loss inside the graph (metrics read one scalar per group)
+                    total = torch.stack([l.detach().float().reshape(()) for l in step_losses]).sum()
             finally:
                 self._pre_inline = False
             if self._bound_pool is None:
                 self._bound_pool = g.pool()
             self._opt_in_graph = True
-            ent = self._multi[key] = (g, step_losses[-1], group, step_losses)
+            ent = self._multi[key] = (g, step_losses[-1], group, step_losses, total)
         ent[0].replay()
+        self.last_group_sum = ent[4]
         if losses is not None:
             losses.extend(ent[3])
         self.steps += len(group)
@@ -342,6 +346,7 @@ class StepRunner:
         and ``unroll`` > 1, each run of ``unroll`` consecutive batches replays as one multi-step
         graph (the same steps, one launch)."""
         loss, i, U = None, 0, self.unroll
+        self.last_group_sum = None
         while i < len(seq):
             if (U > 1 and i + U <= len(seq) and self.graph_requested and seq[i][0].is_cuda
                     and self.steps >= self.warmup_eager and self._bind_ok()):

@@ -150,7 +150,11 @@ class Trainer:
                         losses = [self.runner.step(*group[0])]
                 # the group's losses summed once (one reduction, not one add per step): the metrics
                 # mean over the interval is unchanged (groups never cross a log boundary)
-                gsum = losses[0] if len(losses) == 1 else torch.stack([l.reshape(()) for l in losses]).sum()
+                gsum = losses[0]
+                if len(losses) > 1:
+                    gsum = (self.runner.last_group_sum if (len(losses) == self.runner.unroll
+                                                           and self.runner.last_group_sum is not None)
+                            else torch.stack([l.reshape(()) for l in losses]).sum())
                 last = losses[-1]
                 for j in range(len(losses)):
                     lj = gsum if j == len(losses) - 1 else None

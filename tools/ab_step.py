@@ -2,7 +2,8 @@
 """In-process A/B of transformer-step variants (module-level switches), interleaved rounds so clock
 drift hits every variant alike.  Usage (GPU box):
     python tools/ab_step.py --dtype fp32 --rounds 2 'sparkmi.models.transformer:WGRAD_FLUSH_LAYERS=none,encoder,all'
-Each spec is module:attribute=v1,v2,...; values are parsed as Python literals when possible."""
+Each spec is module:attribute=v1,v2,... (a module attribute) or C:function=v1,v2,... (a setter of
+the native extension, e.g. C:gemm_sp_wg_tm=0,16,128); values are parsed as Python literals."""
 import argparse
 import ast
 import importlib
@@ -23,7 +24,13 @@ def main():
     a = ap.parse_args()
     modname, rest = a.spec.split(":")
     attr, vals = rest.split("=")
-    mod = importlib.import_module(modname)
+    if modname == "C":
+        from sparkmi import _native
+        mod = None
+        setter = getattr(_native.C(), attr)
+    else:
+        mod = importlib.import_module(modname)
+        setter = lambda v: setattr(mod, attr, v)  # noqa: E731
     values = []
     for v in vals.split(","):
         try:
@@ -37,7 +44,7 @@ def main():
     res = {str(v): [] for v in values}
     for _ in range(a.rounds):
         for v in values:
-            setattr(mod, attr, v)
+            setter(v)
             r = bench.bench_transformer(args, rank, world, device, a.dtype)
             res[str(v)].append(r["ms_per_step"])
             print(json.dumps({attr: v, "ms_per_step": r["ms_per_step"]}), flush=True)
