@@ -20,14 +20,16 @@ extern "C" int smi_gemm_sp_tm(int set) {
 // the grouped weight-gradient launch's tile (gemm_sp_wg_tm = 128 | 256 | 16 | 4; default: follow
 // smi_sp_tm).  Per backward the group holds every layer's weight gradients, each a long
 // K = tokens reduction: fewer, larger tiles can leave CUs idle where 128-row tiles fill them.
-// 0 (default): chosen per launch by wave quantization (gemm_sp_wgrad.hip sp_wg_auto); -1: follow
-// smi_sp_tm; 128 / 256 / 16: forced
-static int g_sp_wg_tm = 0;
+// -1 (default): follow smi_sp_tm; 128 / 256 / 16: forced.  128-row tiles for the encoder's
+// 1.5-wave group (384 tiles of 256 x 128 on 256 CUs) measured +0.18 ms per fp32 step
+// (profiles/r5_ab_wgrad_group_tile.log): the 256-row tile's higher efficiency outweighs the
+// half-empty second wave.
+static int g_sp_wg_tm = -1;
 int smi_sp_wg_tm() {
-  return g_sp_wg_tm > 0 ? g_sp_wg_tm : (g_sp_wg_tm == 0 ? 0 : smi_sp_tm());
+  return g_sp_wg_tm > 0 ? g_sp_wg_tm : smi_sp_tm();
 }
 extern "C" int smi_gemm_sp_wg_tm(int set) {
-  if (set == 128 || set == 256 || set == 16 || set == 0 || set == -1) g_sp_wg_tm = set;
+  if (set == 128 || set == 256 || set == 16 || set == -1) g_sp_wg_tm = set;
   return smi_sp_wg_tm();
 }
 extern "C" int smi_gemm_sp_waves(int set) {  // set 4 / 8 (A/B runs in one process); other values query

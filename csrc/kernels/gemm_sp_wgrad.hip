@@ -93,21 +93,7 @@ extern "C" int smi_gemm_sp_wgrad_group(const void* const* A, const long* lda, co
   if (count < 1 || count > SPG_MAX) return -1;
   SpWgradGroup gm{}, gb{};
   int tm = 0, tb = 0, cm = 0, cb = 0;
-  int wtm = smi_sp_wg_tm();
-  if (wtm == 0) {
-    // Wave quantization: a group is one launch of independent, equally long tiles, so its time is
-    // (waves of tiles) x (tile time).  An encoder backward's 24 weight gradients are 384 tiles of
-    // 256 x 128 = 1.5 waves of 256 CUs (the second wave half empty) but 768 tiles of 128 x 128 = 3
-    // full waves of half-length tiles; the 128-row tile is ~10 % less efficient per FLOP.
-    long t256 = 0, t128 = 0;
-    for (int i = 0; i < count; ++i) {
-      const long ntn = (k[i] + 127) / 128;
-      t256 += ((n[i] + 255) / 256 * ntn + 7) / 8 * 8;
-      t128 += ((n[i] + 127) / 128 * ntn + 7) / 8 * 8;
-    }
-    const long w256 = (t256 + SP_NUM_CU - 1) / SP_NUM_CU, w128 = (t128 + SP_NUM_CU - 1) / SP_NUM_CU;
-    wtm = (20 * w256 <= 11 * w128) ? smi_sp_tm() : 128;
-  }
+  const int wtm = smi_sp_wg_tm();
   const bool t16 = wtm == 16, t256 = wtm == 256 || t16;
   for (int i = 0; i < count; ++i) {
     int ab = 0, bb = 0;
