@@ -367,12 +367,13 @@ def bench_cnn_recipe(args, rank, world, device, dtype="bf16"):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     steps = res["steps"]
+    gather = "in the step kernel" if tr.runner.pre_step is None else "in the step graph"
     tr.close()
     v = world * args.cnn_batch * steps / elapsed
     return {"samples_per_s": round(v, 1), "ms_per_step": round(elapsed / steps * 1000, 4), "steps": steps,
             "final_loss": round(res["final_loss"], 4), "dtype": dtype, "global_batch": world * args.cnn_batch,
             "vs_baseline": round(v / BASELINE_CNN, 2),
-            "config": f"Trainer.fit over a shuffled 60k-image HBM shard per executor, batch gather in the step graph, "
+            "config": f"Trainer.fit over a shuffled 60k-image HBM shard per executor, batch gather {gather}, "
                       f"{cfg.unroll}-step graphs, dp{world}"}
 
 

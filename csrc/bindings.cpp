@@ -540,7 +540,7 @@ PYBIND11_MODULE(_C, m) {
   // the fused slab reduction + SGD update in the kernel's tail (CNNArgs::fused)
   m.def("cnn_sgd_step", [](u x, int x_u8, float x_scale, u y, int B, int cin, int C, int classes, std::vector<u> w,
                            std::vector<u> b, std::vector<u> shadow, u slab, u part, u row_loss, u loss,
-                           float loss_scale, u lr, u step, u tick, int bf16, u st) {
+                           float loss_scale, u lr, u step, u tick, int bf16, u perm, u cursor, u st) {
     CNNArgs a{};
     a.bf16 = bf16;
     if (w.size() != 5 || b.size() != 5) throw std::runtime_error("cnn_sgd_step: need 5 weight and 5 bias pointers");
@@ -555,13 +555,14 @@ PYBIND11_MODULE(_C, m) {
     a.P = o; a.slab = (float*)slab; a.part = (float*)part; a.row_loss = (float*)row_loss; a.loss = (float*)loss;
     a.loss_scale = loss_scale; a.train = 1; a.fused = 1;
     a.lr = (const float*)lr; a.step = (float*)step; a.tick = (unsigned*)tick;
+    a.perm = (const long long*)perm; a.cursor = (int*)cursor;
     chk(smi_cnn(&a, S(st)), "cnn_sgd_step");
   });
   // the same launch in GRADIENT mode (the data-parallel step): the tail adds the batch gradient
   // to gw / gb (the flat gradient buffer) instead of updating the parameters
   m.def("cnn_grad_step", [](u x, int x_u8, float x_scale, u y, int B, int cin, int C, int classes, std::vector<u> w,
                             std::vector<u> b, std::vector<u> gw, std::vector<u> gb, u slab, u part, u row_loss, u loss,
-                            float loss_scale, u tick, int bf16, u st) {
+                            float loss_scale, u tick, int bf16, u perm, u cursor, u st) {
     CNNArgs a{};
     a.bf16 = bf16;
     if (w.size() != 5 || b.size() != 5 || gw.size() != 5 || gb.size() != 5)
@@ -576,6 +577,7 @@ PYBIND11_MODULE(_C, m) {
     for (int i = 0; i < 10; ++i) { a.off[i] = o; o += sz[i]; }
     a.P = o; a.slab = (float*)slab; a.part = (float*)part; a.row_loss = (float*)row_loss; a.loss = (float*)loss;
     a.loss_scale = loss_scale; a.train = 1; a.fused = 1; a.lr = nullptr; a.tick = (unsigned*)tick;
+    a.perm = (const long long*)perm; a.cursor = (int*)cursor;
     chk(smi_cnn(&a, S(st)), "cnn_grad_step");
   });
   m.def("attn_ae", [](int set) { return smi_attn_ae(set); },

@@ -22,6 +22,10 @@ struct CNNArgs {
   int wstage;  // set by the launcher: the bf16 convs read LDS-staged weights (when they fit)
   float* part; unsigned* tick; const float* lr; float* step;
   unsigned short* shadow[10];                // per-parameter bf16 shadows (slab order) or null
+  // INDEX mode (fused steps only; sparkmi/data/dataset.py DeviceLoader fixed=True): x / y are the
+  // whole HBM-resident dataset and image i of the batch is row perm[cursor[0] * B + i]; the step's
+  // last workgroup advances the device cursor — the shuffled batch gather inside the step kernel
+  const long long* perm; int* cursor;
 };
 #ifndef CNN_GRP
 #define CNN_GRP 8

@@ -747,6 +747,7 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
     if (threadIdx.x == 0) {
       if (g.loss) g.loss[0] = ls * g.loss_scale;
       if (g.step && !gmode) g.step[0] += 1.f;
+      if (g.cursor) g.cursor[0] += 1;  // index mode: every workgroup read it before its ticket
       g.tick[CNN_GRP] = 0u;
     }
   }
@@ -758,6 +759,9 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int C = EX ? CC : g.C, CI = g.cin, NC = g.classes;
   const int img = blockIdx.x;
+  // the dataset row of this image (index mode: two dependent scalar loads, issued before the
+  // weight staging and LDS clearing so their latency hides behind them)
+  const long src = g.perm ? g.perm[(long)g.cursor[0] * g.B + img] : (long)img;
   float* xin = sm;                       // CI x 30x30
   float* a1 = xin + CI * PL28;           // C x 30x30
   float* a2 = a1 + C * PL28;             // C x 30x30
@@ -799,11 +803,11 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   // the label (thread 0 computes the loss), loaded now so its memory round trip overlaps the
   // image load and conv1 instead of stalling the cross-entropy (measured ~2k clocks)
   int lab0 = 0;
-  if (threadIdx.x == 0 && g.y) lab0 = (int)g.y[img];
+  if (threadIdx.x == 0 && g.y) lab0 = (int)g.y[src];
   // image load (+ ToTensor scaling)
   for (int e = threadIdx.x; e < CI * 784; e += blockDim.x) {
     const int c = e / 784, r = e % 784;
-    const long gi = (long)img * CI * 784 + e;
+    const long gi = src * CI * 784 + e;
     const float v = g.x_u8 ? (float)((const unsigned char*)g.x)[gi] * g.x_scale : ((const float*)g.x)[gi];
     xin[i28(c, r / 28, r % 28)] = v;
   }
@@ -1005,6 +1009,7 @@ extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
   CNNArgs g = *args;
   // the fused tail's group tickets are tick[0 .. ngrp) below the level-2 ticket tick[CNN_GRP]
   if (g.fused && (g.P % 4 || (g.B + CNN_GRP - 1) / CNN_GRP > CNN_GRP || !g.part || !g.tick || !g.slab || !g.row_loss || !g.train)) return -1;
+  if (g.perm && (!g.fused || !g.cursor)) return -1;  // index mode: fused steps only
   if (g.fused && !g.lr) {  // gradient mode: every gradient destination, no shadows
     for (int i = 0; i < 5; ++i)
       if (!g.gw[i] || !g.gb[i]) return -1;

@@ -18,8 +18,12 @@ __global__ __launch_bounds__(512, 1) void gemm_bf256_kernel(GemmSpArgs g) {
   gemm_sp_tile256m<AK, BKM, EPI, OUT, false, 2>(g, sp_tile_remap(blockIdx.x, nwg), lds);
 }
 
-// the 256 x 128 bf16 kernels (1, default) or always gemm.hip's 128 x 128 kernel (0: tests, A/B)
-static int g_bf256 = 1;
+// the 256 x 128 bf16 kernels (1) or always gemm.hip's 128 x 128 kernel (0, default).  Measured in
+// the bf16 transformer step (profiles/r5_ab_gemm_bf256.log): QKV 28.3 vs 22.2 us (384 tiles = 1.5
+// waves of one 8-wave WG per CU), FFN1 21.5 vs 20.4, vocab 83.6 vs 80.7, wgrad groups 0.90 vs
+// 0.87 ms -- the 2-plane k-step does not hide its LDS stage the way the 6-product fp32 step does,
+// so the 128 x 128 kernel (2 WGs per CU) stays the bf16 default; opt-in for tests and A/B.
+static int g_bf256 = 0;
 extern "C" int smi_gemm_bf256_enable(int set) {
   if (set == 0 || set == 1) g_bf256 = set;
   return g_bf256;

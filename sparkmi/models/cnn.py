@@ -40,6 +40,33 @@ class FashionMNISTModel(nn.Module):
     def forward(self, x):
         return cnn_logits(x, self.param_list(), self.conv_dtype == "bf16")
 
+    def gather_in_step(self, opt, ddp, x):
+        """True when every training step of this model will run as one of its fused kernels, which
+        then read their shuffled batch straight from the dataset (index mode: perm[cursor * B + i],
+        device cursor advanced by the kernel) — the loop needs no separate gather launch
+        (sparkmi/train/trainer.py with a DeviceLoader(fixed=True))."""
+        from .. import _native
+        from ..optim.sgd import SGD
+        params = self.param_list()
+        if (not x.is_cuda or not _native.use_native(x) or x.dim() != 4 or getattr(self, "_smi_flat", None) is None
+                or not _native.C().cnn_fused_ok(params[0].shape[0], params[0].shape[1], params[8].shape[0],
+                                                 x.shape[0])):
+            return False
+        if ddp is not None:
+            return True  # fused_grad_step
+        flat = opt.flat
+        return (isinstance(opt, SGD) and not opt.momentum and not opt.weight_decay and opt.grad_scale == 1.0
+                and getattr(opt, "ranges", None) is None and getattr(flat, "planes", None) is None)
+
+    @staticmethod
+    def _gather(x, y):
+        """(x, y, index) for the fused kernels: the dataset and (batch, perm, cursor) when ``x`` is a
+        fixed loader's batch buffer in index mode, else the batch itself."""
+        g = getattr(x, "_smi_gather", None)
+        if g is None:
+            return x, y, None
+        return g[1], g[2], (g[0], g[3], g[4])
+
     def fused_sgd_step(self, opt, x, y):
         """The whole single-executor training step (forward, CE, backward, batch gradient sum,
         SGD update) as ONE HIP launch (csrc/kernels/cnn.hip, fused tail); returns the loss.  None
@@ -49,18 +76,21 @@ class FashionMNISTModel(nn.Module):
         from ..optim.sgd import SGD
         flat = getattr(opt, "flat", None)
         params = self.param_list()
+        x, y, index = self._gather(x, y)
+        bs = index[0] if index is not None else x.shape[0]
         if (not x.is_cuda or not _native.use_native(x) or not isinstance(opt, SGD) or opt.momentum
                 or opt.weight_decay or opt.grad_scale != 1.0 or getattr(opt, "ranges", None) is not None
                 or flat is None or getattr(flat, "planes", None) is not None or x.dim() != 4
-                or not _native.C().cnn_fused_ok(params[0].shape[0], params[0].shape[1], params[8].shape[0],
-                                                 x.shape[0])):
+                or not _native.C().cnn_fused_ok(params[0].shape[0], params[0].shape[1], params[8].shape[0], bs)):
+            if index is not None:
+                raise RuntimeError("FashionMNISTModel: index-mode batch but the fused step does not apply")
             return None
         shadows = None
         if flat.shadow is not None:
             offs = [flat.offsets[flat.index[id(p)]] for p in params]
             shadows = [flat.shadow[o:o + p.numel()] for p, o in zip(params, offs)]
         return cnn_sgd_step(x.contiguous(), y.to(torch.int64).contiguous(), params, opt.lr_t, opt.step_t,
-                            self._step_tick, shadows, self.conv_dtype == "bf16")
+                            self._step_tick, shadows, self.conv_dtype == "bf16", index)
 
     def fused_grad_step(self, x, y):
         """Forward, mean CE, backward and the batch gradient sum as ONE HIP launch, the gradient
@@ -71,14 +101,17 @@ class FashionMNISTModel(nn.Module):
         from .. import _native
         from ..ops._grad import grad_buf
         params = self.param_list()
+        x, y, index = self._gather(x, y)
+        bs = index[0] if index is not None else x.shape[0]
         if (not x.is_cuda or not _native.use_native(x) or x.dim() != 4
                 or getattr(self, "_smi_flat", None) is None
-                or not _native.C().cnn_fused_ok(params[0].shape[0], params[0].shape[1], params[8].shape[0],
-                                                 x.shape[0])):
+                or not _native.C().cnn_fused_ok(params[0].shape[0], params[0].shape[1], params[8].shape[0], bs)):
+            if index is not None:
+                raise RuntimeError("FashionMNISTModel: index-mode batch but the fused step does not apply")
             return None
         grads = [grad_buf(p) for p in params]
         return cnn_grad_step(x.contiguous(), y.to(torch.int64).contiguous(), params, grads, self._step_tick,
-                             self.conv_dtype == "bf16")
+                             self.conv_dtype == "bf16", index)
 
     def loss(self, x, y):
         """Mean CE over the batch (distributed_cnn.py:141,177)."""

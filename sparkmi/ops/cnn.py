@@ -112,14 +112,17 @@ def cnn_logits(x, params, bf16=False):
         return reference_logits(x, [p.float() for p in params])
 
 
-def cnn_sgd_step(x, y, params, lr_t, step_t, tick, shadows=None, bf16=False):
+def cnn_sgd_step(x, y, params, lr_t, step_t, tick, shadows=None, bf16=False, index=None):
     """The whole training step — forward, mean CE, backward, gradient reduction over the batch
     and the SGD update — as ONE launch (csrc/kernels/cnn.hip, CNNArgs::fused): the per-image
     slabs are summed in the kernel's ticketed tail, which then updates ``params`` in place
     (p -= lr * g; ``lr_t`` / ``step_t`` are the optimizer's device scalars) and their bf16
     ``shadows`` (10 tensors or None).  Returns the step's mean loss (device scalar).  ``tick``:
-    CNN_GRP + 1 zeroed int32 counters owned by the model (the kernel re-arms them)."""
-    B = x.shape[0]
+    CNN_GRP + 1 zeroed int32 counters owned by the model (the kernel re-arms them).
+    ``index`` = (batch, perm, cursor): ``x`` / ``y`` are the whole dataset and the kernel reads image
+    i of the batch from row perm[cursor * batch + i], then advances the device cursor (the shuffled
+    batch gather inside the step kernel; DeviceLoader fixed=True, index mode)."""
+    B = index[0] if index is not None else x.shape[0]
     w = [params[i] for i in (0, 2, 4, 6, 8)]
     b = [params[i] for i in (1, 3, 5, 7, 9)]
     P = num_params(params)
@@ -132,16 +135,18 @@ def cnn_sgd_step(x, y, params, lr_t, step_t, tick, shadows=None, bf16=False):
                              w[0].shape[0], w[4].shape[0], [t.data_ptr() for t in w], [t.data_ptr() for t in b],
                              [t.data_ptr() for t in shadows] if shadows else [], slab.data_ptr(), part.data_ptr(),
                              row_loss.data_ptr(), loss.data_ptr(), 1.0 / B, lr_t.data_ptr(), step_t.data_ptr(),
-                             tick.data_ptr(), int(bf16), _native.stream())
+                             tick.data_ptr(), int(bf16), index[1].data_ptr() if index else 0,
+                             index[2].data_ptr() if index else 0, _native.stream())
     return loss[0]
 
 
-def cnn_grad_step(x, y, params, grads, tick, bf16=False):
+def cnn_grad_step(x, y, params, grads, tick, bf16=False, index=None):
     """Forward, mean CE, backward and the gradient reduction over the batch as ONE launch, the
     batch gradient ADDED to ``grads`` (10 fp32 tensors: the flat gradient buffer's slices) — the
     data-parallel step's local half (csrc/kernels/cnn.hip gradient mode): the executors'
-    gradients are then all-reduced and the optimizer applies them.  Returns the mean loss."""
-    B = x.shape[0]
+    gradients are then all-reduced and the optimizer applies them.  Returns the mean loss.
+    ``index``: as in cnn_sgd_step."""
+    B = index[0] if index is not None else x.shape[0]
     w = [params[i] for i in (0, 2, 4, 6, 8)]
     b = [params[i] for i in (1, 3, 5, 7, 9)]
     P = num_params(params)
@@ -155,5 +160,6 @@ def cnn_grad_step(x, y, params, grads, tick, bf16=False):
                               [grads[i].data_ptr() for i in (0, 2, 4, 6, 8)],
                               [grads[i].data_ptr() for i in (1, 3, 5, 7, 9)], slab.data_ptr(), part.data_ptr(),
                               row_loss.data_ptr(), loss.data_ptr(), 1.0 / B, tick.data_ptr(), int(bf16),
+                              index[1].data_ptr() if index else 0, index[2].data_ptr() if index else 0,
                               _native.stream())
     return loss[0]

@@ -233,6 +233,9 @@ class StepRunner:
         did every lazy initialisation (allocator pools, GEMM autotuning, library handles), and
         the caller replays the graph for the current step right after."""
         self.static_in = [b.clone() for b in batch]
+        for s, b in zip(self.static_in, batch):
+            if hasattr(b, "_smi_gather"):  # index-mode batch: the step reads the dataset itself
+                s._smi_gather = b._smi_gather
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         if self._dp and self.split_fn is not None:

@@ -95,7 +95,17 @@ class Trainer:
         if not (getattr(loader, "fixed", False) and self.device.type == "cuda" and self.runner.graph_requested):
             return 1
         loader.deferred = True
-        self.runner.pre_step = loader.pre_step
+        gis = getattr(self.model, "gather_in_step", None)
+        fused = self.runner.fused_step if self.world == 1 else self.runner.fused_grad
+        if (gis is not None and fused is not None and self.runner.split_fn is None and len(loader.static) == 2
+                and gis(self.opt, self.ddp if self.world > 1 else None, loader.static[0])):
+            # the model's fused kernels read the shuffled batch from the dataset themselves (index
+            # mode): no gather launch at all; the batch buffers carry the dataset + device cursor
+            loader.static[0]._smi_gather = (loader.batch_size, loader.arrays[0], loader.arrays[1], loader._perm_buf,
+                                            loader._cursor)
+            self.runner.pre_step = None
+        else:
+            self.runner.pre_step = loader.pre_step
         self.runner.bind_inputs = True
         self.runner.unroll = max(1, int(getattr(self.cfg, "unroll", 1)))
         return self.runner.unroll

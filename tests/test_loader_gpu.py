@@ -28,7 +28,7 @@ def test_gather_batch_device_cursor_matches_index_gather():
     assert int(b._cursor.item()) == 203 // 16
 
 
-def _trainer(fixed, steps, unroll, world=1):
+def _trainer(fixed, steps, unroll, world=1, index=True):
     from sparkmi.data.dataset import DeviceLoader
     from sparkmi.data.synthetic import fashion_mnist_like
     from sparkmi.models.cnn import FashionMNISTModel
@@ -42,6 +42,8 @@ def _trainer(fixed, steps, unroll, world=1):
     cfg = CNNConfig(batch_size=32, lr=0.05, log_every=5, verbose=False, unroll=unroll, max_steps=steps)
     loader = DeviceLoader([x, y], 32, dev, shuffle=True, drop_last=True, seed=3, fixed=fixed)
     model = FashionMNISTModel(1, 10, 10)
+    if not index:
+        model.gather_in_step = lambda *a: False  # the separate gather launch (pre_step)
     tr = Trainer(model, lambda m, a, b: m.loss(a, b), lambda flat: SGD(flat, lr=cfg.lr), cfg, dev, 0, world, "t",
                  shadow=False, fused_step=lambda m, o, a, b: m.fused_sgd_step(o, a, b))
     res = tr.fit(loader, 10)
@@ -51,13 +53,16 @@ def _trainer(fixed, steps, unroll, world=1):
 
 
 @pytest.mark.gpu
-def test_trainer_fixed_loader_multistep_graphs_bitwise():
+@pytest.mark.parametrize("index", [True, False])
+def test_trainer_fixed_loader_multistep_graphs_bitwise(index):
     """The fixed-buffer loader's in-graph gather with 4-step graphs (and a 25-step run crossing an
     epoch boundary at 20 batches) trains bitwise the same parameters and logs the same losses as
-    the per-batch gather with per-step graphs."""
+    the per-batch gather with per-step graphs — both with the separate gather launch and with the
+    fused step kernel reading the shuffled rows from the dataset itself (index mode)."""
     pa, ra, la, _ = _trainer(False, 25, 1)
-    pb, rb, lb, runner = _trainer(True, 25, 4)
+    pb, rb, lb, runner = _trainer(True, 25, 4, index=index)
     assert ra["steps"] == rb["steps"] == 25
+    assert (runner.pre_step is None) == index, "index mode engaged as requested"
     assert torch.equal(pa, pb)
     assert runner._multi, "the fixed loader's steps ran as multi-step graphs"
     assert [r["step"] for r in la] == [r["step"] for r in lb]
