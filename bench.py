@@ -424,11 +424,15 @@ def bench_mlp(args, rank, world, device):
     # forward + backward in one kernel (gradients to the flat buffer), the IPC all-reduce and SGD
     fused = (lambda m, o, x, y: m.fused_sgd_step(o, x, y)) if world == 1 else None
     fgrad = (lambda m, x, y: m.fused_grad_step(x, y)) if world > 1 else None
+    # one executor, multi-step graphs: each run of `unroll` steps is ONE launch of the multi-step
+    # kernel (parameters on chip between the steps)
+    fsteps = (lambda m, o, bs: m.fused_sgd_steps(o, bs)) if world == 1 else None
     runner = StepRunner(model, lambda m, x, y: m.loss(x, y), opt, ddp, graph=device.type == "cuda" and args.graph != "off",
-                        fused_step=fused, bind_inputs=True, fused_grad=fgrad)
+                        fused_step=fused, bind_inputs=True, fused_grad=fgrad, fused_steps=fsteps)
     g = torch.Generator().manual_seed(31 + rank)
+    # 32 distinct batches: one cycle over them is one launch of the multi-step kernel (its capacity)
     batches = [(torch.rand(30, 4, generator=g).to(device) * 2 - 1, torch.randint(0, 3, (30,), generator=g).to(device))
-               for _ in range(8)]
+               for _ in range(32)]
     steps = args.aux_steps
     elapsed, _ = time_steps(runner, batches, steps, max(args.warmup, 5), device, world)
     if ddp is not None:

@@ -71,6 +71,7 @@ int smi_lbfgs_update(float*, float*, float*, int*, int, long, const float*, floa
 int smi_mlp(const MLPArgs*, int, hipStream_t);
 int smi_mlp_grid(int);
 int smi_mlp_small(int);
+int smi_mlp_steps(const MLPArgs*, const MLPSteps*, hipStream_t);
 int smi_gemm_bf256_enable(int);
 int smi_gemm(const GemmArgs*, hipStream_t);
 int smi_gemm_f32(const GemmF32Args*, hipStream_t);
@@ -351,6 +352,26 @@ PYBIND11_MODULE(_C, m) {
     a.lr = (const float*)lr; a.step = (float*)step; a.gscale = gscale;
     chk(smi_mlp(&a, mode, S(st)), "mlp");
   });
+  m.def("mlp_steps", [](std::vector<u> xs, std::vector<u> ys, std::vector<u> losses, int n, std::vector<int> dims,
+                        std::vector<u> W, std::vector<u> b, int act, u lr, u step, float gscale, u perm, u cursor,
+                        u loss_sum, u st) {
+    MLPArgs a{};
+    MLPSteps sv{};
+    sv.perm = (const long long*)perm; sv.cursor = (int*)cursor; sv.B = n; sv.loss_sum = (float*)loss_sum;
+    const int L = (int)dims.size() - 1;
+    if (L < 1 || L > MLP_MAXL || (int)W.size() != L || (int)b.size() != L) throw std::runtime_error("mlp_steps: bad layer lists");
+    if (xs.empty() || xs.size() > MLP_MAX_STEPS || ys.size() != xs.size() || losses.size() != xs.size())
+      throw std::runtime_error("mlp_steps: bad step lists");
+    a.n = n; a.nlayers = L; a.act = act; a.lr = (const float*)lr; a.step = (float*)step; a.gscale = gscale;
+    for (int i = 0; i <= L; ++i) a.dims[i] = dims[i];
+    for (int l = 0; l < L; ++l) { a.W[l] = (const float*)W[l]; a.b[l] = (const float*)b[l]; }
+    a.x = (const float*)xs[0]; a.y = (const long long*)ys[0];
+    sv.n = (int)xs.size();
+    for (int t = 0; t < sv.n; ++t) {
+      sv.x[t] = (const float*)xs[t]; sv.y[t] = (const long long*)ys[t]; sv.loss[t] = (float*)losses[t];
+    }
+    return smi_mlp_steps(&a, &sv, S(st)) == 0;
+  }, "s fused SGD steps of the 4-5-4-3 MLP in one launch; False when the shapes are not covered");
   m.def("mlp_grid", [](int n) { return smi_mlp_grid(n); });
   m.def("gemm_bf256", [](int set) { return smi_gemm_bf256_enable(set); },
         "bf16 GEMMs that fill the chip on the 256x128 8-wave 16x16x32 tile (1, default) or always the 128x128 kernel (0); -1 queries");

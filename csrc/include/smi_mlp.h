@@ -31,3 +31,18 @@ struct MLPArgs {
 };
 #define MLP_MAX_GRID 256
 
+// consecutive fused SGD steps in one launch (smi_mlp_steps): step t's batch and loss
+#define MLP_MAX_STEPS 32
+struct MLPSteps {
+  int n;
+  const float* x[MLP_MAX_STEPS];
+  const long long* y[MLP_MAX_STEPS];
+  float* loss[MLP_MAX_STEPS];
+  float* loss_sum;  // optional: the step losses summed in step order (the metrics' group sum)
+  // index mode (perm != null): x[t] / y[t] are the whole dataset and step t's row i is dataset row
+  // perm[(cursor + t) * B + i] (the shuffled batch gather inside the kernel); cursor += n at the end
+  const long long* perm;
+  int* cursor;
+  int B;
+};
+

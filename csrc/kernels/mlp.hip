@@ -238,143 +238,223 @@ __global__ __launch_bounds__(64) void mlp_kernel(MLPArgs a, int mode) {
 // parameters are uniform (scalar) loads, and the only LDS round trip is the per-parameter row sum:
 // each lane writes its row's T products, then lane e sums parameter e over the rows in row order.
 // Same modes as mlp_kernel (0 loss, 1 gradients, 2 fused SGD step).
-template <int D0, int D1, int D2, int D3>
+//
+// Parameter q (layer-major: W[o][i] then b[o] per layer — also the gradient-row order) is read
+// through an accessor P(q) with a compile-time q: the global tensors (scalar loads) in the one-step
+// kernel, an LDS copy in the multi-step kernel.
+template <int D0, int D1, int D2, int D3, int ACT>  // ACT: 1 relu, 2 sigmoid (compile-time: no branches)
+struct Mlp43 {
+  static constexpr int T1 = D1 * (D0 + 1), T2 = D2 * (D1 + 1), T3 = D3 * (D2 + 1), T = T1 + T2 + T3;
+  static constexpr int PT = T + 1;  // odd pitch: the 64 lanes' product rows on distinct banks
+  // the parameter (GRAD = false) or gradient (true) tensor element of entry q
+  template <bool GRAD = false>
+  static __device__ __forceinline__ float* addr(const MLPArgs& a, int q) {
+    const int l = q < T1 ? 0 : (q < T1 + T2 ? 1 : 2);
+    const int r = q - (l == 0 ? 0 : (l == 1 ? T1 : T1 + T2));
+    const int din = l == 0 ? D0 : (l == 1 ? D1 : D2), dout = l == 0 ? D1 : (l == 1 ? D2 : D3);
+    if (GRAD) return r >= dout * din ? a.gb[l] + (r - dout * din) : a.gW[l] + r;
+    return r >= dout * din ? const_cast<float*>(a.b[l]) + (r - dout * din) : const_cast<float*>(a.W[l]) + r;
+  }
+  // One row (this lane's) through forward + softmax-CE (+ backward: the row's T per-parameter
+  // products into the lane-private LDS row `pr`).  Returns the wave's weighted loss sum.
+  template <typename PF>
+  static __device__ __forceinline__ float row(PF P, const float (&x)[D0], int lab, float w, float dl, bool valid,
+                                              bool bwd, float* pr, float* logits_row) {
+    constexpr int act = ACT;
+    float h1[D1], h2[D2], z[D3];
+#pragma unroll
+    for (int o = 0; o < D1; ++o) {
+      float s = P(D1 * D0 + o);
+#pragma unroll
+      for (int i = 0; i < D0; ++i) s += P(o * D0 + i) * x[i];
+      h1[o] = mlp_act(s, act);
+    }
+#pragma unroll
+    for (int o = 0; o < D2; ++o) {
+      float s = P(T1 + D2 * D1 + o);
+#pragma unroll
+      for (int i = 0; i < D1; ++i) s += P(T1 + o * D1 + i) * h1[i];
+      h2[o] = mlp_act(s, act);
+    }
+#pragma unroll
+    for (int o = 0; o < D3; ++o) {
+      float s = P(T1 + T2 + D3 * D2 + o);
+#pragma unroll
+      for (int i = 0; i < D2; ++i) s += P(T1 + T2 + o * D2 + i) * h2[i];
+      z[o] = s;
+    }
+    float m = z[0];
+#pragma unroll
+    for (int c = 1; c < D3; ++c) m = fmaxf(m, z[c]);
+    float e[D3], se = 0.f;
+#pragma unroll
+    for (int c = 0; c < D3; ++c) { e[c] = __expf(z[c] - m); se += e[c]; }
+    const float lse = m + __logf(se);
+    float zl = z[0];
+#pragma unroll
+    for (int c = 1; c < D3; ++c) zl = c == lab ? z[c] : zl;
+    const float lsum = wave_sum(valid ? w * (lse - zl) : 0.f);
+    if (logits_row && valid) {
+#pragma unroll
+      for (int c = 0; c < D3; ++c) logits_row[c] = z[c];
+    }
+    if (!bwd) return lsum;
+    // backward (rows past n: w = 0, every product 0)
+    float dz[D3], d2[D2], d1[D1];
+    const float inv = 1.f / se, wd = w * dl;
+#pragma unroll
+    for (int c = 0; c < D3; ++c) dz[c] = (e[c] * inv - (c == lab ? 1.f : 0.f)) * wd;
+#pragma unroll
+    for (int i = 0; i < D2; ++i) {
+      float s = 0.f;
+#pragma unroll
+      for (int o = 0; o < D3; ++o) s += P(T1 + T2 + o * D2 + i) * dz[o];
+      d2[i] = act == 1 ? (h2[i] > 0.f ? s : 0.f) : s * h2[i] * (1.f - h2[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < D1; ++i) {
+      float s = 0.f;
+#pragma unroll
+      for (int o = 0; o < D2; ++o) s += P(T1 + o * D1 + i) * d2[o];
+      d1[i] = act == 1 ? (h1[i] > 0.f ? s : 0.f) : s * h1[i] * (1.f - h1[i]);
+    }
+#pragma unroll
+    for (int o = 0; o < D1; ++o) {
+#pragma unroll
+      for (int i = 0; i < D0; ++i) pr[o * D0 + i] = d1[o] * x[i];
+      pr[D1 * D0 + o] = d1[o];
+    }
+#pragma unroll
+    for (int o = 0; o < D2; ++o) {
+#pragma unroll
+      for (int i = 0; i < D1; ++i) pr[T1 + o * D1 + i] = d2[o] * h1[i];
+      pr[T1 + D2 * D1 + o] = d2[o];
+    }
+#pragma unroll
+    for (int o = 0; o < D3; ++o) {
+#pragma unroll
+      for (int i = 0; i < D2; ++i) pr[T1 + T2 + o * D2 + i] = dz[o] * h2[i];
+      pr[T1 + T2 + D3 * D2 + o] = dz[o];
+    }
+    return lsum;
+  }
+  // entry q's gradient: the row-order sum of the 64 product rows
+  static __device__ __forceinline__ float colsum(const float* prod, int q) {
+    float g = 0.f;
+#pragma unroll 16
+    for (int k = 0; k < 64; ++k) g += prod[k * PT + q];
+    return g;
+  }
+  static __device__ __forceinline__ void load_row(const float* xp, const long long* yp, int row, float (&x)[D0],
+                                                  long long& lab) {
+#pragma unroll
+    for (int i = 0; i < D0; ++i) x[i] = xp[(long)row * D0 + i];
+    lab = yp ? yp[row] : 0;
+  }
+  static __device__ __forceinline__ int clamp_label(long long l0) { return l0 < 0 ? 0 : (l0 >= D3 ? D3 - 1 : (int)l0); }
+};
+
+template <int D0, int D1, int D2, int D3, int ACT>
 __global__ __launch_bounds__(64) void mlp_small_kernel(MLPArgs a, int mode) {
-  constexpr int T1 = D1 * (D0 + 1), T2 = D2 * (D1 + 1), T3 = D3 * (D2 + 1), T = T1 + T2 + T3;
-  constexpr int PT = T + 1;  // odd pitch: the 64 lanes' rows on distinct banks
-  __shared__ float prod[64 * PT];
+  using M = Mlp43<D0, D1, D2, D3, ACT>;
+  __shared__ float prod[64 * M::PT];
   const int lane = threadIdx.x;
   const bool valid = lane < a.n;
   const int row = valid ? lane : 0;
-  // parameters (uniform addresses: scalar loads, all in flight together)
-  float W1[D1][D0], b1[D1], W2[D2][D1], b2[D2], W3[D3][D2], b3[D3];
-#pragma unroll
-  for (int o = 0; o < D1; ++o) {
-    b1[o] = a.b[0][o];
-#pragma unroll
-    for (int i = 0; i < D0; ++i) W1[o][i] = a.W[0][o * D0 + i];
-  }
-#pragma unroll
-  for (int o = 0; o < D2; ++o) {
-    b2[o] = a.b[1][o];
-#pragma unroll
-    for (int i = 0; i < D1; ++i) W2[o][i] = a.W[1][o * D1 + i];
-  }
-#pragma unroll
-  for (int o = 0; o < D3; ++o) {
-    b3[o] = a.b[2][o];
-#pragma unroll
-    for (int i = 0; i < D2; ++i) W3[o][i] = a.W[2][o * D2 + i];
-  }
+  // parameters: uniform addresses (scalar loads, all in flight together)
+  auto P = [&](int q) -> float { return *M::addr(a, q); };
   float x[D0];
-#pragma unroll
-  for (int i = 0; i < D0; ++i) x[i] = a.x[(long)row * D0 + i];
-  const long long lab0 = a.y ? a.y[row] : 0;
-  const int lab = lab0 < 0 ? 0 : (lab0 >= D3 ? D3 - 1 : (int)lab0);
+  long long lab;
+  M::load_row(a.x, a.y, row, x, lab);
   const float w = valid ? (a.row_w ? a.row_w[row] : 1.f / (float)a.n) : 0.f;
   const float dl = a.dloss ? a.dloss[0] : 1.f;
-  // forward
-  float h1[D1], h2[D2], z[D3];
-#pragma unroll
-  for (int o = 0; o < D1; ++o) {
-    float s = b1[o];
-#pragma unroll
-    for (int i = 0; i < D0; ++i) s += W1[o][i] * x[i];
-    h1[o] = mlp_act(s, a.act);
-  }
-#pragma unroll
-  for (int o = 0; o < D2; ++o) {
-    float s = b2[o];
-#pragma unroll
-    for (int i = 0; i < D1; ++i) s += W2[o][i] * h1[i];
-    h2[o] = mlp_act(s, a.act);
-  }
-#pragma unroll
-  for (int o = 0; o < D3; ++o) {
-    float s = b3[o];
-#pragma unroll
-    for (int i = 0; i < D2; ++i) s += W3[o][i] * h2[i];
-    z[o] = s;
-  }
-  float m = z[0];
-#pragma unroll
-  for (int c = 1; c < D3; ++c) m = fmaxf(m, z[c]);
-  float e[D3], se = 0.f;
-#pragma unroll
-  for (int c = 0; c < D3; ++c) { e[c] = __expf(z[c] - m); se += e[c]; }
-  const float lse = m + __logf(se);
-  float zl = z[0];
-#pragma unroll
-  for (int c = 1; c < D3; ++c) zl = c == lab ? z[c] : zl;
-  const float lsum = wave_sum(valid ? w * (lse - zl) : 0.f);
-  if (a.logits && valid) {
-#pragma unroll
-    for (int c = 0; c < D3; ++c) a.logits[(long)row * D3 + c] = z[c];
-  }
+  const float lsum = M::row(P, x, M::clamp_label(lab), w, dl, valid, mode != 0, prod + lane * M::PT,
+                            a.logits ? a.logits + (long)row * D3 : nullptr);
   if (mode == 0) {
     if (lane == 0 && a.loss) a.loss[0] = lsum;
     return;
   }
-  // backward (rows past n: w = 0, every product 0)
-  float dz[D3], d2[D2], d1[D1];
-  const float inv = 1.f / se, wd = w * dl;
-#pragma unroll
-  for (int c = 0; c < D3; ++c) dz[c] = (e[c] * inv - (c == lab ? 1.f : 0.f)) * wd;
-#pragma unroll
-  for (int i = 0; i < D2; ++i) {
-    float s = 0.f;
-#pragma unroll
-    for (int o = 0; o < D3; ++o) s += W3[o][i] * dz[o];
-    d2[i] = a.act == 1 ? (h2[i] > 0.f ? s : 0.f) : s * h2[i] * (1.f - h2[i]);
-  }
-#pragma unroll
-  for (int i = 0; i < D1; ++i) {
-    float s = 0.f;
-#pragma unroll
-    for (int o = 0; o < D2; ++o) s += W2[o][i] * d2[o];
-    d1[i] = a.act == 1 ? (h1[i] > 0.f ? s : 0.f) : s * h1[i] * (1.f - h1[i]);
-  }
-  // the row's per-parameter products, layer-major (W[o][i] then b[o]) like mlp_kernel
-  float* pr = prod + lane * PT;
-#pragma unroll
-  for (int o = 0; o < D1; ++o) {
-#pragma unroll
-    for (int i = 0; i < D0; ++i) pr[o * D0 + i] = d1[o] * x[i];
-    pr[D1 * D0 + o] = d1[o];
-  }
-#pragma unroll
-  for (int o = 0; o < D2; ++o) {
-#pragma unroll
-    for (int i = 0; i < D1; ++i) pr[T1 + o * D1 + i] = d2[o] * h1[i];
-    pr[T1 + D2 * D1 + o] = d2[o];
-  }
-#pragma unroll
-  for (int o = 0; o < D3; ++o) {
-#pragma unroll
-    for (int i = 0; i < D2; ++i) pr[T1 + T2 + o * D2 + i] = dz[o] * h2[i];
-    pr[T1 + T2 + D3 * D2 + o] = dz[o];
-  }
   __syncthreads();
   const float lr = mode == 2 ? a.lr[0] * a.gscale : 0.f;
-  for (int q = lane; q < T; q += 64) {
-    float g = 0.f;
-#pragma unroll 16
-    for (int k = 0; k < 64; ++k) g += prod[k * PT + q];  // row order
-    const int l = q < T1 ? 0 : (q < T1 + T2 ? 1 : 2);
-    const int r = q - (l == 0 ? 0 : (l == 1 ? T1 : T1 + T2));
-    const int din = l == 0 ? D0 : (l == 1 ? D1 : D2), dout = l == 0 ? D1 : (l == 1 ? D2 : D3);
-    const bool bias = r >= dout * din;
+  for (int q = lane; q < M::T; q += 64) {
+    const float g = M::colsum(prod, q);
     if (mode == 2) {
-      float* p = bias ? const_cast<float*>(a.b[l]) + (r - dout * din) : const_cast<float*>(a.W[l]) + r;
+      float* p = M::addr(a, q);
       *p -= lr * g;
     } else {
-      float* p = bias ? a.gb[l] + (r - dout * din) : a.gW[l] + r;
-      *p = a.accumulate ? *p + g : g;
+      float* gp = M::template addr<true>(a, q);
+      *gp = a.accumulate ? *gp + g : g;
     }
   }
   if (lane == 0) {
     if (a.loss) a.loss[0] = lsum;
     if (mode == 2 && a.step) a.step[0] += 1.f;
+  }
+}
+
+// ``s.n`` consecutive fused SGD steps (mode 2) in ONE launch: step t trains on batch (s.x[t],
+// s.y[t]) and writes its loss to s.loss[t].  The parameters live in LDS between steps (lane q
+// updates entry q after the row sums, a barrier, every lane reads the new values), so each step is
+// bitwise the one-step kernel's step; they are written back once at the end, the step counter
+// advanced by s.n.  The next step's rows are loaded while the current step computes.  A launch per
+// step left the step latency-bound on launch gaps (~5 us per step inside a multi-step graph).
+template <int D0, int D1, int D2, int D3, int ACT>
+__global__ __launch_bounds__(64) void mlp_small_steps_kernel(MLPArgs a, MLPSteps s) {
+  using M = Mlp43<D0, D1, D2, D3, ACT>;
+  __shared__ float prod[64 * M::PT];
+  __shared__ float pl[M::T];
+  __shared__ int srcs[MLP_MAX_STEPS][64];  // index mode: every step's dataset row of each lane
+  __shared__ float lsums[MLP_MAX_STEPS];    // the step losses, stored once at the end
+  const int lane = threadIdx.x;
+  for (int q = lane; q < M::T; q += 64) pl[q] = *M::addr(a, q);
+  const bool valid = lane < a.n;
+  const int row = valid ? lane : 0;
+  const int c0 = s.perm ? s.cursor[0] : 0;
+  if (s.perm) {  // all steps' permutation entries in flight at once, then one LDS table
+    for (int t = 0; t < s.n; ++t) srcs[t][lane] = (int)s.perm[(long)(c0 + t) * s.B + row];
+  }
+  const float w = valid ? (a.row_w ? a.row_w[row] : 1.f / (float)a.n) : 0.f;
+  const float lr = a.lr[0] * a.gscale;
+  const float dl = a.dloss ? a.dloss[0] : 1.f;
+  auto P = [&](int q) -> float { return pl[q]; };
+  __syncthreads();
+  auto src = [&](int t) -> int { return s.perm ? srcs[t][lane] : row; };
+  float x[D0];
+  long long lab;
+  M::load_row(s.x[0], s.y[0], src(0), x, lab);
+  // the first rows arrive here: no load is outstanding at the loop head, so the waitcnt pass does
+  // not make every step wait for its own prefetch (the loop-head wait merges the entry path)
+#pragma unroll
+  for (int i = 0; i < D0; ++i) asm volatile("" : "+v"(x[i]));
+  asm volatile("" : "+v"(lab));
+  for (int t = 0; t < s.n; ++t) {
+    // the next step's rows, loaded now: their wait sits at the end of this step (the label is
+    // clamped at its use, not at the load)
+    float xn[D0];
+    long long ln;
+    const int tn = t + 1 < s.n ? t + 1 : t;  // the last step reloads its own rows (unused)
+    M::load_row(s.x[tn], s.y[tn], src(tn), xn, ln);
+    const float lsum = M::row(P, x, M::clamp_label(lab), w, dl, valid, true, prod + lane * M::PT, nullptr);
+    __syncthreads();
+    for (int q = lane; q < M::T; q += 64) pl[q] -= lr * M::colsum(prod, q);
+    // no global store inside the loop: stores share the in-order vmcnt with the prefetch loads, so
+    // the step-end wait for the next rows would also wait out the store's round trip
+    if (lane == 0) lsums[t] = lsum;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < D0; ++i) x[i] = xn[i];
+    lab = ln;
+  }
+  for (int q = lane; q < M::T; q += 64) *M::addr(a, q) = pl[q];
+  if (lane == 0) {
+    float tot = 0.f;
+    for (int t = 0; t < s.n; ++t) {
+      if (s.loss[t]) s.loss[t][0] = lsums[t];
+      tot += lsums[t];
+    }
+    if (s.loss_sum) s.loss_sum[0] = tot;
+    if (a.step) a.step[0] += (float)s.n;
+    if (s.perm) s.cursor[0] = c0 + s.n;
   }
 }
 
@@ -415,7 +495,35 @@ extern "C" int smi_mlp(const MLPArgs* args, int mode, hipStream_t st) {
   if (mode > 0 && !a.y) return -1;
   if (mode == 1) for (int l = 0; l < a.nlayers; ++l) if (!a.gW[l] || !a.gb[l]) return -1;
   if (mode == 2 && !a.lr) return -1;
-  if (mlp_small_ok(a) && g_mlp_small) hipLaunchKernelGGL((mlp_small_kernel<4, 5, 4, 3>), dim3(1), dim3(64), 0, st, a, mode);
-  else hipLaunchKernelGGL(mlp_kernel, dim3(grid), dim3(64), 0, st, a, mode);
+  if (mlp_small_ok(a) && g_mlp_small) {
+    if (mode == 2 && !a.logits) {
+      // the fused SGD step IS the multi-step kernel with one step: a step is then the same code
+      // whether it runs alone or inside a multi-step launch (bitwise the same training run)
+      MLPSteps s{};
+      s.n = 1; s.x[0] = a.x; s.y[0] = a.y; s.loss[0] = a.loss;
+      if (a.act == 1) hipLaunchKernelGGL((mlp_small_steps_kernel<4, 5, 4, 3, 1>), dim3(1), dim3(64), 0, st, a, s);
+      else hipLaunchKernelGGL((mlp_small_steps_kernel<4, 5, 4, 3, 2>), dim3(1), dim3(64), 0, st, a, s);
+    } else if (a.act == 1) {
+      hipLaunchKernelGGL((mlp_small_kernel<4, 5, 4, 3, 1>), dim3(1), dim3(64), 0, st, a, mode);
+    } else {
+      hipLaunchKernelGGL((mlp_small_kernel<4, 5, 4, 3, 2>), dim3(1), dim3(64), 0, st, a, mode);
+    }
+  } else {
+    hipLaunchKernelGGL(mlp_kernel, dim3(grid), dim3(64), 0, st, a, mode);
+  }
+  SMI_CHECK_LAUNCH();
+}
+
+// s.n fused SGD steps in one launch (the 4-5-4-3 kernel's shapes only: -1 otherwise, the caller
+// runs one launch per step)
+extern "C" int smi_mlp_steps(const MLPArgs* args, const MLPSteps* steps, hipStream_t st) {
+  const MLPArgs& a = *args;
+  const MLPSteps& s = *steps;
+  if (mlp_check(a) || !mlp_small_ok(a) || !g_mlp_small || !a.lr || !a.y || a.logits) return -1;
+  if (s.n < 1 || s.n > MLP_MAX_STEPS || (s.perm && (!s.cursor || s.B != a.n))) return -1;
+  for (int t = 0; t < s.n; ++t)
+    if (!s.x[t] || !s.y[t] || !s.loss[t]) return -1;
+  if (a.act == 1) hipLaunchKernelGGL((mlp_small_steps_kernel<4, 5, 4, 3, 1>), dim3(1), dim3(64), 0, st, a, s);
+  else hipLaunchKernelGGL((mlp_small_steps_kernel<4, 5, 4, 3, 2>), dim3(1), dim3(64), 0, st, a, s);
   SMI_CHECK_LAUNCH();
 }

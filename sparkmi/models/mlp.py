@@ -37,22 +37,59 @@ class MultilayerPerceptron(nn.Module):
         return mlp_loss(x, y, [l.weight for l in lins], [l.bias for l in lins], self.activation, row_weight)
 
 
+    def _fused_sgd_ok(self, opt, x):
+        from .. import _native
+        from ..optim.sgd import SGD
+        flat = getattr(opt, "flat", None)
+        return (x.is_cuda and isinstance(opt, SGD) and not opt.momentum and not opt.weight_decay
+                and getattr(opt, "ranges", None) is None and (flat is None or flat.shadow is None)
+                and _native.use_native(x))
+
+    def gather_in_step(self, opt, ddp, x):
+        """True when every training step will run as the multi-step SGD kernel reading its shuffled
+        rows from the dataset itself (index mode: perm[cursor * B + i]; sparkmi/train/trainer.py
+        with a DeviceLoader(fixed=True)): single executor, plain SGD, the 4-5-4-3 shape, B <= 64."""
+        dims = [self.linears()[0].weight.shape[1]] + [l.weight.shape[0] for l in self.linears()]
+        return (ddp is None and x.dim() == 2 and x.dtype == torch.float32 and x.shape[0] <= 64
+                and dims == [4, 5, 4, 3] and self._fused_sgd_ok(opt, x))
+
     def fused_sgd_step(self, opt, x, y):
         """The whole training step — forward, CE, backward, SGD update — as ONE HIP launch
         (csrc/kernels/mlp.hip mode 2); the loss of the step is returned.  None when it does not
         apply (CPU, an optimizer other than plain SGD, a bf16 shadow to refresh): the caller
         then runs the usual forward/backward/step."""
-        from .. import _native
-        from ..optim.sgd import SGD
-        flat = getattr(opt, "flat", None)
-        if (not x.is_cuda or not isinstance(opt, SGD) or opt.momentum or opt.weight_decay
-                or getattr(opt, "ranges", None) is not None or (flat is not None and flat.shadow is not None)
-                or not _native.use_native(x)):
+        if getattr(x, "_smi_gather", None) is not None:  # index mode: a one-step multi-step launch
+            return self.fused_sgd_steps(opt, [(x, y)])[0]
+        if not self._fused_sgd_ok(opt, x):
             return None
         lins = self.linears()
         return mlp_sgd_step(x, y, [l.weight for l in lins], [l.bias for l in lins], opt.lr_t, opt.step_t,
                             self.activation, grad_scale=opt.grad_scale)
 
+
+    def fused_sgd_steps(self, opt, batches):
+        """Several consecutive fused SGD steps (one per (x, y) of ``batches``) as ONE launch
+        (csrc/kernels/mlp.hip mlp_small_steps_kernel): bitwise the steps of ``fused_sgd_step`` one
+        after another.  Returns the per-step losses, or None when it does not apply (the caller
+        then runs the steps one by one)."""
+        from ..ops.mlp import mlp_sgd_steps
+        lins = self.linears()
+        g = getattr(batches[0][0], "_smi_gather", None)
+        if g is not None:
+            # index mode: every batch is the fixed loader's (empty) buffer; the kernel reads the rows
+            if any(getattr(b[0], "_smi_gather", None) is not g for b in batches):
+                raise RuntimeError("MultilayerPerceptron: index-mode and ordinary batches mixed")
+            out = mlp_sgd_steps([(g[1], g[2])], [l.weight for l in lins], [l.bias for l in lins], opt.lr_t,
+                                opt.step_t, self.activation, grad_scale=opt.grad_scale,
+                                index=(g[0], g[3], g[4], len(batches)))
+            if out is None:
+                raise RuntimeError("MultilayerPerceptron: index-mode batch but the fused step does not apply")
+            return out
+        if (len(batches) > 32 or not all(self._fused_sgd_ok(opt, b[0]) for b in batches)
+                or len({b[0].data_ptr() for b in batches}) != len(batches)):
+            return None
+        return mlp_sgd_steps(batches, [l.weight for l in lins], [l.bias for l in lins], opt.lr_t, opt.step_t,
+                             self.activation, grad_scale=opt.grad_scale)
 
     def fused_grad_step(self, x, y):
         """Forward, CE and backward as ONE HIP launch, the gradients added to the flat gradient

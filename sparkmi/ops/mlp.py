@@ -117,6 +117,41 @@ def mlp_sgd_step(x, y, weights, biases, lr_t, step_t=None, act="sigmoid", row_we
     return loss[0]
 
 
+def mlp_sgd_steps(batches, weights, biases, lr_t, step_t=None, act="sigmoid", grad_scale=1.0, index=None):
+    """``len(batches)`` consecutive fused SGD steps (``mlp_sgd_step`` on each (x, y) in order) in
+    ONE launch — the 4-5-4-3 kernel keeps the parameters on chip between steps, bitwise the same
+    steps.  Returns the per-step losses (device scalars), or None when the shapes are not covered
+    (the caller then runs one launch per step).  ``index`` = (batch, perm, cursor, steps): the
+    batches are read from the dataset ``batches[0]`` = (x_all, y_all), step t's row i being
+    perm[(cursor + t) * batch + i] (DeviceLoader fixed=True, index mode; cursor += steps)."""
+    a = ACT[act] if isinstance(act, str) else act
+    if index is not None:
+        n, perm, cursor, nsteps = index
+        batches = [batches[0]] * nsteps
+    else:
+        n, perm, cursor = batches[0][0].shape[0], None, None
+    if any((index is None and x.shape[0] != n) or x.dtype != torch.float32 or not x.is_contiguous()
+           or y.dtype != torch.int64 or not y.is_contiguous() for x, y in batches):
+        return None
+    # [step losses..., their sum in step order] (the sum: the runner's group total, no reduction launch)
+    losses = torch.empty(len(batches) + 1, device=batches[0][0].device, dtype=torch.float32)
+    ok = _native.C().mlp_steps([x.data_ptr() for x, _ in batches], [y.data_ptr() for _, y in batches],
+                               [losses[i:].data_ptr() for i in range(len(batches))], n, _dims(weights),
+                               [W.data_ptr() for W in weights], [b.data_ptr() for b in biases], a,
+                               lr_t.data_ptr(), _native.ptr(step_t), float(grad_scale), _native.ptr(perm),
+                               _native.ptr(cursor), losses[len(batches):].data_ptr(), _native.stream())
+    if not ok:
+        return None
+    out = StepLosses(losses[i] for i in range(len(batches)))
+    out.total = losses[len(batches)]
+    return out
+
+
+class StepLosses(list):
+    """Per-step losses of a multi-step launch; ``total``: their sum, written by the same kernel."""
+    total = None
+
+
 def mlp_grad_step(x, y, weights, biases, act="sigmoid", row_weight=None):
     """Forward, weighted softmax-CE and backward in ONE launch, the gradients ADDED to the
     parameters' (flat) gradient buffers — the data-parallel step's local half (the all-reduce and

@@ -69,7 +69,8 @@ def train_fn(cfg):
     # one executor: each step is ONE kernel (forward + CE + backward + SGD, csrc/kernels/mlp.hip)
     trainer = Trainer(model, lambda m, x, y: m.loss(x, y), lambda flat: SGD(flat, lr=cfg.lr), cfg, device, rank,
                       world, "mlp", shadow=False, fused_step=lambda m, o, x, y: m.fused_sgd_step(o, x, y),
-                      fused_grad=lambda m, x, y: m.fused_grad_step(x, y))
+                      fused_grad=lambda m, x, y: m.fused_grad_step(x, y),
+                      fused_steps=lambda m, o, bs: m.fused_sgd_steps(o, bs))
     stats = trainer.fit(loader, cfg.epochs)
     trainer.close()
     out = dict(stats, data=source, world=world, n_train=len(ytr), n_test=len(yte))

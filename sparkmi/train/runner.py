@@ -28,7 +28,7 @@ from ..ops.embedding import join_plans
 
 class StepRunner:
     def __init__(self, model, loss_fn, optimizer, ddp=None, graph=False, warmup_eager=3, split_fn=None,
-                 fused_step=None, bind_inputs=False, max_bound=32, fused_grad=None):
+                 fused_step=None, bind_inputs=False, max_bound=32, fused_grad=None, fused_steps=None):
         self.model = model
         # bind_inputs: batches that live at fixed device addresses (an HBM-resident dataset's
         # batch views) are read IN PLACE by a graph captured per batch (shared memory pool, at
@@ -50,6 +50,10 @@ class StepRunner:
         # gradient reduction (data-parallel) and the optimizer follow as usual — a data-parallel
         # small-model step is then that kernel + the IPC all-reduce + the optimizer
         self.fused_grad = fused_grad
+        # fused_steps(model, optimizer, batches) -> [loss per step] or None: several consecutive
+        # single-executor steps in ONE kernel (e.g. MultilayerPerceptron.fused_sgd_steps), used for
+        # the multi-step graphs of run_steps; None falls back to one step at a time
+        self.fused_steps = fused_steps
         # pre_step(): launches that produce the step's inputs in place (e.g. DeviceLoader(fixed=
         # True).pre_step: the next shuffled batch gathered at a device cursor into the buffers the
         # step reads).  Bound / multi-step graphs capture it with the step; every other mode runs
@@ -324,10 +328,19 @@ class StepRunner:
             self._pre_inline = True
             try:
                 with torch.cuda.graph(g, pool=self._bound_pool):
-                    for batch in group:
-                        step_losses.append(self._eager(*batch))
-                    # the group's summed loss inside the graph (metrics read one scalar per group)
-                    total = torch.stack([l.detach().float().reshape(()) for l in step_losses]).sum()
+                    fused = None
+                    if self.fused_steps is not None and self.ddp is None and self.pre_step is None:
+                        fused = self.fused_steps(self.model, self.opt, list(group))
+                    if fused is not None:
+                        step_losses = list(fused)
+                    else:
+                        for batch in group:
+                            step_losses.append(self._eager(*batch))
+                    # the group's summed loss inside the graph (metrics read one scalar per group);
+                    # a multi-step kernel may already have written it
+                    total = getattr(fused, "total", None)
+                    if total is None:
+                        total = torch.stack([l.detach().float().reshape(()) for l in step_losses]).sum()
             finally:
                 self._pre_inline = False
             if self._bound_pool is None:
@@ -359,7 +372,9 @@ class StepRunner:
                     continue
             loss = self.step(*seq[i])
             if losses is not None:
-                losses.append(loss)
+                # a replayed graph returns its static loss, which the next replay of the same graph
+                # (a fixed loader's batches are one key) overwrites: keep this step's value
+                losses.append(loss.detach().clone() if self.graph_requested and loss.is_cuda else loss)
             i += 1
         return loss
 

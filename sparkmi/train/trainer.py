@@ -39,7 +39,8 @@ def setup_executor(cfg):
 
 class Trainer:
     def __init__(self, model, loss_fn, make_optimizer, cfg, device, rank=0, world=1, name="run", shadow=None,
-                 fused_step=None, split_fn=None, flops_per_sample=None, fused_grad=None, sparse_cap=None):
+                 fused_step=None, split_fn=None, flops_per_sample=None, fused_grad=None, sparse_cap=None,
+                 fused_steps=None):
         self.model = model.to(device)
         self.cfg = cfg
         self.device = torch.device(device)
@@ -58,6 +59,7 @@ class Trainer:
         # one kernel (the data-parallel step's local half, reduction and optimizer follow)
         self.runner = StepRunner(self.model, loss_fn, self.opt, ddp=self.ddp, graph=use_graph,
                                  fused_step=fused_step if world == 1 else None,
+                                 fused_steps=fused_steps if world == 1 else None,
                                  fused_grad=fused_grad if world > 1 else None,
                                  split_fn=split_fn if (world > 1 and use_graph) else None)
         path = f"{cfg.metrics}.rank{rank}.jsonl" if cfg.metrics else None

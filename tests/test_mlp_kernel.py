@@ -125,3 +125,65 @@ def test_mlp_small_kernel_matches_generic(n, act, weighted):
     for pa, pb in zip(a[3], b[3]):
         torch.testing.assert_close(pa, pb, rtol=1e-6, atol=1e-7)
     assert float(a[4]) == float(b[4]) == 1.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("steps,n", [(8, 30), (1, 64), (32, 7)])
+def test_mlp_multi_step_kernel_bitwise_equals_single_steps(steps, n):
+    """``steps`` fused SGD steps in ONE launch (parameters on chip between the steps,
+    csrc/kernels/mlp.hip mlp_small_steps_kernel) == the same steps as one launch each: bitwise
+    parameters, per-step losses and the step counter."""
+    from sparkmi.optim import SGD
+    from sparkmi.utils.flat import FlatParams
+    torch.manual_seed(4)
+    a = MultilayerPerceptron((4, 5, 4, 3)).cuda()
+    b = MultilayerPerceptron((4, 5, 4, 3)).cuda()
+    b.load_state_dict(a.state_dict())
+    fa, fb = FlatParams(a, shadow=False), FlatParams(b, shadow=False)
+    oa, ob = SGD(fa, lr=0.3), SGD(fb, lr=0.3)
+    g = torch.Generator().manual_seed(5)
+    batches = [((torch.rand(n, 4, generator=g) * 2 - 1).cuda(), torch.randint(0, 3, (n,), generator=g).cuda())
+               for _ in range(steps)]
+    la = a.fused_sgd_steps(oa, batches)
+    assert la is not None and len(la) == steps
+    lb = [b.fused_sgd_step(ob, x, y) for x, y in batches]
+    assert torch.equal(torch.stack(la), torch.stack(lb))
+    assert torch.equal(fa.master, fb.master)
+    assert float(oa.step_t) == float(ob.step_t) == float(steps)
+
+
+@pytest.mark.gpu
+def test_mlp_trainer_index_mode_multistep_bitwise():
+    """The MLP recipe path: Trainer + DeviceLoader(fixed=True) with the multi-step kernel reading
+    its shuffled rows from the dataset (index mode, 4 steps per launch, an epoch boundary inside the
+    run) trains bitwise the same parameters as the per-batch gather with one launch per step."""
+    from sparkmi.data.dataset import DeviceLoader
+    from sparkmi.optim import SGD
+    from sparkmi.recipes.mlp import MLPConfig
+    from sparkmi.train.trainer import Trainer
+
+    def run(fixed, unroll):
+        torch.manual_seed(0)
+        g = torch.Generator().manual_seed(8)
+        x = torch.rand(30 * 10, 4, generator=g) * 2 - 1
+        y = torch.randint(0, 3, (30 * 10,), generator=g)
+        cfg = MLPConfig(batch_size=30, lr=0.2, log_every=5, verbose=False, unroll=unroll, max_steps=23)
+        loader = DeviceLoader([x, y], 30, "cuda", shuffle=True, drop_last=True, seed=3, fixed=fixed)
+        model = MultilayerPerceptron((4, 5, 4, 3))
+        tr = Trainer(model, lambda m, a, b: m.loss(a, b), lambda flat: SGD(flat, lr=cfg.lr), cfg, "cuda", 0, 1, "t",
+                     shadow=False, fused_step=lambda m, o, a, b: m.fused_sgd_step(o, a, b),
+                     fused_steps=lambda m, o, bs: m.fused_sgd_steps(o, bs))
+        res = tr.fit(loader, 10)
+        recs = list(tr.metrics.records)
+        tr.close()
+        return tr.flat.master.cpu().clone(), res, recs, tr.runner
+
+    pa, ra, la, _ = run(False, 1)
+    pb, rb, lb, runner = run(True, 4)
+    assert ra["steps"] == rb["steps"] == 23
+    assert runner.pre_step is None, "index mode engaged"
+    assert runner._multi, "multi-step graphs ran"
+    assert torch.equal(pa, pb)
+    assert [r["step"] for r in la] == [r["step"] for r in lb]
+    for u, v in zip(la, lb):
+        assert abs(u["loss"] - v["loss"]) <= 1e-6 * max(1.0, abs(u["loss"])), (u, v)

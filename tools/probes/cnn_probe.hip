@@ -1,7 +1,12 @@
 // Per-phase timing of the fused CNN kernel (one workgroup per image): s_memtime after every
 // barrier (-DCNN_STAMPS diagnostic build), averaged over images.
+#ifndef CNN_PROBE_NOSTAMP  // -DCNN_PROBE_NOSTAMP: the production kernel, launch timing only
 #define CNN_STAMPS
-#include "../../csrc/kernels/cnn.hip"
+#endif
+#ifndef CNN_SRC  // -DCNN_SRC='"path"': another version of the kernel (tools/cnn_ab.sh)
+#define CNN_SRC "../../csrc/kernels/cnn.hip"
+#endif
+#include CNN_SRC
 #include <cstdio>
 #include <vector>
 
@@ -48,7 +53,9 @@ int main(int argc, char** argv) {
   for (int it = 0; it < 20; ++it) smi_cnn(&g, 0);
   (void)hipDeviceSynchronize();
   std::vector<unsigned long long> st(64 * 32);
+#ifdef CNN_STAMPS
   (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(cnn_stamps), st.size() * 8);
+#endif
   int nph = 0;
   for (int i = 0; i < 21; ++i) if (st[i]) nph = i + 1;
   printf("phases %d\n", nph);
@@ -98,5 +105,20 @@ int main(int argc, char** argv) {
   (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
   float ms; (void)hipEventElapsedTime(&ms, e0, e1);
   printf("kernel+loss: %.1f us per call\n", ms * 1000 / 50);
+  // the same launches captured in one graph (the bench's replay: no host launch gaps)
+  hipStream_t cs; (void)hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
+  hipGraph_t gr; hipGraphExec_t ge;
+  (void)hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed);
+  for (int it = 0; it < 50; ++it) smi_cnn(&g, cs);
+  (void)hipStreamEndCapture(cs, &gr);
+  (void)hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0);
+  (void)hipGraphLaunch(ge, cs); (void)hipStreamSynchronize(cs);
+  float best = 1e9f;
+  for (int r = 0; r < 5; ++r) {
+    (void)hipEventRecord(e0, cs); (void)hipGraphLaunch(ge, cs); (void)hipEventRecord(e1, cs);
+    (void)hipEventSynchronize(e1); (void)hipEventElapsedTime(&ms, e0, e1);
+    best = ms < best ? ms : best;
+  }
+  printf("graph: %.2f us per step (best of 5 x 50)\n", best * 1000 / 50);
   return 0;
 }
