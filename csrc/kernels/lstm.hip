@@ -193,7 +193,9 @@ __global__ __launch_bounds__(NT) void lstm_fwd_kernel(LSTMArgs a) {
     __shared__ float s_plast[LSTM_MAXC];
     const float* top = wsb + (size_t)(L - 1) * T * 6 * H + 5 * H;
     for (int i = tid; i < C * H; i += blockDim.x) s_wfc[i] = a.w_fc[i];
-    for (int t0 = 0; t0 < T; t0 += LSTM_TCH) {
+    // pred == null (the fused-CE training step, whose loss reads the last step only): the head at
+    // the last step alone (the other steps' predictions have no consumer)
+    for (int t0 = a.pred ? 0 : T - 1; t0 < T; t0 += LSTM_TCH) {
       const int nc = min(LSTM_TCH, T - t0);
       __syncthreads();
       for (int i = tid; i < nc * H; i += blockDim.x) s_top[i] = top[(size_t)(t0 + i / H) * 6 * H + i % H];
@@ -206,7 +208,7 @@ __global__ __launch_bounds__(NT) void lstm_fwd_kernel(LSTMArgs a) {
           s0 += s_wfc[cc * H + j] * s_top[t * H + j];
           s1 += s_wfc[cc * H + j + 1] * s_top[t * H + j + 1];
         }
-        a.pred[((size_t)b * T + t0 + t) * C + cc] = s0 + s1;
+        if (a.pred) a.pred[((size_t)b * T + t0 + t) * C + cc] = s0 + s1;
         if (a.pred_last && t0 + t == T - 1) a.pred_last[(size_t)b * C + cc] = s0 + s1;
         if (t0 + t == T - 1) s_plast[cc] = s0 + s1;
       }
@@ -612,7 +614,9 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
     __shared__ float s_plast[LSTM_MAXC];
     const float* top = wsb + (size_t)(L - 1) * T * 6 * H + 5 * H;
     for (int i = tid; i < C * H; i += blockDim.x) s_wfc[i] = a.w_fc[i];
-    for (int t0 = 0; t0 < T; t0 += LSTM_TCH) {
+    // pred == null (the fused-CE training step, whose loss reads the last step only): the head at
+    // the last step alone (the other steps' predictions have no consumer)
+    for (int t0 = a.pred ? 0 : T - 1; t0 < T; t0 += LSTM_TCH) {
       const int nc = min(LSTM_TCH, T - t0);
       __syncthreads();
       for (int i = tid; i < nc * H; i += blockDim.x) s_top[i] = top[(size_t)(t0 + i / H) * 6 * H + i % H];
@@ -625,7 +629,7 @@ __global__ __launch_bounds__(128) void lstm_fwd_w2_kernel(LSTMArgs a) {
           s0 += s_wfc[cc * H + q] * s_top[t * H + q];
           s1 += s_wfc[cc * H + q + 1] * s_top[t * H + q + 1];
         }
-        a.pred[((size_t)b * T + t0 + t) * C + cc] = s0 + s1;
+        if (a.pred) a.pred[((size_t)b * T + t0 + t) * C + cc] = s0 + s1;
         if (a.pred_last && t0 + t == T - 1) a.pred_last[(size_t)b * C + cc] = s0 + s1;
         if (t0 + t == T - 1) s_plast[cc] = s0 + s1;
       }

@@ -78,7 +78,8 @@ class LSTMFn(torch.autograd.Function):
         ids = ids.to(torch.int64).contiguous()
         if not all(t.is_contiguous() and t.dtype == torch.float32 for t in params):
             raise ValueError("LSTM parameters must be contiguous fp32")
-        pred = torch.empty(B, T, C, device=dev, dtype=torch.float32)
+        # the fused-CE step returns (loss, pred[:, -1]) only: no [B, T, C] head output is computed
+        pred = torch.empty(B, T, C, device=dev, dtype=torch.float32) if labels is None else None
         last = torch.empty(B, C, device=dev, dtype=torch.float32)  # pred[:, -1] written by the kernel too
         hn = torch.empty(L, B, H, device=dev, dtype=torch.float32)
         cn = torch.empty_like(hn)
@@ -101,7 +102,7 @@ class LSTMFn(torch.autograd.Function):
         _native.C().lstm(0, ids.data_ptr(), B, T, E, H, L, C, pad_idx, emb.data_ptr(),
                          [lw[0].data_ptr() for lw in layers], [lw[1].data_ptr() for lw in layers],
                          [lw[2].data_ptr() for lw in layers], [lw[3].data_ptr() for lw in layers],
-                         w_fc.data_ptr(), b_fc.data_ptr(), _native.ptr(h0c), _native.ptr(c0c), pred.data_ptr(),
+                         w_fc.data_ptr(), b_fc.data_ptr(), _native.ptr(h0c), _native.ptr(c0c), _native.ptr(pred),
                          hn.data_ptr(), cn.data_ptr(), ws.data_ptr(), 0, rng.ptr() if rng is not None else 0, salt,
                          thresh, _rng.scale(p), 0, 0, 0, 0, [], [], [], [], 0, 0, 0, 0, 0, 0,
                          emb.shape[0] if plan_ws is not None else 0, _native.ptr(plan_ws),
