@@ -355,7 +355,10 @@ def bench_cnn_recipe(args, rank, world, device, dtype="bf16"):
     barrier()
     _sync(device)
     t0 = time.perf_counter()
-    tr.cfg = dataclasses.replace(cfg, max_steps=warm + args.cnn_steps)
+    # one whole epoch of the shard (or more): the per-fit setup (epoch shuffle, loader reset) is
+    # amortised as in a real run instead of dominating a short timed window
+    timed = max(args.cnn_steps, n // cfg.batch_size)
+    tr.cfg = dataclasses.replace(cfg, max_steps=warm + timed)
     res = tr.fit(loader, 10 ** 6)
     _sync(device)
     barrier()
