@@ -94,6 +94,7 @@ void smi_gemm_set_bm(int);
 int smi_gemm_wgrad_group(const void* const*, const long*, const void* const*, const long*, void* const*, void* const*,
                          const int*, const int*, const int*, int, hipStream_t);
 int smi_cnn(const CNNArgs*, hipStream_t);
+int smi_cnn_hand_floats(int C);
 int smi_cnn_fused_ok(int, int, int, int);
 long smi_emb_pair_max(long);
 int smi_emb_plan_algo(long, long);
@@ -561,7 +562,7 @@ PYBIND11_MODULE(_C, m) {
   // the fused slab reduction + SGD update in the kernel's tail (CNNArgs::fused)
   m.def("cnn_sgd_step", [](u x, int x_u8, float x_scale, u y, int B, int cin, int C, int classes, std::vector<u> w,
                            std::vector<u> b, std::vector<u> shadow, u slab, u part, u row_loss, u loss,
-                           float loss_scale, u lr, u step, u tick, int bf16, u perm, u cursor, u st) {
+                           float loss_scale, u lr, u step, u tick, int bf16, u perm, u cursor, u hand, u st) {
     CNNArgs a{};
     a.bf16 = bf16;
     if (w.size() != 5 || b.size() != 5) throw std::runtime_error("cnn_sgd_step: need 5 weight and 5 bias pointers");
@@ -576,6 +577,8 @@ PYBIND11_MODULE(_C, m) {
     a.P = o; a.slab = (float*)slab; a.part = (float*)part; a.row_loss = (float*)row_loss; a.loss = (float*)loss;
     a.loss_scale = loss_scale; a.train = 1; a.fused = 1;
     a.lr = (const float*)lr; a.step = (float*)step; a.tick = (unsigned*)tick;
+    // the helpers' flags follow the tail's CNN_GRP + 1 tickets in the model's tick block
+    a.hand = (float*)hand; a.hflag = hand ? a.tick + CNN_GRP + 1 : nullptr;
     a.perm = (const long long*)perm; a.cursor = (int*)cursor;
     chk(smi_cnn(&a, S(st)), "cnn_sgd_step");
   });
@@ -583,7 +586,7 @@ PYBIND11_MODULE(_C, m) {
   // to gw / gb (the flat gradient buffer) instead of updating the parameters
   m.def("cnn_grad_step", [](u x, int x_u8, float x_scale, u y, int B, int cin, int C, int classes, std::vector<u> w,
                             std::vector<u> b, std::vector<u> gw, std::vector<u> gb, u slab, u part, u row_loss, u loss,
-                            float loss_scale, u tick, int bf16, u perm, u cursor, u st) {
+                            float loss_scale, u tick, int bf16, u perm, u cursor, u hand, u st) {
     CNNArgs a{};
     a.bf16 = bf16;
     if (w.size() != 5 || b.size() != 5 || gw.size() != 5 || gb.size() != 5)
@@ -598,6 +601,7 @@ PYBIND11_MODULE(_C, m) {
     for (int i = 0; i < 10; ++i) { a.off[i] = o; o += sz[i]; }
     a.P = o; a.slab = (float*)slab; a.part = (float*)part; a.row_loss = (float*)row_loss; a.loss = (float*)loss;
     a.loss_scale = loss_scale; a.train = 1; a.fused = 1; a.lr = nullptr; a.tick = (unsigned*)tick;
+    a.hand = (float*)hand; a.hflag = hand ? a.tick + CNN_GRP + 1 : nullptr;
     a.perm = (const long long*)perm; a.cursor = (int*)cursor;
     chk(smi_cnn(&a, S(st)), "cnn_grad_step");
   });
@@ -619,6 +623,7 @@ PYBIND11_MODULE(_C, m) {
         "deterministic embedding backward: 1 = pair-compare (<= 8192 tokens), 0 = bucketed lists; -1 queries");
   m.def("cnn_fused_ok", [](int C, int cin, int classes, int B) { return smi_cnn_fused_ok(C, cin, classes, B) != 0; });
   m.def("cnn_grp", []() { return (int)CNN_GRP; });  // images per fused-tail group (part rows, tickets)
+  m.def("cnn_hand_floats", [](int C) { return smi_cnn_hand_floats(C); });  // 0: weight-gradient helpers off
 
   m.def("lstm_supported", [](int E, int H, int L, int C) { return smi_lstm_supported(E, H, L, C) != 0; });
   m.def("lstm_slab_floats", [](int B, int E, int H, int L, int C) { return smi_lstm_slab_floats(B, E, H, L, C); });

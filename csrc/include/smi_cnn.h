@@ -26,6 +26,11 @@ struct CNNArgs {
   // whole HBM-resident dataset and image i of the batch is row perm[cursor[0] * B + i]; the step's
   // last workgroup advances the device cursor — the shuffled batch gather inside the step kernel
   const long long* perm; int* cursor;
+  // WEIGHT-GRADIENT HELPERS (fused steps; hand != null): 3 extra workgroups per image compute the
+  // conv4 / conv3 / conv2 weight gradients from (dz, input) plane sets the image's workgroup hands
+  // over through `hand` ([B][cnn_hand_floats(C)]); hflag: 3 * B zeroed flags (re-armed by the
+  // helpers) — the image's workgroup runs the dgrad chain meanwhile
+  float* hand; unsigned* hflag;
 };
 #ifndef CNN_GRP
 #define CNN_GRP 8

@@ -23,7 +23,7 @@
 // enough independent work items (the batch of 32 images occupies only 32 CUs)
 #define CNN_THREADS 1024
 #ifdef CNN_STAMPS  // diagnostic build only (tools/probes/cnn_probe.hip): per-phase s_memtime
-__device__ unsigned long long cnn_stamps[64 * 32];
+__device__ unsigned long long cnn_stamps[256 * 32];  // image + helper workgroups
 #define STAMP(i)                                                                            \
   do {                                                                                      \
     if (threadIdx.x == 0) {                                                                 \
@@ -32,8 +32,15 @@ __device__ unsigned long long cnn_stamps[64 * 32];
       cnn_stamps[blockIdx.x * 32 + (i)] = t_;                                               \
     }                                                                                       \
   } while (0)
+// global-clock (s_memrealtime, 100 MHz, one clock for every XCD) stamps: cross-workgroup timing
+__device__ unsigned long long cnn_rstamps[256 * 8];
+#define RSTAMP(i)                                                                           \
+  do {                                                                                      \
+    if (threadIdx.x == 0) cnn_rstamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #else
 #define STAMP(i) do {} while (0)
+#define RSTAMP(i) do {} while (0)
 #endif
 #define P28 30   // 28x28 plane with 1-pixel zero halo
 #define P14 16   // 14x14 plane with 1-pixel zero halo
@@ -54,6 +61,9 @@ __device__ unsigned long long cnn_stamps[64 * 32];
 #endif
 #define PL28 CPL(P28)
 #define PL14 CPL(P14)
+// weight-gradient helper workgroups per image (CNNArgs::hand): conv4, conv3, conv2 (two halves of
+// its columns)
+#define CNN_HELPERS 4
 
 __device__ __forceinline__ int i28(int c, int y, int x) { return c * PL28 + (y + 1) * P28 + (x + 1); }
 __device__ __forceinline__ int i14(int c, int y, int x) { return c * PL14 + (y + 1) * P14 + (x + 1); }
@@ -207,8 +217,10 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 #define WG_SCRATCH (12 * 256)  // floats: up to 12 units of one 16x16 tile
 
 template <int H, int PP>
+// [tlo, thi): the 16-column tiles to compute (a weight-gradient helper takes half of conv2's)
 __device__ __forceinline__ void conv_wgrad(const float* __restrict__ dz, const float* __restrict__ in, int cin, int cout,
-                           float* __restrict__ acc, float* __restrict__ scratch, int sb = -1) {
+                           float* __restrict__ acc, float* __restrict__ scratch, int sb = -1, int tlo = 0,
+                           int thi = 1 << 20) {
   // k-steps come in groups of 7 = 28 positions (one row at H = 28, two at H = 14), so a lane's
   // 7 gather offsets inside a group are fixed: per group, 14 LDS reads at precomputed addresses,
   // 14 address increments and 7 MFMAs — no per-step index math (per-step y/x updates and
@@ -217,7 +229,7 @@ __device__ __forceinline__ void conv_wgrad(const float* __restrict__ dz, const f
   static_assert(H * H % 28 == 0, "position groups");
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
   const int ncol = cin * 9 + 1;            // im2col columns + bias column
-  const int nt = (ncol + 15) >> 4;         // 16-column tiles
+  const int t_hi = min(thi, (ncol + 15) >> 4), nt = t_hi - tlo;  // 16-column tiles of this call
   const int nch = max(1, min(min(nw, WG_SCRATCH / 256) / nt, NG));  // group chunks per tile
   const int units = nt * nch;
   const int i = lane & 15, kq = lane >> 4;
@@ -233,7 +245,7 @@ __device__ __forceinline__ void conv_wgrad(const float* __restrict__ dz, const f
   const int astr = aok ? GROWS * PP : 0;
   for (int u = wv; u < units; u += nw) {
     const int t = u % nt, ch = u / nt;
-    const int n = t * 16 + i;              // this lane's B column (j = lane & 15)
+    const int n = (tlo + t) * 16 + i;      // this lane's B column (j = lane & 15)
     const float* bbase;
     int bstr = 0;
     const bool bg = n < cin * 9;
@@ -278,7 +290,8 @@ __device__ __forceinline__ void conv_wgrad(const float* __restrict__ dz, const f
   for (int e = threadIdx.x; e < nwt + cout; e += blockDim.x) {
     const int co = e < nwt ? e / (cin * 9) : e - nwt;
     const int col = e < nwt ? e - co * cin * 9 : cin * 9;
-    const int tt = col >> 4, j = col & 15;
+    const int tt = (col >> 4) - tlo, j = col & 15;
+    if (tt < 0 || tt >= nt) continue;  // another call's tile
     float v = 0.f;
     for (int c = 0; c < nch; ++c) v += scratch[(c * nt + tt) * 256 + co * 16 + j];
     acc[e] = v;
@@ -428,11 +441,12 @@ __device__ __forceinline__ void conv_mfma(const float* __restrict__ in, int nin,
 // plane read the next buffer's finite values (times dz = 0).
 template <int H, int PP>
 __device__ __forceinline__ void conv_wgrad_bf16(const float* __restrict__ dz, const float* __restrict__ in, int cin, int cout,
-                                                float* __restrict__ acc, float* __restrict__ scratch) {
+                                                float* __restrict__ acc, float* __restrict__ scratch, int tlo = 0,
+                                                int thi = 1 << 20) {
   constexpr int KS = (H * PP + H - PP + 1 + 31) / 32;  // 32-position k-steps
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
   const int ncol = cin * 9 + 1;
-  const int nt = (ncol + 15) >> 4;
+  const int t_hi = min(thi, (ncol + 15) >> 4), nt = t_hi - tlo;  // 16-column tiles of this call
   const int nch = max(1, min(min(nw, WG_SCRATCH / 256) / nt, KS));
   const int units = nt * nch;
   const int i = lane & 15, g = lane >> 4;
@@ -440,7 +454,7 @@ __device__ __forceinline__ void conv_wgrad_bf16(const float* __restrict__ dz, co
   const float* pa = dz + (aok ? i : 0) * CPL(PP);
   for (int u = wv; u < units; u += nw) {
     const int t = u % nt, ch = u / nt;
-    const int n = t * 16 + i;  // this lane's B column
+    const int n = (tlo + t) * 16 + i;  // this lane's B column
     const int mode = n < cin * 9 ? 0 : (n == cin * 9 ? 1 : 2);  // gather / bias ones / padding zeros
     int boff = 0;
     if (mode == 0) {
@@ -488,7 +502,8 @@ __device__ __forceinline__ void conv_wgrad_bf16(const float* __restrict__ dz, co
   for (int e = threadIdx.x; e < nwt + cout; e += blockDim.x) {
     const int co = e < nwt ? e / (cin * 9) : e - nwt;
     const int col = e < nwt ? e - co * cin * 9 : cin * 9;
-    const int tt = col >> 4, j = col & 15;
+    const int tt = (col >> 4) - tlo, j = col & 15;
+    if (tt < 0 || tt >= nt) continue;  // another call's tile
     float v = 0.f;
     for (int c = 0; c < nch; ++c) v += scratch[(c * nt + tt) * 256 + co * 16 + j];
     acc[e] = v;
@@ -528,9 +543,11 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
   const __amdgpu_buffer_rsrc_t rpart = smi_rsrc(g.part, ngrp * P * 4);
   smi_wt_drain();  // this wave's slab stores reached the coherence point
   __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(g.tick + grp, 1u) == (unsigned)(g1 - g0 - 1);
+  const unsigned parts = g.hand ? 1u + CNN_HELPERS : 1u;  // the image's workgroup + its helpers
+  if (threadIdx.x == 0) last = atomicAdd(g.tick + grp, 1u) == parts * (unsigned)(g1 - g0) - 1u;
   __syncthreads();
   if (!last) return;
+  RSTAMP(5);
   STAMP(26);
   // Loads below are unconditional (a lane's or image's out-of-range granule reads 0 through the
   // buffer resource's range check, or a clamped valid address): a load under a branch makes the
@@ -555,6 +572,7 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
   }
   __syncthreads();
   if (!last) return;
+  RSTAMP(6);
   STAMP(28);
   // level 2.  Stage every image's dl / p2 row (R4 floats) in LDS (the activation planes are free),
   // sum the conv group partials in group order and form the fc gradient from the staged rows
@@ -742,6 +760,7 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
     if (g.shadow[9]) g.shadow[9][o] = f2bf(np);
   }
   STAMP(29);
+  RSTAMP(7);
   if (threadIdx.x < 64) {
     const float ls = wave_sum(rl);
     if (threadIdx.x == 0) {
@@ -751,14 +770,79 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
       g.tick[CNN_GRP] = 0u;
     }
   }
+  // the weight-gradient helpers' hand-off flags, re-armed for the next launch (every helper read
+  // its flag before its ticket; conv2's flag is read by two helpers, so none of them re-arms it)
+  if (g.hflag)
+    for (int i = threadIdx.x; i < 3 * g.B; i += blockDim.x)
+      __hip_atomic_store(g.hflag + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// CC: channel capacity; EX: g.C == CC exactly (compile-time channel count, no clamps)
+// ---- weight-gradient helpers (CNNArgs::hand): the weight gradients off the image's critical path
+// The image workgroup's backward is a chain (unpool, dgrad, unpool, dgrad) with a weight gradient
+// beside every dgrad; the three large ones (conv4, conv3, conv2: ~60 % of the weight-gradient
+// clocks) need only the layer's dz and input planes.  The image workgroup hands those two plane
+// sets over through global memory (write-through 16-B stores issued before the dgrad that
+// overwrites the input in place, drained by the barrier after it; conv2's drained at once: it is
+// the longest) and raises a flag; helper workgroup (image, layer) polls the flag (one lane,
+// bounded: a timed-out helper writes NaN gradients instead of hanging), loads the planes into the
+// same padded LDS layout, runs the same conv_wgrad, writes the layer's slab entries and joins the
+// fused tail's ticket (4 arrivals per image).  Helpers are dispatched after every image workgroup
+// (higher block index), so an image never waits for a slot held by a helper.
+__host__ __device__ __forceinline__ int cnn_hand_f(int C) { return 2 * C * PL14 + C * PL28; }
+// dz plane-set offset of helper j (0: conv4, 1: conv3, 2: conv2) in an image's hand-off area
+__host__ __device__ __forceinline__ int cnn_hand_dz(int C, int j) { return j * C * PL14; }
+
+// copy n floats (n % 4 == 0, 16-B aligned) of LDS plane sets into the hand-off area (write-through)
+__device__ __forceinline__ void cnn_hand_put(__amdgpu_buffer_rsrc_t rs, int dst, const float* src, int n) {
+  for (int i = threadIdx.x; i < n / 4; i += blockDim.x)
+    smi_wt_store4(rs, (dst + 4 * i) * 4, reinterpret_cast<const float4*>(src)[i]);
+}
+__device__ __forceinline__ void cnn_hand_publish(const CNNArgs& g, int img, int j) {
+  if (threadIdx.x == 0) __hip_atomic_store(g.hflag + 3 * img + j, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Helper j of image img, after recomputing its layer's input planes (the image's forward prefix, in
+// the same LDS layout: bitwise the image workgroup's values) while the image workgroup works: wait
+// for the flag, load dz into its plane set, the layer's weight gradient, the slab entries.
+template <int H, int PP, bool BF>
+__device__ __forceinline__ void cnn_helper_finish(const CNNArgs& g, int img, int j, int C, float* dz, const float* in,
+                                                  float* wacc, float* wscr, int tlo = 0, int thi = 1 << 20) {
+  __shared__ int s_bad;
+  if (threadIdx.x == 0) {
+    int bad = 0;
+    for (int it = 0; __hip_atomic_load(g.hflag + 3 * img + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u; ++it) {
+      if (it >= (1 << 22)) { bad = 1; break; }
+      __builtin_amdgcn_s_sleep(4);
+    }
+    s_bad = bad;
+  }
+  __syncthreads();
+  RSTAMP(1);
+  const __amdgpu_buffer_rsrc_t rs = smi_rsrc(g.hand + (long)img * cnn_hand_f(C), cnn_hand_f(C) * 4);
+  const int d0 = cnn_hand_dz(C, j), n4 = C * CPL(PP) / 4;
+  for (int i = threadIdx.x; i < n4; i += blockDim.x) reinterpret_cast<float4*>(dz)[i] = smi_cc_load4(rs, (d0 + 4 * i) * 4);
+  __syncthreads();
+  RSTAMP(2);
+  if (BF) conv_wgrad_bf16<H, PP>(dz, in, C, C, wacc, wscr, tlo, thi);
+  else conv_wgrad<H, PP>(dz, in, C, C, wacc, wscr, -1, tlo, thi);
+  __syncthreads();
+  RSTAMP(3);
+  const bool bad = s_bad != 0;
+  const int ow = g.off[6 - 2 * j], ob = g.off[7 - 2 * j];  // conv4 / conv3 / conv2 weight, bias
+  float* gs = g.slab + (long)img * g.P;
+  for (int e = threadIdx.x; e < C * C * 9 + C; e += blockDim.x) {
+    const int col = e < C * C * 9 ? e % (C * 9) : C * 9;
+    if ((col >> 4) < tlo || (col >> 4) >= thi) continue;  // the other helper's columns
+    smi_wt_store(gs + (e < C * C * 9 ? ow + e : ob + e - C * C * 9), bad ? __builtin_nanf("") : wacc[e]);
+  }
+}
+
+// One image's forward + backward; true when the fused tail follows (training).  role >= 0: weight-
+// gradient helper role (0: conv4, 1: conv3, 2: conv2) of image img — the forward prefix up to that
+// layer's input, then cnn_helper_finish.  CC: channel capacity; EX: g.C == CC exactly (compile-time channel count)
 template <int CC, bool EX, bool BF>
-__global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
+__device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int img, const int role) {
   const int C = EX ? CC : g.C, CI = g.cin, NC = g.classes;
-  const int img = blockIdx.x;
   // the dataset row of this image (index mode: two dependent scalar loads, issued before the
   // weight staging and LDS clearing so their latency hides behind them)
   const long src = g.perm ? g.perm[(long)g.cursor[0] * g.B + img] : (long)img;
@@ -803,7 +887,7 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   // the label (thread 0 computes the loss), loaded now so its memory round trip overlaps the
   // image load and conv1 instead of stalling the cross-entropy (measured ~2k clocks)
   int lab0 = 0;
-  if (threadIdx.x == 0 && g.y) lab0 = (int)g.y[src];
+  if (threadIdx.x == 0 && g.y && role < 0) lab0 = (int)g.y[src];
   // image load (+ ToTensor scaling)
   for (int e = threadIdx.x; e < CI * 784; e += blockDim.x) {
     const int c = e / 784, r = e % 784;
@@ -821,6 +905,10 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   else conv_fwd<28, P28, CC, EX>(xin, CI, a1, C, g.w[0], g.b[0]);
   __syncthreads();
   STAMP(2);
+  if (role >= 2) {  // conv2's two helpers (column tiles [0, 3) / [3, 6)): their input is a1
+    cnn_helper_finish<28, P28, BF>(g, img, 2, C, a2, a1, wacc, wscr, role == 2 ? 0 : 3, role == 2 ? 3 : 1 << 20);
+    return true;
+  }
   CNN_PIN(lab0);  // arrived during conv1
   if (BF) conv_mfma<28, P28, false, false>(a1, C, a2, C, lw[1], lb[1], wscr);
   else conv_fwd<28, P28, CC, EX>(a1, C, a2, C, g.w[1], g.b[1]);
@@ -829,10 +917,18 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   pool_fwd<28, P28, P14, 1>(a2, p1, C);
   __syncthreads();
   STAMP(4);
+  if (role == 1) {  // conv3's helper: its input is p1
+    cnn_helper_finish<14, P14, BF>(g, img, 1, C, a3, p1, wacc, wscr);
+    return true;
+  }
   if (BF) conv_mfma<14, P14, false, false>(p1, C, a3, C, lw[2], lb[2], wscr);
   else conv_fwd<14, P14, CC, EX>(p1, C, a3, C, g.w[2], g.b[2]);
   __syncthreads();
   STAMP(5);
+  if (role == 0) {  // conv4's helper: its input is a3
+    cnn_helper_finish<14, P14, BF>(g, img, 0, C, a4, a3, wacc, wscr);
+    return true;
+  }
   if (BF) conv_mfma<14, P14, false, false>(a3, C, a4, C, lw[3], lb[3], wscr);
   else conv_fwd<14, P14, CC, EX>(a3, C, a4, C, g.w[3], g.b[3]);
   __syncthreads();
@@ -874,7 +970,7 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
     __shared__ int cnn_last;
     smi_wt_drain();
     __syncthreads();
-    if (threadIdx.x == 0) cnn_last = atomicAdd(&cnn_loss_ticket, 1u) == gridDim.x - 1;
+    if (threadIdx.x == 0) cnn_last = atomicAdd(&cnn_loss_ticket, 1u) == (unsigned)g.B - 1;
     __syncthreads();
     if (cnn_last && threadIdx.x < 64) {
       float s = 0.f;
@@ -887,7 +983,7 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
       }
     }
   }
-  if (!g.train) return;
+  if (!g.train) return false;
   __syncthreads();
   STAMP(9);
   float* gs = g.slab + (long)img * g.P;  // this image's gradient slab
@@ -909,6 +1005,46 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   unpool_relu_inplace<14, P14>(a4, p2, 7, 0, C);
   __syncthreads();
   STAMP(12);
+  if (g.hand) {
+    // conv4 / conv3 / conv2 weight gradients by the helpers (which recomputed the layers' inputs);
+    // this workgroup hands over each dz and runs the dgrad chain.  dz4 / dz3 are drained by the
+    // barrier after the next dgrad, conv2's (the largest weight gradient) at once
+    const __amdgpu_buffer_rsrc_t rh = smi_rsrc(g.hand + (long)img * cnn_hand_f(C), cnn_hand_f(C) * 4);
+    cnn_hand_put(rh, cnn_hand_dz(C, 0), a4, C * PL14);  // dz4
+    if (BF) conv_mfma<14, P14, true, true>(a4, C, a3, C, lw[3], nullptr, wscr);
+    else conv_dgrad<14, P14, CC, EX>(a4, C, g.w[3], C, a3, true);
+    smi_wt_drain();
+    __syncthreads();
+    cnn_hand_publish(g, img, 0);
+    STAMP(14);
+    cnn_hand_put(rh, cnn_hand_dz(C, 1), a3, C * PL14);  // dz3
+    if (BF) conv_mfma<14, P14, true, false>(a3, C, p1, C, lw[2], nullptr, wscr);
+    else conv_dgrad<14, P14, CC, EX>(a3, C, g.w[2], C, p1, false);
+    smi_wt_drain();
+    __syncthreads();
+    cnn_hand_publish(g, img, 1);
+    STAMP(16);
+    unpool_relu_inplace<28, P28>(a2, p1, P14, 1, C);
+    __syncthreads();
+    STAMP(17);
+    cnn_hand_put(rh, cnn_hand_dz(C, 2), a2, C * PL28);  // dz2
+    smi_wt_drain();
+    __syncthreads();
+    cnn_hand_publish(g, img, 2);
+    STAMP(18);
+    RSTAMP(1);
+    if (BF) conv_mfma<28, P28, true, true>(a2, C, a1, C, lw[1], nullptr, wscr);
+    else conv_dgrad<28, P28, CC, EX>(a2, C, g.w[1], C, a1, true);
+    __syncthreads();
+    STAMP(19);
+    if (BF) conv_wgrad_bf16<28, P28>(a1, xin, CI, C, wacc, wscr);
+    else conv_wgrad<28, P28>(a1, xin, CI, C, wacc, wscr, 23);
+    __syncthreads();
+    STAMP(20);
+    for (int e = threadIdx.x; e < C * CI * 9 + C; e += blockDim.x)
+      smi_wt_store(gs + (e < C * CI * 9 ? g.off[0] + e : g.off[1] + e - C * CI * 9), wacc[e]);
+    return true;
+  }
   // conv4: dW4, db4 (from dz4, a3); then dz3 = convT(dz4) * relu'(a3) in a3
   if (BF) conv_wgrad_bf16<14, P14>(a4, a3, C, C, wacc, wscr);
   else conv_wgrad<14, P14>(a4, a3, C, C, wacc, wscr, 25);
@@ -959,6 +1095,21 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   STAMP(20);
   for (int e = threadIdx.x; e < C * CI * 9 + C; e += blockDim.x)
     smi_wt_store(gs + (e < C * CI * 9 ? g.off[0] + e : g.off[1] + e - C * CI * 9), wacc[e]);
+  return true;
+}
+
+// one workgroup per image (+ with CNNArgs::hand, three weight-gradient helpers per image after
+// them); every workgroup of a fused step then joins the tail (its one call site: a second inlined
+// copy of the register-heavy tail made the whole kernel spill)
+template <int CC, bool EX, bool BF>
+__global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  RSTAMP(0);
+  const int wg = blockIdx.x;
+  const bool helper = g.hand && wg >= g.B;  // uniform per workgroup
+  const int img = helper ? (wg - g.B) / CNN_HELPERS : wg;
+  if (!cnn_image<CC, EX, BF>(g, sm, img, helper ? (wg - g.B) % CNN_HELPERS : -1)) return;
+  RSTAMP(4);
   if (g.fused) cnn_fused_tail(g, img, sm);
 }
 
@@ -1010,6 +1161,7 @@ extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
   // the fused tail's group tickets are tick[0 .. ngrp) below the level-2 ticket tick[CNN_GRP]
   if (g.fused && (g.P % 4 || (g.B + CNN_GRP - 1) / CNN_GRP > CNN_GRP || !g.part || !g.tick || !g.slab || !g.row_loss || !g.train)) return -1;
   if (g.perm && (!g.fused || !g.cursor)) return -1;  // index mode: fused steps only
+  if (g.hand && (!g.fused || !g.hflag)) return -1;    // helpers: fused steps only
   if (g.fused && !g.lr) {  // gradient mode: every gradient destination, no shadows
     for (int i = 0; i < 5; ++i)
       if (!g.gw[i] || !g.gb[i]) return -1;
@@ -1028,9 +1180,12 @@ extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
   auto kern = g.bf16 ? (g.C == 10 ? cnn_kernel<10, true, true> : cnn_kernel<CNN_MAXC, false, true>)
                      : (g.C == 10 ? cnn_kernel<10, true, false> : cnn_kernel<CNN_MAXC, false, false>);
   hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(kern, dim3(g.B), dim3(CNN_THREADS), lds, st, g);
+  hipLaunchKernelGGL(kern, dim3(g.hand ? (1 + CNN_HELPERS) * g.B : g.B), dim3(CNN_THREADS), lds, st, g);
   SMI_CHECK_LAUNCH();
 }
+
+// floats of one image's hand-off area for the weight-gradient helpers (0: helpers not available)
+extern "C" int smi_cnn_hand_floats(int C) { return (C >= 1 && C <= CNN_MAXC) ? cnn_hand_f(C) : 0; }
 
 extern "C" int smi_cnn_fused_ok(int C, int cin, int classes, int B) {
   // the fused tail stages every image's dl and p2 in the kernel's LDS (see smi_cnn)

@@ -112,6 +112,17 @@ def cnn_logits(x, params, bf16=False):
         return reference_logits(x, [p.float() for p in params])
 
 
+# the conv4 / conv3 / conv2 weight gradients on helper workgroups beside the image's dgrad chain
+# (csrc/kernels/cnn.hip cnn_wgrad_helper; fused steps)
+WGRAD_HELPERS = True
+
+
+def _hand(B, C, device):
+    """The helpers' hand-off area ([B][cnn_hand_floats(C)] floats) or None (helpers off)."""
+    n = _native.C().cnn_hand_floats(C) if WGRAD_HELPERS else 0
+    return torch.empty(B * n, device=device, dtype=torch.float32) if n else None
+
+
 def cnn_sgd_step(x, y, params, lr_t, step_t, tick, shadows=None, bf16=False, index=None):
     """The whole training step — forward, mean CE, backward, gradient reduction over the batch
     and the SGD update — as ONE launch (csrc/kernels/cnn.hip, CNNArgs::fused): the per-image
@@ -136,7 +147,8 @@ def cnn_sgd_step(x, y, params, lr_t, step_t, tick, shadows=None, bf16=False, ind
                              [t.data_ptr() for t in shadows] if shadows else [], slab.data_ptr(), part.data_ptr(),
                              row_loss.data_ptr(), loss.data_ptr(), 1.0 / B, lr_t.data_ptr(), step_t.data_ptr(),
                              tick.data_ptr(), int(bf16), index[1].data_ptr() if index else 0,
-                             index[2].data_ptr() if index else 0, _native.stream())
+                             index[2].data_ptr() if index else 0, _native.ptr(_hand(B, w[0].shape[0], x.device)),
+                             _native.stream())
     return loss[0]
 
 
@@ -161,5 +173,5 @@ def cnn_grad_step(x, y, params, grads, tick, bf16=False, index=None):
                               [grads[i].data_ptr() for i in (1, 3, 5, 7, 9)], slab.data_ptr(), part.data_ptr(),
                               row_loss.data_ptr(), loss.data_ptr(), 1.0 / B, tick.data_ptr(), int(bf16),
                               index[1].data_ptr() if index else 0, index[2].data_ptr() if index else 0,
-                              _native.stream())
+                              _native.ptr(_hand(B, w[0].shape[0], x.device)), _native.stream())
     return loss[0]

@@ -44,25 +44,31 @@ int main(int argc, char** argv) {
   if (argc > 2) {  // the fused single-executor SGD step (ticketed slab reduction + SGD in the tail)
     float *part, *lr, *step; unsigned* tick;
     (void)hipMalloc(&part, (size_t)((B + CNN_GRP - 1) / CNN_GRP) * g.P * 4);
-    (void)hipMalloc(&tick, (CNN_GRP + 1) * 4); (void)hipMemset(tick, 0, (CNN_GRP + 1) * 4);
+    (void)hipMalloc(&tick, (CNN_GRP + 1 + 3 * B) * 4); (void)hipMemset(tick, 0, (CNN_GRP + 1 + 3 * B) * 4);
     (void)hipMalloc(&lr, 4); (void)hipMemset(lr, 0, 4);
     (void)hipMalloc(&step, 4); (void)hipMemset(step, 0, 4);
     g.fused = 1; g.part = part; g.tick = tick; g.lr = lr; g.step = step;
+    if (argc > 3) {  // the weight-gradient helper workgroups (CNNArgs::hand)
+      (void)hipMalloc(&g.hand, (size_t)B * smi_cnn_hand_floats(C) * 4);
+      g.hflag = tick + CNN_GRP + 1;
+    }
   }
-  printf("mode: %s%s\n", g.bf16 ? "bf16" : "fp32", g.fused ? " fused" : "");
+  printf("mode: %s%s%s\n", g.bf16 ? "bf16" : "fp32", g.fused ? " fused" : "", g.hand ? " helpers" : "");
   for (int it = 0; it < 20; ++it) smi_cnn(&g, 0);
   (void)hipDeviceSynchronize();
-  std::vector<unsigned long long> st(64 * 32);
+  std::vector<unsigned long long> st(256 * 32);
 #ifdef CNN_STAMPS
   (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(cnn_stamps), st.size() * 8);
 #endif
   int nph = 0;
   for (int i = 0; i < 21; ++i) if (st[i]) nph = i + 1;
   printf("phases %d\n", nph);
-  for (int p = 1; p < nph; ++p) {
+  for (int p = 1, q = 0; p < nph; ++p) {  // consecutive stamps that were set (paths skip some)
+    if (!st[p]) continue;
     double d = 0;
-    for (int im = 0; im < B; ++im) d += (double)(st[im * 32 + p] - st[im * 32 + p - 1]);
-    printf("phase %2d -> %2d: %8.0f ticks\n", p - 1, p, d / B);
+    for (int im = 0; im < B; ++im) d += (double)(st[im * 32 + p] - st[im * 32 + q]);
+    printf("phase %2d -> %2d: %8.0f ticks\n", q, p, d / B);
+    q = p;
   }
   // conv_wgrad sub-stamps (slot sb: wave 0's units done, sb+1: all units done; phase end = combine done)
   const int sub[3][3] = {{21, 17, 18}, {23, 19, 20}, {25, 12, 13}};
@@ -96,6 +102,30 @@ int main(int argc, char** argv) {
     for (int k = (g.bf16 ? 21 : 26); k < 31; ++k)
       if (st[im * 32 + k]) printf("img %2d slot %d: %+8lld ticks after its body end\n", im, k,
                                   (long long)(st[im * 32 + k] - st[im * 32 + 20]));
+  if (g.hand) {  // global-clock timeline (10 ns ticks) from the kernel's earliest start
+    std::vector<unsigned long long> rt(256 * 8);
+    (void)hipMemcpyFromSymbol(rt.data(), HIP_SYMBOL(cnn_rstamps), rt.size() * 8);
+    unsigned long long t0 = ~0ull;
+    for (int w = 0; w < 5 * B; ++w) if (rt[w * 8] && rt[w * 8] < t0) t0 = rt[w * 8];
+    auto avg = [&](int w0, int w1, int step, int k) {
+      double s = 0; int n = 0;
+      for (int w = w0; w < w1; w += step) if (rt[w * 8 + k]) { s += (double)(rt[w * 8 + k] - t0) * 10.0 / 1000.0; ++n; }
+      return n ? s / n : -1.0;
+    };
+    printf("image wg (us from kernel start): start %.2f, conv2 handed over %.2f, body done %.2f\n", avg(0, B, 1, 0),
+           avg(0, B, 1, 1), avg(0, B, 1, 4));
+    const char* hn[4] = {"conv4", "conv3", "conv2 a", "conv2 b"};
+    for (int j = 0; j < 4; ++j)
+      printf("helper %s: start %.2f, flag %.2f, loaded %.2f, wgrad %.2f, done %.2f\n", hn[j], avg(B + j, 5 * B, 4, 0),
+             avg(B + j, 5 * B, 4, 1), avg(B + j, 5 * B, 4, 2), avg(B + j, 5 * B, 4, 3), avg(B + j, 5 * B, 4, 4));
+    double l1 = 0, l2 = 0, l3 = 0; int n1 = 0;
+    for (int w = 0; w < 5 * B; ++w) {
+      if (rt[w * 8 + 5]) { l1 += (double)(rt[w * 8 + 5] - t0) * 0.01; ++n1; }
+      if (rt[w * 8 + 6]) l2 = (double)(rt[w * 8 + 6] - t0) * 0.01;
+      if (rt[w * 8 + 7]) l3 = (double)(rt[w * 8 + 7] - t0) * 0.01;
+    }
+    printf("tail: level-1 starts (avg of %d) %.2f, level 2 start %.2f, SGD done %.2f us\n", n1, n1 ? l1 / n1 : -1.0, l2, l3);
+  }
   double tot = 0;
   for (int im = 0; im < B; ++im) tot += (double)(st[im * 32 + nph - 1] - st[im * 32]);
   printf("total %8.0f ticks\n", tot / B);
