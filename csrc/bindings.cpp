@@ -577,8 +577,8 @@ PYBIND11_MODULE(_C, m) {
     a.P = o; a.slab = (float*)slab; a.part = (float*)part; a.row_loss = (float*)row_loss; a.loss = (float*)loss;
     a.loss_scale = loss_scale; a.train = 1; a.fused = 1;
     a.lr = (const float*)lr; a.step = (float*)step; a.tick = (unsigned*)tick;
-    // the helpers' flags follow the tail's CNN_GRP + 1 tickets in the model's tick block
-    a.hand = (float*)hand; a.hflag = hand ? a.tick + CNN_GRP + 1 : nullptr;
+    // the helpers' flags follow the tail's CNN_GRP + 2 counters in the model's tick block
+    a.hand = (float*)hand; a.hflag = hand ? a.tick + CNN_GRP + 2 : nullptr;
     a.perm = (const long long*)perm; a.cursor = (int*)cursor;
     chk(smi_cnn(&a, S(st)), "cnn_sgd_step");
   });
@@ -601,7 +601,7 @@ PYBIND11_MODULE(_C, m) {
     for (int i = 0; i < 10; ++i) { a.off[i] = o; o += sz[i]; }
     a.P = o; a.slab = (float*)slab; a.part = (float*)part; a.row_loss = (float*)row_loss; a.loss = (float*)loss;
     a.loss_scale = loss_scale; a.train = 1; a.fused = 1; a.lr = nullptr; a.tick = (unsigned*)tick;
-    a.hand = (float*)hand; a.hflag = hand ? a.tick + CNN_GRP + 1 : nullptr;
+    a.hand = (float*)hand; a.hflag = hand ? a.tick + CNN_GRP + 2 : nullptr;
     a.perm = (const long long*)perm; a.cursor = (int*)cursor;
     chk(smi_cnn(&a, S(st)), "cnn_grad_step");
   });

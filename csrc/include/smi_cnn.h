@@ -16,7 +16,7 @@ struct CNNArgs {
   // fused SGD step (cnn_kernel's tail, one launch per training step): the per-image slabs are
   // summed in two ticketed levels (groups of CNN_GRP images, then the groups) and the LAST
   // workgroup applies p -= lr * g to the parameters (+ their bf16 shadows), the mean loss and the
-  // step counter.  part: [ceil(B / CNN_GRP)][P] group sums; tick: CNN_GRP + 1 zeroed counters
+  // step counter.  part: [ceil(B / CNN_GRP)][P] group sums; tick: CNN_GRP + 2 zeroed counters
   // (re-armed by the kernel), owned by the model.
   int fused;
   int wstage;  // set by the launcher: the bf16 convs read LDS-staged weights (when they fit)
@@ -35,4 +35,4 @@ struct CNNArgs {
 #ifndef CNN_GRP
 #define CNN_GRP 8
 #endif
-static_assert(CNN_GRP >= 1 && CNN_GRP <= 32, "the model owns CNN_GRP + 1 <= 33 tickets");
+static_assert(CNN_GRP >= 1 && CNN_GRP <= 32, "the model owns CNN_GRP + 2 <= 34 tickets");

@@ -566,19 +566,33 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
   smi_wt_drain();
   __syncthreads();
   STAMP(27);
+  // level 2, split over the ngrp level-1 workgroups (slice = group): each waits until every
+  // group's partial is in (they are all running: a bounded wait among resident workgroups; a time-
+  // out poisons the slice with NaN), then updates its slice of the parameters.  One workgroup doing
+  // all of level 2 was bound by its CU's device-scope load rate (~8.6 us)
   if (threadIdx.x == 0) {
     g.tick[grp] = 0u;  // re-arm (every image of the group has taken its ticket)
-    last = atomicAdd(g.tick + CNN_GRP, 1u) == (unsigned)(ngrp - 1);
+    atomicAdd(g.tick + CNN_GRP, 1u);
+    int bad = 0;
+    for (int it = 0; __hip_atomic_load(g.tick + CNN_GRP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)ngrp;
+         ++it) {
+      if (it >= (1 << 22)) { bad = 1; break; }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    last = bad;
   }
   __syncthreads();
-  if (!last) return;
+  const bool poison = last != 0;
   RSTAMP(6);
   STAMP(28);
+  const int slice = grp;
   // level 2.  Stage every image's dl / p2 row (R4 floats) in LDS (the activation planes are free),
   // sum the conv group partials in group order and form the fc gradient from the staged rows
   const int R4 = (NC + F + 3) & ~3, ns4 = g.B * (R4 >> 2);
   const bool gmode = g.lr == nullptr;
-  const float lr = gmode ? -1.f : g.lr[0];
+  const float lr = poison ? __builtin_nanf("") : (gmode ? -1.f : g.lr[0]);
+  const int ilo = slice * F / ngrp, ihi = (slice + 1) * F / ngrp, Fs = ihi - ilo;  // fc columns
+  const int q4lo = slice * n4 / ngrp, q4hi = (slice + 1) * n4 / ngrp;                // conv granules
   // the tensor level 2 updates for slab segment seg: the parameter, or (gradient mode) its gradient
   auto dst_of = [&](int seg) -> float* {
     return gmode ? (seg % 2 == 0 ? g.gw[seg / 2] : g.gb[seg / 2]) : const_cast<float*>(seg % 2 == 0 ? g.w[seg / 2] : g.b[seg / 2]);
@@ -588,10 +602,10 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
     for (int i = threadIdx.x; i < g.B; i += 64) rl += smi_cc_load(g.row_loss + i);
   // fc: thread t owns column i of the fc weight for the classes of its half h (two halves of 8
   // classes, o4 granules ob, ob+1, when NC > 8 and two columns per thread fit: all 16 waves busy)
-  const int H = (NC > 8 && 2 * F <= nt) ? 2 : 1, no4 = (H == 2 || NC <= 8) ? 2 : 4;
-  const int h = H == 2 ? (int)threadIdx.x / F : 0, ob = H == 2 ? 2 * h : 0;
-  const int i0 = (int)threadIdx.x - h * F;
-  const bool fc_on = h < H && i0 < F;
+  const int H = (NC > 8 && 2 * Fs <= nt) ? 2 : 1, no4 = (H == 2 || NC <= 8) ? 2 : 4;
+  const int h = H == 2 ? (int)threadIdx.x / Fs : 0, ob = H == 2 ? 2 * h : 0;
+  const int i0 = ilo + (int)threadIdx.x - h * Fs;
+  const bool fc_on = h < H && i0 < ihi;
   float* fw = dst_of(8);
   auto fc_load = [&](int i, float* pv) {  // column i's parameters (clamped addresses: no branch)
 #pragma unroll
@@ -642,37 +656,50 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
       if (g.shadow[seg]) g.shadow[seg][r] = f2bf(np[u]);
     }
   };
+  // granules of an image's row this slice stages: dl (the first ndl4) and its p2 columns
+  const int ndl4 = (NC + 3) >> 2, p4lo = (NC + ilo) >> 2, np4 = ((NC + ihi + 3) >> 2) - p4lo, ng = ndl4 + np4;
+  const int nst = g.B * ng;
+  auto stage_j4 = [&](int e, int& im) {
+    im = e / ng;
+    const int jj = e - im * ng;
+    return jj < ndl4 ? jj : p4lo + (jj - ndl4);
+  };
   auto stage_load = [&](int e4, float4* v) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int e = e4 + u * nt, im = e / (R4 >> 2), j4 = e - im * (R4 >> 2);
+      int im;
+      const int j4 = stage_j4(e4 + u * nt, im);
       v[u] = smi_cc_load4(rslab, (im * P + cs + 4 * j4) * 4);  // im >= B: 0
     }
   };
   auto stage_store = [&](int e4, const float4* v) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (e4 + u * nt < ns4) reinterpret_cast<float4*>(sm)[e4 + u * nt] = v[u];
+    for (int u = 0; u < 4; ++u) {
+      int im;
+      const int j4 = stage_j4(e4 + u * nt, im);
+      if (e4 + u * nt < nst) reinterpret_cast<float4*>(sm + im * R4)[j4] = v[u];
+    }
   };
-  if (n4 <= nt && ns4 <= 4 * nt) {
+  if (q4hi - q4lo <= nt && nst <= 4 * nt) {
     // one round trip: every staging and partial-sum load of the thread issued before the first use
     float4 v[4];
     Conv4 k;
+    const int q4 = q4lo + (int)threadIdx.x;
     stage_load(threadIdx.x, v);
-    conv_load(threadIdx.x, k);
+    conv_load(min(q4, q4hi - 1), k);
     stage_store(threadIdx.x, v);
 #pragma unroll
     for (int t = 0; t < 16; ++t) CNN_PIN(pfc[t]);
     STAMP(21);
-    conv_apply(threadIdx.x, k);
+    if (q4 < q4hi) conv_apply(q4, k);
     STAMP(22);
   } else {
-    for (int e4 = threadIdx.x; e4 < ns4; e4 += 4 * nt) {
+    for (int e4 = threadIdx.x; e4 < nst; e4 += 4 * nt) {
       float4 v[4];
       stage_load(e4, v);
       stage_store(e4, v);
     }
-    for (int q4 = threadIdx.x; q4 < n4; q4 += nt) {
+    for (int q4 = q4lo + (int)threadIdx.x; q4 < q4hi; q4 += nt) {
       Conv4 k;
       conv_load(q4, k);
       conv_apply(q4, k);
@@ -740,17 +767,17 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
     if (no4 == 2) fc_column_n(std::integral_constant<int, 2>{}, i, pv);
     else fc_column_n(std::integral_constant<int, 4>{}, i, pv);
   };
-  if (H * F <= nt) {  // one column per thread: no loop (a loop's loads make every store wait)
+  if (H * Fs <= nt) {  // one column per thread: no loop (a loop's loads make every store wait)
     if (fc_on) fc_column(i0, pfc);
   } else {
-    for (int i = i0; i < F; i += nt) {
+    for (int i = i0; i < ihi; i += nt) {
       float pv[16];
       fc_load(i, pv);
       fc_column(i, pv);
     }
   }
   STAMP(23);
-  if ((int)threadIdx.x < NC) {
+  if (slice == 0 && (int)threadIdx.x < NC) {
     const int o = threadIdx.x;
     float gb = 0.f;
 #pragma unroll 8
@@ -761,6 +788,11 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
   }
   STAMP(29);
   RSTAMP(7);
+  // the last slice to finish: the mean loss (image order), the step counter, the cursor, re-arms
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(g.tick + CNN_GRP + 1, 1u) == (unsigned)(ngrp - 1);
+  __syncthreads();
+  if (!last) return;
   if (threadIdx.x < 64) {
     const float ls = wave_sum(rl);
     if (threadIdx.x == 0) {
@@ -768,6 +800,7 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
       if (g.step && !gmode) g.step[0] += 1.f;
       if (g.cursor) g.cursor[0] += 1;  // index mode: every workgroup read it before its ticket
       g.tick[CNN_GRP] = 0u;
+      g.tick[CNN_GRP + 1] = 0u;
     }
   }
   // the weight-gradient helpers' hand-off flags, re-armed for the next launch (every helper read
@@ -984,7 +1017,9 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
     }
   }
   if (!g.train) return false;
-  __syncthreads();
+  // LDS-only barriers from here to the dgrad chain: the row loss / slab stores stay in flight (a
+  // plain __syncthreads waits for them: ~1.5k clocks each); the tail drains before its ticket
+  smi_lds_barrier();
   STAMP(9);
   float* gs = g.slab + (long)img * g.P;  // this image's gradient slab
   // fc grads: the slab keeps this image's dl (NC) and p2 (F) in place of the NC x F outer product
@@ -992,7 +1027,7 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
   // third of the bytes to reduce); dp2[i] = sum_o W[o][i] dl[o] goes into the p2 buffer after
   for (int i = threadIdx.x; i < F; i += blockDim.x) smi_wt_store(gs + cnn_cs(g) + NC + i, p2[i]);
   for (int o = threadIdx.x; o < NC; o += blockDim.x) smi_wt_store(gs + cnn_cs(g) + o, lg[o]);
-  __syncthreads();
+  smi_lds_barrier();
   STAMP(10);
   for (int i = threadIdx.x; i < F; i += blockDim.x) {
     float s = 0.f;

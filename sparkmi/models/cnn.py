@@ -28,9 +28,9 @@ class FashionMNISTModel(nn.Module):
         self.classifier = nn.Sequential(nn.Flatten(), nn.Linear(hidden_units * 7 * 7, output_shape))
         # fused-step tickets (CNN_GRP + 1 <= 33 counters, re-armed by the kernel): per model, so
         # two models never share them; not part of the state_dict (reference key parity)
-        # the fused step's tickets: CNN_GRP + 1 for the tail, then 3 per image (<= CNN_GRP^2 = 64)
+        # the fused step's counters: CNN_GRP + 2 for the tail, then 3 per image (<= CNN_GRP^2 = 64)
         # for the weight-gradient helpers' hand-off flags
-        self.register_buffer("_step_tick", torch.zeros(33 + 3 * 64, dtype=torch.int32), persistent=False)
+        self.register_buffer("_step_tick", torch.zeros(34 + 3 * 64, dtype=torch.int32), persistent=False)
 
     def param_list(self):
         c = [self.block_1[0], self.block_1[2], self.block_2[0], self.block_2[2], self.classifier[1]]

@@ -129,7 +129,7 @@ def cnn_sgd_step(x, y, params, lr_t, step_t, tick, shadows=None, bf16=False, ind
     slabs are summed in the kernel's ticketed tail, which then updates ``params`` in place
     (p -= lr * g; ``lr_t`` / ``step_t`` are the optimizer's device scalars) and their bf16
     ``shadows`` (10 tensors or None).  Returns the step's mean loss (device scalar).  ``tick``:
-    CNN_GRP + 1 zeroed int32 counters owned by the model (the kernel re-arms them).
+    CNN_GRP + 2 + 3 B zeroed int32 counters owned by the model (the kernel re-arms them).
     ``index`` = (batch, perm, cursor): ``x`` / ``y`` are the whole dataset and the kernel reads image
     i of the batch from row perm[cursor * batch + i], then advances the device cursor (the shuffled
     batch gather inside the step kernel; DeviceLoader fixed=True, index mode)."""

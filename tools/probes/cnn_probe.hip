@@ -44,13 +44,13 @@ int main(int argc, char** argv) {
   if (argc > 2) {  // the fused single-executor SGD step (ticketed slab reduction + SGD in the tail)
     float *part, *lr, *step; unsigned* tick;
     (void)hipMalloc(&part, (size_t)((B + CNN_GRP - 1) / CNN_GRP) * g.P * 4);
-    (void)hipMalloc(&tick, (CNN_GRP + 1 + 3 * B) * 4); (void)hipMemset(tick, 0, (CNN_GRP + 1 + 3 * B) * 4);
+    (void)hipMalloc(&tick, (CNN_GRP + 2 + 3 * B) * 4); (void)hipMemset(tick, 0, (CNN_GRP + 2 + 3 * B) * 4);
     (void)hipMalloc(&lr, 4); (void)hipMemset(lr, 0, 4);
     (void)hipMalloc(&step, 4); (void)hipMemset(step, 0, 4);
     g.fused = 1; g.part = part; g.tick = tick; g.lr = lr; g.step = step;
     if (argc > 3) {  // the weight-gradient helper workgroups (CNNArgs::hand)
       (void)hipMalloc(&g.hand, (size_t)B * smi_cnn_hand_floats(C) * 4);
-      g.hflag = tick + CNN_GRP + 1;
+      g.hflag = tick + CNN_GRP + 2;
     }
   }
   printf("mode: %s%s%s\n", g.bf16 ? "bf16" : "fp32", g.fused ? " fused" : "", g.hand ? " helpers" : "");
@@ -118,13 +118,15 @@ int main(int argc, char** argv) {
     for (int j = 0; j < 4; ++j)
       printf("helper %s: start %.2f, flag %.2f, loaded %.2f, wgrad %.2f, done %.2f\n", hn[j], avg(B + j, 5 * B, 4, 0),
              avg(B + j, 5 * B, 4, 1), avg(B + j, 5 * B, 4, 2), avg(B + j, 5 * B, 4, 3), avg(B + j, 5 * B, 4, 4));
-    double l1 = 0, l2 = 0, l3 = 0; int n1 = 0;
-    for (int w = 0; w < 5 * B; ++w) {
-      if (rt[w * 8 + 5]) { l1 += (double)(rt[w * 8 + 5] - t0) * 0.01; ++n1; }
-      if (rt[w * 8 + 6]) l2 = (double)(rt[w * 8 + 6] - t0) * 0.01;
-      if (rt[w * 8 + 7]) l3 = (double)(rt[w * 8 + 7] - t0) * 0.01;
+    // tail stamps of THIS launch only (earlier launches' last workgroups left older values)
+    auto cur = [&](unsigned long long v) { return v >= t0 && v < t0 + 100000ull; };
+    for (int k = 5; k < 8; ++k) {
+      const char* kn = k == 5 ? "level 1 start" : (k == 6 ? "level 2 slice start" : "level 2 slice done");
+      printf("tail %s:", kn);
+      for (int w = 0; w < 5 * B; ++w)
+        if (cur(rt[w * 8 + k])) printf(" %.2f", (double)(rt[w * 8 + k] - t0) * 0.01);
+      printf(" us\n");
     }
-    printf("tail: level-1 starts (avg of %d) %.2f, level 2 start %.2f, SGD done %.2f us\n", n1, n1 ? l1 / n1 : -1.0, l2, l3);
   }
   double tot = 0;
   for (int im = 0; im < B; ++im) tot += (double)(st[im * 32 + nph - 1] - st[im * 32]);
