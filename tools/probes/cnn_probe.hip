@@ -127,6 +127,14 @@ int main(int argc, char** argv) {
         if (cur(rt[w * 8 + k])) printf(" %.2f", (double)(rt[w * 8 + k] - t0) * 0.01);
       printf(" us\n");
     }
+    // the level-2 slices' phases (same-workgroup s_memtime differences)
+    for (int w = 0; w < 5 * B; ++w) {
+      if (!cur(rt[w * 8 + 6])) continue;
+      const unsigned long long* q = &st[w * 32];
+      printf("slice wg %3d: loads %lld, conv apply %lld, barrier %lld, fc %lld, bias %lld ticks\n", w,
+             (long long)(q[21] - q[28]), (long long)(q[22] - q[21]), (long long)(q[30] - q[22]),
+             (long long)(q[23] - q[30]), (long long)(q[29] - q[23]));
+    }
   }
   double tot = 0;
   for (int im = 0; im < B; ++im) tot += (double)(st[im * 32 + nph - 1] - st[im * 32]);
