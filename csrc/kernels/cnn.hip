@@ -588,7 +588,7 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
   const int slice = grp;
   // level 2.  Stage every image's dl / p2 row (R4 floats) in LDS (the activation planes are free),
   // sum the conv group partials in group order and form the fc gradient from the staged rows
-  const int R4 = (NC + F + 3) & ~3, ns4 = g.B * (R4 >> 2);
+  const int R4 = (NC + F + 3) & ~3;
   const bool gmode = g.lr == nullptr;
   const float lr = poison ? __builtin_nanf("") : (gmode ? -1.f : g.lr[0]);
   const int ilo = slice * F / ngrp, ihi = (slice + 1) * F / ngrp, Fs = ihi - ilo;  // fc columns

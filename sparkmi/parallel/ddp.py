@@ -215,7 +215,19 @@ class DataParallel:
         rccl_ms = timed(lambda: dist.all_reduce(x, group=self.group))
         mc_ms = timed(lambda: dist.all_reduce(x, group=mc)) if mc is not None else None
         if self.ipc is not None:
-            self.ipc.check()
+            # a peer the IPC kernels could not reach (timed-out signal rounds: sticky error) takes
+            # the IPC path out of the running on EVERY rank (the error flag is agreed), instead of
+            # one rank raising while the others go on
+            from .comm import IpcPeerLost
+            try:
+                self.ipc.check()
+                bad = 0.0
+            except IpcPeerLost:
+                bad = 1.0
+            f = torch.tensor([bad], dtype=torch.float32, device=fdev)
+            dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
+            if float(f.item()) > 0:
+                ipc_ms = None
         return ipc_ms, rccl_ms, mc_ms
 
     def _ipc_capacity(self):

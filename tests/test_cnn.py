@@ -146,12 +146,13 @@ def test_fused_cnn_gradients_bit_reproducible(dtype):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dtype,B", [("fp32", 32), ("bf16", 32), ("fp32", 20)])
+@pytest.mark.parametrize("dtype,B", [("fp32", 32), ("bf16", 32), ("fp32", 20), ("bf16", 56)])
 def test_fused_sgd_step_matches_unfused(dtype, B):
     """The one-launch CNN step (fused slab reduction + SGD in the kernel's ticketed tail) follows
     the three-launch path (kernel -> batch gradient reduce -> SGD kernel) step for step, keeps the
     bf16 shadow in sync, is bit-reproducible, and replays identically inside a HIP graph
-    (StepRunner's single-executor fused_step path).  B = 20: a ragged last group of images."""
+    (StepRunner's single-executor fused_step path).  B = 20: a ragged last group of images; B = 56:
+    with its weight-gradient helpers, 280 workgroups: more than the CUs."""
     from sparkmi.optim import SGD
     from sparkmi.train.runner import StepRunner
     from sparkmi.utils.flat import FlatParams
@@ -192,4 +193,4 @@ def test_fused_sgd_step_matches_unfused(dtype, B):
     assert tf == tu == 6.0                              # step counter advanced per step
     for a, b in zip(lf, lu):
         assert abs(a - b) <= 1e-5 * abs(b) + 1e-6, (lf, lu)
-    torch.testing.assert_close(pf, pu, rtol=1e-5, atol=2e-6)
+    torch.testing.assert_close(pf, pu, rtol=1e-5, atol=5e-6)  # fp32 sums in another order
