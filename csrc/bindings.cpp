@@ -561,7 +561,7 @@ PYBIND11_MODULE(_C, m) {
   // the whole single-executor CNN training step in ONE launch: forward + backward per image and
   // the fused slab reduction + SGD update in the kernel's tail (CNNArgs::fused)
   m.def("cnn_sgd_step", [](u x, int x_u8, float x_scale, u y, int B, int cin, int C, int classes, std::vector<u> w,
-                           std::vector<u> b, std::vector<u> shadow, u slab, u part, u row_loss, u loss,
+                           std::vector<u> b, std::vector<u> shadow, u slab, u row_loss, u loss,
                            float loss_scale, u lr, u step, u tick, int bf16, u perm, u cursor, u hand, u st) {
     CNNArgs a{};
     a.bf16 = bf16;
@@ -574,18 +574,18 @@ PYBIND11_MODULE(_C, m) {
     const int sz[10] = {C * cin * 9, C, C * C * 9, C, C * C * 9, C, C * C * 9, C, classes * C * 49, classes};
     int o = 0;
     for (int i = 0; i < 10; ++i) { a.off[i] = o; o += sz[i]; }
-    a.P = o; a.slab = (float*)slab; a.part = (float*)part; a.row_loss = (float*)row_loss; a.loss = (float*)loss;
+    a.P = o; a.slab = (float*)slab; a.row_loss = (float*)row_loss; a.loss = (float*)loss;
     a.loss_scale = loss_scale; a.train = 1; a.fused = 1;
     a.lr = (const float*)lr; a.step = (float*)step; a.tick = (unsigned*)tick;
-    // the helpers' flags follow the tail's CNN_GRP + 2 counters in the model's tick block
-    a.hand = (float*)hand; a.hflag = hand ? a.tick + CNN_GRP + 2 : nullptr;
+    // the helpers' flags follow the tail's counters in the model's tick block
+    a.hand = (float*)hand; a.hflag = hand ? a.tick + CNN_TICKS : nullptr;
     a.perm = (const long long*)perm; a.cursor = (int*)cursor;
     chk(smi_cnn(&a, S(st)), "cnn_sgd_step");
   });
   // the same launch in GRADIENT mode (the data-parallel step): the tail adds the batch gradient
   // to gw / gb (the flat gradient buffer) instead of updating the parameters
   m.def("cnn_grad_step", [](u x, int x_u8, float x_scale, u y, int B, int cin, int C, int classes, std::vector<u> w,
-                            std::vector<u> b, std::vector<u> gw, std::vector<u> gb, u slab, u part, u row_loss, u loss,
+                            std::vector<u> b, std::vector<u> gw, std::vector<u> gb, u slab, u row_loss, u loss,
                             float loss_scale, u tick, int bf16, u perm, u cursor, u hand, u st) {
     CNNArgs a{};
     a.bf16 = bf16;
@@ -599,9 +599,9 @@ PYBIND11_MODULE(_C, m) {
     const int sz[10] = {C * cin * 9, C, C * C * 9, C, C * C * 9, C, C * C * 9, C, classes * C * 49, classes};
     int o = 0;
     for (int i = 0; i < 10; ++i) { a.off[i] = o; o += sz[i]; }
-    a.P = o; a.slab = (float*)slab; a.part = (float*)part; a.row_loss = (float*)row_loss; a.loss = (float*)loss;
+    a.P = o; a.slab = (float*)slab; a.row_loss = (float*)row_loss; a.loss = (float*)loss;
     a.loss_scale = loss_scale; a.train = 1; a.fused = 1; a.lr = nullptr; a.tick = (unsigned*)tick;
-    a.hand = (float*)hand; a.hflag = hand ? a.tick + CNN_GRP + 2 : nullptr;
+    a.hand = (float*)hand; a.hflag = hand ? a.tick + CNN_TICKS : nullptr;
     a.perm = (const long long*)perm; a.cursor = (int*)cursor;
     chk(smi_cnn(&a, S(st)), "cnn_grad_step");
   });
@@ -622,7 +622,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("emb_pair", [](int set) { return smi_emb_pair(set); },
         "deterministic embedding backward: 1 = pair-compare (<= 8192 tokens), 0 = bucketed lists; -1 queries");
   m.def("cnn_fused_ok", [](int C, int cin, int classes, int B) { return smi_cnn_fused_ok(C, cin, classes, B) != 0; });
-  m.def("cnn_grp", []() { return (int)CNN_GRP; });  // images per fused-tail group (part rows, tickets)
   m.def("cnn_hand_floats", [](int C) { return smi_cnn_hand_floats(C); });  // 0: weight-gradient helpers off
 
   m.def("lstm_supported", [](int E, int H, int L, int C) { return smi_lstm_supported(E, H, L, C) != 0; });

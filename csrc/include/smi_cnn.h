@@ -13,14 +13,14 @@ struct CNNArgs {
   const float* dloss;                        // upstream grad of the loss (reduce kernel)
   int train;
   int bf16;                                  // convolutions on bf16 matrix cores (fp32 accumulate)
-  // fused SGD step (cnn_kernel's tail, one launch per training step): the per-image slabs are
-  // summed in two ticketed levels (groups of CNN_GRP images, then the groups) and the LAST
-  // workgroup applies p -= lr * g to the parameters (+ their bf16 shadows), the mean loss and the
-  // step counter.  part: [ceil(B / CNN_GRP)][P] group sums; tick: CNN_GRP + 2 zeroed counters
-  // (re-armed by the kernel), owned by the model.
+  // fused SGD step (cnn_kernel's tail, one launch per training step): the last min(CNN_NSL, B)
+  // workgroups to finish (one ticket counter) become slice workgroups; the slices sum the
+  // per-image slabs of their part of the parameters and apply p -= lr * g (+ the bf16 shadows);
+  // the last one writes the mean loss and the step counter.  tick: CNN_TICKS zeroed counters
+  // (re-armed by the kernel), owned by the model, followed by the helpers' flags (hflag).
   int fused;
   int wstage;  // set by the launcher: the bf16 convs read LDS-staged weights (when they fit)
-  float* part; unsigned* tick; const float* lr; float* step;
+  unsigned* tick; const float* lr; float* step;
   unsigned short* shadow[10];                // per-parameter bf16 shadows (slab order) or null
   // INDEX mode (fused steps only; sparkmi/data/dataset.py DeviceLoader fixed=True): x / y are the
   // whole HBM-resident dataset and image i of the batch is row perm[cursor[0] * B + i]; the step's
@@ -32,7 +32,9 @@ struct CNNArgs {
   // helpers) — the image's workgroup runs the dgrad chain meanwhile
   float* hand; unsigned* hflag;
 };
-#ifndef CNN_GRP
-#define CNN_GRP 8
+#ifndef CNN_NSL
+#define CNN_NSL 16  // fused tail: at most this many parameter slices (slice workgroups)
 #endif
-static_assert(CNN_GRP >= 1 && CNN_GRP <= 32, "the model owns CNN_GRP + 2 <= 34 tickets");
+#define CNN_TICKS 2    // the tail's ticket and departure counters
+#define CNN_MAXB 64    // fused steps: batch limit (the model's counter block: CNN_TICKS + 3 B <= 226)
+static_assert(CNN_NSL >= 1 && CNN_TICKS + 3 * CNN_MAXB <= 226, "sparkmi/models/cnn.py owns 226 counters");

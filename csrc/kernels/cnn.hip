@@ -521,142 +521,117 @@ __device__ __forceinline__ int cnn_cs(const CNNArgs& g) { return (g.off[8] + 3) 
 // conservative count-to-zero wait also drains every store before (one round trip per store).
 #define CNN_PIN(x) asm volatile("" : "+v"(x))
 
-// Fused SGD tail (CNNArgs::fused): the step's remaining work without a second launch.  Level 1:
-// the last image of each group of CNN_GRP to finish (ticket) sums the group's conv slab parts in
-// image order into part[group]; level 2: the last group to finish stages every image's dl / p2 in
-// LDS, sums the group partials in group order, forms the fc gradient as the image-order batch sum
-// of dl[o] * p2[i], and applies torch SGD (p -= lr * g) to every parameter, then the mean loss
-// (image order) and the step counter.  Hand-offs are write-through stores + device-scope loads in
-// 16-B granules (smi_common.h), no L2 fences.  Deterministic: every sum has a fixed order.  No
-// spinning: a workgroup that is not the last simply exits.
-// GRADIENT mode (lr == null; the data-parallel step): the same two levels, but level 2 ADDS the
-// batch gradient to gw / gb (the flat fp32 gradient buffer, reduced across executors next and
-// consumed by the optimizer) instead of updating the parameters: g += batch sum, written as
-// g - (-1) * sum so both modes share one code path (exact), no step bump, no shadows.
-__device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float* sm) {
+// Fused SGD tail (CNNArgs::fused): the step's remaining work without a second launch.  Every
+// workgroup of the launch (images and their helpers) counts itself done on one counter; the
+// workgroups of images 0 .. nsl - 1 (nsl = min(CNN_NSL, B)) are the SLICE workgroups: a slice loads
+// its parameters, waits until the counter says every workgroup is done (a bounded wait: the
+// slices are the first workgroups of the grid, so every workgroup they wait for is running or
+// gets a CU; a time-out poisons the slice with NaN), then slice s owns the s-th part of the
+// parameters: it sums every image's slab entries of its conv granules (image chunks over the
+// threads, chunk partials in LDS, fixed order), stages every image's dl and its p2 columns in LDS,
+// forms its fc columns' gradient as the batch sum of dl[o] * p2[i] (image chunks over lanes, a
+// fixed-order butterfly), and applies torch SGD (p -= lr * g); the last slice to finish writes the
+// mean loss (image order), the step counter and the index-mode cursor.  Hand-offs are write-
+// through stores + device-scope loads in 16-B granules (smi_common.h), no L2 fences.
+// Deterministic: every sum has a fixed order.  One level, fixed slices: the earlier two-level
+// form (per-group tickets, group partial sums handed over, then 4 slices) paid two more round
+// trips, and slices picked by ticket order loaded their parameters only after their ticket
+// (docs/PERF_NOTES.md).
+// GRADIENT mode (lr == null; the data-parallel step): the same, but the slices ADD the batch
+// gradient to gw / gb (the flat fp32 gradient buffer, reduced across executors next and consumed
+// by the optimizer) instead of updating the parameters: g += batch sum, written as g - (-1) * sum so
+// both modes share one code path (exact), no step bump, no shadows.
+__device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, float* sm, int slice) {
   __shared__ int last;
-  const int ngrp = (g.B + CNN_GRP - 1) / CNN_GRP;
-  const int grp = img / CNN_GRP, g0 = grp * CNN_GRP, g1 = min(g.B, g0 + CNN_GRP);
+  const int nsl = min(CNN_NSL, g.B);
+  const unsigned total = (g.hand ? 1u + CNN_HELPERS : 1u) * (unsigned)g.B;  // workgroups of the launch
   const int off8 = g.off[8], NC = g.classes, F = g.C * 49, nt = blockDim.x, P = g.P;
   const int cs = cnn_cs(g), n4 = cs >> 2;  // conv part in 16-B granules
   const __amdgpu_buffer_rsrc_t rslab = smi_rsrc(g.slab, g.B * P * 4);
-  const __amdgpu_buffer_rsrc_t rpart = smi_rsrc(g.part, ngrp * P * 4);
   smi_wt_drain();  // this wave's slab stores reached the coherence point
   __syncthreads();
-  const unsigned parts = g.hand ? 1u + CNN_HELPERS : 1u;  // the image's workgroup + its helpers
-  if (threadIdx.x == 0) last = atomicAdd(g.tick + grp, 1u) == parts * (unsigned)(g1 - g0) - 1u;
-  __syncthreads();
-  if (!last) return;
+  if (threadIdx.x == 0) atomicAdd(g.tick, 1u);  // done
+  if (slice < 0 || slice >= nsl) return;
   RSTAMP(5);
   STAMP(26);
-  // Loads below are unconditional (a lane's or image's out-of-range granule reads 0 through the
-  // buffer resource's range check, or a clamped valid address): a load under a branch makes the
-  // compiler wait for EVERY outstanding memory operation, stores included, before its first use,
-  // which serialised one store round trip per parameter (measured: 6 us in the fc update).
-  // level 1: the group's conv gradients, the group's slabs of a granule all in flight together
-  for (int q4 = threadIdx.x; q4 < n4; q4 += nt) {
-    float4 v[CNN_GRP];
-#pragma unroll
-    for (int i = 0; i < CNN_GRP; ++i) v[i] = smi_cc_load4(rslab, ((g0 + i) * P + 4 * q4) * 4);  // >= B: 0
-    float4 acc = v[0];
-#pragma unroll
-    for (int i = 1; i < CNN_GRP; ++i) acc = make_float4(acc.x + v[i].x, acc.y + v[i].y, acc.z + v[i].z, acc.w + v[i].w);
-    smi_wt_store4(rpart, (grp * P + 4 * q4) * 4, acc);
+  const bool gmode = g.lr == nullptr;
+  const int ilo = slice * F / nsl, ihi = (slice + 1) * F / nsl, Fs = ihi - ilo;         // fc columns
+  const int q4lo = slice * n4 / nsl, q4hi = (slice + 1) * n4 / nsl, nq = q4hi - q4lo;  // conv granules
+  // the tensor the slice updates for slab segment seg: the parameter, or (gradient mode) its gradient
+  auto dst_of = [&](int seg) -> float* {
+    return gmode ? (seg % 2 == 0 ? g.gw[seg / 2] : g.gb[seg / 2]) : const_cast<float*>(seg % 2 == 0 ? g.w[seg / 2] : g.b[seg / 2]);
+  };
+  // parameter p's segment (compares against the uniform offsets), offset in it and destination (a
+  // table in LDS: a lane-varying index into the argument block reads it from memory, one dependent
+  // load per step, and selects over the 8 pointers spill)
+  __shared__ float* seg_dst[8];
+  __shared__ unsigned short* seg_sh[8];
+  if (threadIdx.x < 8) {
+    seg_dst[threadIdx.x] = dst_of(threadIdx.x);
+    seg_sh[threadIdx.x] = g.shadow[threadIdx.x];
   }
-  smi_wt_drain();
   __syncthreads();
-  STAMP(27);
-  // level 2, split over the ngrp level-1 workgroups (slice = group): each waits until every
-  // group's partial is in (they are all running: a bounded wait among resident workgroups; a time-
-  // out poisons the slice with NaN), then updates its slice of the parameters.  One workgroup doing
-  // all of level 2 was bound by its CU's device-scope load rate (~8.6 us)
+  auto conv_seg = [&](int p, int& seg, int& r) {
+    seg = 0;
+    int base = g.off[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k)
+      if (p >= g.off[k]) { seg = k; base = g.off[k]; }
+    r = p - base;
+    return seg_dst[seg] + r;
+  };
+  auto shadow_of = [&](int seg) { return seg_sh[seg]; };
+  // The slice's own parameters first: nothing else writes them in this launch, so their loads fly
+  // during the wait.  Loads are unconditional (clamped addresses; a range-checked buffer load past
+  // the end reads 0): a load under a branch makes the compiler wait for EVERY outstanding memory
+  // operation, stores included, before its first use (measured: one store round trip per
+  // parameter, 6 us in the fc update).
+  // fc: slot = (column i, class half h: two halves of 8 classes, o4 granules ob, ob+1, when NC > 8
+  // and two columns per thread fit), KCH consecutive lanes per slot, lane kc taking images kc,
+  // kc + KCH, ...
+  const int H = (NC > 8 && 2 * Fs <= nt) ? 2 : 1, no4 = (H == 2 || NC <= 8) ? 2 : 4, nslot = H * Fs;
+  int KCH = 1;
+  while (KCH < 8 && 2 * KCH * nslot <= nt) KCH *= 2;
+  const int slot = (int)threadIdx.x / KCH, kc = (int)threadIdx.x - slot * KCH;
+  const int h = H == 2 ? slot / Fs : 0, ob = H == 2 ? 2 * h : 0;
+  const int i0 = ilo + slot - h * Fs;
+  const bool fc_on = h < H && i0 < ihi;
+  float* fw = dst_of(8);
+  auto fc_load = [&](int i, float* pv) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) pv[t] = fw[min(4 * ob + t, NC - 1) * F + min(max(i, 0), F - 1)];
+  };
+  float pfc[16];  // the thread's first column
+  fc_load(i0, pfc);
+  float* fb = dst_of(9);
+  const float pb = fb[min((int)threadIdx.x, NC - 1)];
+  auto conv_pload = [&](int q4, float* pv) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      int seg, r;
+      pv[u] = *conv_seg(min(max(4 * q4 + u, 0), off8 - 1), seg, r);
+    }
+  };
+  float pcv[4];  // granule q4lo + threadIdx.x (the one-granule-per-thread case)
+  conv_pload(min(q4lo + (int)threadIdx.x, q4hi - 1), pcv);
+  const float lr0 = gmode ? -1.f : g.lr[0];  // (a load after the wait: one more round trip)
+  // wait until every workgroup is done
   if (threadIdx.x == 0) {
-    g.tick[grp] = 0u;  // re-arm (every image of the group has taken its ticket)
-    atomicAdd(g.tick + CNN_GRP, 1u);
     int bad = 0;
-    for (int it = 0; __hip_atomic_load(g.tick + CNN_GRP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)ngrp;
-         ++it) {
+    for (int it = 0; __hip_atomic_load(g.tick, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < total; ++it) {
       if (it >= (1 << 22)) { bad = 1; break; }
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(1);
     }
     last = bad;
   }
   __syncthreads();
   const bool poison = last != 0;
+  const float lr = poison ? __builtin_nanf("") : lr0;
   RSTAMP(6);
   STAMP(28);
-  const int slice = grp;
-  // level 2.  Stage every image's dl / p2 row (R4 floats) in LDS (the activation planes are free),
-  // sum the conv group partials in group order and form the fc gradient from the staged rows
+  // one round trip: the staging loads (every image's dl and this slice's p2 granules into R4-float
+  // rows in the free activation planes), the row losses and the conv slab chunks all in flight
   const int R4 = (NC + F + 3) & ~3;
-  const bool gmode = g.lr == nullptr;
-  const float lr = poison ? __builtin_nanf("") : (gmode ? -1.f : g.lr[0]);
-  const int ilo = slice * F / ngrp, ihi = (slice + 1) * F / ngrp, Fs = ihi - ilo;  // fc columns
-  const int q4lo = slice * n4 / ngrp, q4hi = (slice + 1) * n4 / ngrp;                // conv granules
-  // the tensor level 2 updates for slab segment seg: the parameter, or (gradient mode) its gradient
-  auto dst_of = [&](int seg) -> float* {
-    return gmode ? (seg % 2 == 0 ? g.gw[seg / 2] : g.gb[seg / 2]) : const_cast<float*>(seg % 2 == 0 ? g.w[seg / 2] : g.b[seg / 2]);
-  };
-  float rl = 0.f;  // lane i: row losses i, i + 64, ...
-  if (threadIdx.x < 64)
-    for (int i = threadIdx.x; i < g.B; i += 64) rl += smi_cc_load(g.row_loss + i);
-  // fc: thread t owns column i of the fc weight for the classes of its half h (two halves of 8
-  // classes, o4 granules ob, ob+1, when NC > 8 and two columns per thread fit: all 16 waves busy)
-  const int H = (NC > 8 && 2 * Fs <= nt) ? 2 : 1, no4 = (H == 2 || NC <= 8) ? 2 : 4;
-  const int h = H == 2 ? (int)threadIdx.x / Fs : 0, ob = H == 2 ? 2 * h : 0;
-  const int i0 = ilo + (int)threadIdx.x - h * Fs;
-  const bool fc_on = h < H && i0 < ihi;
-  float* fw = dst_of(8);
-  auto fc_load = [&](int i, float* pv) {  // column i's parameters (clamped addresses: no branch)
-#pragma unroll
-    for (int t = 0; t < 16; ++t) pv[t] = fw[min(4 * ob + t, NC - 1) * F + min(max(i, 0), F - 1)];
-  };
-  float pfc[16];  // the thread's first column, loaded with the level's other loads
-  fc_load(i0, pfc);
-  float* fb = dst_of(9);
-  const float pb = fb[min((int)threadIdx.x, NC - 1)];
-  auto conv_seg = [&](int p, int& seg, int& r) {
-    seg = 0;
-    while (seg < 7 && p >= g.off[seg + 1]) ++seg;
-    r = p - g.off[seg];
-    return dst_of(seg) + r;
-  };
-  struct Conv4 { float pv[4]; float4 c[4]; };  // group partials 0..3 (batches up to 32 images)
-  auto conv_load = [&](int q4, Conv4& k) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      int seg, r;
-      k.pv[u] = *conv_seg(min(4 * q4 + u, off8 - 1), seg, r);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) k.c[j] = smi_cc_load4(rpart, (j * P + 4 * q4) * 4);  // j >= ngrp: 0
-  };
-  auto conv_apply = [&](int q4, const Conv4& k) {
-    float4 gsum = k.c[0];
-#pragma unroll
-    for (int j = 1; j < 4; ++j) gsum = make_float4(gsum.x + k.c[j].x, gsum.y + k.c[j].y, gsum.z + k.c[j].z, gsum.w + k.c[j].w);
-    for (int j = 4; j < ngrp; ++j) {  // batches above 32 images
-      const float4 cj = smi_cc_load4(rpart, (j * P + 4 * q4) * 4);
-      gsum = make_float4(gsum.x + cj.x, gsum.y + cj.y, gsum.z + cj.z, gsum.w + cj.w);
-    }
-    const float gv[4] = {gsum.x, gsum.y, gsum.z, gsum.w};
-    float np[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      np[u] = k.pv[u] - lr * gv[u];
-      CNN_PIN(np[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int p = 4 * q4 + u;
-      if (q4 >= n4 || p >= off8) continue;
-      int seg, r;
-      float* dst = conv_seg(p, seg, r);
-      *dst = np[u];
-      if (g.shadow[seg]) g.shadow[seg][r] = f2bf(np[u]);
-    }
-  };
-  // granules of an image's row this slice stages: dl (the first ndl4) and its p2 columns
   const int ndl4 = (NC + 3) >> 2, p4lo = (NC + ilo) >> 2, np4 = ((NC + ihi + 3) >> 2) - p4lo, ng = ndl4 + np4;
   const int nst = g.B * ng;
   auto stage_j4 = [&](int e, int& im) {
@@ -664,65 +639,103 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
     const int jj = e - im * ng;
     return jj < ndl4 ? jj : p4lo + (jj - ndl4);
   };
-  auto stage_load = [&](int e4, float4* v) {
+  float4 sv[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      int im;
-      const int j4 = stage_j4(e4 + u * nt, im);
-      v[u] = smi_cc_load4(rslab, (im * P + cs + 4 * j4) * 4);  // im >= B: 0
-    }
-  };
-  auto stage_store = [&](int e4, const float4* v) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      int im;
-      const int j4 = stage_j4(e4 + u * nt, im);
-      if (e4 + u * nt < nst) reinterpret_cast<float4*>(sm + im * R4)[j4] = v[u];
-    }
-  };
-  if (q4hi - q4lo <= nt && nst <= 4 * nt) {
-    // one round trip: every staging and partial-sum load of the thread issued before the first use
-    float4 v[4];
-    Conv4 k;
-    const int q4 = q4lo + (int)threadIdx.x;
-    stage_load(threadIdx.x, v);
-    conv_load(min(q4, q4hi - 1), k);
-    stage_store(threadIdx.x, v);
-#pragma unroll
-    for (int t = 0; t < 16; ++t) CNN_PIN(pfc[t]);
-    STAMP(21);
-    if (q4 < q4hi) conv_apply(q4, k);
-    STAMP(22);
-  } else {
-    for (int e4 = threadIdx.x; e4 < nst; e4 += 4 * nt) {
+  for (int u = 0; u < 4; ++u) {
+    int im;
+    const int j4 = stage_j4(threadIdx.x + u * nt, im);
+    sv[u] = smi_cc_load4(rslab, (im * P + cs + 4 * j4) * 4);  // im >= B: 0
+  }
+  float rl = 0.f;  // lane i: row losses i, i + 64, ... (the last slice's mean loss)
+  if (threadIdx.x < 64)
+    for (int i = threadIdx.x; i < g.B; i += 64) rl += smi_cc_load(g.row_loss + i);
+  // conv: chunk c of nch (<= 8) sums images [c B / nch, (c + 1) B / nch) of granule q in image order
+  const int nch = max(1, min(min(nt / max(nq, 1), g.B), 8));
+  float4* cpart = reinterpret_cast<float4*>(sm + g.B * R4);  // [nch][nq] after the staged rows
+  for (int u = threadIdx.x; u < nch * nq; u += nt) {
+    const int c = u / nq, q4 = q4lo + (u - c * nq);
+    const int lo = c * g.B / nch, hi = (c + 1) * g.B / nch;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int im = lo; im < hi; im += 4) {
       float4 v[4];
-      stage_load(e4, v);
-      stage_store(e4, v);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = smi_cc_load4(rslab, ((im + k < hi ? im + k : g.B) * P + 4 * q4) * 4);  // B: 0
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc = make_float4(acc.x + v[k].x, acc.y + v[k].y, acc.z + v[k].z, acc.w + v[k].w);
     }
-    for (int q4 = q4lo + (int)threadIdx.x; q4 < q4hi; q4 += nt) {
-      Conv4 k;
-      conv_load(q4, k);
-      conv_apply(q4, k);
+    cpart[u] = acc;
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    int im;
+    const int e = threadIdx.x + u * nt;
+    const int j4 = stage_j4(e, im);
+    if (e < nst) reinterpret_cast<float4*>(sm + im * R4)[j4] = sv[u];
+  }
+  for (int e = threadIdx.x + 4 * nt; e < nst; e += nt) {  // past 4 granules per thread
+    int im;
+    const int j4 = stage_j4(e, im);
+    reinterpret_cast<float4*>(sm + im * R4)[j4] = smi_cc_load4(rslab, (im * P + cs + 4 * j4) * 4);
+  }
+#pragma unroll
+  for (int t = 0; t < 16; ++t) CNN_PIN(pfc[t]);
+  __syncthreads();
+  STAMP(21);
+  // conv SGD from the chunk partials (chunk order; every LDS read issued before the adds)
+  auto conv_apply = [&](int q, const float* pv) {
+    float4 cp[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) cp[c] = cpart[min(c, nch - 1) * nq + q];
+    float4 gs4 = cp[0];
+#pragma unroll
+    for (int c = 1; c < 8; ++c)
+      if (c < nch) gs4 = make_float4(gs4.x + cp[c].x, gs4.y + cp[c].y, gs4.z + cp[c].z, gs4.w + cp[c].w);
+    const float gv[4] = {gs4.x, gs4.y, gs4.z, gs4.w};
+    float np[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      np[u] = pv[u] - lr * gv[u];
+      CNN_PIN(np[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = 4 * (q4lo + q) + u;
+      if (p >= off8) continue;
+      int seg, r;
+      float* dst = conv_seg(p, seg, r);
+      *dst = np[u];
+      unsigned short* sh = shadow_of(seg);
+      if (sh) sh[r] = f2bf(np[u]);
+    }
+  };
+  if (nq <= nt) {
+    if ((int)threadIdx.x < nq) conv_apply(threadIdx.x, pcv);
+  } else {
+    for (int q = threadIdx.x; q < nq; q += nt) {
+      float pv[4];
+      conv_pload(q4lo + q, pv);
+      conv_apply(q, pv);
     }
   }
-  __syncthreads();
+  STAMP(22);
   STAMP(30);
-  // gW[o][i] = sum_im dl[im][o] * p2[im][i] in image order (o = 4 * (ob + t4) + c)
-  // NO4 (compile time): the class granules of the thread's half.  Images in batches of IB with every
-  // LDS read of a batch issued before the FMAs (one LDS latency per batch, not per read)
-  auto fc_column_n = [&](auto no4c, int i, const float* pv) {
+  // gW[o][i] = sum_im dl[im][o] * p2[im][i] (o = 4 * (ob + t4) + c): lane kc of the slot sums
+  // images kc, kc + KCH, ... in batches of IB with every LDS read of a batch issued before the
+  // FMAs (one LDS latency per batch), then the slot's lanes combine by a butterfly.
+  // NO4 (compile time): the class granules of the slot's half
+  auto fc_column_n = [&](auto no4c, int i, const float* pv, int k0, int kst) {
     constexpr int NO4 = decltype(no4c)::value;
     float gw[4 * NO4];
 #pragma unroll
     for (int t = 0; t < 4 * NO4; ++t) gw[t] = 0.f;
     constexpr int IB = 8 / NO4;  // images per batch: 32 registers of dl granules in flight
-    int im = 0;
-    for (; im + IB <= g.B; im += IB) {
+    int im = k0;
+    for (; im + (IB - 1) * kst < g.B; im += IB * kst) {
       float x[IB];
       float4 d[IB][NO4];
 #pragma unroll
       for (int u = 0; u < IB; ++u) {
-        const float* row = sm + (im + u) * R4;
+        const float* row = sm + (im + u * kst) * R4;
         x[u] = row[NC + i];
 #pragma unroll
         for (int t4 = 0; t4 < NO4; ++t4) d[u][t4] = reinterpret_cast<const float4*>(row)[ob + t4];
@@ -737,7 +750,7 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
           gw[4 * t4 + 3] += d[u][t4].w * x[u];
         }
     }
-    for (; im < g.B; ++im) {
+    for (; im < g.B; im += kst) {
       const float* row = sm + im * R4;
       const float x = row[NC + i];
 #pragma unroll
@@ -749,12 +762,16 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
         gw[4 * t4 + 3] += d.w * x;
       }
     }
+    for (int m = 1; m < kst; m <<= 1)  // the slot's kst lanes (aligned, all active): a + b == b + a
+#pragma unroll
+      for (int t = 0; t < 4 * NO4; ++t) gw[t] += __shfl_xor(gw[t], m, 64);
     float np[4 * NO4];
 #pragma unroll
     for (int t = 0; t < 4 * NO4; ++t) {
       np[t] = pv[t] - lr * gw[t];
       CNN_PIN(np[t]);
     }
+    if (k0 != 0) return;
 #pragma unroll
     for (int t = 0; t < 4 * NO4; ++t) {
       const int o = 4 * ob + t;
@@ -763,17 +780,17 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
       if (g.shadow[8]) g.shadow[8][o * F + i] = f2bf(np[t]);
     }
   };
-  auto fc_column = [&](int i, const float* pv) {
-    if (no4 == 2) fc_column_n(std::integral_constant<int, 2>{}, i, pv);
-    else fc_column_n(std::integral_constant<int, 4>{}, i, pv);
+  auto fc_column = [&](int i, const float* pv, int k0, int kst) {
+    if (no4 == 2) fc_column_n(std::integral_constant<int, 2>{}, i, pv, k0, kst);
+    else fc_column_n(std::integral_constant<int, 4>{}, i, pv, k0, kst);
   };
-  if (H * Fs <= nt) {  // one column per thread: no loop (a loop's loads make every store wait)
-    if (fc_on) fc_column(i0, pfc);
-  } else {
+  if (nslot * KCH <= nt) {  // one slot per lane group: no loop (a loop's loads make every store wait)
+    if (fc_on) fc_column(i0, pfc, kc, KCH);
+  } else {  // KCH == 1
     for (int i = i0; i < ihi; i += nt) {
       float pv[16];
       fc_load(i, pv);
-      fc_column(i, pv);
+      fc_column(i, pv, 0, 1);
     }
   }
   STAMP(23);
@@ -790,7 +807,7 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
   RSTAMP(7);
   // the last slice to finish: the mean loss (image order), the step counter, the cursor, re-arms
   __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(g.tick + CNN_GRP + 1, 1u) == (unsigned)(ngrp - 1);
+  if (threadIdx.x == 0) last = atomicAdd(g.tick + 1, 1u) == (unsigned)(nsl - 1);
   __syncthreads();
   if (!last) return;
   if (threadIdx.x < 64) {
@@ -799,8 +816,8 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, int img, float*
       if (g.loss) g.loss[0] = ls * g.loss_scale;
       if (g.step && !gmode) g.step[0] += 1.f;
       if (g.cursor) g.cursor[0] += 1;  // index mode: every workgroup read it before its ticket
-      g.tick[CNN_GRP] = 0u;
-      g.tick[CNN_GRP + 1] = 0u;
+      g.tick[0] = 0u;
+      g.tick[1] = 0u;
     }
   }
   // the weight-gradient helpers' hand-off flags, re-armed for the next launch (every helper read
@@ -1145,7 +1162,7 @@ __global__ __launch_bounds__(CNN_THREADS) void cnn_kernel(CNNArgs g) {
   const int img = helper ? (wg - g.B) / CNN_HELPERS : wg;
   if (!cnn_image<CC, EX, BF>(g, sm, img, helper ? (wg - g.B) % CNN_HELPERS : -1)) return;
   RSTAMP(4);
-  if (g.fused) cnn_fused_tail(g, img, sm);
+  if (g.fused) cnn_fused_tail(g, sm, helper ? -1 : img);
 }
 
 // grad[p] (+)= dloss * sum_img slab[img][p], scattered to the 10 parameter tensors; also the mean
@@ -1191,10 +1208,17 @@ static size_t cnn_lds_bytes(const CNNArgs& g) {
                                   WG_SCRATCH + 2 + (g.wstage ? C * CI * 9 + 3 * C * C * 9 + 4 * C : 0));
 }
 
+// the fused tail's LDS: every image's staged dl / p2 row, then the conv chunk partials (at most 8
+// chunks of a slice's granules, float4; cnn_fused_tail)
+static size_t cnn_tail_lds(int C, int cin, int classes, int B) {
+  const int n4 = ((C * cin * 9 + C + 3 * (C * C * 9 + C)) + 3) >> 2, nsl = B < CNN_NSL ? B : CNN_NSL;
+  const int nq = (n4 + nsl - 1) / nsl;  // a slice's conv granules (at most)
+  return sizeof(float) * ((size_t)B * ((classes + C * 49 + 3) & ~3) + 4 * 8 * (size_t)nq);
+}
+
 extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
   CNNArgs g = *args;
-  // the fused tail's group tickets are tick[0 .. ngrp) below the level-2 ticket tick[CNN_GRP]
-  if (g.fused && (g.P % 4 || (g.B + CNN_GRP - 1) / CNN_GRP > CNN_GRP || !g.part || !g.tick || !g.slab || !g.row_loss || !g.train)) return -1;
+  if (g.fused && (g.P % 4 || g.B > CNN_MAXB || !g.tick || !g.slab || !g.row_loss || !g.train)) return -1;
   if (g.perm && (!g.fused || !g.cursor)) return -1;  // index mode: fused steps only
   if (g.hand && (!g.fused || !g.hflag)) return -1;    // helpers: fused steps only
   if (g.fused && !g.lr) {  // gradient mode: every gradient destination, no shadows
@@ -1208,8 +1232,7 @@ extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
   if (g.wstage && cnn_lds_bytes(g) > 160 * 1024) g.wstage = 0;  // the weights then stay global
   const size_t lds = cnn_lds_bytes(g);
   if (lds > 160 * 1024) return -1;
-  // the fused tail stages every image's dl and p2 in the (then free) LDS planes
-  if (g.fused && (size_t)g.B * ((g.classes + g.C * 49 + 3) & ~3) * sizeof(float) > lds) return -1;
+  if (g.fused && cnn_tail_lds(g.C, g.cin, g.classes, g.B) > lds) return -1;
   // channel capacity 10 (the reference model's hidden_units) gets exact compile-time groups
   // (LDS residency caps C at 13 for 1-channel input, so no exact instance above 10)
   auto kern = g.bf16 ? (g.C == 10 ? cnn_kernel<10, true, true> : cnn_kernel<CNN_MAXC, false, true>)
@@ -1223,12 +1246,10 @@ extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
 extern "C" int smi_cnn_hand_floats(int C) { return (C >= 1 && C <= CNN_MAXC) ? cnn_hand_f(C) : 0; }
 
 extern "C" int smi_cnn_fused_ok(int C, int cin, int classes, int B) {
-  // the fused tail stages every image's dl and p2 in the kernel's LDS (see smi_cnn)
   CNNArgs g{};
   g.C = C; g.cin = cin; g.classes = classes;
   const int P = C * cin * 9 + C + 3 * (C * C * 9 + C) + classes * C * 49 + classes;
-  return P % 4 == 0 && B <= CNN_GRP * CNN_GRP &&
-         (size_t)B * ((classes + C * 49 + 3) & ~3) * sizeof(float) <= cnn_lds_bytes(g);
+  return P % 4 == 0 && B >= 1 && B <= CNN_MAXB && cnn_tail_lds(C, cin, classes, B) <= cnn_lds_bytes(g);
 }
 
 extern "C" int smi_cnn_reduce(const CNNArgs* args, hipStream_t st) {

@@ -26,9 +26,9 @@ class FashionMNISTModel(nn.Module):
             nn.Conv2d(hidden_units, hidden_units, 3, padding=1), nn.ReLU(),
             nn.MaxPool2d(2))
         self.classifier = nn.Sequential(nn.Flatten(), nn.Linear(hidden_units * 7 * 7, output_shape))
-        # fused-step tickets (CNN_GRP + 1 <= 33 counters, re-armed by the kernel): per model, so
-        # two models never share them; not part of the state_dict (reference key parity)
-        # the fused step's counters: CNN_GRP + 2 for the tail, then 3 per image (<= CNN_GRP^2 = 64)
+        # the fused step's counters (re-armed by the kernel): CNN_TICKS for the tail, then 3 per
+        # image (batch <= CNN_MAXB = 64; csrc/include/smi_cnn.h); per model, so two models never
+        # share them; not part of the state_dict (reference key parity)
         # for the weight-gradient helpers' hand-off flags
         self.register_buffer("_step_tick", torch.zeros(34 + 3 * 64, dtype=torch.int32), persistent=False)
 

@@ -129,7 +129,7 @@ def cnn_sgd_step(x, y, params, lr_t, step_t, tick, shadows=None, bf16=False, ind
     slabs are summed in the kernel's ticketed tail, which then updates ``params`` in place
     (p -= lr * g; ``lr_t`` / ``step_t`` are the optimizer's device scalars) and their bf16
     ``shadows`` (10 tensors or None).  Returns the step's mean loss (device scalar).  ``tick``:
-    CNN_GRP + 2 + 3 B zeroed int32 counters owned by the model (the kernel re-arms them).
+    CNN_TICKS + 3 B zeroed int32 counters owned by the model (the kernel re-arms them).
     ``index`` = (batch, perm, cursor): ``x`` / ``y`` are the whole dataset and the kernel reads image
     i of the batch from row perm[cursor * batch + i], then advances the device cursor (the shuffled
     batch gather inside the step kernel; DeviceLoader fixed=True, index mode)."""
@@ -138,13 +138,11 @@ def cnn_sgd_step(x, y, params, lr_t, step_t, tick, shadows=None, bf16=False, ind
     b = [params[i] for i in (1, 3, 5, 7, 9)]
     P = num_params(params)
     slab = torch.empty(B, P, device=x.device, dtype=torch.float32)
-    grp = _native.C().cnn_grp()
-    part = torch.empty((B + grp - 1) // grp, P, device=x.device, dtype=torch.float32)
     row_loss = torch.empty(B, device=x.device, dtype=torch.float32)
     loss = torch.empty(1, device=x.device, dtype=torch.float32)
     _native.C().cnn_sgd_step(x.data_ptr(), int(x.dtype == torch.uint8), 1.0 / 255.0, y.data_ptr(), B, x.shape[1],
                              w[0].shape[0], w[4].shape[0], [t.data_ptr() for t in w], [t.data_ptr() for t in b],
-                             [t.data_ptr() for t in shadows] if shadows else [], slab.data_ptr(), part.data_ptr(),
+                             [t.data_ptr() for t in shadows] if shadows else [], slab.data_ptr(),
                              row_loss.data_ptr(), loss.data_ptr(), 1.0 / B, lr_t.data_ptr(), step_t.data_ptr(),
                              tick.data_ptr(), int(bf16), index[1].data_ptr() if index else 0,
                              index[2].data_ptr() if index else 0, _native.ptr(_hand(B, w[0].shape[0], x.device)),
@@ -163,14 +161,12 @@ def cnn_grad_step(x, y, params, grads, tick, bf16=False, index=None):
     b = [params[i] for i in (1, 3, 5, 7, 9)]
     P = num_params(params)
     slab = torch.empty(B, P, device=x.device, dtype=torch.float32)
-    grp = _native.C().cnn_grp()
-    part = torch.empty((B + grp - 1) // grp, P, device=x.device, dtype=torch.float32)
     row_loss = torch.empty(B, device=x.device, dtype=torch.float32)
     loss = torch.empty(1, device=x.device, dtype=torch.float32)
     _native.C().cnn_grad_step(x.data_ptr(), int(x.dtype == torch.uint8), 1.0 / 255.0, y.data_ptr(), B, x.shape[1],
                               w[0].shape[0], w[4].shape[0], [t.data_ptr() for t in w], [t.data_ptr() for t in b],
                               [grads[i].data_ptr() for i in (0, 2, 4, 6, 8)],
-                              [grads[i].data_ptr() for i in (1, 3, 5, 7, 9)], slab.data_ptr(), part.data_ptr(),
+                              [grads[i].data_ptr() for i in (1, 3, 5, 7, 9)], slab.data_ptr(),
                               row_loss.data_ptr(), loss.data_ptr(), 1.0 / B, tick.data_ptr(), int(bf16),
                               index[1].data_ptr() if index else 0, index[2].data_ptr() if index else 0,
                               _native.ptr(_hand(B, w[0].shape[0], x.device)), _native.stream())

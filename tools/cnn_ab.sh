@@ -1,17 +1,19 @@
 #!/bin/bash
-# Build the CNN probe for two versions of csrc/kernels/cnn.hip (a git revision vs the working tree),
-# stamped and unstamped, into tools/probes/ab_*; run tools/cnn_ab_run.sh on the GPU box.
+# Build the CNN probe (the working tree's) for two versions of the kernel (a git revision vs the
+# working tree, each with its own header), stamped and unstamped, into tools/probes/ab_*; run
+# tools/cnn_ab_run.sh on the GPU box.
 # usage: bash tools/cnn_ab.sh [REV]   (default HEAD)
 set -e
 cd "$(dirname "$0")/.."
 REV=${1:-HEAD}
-mkdir -p /tmp/cnn_ab && git show "$REV:csrc/kernels/cnn.hip" > /tmp/cnn_ab/cnn_a.hip
-cp csrc/kernels/cnn.hip /tmp/cnn_ab/cnn_b.hip
+rm -rf /tmp/cnn_ab && mkdir -p /tmp/cnn_ab/a
+git archive "$REV" csrc | tar -x -C /tmp/cnn_ab/a
 for v in a b; do
+  root=$PWD; [ $v = a ] && root=/tmp/cnn_ab/a
   for m in stamp plain; do
     extra=""; [ $m = plain ] && extra="-DCNN_PROBE_NOSTAMP"
-    /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -Icsrc/include -Wno-unused-value $extra \
-      -DCNN_SRC="\"/tmp/cnn_ab/cnn_$v.hip\"" tools/probes/cnn_probe.hip -o tools/probes/ab_${v}_$m &
+    /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -I$root/csrc/include -Wno-unused-value $extra \
+      -DCNN_SRC="\"$root/csrc/kernels/cnn.hip\"" tools/probes/cnn_probe.hip -o tools/probes/ab_${v}_$m &
   done
 done
 wait
