@@ -566,18 +566,20 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, float* sm, int 
   // load per step, and selects over the 8 pointers spill)
   __shared__ float* seg_dst[8];
   __shared__ unsigned short* seg_sh[8];
+  __shared__ int seg_off[8];
   if (threadIdx.x < 8) {
     seg_dst[threadIdx.x] = dst_of(threadIdx.x);
     seg_sh[threadIdx.x] = g.shadow[threadIdx.x];
+    seg_off[threadIdx.x] = g.off[threadIdx.x];
   }
   __syncthreads();
+  // (the segment's offset from the LDS table too: selecting it from the argument block compiled to
+  // a global load of the selected address, whose wait also waited out every earlier store)
   auto conv_seg = [&](int p, int& seg, int& r) {
     seg = 0;
-    int base = g.off[0];
 #pragma unroll
-    for (int k = 1; k < 8; ++k)
-      if (p >= g.off[k]) { seg = k; base = g.off[k]; }
-    r = p - base;
+    for (int k = 1; k < 8; ++k) seg += p >= g.off[k] ? 1 : 0;
+    r = p - seg_off[seg];
     return seg_dst[seg] + r;
   };
   auto shadow_of = [&](int seg) { return seg_sh[seg]; };
@@ -609,7 +611,7 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, float* sm, int 
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       int seg, r;
-      pv[u] = *conv_seg(min(max(4 * q4 + u, 0), off8 - 1), seg, r);
+      pv[u] = *(const __attribute__((address_space(1))) float*)conv_seg(min(max(4 * q4 + u, 0), off8 - 1), seg, r);
     }
   };
   float pcv[4];  // granule q4lo + threadIdx.x (the one-granule-per-thread case)
@@ -639,40 +641,64 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, float* sm, int 
     const int jj = e - im * ng;
     return jj < ndl4 ? jj : p4lo + (jj - ndl4);
   };
-  float4 sv[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  float4 sv;  // the thread's first staging granule (B <= 64: one per thread at C = 10)
+  {
     int im;
-    const int j4 = stage_j4(threadIdx.x + u * nt, im);
-    sv[u] = smi_cc_load4(rslab, (im * P + cs + 4 * j4) * 4);  // im >= B: 0
+    const int j4 = stage_j4(threadIdx.x, im);
+    sv = smi_cc_load4(rslab, (im * P + cs + 4 * j4) * 4);  // im >= B: 0
   }
-  float rl = 0.f;  // lane i: row losses i, i + 64, ... (the last slice's mean loss)
-  if (threadIdx.x < 64)
-    for (int i = threadIdx.x; i < g.B; i += 64) rl += smi_cc_load(g.row_loss + i);
+  // Straight-line loads only: a load inside a loop makes the compiler wait for every outstanding
+  // load (vmcnt(0)) at the loop, which serialised the staging, row-loss and chunk round trips
+  // lane i: row loss i (B <= 64; wave 0 forms the last slice's mean loss; used there only)
+  const float rlv = smi_cc_load(g.row_loss + min((int)(threadIdx.x & 63), g.B - 1));
   // conv: chunk c of nch (<= 8) sums images [c B / nch, (c + 1) B / nch) of granule q in image order
   const int nch = max(1, min(min(nt / max(nq, 1), g.B), 8));
   float4* cpart = reinterpret_cast<float4*>(sm + g.B * R4);  // [nch][nq] after the staged rows
-  for (int u = threadIdx.x; u < nch * nq; u += nt) {
+  auto chunk_sum = [&](int u, float4* v) {  // the 4 first images' loads of (chunk, granule) u
+    const int c = u / nq, q4 = q4lo + (u - c * nq);
+    const int lo = c * g.B / nch, hi = (c + 1) * g.B / nch;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = smi_cc_load4(rslab, ((lo + k < hi ? lo + k : g.B) * P + 4 * q4) * 4);  // B: 0
+  };
+  auto chunk_add = [&](int u, const float4* v) {
     const int c = u / nq, q4 = q4lo + (u - c * nq);
     const int lo = c * g.B / nch, hi = (c + 1) * g.B / nch;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int im = lo; im < hi; im += 4) {
-      float4 v[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = smi_cc_load4(rslab, ((im + k < hi ? im + k : g.B) * P + 4 * q4) * 4);  // B: 0
-#pragma unroll
-      for (int k = 0; k < 4; ++k) acc = make_float4(acc.x + v[k].x, acc.y + v[k].y, acc.z + v[k].z, acc.w + v[k].w);
+    for (int k = 0; k < 4; ++k) acc = make_float4(acc.x + v[k].x, acc.y + v[k].y, acc.z + v[k].z, acc.w + v[k].w);
+    for (int im = lo + 4; im < hi; ++im) {  // chunks past 4 images (batches above 32)
+      const float4 w = smi_cc_load4(rslab, (im * P + 4 * q4) * 4);
+      acc = make_float4(acc.x + w.x, acc.y + w.y, acc.z + w.z, acc.w + w.w);
     }
-    cpart[u] = acc;
-  }
+    return acc;
+  };
+  // one (chunk, granule) per thread and at most 4 images a chunk: no loop; the loads pinned here,
+  // after every load of the phase is issued (the compiler otherwise sinks them into the store's
+  // branch behind a vmcnt(0))
+  const bool one_chunk = nch * nq <= nt && (g.B + nch - 1) / nch <= 4;
+  float4 cv[4];
+  chunk_sum(min((int)threadIdx.x, nch * nq - 1), cv);
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    int im;
-    const int e = threadIdx.x + u * nt;
-    const int j4 = stage_j4(e, im);
-    if (e < nst) reinterpret_cast<float4*>(sm + im * R4)[j4] = sv[u];
+  for (int k = 0; k < 4; ++k) {
+    CNN_PIN(cv[k].x);
+    CNN_PIN(cv[k].y);
+    CNN_PIN(cv[k].z);
+    CNN_PIN(cv[k].w);
   }
-  for (int e = threadIdx.x + 4 * nt; e < nst; e += nt) {  // past 4 granules per thread
+  if (one_chunk) {
+    if ((int)threadIdx.x < nch * nq) cpart[threadIdx.x] = chunk_add(threadIdx.x, cv);
+  } else {
+    for (int u = threadIdx.x; u < nch * nq; u += nt) {
+      chunk_sum(u, cv);
+      cpart[u] = chunk_add(u, cv);
+    }
+  }
+  {
+    int im;
+    const int j4 = stage_j4(threadIdx.x, im);
+    if ((int)threadIdx.x < nst) reinterpret_cast<float4*>(sm + im * R4)[j4] = sv;
+  }
+  for (int e = threadIdx.x + nt; e < nst; e += nt) {  // past one granule per thread
     int im;
     const int j4 = stage_j4(e, im);
     reinterpret_cast<float4*>(sm + im * R4)[j4] = smi_cc_load4(rslab, (im * P + cs + 4 * j4) * 4);
@@ -702,10 +728,12 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, float* sm, int 
       const int p = 4 * (q4lo + q) + u;
       if (p >= off8) continue;
       int seg, r;
+      // global-address-space stores: through a generic pointer (read from the LDS table) they are
+      // flat stores, which also count in lgkmcnt, so the next LDS wait would wait them out
       float* dst = conv_seg(p, seg, r);
-      *dst = np[u];
+      *(__attribute__((address_space(1))) float*)dst = np[u];
       unsigned short* sh = shadow_of(seg);
-      if (sh) sh[r] = f2bf(np[u]);
+      if (sh) *(__attribute__((address_space(1))) unsigned short*)(sh + r) = f2bf(np[u]);
     }
   };
   if (nq <= nt) {
@@ -811,7 +839,7 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, float* sm, int 
   __syncthreads();
   if (!last) return;
   if (threadIdx.x < 64) {
-    const float ls = wave_sum(rl);
+    const float ls = wave_sum((int)threadIdx.x < g.B ? rlv : 0.f);
     if (threadIdx.x == 0) {
       if (g.loss) g.loss[0] = ls * g.loss_scale;
       if (g.step && !gmode) g.step[0] += 1.f;
@@ -983,57 +1011,86 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
   else conv_fwd<14, P14, CC, EX>(a3, C, a4, C, g.w[3], g.b[3]);
   __syncthreads();
   STAMP(6);
-  pool_fwd<14, P14, 7, 0>(a4, p2, C);
-  __syncthreads();
-  STAMP(7);
-  // classifier: wave w computes logits o = w, w+4, ...
+  // classifier: wave w computes logit o = w (NC <= 16 = the waves); its weight row is loaded
+  // before pool2 (its round trip overlaps the pool; an LDS-only barrier after the pool leaves it
+  // in flight)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int F = C * 49;
-  for (int o = wv; o < NC; o += CNN_THREADS / 64) {
+  constexpr int FK = (CC * 49 + 63) / 64;  // lane's share of a row: i = lane + 64 k
+  float fcw[FK];
+  if (wv < NC) {  // (wave-uniform) every load unconditional inside: clamped addresses
+    const float* wr = g.w[4] + wv * F;
+#pragma unroll
+    for (int k = 0; k < FK; ++k) fcw[k] = wr[min(lane + 64 * k, F - 1)];
+  }
+  pool_fwd<14, P14, 7, 0>(a4, p2, C);
+  smi_lds_barrier();
+  STAMP(7);
+  if (wv < NC) {
     float s = 0.f;
-    for (int i = lane; i < F; i += 64) s += g.w[4][o * F + i] * p2[i];
+#pragma unroll
+    for (int k = 0; k < FK; ++k)
+      if (lane + 64 * k < F) s += fcw[k] * p2[lane + 64 * k];
     s = wave_sum(s);
-    if (lane == 0) lg[o] = s + g.b[4][o];
+    if (lane == 0) lg[wv] = s + g.b[4][wv];
   }
   __syncthreads();
   STAMP(8);
-  if (threadIdx.x == 0) {
-    float m = lg[0];
-    int am = 0;
-    for (int o = 1; o < NC; ++o) if (lg[o] > m) { m = lg[o]; am = o; }
-    float se = 0.f;
-    for (int o = 0; o < NC; ++o) se += __expf(lg[o] - m);
-    const float lse = m + __logf(se);
-    const int lab = lab0;
-    if (g.row_loss) smi_wt_store(g.row_loss + img, lse - lg[lab]);  // read by the last workgroup
-    if (g.pred) g.pred[img] = am;
-    if (g.logits)
-      for (int o = 0; o < NC; ++o) g.logits[(long)img * NC + o] = lg[o];
-    if (g.train) {
+  // the fc backward's weight columns (thread i < F holds W[o][i] of every class; F <= 784 < the
+  // 1024 threads), loaded now: their round trip overlaps the cross-entropy
+  float wc[16];
+  if (g.train && wv * 64 < F) {
+    const int i = min((int)threadIdx.x, F - 1);
+#pragma unroll
+    for (int o = 0; o < 16; ++o) wc[o] = g.w[4][min(o, NC - 1) * F + i];
+  }
+  // cross-entropy on wave 0, lane o = class o (NC <= 16): max, log-sum-exp and the logit gradient
+  // as DPP wave reductions, the argmax from a ballot, the label's logit by readlane (one lane
+  // walking the classes through dependent LDS reads took ~3k clocks, shuffles ~2.7k)
+  float row_l = 0.f;  // lane 0: this image's loss, stored after the fc backward's loads are used
+  if (threadIdx.x < 64) {
+    const int o = threadIdx.x;
+    const float v = o < NC ? lg[o] : -INFINITY;
+    const float m = wave_max(v);
+    const unsigned long long top = __ballot(v == m);
+    const int am = top ? __builtin_ctzll(top) : 0;  // the first maximum
+    const float lse = m + __logf(wave_sum(o < NC ? __expf(v - m) : 0.f));
+    const int lab = min(max(__builtin_amdgcn_readfirstlane(lab0), 0), NC - 1);
+    row_l = lse - __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lab));
+    if (o == 0 && g.pred) g.pred[img] = am;
+    if (o < NC) {
+      if (g.logits) g.logits[(long)img * NC + o] = v;
       // dlogits = (softmax - onehot) * loss_scale   (loss_scale = 1/B for a mean loss)
-      for (int o = 0; o < NC; ++o) lg[o] = (__expf(lg[o] - lse) - (o == lab ? 1.f : 0.f)) * g.loss_scale;
+      if (g.train) lg[o] = (__expf(v - lse) - (o == lab ? 1.f : 0.f)) * g.loss_scale;
     }
   }
-  // mean loss without a second launch: the last workgroup to get here (atomic ticket) sums
-  // row_loss in image order with wave 0 and re-arms the ticket
-  if (g.loss && g.row_loss && !g.fused) {
-    __shared__ int cnn_last;
-    smi_wt_drain();
-    __syncthreads();
-    if (threadIdx.x == 0) cnn_last = atomicAdd(&cnn_loss_ticket, 1u) == (unsigned)g.B - 1;
-    __syncthreads();
-    if (cnn_last && threadIdx.x < 64) {
-      float s = 0.f;
-      for (int i = threadIdx.x; i < g.B; i += 64)
-        s += __hip_atomic_load(g.row_loss + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s = wave_sum(s);
-      if (threadIdx.x == 0) {
-        g.loss[0] = s * g.loss_scale;
-        cnn_loss_ticket = 0u;
+  // the row loss (thread 0) and, unfused, the mean loss without a second launch: the last
+  // workgroup to get here (atomic ticket) sums row_loss in image order with wave 0 and re-arms the
+  // ticket (the fused step's tail forms the mean loss instead)
+  auto store_loss = [&]() {
+    if (threadIdx.x == 0 && g.row_loss) smi_wt_store(g.row_loss + img, row_l);
+    if (g.loss && g.row_loss && !g.fused) {
+      __shared__ int cnn_last;
+      smi_wt_drain();
+      __syncthreads();
+      if (threadIdx.x == 0) cnn_last = atomicAdd(&cnn_loss_ticket, 1u) == (unsigned)g.B - 1;
+      __syncthreads();
+      if (cnn_last && threadIdx.x < 64) {
+        float s = 0.f;
+        for (int i = threadIdx.x; i < g.B; i += 64)
+          s += __hip_atomic_load(g.row_loss + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s = wave_sum(s);
+        if (threadIdx.x == 0) {
+          g.loss[0] = s * g.loss_scale;
+          cnn_loss_ticket = 0u;
+        }
       }
     }
+  };
+  if (!g.train) {
+    store_loss();
+    return false;
   }
-  if (!g.train) return false;
   // LDS-only barriers from here to the dgrad chain: the row loss / slab stores stay in flight (a
   // plain __syncthreads waits for them: ~1.5k clocks each); the tail drains before its ticket
   smi_lds_barrier();
@@ -1041,17 +1098,23 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
   float* gs = g.slab + (long)img * g.P;  // this image's gradient slab
   // fc grads: the slab keeps this image's dl (NC) and p2 (F) in place of the NC x F outer product
   // gW[o][i] = dl[o] * p2[i] (gb[o] = dl[o]): the reducers form the batch sum of products (a
-  // third of the bytes to reduce); dp2[i] = sum_o W[o][i] dl[o] goes into the p2 buffer after
-  for (int i = threadIdx.x; i < F; i += blockDim.x) smi_wt_store(gs + cnn_cs(g) + NC + i, p2[i]);
-  for (int o = threadIdx.x; o < NC; o += blockDim.x) smi_wt_store(gs + cnn_cs(g) + o, lg[o]);
+  // third of the bytes to reduce).  dp2[i] = sum_o W[o][i] dl[o] replaces p2[i] in place (the
+  // thread that read p2[i]: no barrier between).  Every store comes after the W loads' use (a
+  // wait for a load issued after a store would wait out the store too: vmcnt retires in order)
+  if ((int)threadIdx.x < F) {
+    const int i = threadIdx.x;
+    const float pv = p2[i];
+    float s = 0.f;
+#pragma unroll
+    for (int o = 0; o < 16; ++o)
+      if (o < NC) s += wc[o] * lg[o];
+    p2[i] = s;  // dp2 (flat NCHW)
+    smi_wt_store(gs + cnn_cs(g) + NC + i, pv);
+  }
+  if ((int)threadIdx.x < NC) smi_wt_store(gs + cnn_cs(g) + threadIdx.x, lg[threadIdx.x]);
+  store_loss();
   smi_lds_barrier();
   STAMP(10);
-  for (int i = threadIdx.x; i < F; i += blockDim.x) {
-    float s = 0.f;
-    for (int o = 0; o < NC; ++o) s += g.w[4][o * F + i] * lg[o];
-    p2[i] = s;  // dp2 (flat NCHW)
-  }
-  __syncthreads();
   STAMP(11);
   // pool2 backward + relu'(a4): dz4 in a4
   unpool_relu_inplace<14, P14>(a4, p2, 7, 0, C);
