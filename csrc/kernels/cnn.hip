@@ -431,6 +431,81 @@ __device__ __forceinline__ void conv_mfma(const float* __restrict__ in, int nin,
 }
 
 
+// ---- 28 x 28 MFMA convolutions from a channels-last bf16 copy (the exact C = 10 instance) ----
+// conv_mfma gathers each lane's 8 consecutive k of one position from the fp32 planes: 8 scalar LDS
+// reads + 2 offset-table reads per k-step, LDS-issue bound (conv2's forward and dgrad were the two
+// longest phases of the image).  Ordering k tap-major over 16 (padded) channels — k = tap * 16 +
+// channel — makes those 8 values 8 consecutive channels of one position: with the input first
+// copied to position-major bf16 rows of 16 channels, one 16-B read.  9 taps x 16 = 144 k in 5
+// k-steps (vs 3 for 90 k): more MFMAs, a fifth of the LDS instructions.  Same bf16 operand values
+// (round-to-nearest of the same fp32 activations and weights), fp32 accumulation.  The copy (900
+// padded positions x 32 B) lives in the 14 x 14 planes' region, dead during conv2's forward and
+// during its dgrad.
+#define HWC_KS 5
+
+// hw[half * ...]: row pos (padded position of the PP x PP plane) = 2 granules of 8 channels
+template <int PP>
+__device__ __forceinline__ void cnn_to_hwc(const float* __restrict__ in, int nin, uint4* __restrict__ hw) {
+  for (int e = threadIdx.x; e < 2 * PP * PP; e += blockDim.x) {
+    const int half = e >= PP * PP, pos = e - half * PP * PP, c0 = 8 * half;  // lanes: consecutive positions
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = c0 + j < nin ? in[(c0 + j) * CPL(PP) + pos] : 0.f;
+    hw[2 * pos + half] = make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+  }
+}
+
+// conv_mfma's contract (DG / RELU / out / epilogue) with the input `in` given as fp32 planes and
+// copied to the channels-last bf16 rows `hw` first (nin, nout <= 16)
+template <int H, int PP, bool DG, bool RELU>
+__device__ __forceinline__ void conv_mfma_hwc(const float* __restrict__ in, int nin, uint4* __restrict__ hw,
+                                              float* __restrict__ out, int nout, const float* __restrict__ wg,
+                                              const float* __restrict__ bg, float* __restrict__ tab) {
+  constexpr int NT = (H * H + 15) / 16;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  cnn_to_hwc<PP>(in, nin, hw);
+  bf16x8_t* wtab = (bf16x8_t*)tab;  // [HWC_KS][64 lanes] B fragments: B[k = tap * 16 + c][col]
+  for (int e = threadIdx.x; e < HWC_KS * 64; e += blockDim.x) {
+    const int s = e >> 6, l = e & 63, col = l & 15;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 32 * s + 8 * (l >> 4) + j, tap = k >> 4, c = k & 15;
+      // forward: W[col][c][tap]; dgrad (A offset (dy, dx) = (1 - ky, 1 - kx)): W[c][col][8 - tap]
+      v[j] = (tap < 9 && c < nin && col < nout) ? wg[DG ? (c * nout + col) * 9 + (8 - tap) : (col * nin + c) * 9 + tap] : 0.f;
+    }
+    wtab[e] = cnn_pack8(v);
+  }
+  __syncthreads();
+  const int col = lane & 15, half = (lane >> 4) & 1, tsel = lane >> 5;  // k = 32 s + 8 (lane >> 4) + j
+  const float bias = (!DG && col < nout) ? bg[col] : 0.f;
+  const bf16x8_t* hb = (const bf16x8_t*)hw;
+  for (int t = wv; t < NT; t += nw) {
+    const int p = t * 16 + col;  // this lane's A row (position)
+    const bool pv = p < H * H;
+    const int base = pv ? (p / H + 1) * PP + (p % H + 1) : PP + 1;  // padded position
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < HWC_KS; ++s) {
+      const int tap = 2 * s + tsel;  // this lane's tap (dy, dx) = (tap / 3 - 1, tap % 3 - 1)
+      const bf16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+      const bf16x8_t a = (pv && tap < 9) ? hb[2 * (base + (tap / 3 - 1) * PP + (tap % 3 - 1)) + half] : z;
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wtab[s * 64 + lane], acc, 0, 0, 0);
+    }
+    if (col < nout) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = t * 16 + 4 * (lane >> 4) + r;
+        if (q < H * H) {
+          float* o = out + col * CPL(PP) + (q / H + 1) * PP + (q % H + 1);
+          if (!DG) *o = fmaxf(acc[r] + bias, 0.f);
+          else *o = RELU ? (*o > 0.f ? acc[r] : 0.f) : acc[r];
+        }
+      }
+    }
+  }
+}
+
 // bf16 weight gradient (the bf16 path): the same GEMM D[co][n] = sum_pos dz[co][pos] X[pos][n] on
 // v_mfma_f32_16x16x32_bf16 (fp32 accumulation), summed over the PADDED position index q (rows of
 // the halo plane, halo columns included: dz is zero there), so a lane's 8 positions of a 32-deep
@@ -930,6 +1005,9 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
   float* p1 = a2 + C * PL28;             // C x 16x16
   float* a3 = p1 + C * PL14;             // C x 16x16
   float* a4 = a3 + C * PL14;             // C x 16x16
+  // conv2's channels-last bf16 copy (conv_mfma_hwc) overlays p1 .. a4
+  static_assert(!(BF && EX) || (3 * CC * PL14 * 4 >= 2 * P28 * P28 * 16 && 3 * CC * PL14 % 4 == 0),
+                "conv_mfma_hwc copy exceeds the 14x14 planes");
   float* p2 = a4 + C * PL14;             // C*49 (flat, NCHW)
   float* lg = p2 + C * 49;               // logits / dlogits [16]
   float* wacc = lg + 16;                 // max(C, CI)*C*9 + C wgrad accumulators
@@ -988,8 +1066,16 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
     return true;
   }
   CNN_PIN(lab0);  // arrived during conv1
-  if (BF) conv_mfma<28, P28, false, false>(a1, C, a2, C, lw[1], lb[1], wscr);
-  else conv_fwd<28, P28, CC, EX>(a1, C, a2, C, g.w[1], g.b[1]);
+  if (BF && EX) {
+    conv_mfma_hwc<28, P28, false, false>(a1, C, (uint4*)p1, a2, C, lw[1], lb[1], wscr);
+    __syncthreads();
+    // the copy overlaid the 14 x 14 planes: their zero halos again
+    for (int i = threadIdx.x; i < 3 * C * PL14 / 4; i += blockDim.x) reinterpret_cast<float4*>(p1)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  } else if (BF) {
+    conv_mfma<28, P28, false, false>(a1, C, a2, C, lw[1], lb[1], wscr);
+  } else {
+    conv_fwd<28, P28, CC, EX>(a1, C, a2, C, g.w[1], g.b[1]);
+  }
   __syncthreads();
   STAMP(3);
   pool_fwd<28, P28, P14, 1>(a2, p1, C);
@@ -1148,7 +1234,8 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
     cnn_hand_publish(g, img, 2);
     STAMP(18);
     RSTAMP(1);
-    if (BF) conv_mfma<28, P28, true, true>(a2, C, a1, C, lw[1], nullptr, wscr);
+    if (BF && EX) conv_mfma_hwc<28, P28, true, true>(a2, C, (uint4*)p1, a1, C, lw[1], nullptr, wscr);
+    else if (BF) conv_mfma<28, P28, true, true>(a2, C, a1, C, lw[1], nullptr, wscr);
     else conv_dgrad<28, P28, CC, EX>(a2, C, g.w[1], C, a1, true);
     __syncthreads();
     STAMP(19);
@@ -1199,7 +1286,8 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
     smi_wt_store(gs + (e < C * C * 9 ? g.off[2] + e : g.off[3] + e - C * C * 9), wacc[e]);
     wacc[e] = 0.f;
   }
-  if (BF) conv_mfma<28, P28, true, true>(a2, C, a1, C, lw[1], nullptr, wscr);
+  if (BF && EX) conv_mfma_hwc<28, P28, true, true>(a2, C, (uint4*)p1, a1, C, lw[1], nullptr, wscr);
+  else if (BF) conv_mfma<28, P28, true, true>(a2, C, a1, C, lw[1], nullptr, wscr);
   else conv_dgrad<28, P28, CC, EX>(a2, C, g.w[1], C, a1, true);
   __syncthreads();
   STAMP(19);
