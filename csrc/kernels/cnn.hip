@@ -376,31 +376,36 @@ __device__ __forceinline__ bf16x8_t cnn_pack8(const float (&v)[8]) {
 // `tab` (LDS scratch): the layer's k -> plane-offset table and the bf16 B fragments of every
 // k-step, built once per call so the per-tile loop keeps almost nothing in registers (the
 // kernel runs 16 waves: 128 VGPRs per lane).
+// fragment-table entries (per layer: built once per call, or for the exact instance once per
+// launch: cnn_pretab).  Entry e = k-step s (e >> 6) x lane l: 8 bf16 of B[k = 32 s + 8 (l >> 4) + j]
+// [col = l & 15].  conv_mfma orders k channel-major (k = c * 9 + tap), the channels-last form
+// tap-major over 16 channels (k = tap * 16 + c).
+template <bool DG>
+__device__ __forceinline__ bf16x8_t cnn_wtab_entry(int e, const float* __restrict__ wg, int nin, int nout) {
+  const int s = e >> 6, l = e & 63, col = l & 15, K = nin * 9;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 32 * s + 8 * (l >> 4) + j;
+    const int c = k / 9, kk = k - c * 9;
+    v[j] = (k < K && col < nout) ? wg[DG ? (c * nout + col) * 9 + kk : (col * nin + c) * 9 + kk] : 0.f;
+  }
+  return cnn_pack8(v);
+}
+template <int PP, bool DG>
+__device__ __forceinline__ int cnn_otab_entry(int k, int nin) {
+  const int c = k / 9, kk = k - c * 9, ky = kk / 3, kx = kk - ky * 3;
+  return k < nin * 9 ? (DG ? c * CPL(PP) + (2 - ky) * PP + (2 - kx) : c * CPL(PP) + ky * PP + kx) : -1;
+}
+
+// the per-tile loop of conv_mfma over built tables (otab: [ks * 32] plane offsets, -1 padding;
+// wtab: [ks][64] B fragments; bg: the bias (forward))
 template <int H, int PP, bool DG, bool RELU>
-__device__ __forceinline__ void conv_mfma(const float* __restrict__ in, int nin, float* __restrict__ out, int nout,
-                                          const float* __restrict__ wg, const float* __restrict__ bg,
-                                          float* __restrict__ tab) {
+__device__ __forceinline__ void conv_mfma_tiles(const float* __restrict__ in, float* __restrict__ out, int nout,
+                                                const int* __restrict__ otab, const bf16x8_t* __restrict__ wtab, int ks,
+                                                const float* __restrict__ bg) {
   constexpr int NT = (H * H + 15) / 16;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int K = nin * 9, ks = (K + 31) / 32;
-  int* otab = (int*)tab;                          // [ks * 32] plane offsets (-1: padding k)
-  bf16x8_t* wtab = (bf16x8_t*)(tab + 256);        // [ks][64 lanes] B fragments
-  for (int k = threadIdx.x; k < ks * 32; k += blockDim.x) {
-    const int c = k / 9, kk = k - c * 9, ky = kk / 3, kx = kk - ky * 3;
-    otab[k] = k < K ? (DG ? c * CPL(PP) + (2 - ky) * PP + (2 - kx) : c * CPL(PP) + ky * PP + kx) : -1;
-  }
-  for (int e = threadIdx.x; e < ks * 64; e += blockDim.x) {
-    const int s = e >> 6, l = e & 63, col = l & 15;
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 32 * s + 8 * (l >> 4) + j;
-      const int c = k / 9, kk = k - c * 9;
-      v[j] = (k < K && col < nout) ? wg[DG ? (c * nout + col) * 9 + kk : (col * nin + c) * 9 + kk] : 0.f;
-    }
-    wtab[e] = cnn_pack8(v);
-  }
-  __syncthreads();
   const int col = lane & 15, kq = lane >> 4;
   const float bias = (!DG && col < nout) ? bg[col] : 0.f;
   for (int t = wv; t < NT; t += nw) {
@@ -430,6 +435,23 @@ __device__ __forceinline__ void conv_mfma(const float* __restrict__ in, int nin,
   }
 }
 
+// DG = false: forward (+bias, ReLU) into `out`; DG = true: transposed conv into `out` in place of
+// the forward activation, times relu'(out) when RELU (dz of the layer below), plain otherwise.
+// `tab` (LDS scratch): the layer's k -> plane-offset table and the bf16 B fragments of every
+// k-step, built once per call so the per-tile loop keeps almost nothing in registers (the
+// kernel runs 16 waves: 128 VGPRs per lane).
+template <int H, int PP, bool DG, bool RELU>
+__device__ __forceinline__ void conv_mfma(const float* __restrict__ in, int nin, float* __restrict__ out, int nout,
+                                          const float* __restrict__ wg, const float* __restrict__ bg,
+                                          float* __restrict__ tab) {
+  const int ks = (nin * 9 + 31) / 32;
+  int* otab = (int*)tab;                          // [ks * 32] plane offsets (-1: padding k)
+  bf16x8_t* wtab = (bf16x8_t*)(tab + 256);        // [ks][64 lanes] B fragments
+  for (int k = threadIdx.x; k < ks * 32; k += blockDim.x) otab[k] = cnn_otab_entry<PP, DG>(k, nin);
+  for (int e = threadIdx.x; e < ks * 64; e += blockDim.x) wtab[e] = cnn_wtab_entry<DG>(e, wg, nin, nout);
+  __syncthreads();
+  conv_mfma_tiles<H, PP, DG, RELU>(in, out, nout, otab, wtab, ks, bg);
+}
 
 // ---- 28 x 28 MFMA convolutions from a channels-last bf16 copy (the exact C = 10 instance) ----
 // conv_mfma gathers each lane's 8 consecutive k of one position from the fp32 planes: 8 scalar LDS
@@ -455,28 +477,25 @@ __device__ __forceinline__ void cnn_to_hwc(const float* __restrict__ in, int nin
   }
 }
 
-// conv_mfma's contract (DG / RELU / out / epilogue) with the input `in` given as fp32 planes and
-// copied to the channels-last bf16 rows `hw` first (nin, nout <= 16)
+// channels-last B fragments: forward W[col][c][tap]; dgrad (A offset (dy, dx) = (1 - ky, 1 - kx))
+// W[c][col][8 - tap]
+template <bool DG>
+__device__ __forceinline__ bf16x8_t cnn_wtab_hwc_entry(int e, const float* __restrict__ wg, int nin, int nout) {
+  const int s = e >> 6, l = e & 63, col = l & 15;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 32 * s + 8 * (l >> 4) + j, tap = k >> 4, c = k & 15;
+    v[j] = (tap < 9 && c < nin && col < nout) ? wg[DG ? (c * nout + col) * 9 + (8 - tap) : (col * nin + c) * 9 + tap] : 0.f;
+  }
+  return cnn_pack8(v);
+}
+
 template <int H, int PP, bool DG, bool RELU>
-__device__ __forceinline__ void conv_mfma_hwc(const float* __restrict__ in, int nin, uint4* __restrict__ hw,
-                                              float* __restrict__ out, int nout, const float* __restrict__ wg,
-                                              const float* __restrict__ bg, float* __restrict__ tab) {
+__device__ __forceinline__ void conv_hwc_tiles(const uint4* __restrict__ hw, float* __restrict__ out, int nout,
+                                               const bf16x8_t* __restrict__ wtab, const float* __restrict__ bg) {
   constexpr int NT = (H * H + 15) / 16;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  cnn_to_hwc<PP>(in, nin, hw);
-  bf16x8_t* wtab = (bf16x8_t*)tab;  // [HWC_KS][64 lanes] B fragments: B[k = tap * 16 + c][col]
-  for (int e = threadIdx.x; e < HWC_KS * 64; e += blockDim.x) {
-    const int s = e >> 6, l = e & 63, col = l & 15;
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 32 * s + 8 * (l >> 4) + j, tap = k >> 4, c = k & 15;
-      // forward: W[col][c][tap]; dgrad (A offset (dy, dx) = (1 - ky, 1 - kx)): W[c][col][8 - tap]
-      v[j] = (tap < 9 && c < nin && col < nout) ? wg[DG ? (c * nout + col) * 9 + (8 - tap) : (col * nin + c) * 9 + tap] : 0.f;
-    }
-    wtab[e] = cnn_pack8(v);
-  }
-  __syncthreads();
   const int col = lane & 15, half = (lane >> 4) & 1, tsel = lane >> 5;  // k = 32 s + 8 (lane >> 4) + j
   const float bias = (!DG && col < nout) ? bg[col] : 0.f;
   const bf16x8_t* hb = (const bf16x8_t*)hw;
@@ -503,6 +522,72 @@ __device__ __forceinline__ void conv_mfma_hwc(const float* __restrict__ in, int 
         }
       }
     }
+  }
+}
+
+// conv_mfma's contract (DG / RELU / out / epilogue) with the input `in` given as fp32 planes and
+// copied to the channels-last bf16 rows `hw` first (nin, nout <= 16); wtab: prebuilt fragments
+// (cnn_pretab) or null (built here in `tab`)
+template <int H, int PP, bool DG, bool RELU>
+__device__ __forceinline__ void conv_mfma_hwc(const float* __restrict__ in, int nin, uint4* __restrict__ hw,
+                                              float* __restrict__ out, int nout, const float* __restrict__ wg,
+                                              const float* __restrict__ bg, float* __restrict__ tab,
+                                              const bf16x8_t* __restrict__ wtab_pre = nullptr) {
+  cnn_to_hwc<PP>(in, nin, hw);
+  const bf16x8_t* wtab = wtab_pre;
+  if (!wtab_pre) {
+    bf16x8_t* wt = (bf16x8_t*)tab;
+    for (int e = threadIdx.x; e < HWC_KS * 64; e += blockDim.x) wt[e] = cnn_wtab_hwc_entry<DG>(e, wg, nin, nout);
+    wtab = wt;
+  }
+  __syncthreads();
+  conv_hwc_tiles<H, PP, DG, RELU>(hw, out, nout, wtab, bg);
+}
+
+// ---- the exact bf16 instance's fragment tables, built once per launch (cnn_pretab) ----
+// Every MFMA conv of the image then skips its table build (per call: ~1k clocks of weight reads,
+// packing and a barrier); the weights are read from global memory once, while the workgroup
+// clears its LDS.  Layout (16-B granules): conv2 forward / dgrad channels-last [HWC_KS][64] each,
+// conv3 / conv4 forward / dgrad [3][64] each, the 14 x 14 forward / dgrad offset tables [96] ints
+// each, the four conv biases [4][16].
+struct CnnTabs {
+  bf16x8_t *t2f, *t2d, *t3f, *t3d, *t4f, *t4d;
+  int *o14f, *o14d;
+  float* bias;
+};
+#define CNN_PRETAB_FLOATS (4 * (2 * HWC_KS * 64 + 4 * 3 * 64) + 2 * 96 + 64 + 4)
+__device__ __forceinline__ CnnTabs cnn_tabs(float* at) {
+  CnnTabs t;
+  bf16x8_t* b = (bf16x8_t*)(((uintptr_t)at + 15) & ~(uintptr_t)15);
+  t.t2f = b; t.t2d = b + HWC_KS * 64;
+  t.t3f = t.t2d + HWC_KS * 64; t.t3d = t.t3f + 3 * 64; t.t4f = t.t3d + 3 * 64; t.t4d = t.t4f + 3 * 64;
+  t.o14f = (int*)(t.t4d + 3 * 64); t.o14d = t.o14f + 96;
+  t.bias = (float*)(t.o14d + 96);
+  return t;
+}
+// C = nin = nout = 10 (three 32-deep k-steps of 90 channel-major k)
+__device__ __forceinline__ void cnn_pretab(const CNNArgs& g, const CnnTabs& t, int C) {
+  constexpr int NH = HWC_KS * 64, NO = 3 * 64;
+  for (int e = threadIdx.x; e < 2 * NH + 4 * NO + 2 * 96 + 64; e += blockDim.x) {
+    int r = e;
+    if (r < NH) { t.t2f[r] = cnn_wtab_hwc_entry<false>(r, g.w[1], C, C); continue; }
+    r -= NH;
+    if (r < NH) { t.t2d[r] = cnn_wtab_hwc_entry<true>(r, g.w[1], C, C); continue; }
+    r -= NH;
+    if (r < NO) { t.t3f[r] = cnn_wtab_entry<false>(r, g.w[2], C, C); continue; }
+    r -= NO;
+    if (r < NO) { t.t3d[r] = cnn_wtab_entry<true>(r, g.w[2], C, C); continue; }
+    r -= NO;
+    if (r < NO) { t.t4f[r] = cnn_wtab_entry<false>(r, g.w[3], C, C); continue; }
+    r -= NO;
+    if (r < NO) { t.t4d[r] = cnn_wtab_entry<true>(r, g.w[3], C, C); continue; }
+    r -= NO;
+    if (r < 96) { t.o14f[r] = cnn_otab_entry<P14, false>(r, C); continue; }
+    r -= 96;
+    if (r < 96) { t.o14d[r] = cnn_otab_entry<P14, true>(r, C); continue; }
+    r -= 96;
+    const int l = r >> 4, c = r & 15;
+    t.bias[r] = c < C ? g.b[l][c] : 0.f;
   }
 }
 
@@ -1017,13 +1102,17 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
   // layer fragment tables read them element-wise (the fp32 convs keep global weights: they read
   // them through the constant address space as scalar loads)
   float* wst = wscr + WG_SCRATCH + 2;
+  // the exact bf16 instance: every MFMA conv's fragment tables built once here instead (cnn_pretab)
+  constexpr bool PRE = BF && EX;
+  const CnnTabs tabs = cnn_tabs(wst);
+  if (PRE) cnn_pretab(g, tabs, C);
   const float* lw[4] = {};
   const float* lb[4] = {};
   {
     int o = 0;
     for (int l = 0; l < 4; ++l) {
       const int n = C * (l == 0 ? CI : C) * 9;
-      if (BF && g.wstage) {
+      if (BF && !PRE && g.wstage) {
         for (int i = threadIdx.x; i < n; i += blockDim.x) wst[o + i] = g.w[l][i];
         for (int i = threadIdx.x; i < C; i += blockDim.x) wst[o + n + i] = g.b[l][i];
         lw[l] = wst + o;
@@ -1067,7 +1156,7 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
   }
   CNN_PIN(lab0);  // arrived during conv1
   if (BF && EX) {
-    conv_mfma_hwc<28, P28, false, false>(a1, C, (uint4*)p1, a2, C, lw[1], lb[1], wscr);
+    conv_mfma_hwc<28, P28, false, false>(a1, C, (uint4*)p1, a2, C, nullptr, tabs.bias + 16, wscr, tabs.t2f);
     __syncthreads();
     // the copy overlaid the 14 x 14 planes: their zero halos again
     for (int i = threadIdx.x; i < 3 * C * PL14 / 4; i += blockDim.x) reinterpret_cast<float4*>(p1)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1085,7 +1174,8 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
     cnn_helper_finish<14, P14, BF>(g, img, 1, C, a3, p1, wacc, wscr);
     return true;
   }
-  if (BF) conv_mfma<14, P14, false, false>(p1, C, a3, C, lw[2], lb[2], wscr);
+  if (PRE) conv_mfma_tiles<14, P14, false, false>(p1, a3, C, tabs.o14f, tabs.t3f, 3, tabs.bias + 32);
+  else if (BF) conv_mfma<14, P14, false, false>(p1, C, a3, C, lw[2], lb[2], wscr);
   else conv_fwd<14, P14, CC, EX>(p1, C, a3, C, g.w[2], g.b[2]);
   __syncthreads();
   STAMP(5);
@@ -1093,7 +1183,8 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
     cnn_helper_finish<14, P14, BF>(g, img, 0, C, a4, a3, wacc, wscr);
     return true;
   }
-  if (BF) conv_mfma<14, P14, false, false>(a3, C, a4, C, lw[3], lb[3], wscr);
+  if (PRE) conv_mfma_tiles<14, P14, false, false>(a3, a4, C, tabs.o14f, tabs.t4f, 3, tabs.bias + 48);
+  else if (BF) conv_mfma<14, P14, false, false>(a3, C, a4, C, lw[3], lb[3], wscr);
   else conv_fwd<14, P14, CC, EX>(a3, C, a4, C, g.w[3], g.b[3]);
   __syncthreads();
   STAMP(6);
@@ -1212,14 +1303,16 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
     // barrier after the next dgrad, conv2's (the largest weight gradient) at once
     const __amdgpu_buffer_rsrc_t rh = smi_rsrc(g.hand + (long)img * cnn_hand_f(C), cnn_hand_f(C) * 4);
     cnn_hand_put(rh, cnn_hand_dz(C, 0), a4, C * PL14);  // dz4
-    if (BF) conv_mfma<14, P14, true, true>(a4, C, a3, C, lw[3], nullptr, wscr);
+    if (PRE) conv_mfma_tiles<14, P14, true, true>(a4, a3, C, tabs.o14d, tabs.t4d, 3, nullptr);
+    else if (BF) conv_mfma<14, P14, true, true>(a4, C, a3, C, lw[3], nullptr, wscr);
     else conv_dgrad<14, P14, CC, EX>(a4, C, g.w[3], C, a3, true);
     smi_wt_drain();
     __syncthreads();
     cnn_hand_publish(g, img, 0);
     STAMP(14);
     cnn_hand_put(rh, cnn_hand_dz(C, 1), a3, C * PL14);  // dz3
-    if (BF) conv_mfma<14, P14, true, false>(a3, C, p1, C, lw[2], nullptr, wscr);
+    if (PRE) conv_mfma_tiles<14, P14, true, false>(a3, p1, C, tabs.o14d, tabs.t3d, 3, nullptr);
+    else if (BF) conv_mfma<14, P14, true, false>(a3, C, p1, C, lw[2], nullptr, wscr);
     else conv_dgrad<14, P14, CC, EX>(a3, C, g.w[2], C, p1, false);
     smi_wt_drain();
     __syncthreads();
@@ -1234,7 +1327,7 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
     cnn_hand_publish(g, img, 2);
     STAMP(18);
     RSTAMP(1);
-    if (BF && EX) conv_mfma_hwc<28, P28, true, true>(a2, C, (uint4*)p1, a1, C, lw[1], nullptr, wscr);
+    if (BF && EX) conv_mfma_hwc<28, P28, true, true>(a2, C, (uint4*)p1, a1, C, nullptr, nullptr, wscr, tabs.t2d);
     else if (BF) conv_mfma<28, P28, true, true>(a2, C, a1, C, lw[1], nullptr, wscr);
     else conv_dgrad<28, P28, CC, EX>(a2, C, g.w[1], C, a1, true);
     __syncthreads();
@@ -1256,7 +1349,8 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
     smi_wt_store(gs + (e < C * C * 9 ? g.off[6] + e : g.off[7] + e - C * C * 9), wacc[e]);
     wacc[e] = 0.f;
   }
-  if (BF) conv_mfma<14, P14, true, true>(a4, C, a3, C, lw[3], nullptr, wscr);
+  if (PRE) conv_mfma_tiles<14, P14, true, true>(a4, a3, C, tabs.o14d, tabs.t4d, 3, nullptr);
+  else if (BF) conv_mfma<14, P14, true, true>(a4, C, a3, C, lw[3], nullptr, wscr);
   else conv_dgrad<14, P14, CC, EX>(a4, C, g.w[3], C, a3, true);
   __syncthreads();
   STAMP(14);
@@ -1269,7 +1363,8 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
     smi_wt_store(gs + (e < C * C * 9 ? g.off[4] + e : g.off[5] + e - C * C * 9), wacc[e]);
     wacc[e] = 0.f;
   }
-  if (BF) conv_mfma<14, P14, true, false>(a3, C, p1, C, lw[2], nullptr, wscr);
+  if (PRE) conv_mfma_tiles<14, P14, true, false>(a3, p1, C, tabs.o14d, tabs.t3d, 3, nullptr);
+  else if (BF) conv_mfma<14, P14, true, false>(a3, C, p1, C, lw[2], nullptr, wscr);
   else conv_dgrad<14, P14, CC, EX>(a3, C, g.w[2], C, p1, false);
   __syncthreads();
   STAMP(16);
@@ -1286,7 +1381,7 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
     smi_wt_store(gs + (e < C * C * 9 ? g.off[2] + e : g.off[3] + e - C * C * 9), wacc[e]);
     wacc[e] = 0.f;
   }
-  if (BF && EX) conv_mfma_hwc<28, P28, true, true>(a2, C, (uint4*)p1, a1, C, lw[1], nullptr, wscr);
+  if (BF && EX) conv_mfma_hwc<28, P28, true, true>(a2, C, (uint4*)p1, a1, C, nullptr, nullptr, wscr, tabs.t2d);
   else if (BF) conv_mfma<28, P28, true, true>(a2, C, a1, C, lw[1], nullptr, wscr);
   else conv_dgrad<28, P28, CC, EX>(a2, C, g.w[1], C, a1, true);
   __syncthreads();
@@ -1355,8 +1450,10 @@ static size_t cnn_lds_bytes(const CNNArgs& g) {
   // + conv_wgrad scratch (WG_SCRATCH floats)
   const int WC = C > CI ? C : CI;  // wgrad accumulators hold [C][max(C, CI)*9] + C
   // + the staged conv weights and biases (C * CI * 9 + 3 * C * C * 9 + 4 * C) when wstage
+  // + the launch-wide fragment tables instead (wstage 2: the exact C = 10 bf16 instance)
   return sizeof(float) * (size_t)(CI * PL28 + 2 * C * PL28 + 3 * C * PL14 + C * 49 + 16 + WC * C * 9 + C + 4 +
-                                  WG_SCRATCH + 2 + (g.wstage ? C * CI * 9 + 3 * C * C * 9 + 4 * C : 0));
+                                  WG_SCRATCH + 2 +
+                                  (g.wstage == 2 ? CNN_PRETAB_FLOATS : g.wstage ? C * CI * 9 + 3 * C * C * 9 + 4 * C : 0));
 }
 
 // the fused tail's LDS: every image's staged dl / p2 row, then the conv chunk partials (at most 8
@@ -1379,8 +1476,8 @@ extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
       if (g.shadow[i]) return -1;
   }
   if (g.C < 1 || g.C > CNN_MAXC || g.cin < 1 || g.cin > 4 || g.classes < 1 || g.classes > 16) return -1;
-  g.wstage = g.bf16 ? 1 : 0;
-  if (g.wstage && cnn_lds_bytes(g) > 160 * 1024) g.wstage = 0;  // the weights then stay global
+  g.wstage = g.bf16 ? (g.C == 10 ? 2 : 1) : 0;
+  if (g.wstage == 1 && cnn_lds_bytes(g) > 160 * 1024) g.wstage = 0;  // the weights then stay global
   const size_t lds = cnn_lds_bytes(g);
   if (lds > 160 * 1024) return -1;
   if (g.fused && cnn_tail_lds(g.C, g.cin, g.classes, g.B) > lds) return -1;
