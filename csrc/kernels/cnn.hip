@@ -1200,6 +1200,14 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
 #pragma unroll
     for (int k = 0; k < FK; ++k) fcw[k] = wr[min(lane + 64 * k, F - 1)];
   }
+  // the fc backward's weight columns (thread i < F holds W[o][i] of every class; F <= 784 < the
+  // 1024 threads), loaded now too: their round trip overlaps pool2, the classifier and the CE
+  float wc[16];
+  if (g.train && wv * 64 < F) {
+    const int i = min((int)threadIdx.x, F - 1);
+#pragma unroll
+    for (int o = 0; o < 16; ++o) wc[o] = g.w[4][min(o, NC - 1) * F + i];
+  }
   pool_fwd<14, P14, 7, 0>(a4, p2, C);
   smi_lds_barrier();
   STAMP(7);
@@ -1213,14 +1221,6 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
   }
   __syncthreads();
   STAMP(8);
-  // the fc backward's weight columns (thread i < F holds W[o][i] of every class; F <= 784 < the
-  // 1024 threads), loaded now: their round trip overlaps the cross-entropy
-  float wc[16];
-  if (g.train && wv * 64 < F) {
-    const int i = min((int)threadIdx.x, F - 1);
-#pragma unroll
-    for (int o = 0; o < 16; ++o) wc[o] = g.w[4][min(o, NC - 1) * F + i];
-  }
   // cross-entropy on wave 0, lane o = class o (NC <= 16): max, log-sum-exp and the logit gradient
   // as DPP wave reductions, the argmax from a ballot, the label's logit by readlane (one lane
   // walking the classes through dependent LDS reads took ~3k clocks, shuffles ~2.7k)
