@@ -1281,10 +1281,14 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
   if ((int)threadIdx.x < F) {
     const int i = threadIdx.x;
     const float pv = p2[i];
+    // all 16 logit-gradient slots read unconditionally, issued together (slots >= NC hold 0 from
+    // the LDS clear: their terms add +0, the sum is unchanged); a guarded loop waited per read
+    float l16[16];
+#pragma unroll
+    for (int o = 0; o < 16; ++o) l16[o] = lg[o];
     float s = 0.f;
 #pragma unroll
-    for (int o = 0; o < 16; ++o)
-      if (o < NC) s += wc[o] * lg[o];
+    for (int o = 0; o < 16; ++o) s += wc[o] * l16[o];
     p2[i] = s;  // dp2 (flat NCHW)
     smi_wt_store(gs + cnn_cs(g) + NC + i, pv);
   }
