@@ -63,7 +63,10 @@ __device__ unsigned long long cnn_rstamps[256 * 8];
 #define PL14 CPL(P14)
 // weight-gradient helper workgroups per image (CNNArgs::hand): conv4, conv3, conv2 (two halves of
 // its columns)
-#define CNN_HELPERS 4
+#ifndef CNN_HELPERS
+#define CNN_HELPERS 4  // >= 3: conv4, conv3, then conv2's column tiles split over the rest
+#endif
+static_assert(CNN_HELPERS >= 3, "conv4, conv3 and at least one conv2 helper");
 
 __device__ __forceinline__ int i28(int c, int y, int x) { return c * PL28 + (y + 1) * P28 + (x + 1); }
 __device__ __forceinline__ int i14(int c, int y, int x) { return c * PL14 + (y + 1) * P14 + (x + 1); }
@@ -1150,8 +1153,9 @@ __device__ __forceinline__ bool cnn_image(const CNNArgs& g, float* sm, const int
   else conv_fwd<28, P28, CC, EX>(xin, CI, a1, C, g.w[0], g.b[0]);
   __syncthreads();
   STAMP(2);
-  if (role >= 2) {  // conv2's two helpers (column tiles [0, 3) / [3, 6)): their input is a1
-    cnn_helper_finish<28, P28, BF>(g, img, 2, C, a2, a1, wacc, wscr, role == 2 ? 0 : 3, role == 2 ? 3 : 1 << 20);
+  if (role >= 2) {  // conv2's helpers (their share of its 16-column tiles): their input is a1
+    const int np = CNN_HELPERS - 2, j = role - 2, nt2 = (C * 9 + 1 + 15) / 16;
+    cnn_helper_finish<28, P28, BF>(g, img, 2, C, a2, a1, wacc, wscr, j * nt2 / np, j == np - 1 ? 1 << 20 : (j + 1) * nt2 / np);
     return true;
   }
   CNN_PIN(lab0);  // arrived during conv1

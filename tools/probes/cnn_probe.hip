@@ -110,7 +110,7 @@ int main(int argc, char** argv) {
     std::vector<unsigned long long> rt(256 * 8);
     (void)hipMemcpyFromSymbol(rt.data(), HIP_SYMBOL(cnn_rstamps), rt.size() * 8);
     unsigned long long t0 = ~0ull;
-    for (int w = 0; w < 5 * B; ++w) if (rt[w * 8] && rt[w * 8] < t0) t0 = rt[w * 8];
+    for (int w = 0; w < (1 + CNN_HELPERS) * B; ++w) if (rt[w * 8] && rt[w * 8] < t0) t0 = rt[w * 8];
     auto avg = [&](int w0, int w1, int step, int k) {
       double s = 0; int n = 0;
       for (int w = w0; w < w1; w += step) if (rt[w * 8 + k]) { s += (double)(rt[w * 8 + k] - t0) * 10.0 / 1000.0; ++n; }
@@ -118,24 +118,24 @@ int main(int argc, char** argv) {
     };
     printf("image wg (us from kernel start): start %.2f, conv2 handed over %.2f, body done %.2f\n", avg(0, B, 1, 0),
            avg(0, B, 1, 1), avg(0, B, 1, 4));
-    const char* hn[4] = {"conv4", "conv3", "conv2 a", "conv2 b"};
-    for (int j = 0; j < 4; ++j)
-      printf("helper %s: start %.2f, flag %.2f, loaded %.2f, wgrad %.2f, done %.2f\n", hn[j], avg(B + j, 5 * B, 4, 0),
-             avg(B + j, 5 * B, 4, 1), avg(B + j, 5 * B, 4, 2), avg(B + j, 5 * B, 4, 3), avg(B + j, 5 * B, 4, 4));
+    const int HW = CNN_HELPERS, NW = (1 + CNN_HELPERS) * B;
+    for (int j = 0; j < HW; ++j)
+      printf("helper %s %d: start %.2f, flag %.2f, loaded %.2f, wgrad %.2f, done %.2f\n", j == 0 ? "conv4" : j == 1 ? "conv3" : "conv2",
+             j, avg(B + j, NW, HW, 0), avg(B + j, NW, HW, 1), avg(B + j, NW, HW, 2), avg(B + j, NW, HW, 3), avg(B + j, NW, HW, 4));
     // tail stamps of THIS launch only (earlier launches' last workgroups left older values)
     auto cur = [&](unsigned long long v) { return v >= t0 && v < t0 + 100000ull; };
     unsigned long long tl = 0;  // the last workgroup to finish its image / helper work
-    for (int w = 0; w < 5 * B; ++w) if (cur(rt[w * 8 + 4]) && rt[w * 8 + 4] > tl) tl = rt[w * 8 + 4];
+    for (int w = 0; w < (1 + CNN_HELPERS) * B; ++w) if (cur(rt[w * 8 + 4]) && rt[w * 8 + 4] > tl) tl = rt[w * 8 + 4];
     printf("last workgroup done: %.2f us\n", (double)(tl - t0) * 0.01);
     for (int k = 5; k < 8; ++k) {
       const char* kn = k == 5 ? "slice ticket" : (k == 6 ? "slice start" : "slice done");
       printf("tail %s:", kn);
-      for (int w = 0; w < 5 * B; ++w)
+      for (int w = 0; w < (1 + CNN_HELPERS) * B; ++w)
         if (cur(rt[w * 8 + k])) printf(" %.2f", (double)(rt[w * 8 + k] - t0) * 0.01);
       printf(" us\n");
     }
     // the level-2 slices' phases (same-workgroup s_memtime differences)
-    for (int w = 0; w < 5 * B; ++w) {
+    for (int w = 0; w < (1 + CNN_HELPERS) * B; ++w) {
       if (!cur(rt[w * 8 + 6])) continue;
       const unsigned long long* q = &st[w * 32];
       printf("slice wg %3d: loads %lld, conv apply %lld, fc %lld, bias %lld ticks\n", w,
