@@ -777,8 +777,12 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, float* sm, int 
       pv[u] = *(const __attribute__((address_space(1))) float*)conv_seg(min(max(4 * q4 + u, 0), off8 - 1), seg, r);
     }
   };
-  float pcv[4];  // granule q4lo + threadIdx.x (the one-granule-per-thread case)
-  conv_pload(min(q4lo + (int)threadIdx.x, q4hi - 1), pcv);
+  // the conv update runs on the LAST threads (granule q = nt - 1 - threadIdx.x) and the fc update
+  // on the first ones: different waves, so the two run side by side instead of one after the
+  // other on wave 0
+  const int cq = nt - 1 - (int)threadIdx.x;
+  float pcv[4];  // granule q4lo + cq (the one-granule-per-thread case)
+  conv_pload(min(q4lo + cq, q4hi - 1), pcv);
   const float lr0 = gmode ? -1.f : g.lr[0];  // (a load after the wait: one more round trip)
   // wait until every workgroup is done
   if (threadIdx.x == 0) {
@@ -900,7 +904,7 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, float* sm, int 
     }
   };
   if (nq <= nt) {
-    if ((int)threadIdx.x < nq) conv_apply(threadIdx.x, pcv);
+    if (cq < nq) conv_apply(cq, pcv);
   } else {
     for (int q = threadIdx.x; q < nq; q += nt) {
       float pv[4];
