@@ -769,7 +769,8 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, float* sm, int 
   float pfc[16];  // the thread's first column
   fc_load(i0, pfc);
   float* fb = dst_of(9);
-  const float pb = fb[min((int)threadIdx.x, NC - 1)];
+  const int bo = (int)threadIdx.x - (nt - 128);  // fc bias entry of this thread (wave nt / 64 - 2)
+  const float pb = fb[min(max(bo, 0), NC - 1)];
   auto conv_pload = [&](int q4, float* pv) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -957,9 +958,15 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, float* sm, int 
         gw[4 * t4 + 3] += d.w * x;
       }
     }
-    for (int m = 1; m < kst; m <<= 1)  // the slot's kst lanes (aligned, all active): a + b == b + a
+    // the slot's kst (1, 2, 4 or 8) aligned lanes, all active: a DPP butterfly over lane ^ 7 (half-row
+    // mirror), ^ 2, ^ 1 (quad perms) — VALU exchanges, not LDS permutes; a + b == b + a, so every
+    // lane of the slot holds the same sum
 #pragma unroll
-      for (int t = 0; t < 4 * NO4; ++t) gw[t] += __shfl_xor(gw[t], m, 64);
+    for (int t = 0; t < 4 * NO4; ++t) {
+      if (kst >= 8) gw[t] += smi_dpp<SMI_DPP_HMIRROR>(gw[t]);
+      if (kst >= 4) gw[t] += smi_dpp<SMI_DPP_QP2301>(gw[t]);
+      if (kst >= 2) gw[t] += smi_dpp<SMI_DPP_QP1032>(gw[t]);
+    }
     float np[4 * NO4];
 #pragma unroll
     for (int t = 0; t < 4 * NO4; ++t) {
@@ -989,8 +996,8 @@ __device__ __forceinline__ void cnn_fused_tail(const CNNArgs& g, float* sm, int 
     }
   }
   STAMP(23);
-  if (slice == 0 && (int)threadIdx.x < NC) {
-    const int o = threadIdx.x;
+  if (slice == 0 && bo >= 0 && bo < NC) {  // the fc bias on the second-to-last wave (beside the rest)
+    const int o = bo;
     float gb = 0.f;
 #pragma unroll 8
     for (int im = 0; im < g.B; ++im) gb += sm[im * R4 + o];
