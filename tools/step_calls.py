@@ -13,6 +13,7 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--marker", default="adam_kernel")
     ap.add_argument("--step", type=int, default=-1, help="which step (python index over the marker-delimited steps)")
+    ap.add_argument("--abs", action="store_true", help="print start / end (us from the step's first kernel) instead")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     cols = [r[1] for r in c.execute("pragma table_info(kernels)").fetchall()]
@@ -23,12 +24,16 @@ def main():
     steps = list(zip(marks[:-1], marks[1:]))
     lo, hi = steps[a.step]
     tot = 0.0
+    t0 = rows[lo + 1][1]
     for r in rows[lo + 1:hi + 1]:
         name = re.sub(r"\(.*", "", re.sub(r"^void ", "", r[0]))[:60]
         us = (r[2] - r[1]) / 1e3
         tot += us
         dims = " ".join(str(v) for v in r[3:])
-        print(f"{us:9.1f} {tot:10.1f}  {name:60s} {dims}")
+        if a.abs:
+            print(f"{(r[1] - t0) / 1e3:9.1f} {(r[2] - t0) / 1e3:9.1f} {us:8.1f}  {name:60s} {dims}")
+        else:
+            print(f"{us:9.1f} {tot:10.1f}  {name:60s} {dims}")
 
 
 if __name__ == "__main__":
