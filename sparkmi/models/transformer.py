@@ -79,6 +79,11 @@ class PositionalEncoding(nn.Module):
         return self.table
 
 
+# The encoder's token embedding launches the queued grouped weight gradients at the start of its
+# backward (sparkmi/ops/embedding.py), so the encoder's group runs beside the embedding sum.
+ENC_EMB_FLUSH = True
+
+
 class SentenceEmbedding(nn.Module):
     def __init__(self, max_sequence_length, d_model, vocab_size, rng, p=0.1, dtype="bf16"):
         super().__init__()
@@ -90,13 +95,14 @@ class SentenceEmbedding(nn.Module):
         self.dropout = nn.Dropout(p=p)
         _share(self, "_rng", rng)
         self.salt = new_salt()
+        self.flush_wgrad = False  # the Encoder's: its backward ends the backward pass
 
     def forward(self, x):
         p = self.dropout.p if self.training else 0.0
         # the embedding's output dtype sets the dtype of every downstream fused op
         dtype = torch.bfloat16 if (x.is_cuda and self.act_dtype == "bf16") else torch.float32
         return embedding(x, self.embedding.weight, self.position_encoder.table, p, self._rng, self.salt,
-                         out_dtype=dtype)
+                         out_dtype=dtype, flush_wgrad=self.flush_wgrad)
 
 
 def _gp(t):
@@ -215,6 +221,7 @@ class Encoder(nn.Module):
                  emb_dropout=0.1, dtype="bf16"):
         super().__init__()
         self.sentence_embedding = SentenceEmbedding(max_sequence_length, d_model, vocab_size, rng, emb_dropout, dtype)
+        self.sentence_embedding.flush_wgrad = ENC_EMB_FLUSH
         self.layers = SequentialEncoder(*[EncoderLayer(d_model, ffn_hidden, num_heads, drop_prob, rng)
                                           for _ in range(num_layers)])
 

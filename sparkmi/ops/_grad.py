@@ -436,20 +436,27 @@ def flush_deferred():
     """Launch every queued weight-gradient GEMM / fold, then report the parameters final.
     The queues are emptied first (try/finally): a launch that raises leaves no stale entries."""
     from .. import _native
-    for e in _join_async():  # overlapped groups: joined into the main stream, now final
-        grad_ready(*e[4])
     gq, lq, fq = list(_group_queue), list(_ln_queue), list(_fold_queue)
     _group_queue.clear()
     _group_bytes.clear()
     _ln_queue.clear()
     _fold_queue.clear()
     _cb[0] = False
-    if not (gq or lq or fq):
-        return
-    C = _native.C()
-    _flush_groups(C, gq)
-    _flush_ln(C, lq)
-    _flush_folds(C, fq)
+    # launched before the join when no output is one an overlapped group (still running on the
+    # side stream) writes: they then run beside it
+    side_out = {t.data_ptr() for e in _async["hold"] for t in (e[2], e[3]) if t is not None}
+    early = not side_out.intersection(t.data_ptr() for e in gq + lq + fq for t in (e[2], e[3], e[4], e[5])
+                                      if isinstance(t, torch.Tensor))
+    held = [] if early else _join_async()
+    if gq or lq or fq:
+        C = _native.C()
+        _flush_groups(C, gq)
+        _flush_ln(C, lq)
+        _flush_folds(C, fq)
+    if early:
+        held = _join_async()
+    for e in held:  # overlapped groups: joined into the main stream, now final
+        grad_ready(*e[4])
     for e in lq:
         grad_ready(*e[6])
     for e in fq:

@@ -83,12 +83,13 @@ def plan_backward(ids, T, pad_idx, weight):
 
 class EmbeddingFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, ids, weight, pe, p, rng, salt, padding_idx, out_dtype, plan=False):
+    def forward(ctx, ids, weight, pe, p, rng, salt, padding_idx, out_dtype, plan=False, flush_wgrad=False):
         B = ids.shape
         D = weight.shape[1]
         T = ids.numel()
         S = ids.shape[-1]
         ctx.p, ctx.rng, ctx.salt, ctx.pad = p, rng, salt, -1 if padding_idx is None else padding_idx
+        ctx.flush_wgrad = flush_wgrad
         ctx.native = _native.use_native(ids)
         ids_c = ids.contiguous().to(torch.int64)
         if ctx.native:
@@ -133,6 +134,12 @@ class EmbeddingFn(torch.autograd.Function):
         gw = grad_buf(weight)
         if ctx.native:
             C = _native.C()
+            if ctx.flush_wgrad:
+                # the last op of the backward (the encoder's embedding): every weight gradient
+                # queued so far is final, so the grouped launch starts now on the side stream and
+                # runs beside this sum instead of after it
+                from . import _grad as _g
+                _g.flush_groups_async(dout.device)
             dout = dout.contiguous()
             V = weight.shape[0]
             # deterministic backward (bit-reproducible, no float atomics): the ordering ran beside
@@ -159,11 +166,15 @@ class EmbeddingFn(torch.autograd.Function):
                 g, idf = g[keep], idf[keep]
             gw.index_add_(0, idf, g)
         grad_ready(weight)
-        return None, None, None, None, None, None, None, None, None
+        return None, None, None, None, None, None, None, None, None, None
 
 
-def embedding(ids, weight, pe=None, p=0.0, rng=None, salt=0, padding_idx=None, out_dtype=torch.float32):
+def embedding(ids, weight, pe=None, p=0.0, rng=None, salt=0, padding_idx=None, out_dtype=torch.float32,
+              flush_wgrad=False):
+    """``flush_wgrad``: this embedding's backward is the last op of the backward pass (the
+    encoder's token embedding): it launches the queued grouped weight gradients first."""
     if rng is None:
         from .layernorm import _NULL_RNG
         rng, p = _NULL_RNG, 0.0
-    return EmbeddingFn.apply(ids, weight, pe, float(p), rng, int(salt), padding_idx, out_dtype, torch.is_grad_enabled())
+    return EmbeddingFn.apply(ids, weight, pe, float(p), rng, int(salt), padding_idx, out_dtype, torch.is_grad_enabled(),
+                             bool(flush_wgrad))
