@@ -375,7 +375,7 @@ PYBIND11_MODULE(_C, m) {
   }, "s fused SGD steps of the 4-5-4-3 MLP in one launch; False when the shapes are not covered");
   m.def("mlp_grid", [](int n) { return smi_mlp_grid(n); });
   m.def("gemm_bf256", [](int set) { return smi_gemm_bf256_enable(set); },
-        "bf16 GEMMs that fill the chip on the 256x128 8-wave 16x16x32 tile (1, default) or always the 128x128 kernel (0); -1 queries");
+        "bf16 GEMMs that fill the chip on the 256x128 8-wave 16x16x32 tile (1; measured slower in the step) or always the persistent 128x128 kernel (0, default); -1 queries");
   m.def("mlp_small", [](int set) { return smi_mlp_small(set); },
         "MLP kernel: 1 = the compile-time 4-5-4-3 kernel for batches <= 64 (default), 0 = the generic one; -1 queries");
 

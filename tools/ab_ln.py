@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """The fp32 LayerNorm forward at the transformer's shape (8192 x 512, residual, dropout 0.1, split
 planes out: 88 MB) against a plain torch copy of the same byte count, interleaved rounds — is the
-kernel at HBM speed?  (Round 5: 16.4 us vs 16.2 us for the copy, profiles/r5_ab_ln_rows.txt.)
+kernel at HBM speed?  (Round 5: 16.4 us vs 16.2 us for the copy, profiles/r5_ab_ln_rows.txt.)  Also
+times the backward (fp32: dres + dh planes, bf16: dres + dh).
 Usage (GPU box): python tools/ab_ln.py"""
 import argparse
 import os
@@ -49,6 +50,27 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) * 1e3 / a.iters
 
+    # backward, fp32 (planes-only dh) and bf16
+    dy = torch.randn(M, D, generator=g).to(dev)
+    dres = torch.empty_like(dy)
+    part = torch.empty(2, M // 4, D, device=dev)
+    dhp = torch.empty(3, M, D, device=dev, dtype=torch.bfloat16)
+    dyb, xsb = dy.bfloat16(), xs.bfloat16()
+    dresb, dhb = torch.empty_like(dyb), torch.empty_like(dyb)
+
+    def bwd32():
+        C.ln_bwd_f32(dy.data_ptr(), xs.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gam.data_ptr(), dres.data_ptr(),
+                     0, 0, part[0].data_ptr(), part[1].data_ptr(), M // 4, 0, 0, 1, M, D, seed.data_ptr(), 7,
+                     R.threshold(0.1), R.scale(0.1), dhp.data_ptr(), dhp.stride(0), st)
+
+    def bwd16():
+        C.ln_bwd(dyb.data_ptr(), xsb.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gam.data_ptr(), dresb.data_ptr(),
+                 dhb.data_ptr(), 0, part[0].data_ptr(), part[1].data_ptr(), M // 4, 0, 0, 1, M, D, seed.data_ptr(), 7,
+                 R.threshold(0.1), R.scale(0.1), st)
+
+    for rd in range(a.rounds):
+        print(f"round {rd}: ln_bwd fp32 (dres + dh planes) {timeit(bwd32):6.2f} us | bf16 {timeit(bwd16):6.2f} us",
+              flush=True)
     src = torch.empty(32 * (1 << 20) // 4, device=dev)
     dst = torch.empty(56 * (1 << 20) // 4, device=dev)
     nbytes = M * D * 4 * 2 + M * D * 4 * 2 + M * D * 2 * 3
