@@ -86,6 +86,7 @@ int smi_gemm_sp_waves(int);
 int smi_gemm_sp_tm(int);
 int smi_gemm_sp_wg_tm(int);
 int smi_attn_ae(int);
+int smi_attn_bwd1(int);
 int smi_adam_wide(int);
 int smi_splitk_reduce(const float*, int, long, float*, long, float*, int, hipStream_t);
 int smi_splitk_fold_multi(const float* const*, float* const*, float* const*, const long*, const int*, const int*, int,
@@ -607,6 +608,9 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("attn_ae", [](int set) { return smi_attn_ae(set); },
         "fp32 attention outputs (forward and backward): 1 = whole-row stores through LDS (default), 0 = per-lane stores; -1 queries");
+  m.def("attn_bwd1", [](int set) { return smi_attn_bwd1(set); },
+        "attention backward at Sk <= 256 (fp32 and bf16): 1 = one single-pass kernel (default), 0 = the dQ + "
+        "dK/dV pair; -1 queries");
   m.def("emb_pair_max", [](long set) { return smi_emb_pair_max(set); },
         "largest token batch the pair-compare embedding backward takes (set < 0 queries)");
   m.def("emb_plan_algo", [](long T, long V) { return smi_emb_plan_algo(T, V); },

@@ -525,19 +525,236 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   }
 }
 
-#define SMI_ATTN_DISPATCH(KERNEL, GRID, ARGS)                                                               \
+// Single-pass backward (Sk <= 256, the default there): one 8-wave workgroup owns every key of its
+// (batch, head) — wave w keys 32 w .. + 31, K / V in registers as in the dK/dV kernel — and streams
+// 64-query chunks of Q / dO once.  Per chunk: S, dP, P, dS (keys on the lane), dV^T += dO^T P and
+// dK^T += Q^T dS; every wave also writes its bf16 dS tile into a [256 keys][64 queries] LDS image
+// (8-B stores of the accumulator's four consecutive queries), and after a barrier the chunk's dQ^T
+// = K^T dS^T is formed as sixteen 16 x 16 tiles, two per wave (one head-dim block x two query
+// blocks: the K^T fragment is shared), both operands by ds_read_b64_tr_b16 in the same permuted key
+// order from the K image (all 256 keys, staged once) and the dS image; fixed order, no atomics.
+// delta = rowsum(dO o O) is formed per chunk by the threads that stage dO (they load O beside it).
+// 5 products per query-key block instead of the pair's 7 (S and dP formed once), one launch.
+// LDS: 8 + 8 KiB staging (single buffer: the second barrier of a chunk separates its readers from
+// the next store) + 32 KiB K image + 32 KiB dS image.
+template <int MODE, bool KPAD>
+__global__ __launch_bounds__(512, 1) void attn_bwd8_kernel(AttnBwdArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned short Qs[IMG_ELEMS];
+  __shared__ __attribute__((aligned(16))) unsigned short Ds[IMG_ELEMS];
+  __shared__ __attribute__((aligned(16))) unsigned short Ki[4][IMG_ELEMS];   // keys 64 i .. + 63
+  __shared__ __attribute__((aligned(16))) unsigned short dSi[4][IMG_ELEMS];  // [keys 64 i ..][64 queries]
+  __shared__ float lse_s[64], dl_s[64];
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  const int ti = tid & 255;
+  const bool stq = tid < 256;  // stages Q (waves 0-3) or dO + delta (waves 4-7)
+  const int kwave = w * 32;
+  const unsigned short* Q = a.q + b * a.q_sb + h * a.q_sh;
+  const unsigned short* K = a.k + b * a.k_sb + h * a.k_sh;
+  const unsigned short* V = a.v + b * a.v_sb + h * a.v_sh;
+  const unsigned short* dO = a.dout + b * a.o_sb + h * a.o_sh;
+  const unsigned short* Og = a.o + b * a.o_sb + h * a.o_sh;
+  const long rowbase = ((long)b * a.H + h) * a.Sq;
+  const int nchunks = (a.Sq + 63) / 64;
+  const int nstep = (a.Sk + 31) >> 5;  // 32-key steps of the dQ product holding at least one key
+  // thread ti stages 16-B pieces i = ti, ti + 256 of a 64 x 64 chunk: row i >> 3, chunk i & 7
+  Piece2 ps, po;
+  float lse_r = INFINITY;
+  const unsigned short* SQ = stq ? Q : dO;
+  const long sss = stq ? a.q_ss : a.o_ss;
+  auto ld = [&](const unsigned short* base, long ss, int r0, int rmax, Piece2& p) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = ti + 256 * u, r = r0 + (i >> 3);
+      if (r < rmax) p.v[u] = *(const u16x8_t*)(base + (long)r * ss + (i & 7) * 8);
+      else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) p.v[u][j] = 0;
+      }
+    }
+  };
+  auto stage_load = [&](int r0) {
+    ld(SQ, sss, r0, a.Sq, ps);
+    lse_r = (tid < 64 && r0 + tid < a.Sq) ? a.lse[rowbase + r0 + tid] : INFINITY;
+  };
+  auto stage_store = [&]() {
+    unsigned short* img = stq ? Qs : Ds;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = ti + 256 * u;
+      *(u16x8_t*)(img + swz(i >> 3, i & 7)) = ps.v[u];
+      if (!stq) {  // delta of row i >> 3: 8 consecutive lanes hold its 64 values
+        float d = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d = fmaf(bf2f(ps.v[u][j]), bf2f(po.v[u][j]), d);
+        d += smi_dpp<SMI_DPP_QP1032>(d);
+        d += smi_dpp<SMI_DPP_QP2301>(d);
+        d += smi_dpp<SMI_DPP_HMIRROR>(d);
+        if ((i & 7) == 0) dl_s[i >> 3] = d;
+      }
+    }
+    if (tid < 64) lse_s[tid] = lse_r;
+  };
+  if (nchunks) { stage_load(0); if (!stq) ld(Og, a.o_ss, 0, a.Sq, po); }
+  // the head's K rows -> four 64-row images (pieces of 16 B, 4 per thread)
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = tid + 512 * u, r = i >> 3;
+    u16x8_t v;
+    if (r < a.Sk) v = *(const u16x8_t*)(K + (long)r * a.k_ss + (i & 7) * 8);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = 0;
+    }
+    *(u16x8_t*)(&Ki[r >> 6][0] + swz(r & 63, i & 7)) = v;
+  }
+  bf16x8_t kf[2][2], vf[2][2];
+  bool kok[2];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int kj = kwave + kt * 16 + n;
+    const bool ok = kj < a.Sk;
+    kok[kt] = ok && !(KPAD && a.kpad[(long)b * a.Sk + kj]);
+    kf[kt][0] = load8(K + (long)kj * a.k_ss + 8 * g, ok);
+    kf[kt][1] = load8(K + (long)kj * a.k_ss + 32 + 8 * g, ok);
+    vf[kt][0] = load8(V + (long)kj * a.v_ss + 8 * g, ok);
+    vf[kt][1] = load8(V + (long)kj * a.v_ss + 32 + 8 * g, ok);
+  }
+  f32x4_t dk[2][4], dv[2][4];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) { dk[kt][dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f}; dv[kt][dt] = dk[kt][dt]; }
+  if (nchunks) stage_store();
+  __syncthreads();
+  // this wave's dQ tiles: head dims 16 dtq .. + 15 x query blocks 2 qpq, 2 qpq + 1 (16 each)
+  const int dtq = w & 3, qpq = w >> 2;
+  unsigned short* dQ = a.dq + b * a.q_sb + h * a.q_sh;
+  unsigned short* dSw = &dSi[w >> 1][0];  // this wave's 32 key rows start at row 32 (w & 1)
+  for (int c = 0; c < nchunks; ++c) {
+    const int q0 = c * 64;
+    const bool more = c + 1 < nchunks;
+    if (more) stage_load(q0 + 64);
+    if (!(MODE == 2 && q0 + 63 < kwave) && kwave < a.Sk) {  // else P = dS = 0 for every key of the wave
+      f32x4_t s[2][4], dp[2][4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf16x8_t q0f = frag_row(Qs, t * 16 + n, g), q1f = frag_row(Qs, t * 16 + n, 4 + g);
+        const bf16x8_t d0f = frag_row(Ds, t * 16 + n, g), d1f = frag_row(Ds, t * 16 + n, 4 + g);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          s[kt][t] = MFMA16(q0f, kf[kt][0], ((f32x4_t){0.f, 0.f, 0.f, 0.f}));
+          s[kt][t] = MFMA16(q1f, kf[kt][1], s[kt][t]);
+          dp[kt][t] = MFMA16(d0f, vf[kt][0], ((f32x4_t){0.f, 0.f, 0.f, 0.f}));
+          dp[kt][t] = MFMA16(d1f, vf[kt][1], dp[kt][t]);
+        }
+      }
+      // s[kt][t][j]: query q0 + t*16 + 4g + j, key kwave + kt*16 + n
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const int kj = kwave + kt * 16 + n;
+        const float kbias = kok[kt] ? 0.f : -INFINITY;
+        const int krow = 32 * (w & 1) + kt * 16 + n;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int ql = t * 16 + 4 * g + j;
+            const int qq = q0 + ql;
+            float x = fmaf(s[kt][t][j], a.scale_log2, kbias);
+            if (MODE == 1) x += (kj < qq) ? LOG2E_F : 0.f;
+            if (MODE == 2) x = (kj > qq) ? -INFINITY : x;
+            const float p = __builtin_amdgcn_exp2f(x - lse_s[ql]);
+            s[kt][t][j] = p;
+            dp[kt][t][j] = p * (dp[kt][t][j] - dl_s[ql]);
+          }
+          // dS row krow, queries t*16 + 4g .. + 3 (the same bf16 values the dK product takes)
+          const int col = t * 16 + 4 * g;
+          *(uint2*)(dSw + swz(krow, col >> 3) + (col & 7)) =
+              make_uint2(pack2bf(dp[kt][t][0], dp[kt][t][1]), pack2bf(dp[kt][t][2], dp[kt][t][3]));
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8_t p0 = pack_acc(s[0][2 * s2], s[0][2 * s2 + 1]);
+        const bf16x8_t p1 = pack_acc(s[1][2 * s2], s[1][2 * s2 + 1]);
+        const bf16x8_t e0 = pack_acc(dp[0][2 * s2], dp[0][2 * s2 + 1]);
+        const bf16x8_t e1 = pack_acc(dp[1][2 * s2], dp[1][2 * s2 + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const bf16x8_t dot = frag_tr(Ds, 32 * s2, dt * 16, lane);
+          const bf16x8_t qt = frag_tr(Qs, 32 * s2, dt * 16, lane);
+          dv[0][dt] = MFMA16(dot, p0, dv[0][dt]);
+          dv[1][dt] = MFMA16(dot, p1, dv[1][dt]);
+          dk[0][dt] = MFMA16(qt, e0, dk[0][dt]);
+          dk[1][dt] = MFMA16(qt, e1, dk[1][dt]);
+        }
+      }
+    }
+    // O rows of the next chunk (delta) only now: held across the dQ phase, not the products
+    if (more && !stq) ld(Og, a.o_ss, q0 + 64, a.Sq, po);
+    smi_lds_barrier();  // dS image complete; every read of the staged chunk done
+    {
+      // dQ^T tiles = sum over 32-key steps of K^T dS^T; causal: steps past the chunk are 0
+      const int ns = MODE == 2 ? min(nstep, 2 * c + 2) : nstep;
+      f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+      // fully unrolled, step st8 + 1's fragments read before step st8's MFMAs (reads past ns are
+      // in bounds and unused)
+      bf16x8_t kt[2], d0[2], d1[2];
+      auto ldq = [&](int st8, int sl) {
+        const int img = st8 >> 1, kr = 32 * (st8 & 1);
+        kt[sl] = frag_tr(Ki[img], kr, 16 * dtq, lane);
+        d0[sl] = frag_tr(dSi[img], kr, 32 * qpq, lane);
+        d1[sl] = frag_tr(dSi[img], kr, 32 * qpq + 16, lane);
+      };
+      ldq(0, 0);
+#pragma unroll
+      for (int st8 = 0; st8 < 8; ++st8) {
+        if (st8 + 1 < 8) ldq(st8 + 1, (st8 + 1) & 1);
+        if (st8 < ns) {
+          acc0 = MFMA16(kt[st8 & 1], d0[st8 & 1], acc0);
+          acc1 = MFMA16(kt[st8 & 1], d1[st8 & 1], acc1);
+        }
+      }
+      // lane: query q0 + 32 qpq (+ 16) + n, head dims 16 dtq + 4g .. + 3
+      const int qa = q0 + 32 * qpq + n, qb = qa + 16;
+      if (qa < a.Sq) store4(dQ + (long)qa * a.q_ss + 16 * dtq + 4 * g, acc0, a.scale);
+      if (qb < a.Sq) store4(dQ + (long)qb * a.q_ss + 16 * dtq + 4 * g, acc1, a.scale);
+    }
+    if (more) stage_store();
+    smi_lds_barrier();  // next chunk staged; every dS read done before the next chunk's writes
+  }
+  unsigned short* dK = a.dk + b * a.k_sb + h * a.k_sh;
+  unsigned short* dV = a.dv + b * a.v_sb + h * a.v_sh;
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int kj = kwave + kt * 16 + n;
+    if (kj < a.Sk) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        store4(dK + (long)kj * a.k_ss + dt * 16 + 4 * g, dk[kt][dt], a.scale);
+        store4(dV + (long)kj * a.v_ss + dt * 16 + 4 * g, dv[kt][dt], 1.0f);
+      }
+    }
+  }
+}
+
+#define SMI_ATTN_DISPATCH_NT(KERNEL, GRID, NT, ARGS)                                                        \
   do {                                                                                                     \
     const bool kp_ = (ARGS).kpad != nullptr;                                                               \
     switch ((ARGS).mode) {                                                                                 \
-      case 0: if (kp_) hipLaunchKernelGGL((KERNEL<0, true>), GRID, dim3(256), 0, st, ARGS);                \
-              else hipLaunchKernelGGL((KERNEL<0, false>), GRID, dim3(256), 0, st, ARGS); break;            \
-      case 1: if (kp_) hipLaunchKernelGGL((KERNEL<1, true>), GRID, dim3(256), 0, st, ARGS);                \
-              else hipLaunchKernelGGL((KERNEL<1, false>), GRID, dim3(256), 0, st, ARGS); break;            \
-      case 2: if (kp_) hipLaunchKernelGGL((KERNEL<2, true>), GRID, dim3(256), 0, st, ARGS);                \
-              else hipLaunchKernelGGL((KERNEL<2, false>), GRID, dim3(256), 0, st, ARGS); break;            \
+      case 0: if (kp_) hipLaunchKernelGGL((KERNEL<0, true>), GRID, dim3(NT), 0, st, ARGS);                 \
+              else hipLaunchKernelGGL((KERNEL<0, false>), GRID, dim3(NT), 0, st, ARGS); break;             \
+      case 1: if (kp_) hipLaunchKernelGGL((KERNEL<1, true>), GRID, dim3(NT), 0, st, ARGS);                 \
+              else hipLaunchKernelGGL((KERNEL<1, false>), GRID, dim3(NT), 0, st, ARGS); break;             \
+      case 2: if (kp_) hipLaunchKernelGGL((KERNEL<2, true>), GRID, dim3(NT), 0, st, ARGS);                 \
+              else hipLaunchKernelGGL((KERNEL<2, false>), GRID, dim3(NT), 0, st, ARGS); break;             \
       default: return -1;                                                                                  \
     }                                                                                                      \
   } while (0)
+#define SMI_ATTN_DISPATCH(KERNEL, GRID, ARGS) SMI_ATTN_DISPATCH_NT(KERNEL, GRID, 256, ARGS)
+extern "C" int smi_attn_bwd1(int);
 
 extern "C" int smi_attn_fwd(const AttnFwdArgs* args, hipStream_t st) {
   const AttnFwdArgs& a = *args;
@@ -554,7 +771,11 @@ extern "C" int smi_attn_bwd(const AttnBwdArgs* args, const void* o, float* delta
   b2.o = (const unsigned short*)o;
   b2.delta_out = delta;
   b2.delta = delta;
-  SMI_ATTN_DISPATCH(attn_bwd_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), b2);
-  SMI_ATTN_DISPATCH(attn_bwd_dkdv_kernel, dim3((a.Sk + 127) / 128, a.H, a.B), b2);
+  if (a.Sk <= 256 && smi_attn_bwd1(-1)) {
+    SMI_ATTN_DISPATCH_NT(attn_bwd8_kernel, dim3(1, a.H, a.B), 512, b2);
+  } else {
+    SMI_ATTN_DISPATCH(attn_bwd_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), b2);
+    SMI_ATTN_DISPATCH(attn_bwd_dkdv_kernel, dim3((a.Sk + 127) / 128, a.H, a.B), b2);
+  }
   SMI_CHECK_LAUNCH();
 }

@@ -1021,6 +1021,237 @@ __global__ __launch_bounds__(512, 1) void attn_sp_dkdv8_kernel(AttnF32Args a) {
   }
 }
 
+// SINGLE-PASS backward (Sk <= 256: the default whenever a head's keys fit one workgroup).  The
+// dQ + dK/dV pair above forms S and dP twice (once per kernel: 7 products per query-key block);
+// here one 8-wave workgroup owns every key of its (batch, head), streams 32-query chunks of Q / dO
+// once, forms P and dS once and finishes the chunk's dQ itself (5 products):
+//  * products phase (wave w, keys 32 w .. + 31 on the lane, as attn_sp_dkdv8_kernel with the roles
+//    of K and V swapped): S = Q K^T with K's B fragments read from the wave's K plane image, dP =
+//    dO V^T with the owned V rows split in registers, P, dS; dV^T += dO^T P, dK^T += Q^T dS.  Each
+//    wave also writes its dS tile (fp32) into a [32 queries][256 keys] LDS image — the transpose the
+//    dQ product needs (its reduction index, the key, is the lane index of dS);
+//  * dQ phase: dQ^T = K^T dS^T for the chunk as eight 16 x 16 tiles on v_mfma_f32_16x16x32_bf16,
+//    one per wave (16 head dims x 16 queries, all 256 keys: K^T fragments by ds_read_b64_tr_b16 from
+//    the eight K images, dS^T fragments read as fp32 rows and split), fixed order, no atomics; the
+//    tile is stored directly (one 16-B fp32 store / three 8-B plane stores per lane).
+//  * delta = rowsum(dO o O) per chunk by the threads that stage dO (no dQ kernel to hand it over).
+// Per chunk: products -> barrier (dS complete, staged chunk consumed) -> dQ + store of the next
+// staged chunk -> barrier.  LDS: 12 + 12 KiB staging (single buffer: the second barrier already
+// separates the consumers from the next store) + 8 x 12 KiB K images + 32.5 KiB dS = 153 KiB.
+#define AS_BWD8_PITCH 260  // dS image row pitch (floats): = 4 mod 64 -> conflict-free 16-row b128 reads
+#define MF16X32(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
+template <int MODE, bool KPAD>
+__global__ __launch_bounds__(512, 1) void attn_sp_bwd8_kernel(AttnF32Args a) {
+  __shared__ __attribute__((aligned(16))) unsigned short Qs[AS_OP];
+  __shared__ __attribute__((aligned(16))) unsigned short Ds[AS_OP];
+  __shared__ __attribute__((aligned(16))) unsigned short Ko[8][AS_OP];
+  __shared__ __attribute__((aligned(16))) float dSs[FCH * AS_BWD8_PITCH];
+  __shared__ float lse_s[FCH], dl_s[FCH];
+  AST_DECL;
+  AST_T(tk0);
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  const int kwave = w * 32;
+  const int kj = kwave + (lane & 31);
+  const bool stq = tid < 256;  // this thread stages Q (waves 0-3) or dO and delta (waves 4-7)
+  const int ti = tid & 255;
+  AS_SRC(Q, a.q, a.q_sb, a.q_sh, a.q_ss);
+  AS_SRC(K, a.k, a.k_sb, a.k_sh, a.k_ss);
+  AS_SRC(V, a.v, a.v_sb, a.v_sh, a.v_ss);
+  AS_SRC(dO, a.dout, a.o_sb, a.o_sh, a.o_ss);
+  AS_SRC(Og, a.o, a.o_sb, a.o_sh, a.o_ss);
+  const AsSrc& SQ = stq ? Q : dO;
+  const long rbase = ((long)b * a.H + hh) * a.Sq;
+  const int nchunks = (a.Sq + FCH - 1) / FCH;
+  const int nimg = (a.Sk + 31) >> 5;  // K images holding at least one key
+  AStage ps, po;
+  float lse_r = INFINITY;
+  auto stage_load = [&](int r0) {
+    SQ.load(r0, a.Sq, ps, ti);
+    lse_r = (tid < FCH && r0 + tid < a.Sq) ? a.lse[rbase + r0 + tid] : INFINITY;
+  };
+  auto stage_store = [&]() {
+    as_store(stq ? Qs : Ds, ps, ti);
+    if (!stq) {  // delta of row ti >> 3: its 64 values are 8 consecutive lanes' 8 each
+      float d = ps.v[0].x * po.v[0].x;
+      d = fmaf(ps.v[0].y, po.v[0].y, d); d = fmaf(ps.v[0].z, po.v[0].z, d); d = fmaf(ps.v[0].w, po.v[0].w, d);
+      d = fmaf(ps.v[1].x, po.v[1].x, d); d = fmaf(ps.v[1].y, po.v[1].y, d);
+      d = fmaf(ps.v[1].z, po.v[1].z, d); d = fmaf(ps.v[1].w, po.v[1].w, d);
+      d += smi_dpp<SMI_DPP_QP1032>(d);
+      d += smi_dpp<SMI_DPP_QP2301>(d);
+      d += smi_dpp<SMI_DPP_HMIRROR>(d);  // lanes 0-3 + 4-7 of each 8-lane group: the row's sum
+      if ((ti & 7) == 0) dl_s[ti >> 3] = d;
+    }
+    if (tid < FCH) lse_s[tid] = lse_r;
+  };
+  if (nchunks) { stage_load(0); if (!stq) Og.load(0, a.Sq, po, ti); }
+  // every wave's 32 K rows -> its plane image (four 32-row passes of 512 threads)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = tid + 512 * i, blk = idx >> 8;
+    AStage pk;
+    K.load(32 * blk, a.Sk, pk, idx & 255);
+    as_store(Ko[blk], pk, idx & 255);
+  }
+  F32Pre<1, 32> vs;
+  V.own(kj, a.Sk, lane, vs);
+  const bool kok = kj < a.Sk && !(KPAD && a.kpad[(long)b * a.Sk + kj]);
+  const float kbias = kok ? 0.f : -INFINITY;
+  f32x16_t dk[2], dv[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
+  if (nchunks) stage_store();
+  __syncthreads();
+  AST_T(tk1);
+  AST_ADD(0, tk0, tk1);  // prologue
+  const unsigned short* kimg = Ko[w];
+  // dQ tile of this wave: head dims 16 dtq .. + 15 x queries 16 qtq .. + 15 of each chunk
+  const int dtq = w & 3, qtq = w >> 2, l16 = lane & 15, g4 = lane >> 4;
+  for (int c = 0; c < nchunks; ++c) {
+    const int q0 = c * FCH;
+    const bool more = c + 1 < nchunks;
+    AST_T(tc0);
+    if (more) stage_load(q0 + FCH);
+    // a wave whose keys all follow the chunk's queries (causal) or lie past Sk has P = dS = 0
+    if (!(MODE == 2 && q0 + 31 < kwave) && kwave < a.Sk) {
+      f32x16_t s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)  // S = Q K^T, K's fragments from the wave's image
+        s = as_mma(as_rowfrag(Qs, lane, j), as_rowfrag(kimg, lane, j), s);
+      dp = as_rows_dot(Ds, lane, vs, dp);  // dP = dO V^T
+      float pvv[16], dsv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ql = fa_kl(r, h);
+        const int qq = q0 + ql;
+        float x = fmaf(s[r], a.scale_log2, kbias);
+        if (MODE == 1) x += (kj < qq) ? LOG2E_F : 0.f;
+        if (MODE == 2) x = (kj > qq) ? -INFINITY : x;
+        const float pr = __builtin_amdgcn_exp2f(x - lse_s[ql]);  // rows past Sq: lse = +inf -> 0
+        pvv[r] = pr;
+        dsv[r] = pr * (dp[r] - dl_s[ql]);
+        dSs[ql * AS_BWD8_PITCH + kj] = dsv[r];
+      }
+      AST_T(tc1);
+      AST_ADD(1, tc0, tc1);  // S, dP, P, dS (+ dS image stores)
+      as_cols_acc(Ds, lane, pvv, dv);  // dV^T += dO^T P
+      as_cols_acc(Qs, lane, dsv, dk);  // dK^T += Q^T dS
+      AST_T(tc2);
+      AST_ADD(2, tc1, tc2);  // dV, dK products issue
+    }
+    AST_T(tc2b);
+    // O rows of the next chunk (delta) only now: held across the dQ phase, not the products
+    if (more && !stq) Og.load(q0 + FCH, a.Sq, po, ti);
+    smi_lds_barrier();  // dS complete; every read of the staged chunk done
+    AST_T(tc3);
+    AST_ADD(3, tc2b, tc3);  // first barrier (waits for the MFMAs too)
+    {
+      // dQ^T (16 x 16) = sum over the key images of K^T dS^T; causal: images past the chunk are 0
+      const int nk = MODE == 2 ? min(nimg, c + 1) : nimg;
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+      const float* srow = dSs + (16 * qtq + l16) * AS_BWD8_PITCH + 8 * g4;
+      const int o0 = as_off(8 * g4 + (l16 >> 2), 16 * dtq + 4 * (l16 & 3));
+      const int o1 = as_off(8 * g4 + 4 + (l16 >> 2), 16 * dtq + 4 * (l16 & 3));
+      // fully unrolled, image kw + 1's reads issued before image kw's split and MFMAs (reads past
+      // nk are in bounds and unused: images past Sk are zero rows, their dS columns never read)
+      Split3 kt[2];
+      float4 u[2][2];
+      auto ldq = [&](int kw, int sl) {
+        bf16x8_t* outs[3] = {&kt[sl].h, &kt[sl].m, &kt[sl].l};
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          const unsigned short* bp = Ko[kw] + pl * AS_PL;
+          const as_s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) as_s16x4_t*)(bp + o0));
+          const as_s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) as_s16x4_t*)(bp + o1));
+          *outs[pl] = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+        u[sl][0] = *(const float4*)(srow + 32 * kw);
+        u[sl][1] = *(const float4*)(srow + 32 * kw + 4);
+      };
+      ldq(0, 0);
+#pragma unroll
+      for (int kw = 0; kw < 8; ++kw) {
+        if (kw + 1 < 8) ldq(kw + 1, (kw + 1) & 1);
+        if (kw < nk) {
+          const int sl = kw & 1;
+          const float f[8] = {u[sl][0].x, u[sl][0].y, u[sl][0].z, u[sl][0].w,
+                              u[sl][1].x, u[sl][1].y, u[sl][1].z, u[sl][1].w};
+          const Split3 sd = split3_8(f);
+          acc = MF16X32(kt[sl].l, sd.h, acc);
+          acc = MF16X32(kt[sl].m, sd.m, acc);
+          acc = MF16X32(kt[sl].h, sd.l, acc);
+          acc = MF16X32(kt[sl].m, sd.h, acc);
+          acc = MF16X32(kt[sl].h, sd.m, acc);
+          acc = MF16X32(kt[sl].h, sd.h, acc);
+        }
+      }
+      // lane: query q0 + 16 qtq + l16, head dims 16 dtq + 4 g4 .. + 3
+      const int qi = q0 + 16 * qtq + l16;
+      if (qi < a.Sq) {
+        const long off = (long)b * a.q_sb + hh * a.q_sh + (long)qi * a.q_ss + 16 * dtq + 4 * g4;
+        const float v0 = acc[0] * a.scale, v1 = acc[1] * a.scale, v2 = acc[2] * a.scale, v3 = acc[3] * a.scale;
+        if (!a.no_f32_grad) *(float4*)(a.dq + off) = make_float4(v0, v1, v2, v3);
+        if (a.dqp) {
+          uint32_t h0, m0, l0, h1, m1, l1;
+          split3_pair(v0, v1, h0, m0, l0);
+          split3_pair(v2, v3, h1, m1, l1);
+          unsigned short* qp = a.dqp + off;
+          *(uint2*)qp = make_uint2(h0, h1);
+          *(uint2*)(qp + a.dq_ps) = make_uint2(m0, m1);
+          *(uint2*)(qp + 2 * a.dq_ps) = make_uint2(l0, l1);
+        }
+      }
+    }
+    AST_T(tc4);
+    AST_ADD(4, tc3, tc4);  // dQ phase + its stores
+    if (more) stage_store();
+    AST_T(tc5);
+    AST_ADD(5, tc4, tc5);  // next chunk's stage store + delta
+    smi_lds_barrier();  // next chunk staged; every dS read done before the next chunk's writes
+    AST_T(tc6);
+    AST_ADD(6, tc5, tc6);  // second barrier
+  }
+  // dK / dV through the (now free: the last barrier follows every dQ read) K images
+  if (a.ae16) {
+    float* img = (float*)&Ko[w][0];
+    ae_stage(img, dk, lane, a.scale);
+    __syncthreads();
+    const long rk = (long)b * a.k_sb + hh * a.k_sh + (long)kwave * a.k_ss;
+    const long rv = (long)b * a.v_sb + hh * a.v_sh + (long)kwave * a.v_ss;
+    ae_store(img, a.no_f32_grad ? nullptr : a.dk + rk, a.dkp ? a.dkp + rk : nullptr, a.k_ss, a.dkv_ps, a.Sk - kwave,
+             lane);
+    __syncthreads();
+    ae_stage(img, dv, lane, 1.0f);
+    __syncthreads();
+    ae_store(img, a.no_f32_grad ? nullptr : a.dv + rv, a.dvp ? a.dvp + rv : nullptr, a.v_ss, a.dkv_ps, a.Sk - kwave,
+             lane);
+  } else if (kj < a.Sk) {
+    float* dK = a.dk + b * a.k_sb + hh * a.k_sh + (long)kj * a.k_ss;
+    float* dV = a.dv + b * a.v_sb + hh * a.v_sh + (long)kj * a.v_ss;
+    if (!a.no_f32_grad) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        fa_store_rowT(dK + dt * 32, dk[dt], lane, a.scale);
+        fa_store_rowT(dV + dt * 32, dv[dt], lane, 1.0f);
+      }
+    }
+    if (a.dkp) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        fa_store_rowT_planes(a.dkp + (dK - a.dk) + dt * 32, a.dkv_ps, dk[dt], lane, a.scale);
+        fa_store_rowT_planes(a.dvp + (dV - a.dv) + dt * 32, a.dkv_ps, dv[dt], lane, 1.0f);
+      }
+    }
+  }
+  AST_T(tk3);
+  AST_ADD(7, tk0, tk3);  // wave lifetime
+  AST_END();
+}
+
 // Launch over the compile-time (mask mode, key padding) instances of a kernel, NT threads
 #define SMI_ATTN_SP_MODES(KERNEL, GRID, NT, ARGS)                                                        \
   do {                                                                                                   \
@@ -1091,6 +1322,18 @@ extern "C" int smi_attn_ae(int set) {
   return g_attn_ae;
 }
 
+// Single-pass backward at Sk <= 256 (attn_sp_bwd8_kernel here, attn_bwd8_kernel in attention.hip):
+// 1 = on (default), 0 = the dQ + dK/dV kernel pair (SMI_ATTN_BWD1=0; A/B and tests).
+static int g_attn_bwd1 = -1;
+extern "C" int smi_attn_bwd1(int set) {
+  if (set == 0 || set == 1) g_attn_bwd1 = set;
+  if (g_attn_bwd1 < 0) {
+    const char* e = getenv("SMI_ATTN_BWD1");
+    g_attn_bwd1 = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_attn_bwd1;
+}
+
 extern "C" int smi_attn_f32_fwd(const AttnF32Args* args, hipStream_t st) {
   AttnF32Args a = *args;
   if (!fa_ok(a)) return -1;
@@ -1109,8 +1352,12 @@ extern "C" int smi_attn_f32_bwd(const AttnF32Args* args, hipStream_t st) {
            fa_ae16(a.dvp, a.v_sb, a.v_sh, a.v_ss);
   if (a.no_f32_grad && (!a.dqp || !a.dkp || !a.dvp)) return -1;  // planes-only needs every plane output
   if (smi_gemm_f32_algo(-1) != 0) {
-    SMI_ATTN_SP_MODES(attn_sp_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), 256, a);
-    SMI_ATTN_SP_MODES(attn_sp_dkdv8_kernel, dim3((a.Sk + AS_DKDV8_KEYS - 1) / AS_DKDV8_KEYS, a.H, a.B), 512, a);
+    if (a.Sk <= AS_DKDV8_KEYS && smi_attn_bwd1(-1)) {
+      SMI_ATTN_SP_MODES(attn_sp_bwd8_kernel, dim3(1, a.H, a.B), 512, a);
+    } else {
+      SMI_ATTN_SP_MODES(attn_sp_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), 256, a);
+      SMI_ATTN_SP_MODES(attn_sp_dkdv8_kernel, dim3((a.Sk + AS_DKDV8_KEYS - 1) / AS_DKDV8_KEYS, a.H, a.B), 512, a);
+    }
   } else {
     SMI_ATTN_F32_DISPATCH(attn_f32_dq_kernel, dim3((a.Sq + 127) / 128, a.H, a.B), a);
     SMI_ATTN_F32_DISPATCH(attn_f32_dkdv_kernel, dim3((a.Sk + 127) / 128, a.H, a.B), a);

@@ -250,15 +250,46 @@ def attn_kernel(request):
     C.attn_ae(prev)
 
 
+@pytest.fixture(params=[1, 0], ids=["single_pass_bwd", "dq_dkdv_pair"])
+def bwd_path(request):
+    """Split-product attention backward at Sk <= 256: the single-pass 8-wave kernel (default) or
+    the dQ + dK/dV pair (C.attn_bwd1(0)); past 256 keys (and under the f32-MFMA algorithm) the
+    pair always runs."""
+    C = _native.C()
+    prev = C.attn_bwd1(-1)
+    C.attn_bwd1(request.param)
+    yield request.param
+    C.attn_bwd1(prev)
+
+
 @pytest.mark.parametrize("mode", ["none", "reference", "causal"])
-@pytest.mark.parametrize("S", [256, 200, 37])
-def test_self_attention_f32(attn_kernel, mode, S):
+@pytest.mark.parametrize("S", [256, 200, 37, 300])
+def test_self_attention_f32(attn_kernel, bwd_path, mode, S):
     _attn_f32(2, 4, S, S, mode, False, False)
 
 
 @pytest.mark.parametrize("mode,kp", [("none", False), ("none", True), ("reference", False)])
-def test_cross_attention_f32(attn_kernel, mode, kp):
+def test_cross_attention_f32(attn_kernel, bwd_path, mode, kp):
     _attn_f32(2, 3, 130, 130 if mode == "reference" else 77, mode, True, kp)
+
+
+@pytest.mark.parametrize("mode", ["reference", "causal"])
+def test_attention_f32_single_pass_repeatable(mode):
+    """The single-pass backward's dQ tiles are fixed-order sums over the eight key images (no
+    atomics): two runs are bitwise equal (gradients and their planes); Sq 300 > Sk 256 streams
+    more query chunks than key images."""
+    torch.manual_seed(5)
+    B, H, hd = 2, 3, 64
+    ins = (torch.randn(B, 300, H * hd, device=dev), torch.randn(B, 256, 2 * H * hd, device=dev))
+    do = torch.randn(B, 300, H * hd, device=dev)
+    outs = []
+    for _ in range(2):
+        xs = [t.clone().requires_grad_() for t in ins]
+        o = cross_attention(xs[0], xs[1], H, mode)
+        o.backward(do)
+        outs.append([t.grad.clone() for t in xs])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("M,V", [(8192, 10000), (300, 10000), (77, 45), (256, 384)])

@@ -93,16 +93,48 @@ def _attn_case(B, H, Sq, Sk, mode, cross, kp):
         _close(qg.grad, qc.grad, 3e-2, 3e-2, f"dqkv {mode}")
 
 
+@pytest.fixture(params=[1, 0], ids=["single_pass_bwd", "dq_dkdv_pair"])
+def bwd_path(request):
+    """Attention backward at Sk <= 256: the single-pass 8-wave kernel (default) or the dQ + dK/dV
+    kernel pair (C.attn_bwd1(0)); past 256 keys the pair always runs."""
+    C = _native.C()
+    prev = C.attn_bwd1(-1)
+    C.attn_bwd1(request.param)
+    yield request.param
+    C.attn_bwd1(prev)
+
+
 @pytest.mark.parametrize("mode", ["none", "reference", "causal"])
-@pytest.mark.parametrize("S", [256, 200, 37])
-def test_self_attention(mode, S):
+@pytest.mark.parametrize("S", [256, 200, 37, 300])
+def test_self_attention(bwd_path, mode, S):
     _attn_case(2, 4, S, S, mode, False, False)
 
 
 @pytest.mark.parametrize("mode", ["none", "reference"])
 @pytest.mark.parametrize("kp", [False, True])
-def test_cross_attention(mode, kp):
+def test_cross_attention(bwd_path, mode, kp):
     _attn_case(2, 3, 130, 130 if mode == "reference" else 77, mode, True, kp)
+
+
+@pytest.mark.parametrize("cross", [False, True])
+def test_attention_bwd_single_pass_repeatable(cross):
+    """The single-pass backward sums every dQ tile over the key images in a fixed order (no
+    atomics): two runs are bitwise equal; Sq (300) > Sk exercises the streamed query chunks."""
+    torch.manual_seed(3)
+    B, H, hd = 2, 3, 64
+    if cross:
+        ins = (torch.randn(B, 300, H * hd, device=dev).bfloat16(), torch.randn(B, 250, 2 * H * hd, device=dev).bfloat16())
+    else:
+        ins = (torch.randn(B, 256, 3 * H * hd, device=dev).bfloat16(),)
+    do = torch.randn(B, ins[0].shape[1], H * hd, device=dev).bfloat16()
+    outs = []
+    for _ in range(2):
+        xs = [t.clone().requires_grad_() for t in ins]
+        o = cross_attention(xs[0], xs[1], H, "reference") if cross else self_attention(xs[0], H, "reference")
+        o.backward(do)
+        outs.append([t.grad.clone() for t in xs])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
