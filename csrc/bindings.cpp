@@ -116,7 +116,7 @@ int smi_adam(float*, float*, float*, float*, void*, long, const float*, float*, 
 int smi_sgd(float*, float*, float*, void*, long, const float*, float*, unsigned*, float, float, float, int, float, int,
             void*, long, int*, hipStream_t);
 int smi_adam_multi(float* const*, float* const*, float* const*, float* const*, void* const*, const long*, int, const float*,
-                   float*, unsigned*, float, float, float, float, float, int, int, void* const*, long, int*, hipStream_t);
+                   float*, unsigned*, float, float, float, float, float, int, int, void* const*, long, int*, int, hipStream_t);
 int smi_multi_copy(void* const*, const void* const*, const long*, int, hipStream_t);
 }
 
@@ -305,7 +305,7 @@ PYBIND11_MODULE(_C, m) {
   // Adam over several disjoint ranges, one launch, one step advance (ZeRO-1 shard update)
   m.def("adam_multi", [](std::vector<u> p, std::vector<u> g, std::vector<u> mm, std::vector<u> v, std::vector<u> pbf,
                          std::vector<long> n, u lr, u step, u done, float b1, float b2, float eps, float wd, float gscale,
-                         int adamw, int zero_grad, std::vector<u> pl, long ps, u seed, u st) {
+                         int adamw, int zero_grad, std::vector<u> pl, long ps, u seed, int advance, u st) {
     const size_t c = p.size();
     if (g.size() != c || mm.size() != c || v.size() != c || pbf.size() != c || n.size() != c ||
         (!pl.empty() && pl.size() != c))
@@ -318,7 +318,7 @@ PYBIND11_MODULE(_C, m) {
     }
     chk(smi_adam_multi(a.data(), b.data(), d.data(), e.data(), f.data(), n.data(), (int)c, PF(lr), PF(step),
                        reinterpret_cast<unsigned*>(done), b1, b2, eps, wd, gscale, adamw, zero_grad,
-                       pl.empty() ? nullptr : q.data(), ps, reinterpret_cast<int*>(seed), S(st)),
+                       pl.empty() ? nullptr : q.data(), ps, reinterpret_cast<int*>(seed), advance, S(st)),
         "adam_multi");
   });
   m.def("sgd", [](u p, u g, u buf, u pbf, long n, u lr, u step, u done, float mom, float damp, float wd, int nesterov,

@@ -111,8 +111,11 @@ __global__ __launch_bounds__(NT) void adam_kernel(float* __restrict__ p, float* 
 
 // Adam over several disjoint ranges in ONE launch with ONE step advance: the ZeRO-1 update of
 // a data-parallel rank, which owns one piece of every gradient bucket (sparkmi/parallel/ddp.py)
-// and keeps the moments of its pieces only (compact m / v).  Range e owns blocks
-// [blk0[e], blk0[e+1]); float4 body (every piece is a multiple of 4 floats, 16-B aligned).
+// and keeps the moments of its pieces only (compact m / v); and a step's update in parts (the
+// parameters already final while the backward still runs, then the rest: sparkmi/optim/adam.py
+// step_ranges).  Range e owns blocks [blk0[e], blk0[e+1]); float4 body (every piece is a multiple
+// of 4 floats, 16-B aligned).  advance = 0: an early part — it reads the step counter like every
+// part (same t, same bias corrections) but neither advances it nor takes a ticket.
 #define ADAM_MULTI_MAX 64
 struct AdamMulti {
   float* p[ADAM_MULTI_MAX]; float* g[ADAM_MULTI_MAX]; float* m[ADAM_MULTI_MAX]; float* v[ADAM_MULTI_MAX];
@@ -122,7 +125,7 @@ struct AdamMulti {
 __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a, const float* __restrict__ lr_p,
                                                          float* __restrict__ step_p, unsigned* __restrict__ done, float b1,
                                                          float b2, float eps, float wd, float gscale, int adamw,
-                                                         int zero_grad, int* __restrict__ seed) {
+                                                         int zero_grad, int* __restrict__ seed, int advance) {
   const float t = step_p[0] + 1.f;
   const float lr = lr_p[0];
   const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
@@ -159,7 +162,7 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a, const floa
     }
     if (pl) store_planes4(pl, a.ps, i, pa);
   }
-  finish_step(step_p, done, t, seed);
+  if (advance) finish_step(step_p, done, t, seed);
 }
 
 // p -= lr * (g*gscale + wd*p) with optional (heavy-ball, torch-style) momentum buffer
@@ -239,7 +242,7 @@ extern "C" int smi_adam(float* p, float* g, float* m, float* v, void* pbf, long 
 extern "C" int smi_adam_multi(float* const* p, float* const* g, float* const* m, float* const* v, void* const* pbf,
                               const long* n, int count, const float* lr, float* step, unsigned* done, float b1, float b2,
                               float eps, float wd, float gscale, int adamw, int zero_grad, void* const* pl, long ps,
-                              int* seed, hipStream_t st) {
+                              int* seed, int advance, hipStream_t st) {
   if (count < 1 || count > ADAM_MULTI_MAX) return -1;
   AdamMulti a{};
   long total4 = 0;
@@ -262,7 +265,7 @@ extern "C" int smi_adam_multi(float* const* p, float* const* g, float* const* m,
   a.count = count;
   a.ps = ps;
   hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)tot), dim3(256), 0, st, a, lr, step, done, b1, b2, eps, wd, gscale,
-                     adamw, zero_grad, seed);
+                     adamw, zero_grad, advance ? seed : nullptr, advance);
   SMI_CHECK_LAUNCH();
 }
 

@@ -395,7 +395,28 @@ def _flush_folds(C, fq):
 # fp32 step (profiles/r5_ab_wgrad_flush_points.log): the side-stream wgrad workgroups (one per CU,
 # 147 KiB of LDS) take CUs from the critical dgrad chain.
 WGRAD_OVERLAP = True
-_async = {"main": None, "dev": None, "hold": []}
+_async = {"main": None, "dev": None, "hold": [], "hold_ln": []}
+
+# ---- the cut: work launched at the overlapped flush ------------------------------------------
+# Cut hooks run on the side stream right after the overlapped flush has launched the queued
+# weight gradients (and, when a hook is registered, the queued LayerNorm folds): fn(launched
+# params).  Everything reported final before the cut plus the launched parameters are final once
+# the side stream reaches the hook's launches — the training-step runner updates them there
+# (sparkmi/train/runner.py _EarlyUpdate: the decoder's Adam beside the encoder's backward).
+# CONFIRMING[0] is True while flush_deferred reports the cut's held parameters final (after the
+# join): a listener that tracks when gradients become final can tell those reports apart.
+_cut_hooks = []
+CONFIRMING = [False]
+
+
+def add_cut_hook(fn):
+    _cut_hooks.append(fn)
+    return fn
+
+
+def remove_cut_hook(fn):
+    if fn in _cut_hooks:
+        _cut_hooks.remove(fn)
 
 
 def flush_groups_async(device):
@@ -409,27 +430,41 @@ def flush_groups_async(device):
     gq = list(_group_queue)
     _group_queue.clear()
     _group_bytes.clear()
+    hooks = list(_cut_hooks)
+    lq = list(_ln_queue) if hooks else []  # with a hook: the LayerNorm folds so far go out too
+    if lq:
+        _ln_queue.clear()
     main = torch.cuda.current_stream(dev)
     side = _side_stream(dev)
     side.wait_stream(main)
     with torch.cuda.stream(side):
         st = _native.stream()
-        _flush_groups(_native.C(), [e[:5] + (st,) for e in gq])
+        C = _native.C()
+        _flush_groups(C, [e[:5] + (st,) for e in gq])
+        if lq:
+            _flush_ln(C, [e[:7] + (st,) for e in lq])
+        if hooks:
+            launched = [p for e in gq for p in e[4] if p is not None] + [p for e in lq for p in e[6] if p is not None]
+            for fn in hooks:
+                fn(launched)
     if _async["main"] is None:
         _async["main"], _async["dev"] = main, dev
     _async["hold"].extend(gq)
+    _async["hold_ln"].extend(lq)
     _queue_flush()  # the end-of-backward flush joins the side stream
     return True
 
 
 def _join_async():
+    """Join the overlapped flush's side stream; returns its held (group entries, LayerNorm fold
+    entries)."""
     main = _async["main"]
     if main is None:
-        return []
+        return [], []
     main.wait_stream(_side_streams[_async["dev"]])
-    held = _async["hold"]
-    _async["main"], _async["dev"], _async["hold"] = None, None, []
-    return held
+    held, held_ln = _async["hold"], _async["hold_ln"]
+    _async["main"], _async["dev"], _async["hold"], _async["hold_ln"] = None, None, [], []
+    return held, held_ln
 
 
 def flush_deferred():
@@ -445,18 +480,25 @@ def flush_deferred():
     # launched before the join when no output is one an overlapped group (still running on the
     # side stream) writes: they then run beside it
     side_out = {t.data_ptr() for e in _async["hold"] for t in (e[2], e[3]) if t is not None}
+    side_out |= {t.data_ptr() for e in _async["hold_ln"] for t in (e[4], e[5])}
     early = not side_out.intersection(t.data_ptr() for e in gq + lq + fq for t in (e[2], e[3], e[4], e[5])
                                       if isinstance(t, torch.Tensor))
-    held = [] if early else _join_async()
+    held, held_ln = ([], []) if early else _join_async()
     if gq or lq or fq:
         C = _native.C()
         _flush_groups(C, gq)
         _flush_ln(C, lq)
         _flush_folds(C, fq)
     if early:
-        held = _join_async()
-    for e in held:  # overlapped groups: joined into the main stream, now final
-        grad_ready(*e[4])
+        held, held_ln = _join_async()
+    CONFIRMING[0] = True
+    try:
+        for e in held:  # overlapped groups: joined into the main stream, now final
+            grad_ready(*e[4])
+        for e in held_ln:
+            grad_ready(*e[6])
+    finally:
+        CONFIRMING[0] = False
     for e in lq:
         grad_ready(*e[6])
     for e in fq:

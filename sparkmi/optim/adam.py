@@ -53,6 +53,7 @@ class Adam(_FlatOptimizer):
         self.m = torch.zeros_like(flat.master)
         self.v = torch.zeros_like(flat.master)
         self.ranges = None
+        self._early = []  # flat ranges already updated this step (step_ranges); step() does the rest
 
     def shard(self, ranges):
         """ZeRO-1: update only the [start, end) ranges of the flat buffer (this data-parallel
@@ -68,27 +69,30 @@ class Adam(_FlatOptimizer):
         self.v = torch.zeros(o, dtype=torch.float32, device=self.flat.device)
         return self
 
-    def _step_shard(self):
+    def _multi(self, ranges, moff, advance):
+        """Update the flat ranges [s, e) (moments at moff) in launches of <= 64 ranges; only the
+        last launch advances the step counter (and the dropout seed) when ``advance``."""
         f = self.flat
-        if _native.use_native(f.master):
-            C = _native.C()
-            mp, gp, sp = f.master.data_ptr(), f.grad.data_ptr(), _native.ptr(f.shadow)
-            C.adam_multi([mp + 4 * s for s, _ in self.ranges], [gp + 4 * s for s, _ in self.ranges],
-                         [self.m.data_ptr() + 4 * o for o in self._moff], [self.v.data_ptr() + 4 * o for o in self._moff],
-                         [sp + 2 * s if sp else 0 for s, _ in self.ranges], [e - s for s, e in self.ranges],
+        C = _native.C()
+        mp, gp, sp = f.master.data_ptr(), f.grad.data_ptr(), _native.ptr(f.shadow)
+        for i in range(0, len(ranges), 64):
+            rs, os_ = ranges[i:i + 64], moff[i:i + 64]
+            last = advance and i + 64 >= len(ranges)
+            C.adam_multi([mp + 4 * s for s, _ in rs], [gp + 4 * s for s, _ in rs],
+                         [self.m.data_ptr() + 4 * o for o in os_], [self.v.data_ptr() + 4 * o for o in os_],
+                         [sp + 2 * s if sp else 0 for s, _ in rs], [e - s for s, e in rs],
                          self.lr_t.data_ptr(), self.step_t.data_ptr(), self.done_t.data_ptr(), self.b1, self.b2,
                          self.eps, self.weight_decay, self.grad_scale, int(self.adamw), int(self.zero_grad_after_step),
-                         [_native.ptr(f.planes) + 2 * s for s, _ in self.ranges] if f.planes is not None else [],
-                         f.plane_stride(), _native.ptr(self.bump_seed), _native.stream())
-            return
+                         [_native.ptr(f.planes) + 2 * s for s, _ in rs] if f.planes is not None else [],
+                         f.plane_stride(), _native.ptr(self.bump_seed) if last else 0, int(last), _native.stream())
+
+    def _torch_ranges(self, ranges, moff, t):
+        """CPU / fallback update of flat ranges at step count t (no advance)."""
+        f = self.flat
         with torch.no_grad():
-            self.step_t.add_(1)
-            if self.bump_seed is not None:
-                self.bump_seed.add_(1)
-            t = float(self.step_t.item())
             lr = float(self.lr_t.item())
             bc1, bc2 = 1 - self.b1 ** t, 1 - self.b2 ** t
-            for (s, e), o in zip(self.ranges, self._moff):
+            for (s, e), o in zip(ranges, moff):
                 p, g = f.master[s:e], f.grad[s:e] * self.grad_scale
                 m, v = self.m[o:o + e - s], self.v[o:o + e - s]
                 if self.weight_decay:
@@ -101,12 +105,74 @@ class Adam(_FlatOptimizer):
                 p.addcdiv_(m, v.sqrt() / (bc2 ** 0.5) + self.eps, value=-lr / bc1)
                 if self.zero_grad_after_step:
                     f.grad[s:e].zero_()
-            f.refresh_planes()
+                if f.shadow is not None:
+                    f.shadow[s:e].copy_(p.to(torch.bfloat16))
+
+    def _advance_torch(self):
+        with torch.no_grad():
+            self.step_t.add_(1)
+            if self.bump_seed is not None:
+                self.bump_seed.add_(1)
+        return float(self.step_t.item())
+
+    def _step_shard(self):
+        f = self.flat
+        if _native.use_native(f.master):
+            self._multi(self.ranges, self._moff, True)
+            return
+        t = self._advance_torch()
+        self._torch_ranges(self.ranges, self._moff, t)
+        f.refresh_planes()
+
+    def step_ranges(self, ranges):
+        """Update the parameters in the flat ranges [s, e) NOW, ahead of this step's ``step()``
+        (their gradients are final while the backward still produces others): same step count and
+        bias corrections, the counter is advanced by ``step()``, which then updates only the rest.
+        Element for element the same arithmetic as the one-launch update (tests pin it bitwise)."""
+        if self.ranges is not None:
+            raise RuntimeError("step_ranges: not with a ZeRO-1 sharded optimizer")
+        ranges = [(int(s), int(e)) for s, e in ranges if e > s]
+        if not ranges:
+            return
+        if _native.use_native(self.flat.master):
+            self._multi(ranges, [s for s, _ in ranges], False)
+        else:
+            self._torch_ranges(ranges, [s for s, _ in ranges], float(self.step_t.item()) + 1)
+            self.flat.refresh_planes()
+        self._early.extend(ranges)
+
+    def _rest(self):
+        """The flat ranges not updated by step_ranges this step (sorted, merged)."""
+        done = sorted(self._early)
+        self._early = []
+        out, pos = [], 0
+        for s, e in done:
+            if s > pos:
+                out.append((pos, s))
+            pos = max(pos, e)
+        if pos < self.flat.numel:
+            out.append((pos, self.flat.numel))
+        return out
 
     def step(self):
         f = self.flat
         if self.ranges is not None:
             return self._step_shard()
+        if self._early:
+            rest = self._rest()
+            if _native.use_native(f.master):
+                if rest:
+                    self._multi(rest, [s for s, _ in rest], True)
+                else:  # everything went early: the counter (and the seed) still advance once
+                    C = _native.C()
+                    C.step_inc(self.step_t.data_ptr(), _native.stream())
+                    if self.bump_seed is not None:
+                        C.seed_inc(self.bump_seed.data_ptr(), _native.stream())
+                return
+            t = self._advance_torch()
+            self._torch_ranges(rest, [s for s, _ in rest], t)
+            f.refresh_planes()
+            return
         if _native.use_native(f.master):
             C = _native.C()
             st = _native.stream()

@@ -25,6 +25,61 @@ import torch
 from ..ops import _grad
 from ..ops.embedding import join_plans
 
+# Optimizer update in two parts (single executor, an optimizer with step_ranges): the parameters
+# whose gradients are final at the backward's overlapped flush (the decoder's, once the backward
+# reaches the encoder: sparkmi/ops/_grad.py flush_groups_async) are updated right there on the
+# side stream, behind their weight-gradient group and beside the encoder's backward; step()
+# then updates the rest and advances the step counter.  Bitwise the one-launch update.
+EARLY_UPDATE = True
+
+
+class _EarlyUpdate:
+    """Learns, on the first backward, which parameters are final at the cut (reported final
+    before it, or launched by it, and never reported again after it), and from the next backward
+    on updates their flat ranges at the cut.  Reference: the per-step Adam of
+    pytorch_machine_translator.py:192-196 / distributed_lstm.py:193-195, split by readiness."""
+
+    def __init__(self, opt):
+        self.opt = opt
+        self.plan = None      # flat ranges updated at the cut
+        self.plan_ids = None
+        self.before, self.after, self.at = set(), set(), None
+        self.used = False
+
+    def begin(self):
+        self.before, self.after, self.at, self.used = set(), set(), None, False
+
+    def on_ready(self, p):
+        if _grad.CONFIRMING[0]:
+            return
+        (self.before if self.at is None else self.after).add(id(p))
+
+    def at_cut(self, launched):
+        if self.at is not None:
+            return  # one cut per backward
+        self.at = self.before | {id(p) for p in launched}
+        if self.plan is not None and self.plan_ids <= self.at:
+            self.opt.step_ranges(self.plan)  # on the side stream, behind the launched work
+            self.used = True
+
+    def end(self):
+        if self.at is None:
+            return
+        if self.plan is None:
+            flat = self.opt.flat
+            ids = self.at - self.after
+            rs = []
+            for p, o in zip(flat.params, flat.offsets):
+                if id(p) in ids:
+                    e = o + (p.numel() + 63) // 64 * 64
+                    if rs and rs[-1][1] == o:
+                        rs[-1] = (rs[-1][0], e)
+                    else:
+                        rs.append((o, e))
+            self.plan, self.plan_ids = rs, ids
+        elif self.used and self.plan_ids & self.after:
+            raise RuntimeError("early optimizer update: a parameter updated at the cut received more gradient after it")
+
 
 class StepRunner:
     def __init__(self, model, loss_fn, optimizer, ddp=None, graph=False, warmup_eager=3, split_fn=None,
@@ -106,13 +161,37 @@ class StepRunner:
                 and not torch.cuda.is_current_stream_capturing()):
             self.opt.bump_seed = rng.seed
 
+    def _early_update(self):
+        """The two-part optimizer update (EARLY_UPDATE), when it applies: one executor, an
+        optimizer over a flat buffer with step_ranges and no sharding."""
+        if not EARLY_UPDATE or self.ddp is not None or not hasattr(self.opt, "step_ranges"):
+            return None
+        if getattr(self.opt, "ranges", None) is not None or getattr(self.opt, "flat", None) is None:
+            return None
+        eu = getattr(self, "_eu", None)
+        if eu is None or eu.opt is not self.opt:
+            eu = self._eu = _EarlyUpdate(self.opt)
+        return eu
+
     def _fwd_bwd(self, *batch):
         _grad.reset_deferred()  # a previous backward that raised must not leave queued work behind
         self._advance_seed()
-        loss = self.loss_fn(self.model, *batch)
-        loss.backward(self._seed(loss))
-        _grad.join()
-        join_plans()  # a forward whose embedding backward did not run (frozen table): joined here
+        eu = self._early_update()
+        if eu is not None:
+            eu.begin()
+            _grad.add_listener(eu.on_ready)
+            _grad.add_cut_hook(eu.at_cut)
+        try:
+            loss = self.loss_fn(self.model, *batch)
+            loss.backward(self._seed(loss))
+            _grad.join()
+            join_plans()  # a forward whose embedding backward did not run (frozen table): joined here
+        finally:
+            if eu is not None:
+                _grad.remove_listener(eu.on_ready)
+                _grad.remove_cut_hook(eu.at_cut)
+        if eu is not None:
+            eu.end()
         return loss.detach()
 
     def _seed(self, loss):

@@ -425,6 +425,50 @@ def test_transformer_wgrad_overlap_bitwise(monkeypatch, graph):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("graph", [False, True])
+def test_transformer_early_update_bitwise(monkeypatch, graph, dtype):
+    """The two-part optimizer update (sparkmi/train/runner.py EARLY_UPDATE: the parameters final at
+    the backward's overlapped flush updated there on the side stream, step() updating the rest and
+    advancing the step) gives BITWISE the weights, moments, planes and step counter of the
+    one-launch update — eager and graph-captured StepRunner steps; the early part really ran."""
+    import copy
+    from sparkmi.data.synthetic import translation_pairs
+    from sparkmi.models.transformer import Transformer
+    from sparkmi.optim import Adam
+    from sparkmi.train import runner as R
+    from sparkmi.utils.flat import FlatParams
+    torch.manual_seed(0)
+    base = Transformer(d_model=128, ffn_hidden=256, num_heads=2, num_layers=2, max_sequence_length=32,
+                       src_vocab_size=96, tgt_vocab_size=96, seed=5, dtype=dtype)
+    src, tgt = translation_pairs(4, 32, 96, 96, seed=3)
+    src, tgt = src.to(dev), tgt.to(dev)
+    out = []
+    for early in (False, True):
+        monkeypatch.setattr(R, "EARLY_UPDATE", early)
+        m = copy.deepcopy(base).to(dev).train()
+        flat = FlatParams(m, shadow=dtype == "bf16")
+        opt = Adam(flat, lr=1e-3)
+        runner = R.StepRunner(m, lambda mm, a, b: mm.training_step_loss(a, b), opt, graph=graph)
+        for _ in range(6):
+            runner.step(src, tgt)
+        torch.cuda.synchronize()
+        if early:
+            eu = runner._eu
+            assert eu.plan and sum(e - s for s, e in eu.plan) > flat.numel // 4, eu.plan
+            assert eu.used
+        st = [p.detach().clone() for p in m.parameters()] + [flat.grad.clone(), opt.m.clone(), opt.v.clone(),
+                                                               opt.step_t.clone()]
+        if flat.planes is not None:
+            st.append(flat.planes.clone())
+        if flat.shadow is not None:
+            st.append(flat.shadow.clone())
+        out.append(st)
+    assert len(out[0]) == len(out[1])
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+
+
 def test_transformer_f32_loss_curve_matches_cpu():
     """60 Adam steps (dropout on, identical counter-based masks): the GPU fp32 trajectory stays on
     the CPU fp32 reference trajectory."""
