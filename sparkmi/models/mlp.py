@@ -9,6 +9,9 @@ from torch import nn
 from ..ops.mlp import mlp_grad_step, mlp_logits, mlp_loss, mlp_sgd_step
 
 
+# steps per launch of the multi-step SGD kernel (csrc/include/smi_mlp.h MLP_MAX_STEPS)
+MLP_MAX_STEPS = 32
+
 class MultilayerPerceptron(nn.Module):
     def __init__(self, layers=(4, 5, 4, 3), activation="sigmoid"):
         super().__init__()
@@ -79,13 +82,21 @@ class MultilayerPerceptron(nn.Module):
             # index mode: every batch is the fixed loader's (empty) buffer; the kernel reads the rows
             if any(getattr(b[0], "_smi_gather", None) is not g for b in batches):
                 raise RuntimeError("MultilayerPerceptron: index-mode and ordinary batches mixed")
-            out = mlp_sgd_steps([(g[1], g[2])], [l.weight for l in lins], [l.bias for l in lins], opt.lr_t,
-                                opt.step_t, self.activation, grad_scale=opt.grad_scale,
-                                index=(g[0], g[3], g[4], len(batches)))
-            if out is None:
-                raise RuntimeError("MultilayerPerceptron: index-mode batch but the fused step does not apply")
+            # the kernel runs at most MLP_MAX_STEPS steps per launch: a longer group (Trainer unroll
+            # > 32) is several consecutive launches, each advancing the device cursor
+            from ..ops.mlp import StepLosses
+            out, totals = StepLosses(), []
+            for i0 in range(0, len(batches), MLP_MAX_STEPS):
+                part = mlp_sgd_steps([(g[1], g[2])], [l.weight for l in lins], [l.bias for l in lins], opt.lr_t,
+                                     opt.step_t, self.activation, grad_scale=opt.grad_scale,
+                                     index=(g[0], g[3], g[4], min(MLP_MAX_STEPS, len(batches) - i0)))
+                if part is None:
+                    raise RuntimeError("MultilayerPerceptron: index-mode batch but the fused step does not apply")
+                out.extend(part)
+                totals.append(part.total)
+            out.total = totals[0] if len(totals) == 1 else torch.stack([t.reshape(()) for t in totals]).sum()
             return out
-        if (len(batches) > 32 or not all(self._fused_sgd_ok(opt, b[0]) for b in batches)
+        if (len(batches) > MLP_MAX_STEPS or not all(self._fused_sgd_ok(opt, b[0]) for b in batches)
                 or len({b[0].data_ptr() for b in batches}) != len(batches)):
             return None
         return mlp_sgd_steps(batches, [l.weight for l in lins], [l.bias for l in lins], opt.lr_t, opt.step_t,

@@ -425,6 +425,11 @@ class FFNFn(torch.autograd.Function):
         return dx, None, None, None, None, None, None, None, None
 
 
+# ConcatLinearFn.backward: launch the projection's dgrad before forking the queued weight-gradient
+# group onto the side stream (True) or after it (False, rounds 3-5)
+CONCAT_DGRAD_FIRST = True
+
+
 class ConcatLinearFn(torch.autograd.Function):
     """y = x @ W^T + b over linears stored back to back in the flat buffer (FlatParams.concat):
     one GEMM in place of several on the same input.  The consumers read column slices of y and
@@ -457,11 +462,17 @@ class ConcatLinearFn(torch.autograd.Function):
             grad_ready(*ctx.params)
             return None, None, None, None, None, None
         # every consumer of this projection (the decoder) has finished its backward: its queued
-        # weight gradients run on a side stream beside the rest (the encoder's backward)
-        _grad.flush_groups_async(g.device)
+        # weight gradients run on a side stream beside the rest (the encoder's backward).  The
+        # fork goes AFTER this projection's dgrad (CONCAT_DGRAD_FIRST): the side stream waits for
+        # it, so the group's one-workgroup-per-CU tiles do not take the chip from the dgrad the
+        # whole encoder backward waits on
+        if not CONCAT_DGRAD_FIRST:
+            _grad.flush_groups_async(g.device)
         g2 = g.reshape(-1, N)
         w = wm.view(N, K) if g2.dtype == torch.float32 else ws.view(N, K)
         dx = _dgrad(g2, w, wp=ctx.wp) if ctx.needs_input_grad[0] else None
+        if CONCAT_DGRAD_FIRST:
+            _grad.flush_groups_async(g.device)
         if ctx.wp is not None and ctx.x_planes is not None:
             _pl.attach(x2, ctx.x_planes)
             _pl.of(g2, kpad=N % 32 != 0)

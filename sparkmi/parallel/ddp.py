@@ -105,6 +105,7 @@ class DataParallel:
         # parameter index -> callable returning the step's touched row ids (row-sparse exchange),
         # and its optional fixed list capacity
         self._sparse, self._sparse_cap, self._sparse_pos = {}, {}, {}
+        self._sparse_flags = []  # (gathered overflow flags, nrow, cap) of fixed-capacity exchanges, for check()
         for p, fn in (sparse_rows or {}).items():
             fn, cap = fn if isinstance(fn, tuple) else (fn, None)
             self._sparse[flat.index[id(p)]] = fn
@@ -365,15 +366,26 @@ class DataParallel:
         first[1:] = srt[1:] != srt[:-1]
         uid = torch.where(first, srt, torch.full_like(srt, nrow))
         k = self._sparse_cap.get(i)
+        flag = None
         if k is None:
             # ranks may hold different numbers of ids (per-batch padded lengths): the longest list
             kt = torch.tensor([uid.numel()], dtype=torch.int64, device=g.device)
             dist.all_reduce(kt, op=dist.ReduceOp.MAX, group=self.group)
             k = int(kt.item())
-        elif uid.numel() > k:
-            raise ValueError(f"sparse_rows: {uid.numel()} ids exceed the list capacity {k}")
+        else:
+            # fixed capacity (no host sync): a rank over it must not leave its peers blocked in the
+            # gather below — it sends its first k ids plus an overflow flag in one extra
+            # slot of the id list (id nrow + 1: outside every row range, so the sums skip it), and
+            # check() raises on EVERY rank once any rank's flag is set
+            over = uid.numel() > k
+            if over:
+                uid = uid[:k]
+            flag = uid.new_full((1,), nrow + 1 if over else nrow)
         if k > uid.numel():
             uid = torch.cat([uid, uid.new_full((k - uid.numel(),), nrow)])
+        if flag is not None:
+            uid = torch.cat([uid, flag])
+            k += 1
         valid = uid < nrow
         rows = g.index_select(0, uid.clamp(max=nrow - 1)) * valid[:, None].to(g.dtype)
         # (gloo moves host tensors: device rows of a gloo group are staged through host memory)
@@ -402,6 +414,8 @@ class DataParallel:
                 m = ir < nrow
                 g.index_add_(0, ir[m], all_rows[r * k:(r + 1) * k][m])
         self.bytes_reduced += k * (8 + 4 * d)  # bytes this rank contributed
+        if flag is not None:
+            self._sparse_flags.append((all_ids.view(self.world, k)[:, -1], nrow, k - 1))
 
     def reshard_optimizer(self, opt, old_ranges):
         """Carry a sharded optimizer's moments over a bucket re-cut (the split-graph capture aligns
@@ -503,6 +517,11 @@ class DataParallel:
         log interval (Trainer) — inside a replayed HIP graph nothing else looks."""
         if self.ipc is not None:
             self.ipc.check()
+        flags, self._sparse_flags = self._sparse_flags, []
+        for f, nrow, cap in flags:
+            if int(f.max().item()) > nrow:
+                raise ValueError(f"sparse_rows: a rank's unique ids exceeded the list capacity {cap} (its gradient "
+                                 f"rows past the capacity were dropped); raise sparse_cap")
 
     def close(self):
         if self.ipc is not None:

@@ -378,11 +378,14 @@ class StepRunner:
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             self._pre_inline = True
+            reduced0 = self.ddp.bytes_reduced if self._dp else 0  # capture records, it reduces nothing
             try:
                 with torch.cuda.graph(g, pool=self._bound_pool):
                     loss = self._eager(*batch)
             finally:
                 self._pre_inline = False
+                if self._dp:
+                    self.ddp.bytes_reduced = reduced0  # the replay below counts the step
             if self._bound_pool is None:
                 self._bound_pool = g.pool()
             self._opt_in_graph = True
@@ -405,6 +408,7 @@ class StepRunner:
             g = torch.cuda.CUDAGraph()
             step_losses = []
             self._pre_inline = True
+            reduced0 = self.ddp.bytes_reduced if self._dp else 0
             try:
                 with torch.cuda.graph(g, pool=self._bound_pool):
                     fused = None
@@ -422,6 +426,8 @@ class StepRunner:
                         total = torch.stack([l.detach().float().reshape(()) for l in step_losses]).sum()
             finally:
                 self._pre_inline = False
+                if self._dp:
+                    self.ddp.bytes_reduced = reduced0
             if self._bound_pool is None:
                 self._bound_pool = g.pool()
             self._opt_in_graph = True

@@ -113,12 +113,14 @@ class Trainer:
         return self.runner.unroll
 
     def _group(self, it, U):
-        """Up to U batches of ``it`` without crossing a log / checkpoint / max_steps boundary."""
+        """Up to U batches of ``it`` without crossing a log / checkpoint / max_steps boundary.
+        The log boundary is the metrics logger's own (its step count restarts at 0 after a resume
+        and it clamps log_every to >= 1): the group's summed loss goes to its last step, so a group
+        spanning a record would credit one interval's losses to the next."""
         cfg = self.cfg
-        n = U
-        for every in (cfg.log_every, cfg.ckpt_every if self.ckpt is not None else 0):
-            if every:
-                n = min(n, every - self.step % every)
+        n = min(U, self.metrics.until_flush())
+        if self.ckpt is not None and cfg.ckpt_every:
+            n = min(n, cfg.ckpt_every - self.step % cfg.ckpt_every)
         if cfg.max_steps:
             n = min(n, cfg.max_steps - self.step)
         group = []

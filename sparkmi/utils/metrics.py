@@ -49,6 +49,11 @@ class MetricsLogger:
         """Steps accumulated since the last record."""
         return self._n
 
+    def until_flush(self):
+        """step() calls left until (and including) the one that writes the next record: a group
+        of steps whose summed loss is credited to its last step must not span a record."""
+        return self.every - self._step % self.every
+
     def step(self, loss=None, n_samples=0, **scalars):
         if self._t0 is None:
             self._sync(loss)

@@ -72,3 +72,42 @@ def test_sparse_exchange_fixed_capacity_and_eval_between_steps():
     dense, _ = _dp(False, eval_between=True)
     capped, _ = _dp(True, cap=B * T + 7, eval_between=True)
     assert torch.allclose(capped, dense, rtol=1e-6, atol=1e-7), float((capped - dense).abs().max())
+
+
+def _run_over(cap):
+    """Rank 0 alone exceeds the fixed capacity; both ranks must still complete the exchange and
+    then raise together at check().  Returns every rank's outcome (gathered to rank 0)."""
+    import torch
+    import torch.distributed as dist
+    from sparkmi.models.lstm import LSTM
+    from sparkmi.optim import Adam
+    from sparkmi.parallel import DataParallel, init_distributed, rank
+    from sparkmi.train.runner import StepRunner
+    from sparkmi.utils.flat import FlatParams
+    init_distributed()
+    torch.manual_seed(4)
+    m = LSTM(V, 32, 32, 4, num_layers=2, padding_idx=0, dropout=0.0).train()
+    flat = FlatParams(m)
+    ddp = DataParallel(flat, bucket_mb=0.05, sparse_rows=m.sparse_rows(cap=cap))
+    runner = StepRunner(m, lambda mm, x, y: mm.loss(x, y)[0], Adam(flat, lr=1e-2), ddp, graph=False)
+    r = rank()
+    hi = 120 if r == 0 else 3  # rank 0: many distinct ids; rank 1: ids 1-2 only (under the cap)
+    g = torch.Generator().manual_seed(5 + r)
+    runner.step(torch.randint(1, hi, (B, T), generator=g), torch.randint(0, 4, (B,), generator=g))
+    try:
+        ddp.check()
+        out = "ok"
+    except ValueError as e:
+        out = "raised: " + str(e)[:40]
+    outs = [None, None]
+    dist.all_gather_object(outs, out)
+    ddp.close()
+    return outs
+
+
+def test_sparse_capacity_overflow_raises_on_every_rank():
+    """a rank whose unique ids exceed the fixed capacity used to raise BEFORE the
+    all-gather and leave its peer blocked in it; now the overflow travels as a flag slot of the
+    gathered id list and check() raises on every rank."""
+    outs = Distributor(num_processes=2, use_gpu=False, log_sink=None, timeout=300).run(_run_over, 8)
+    assert all(o.startswith("raised") for o in outs), outs

@@ -153,10 +153,12 @@ def test_mlp_multi_step_kernel_bitwise_equals_single_steps(steps, n):
 
 
 @pytest.mark.gpu
-def test_mlp_trainer_index_mode_multistep_bitwise():
+@pytest.mark.parametrize("unroll,nb,log_every,steps", [(4, 10, 5, 23), (40, 50, 50, 95)])
+def test_mlp_trainer_index_mode_multistep_bitwise(unroll, nb, log_every, steps):
     """The MLP recipe path: Trainer + DeviceLoader(fixed=True) with the multi-step kernel reading
-    its shuffled rows from the dataset (index mode, 4 steps per launch, an epoch boundary inside the
-    run) trains bitwise the same parameters as the per-batch gather with one launch per step."""
+    its shuffled rows from the dataset (index mode, `unroll` steps per graph, an epoch boundary
+    inside the run) trains bitwise the same parameters as the per-batch gather with one launch per
+    step.  unroll 40 > the kernel's 32 steps per launch: two launches per group."""
     from sparkmi.data.dataset import DeviceLoader
     from sparkmi.optim import SGD
     from sparkmi.recipes.mlp import MLPConfig
@@ -165,9 +167,9 @@ def test_mlp_trainer_index_mode_multistep_bitwise():
     def run(fixed, unroll):
         torch.manual_seed(0)
         g = torch.Generator().manual_seed(8)
-        x = torch.rand(30 * 10, 4, generator=g) * 2 - 1
-        y = torch.randint(0, 3, (30 * 10,), generator=g)
-        cfg = MLPConfig(batch_size=30, lr=0.2, log_every=5, verbose=False, unroll=unroll, max_steps=23)
+        x = torch.rand(30 * nb, 4, generator=g) * 2 - 1
+        y = torch.randint(0, 3, (30 * nb,), generator=g)
+        cfg = MLPConfig(batch_size=30, lr=0.2, log_every=log_every, verbose=False, unroll=unroll, max_steps=steps)
         loader = DeviceLoader([x, y], 30, "cuda", shuffle=True, drop_last=True, seed=3, fixed=fixed)
         model = MultilayerPerceptron((4, 5, 4, 3))
         tr = Trainer(model, lambda m, a, b: m.loss(a, b), lambda flat: SGD(flat, lr=cfg.lr), cfg, "cuda", 0, 1, "t",
@@ -179,8 +181,8 @@ def test_mlp_trainer_index_mode_multistep_bitwise():
         return tr.flat.master.cpu().clone(), res, recs, tr.runner
 
     pa, ra, la, _ = run(False, 1)
-    pb, rb, lb, runner = run(True, 4)
-    assert ra["steps"] == rb["steps"] == 23
+    pb, rb, lb, runner = run(True, unroll)
+    assert ra["steps"] == rb["steps"] == steps
     assert runner.pre_step is None, "index mode engaged"
     assert runner._multi, "multi-step graphs ran"
     assert torch.equal(pa, pb)

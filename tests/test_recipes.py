@@ -168,3 +168,37 @@ def test_pinned_stream_loader_cpu_order():
         got = [b[1].numpy() for b in loader]
         assert len(got) == 6
         np.testing.assert_array_equal(np.concatenate(got), order[:48])
+
+
+def test_multistep_groups_follow_the_metrics_logger():
+    """Trainer._group never spans a metrics record: the boundary comes from the logger's own step
+    count (restarted at 0 after a resume, log_every clamped to >= 1), so a group's summed loss is
+    credited to the interval it belongs to (resume at step % log_every != 0, and
+    log_every = 0, both used to mis-credit)."""
+    from types import SimpleNamespace
+
+    from sparkmi.train.trainer import Trainer
+    from sparkmi.utils.metrics import MetricsLogger
+
+    def sizes(step, log_every, ckpt_every=0, U=16, n=40):
+        t = Trainer.__new__(Trainer)
+        t.cfg = SimpleNamespace(log_every=log_every, ckpt_every=ckpt_every, max_steps=0)
+        t.metrics = MetricsLogger(None, every=log_every)
+        t.ckpt = object() if ckpt_every else None
+        t.step = step
+        it, out = iter(range(n)), []
+        while True:
+            g = t._group(it, U)
+            if not g:
+                return out, t.metrics
+            out.append(len(g))
+            for _ in g:
+                t.step += 1
+                t.metrics.step(torch.tensor(1.0), 1)
+
+    out, m = sizes(13, 10)  # resumed at 13: the logger flushes every 10 of ITS steps
+    assert out[:4] == [10, 10, 10, 10] and all(r["loss"] == 1.0 for r in m.records)
+    out, m = sizes(0, 0, n=5)  # log_every 0 -> every step is a record
+    assert out == [1] * 5 and [r["loss"] for r in m.records] == [1.0] * 5
+    out, _ = sizes(13, 10, ckpt_every=8, n=24)  # checkpoints stay on global-step multiples
+    assert out[0] == 3 and all(x <= 8 for x in out)
