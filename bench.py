@@ -122,18 +122,6 @@ def spawn_ranks(n, argv):
     return rc
 
 
-def transformer_flops_per_sample(layers, seq, vocab, d=512, ffn=1024):
-    """Matmul FLOPs of one training sample (forward + backward = 3x forward): per token, each
-    encoder layer's QKV / out-projection / FFN GEMMs, each decoder layer's self QKV / out,
-    cross Q / KV / out and FFN GEMMs, the vocab projection, plus QK^T and PV of the 3 attention
-    sites per layer pair (63.4 GFLOP at L6 S256 V10k)."""
-    enc = 2 * d * (3 * d + d + 2 * ffn)
-    dec = 2 * d * (3 * d + d + d + 2 * d + d + 2 * ffn)
-    attn = 3 * 4 * seq * d
-    per_token = layers * (enc + dec + attn) + 2 * d * vocab
-    return 3 * per_token * seq
-
-
 def _sync(device):
     import torch
     if device.type == "cuda":
@@ -450,7 +438,7 @@ def bench_transformer(args, rank, world, device, dtype, zero=False):
     precision, or 'bf16' = bf16 activations/weights with fp32 master weights and fp32 accumulate)."""
     import torch
     from sparkmi.data.synthetic import copy_pairs, translation_pairs
-    from sparkmi.models.transformer import Transformer
+    from sparkmi.models.transformer import Transformer, transformer_flops_per_sample
     from sparkmi.optim import Adam
     from sparkmi.parallel.ddp import DataParallel
     from sparkmi.train.runner import StepRunner

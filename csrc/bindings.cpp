@@ -48,8 +48,6 @@ int smi_attn_bwd(const AttnBwdArgs*, const void*, float*, hipStream_t);
 int smi_ce_fwd(const void*, int, const long long*, int, int, long long, float*, float*, float*, float*, hipStream_t);
 int smi_ce_bwd(const void*, int, const long long*, int, int, long long, const float*, const float*, const float*, void*,
                void*, long, long, hipStream_t);
-int smi_ce_fwd_part(const void*, int, const float*, const long long*, int, int, long long, float*, float*, float*, float*,
-                    hipStream_t);
 int smi_emb_fwd(const long long*, const void*, const float*, void*, long, int, int, const uint32_t*, uint32_t, uint32_t, float,
                 hipStream_t);
 int smi_emb_bwd(const long long*, const void*, float*, long, int, long long, const uint32_t*, uint32_t, uint32_t, float, long,
@@ -96,7 +94,8 @@ int smi_gemm_wgrad_group(const void* const*, const long*, const void* const*, co
                          const int*, const int*, const int*, int, hipStream_t);
 int smi_cnn(const CNNArgs*, hipStream_t);
 int smi_cnn_hand_floats(int C);
-int smi_cnn_fused_ok(int, int, int, int);
+int smi_cnn_fused_ok(int, int, int, int, int);
+int smi_cnn_max_batch(int, int, int, int);
 long smi_emb_pair_max(long);
 int smi_emb_plan_algo(long, long);
 int smi_emb_plan(const long long*, long, long long, long, void*, hipStream_t);
@@ -242,12 +241,6 @@ PYBIND11_MODULE(_C, m) {
                      u row_loss, u st) {
     chk(smi_ce_fwd(P(logits), is_bf16, (const long long*)labels, M, V, ignore, PF(lse), PF(count), PF(loss),
                    PF(row_loss), S(st)), "ce_fwd");
-  });
-  // the loss from the vocab projection's epilogue statistics (gemm_sp lse_part): no logits pass
-  m.def("ce_fwd_part", [](u part, int nt, u logits, u labels, int M, int V, long long ignore, u lse, u count, u loss,
-                          u row_loss, u st) {
-    chk(smi_ce_fwd_part(P(part), nt, PF(logits), (const long long*)labels, M, V, ignore, PF(lse), PF(count), PF(loss),
-                        PF(row_loss), S(st)), "ce_fwd_part");
   });
   // planes / ldp / pps: optional split planes of the fp32 gradient (0 for none)
   m.def("ce_bwd", [](u logits, int is_bf16, u labels, int M, int V, long long ignore, u lse, u count, u dloss, u grad,
@@ -461,10 +454,9 @@ PYBIND11_MODULE(_C, m) {
   // (plane stride aps / bps), optional plane output P of the epilogue result
   m.def("gemm_sp", [](int mode, u A, long lda, long aps, u B, long ldb, long bps, int M, int N, int K, int kpad, u C,
                       long ldc, u Pp, long ldp, long pps, int beta_acc, u bias, int relu, u resid, long ldr, u dact_y,
-                      long ldy, u seedp, uint32_t salt, uint32_t thresh, float dscale, u bias_grad, u lse_part, u mask,
+                      long ldy, u seedp, uint32_t salt, uint32_t thresh, float dscale, u bias_grad, u mask,
                       long ldm, u st) {
     GemmSpArgs g{};
-    g.lse_part = (float*)lse_part;
     g.mask = (unsigned char*)mask; g.ldm = ldm;
     g.mode = mode; g.A = (const unsigned short*)A; g.lda = lda; g.aps = aps;
     g.B = (const unsigned short*)B; g.ldb = ldb; g.bps = bps; g.M = M; g.N = N; g.K = K; g.kpad = kpad;
@@ -625,7 +617,11 @@ PYBIND11_MODULE(_C, m) {
         "summing half of the embedding backward after emb_plan");
   m.def("emb_pair", [](int set) { return smi_emb_pair(set); },
         "deterministic embedding backward: 1 = pair-compare (<= 8192 tokens), 0 = bucketed lists; -1 queries");
-  m.def("cnn_fused_ok", [](int C, int cin, int classes, int B) { return smi_cnn_fused_ok(C, cin, classes, B) != 0; });
+  m.def("cnn_fused_ok", [](int C, int cin, int classes, int B, int bf16) {
+        return smi_cnn_fused_ok(C, cin, classes, B, bf16) != 0; },
+        "whether a fused CNN step (one launch: forward, backward, SGD) takes batch B for this model and dtype");
+  m.def("cnn_max_batch", [](int C, int cin, int classes, int bf16) { return smi_cnn_max_batch(C, cin, classes, bf16); },
+        "the largest batch a fused CNN step takes for this model and dtype (the LDS of the fused tail)");
   m.def("cnn_hand_floats", [](int C) { return smi_cnn_hand_floats(C); });  // 0: weight-gradient helpers off
 
   m.def("lstm_supported", [](int E, int H, int L, int C) { return smi_lstm_supported(E, H, L, C) != 0; });

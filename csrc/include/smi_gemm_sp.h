@@ -24,8 +24,5 @@ struct GemmSpArgs {
   float* bias_grad;                 // WGRAD: += row sums of A (dY^T 1, the bias gradient)
   unsigned char* mask; long ldm;    // FWD (out): bit e of mask[row][col / 4] = output (col + e) > 0;
                                     // DGRAD (in): the same mask replaces dact_y (relu' x dropout)
-  float* lse_part;                  // FWD: per (128-column tile, row) softmax statistics (max, sum
-                                    // exp(x - max)) of the output row, float2 [ceil(N/128)][M]: the
-                                    // cross-entropy forward fused into the vocab projection
   int a_bytes, b_bytes;             // per-plane operand extents (filled by the launcher)
 };

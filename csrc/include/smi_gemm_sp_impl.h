@@ -68,7 +68,7 @@ __device__ unsigned long long* g_sp_stamps;
 
 // SE_BF: bf16 activations (csrc/kernels/gemm_bf.hip): resid / dact_y are read as bf16 and the
 // non-accumulating C output is written as bf16 (weight gradients stay fp32 accumulations)
-enum : int { SE_BIAS = 1, SE_RELU = 2, SE_DROP = 8, SE_RESID = 16, SE_DACT = 32, SE_ACC = 64, SE_LSE = 128,
+enum : int { SE_BIAS = 1, SE_RELU = 2, SE_DROP = 8, SE_RESID = 16, SE_DACT = 32, SE_ACC = 64,
               SE_DMASK = 256, SE_BF = 512 };
 enum : int { SO_C = 1, SO_P = 2, SO_M = 4 };  // epilogue outputs: fp32 C, planes P, positivity mask
 
@@ -196,13 +196,11 @@ __device__ __forceinline__ void sp_store_tile(const GemmSpArgs& g, const float* 
   for (int q = 0; q < TM / RS; ++q) {
     const int rl = (tid >> 5) + RS * q, row = m0 + rl;
     if (row >= g.M) continue;  // uniform over the 32 lanes that share the row
-    if (!(EPI & SE_LSE) && col >= g.N) continue;
+    if (col >= g.N) continue;
     const float4 t = *(const float4*)(ep + rl * SP_EPI_PITCH + c4);
     float v[4] = {t.x, t.y, t.z, t.w};
     const long cidx = (long)row * g.ldc + col;
-    if ((EPI & SE_LSE) && col >= g.N) {
-      // past the last column: only joins the row statistics below
-    } else if (full_cols) {
+    if (full_cols) {
       float4 rs = make_float4(0.f, 0.f, 0.f, 0.f), dy = rs, cc = rs;
       if constexpr ((EPI & SE_BF) != 0) {
         if (EPI & SE_RESID) {
@@ -266,21 +264,6 @@ __device__ __forceinline__ void sp_store_tile(const GemmSpArgs& g, const float* 
         v[e] = x;
       }
       if (OUT & SO_M) g.mask[(long)row * g.ldm + (col >> 2)] = (unsigned char)bits;
-    }
-    if constexpr ((EPI & SE_LSE) != 0) {
-      // the row's (max, sum exp) over this tile's 128 columns: the 32 lanes of the half-wave hold
-      // the row's 4-column groups; one lane stores the pair (fp32, natural-log units)
-      float lm = -INFINITY;
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (col + e < g.N) lm = fmaxf(lm, v[e]);
-      const float rm = half_wave_max(lm);  // DPP: no LDS-crossbar round trips
-      float ls = 0.f;
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (col + e < g.N) ls += __expf(v[e] - rm);
-      const float rsum = half_wave_sum(ls);
-      if ((tid & 31) == 0) ((float2*)g.lse_part)[(long)(n0 >> 7) * g.M + row] = make_float2(rm, rsum);
     }
   }
 }

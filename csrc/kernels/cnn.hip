@@ -15,6 +15,8 @@
 // Per-image gradients go to a slab [B][P] (P = all parameters, packed in the order
 // w1 b1 w2 b2 w3 b3 w4 b4 wfc bfc); cnn_grad_reduce sums the slab over images (fixed order:
 // bit-reproducible) and accumulates into the model's gradient buffers.
+#include <algorithm>
+
 #include "smi_common.h"
 #include "smi_cnn.h"
 #include <type_traits>
@@ -1497,9 +1499,11 @@ extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
   if (g.C < 1 || g.C > CNN_MAXC || g.cin < 1 || g.cin > 4 || g.classes < 1 || g.classes > 16) return -1;
   g.wstage = g.bf16 ? (g.C == 10 ? 2 : 1) : 0;
   if (g.wstage == 1 && cnn_lds_bytes(g) > 160 * 1024) g.wstage = 0;  // the weights then stay global
-  const size_t lds = cnn_lds_bytes(g);
+  // the fused tail reuses the kernel's LDS: the allocation covers the larger of the two (the
+  // body's ~125 KiB already keeps one workgroup per CU, so a few KiB more cost no occupancy)
+  size_t lds = cnn_lds_bytes(g);
+  if (g.fused) lds = std::max(lds, cnn_tail_lds(g.C, g.cin, g.classes, g.B));
   if (lds > 160 * 1024) return -1;
-  if (g.fused && cnn_tail_lds(g.C, g.cin, g.classes, g.B) > lds) return -1;
   // channel capacity 10 (the reference model's hidden_units) gets exact compile-time groups
   // (LDS residency caps C at 13 for 1-channel input, so no exact instance above 10)
   auto kern = g.bf16 ? (g.C == 10 ? cnn_kernel<10, true, true> : cnn_kernel<CNN_MAXC, false, true>)
@@ -1512,11 +1516,23 @@ extern "C" int smi_cnn(const CNNArgs* args, hipStream_t st) {
 // floats of one image's hand-off area for the weight-gradient helpers (0: helpers not available)
 extern "C" int smi_cnn_hand_floats(int C) { return (C >= 1 && C <= CNN_MAXC) ? cnn_hand_f(C) : 0; }
 
-extern "C" int smi_cnn_fused_ok(int C, int cin, int classes, int B) {
+// The fused step's batch limit: the counter block (CNN_MAXB) and the fused tail's LDS, which with the
+// body's (dtype-dependent: the exact bf16 C = 10 instance keeps its fragment tables there, wstage 2
+// — the same choice as smi_cnn) must fit one 160 KiB allocation.
+extern "C" int smi_cnn_fused_ok(int C, int cin, int classes, int B, int bf16) {
+  if (C < 1 || C > CNN_MAXC || cin < 1 || cin > 4 || classes < 1 || classes > 16) return 0;
   CNNArgs g{};
-  g.C = C; g.cin = cin; g.classes = classes;
+  g.C = C; g.cin = cin; g.classes = classes; g.bf16 = bf16;
+  g.wstage = bf16 ? (C == 10 ? 2 : 1) : 0;
+  if (g.wstage == 1 && cnn_lds_bytes(g) > 160 * 1024) g.wstage = 0;
   const int P = C * cin * 9 + C + 3 * (C * C * 9 + C) + classes * C * 49 + classes;
-  return P % 4 == 0 && B >= 1 && B <= CNN_MAXB && cnn_tail_lds(C, cin, classes, B) <= cnn_lds_bytes(g);
+  return P % 4 == 0 && B >= 1 && B <= CNN_MAXB && std::max(cnn_lds_bytes(g), cnn_tail_lds(C, cin, classes, B)) <= 160 * 1024;
+}
+// the largest batch a fused step takes for this model and dtype (0: none)
+extern "C" int smi_cnn_max_batch(int C, int cin, int classes, int bf16) {
+  for (int B = CNN_MAXB; B >= 1; --B)
+    if (smi_cnn_fused_ok(C, cin, classes, B, bf16)) return B;
+  return 0;
 }
 
 extern "C" int smi_cnn_reduce(const CNNArgs* args, hipStream_t st) {

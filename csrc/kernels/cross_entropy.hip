@@ -194,45 +194,6 @@ extern "C" int smi_ce_fwd(const void* logits, int is_bf16, const long long* labe
   SMI_CHECK_LAUNCH();
 }
 
-// Forward from the vocab projection's epilogue statistics (csrc/include/smi_gemm_sp_impl.h,
-// SE_LSE): part[t][row] = (max, sum exp(x - max)) of row's logits in 128-column tile t.  One
-// thread per row merges the tiles in order (deterministic), then reads its target's logit: the
-// logits are never streamed again for the loss (ce_fwd_kernel's 4 B/logit pass).
-// one wave per row: lane l merges tiles l, l + 64, ... in order, then a fixed-shape cross-lane
-// merge (wave max, rescaled wave sum): deterministic
-__global__ __launch_bounds__(256) void ce_fwd_part_kernel(const float2* __restrict__ part, int nt,
-                                                          const float* __restrict__ logits,
-                                                          const long long* __restrict__ labels, int M, int V,
-                                                          long long ignore, float* __restrict__ lse_out,
-                                                          float* __restrict__ row_loss) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (row >= M) return;  // uniform per wave
-  float m = -INFINITY, s = 0.f;
-  for (int t = lane; t < nt; t += 64) {
-    const float2 p = part[(long)t * M + row];
-    const float nm = fmaxf(m, p.x);
-    s = (nm == -INFINITY) ? 0.f : s * __expf(m - nm) + p.y * __expf(p.x - nm);
-    m = nm;
-  }
-  const float wm = wave_max(m);
-  const float ws = wave_sum(m == -INFINITY ? 0.f : s * __expf(m - wm));
-  if (lane == 0) {
-    const float lse = wm + __logf(ws);
-    lse_out[row] = lse;
-    const long long lab = labels[row];
-    row_loss[row] = (lab != ignore) ? lse - logits[(long)row * V + lab] : 0.f;
-  }
-}
-
-extern "C" int smi_ce_fwd_part(const void* part, int nt, const float* logits, const long long* labels, int M, int V,
-                               long long ignore, float* lse, float* count, float* loss, float* row_loss, hipStream_t st) {
-  if (!row_loss || !part || nt < 1 || nt != (V + 127) / 128 || ((uintptr_t)part & 7)) return -1;
-  hipLaunchKernelGGL(ce_fwd_part_kernel, dim3((M + 3) / 4), dim3(256), 0, st, (const float2*)part, nt, logits,
-                     labels, M, V, ignore, lse, row_loss);
-  hipLaunchKernelGGL(ce_finalize_kernel, dim3(1), dim3(1024), 0, st, labels, row_loss, M, ignore, count, loss);
-  SMI_CHECK_LAUNCH();
-}
-
 extern "C" int smi_ce_bwd(const void* logits, int is_bf16, const long long* labels, int M, int V, long long ignore,
                           const float* lse, const float* count, const float* dloss, void* grad, void* planes, long ldp,
                           long pps, hipStream_t st) {

@@ -88,8 +88,7 @@ extern "C" int smi_gemm_sp(const GemmSpArgs* args, hipStream_t st) {
   const int nwg = t256 ? ((g.M + 255) / 256) * ((g.N + 127) / 128) : ((g.M + 127) / 128) * ((g.N + 127) / 128);
   const dim3 grid((unsigned)nwg);
   int epi = 0;
-  if (g.mode == 0) epi = (g.bias ? SE_BIAS : 0) | (g.relu == 1 ? SE_RELU : 0) | (g.thresh ? SE_DROP : 0) |
-                        (g.lse_part ? SE_LSE : 0);
+  if (g.mode == 0) epi = (g.bias ? SE_BIAS : 0) | (g.relu == 1 ? SE_RELU : 0) | (g.thresh ? SE_DROP : 0);
   else if (g.mode == 1) epi = (g.resid ? SE_RESID : 0) | (g.dact_y ? SE_DACT : 0) | (g.mask ? SE_DMASK : 0);
   if (g.beta_acc) epi |= SE_ACC;
   if (g.mode == 1) return smi_sp_launch_dgrad(g, epi, out, grid, t256, st);  // csrc/kernels/gemm_sp_dgrad.hip
@@ -124,10 +123,6 @@ extern "C" int smi_gemm_sp(const GemmSpArgs* args, hipStream_t st) {
     case SE_BIAS: SPF_OUT(SE_BIAS); break;
     case SE_BIAS | SE_RELU: SPF_OUT(SE_BIAS | SE_RELU); break;
     case SE_BIAS | SE_RELU | SE_DROP: SPF_OUT(SE_BIAS | SE_RELU | SE_DROP); break;
-    case SE_BIAS | SE_LSE:  // the vocab projection + cross-entropy statistics (fp32 output only)
-      if (out != SO_C || ((uintptr_t)g.lse_part & 7)) return -1;
-      SPF(SE_BIAS | SE_LSE, SO_C);
-      break;
     default: return -1;
   }
 #undef SPF_OUT

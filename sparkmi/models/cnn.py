@@ -42,6 +42,32 @@ class FashionMNISTModel(nn.Module):
     def forward(self, x):
         return cnn_logits(x, self.param_list(), self.conv_dtype == "bf16")
 
+    def fused_batch_limit(self):
+        """The largest batch the one-launch fused step takes for this model and its dtype (the
+        fused tail stages every image's fc row in the kernel's LDS; csrc/kernels/cnn.hip
+        smi_cnn_max_batch); 0 without the native library."""
+        from .. import _native
+        if not _native.has_native():
+            return 0
+        p = self.param_list()
+        return int(_native.C().cnn_max_batch(p[0].shape[0], p[0].shape[1], p[8].shape[0], int(self.conv_dtype == "bf16")))
+
+    def _fused_ok(self, bs):
+        """Whether a fused step takes batch ``bs``; warns once per model when the batch alone (past
+        fused_batch_limit) sends an otherwise fused-eligible step to the multi-launch path."""
+        from .. import _native
+        p = self.param_list()
+        ok = bool(_native.C().cnn_fused_ok(p[0].shape[0], p[0].shape[1], p[8].shape[0], bs,
+                                           int(self.conv_dtype == "bf16")))
+        if not ok and not getattr(self, "_warned_batch", False):
+            lim = self.fused_batch_limit()
+            if lim and bs > lim:
+                import warnings
+                warnings.warn(f"FashionMNISTModel: batch {bs} exceeds the fused step's limit {lim} for this model "
+                              f"({self.conv_dtype}); running the multi-launch step", RuntimeWarning, stacklevel=3)
+                self._warned_batch = True
+        return ok
+
     def gather_in_step(self, opt, ddp, x):
         """True when every training step of this model will run as one of its fused kernels, which
         then read their shuffled batch straight from the dataset (index mode: perm[cursor * B + i],
@@ -51,8 +77,7 @@ class FashionMNISTModel(nn.Module):
         from ..optim.sgd import SGD
         params = self.param_list()
         if (not x.is_cuda or not _native.use_native(x) or x.dim() != 4 or getattr(self, "_smi_flat", None) is None
-                or not _native.C().cnn_fused_ok(params[0].shape[0], params[0].shape[1], params[8].shape[0],
-                                                 x.shape[0])):
+                or not self._fused_ok(x.shape[0])):
             return False
         if ddp is not None:
             return True  # fused_grad_step
@@ -83,7 +108,7 @@ class FashionMNISTModel(nn.Module):
         if (not x.is_cuda or not _native.use_native(x) or not isinstance(opt, SGD) or opt.momentum
                 or opt.weight_decay or opt.grad_scale != 1.0 or getattr(opt, "ranges", None) is not None
                 or flat is None or getattr(flat, "planes", None) is not None or x.dim() != 4
-                or not _native.C().cnn_fused_ok(params[0].shape[0], params[0].shape[1], params[8].shape[0], bs)):
+                or not self._fused_ok(bs)):
             if index is not None:
                 raise RuntimeError("FashionMNISTModel: index-mode batch but the fused step does not apply")
             return None
@@ -107,7 +132,7 @@ class FashionMNISTModel(nn.Module):
         bs = index[0] if index is not None else x.shape[0]
         if (not x.is_cuda or not _native.use_native(x) or x.dim() != 4
                 or getattr(self, "_smi_flat", None) is None
-                or not _native.C().cnn_fused_ok(params[0].shape[0], params[0].shape[1], params[8].shape[0], bs)):
+                or not self._fused_ok(bs)):
             if index is not None:
                 raise RuntimeError("FashionMNISTModel: index-mode batch but the fused step does not apply")
             return None

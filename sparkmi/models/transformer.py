@@ -105,17 +105,23 @@ class SentenceEmbedding(nn.Module):
                          out_dtype=dtype, flush_wgrad=self.flush_wgrad)
 
 
+
+def transformer_flops_per_sample(layers, seq, vocab, d=512, ffn=1024):
+    """Matmul FLOPs of one training sample (forward + backward = 3x forward): per token, each
+    encoder layer's QKV / out-projection / FFN GEMMs, each decoder layer's self QKV / out, cross
+    Q / KV / out and FFN GEMMs, the vocab projection, plus QK^T and PV of the 3 attention sites per
+    layer pair (63.4 GFLOP at L6 S256 V10k).  The one definition bench.py and the
+    translator recipe report TFLOP/s with."""
+    enc = 2 * d * (3 * d + d + 2 * ffn)
+    dec = 2 * d * (3 * d + d + d + 2 * d + d + 2 * ffn)
+    attn = 3 * 4 * seq * d
+    return 3 * (layers * (enc + dec + attn) + 2 * d * vocab) * seq
+
+
 def _gp(t):
     """A sublayer-internal tensor with one consumer (attention core / LayerNorm / loss): its
     gradient may come back as split planes only (sparkmi/ops/planes.py, SMI_PLANES_ONLY)."""
     return _pl.mark_grad_planes_ok(t)
-
-
-# fp32 GPU path: the vocab projection's epilogue computes the cross-entropy row statistics
-# (True).  Off: step-time neutral (-0.01 ms, profiles/r3b_ab_planes_only.txt), and its tile-merged
-# logsumexp moves the early flagship trajectory off the CPU reference by more than the standalone
-# pass (tests/test_f32_gpu.py::test_transformer_f32_flagship_trajectory); tests exercise it
-CE_FUSED = False
 
 
 class MultiHeadAttention(nn.Module):
@@ -361,7 +367,7 @@ class Transformer(nn.Module):
         out = self.decoder(x, y, self_mode, cross_mode, kp, getattr(self, "_smi_flat", None))
         # fp32 GPU: the epilogue also reduces each logits row (softmax statistics per 128 columns),
         # so the cross-entropy forward never re-reads the logits (sparkmi/ops/loss.py)
-        return linear(out, self.linear.weight, self.linear.bias, lse_stats=CE_FUSED)
+        return linear(out, self.linear.weight, self.linear.bias)
 
     def loss(self, logits, target):
         """Token CE ignoring pad, mean over non-pad targets (pytorch_machine_translator.py:182-188)."""
@@ -404,7 +410,7 @@ class Transformer(nn.Module):
             segments.append((leaf, x))
             x, start = leaf, c
         out = self.decoder(x, dec_in, self_mode, cross_mode, kp, getattr(self, "_smi_flat", None))
-        logits = _gp(linear(out, self.linear.weight, self.linear.bias, lse_stats=CE_FUSED))
+        logits = _gp(linear(out, self.linear.weight, self.linear.bias))
         return self.loss(logits, target), segments[::-1]
 
 

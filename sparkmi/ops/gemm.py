@@ -181,12 +181,9 @@ def _sp_ok(*ts):
                              and (t.dim() < 2 or t.stride(-2) % 4 == 0)) for t in ts)
 
 
-def sp_fwd(xp, wp, M, N, K, bias=None, act=0, rng=None, salt=0, thresh=0, dscale=1.0, out_planes=False,
-           lse_part=None, mask=None):
+def sp_fwd(xp, wp, M, N, K, bias=None, act=0, rng=None, salt=0, thresh=0, dscale=1.0, out_planes=False, mask=None):
     """y[M,N] = dropout(act(x @ w^T + bias)) from planes xp [3,M,>=K], wp [3,N,>=K].  Returns
     (y, y_planes or None), or None when the kernel does not cover the case (caller falls back).
-    ``lse_part``: fp32 [ceil(N/128), M, 2] filled with each row's per-128-column softmax
-    statistics (max, sum exp(y - max)) by the epilogue (the fused cross-entropy forward).
     ``mask``: uint8 [M, ceil(N/4)] receiving bit e of column group c = (y[:, 4c + e] > 0) INSTEAD
     of the fp32 y (returned None; planes required) — the FFN hidden activation's sign for the
     linear2 dgrad epilogue."""
@@ -202,8 +199,7 @@ def sp_fwd(xp, wp, M, N, K, bias=None, act=0, rng=None, salt=0, thresh=0, dscale
                              # ldc = N without an fp32 output: the dropout hash index is row * ldc + col
                              M, N, K, 0, _native.ptr(y), y.stride(0) if y is not None else N, _native.ptr(yp), N,
                              yp.stride(0) if yp is not None else 0, 0, _native.ptr(bias), int(act), 0, 0, 0, 0,
-                             rng.ptr() if rng is not None else 0, salt, thresh, dscale, 0, _native.ptr(lse_part),
-                             _native.ptr(mask), mask.stride(0) if mask is not None else 0, _native.stream())
+                             rng.ptr() if rng is not None else 0, salt, thresh, dscale, 0, _native.ptr(mask), mask.stride(0) if mask is not None else 0, _native.stream())
     return (y, yp) if ok else None
 
 

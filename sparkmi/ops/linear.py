@@ -169,34 +169,23 @@ def compute_weight(p: torch.Tensor, dtype) -> torch.Tensor:
     return p.detach() if dtype == torch.float32 else bf16_weight(p)
 
 
-def _fwd_sp(x2, wp, N, bias, act, p, rng, salt, out_planes=False, lse_stats=False, relu_mask=None):
-    """fp32 forward on the split-plane GEMM (x2's planes: cached or split now); None if not covered.
-    ``lse_stats``: the epilogue also writes per-row softmax statistics, attached to y for the
-    cross-entropy that consumes it (sparkmi/ops/loss.py)."""
+def _fwd_sp(x2, wp, N, bias, act, p, rng, salt, out_planes=False, relu_mask=None):
+    """fp32 forward on the split-plane GEMM (x2's planes: cached or split now); None if not covered."""
     M, K = x2.shape
     if wp is None or not G.SP or not G._sp_ok(x2) or act not in (0, 1):
         return None
-    part = None
-    if lse_stats and bias is not None and act == 0 and p == 0 and not out_planes:
-        part = torch.empty((N + 127) // 128, M, 2, device=x2.device, dtype=torch.float32)
     if relu_mask is not None:  # planes + positivity mask, no fp32 tensor (FFNFn)
         r = G.sp_fwd(_pl.of(x2), wp, M, N, K, bias, act, rng, salt, _rng.threshold(p), _rng.scale(p),
                      out_planes=True, mask=relu_mask)
         if r is not None:
             return _pl.placeholder((M, N), r[1], x2.device)
     r = G.sp_fwd(_pl.of(x2), wp, M, N, K, bias, act, rng, salt, _rng.threshold(p), _rng.scale(p),
-                 out_planes=out_planes, lse_part=part)
-    if r is None and part is not None:  # the statistics epilogue not covered: plain forward
-        part = None
-        r = G.sp_fwd(_pl.of(x2), wp, M, N, K, bias, act, rng, salt, _rng.threshold(p), _rng.scale(p),
-                     out_planes=out_planes)
+                 out_planes=out_planes)
     if r is None:
         return None
     y, yp = r
     if yp is not None:
         _pl.attach(y, yp)
-    if part is not None:
-        y._smi_lse = (part, y._version)
     return y
 
 
@@ -204,13 +193,12 @@ def _wplanes(weight):
     return _pl.weight(weight) if G.SP and weight.dim() == 2 and weight.shape[1] % 8 == 0 else None
 
 
-def _fwd_native(x2, weight, bias, act, p, rng, salt, w_bf=None, out_planes=False, wp=None, lse_stats=False,
-                relu_mask=None):
+def _fwd_native(x2, weight, bias, act, p, rng, salt, w_bf=None, out_planes=False, wp=None, relu_mask=None):
     N, K = weight.shape
     M = x2.shape[0]
     if x2.dtype == torch.float32:
         y = _fwd_sp(x2, wp if wp is not None else _wplanes(weight), N, bias, act, p, rng, salt, out_planes,
-                    lse_stats, relu_mask)
+                    relu_mask)
         if y is not None:
             return y
         return _fwd32_any(_pl.f32(x2), weight.detach(), bias, act, rng, salt, p)
@@ -256,8 +244,7 @@ class LinearFn(torch.autograd.Function):
         ctx.native = _native.use_native(x)
         if ctx.native:
             x2 = x2.contiguous()
-            y2 = _fwd_native(x2, weight, bias, act, p, rng, salt, out_planes=bool(planes & 1),
-                             lse_stats=bool(planes & 4))
+            y2 = _fwd_native(x2, weight, bias, act, p, rng, salt, out_planes=bool(planes & 1))
             ctx.x_planes = _pl.cached(x2)  # kept for the weight-gradient GEMM
             ctx.seed = 0
         else:
@@ -325,13 +312,11 @@ def _slot_grad(slot, rows):
     return g.reshape(rows, -1).contiguous() if g is not None else None
 
 
-def linear(x, weight, bias=None, act=None, p=0.0, rng=None, salt=0, x_slot=None, out_planes=False, dx_planes=False,
-           lse_stats=False):
+def linear(x, weight, bias=None, act=None, p=0.0, rng=None, salt=0, x_slot=None, out_planes=False, dx_planes=False):
     """y = dropout_p(act(x @ weight^T + bias)); act in {None, 'relu', 'sigmoid'}.  ``x_slot``:
     a ResidualGrad whose parked gradient is added to dX in the dgrad epilogue.  fp32 GPU path:
     ``out_planes`` / ``dx_planes`` make the forward / dgrad epilogue also write the split planes of
-    y / dX (sparkmi/ops/planes.py) for a consumer that reads planes (the attention kernels);
-    ``lse_stats``: per-row softmax statistics of y for a cross-entropy on it (sparkmi/ops/loss.py)."""
+    y / dX (sparkmi/ops/planes.py) for a consumer that reads planes (the attention kernels)."""
     a = ACTS[act] if not isinstance(act, int) else act
     if a == 2 and p > 0:
         raise ValueError("sigmoid + dropout epilogue is not supported")
@@ -339,7 +324,7 @@ def linear(x, weight, bias=None, act=None, p=0.0, rng=None, salt=0, x_slot=None,
         from .layernorm import _NULL_RNG
         rng, p = _NULL_RNG, 0.0
     return LinearFn.apply(x, weight, bias, a, float(p), rng, int(salt), x_slot,
-                          (1 if out_planes else 0) | (2 if dx_planes else 0) | (4 if lse_stats else 0))
+                          (1 if out_planes else 0) | (2 if dx_planes else 0))
 
 
 class FFNFn(torch.autograd.Function):

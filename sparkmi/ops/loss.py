@@ -11,16 +11,6 @@ import torch
 from .. import _native
 
 
-def _lse_part(x2):
-    """The softmax statistics the producing GEMM's epilogue attached to the logits (or to the
-    tensor a reshape view of them shares storage with), if still valid."""
-    for t in (x2, x2._base):
-        e = getattr(t, "_smi_lse", None) if t is not None else None
-        if e is not None and t.data_ptr() == x2.data_ptr() and t.numel() == x2.numel() and e[1] == x2._version:
-            return e[0]
-    return None
-
-
 class CrossEntropyFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, labels, ignore_index):
@@ -37,14 +27,8 @@ class CrossEntropyFn(torch.autograd.Function):
             stats = torch.empty(1, device=x2.device, dtype=torch.float32)  # valid-row count
             loss = torch.empty((), device=x2.device, dtype=torch.float32)  # its own buffer: no copy kernel
             row_loss = torch.empty(M, device=x2.device, dtype=torch.float32)
-            part = _lse_part(x2) if x2.dtype == torch.float32 else None
-            if part is not None and part.shape == ((V + 127) // 128, M, 2):
-                # fused: the vocab projection's epilogue already reduced each row per 128 columns
-                C.ce_fwd_part(part.data_ptr(), part.shape[0], x2.data_ptr(), lab.data_ptr(), M, V, ignore_index,
-                              lse.data_ptr(), stats.data_ptr(), loss.data_ptr(), row_loss.data_ptr(), _native.stream())
-            else:
-                C.ce_fwd(x2.data_ptr(), int(x2.dtype == torch.bfloat16), lab.data_ptr(), M, V, ignore_index,
-                         lse.data_ptr(), stats.data_ptr(), loss.data_ptr(), row_loss.data_ptr(), _native.stream())
+            C.ce_fwd(x2.data_ptr(), int(x2.dtype == torch.bfloat16), lab.data_ptr(), M, V, ignore_index,
+                     lse.data_ptr(), stats.data_ptr(), loss.data_ptr(), row_loss.data_ptr(), _native.stream())
             ctx.save_for_backward(x2, lab, lse, stats)
             ctx.shape = logits.shape
             return loss

@@ -19,7 +19,7 @@ import torch
 from ..data.dataset import DeviceLoader
 from ..data.synthetic import translation_text
 from ..data.text import build_vocab_from_iterator, get_tokenizer, text_pipeline
-from ..models.transformer import Transformer
+from ..models.transformer import Transformer, transformer_flops_per_sample
 from ..optim import Adam
 from ..train.config import TrainConfig, parse
 from ..train.trainer import Trainer, setup_executor
@@ -45,16 +45,6 @@ class TranslatorConfig(TrainConfig):
     shift_targets: bool = False
     n_train: int = 29000
     log_every: int = 100
-
-
-def transformer_flops_per_sample(layers, seq, vocab, d=512, ffn=1024):
-    """Matmul FLOPs of one training sample (forward + backward = 3x forward): the GEMMs of every
-    encoder / decoder layer, the vocab projection, QK^T and PV of the 3 attention sites per layer
-    pair (63.4 GFLOP at L6 S256 V10k)."""
-    enc = 2 * d * (3 * d + d + 2 * ffn)
-    dec = 2 * d * (3 * d + d + d + 2 * d + d + 2 * ffn)
-    attn = 3 * 4 * seq * d
-    return 3 * (layers * (enc + dec + attn) + 2 * d * vocab) * seq
 
 
 def build_corpus(cfg):

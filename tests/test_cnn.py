@@ -145,14 +145,33 @@ def test_fused_cnn_gradients_bit_reproducible(dtype):
         assert torch.equal(a, b)
 
 
+CNN_MAXB = 64  # csrc/include/smi_cnn.h
+
+
+def test_cnn_fused_batch_limit_is_cnn_maxb():
+    """The fused step takes every batch up to CNN_MAXB for the reference model in both dtypes (the
+    fused tail's LDS is part of the kernel's allocation, checked per dtype: csrc/kernels/cnn.hip
+    smi_cnn_fused_ok) and none past it; the Python model reports the same limit."""
+    from sparkmi import _native
+    if not _native.has_native():
+        pytest.skip("native library not built")
+    C = _native.C()
+    for bf in (0, 1):
+        assert C.cnn_max_batch(10, 1, 10, bf) == CNN_MAXB
+        assert all(C.cnn_fused_ok(10, 1, 10, b, bf) for b in (1, 20, 32, 59, 63, CNN_MAXB))
+        assert not C.cnn_fused_ok(10, 1, 10, CNN_MAXB + 1, bf) and not C.cnn_fused_ok(10, 1, 10, 0, bf)
+    assert FashionMNISTModel(1, 10, 10).fused_batch_limit() == CNN_MAXB
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("dtype,B", [("fp32", 32), ("bf16", 32), ("fp32", 20), ("bf16", 56)])
+@pytest.mark.parametrize("dtype,B", [("fp32", 32), ("bf16", 32), ("fp32", 20), ("bf16", CNN_MAXB),
+                                     ("fp32", CNN_MAXB)])
 def test_fused_sgd_step_matches_unfused(dtype, B):
     """The one-launch CNN step (fused slab reduction + SGD in the kernel's ticketed tail) follows
     the three-launch path (kernel -> batch gradient reduce -> SGD kernel) step for step, keeps the
     bf16 shadow in sync, is bit-reproducible, and replays identically inside a HIP graph
-    (StepRunner's single-executor fused_step path).  B = 20: a ragged last group of images; B = 56:
-    with its weight-gradient helpers, 280 workgroups: more than the CUs."""
+    (StepRunner's single-executor fused_step path).  B = 20: a ragged last group of images;
+    B = CNN_MAXB: the limit itself, 320 workgroups with the weight-gradient helpers — more than the CUs."""
     from sparkmi.optim import SGD
     from sparkmi.train.runner import StepRunner
     from sparkmi.utils.flat import FlatParams
@@ -194,3 +213,20 @@ def test_fused_sgd_step_matches_unfused(dtype, B):
     for a, b in zip(lf, lu):
         assert abs(a - b) <= 1e-5 * abs(b) + 1e-6, (lf, lu)
     torch.testing.assert_close(pf, pu, rtol=1e-5, atol=5e-6)  # fp32 sums in another order
+
+
+@pytest.mark.gpu
+def test_fused_step_past_the_limit_warns_and_falls_back():
+    """A batch past CNN_MAXB runs the multi-launch step (None from the fused step) and says so once."""
+    from sparkmi.optim import SGD
+    from sparkmi.utils.flat import FlatParams
+    m = FashionMNISTModel(1, 10, 10, dtype="bf16").cuda().train()
+    opt = SGD(FlatParams(m, shadow=True), lr=0.05)
+    x = torch.rand(CNN_MAXB + 1, 1, 28, 28, device="cuda")
+    y = torch.randint(0, 10, (CNN_MAXB + 1,), device="cuda")
+    with pytest.warns(RuntimeWarning, match="exceeds the fused step's limit"):
+        assert m.fused_sgd_step(opt, x, y) is None
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        assert m.fused_sgd_step(opt, x, y) is None  # once per model

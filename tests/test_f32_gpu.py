@@ -292,33 +292,6 @@ def test_attention_f32_single_pass_repeatable(mode):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("M,V", [(8192, 10000), (300, 10000), (77, 45), (256, 384)])
-def test_vocab_linear_ce_fused_stats(M, V):
-    """The vocab projection's epilogue reduces each logits row per 128 columns (max, sum exp) and
-    the cross-entropy forward merges those (ce_fwd_part) instead of re-reading the logits: the
-    loss and its gradients equal the standalone ce_fwd path (a clone of the logits carries no
-    statistics) to fp32 rounding; ignored rows stay out of the mean."""
-    from sparkmi.ops.linear import linear
-    from sparkmi.ops.loss import _lse_part, cross_entropy
-    torch.manual_seed(12)
-    K = 512
-    x = torch.randn(M, K, device=dev) * 0.5
-    lin = torch.nn.Linear(K, V).to(dev)
-    lab = torch.randint(0, V, (M,), device=dev)
-    lab[::7] = 0
-    outs = []
-    for fused in (True, False):
-        xg = x.clone().requires_grad_()
-        logits = linear(xg, lin.weight, lin.bias, lse_stats=True)
-        if fused and G.SP and V % 8 == 0:
-            assert _lse_part(logits.reshape(-1, V)) is not None
-        loss = cross_entropy(logits if fused else logits.clone(), lab, ignore_index=0)
-        loss.backward()
-        outs.append((loss.detach(), xg.grad))
-    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=2e-6, atol=2e-6)
-    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-4, atol=1e-7)
-
-
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_layernorm_f32(p):
     from sparkmi.ops.layernorm import add_dropout_layernorm
