@@ -220,7 +220,7 @@ def sp_dgrad(dyp, wp, M, K, N, resid=None, dact_y=None, dscale=1.0, out_planes=F
                              dx.stride(0) if dx is not None else K, _native.ptr(dxp), K,
                              dxp.stride(0) if dxp is not None else 0, 0, 0, 0, _native.ptr(resid),
                              resid.stride(0) if resid is not None else 0, _native.ptr(dact_y),
-                             dact_y.stride(0) if dact_y is not None else 0, 0, 0, 0, dscale, 0, 0,
+                             dact_y.stride(0) if dact_y is not None else 0, 0, 0, 0, dscale, 0,
                              _native.ptr(dmask), dmask.stride(0) if dmask is not None else 0, _native.stream())
     return (dx, dxp) if ok else None
 
@@ -234,4 +234,4 @@ def sp_wgrad(dyp, xp, gw, gb=None):
     M = dyp.shape[1]
     return bool(_native.C().gemm_sp(2, dyp.data_ptr(), dyp.stride(1), dyp.stride(0), xp.data_ptr(), xp.stride(1),
                                     xp.stride(0), N, K, M, 0, gw.data_ptr(), gw.stride(0), 0, 0, 0, 1, 0, 0, 0, 0, 0,
-                                    0, 0, 0, 0, 1.0, _native.ptr(gb), 0, 0, 0, _native.stream()))
+                                    0, 0, 0, 0, 1.0, _native.ptr(gb), 0, 0, _native.stream()))
