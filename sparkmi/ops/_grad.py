@@ -221,7 +221,7 @@ def _queued(params):
 
 def pending():
     """True when deferred work is queued or a flush is scheduled."""
-    return bool(_cb[0] or _ln_queue or _fold_queue or _group_queue or _async["main"] is not None)
+    return bool(_cb[0] or _ln_queue or _fold_queue or _group_queue or _late or _async["main"] is not None)
 
 
 def reset_deferred():
@@ -235,6 +235,7 @@ def reset_deferred():
     _fold_queue.clear()
     _group_queue.clear()
     _group_bytes.clear()
+    _late.clear()
     _cb[0] = False
     return stale
 
@@ -396,6 +397,10 @@ def _flush_folds(C, fq):
 # 147 KiB of LDS) take CUs from the critical dgrad chain.
 WGRAD_OVERLAP = True
 _async = {"main": None, "dev": None, "hold": [], "hold_ln": []}
+# defer_late(): gradient-only launches issued while an overlapped flush is in flight run at the end
+# of the backward (False: in place)
+LATE_GRADS = True
+_late = []
 
 # ---- the cut: work launched at the overlapped flush ------------------------------------------
 # Cut hooks run on the side stream right after the overlapped flush has launched the queued
@@ -455,6 +460,21 @@ def flush_groups_async(device):
     return True
 
 
+def defer_late(device, fn, params, hold=()):
+    """Defer ``fn`` (launches that only produce parameter gradients, e.g. an embedding table's
+    gradient sum) to the end of the backward when an overlapped flush is in flight on ``device``:
+    run in place, right after the flush, it sat on the main stream ahead of the rest of the
+    backward, starved of CUs by the weight-gradient group (a 50 us sum took 460 us on the bf16
+    step's critical path); at the end it runs beside the last group instead.  (A fork onto another
+    stream did not help: in the replayed graph the fork landed on the main branch's queue.)
+    ``params`` are reported final after it; ``hold`` keeps the operands alive.  Returns False
+    (nothing deferred) otherwise: the caller runs ``fn`` now."""
+    if _async["main"] is None or device.type != "cuda" or not LATE_GRADS:
+        return False
+    _late.append((fn, tuple(params), tuple(hold)))
+    return True
+
+
 def _join_async():
     """Join the overlapped flush's side stream; returns its held (group entries, LayerNorm fold
     entries)."""
@@ -472,11 +492,15 @@ def flush_deferred():
     The queues are emptied first (try/finally): a launch that raises leaves no stale entries."""
     from .. import _native
     gq, lq, fq = list(_group_queue), list(_ln_queue), list(_fold_queue)
+    late = list(_late)
     _group_queue.clear()
     _group_bytes.clear()
     _ln_queue.clear()
     _fold_queue.clear()
+    _late.clear()
     _cb[0] = False
+    for fn, _, _ in late:  # deferred gradient-only work: beside the still-running side-stream group
+        fn()
     # launched before the join when no output is one an overlapped group (still running on the
     # side stream) writes: they then run beside it
     side_out = {t.data_ptr() for e in _async["hold"] for t in (e[2], e[3]) if t is not None}
@@ -501,6 +525,8 @@ def flush_deferred():
         CONFIRMING[0] = False
     for e in lq:
         grad_ready(*e[6])
+    for _, ps, _ in late:
+        grad_ready(*ps)
     for e in fq:
         grad_ready(*e[6])
     for e in gq:

@@ -145,16 +145,27 @@ class EmbeddingFn(torch.autograd.Function):
             # deterministic backward (bit-reproducible, no float atomics): the ordering ran beside
             # the forward (plan_backward); join it and sum
             plan, ctx.plan = ctx.plan, None
-            if plan is not None:
-                _join(plan)
-                C.emb_sum(plan[2], int(dout.dtype != torch.float32), ids.data_ptr(), dout.data_ptr(), gw.data_ptr(), T,
-                          D, ctx.pad, ctx.rng.ptr(), ctx.salt, _rng.threshold(ctx.p), _rng.scale(ctx.p), V,
-                          plan[0].data_ptr(), _native.stream())
-            else:
-                bwd = C.emb_bwd_f32 if dout.dtype == torch.float32 else C.emb_bwd
-                ws = torch.empty(C.emb_det_ws_bytes(T, V, D), device=dout.device, dtype=torch.uint8)
-                bwd(ids.data_ptr(), dout.data_ptr(), gw.data_ptr(), T, D, ctx.pad, ctx.rng.ptr(), ctx.salt,
-                    _rng.threshold(ctx.p), _rng.scale(ctx.p), V, ws.data_ptr(), _native.stream())
+            rng, salt, pad, p = ctx.rng, ctx.salt, ctx.pad, ctx.p
+
+            def run():
+                if plan is not None:
+                    _join(plan)
+                    C.emb_sum(plan[2], int(dout.dtype != torch.float32), ids.data_ptr(), dout.data_ptr(), gw.data_ptr(),
+                              T, D, pad, rng.ptr(), salt, _rng.threshold(p), _rng.scale(p), V, plan[0].data_ptr(),
+                              _native.stream())
+                else:
+                    bwd = C.emb_bwd_f32 if dout.dtype == torch.float32 else C.emb_bwd
+                    ws = torch.empty(C.emb_det_ws_bytes(T, V, D), device=dout.device, dtype=torch.uint8)
+                    bwd(ids.data_ptr(), dout.data_ptr(), gw.data_ptr(), T, D, pad, rng.ptr(), salt,
+                        _rng.threshold(p), _rng.scale(p), V, ws.data_ptr(), _native.stream())
+                    run.ws = ws  # held with the launch's operands
+            # the table's gradient is read by nothing but the optimizer: at the end of the backward
+            # when an overlapped weight-gradient group is in flight (the decoder's embedding, after
+            # the cross-attention projection's backward), else now
+            from . import _grad as _g
+            if not ctx.flush_wgrad and _g.defer_late(dout.device, run, (weight,), hold=(dout, ids, plan)):
+                return None, None, None, None, None, None, None, None, None, None
+            run()
         else:
             g = dout.float()
             if ctx.p > 0:

@@ -9,6 +9,6 @@ cd /tmp && export TMPDIR=/tmp && cd "$ROOT"
 rm -rf "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format rocpd -d "$OUT" -o run -- \
   python3 bench.py --model transformer --dtype "$DT" --steps 10 --warmup 3 --no-aux --no-f32-compare > "$OUT.log" 2>&1
-python3 tools/step_timeline.py "$OUT/run_results.db" --steps 4 > "$OUT.txt"
+python3 tools/step_timeline.py "$OUT/run_results.db" --steps 4 --marker multi_copy_kernel > "$OUT.txt"
 grep '^{' "$OUT.log" | tail -1
 head -40 "$OUT.txt"
