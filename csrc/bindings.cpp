@@ -70,7 +70,6 @@ int smi_mlp(const MLPArgs*, int, hipStream_t);
 int smi_mlp_grid(int);
 int smi_mlp_small(int);
 int smi_mlp_steps(const MLPArgs*, const MLPSteps*, hipStream_t);
-int smi_gemm_bf256_enable(int);
 int smi_gemm(const GemmArgs*, hipStream_t);
 int smi_gemm_f32(const GemmF32Args*, hipStream_t);
 int smi_gemm_f32_algo(int);
@@ -368,8 +367,6 @@ PYBIND11_MODULE(_C, m) {
     return smi_mlp_steps(&a, &sv, S(st)) == 0;
   }, "s fused SGD steps of the 4-5-4-3 MLP in one launch; False when the shapes are not covered");
   m.def("mlp_grid", [](int n) { return smi_mlp_grid(n); });
-  m.def("gemm_bf256", [](int set) { return smi_gemm_bf256_enable(set); },
-        "bf16 GEMMs that fill the chip on the 256x128 8-wave 16x16x32 tile (1; measured slower in the step) or always the persistent 128x128 kernel (0, default); -1 queries");
   m.def("mlp_small", [](int set) { return smi_mlp_small(set); },
         "MLP kernel: 1 = the compile-time 4-5-4-3 kernel for batches <= 64 (default), 0 = the generic one; -1 queries");
 

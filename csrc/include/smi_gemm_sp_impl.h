@@ -66,10 +66,7 @@ __device__ unsigned long long* g_sp_stamps;
 #define SP_STAMP(slot) do {} while (0)
 #endif
 
-// SE_BF: bf16 activations (csrc/kernels/gemm_bf.hip): resid / dact_y are read as bf16 and the
-// non-accumulating C output is written as bf16 (weight gradients stay fp32 accumulations)
-enum : int { SE_BIAS = 1, SE_RELU = 2, SE_DROP = 8, SE_RESID = 16, SE_DACT = 32, SE_ACC = 64,
-              SE_DMASK = 256, SE_BF = 512 };
+enum : int { SE_BIAS = 1, SE_RELU = 2, SE_DROP = 8, SE_RESID = 16, SE_DACT = 32, SE_ACC = 64, SE_DMASK = 256 };
 enum : int { SO_C = 1, SO_P = 2, SO_M = 4 };  // epilogue outputs: fp32 C, planes P, positivity mask
 
 typedef __attribute__((address_space(3))) void sp_lds_void;
@@ -172,10 +169,6 @@ __device__ __forceinline__ void sp_store_tile(const GemmSpArgs& g, const float* 
   const int tid = threadIdx.x;
   const int c4 = (tid & 31) * 4, col = n0 + c4;
   const bool hasC = (OUT & SO_C) && g.C;
-  constexpr bool BFO = (EPI & SE_BF) != 0 && (EPI & SE_ACC) == 0;  // bf16 C
-  const unsigned short* rsb = (const unsigned short*)g.resid;
-  const unsigned short* dyb = (const unsigned short*)g.dact_y;
-  unsigned short* cb = (unsigned short*)g.C;
   const bool vec = ((g.ldc | ((EPI & SE_RESID) ? g.ldr : 0) | ((EPI & SE_DACT) ? g.ldy : 0) |
                      ((OUT & SO_P) ? g.ldp : 0)) & 3) == 0;
   const bool full_cols = vec && col + 3 < g.N;
@@ -202,19 +195,8 @@ __device__ __forceinline__ void sp_store_tile(const GemmSpArgs& g, const float* 
     const long cidx = (long)row * g.ldc + col;
     if (full_cols) {
       float4 rs = make_float4(0.f, 0.f, 0.f, 0.f), dy = rs, cc = rs;
-      if constexpr ((EPI & SE_BF) != 0) {
-        if (EPI & SE_RESID) {
-          const uint2 t = *(const uint2*)(rsb + (long)row * g.ldr + col);
-          rs = make_float4(bf2f(t.x & 0xFFFF), bf2f(t.x >> 16), bf2f(t.y & 0xFFFF), bf2f(t.y >> 16));
-        }
-        if (EPI & SE_DACT) {
-          const uint2 t = *(const uint2*)(dyb + (long)row * g.ldy + col);
-          dy = make_float4(bf2f(t.x & 0xFFFF), bf2f(t.x >> 16), bf2f(t.y & 0xFFFF), bf2f(t.y >> 16));
-        }
-      } else {
-        if (EPI & SE_RESID) rs = *(const float4*)(g.resid + (long)row * g.ldr + col);
-        if (EPI & SE_DACT) dy = *(const float4*)(g.dact_y + (long)row * g.ldy + col);
-      }
+      if (EPI & SE_RESID) rs = *(const float4*)(g.resid + (long)row * g.ldr + col);
+      if (EPI & SE_DACT) dy = *(const float4*)(g.dact_y + (long)row * g.ldy + col);
       if ((EPI & SE_ACC) && hasC) cc = *(const float4*)(g.C + cidx);
       const unsigned mk = (EPI & SE_DMASK) ? g.mask[(long)row * g.ldm + (col >> 2)] : 0u;
       const float rv[4] = {rs.x, rs.y, rs.z, rs.w}, dv[4] = {dy.x, dy.y, dy.z, dy.w}, cv[4] = {cc.x, cc.y, cc.z, cc.w};
@@ -231,11 +213,7 @@ __device__ __forceinline__ void sp_store_tile(const GemmSpArgs& g, const float* 
         bits |= (x > 0.f ? 1u : 0u) << e;
         v[e] = x;
       }
-      if constexpr (BFO) {
-        if (hasC) *(uint2*)(cb + cidx) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
-      } else {
-        if (hasC) *(float4*)(g.C + cidx) = make_float4(v[0], v[1], v[2], v[3]);
-      }
+      if (hasC) *(float4*)(g.C + cidx) = make_float4(v[0], v[1], v[2], v[3]);
       if (OUT & SO_P) sp_store4(g.P + (long)row * g.ldp + col, g.pps, v);
       if (OUT & SO_M) g.mask[(long)row * g.ldm + (col >> 2)] = (unsigned char)bits;
     } else {
@@ -245,20 +223,11 @@ __device__ __forceinline__ void sp_store_tile(const GemmSpArgs& g, const float* 
         float x = v[e] + bb[e];
         if (EPI & SE_RELU) x = fmaxf(x, 0.f);
         if (EPI & SE_DROP) x = smi_keep(seed, (uint32_t)(cidx + e), g.thresh) ? x * g.dscale : 0.f;
-        if constexpr ((EPI & SE_BF) != 0) {
-          if (EPI & SE_RESID) x += bf2f(rsb[(long)row * g.ldr + col + e]);
-          if (EPI & SE_DACT) x = bf2f(dyb[(long)row * g.ldy + col + e]) > 0.f ? x * g.dscale : 0.f;
-        } else {
-          if (EPI & SE_RESID) x += g.resid[(long)row * g.ldr + col + e];
-          if (EPI & SE_DACT) x = g.dact_y[(long)row * g.ldy + col + e] > 0.f ? x * g.dscale : 0.f;
-        }
+        if (EPI & SE_RESID) x += g.resid[(long)row * g.ldr + col + e];
+        if (EPI & SE_DACT) x = g.dact_y[(long)row * g.ldy + col + e] > 0.f ? x * g.dscale : 0.f;
         if (EPI & SE_DMASK) x = ((mk >> e) & 1u) ? x * g.dscale : 0.f;
         if ((EPI & SE_ACC) && hasC) x += g.C[cidx + e];
-        if constexpr (BFO) {
-          if (hasC) cb[cidx + e] = f2bf(x);
-        } else {
-          if (hasC) g.C[cidx + e] = x;
-        }
+        if (hasC) g.C[cidx + e] = x;
         if (OUT & SO_P) sp_store1(g.P + (long)row * g.ldp + col + e, g.pps, x);
         bits |= (x > 0.f ? 1u : 0u) << e;
         v[e] = x;
@@ -715,22 +684,22 @@ __device__ __forceinline__ int sp16_off(int row, int k) {  // k % 8 == 0; [rows]
   return row * 32 + ((((k >> 3) ^ sp16_swz(row)) & 3) << 3);
 }
 
-// the NPL bf16x8 fragments (h, m[, l]) of a 16-row (k-contig) / 16-column (k-major) block, k 0..31
-template <bool KMAJ, int NPL = 3>
+// the three bf16x8 plane fragments (h, m, l) of a 16-row (k-contig) / 16-column (k-major) block, k 0..31
+template <bool KMAJ>
 __device__ __forceinline__ Split3 sp16_frag(const unsigned short* __restrict__ img, int pl_stride, int c0, int lane) {
   Split3 r;
   if (!KMAJ) {
     const int o = sp16_off(c0 + (lane & 15), 8 * (lane >> 4));
     r.h = *(const bf16x8_t*)(img + o);
     r.m = *(const bf16x8_t*)(img + pl_stride + o);
-    if constexpr (NPL == 3) r.l = *(const bf16x8_t*)(img + 2 * pl_stride + o);
+    r.l = *(const bf16x8_t*)(img + 2 * pl_stride + o);
   } else {
     const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4;
     const int col = c0 + 4 * p;
     const int o0 = sp_koff(8 * g + q, col), o1 = sp_koff(8 * g + 4 + q, col);
     bf16x8_t* outs[3] = {&r.h, &r.m, &r.l};
 #pragma unroll
-    for (int pl = 0; pl < NPL; ++pl) {
+    for (int pl = 0; pl < 3; ++pl) {
       const unsigned short* base = img + pl * pl_stride;
       const sp_s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) sp_s16x4_t*)(base + o0));
       const sp_s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) sp_s16x4_t*)(base + o1));
@@ -760,11 +729,6 @@ struct SpBiasSum16 {
     c[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.m, sel_ml, c[i], 0, 0, 0);
     c[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h, sel_hi, c[i], 0, 0, 0);
   }
-  // bf16 operands: h and m are the two 32-deep k-halves of one 64-deep step (one chain)
-  __device__ __forceinline__ void add2(int i, const Split3& f) {
-    c[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h, sel_hi, c[i], 0, 0, 0);
-    c[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.m, sel_hi, c[i], 0, 0, 0);
-  }
   // lanes of column 0 own rows 4 (lane >> 4) + r of fragment i; the mid + lo chain is one lane up
   __device__ __forceinline__ void store(const GemmSpArgs& g, int row0, int lane, bool accumulate) {
 #pragma unroll
@@ -783,16 +747,13 @@ struct SpBiasSum16 {
 
 #define MF16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 
-// NPL = 3: fp32 operands as hi / mid / lo planes, six slice products per k-step (32 deep).
-// NPL = 2: bf16 operands (csrc/kernels/gemm_bf.hip): the two "planes" are the two 32-deep halves of
-// a 64-deep k-step (plane stride = 32 elements k-contig, 32 rows k-major), one product each into
-// one accumulator — the same stages, DMA pieces, swizzles and fragment reads as the fp32 form.
-template <bool AK, bool BKM, int EPI, int OUT, bool BIASG = false, int NPL = 3>
+// fp32 operands as hi / mid / lo planes, six slice products per 32-deep k-step.
+template <bool AK, bool BKM, int EPI, int OUT, bool BIASG = false>
 __device__ __forceinline__ void gemm_sp_tile256m(const GemmSpArgs& g, int tile, unsigned short* lds) {
   constexpr int NT = 512, NB = 4;  // 4 x 4 blocks of 16 x 16 per wave
   constexpr int AOP = 3 * 256 * SP_BK;
   constexpr int APL = 256 * SP_BK;
-  constexpr int KSTEP = NPL == 3 ? SP_BK : 2 * SP_BK;  // k per stage
+  constexpr int KSTEP = SP_BK;  // k per stage
   SP_STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -802,13 +763,9 @@ __device__ __forceinline__ void gemm_sp_tile256m(const GemmSpArgs& g, int tile, 
   const int nk = (g.K + KSTEP - 1) / KSTEP;
   __amdgpu_buffer_rsrc_t ra[3], rb[3];
 #pragma unroll
-  for (int p = 0; p < NPL; ++p) {
-    // bf16 k-halves: plane p's base is p * aps elements into the same tensor, so its extent shrinks
-    // by as much (k-major rows past K then read zeros through the range check, as for the fp32 planes)
-    const int ea = NPL == 3 ? g.a_bytes : (int)(g.a_bytes - 2L * p * g.aps);
-    const int eb = NPL == 3 ? g.b_bytes : (int)(g.b_bytes - 2L * p * g.bps);
-    ra[p] = __builtin_amdgcn_make_buffer_rsrc((void*)(g.A + p * g.aps), 0, ea, 0x00020000);
-    rb[p] = __builtin_amdgcn_make_buffer_rsrc((void*)(g.B + p * g.bps), 0, eb, 0x00020000);
+  for (int p = 0; p < 3; ++p) {
+    ra[p] = __builtin_amdgcn_make_buffer_rsrc((void*)(g.A + p * g.aps), 0, g.a_bytes, 0x00020000);
+    rb[p] = __builtin_amdgcn_make_buffer_rsrc((void*)(g.B + p * g.bps), 0, g.b_bytes, 0x00020000);
   }
   // A: 16 pieces per plane (pieces 2w, 2w + 1), B: 8 (piece w); k-contig pieces swizzled by sp16_swz
   uint32_t va[2], vb;
@@ -848,7 +805,7 @@ __device__ __forceinline__ void gemm_sp_tile256m(const GemmSpArgs& g, int tile, 
     const uint32_t sa = real ? (AK ? (uint32_t)((long)k0 * g.lda * 2) : (uint32_t)(k0 * 2)) : SP_OOB;
     const uint32_t sb = real ? (BKM ? (uint32_t)((long)k0 * g.ldb * 2) : (uint32_t)(k0 * 2)) : SP_OOB;
 #pragma unroll
-    for (int p = 0; p < NPL; ++p) {
+    for (int p = 0; p < 3; ++p) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(ra[p], (sp_lds_void*)(st + p * APL + (2 * w + i) * 512), 16, va[i],
@@ -859,8 +816,8 @@ __device__ __forceinline__ void gemm_sp_tile256m(const GemmSpArgs& g, int tile, 
   };
   auto frag_a = [&](const unsigned short* st, int c0) -> Split3 {
     // k-major A: sub-image c0 / 128 of each plane ([32][128] images SP_PL apart inside the plane)
-    return AK ? sp16_frag<true, NPL>(st + (c0 >> 7) * SP_PL, APL, c0 & 127, lane)
-              : sp16_frag<false, NPL>(st, APL, c0, lane);
+    return AK ? sp16_frag<true>(st + (c0 >> 7) * SP_PL, APL, c0 & 127, lane)
+              : sp16_frag<false>(st, APL, c0, lane);
   };
   issue(0, 0);
   issue(1, 1);
@@ -868,15 +825,14 @@ __device__ __forceinline__ void gemm_sp_tile256m(const GemmSpArgs& g, int tile, 
     const int slot = kt & 1;
     // this wave's pieces of stage kt landed (3 DMA instructions per plane and stage; stage kt + 1's
     // still in flight)
-    if constexpr (NPL == 3) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     const unsigned short* st = lds + slot * SP_ST256;
     Split3 fa[NB], fb[NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i) fa[i] = frag_a(st, wm * 64 + i * 16);
 #pragma unroll
-    for (int j = 0; j < NB; ++j) fb[j] = sp16_frag<BKM, NPL>(st + AOP, SP_PL, wn * 64 + j * 16, lane);
+    for (int j = 0; j < NB; ++j) fb[j] = sp16_frag<BKM>(st + AOP, SP_PL, wn * 64 + j * 16, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave's reads of this stage retired -> refill it
     issue(kt + 2, slot);
@@ -885,39 +841,27 @@ __device__ __forceinline__ void gemm_sp_tile256m(const GemmSpArgs& g, int tile, 
     for (int i = 0; i < NB; ++i)
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[i][j] = MF16(fa[i].h, fb[j].h, acc[i][j]);
-    if constexpr (NPL == 3) {
 #pragma unroll
-      for (int i = 0; i < NB; ++i)
+    for (int i = 0; i < NB; ++i)
 #pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          cacc[i][j] = MF16(fa[i].l, fb[j].h, cacc[i][j]);
-          cacc[i][j] = MF16(fa[i].m, fb[j].m, cacc[i][j]);
-          cacc[i][j] = MF16(fa[i].h, fb[j].l, cacc[i][j]);
-          cacc[i][j] = MF16(fa[i].m, fb[j].h, cacc[i][j]);
-          cacc[i][j] = MF16(fa[i].h, fb[j].m, cacc[i][j]);
-        }
-    } else {  // the second k-half
-#pragma unroll
-      for (int i = 0; i < NB; ++i)
-#pragma unroll
-        for (int j = 0; j < NB; ++j) acc[i][j] = MF16(fa[i].m, fb[j].m, acc[i][j]);
-    }
+      for (int j = 0; j < NB; ++j) {
+        cacc[i][j] = MF16(fa[i].l, fb[j].h, cacc[i][j]);
+        cacc[i][j] = MF16(fa[i].m, fb[j].m, cacc[i][j]);
+        cacc[i][j] = MF16(fa[i].h, fb[j].l, cacc[i][j]);
+        cacc[i][j] = MF16(fa[i].m, fb[j].h, cacc[i][j]);
+        cacc[i][j] = MF16(fa[i].h, fb[j].m, cacc[i][j]);
+      }
     if constexpr (BIASG) {
 #pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        if constexpr (NPL == 3) bsum.add(i, fa[i]);
-        else bsum.add2(i, fa[i]);
-      }
+      for (int i = 0; i < NB; ++i) bsum.add(i, fa[i]);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   SP_STAMP(2);
-  if constexpr (NPL == 3) {
 #pragma unroll
-    for (int i = 0; i < NB; ++i)
+  for (int i = 0; i < NB; ++i)
 #pragma unroll
-      for (int j = 0; j < NB; ++j) acc[i][j] += cacc[i][j];
-  }
+    for (int j = 0; j < NB; ++j) acc[i][j] += cacc[i][j];
   __syncthreads();
   float* ep = (float*)lds;
 #pragma unroll

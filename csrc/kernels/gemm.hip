@@ -516,16 +516,7 @@ static int g_bm_force = 0;
 // runtime override of the tile height (64 / 128; 0 = automatic) — A/B probes in one process
 extern "C" void smi_gemm_set_bm(int bm) { g_bm_force = bm; }
 
-extern "C" int smi_gemm_bf256(const GemmArgs* args, hipStream_t st);
-extern "C" int smi_gemm_bf_wgrad_group(const void* const* A, const long* lda, const void* const* B, const long* ldb,
-                                       void* const* C, void* const* bias, const int* n, const int* k, const int* T,
-                                       int count, hipStream_t st);
-
 extern "C" int smi_gemm(const GemmArgs* args, hipStream_t st) {
-  {  // problems that fill the chip with 256 x 128 tiles: csrc/kernels/gemm_bf.hip
-    const int r = smi_gemm_bf256(args, st);
-    if (r) return r > 0 ? 0 : -1;
-  }
   GemmArgs g = *args;
   if (g.K % 8 != 0 || g.K < 8 || g.M < 8 || g.N < 8 || (g.mode != 0 && (g.M % 8 || g.N % 8))) return -1;
   if (g.splits < 1) g.splits = 1;
@@ -784,10 +775,6 @@ __global__ __launch_bounds__(256, 2) void gemm_wgrad_group_kernel(WgradGroup gr)
 extern "C" int smi_gemm_wgrad_group(const void* const* A, const long* lda, const void* const* B, const long* ldb,
                                     void* const* C, void* const* bias, const int* n, const int* k, const int* T,
                                     int count, hipStream_t st) {
-  {  // the 256 x 128 tile when the group fills the chip: csrc/kernels/gemm_bf.hip
-    const int r = smi_gemm_bf_wgrad_group(A, lda, B, ldb, C, bias, n, k, T, count, st);
-    if (r) return r > 0 ? 0 : -1;
-  }
   if (count < 1 || count > WG_MAX) return -1;
   WgradGroup gr{};
   int tot = 0;
