@@ -58,8 +58,11 @@ PYBIND11_MODULE(_comm, m) {
   // ctr: device uint32[3] = {epoch, ticket, signal value}, zero-initialised
   // spins: poll bound before a peer counts as lost (the bucket is then NaN-poisoned, *err set)
   // algo: 1 one-shot, 2 two-shot (reduce-scatter + all-gather)
+  // sgd_p / sgd_pbf / sgd_lr / sgd_step / sgd_seed / sgd_gscale: the optional plain-SGD epilogue of
+  // the one-shot kernel (sgd_p = 0: a plain all-reduce)
   m.def("ipc_allreduce", [](u buf, long n, std::vector<u> data, std::vector<u> sig, long cap, int rank, u ctr,
-                            u err, int blocks, u st, long spins, int algo) {
+                            u err, int blocks, u st, long spins, int algo, u sgd_p, u sgd_pbf, u sgd_lr, u sgd_step,
+                            u sgd_seed, float sgd_gscale) {
     if (data.size() != sig.size() || data.empty() || data.size() > IPC_MAX_RANKS)
       throw std::runtime_error("sparkmi._comm.ipc_allreduce: bad peer lists");
     IpcArgs a{};
@@ -68,6 +71,8 @@ PYBIND11_MODULE(_comm, m) {
     a.err = (int*)err;
     a.spins = spins > 0 ? spins : IPC_DEFAULT_SPINS;
     for (size_t i = 0; i < data.size(); ++i) { a.data[i] = (float*)data[i]; a.sig[i] = (unsigned*)sig[i]; }
+    a.p = (float*)sgd_p; a.pbf = (unsigned short*)sgd_pbf; a.lr = (const float*)sgd_lr; a.step = (float*)sgd_step;
+    a.seed = (int*)sgd_seed; a.gscale = sgd_gscale;
     const int rc = smi_ipc_allreduce(&a, blocks, algo, (hipStream_t)st);
     if (rc != 0) throw std::runtime_error("sparkmi._comm.ipc_allreduce failed: " +
                                           std::string(rc > 0 ? hipGetErrorString((hipError_t)rc) : "bad arguments"));

@@ -71,15 +71,21 @@ __device__ __forceinline__ void ipc_init_lost(const IpcArgs& a, int* timed_out) 
   __syncthreads();
 }
 
-// the last block to finish advances the device state for the next launch
+// the last block to finish advances the device state for the next launch (and, with the SGD
+// epilogue, the optimizer's step counter and the dropout seed, as sgd_kernel's last block does)
 __device__ __forceinline__ void ipc_advance(const IpcArgs& a, unsigned epoch, unsigned sval) {
   __syncthreads();
   if (threadIdx.x == 0 && atomicAdd(a.done, 1u) == gridDim.x - 1) {
     a.ep[0] = epoch;
     a.sv[0] = sval;
     a.done[0] = 0u;
+    if (a.p) {
+      a.step[0] = a.step[0] + 1.f;
+      if (a.seed) a.seed[0] += 1;
+    }
   }
 }
+__device__ __forceinline__ unsigned short ipc_f2bf(float f) { return __builtin_bit_cast(unsigned short, (__bf16)f); }
 
 __global__ __launch_bounds__(256) void ipc_allreduce_kernel(IpcArgs a) {
   const int b = blockIdx.x, nb = gridDim.x;
@@ -96,17 +102,35 @@ __global__ __launch_bounds__(256) void ipc_allreduce_kernel(IpcArgs a) {
   ipc_init_lost(a, &timed_out);
   const bool lost = ipc_round(a, b, sval, &timed_out);
   float4* out = (float4*)a.buf;
-  if (lost) {  // poison: the bucket must not carry a finite partial sum
+  if (lost) {  // poison: the bucket (and, with the SGD epilogue, the parameters) must not carry a finite partial sum
     const float nan = __builtin_nanf("");
-    for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) out[i] = make_float4(nan, nan, nan, nan);
+    for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+      out[i] = make_float4(nan, nan, nan, nan);
+      if (a.p) ((float4*)a.p)[i] = make_float4(nan, nan, nan, nan);
+    }
   } else {
+    const float lr = a.p ? a.lr[0] : 0.f;
     for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
       float4 acc = ((const float4*)(a.data[0] + half))[i];
       for (int r = 1; r < a.world; ++r) {
         const float4 v = ((const float4*)(a.data[r] + half))[i];
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
       }
-      out[i] = acc;
+      if (!a.p) {
+        out[i] = acc;
+      } else {  // SGD epilogue: sgd_kernel's p -= lr * (g * gscale), zero_grad, shadow
+        float4 pp = ((float4*)a.p)[i];
+        pp.x -= lr * (acc.x * a.gscale); pp.y -= lr * (acc.y * a.gscale);
+        pp.z -= lr * (acc.z * a.gscale); pp.w -= lr * (acc.w * a.gscale);
+        ((float4*)a.p)[i] = pp;
+        out[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (a.pbf) {
+          uint2 w;
+          w.x = ipc_f2bf(pp.x) | ((unsigned)ipc_f2bf(pp.y) << 16);
+          w.y = ipc_f2bf(pp.z) | ((unsigned)ipc_f2bf(pp.w) << 16);
+          ((uint2*)a.pbf)[i] = w;
+        }
+      }
     }
   }
   ipc_advance(a, epoch, sval);
@@ -179,6 +203,7 @@ extern "C" int smi_ipc_allreduce(const IpcArgs* args, int blocks, int algo, hipS
   if (a.world < 1 || a.world > IPC_MAX_RANKS || a.rank < 0 || a.rank >= a.world) return -1;
   if (a.n % 4 || a.n > a.cap || ((uintptr_t)a.buf & 15)) return -1;
   if (args->spins < 1 || (algo != 1 && algo != 2)) return -1;
+  if (a.p && (algo != 1 || !a.lr || !a.step || ((uintptr_t)a.p & 15) || ((uintptr_t)a.pbf & 7))) return -1;
   if (blocks < 1) blocks = 1;
   if (blocks > IPC_MAX_BLOCKS) blocks = IPC_MAX_BLOCKS;
   if (algo == 1) hipLaunchKernelGGL(ipc_allreduce_kernel, dim3(blocks), dim3(256), 0, st, a);

@@ -17,4 +17,11 @@ struct IpcArgs {
   unsigned* sv;                        // device signal value: the last value stored into signal slots
   int* err;                            // set to 1 on a poll timeout (sticky)
   long spins;                          // poll bound (s_sleep 8 back-off per poll)
+  // optional plain-SGD epilogue of the one-shot kernel (the optimizer of a data-parallel small-model
+  // step, sparkmi/parallel/ddp.py fuse_sgd): p -= lr * (sum * gscale), bf16 shadow refreshed, the
+  // bucket zeroed instead of overwritten with the sum, the step counter (and dropout seed) advanced
+  // by the last block — sgd_kernel's arithmetic (csrc/kernels/optim.hip), one launch fewer
+  float* p;                            // master parameters at the bucket's offsets (null: no SGD)
+  unsigned short* pbf;                 // their bf16 shadow or null
+  const float* lr; float* step; int* seed; float gscale;
 };

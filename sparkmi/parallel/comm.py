@@ -105,10 +105,21 @@ class IpcAllReduce:
         (w - 1), at the price of a second signal round — worth it past the latency-bound sizes."""
         return 1 if self.world <= 2 or numel * 4 <= ONE_SHOT_MAX_BYTES else 2
 
-    def __call__(self, t, algo=None, stream=None):
+    def __call__(self, t, algo=None, stream=None, sgd=None):
+        """All-reduce ``t`` in place.  ``sgd`` = (params, bf16 shadow or None, lr_t, step_t, seed or
+        None, grad_scale): instead of the sum, apply plain SGD with it to ``params`` (the bucket's
+        parameters, same shape as ``t``), zero ``t`` and advance step_t (and the seed) — the
+        optimizer launch of a data-parallel small-model step folded into the reduction."""
         if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() % 4 or t.numel() > self.cap:
             raise ValueError("IpcAllReduce: contiguous fp32 tensor, numel % 4 == 0, <= capacity")
         algo = algo or self.force_algo or self.algo_for(t.numel())
+        if sgd is not None and algo != 1:
+            raise ValueError("IpcAllReduce: the SGD epilogue is a one-shot feature")
+        sp = (0, 0, 0, 0, 0, 1.0)
+        if sgd is not None:
+            p, pbf, lr, step, seed, gscale = sgd
+            sp = (p.data_ptr(), pbf.data_ptr() if pbf is not None else 0, lr.data_ptr(), step.data_ptr(),
+                  seed.data_ptr() if seed is not None else 0, float(gscale))
         n4 = t.numel() // 4
         if self.blocks:
             blocks = self.blocks
@@ -118,7 +129,7 @@ class IpcAllReduce:
             blocks = max(1, min(self.C.IPC_MAX_BLOCKS, ((n4 + self.world - 1) // self.world + 511) // 512))
         self.C.ipc_allreduce(t.data_ptr(), t.numel(), self.data, self.sig, self.cap, self.rank, self.ctr.data_ptr(),
                              self.err.data_ptr(), blocks, (stream or torch.cuda.current_stream()).cuda_stream,
-                             self.spins, algo)
+                             self.spins, algo, *sp)
         return t
 
     def failed(self):

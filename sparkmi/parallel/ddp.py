@@ -71,6 +71,9 @@ def choose_comm(ipc_ms, rccl_ms, rccl_mc_ms=None):
 
 
 MIN_CTAS = 32  # RCCL channels of the multi-channel communicator the probe measures
+# plain SGD applied inside the one-shot IPC all-reduce (fuse_sgd): a data-parallel small-model step
+# is then the fused gradient kernel + ONE reduction-and-update launch (False: a separate SGD launch)
+FUSE_SGD = True
 
 
 def multichannel_group(world, min_ctas=MIN_CTAS):
@@ -327,6 +330,31 @@ class DataParallel:
     def shard_ranges(self):
         return [self.piece(b) for b in range(len(self.buckets))] if self.zero else [(0, self.flat.numel)]
 
+    def fuse_sgd(self, opt):
+        """Let the gradient reduction apply ``opt`` itself when it is plain SGD (no momentum, no
+        weight decay) over this buffer and the reduction is ONE bucket on the one-shot IPC kernel
+        (the CNN / MLP data-parallel steps, distributed_cnn.py:149-193,
+        distributed_multilayer_perceptron.py:97-145): the kernel's epilogue does sgd_kernel's update
+        (csrc/comm/ipc_allreduce.hip), bitwise the separate launch.  Checked per reduction (the
+        bucket layout may change after the first backward); ``last_step_fused`` tells the runner
+        whether the last finish() already stepped."""
+        from ..optim.sgd import SGD
+        self._sgd_opt = opt if (FUSE_SGD and isinstance(opt, SGD) and not opt.momentum and not opt.weight_decay
+                                and opt.flat is self.flat and opt.zero_grad_after_step) else None
+        return self._sgd_opt is not None
+
+    def _sgd_args(self, s, e):
+        """The SGD epilogue arguments for bucket [s, e) when fuse_sgd applies to it, else None."""
+        o = getattr(self, "_sgd_opt", None)
+        if (o is None or self.ipc is None or self.zero or self._sparse or len(self.buckets) != 1
+                or self.flat.planes is not None or (self.ipc.force_algo or self.ipc.algo_for(e - s)) != 1):
+            return None
+        sh = self.flat.shadow
+        return (self.flat.master[s:e], sh[s:e] if sh is not None else None, o.lr_t, o.step_t, o.bump_seed,
+                o.grad_scale)
+
+    last_step_fused = False
+
     def _launch(self, b):
         if self._launched[b]:
             return
@@ -341,7 +369,9 @@ class DataParallel:
         self.bytes_reduced += g.numel() * g.element_size()
         if self.ipc is not None:
             self._cs.wait_stream(torch.cuda.current_stream(g.device))  # the bucket's gradients are written
-            self.ipc(g, stream=self._cs)
+            sgd = self._sgd_args(s, e)
+            self.ipc(g, stream=self._cs, sgd=sgd)
+            self._sgd_applied = sgd is not None
             self._cs_used = True
             return
         if self.zero:
@@ -495,11 +525,14 @@ class DataParallel:
 
     def finish(self):
         """Complete every bucket's all-reduce (launching any not yet issued) before the optimizer."""
+        self.last_step_fused = False
         if self.world <= 1:
             self.reset()
             return
+        self._sgd_applied = False
         for b in range(len(self.buckets)):
             self._launch(b)
+        self.last_step_fused = self._sgd_applied
         for w in self._works:
             w.wait()
         if self._cs_used:

@@ -141,6 +141,14 @@ class StepRunner:
                     raise ValueError(f"zero=True (ZeRO-1) needs an optimizer with sharded state; "
                                      f"{type(optimizer).__name__} has none (use Adam/AdamW or zero=False)")
                 optimizer.shard(ddp.shard_ranges())
+            elif hasattr(ddp, "fuse_sgd"):
+                ddp.fuse_sgd(optimizer)  # plain SGD inside the one-shot IPC reduction, when it applies
+
+    def _opt_step(self):
+        """The optimizer launch — unless the gradient reduction just applied it (ddp.fuse_sgd)."""
+        if self.ddp is not None and getattr(self.ddp, "last_step_fused", False):
+            return
+        self.opt.step()
 
     @property
     def _dp(self):
@@ -237,7 +245,7 @@ class StepRunner:
         if self.ddp is not None:
             self.ddp.finish()
         e2 = self._event()
-        self.opt.step()
+        self._opt_step()
         if self.ddp is not None:
             self.ddp.gather_params()  # ZeRO-1: all-gather the updated master pieces (no-op otherwise)
         e3 = self._event()
@@ -341,10 +349,10 @@ class StepRunner:
                 self.static_loss = self._fwd_bwd(*self.static_in)
             self._phase_graphs = []
             fns = [lambda: self.ddp.finish()] if self._dp else [None]
-            fns.append(lambda: (self.opt.step(), self.ddp.gather_params() if self._dp else None))
-            for fn in fns:
-                if fn is None:
-                    self._phase_graphs.append(None)
+            fns.append(lambda: (self._opt_step(), self.ddp.gather_params() if self._dp else None))
+            for i, fn in enumerate(fns):
+                if fn is None or (i == 1 and self._dp and self.ddp.last_step_fused and not self.ddp.zero):
+                    self._phase_graphs.append(None)  # (the reduction graph already applied the SGD step)
                     continue
                 pg = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(pg, pool=g.pool()):
@@ -487,7 +495,8 @@ class StepRunner:
             if phased[0] is not None:
                 phased[0].replay()
             e2 = self._event()
-            phased[1].replay()
+            if phased[1] is not None:
+                phased[1].replay()
             e3 = self._event()
             if e0 is not None:
                 self._phase_events.append((e0, e1, e2, e3))
@@ -509,7 +518,7 @@ class StepRunner:
             if self._dp:
                 self.ddp.finish()
             e2 = self._event()
-            self.opt.step()
+            self._opt_step()
             if self._dp:
                 self.ddp.gather_params()
             e3 = self._event()

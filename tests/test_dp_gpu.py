@@ -276,7 +276,7 @@ def test_lstm_dp_sparse_embedding_matches_single_process():
 
 
 # ---- the data-parallel CNN fast step: fused gradient kernel + IPC + SGD ----
-def _cnn_dp(steps, graph, bind, dtype="fp32"):
+def _cnn_dp(steps, graph, bind, dtype="fp32", fuse_sgd=True):
     import torch
     from sparkmi.data.synthetic import fashion_mnist_like
     from sparkmi.models.cnn import FashionMNISTModel
@@ -289,6 +289,8 @@ def _cnn_dp(steps, graph, bind, dtype="fp32"):
     m = FashionMNISTModel(1, 10, 10, dtype=dtype).to(device)
     flat = FlatParams(m, shadow=False)
     opt = SGD(flat, lr=0.05)
+    from sparkmi.parallel import ddp as D
+    D.FUSE_SGD = fuse_sgd
     ddp = DataParallel(flat) if world > 1 else None
     GB = 32
     imgs, labels = fashion_mnist_like(steps * GB, seed=3, device=device)
@@ -309,7 +311,7 @@ def _cnn_dp(steps, graph, bind, dtype="fp32"):
     torch.cuda.synchronize()
     comm = None
     if ddp is not None:
-        comm = ddp.comm
+        comm = (ddp.comm, ddp.last_step_fused, float(opt.step_t.item()))
         ddp.check()
         ddp.close()
     import torch.distributed as dist
@@ -336,7 +338,13 @@ def test_cnn_dp_fused_step_matches_single_process(world):
     for graph, bind in ((False, False), (True, True)):
         rs, comm = launch(_cnn_dp, (7, graph, bind), {}, num_processes=world, use_gpu=True, env=env, log_sink=None,
                           timeout=300)
-        assert comm == "ipc"
+        assert comm[0] == "ipc" and comm[1], comm  # the SGD step ran inside the reduction (ddp.fuse_sgd)
+        assert comm[2] == 7.0, comm                 # and advanced the step counter once per step
         for q in rs[1:]:
             assert torch.equal(rs[0], q), "ranks disagree"
         torch.testing.assert_close(rs[0], r1, rtol=1e-4, atol=2e-6, msg=f"graph={graph} bind={bind}")
+        # the reduction's SGD epilogue is bitwise the separate SGD launch
+        rs2, comm2 = launch(_cnn_dp, (7, graph, bind, "fp32", False), {}, num_processes=world, use_gpu=True, env=env,
+                            log_sink=None, timeout=300)
+        assert not comm2[1] and comm2[2] == 7.0, comm2
+        assert torch.equal(rs2[0], rs[0]), f"fused SGD != sgd_kernel (graph={graph} bind={bind})"
