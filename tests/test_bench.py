@@ -74,9 +74,14 @@ def test_bench_under_torchrun():
 @pytest.mark.timeout(600)
 def test_bench_cnn_two_ranks_on_the_gpu():
     """bench.py --gpus 2 --model cnn on the box's one MI355X: the data-parallel CNN fast step (fused
-    gradient kernel + IPC all-reduce + SGD in bound multi-step graphs) next to the single-rank
-    step on the same box; both ranks share the one device, so the 2-rank step also carries the
-    other rank's kernels (<= 1.3x the 1-rank step)."""
+    gradient kernel + the IPC all-reduce with the SGD update in its epilogue, in bound multi-step
+    graphs) next to the single-rank step on the same box.  Both ranks share the one device: their
+    2 x 160 workgroups (32 images + 128 weight-gradient helpers each) compete for 256 CUs, so the
+    gradient kernel alone goes 36 -> 40-47 us and the reduction waits for the slower rank
+    (profiles/r6_dp_cnn_shared_gpu.txt).  Measured x1.47 (x1.53 with the separate SGD launch); the
+    round-4 bar of x1.3 assumed the two ranks' kernels would overlap for free, which one shared GPU
+    cannot show: the bar here is the measured ratio + 10 %, and the 8-GPU run (one rank per GPU)
+    is where the data-parallel overhead is the reduction alone."""
     base = ["--model", "cnn", "--cnn-steps", "400", "--warmup", "20"]
     one = _run([sys.executable, "bench.py", "--gpus", "1"] + base)
     two = _run([sys.executable, "bench.py", "--gpus", "2"] + base, env={"SPARKMI_DIST_BACKEND": "gloo"})
@@ -85,4 +90,4 @@ def test_bench_cnn_two_ranks_on_the_gpu():
     r1, r2 = one["cnn"]["ms_per_step"], two["cnn"]["ms_per_step"]
     print(f"\ncnn bf16 ms/step: 1 rank {r1}, 2 ranks sharing the GPU {r2} (x{r2 / r1:.2f}); "
           f"recipe path 1 rank {one['cnn_recipe_path']['ms_per_step']}, 2 ranks {two['cnn_recipe_path']['ms_per_step']}")
-    assert r2 <= 2.0 * r1, (r1, r2)
+    assert r2 <= 1.6 * r1, (r1, r2)
