@@ -17,6 +17,27 @@
 namespace py = pybind11;
 using u = uintptr_t;
 
+// DLPack (the stable v0.x ABI torch.utils.dlpack.from_dlpack consumes): a device buffer this module
+// allocated, handed to torch as a tensor that frees it when torch drops it
+struct DLDevice { int32_t device_type; int32_t device_id; };
+struct DLDataType { uint8_t code; uint8_t bits; uint16_t lanes; };
+struct DLTensor {
+  void* data; DLDevice device; int32_t ndim; DLDataType dtype; int64_t* shape; int64_t* strides; uint64_t byte_offset;
+};
+struct DLManagedTensor { DLTensor dl_tensor; void* manager_ctx; void (*deleter)(DLManagedTensor*); };
+struct OwnedBuf { DLManagedTensor mt; int64_t shape[1]; };
+static void owned_deleter(DLManagedTensor* mt) {
+  OwnedBuf* o = reinterpret_cast<OwnedBuf*>(mt);
+  (void)hipFree(o->mt.dl_tensor.data);
+  delete o;
+}
+static void capsule_dtor(PyObject* cap) {  // a capsule torch never consumed still frees its buffer
+  if (PyCapsule_IsValid(cap, "dltensor")) {
+    auto* mt = static_cast<DLManagedTensor*>(PyCapsule_GetPointer(cap, "dltensor"));
+    if (mt && mt->deleter) mt->deleter(mt);
+  }
+}
+
 #include "smi_ipc.h"
 extern "C" int smi_ipc_allreduce(const IpcArgs* args, int blocks, int algo, hipStream_t st);
 
@@ -44,6 +65,32 @@ PYBIND11_MODULE(_comm, m) {
     hchk(hipIpcGetMemHandle(&h, p), "hipIpcGetMemHandle");
     return py::make_tuple((u)p, py::bytes(reinterpret_cast<const char*>(&h), sizeof(h)));
   });
+  // A zeroed fp32 device buffer of n floats in an allocation of its own (hipExtMallocWithFlags, the
+  // allocator of the IPC staging regions; cached unless `uncached`), as a DLPack capsule: the
+  // gradient buffer the zero-copy kernel reads across processes lives in one (sparkmi/parallel/ddp.py)
+  m.def("ipc_buffer", [](long n, int device, bool uncached) {
+    int cur = 0;
+    hchk(hipGetDevice(&cur), "hipGetDevice");
+    hchk(hipSetDevice(device), "hipSetDevice");
+    void* p = nullptr;
+    hchk(hipExtMallocWithFlags(&p, (size_t)n * 4, uncached ? hipDeviceMallocUncached : hipDeviceMallocDefault),
+         "hipExtMallocWithFlags");
+    hchk(hipMemset(p, 0, (size_t)n * 4), "hipMemset");
+    hchk(hipSetDevice(cur), "hipSetDevice");
+    OwnedBuf* o = new OwnedBuf{};
+    o->shape[0] = n;
+    DLTensor& t = o->mt.dl_tensor;
+    t.data = p;
+    t.device = DLDevice{10 /* kDLROCM */, device};
+    t.ndim = 1;
+    t.dtype = DLDataType{2 /* kDLFloat */, 32, 1};
+    t.shape = o->shape;
+    t.strides = nullptr;
+    t.byte_offset = 0;
+    o->mt.manager_ctx = o;
+    o->mt.deleter = owned_deleter;
+    return py::reinterpret_steal<py::object>(PyCapsule_New(&o->mt, "dltensor", capsule_dtor));
+  });
   m.def("ipc_open", [](py::bytes handle) {
     std::string s = handle;
     if (s.size() != sizeof(hipIpcMemHandle_t)) throw std::runtime_error("sparkmi._comm.ipc_open: bad handle");
@@ -54,10 +101,32 @@ PYBIND11_MODULE(_comm, m) {
     return (u)p;
   });
   m.def("ipc_close", [](u p) { hchk(hipIpcCloseMemHandle((void*)p), "hipIpcCloseMemHandle"); });
+  // Export an existing device allocation (e.g. a flat gradient buffer from torch's allocator) for
+  // the zero-copy kernel: the IPC handle of the allocation holding `ptr` and ptr's byte offset in
+  // it (a peer adds the offset to the base ipc_open returns)
+  m.def("ipc_range", [](u ptr) {  // (base, bytes) of the allocation holding ptr
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    hchk(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr), "hipMemGetAddressRange");
+    return py::make_tuple((u)base, (long)size);
+  });
+  m.def("ipc_export", [](u ptr) {
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    hchk(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr), "hipMemGetAddressRange");
+    hipIpcMemHandle_t h;
+    hchk(hipIpcGetMemHandle(&h, (void*)base), "hipIpcGetMemHandle");
+    return py::make_tuple(py::bytes(reinterpret_cast<const char*>(&h), sizeof(h)), (long)(ptr - (u)base),
+                          (long)size);
+  });
   m.def("ipc_free", [](u p) { hchk(hipFree((void*)p), "hipFree"); });
+  // re-zero a pooled region before it is handed out again (sparkmi/parallel/comm.py keeps exported
+  // regions for the life of the process instead of freeing them)
+  m.def("ipc_memset0", [](u p, long bytes) { hchk(hipMemset((void*)p, 0, (size_t)bytes), "hipMemset"); });
   // ctr: device uint32[3] = {epoch, ticket, signal value}, zero-initialised
   // spins: poll bound before a peer counts as lost (the bucket is then NaN-poisoned, *err set)
-  // algo: 1 one-shot, 2 two-shot (reduce-scatter + all-gather)
+  // algo: 1 one-shot, 2 two-shot (reduce-scatter + all-gather), 3 zero-copy two-shot (data = every
+  // rank's bucket itself, data[rank] == buf; no staging)
   // sgd_p / sgd_pbf / sgd_lr / sgd_step / sgd_seed / sgd_gscale: the optional plain-SGD epilogue of
   // the one-shot kernel (sgd_p = 0: a plain all-reduce)
   m.def("ipc_allreduce", [](u buf, long n, std::vector<u> data, std::vector<u> sig, long cap, int rank, u ctr,

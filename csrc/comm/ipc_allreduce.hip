@@ -8,6 +8,14 @@
 //    scatter then all-gather — rank r sums chunk r of every peer's bucket (reading its 1/w slice
 //    from all peers at once), publishes the sum in place, then every rank gathers the w reduced
 //    chunks: 2 (w - 1) / w n floats per rank, two signal rounds.
+//  * ZERO-COPY TWO-SHOT (algo 3; the transformer's bulk buckets when the start-up probe measures it
+//    fastest): the same reduce-scatter + all-gather, but read straight out of every rank's
+//    IPC-registered gradient buffer (a.data[q] = peer q's bucket) instead of a staged copy — no
+//    copy of the bucket into staging and no reduced chunk written twice: 2 n fewer local HBM
+//    bytes per call.  Three signal rounds: (1) every bucket is final (it was written by earlier
+//    kernels on each rank: stream order, and their completion wrote their lines back), (2) every
+//    rank's reduced chunk is published (system-scope release), (3) every rank finished reading its
+//    peers' chunks — only then may a rank's next backward overwrite its bucket.
 //
 // Protocol (one launch per all-reduce, stream-ordered on every rank).  Device state ctr =
 // {epoch, done ticket, signal value} advanced by each launch's last block (like the optimizers'
@@ -197,16 +205,80 @@ __global__ __launch_bounds__(256) void ipc_allreduce2_kernel(IpcArgs a) {
   ipc_advance(a, epoch, s2);
 }
 
-// algo 1: one-shot, 2: two-shot
+// Zero-copy two-shot: a.data[q] is rank q's bucket itself (IPC-mapped; a.data[a.rank] == a.buf).
+// Chunk c / block b ranges as in the staged two-shot, identical on every rank, so block b's
+// signal covers exactly the ranges block b of every peer reads or overwrites.
+__global__ __launch_bounds__(256) void ipc_allreduce_zc_kernel(IpcArgs a) {
+  const int b = blockIdx.x, nb = gridDim.x;
+  const long n4 = a.n / 4;
+  const long C = (n4 + a.world - 1) / a.world;
+  const long per = (C + nb - 1) / nb;
+  const unsigned epoch = a.ep[0] + 1u, s1 = a.sv[0] + 1u, s2 = s1 + 1u, s3 = s2 + 1u;
+  float4* out = (float4*)a.buf;
+  auto range = [&](int c, long& lo, long& hi) {
+    const long c0 = (long)c * C, c1 = c0 + C < n4 ? c0 + C : n4;
+    lo = c0 + (long)b * per;
+    hi = lo + per < c1 ? lo + per : c1;
+  };
+  __shared__ int timed_out;
+  ipc_init_lost(a, &timed_out);
+  const float nan = __builtin_nanf("");
+  // 1. every rank's bucket is final: reduce chunk `rank` straight out of every bucket (rank
+  //    order), in place — no peer reads chunk `rank` of this bucket (each reads its own chunk)
+  bool lost = ipc_round(a, b, s1, &timed_out);
+  {
+    long lo, hi;
+    range(a.rank, lo, hi);
+    for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+      float4 acc = make_float4(nan, nan, nan, nan);
+      if (!lost) {
+        acc = ((const float4*)a.data[0])[i];
+        for (int r = 1; r < a.world; ++r) {
+          const float4 v = ((const float4*)a.data[r])[i];
+          acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
+      }
+      out[i] = acc;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // 2. every reduced chunk is published (the round's release): gather the peers' chunks over
+  //    this bucket's raw ones (each peer finished reading them before it signalled this round)
+  lost = ipc_round(a, b, s2, &timed_out);
+  for (int q = 0; q < a.world; ++q) {
+    if (q == a.rank) continue;
+    long lo, hi;
+    range(q, lo, hi);
+    const float4* peer = (const float4*)a.data[q];
+    for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) out[i] = lost ? make_float4(nan, nan, nan, nan) : peer[i];
+  }
+  if (lost) {
+    long lo, hi;
+    range(a.rank, lo, hi);
+    for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) out[i] = make_float4(nan, nan, nan, nan);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // 3. every peer finished reading this rank's reduced chunk: the bucket is free again
+  ipc_round(a, b, s3, &timed_out);
+  ipc_advance(a, epoch, s3);
+}
+
+// algo 1: one-shot, 2: two-shot (staged), 3: zero-copy two-shot (a.data = the peers' buckets)
 extern "C" int smi_ipc_allreduce(const IpcArgs* args, int blocks, int algo, hipStream_t st) {
   const IpcArgs& a = *args;
   if (a.world < 1 || a.world > IPC_MAX_RANKS || a.rank < 0 || a.rank >= a.world) return -1;
-  if (a.n % 4 || a.n > a.cap || ((uintptr_t)a.buf & 15)) return -1;
-  if (args->spins < 1 || (algo != 1 && algo != 2)) return -1;
+  if (a.n % 4 || (algo != 3 && a.n > a.cap) || ((uintptr_t)a.buf & 15)) return -1;
+  if (args->spins < 1 || algo < 1 || algo > 3) return -1;
+  if (algo == 3) {
+    if (a.data[a.rank] != a.buf) return -1;
+    for (int q = 0; q < a.world; ++q)
+      if ((uintptr_t)a.data[q] & 15) return -1;
+  }
   if (a.p && (algo != 1 || !a.lr || !a.step || ((uintptr_t)a.p & 15) || ((uintptr_t)a.pbf & 7))) return -1;
   if (blocks < 1) blocks = 1;
   if (blocks > IPC_MAX_BLOCKS) blocks = IPC_MAX_BLOCKS;
   if (algo == 1) hipLaunchKernelGGL(ipc_allreduce_kernel, dim3(blocks), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(ipc_allreduce2_kernel, dim3(blocks), dim3(256), 0, st, a);
+  else if (algo == 2) hipLaunchKernelGGL(ipc_allreduce2_kernel, dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(ipc_allreduce_zc_kernel, dim3(blocks), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }

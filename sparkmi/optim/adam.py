@@ -124,45 +124,72 @@ class Adam(_FlatOptimizer):
         self._torch_ranges(self.ranges, self._moff, t)
         f.refresh_planes()
 
+    def _domain(self):
+        """The flat ranges this optimizer updates and their moment offsets (ZeRO-1: the owned
+        pieces, compact moments; otherwise the whole buffer)."""
+        if self.ranges is None:
+            return [(0, self.flat.numel)], [0]
+        return self.ranges, self._moff
+
+    def _moffs(self, ranges):
+        """Moment offsets of flat ranges that lie inside the update domain."""
+        if self.ranges is None:
+            return [s for s, _ in ranges]
+        out = []
+        for s, e in ranges:
+            for (rs, re_), o in zip(self.ranges, self._moff):
+                if rs <= s and e <= re_:
+                    out.append(o + s - rs)
+                    break
+            else:
+                raise ValueError(f"step_ranges: [{s}, {e}) is not inside an owned (ZeRO-1) piece")
+        return out
+
     def step_ranges(self, ranges):
         """Update the parameters in the flat ranges [s, e) NOW, ahead of this step's ``step()``
-        (their gradients are final while the backward still produces others): same step count and
-        bias corrections, the counter is advanced by ``step()``, which then updates only the rest.
-        Element for element the same arithmetic as the one-launch update (tests pin it bitwise)."""
-        if self.ranges is not None:
-            raise RuntimeError("step_ranges: not with a ZeRO-1 sharded optimizer")
+        (their gradients are final while the backward, or the reduction of other gradient
+        buckets, still runs): same step count and bias corrections, the counter is advanced by
+        ``step()``, which then updates only the rest of the domain.  ZeRO-1: the ranges must lie
+        inside owned pieces.  Element for element the same arithmetic as the one-launch update
+        (tests pin it bitwise)."""
         ranges = [(int(s), int(e)) for s, e in ranges if e > s]
         if not ranges:
             return
+        moff = self._moffs(ranges)
         if _native.use_native(self.flat.master):
-            self._multi(ranges, [s for s, _ in ranges], False)
+            self._multi(ranges, moff, False)
         else:
-            self._torch_ranges(ranges, [s for s, _ in ranges], float(self.step_t.item()) + 1)
+            self._torch_ranges(ranges, moff, float(self.step_t.item()) + 1)
             self.flat.refresh_planes()
         self._early.extend(ranges)
 
     def _rest(self):
-        """The flat ranges not updated by step_ranges this step (sorted, merged)."""
+        """The parts of the update domain not updated by step_ranges this step (sorted, merged)
+        and their moment offsets."""
         done = sorted(self._early)
         self._early = []
-        out, pos = [], 0
-        for s, e in done:
-            if s > pos:
-                out.append((pos, s))
-            pos = max(pos, e)
-        if pos < self.flat.numel:
-            out.append((pos, self.flat.numel))
-        return out
+        out, offs = [], []
+        for (ds, de), o in zip(*self._domain()):
+            pos = ds
+            for s, e in done:
+                if e <= ds or s >= de:
+                    continue
+                if s > pos:
+                    out.append((pos, s))
+                    offs.append(o + pos - ds)
+                pos = max(pos, e)
+            if pos < de:
+                out.append((pos, de))
+                offs.append(o + pos - ds)
+        return out, offs
 
     def step(self):
         f = self.flat
-        if self.ranges is not None:
-            return self._step_shard()
         if self._early:
-            rest = self._rest()
+            rest, roff = self._rest()
             if _native.use_native(f.master):
                 if rest:
-                    self._multi(rest, [s for s, _ in rest], True)
+                    self._multi(rest, roff, True)
                 else:  # everything went early: the counter (and the seed) still advance once
                     C = _native.C()
                     C.step_inc(self.step_t.data_ptr(), _native.stream())
@@ -170,9 +197,11 @@ class Adam(_FlatOptimizer):
                         C.seed_inc(self.bump_seed.data_ptr(), _native.stream())
                 return
             t = self._advance_torch()
-            self._torch_ranges(rest, [s for s, _ in rest], t)
+            self._torch_ranges(rest, roff, t)
             f.refresh_planes()
             return
+        if self.ranges is not None:
+            return self._step_shard()
         if _native.use_native(f.master):
             C = _native.C()
             st = _native.stream()

@@ -7,7 +7,12 @@ reading its peers directly over xGMI (one hop on the 7 point-to-point links) ins
     (distributed_multilayer_perceptron.py:103-106, distributed_cnn.py:152-156);
   * two-shot (larger buckets, e.g. the LSTM's 12.3 MB dense embedding gradient): reduce-scatter
     (rank r sums chunk r, reading its 1/w slice from all peers at once) then all-gather —
-    2 (w - 1) / w of the bucket over xGMI per rank instead of (w - 1).
+    2 (w - 1) / w of the bucket over xGMI per rank instead of (w - 1);
+  * zero-copy two-shot (``register(buffer)`` + ``algo=3``): the same reduce-scatter + all-gather
+    read straight out of every rank's IPC-registered gradient buffer (the flat gradient of
+    sparkmi/parallel/ddp.py) — no staging copy, 2 n fewer local HBM bytes per call, one extra
+    signal round so no rank's next backward overwrites a bucket a slow peer still reads.  A probed
+    candidate: DataParallel measures it against the staged kernel and RCCL.
 Both sum in rank order (bit-identical results on every rank) and keep their epoch on the device,
 so a call can sit inside a captured HIP graph (a small model's whole data-parallel step is one
 replay).  A peer that stops signalling is detected by a bounded poll: the bucket is NaN-poisoned,
@@ -24,6 +29,46 @@ import torch.distributed as dist
 from .. import _native
 
 ONE_SHOT_MAX_BYTES = 256 << 10
+
+# IPC lifetime policy (measured, tools/zc_alloc_probe.py: 4 processes creating and closing several
+# instances): once an exported allocation is freed and a new one is exported, peers can map the new
+# handle to stale memory — wrong sums, sometimes only in part of the buffer.  So within a process
+#  * exported staging / signal regions are never hipFree'd: they go back to _POOL (bytes ->
+#    [(ptr, handle)]); a signal region is re-zeroed when handed out again (before the handle
+#    exchange: no peer can signal into it earlier), a staging region is not — a slow peer may
+#    still be reading the last call's chunk from it when this rank has already moved on;
+#  * an allocation is exported once (_EXPORTS: allocation base -> handle), e.g. a torch gradient
+#    segment registered again by a later instance;
+#  * a peer handle is imported once and never closed (_IMPORTS: handle -> mapped base).
+_POOL = {}
+_EXPORTS = {}
+_IMPORTS = {}
+
+
+def _export(C, ptr):
+    """(handle, byte offset of ptr in its allocation) — one export per allocation."""
+    base, size = C.ipc_range(ptr)
+    h = _EXPORTS.get((base, size))
+    if h is None:
+        h = _EXPORTS[(base, size)] = C.ipc_export(base)[0]
+    return h, ptr - base
+
+
+def _open(C, h):
+    p = _IMPORTS.get(h)
+    if p is None:
+        p = _IMPORTS[h] = C.ipc_open(h)
+    return p
+
+
+def _alloc(C, nbytes, zero):
+    free = _POOL.get(nbytes)
+    if free:
+        p, h = free.pop()
+        if zero:
+            C.ipc_memset0(p, nbytes)
+        return p, h
+    return C.ipc_alloc(nbytes)  # (zeroed)
 
 
 class IpcUnavailable(RuntimeError):
@@ -56,12 +101,12 @@ class IpcAllReduce:
         self.blocks = blocks
         # 1 | 2: every call uses that kernel (tests; SPARKMI_IPC_ALGO), else algo_for(size)
         self.force_algo = int(os.environ.get("SPARKMI_IPC_ALGO", "0")) or None
-        data, hdata = C.ipc_alloc(2 * self.cap * 4)
-        sig, hsig = C.ipc_alloc(C.IPC_MAX_BLOCKS * C.IPC_MAX_RANKS * 4)
-        self._own = (data, sig)
+        data, hdata = _alloc(C, 2 * self.cap * 4, zero=False)
+        sig, hsig = _alloc(C, C.IPC_MAX_BLOCKS * C.IPC_MAX_RANKS * 4, zero=True)
+        self._own = ((2 * self.cap * 4, data, hdata), (C.IPC_MAX_BLOCKS * C.IPC_MAX_RANKS * 4, sig, hsig))
         handles = [None] * self.world
         dist.all_gather_object(handles, (hdata, hsig), group=group)
-        self.data, self.sig, self._opened = [], [], []
+        self.data, self.sig = [], []
         opened = True
         for r, (hd, hs) in enumerate(handles):
             if r == self.rank:
@@ -69,11 +114,10 @@ class IpcAllReduce:
                 self.sig.append(sig)
             elif opened:
                 try:
-                    pd, ps = C.ipc_open(hd), C.ipc_open(hs)
+                    pd, ps = _open(C, hd), _open(C, hs)
                 except RuntimeError:
                     opened = False
                     continue
-                self._opened += [pd, ps]
                 self.data.append(pd)
                 self.sig.append(ps)
         self.err = torch.zeros(1, dtype=torch.int32, device="cuda")
@@ -98,7 +142,68 @@ class IpcAllReduce:
             self.close()
             raise IpcUnavailable("IPC all-reduce self-test failed on some rank; using the collective path")
         self.err.zero_()
+        self._reg = None  # (registered tensor, its pointer, every rank's pointer to it)
         dist.barrier(group=group)
+
+    def register(self, buf):
+        """IPC-register ``buf`` (a contiguous fp32 CUDA tensor of the same size on every rank, e.g.
+        the flat gradient buffer) for the zero-copy kernel: every rank maps every peer's copy,
+        then a self-test on ``buf`` (restored afterwards) must give the exact sum on every rank.
+        Collective.  Returns False (every rank agreeing) when mapping or the self-test failed."""
+        C = self.C
+        ok = True
+        why = ""
+        try:
+            h = _export(C, buf.data_ptr())
+        except RuntimeError as e:
+            h, ok, why = None, False, f"export: {e}"
+        hs = [None] * self.world
+        dist.all_gather_object(hs, (h, buf.numel()), group=self.group)
+        ptrs = []
+        ok = ok and all(x[0] is not None and x[1] == buf.numel() for x in hs)
+        if ok:
+            for r, (hq, _) in enumerate(hs):
+                if r == self.rank:
+                    ptrs.append(buf.data_ptr())
+                    continue
+                try:
+                    base = _open(C, hq[0])
+                except RuntimeError as e:
+                    ok, why = False, f"open rank {r}: {e}"
+                    break
+                ptrs.append(base + hq[1])
+        if ok:
+            # the whole buffer (a stale or partial mapping shows up somewhere in it)
+            n = buf.numel() // 4 * 4
+            save = buf[:n].clone()
+            buf[:n].fill_(float(1 << self.rank))  # 2^rank: a wrong sum names the rank it misread
+            self._reg = (buf, buf.data_ptr(), ptrs)
+            self(buf[:n], algo=3)
+            torch.cuda.synchronize()
+            want = float((1 << self.world) - 1)
+            ok = int(self.err.item()) == 0 and bool((buf[:n] == want).all())
+            if not ok:
+                why = (f"self-test: err={int(self.err.item())}, "
+                       f"{int((buf[:n] != want).sum())}/{n} wrong (chunk starts {buf[:n:max(1, n // self.world)].tolist()}, "
+                       f"want {want}); "
+                       f"offsets {[x[0][1] for x in hs]}")
+            dist.barrier(group=self.group)  # every peer finished its self-test reads of this buffer
+            buf[:n].copy_(save)
+            torch.cuda.synchronize()
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                            device="cuda" if dist.get_backend(self.group) == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        self.register_error = why
+        if not int(flag.item()):
+            self._reg = None
+            self.err.zero_()
+            return False
+        self.err.zero_()
+        return True
+
+    @property
+    def registered(self):
+        return self._reg is not None
 
     def algo_for(self, numel):
         """1 = one-shot, 2 = two-shot: two-shot moves 2 (w - 1) / w of the bucket per rank instead of
@@ -110,11 +215,21 @@ class IpcAllReduce:
         None, grad_scale): instead of the sum, apply plain SGD with it to ``params`` (the bucket's
         parameters, same shape as ``t``), zero ``t`` and advance step_t (and the seed) — the
         optimizer launch of a data-parallel small-model step folded into the reduction."""
-        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() % 4 or t.numel() > self.cap:
-            raise ValueError("IpcAllReduce: contiguous fp32 tensor, numel % 4 == 0, <= capacity")
         algo = algo or self.force_algo or self.algo_for(t.numel())
+        if (t.dtype != torch.float32 or not t.is_contiguous() or t.numel() % 4
+                or (algo != 3 and t.numel() > self.cap)):
+            raise ValueError("IpcAllReduce: contiguous fp32 tensor, numel % 4 == 0, <= capacity")
         if sgd is not None and algo != 1:
             raise ValueError("IpcAllReduce: the SGD epilogue is a one-shot feature")
+        data = self.data
+        if algo == 3:  # zero-copy: t must lie in the registered buffer (same offset on every rank)
+            if self._reg is None:
+                raise ValueError("IpcAllReduce: algo 3 needs a registered buffer (register())")
+            reg, base, ptrs = self._reg
+            off = t.data_ptr() - base
+            if off < 0 or off % 16 or off + 4 * t.numel() > 4 * reg.numel():
+                raise ValueError("IpcAllReduce: algo 3 reduces 16-B aligned slices of the registered buffer")
+            data = [p + off for p in ptrs]
         sp = (0, 0, 0, 0, 0, 1.0)
         if sgd is not None:
             p, pbf, lr, step, seed, gscale = sgd
@@ -127,7 +242,7 @@ class IpcAllReduce:
             blocks = max(1, min(self.C.IPC_MAX_BLOCKS, (n4 + 1023) // 1024))
         else:  # >= 512 float4 of every chunk per block
             blocks = max(1, min(self.C.IPC_MAX_BLOCKS, ((n4 + self.world - 1) // self.world + 511) // 512))
-        self.C.ipc_allreduce(t.data_ptr(), t.numel(), self.data, self.sig, self.cap, self.rank, self.ctr.data_ptr(),
+        self.C.ipc_allreduce(t.data_ptr(), t.numel(), data, self.sig, self.cap, self.rank, self.ctr.data_ptr(),
                              self.err.data_ptr(), blocks, (stream or torch.cuda.current_stream()).cuda_stream,
                              self.spins, algo, *sp)
         return t
@@ -144,8 +259,7 @@ class IpcAllReduce:
 
     def close(self):
         torch.cuda.synchronize()
-        for p in self._opened:
-            self.C.ipc_close(p)
-        for p in self._own:
-            self.C.ipc_free(p)
-        self._opened, self._own = [], ()
+        for nbytes, p, h in self._own:
+            _POOL.setdefault(nbytes, []).append((p, h))  # kept for the next instance (see _POOL)
+        self._own = ()  # (peer imports stay mapped: _IMPORTS)
+        self._reg = None

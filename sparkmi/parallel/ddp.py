@@ -26,10 +26,12 @@ module was called, so gradients were never synchronised).  Design for MI355X + R
   <= 256 KB, two-shot reduce-scatter + all-gather above) — no ring latency, and since it is a
   stream-ordered kernel with a device-side epoch, the whole data-parallel step (forward,
   backward, all-reduce, optimizer) is captured as ONE HIP graph (``graph_safe``).  For larger
-  gradients (the transformer's 188 MB) auto MEASURES both paths at start-up on the largest
-  bucket (``comm_probe``: IPC two-shot vs the RCCL process group vs an RCCL communicator with
-  min_ctas = 32, i.e. more rings over the 7 xGMI links; max over ranks) and keeps the
-  faster; ``SPARKMI_DP_PROBE=0`` sends them to RCCL without measuring.  Either way a bucket's
+  gradients (the transformer's 188 MB) auto MEASURES the paths at start-up on the largest
+  bucket (``comm_probe``: the staged IPC two-shot vs the ZERO-COPY IPC two-shot — every rank's
+  flat gradient buffer IPC-registered, peers read the buckets in place, no staging copy — vs the
+  RCCL process group vs an RCCL communicator with min_ctas = 32, i.e. more rings over the 7 xGMI
+  links; max over ranks, each IPC kernel also checked for an exact sum / no timeout) and keeps the
+  fastest; ``SPARKMI_DP_PROBE=0`` sends them to RCCL without measuring.  Either way a bucket's
   reduction runs on a side stream (RCCL's own, or the IPC comm stream forked from the compute
   stream at launch and joined in ``finish()``), overlapped with the rest of the backward.
 * ``sparse_rows={param: ids_fn or (ids_fn, cap)}`` (opt-in; SURVEY §5.8 item 5, the LSTM
@@ -44,6 +46,12 @@ module was called, so gradients were never synchronised).  Design for MI355X + R
   no host sync at all; without it the ranks agree on the longest list with one small all-reduce
   read on the host each step.  Uses the process group, so a DP step with sparse rows is not a
   single-graph (``graph_safe``) step.
+* optimizer per bucket (``attach_optimizer``, PER_BUCKET_OPT): an optimizer with ``step_ranges``
+  (Adam/AdamW, ZeRO-1 included) updates bucket b's range (its owned piece under ZeRO-1) right after
+  bucket b's reduction completed — in launch order, each behind its own RCCL work or IPC event —
+  so the update of early buckets runs under the reduction of later ones; ``step()`` then updates
+  the last bucket and advances the step counter once (same bias corrections: bitwise the
+  one-launch update).
 The CPU/gloo path runs the identical logic (multi-process CPU tests).
 """
 import os
@@ -56,15 +64,18 @@ from ..ops import _grad
 IPC_LIMIT_BYTES = 32 << 20  # auto without a measurement: IPC kernels up to this gradient size
 
 
-def choose_comm(ipc_ms, rccl_ms, rccl_mc_ms=None):
+def choose_comm(ipc_ms, rccl_ms, rccl_mc_ms=None, ipc_zc_ms=None):
     """The auto path for a bulk gradient from a measured all-reduce of its largest bucket (max over
-    ranks): 'ipc' (the IPC two-shot kernel), 'rccl' (the process group's RCCL communicator) or
-    'rccl_mc' (an RCCL communicator created with min_ctas = 32: more channels, i.e. more rings
-    over the 7 point-to-point xGMI links of a node).  The fastest wins; a tie prefers that order
-    (the graph-capturable kernel first).  All run on a side stream overlapped with the backward,
-    so the isolated bucket time is the right comparison.  None = path unavailable."""
-    cands = [(name, ms) for name, ms in (("ipc", ipc_ms), ("rccl", rccl_ms), ("rccl_mc", rccl_mc_ms))
-             if ms is not None]
+    ranks): 'ipc' (the staged IPC two-shot kernel), 'ipc_zc' (the zero-copy IPC two-shot, reading
+    the peers' registered gradient buffers directly), 'rccl' (the process group's RCCL
+    communicator) or 'rccl_mc' (an RCCL communicator created with min_ctas = 32: more channels,
+    i.e. more rings over the 7 point-to-point xGMI links of a node).  The fastest wins; a tie
+    prefers that order (the graph-capturable kernels first, the staged one — no peer access to
+    live gradient memory — before the zero-copy one).  All run on a side stream overlapped with
+    the backward, so the isolated bucket time is the right comparison.  None = path unavailable
+    (not built, or it failed its NaN / timeout check)."""
+    cands = [(name, ms) for name, ms in (("ipc", ipc_ms), ("ipc_zc", ipc_zc_ms), ("rccl", rccl_ms),
+                                         ("rccl_mc", rccl_mc_ms)) if ms is not None]
     if not cands:
         return "rccl"
     return min(cands, key=lambda c: c[1])[0]
@@ -74,6 +85,14 @@ MIN_CTAS = 32  # RCCL channels of the multi-channel communicator the probe measu
 # plain SGD applied inside the one-shot IPC all-reduce (fuse_sgd): a data-parallel small-model step
 # is then the fused gradient kernel + ONE reduction-and-update launch (False: a separate SGD launch)
 FUSE_SGD = True
+# the optimizer per gradient bucket: finish() updates each bucket's parameters
+# as soon as THAT bucket's reduction completed (RCCL work / IPC event wait), while the later buckets
+# still reduce; only the last bucket's update stays behind the collective (False: one update after
+# every bucket)
+PER_BUCKET_OPT = True
+# the zero-copy IPC two-shot (peers read each other's registered gradient buffers, no staging copy)
+# is a candidate of the bulk-gradient probe (False: not registered, never measured)
+ZERO_COPY = True
 
 
 def multichannel_group(world, min_ctas=MIN_CTAS):
@@ -103,7 +122,7 @@ def _single_node(world):
 
 class DataParallel:
     def __init__(self, flat, group=None, bucket_mb=64.0, overlap=True, broadcast=True, zero=False, ipc=None,
-                 sparse_rows=None):
+                 sparse_rows=None, comm=None):
         self.flat = flat
         # parameter index -> callable returning the step's touched row ids (row-sparse exchange),
         # and its optional fixed list capacity
@@ -124,9 +143,13 @@ class DataParallel:
         if self.zero and 64 % self.world:
             raise ValueError("zero=True needs a world size dividing 64 (buckets are 64-element aligned)")
         self.ipc = None
-        mode = os.environ.get("SPARKMI_DP_COMM", "auto")
-        if mode not in ("auto", "ipc", "rccl"):
-            raise ValueError(f"SPARKMI_DP_COMM={mode!r}: auto | ipc | rccl")
+        self._zc = False  # buckets go through the zero-copy IPC kernel (forced, or the probe chose it)
+        # comm: auto | ipc | ipc_zc (every bucket through the zero-copy kernel) | rccl
+        mode = comm or os.environ.get("SPARKMI_DP_COMM", "auto")
+        if mode not in ("auto", "ipc", "ipc_zc", "rccl"):
+            raise ValueError(f"SPARKMI_DP_COMM={mode!r}: auto | ipc | ipc_zc | rccl")
+        if mode == "ipc_zc":
+            ipc = True
         if ipc is None:
             ipc = os.environ.get("SPARKMI_IPC_AR", "1") != "0" and mode != "rccl"
         # bulk gradients in auto mode: measure the paths on the largest bucket and keep the fastest
@@ -148,14 +171,24 @@ class DataParallel:
                 self.ipc = IpcAllReduce(cap_floats=self._ipc_capacity(), group=group)
             except IpcUnavailable:
                 self.ipc = None  # every rank agreed: buckets go through the process group
+        if mode == "ipc_zc":
+            if self.ipc is None or not self.ipc.register(flat.grad):
+                why = getattr(self.ipc, "register_error", "") if self.ipc is not None else "no IPC path"
+                raise RuntimeError(f"comm='ipc_zc': the zero-copy IPC all-reduce is unavailable here "
+                                   f"(rank {self.rank}: {why or 'a peer failed'})")
+            self._zc = True
         if probe:
             n = max(e - s for s, e, _ in self.buckets)
             mc = multichannel_group(self.world) if group is None else None
-            ipc_ms, rccl_ms, mc_ms = self._probe(n, mc)
-            choice = choose_comm(ipc_ms, rccl_ms, mc_ms)
-            self.comm_probe = {"bucket_bytes": n * 4, "ipc_ms": ipc_ms, "rccl_ms": rccl_ms,
+            # the zero-copy candidate: every rank's flat gradient buffer IPC-registered (collective;
+            # all ranks agree whether mapping and its self-test succeeded)
+            zc = (self.ipc is not None and ZERO_COPY and self.ipc.register(flat.grad))
+            ipc_ms, rccl_ms, mc_ms, zc_ms = self._probe(n, mc, zc=zc)
+            choice = choose_comm(ipc_ms, rccl_ms, mc_ms, zc_ms)
+            self.comm_probe = {"bucket_bytes": n * 4, "ipc_ms": ipc_ms, "ipc_zc_ms": zc_ms, "rccl_ms": rccl_ms,
                                f"rccl_min_ctas{MIN_CTAS}_ms": mc_ms, "choice": choice}
-            if choice != "ipc" and self.ipc is not None:
+            self._zc = choice == "ipc_zc"
+            if choice not in ("ipc", "ipc_zc") and self.ipc is not None:
                 self.ipc.close()
                 self.ipc = None
             if choice == "rccl_mc":
@@ -169,6 +202,9 @@ class DataParallel:
         self._cs_used = False
         self._pending = None
         self._works = []
+        self._order = []  # (bucket, completion handle) in launch order: RCCL work, IPC event or None
+        self._bopt = None
+        self.opt_buckets_early = 0
         self._listener = None
         self._dlistener = None
         if self.world > 1:
@@ -182,14 +218,15 @@ class DataParallel:
     @property
     def comm(self):
         if self.ipc is not None:
-            return "ipc"
+            return "ipc_zc" if self._zc else "ipc"
         if self.world <= 1:
             return "none"
         return "rccl_mc" if self._mc_group is not None else "rccl"
 
-    def _probe(self, n, mc=None, iters=3):
-        """(IPC two-shot ms or None, process-group ms, multi-channel RCCL ms or None) of an n-float
-        all-reduce, max over ranks."""
+    def _probe(self, n, mc=None, iters=3, zc=False):
+        """(IPC two-shot ms or None, process-group ms, multi-channel RCCL ms or None, zero-copy IPC
+        two-shot ms or None) of an n-float all-reduce, max over ranks.  The zero-copy kernel runs
+        on the first n floats of the registered gradient buffer (zeroed again afterwards)."""
         import time
         dev = self.flat.grad.device
         x = torch.zeros(n, dtype=torch.float32, device=dev)
@@ -216,6 +253,23 @@ class DataParallel:
             return round(float(t.item()), 3)
 
         ipc_ms = timed(lambda: self.ipc(x)) if self.ipc is not None else None
+        zc_ms = None
+        if zc:
+            gz = self.flat.grad[:n]
+            bad = 0.0
+            try:
+                zc_ms = timed(lambda: self.ipc(gz, algo=3))
+                # a wrong sum must not be chosen: all-ones in, world out, on every rank
+                gz.fill_(1.0)
+                self.ipc(gz, algo=3)
+                sync()
+                bad = 0.0 if bool((gz == float(self.world)).all()) else 1.0
+            finally:
+                gz.zero_()
+            f = torch.tensor([bad], dtype=torch.float32, device=fdev)
+            dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
+            if float(f.item()) > 0:
+                zc_ms = None
         rccl_ms = timed(lambda: dist.all_reduce(x, group=self.group))
         mc_ms = timed(lambda: dist.all_reduce(x, group=mc)) if mc is not None else None
         if self.ipc is not None:
@@ -231,8 +285,8 @@ class DataParallel:
             f = torch.tensor([bad], dtype=torch.float32, device=fdev)
             dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
             if float(f.item()) > 0:
-                ipc_ms = None
-        return ipc_ms, rccl_ms, mc_ms
+                ipc_ms = zc_ms = None
+        return ipc_ms, rccl_ms, mc_ms, zc_ms
 
     def _ipc_capacity(self):
         """Staging floats for the IPC kernels: any bucket _build_buckets can cut (for any set of
@@ -305,6 +359,7 @@ class DataParallel:
         self._settled = set()
         self._launched = [False] * len(self.buckets)
         self._works = []
+        self._order = []
         self.early_flushes = 0
 
     _learning = True
@@ -355,6 +410,17 @@ class DataParallel:
 
     last_step_fused = False
 
+    def attach_optimizer(self, opt):
+        """Update each bucket's parameters as soon as its reduction completes (PER_BUCKET_OPT): for
+        an optimizer over this buffer with ``step_ranges``.  Returns whether it applies."""
+        self._bopt = (opt if (PER_BUCKET_OPT and self.world > 1 and hasattr(opt, "step_ranges")
+                              and getattr(opt, "flat", None) is self.flat) else None)
+        return self._bopt is not None
+
+    def update_range(self, b):
+        """The flat range the optimizer updates for bucket ``b`` (ZeRO-1: the owned piece)."""
+        return self.piece(b) if self.zero else self.buckets[b][:2]
+
     def _launch(self, b):
         if self._launched[b]:
             return
@@ -364,15 +430,19 @@ class DataParallel:
             _grad.join(self.flat.grad.device.index)  # weight grads may still be in flight on the side stream
         if len(idx) == 1 and idx[0] in self._sparse:
             self._sparse_exchange(s, e, idx[0])
+            self._order.append((b, None))  # complete in the current stream's order
             return
         g = self.flat.grad[s:e]
         self.bytes_reduced += g.numel() * g.element_size()
         if self.ipc is not None:
             self._cs.wait_stream(torch.cuda.current_stream(g.device))  # the bucket's gradients are written
             sgd = self._sgd_args(s, e)
-            self.ipc(g, stream=self._cs, sgd=sgd)
+            self.ipc(g, algo=3 if self._zc else None, stream=self._cs, sgd=sgd)
             self._sgd_applied = sgd is not None
             self._cs_used = True
+            ev = torch.cuda.Event()
+            ev.record(self._cs)
+            self._order.append((b, ev))
             return
         if self.zero:
             ps, pe = self.piece(b)
@@ -380,6 +450,7 @@ class DataParallel:
         else:
             w = dist.all_reduce(g, group=self.bulk_group, async_op=True)
         self._works.append(w)
+        self._order.append((b, w))
 
     def _sparse_exchange(self, s, e, i):
         """Row-sparse reduction of parameter ``i``'s gradient (flat slice [s, e), rows of the
@@ -524,8 +595,11 @@ class DataParallel:
             self._launch(b)
 
     def finish(self):
-        """Complete every bucket's all-reduce (launching any not yet issued) before the optimizer."""
+        """Complete every bucket's reduction (launching any not yet issued) before the optimizer
+        step.  With an attached optimizer (attach_optimizer) every bucket but the last launched is
+        updated here, each right after its own reduction completed."""
         self.last_step_fused = False
+        self.opt_buckets_early = 0
         if self.world <= 1:
             self.reset()
             return
@@ -533,10 +607,19 @@ class DataParallel:
         for b in range(len(self.buckets)):
             self._launch(b)
         self.last_step_fused = self._sgd_applied
-        for w in self._works:
-            w.wait()
+        opt = None if self.last_step_fused else self._bopt
+        cur = torch.cuda.current_stream(self.flat.grad.device) if self.flat.grad.is_cuda else None
+        order = self._order
+        for k, (b, h) in enumerate(order):
+            if isinstance(h, torch.cuda.Event):
+                cur.wait_event(h)
+            elif h is not None:
+                h.wait()
+            if opt is not None and k < len(order) - 1:
+                opt.step_ranges([self.update_range(b)])
+                self.opt_buckets_early += 1
         if self._cs_used:
-            torch.cuda.current_stream(self.flat.grad.device).wait_stream(self._cs)
+            cur.wait_stream(self._cs)
             self._cs_used = False
         self.reset()
 

@@ -34,7 +34,9 @@ import time
 
 class LaunchError(RuntimeError):
     def __init__(self, msg, rank=None, returncode=None, log_tail=""):
-        super().__init__(msg)
+        # the failing rank's last log lines travel in the message (pytest / callers show them)
+        super().__init__(msg + (f"\n--- rank {rank} log tail ---\n{log_tail}" if log_tail else ""))
+        self.msg = msg
         self.rank, self.returncode, self.log_tail = rank, returncode, log_tail
 
 

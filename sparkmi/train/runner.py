@@ -143,6 +143,8 @@ class StepRunner:
                 optimizer.shard(ddp.shard_ranges())
             elif hasattr(ddp, "fuse_sgd"):
                 ddp.fuse_sgd(optimizer)  # plain SGD inside the one-shot IPC reduction, when it applies
+            if hasattr(ddp, "attach_optimizer"):
+                ddp.attach_optimizer(optimizer)  # the update per gradient bucket, behind its reduction
 
     def _opt_step(self):
         """The optimizer launch — unless the gradient reduction just applied it (ddp.fuse_sgd)."""

@@ -86,6 +86,18 @@ _CFGS = [  # name, optimizer, zero, graph, split, ipc
     ("sgd_ipc2_eager", "sgd", False, False, False, 2),
     ("sgd_ipc2_split", "sgd", False, True, True, 2),
     ("adam_ipc2_split", "adam", False, True, True, 2),
+    ("adam_ipc2_graph", "adam", False, True, False, 2),
+    # the zero-copy IPC two-shot (3): peers read each other's registered flat gradient in place
+    ("sgd_zc_split", "sgd", False, True, True, 3),
+    ("adam_zc_graph", "adam", False, True, False, 3),
+    ("adam_zc_eager", "adam", False, False, False, 3),
+    # "_1u": one optimizer update after every bucket (PER_BUCKET_OPT off) — the per-bucket update
+    # (each bucket's Adam behind its own RCCL work / IPC event) must equal it bit for bit
+    ("adam_eager_1u", "adam", False, False, False, False),
+    ("adam_zero_split_1u", "adam", True, True, True, False),
+    ("adam_split_1u", "adam", False, True, True, False),
+    ("adam_ipc2_split_1u", "adam", False, True, True, 2),
+    ("adam_ipc2_graph_1u", "adam", False, True, False, 2),
 ]
 
 
@@ -95,6 +107,7 @@ def _dp_grid(steps, only=None):
     from sparkmi.ops.rng import reset_salts
     from sparkmi.optim import SGD, Adam
     from sparkmi.parallel import DataParallel, init_distributed
+    from sparkmi.parallel import ddp as ddp_mod
     from sparkmi.train.runner import StepRunner
     from sparkmi.utils.flat import FlatParams
     rank, world, device = init_distributed()
@@ -107,20 +120,25 @@ def _dp_grid(steps, only=None):
             continue
         if only is not None and name not in only:
             continue
+        ddp_mod.PER_BUCKET_OPT = not name.endswith("_1u")
         reset_salts()
         torch.manual_seed(0)
         m = Transformer(d_model=128, ffn_hidden=256, num_heads=2, drop_prob=0.0, num_layers=2, max_sequence_length=64,
                         src_vocab_size=300, tgt_vocab_size=300, emb_dropout=0.0, dtype="fp32").to(device)
         flat = FlatParams(m, shadow=False)
         opt = SGD(flat, lr=0.05) if ok == "sgd" else Adam(flat, lr=1e-3)
-        ddp = DataParallel(flat, bucket_mb=0.5, zero=zero, ipc=bool(ipc)) if world > 1 else None
+        ddp = (DataParallel(flat, bucket_mb=0.5, zero=zero, ipc=bool(ipc), comm="ipc_zc" if ipc == 3 else None)
+               if world > 1 else None)
         if ddp is not None:
             assert (ddp.ipc is not None) == bool(ipc), name
+            assert (ddp.comm == "ipc_zc") == (ipc == 3), name
             if ipc == 2:
                 ddp.ipc.force_algo = 2
         split_fn = (lambda mm, s, t: mm.training_step_split(s, t)) if split else None
         runner = StepRunner(m, lambda mm, s, t: mm.training_step_loss(s, t), opt, ddp, graph=graph, warmup_eager=2,
                             split_fn=split_fn)
+        if ddp is not None:
+            assert (ddp._bopt is not None) == (ok == "adam" and ddp_mod.PER_BUCKET_OPT), name
         for i in range(steps):
             runner.step(data[i, 0, rank * per:(rank + 1) * per].contiguous(),
                         data[i, 1, rank * per:(rank + 1) * per].contiguous())
@@ -130,6 +148,7 @@ def _dp_grid(steps, only=None):
             ddp.check()
             ddp.close()
         del runner, opt, ddp, flat, m
+    ddp_mod.PER_BUCKET_OPT = True
     import torch.distributed as dist
     if world == 1:
         return [out]
@@ -165,6 +184,14 @@ def test_transformer_dp_parity_grid():
     assert torch.equal(a["sgd_ipc2_split"], a["sgd_ipc2_eager"])
     torch.testing.assert_close(a["sgd_ipc2_eager"], r1["sgd_eager"], rtol=1e-4, atol=1e-5)
     assert (a["adam_ipc2_split"] - r1["adam_eager"]).abs().max() < 5 * 1e-3 * 5
+    assert torch.equal(a["adam_ipc2_graph"], a["adam_ipc2_split"])
+    # zero-copy two-shot: the staged two-shot's rank-order sums, bit for bit
+    assert torch.equal(a["sgd_zc_split"], a["sgd_ipc2_split"])
+    assert torch.equal(a["adam_zc_graph"], a["adam_ipc2_graph"])
+    assert torch.equal(a["adam_zc_eager"], a["adam_ipc2_graph"])
+    # the optimizer per bucket == one update after every bucket, bit for bit
+    for name in ("adam_eager", "adam_zero_split", "adam_split", "adam_ipc2_split", "adam_ipc2_graph"):
+        assert torch.equal(a[name], a[name + "_1u"]), name
 
 
 @pytest.mark.gpu
@@ -175,7 +202,7 @@ def test_transformer_dp_parity_grid_world4():
     2-rank grid cannot reach."""
     env = {"SPARKMI_DIST_BACKEND": "gloo"}
     only = ("sgd_eager", "sgd_split", "sgd_ipc_eager", "sgd_ipc2_split", "adam_eager", "adam_zero_eager",
-            "adam_zero_split", "adam_split")
+            "adam_zero_split", "adam_split", "adam_zero_split_1u", "adam_split_1u", "sgd_zc_split", "adam_zc_graph")
     r4 = launch(_dp_grid, (4, only), {}, num_processes=4, use_gpu=True, env=env, log_sink=None, timeout=380)
     (r1,) = launch(_dp_grid, (4,), {}, num_processes=1, use_gpu=True, env=env, log_sink=None, timeout=380)
     for name in r4[0]:
@@ -189,6 +216,11 @@ def test_transformer_dp_parity_grid_world4():
     assert (a["adam_zero_eager"] - a["adam_eager"]).abs().max() < 5 * 1e-3 * 4
     assert (a["adam_zero_split"] - a["adam_split"]).abs().max() < 5 * 1e-3 * 4
     assert (a["adam_eager"] - r1["adam_eager"]).abs().max() < 5 * 1e-3 * 4
+    for name in ("adam_zero_split", "adam_split"):
+        assert torch.equal(a[name], a[name + "_1u"]), name
+    # zero-copy two-shot at 4 ranks (4-chunk ranges): the staged kernel's sums, bit for bit
+    assert torch.equal(a["sgd_zc_split"], a["sgd_ipc2_split"])
+    assert (a["adam_zc_graph"] - r1["adam_eager"]).abs().max() < 5 * 1e-3 * 4
 
 
 # ---- small models over the IPC kernels: the whole-step graph and the two-shot path ----
@@ -348,3 +380,41 @@ def test_cnn_dp_fused_step_matches_single_process(world):
                             log_sink=None, timeout=300)
         assert not comm2[1] and comm2[2] == 7.0, comm2
         assert torch.equal(rs2[0], rs[0]), f"fused SGD != sgd_kernel (graph={graph} bind={bind})"
+
+
+# ---- the bulk-gradient probe with its four candidates on the GPU ----
+def _probe_gpu():
+    import torch
+    from sparkmi.parallel import ddp, init_distributed
+    from sparkmi.utils.flat import FlatParams
+    rank, world, dev = init_distributed()
+    ddp.IPC_LIMIT_BYTES = 1024  # a "bulk" gradient at test size: the start-up probe runs
+    torch.manual_seed(0)
+    flat = FlatParams(torch.nn.Sequential(torch.nn.Linear(512, 512), torch.nn.Linear(512, 512)).to(dev),
+                      shadow=False)
+    dp = ddp.DataParallel(flat, bucket_mb=0.5)
+    out = dict(dp.comm_probe)
+    out["comm"] = dp.comm
+    ok = True
+    for it in range(3):  # the chosen path reduces every bucket exactly (two operands commute)
+        flat.grad.fill_(float(rank + 1 + it))
+        dp.finish()
+        torch.cuda.synchronize()
+        ok = ok and bool((flat.grad == float(sum(r + 1 + it for r in range(world)))).all())
+    dp.check()
+    dp.close()
+    out["ok"] = ok
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_probe_measures_zero_copy_candidate(world):
+    """Ranks sharing the GPU: the start-up probe registers every rank's flat gradient, measures the
+    staged AND the zero-copy IPC two-shot (both pass their exact-sum checks) and the process group,
+    and the path it keeps reduces exactly."""
+    res = launch(_probe_gpu, (), {}, num_processes=world, use_gpu=True, env={"SPARKMI_DIST_BACKEND": "gloo"},
+                 log_sink=None, timeout=280)
+    assert res["ipc_ms"] is not None and res["ipc_zc_ms"] is not None and res["rccl_ms"] is not None, res
+    assert res["choice"] == res["comm"] and res["ok"], res

@@ -5,6 +5,8 @@
   split (multi-piece) backward and its bucket re-cut + moment re-shard, and with small buckets;
 * transformer data parallelism: 2 ranks x batch b == 1 rank x batch 2b (same global batch),
   params after several Adam steps agree to fp32 reassociation tolerance (SURVEY §4.2 T2);
+* optimizer per bucket: each bucket's Adam update right after its own reduction equals the
+  single update bit for bit (plain and ZeRO-1);
 * per-bucket early flush: with deferred (grouped) weight gradients, buckets still complete
   during the backward (DataParallel.early_flushes) and the result equals the non-deferred run.
 Reference collective sites: distributed_multilayer_perceptron.py:103-106,
@@ -40,13 +42,16 @@ def _make(seed=3):
     return m.train()
 
 
-def _run(steps, zero, split, bucket_mb, dp=True, global_batch=2 * B):
+def _run(steps, zero, split, bucket_mb, dp=True, global_batch=2 * B, per_bucket=None):
     import torch
     from sparkmi.optim import Adam
     from sparkmi.parallel import DataParallel, init_distributed, rank, world_size
+    from sparkmi.parallel import ddp as ddp_mod
     from sparkmi.train.runner import StepRunner
     from sparkmi.utils.flat import FlatParams
     init_distributed()
+    if per_bucket is not None:
+        ddp_mod.PER_BUCKET_OPT = per_bucket
     m = _make()
     flat = FlatParams(m)
     opt = Adam(flat, lr=1e-2)
@@ -61,12 +66,14 @@ def _run(steps, zero, split, bucket_mb, dp=True, global_batch=2 * B):
     out = flat.master.clone()
     if ddp is not None:
         ddp.close()
+        if per_bucket is not None:
+            return out, ddp.opt_buckets_early, len(ddp.buckets)
     return out
 
 
-def _dp(zero, split=False, bucket_mb=0.25, steps=4):
-    return Distributor(num_processes=2, use_gpu=False, log_sink=None, timeout=300).run(_run, steps, zero, split,
-                                                                                         bucket_mb)
+def _dp(zero, split=False, bucket_mb=0.25, steps=4, per_bucket=None):
+    return Distributor(num_processes=2, use_gpu=False, log_sink=None, timeout=300).run(
+        _run, steps, zero, split, bucket_mb, per_bucket=per_bucket)
 
 
 def test_zero1_equals_allreduce_bitwise():
@@ -78,6 +85,18 @@ def test_zero1_equals_allreduce_bitwise():
 def test_zero1_split_backward_reshard_bitwise():
     a = _dp(False, split=True)
     b = _dp(True, split=True)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("zero,split", [(False, False), (True, False), (True, True)])
+def test_per_bucket_optimizer_bitwise(zero, split):
+    """the Adam update per gradient bucket, each behind its own
+    reduction (DataParallel.attach_optimizer), gives the one-update-after-all-buckets parameters bit
+    for bit — plain all-reduce and ZeRO-1 (owned pieces, compact moments), with the split backward's
+    bucket re-cut and moment re-shard; every bucket but the last is updated early."""
+    a, na, nb = _dp(zero, split=split, bucket_mb=0.05, per_bucket=True)
+    b, nb0, _ = _dp(zero, split=split, bucket_mb=0.05, per_bucket=False)
+    assert nb > 2 and na == nb - 1 and nb0 == 0
     assert torch.equal(a, b)
 
 
@@ -210,6 +229,21 @@ def test_choose_comm_three_paths():
     assert choose_comm(None, 2.0, None) == "rccl"
 
 
+def test_choose_comm_four_paths():
+    """the zero-copy IPC two-shot is a fourth probed candidate — fastest wins; ties
+    prefer staged IPC, then zero-copy IPC, then the RCCL groups; a candidate that failed its exact-
+    sum / timeout check (None) is never chosen."""
+    from sparkmi.parallel.ddp import choose_comm
+    assert choose_comm(2.0, 3.0, 3.0, 1.0) == "ipc_zc"
+    assert choose_comm(1.0, 3.0, 3.0, 1.0) == "ipc"        # tie: the staged kernel
+    assert choose_comm(None, 3.0, 3.0, 2.0) == "ipc_zc"
+    assert choose_comm(2.0, 1.0, 3.0, 1.0) == "ipc_zc"     # tie with rccl: the graph-capturable kernel
+    assert choose_comm(2.0, 1.0, 0.5, 1.5) == "rccl_mc"
+    assert choose_comm(2.0, 1.0, None, None) == "rccl"
+    assert choose_comm(None, None, None, None) == "rccl"
+    assert choose_comm(None, 2.0, None, 0.1) == "ipc_zc"
+
+
 def _probe_run():
     import torch
     from sparkmi.parallel import ddp, init_distributed
@@ -229,6 +263,7 @@ def test_dp_probe_lists_three_paths_gloo():
     from sparkmi.api import Distributor
     probe, comm, default_group = Distributor(num_processes=2, use_gpu=False, log_sink=None,
                                              timeout=120).run(_probe_run)
-    assert set(probe) >= {"bucket_bytes", "ipc_ms", "rccl_ms", "rccl_min_ctas32_ms", "choice"}
-    assert probe["ipc_ms"] is None and probe["rccl_min_ctas32_ms"] is None and probe["rccl_ms"] > 0
+    assert set(probe) >= {"bucket_bytes", "ipc_ms", "ipc_zc_ms", "rccl_ms", "rccl_min_ctas32_ms", "choice"}
+    assert probe["ipc_ms"] is None and probe["ipc_zc_ms"] is None and probe["rccl_min_ctas32_ms"] is None
+    assert probe["rccl_ms"] > 0
     assert probe["choice"] == "rccl" and comm == "rccl" and default_group

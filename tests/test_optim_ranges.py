@@ -45,3 +45,29 @@ def test_adam_all_early_still_advances():
     opt.step()
     assert float(opt.step_t) == 1.0
     assert torch.count_nonzero(flat.grad) == 0
+
+
+def test_adam_step_ranges_sharded_equals_one_update():
+    """ZeRO-1 (compact moments over owned pieces): updating parts of the pieces early (the per-bucket
+    update of sparkmi/parallel/ddp.py) then step() == the one multi-range update; a range outside
+    the owned pieces is refused."""
+    base = _model()
+    runs = []
+    for split in (False, True):
+        m = copy.deepcopy(base)
+        flat = FlatParams(m, shadow=False)
+        n = flat.numel
+        opt = Adam(flat, lr=1e-2).shard([(64, n // 2), (n // 2 + 64, n)])
+        g = torch.Generator().manual_seed(2)
+        for step in range(3):
+            flat.grad.copy_(torch.randn(n, generator=g))
+            if split:
+                opt.step_ranges([(64, 128), (n // 2 + 64, n)])  # part of piece 0, all of piece 1
+            opt.step()
+            assert not opt._early
+        runs.append((flat.master.clone(), opt.m.clone(), opt.v.clone(), opt.step_t.clone()))
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+    import pytest
+    with pytest.raises(ValueError):
+        opt.step_ranges([(0, 64)])
