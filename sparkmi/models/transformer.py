@@ -28,6 +28,7 @@ from torch import nn
 
 from ..ops import (DropoutRNG, add_dropout_layernorm, cross_attention, embedding, linear, self_attention,
                    sinusoid_table)
+from ..ops import _grad
 from ..ops._grad import ResidualGrad
 from ..ops._grad import SharedGrad
 from ..ops.linear import concat_linear, ffn
@@ -262,11 +263,28 @@ class DecoderLayer(nn.Module):
         return self.layer_norm3(f, y, ps[2], self._rng, self.salts[2], r_slot=s3)
 
 
+# The top DEC_MID_FLUSH decoder layers' queued weight gradients (and the vocabulary projection's)
+# go to the side stream as soon as those layers' backward is done, instead of with the rest at the
+# decoder/encoder cut (0: one group at the cut).  In-step A/B (profiles/r6_dec_mid_flush_ab.txt):
+# fp32 4 layers -0.06 ms (the first group overlaps the lower decoder layers' backward, the group
+# at the cut is smaller); bf16 +0.04 ms at 4, so bf16 (DEC_MID_FLUSH_BF16) keeps one group
+DEC_MID_FLUSH = 4
+DEC_MID_FLUSH_BF16 = 0
+
+
+def _mid_flush(g):
+    _grad.flush_groups_async(g.device)
+
+
 class SequentialDecoder(nn.Sequential):
     def forward(self, *inputs):
         x, y, self_mode, cross_mode, key_padding = inputs[:5]
         kvs = inputs[5] if len(inputs) > 5 and inputs[5] is not None else [None] * len(self._modules)
-        for module, kv in zip(self._modules.values(), kvs):
+        n = len(self._modules)
+        k = DEC_MID_FLUSH_BF16 if y.dtype == torch.bfloat16 else DEC_MID_FLUSH
+        for i, (module, kv) in enumerate(zip(self._modules.values(), kvs)):
+            if k and i == n - k and y.requires_grad and torch.is_grad_enabled():
+                y.register_hook(_mid_flush)
             y = module(x, y, self_mode, cross_mode, key_padding, kv)
         return y
 
