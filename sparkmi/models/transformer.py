@@ -215,10 +215,27 @@ class EncoderLayer(nn.Module):
         return self.norm2(f, x, p2, self._rng, self.salts[1], r_slot=s2)
 
 
+def _mid_flush(g):
+    _grad.flush_groups_async(g.device)
+
+
+# The top ENC_MID_FLUSH encoder layers' queued weight gradients go to the side stream once their
+# backward is done (0: with the rest, launched by the encoder embedding's backward).  In-step A/B
+# (profiles/r6_dec_mid_flush_ab.txt): bf16 4 layers -0.15 ms (the lower layers' backward runs
+# beside them and the final group is shorter); fp32 +0.06..0.3 ms (its long compute-bound group
+# tiles starve the lower layers' dgrad chain), so fp32 keeps one group
+ENC_MID_FLUSH = 0
+ENC_MID_FLUSH_BF16 = 4
+
+
 class SequentialEncoder(nn.Sequential):
     def forward(self, *inputs):
         x, mode, key_padding = inputs
-        for module in self._modules.values():
+        n = len(self._modules)
+        k = ENC_MID_FLUSH_BF16 if x.dtype == torch.bfloat16 else ENC_MID_FLUSH
+        for i, module in enumerate(self._modules.values()):
+            if k and i == n - k and x.requires_grad and torch.is_grad_enabled():
+                x.register_hook(_mid_flush)
             x = module(x, mode, key_padding)
         return x
 
@@ -270,10 +287,6 @@ class DecoderLayer(nn.Module):
 # at the cut is smaller); bf16 +0.04 ms at 4, so bf16 (DEC_MID_FLUSH_BF16) keeps one group
 DEC_MID_FLUSH = 4
 DEC_MID_FLUSH_BF16 = 0
-
-
-def _mid_flush(g):
-    _grad.flush_groups_async(g.device)
 
 
 class SequentialDecoder(nn.Sequential):
