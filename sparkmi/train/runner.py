@@ -31,54 +31,74 @@ from ..ops.embedding import join_plans
 # side stream, behind their weight-gradient group and beside the encoder's backward; step()
 # then updates the rest and advances the step counter.  Bitwise the one-launch update.
 EARLY_UPDATE = True
+# how many of the backward's overlapped flushes (cuts) get an early update: the second is the bf16
+# step's mid-encoder flush (sparkmi/models/transformer.py ENC_MID_FLUSH_BF16)
+EARLY_UPDATE_CUTS = 2
 
 
 class _EarlyUpdate:
-    """Learns, on the first backward, which parameters are final at the cut (reported final
-    before it, or launched by it, and never reported again after it), and from the next backward
-    on updates their flat ranges at the cut.  Reference: the per-step Adam of
-    pytorch_machine_translator.py:192-196 / distributed_lstm.py:193-195, split by readiness."""
+    """Learns, on the first backward, which parameters are final at each cut (reported final
+    before it, or launched by it, never reported again after it, and not in an earlier cut's
+    plan), and from the next backward on updates their flat ranges at that cut (at most
+    EARLY_UPDATE_CUTS cuts).  Reference: the per-step Adam of pytorch_machine_translator.py:192-196
+    / distributed_lstm.py:193-195, split by readiness."""
 
     def __init__(self, opt):
         self.opt = opt
-        self.plan = None      # flat ranges updated at the cut
-        self.plan_ids = None
-        self.before, self.after, self.at = set(), set(), None
-        self.used = False
+        self.plans = None     # per cut: (flat ranges, ids) updated at that cut
+        self.begin()
 
     def begin(self):
-        self.before, self.after, self.at, self.used = set(), set(), None, False
+        self.ready = []       # (id, number of cuts passed when it was reported)
+        self.ats = []         # per cut: ids final at it
+        self.used = []
 
     def on_ready(self, p):
         if _grad.CONFIRMING[0]:
             return
-        (self.before if self.at is None else self.after).add(id(p))
+        self.ready.append((id(p), len(self.ats)))
 
     def at_cut(self, launched):
-        if self.at is not None:
-            return  # one cut per backward
-        self.at = self.before | {id(p) for p in launched}
-        if self.plan is not None and self.plan_ids <= self.at:
-            self.opt.step_ranges(self.plan)  # on the side stream, behind the launched work
-            self.used = True
+        k = len(self.ats)
+        at = {i for i, _ in self.ready} | {id(p) for p in launched}
+        self.ats.append(at)
+        if self.plans is not None and k < len(self.plans):
+            rs, ids = self.plans[k]
+            if rs and ids <= at:
+                self.opt.step_ranges(rs)  # on the side stream, behind the launched work
+                self.used.append(k)
+
+    def _after(self, k):
+        return {i for i, c in self.ready if c > k}
 
     def end(self):
-        if self.at is None:
+        if not self.ats:
             return
-        if self.plan is None:
+        if self.plans is None:
             flat = self.opt.flat
-            ids = self.at - self.after
-            rs = []
-            for p, o in zip(flat.params, flat.offsets):
-                if id(p) in ids:
-                    e = o + (p.numel() + 63) // 64 * 64
-                    if rs and rs[-1][1] == o:
-                        rs[-1] = (rs[-1][0], e)
-                    else:
-                        rs.append((o, e))
-            self.plan, self.plan_ids = rs, ids
-        elif self.used and self.plan_ids & self.after:
-            raise RuntimeError("early optimizer update: a parameter updated at the cut received more gradient after it")
+            taken, plans = set(), []
+            for k, at in enumerate(self.ats[:EARLY_UPDATE_CUTS]):
+                ids = at - self._after(k) - taken
+                taken |= ids
+                rs = []
+                for p, o in zip(flat.params, flat.offsets):
+                    if id(p) in ids:
+                        e = o + (p.numel() + 63) // 64 * 64
+                        if rs and rs[-1][1] == o:
+                            rs[-1] = (rs[-1][0], e)
+                        else:
+                            rs.append((o, e))
+                plans.append((rs, ids))
+            self.plans = plans
+            return
+        for k in self.used:
+            if self.plans[k][1] & self._after(k):
+                raise RuntimeError("early optimizer update: a parameter updated at a cut received more gradient "
+                                   "after it")
+
+    @property
+    def plan(self):  # the first cut's ranges (tests / tools)
+        return self.plans[0][0] if self.plans else None
 
 
 class StepRunner:

@@ -398,19 +398,25 @@ def test_transformer_wgrad_overlap_bitwise(monkeypatch, graph):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("mid", [0, 1])
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 @pytest.mark.parametrize("graph", [False, True])
-def test_transformer_early_update_bitwise(monkeypatch, graph, dtype):
-    """The two-part optimizer update (sparkmi/train/runner.py EARLY_UPDATE: the parameters final at
-    the backward's overlapped flush updated there on the side stream, step() updating the rest and
-    advancing the step) gives BITWISE the weights, moments, planes and step counter of the
-    one-launch update — eager and graph-captured StepRunner steps; the early part really ran."""
+def test_transformer_early_update_bitwise(monkeypatch, graph, dtype, mid):
+    """The multi-part optimizer update (sparkmi/train/runner.py EARLY_UPDATE: the parameters final at
+    each of the backward's overlapped flushes updated there on the side stream, step() updating the
+    rest and advancing the step) gives BITWISE the weights, moments, planes and step counter of the
+    one-launch update — eager and graph-captured StepRunner steps; the early parts really ran.
+    mid = 1: extra flushes after the top decoder and the top encoder layer (four cuts instead of
+    two; the first two updated early: EARLY_UPDATE_CUTS)."""
     import copy
     from sparkmi.data.synthetic import translation_pairs
+    from sparkmi.models import transformer as T
     from sparkmi.models.transformer import Transformer
     from sparkmi.optim import Adam
     from sparkmi.train import runner as R
     from sparkmi.utils.flat import FlatParams
+    for name in ("DEC_MID_FLUSH", "DEC_MID_FLUSH_BF16", "ENC_MID_FLUSH", "ENC_MID_FLUSH_BF16"):
+        monkeypatch.setattr(T, name, mid)
     torch.manual_seed(0)
     base = Transformer(d_model=128, ffn_hidden=256, num_heads=2, num_layers=2, max_sequence_length=32,
                        src_vocab_size=96, tgt_vocab_size=96, seed=5, dtype=dtype)
@@ -428,8 +434,9 @@ def test_transformer_early_update_bitwise(monkeypatch, graph, dtype):
         torch.cuda.synchronize()
         if early:
             eu = runner._eu
-            assert eu.plan and sum(e - s for s, e in eu.plan) > flat.numel // 4, eu.plan
-            assert eu.used
+            assert eu.plan and sum(e - s for s, e in eu.plan) > (flat.numel // 8 if mid else flat.numel // 4), eu.plan
+            # cuts: [decoder mid,] kv-concat, [encoder mid,] encoder embedding; the first two are updated early
+            assert eu.used == [0, 1], (eu.used, [len(r) for r, _ in eu.plans])
         st = [p.detach().clone() for p in m.parameters()] + [flat.grad.clone(), opt.m.clone(), opt.v.clone(),
                                                                opt.step_t.clone()]
         if flat.planes is not None:
