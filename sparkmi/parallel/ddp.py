@@ -437,7 +437,11 @@ class DataParallel:
         if self.ipc is not None:
             self._cs.wait_stream(torch.cuda.current_stream(g.device))  # the bucket's gradients are written
             sgd = self._sgd_args(s, e)
-            self.ipc(g, algo=3 if self._zc else None, stream=self._cs, sgd=sgd)
+            # zero-copy for every bucket past the latency-bound one-shot sizes (at any world size: it
+            # also drops the staging copy a 2-rank one-shot makes)
+            from .comm import ONE_SHOT_MAX_BYTES
+            zc = self._zc and sgd is None and (e - s) * 4 > ONE_SHOT_MAX_BYTES
+            self.ipc(g, algo=3 if zc else None, stream=self._cs, sgd=sgd)
             self._sgd_applied = sgd is not None
             self._cs_used = True
             ev = torch.cuda.Event()
