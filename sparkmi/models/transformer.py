@@ -219,6 +219,14 @@ def _mid_flush(g):
     _grad.flush_groups_async(g.device)
 
 
+def _flush_depths(k):
+    """A *_MID_FLUSH setting as a set of depths: an int k (0: none) or a string "k1-k2-..." (a
+    flush after each of those many top layers)."""
+    if isinstance(k, str):
+        return {int(v) for v in k.split("-") if v}
+    return {int(k)} if k else set()
+
+
 # The top ENC_MID_FLUSH encoder layers' queued weight gradients go to the side stream once their
 # backward is done (0: with the rest, launched by the encoder embedding's backward).  In-step A/B
 # (profiles/r6_dec_mid_flush_ab.txt): bf16 4 layers -0.15 ms (the lower layers' backward runs
@@ -232,9 +240,9 @@ class SequentialEncoder(nn.Sequential):
     def forward(self, *inputs):
         x, mode, key_padding = inputs
         n = len(self._modules)
-        k = ENC_MID_FLUSH_BF16 if x.dtype == torch.bfloat16 else ENC_MID_FLUSH
+        ks = _flush_depths(ENC_MID_FLUSH_BF16 if x.dtype == torch.bfloat16 else ENC_MID_FLUSH)
         for i, module in enumerate(self._modules.values()):
-            if k and i == n - k and x.requires_grad and torch.is_grad_enabled():
+            if n - i in ks and x.requires_grad and torch.is_grad_enabled():
                 x.register_hook(_mid_flush)
             x = module(x, mode, key_padding)
         return x
@@ -294,9 +302,9 @@ class SequentialDecoder(nn.Sequential):
         x, y, self_mode, cross_mode, key_padding = inputs[:5]
         kvs = inputs[5] if len(inputs) > 5 and inputs[5] is not None else [None] * len(self._modules)
         n = len(self._modules)
-        k = DEC_MID_FLUSH_BF16 if y.dtype == torch.bfloat16 else DEC_MID_FLUSH
+        ks = _flush_depths(DEC_MID_FLUSH_BF16 if y.dtype == torch.bfloat16 else DEC_MID_FLUSH)
         for i, (module, kv) in enumerate(zip(self._modules.values(), kvs)):
-            if k and i == n - k and y.requires_grad and torch.is_grad_enabled():
+            if n - i in ks and y.requires_grad and torch.is_grad_enabled():
                 y.register_hook(_mid_flush)
             y = module(x, y, self_mode, cross_mode, key_padding, kv)
         return y
