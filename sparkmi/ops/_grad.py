@@ -513,6 +513,19 @@ def flush_deferred():
         _flush_groups(C, gq)
         _flush_ln(C, lq)
         _flush_folds(C, fq)
+    # the LATE cut: with an overlapped group still running on the side stream, the parameters whose
+    # gradients the main stream has just finished (deferred sums, LayerNorm / split-K folds) are
+    # handed to the cut hooks on the main stream, ahead of the join (runner._EarlyUpdate updates
+    # them there, beside the group); their reports below are then confirmations
+    late_cut = early and _async["main"] is not None and bool(_cut_hooks)
+    if late_cut:
+        done = ([p for _, ps, _ in late for p in ps] + [p for e in lq for p in e[6] if p is not None]
+                + [p for e in fq for p in e[6] if p is not None])
+        if done:
+            for fn in list(_cut_hooks):
+                fn(done, late=True)
+        else:
+            late_cut = False
     if early:
         held, held_ln = _join_async()
     CONFIRMING[0] = True
@@ -521,14 +534,21 @@ def flush_deferred():
             grad_ready(*e[4])
         for e in held_ln:
             grad_ready(*e[6])
+        if late_cut:
+            _report_main(lq, late, fq)
     finally:
         CONFIRMING[0] = False
+    if not late_cut:
+        _report_main(lq, late, fq)
+    for e in gq:
+        grad_ready(*e[4])
+
+
+def _report_main(lq, late, fq):
     for e in lq:
         grad_ready(*e[6])
     for _, ps, _ in late:
         grad_ready(*ps)
     for e in fq:
         grad_ready(*e[6])
-    for e in gq:
-        grad_ready(*e[4])
 

@@ -34,6 +34,9 @@ EARLY_UPDATE = True
 # how many of the backward's overlapped flushes (cuts) get an early update: the second is the bf16
 # step's mid-encoder flush (sparkmi/models/transformer.py ENC_MID_FLUSH_BF16)
 EARLY_UPDATE_CUTS = 2
+# the late cut (sparkmi/ops/_grad.py flush_deferred): the parameters the main stream finishes while
+# the last group still runs on the side stream (embedding tables, LayerNorm folds) are updated there
+LATE_UPDATE = True
 
 
 class _EarlyUpdate:
@@ -50,7 +53,7 @@ class _EarlyUpdate:
 
     def begin(self):
         self.ready = []       # (id, number of cuts passed when it was reported)
-        self.ats = []         # per cut: ids final at it
+        self.ats = []         # per cut: (ids final at it, late cut)
         self.used = []
 
     def on_ready(self, p):
@@ -58,14 +61,17 @@ class _EarlyUpdate:
             return
         self.ready.append((id(p), len(self.ats)))
 
-    def at_cut(self, launched):
+    def at_cut(self, launched, late=False):
+        """A side-stream cut: everything reported final so far plus the launched parameters are
+        final once the side stream gets here.  The late cut (on the main stream, while a group
+        still runs on the side stream): only the launched parameters are."""
         k = len(self.ats)
-        at = {i for i, _ in self.ready} | {id(p) for p in launched}
-        self.ats.append(at)
+        at = {id(p) for p in launched} if late else {i for i, _ in self.ready} | {id(p) for p in launched}
+        self.ats.append((at, late))
         if self.plans is not None and k < len(self.plans):
             rs, ids = self.plans[k]
             if rs and ids <= at:
-                self.opt.step_ranges(rs)  # on the side stream, behind the launched work
+                self.opt.step_ranges(rs)  # behind the launched work, on the stream the cut runs on
                 self.used.append(k)
 
     def _after(self, k):
@@ -77,7 +83,10 @@ class _EarlyUpdate:
         if self.plans is None:
             flat = self.opt.flat
             taken, plans = set(), []
-            for k, at in enumerate(self.ats[:EARLY_UPDATE_CUTS]):
+            for k, (at, late) in enumerate(self.ats):
+                if not (k < EARLY_UPDATE_CUTS or (late and LATE_UPDATE)):
+                    plans.append(([], set()))
+                    continue
                 ids = at - self._after(k) - taken
                 taken |= ids
                 rs = []

@@ -435,8 +435,10 @@ def test_transformer_early_update_bitwise(monkeypatch, graph, dtype, mid):
         if early:
             eu = runner._eu
             assert eu.plan and sum(e - s for s, e in eu.plan) > (flat.numel // 8 if mid else flat.numel // 4), eu.plan
-            # cuts: [decoder mid,] kv-concat, [encoder mid,] encoder embedding; the first two are updated early
-            assert eu.used == [0, 1], (eu.used, [len(r) for r, _ in eu.plans])
+            # cuts: [decoder mid,] kv-concat, [encoder mid,] encoder embedding, then the late cut on the
+            # main stream (embedding tables, LayerNorm folds); the first two and the late one are updated early
+            assert eu.used[:2] == [0, 1] and eu.ats[eu.used[-1]][1] and len(eu.used) == 3, \
+                (eu.used, [len(r) for r, _ in eu.plans])
         st = [p.detach().clone() for p in m.parameters()] + [flat.grad.clone(), opt.m.clone(), opt.v.clone(),
                                                                opt.step_t.clone()]
         if flat.planes is not None:
