@@ -10,7 +10,12 @@ int smi_sp_waves() { return g_sp_waves; }
 // tile form of the large problems: 16 = 256 x 128 on the 16x16x32 MFMA (default), 256 = the same
 // on 32x32x16, 128 = 128 x 128 tiles (a 4-wave software-pipelined 256 x 128 form measured 157 vs
 // 181-187 TF and was removed in round 5)
-static int g_sp_tm = 16;
+static int sp_tm_env() {  // SMI_SP_TM = 16 | 256 | 128 (profiling A/Bs of whole runs); default 16
+  const char* e = getenv("SMI_SP_TM");
+  const int v = e ? atoi(e) : 16;
+  return (v == 128 || v == 256 || v == 16) ? v : 16;
+}
+static int g_sp_tm = sp_tm_env();
 int smi_sp_tm() { return g_sp_tm; }
 // set 128 / 256 / 16 for A/B runs in one process; other values query
 extern "C" int smi_gemm_sp_tm(int set) {
@@ -24,7 +29,7 @@ extern "C" int smi_gemm_sp_tm(int set) {
 // 1.5-wave group (384 tiles of 256 x 128 on 256 CUs) measured +0.18 ms per fp32 step
 // (profiles/r5_ab_wgrad_group_tile.log): the 256-row tile's higher efficiency outweighs the
 // half-empty second wave.
-static int g_sp_wg_tm = -1;
+static int g_sp_wg_tm = 16;  // (16 = the default sp_tm; pinned so an sp_tm A/B leaves the group alone)
 int smi_sp_wg_tm() {
   return g_sp_wg_tm > 0 ? g_sp_wg_tm : smi_sp_tm();
 }
