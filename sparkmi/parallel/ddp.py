@@ -226,7 +226,7 @@ class DataParallel:
     def _probe(self, n, mc=None, iters=3, zc=False):
         """(IPC two-shot ms or None, process-group ms, multi-channel RCCL ms or None, zero-copy IPC
         two-shot ms or None) of an n-float all-reduce, max over ranks.  The zero-copy kernel runs
-        on the first n floats of the registered gradient buffer (zeroed again afterwards)."""
+        on the first n floats of the registered gradient buffer (restored afterwards)."""
         import time
         dev = self.flat.grad.device
         x = torch.zeros(n, dtype=torch.float32, device=dev)
@@ -256,6 +256,7 @@ class DataParallel:
         zc_ms = None
         if zc:
             gz = self.flat.grad[:n]
+            keep = gz.clone()  # (restored below: the probe may run on a buffer that already holds gradients)
             bad = 0.0
             try:
                 zc_ms = timed(lambda: self.ipc(gz, algo=3))
@@ -265,7 +266,7 @@ class DataParallel:
                 sync()
                 bad = 0.0 if bool((gz == float(self.world)).all()) else 1.0
             finally:
-                gz.zero_()
+                gz.copy_(keep)
             f = torch.tensor([bad], dtype=torch.float32, device=fdev)
             dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
             if float(f.item()) > 0:
