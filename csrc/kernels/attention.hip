@@ -727,6 +727,37 @@ __global__ __launch_bounds__(512, 1) void attn_bwd8_kernel(AttnBwdArgs a) {
   }
   unsigned short* dK = a.dk + b * a.k_sb + h * a.k_sh;
   unsigned short* dV = a.dv + b * a.v_sb + h * a.v_sh;
+  if (a.k_ss % 8 == 0 && a.v_ss % 8 == 0 && !((uintptr_t)dK & 15) && !((uintptr_t)dV & 15)) {
+    // row-coalesced epilogue (the fp32 kernel's ae16): the wave parks its 32 keys x 64 dims of dK
+    // and dV as bf16 in its own 4 KiB of the (now idle) K and dS images — 16-B chunk c of row r at
+    // c ^ (r & 7) — and stores whole 128-B rows (8 rows per wave instruction) instead of 8-B
+    // pieces of 16 rows.  The loop's last barrier retired every read of those images.
+    unsigned short* ik = &Ki[0][0] + w * 2048;
+    unsigned short* iv = &dSi[0][0] + w * 2048;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int r = kt * 16 + n, c = dt * 16 + 4 * g;
+        const int off = r * 64 + ((((c >> 3) ^ r) & 7) << 3) + (c & 7);
+        store4(ik + off, dk[kt][dt], a.scale);
+        store4(iv + off, dv[kt][dt], 1.0f);
+      }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image writes are done
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int pc = it * 64 + lane, r = pc >> 3, ch = pc & 7;
+      const int off = r * 64 + (((ch ^ r) & 7) << 3);
+      const u16x8_t vk = *(const u16x8_t*)(ik + off), vv = *(const u16x8_t*)(iv + off);
+      const int kj = kwave + r;
+      if (kj < a.Sk) {
+        *(u16x8_t*)(dK + (long)kj * a.k_ss + ch * 8) = vk;
+        *(u16x8_t*)(dV + (long)kj * a.v_ss + ch * 8) = vv;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int kt = 0; kt < 2; ++kt) {
     const int kj = kwave + kt * 16 + n;
