@@ -242,6 +242,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
     __syncthreads();
   }
   unsigned short* O = a.o + b * a.o_sb + h * a.o_sh;
+  // (direct 8-B stores: a row-coalesced pass through the idle K staging measured 15.2 -> 15.7 us per
+  // call — two workgroups per CU already overlap one's stores with the other's loop)
 #pragma unroll
   for (int qs = 0; qs < 2; ++qs) {
     const int qi = qwave + qs * 16 + n;
