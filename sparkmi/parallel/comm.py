@@ -172,6 +172,12 @@ class IpcAllReduce:
                     ok, why = False, f"open rank {r}: {e}"
                     break
                 ptrs.append(base + hq[1])
+        # every rank must have mapped every peer BEFORE any rank launches the self-test kernel: a
+        # rank that skipped it would leave the others' signal counters ahead of its own, and the
+        # instance stays in use for the staged kernels after a failed registration
+        if not self._agree(ok):
+            self.register_error = why or "a peer could not export or map its buffer"
+            return False
         if ok:
             # the whole buffer (a stale or partial mapping shows up somewhere in it)
             n = buf.numel() // 4 * 4
@@ -190,16 +196,20 @@ class IpcAllReduce:
             dist.barrier(group=self.group)  # every peer finished its self-test reads of this buffer
             buf[:n].copy_(save)
             torch.cuda.synchronize()
-        flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
-                            device="cuda" if dist.get_backend(self.group) == "nccl" else "cpu")
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
         self.register_error = why
-        if not int(flag.item()):
+        if not self._agree(ok):
             self._reg = None
             self.err.zero_()
             return False
         self.err.zero_()
         return True
+
+    def _agree(self, ok):
+        """True on every rank iff ``ok`` on every rank (collective)."""
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                            device="cuda" if dist.get_backend(self.group) == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(int(flag.item()))
 
     @property
     def registered(self):
