@@ -127,6 +127,7 @@ class IpcAllReduce:
         # this topology (peer reads over xGMI, system-scope flags): a one-call self-test whose
         # verdict all ranks agree on through the regular process group; on failure the caller
         # keeps the RCCL path (IpcUnavailable) instead of risking a hang or a wrong gradient
+        opened = self._agree(opened)  # no rank launches a test kernel its peers will not join
         ok = opened
         if opened:
             want = float(self.world * (self.world + 1) // 2)
@@ -135,10 +136,7 @@ class IpcAllReduce:
                 self(probe, algo=algo)
                 torch.cuda.synchronize()
                 ok = ok and bool(int(self.err.item()) == 0 and bool((probe == want).all()))
-        flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
-                            device="cuda" if dist.get_backend(group) == "nccl" else "cpu")
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
-        if not int(flag.item()):
+        if not self._agree(ok):
             self.close()
             raise IpcUnavailable("IPC all-reduce self-test failed on some rank; using the collective path")
         self.err.zero_()
